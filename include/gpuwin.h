@@ -1,0 +1,206 @@
+/*
+ * gpuwin.h — C ABI of libgpuwin.so, the MI355X-native keyed event-time window
+ * aggregation operator (a drop-in for Flink's WindowOperator on the
+ * keyBy().window(...).aggregate/reduce path).
+ *
+ * Plain C types only: pointers, sizes, int64 timestamps. No torch, no C++.
+ * Every entry point returns an int status (0 = GW_OK, negative = error) and
+ * never lets a C++ exception cross the boundary; gw_last_error() explains a
+ * failure.  The JVM shim turns a negative status into an
+ * Exception, which is exactly how the reference operator fails its task
+ * ("Any exception from processElement or onEventTime fails the
+ * task").
+ *
+ * Reference slot replaced (paths relative to the Flink tree,
+ * RS/ = flink-runtime/src/main/java/org/apache/flink/streaming/):
+ *   gw_create            WindowOperatorFactory.createStreamOperator
+ *                          (RS/runtime/operators/windowing/WindowOperatorFactory.java:96-99)
+ *                        + WindowOperator.open (WindowOperator.java:226-281)
+ *   gw_ingest            WindowOperator.processElement, batched over all records
+ *                        between two watermarks (WindowOperator.java:293-447;
+ *                        per-record dispatch OneInputStreamTask.java:249-252)
+ *   gw_advance_watermark AbstractStreamOperator.processWatermark ->
+ *                        InternalTimerServiceImpl.tryAdvanceWatermark ->
+ *                        WindowOperator.onEventTime
+ *                        (AbstractStreamOperator.java:690-703,
+ *                         InternalTimerServiceImpl.java:328-347,
+ *                         WindowOperator.java:450-494)
+ *   gw_drain             TimestampedCollector / Output.collect of the fired rows
+ *                        (WindowOperator.emitWindowContents :575-580)
+ *   gw_late_dropped      WindowOperator.numLateRecordsDropped (:144,229)
+ *   gw_destroy           WindowOperator.close / dispose
+ *   gw_java_long_hash,
+ *   gw_murmur_hash,
+ *   gw_key_group_*       KeyGroupRangeAssignment (flink-runtime/.../runtime/state/
+ *                        KeyGroupRangeAssignment.java:50-147), MathUtils.murmurHash
+ *                        (flink-core/.../util/MathUtils.java:137-201)
+ *   gw_partition_device  KeyGroupStreamPartitioner.selectChannel
+ *                        (RS/runtime/partitioner/KeyGroupStreamPartitioner.java:55-64)
+ *                        feeding the RCCL all-to-all that replaces the Netty keyBy shuffle
+ */
+#ifndef GPUWIN_H
+#define GPUWIN_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GW_ABI_VERSION 1
+
+/* ---- status codes -------------------------------------------------------- */
+#define GW_OK              0
+#define GW_E_INVALID      -1  /* bad argument / config (Flink: IllegalArgumentException)      */
+#define GW_E_UNSUPPORTED  -2  /* valid in Flink, not (yet) on the GPU path                   */
+#define GW_E_DEVICE       -3  /* HIP runtime error                                            */
+#define GW_E_OOM          -4  /* device or host allocation failed                             */
+#define GW_E_OUTPUT_FULL  -5  /* more fired rows pending: call gw_drain again                 */
+#define GW_E_NO_TIMESTAMP -6  /* record carries Long.MIN_VALUE (assigners throw RuntimeException) */
+#define GW_E_RANGE        -7  /* window bounds overflow int64                                 */
+#define GW_E_STATE        -8  /* illegal call sequence / merge into the past                  */
+
+/* ---- configuration ------------------------------------------------------- */
+typedef enum gw_assigner {
+    GW_TUMBLING = 0, /* TumblingEventTimeWindows.of(size, offset)  (stagger ALIGNED)   */
+    GW_SLIDING  = 1, /* SlidingEventTimeWindows.of(size, slide, offset)                */
+    GW_SESSION  = 2  /* EventTimeSessionWindows.withGap(gap)                           */
+} gw_assigner;
+
+typedef enum gw_trigger {
+    GW_EVENT_TIME_TRIGGER         = 0, /* EventTimeTrigger.create()                   */
+    GW_PURGING_EVENT_TIME_TRIGGER = 1  /* PurgingTrigger.of(EventTimeTrigger.create()) */
+} gw_trigger;
+
+/* The closed set of aggregate functions of the path.
+ * Result column type: int64 for COUNT/SUM_I64/MIN_I64/MAX_I64/SUM_I32 (sign-extended
+ * Java int), IEEE double for SUM_F64/MIN_F64/MAX_F64/AVG_I64/AVG_F64. */
+typedef enum gw_agg {
+    GW_COUNT   = 0, /* AggregateFunction<T, Long, Long> counting records           */
+    GW_SUM_I64 = 1, /* WindowedStream.sum on a Long field (Java wrap-around)        */
+    GW_SUM_F64 = 2, /* WindowedStream.sum on a Double field                         */
+    GW_MIN_I64 = 3, /* WindowedStream.min on a Long field                           */
+    GW_MAX_I64 = 4, /* WindowedStream.max on a Long field                           */
+    GW_MIN_F64 = 5, /* WindowedStream.min on a Double field (Double.compareTo order) */
+    GW_MAX_F64 = 6, /* WindowedStream.max on a Double field                         */
+    GW_AVG_I64 = 7, /* AverageAggregate: acc (long sum, long count) -> (double)sum/count */
+    GW_AVG_F64 = 8, /* acc (double sum, long count) -> sum/count                    */
+    GW_SUM_I32 = 9  /* WindowedStream.sum on an Integer field (int32 wrap-around)   */
+} gw_agg;
+
+typedef struct gw_config {
+    int32_t assigner;         /* gw_assigner                                          */
+    int32_t trigger;          /* gw_trigger                                           */
+    int64_t size;             /* tumbling/sliding window size, ms                     */
+    int64_t slide;            /* sliding slide, ms (ignored for tumbling)             */
+    int64_t offset;           /* window offset, ms                                    */
+    int64_t gap;              /* session gap, ms                                      */
+    int64_t allowed_lateness; /* WindowedStream.allowedLateness, ms (>= 0)            */
+    int32_t agg;              /* gw_agg                                               */
+    int32_t max_parallelism;  /* number of key groups (0 -> 128)                      */
+    int32_t parallelism;      /* operator parallelism (0 -> 1)                        */
+    int32_t operator_index;   /* this subtask                                         */
+    int32_t device;           /* HIP device ordinal                                   */
+    int32_t flags;            /* GW_FLAG_*                                            */
+    int64_t capacity_hint;    /* expected live keys (sizes the HBM state table)       */
+    int64_t max_batch;        /* records per ingest call (sizes staging), 0 -> 1<<20  */
+} gw_config;
+
+#define GW_FLAG_FORCE_LDS_PREAGG   1 /* always pre-aggregate in LDS before the HBM RMW  */
+#define GW_FLAG_NO_LDS_PREAGG      2 /* never pre-aggregate in LDS                       */
+#define GW_FLAG_CHECK_KEY_GROUPS   4 /* reject keys outside this subtask's key groups    */
+
+typedef struct gw_handle gw_handle;
+
+/* Per-operator counters (Flink: numRecordsIn, numLateRecordsDropped, numFiredTimers). */
+typedef struct gw_stats {
+    int64_t events_in;        /* records handed to gw_ingest*                      */
+    int64_t late_dropped;     /* numLateRecordsDropped                             */
+    int64_t rows_fired;       /* fired (key, window) rows so far                   */
+    int64_t live_keys;        /* occupied state-table slots                        */
+    int64_t table_capacity;   /* state-table slots                                 */
+    int64_t table_bytes;      /* HBM bytes of the state table                      */
+    int64_t deferred;         /* partial aggregates parked outside the pane ring   */
+    int64_t batches;          /* ingest calls                                      */
+    int64_t fires;            /* fire passes launched                              */
+    int64_t rehashes;         /* table growths                                     */
+    int64_t preagg_batches;   /* batches that used the LDS pre-aggregation kernel  */
+    int64_t session_merges;   /* sessions merged away (M_b)                        */
+} gw_stats;
+
+/* ---- lifecycle ------------------------------------------------------------ */
+int  gw_create(const gw_config* cfg, gw_handle** out);
+int  gw_destroy(gw_handle* h);
+/* Last error text of h (or of the last failed gw_create when h == NULL). */
+const char* gw_last_error(const gw_handle* h);
+int  gw_abi_version(void);
+
+/* ---- data path ------------------------------------------------------------ */
+/* Host columns: key[n], ts[n], value[n] (8 bytes each: int64 or IEEE double per agg;
+ * value may be NULL for GW_COUNT).  key_hash[n] (Java key.hashCode()) may be NULL:
+ * the key group is then computed from Long.hashCode(key).  Buffers are reusable as
+ * soon as the call returns.  All records of one call see the same current
+ * watermark (the one last passed to gw_advance_watermark), which is exactly what a
+ * Flink operator sees for the records between two watermarks. */
+int  gw_ingest(gw_handle* h, int64_t n, const int64_t* key, const int32_t* key_hash,
+               const int64_t* ts, const void* value);
+/* Same, with the columns already resident in device memory (d_* are device
+ * pointers).  `stream` is a hipStream_t the inputs were produced on (NULL = the
+ * handle's own stream); the call orders itself after it. */
+int  gw_ingest_device(gw_handle* h, int64_t n, const int64_t* d_key, const int32_t* d_key_hash,
+                      const int64_t* d_ts, const void* d_value, void* stream);
+/* Advance event time to wm: fire every window whose maxTimestamp (end-1) <= wm,
+ * purge its state, and append the fired rows to the output.  *rows_fired (may be
+ * NULL) receives the number of rows this call produced.  Watermarks that do not
+ * advance are ignored, as in InternalTimerServiceImpl.tryAdvanceWatermark. */
+int  gw_advance_watermark(gw_handle* h, int64_t wm, int64_t* rows_fired);
+/* Bounded input ended (BoundedOneInput.endInput) — equivalent to MAX_WATERMARK. */
+int  gw_end_input(gw_handle* h, int64_t* rows_fired);
+
+/* ---- output ---------------------------------------------------------------- */
+int  gw_pending_rows(gw_handle* h, int64_t* n);
+/* Copy up to cap pending rows (key, window start, window end, result) to host
+ * arrays and remove them.  Returns GW_E_OUTPUT_FULL if rows remain. */
+int  gw_drain(gw_handle* h, int64_t* key, int64_t* start, int64_t* end, void* result,
+              int64_t cap, int64_t* n);
+/* Zero-copy device view of the pending rows (for a device-side consumer). */
+int  gw_rows_device(gw_handle* h, const int64_t** d_key, const int64_t** d_start,
+                    const int64_t** d_end, const void** d_result, int64_t* n);
+/* Drop all pending rows (after a device consumer read them). */
+int  gw_clear_rows(gw_handle* h);
+
+int64_t gw_late_dropped(const gw_handle* h);
+int  gw_get_stats(const gw_handle* h, gw_stats* out);
+int  gw_synchronize(gw_handle* h);
+/* hipStream_t the handle launches on (for ordering / event timing by callers). */
+void* gw_stream(gw_handle* h);
+/* Average device duration (ms) of the last launch of each named kernel family,
+ * measured with HIP events on the handle's stream.  which: 0 = ingest, 1 = fire. */
+int  gw_kernel_time_ms(gw_handle* h, int which, double* ms, int64_t* launches);
+int  gw_enable_kernel_timing(gw_handle* h, int enable);
+
+/* ---- key groups (stateless) ---------------------------------------------- */
+int32_t gw_java_long_hash(int64_t key);             /* Long.hashCode                     */
+int32_t gw_murmur_hash(int32_t code);               /* MathUtils.murmurHash              */
+int32_t gw_key_group_for_hash(int32_t key_hash, int32_t max_parallelism);
+int32_t gw_operator_for_key_group(int32_t max_parallelism, int32_t parallelism, int32_t kg);
+int32_t gw_default_max_parallelism(int32_t parallelism);
+/* Device kernel: kg[i] / owner[i] (either may be NULL) for n keys. */
+int  gw_key_groups_device(int64_t n, const int64_t* d_key, const int32_t* d_key_hash,
+                          int32_t max_parallelism, int32_t parallelism,
+                          int32_t* d_kg, int32_t* d_owner, void* stream);
+/* Device kernel: stable partition of (key, ts, value) by owner subtask
+ * (KeyGroupStreamPartitioner).  Output columns are grouped by destination; counts[p]
+ * (device int64[parallelism]) receives the number of records for subtask p.
+ * d_scratch must hold gw_partition_scratch_bytes(n, parallelism) bytes. */
+int64_t gw_partition_scratch_bytes(int64_t n, int32_t parallelism);
+int  gw_partition_device(int64_t n, const int64_t* d_key, const int32_t* d_key_hash,
+                         const int64_t* d_ts, const void* d_value,
+                         int32_t max_parallelism, int32_t parallelism,
+                         int64_t* d_key_out, int64_t* d_ts_out, void* d_value_out,
+                         int64_t* d_counts, void* d_scratch, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GPUWIN_H */

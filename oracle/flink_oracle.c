@@ -1,0 +1,999 @@
+/*
+ * flink_oracle.c — TEST INFRASTRUCTURE ONLY (see flink_oracle.h).
+ *
+ * CPU restatement of the reference's keyed event-time window path, record by
+ * record.  Every function cites the reference code it follows; paths are
+ * relative to the Flink tree:
+ *   RS/ = flink-runtime/src/main/java/org/apache/flink/streaming/
+ *   RR/ = flink-runtime/src/main/java/org/apache/flink/runtime/
+ *   C/  = flink-core/src/main/java/org/apache/flink/
+ *   SJ/ = flink-streaming-java/src/main/java/org/apache/flink/streaming/
+ *
+ * Java `long`/`int` arithmetic wraps; it is reproduced with unsigned casts.
+ */
+#define _POSIX_C_SOURCE 200809L
+#include "flink_oracle.h"
+
+#include <math.h>
+#include <pthread.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+
+#define JADD(a, b) ((int64_t)((uint64_t)(a) + (uint64_t)(b)))
+#define JSUB(a, b) ((int64_t)((uint64_t)(a) - (uint64_t)(b)))
+#define JMUL32(a, b) ((int32_t)((uint32_t)(a) * (uint32_t)(b)))
+
+/* ------------------------------------------------------------------------ */
+/* MathUtils (C/util/MathUtils.java)                                          */
+/* ------------------------------------------------------------------------ */
+static inline int32_t rotl32(int32_t x, int r) {
+    uint32_t u = (uint32_t)x;
+    return (int32_t)((u << r) | (u >> (32 - r)));
+}
+
+/* MathUtils.bitMix, MathUtils.java:194-201 (Murmur3 fmix32). */
+int32_t wo_bit_mix(int32_t in) {
+    uint32_t h = (uint32_t)in;
+    h ^= h >> 16;
+    h *= 0x85ebca6bu;
+    h ^= h >> 13;
+    h *= 0xc2b2ae35u;
+    h ^= h >> 16;
+    return (int32_t)h;
+}
+
+/* MathUtils.murmurHash(int), MathUtils.java:137-155. */
+int32_t wo_murmur_hash(int32_t code) {
+    code = JMUL32(code, 0xcc9e2d51u);
+    code = rotl32(code, 15);
+    code = JMUL32(code, 0x1b873593u);
+    code = rotl32(code, 13);
+    code = (int32_t)((uint32_t)JMUL32(code, 5u) + 0xe6546b64u);
+    code ^= 4;
+    code = wo_bit_mix(code);
+    if (code >= 0) return code;
+    if (code != INT32_MIN) return -code;
+    return 0;
+}
+
+/* MathUtils.longToIntWithBitMixing, MathUtils.java:180-185 (TimeWindow.hashCode). */
+int32_t wo_long_to_int_with_bit_mixing(int64_t in) {
+    uint64_t x = (uint64_t)in;
+    x = (x ^ (x >> 30)) * 0xbf58476d1ce4e5b9ull;
+    x = (x ^ (x >> 27)) * 0x94d049bb133111ebull;
+    x = x ^ (x >> 31);
+    return (int32_t)(uint32_t)x;
+}
+
+/* JDK Long.hashCode: (int)(value ^ (value >>> 32)). */
+int32_t wo_long_hash(int64_t v) {
+    uint64_t u = (uint64_t)v;
+    return (int32_t)(uint32_t)(u ^ (u >> 32));
+}
+
+/* JDK String.hashCode: s[0]*31^(n-1) + ... + s[n-1], int arithmetic. */
+int32_t wo_string_hash(const uint16_t* s, int64_t n) {
+    uint32_t h = 0;
+    for (int64_t i = 0; i < n; i++) h = 31u * h + s[i];
+    return (int32_t)h;
+}
+
+/* ------------------------------------------------------------------------ */
+/* KeyGroupRangeAssignment (RR/state/KeyGroupRangeAssignment.java)            */
+/* ------------------------------------------------------------------------ */
+/* computeKeyGroupForKeyHash :75-77 */
+int32_t wo_assign_to_key_group(int32_t key_hash, int32_t max_parallelism) {
+    return wo_murmur_hash(key_hash) % max_parallelism;
+}
+/* computeOperatorIndexForKeyGroup :124-127 */
+int32_t wo_operator_index_for_key_group(int32_t max_p, int32_t p, int32_t kg) {
+    return kg * p / max_p;
+}
+/* computeKeyGroupRangeForOperatorIndex :93-106 */
+void wo_key_group_range(int32_t max_p, int32_t p, int32_t idx, int32_t* start, int32_t* end) {
+    *start = (idx * max_p + p - 1) / p;
+    *end = ((idx + 1) * max_p - 1) / p;
+}
+/* MathUtils.roundUpToPowerOfTwo :163-171 */
+static int32_t round_up_pow2(int32_t x) {
+    uint32_t u = (uint32_t)x - 1u;
+    u |= u >> 1; u |= u >> 2; u |= u >> 4; u |= u >> 8; u |= u >> 16;
+    return (int32_t)(u + 1u);
+}
+/* computeDefaultMaxParallelism :137-147 (lower bound 128, upper 1<<15) */
+int32_t wo_default_max_parallelism(int32_t p) {
+    int32_t v = round_up_pow2(p + p / 2);
+    if (v < 128) v = 128;
+    if (v > 32768) v = 32768;
+    return v;
+}
+
+/* ------------------------------------------------------------------------ */
+/* TimeWindow / assigners                                                     */
+/* ------------------------------------------------------------------------ */
+/* TimeWindow.getWindowStartWithOffset, RS/api/windowing/windows/TimeWindow.java:264-272 */
+int64_t wo_window_start_with_offset(int64_t ts, int64_t offset, int64_t size) {
+    int64_t rem = JSUB(ts, offset) % size;
+    if (rem < 0) return JSUB(ts, rem + size);
+    return JSUB(ts, rem);
+}
+
+int wo_validate(const gw_config* c) {
+    if (c->assigner == GW_TUMBLING) {
+        /* TumblingEventTimeWindows ctor :55-62: abs(offset) >= size -> IAE */
+        int64_t ao = c->offset < 0 ? -c->offset : c->offset;
+        if (c->size <= 0 || ao >= c->size) return GW_E_INVALID;
+    } else if (c->assigner == GW_SLIDING) {
+        /* SlidingEventTimeWindows ctor :57-70 */
+        int64_t ao = c->offset < 0 ? -c->offset : c->offset;
+        if (c->slide <= 0 || ao >= c->slide || c->size <= 0) return GW_E_INVALID;
+        if (c->size / c->slide > 10000000) return GW_E_INVALID;
+    } else if (c->assigner == GW_SESSION) {
+        /* EventTimeSessionWindows ctor: sessionTimeout <= 0 -> IAE (:52-53) */
+        if (c->gap <= 0) return GW_E_INVALID;
+    } else {
+        return GW_E_INVALID;
+    }
+    if (c->allowed_lateness < 0) return GW_E_INVALID;
+    if (c->agg < GW_COUNT || c->agg > GW_SUM_I32) return GW_E_INVALID;
+    if (c->trigger != GW_EVENT_TIME_TRIGGER && c->trigger != GW_PURGING_EVENT_TIME_TRIGGER)
+        return GW_E_INVALID;
+    return GW_OK;
+}
+
+/* TumblingEventTimeWindows.assignWindows :69-85, SlidingEventTimeWindows.assignWindows
+ * :77-90, EventTimeSessionWindows.assignWindows (SJ/api/windowing/assigners/
+ * EventTimeSessionWindows.java:61-64).  Order = the reference's list order. */
+int wo_assign_windows(const gw_config* c, int64_t ts, int64_t* ws, int64_t* we, int cap) {
+    if (ts == INT64_MIN) return GW_E_NO_TIMESTAMP;
+    if (c->assigner == GW_TUMBLING) {
+        if (cap < 1) return GW_E_INVALID;
+        int64_t off = c->offset % c->size; /* (globalOffset + staggerOffset(ALIGNED=0)) % size */
+        int64_t s = wo_window_start_with_offset(ts, off, c->size);
+        ws[0] = s;
+        we[0] = JADD(s, c->size);
+        return 1;
+    }
+    if (c->assigner == GW_SLIDING) {
+        int n = 0;
+        int64_t last = wo_window_start_with_offset(ts, c->offset, c->slide);
+        int64_t lim = JSUB(ts, c->size);
+        for (int64_t s = last; s > lim; s = JSUB(s, c->slide)) {
+            if (n >= cap) return GW_E_RANGE;
+            ws[n] = s;
+            we[n] = JADD(s, c->size);
+            n++;
+        }
+        return n;
+    }
+    if (cap < 1) return GW_E_INVALID;
+    ws[0] = ts;
+    we[0] = JADD(ts, c->gap);
+    return 1;
+}
+
+/* TimeWindow.intersects :116-118 (inclusive: touching windows merge) */
+static inline int tw_intersects(int64_t s1, int64_t e1, int64_t s2, int64_t e2) {
+    return s1 <= e2 && e1 >= s2;
+}
+
+/* TimeWindow.mergeWindows :208-254: stable sort by start, sweep, cover. */
+int wo_merge_windows(int n, const int64_t* s, const int64_t* e, int32_t* group_of,
+                     int64_t* gs, int64_t* ge) {
+    int* idx = (int*)malloc(sizeof(int) * (n > 0 ? n : 1));
+    for (int i = 0; i < n; i++) idx[i] = i;
+    for (int i = 1; i < n; i++) { /* insertion sort = stable */
+        int v = idx[i], j = i - 1;
+        while (j >= 0 && s[idx[j]] > s[v]) { idx[j + 1] = idx[j]; j--; }
+        idx[j + 1] = v;
+    }
+    int g = -1;
+    for (int k = 0; k < n; k++) {
+        int i = idx[k];
+        if (g >= 0 && tw_intersects(gs[g], ge[g], s[i], e[i])) {
+            if (s[i] < gs[g]) gs[g] = s[i];
+            if (e[i] > ge[g]) ge[g] = e[i];
+        } else {
+            g++;
+            gs[g] = s[i];
+            ge[g] = e[i];
+        }
+        group_of[i] = g;
+    }
+    free(idx);
+    return g + 1;
+}
+
+/* ------------------------------------------------------------------------ */
+/* open-addressing map: 4 x int64 key -> int64 value                          */
+/* ------------------------------------------------------------------------ */
+typedef struct { int64_t k[4]; int64_t v; int64_t st; } ment_t; /* st 0 empty 1 full 2 tomb */
+typedef struct { ment_t* e; int64_t cap, n, used; } map_t;
+
+static uint64_t mix64(uint64_t x) {
+    x ^= x >> 33; x *= 0xff51afd7ed558ccdull;
+    x ^= x >> 33; x *= 0xc4ceb9fe1a85ec53ull;
+    x ^= x >> 33;
+    return x;
+}
+static uint64_t hash4(const int64_t* k) {
+    uint64_t h = mix64((uint64_t)k[0] + 0x9e3779b97f4a7c15ull);
+    h = mix64(h ^ (uint64_t)k[1]);
+    h = mix64(h ^ (uint64_t)k[2]);
+    return mix64(h ^ (uint64_t)k[3]);
+}
+static int map_init(map_t* m, int64_t cap) {
+    int64_t c = 16;
+    while (c < cap) c <<= 1;
+    m->e = (ment_t*)calloc((size_t)c, sizeof(ment_t));
+    m->cap = c; m->n = 0; m->used = 0;
+    return m->e ? 0 : -1;
+}
+static void map_free(map_t* m) { free(m->e); m->e = NULL; m->cap = m->n = m->used = 0; }
+static ment_t* map_find(const map_t* m, const int64_t* k) {
+    uint64_t mask = (uint64_t)m->cap - 1, i = hash4(k) & mask;
+    for (;;) {
+        ment_t* e = &m->e[i];
+        if (e->st == 0) return NULL;
+        if (e->st == 1 && e->k[0] == k[0] && e->k[1] == k[1] && e->k[2] == k[2] && e->k[3] == k[3])
+            return e;
+        i = (i + 1) & mask;
+    }
+}
+static int map_grow(map_t* m) {
+    map_t nm;
+    int64_t nc = m->n * 4 > m->cap ? m->cap * 2 : m->cap;
+    if (map_init(&nm, nc) != 0) return -1;
+    for (int64_t i = 0; i < m->cap; i++) {
+        if (m->e[i].st != 1) continue;
+        uint64_t mask = (uint64_t)nm.cap - 1, j = hash4(m->e[i].k) & mask;
+        while (nm.e[j].st) j = (j + 1) & mask;
+        nm.e[j] = m->e[i];
+        nm.n++; nm.used++;
+    }
+    free(m->e);
+    *m = nm;
+    return 0;
+}
+/* Returns the entry (existing or newly inserted with v = dflt); *created set. */
+static ment_t* map_upsert(map_t* m, const int64_t* k, int64_t dflt, int* created) {
+    ment_t* f = map_find(m, k);
+    if (f) { if (created) *created = 0; return f; }
+    if ((m->used + 1) * 2 > m->cap) {
+        if (map_grow(m) != 0) return NULL;
+    }
+    uint64_t mask = (uint64_t)m->cap - 1, i = hash4(k) & mask;
+    while (m->e[i].st == 1) i = (i + 1) & mask;
+    if (m->e[i].st == 0) m->used++;
+    ment_t* e = &m->e[i];
+    memcpy(e->k, k, sizeof(e->k));
+    e->v = dflt; e->st = 1;
+    m->n++;
+    if (created) *created = 1;
+    return e;
+}
+static int map_del(map_t* m, const int64_t* k) {
+    ment_t* f = map_find(m, k);
+    if (!f) return 0;
+    f->st = 2;
+    m->n--;
+    return 1;
+}
+
+/* ------------------------------------------------------------------------ */
+/* accumulators (SumFunction / ComparableAggregator / AggregateFunction)      */
+/* ------------------------------------------------------------------------ */
+typedef struct { int64_t i; double d; int64_t c; } acc_t;
+
+static inline double bits2d(int64_t b) { double d; memcpy(&d, &b, 8); return d; }
+static inline int64_t d2bits(double d) { int64_t b; memcpy(&b, &d, 8); return b; }
+
+/* Double.compare (JDK): numeric order, then doubleToLongBits (NaN canonical,
+ * largest; -0.0 < 0.0). */
+static int java_double_compare(double a, double b) {
+    if (a < b) return -1;
+    if (a > b) return 1;
+    int64_t x = (a != a) ? 0x7ff8000000000000LL : d2bits(a);
+    int64_t y = (b != b) ? 0x7ff8000000000000LL : d2bits(b);
+    return x == y ? 0 : (x < y ? -1 : 1);
+}
+
+/* ReduceFunction.reduce(a, b) for the positional aggregations:
+ *  SumAggregator.reduce (RS/api/functions/aggregation/SumAggregator.java:66-76) with
+ *  SumFunction.{Long,Int,Double}Sum (SumFunction.java:34-105);
+ *  ComparableAggregator.reduce non-By branch (ComparableAggregator.java:83-104) with
+ *  Min/MaxComparator (Comparator.java:33-90): c==0 -> take b's field. */
+static void reduce_into(acc_t* a, int64_t b, int agg) {
+    switch (agg) {
+    case GW_SUM_I64: a->i = JADD(a->i, b); break;
+    case GW_SUM_I32: a->i = (int32_t)((uint32_t)a->i + (uint32_t)b); break;
+    case GW_SUM_F64: a->d = a->d + bits2d(b); break;
+    case GW_MIN_I64: a->i = (a->i < b) ? a->i : b; break;
+    case GW_MAX_I64: a->i = (a->i > b) ? a->i : b; break;
+    case GW_MIN_F64: a->d = (java_double_compare(a->d, bits2d(b)) < 0) ? a->d : bits2d(b); break;
+    case GW_MAX_F64: a->d = (java_double_compare(a->d, bits2d(b)) > 0) ? a->d : bits2d(b); break;
+    default: break;
+    }
+}
+
+/* First element of a window: ReducingState stores the value itself
+ * (HeapReducingState.java:90-97 ReduceTransformation: previous == null ? value : ...);
+ * AggregatingState calls createAccumulator then add (HeapAggregatingState.java:94-102). */
+static void acc_first(acc_t* a, int agg, int64_t v) {
+    memset(a, 0, sizeof(*a));
+    switch (agg) {
+    case GW_COUNT: a->c = 1; break;
+    case GW_AVG_I64: a->i = v; a->c = 1; break;
+    case GW_AVG_F64: a->d = 0.0 + bits2d(v); a->c = 1; break;
+    case GW_SUM_I32: a->i = (int32_t)v; break;
+    case GW_SUM_F64: case GW_MIN_F64: case GW_MAX_F64: a->d = bits2d(v); break;
+    default: a->i = v; break;
+    }
+}
+static void acc_add(acc_t* a, int agg, int64_t v) {
+    switch (agg) {
+    case GW_COUNT: a->c += 1; break;
+    case GW_AVG_I64: a->i = JADD(a->i, v); a->c += 1; break;
+    case GW_AVG_F64: a->d = a->d + bits2d(v); a->c += 1; break;
+    default: reduce_into(a, v, agg); break;
+    }
+}
+/* AbstractHeapMergingState.mergeState(a, b): AggregateFunction.merge or
+ * ReduceFunction.reduce (HeapAggregatingState / HeapReducingState). */
+static void acc_merge(acc_t* a, const acc_t* b, int agg) {
+    switch (agg) {
+    case GW_COUNT: a->c += b->c; break;
+    case GW_AVG_I64: a->i = JADD(a->i, b->i); a->c += b->c; break;
+    case GW_AVG_F64: a->d = a->d + b->d; a->c += b->c; break;
+    case GW_SUM_F64: case GW_MIN_F64: case GW_MAX_F64: reduce_into(a, d2bits(b->d), agg); break;
+    default: reduce_into(a, b->i, agg); break;
+    }
+}
+/* getResult (AggregateFunction) / the reduced field (PassThroughWindowFunction). */
+static int64_t acc_result_bits(const acc_t* a, int agg) {
+    switch (agg) {
+    case GW_COUNT: return a->c;
+    case GW_AVG_I64: return d2bits((double)a->i / (double)a->c);
+    case GW_AVG_F64: return d2bits(a->d / (double)a->c);
+    case GW_SUM_F64: case GW_MIN_F64: case GW_MAX_F64: return d2bits(a->d);
+    default: return a->i;
+    }
+}
+
+/* ------------------------------------------------------------------------ */
+/* operator state                                                             */
+/* ------------------------------------------------------------------------ */
+typedef struct { int64_t ts, key, s, e, gen; } tmr_t;
+typedef struct { int n, cap; int64_t* w; /* [4*i]: ws, we, ss, se */ } mws_t;
+
+struct wo_op {
+    gw_config c;
+    int64_t wm;
+    int64_t late;
+    int64_t merges;
+    map_t state;  /* (key, ns_start, ns_end, 0) -> acc index */
+    acc_t* accs;
+    int64_t nacc, cap_acc;
+    int64_t* freel;
+    int64_t nfree, cap_free;
+    map_t timers; /* (ts, key, s, e) -> generation */
+    tmr_t* heap;
+    int64_t nheap, cap_heap;
+    int64_t gen;
+    map_t sets;   /* (key,0,0,0) -> index into msets */
+    mws_t* msets;
+    int64_t nsets, cap_sets;
+    int64_t *ok, *os, *oe, *orr;
+    int64_t on, ocap, ohead;
+    char err[256];
+};
+
+static void op_err(wo_op* op, const char* fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(op->err, sizeof(op->err), fmt, ap);
+    va_end(ap);
+}
+
+static int64_t acc_alloc(wo_op* op) {
+    if (op->nfree > 0) return op->freel[--op->nfree];
+    if (op->nacc == op->cap_acc) {
+        int64_t nc = op->cap_acc ? op->cap_acc * 2 : 1024;
+        acc_t* na = (acc_t*)realloc(op->accs, sizeof(acc_t) * (size_t)nc);
+        if (!na) return -1;
+        op->accs = na; op->cap_acc = nc;
+    }
+    return op->nacc++;
+}
+static void acc_release(wo_op* op, int64_t i) {
+    if (op->nfree == op->cap_free) {
+        int64_t nc = op->cap_free ? op->cap_free * 2 : 1024;
+        op->freel = (int64_t*)realloc(op->freel, sizeof(int64_t) * (size_t)nc);
+        op->cap_free = nc;
+    }
+    op->freel[op->nfree++] = i;
+}
+
+/* --- windowState (HeapReducingState / HeapAggregatingState on the
+ *     CopyOnWriteStateMap keyed by (key, namespace)) --- */
+static int state_add(wo_op* op, int64_t key, int64_t s, int64_t e, int64_t v) {
+    int64_t k[4] = {key, s, e, 0};
+    int created = 0;
+    ment_t* m = map_upsert(&op->state, k, -1, &created);
+    if (!m) return GW_E_OOM;
+    if (created) {
+        int64_t a = acc_alloc(op);
+        if (a < 0) return GW_E_OOM;
+        m = map_find(&op->state, k);
+        m->v = a;
+        acc_first(&op->accs[a], op->c.agg, v);
+    } else {
+        acc_add(&op->accs[m->v], op->c.agg, v);
+    }
+    return GW_OK;
+}
+static acc_t* state_get(wo_op* op, int64_t key, int64_t s, int64_t e) {
+    int64_t k[4] = {key, s, e, 0};
+    ment_t* m = map_find(&op->state, k);
+    return m ? &op->accs[m->v] : NULL;
+}
+static void state_clear(wo_op* op, int64_t key, int64_t s, int64_t e) {
+    int64_t k[4] = {key, s, e, 0};
+    ment_t* m = map_find(&op->state, k);
+    if (!m) return;
+    acc_release(op, m->v);
+    map_del(&op->state, k);
+}
+
+/* --- timers: InternalTimerServiceImpl + HeapPriorityQueueSet (dedup set + min-heap
+ *     on timestamp; InternalTimerServiceImpl.java:249-264,328-347). --- */
+static void heap_push(wo_op* op, tmr_t t) {
+    if (op->nheap == op->cap_heap) {
+        int64_t nc = op->cap_heap ? op->cap_heap * 2 : 1024;
+        op->heap = (tmr_t*)realloc(op->heap, sizeof(tmr_t) * (size_t)nc);
+        op->cap_heap = nc;
+    }
+    int64_t i = op->nheap++;
+    while (i > 0) {
+        int64_t p = (i - 1) / 2;
+        if (op->heap[p].ts <= t.ts) break;
+        op->heap[i] = op->heap[p];
+        i = p;
+    }
+    op->heap[i] = t;
+}
+static tmr_t heap_pop(wo_op* op) {
+    tmr_t top = op->heap[0];
+    tmr_t last = op->heap[--op->nheap];
+    int64_t i = 0, n = op->nheap;
+    for (;;) {
+        int64_t l = 2 * i + 1, r = l + 1, m = i;
+        int64_t mts = last.ts;
+        if (l < n && op->heap[l].ts < mts) { m = l; mts = op->heap[l].ts; }
+        if (r < n && op->heap[r].ts < mts) { m = r; }
+        if (m == i) break;
+        op->heap[i] = op->heap[m];
+        i = m;
+    }
+    if (n > 0) op->heap[i] = last;
+    return top;
+}
+static int tmr_register(wo_op* op, int64_t key, int64_t s, int64_t e, int64_t ts) {
+    int64_t k[4] = {ts, key, s, e};
+    int created = 0;
+    ment_t* m = map_upsert(&op->timers, k, 0, &created);
+    if (!m) return GW_E_OOM;
+    if (!created) return GW_OK; /* HeapPriorityQueueSet.add dedups */
+    m->v = ++op->gen;
+    tmr_t t = {ts, key, s, e, m->v};
+    heap_push(op, t);
+    return GW_OK;
+}
+static void tmr_delete(wo_op* op, int64_t key, int64_t s, int64_t e, int64_t ts) {
+    int64_t k[4] = {ts, key, s, e};
+    map_del(&op->timers, k); /* lazily skipped when popped */
+}
+
+/* WindowOperator.cleanupTime :670-677 (overflow -> Long.MAX_VALUE) */
+static int64_t cleanup_time(const wo_op* op, int64_t end) {
+    int64_t mx = JSUB(end, 1);
+    int64_t ct = JADD(mx, op->c.allowed_lateness);
+    return ct >= mx ? ct : INT64_MAX;
+}
+/* WindowOperator.isWindowLate :609-612 */
+static int is_window_late(const wo_op* op, int64_t end) { return cleanup_time(op, end) <= op->wm; }
+/* WindowOperator.isElementLate :620-624 */
+static int is_element_late(const wo_op* op, int64_t ts) {
+    return JADD(ts, op->c.allowed_lateness) <= op->wm;
+}
+/* WindowOperator.registerCleanupTimer :631-643 / deleteCleanupTimer :650-662 */
+static int register_cleanup_timer(wo_op* op, int64_t key, int64_t s, int64_t e) {
+    int64_t ct = cleanup_time(op, e);
+    if (ct == INT64_MAX) return GW_OK;
+    return tmr_register(op, key, s, e, ct);
+}
+static void delete_cleanup_timer(wo_op* op, int64_t key, int64_t s, int64_t e) {
+    int64_t ct = cleanup_time(op, e);
+    if (ct == INT64_MAX) return;
+    tmr_delete(op, key, s, e, ct);
+}
+
+/* EventTimeTrigger (RS/api/windowing/triggers/EventTimeTrigger.java:37-79), optionally
+ * wrapped in PurgingTrigger (FIRE -> FIRE_AND_PURGE).  Returns 0 CONTINUE, 1 FIRE,
+ * 3 FIRE_AND_PURGE. */
+static int trigger_on_element(wo_op* op, int64_t key, int64_t s, int64_t e, int* rc) {
+    int64_t mx = JSUB(e, 1);
+    *rc = GW_OK;
+    if (mx <= op->wm) return op->c.trigger == GW_PURGING_EVENT_TIME_TRIGGER ? 3 : 1;
+    *rc = tmr_register(op, key, s, e, mx);
+    return 0;
+}
+static int trigger_on_event_time(wo_op* op, int64_t time, int64_t e) {
+    if (time != JSUB(e, 1)) return 0;
+    return op->c.trigger == GW_PURGING_EVENT_TIME_TRIGGER ? 3 : 1;
+}
+static void trigger_clear(wo_op* op, int64_t key, int64_t s, int64_t e) {
+    tmr_delete(op, key, s, e, JSUB(e, 1));
+}
+static int trigger_on_merge(wo_op* op, int64_t key, int64_t s, int64_t e) {
+    int64_t mx = JSUB(e, 1);
+    if (mx > op->wm) return tmr_register(op, key, s, e, mx);
+    return GW_OK;
+}
+
+/* WindowOperator.emitWindowContents :575-580 (+ InternalSingleValueWindowFunction /
+ * PassThroughWindowFunction): row (key, window, result) at timestamp end-1. */
+static int emit(wo_op* op, int64_t key, int64_t s, int64_t e, const acc_t* a) {
+    if (op->on == op->ocap) {
+        int64_t nc = op->ocap ? op->ocap * 2 : 1024;
+        op->ok = (int64_t*)realloc(op->ok, 8 * (size_t)nc);
+        op->os = (int64_t*)realloc(op->os, 8 * (size_t)nc);
+        op->oe = (int64_t*)realloc(op->oe, 8 * (size_t)nc);
+        op->orr = (int64_t*)realloc(op->orr, 8 * (size_t)nc);
+        if (!op->ok || !op->os || !op->oe || !op->orr) return GW_E_OOM;
+        op->ocap = nc;
+    }
+    op->ok[op->on] = key;
+    op->os[op->on] = s;
+    op->oe[op->on] = e;
+    op->orr[op->on] = acc_result_bits(a, op->c.agg);
+    op->on++;
+    return GW_OK;
+}
+
+/* --- MergingWindowSet (RS/runtime/operators/windowing/MergingWindowSet.java) --- */
+static mws_t* mws_get(wo_op* op, int64_t key, int create) {
+    int64_t k[4] = {key, 0, 0, 0};
+    ment_t* m = map_find(&op->sets, k);
+    if (m) return &op->msets[m->v];
+    if (!create) return NULL;
+    if (op->nsets == op->cap_sets) {
+        int64_t nc = op->cap_sets ? op->cap_sets * 2 : 256;
+        op->msets = (mws_t*)realloc(op->msets, sizeof(mws_t) * (size_t)nc);
+        op->cap_sets = nc;
+    }
+    int64_t idx = op->nsets++;
+    memset(&op->msets[idx], 0, sizeof(mws_t));
+    map_upsert(&op->sets, k, idx, NULL);
+    return &op->msets[idx];
+}
+static int mws_find(const mws_t* m, int64_t s, int64_t e) {
+    for (int i = 0; i < m->n; i++)
+        if (m->w[4 * i] == s && m->w[4 * i + 1] == e) return i;
+    return -1;
+}
+/* mapping.put (replace or append) */
+static void mws_put(mws_t* m, int64_t s, int64_t e, int64_t ss, int64_t se) {
+    int i = mws_find(m, s, e);
+    if (i < 0) {
+        if (m->n == m->cap) {
+            m->cap = m->cap ? m->cap * 2 : 4;
+            m->w = (int64_t*)realloc(m->w, sizeof(int64_t) * 4 * (size_t)m->cap);
+        }
+        i = m->n++;
+        m->w[4 * i] = s;
+        m->w[4 * i + 1] = e;
+    }
+    m->w[4 * i + 2] = ss;
+    m->w[4 * i + 3] = se;
+}
+/* mapping.remove -> returns 1 and the state window if present */
+static int mws_remove(mws_t* m, int64_t s, int64_t e, int64_t* ss, int64_t* se) {
+    int i = mws_find(m, s, e);
+    if (i < 0) return 0;
+    if (ss) { *ss = m->w[4 * i + 2]; *se = m->w[4 * i + 3]; }
+    m->n--;
+    if (i != m->n) memcpy(&m->w[4 * i], &m->w[4 * m->n], 4 * sizeof(int64_t));
+    return 1;
+}
+
+/* The merge callback of WindowOperator.processElement (WindowOperator.java:314-366). */
+static int merge_function(wo_op* op, int64_t key, int64_t rs, int64_t re,
+                          const int64_t* mw, int nmw, int64_t tss, int64_t tse,
+                          const int64_t* msw, int nmsw) {
+    if (JADD(JSUB(re, 1), op->c.allowed_lateness) <= op->wm) {
+        op_err(op, "The end timestamp of an event-time window cannot become earlier than the "
+                   "current watermark by merging. Current watermark: %lld window: [%lld,%lld)",
+               (long long)op->wm, (long long)rs, (long long)re);
+        return GW_E_STATE;
+    }
+    int rc = trigger_on_merge(op, key, rs, re);
+    if (rc) return rc;
+    for (int i = 0; i < nmw; i++) {
+        trigger_clear(op, key, mw[2 * i], mw[2 * i + 1]);
+        delete_cleanup_timer(op, key, mw[2 * i], mw[2 * i + 1]);
+    }
+    /* AbstractHeapMergingState.mergeNamespaces (RR/state/heap/AbstractHeapMergingState.java:65-91) */
+    if (nmsw == 0) return GW_OK;
+    acc_t merged;
+    int have = 0;
+    for (int i = 0; i < nmsw; i++) {
+        acc_t* src = state_get(op, key, msw[2 * i], msw[2 * i + 1]);
+        if (!src) continue;
+        acc_t tmp = *src;
+        state_clear(op, key, msw[2 * i], msw[2 * i + 1]);
+        if (!have) { merged = tmp; have = 1; }
+        else acc_merge(&merged, &tmp, op->c.agg);
+        op->merges++;
+    }
+    if (have) {
+        int64_t k[4] = {key, tss, tse, 0};
+        int created = 0;
+        ment_t* m = map_upsert(&op->state, k, -1, &created);
+        if (!m) return GW_E_OOM;
+        if (created) {
+            int64_t a = acc_alloc(op);
+            if (a < 0) return GW_E_OOM;
+            m = map_find(&op->state, k);
+            m->v = a;
+            op->accs[a] = merged;
+        } else {
+            acc_t t = op->accs[m->v];
+            acc_merge(&t, &merged, op->c.agg); /* mergeState(targetState, merged) */
+            op->accs[m->v] = t;
+        }
+    }
+    return GW_OK;
+}
+
+/* MergingWindowSet.addWindow (MergingWindowSet.java:153-224). */
+static int mws_add_window(wo_op* op, int64_t key, mws_t* m, int64_t ns, int64_t ne,
+                          int64_t* rs_out, int64_t* re_out) {
+    int n = m->n + 1;
+    int64_t* s = (int64_t*)malloc(sizeof(int64_t) * 6 * (size_t)n);
+    int64_t* e = s + n;
+    int64_t* gs = e + n;
+    int64_t* ge = gs + n;
+    int32_t* grp = (int32_t*)(ge + n);
+    for (int i = 0; i < m->n; i++) { s[i] = m->w[4 * i]; e[i] = m->w[4 * i + 1]; }
+    s[m->n] = ns;
+    e[m->n] = ne;
+    int ng = wo_merge_windows(n, s, e, grp, gs, ge);
+
+    int64_t rs = ns, re = ne;
+    int merged_new = 0, any_merge = 0, rc = GW_OK;
+    int64_t* mw = (int64_t*)malloc(sizeof(int64_t) * 2 * (size_t)n);
+    int64_t* msw = (int64_t*)malloc(sizeof(int64_t) * 2 * (size_t)n);
+    for (int g = 0; g < ng && rc == GW_OK; g++) {
+        /* members as a Set (duplicates collapse, TimeWindow.mergeWindows builds a HashSet) */
+        int nm = 0;
+        int has_new = 0;
+        for (int i = 0; i < n; i++) {
+            if (grp[i] != g) continue;
+            int dup = 0;
+            for (int j = 0; j < nm; j++)
+                if (mw[2 * j] == s[i] && mw[2 * j + 1] == e[i]) dup = 1;
+            if (dup) continue;
+            mw[2 * nm] = s[i];
+            mw[2 * nm + 1] = e[i];
+            nm++;
+        }
+        if (nm <= 1) continue; /* mergeWindows only calls back for size > 1 */
+        any_merge = 1;
+        /* mergedWindows.remove(newWindow) */
+        for (int j = 0; j < nm; j++) {
+            if (mw[2 * j] == ns && mw[2 * j + 1] == ne) {
+                has_new = 1;
+                memmove(&mw[2 * j], &mw[2 * j + 2], sizeof(int64_t) * 2 * (size_t)(nm - j - 1));
+                nm--;
+                break;
+            }
+        }
+        if (has_new) { merged_new = 1; rs = gs[g]; re = ge[g]; }
+        /* mergedStateWindow = mapping.get(mergedWindows.iterator().next()) */
+        int fi = mws_find(m, mw[0], mw[1]);
+        int64_t tss = m->w[4 * fi + 2], tse = m->w[4 * fi + 3];
+        int nmsw = 0;
+        for (int j = 0; j < nm; j++) {
+            int64_t a, b;
+            if (mws_remove(m, mw[2 * j], mw[2 * j + 1], &a, &b)) {
+                msw[2 * nmsw] = a;
+                msw[2 * nmsw + 1] = b;
+                nmsw++;
+            }
+        }
+        mws_put(m, gs[g], ge[g], tss, tse);
+        for (int j = 0; j < nmsw; j++) { /* mergedStateWindows.remove(mergedStateWindow) */
+            if (msw[2 * j] == tss && msw[2 * j + 1] == tse) {
+                memmove(&msw[2 * j], &msw[2 * j + 2], sizeof(int64_t) * 2 * (size_t)(nmsw - j - 1));
+                nmsw--;
+                break;
+            }
+        }
+        int contains_result = 0;
+        for (int j = 0; j < nm; j++)
+            if (mw[2 * j] == gs[g] && mw[2 * j + 1] == ge[g]) contains_result = 1;
+        if (!(contains_result && nm == 1))
+            rc = merge_function(op, key, gs[g], ge[g], mw, nm, tss, tse, msw, nmsw);
+    }
+    if (rc == GW_OK && (!any_merge || (rs == ns && re == ne && !merged_new)))
+        mws_put(m, rs, re, rs, re);
+    free(mw);
+    free(msw);
+    free(s);
+    *rs_out = rs;
+    *re_out = re;
+    return rc;
+}
+
+/* ------------------------------------------------------------------------ */
+/* WindowOperator.processElement (WindowOperator.java:293-447)                */
+/* ------------------------------------------------------------------------ */
+int wo_process_element(wo_op* op, int64_t key, int64_t ts, int64_t v) {
+    int64_t ws[64], we[64];
+    int64_t* pws = ws;
+    int64_t* pwe = we;
+    int cap = 64;
+    if (op->c.assigner == GW_SLIDING) {
+        int64_t need = op->c.size / op->c.slide + 2;
+        if (need > cap) {
+            pws = (int64_t*)malloc(sizeof(int64_t) * 2 * (size_t)need);
+            pwe = pws + need;
+            cap = (int)need;
+        }
+    }
+    int nw = wo_assign_windows(&op->c, ts, pws, pwe, cap);
+    int rc = GW_OK;
+    if (nw < 0) {
+        op_err(op, "Record has Long.MIN_VALUE timestamp (= no timestamp marker).");
+        rc = nw;
+        goto out;
+    }
+    int skipped = 1;
+    if (op->c.assigner == GW_SESSION) {
+        mws_t* m = mws_get(op, key, 1);
+        for (int w = 0; w < nw && rc == GW_OK; w++) {
+            int64_t as, ae;
+            rc = mws_add_window(op, key, m, pws[w], pwe[w], &as, &ae);
+            if (rc) break;
+            if (is_window_late(op, ae)) {
+                mws_remove(m, as, ae, NULL, NULL); /* retireWindow */
+                continue;
+            }
+            skipped = 0;
+            int i = mws_find(m, as, ae);
+            if (i < 0) { op_err(op, "Window is not in in-flight window set."); rc = GW_E_STATE; break; }
+            int64_t ss = m->w[4 * i + 2], se = m->w[4 * i + 3];
+            rc = state_add(op, key, ss, se, v);
+            if (rc) break;
+            int r = trigger_on_element(op, key, as, ae, &rc);
+            if (rc) break;
+            if (r & 1) {
+                acc_t* a = state_get(op, key, ss, se);
+                if (a) rc = emit(op, key, as, ae, a);
+            }
+            if (r & 2) state_clear(op, key, ss, se);
+            if (rc == GW_OK) rc = register_cleanup_timer(op, key, as, ae);
+        }
+    } else {
+        for (int w = 0; w < nw && rc == GW_OK; w++) {
+            if (is_window_late(op, pwe[w])) continue;
+            skipped = 0;
+            rc = state_add(op, key, pws[w], pwe[w], v);
+            if (rc) break;
+            int r = trigger_on_element(op, key, pws[w], pwe[w], &rc);
+            if (rc) break;
+            if (r & 1) {
+                acc_t* a = state_get(op, key, pws[w], pwe[w]);
+                if (a) rc = emit(op, key, pws[w], pwe[w], a);
+            }
+            if (r & 2) state_clear(op, key, pws[w], pwe[w]);
+            if (rc == GW_OK) rc = register_cleanup_timer(op, key, pws[w], pwe[w]);
+        }
+    }
+    if (rc == GW_OK && skipped && is_element_late(op, ts)) op->late++;
+out:
+    if (pws != ws) free(pws);
+    return rc;
+}
+
+int wo_process_batch(wo_op* op, int64_t n, const int64_t* key, const int64_t* ts,
+                     const int64_t* v) {
+    for (int64_t i = 0; i < n; i++) {
+        int rc = wo_process_element(op, key[i], ts[i], v ? v[i] : 0);
+        if (rc) return rc;
+    }
+    return GW_OK;
+}
+
+/* WindowOperator.onEventTime (WindowOperator.java:450-494) + clearAllState :560-571 */
+static int on_event_time(wo_op* op, const tmr_t* t) {
+    int64_t ns_s, ns_e;
+    mws_t* m = NULL;
+    if (op->c.assigner == GW_SESSION) {
+        m = mws_get(op, t->key, 0);
+        int i = m ? mws_find(m, t->s, t->e) : -1;
+        if (i < 0) return GW_OK; /* timer for a non-existent window */
+        ns_s = m->w[4 * i + 2];
+        ns_e = m->w[4 * i + 3];
+    } else {
+        ns_s = t->s;
+        ns_e = t->e;
+    }
+    int r = trigger_on_event_time(op, t->ts, t->e);
+    int rc = GW_OK;
+    if (r & 1) {
+        acc_t* a = state_get(op, t->key, ns_s, ns_e);
+        if (a) rc = emit(op, t->key, t->s, t->e, a);
+    }
+    if (r & 2) state_clear(op, t->key, ns_s, ns_e);
+    if (t->ts == cleanup_time(op, t->e)) { /* isCleanupTime */
+        state_clear(op, t->key, ns_s, ns_e);
+        trigger_clear(op, t->key, t->s, t->e);
+        if (m) mws_remove(m, t->s, t->e, NULL, NULL);
+    }
+    return rc;
+}
+
+/* AbstractStreamOperator.processWatermark -> InternalTimerServiceImpl.tryAdvanceWatermark
+ * (InternalTimerServiceImpl.java:328-347): currentWatermark = wm, then poll every
+ * timer with timestamp <= wm. */
+int wo_process_watermark(wo_op* op, int64_t wm) {
+    if (wm <= op->wm) return GW_OK;
+    op->wm = wm;
+    while (op->nheap > 0 && op->heap[0].ts <= wm) {
+        tmr_t t = heap_pop(op);
+        int64_t k[4] = {t.ts, t.key, t.s, t.e};
+        ment_t* m = map_find(&op->timers, k);
+        if (!m || m->v != t.gen) continue; /* deleted (or re-registered later) */
+        map_del(&op->timers, k);
+        int rc = on_event_time(op, &t);
+        if (rc) return rc;
+    }
+    return GW_OK;
+}
+
+/* ------------------------------------------------------------------------ */
+wo_op* wo_create(const gw_config* cfg) {
+    if (wo_validate(cfg) != GW_OK) return NULL;
+    wo_op* op = (wo_op*)calloc(1, sizeof(wo_op));
+    if (!op) return NULL;
+    op->c = *cfg;
+    op->wm = INT64_MIN;
+    if (map_init(&op->state, 1024) || map_init(&op->timers, 1024) || map_init(&op->sets, 256)) {
+        wo_destroy(op);
+        return NULL;
+    }
+    return op;
+}
+
+void wo_destroy(wo_op* op) {
+    if (!op) return;
+    map_free(&op->state);
+    map_free(&op->timers);
+    map_free(&op->sets);
+    for (int64_t i = 0; i < op->nsets; i++) free(op->msets[i].w);
+    free(op->msets);
+    free(op->accs);
+    free(op->freel);
+    free(op->heap);
+    free(op->ok); free(op->os); free(op->oe); free(op->orr);
+    free(op);
+}
+
+int64_t wo_output_count(const wo_op* op) { return op->on - op->ohead; }
+
+int64_t wo_drain(wo_op* op, int64_t* key, int64_t* s, int64_t* e, int64_t* r, int64_t cap) {
+    int64_t n = op->on - op->ohead;
+    if (n > cap) n = cap;
+    for (int64_t i = 0; i < n; i++) {
+        int64_t j = op->ohead + i;
+        if (key) key[i] = op->ok[j];
+        if (s) s[i] = op->os[j];
+        if (e) e[i] = op->oe[j];
+        if (r) r[i] = op->orr[j];
+    }
+    op->ohead += n;
+    if (op->ohead == op->on) op->ohead = op->on = 0;
+    return n;
+}
+
+int64_t wo_late_dropped(const wo_op* op) { return op->late; }
+int64_t wo_current_watermark(const wo_op* op) { return op->wm; }
+int64_t wo_state_entries(const wo_op* op) { return op->state.n; }
+int64_t wo_timer_count(const wo_op* op) { return op->timers.n; }
+int64_t wo_session_merges(const wo_op* op) { return op->merges; }
+const char* wo_last_error(const wo_op* op) { return op ? op->err : "null operator"; }
+
+/* ------------------------------------------------------------------------ */
+/* multi-threaded CPU baseline: one operator per simulated subtask            */
+/* ------------------------------------------------------------------------ */
+typedef struct {
+    const gw_config* cfg;
+    int idx, threads;
+    int64_t nb;
+    const int64_t *blen, *wm, *key, *ts, *val;
+    int64_t rows, checksum;
+    int rc;
+} par_arg;
+
+static void* par_main(void* p) {
+    par_arg* a = (par_arg*)p;
+    wo_op* op = wo_create(a->cfg);
+    if (!op) { a->rc = GW_E_OOM; return NULL; }
+    int32_t maxp = a->cfg->max_parallelism > 0 ? a->cfg->max_parallelism : 128;
+    int64_t off = 0, rows = 0;
+    uint64_t cs = 0;
+    int64_t* bk = (int64_t*)malloc(4 * 8 * 1024);
+    int64_t* bs = bk + 1024;
+    int64_t* be = bs + 1024;
+    int64_t* br = be + 1024;
+    for (int64_t b = 0; b <= a->nb; b++) {
+        if (b < a->nb) {
+            for (int64_t i = off; i < off + a->blen[b]; i++) {
+                int32_t kg = wo_assign_to_key_group(wo_long_hash(a->key[i]), maxp);
+                if (wo_operator_index_for_key_group(maxp, a->threads, kg) != a->idx) continue;
+                int rc = wo_process_element(op, a->key[i], a->ts[i], a->val ? a->val[i] : 0);
+                if (rc) { a->rc = rc; goto done; }
+            }
+            off += a->blen[b];
+        }
+        int rc = wo_process_watermark(op, b < a->nb ? a->wm[b] : INT64_MAX);
+        if (rc) { a->rc = rc; goto done; }
+        int64_t n;
+        while ((n = wo_drain(op, bk, bs, be, br, 1024)) > 0) {
+            for (int64_t i = 0; i < n; i++)
+                cs += (uint64_t)bk[i] * 0x9e3779b97f4a7c15ull ^ (uint64_t)bs[i] * 31u ^
+                      (uint64_t)be[i] * 17u ^ (uint64_t)br[i];
+            rows += n;
+        }
+    }
+done:
+    free(bk);
+    a->rows = rows;
+    a->checksum = (int64_t)cs;
+    wo_destroy(op);
+    return NULL;
+}
+
+int64_t wo_run_parallel(const gw_config* cfg, int threads, int64_t nb, const int64_t* blen,
+                        const int64_t* wm, const int64_t* key, const int64_t* ts,
+                        const int64_t* val, int64_t* checksum, double* seconds) {
+    if (threads < 1) threads = 1;
+    pthread_t* th = (pthread_t*)calloc((size_t)threads, sizeof(pthread_t));
+    par_arg* args = (par_arg*)calloc((size_t)threads, sizeof(par_arg));
+    struct timespec t0, t1;
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    for (int i = 0; i < threads; i++) {
+        args[i] = (par_arg){cfg, i, threads, nb, blen, wm, key, ts, val, 0, 0, 0};
+        pthread_create(&th[i], NULL, par_main, &args[i]);
+    }
+    int64_t rows = 0;
+    uint64_t cs = 0;
+    int rc = 0;
+    for (int i = 0; i < threads; i++) {
+        pthread_join(th[i], NULL);
+        rows += args[i].rows;
+        cs += (uint64_t)args[i].checksum;
+        if (args[i].rc) rc = args[i].rc;
+    }
+    clock_gettime(CLOCK_MONOTONIC, &t1);
+    if (seconds) *seconds = (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
+    if (checksum) *checksum = (int64_t)cs;
+    free(th);
+    free(args);
+    return rc ? rc : rows;
+}

@@ -1,0 +1,79 @@
+/*
+ * flink_oracle.h — TEST INFRASTRUCTURE ONLY.
+ *
+ * A CPU restatement of Apache Flink's keyed event-time window operator
+ * (WindowOperator + HashMapStateBackend + EventTimeTrigger + MergingWindowSet),
+ * used as the parity oracle for libgpuwin.so and as the CPU baseline in
+ * bench.py.  Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline
+ * leg may load it.  The product path (flink_amd/, libgpuwin.so) never does.
+ *
+ * It follows the reference algorithm record by record — one state entry per
+ * (key, window), a deduplicated timer heap, per-key merging window sets —
+ * NOT the GPU's pane/slice design, so the two are independent restatements.
+ *
+ * Pinning: tests/test_oracle_golden.py checks it against every golden vector
+ * transcribed from the reference's own tests (tests/golden/).
+ */
+#ifndef FLINK_ORACLE_H
+#define FLINK_ORACLE_H
+#include <stdint.h>
+#include "../include/gpuwin.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct wo_op wo_op;
+
+/* primitives (MathUtils / KeyGroupRangeAssignment / TimeWindow / JDK hashCode) */
+int32_t wo_murmur_hash(int32_t code);
+int32_t wo_bit_mix(int32_t in);
+int32_t wo_long_to_int_with_bit_mixing(int64_t in);
+int32_t wo_long_hash(int64_t v);
+int32_t wo_string_hash(const uint16_t* utf16, int64_t n);
+int32_t wo_assign_to_key_group(int32_t key_hash, int32_t max_parallelism);
+int32_t wo_operator_index_for_key_group(int32_t max_p, int32_t p, int32_t kg);
+void    wo_key_group_range(int32_t max_p, int32_t p, int32_t idx, int32_t* start, int32_t* end);
+int32_t wo_default_max_parallelism(int32_t p);
+int64_t wo_window_start_with_offset(int64_t ts, int64_t offset, int64_t size);
+/* Windows of one record; returns count (<= cap) or a negative GW_E_* code. */
+int     wo_assign_windows(const gw_config* cfg, int64_t ts, int64_t* start, int64_t* end, int cap);
+/* TimeWindow.mergeWindows on n windows: writes, per input window, the index of its
+ * merge group (groups numbered in sort order) and per group the cover window.
+ * Returns the number of groups. */
+int     wo_merge_windows(int n, const int64_t* start, const int64_t* end,
+                         int32_t* group_of, int64_t* gstart, int64_t* gend);
+
+/* operator */
+int     wo_validate(const gw_config* cfg);
+wo_op*  wo_create(const gw_config* cfg);
+void    wo_destroy(wo_op* op);
+int     wo_process_element(wo_op* op, int64_t key, int64_t ts, int64_t value_bits);
+int     wo_process_batch(wo_op* op, int64_t n, const int64_t* key, const int64_t* ts,
+                         const int64_t* value_bits);
+int     wo_process_watermark(wo_op* op, int64_t wm);
+int64_t wo_output_count(const wo_op* op);
+/* Copies and removes up to cap rows. result is 8 bytes per row (int64 or double). */
+int64_t wo_drain(wo_op* op, int64_t* key, int64_t* start, int64_t* end, int64_t* result_bits,
+                 int64_t cap);
+int64_t wo_late_dropped(const wo_op* op);
+int64_t wo_current_watermark(const wo_op* op);
+int64_t wo_state_entries(const wo_op* op);
+int64_t wo_timer_count(const wo_op* op);
+int64_t wo_session_merges(const wo_op* op);
+const char* wo_last_error(const wo_op* op);
+
+/* Multi-threaded CPU baseline: `threads` operator instances, each owning the key
+ * groups of one subtask (computeKeyGroupRangeForOperatorIndex), like a Flink job
+ * at parallelism = threads.  Runs the whole stream: batches of batch_len records,
+ * each followed by watermark wm[b]; then MAX_WATERMARK.  Returns rows fired and
+ * writes the wall time to *seconds. */
+int64_t wo_run_parallel(const gw_config* cfg, int threads, int64_t n_batches,
+                        const int64_t* batch_len, const int64_t* wm,
+                        const int64_t* key, const int64_t* ts, const int64_t* value_bits,
+                        int64_t* checksum, double* seconds);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

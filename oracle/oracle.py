@@ -1,0 +1,190 @@
+"""ctypes wrapper of the CPU restatement oracle — TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import
+this module; it is the checker, never the thing measured or shipped.  The product
+path (flink_amd/, libgpuwin.so) does not import it and fails loudly without its
+own HIP extension.
+
+The oracle restates Flink's WindowOperator record by record (see
+oracle/flink_oracle.c for per-function reference citations) and is pinned by the
+reference's own golden vectors in tests/golden/ (tests/test_oracle_golden.py).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "libflink_oracle.so")
+
+INT64_MIN = -(1 << 63)
+INT64_MAX = (1 << 63) - 1
+
+ASSIGNERS = {"tumbling": 0, "sliding": 1, "session": 2}
+TRIGGERS = {"event_time": 0, "purging_event_time": 1}
+AGGS = {
+    "count": 0, "sum_i64": 1, "sum_f64": 2, "min_i64": 3, "max_i64": 4,
+    "min_f64": 5, "max_f64": 6, "avg_i64": 7, "avg_f64": 8, "sum_i32": 9,
+}
+DOUBLE_RESULT = {"sum_f64", "min_f64", "max_f64", "avg_i64", "avg_f64"}
+DOUBLE_INPUT = {"sum_f64", "min_f64", "max_f64", "avg_f64"}
+
+
+class GwConfig(ctypes.Structure):
+    """Mirror of gw_config in include/gpuwin.h."""
+    _fields_ = [
+        ("assigner", ctypes.c_int32), ("trigger", ctypes.c_int32),
+        ("size", ctypes.c_int64), ("slide", ctypes.c_int64), ("offset", ctypes.c_int64),
+        ("gap", ctypes.c_int64), ("allowed_lateness", ctypes.c_int64),
+        ("agg", ctypes.c_int32), ("max_parallelism", ctypes.c_int32),
+        ("parallelism", ctypes.c_int32), ("operator_index", ctypes.c_int32),
+        ("device", ctypes.c_int32), ("flags", ctypes.c_int32),
+        ("capacity_hint", ctypes.c_int64), ("max_batch", ctypes.c_int64),
+    ]
+
+
+def make_config(assigner="tumbling", size=0, slide=0, offset=0, gap=0, lateness=0,
+                agg="sum_i64", trigger="event_time", max_parallelism=128, parallelism=1,
+                operator_index=0, device=0, flags=0, capacity_hint=0, max_batch=0) -> GwConfig:
+    c = GwConfig()
+    c.assigner = ASSIGNERS[assigner]
+    c.trigger = TRIGGERS[trigger]
+    c.size, c.slide, c.offset, c.gap = size, slide, offset, gap
+    c.allowed_lateness = lateness
+    c.agg = AGGS[agg]
+    c.max_parallelism, c.parallelism, c.operator_index = max_parallelism, parallelism, operator_index
+    c.device, c.flags, c.capacity_hint, c.max_batch = device, flags, capacity_hint, max_batch
+    return c
+
+
+def build(force: bool = False) -> str:
+    src = os.path.join(_HERE, "flink_oracle.c")
+    if force or not os.path.exists(_LIB_PATH) or os.path.getmtime(_LIB_PATH) < os.path.getmtime(src):
+        subprocess.run(["make", "-C", _HERE, "-s"], check=True)
+    return _LIB_PATH
+
+
+_lib = None
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        L = ctypes.CDLL(_LIB_PATH)
+        i32, i64, p = ctypes.c_int32, ctypes.c_int64, ctypes.c_void_p
+        P64 = ctypes.POINTER(ctypes.c_int64)
+        for name, res, args in [
+            ("wo_murmur_hash", i32, [i32]), ("wo_bit_mix", i32, [i32]),
+            ("wo_long_to_int_with_bit_mixing", i32, [i64]), ("wo_long_hash", i32, [i64]),
+            ("wo_string_hash", i32, [p, i64]), ("wo_assign_to_key_group", i32, [i32, i32]),
+            ("wo_operator_index_for_key_group", i32, [i32, i32, i32]),
+            ("wo_key_group_range", None, [i32, i32, i32, ctypes.POINTER(i32), ctypes.POINTER(i32)]),
+            ("wo_default_max_parallelism", i32, [i32]),
+            ("wo_window_start_with_offset", i64, [i64, i64, i64]),
+            ("wo_assign_windows", ctypes.c_int, [ctypes.POINTER(GwConfig), i64, P64, P64, ctypes.c_int]),
+            ("wo_merge_windows", ctypes.c_int, [ctypes.c_int, P64, P64, ctypes.POINTER(i32), P64, P64]),
+            ("wo_validate", ctypes.c_int, [ctypes.POINTER(GwConfig)]),
+            ("wo_create", p, [ctypes.POINTER(GwConfig)]), ("wo_destroy", None, [p]),
+            ("wo_process_element", ctypes.c_int, [p, i64, i64, i64]),
+            ("wo_process_batch", ctypes.c_int, [p, i64, p, p, p]),
+            ("wo_process_watermark", ctypes.c_int, [p, i64]),
+            ("wo_output_count", i64, [p]), ("wo_drain", i64, [p, p, p, p, p, i64]),
+            ("wo_late_dropped", i64, [p]), ("wo_current_watermark", i64, [p]),
+            ("wo_state_entries", i64, [p]), ("wo_timer_count", i64, [p]),
+            ("wo_session_merges", i64, [p]), ("wo_last_error", ctypes.c_char_p, [p]),
+            ("wo_run_parallel", i64, [ctypes.POINTER(GwConfig), ctypes.c_int, i64, p, p, p, p, p,
+                                       P64, ctypes.POINTER(ctypes.c_double)]),
+        ]:
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+def java_string_hash(s: str) -> int:
+    """JDK String.hashCode over UTF-16 code units (via the oracle)."""
+    units = np.frombuffer(s.encode("utf-16-le"), dtype=np.uint16).copy()
+    return lib().wo_string_hash(units.ctypes.data, len(units))
+
+
+def _p(a: np.ndarray):
+    return a.ctypes.data if a is not None else None
+
+
+class OracleError(RuntimeError):
+    pass
+
+
+class OracleOperator:
+    """One reference WindowOperator instance (one keyed subtask)."""
+
+    def __init__(self, cfg: GwConfig):
+        self.cfg = cfg
+        self._h = lib().wo_create(ctypes.byref(cfg))
+        if not self._h:
+            raise OracleError("invalid window operator configuration")
+
+    def close(self):
+        if self._h:
+            lib().wo_destroy(self._h)
+            self._h = None
+
+    __del__ = close
+
+    def _check(self, rc):
+        if rc != 0:
+            raise OracleError(f"oracle error {rc}: {lib().wo_last_error(self._h).decode()}")
+
+    def process_element(self, key: int, ts: int, value_bits: int = 0):
+        self._check(lib().wo_process_element(self._h, key, ts, value_bits))
+
+    def process_batch(self, key: np.ndarray, ts: np.ndarray, value_bits: np.ndarray | None):
+        key = np.ascontiguousarray(key, dtype=np.int64)
+        ts = np.ascontiguousarray(ts, dtype=np.int64)
+        vb = None if value_bits is None else np.ascontiguousarray(value_bits).view(np.int64)
+        self._check(lib().wo_process_batch(self._h, len(key), _p(key), _p(ts), _p(vb)))
+
+    def process_watermark(self, wm: int):
+        self._check(lib().wo_process_watermark(self._h, wm))
+
+    def drain(self):
+        n = lib().wo_output_count(self._h)
+        k = np.empty(n, np.int64); s = np.empty(n, np.int64)
+        e = np.empty(n, np.int64); r = np.empty(n, np.int64)
+        got = lib().wo_drain(self._h, _p(k), _p(s), _p(e), _p(r), n)
+        assert got == n
+        return k, s, e, r
+
+    @property
+    def late_dropped(self) -> int:
+        return lib().wo_late_dropped(self._h)
+
+    @property
+    def state_entries(self) -> int:
+        return lib().wo_state_entries(self._h)
+
+    @property
+    def session_merges(self) -> int:
+        return lib().wo_session_merges(self._h)
+
+
+def run_parallel(cfg: GwConfig, threads: int, batch_len, wm, key, ts, value_bits):
+    """Multi-threaded CPU baseline (one operator per simulated Flink subtask)."""
+    batch_len = np.ascontiguousarray(batch_len, dtype=np.int64)
+    wm = np.ascontiguousarray(wm, dtype=np.int64)
+    key = np.ascontiguousarray(key, dtype=np.int64)
+    ts = np.ascontiguousarray(ts, dtype=np.int64)
+    vb = None if value_bits is None else np.ascontiguousarray(value_bits).view(np.int64)
+    cs = ctypes.c_int64(0)
+    sec = ctypes.c_double(0)
+    rows = lib().wo_run_parallel(ctypes.byref(cfg), threads, len(batch_len), _p(batch_len),
+                                 _p(wm), _p(key), _p(ts), _p(vb), ctypes.byref(cs), ctypes.byref(sec))
+    if rows < 0:
+        raise OracleError(f"parallel oracle failed: {rows}")
+    return rows, cs.value, sec.value

@@ -1,0 +1,209 @@
+"""Writes the golden vectors of tests/golden/*.json.
+
+Every vector below is transcribed by hand from the reference's own tests (Flink
+2.3-SNAPSHOT at /root/reference, read as text; the reference is Java and cannot be
+compiled or run in this container — SURVEY.md §8c).  The citation next to each block
+names the file:line it comes from.  Only data is recorded: inputs and the outputs the
+reference's assertions expect.
+
+Run:  python tests/golden/make_golden.py   (rewrites the JSON files next to it)
+"""
+import json
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+WOT = ("flink-streaming-java/src/test/java/org/apache/flink/streaming/runtime/operators/"
+       "windowing/WindowOperatorTest.java")
+
+
+def dump(name, obj):
+    with open(os.path.join(HERE, name), "w") as f:
+        json.dump(obj, f, indent=1)
+        f.write("\n")
+
+
+# --------------------------------------------------------------------------------------
+# Key groups: RocksIncrementalCheckpointRescalingTest.java:66-132
+#   assignToKeyGroup(String key, maxParallelism = 10) with a pass-through key selector.
+# --------------------------------------------------------------------------------------
+dump("key_groups.json", {
+    "source": "flink-state-backends/flink-statebackend-rocksdb/src/test/java/org/apache/flink/"
+              "state/rocksdb/RocksIncrementalCheckpointRescalingTest.java:66-132",
+    "max_parallelism": 10,
+    "string_keys": [["8", 0], ["5", 1], ["25", 2], ["13", 3], ["4", 4],
+                    ["7", 5], ["1", 6], ["6", 7], ["9", 8], ["3", 9]],
+})
+
+# --------------------------------------------------------------------------------------
+# TimeWindow.getWindowStartWithOffset: TimeWindowTest.java:32-77  [ts, offset, size, start]
+# --------------------------------------------------------------------------------------
+TWT = "flink-runtime/src/test/java/org/apache/flink/streaming/runtime/operators/windowing/TimeWindowTest.java"
+ws = []
+for ts, st in [(-8, -14), (-7, -7), (-6, -7), (-1, -7), (1, 0), (6, 0), (7, 7), (8, 7)]:
+    ws.append([ts, 0, 7, st])
+for ts, st in [(-10, -11), (-9, -11), (-3, -4), (-2, -4), (-1, -4), (1, -4), (2, -4),
+               (3, 3), (9, 3), (10, 10)]:
+    ws.append([ts, 3, 7, st])
+for ts, st in [(-12, -16), (-7, -9), (-4, -9), (-3, -9), (2, -2), (-1, -2), (1, -2), (-2, -2),
+               (3, -2), (4, -2), (7, 5), (12, 12)]:
+    ws.append([ts, -2, 7, st])
+ws.append([1470902048450, -8 * 3600 * 1000, 24 * 3600 * 1000, 1470844800000])
+dump("window_start.json", {"source": TWT + ":32-77", "cases": ws})
+
+# --------------------------------------------------------------------------------------
+# Assigners: [assigner, size, slide, offset, ts, [[start, end], ...]]
+# --------------------------------------------------------------------------------------
+SEW = ("flink-runtime/src/test/java/org/apache/flink/streaming/runtime/operators/windowing/"
+       "SlidingEventTimeWindowsTest.java")
+TEW = ("flink-runtime/src/test/java/org/apache/flink/streaming/runtime/operators/windowing/"
+       "TumblingEventTimeWindowsTest.java")
+SES = ("flink-streaming-java/src/test/java/org/apache/flink/streaming/runtime/operators/"
+       "windowing/EventTimeSessionWindowsTest.java")
+asg = [
+    # SlidingEventTimeWindowsTest.java:39-70 (size 5000, slide 1000)
+    ["sliding", 5000, 1000, 0, 0, [[-4000, 1000], [-3000, 2000], [-2000, 3000], [-1000, 4000], [0, 5000]]],
+    ["sliding", 5000, 1000, 0, 4999, [[0, 5000], [1000, 6000], [2000, 7000], [3000, 8000], [4000, 9000]]],
+    ["sliding", 5000, 1000, 0, 5000, [[1000, 6000], [2000, 7000], [3000, 8000], [4000, 9000], [5000, 10000]]],
+    # :72-103 (offset 100)
+    ["sliding", 5000, 1000, 100, 100, [[-3900, 1100], [-2900, 2100], [-1900, 3100], [-900, 4100], [100, 5100]]],
+    ["sliding", 5000, 1000, 100, 5099, [[100, 5100], [1100, 6100], [2100, 7100], [3100, 8100], [4100, 9100]]],
+    ["sliding", 5000, 1000, 100, 5100, [[1100, 6100], [2100, 7100], [3100, 8100], [4100, 9100], [5100, 10100]]],
+    # :105-135 (offset -100)
+    ["sliding", 5000, 1000, -100, 0, [[-4100, 900], [-3100, 1900], [-2100, 2900], [-1100, 3900], [-100, 4900]]],
+    ["sliding", 5000, 1000, -100, 4899, [[-100, 4900], [900, 5900], [1900, 6900], [2900, 7900], [3900, 8900]]],
+    ["sliding", 5000, 1000, -100, 4900, [[900, 5900], [1900, 6900], [2900, 7900], [3900, 8900], [4900, 9900]]],
+    # TumblingEventTimeWindowsTest.java:41-52
+    ["tumbling", 5000, 0, 0, 0, [[0, 5000]]],
+    ["tumbling", 5000, 0, 0, 4999, [[0, 5000]]],
+    ["tumbling", 5000, 0, 0, 5000, [[5000, 10000]]],
+    # :70-82 (global offset 100)
+    ["tumbling", 5000, 0, 100, 100, [[100, 5100]]],
+    ["tumbling", 5000, 0, 100, 5099, [[100, 5100]]],
+    ["tumbling", 5000, 0, 100, 5100, [[5100, 10100]]],
+    # :84-97 (global offset -100)
+    ["tumbling", 5000, 0, -100, 0, [[-100, 4900]]],
+    ["tumbling", 5000, 0, -100, 4899, [[-100, 4900]]],
+    ["tumbling", 5000, 0, -100, 4900, [[4900, 9900]]],
+    # EventTimeSessionWindowsTest.java:53-66 (gap 5000; "size" column carries the gap)
+    ["session", 5000, 0, 0, 0, [[0, 5000]]],
+    ["session", 5000, 0, 0, 4999, [[4999, 9999]]],
+    ["session", 5000, 0, 0, 5000, [[5000, 10000]]],
+]
+dump("assigners.json", {"source": [SEW + ":39-135", TEW + ":41-97", SES + ":53-66"], "cases": asg})
+
+# --------------------------------------------------------------------------------------
+# TimeWindow.mergeWindows via EventTimeSessionWindows.mergeWindows:
+#   [[input windows], [[merged members...], cover], ...]  (only groups of size > 1)
+# --------------------------------------------------------------------------------------
+dump("merge_windows.json", {"source": SES + ":68-165", "cases": [
+    [[[0, 0]], []],                                   # testMergeSinglePointWindow
+    [[[0, 1]], []],                                   # testMergeSingleWindow
+    [[[0, 1], [1, 2], [2, 3], [4, 5], [5, 6]],        # testMergeConsecutiveWindows
+     [[[[0, 1], [1, 2], [2, 3]], [0, 3]], [[[4, 5], [5, 6]], [4, 6]]]],
+    [[[1, 1], [0, 2], [4, 7], [5, 6]],                # testMergeCoveringWindow
+     [[[[1, 1], [0, 2]], [0, 2]], [[[5, 6], [4, 7]], [4, 7]]]],
+]})
+
+# --------------------------------------------------------------------------------------
+# Operator harness tests (KeyedOneInputStreamOperatorTestHarness, HashMapStateBackend).
+# ops: ["e", key, value, ts] | ["w", wm, [expected rows]]
+# expected row: [key, result, timestamp(=end-1), start|null, end|null]
+# Snapshot/restore points of the reference tests do not change the expected output
+# and are recorded as ["snapshot"] markers.
+# --------------------------------------------------------------------------------------
+common_in = [["e", "key2", 1, 3999], ["e", "key2", 1, 3000], ["e", "key1", 1, 20],
+             ["e", "key1", 1, 0], ["e", "key1", 1, 999], ["e", "key2", 1, 1998],
+             ["e", "key2", 1, 1999], ["e", "key2", 1, 1000]]
+ops_tests = []
+# testSlidingEventTimeWindows (:116-219): SlidingEventTimeWindows.of(3s, 1s), SumReducer
+ops_tests.append({
+    "name": "sliding_3s_1s_sum", "source": WOT + ":116-219",
+    "config": {"assigner": "sliding", "size": 3000, "slide": 1000, "agg": "sum_i32"},
+    "ops": common_in + [
+        ["w", 999, [["key1", 3, 999, None, None]]],
+        ["w", 1999, [["key1", 3, 1999, None, None], ["key2", 3, 1999, None, None]]],
+        ["w", 2999, [["key1", 3, 2999, None, None], ["key2", 3, 2999, None, None]]],
+        ["snapshot"],
+        ["w", 3999, [["key2", 5, 3999, None, None]]],
+        ["w", 4999, [["key2", 2, 4999, None, None]]],
+        ["w", 5999, [["key2", 2, 5999, None, None]]],
+        ["w", 6999, []], ["w", 7999, []]],
+    "late": 0,
+})
+# testTumblingEventTimeWindows (:333-434): TumblingEventTimeWindows.of(3s), SumReducer
+ops_tests.append({
+    "name": "tumbling_3s_sum", "source": WOT + ":333-434",
+    "config": {"assigner": "tumbling", "size": 3000, "agg": "sum_i32"},
+    "ops": common_in + [
+        ["w", 999, []], ["w", 1999, []], ["snapshot"],
+        ["w", 2999, [["key1", 3, 2999, None, None], ["key2", 3, 2999, None, None]]],
+        ["w", 3999, []], ["w", 4999, []],
+        ["w", 5999, [["key2", 2, 5999, None, None]]],
+        ["w", 6999, []], ["w", 7999, []]],
+    "late": 0,
+})
+# testSessionWindows (:543-632) and testReduceSessionWindows (:730-816): gap 3s,
+# SessionWindowFunction / ReducedSessionWindowFunction emit (key-sum, start, end)@end-1.
+sess_ops = [["e", "key2", 1, 0], ["e", "key2", 2, 1000], ["e", "key2", 3, 2500],
+            ["e", "key1", 1, 10], ["e", "key1", 2, 1000], ["snapshot"],
+            ["e", "key1", 3, 2500], ["e", "key2", 4, 5501], ["e", "key2", 5, 6000],
+            ["e", "key2", 5, 6000], ["e", "key2", 6, 6050],
+            ["w", 12000, [["key1", 6, 5499, 10, 5500], ["key2", 6, 5499, 0, 5500],
+                          ["key2", 20, 9049, 5501, 9050]]],
+            ["e", "key2", 10, 15000], ["e", "key2", 20, 15000],
+            ["w", 17999, [["key2", 30, 17999, 15000, 18000]]]]
+ops_tests.append({"name": "session_3s_sum", "source": WOT + ":543-632",
+                  "config": {"assigner": "session", "gap": 3000, "agg": "sum_i32"},
+                  "ops": sess_ops, "late": 0})
+red_ops = [["e", "key2", 1, 0], ["e", "key2", 2, 1000], ["e", "key2", 3, 2500], ["snapshot"],
+           ["e", "key1", 1, 10], ["e", "key1", 2, 1000], ["e", "key1", 3, 2500],
+           ["e", "key2", 4, 5501], ["e", "key2", 5, 6000], ["e", "key2", 5, 6000],
+           ["e", "key2", 6, 6050],
+           ["w", 12000, [["key1", 6, 5499, 10, 5500], ["key2", 6, 5499, 0, 5500],
+                         ["key2", 20, 9049, 5501, 9050]]],
+           ["e", "key2", 10, 15000], ["e", "key2", 20, 15000],
+           ["w", 17999, [["key2", 30, 17999, 15000, 18000]]]]
+ops_tests.append({"name": "reduce_session_3s_sum", "source": WOT + ":730-816",
+                  "config": {"assigner": "session", "gap": 3000, "agg": "sum_i32"},
+                  "ops": red_ops, "late": 0})
+# testLateness (:2038-2137): Tumbling 2s, PurgingTrigger(EventTimeTrigger), lateness 500,
+# late element 1998 goes to the side output (counted as late_dropped here).
+ops_tests.append({
+    "name": "lateness_tumbling_2s_purging", "source": WOT + ":2038-2137",
+    "config": {"assigner": "tumbling", "size": 2000, "agg": "sum_i32", "lateness": 500,
+               "trigger": "purging_event_time"},
+    "ops": [["e", "key2", 1, 500], ["w", 1500, []],
+            ["e", "key2", 1, 1300], ["w", 2300, [["key2", 2, 1999, None, None]]],
+            ["e", "key2", 1, 1997], ["w", 6000, [["key2", 1, 1999, None, None]]],
+            ["e", "key2", 1, 1998], ["w", 7000, []]],
+    "late": 1,
+})
+# testCleanupTimeOverflow (:2139-2248): Tumbling 1000 ms, lateness 2000,
+# ts = Long.MAX_VALUE - 1750 -> window [MAX-1807, MAX-807), maxTs = MAX - 808.
+MAXL = (1 << 63) - 1
+_ts = MAXL - 1750
+_start = _ts - (_ts % 1000)
+ops_tests.append({
+    "name": "cleanup_time_overflow", "source": WOT + ":2139-2248",
+    "config": {"assigner": "tumbling", "size": 1000, "agg": "sum_i32", "lateness": 2000},
+    "ops": [["e", "key2", 1, _ts], ["w", MAXL - 1500, []],
+            ["w", _start + 999, [["key2", 1, _start + 999, None, None]]]],
+    "late": 0,
+})
+# SessionWindowing example (flink-examples-streaming SessionWindowing.java:58-69, gap 3 ms
+# at :94, sum(2)) with expected output SessionWindowingData.java:23-24.  The tuple's f1
+# (first element's timestamp) equals the session start for this input.
+EXS = "flink-examples/flink-examples-streaming/src/main/java/org/apache/flink/streaming/examples/windowing/"
+ops_tests.append({
+    "name": "session_windowing_example", "source": [EXS + "SessionWindowing.java:58-94",
+                                                    EXS + "util/SessionWindowingData.java:23-24"],
+    "config": {"assigner": "session", "gap": 3, "agg": "sum_i32"},
+    "ops": [["e", "a", 1, 1], ["e", "b", 1, 1], ["e", "b", 1, 3], ["e", "b", 1, 5],
+            ["e", "c", 1, 6], ["e", "a", 1, 10], ["e", "c", 1, 11],
+            ["w", MAXL, [["a", 1, 3, 1, 4], ["c", 1, 8, 6, 9], ["c", 1, 13, 11, 14],
+                         ["b", 3, 7, 1, 8], ["a", 1, 12, 10, 13]]]],
+    "late": 0,
+})
+dump("operator_harness.json", {"tests": ops_tests})
+
+print("golden vectors written to", HERE)

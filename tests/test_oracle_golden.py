@@ -1,0 +1,183 @@
+"""Pins the CPU oracle (oracle/flink_oracle.c) to the reference's own golden vectors
+(tests/golden/, transcribed from Flink's tests — see make_golden.py for file:line)."""
+import ctypes
+
+import numpy as np
+import pytest
+
+from tests.harness import itcase_expected_sum, itcase_stream, load_golden, replay, config_kwargs
+
+
+def test_key_groups_kat(oracle_lib):
+    o = oracle_lib
+    g = load_golden("key_groups.json")
+    for key, group in g["string_keys"]:
+        h = o.java_string_hash(key)
+        assert o.lib().wo_assign_to_key_group(h, g["max_parallelism"]) == group, key
+
+
+def test_murmur_known_properties(oracle_lib):
+    L = oracle_lib.lib()
+    # murmurHash is non-negative for every input (MathUtils.java:150-155)
+    for x in [0, 1, -1, 2**31 - 1, -(2**31), 123456789, -987654321]:
+        assert L.wo_murmur_hash(x) >= 0
+    # Long.hashCode (JDK): (int)(v ^ (v >>> 32))
+    assert L.wo_long_hash(0) == 0
+    assert L.wo_long_hash(1) == 1
+    assert L.wo_long_hash(-1) == 0
+    assert L.wo_long_hash(1 << 32) == 1
+    assert L.wo_long_hash(-(1 << 63)) == -(1 << 31)
+
+
+def test_key_group_ranges(oracle_lib):
+    L = oracle_lib.lib()
+    assert L.wo_default_max_parallelism(1) == 128
+    assert L.wo_default_max_parallelism(100) == 256
+    assert L.wo_default_max_parallelism(30000) == 32768
+    for p in [1, 2, 3, 4, 7, 8]:
+        covered = []
+        for i in range(p):
+            s, e = ctypes.c_int32(), ctypes.c_int32()
+            L.wo_key_group_range(128, p, i, ctypes.byref(s), ctypes.byref(e))
+            covered.extend(range(s.value, e.value + 1))
+            for kg in range(s.value, e.value + 1):
+                assert L.wo_operator_index_for_key_group(128, p, kg) == i
+        assert covered == list(range(128))
+
+
+def test_window_start_with_offset(oracle_lib):
+    L = oracle_lib.lib()
+    for ts, off, size, start in load_golden("window_start.json")["cases"]:
+        assert L.wo_window_start_with_offset(ts, off, size) == start, (ts, off, size)
+
+
+def test_assigners(oracle_lib):
+    o = oracle_lib
+    for kind, size, slide, off, ts, windows in load_golden("assigners.json")["cases"]:
+        if kind == "session":
+            cfg = o.make_config(assigner="session", gap=size)
+        else:
+            cfg = o.make_config(assigner=kind, size=size, slide=slide or size, offset=off)
+        s = np.zeros(16, np.int64)
+        e = np.zeros(16, np.int64)
+        P = ctypes.POINTER(ctypes.c_int64)
+        n = o.lib().wo_assign_windows(ctypes.byref(cfg), ts, s.ctypes.data_as(P), e.ctypes.data_as(P), 16)
+        got = sorted(zip(s[:n].tolist(), e[:n].tolist()))
+        assert got == sorted(tuple(w) for w in windows), (kind, ts)
+
+
+def test_assign_rejects_no_timestamp(oracle_lib):
+    o = oracle_lib
+    cfg = o.make_config(assigner="tumbling", size=1000, slide=1000)
+    s = np.zeros(2, np.int64)
+    P = ctypes.POINTER(ctypes.c_int64)
+    assert o.lib().wo_assign_windows(ctypes.byref(cfg), -(1 << 63), s.ctypes.data_as(P),
+                                     s.ctypes.data_as(P), 2) == -6
+
+
+def test_config_validation(oracle_lib):
+    o = oracle_lib
+    L = o.lib()
+    bad = [
+        o.make_config(assigner="tumbling", size=1000, offset=1000),
+        o.make_config(assigner="tumbling", size=0),
+        o.make_config(assigner="sliding", size=1000, slide=100, offset=-100),
+        o.make_config(assigner="sliding", size=0, slide=100),
+        o.make_config(assigner="sliding", size=10**9, slide=1),
+        o.make_config(assigner="session", gap=0),
+        o.make_config(assigner="tumbling", size=1000, lateness=-1),
+    ]
+    for c in bad:
+        assert L.wo_validate(ctypes.byref(c)) == -1
+    assert L.wo_validate(ctypes.byref(o.make_config(assigner="sliding", size=1000, slide=300))) == 0
+
+
+def test_merge_windows(oracle_lib):
+    L = oracle_lib.lib()
+    P = ctypes.POINTER(ctypes.c_int64)
+    for windows, merges in load_golden("merge_windows.json")["cases"]:
+        n = len(windows)
+        s = np.array([w[0] for w in windows], np.int64)
+        e = np.array([w[1] for w in windows], np.int64)
+        grp = np.zeros(n, np.int32)
+        gs = np.zeros(n, np.int64)
+        ge = np.zeros(n, np.int64)
+        ng = L.wo_merge_windows(n, s.ctypes.data_as(P), e.ctypes.data_as(P),
+                                grp.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)),
+                                gs.ctypes.data_as(P), ge.ctypes.data_as(P))
+        got = []
+        for g in range(ng):
+            members = sorted({(int(s[i]), int(e[i])) for i in range(n) if grp[i] == g})
+            if len(members) > 1:
+                got.append((members, (int(gs[g]), int(ge[g]))))
+        exp = [(sorted(tuple(m) for m in mm), tuple(c)) for mm, c in merges]
+        assert sorted(got) == sorted(exp)
+
+
+@pytest.mark.parametrize("test", load_golden("operator_harness.json")["tests"], ids=lambda t: t["name"])
+def test_operator_harness_vectors(oracle_lib, test):
+    o = oracle_lib
+
+    class Backend:
+        def __init__(self, cfg):
+            self.op = o.OracleOperator(o.make_config(**config_kwargs(cfg)))
+
+        def process_element(self, k, ts, v):
+            self.op.process_element(k, ts, v)
+
+        def process_watermark(self, wm):
+            self.op.process_watermark(wm)
+
+        def drain(self):
+            return self.op.drain()
+
+        @property
+        def late_dropped(self):
+            return self.op.late_dropped
+
+    assert replay(test, Backend) == []
+
+
+@pytest.mark.parametrize("assigner,size,slide", [("tumbling", 1000, 1000), ("sliding", 1000, 100)])
+def test_itcase_closed_form(oracle_lib, assigner, size, slide):
+    """EventTimeWindowCheckpointingITCase (flink-tests/.../EventTimeWindowCheckpointingITCase.java:
+    314-383 tumbling, 480-552 sliding; generator :798-838, validator :749-771), scaled to
+    10 keys x 3000 elements."""
+    o = oracle_lib
+    nk, n = 10, 3000
+    keys, ts, vals, blen, wm = itcase_stream(nk, n, size)
+    op = o.OracleOperator(o.make_config(assigner=assigner, size=size, slide=slide, agg="sum_i32"))
+    off = 0
+    rows = []
+    for b in range(n):
+        op.process_batch(keys[off:off + blen[b]], ts[off:off + blen[b]], vals[off:off + blen[b]])
+        off += blen[b]
+        op.process_watermark(int(wm[b]))
+        rows.append(op.drain())
+    op.process_watermark((1 << 63) - 1)
+    rows.append(op.drain())
+    k = np.concatenate([r[0] for r in rows]); s = np.concatenate([r[1] for r in rows])
+    e = np.concatenate([r[2] for r in rows]); r = np.concatenate([r[3] for r in rows])
+    assert op.late_dropped == 0
+    for i in range(len(k)):
+        assert r[i] == itcase_expected_sum(int(s[i]), int(e[i]), n)
+    # every key gets every window that overlaps [0, n)
+    n_windows = len({(int(a), int(b)) for a, b in zip(s, e)})
+    assert len(k) == nk * n_windows
+    expected_windows = (n + size - 1) // slide if assigner == "sliding" else n // size
+    assert n_windows == expected_windows
+
+
+def test_parallel_matches_single(oracle_lib):
+    o = oracle_lib
+    rng = np.random.default_rng(7)
+    n = 20000
+    keys = rng.integers(0, 500, n).astype(np.int64)
+    ts = np.sort(rng.integers(0, 20000, n)).astype(np.int64)
+    vals = rng.integers(-1000, 1000, n).astype(np.int64)
+    blen = np.full(20, n // 20, np.int64)
+    wm = np.array([ts[(i + 1) * (n // 20) - 1] - 50 for i in range(20)], np.int64)
+    cfg = o.make_config(assigner="sliding", size=1000, slide=250, agg="sum_i64")
+    r1, c1, _ = o.run_parallel(cfg, 1, blen, wm, keys, ts, vals)
+    r4, c4, _ = o.run_parallel(cfg, 4, blen, wm, keys, ts, vals)
+    assert r1 == r4 and c1 == c4 and r1 > 0
