@@ -1,0 +1,325 @@
+#!/usr/bin/env python3
+"""bench.py — events/sec of keyed sliding-window aggregation on MI355X (BASELINE.json metric).
+
+Workload (BASELINE.json configs[2], SURVEY.md §8d "Config 3"): Nexmark Q5 shape — keyBy(auction)
+.window(SlidingEventTimeWindows.of(10 s, 2 s)) over 10M distinct keys, synthetic bids
+(auction = splitmix64(i) mod 10M, value = splitmix64(i') mod 1e6), 100M events per 2-s pane
+per GPU, bounded disorder 100 ms, a watermark every 200 ms of event time (= one step).
+Aggregate defaults to SUM over int64 (the north star's "keyed sliding-window sum"); --agg count
+gives the Q5 count.
+
+One step = one watermark batch: (multi-GPU: partition by key group -> RCCL all-to-all) ->
+gw_ingest_device -> gw_advance_watermark (fires every 10th step) -> fired rows consumed
+(discarded, like the reference's DiscardingSink).  Inputs are pre-generated in HBM before
+the timed region.  N GPUs = N processes, key groups sharded by
+KeyGroupRangeAssignment.computeKeyGroupRangeForOperatorIndex, weak scaling (each rank
+generates the same number of events over the full key space).
+
+Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+
+C1 = -7046029254386353131   # 0x9E3779B97F4A7C15 as int64
+C2 = -4658895280553007687   # 0xBF58476D1CE4E5B9
+C3 = -7723592293110705685   # 0x94D049BB133111EB
+MASK63 = (1 << 63) - 1
+
+
+def splitmix64(idx: torch.Tensor, seed: int) -> torch.Tensor:
+    """splitmix64(seed + (i+1)*golden) on int64 tensors (wrapping arithmetic)."""
+    z = (idx + 1) * C1 + seed
+    z = (z ^ ((z >> 30) & ((1 << 34) - 1))) * C2
+    z = (z ^ ((z >> 27) & ((1 << 37) - 1))) * C3
+    return z ^ ((z >> 31) & ((1 << 33) - 1))
+
+
+def log(msg):
+    print(f"[bench] {msg}", file=sys.stderr, flush=True)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--agg", default="sum_i64")
+    ap.add_argument("--keys", type=int, default=10_000_000)
+    ap.add_argument("--events-per-pane", type=int, default=100_000_000, help="per GPU, per 2-s pane")
+    ap.add_argument("--size-ms", type=int, default=10_000)
+    ap.add_argument("--slide-ms", type=int, default=2_000)
+    ap.add_argument("--wm-interval-ms", type=int, default=200)
+    ap.add_argument("--disorder-ms", type=int, default=100)
+    ap.add_argument("--exchange", choices=["a2a", "none"], default="a2a",
+                    help="a2a: RCCL all-to-all keyBy exchange; none: each rank generates only its own key groups")
+    ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--preagg", choices=["auto", "force", "off"], default="auto")
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        if world == 1 and args.gpus > 1:
+            raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run (one rank per GPU)")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+
+    from flink_amd import _native as N
+    from flink_amd import windowing as W
+
+    agg = args.agg
+    size, slide = args.size_ms, args.slide_ms
+    E = args.events_per_pane
+    nb = E * args.wm_interval_ms // slide           # events per step per rank
+    steps_total = args.warmup + args.steps
+    K = args.keys
+    maxp = 128
+    b_in = 16 if agg == "count" else 24
+    s_acc = 16 if agg.startswith("avg") else 8
+
+    # ------------------------------------------------------------------ data
+    t_gen = time.time()
+    n_all = nb * steps_total
+    idx = torch.arange(n_all, device=dev, dtype=torch.int64)
+    seed = 0x5EED0005 + 7919 * rank
+    keys = (splitmix64(idx, seed) & MASK63) % K
+    if args.exchange == "none" and world > 1:
+        # key-partitioned source: remap every key onto this rank's key groups
+        kg = torch.empty(n_all, dtype=torch.int32, device=dev)
+        owner = torch.empty_like(kg)
+        N.check(N.lib().gw_key_groups_device(n_all, keys.data_ptr(), None, maxp, world, kg.data_ptr(),
+                                             owner.data_ptr(), None))
+        torch.cuda.synchronize()
+        keys = keys[owner == rank]
+        n_all = keys.numel() // steps_total * steps_total
+        keys = keys[:n_all]
+        nb = n_all // steps_total
+        idx = torch.arange(n_all, device=dev, dtype=torch.int64)
+    t0_ms = 1_700_000_000_000
+    jitter = (splitmix64(idx, seed ^ 0x77) & MASK63) % (args.disorder_ms + 1)
+    ts = t0_ms + (idx * slide) // E - jitter
+    vals = None
+    if agg != "count":
+        v = (splitmix64(idx, seed ^ 0x1234) & MASK63) % 1_000_000
+        vals = v.to(torch.float64).view(torch.int64) if agg.endswith("f64") else v
+    del idx, jitter
+    # watermark after step b: BoundedOutOfOrdernessWatermarks (maxTs - bound - 1) over the
+    # un-jittered maximum, identical on every rank
+    wms = [t0_ms + (((b + 1) * nb - 1) * slide) // E - args.disorder_ms - 1 for b in range(steps_total)]
+    torch.cuda.synchronize()
+    log(f"rank {rank}: generated {n_all} events ({n_all * b_in / 1e9:.1f} GB) in {time.time() - t_gen:.1f}s")
+
+    flags = {"auto": 0, "force": N.FLAG_FORCE_LDS_PREAGG, "off": N.FLAG_NO_LDS_PREAGG}[args.preagg]
+    op = W.GpuWindowOperator(W.SlidingEventTimeWindows.of(size, slide), agg, capacity_hint=max(K // world, 1024),
+                             max_parallelism=maxp, parallelism=world, operator_index=rank, device=local,
+                             flags=flags, max_batch=nb * 2).open()
+    op_stream = op.stream()
+    cur = torch.cuda.current_stream().cuda_stream
+
+    # exchange buffers (multi-GPU)
+    if world > 1 and args.exchange == "a2a":
+        pk = torch.empty(nb, dtype=torch.int64, device=dev)
+        pt = torch.empty_like(pk)
+        pv = torch.empty_like(pk) if vals is not None else None
+        counts = torch.empty(world, dtype=torch.int64, device=dev)
+        rcounts = torch.empty_like(counts)
+        scratch = torch.empty(N.lib().gw_partition_scratch_bytes(nb, world), dtype=torch.uint8, device=dev)
+        rk = torch.empty(nb * 2, dtype=torch.int64, device=dev)
+        rt = torch.empty_like(rk)
+        rv = torch.empty_like(rk) if vals is not None else None
+
+    exch_bytes = 0
+    d_b = []  # distinct (key, pane) accumulators per timed batch (rank-local)
+
+    def step(b, timed):
+        nonlocal exch_bytes
+        lo, hi = b * nb, (b + 1) * nb
+        k, t, v = keys[lo:hi], ts[lo:hi], (vals[lo:hi] if vals is not None else None)
+        if world > 1 and args.exchange == "a2a":
+            N.check(N.lib().gw_partition_device(nb, k.data_ptr(), None, t.data_ptr(),
+                                                v.data_ptr() if v is not None else None, maxp, world,
+                                                pk.data_ptr(), pt.data_ptr(),
+                                                pv.data_ptr() if v is not None else None,
+                                                counts.data_ptr(), scratch.data_ptr(), cur))
+            dist.all_to_all_single(rcounts, counts)
+            sc = counts.tolist()
+            rc = rcounts.tolist()
+            nrecv = sum(rc)
+            dist.all_to_all_single(rk[:nrecv], pk, rc, sc)
+            dist.all_to_all_single(rt[:nrecv], pt, rc, sc)
+            if v is not None:
+                dist.all_to_all_single(rv[:nrecv], pv, rc, sc)
+            k, t, v = rk[:nrecv], rt[:nrecv], (rv[:nrecv] if v is not None else None)
+            if timed:
+                exch_bytes += (nb - sc[rank]) * b_in
+        n = k.numel()
+        N.check(N.lib().gw_ingest_device(op.handle, n, k.data_ptr(), None, t.data_ptr(),
+                                         v.data_ptr() if v is not None else None, cur), op.handle)
+        wm = wms[b]
+        if world > 1:
+            w = torch.tensor([wm], dtype=torch.int64, device=dev)
+            dist.all_reduce(w, op=dist.ReduceOp.MIN)  # StatusWatermarkValve: min over inputs
+            wm = int(w.item())
+        op.advance_watermark(wm)
+        op.clear_rows()  # DiscardingSink
+        return k, t
+
+    op.enable_kernel_timing(True)
+    for b in range(args.warmup):
+        step(b, False)
+    op.kernel_time_ms(0)
+    op.kernel_time_ms(1)  # reset timers after warmup
+    st0 = op.stats()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    last = t0
+    for b in range(args.warmup, steps_total):
+        step(b, True)
+        if rank == 0 and time.perf_counter() - last > 30:
+            last = time.perf_counter()
+            log(f"step {b - args.warmup + 1}/{args.steps}")
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        e = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        elapsed = float(e.item())
+    ingest_ms, ingest_launches = op.kernel_time_ms(0)
+    fire_ms, fire_launches = op.kernel_time_ms(1)
+    st1 = op.stats()
+    events_rank = nb * args.steps
+    rows_rank = st1["rows_fired"] - st0["rows_fired"]
+
+    # ------------------------------------------ algorithmic bytes
+    # D_b: distinct (key, pane) accumulators each timed batch touches.  Exact on the
+    # rank's own generated batches (N=1: the ingested batch itself).
+    g = int(np.gcd(size, slide))
+    dsum = 0
+    for b in range(args.warmup, steps_total):
+        lo, hi = b * nb, (b + 1) * nb
+        comp = keys[lo:hi] * 4096 + ((ts[lo:hi] // g) % 4096)
+        dsum += int(torch.unique(comp).numel())
+    ingest_bytes_total = events_rank * b_in + 2 * s_acc * dsum
+    fire_bytes_total = rows_rank * (32 + s_acc)
+    per_launch = ingest_bytes_total / max(ingest_launches, 1)
+    achieved = per_launch / (ingest_ms / 1e3) / 1e9 if ingest_ms > 0 else 0.0
+    pipeline_gbs = (ingest_bytes_total + fire_bytes_total) / elapsed / 1e9
+
+    tot = torch.tensor([events_rank, rows_rank], dtype=torch.int64, device=dev)
+    if dist:
+        dist.all_reduce(tot)
+    events_all, rows_all = int(tot[0].item()), int(tot[1].item())
+    value = events_all / elapsed
+
+    # ------------------------------------------------------------ CPU baseline
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args, keys, ts, vals, wms, nb, agg, size, slide)
+
+    if rank == 0:
+        out = {
+            "metric": "events/sec keyed sliding-window agg at 1/2/4/8 GPUs; % of HBM roofline",
+            "value": value,
+            "unit": "events/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed * 1e3 / args.steps,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64" if agg.endswith("f64") else "int64",
+            "data": "synthetic (splitmix64 Nexmark-Q5-shaped bids, generated in HBM)",
+            "config": {
+                "workload": f"nexmark_q5_sliding_{size // 1000}s_{slide // 1000}s_{agg}",
+                "keys": K, "events_per_pane_per_gpu": E, "events_per_step_per_gpu": nb,
+                "watermark_interval_ms": args.wm_interval_ms, "disorder_ms": args.disorder_ms,
+                "window": {"assigner": "sliding", "size_ms": size, "slide_ms": slide},
+                "aggregate": agg, "max_parallelism": maxp,
+                "parallelism": f"keygroup-sharded x{world}" + (f" ({args.exchange} exchange)" if world > 1 else ""),
+            },
+            "roofline": {
+                "bound": "hbm", "kernel": "k_ingest (pane RMW)",
+                "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                "bytes_per_launch": per_launch, "avg_launch_ms": ingest_ms, "launches": ingest_launches,
+                "pipeline_achieved": pipeline_gbs, "pipeline_frac": pipeline_gbs / HBM_PEAK_GBS,
+                "fire_avg_launch_ms": fire_ms, "fire_launches": fire_launches,
+                "d_over_n": dsum / max(events_rank, 1),
+            },
+            "rows_fired": rows_all,
+            "cpu_baseline": cpu,
+        }
+        if world > 1:
+            out["exchange_gbs_per_gpu"] = exch_bytes / elapsed / 1e9
+        print(json.dumps(out), flush=True)
+    op.close()
+    if dist:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(args, keys, ts, vals, wms, nb, agg, size, slide):
+    """CPU restatement of Flink's operator (oracle/, 'port') on the host cores: one operator
+    per simulated subtask thread over a bounded prefix of the same stream."""
+    try:
+        from oracle import oracle as O
+        O.build()
+    except Exception as e:  # noqa: BLE001
+        return {"value": None, "unit": "events/s", "cores": 0, "kind": "port", "sample": f"unavailable: {e}"}
+    threads = min(16, os.cpu_count() or 1)
+    cfg = O.make_config(assigner="sliding", size=size, slide=slide, agg=agg, max_parallelism=128)
+
+    def run(nbatches, per_batch):
+        n = nbatches * per_batch
+        k = keys[:n].cpu().numpy()
+        t = ts[:n].cpu().numpy()
+        v = vals[:n].cpu().numpy() if vals is not None else None
+        blen = np.full(nbatches, per_batch, np.int64)
+        wm = np.array(wms[:nbatches], np.int64) if per_batch == nb else \
+            np.array([int(t[(b + 1) * per_batch - 1]) - args.disorder_ms - 1 for b in range(nbatches)], np.int64)
+        rows, _, sec = O.run_parallel(cfg, threads, blen, wm, k, t, v)
+        return n, sec, rows
+
+    # calibrate on 1/50 of a step, then size the sample for ~cpu_baseline_seconds
+    n0, s0, _ = run(1, max(nb // 50, 10000))
+    rate0 = n0 / max(s0, 1e-6)
+    target = int(rate0 * args.cpu_baseline_seconds)
+    nbatches = max(1, min(len(wms), target // nb))
+    if target < nb:
+        n, sec, rows = run(1, max(target, 10000))
+        sample = f"first {n} events of the GPU stream as one batch + final watermark"
+    else:
+        n, sec, rows = run(nbatches, nb)
+        sample = f"first {nbatches} watermark batches ({n} events) of the GPU stream + final watermark"
+    return {"value": n / sec, "unit": "events/s", "cores": threads, "kind": "port", "sample": sample,
+            "seconds": sec, "rows": rows}
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,134 @@
+"""ctypes binding of libgpuwin.so (include/gpuwin.h).
+
+The product path has no CPU fallback: if the HIP library is missing or cannot be
+loaded, import-time use fails loudly with NativeLibraryError.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libgpuwin.so")
+
+GW_OK = 0
+ERRORS = {
+    -1: "GW_E_INVALID", -2: "GW_E_UNSUPPORTED", -3: "GW_E_DEVICE", -4: "GW_E_OOM",
+    -5: "GW_E_OUTPUT_FULL", -6: "GW_E_NO_TIMESTAMP", -7: "GW_E_RANGE", -8: "GW_E_STATE",
+}
+GW_E_OUTPUT_FULL = -5
+
+ASSIGNERS = {"tumbling": 0, "sliding": 1, "session": 2}
+TRIGGERS = {"event_time": 0, "purging_event_time": 1}
+AGGS = {
+    "count": 0, "sum_i64": 1, "sum_f64": 2, "min_i64": 3, "max_i64": 4,
+    "min_f64": 5, "max_f64": 6, "avg_i64": 7, "avg_f64": 8, "sum_i32": 9,
+}
+DOUBLE_RESULT = {"sum_f64", "min_f64", "max_f64", "avg_i64", "avg_f64"}
+DOUBLE_INPUT = {"sum_f64", "min_f64", "max_f64", "avg_f64"}
+
+FLAG_FORCE_LDS_PREAGG = 1
+FLAG_NO_LDS_PREAGG = 2
+FLAG_CHECK_KEY_GROUPS = 4
+
+EXPORTS = [
+    "gw_create", "gw_destroy", "gw_last_error", "gw_abi_version", "gw_ingest", "gw_ingest_device",
+    "gw_advance_watermark", "gw_end_input", "gw_pending_rows", "gw_drain", "gw_rows_device",
+    "gw_clear_rows", "gw_late_dropped", "gw_get_stats", "gw_synchronize", "gw_stream",
+    "gw_kernel_time_ms", "gw_enable_kernel_timing", "gw_java_long_hash", "gw_murmur_hash",
+    "gw_key_group_for_hash", "gw_operator_for_key_group", "gw_default_max_parallelism",
+    "gw_key_groups_device", "gw_partition_scratch_bytes", "gw_partition_device",
+]
+
+
+class NativeLibraryError(RuntimeError):
+    pass
+
+
+class GpuWinError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"{ERRORS.get(code, code)}: {msg}")
+        self.code = code
+
+
+class GwConfig(ctypes.Structure):
+    _fields_ = [
+        ("assigner", ctypes.c_int32), ("trigger", ctypes.c_int32),
+        ("size", ctypes.c_int64), ("slide", ctypes.c_int64), ("offset", ctypes.c_int64),
+        ("gap", ctypes.c_int64), ("allowed_lateness", ctypes.c_int64),
+        ("agg", ctypes.c_int32), ("max_parallelism", ctypes.c_int32),
+        ("parallelism", ctypes.c_int32), ("operator_index", ctypes.c_int32),
+        ("device", ctypes.c_int32), ("flags", ctypes.c_int32),
+        ("capacity_hint", ctypes.c_int64), ("max_batch", ctypes.c_int64),
+    ]
+
+
+class GwStats(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int64) for n in (
+        "events_in", "late_dropped", "rows_fired", "live_keys", "table_capacity", "table_bytes",
+        "deferred", "batches", "fires", "rehashes", "preagg_batches", "session_merges")]
+
+    def as_dict(self):
+        return {n: getattr(self, n) for n, _ in self._fields_}
+
+
+_lib = None
+
+
+def lib() -> ctypes.CDLL:
+    """Load libgpuwin.so (built in-tree by flink_amd.build); raise if absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise NativeLibraryError(
+            f"{LIB_PATH} not found: build it with `python -m flink_amd.build` (hipcc, gfx950). "
+            "There is no CPU fallback on the product path.")
+    try:
+        L = ctypes.CDLL(LIB_PATH)
+    except OSError as e:
+        raise NativeLibraryError(f"cannot load {LIB_PATH}: {e}") from e
+    i32, i64, p, c_int = ctypes.c_int32, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int
+    P64 = ctypes.POINTER(ctypes.c_int64)
+    sig = {
+        "gw_create": (c_int, [ctypes.POINTER(GwConfig), ctypes.POINTER(p)]),
+        "gw_destroy": (c_int, [p]),
+        "gw_last_error": (ctypes.c_char_p, [p]),
+        "gw_abi_version": (c_int, []),
+        "gw_ingest": (c_int, [p, i64, p, p, p, p]),
+        "gw_ingest_device": (c_int, [p, i64, p, p, p, p, p]),
+        "gw_advance_watermark": (c_int, [p, i64, P64]),
+        "gw_end_input": (c_int, [p, P64]),
+        "gw_pending_rows": (c_int, [p, P64]),
+        "gw_drain": (c_int, [p, p, p, p, p, i64, P64]),
+        "gw_rows_device": (c_int, [p, ctypes.POINTER(p), ctypes.POINTER(p), ctypes.POINTER(p),
+                                   ctypes.POINTER(p), P64]),
+        "gw_clear_rows": (c_int, [p]),
+        "gw_late_dropped": (i64, [p]),
+        "gw_get_stats": (c_int, [p, ctypes.POINTER(GwStats)]),
+        "gw_synchronize": (c_int, [p]),
+        "gw_stream": (p, [p]),
+        "gw_kernel_time_ms": (c_int, [p, c_int, ctypes.POINTER(ctypes.c_double), P64]),
+        "gw_enable_kernel_timing": (c_int, [p, c_int]),
+        "gw_java_long_hash": (i32, [i64]),
+        "gw_murmur_hash": (i32, [i32]),
+        "gw_key_group_for_hash": (i32, [i32, i32]),
+        "gw_operator_for_key_group": (i32, [i32, i32, i32]),
+        "gw_default_max_parallelism": (i32, [i32]),
+        "gw_key_groups_device": (c_int, [i64, p, p, i32, i32, p, p, p]),
+        "gw_partition_scratch_bytes": (i64, [i64, i32]),
+        "gw_partition_device": (c_int, [i64, p, p, p, p, i32, i32, p, p, p, p, p, p]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    _lib = L
+    return _lib
+
+
+def check(rc: int, handle=None):
+    if rc != GW_OK:
+        msg = lib().gw_last_error(handle)
+        raise GpuWinError(rc, msg.decode() if msg else "")
+    return rc

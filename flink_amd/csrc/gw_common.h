@@ -1,0 +1,162 @@
+// gw_common.h — shared by the gfx950 kernels and the host runtime of libgpuwin.so.
+//
+// Semantics restated here (cited per function) are those of the reference's
+// keyed event-time window path; the state layout is this library's own
+// MI355X-first design: an open-addressing table of per-key slots in
+// HBM, each slot holding a ring of pane (slice) accumulators.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/gpuwin.h"
+
+#define GW_HD __host__ __device__ __forceinline__
+
+namespace gw {
+
+constexpr int64_t kEmptyKey = INT64_MIN;  // slot sentinel; the real key INT64_MIN lives in slot `cap`
+constexpr int kMaxRing = 64;              // pane ring length limit (64-bit presence mask)
+constexpr int kMaxProbe = 128;            // linear-probe limit before a record is parked
+
+// ---------------------------------------------------------------------------
+// Java hashing (bit-exact with the reference)
+// ---------------------------------------------------------------------------
+GW_HD uint32_t rotl32(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
+
+// MathUtils.bitMix (flink-core/.../util/MathUtils.java:194-201)
+GW_HD int32_t bit_mix(int32_t in) {
+    uint32_t h = (uint32_t)in;
+    h ^= h >> 16;
+    h *= 0x85ebca6bu;
+    h ^= h >> 13;
+    h *= 0xc2b2ae35u;
+    h ^= h >> 16;
+    return (int32_t)h;
+}
+
+// MathUtils.murmurHash(int) (MathUtils.java:137-155)
+GW_HD int32_t murmur_hash(int32_t code) {
+    uint32_t c = (uint32_t)code;
+    c *= 0xcc9e2d51u;
+    c = rotl32(c, 15);
+    c *= 0x1b873593u;
+    c = rotl32(c, 13);
+    c = c * 5u + 0xe6546b64u;
+    c ^= 4u;
+    int32_t r = bit_mix((int32_t)c);
+    if (r >= 0) return r;
+    if (r != INT32_MIN) return -r;
+    return 0;
+}
+
+// JDK Long.hashCode
+GW_HD int32_t java_long_hash(int64_t v) {
+    uint64_t u = (uint64_t)v;
+    return (int32_t)(uint32_t)(u ^ (u >> 32));
+}
+
+// KeyGroupRangeAssignment.computeKeyGroupForKeyHash (:75-77)
+GW_HD int32_t key_group_for_hash(int32_t h, int32_t max_p) { return murmur_hash(h) % max_p; }
+// KeyGroupRangeAssignment.computeOperatorIndexForKeyGroup (:124-127)
+GW_HD int32_t operator_for_key_group(int32_t max_p, int32_t p, int32_t kg) { return kg * p / max_p; }
+
+// State-table hash (this library's own; independent of the key-group hash so that
+// the slots of one key group are spread over the whole table).
+GW_HD uint64_t slot_hash(int64_t key) {
+    uint64_t x = (uint64_t)key;
+    x ^= x >> 33;
+    x *= 0xff51afd7ed558ccdull;
+    x ^= x >> 33;
+    x *= 0xc4ceb9fe1a85ec53ull;
+    x ^= x >> 33;
+    return x;
+}
+
+// ---------------------------------------------------------------------------
+// Double ordering (Double.compare: NaN largest and canonical, -0.0 < 0.0) as a
+// signed int64 order, so min/max run as integer atomics.
+// ---------------------------------------------------------------------------
+GW_HD int64_t f64_order_key(int64_t bits) {
+    if (((bits >> 52) & 0x7ff) == 0x7ff && (bits & 0xfffffffffffffLL)) bits = 0x7ff8000000000000LL;
+    return bits ^ ((bits >> 63) & 0x7fffffffffffffffLL);
+}
+GW_HD int64_t f64_from_order_key(int64_t k) { return k ^ ((k >> 63) & 0x7fffffffffffffffLL); }
+
+GW_HD double bits_to_f64(int64_t b) { return __builtin_bit_cast(double, b); }
+GW_HD int64_t f64_to_bits(double d) { return __builtin_bit_cast(int64_t, d); }
+
+// ---------------------------------------------------------------------------
+// Accumulator cells (one per (key, pane)).  Two 8-byte words; word 1 is only
+// used by AVG.  Identity values make "merge into an empty cell" a plain RMW.
+// ---------------------------------------------------------------------------
+GW_HD int cell_words(int agg) { return (agg == GW_AVG_I64 || agg == GW_AVG_F64) ? 2 : 1; }
+GW_HD bool result_is_double(int agg) {
+    return agg == GW_SUM_F64 || agg == GW_MIN_F64 || agg == GW_MAX_F64 || agg == GW_AVG_I64 ||
+           agg == GW_AVG_F64;
+}
+GW_HD int64_t identity0(int agg) {
+    switch (agg) {
+    case GW_SUM_F64: return (int64_t)0x8000000000000000ull;  // -0.0: x + (-0.0) == x for all x
+    case GW_MIN_I64: case GW_MIN_F64: return INT64_MAX;
+    case GW_MAX_I64: case GW_MAX_F64: return INT64_MIN;
+    default: return 0;  // COUNT, SUM_I64, SUM_I32, AVG_*(sum; +0.0 for AVG_F64)
+    }
+}
+// The accumulator contribution of a single raw record value.
+GW_HD void record_cell(int agg, int64_t v, int64_t& a0, int64_t& a1) {
+    a1 = 1;
+    switch (agg) {
+    case GW_COUNT: a0 = 1; break;
+    case GW_MIN_F64: case GW_MAX_F64: a0 = f64_order_key(v); break;
+    default: a0 = v; break;
+    }
+}
+// Fold cell (b0,b1) into (a0,a1) on the host / in registers.
+GW_HD void fold_cell(int agg, int64_t& a0, int64_t& a1, int64_t b0, int64_t b1) {
+    switch (agg) {
+    case GW_COUNT: case GW_SUM_I64: case GW_SUM_I32:
+        a0 = (int64_t)((uint64_t)a0 + (uint64_t)b0); break;
+    case GW_SUM_F64: a0 = f64_to_bits(bits_to_f64(a0) + bits_to_f64(b0)); break;
+    case GW_MIN_I64: case GW_MIN_F64: a0 = a0 < b0 ? a0 : b0; break;
+    case GW_MAX_I64: case GW_MAX_F64: a0 = a0 > b0 ? a0 : b0; break;
+    case GW_AVG_I64:
+        a0 = (int64_t)((uint64_t)a0 + (uint64_t)b0); a1 += b1; break;
+    case GW_AVG_F64:
+        a0 = f64_to_bits(bits_to_f64(a0) + bits_to_f64(b0)); a1 += b1; break;
+    }
+}
+// Output column bits (int64 or IEEE double) — AggregateFunction.getResult / the
+// reduced field of SumAggregator / ComparableAggregator.
+GW_HD int64_t cell_result(int agg, int64_t a0, int64_t a1) {
+    switch (agg) {
+    case GW_SUM_I32: return (int64_t)(int32_t)(uint32_t)(uint64_t)a0;  // Java int wrap-around
+    case GW_MIN_F64: case GW_MAX_F64: return f64_from_order_key(a0);
+    case GW_AVG_I64: return f64_to_bits((double)a0 / (double)a1);
+    case GW_AVG_F64: return f64_to_bits(bits_to_f64(a0) / (double)a1);
+    default: return a0;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// 64-bit unsigned division by a runtime-invariant divisor (Granlund-Montgomery
+// round-up method): q = (t + ((n - t) >> 1)) >> (l - 1), t = mulhi(M, n).
+// ---------------------------------------------------------------------------
+struct UDiv64 {
+    uint64_t magic;
+    uint32_t shift;   // l - 1 (or 0 with is_pow2 handling)
+    uint32_t mode;    // 0: general, 1: divisor == 1
+};
+GW_HD uint64_t mulhi64(uint64_t a, uint64_t b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __umul64hi(a, b);
+#else
+    return (uint64_t)(((unsigned __int128)a * b) >> 64);
+#endif
+}
+GW_HD uint64_t udiv64(uint64_t n, const UDiv64& d) {
+    if (d.mode == 1) return n;
+    uint64_t t = mulhi64(d.magic, n);
+    return (t + ((n - t) >> 1)) >> d.shift;
+}
+
+}  // namespace gw

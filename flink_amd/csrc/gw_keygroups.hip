@@ -1,0 +1,153 @@
+// gw_keygroups.hip — key-group hashing and the keyBy partition on the device.
+//
+//   KeyGroupRangeAssignment.assignToKeyGroup / computeOperatorIndexForKeyGroup
+//     (flink-runtime/src/main/java/org/apache/flink/runtime/state/
+//      KeyGroupRangeAssignment.java:63-77,124-127) with MathUtils.murmurHash
+//     (flink-core/src/main/java/org/apache/flink/util/MathUtils.java:137-155)
+//   KeyGroupStreamPartitioner.selectChannel (flink-runtime/src/main/java/org/apache/
+//     flink/streaming/runtime/partitioner/KeyGroupStreamPartitioner.java:55-64)
+//
+// The partition is a stable counting sort of the record columns by destination
+// subtask (= GPU rank), the send-side half of the RCCL all-to-all that replaces the
+// Netty keyBy shuffle.  Three passes: per-block histogram, one-block scan, stable
+// scatter (wave64 ballot matching for in-wave ranks).
+#include "gw_kernels.h"
+
+namespace gw {
+
+constexpr int kPartMaxDest = 256;
+constexpr int kPartItems = 8;  // records per thread per block tile
+
+__device__ __forceinline__ int32_t owner_of(const int64_t* key, const int32_t* key_hash, int64_t i,
+                                            int32_t max_p, int32_t p) {
+    const int32_t h = key_hash ? key_hash[i] : java_long_hash(key[i]);
+    return operator_for_key_group(max_p, p, key_group_for_hash(h, max_p));
+}
+
+__global__ void __launch_bounds__(256) k_key_groups(int64_t n, const int64_t* key, const int32_t* key_hash,
+                                                    int32_t max_p, int32_t p, int32_t* kg, int32_t* owner) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const int32_t h = key_hash ? key_hash[i] : java_long_hash(key[i]);
+        const int32_t g = key_group_for_hash(h, max_p);
+        if (kg) kg[i] = g;
+        if (owner) owner[i] = operator_for_key_group(max_p, p, g);
+    }
+}
+
+// pass 1: counts[block][dest]
+__global__ void __launch_bounds__(256) k_part_hist(int64_t n, const int64_t* key, const int32_t* key_hash,
+                                                   int32_t max_p, int32_t p, uint32_t* block_counts) {
+    __shared__ uint32_t h[kPartMaxDest];
+    for (int d = threadIdx.x; d < p; d += blockDim.x) h[d] = 0;
+    __syncthreads();
+    const int64_t t0 = (int64_t)blockIdx.x * blockDim.x * kPartItems;
+    for (int it = 0; it < kPartItems; ++it) {
+        const int64_t i = t0 + (int64_t)it * blockDim.x + threadIdx.x;
+        if (i < n) atomicAdd(&h[owner_of(key, key_hash, i, max_p, p)], 1u);
+    }
+    __syncthreads();
+    for (int d = threadIdx.x; d < p; d += blockDim.x) block_counts[(int64_t)d * gridDim.x + blockIdx.x] = h[d];
+}
+
+// pass 2: exclusive scan over (dest-major, block-minor); totals per dest.
+__global__ void __launch_bounds__(1024) k_part_scan(uint32_t* block_counts, int64_t nblk, int32_t p,
+                                                    int64_t* offsets, int64_t* counts) {
+    __shared__ unsigned long long part[1024];
+    const int64_t total = nblk * p;
+    const int64_t per = (total + blockDim.x - 1) / blockDim.x;
+    const int64_t lo = threadIdx.x * per, hi = min(total, lo + per);
+    unsigned long long s = 0;
+    for (int64_t i = lo; i < hi; ++i) s += block_counts[i];
+    part[threadIdx.x] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long run = 0;
+        for (int i = 0; i < (int)blockDim.x; ++i) { unsigned long long v = part[i]; part[i] = run; run += v; }
+    }
+    __syncthreads();
+    unsigned long long run = part[threadIdx.x];
+    for (int64_t i = lo; i < hi; ++i) { unsigned long long v = block_counts[i]; offsets[i] = (int64_t)run; run += v; }
+    __syncthreads();
+    for (int d = threadIdx.x; d < p; d += blockDim.x) {
+        unsigned long long c = 0;
+        for (int64_t b = 0; b < nblk; ++b) c += block_counts[(int64_t)d * nblk + b];
+        counts[d] = (int64_t)c;
+    }
+}
+
+// pass 3: stable scatter.  Tile order = it-major then thread, i.e. global order.
+__global__ void __launch_bounds__(256) k_part_scatter(int64_t n, const int64_t* key, const int32_t* key_hash,
+                                                      const int64_t* ts, const int64_t* val, int32_t max_p,
+                                                      int32_t p, const int64_t* offsets, int64_t* key_out,
+                                                      int64_t* ts_out, int64_t* val_out) {
+    __shared__ int64_t cursor[kPartMaxDest];
+    __shared__ uint32_t wave_cnt[4][kPartMaxDest];
+    const int lane = __lane_id();
+    const int wave = threadIdx.x >> 6;
+    for (int d = threadIdx.x; d < p; d += blockDim.x) cursor[d] = offsets[(int64_t)d * gridDim.x + blockIdx.x];
+    const int64_t t0 = (int64_t)blockIdx.x * blockDim.x * kPartItems;
+    for (int it = 0; it < kPartItems; ++it) {
+        for (int d = threadIdx.x; d < 4 * p; d += blockDim.x) wave_cnt[d / p][d % p] = 0;
+        __syncthreads();
+        const int64_t i = t0 + (int64_t)it * blockDim.x + threadIdx.x;
+        const bool valid = i < n;
+        const int32_t d = valid ? owner_of(key, key_hash, i, max_p, p) : -1;
+        // peers: lanes of this wave with the same destination (8 ballots cover p <= 256)
+        unsigned long long peers = __ballot(valid);
+        for (int b = 0; b < 8; ++b) {
+            const bool bit = (d >> b) & 1;
+            const unsigned long long bb = __ballot(bit);
+            peers &= bit ? bb : ~bb;
+        }
+        const unsigned rank_in_wave = (unsigned)__popcll(peers & ((1ull << lane) - 1ull));
+        if (valid && rank_in_wave == 0) wave_cnt[wave][d] = (uint32_t)__popcll(peers);
+        __syncthreads();
+        if (valid) {
+            int64_t pos = cursor[d] + rank_in_wave;
+            for (int w = 0; w < wave; ++w) pos += wave_cnt[w][d];
+            key_out[pos] = key[i];
+            ts_out[pos] = ts[i];
+            if (val) val_out[pos] = val[i];
+        }
+        __syncthreads();
+        for (int dd = threadIdx.x; dd < p; dd += blockDim.x)
+            cursor[dd] += wave_cnt[0][dd] + wave_cnt[1][dd] + wave_cnt[2][dd] + wave_cnt[3][dd];
+        __syncthreads();
+    }
+}
+
+hipError_t launch_key_groups(int64_t n, const int64_t* key, const int32_t* key_hash, int32_t max_p,
+                             int32_t p, int32_t* kg, int32_t* owner, hipStream_t s) {
+    int64_t g = (n + 255) / 256;
+    if (g < 1) g = 1;
+    if (g > 4096) g = 4096;
+    hipLaunchKernelGGL(k_key_groups, dim3((unsigned)g), dim3(256), 0, s, n, key, key_hash, max_p, p, kg, owner);
+    return hipGetLastError();
+}
+
+static int64_t part_blocks(int64_t n) {
+    int64_t b = (n + 256 * kPartItems - 1) / (256 * kPartItems);
+    return b < 1 ? 1 : b;
+}
+
+int64_t partition_scratch_bytes(int64_t n, int32_t p) {
+    const int64_t nb = part_blocks(n);
+    return nb * p * (int64_t)sizeof(uint32_t) + nb * p * (int64_t)sizeof(int64_t) + 256;
+}
+
+hipError_t launch_partition(int64_t n, const int64_t* key, const int32_t* key_hash, const int64_t* ts,
+                            const int64_t* val, int32_t max_p, int32_t p, int64_t* key_out, int64_t* ts_out,
+                            int64_t* val_out, int64_t* counts, void* scratch, hipStream_t s) {
+    if (p < 1 || p > kPartMaxDest) return hipErrorInvalidValue;
+    const int64_t nb = part_blocks(n);
+    uint32_t* bc = (uint32_t*)scratch;
+    int64_t* off = (int64_t*)(((uintptr_t)(bc + nb * p) + 15) & ~(uintptr_t)15);
+    hipLaunchKernelGGL(k_part_hist, dim3((unsigned)nb), dim3(256), 0, s, n, key, key_hash, max_p, p, bc);
+    hipLaunchKernelGGL(k_part_scan, dim3(1), dim3(1024), 0, s, bc, nb, p, off, counts);
+    hipLaunchKernelGGL(k_part_scatter, dim3((unsigned)nb), dim3(256), 0, s, n, key, key_hash, ts, val, max_p, p,
+                       off, key_out, ts_out, val_out);
+    return hipGetLastError();
+}
+
+}  // namespace gw

@@ -1,0 +1,912 @@
+// gw_runtime.cpp — host orchestration behind the C ABI of include/gpuwin.h.
+//
+// One gw_handle = one keyed window operator subtask (Flink: one WindowOperator
+// instance on one mailbox thread, RS/runtime/tasks/mailbox/MailboxProcessor.java:45-49).
+// Calls on a handle are serialised by the caller; the handle owns its HIP stream,
+// its HBM state table and every device buffer.  No C++ exception crosses the ABI.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "gw_kernels.h"
+#include "gw_session.h"
+
+using namespace gw;
+
+namespace {
+
+thread_local std::string g_create_error;
+
+typedef __int128 i128;
+
+i128 floor_div(i128 a, i128 b) {  // b > 0
+    i128 q = a / b;
+    if ((a % b) != 0 && a < 0) --q;
+    return q;
+}
+i128 floor_mod(i128 a, i128 b) { return a - floor_div(a, b) * b; }
+int64_t gcd64(int64_t a, int64_t b) {
+    while (b) { int64_t t = a % b; a = b; b = t; }
+    return a;
+}
+bool fits64(i128 v) { return v >= (i128)INT64_MIN && v <= (i128)INT64_MAX; }
+
+UDiv64 make_udiv(uint64_t d) {
+    UDiv64 r{};
+    if (d == 1) { r.mode = 1; return r; }
+    unsigned l = 0;
+    while (l < 64 && (1ull << l) < d) ++l;  // l = ceil(log2 d), d >= 2 -> l >= 1
+    unsigned __int128 two_l = (unsigned __int128)1 << l;
+    unsigned __int128 m = (((two_l - d) << 64) / d) + 1;
+    r.magic = (uint64_t)m;
+    r.shift = l - 1;
+    r.mode = 0;
+    return r;
+}
+
+struct KernelTimer {
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> pending;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> pool;
+    double total_ms = 0, last_ms = 0;
+    int64_t launches = 0;
+    std::pair<hipEvent_t, hipEvent_t> get() {
+        if (!pool.empty()) { auto p = pool.back(); pool.pop_back(); return p; }
+        std::pair<hipEvent_t, hipEvent_t> p;
+        hipEventCreate(&p.first);
+        hipEventCreate(&p.second);
+        return p;
+    }
+    void resolve() {  // stream already synchronised
+        for (auto& p : pending) {
+            float ms = 0;
+            if (hipEventElapsedTime(&ms, p.first, p.second) == hipSuccess) {
+                total_ms += ms;
+                last_ms = ms;
+                launches++;
+            }
+            pool.push_back(p);
+        }
+        pending.clear();
+    }
+    void destroy() {
+        for (auto& p : pending) pool.push_back(p);
+        for (auto& p : pool) { hipEventDestroy(p.first); hipEventDestroy(p.second); }
+        pool.clear();
+        pending.clear();
+    }
+};
+
+}  // namespace
+
+struct gw_handle {
+    gw_config cfg{};
+    std::string err;
+    bool failed = false;
+    hipStream_t stream = nullptr;
+    bool session = false;
+
+    // pane geometry
+    int64_t g = 1, m = 1, n = 1;
+    int R = 2;
+    UDiv64 div{};
+
+    // state table
+    TableView tv{};
+    size_t table_bytes = 0;
+
+    // event-time state
+    int64_t wm = INT64_MIN;
+    i128 fired_k = 0;  // first window index not yet fired
+    i128 B = 0;        // ring base pane
+    uint64_t occ = 0;  // ring positions that may hold data
+
+    // deferred lists (double-buffered)
+    int64_t* dk[2] = {nullptr, nullptr};
+    int64_t* dp[2] = {nullptr, nullptr};
+    int64_t* da0[2] = {nullptr, nullptr};
+    int64_t* da1[2] = {nullptr, nullptr};
+    int64_t def_cap = 0;
+    int cur = 0;
+
+    // host-ingest staging
+    int64_t* h_stage = nullptr;  // pinned: key | ts | val
+    int64_t* d_stage = nullptr;  // device: key | ts | val
+    int32_t* d_hash_stage = nullptr;
+    int64_t stage_cap = 0;
+
+    // output rows (device SoA), [rows_head, st.rows) pending
+    int64_t* o_key = nullptr;
+    int64_t* o_start = nullptr;
+    int64_t* o_end = nullptr;
+    int64_t* o_res = nullptr;
+    int64_t o_cap = 0;
+    int64_t rows_head = 0;
+
+    // status
+    DevStatus* d_st = nullptr;
+    DevStatus* h_st = nullptr;
+    unsigned long long* d_tmp = nullptr;
+
+    gw_stats stats{};
+    bool timing = false;
+    KernelTimer t_ingest, t_fire;
+
+    SessionState* sess = nullptr;
+
+    int fail(int code, const char* fmt, ...) {
+        char buf[512];
+        va_list ap;
+        va_start(ap, fmt);
+        vsnprintf(buf, sizeof(buf), fmt, ap);
+        va_end(ap);
+        err = buf;
+        if (code == GW_E_DEVICE || code == GW_E_NO_TIMESTAMP || code == GW_E_RANGE) failed = true;
+        return code;
+    }
+#define HIPCHECK(x)                                                                                  \
+    do {                                                                                             \
+        hipError_t e_ = (x);                                                                         \
+        if (e_ != hipSuccess) return fail(GW_E_DEVICE, "%s failed: %s", #x, hipGetErrorString(e_)); \
+    } while (0)
+
+    int refresh() {
+        HIPCHECK(hipMemcpyAsync(h_st, d_st, sizeof(DevStatus), hipMemcpyDeviceToHost, stream));
+        HIPCHECK(hipStreamSynchronize(stream));
+        if (timing) { t_ingest.resolve(); t_fire.resolve(); }
+        if (h_st->flags & GW_DF_NO_TS)
+            return fail(GW_E_NO_TIMESTAMP,
+                        "Record has Long.MIN_VALUE timestamp (= no timestamp marker). Did you forget to "
+                        "call 'DataStream.assignTimestampsAndWatermarks(...)'?");
+        if (h_st->flags & GW_DF_RANGE)
+            return fail(GW_E_RANGE, "record timestamp/pane outside the supported int64 window range");
+        stats.late_dropped = (int64_t)h_st->late;
+        stats.live_keys = (int64_t)h_st->used_slots;
+        stats.deferred = (int64_t)h_st->n_deferred;
+        stats.session_merges = (int64_t)h_st->merges;
+        return GW_OK;
+    }
+    int set_field(size_t off, unsigned long long v) {
+        // small H2D write of one DevStatus word, ordered on the stream
+        unsigned long long* hv = reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(h_st) + off);
+        *hv = v;
+        HIPCHECK(hipMemcpyAsync(reinterpret_cast<char*>(d_st) + off, hv, 8, hipMemcpyHostToDevice, stream));
+        HIPCHECK(hipStreamSynchronize(stream));  // h_st reused as the source
+        return GW_OK;
+    }
+    int take_occ() {  // fold device ring occupancy into the host view and clear it
+        occ |= h_st->occ;
+        if (h_st->occ) return set_field(offsetof(DevStatus, occ), 0);
+        return GW_OK;
+    }
+
+    // ---------------------------------------------------------------- memory
+    int alloc_table(TableView& t, int64_t cap) {
+        t = tv;
+        t.cap = cap;
+        const size_t bytes = (size_t)(cap + 1) * (size_t)t.stride_w * 8;
+        HIPCHECK(hipMalloc((void**)&t.base, bytes));
+        HIPCHECK(launch_table_init(t, stream));
+        return GW_OK;
+    }
+    int ensure_deferred(int64_t need) {
+        if (need <= def_cap) return GW_OK;
+        int64_t nc = std::max<int64_t>(need + need / 2, 1 << 16);
+        for (int b = 0; b < 2; ++b) {
+            int64_t* nk; int64_t* np; int64_t* n0; int64_t* n1;
+            HIPCHECK(hipMalloc((void**)&nk, nc * 8));
+            HIPCHECK(hipMalloc((void**)&np, nc * 8));
+            HIPCHECK(hipMalloc((void**)&n0, nc * 8));
+            HIPCHECK(hipMalloc((void**)&n1, nc * 8));
+            if (dk[b] && b == cur) {
+                const int64_t used = (int64_t)h_st->n_deferred;
+                if (used) {
+                    HIPCHECK(hipMemcpyAsync(nk, dk[b], used * 8, hipMemcpyDeviceToDevice, stream));
+                    HIPCHECK(hipMemcpyAsync(np, dp[b], used * 8, hipMemcpyDeviceToDevice, stream));
+                    HIPCHECK(hipMemcpyAsync(n0, da0[b], used * 8, hipMemcpyDeviceToDevice, stream));
+                    HIPCHECK(hipMemcpyAsync(n1, da1[b], used * 8, hipMemcpyDeviceToDevice, stream));
+                }
+            }
+            if (dk[b]) {
+                hipStreamSynchronize(stream);
+                hipFree(dk[b]); hipFree(dp[b]); hipFree(da0[b]); hipFree(da1[b]);
+            }
+            dk[b] = nk; dp[b] = np; da0[b] = n0; da1[b] = n1;
+        }
+        def_cap = nc;
+        return GW_OK;
+    }
+    int ensure_output(int64_t need) {  // need = total rows (pending + new)
+        if (need <= o_cap) return GW_OK;
+        int64_t nc = std::max<int64_t>(need + need / 4, 1 << 16);
+        int64_t* nb[4];
+        for (int i = 0; i < 4; ++i) HIPCHECK(hipMalloc((void**)&nb[i], nc * 8));
+        const int64_t used = (int64_t)h_st->rows;
+        int64_t* old[4] = {o_key, o_start, o_end, o_res};
+        for (int i = 0; i < 4; ++i) {
+            if (old[i]) {
+                if (used) HIPCHECK(hipMemcpyAsync(nb[i], old[i], used * 8, hipMemcpyDeviceToDevice, stream));
+                hipStreamSynchronize(stream);
+                hipFree(old[i]);
+            }
+        }
+        o_key = nb[0]; o_start = nb[1]; o_end = nb[2]; o_res = nb[3];
+        o_cap = nc;
+        return GW_OK;
+    }
+    int ensure_stage(int64_t n) {
+        if (n <= stage_cap) return GW_OK;
+        if (h_stage) { hipHostFree(h_stage); hipFree(d_stage); hipFree(d_hash_stage); }
+        h_stage = nullptr;
+        HIPCHECK(hipHostMalloc((void**)&h_stage, (size_t)n * 24, hipHostMallocDefault));
+        HIPCHECK(hipMalloc((void**)&d_stage, (size_t)n * 24));
+        HIPCHECK(hipMalloc((void**)&d_hash_stage, (size_t)n * 4));
+        stage_cap = n;
+        return GW_OK;
+    }
+
+    // Re-hash the live slots into a table of `new_cap` slots (drops dead keys).
+    int rehash(int64_t new_cap) {
+        TableView nt;
+        int rc = alloc_table(nt, new_cap);
+        if (rc) return rc;
+        if ((rc = set_field(offsetof(DevStatus, used_slots), 0))) return rc;
+        HIPCHECK(launch_rehash(tv, nt, d_st, stream));
+        HIPCHECK(hipStreamSynchronize(stream));
+        HIPCHECK(hipFree(tv.base));
+        tv = nt;
+        table_bytes = (size_t)(nt.cap + 1) * (size_t)nt.stride_w * 8;
+        stats.rehashes++;
+        if ((rc = refresh())) return rc;
+        if (h_st->flags & GW_DF_TABLE_FULL) return fail(GW_E_OOM, "state table rehash overflow");
+        return GW_OK;
+    }
+    int64_t live_count() {
+        hipMemsetAsync(d_tmp, 0, 8, stream);
+        launch_count_live(tv, d_tmp, stream);
+        unsigned long long v = 0;
+        hipMemcpyAsync(&h_st->pad[0], d_tmp, 8, hipMemcpyDeviceToHost, stream);
+        hipStreamSynchronize(stream);
+        v = h_st->pad[0];
+        return (int64_t)v;
+    }
+    // Keep the load factor of the linear-probing table below 0.7.
+    int maybe_grow(int64_t incoming) {
+        const int64_t used = (int64_t)h_st->used_slots;
+        const bool full = (h_st->flags & GW_DF_TABLE_FULL) != 0;
+        if (!full && (double)used <= 0.7 * (double)tv.cap) return GW_OK;
+        const int64_t live = live_count();
+        int64_t want = std::max<int64_t>(tv.cap, 1024);
+        while ((double)live > 0.45 * (double)want || (full && want <= tv.cap)) want *= 2;
+        (void)incoming;
+        int rc = rehash(want);
+        if (rc) return rc;
+        if (full) {
+            unsigned long long f = h_st->flags & ~GW_DF_TABLE_FULL;
+            if ((rc = set_field(offsetof(DevStatus, flags), f))) return rc;
+        }
+        return GW_OK;
+    }
+
+    // ---------------------------------------------------------------- pane mode
+    int64_t pos_of(i128 pane) const { return (int64_t)floor_mod(pane, R); }
+
+    int merge_deferred() {
+        int rc;
+        const int64_t nin = (int64_t)h_st->n_deferred;
+        if (nin == 0) return GW_OK;
+        for (int attempt = 0; attempt < 8; ++attempt) {
+            if ((rc = ensure_deferred(nin))) return rc;
+            if ((rc = set_field(offsetof(DevStatus, n_deferred), 0))) return rc;
+            MergeArgs a{};
+            a.i_key = dk[cur]; a.i_pane = dp[cur]; a.i_a0 = da0[cur]; a.i_a1 = da1[cur];
+            a.n = nin;
+            a.b = (int64_t)B;
+            a.b_pos = (int32_t)pos_of(B);
+            a.t = tv;
+            const int o = cur ^ 1;
+            a.d_key = dk[o]; a.d_pane = dp[o]; a.d_a0 = da0[o]; a.d_a1 = da1[o];
+            a.st = d_st;
+            HIPCHECK(launch_merge_deferred(a, stream));
+            cur = o;
+            if ((rc = refresh())) return rc;
+            if ((rc = take_occ())) return rc;
+            if (!(h_st->flags & GW_DF_TABLE_FULL)) return GW_OK;
+            if ((rc = maybe_grow(0))) return rc;  // grow, then retry the leftovers
+            if ((int64_t)h_st->n_deferred == 0) return GW_OK;
+            return merge_deferred();
+        }
+        return GW_OK;
+    }
+
+    // Lowest pane with data in the ring (or INT128 max).
+    i128 ring_min() const {
+        if (!occ) return ((i128)1) << 100;
+        for (int j = 0; j < R; ++j)
+            if (occ & (1ull << pos_of(B + j))) return B + j;
+        return ((i128)1) << 100;
+    }
+
+    int deferred_min(i128& out) {
+        out = ((i128)1) << 100;
+        const int64_t nd = (int64_t)h_st->n_deferred;
+        if (!nd) return GW_OK;
+        int rc;
+        if ((rc = set_field(offsetof(DevStatus, def_min_pane), (unsigned long long)INT64_MAX))) return rc;
+        HIPCHECK(launch_deferred_min(dp[cur], nd, d_st, stream));
+        if ((rc = refresh())) return rc;
+        out = (i128)h_st->def_min_pane;
+        return GW_OK;
+    }
+
+    // Move the ring base to pane nb (nb <= every pane holding data).
+    int rebase(i128 nb) {
+        int rc;
+        if (nb < B) {
+            uint64_t emask = 0;
+            EvictArgs e{};
+            for (i128 p = std::max(nb + R, B); p < B + R; ++p) {
+                const int pos = (int)pos_of(p);
+                if (occ & (1ull << pos)) {
+                    emask |= 1ull << pos;
+                    e.pane_of_pos[pos] = (int64_t)p;
+                }
+            }
+            if (emask) {
+                if ((rc = ensure_deferred((int64_t)h_st->n_deferred + (int64_t)(popcount(emask)) *
+                                                                       ((int64_t)h_st->used_slots + 1))))
+                    return rc;
+                e.t = tv;
+                e.emask = emask;
+                e.d_key = dk[cur]; e.d_pane = dp[cur]; e.d_a0 = da0[cur]; e.d_a1 = da1[cur];
+                e.st = d_st;
+                HIPCHECK(launch_evict(e, stream));
+                occ &= ~emask;
+                if ((rc = refresh())) return rc;
+            }
+        }
+        B = nb;
+        return GW_OK;
+    }
+    static int popcount(uint64_t x) { return __builtin_popcountll(x); }
+
+    // Fire every window k <= k_target (end-1 <= wm).
+    int fire_until(i128 k_target) {
+        int rc;
+        while (fired_k <= k_target) {
+            i128 dmin;
+            if ((rc = deferred_min(dmin))) return rc;
+            const i128 rmin = ring_min();
+            const i128 L = std::min(rmin, dmin);
+            const i128 NONE = ((i128)1) << 100;
+            if (L >= NONE) { fired_k = k_target + 1; break; }
+            i128 k_first = floor_div(L - n, m) + 1;
+            if (k_first < fired_k) k_first = fired_k;
+            if (k_first > k_target) { fired_k = k_target + 1; break; }
+            if ((rc = rebase(k_first * m))) return rc;
+            if ((int64_t)h_st->n_deferred) {
+                if ((rc = merge_deferred())) return rc;
+            }
+            i128 k_last = floor_div(B + R - n, m);
+            if (k_last > k_target) k_last = k_target;
+            const int nwin = (int)(k_last - k_first + 1);
+            FireArgs f{};
+            f.t = tv;
+            f.nwin = nwin;
+            const i128 start0 = (i128)cfg.offset + k_first * (i128)slide();
+            const i128 endl = (i128)cfg.offset + k_last * (i128)slide() + size();
+            if (!fits64(start0) || !fits64(endl))
+                return fail(GW_E_RANGE, "window bounds overflow int64");
+            f.start0 = (int64_t)start0;
+            f.slide = slide();
+            f.size = size();
+            for (int w = 0; w < nwin; ++w) {
+                uint64_t wm_ = 0;
+                const i128 p0 = (k_first + w) * m;
+                for (int j = 0; j < n; ++j) wm_ |= 1ull << pos_of(p0 + j);
+                f.wmask[w] = wm_;
+            }
+            uint64_t rmask = 0;
+            for (i128 p = B; p < (k_last + 1) * m && p < B + R; ++p) rmask |= 1ull << pos_of(p);
+            f.rmask = rmask;
+            if ((rc = ensure_output((int64_t)h_st->rows + (int64_t)nwin * ((int64_t)h_st->used_slots + 1))))
+                return rc;
+            f.o_key = o_key; f.o_start = o_start; f.o_end = o_end; f.o_res = o_res;
+            f.st = d_st;
+            if (timing) {
+                auto ev = t_fire.get();
+                HIPCHECK(hipEventRecord(ev.first, stream));
+                HIPCHECK(launch_fire(f, stream));
+                HIPCHECK(hipEventRecord(ev.second, stream));
+                t_fire.pending.push_back(ev);
+            } else {
+                HIPCHECK(launch_fire(f, stream));
+            }
+            stats.fires++;
+            occ &= ~rmask;
+            fired_k = k_last + 1;
+            if (B < fired_k * m) B = fired_k * m;
+            if ((rc = refresh())) return rc;
+        }
+        if (B < fired_k * m) B = fired_k * m;
+        return GW_OK;
+    }
+
+    int64_t size() const { return cfg.assigner == GW_TUMBLING ? cfg.size : cfg.size; }
+    int64_t slide() const { return cfg.assigner == GW_TUMBLING ? cfg.size : cfg.slide; }
+
+    // Windows k <= K are complete at watermark wm: offset + k*slide + size - 1 <= wm.
+    i128 k_for_wm(int64_t w) const {
+        return floor_div((i128)w + 1 - (i128)size() - (i128)cfg.offset, (i128)slide());
+    }
+
+    int ingest_pane(int64_t nrec, const int64_t* key, const int64_t* ts, const int64_t* val) {
+        int rc;
+        if ((rc = refresh())) return rc;
+        if ((rc = maybe_grow(nrec))) return rc;
+        if ((rc = ensure_deferred((int64_t)h_st->n_deferred + nrec))) return rc;
+        // first non-late pane: the first window not fired at the current watermark
+        const i128 p_late = fired_k * m;
+        i128 t_late = (i128)cfg.offset + p_late * g;
+        i128 pl = p_late;
+        int exact = 1;
+        if (t_late <= (i128)INT64_MIN) {  // nothing can be late yet
+            pl = floor_div((i128)INT64_MIN - cfg.offset + g - 1, g);
+            t_late = (i128)cfg.offset + pl * g;
+            exact = 0;
+        }
+        if (t_late > (i128)INT64_MAX) return fail(GW_E_RANGE, "watermark beyond the last representable window");
+        if (B < pl) B = pl;
+        IngestArgs a{};
+        a.key = key; a.ts = ts; a.val = val; a.n = nrec;
+        a.t_late = (int64_t)t_late;
+        a.p_late = (int64_t)pl;
+        a.delta = (uint64_t)(B - pl);
+        a.div = div;
+        a.b_pos = (int32_t)pos_of(B);
+        a.late_exact = exact;
+        a.t = tv;
+        a.d_key = dk[cur]; a.d_pane = dp[cur]; a.d_a0 = da0[cur]; a.d_a1 = da1[cur];
+        a.st = d_st;
+        bool preagg;
+        if (cfg.flags & GW_FLAG_FORCE_LDS_PREAGG) preagg = true;
+        else if (cfg.flags & GW_FLAG_NO_LDS_PREAGG) preagg = false;
+        else {
+            const int64_t keys = std::max<int64_t>((int64_t)h_st->used_slots, cfg.capacity_hint > 0 ? 0 : 1);
+            const int64_t est = h_st->used_slots ? (int64_t)h_st->used_slots : cfg.capacity_hint;
+            preagg = est > 0 && nrec >= 8 * est;
+            (void)keys;
+        }
+        if (preagg) stats.preagg_batches++;
+        if (timing) {
+            auto ev = t_ingest.get();
+            HIPCHECK(hipEventRecord(ev.first, stream));
+            HIPCHECK(launch_ingest(a, preagg, stream));
+            HIPCHECK(hipEventRecord(ev.second, stream));
+            t_ingest.pending.push_back(ev);
+        } else {
+            HIPCHECK(launch_ingest(a, preagg, stream));
+        }
+        stats.events_in += nrec;
+        stats.batches++;
+        if ((rc = refresh())) return rc;
+        if ((rc = take_occ())) return rc;
+        if (h_st->flags & GW_DF_TABLE_FULL) {
+            if ((rc = maybe_grow(0))) return rc;
+            if ((rc = merge_deferred())) return rc;
+        }
+        // An empty ring with parked records: jump the ring to the data.
+        if (!occ && h_st->n_deferred) {
+            i128 dmin;
+            if ((rc = deferred_min(dmin))) return rc;
+            const i128 lo = fired_k * m;
+            B = std::max(lo, dmin);
+            if ((rc = merge_deferred())) return rc;
+        }
+        return GW_OK;
+    }
+
+    int advance_pane(int64_t w, int64_t* rows_out) {
+        int rc;
+        if ((rc = refresh())) return rc;
+        if ((rc = take_occ())) return rc;
+        const int64_t before = (int64_t)h_st->rows;
+        if (w > wm) {
+            const i128 kt = k_for_wm(w);
+            if ((rc = fire_until(kt))) return rc;
+            wm = w;
+        }
+        if ((rc = refresh())) return rc;
+        const int64_t fired = (int64_t)h_st->rows - before;
+        stats.rows_fired += fired;
+        if (rows_out) *rows_out = fired;
+        return GW_OK;
+    }
+};
+
+// ------------------------------------------------------------------------- ABI
+extern "C" {
+
+int gw_abi_version(void) { return GW_ABI_VERSION; }
+
+const char* gw_last_error(const gw_handle* h) {
+    if (!h) return g_create_error.c_str();
+    return h->err.c_str();
+}
+
+static int validate(const gw_config* c, std::string& why) {
+    auto ab = [](int64_t v) { return v < 0 ? -v : v; };
+    if (c->assigner == GW_TUMBLING) {
+        if (c->size <= 0 || ab(c->offset) >= c->size) {
+            why = "TumblingEventTimeWindows parameters must satisfy abs(offset) < size";
+            return GW_E_INVALID;
+        }
+    } else if (c->assigner == GW_SLIDING) {
+        if (c->slide <= 0 || ab(c->offset) >= c->slide || c->size <= 0) {
+            why = "SlidingEventTimeWindows parameters must satisfy abs(offset) < slide and size > 0";
+            return GW_E_INVALID;
+        }
+        if (c->size / c->slide > 10000000) {
+            why = "SlidingEventTimeWindows parameters must satisfy size / slide <= 10000000";
+            return GW_E_INVALID;
+        }
+    } else if (c->assigner == GW_SESSION) {
+        if (c->gap <= 0) {
+            why = "EventTimeSessionWindows parameters must satisfy 0 < size";
+            return GW_E_INVALID;
+        }
+    } else {
+        why = "unknown window assigner";
+        return GW_E_INVALID;
+    }
+    if (c->allowed_lateness < 0) { why = "The allowed lateness cannot be negative."; return GW_E_INVALID; }
+    if (c->agg < GW_COUNT || c->agg > GW_SUM_I32) { why = "unknown aggregate"; return GW_E_INVALID; }
+    if (c->trigger != GW_EVENT_TIME_TRIGGER && c->trigger != GW_PURGING_EVENT_TIME_TRIGGER) {
+        why = "unknown trigger";
+        return GW_E_INVALID;
+    }
+    if (c->allowed_lateness != 0) {
+        why = "allowed lateness > 0 is not yet supported on the GPU path";
+        return GW_E_UNSUPPORTED;
+    }
+    return GW_OK;
+}
+
+int gw_create(const gw_config* cfg, gw_handle** out) {
+    if (!cfg || !out) { g_create_error = "null argument"; return GW_E_INVALID; }
+    *out = nullptr;
+    std::string why;
+    int rc = validate(cfg, why);
+    if (rc) { g_create_error = why; return rc; }
+    gw_handle* h = new (std::nothrow) gw_handle();
+    if (!h) { g_create_error = "out of host memory"; return GW_E_OOM; }
+    h->cfg = *cfg;
+    if (h->cfg.max_parallelism <= 0) h->cfg.max_parallelism = 128;
+    if (h->cfg.parallelism <= 0) h->cfg.parallelism = 1;
+    if (h->cfg.max_batch <= 0) h->cfg.max_batch = 1 << 20;
+    auto bail = [&](int code, const std::string& msg) {
+        g_create_error = msg;
+        gw_destroy(h);
+        return code;
+    };
+    hipError_t e = hipSetDevice(cfg->device);
+    if (e != hipSuccess) return bail(GW_E_DEVICE, std::string("hipSetDevice: ") + hipGetErrorString(e));
+    if ((e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking)) != hipSuccess)
+        return bail(GW_E_DEVICE, std::string("hipStreamCreate: ") + hipGetErrorString(e));
+    if ((e = hipMalloc((void**)&h->d_st, sizeof(DevStatus))) != hipSuccess ||
+        (e = hipMalloc((void**)&h->d_tmp, 64)) != hipSuccess ||
+        (e = hipHostMalloc((void**)&h->h_st, sizeof(DevStatus), hipHostMallocDefault)) != hipSuccess)
+        return bail(GW_E_DEVICE, std::string("status alloc: ") + hipGetErrorString(e));
+    hipMemset(h->d_st, 0, sizeof(DevStatus));
+    memset(h->h_st, 0, sizeof(DevStatus));
+
+    const int agg = cfg->agg;
+    const int words = cell_words(agg);
+    h->tv.agg = agg;
+    h->tv.words = words;
+    int64_t hint = cfg->capacity_hint > 0 ? cfg->capacity_hint : 1 << 16;
+    int64_t cap = 1024;
+    while ((double)cap * 0.7 < (double)hint) cap *= 2;
+
+    if (cfg->assigner == GW_SESSION) {
+        h->session = true;
+        rc = session_create(h->sess, *cfg, cap, h->stream, h->d_st, why);
+        if (rc) return bail(rc, why);
+        hipStreamSynchronize(h->stream);
+        *out = h;
+        return GW_OK;
+    }
+    const int64_t size = cfg->size;
+    const int64_t slide = cfg->assigner == GW_TUMBLING ? cfg->size : cfg->slide;
+    h->g = gcd64(size, slide);
+    h->m = slide / h->g;
+    h->n = size / h->g;
+    // ring: n panes of the oldest unfired window + at least one pane ahead, filling
+    // the slot up to the next 64-byte line
+    int64_t need = h->n + std::max<int64_t>(h->m, 1);
+    if (need > kMaxRing)
+        return bail(GW_E_UNSUPPORTED, "size/gcd(size,slide) + slide/gcd(size,slide) > 64 panes is not supported "
+                                      "on the GPU path");
+    int stride_w = (int)(((2 + need * words) + 7) / 8 * 8);
+    int R = (stride_w - 2) / words;
+    if (R > kMaxRing) R = kMaxRing;
+    h->R = R;
+    h->tv.ring = R;
+    h->tv.stride_w = stride_w;
+    h->div = make_udiv((uint64_t)h->g);
+    h->fired_k = h->k_for_wm(INT64_MIN) + 1;
+    h->B = h->fired_k * h->m;
+    rc = h->alloc_table(h->tv, cap);
+    if (rc) return bail(rc, h->err);
+    h->table_bytes = (size_t)(cap + 1) * (size_t)stride_w * 8;
+    rc = h->ensure_deferred(1 << 16);
+    if (rc) return bail(rc, h->err);
+    if ((e = hipStreamSynchronize(h->stream)) != hipSuccess)
+        return bail(GW_E_DEVICE, std::string("init: ") + hipGetErrorString(e));
+    *out = h;
+    return GW_OK;
+}
+
+int gw_destroy(gw_handle* h) {
+    if (!h) return GW_OK;
+    if (h->stream) hipStreamSynchronize(h->stream);
+    if (h->sess) session_destroy(h->sess);
+    if (h->tv.base) hipFree(h->tv.base);
+    for (int b = 0; b < 2; ++b) {
+        if (h->dk[b]) { hipFree(h->dk[b]); hipFree(h->dp[b]); hipFree(h->da0[b]); hipFree(h->da1[b]); }
+    }
+    if (h->o_key) { hipFree(h->o_key); hipFree(h->o_start); hipFree(h->o_end); hipFree(h->o_res); }
+    if (h->h_stage) { hipHostFree(h->h_stage); hipFree(h->d_stage); hipFree(h->d_hash_stage); }
+    if (h->d_st) hipFree(h->d_st);
+    if (h->d_tmp) hipFree(h->d_tmp);
+    if (h->h_st) hipHostFree(h->h_st);
+    h->t_ingest.destroy();
+    h->t_fire.destroy();
+    if (h->stream) hipStreamDestroy(h->stream);
+    delete h;
+    return GW_OK;
+}
+
+static int ingest_device_impl(gw_handle* h, int64_t n, const int64_t* key, const int64_t* ts,
+                              const int64_t* val) {
+    if (h->session) {
+        int rc = session_ingest(h->sess, n, key, ts, val, h->wm, h->err);
+        if (rc == GW_OK) { h->stats.events_in += n; h->stats.batches++; }
+        else if (rc == GW_E_DEVICE || rc == GW_E_NO_TIMESTAMP || rc == GW_E_RANGE) h->failed = true;
+        return rc;
+    }
+    return h->ingest_pane(n, key, ts, val);
+}
+
+int gw_ingest(gw_handle* h, int64_t n, const int64_t* key, const int32_t* key_hash, const int64_t* ts,
+              const void* value) {
+    if (!h) return GW_E_INVALID;
+    if (h->failed) return h->fail(GW_E_STATE, "operator failed earlier: %s", h->err.c_str());
+    if (n < 0 || (n > 0 && (!key || !ts))) return h->fail(GW_E_INVALID, "null key/ts column");
+    if (n > 0 && !value && h->cfg.agg != GW_COUNT) return h->fail(GW_E_INVALID, "value column required");
+    (void)key_hash;
+    hipSetDevice(h->cfg.device);
+    const int64_t chunk = h->cfg.max_batch;
+    for (int64_t off = 0; off < n; off += chunk) {
+        const int64_t c = std::min(chunk, n - off);
+        int rc = h->ensure_stage(c);
+        if (rc) return rc;
+        memcpy(h->h_stage, key + off, (size_t)c * 8);
+        memcpy(h->h_stage + c, ts + off, (size_t)c * 8);
+        if (value) memcpy(h->h_stage + 2 * c, (const int64_t*)value + off, (size_t)c * 8);
+        {
+            hipError_t e = hipMemcpyAsync(h->d_stage, h->h_stage, (size_t)c * (value ? 24 : 16),
+                                          hipMemcpyHostToDevice, h->stream);
+            if (e != hipSuccess) return h->fail(GW_E_DEVICE, "H2D: %s", hipGetErrorString(e));
+        }
+        rc = ingest_device_impl(h, c, h->d_stage, h->d_stage + c, value ? h->d_stage + 2 * c : nullptr);
+        if (rc) return rc;
+    }
+    return GW_OK;
+}
+
+int gw_ingest_device(gw_handle* h, int64_t n, const int64_t* d_key, const int32_t* d_key_hash,
+                     const int64_t* d_ts, const void* d_value, void* stream) {
+    if (!h) return GW_E_INVALID;
+    if (h->failed) return h->fail(GW_E_STATE, "operator failed earlier: %s", h->err.c_str());
+    if (n < 0 || (n > 0 && (!d_key || !d_ts))) return h->fail(GW_E_INVALID, "null key/ts column");
+    if (n > 0 && !d_value && h->cfg.agg != GW_COUNT) return h->fail(GW_E_INVALID, "value column required");
+    (void)d_key_hash;
+    hipSetDevice(h->cfg.device);
+    if (stream && (hipStream_t)stream != h->stream) {
+        hipEvent_t ev;
+        hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+        hipEventRecord(ev, (hipStream_t)stream);
+        hipStreamWaitEvent(h->stream, ev, 0);
+        hipEventDestroy(ev);
+    }
+    if (n == 0) return GW_OK;
+    return ingest_device_impl(h, n, d_key, d_ts, (const int64_t*)d_value);
+}
+
+int gw_advance_watermark(gw_handle* h, int64_t wm, int64_t* rows_fired) {
+    if (!h) return GW_E_INVALID;
+    if (h->failed) return h->fail(GW_E_STATE, "operator failed earlier: %s", h->err.c_str());
+    hipSetDevice(h->cfg.device);
+    if (h->session) {
+        int64_t fired = 0;
+        int rc = GW_OK;
+        if (wm > h->wm) {
+            rc = session_fire(h->sess, wm, &fired, h->err);
+            if (rc == GW_OK) h->wm = wm;
+            else if (rc == GW_E_DEVICE) h->failed = true;
+        }
+        h->stats.rows_fired += fired;
+        if (rows_fired) *rows_fired = fired;
+        return rc;
+    }
+    return h->advance_pane(wm, rows_fired);
+}
+
+int gw_end_input(gw_handle* h, int64_t* rows_fired) { return gw_advance_watermark(h, INT64_MAX, rows_fired); }
+
+static void rows_view(gw_handle* h, int64_t** k, int64_t** s, int64_t** e, int64_t** r, int64_t* total) {
+    if (h->session) {
+        session_rows(h->sess, k, s, e, r, total);
+    } else {
+        *k = h->o_key; *s = h->o_start; *e = h->o_end; *r = h->o_res;
+        *total = (int64_t)h->h_st->rows;
+    }
+}
+
+int gw_pending_rows(gw_handle* h, int64_t* n) {
+    if (!h || !n) return GW_E_INVALID;
+    int rc = h->session ? session_refresh(h->sess, h->err) : h->refresh();
+    if (rc) return rc;
+    int64_t *k, *s, *e, *r, total;
+    rows_view(h, &k, &s, &e, &r, &total);
+    *n = total - h->rows_head;
+    return GW_OK;
+}
+
+int gw_drain(gw_handle* h, int64_t* key, int64_t* start, int64_t* end, void* result, int64_t cap,
+             int64_t* n) {
+    if (!h || !n) return GW_E_INVALID;
+    int64_t pending;
+    int rc = gw_pending_rows(h, &pending);
+    if (rc) return rc;
+    int64_t *k, *s, *e, *r, total;
+    rows_view(h, &k, &s, &e, &r, &total);
+    const int64_t c = std::min(cap, pending);
+    const int64_t o = h->rows_head;
+    hipError_t err = hipSuccess;
+    if (c > 0) {
+        if (key) err = hipMemcpyAsync(key, k + o, c * 8, hipMemcpyDeviceToHost, h->stream);
+        if (start && err == hipSuccess) err = hipMemcpyAsync(start, s + o, c * 8, hipMemcpyDeviceToHost, h->stream);
+        if (end && err == hipSuccess) err = hipMemcpyAsync(end, e + o, c * 8, hipMemcpyDeviceToHost, h->stream);
+        if (result && err == hipSuccess) err = hipMemcpyAsync(result, r + o, c * 8, hipMemcpyDeviceToHost, h->stream);
+        if (err == hipSuccess) err = hipStreamSynchronize(h->stream);
+        if (err != hipSuccess) return h->fail(GW_E_DEVICE, "D2H rows: %s", hipGetErrorString(err));
+    }
+    *n = c;
+    h->rows_head += c;
+    if (h->rows_head == total) {
+        rc = gw_clear_rows(h);
+        if (rc) return rc;
+    }
+    return c < pending ? GW_E_OUTPUT_FULL : GW_OK;
+}
+
+int gw_rows_device(gw_handle* h, const int64_t** d_key, const int64_t** d_start, const int64_t** d_end,
+                   const void** d_result, int64_t* n) {
+    if (!h) return GW_E_INVALID;
+    int64_t pending;
+    int rc = gw_pending_rows(h, &pending);
+    if (rc) return rc;
+    int64_t *k, *s, *e, *r, total;
+    rows_view(h, &k, &s, &e, &r, &total);
+    const int64_t o = h->rows_head;
+    if (d_key) *d_key = k ? k + o : nullptr;
+    if (d_start) *d_start = s ? s + o : nullptr;
+    if (d_end) *d_end = e ? e + o : nullptr;
+    if (d_result) *d_result = r ? r + o : nullptr;
+    if (n) *n = pending;
+    return GW_OK;
+}
+
+int gw_clear_rows(gw_handle* h) {
+    if (!h) return GW_E_INVALID;
+    h->rows_head = 0;
+    if (h->session) return session_clear_rows(h->sess, h->err);
+    return h->set_field(offsetof(DevStatus, rows), 0);
+}
+
+int64_t gw_late_dropped(const gw_handle* h) {
+    if (!h) return 0;
+    if (h->session) return session_late(h->sess);
+    return (int64_t)h->h_st->late;
+}
+
+int gw_get_stats(const gw_handle* h, gw_stats* out) {
+    if (!h || !out) return GW_E_INVALID;
+    *out = h->stats;
+    if (h->session) {
+        session_stats(h->sess, out);
+    } else {
+        out->late_dropped = (int64_t)h->h_st->late;
+        out->live_keys = (int64_t)h->h_st->used_slots;
+        out->deferred = (int64_t)h->h_st->n_deferred;
+        out->table_capacity = h->tv.cap;
+        out->table_bytes = (int64_t)h->table_bytes;
+    }
+    return GW_OK;
+}
+
+int gw_synchronize(gw_handle* h) {
+    if (!h) return GW_E_INVALID;
+    hipError_t e = hipStreamSynchronize(h->stream);
+    if (e != hipSuccess) return h->fail(GW_E_DEVICE, "sync: %s", hipGetErrorString(e));
+    return GW_OK;
+}
+
+void* gw_stream(gw_handle* h) { return h ? (void*)h->stream : nullptr; }
+
+int gw_enable_kernel_timing(gw_handle* h, int enable) {
+    if (!h) return GW_E_INVALID;
+    h->timing = enable != 0;
+    if (h->sess) session_enable_timing(h->sess, h->timing);
+    return GW_OK;
+}
+
+int gw_kernel_time_ms(gw_handle* h, int which, double* ms, int64_t* launches) {
+    if (!h) return GW_E_INVALID;
+    hipStreamSynchronize(h->stream);
+    if (h->sess) return session_kernel_time(h->sess, which, ms, launches);
+    KernelTimer& t = which == 0 ? h->t_ingest : h->t_fire;
+    t.resolve();
+    if (ms) *ms = t.launches ? t.total_ms / (double)t.launches : 0.0;
+    if (launches) *launches = t.launches;
+    t.total_ms = 0;
+    t.launches = 0;
+    return GW_OK;
+}
+
+// ---------------------------------------------------------------- key groups
+int32_t gw_java_long_hash(int64_t key) { return java_long_hash(key); }
+int32_t gw_murmur_hash(int32_t code) { return murmur_hash(code); }
+int32_t gw_key_group_for_hash(int32_t h, int32_t max_p) { return key_group_for_hash(h, max_p); }
+int32_t gw_operator_for_key_group(int32_t max_p, int32_t p, int32_t kg) { return operator_for_key_group(max_p, p, kg); }
+int32_t gw_default_max_parallelism(int32_t p) {
+    uint32_t u = (uint32_t)(p + p / 2) - 1u;
+    u |= u >> 1; u |= u >> 2; u |= u >> 4; u |= u >> 8; u |= u >> 16;
+    int32_t v = (int32_t)(u + 1u);
+    return std::min(std::max(v, 128), 32768);
+}
+
+int gw_key_groups_device(int64_t n, const int64_t* d_key, const int32_t* d_key_hash, int32_t max_p, int32_t p,
+                         int32_t* d_kg, int32_t* d_owner, void* stream) {
+    if (n < 0 || max_p <= 0 || p <= 0 || p > max_p) return GW_E_INVALID;
+    if (n == 0) return GW_OK;
+    hipError_t e = launch_key_groups(n, d_key, d_key_hash, max_p, p, d_kg, d_owner, (hipStream_t)stream);
+    if (e != hipSuccess) { g_create_error = hipGetErrorString(e); return GW_E_DEVICE; }
+    return GW_OK;
+}
+
+int64_t gw_partition_scratch_bytes(int64_t n, int32_t p) { return partition_scratch_bytes(n, p); }
+
+int gw_partition_device(int64_t n, const int64_t* d_key, const int32_t* d_key_hash, const int64_t* d_ts,
+                        const void* d_value, int32_t max_p, int32_t p, int64_t* d_key_out, int64_t* d_ts_out,
+                        void* d_value_out, int64_t* d_counts, void* d_scratch, void* stream) {
+    if (n < 0 || max_p <= 0 || p <= 0 || p > max_p || p > 256) return GW_E_INVALID;
+    hipStream_t s = (hipStream_t)stream;
+    if (n == 0) {
+        hipError_t e = hipMemsetAsync(d_counts, 0, (size_t)p * 8, s);
+        return e == hipSuccess ? GW_OK : GW_E_DEVICE;
+    }
+    hipError_t e = launch_partition(n, d_key, d_key_hash, d_ts, (const int64_t*)d_value, max_p, p, d_key_out,
+                                    d_ts_out, (int64_t*)d_value_out, d_counts, d_scratch, s);
+    if (e != hipSuccess) { g_create_error = hipGetErrorString(e); return GW_E_DEVICE; }
+    return GW_OK;
+}
+
+}  // extern "C"

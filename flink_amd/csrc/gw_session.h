@@ -1,0 +1,25 @@
+// gw_session.h — host interface of the event-time session-window path (gw_session.hip).
+#pragma once
+#include <string>
+
+#include "gw_device.h"
+
+namespace gw {
+
+struct SessionState;
+
+int session_create(SessionState*& s, const gw_config& cfg, int64_t cap, hipStream_t stream, DevStatus* unused,
+                   std::string& why);
+void session_destroy(SessionState* s);
+int session_ingest(SessionState* s, int64_t n, const int64_t* key, const int64_t* ts, const int64_t* val,
+                   int64_t wm, std::string& err);
+int session_fire(SessionState* s, int64_t wm, int64_t* fired, std::string& err);
+void session_rows(SessionState* s, int64_t** k, int64_t** st, int64_t** en, int64_t** r, int64_t* total);
+int session_refresh(SessionState* s, std::string& err);
+int session_clear_rows(SessionState* s, std::string& err);
+int64_t session_late(SessionState* s);
+void session_stats(SessionState* s, gw_stats* out);
+void session_enable_timing(SessionState* s, bool on);
+int session_kernel_time(SessionState* s, int which, double* ms, int64_t* launches);
+
+}  // namespace gw

@@ -1,0 +1,646 @@
+// gw_session.hip — event-time session windows (gap merge) on gfx950.
+//
+// Reference semantics (paths relative to the Flink tree):
+//   EventTimeSessionWindows.assignWindows -> [ts, ts + gap)
+//     (flink-streaming-java/.../api/windowing/assigners/EventTimeSessionWindows.java:61-64)
+//   TimeWindow.intersects (inclusive: touching windows merge) / cover / mergeWindows
+//     (RS/api/windowing/windows/TimeWindow.java:116-123,208-254)
+//   MergingWindowSet.addWindow (RS/runtime/operators/windowing/MergingWindowSet.java:153-224)
+//   WindowOperator.processElement merging branch incl. "drop if the window is already
+//     late" (RS/runtime/operators/windowing/WindowOperator.java:303-403)
+//   AbstractHeapMergingState.mergeNamespaces (RR/state/heap/AbstractHeapMergingState.java:65-91)
+//   EventTimeTrigger + onEventTime: a session fires once when end-1 <= watermark.
+//
+// MI355X design: per watermark batch, records are grouped by (state
+// slot, timestamp) with a hand-written radix sort; each slot's sorted records are
+// swept against its in-flight sessions (<= K kept inline in the 64/128-byte slot).
+// Without late records the result of the reference's record-at-a-time merging is the
+// set of connected components of all windows (inclusive intersection), which a
+// sorted sweep computes in one pass.  If a slot's batch holds a record whose own
+// window is already late, the reference's outcome depends on arrival order (a late
+// window is dropped unless it touches an in-flight session at that moment), so that
+// slot is replayed record by record in arrival order.
+#include "gw_kernels.h"
+#include "gw_session.h"
+#include "gw_sort.h"
+
+#include <algorithm>
+#include <cstring>
+#include <cstdio>
+#include <vector>
+
+namespace gw {
+
+constexpr int kMaxLocalSess = 32;
+
+struct SegArgs {
+    const uint64_t* skey;   // sorted (slot << ts_bits) | (ts - ts_min)
+    const uint32_t* perm;   // original record index
+    int64_t n;
+    int ts_bits;
+    int64_t ts_min;
+    const int64_t* val;
+    int64_t gap;
+    int64_t wm;             // current watermark (all records of the batch see it)
+    TableView t;            // ring = K sessions per slot, words = words per session
+    const uint32_t* retry_in;
+    int64_t n_retry_in;
+    uint32_t* retry_out;    // appended at st->overflow
+    DevStatus* st;
+};
+
+__global__ void __launch_bounds__(256) k_sess_minmax(const int64_t* ts, int64_t n, long long* mm,
+                                                     DevStatus* st) {
+    long long lo = INT64_MAX, hi = INT64_MIN;
+    unsigned long long flags = 0;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const long long t = ts[i];
+        if (t == INT64_MIN) { flags |= GW_DF_NO_TS; continue; }
+        lo = t < lo ? t : lo;
+        hi = t > hi ? t : hi;
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        long long a = __shfl_xor(lo, o), b = __shfl_xor(hi, o);
+        lo = a < lo ? a : lo;
+        hi = b > hi ? b : hi;
+    }
+    if (__lane_id() == 0) {
+        if (lo != INT64_MAX) atomicMin(&mm[0], lo);
+        if (hi != INT64_MIN) atomicMax(&mm[1], hi);
+    }
+    wave_or(&st->flags, flags);
+}
+
+__global__ void __launch_bounds__(256) k_sess_prep(const int64_t* key, const int64_t* ts, int64_t n, int64_t ts_min,
+                                                   int ts_bits, TableView t, uint64_t* skey, uint32_t* perm,
+                                                   DevStatus* st) {
+    unsigned long long ins = 0, flags = 0;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        bool inserted;
+        int64_t s = find_or_insert(t, key[i], inserted);
+        ins += inserted;
+        if (s < 0) { flags |= GW_DF_TABLE_FULL; s = 0; }
+        skey[i] = ((uint64_t)s << ts_bits) | (uint64_t)(ts[i] - ts_min);
+        perm[i] = (uint32_t)i;
+    }
+    wave_add(&st->used_slots, ins);
+    wave_or(&st->flags, flags);
+}
+
+struct Sess {
+    int64_t s, e, a0, a1;
+};
+
+template <int AGG>
+__device__ void seg_process(const SegArgs& a, int64_t i) {
+    const uint64_t tsmask = (a.ts_bits >= 64) ? ~0ull : ((1ull << a.ts_bits) - 1ull);
+    const int64_t slot = (int64_t)(a.skey[i] >> a.ts_bits);
+    int64_t j = i + 1;
+    while (j < a.n && (int64_t)(a.skey[j] >> a.ts_bits) == slot) ++j;
+    int64_t* sp = slot_ptr(a.t, slot);
+    const int SW = a.t.words;
+    const int K = a.t.ring;
+    Sess cur_list[kMaxLocalSess];
+    int cnt = (int)sp[1];
+    for (int q = 0; q < cnt; ++q) {
+        const int64_t* x = sp + 2 + q * SW;
+        cur_list[q] = Sess{x[0], x[1], x[2], SW == 4 ? x[3] : 0};
+    }
+    unsigned long long late = 0, merges = 0, flags = 0;
+    const int64_t ts_first = a.ts_min + (int64_t)(a.skey[i] & tsmask);
+    bool ok = true;
+    if ((uint64_t)ts_first > (uint64_t)INT64_MAX - (uint64_t)a.gap && ts_first > 0) flags |= GW_DF_RANGE;
+    const bool any_late = ts_first + a.gap - 1 <= a.wm;  // sorted by ts: the first is the earliest
+    if (!any_late) {
+        // Sweep old sessions and the batch's windows in start order; merge on inclusive intersect.
+        Sess out[kMaxLocalSess];
+        int nout = 0, oi = 0;
+        int64_t e = i;
+        bool have = false;
+        bool cur_has_state = false;
+        Sess cur{0, 0, 0, 0};
+        while (oi < cnt || e < j) {
+            Sess item;
+            bool is_old;
+            const int64_t te = e < j ? a.ts_min + (int64_t)(a.skey[e] & tsmask) : INT64_MAX;
+            if (oi < cnt && (e >= j || cur_list[oi].s <= te)) {
+                item = cur_list[oi++];
+                is_old = true;
+            } else {
+                int64_t c0, c1;
+                record_cell(AGG, a.val ? a.val[a.perm[e]] : 0, c0, c1);
+                item = Sess{te, te + a.gap, c0, c1};
+                is_old = false;
+                ++e;
+            }
+            if (!have) {
+                cur = item;
+                have = true;
+                cur_has_state = is_old;
+            } else if (item.s <= cur.e) {
+                if (item.e > cur.e) cur.e = item.e;
+                fold_cell(AGG, cur.a0, cur.a1, item.a0, item.a1);
+                if (is_old && cur_has_state) merges++;
+                cur_has_state |= is_old;
+            } else {
+                if (nout == kMaxLocalSess) { ok = false; break; }
+                out[nout++] = cur;
+                cur = item;
+                cur_has_state = is_old;
+            }
+        }
+        if (ok && have) {
+            if (nout == kMaxLocalSess) ok = false;
+            else out[nout++] = cur;
+        }
+        if (ok) {
+            for (int q = 0; q < nout; ++q) cur_list[q] = out[q];
+            cnt = nout;
+        }
+    } else {
+        // Arrival-order replay (MergingWindowSet.addWindow per record).
+        int64_t last = -1;
+        for (int64_t step = i; step < j && ok; ++step) {
+            int64_t best = -1;
+            uint32_t bp = 0xffffffffu;
+            for (int64_t x = i; x < j; ++x) {
+                const uint32_t p = a.perm[x];
+                if ((int64_t)p > last && p < bp) { bp = p; best = x; }
+            }
+            last = bp;
+            const int64_t ts = a.ts_min + (int64_t)(a.skey[best] & tsmask);
+            const int64_t ws = ts, we = ts + a.gap;
+            int lo = -1, hi = -1;
+            for (int q = 0; q < cnt; ++q) {
+                if (cur_list[q].s <= we && cur_list[q].e >= ws) {
+                    if (lo < 0) lo = q;
+                    hi = q;
+                }
+            }
+            int64_t c0, c1;
+            record_cell(AGG, a.val ? a.val[bp] : 0, c0, c1);
+            if (lo < 0) {
+                if (we - 1 <= a.wm) { late++; continue; }  // isWindowLate -> retireWindow, dropped
+                if (cnt == kMaxLocalSess) { ok = false; break; }
+                int q = cnt;
+                while (q > 0 && cur_list[q - 1].s > ws) { cur_list[q] = cur_list[q - 1]; --q; }
+                cur_list[q] = Sess{ws, we, c0, c1};
+                cnt++;
+            } else {
+                Sess m = cur_list[lo];
+                if (ws < m.s) m.s = ws;
+                for (int q = lo + 1; q <= hi; ++q) {
+                    if (cur_list[q].e > m.e) m.e = cur_list[q].e;
+                    fold_cell(AGG, m.a0, m.a1, cur_list[q].a0, cur_list[q].a1);
+                    merges++;
+                }
+                if (we > m.e) m.e = we;
+                fold_cell(AGG, m.a0, m.a1, c0, c1);
+                cur_list[lo] = m;
+                const int removed = hi - lo;
+                for (int q = hi + 1; q < cnt; ++q) cur_list[q - removed] = cur_list[q];
+                cnt -= removed;
+            }
+        }
+    }
+    if (!ok || cnt > K) {
+        // does not fit the slot: leave the slot untouched, retry after widening
+        const unsigned long long at = atomicAdd(&a.st->overflow, 1ull);
+        a.retry_out[at] = (uint32_t)i;
+        atomicMax(&a.st->pad[1], (unsigned long long)(ok ? cnt : kMaxLocalSess + 1));
+        return;
+    }
+    for (int q = 0; q < cnt; ++q) {
+        int64_t* x = sp + 2 + q * SW;
+        x[0] = cur_list[q].s;
+        x[1] = cur_list[q].e;
+        x[2] = cur_list[q].a0;
+        if (SW == 4) x[3] = cur_list[q].a1;
+    }
+    sp[1] = cnt;
+    if (late) atomicAdd(&a.st->late, late);
+    if (merges) atomicAdd(&a.st->merges, merges);
+    if (flags) atomicOr(&a.st->flags, flags);
+}
+
+template <int AGG>
+__global__ void __launch_bounds__(256) k_sess_segment(SegArgs a) {
+    if (a.retry_in) {
+        for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < a.n_retry_in;
+             r += (int64_t)gridDim.x * blockDim.x)
+            seg_process<AGG>(a, (int64_t)a.retry_in[r]);
+        return;
+    }
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < a.n; i += (int64_t)gridDim.x * blockDim.x) {
+        if (i > 0 && (a.skey[i] >> a.ts_bits) == (a.skey[i - 1] >> a.ts_bits)) continue;
+        seg_process<AGG>(a, i);
+    }
+}
+
+// Fire every in-flight session with end-1 <= wm (sessions in a slot are disjoint and
+// sorted, so the fired ones are a prefix), emit (key, start, end, result), purge.
+template <int AGG>
+__global__ void __launch_bounds__(256) k_sess_fire(TableView t, int64_t wm, int64_t* o_key, int64_t* o_start,
+                                                   int64_t* o_end, int64_t* o_res, DevStatus* st) {
+    const int64_t nslots = t.cap + 1;
+    const int SW = t.words;
+    for (int64_t base = blockIdx.x * (int64_t)blockDim.x; base < nslots; base += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t i = base + threadIdx.x;
+        int64_t* s = nullptr;
+        int cnt = 0, nf = 0;
+        if (i < nslots) {
+            s = slot_ptr(t, i);
+            cnt = (int)s[1];
+            while (nf < cnt && s[2 + nf * SW + 1] - 1 <= wm) ++nf;
+        }
+        unsigned long long off = wave_reserve_n(&st->rows, (unsigned)nf);
+        if (nf) {
+            const int64_t key = s[0];
+            for (int q = 0; q < nf; ++q) {
+                const int64_t* x = s + 2 + q * SW;
+                o_key[off] = key;
+                o_start[off] = x[0];
+                o_end[off] = x[1];
+                o_res[off] = cell_result(AGG, x[2], SW == 4 ? x[3] : 0);
+                off++;
+            }
+            for (int q = nf; q < cnt; ++q)
+                for (int w = 0; w < SW; ++w) s[2 + (q - nf) * SW + w] = s[2 + q * SW + w];
+            s[1] = cnt - nf;
+        }
+    }
+}
+
+__global__ void __launch_bounds__(256) k_sess_rewiden(TableView o, TableView n) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i <= o.cap; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t* s = slot_ptr(o, i);
+        int64_t* d = slot_ptr(n, i);
+        d[0] = s[0];
+        d[1] = s[1];
+        const int cnt = (int)s[1];
+        for (int w = 0; w < cnt * o.words; ++w) d[2 + w] = s[2 + w];
+    }
+}
+
+__global__ void __launch_bounds__(256) k_sess_init(TableView t) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i <= t.cap; i += (int64_t)gridDim.x * blockDim.x) {
+        int64_t* s = slot_ptr(t, i);
+        s[0] = kEmptyKey;
+        s[1] = 0;
+    }
+}
+
+#define GW_AGG_SWITCH(agg, CALL)                  \
+    switch (agg) {                                \
+    case GW_COUNT: CALL(GW_COUNT); break;         \
+    case GW_SUM_I64: CALL(GW_SUM_I64); break;     \
+    case GW_SUM_F64: CALL(GW_SUM_F64); break;     \
+    case GW_MIN_I64: CALL(GW_MIN_I64); break;     \
+    case GW_MAX_I64: CALL(GW_MAX_I64); break;     \
+    case GW_MIN_F64: CALL(GW_MIN_F64); break;     \
+    case GW_MAX_F64: CALL(GW_MAX_F64); break;     \
+    case GW_AVG_I64: CALL(GW_AVG_I64); break;     \
+    case GW_AVG_F64: CALL(GW_AVG_F64); break;     \
+    case GW_SUM_I32: CALL(GW_SUM_I32); break;     \
+    default: break;                               \
+    }
+
+static unsigned grid_of(int64_t n) {
+    int64_t g = (n + 255) / 256;
+    if (g < 1) g = 1;
+    if (g > 4096) g = 4096;
+    return (unsigned)g;
+}
+
+// --------------------------------------------------------------------------- host
+struct SessionState {
+    gw_config cfg{};
+    hipStream_t stream = nullptr;
+    TableView tv{};
+    DevStatus* d_st = nullptr;
+    DevStatus* h_st = nullptr;
+    long long* d_mm = nullptr;
+    uint64_t* k0 = nullptr;
+    uint64_t* k1 = nullptr;
+    uint32_t* v0 = nullptr;
+    uint32_t* v1 = nullptr;
+    uint32_t* r0 = nullptr;
+    uint32_t* r1 = nullptr;
+    void* scratch = nullptr;
+    int64_t buf_cap = 0;
+    int64_t* o_key = nullptr;
+    int64_t* o_start = nullptr;
+    int64_t* o_end = nullptr;
+    int64_t* o_res = nullptr;
+    int64_t o_cap = 0;
+    int64_t wm = INT64_MIN;
+    gw_stats stats{};
+    bool timing = false;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pending[2], ev_pool;
+    double t_total[2] = {0, 0};
+    int64_t t_count[2] = {0, 0};
+};
+
+static int dev_err(std::string& err, const char* what, hipError_t e) {
+    char b[256];
+    snprintf(b, sizeof(b), "%s: %s", what, hipGetErrorString(e));
+    err = b;
+    return GW_E_DEVICE;
+}
+#define SCHECK(x)                                        \
+    do {                                                 \
+        hipError_t e_ = (x);                             \
+        if (e_ != hipSuccess) return dev_err(err, #x, e_); \
+    } while (0)
+
+static void resolve_timers(SessionState* s) {
+    for (int w = 0; w < 2; ++w) {
+        for (auto& p : s->ev_pending[w]) {
+            float ms = 0;
+            if (hipEventElapsedTime(&ms, p.first, p.second) == hipSuccess) { s->t_total[w] += ms; s->t_count[w]++; }
+            s->ev_pool.push_back(p);
+        }
+        s->ev_pending[w].clear();
+    }
+}
+static std::pair<hipEvent_t, hipEvent_t> get_ev(SessionState* s) {
+    if (!s->ev_pool.empty()) { auto p = s->ev_pool.back(); s->ev_pool.pop_back(); return p; }
+    std::pair<hipEvent_t, hipEvent_t> p;
+    hipEventCreate(&p.first);
+    hipEventCreate(&p.second);
+    return p;
+}
+
+int session_refresh(SessionState* s, std::string& err) {
+    SCHECK(hipMemcpyAsync(s->h_st, s->d_st, sizeof(DevStatus), hipMemcpyDeviceToHost, s->stream));
+    SCHECK(hipStreamSynchronize(s->stream));
+    if (s->timing) resolve_timers(s);
+    if (s->h_st->flags & GW_DF_NO_TS) {
+        err = "Record has Long.MIN_VALUE timestamp (= no timestamp marker). Did you forget to call "
+              "'DataStream.assignTimestampsAndWatermarks(...)'?";
+        return GW_E_NO_TIMESTAMP;
+    }
+    if (s->h_st->flags & GW_DF_RANGE) {
+        err = "session window end overflows int64";
+        return GW_E_RANGE;
+    }
+    return GW_OK;
+}
+
+static int set_word(SessionState* s, size_t off, unsigned long long v, std::string& err) {
+    unsigned long long* hv = reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(s->h_st) + off);
+    *hv = v;
+    SCHECK(hipMemcpyAsync(reinterpret_cast<char*>(s->d_st) + off, hv, 8, hipMemcpyHostToDevice, s->stream));
+    SCHECK(hipStreamSynchronize(s->stream));
+    return GW_OK;
+}
+
+static int alloc_sess_table(SessionState* s, TableView& t, int64_t cap, int K, std::string& err) {
+    t = s->tv;
+    t.cap = cap;
+    t.ring = K;
+    t.stride_w = (int)(((2 + K * t.words) + 7) / 8 * 8);
+    SCHECK(hipMalloc((void**)&t.base, (size_t)(cap + 1) * t.stride_w * 8));
+    hipLaunchKernelGGL(k_sess_init, dim3(grid_of(cap + 1)), dim3(256), 0, s->stream, t);
+    SCHECK(hipGetLastError());
+    return GW_OK;
+}
+
+int session_create(SessionState*& out, const gw_config& cfg, int64_t cap, hipStream_t stream, DevStatus*,
+                   std::string& why) {
+    SessionState* s = new SessionState();
+    s->cfg = cfg;
+    s->stream = stream;
+    s->tv.agg = cfg.agg;
+    s->tv.words = cell_words(cfg.agg) == 2 ? 4 : 3;
+    std::string& err = why;
+    SCHECK(hipMalloc((void**)&s->d_st, sizeof(DevStatus)));
+    SCHECK(hipHostMalloc((void**)&s->h_st, sizeof(DevStatus), hipHostMallocDefault));
+    SCHECK(hipMalloc((void**)&s->d_mm, 16));
+    SCHECK(hipMemset(s->d_st, 0, sizeof(DevStatus)));
+    memset(s->h_st, 0, sizeof(DevStatus));
+    // K so that the slot fills a 64-byte (sum/count/min/max) or 128-byte (avg) line
+    const int K = s->tv.words == 3 ? 2 : 3;
+    int rc = alloc_sess_table(s, s->tv, cap, K, why);
+    if (rc) { session_destroy(s); return rc; }
+    out = s;
+    return GW_OK;
+}
+
+void session_destroy(SessionState* s) {
+    if (!s) return;
+    hipStreamSynchronize(s->stream);
+    hipFree(s->tv.base);
+    hipFree(s->d_st);
+    hipHostFree(s->h_st);
+    hipFree(s->d_mm);
+    hipFree(s->k0); hipFree(s->k1); hipFree(s->v0); hipFree(s->v1); hipFree(s->r0); hipFree(s->r1);
+    hipFree(s->scratch);
+    hipFree(s->o_key); hipFree(s->o_start); hipFree(s->o_end); hipFree(s->o_res);
+    for (int w = 0; w < 2; ++w) for (auto& p : s->ev_pending[w]) s->ev_pool.push_back(p);
+    for (auto& p : s->ev_pool) { hipEventDestroy(p.first); hipEventDestroy(p.second); }
+    delete s;
+}
+
+static int ensure_bufs(SessionState* s, int64_t n, std::string& err) {
+    if (n <= s->buf_cap) return GW_OK;
+    const int64_t c = std::max<int64_t>(n + n / 4, 1 << 16);
+    hipStreamSynchronize(s->stream);
+    hipFree(s->k0); hipFree(s->k1); hipFree(s->v0); hipFree(s->v1); hipFree(s->r0); hipFree(s->r1);
+    hipFree(s->scratch);
+    SCHECK(hipMalloc((void**)&s->k0, c * 8));
+    SCHECK(hipMalloc((void**)&s->k1, c * 8));
+    SCHECK(hipMalloc((void**)&s->v0, c * 4));
+    SCHECK(hipMalloc((void**)&s->v1, c * 4));
+    SCHECK(hipMalloc((void**)&s->r0, c * 4));
+    SCHECK(hipMalloc((void**)&s->r1, c * 4));
+    SCHECK(hipMalloc((void**)&s->scratch, radix_sort_scratch_bytes(c)));
+    s->buf_cap = c;
+    return GW_OK;
+}
+
+static int rehash_sess(SessionState* s, int64_t new_cap, std::string& err) {
+    TableView nt;
+    int rc = alloc_sess_table(s, nt, new_cap, s->tv.ring, err);
+    if (rc) return rc;
+    if ((rc = set_word(s, offsetof(DevStatus, used_slots), 0, err))) return rc;
+    SCHECK(launch_rehash(s->tv, nt, s->d_st, s->stream));
+    SCHECK(hipStreamSynchronize(s->stream));
+    hipFree(s->tv.base);
+    s->tv = nt;
+    s->stats.rehashes++;
+    return session_refresh(s, err);
+}
+
+static int widen(SessionState* s, int newK, std::string& err) {
+    TableView nt;
+    int rc = alloc_sess_table(s, nt, s->tv.cap, newK, err);
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_sess_rewiden, dim3(grid_of(s->tv.cap + 1)), dim3(256), 0, s->stream, s->tv, nt);
+    SCHECK(hipGetLastError());
+    SCHECK(hipStreamSynchronize(s->stream));
+    hipFree(s->tv.base);
+    s->tv = nt;
+    return GW_OK;
+}
+
+int session_ingest(SessionState* s, int64_t n, const int64_t* key, const int64_t* ts, const int64_t* val, int64_t wm,
+                   std::string& err) {
+    int rc;
+    if ((rc = session_refresh(s, err))) return rc;
+    if (n <= 0) return GW_OK;
+    if ((int64_t)n > (int64_t)0xffffffffLL) { err = "batch too large"; return GW_E_INVALID; }
+    // keep the linear-probing load below 0.7 (worst case: every record a new key)
+    if ((double)s->h_st->used_slots > 0.7 * (double)s->tv.cap ||
+        (double)(s->h_st->used_slots + n) > 0.95 * (double)s->tv.cap) {
+        int64_t want = s->tv.cap;
+        while ((double)(s->h_st->used_slots + n) > 0.7 * (double)want) want *= 2;
+        if ((rc = rehash_sess(s, want, err))) return rc;
+    }
+    if ((rc = ensure_bufs(s, n, err))) return rc;
+    const long long init_mm[2] = {INT64_MAX, INT64_MIN};
+    SCHECK(hipMemcpyAsync(s->d_mm, init_mm, 16, hipMemcpyHostToDevice, s->stream));
+    hipLaunchKernelGGL(k_sess_minmax, dim3(grid_of(n)), dim3(256), 0, s->stream, ts, n, s->d_mm, s->d_st);
+    long long mm[2];
+    SCHECK(hipMemcpyAsync(mm, s->d_mm, 16, hipMemcpyDeviceToHost, s->stream));
+    if ((rc = session_refresh(s, err))) return rc;
+    const uint64_t span = (uint64_t)mm[1] - (uint64_t)mm[0];
+    int ts_bits = 1;
+    while (ts_bits < 64 && (span >> ts_bits)) ++ts_bits;
+    int slot_bits = 1;
+    while (slot_bits < 63 && ((uint64_t)(s->tv.cap) >> slot_bits)) ++slot_bits;
+    if (ts_bits + slot_bits > 64) {
+        err = "session batch spans too many milliseconds for the (slot, ts) sort key";
+        return GW_E_UNSUPPORTED;
+    }
+    auto ev = s->timing ? get_ev(s) : std::pair<hipEvent_t, hipEvent_t>{};
+    if (s->timing) SCHECK(hipEventRecord(ev.first, s->stream));
+    for (int attempt = 0;; ++attempt) {
+        hipLaunchKernelGGL(k_sess_prep, dim3(grid_of(n)), dim3(256), 0, s->stream, key, ts, n, (int64_t)mm[0], ts_bits,
+                           s->tv, s->k0, s->v0, s->d_st);
+        if ((rc = session_refresh(s, err))) return rc;
+        if (!(s->h_st->flags & GW_DF_TABLE_FULL)) break;
+        if (attempt > 4) { err = "session state table full"; return GW_E_OOM; }
+        if ((rc = set_word(s, offsetof(DevStatus, flags), s->h_st->flags & ~GW_DF_TABLE_FULL, err))) return rc;
+        if ((rc = rehash_sess(s, s->tv.cap * 2, err))) return rc;
+        slot_bits++;
+        if (ts_bits + slot_bits > 64) { err = "session sort key overflow"; return GW_E_UNSUPPORTED; }
+    }
+    int alt = 0;
+    SCHECK(radix_sort_pairs(s->k0, s->v0, s->k1, s->v1, n, ts_bits + slot_bits, s->scratch, s->stream, &alt));
+    SegArgs a{};
+    a.skey = alt ? s->k1 : s->k0;
+    a.perm = alt ? s->v1 : s->v0;
+    a.n = n;
+    a.ts_bits = ts_bits;
+    a.ts_min = mm[0];
+    a.val = val;
+    a.gap = s->cfg.gap;
+    a.wm = wm;
+    a.st = s->d_st;
+    uint32_t* rin = s->r0;
+    uint32_t* rout = s->r1;
+    int64_t n_retry = 0;
+    for (int pass = 0;; ++pass) {
+        if ((rc = set_word(s, offsetof(DevStatus, overflow), 0, err))) return rc;
+        if ((rc = set_word(s, offsetof(DevStatus, pad[1]), 0, err))) return rc;
+        a.t = s->tv;
+        a.retry_in = pass ? rin : nullptr;
+        a.n_retry_in = n_retry;
+        a.retry_out = rout;
+        const unsigned g = pass ? grid_of(n_retry) : grid_of(n);
+#define L(A) hipLaunchKernelGGL(k_sess_segment<A>, dim3(g), dim3(256), 0, s->stream, a)
+        GW_AGG_SWITCH(s->cfg.agg, L);
+#undef L
+        SCHECK(hipGetLastError());
+        if ((rc = session_refresh(s, err))) return rc;
+        if (!s->h_st->overflow) break;
+        const unsigned long long need = s->h_st->pad[1];
+        if (need > (unsigned long long)kMaxLocalSess || pass > 8) {
+            err = "more than 32 in-flight sessions for one key in one batch is not supported on the GPU path";
+            return GW_E_UNSUPPORTED;
+        }
+        int newK = s->tv.ring;
+        while ((unsigned long long)newK < need) newK *= 2;
+        if (newK > kMaxLocalSess) newK = kMaxLocalSess;
+        if ((rc = widen(s, newK, err))) return rc;
+        n_retry = (int64_t)s->h_st->overflow;
+        std::swap(rin, rout);
+    }
+    if (s->timing) {
+        SCHECK(hipEventRecord(ev.second, s->stream));
+        s->ev_pending[0].push_back(ev);
+    }
+    return GW_OK;
+}
+
+int session_fire(SessionState* s, int64_t wm, int64_t* fired, std::string& err) {
+    int rc;
+    if ((rc = session_refresh(s, err))) return rc;
+    const int64_t before = (int64_t)s->h_st->rows;
+    const int64_t need = before + (int64_t)(s->h_st->used_slots + 1) * s->tv.ring;
+    if (need > s->o_cap) {
+        const int64_t c = std::max<int64_t>(need + need / 4, 1 << 16);
+        int64_t* nb[4];
+        for (int q = 0; q < 4; ++q) SCHECK(hipMalloc((void**)&nb[q], c * 8));
+        int64_t* old[4] = {s->o_key, s->o_start, s->o_end, s->o_res};
+        for (int q = 0; q < 4; ++q) {
+            if (old[q] && before) SCHECK(hipMemcpyAsync(nb[q], old[q], before * 8, hipMemcpyDeviceToDevice, s->stream));
+        }
+        SCHECK(hipStreamSynchronize(s->stream));
+        for (int q = 0; q < 4; ++q) hipFree(old[q]);
+        s->o_key = nb[0]; s->o_start = nb[1]; s->o_end = nb[2]; s->o_res = nb[3];
+        s->o_cap = c;
+    }
+    auto ev = s->timing ? get_ev(s) : std::pair<hipEvent_t, hipEvent_t>{};
+    if (s->timing) SCHECK(hipEventRecord(ev.first, s->stream));
+#define L(A)                                                                                                     \
+    hipLaunchKernelGGL(k_sess_fire<A>, dim3(grid_of(s->tv.cap + 1)), dim3(256), 0, s->stream, s->tv, wm, s->o_key, \
+                       s->o_start, s->o_end, s->o_res, s->d_st)
+    GW_AGG_SWITCH(s->cfg.agg, L);
+#undef L
+    SCHECK(hipGetLastError());
+    if (s->timing) {
+        SCHECK(hipEventRecord(ev.second, s->stream));
+        s->ev_pending[1].push_back(ev);
+    }
+    s->stats.fires++;
+    if ((rc = session_refresh(s, err))) return rc;
+    *fired = (int64_t)s->h_st->rows - before;
+    s->wm = wm;
+    return GW_OK;
+}
+
+void session_rows(SessionState* s, int64_t** k, int64_t** st, int64_t** en, int64_t** r, int64_t* total) {
+    *k = s->o_key; *st = s->o_start; *en = s->o_end; *r = s->o_res;
+    *total = (int64_t)s->h_st->rows;
+}
+
+int session_clear_rows(SessionState* s, std::string& err) { return set_word(s, offsetof(DevStatus, rows), 0, err); }
+
+int64_t session_late(SessionState* s) { return (int64_t)s->h_st->late; }
+
+void session_stats(SessionState* s, gw_stats* out) {
+    out->late_dropped = (int64_t)s->h_st->late;
+    out->live_keys = (int64_t)s->h_st->used_slots;
+    out->table_capacity = s->tv.cap;
+    out->table_bytes = (int64_t)(s->tv.cap + 1) * s->tv.stride_w * 8;
+    out->session_merges = (int64_t)s->h_st->merges;
+    out->fires = s->stats.fires;
+    out->rehashes = s->stats.rehashes;
+}
+
+void session_enable_timing(SessionState* s, bool on) { s->timing = on; }
+
+int session_kernel_time(SessionState* s, int which, double* ms, int64_t* launches) {
+    hipStreamSynchronize(s->stream);
+    resolve_timers(s);
+    const int w = which ? 1 : 0;
+    if (ms) *ms = s->t_count[w] ? s->t_total[w] / (double)s->t_count[w] : 0.0;
+    if (launches) *launches = s->t_count[w];
+    s->t_total[w] = 0;
+    s->t_count[w] = 0;
+    return GW_OK;
+}
+
+}  // namespace gw

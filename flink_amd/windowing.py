@@ -1,0 +1,524 @@
+"""Host-side mirror of the reference's keyed event-time window operator interface.
+
+Names, argument meaning and error behaviour follow Flink's DataStream windowing API
+so a job (or a harness test) reads the same:
+
+  * assigners   TumblingEventTimeWindows.of / SlidingEventTimeWindows.of /
+                EventTimeSessionWindows.with_gap
+                (flink-runtime/.../streaming/api/windowing/assigners/*.java,
+                 flink-streaming-java/.../EventTimeSessionWindows.java)
+  * triggers    EventTimeTrigger.create(), PurgingTrigger.of(...)
+  * operator    GpuWindowOperator — the OneInputStreamOperator slot of WindowOperator
+                (RS/runtime/operators/windowing/WindowOperator.java:102): open,
+                process_element, process_watermark, end_input, close.  Records between
+                two watermarks are batched into columns and handed to libgpuwin.so in one
+                gw_ingest call; process_watermark fires through gw_advance_watermark.
+  * errors      invalid configurations raise ValueError (IllegalArgumentException in
+                the reference), runtime failures raise GpuWinError (the task fails).
+
+Every call goes to the HIP library; there is no CPU path here.
+"""
+from __future__ import annotations
+
+import ctypes
+import struct
+from dataclasses import dataclass
+from typing import Any, Callable, Iterable, List, Optional
+
+import numpy as np
+
+from . import _native as N
+
+LONG_MIN = -(1 << 63)
+LONG_MAX = (1 << 63) - 1
+
+
+# --------------------------------------------------------------------------- time
+class Duration:
+    """java.time.Duration stand-in: milliseconds."""
+
+    @staticmethod
+    def of_millis(ms: int) -> int:
+        return int(ms)
+
+    @staticmethod
+    def of_seconds(s: int) -> int:
+        return int(s) * 1000
+
+    @staticmethod
+    def of_minutes(m: int) -> int:
+        return int(m) * 60_000
+
+
+# ---------------------------------------------------------------------- assigners
+class WindowAssigner:
+    kind = ""
+
+    def config(self) -> dict:
+        raise NotImplementedError
+
+
+class TumblingEventTimeWindows(WindowAssigner):
+    """TumblingEventTimeWindows.of(size[, offset]) — stagger ALIGNED."""
+    kind = "tumbling"
+
+    def __init__(self, size: int, offset: int = 0):
+        if abs(offset) >= size:  # TumblingEventTimeWindows.java:55-62
+            raise ValueError("TumblingEventTimeWindows parameters must satisfy abs(offset) < size")
+        self.size, self.offset = int(size), int(offset)
+
+    @staticmethod
+    def of(size: int, offset: int = 0) -> "TumblingEventTimeWindows":
+        return TumblingEventTimeWindows(size, offset)
+
+    def config(self):
+        return dict(assigner="tumbling", size=self.size, slide=self.size, offset=self.offset)
+
+
+class SlidingEventTimeWindows(WindowAssigner):
+    kind = "sliding"
+    MAX_WINDOW_NUM = 10_000_000
+
+    def __init__(self, size: int, slide: int, offset: int = 0):
+        if abs(offset) >= slide or size <= 0:  # SlidingEventTimeWindows.java:57-70
+            raise ValueError("SlidingEventTimeWindows parameters must satisfy abs(offset) < slide and size > 0")
+        if size // slide > self.MAX_WINDOW_NUM:
+            raise ValueError(f"SlidingEventTimeWindows parameters must satisfy size / slide <= {self.MAX_WINDOW_NUM}")
+        self.size, self.slide, self.offset = int(size), int(slide), int(offset)
+
+    @staticmethod
+    def of(size: int, slide: int, offset: int = 0) -> "SlidingEventTimeWindows":
+        return SlidingEventTimeWindows(size, slide, offset)
+
+    def config(self):
+        return dict(assigner="sliding", size=self.size, slide=self.slide, offset=self.offset)
+
+
+class EventTimeSessionWindows(WindowAssigner):
+    kind = "session"
+
+    def __init__(self, gap: int):
+        if gap <= 0:  # EventTimeSessionWindows.java:52-53
+            raise ValueError("EventTimeSessionWindows parameters must satisfy 0 < size")
+        self.gap = int(gap)
+
+    @staticmethod
+    def with_gap(gap: int) -> "EventTimeSessionWindows":
+        return EventTimeSessionWindows(gap)
+
+    withGap = with_gap
+
+    def config(self):
+        return dict(assigner="session", gap=self.gap)
+
+
+# ----------------------------------------------------------------------- triggers
+class EventTimeTrigger:
+    name = "event_time"
+
+    @staticmethod
+    def create() -> "EventTimeTrigger":
+        return EventTimeTrigger()
+
+
+class PurgingTrigger:
+    def __init__(self, nested):
+        if not isinstance(nested, EventTimeTrigger):
+            raise ValueError("only PurgingTrigger.of(EventTimeTrigger) is on the GPU path")
+        self.name = "purging_event_time"
+
+    @staticmethod
+    def of(nested) -> "PurgingTrigger":
+        return PurgingTrigger(nested)
+
+
+# ------------------------------------------------------------------ stream elements
+@dataclass
+class StreamRecord:
+    value: Any
+    timestamp: int
+
+
+@dataclass
+class Watermark:
+    timestamp: int
+
+
+MAX_WATERMARK = Watermark(LONG_MAX)
+
+
+def java_string_hash(s: str) -> int:
+    """JDK String.hashCode (UTF-16 code units, int arithmetic)."""
+    h = 0
+    data = s.encode("utf-16-le")
+    for i in range(0, len(data), 2):
+        h = (31 * h + (data[i] | (data[i + 1] << 8))) & 0xFFFFFFFF
+    return h - (1 << 32) if h >= (1 << 31) else h
+
+
+def java_hash(key) -> int:
+    """key.hashCode() for the key types the path supports."""
+    if isinstance(key, bool):
+        return 1231 if key else 1237
+    if isinstance(key, int):
+        if -(1 << 31) <= key < (1 << 31):
+            return key  # Integer.hashCode
+        return N.lib().gw_java_long_hash(key)
+    if isinstance(key, str):
+        return java_string_hash(key)
+    raise TypeError(f"unsupported key type {type(key).__name__}")
+
+
+def assign_to_key_group(key, max_parallelism: int) -> int:
+    """KeyGroupRangeAssignment.assignToKeyGroup (bit-exact, via libgpuwin.so)."""
+    return N.lib().gw_key_group_for_hash(java_hash(key), max_parallelism)
+
+
+def compute_operator_index_for_key_group(max_parallelism: int, parallelism: int, key_group: int) -> int:
+    return N.lib().gw_operator_for_key_group(max_parallelism, parallelism, key_group)
+
+
+def compute_key_group_range_for_operator_index(max_parallelism: int, parallelism: int, index: int):
+    """KeyGroupRangeAssignment.computeKeyGroupRangeForOperatorIndex (:93-106)."""
+    start = (index * max_parallelism + parallelism - 1) // parallelism
+    end = ((index + 1) * max_parallelism - 1) // parallelism
+    return start, end
+
+
+def compute_default_max_parallelism(parallelism: int) -> int:
+    return N.lib().gw_default_max_parallelism(parallelism)
+
+
+def _ptr(a: Optional[np.ndarray]):
+    return None if a is None else ctypes.c_void_p(a.ctypes.data)
+
+
+# ------------------------------------------------------------------------ operator
+class GpuWindowOperator:
+    """Keyed event-time window operator on one MI355X (one Flink subtask).
+
+    aggregate: one of count, sum_i64, sum_i32, sum_f64, min_i64, max_i64, min_f64,
+    max_f64, avg_i64, avg_f64 (the closed set of include/gpuwin.h).
+    key_selector / value_selector extract key and aggregated field from a record
+    value (defaults: value[0] and value[1], i.e. Tuple2 f0 / f1).
+    """
+
+    def __init__(self, assigner: WindowAssigner, aggregate: str, allowed_lateness: int = 0,
+                 trigger=None, key_selector: Callable = None, value_selector: Callable = None,
+                 max_parallelism: int = 128, parallelism: int = 1, operator_index: int = 0,
+                 device: int = 0, capacity_hint: int = 0, max_batch: int = 1 << 22, flags: int = 0):
+        if aggregate not in N.AGGS:
+            raise ValueError(f"unknown aggregate {aggregate!r}")
+        if allowed_lateness < 0:
+            raise ValueError("The allowed lateness cannot be negative.")
+        self.assigner = assigner
+        self.aggregate = aggregate
+        self.trigger = trigger or EventTimeTrigger.create()
+        self.key_selector = key_selector or (lambda v: v[0])
+        self.value_selector = value_selector or (lambda v: v[1])
+        self.is_double_out = aggregate in N.DOUBLE_RESULT
+        self.is_double_in = aggregate in N.DOUBLE_INPUT
+        c = N.GwConfig()
+        a = assigner.config()
+        c.assigner = N.ASSIGNERS[a["assigner"]]
+        c.trigger = N.TRIGGERS[self.trigger.name]
+        c.size, c.slide, c.offset = a.get("size", 0), a.get("slide", 0), a.get("offset", 0)
+        c.gap = a.get("gap", 0)
+        c.allowed_lateness = allowed_lateness
+        c.agg = N.AGGS[aggregate]
+        c.max_parallelism, c.parallelism, c.operator_index = max_parallelism, parallelism, operator_index
+        c.device, c.flags, c.capacity_hint, c.max_batch = device, flags, capacity_hint, max_batch
+        self.cfg = c
+        self._h = None
+        self._keys_in: dict = {}
+        self._keys_out: list = []
+        self._int_keys = True
+        self._buf_k: List[int] = []
+        self._buf_t: List[int] = []
+        self._buf_v: List = []
+        self.output: list = []
+
+    # lifecycle -------------------------------------------------------------
+    def open(self):
+        h = ctypes.c_void_p()
+        rc = N.lib().gw_create(ctypes.byref(self.cfg), ctypes.byref(h))
+        if rc == -1:
+            raise ValueError(N.lib().gw_last_error(None).decode())
+        N.check(rc, None)
+        self._h = h
+        return self
+
+    def close(self):
+        if self._h:
+            N.lib().gw_destroy(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self.open() if self._h is None else self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def handle(self):
+        return self._h
+
+    # keys --------------------------------------------------------------------
+    def _encode_key(self, key) -> int:
+        if isinstance(key, int) and not isinstance(key, bool) and LONG_MIN <= key <= LONG_MAX and self._int_keys \
+                and not self._keys_out:
+            return key
+        self._int_keys = False
+        kid = self._keys_in.get(key)
+        if kid is None:
+            kid = len(self._keys_out)
+            self._keys_in[key] = kid
+            self._keys_out.append(key)
+        return kid
+
+    def _decode_key(self, kid: int):
+        return kid if self._int_keys else self._keys_out[kid]
+
+    # record-at-a-time surface (StreamRecord / Watermark) ----------------------
+    def process_element(self, record: StreamRecord):
+        v = record.value
+        self._buf_k.append(self._encode_key(self.key_selector(v)))
+        self._buf_t.append(int(record.timestamp))
+        self._buf_v.append(self.value_selector(v) if self.aggregate != "count" else 0)
+
+    def _flush(self):
+        if not self._buf_k:
+            return
+        k = np.asarray(self._buf_k, dtype=np.int64)
+        t = np.asarray(self._buf_t, dtype=np.int64)
+        if self.is_double_in:
+            v = np.asarray(self._buf_v, dtype=np.float64).view(np.int64)
+        else:
+            v = np.asarray(self._buf_v, dtype=np.int64)
+        self._buf_k, self._buf_t, self._buf_v = [], [], []
+        self.process_batch(k, t, v)
+
+    def process_watermark(self, wm):
+        ts = wm.timestamp if isinstance(wm, Watermark) else int(wm)
+        self._flush()
+        self.advance_watermark(ts)
+        k, s, e, r = self.drain()
+        for i in range(len(k)):
+            res = r[i]
+            self.output.append(StreamRecord((self._decode_key(int(k[i])), int(s[i]), int(e[i]), res), int(e[i]) - 1))
+        self.output.append(Watermark(ts))
+
+    def end_input(self):
+        """BoundedOneInput.endInput followed by MAX_WATERMARK."""
+        self.process_watermark(MAX_WATERMARK)
+
+    def get_output(self):
+        out, self.output = self.output, []
+        return out
+
+    # columnar surface ------------------------------------------------------------
+    def process_batch(self, keys: np.ndarray, timestamps: np.ndarray, values: Optional[np.ndarray] = None,
+                      key_hashes: Optional[np.ndarray] = None):
+        keys = np.ascontiguousarray(keys, dtype=np.int64)
+        timestamps = np.ascontiguousarray(timestamps, dtype=np.int64)
+        if values is not None:
+            values = np.ascontiguousarray(values)
+            if values.dtype == np.float64:
+                values = values.view(np.int64)
+            values = values.astype(np.int64, copy=False)
+        if key_hashes is not None:
+            key_hashes = np.ascontiguousarray(key_hashes, dtype=np.int32)
+        if len(keys) != len(timestamps) or (values is not None and len(values) != len(keys)):
+            raise ValueError("column lengths differ")
+        rc = N.lib().gw_ingest(self._h, len(keys), _ptr(keys), _ptr(key_hashes), _ptr(timestamps), _ptr(values))
+        N.check(rc, self._h)
+
+    def process_batch_device(self, keys, timestamps, values=None, stream=None):
+        """Columns already in HBM (torch tensors or raw device pointers)."""
+        def p(x):
+            if x is None:
+                return None
+            return ctypes.c_void_p(x if isinstance(x, int) else x.data_ptr())
+        n = keys if isinstance(keys, int) else keys.numel()
+        if isinstance(keys, int):
+            raise ValueError("pass tensors, or use process_batch_device_ptr for raw pointers")
+        rc = N.lib().gw_ingest_device(self._h, n, p(keys), None, p(timestamps), p(values),
+                                      ctypes.c_void_p(stream) if stream else None)
+        N.check(rc, self._h)
+
+    def process_batch_device_ptr(self, n: int, key_ptr: int, ts_ptr: int, val_ptr: Optional[int], stream=None):
+        rc = N.lib().gw_ingest_device(self._h, n, ctypes.c_void_p(key_ptr), None, ctypes.c_void_p(ts_ptr),
+                                      ctypes.c_void_p(val_ptr) if val_ptr else None,
+                                      ctypes.c_void_p(stream) if stream else None)
+        N.check(rc, self._h)
+
+    def advance_watermark(self, wm: int) -> int:
+        fired = ctypes.c_int64(0)
+        N.check(N.lib().gw_advance_watermark(self._h, int(wm), ctypes.byref(fired)), self._h)
+        return fired.value
+
+    def pending_rows(self) -> int:
+        n = ctypes.c_int64(0)
+        N.check(N.lib().gw_pending_rows(self._h, ctypes.byref(n)), self._h)
+        return n.value
+
+    def drain(self):
+        """All pending fired rows as numpy (key, start, end, result) columns."""
+        n = self.pending_rows()
+        k = np.empty(n, np.int64)
+        s = np.empty(n, np.int64)
+        e = np.empty(n, np.int64)
+        r = np.empty(n, np.int64)
+        got = ctypes.c_int64(0)
+        if n:
+            rc = N.lib().gw_drain(self._h, _ptr(k), _ptr(s), _ptr(e), _ptr(r), n, ctypes.byref(got))
+            N.check(rc, self._h)
+            assert got.value == n
+        if self.is_double_out:
+            r = r.view(np.float64)
+        return k, s, e, r
+
+    def clear_rows(self):
+        N.check(N.lib().gw_clear_rows(self._h), self._h)
+
+    def rows_device(self):
+        p = [ctypes.c_void_p() for _ in range(4)]
+        n = ctypes.c_int64(0)
+        rc = N.lib().gw_rows_device(self._h, *[ctypes.byref(x) for x in p], ctypes.byref(n))
+        N.check(rc, self._h)
+        return [x.value for x in p], n.value
+
+    @property
+    def num_late_records_dropped(self) -> int:
+        return N.lib().gw_late_dropped(self._h)
+
+    def stats(self) -> dict:
+        s = N.GwStats()
+        N.check(N.lib().gw_get_stats(self._h, ctypes.byref(s)), self._h)
+        return s.as_dict()
+
+    def stream(self) -> int:
+        return N.lib().gw_stream(self._h)
+
+    def enable_kernel_timing(self, on: bool = True):
+        N.check(N.lib().gw_enable_kernel_timing(self._h, 1 if on else 0), self._h)
+
+    def kernel_time_ms(self, which: int = 0):
+        ms = ctypes.c_double(0)
+        n = ctypes.c_int64(0)
+        N.check(N.lib().gw_kernel_time_ms(self._h, which, ctypes.byref(ms), ctypes.byref(n)), self._h)
+        return ms.value, n.value
+
+    def synchronize(self):
+        N.check(N.lib().gw_synchronize(self._h), self._h)
+
+
+# -------------------------------------------------------------- DataStream surface
+class WindowedStream:
+    """keyBy(...).window(assigner) — WindowedStream (RS/api/datastream/WindowedStream.java:84-96)."""
+
+    def __init__(self, keyed: "KeyedStream", assigner: WindowAssigner):
+        self.keyed = keyed
+        self.assigner = assigner
+        self._lateness = 0
+        self._trigger = None
+
+    def allowed_lateness(self, ms: int) -> "WindowedStream":
+        if ms < 0:
+            raise ValueError("The allowed lateness cannot be negative.")
+        self._lateness = ms
+        return self
+
+    allowedLateness = allowed_lateness
+
+    def trigger(self, trig) -> "WindowedStream":
+        self._trigger = trig
+        return self
+
+    def _op(self, agg, field):
+        return GpuWindowOperator(self.assigner, agg, self._lateness, self._trigger, self.keyed.key_selector,
+                                 (lambda v: v[field]) if field is not None else (lambda v: 0),
+                                 **self.keyed.env.op_kwargs)
+
+    # WindowedStream.sum / min / max (:660, :687, :788) on a typed field, aggregate (:310)
+    def sum(self, field: int, kind: str = "i64") -> "DataStreamResult":
+        return DataStreamResult(self, self._op(f"sum_{kind}", field))
+
+    def min(self, field: int, kind: str = "i64") -> "DataStreamResult":
+        return DataStreamResult(self, self._op(f"min_{kind}", field))
+
+    def max(self, field: int, kind: str = "i64") -> "DataStreamResult":
+        return DataStreamResult(self, self._op(f"max_{kind}", field))
+
+    def aggregate(self, function: str, field: Optional[int] = None) -> "DataStreamResult":
+        return DataStreamResult(self, self._op(function, field))
+
+    def count(self) -> "DataStreamResult":
+        return DataStreamResult(self, self._op("count", None))
+
+
+class DataStreamResult:
+    def __init__(self, ws: WindowedStream, op: GpuWindowOperator):
+        self.ws, self.op = ws, op
+
+    def execute_and_collect(self) -> list:
+        """Run the bounded source through the operator, like env.execute() on a MiniCluster
+        with parallelism 1; returns the fired StreamRecords (watermarks dropped)."""
+        env = self.ws.keyed.env
+        out = []
+        with self.op:
+            for el in env.elements:
+                if isinstance(el, Watermark):
+                    self.op.process_watermark(el)
+                else:
+                    self.op.process_element(el)
+            self.op.end_input()
+            out = [r for r in self.op.get_output() if isinstance(r, StreamRecord)]
+        return out
+
+
+class KeyedStream:
+    def __init__(self, env, key_selector):
+        self.env, self.key_selector = env, key_selector
+
+    def window(self, assigner: WindowAssigner) -> WindowedStream:
+        return WindowedStream(self, assigner)
+
+
+class DataStream:
+    def __init__(self, env):
+        self.env = env
+
+    def key_by(self, key_selector) -> KeyedStream:
+        return KeyedStream(self.env, key_selector)
+
+    keyBy = key_by
+
+
+class StreamExecutionEnvironment:
+    """Minimal local environment: a bounded, timestamped source (list of StreamRecord and
+    Watermark elements) feeding one GPU window operator."""
+
+    def __init__(self, **op_kwargs):
+        self.elements: list = []
+        self.op_kwargs = op_kwargs
+
+    @staticmethod
+    def get_execution_environment(**op_kwargs) -> "StreamExecutionEnvironment":
+        return StreamExecutionEnvironment(**op_kwargs)
+
+    def from_elements(self, elements: Iterable) -> DataStream:
+        self.elements = list(elements)
+        return DataStream(self)
+
+
+def result_value(bits: int, is_double: bool):
+    if is_double:
+        return struct.unpack("<d", struct.pack("<q", int(bits)))[0]
+    return int(bits)

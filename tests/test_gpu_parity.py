@@ -1,0 +1,318 @@
+"""GPU parity tests: libgpuwin.so (through the flink_amd host mirror) against the CPU
+oracle and the reference's golden vectors.  Bit-exact for integer/count/min/max and
+avg over longs; 1e-6 relative for f64 sums/averages (BASELINE.json north_star)."""
+import zlib
+
+import numpy as np
+import pytest
+
+from flink_amd import _native as N
+from flink_amd import windowing as W
+from tests.gpu_helpers import compare, gpu_operator, random_stream, run_gpu, run_oracle
+from tests.harness import config_kwargs, itcase_expected_sum, itcase_stream, load_golden, replay
+
+pytestmark = pytest.mark.gpu
+
+TOL_AGGS = {"sum_f64", "avg_f64"}
+ALL_AGGS = ["count", "sum_i64", "sum_i32", "sum_f64", "min_i64", "max_i64", "min_f64", "max_f64",
+            "avg_i64", "avg_f64"]
+
+
+def _cmp(gpu, ora, agg):
+    if agg in TOL_AGGS:
+        return compare(gpu, ora, True)
+    return compare(gpu, ora, False)
+
+
+# ------------------------------------------------------------------ golden vectors
+class GpuBackend:
+    def __init__(self, cfg):
+        self.kw = config_kwargs(cfg)
+        self.op = gpu_operator(self.kw)
+        self.k, self.t, self.v = [], [], []
+
+    def process_element(self, k, ts, v):
+        self.k.append(k); self.t.append(ts); self.v.append(v)
+
+    def process_watermark(self, wm):
+        if self.k:
+            self.op.process_batch(np.array(self.k, np.int64), np.array(self.t, np.int64),
+                                  np.array(self.v, np.int64))
+            self.k, self.t, self.v = [], [], []
+        self.op.advance_watermark(wm)
+
+    def drain(self):
+        k, s, e, r = self.op.drain()
+        return k, s, e, r.view(np.int64)
+
+    @property
+    def late_dropped(self):
+        return self.op.num_late_records_dropped
+
+
+@pytest.mark.parametrize("test", load_golden("operator_harness.json")["tests"], ids=lambda t: t["name"])
+def test_golden_harness_vectors(test):
+    if test["config"].get("lateness", 0) > 0:
+        with pytest.raises(N.GpuWinError) as ei:
+            GpuBackend(test["config"])
+        assert ei.value.code == -2  # GW_E_UNSUPPORTED: allowed lateness > 0 is a "next" row
+        return
+    assert replay(test, GpuBackend) == []
+
+
+@pytest.mark.parametrize("assigner,size,slide", [("tumbling", 1000, 1000), ("sliding", 1000, 100)])
+def test_itcase_closed_form(assigner, size, slide):
+    """EventTimeWindowCheckpointingITCase generator/validator (see tests/harness.py)."""
+    nk, n = 100, 3000
+    keys, ts, vals, blen, wm = itcase_stream(nk, n, size)
+    op = gpu_operator(dict(assigner=assigner, size=size, slide=slide, agg="sum_i32"))
+    rows = []
+    off = 0
+    for b in range(0, n, 50):  # 50 generator steps per batch, watermark of the last one
+        hi = off + int(blen[b:b + 50].sum())
+        op.process_batch(keys[off:hi], ts[off:hi], vals[off:hi])
+        off = hi
+        op.advance_watermark(int(wm[min(b + 49, n - 1)]))
+        rows.append(op.drain())
+    op.advance_watermark(W.LONG_MAX)
+    rows.append(op.drain())
+    assert op.num_late_records_dropped == 0
+    op.close()
+    k = np.concatenate([r[0] for r in rows]); s = np.concatenate([r[1] for r in rows])
+    e = np.concatenate([r[2] for r in rows]); r = np.concatenate([r[3] for r in rows])
+    exp = np.array([itcase_expected_sum(int(a), int(b), n) for a, b in zip(s, e)], np.int64)
+    assert np.array_equal(r, exp)
+    n_windows = (n + size - 1) // slide if assigner == "sliding" else n // size
+    assert len(k) == nk * n_windows
+    assert len(set(zip(k.tolist(), s.tolist()))) == len(k)  # each (key, window) exactly once
+
+
+# ------------------------------------------------------------------ random streams
+CONFIGS = [
+    dict(assigner="tumbling", size=1000, slide=1000),
+    dict(assigner="tumbling", size=700, slide=700, offset=-300),
+    dict(assigner="sliding", size=1000, slide=250),
+    dict(assigner="sliding", size=1000, slide=300, offset=-50),  # size % slide != 0 -> pane 100
+    dict(assigner="sliding", size=10000, slide=2000),             # Nexmark Q5 shape
+    dict(assigner="session", gap=100),
+]
+
+
+@pytest.mark.parametrize("agg", ALL_AGGS)
+@pytest.mark.parametrize("cfg", CONFIGS, ids=lambda c: "-".join(str(v) for v in c.values()))
+def test_random_stream_vs_oracle(oracle_lib, cfg, agg):
+    kw = dict(cfg, agg=agg)
+    keys, ts, vals, batches = random_stream(seed=zlib.crc32(f"{agg}{cfg}".encode()) & 0xffff, n=20000, num_keys=300,
+                                            n_batches=25, agg=agg)
+    g, glate, _ = run_gpu(kw, keys, ts, vals, batches)
+    o, olate = run_oracle(oracle_lib, kw, keys, ts, vals, batches)
+    assert glate == olate == 0
+    assert _cmp(g, o, agg) == []
+
+
+@pytest.mark.parametrize("cfg", CONFIGS, ids=lambda c: "-".join(str(v) for v in c.values()))
+def test_late_records_dropped_like_reference(oracle_lib, cfg):
+    """Disorder larger than the watermark lag: some records are late (isWindowLate /
+    isElementLate, WindowOperator.java:609-624) and are dropped and counted; sessions
+    with late records take the arrival-order replay path."""
+    kw = dict(cfg, agg="sum_i64")
+    keys, ts, vals, batches = random_stream(seed=11, n=20000, num_keys=50, n_batches=40, disorder=2500,
+                                            wm_lag=200, agg="sum_i64")
+    g, glate, _ = run_gpu(kw, keys, ts, vals, batches)
+    o, olate = run_oracle(oracle_lib, kw, keys, ts, vals, batches)
+    assert olate > 0
+    assert glate == olate
+    assert _cmp(g, o, "sum_i64") == []
+
+
+@pytest.mark.parametrize("cfg", CONFIGS, ids=lambda c: "-".join(str(v) for v in c.values()))
+def test_far_future_records_and_watermark_jumps(oracle_lib, cfg):
+    """Records far ahead of the pane ring are parked and merged when their windows
+    come up; big watermark jumps fire many windows at once."""
+    kw = dict(cfg, agg="count")
+    rng = np.random.default_rng(5)
+    n = 6000
+    keys = rng.integers(0, 40, n).astype(np.int64)
+    ts = rng.integers(0, 2_000_000, n).astype(np.int64)  # unordered over a wide span
+    vals = np.zeros(n, np.int64)
+    batches = [(0, 2000, -1), (2000, 4000, 100_000), (4000, 6000, 1_500_000)]
+    g, glate, _ = run_gpu(kw, keys, ts, vals, batches)
+    o, olate = run_oracle(oracle_lib, kw, keys, ts, vals, batches)
+    assert glate == olate
+    assert compare(g, o, False) == []
+
+
+def test_table_growth(oracle_lib):
+    kw = dict(assigner="sliding", size=1000, slide=500, agg="sum_i64")
+    keys, ts, vals, batches = random_stream(seed=2, n=200000, num_keys=150000, n_batches=10, agg="sum_i64")
+    g, _, stats = run_gpu(kw, keys, ts, vals, batches, capacity_hint=16)
+    o, _ = run_oracle(oracle_lib, kw, keys, ts, vals, batches)
+    assert stats["rehashes"] > 0
+    assert compare(g, o, False) == []
+
+
+@pytest.mark.parametrize("agg", ["count", "sum_i64", "sum_f64", "min_f64", "max_i64", "avg_f64"])
+@pytest.mark.parametrize("flags", [N.FLAG_FORCE_LDS_PREAGG, 0])
+def test_lds_preaggregation_low_cardinality(oracle_lib, agg, flags):
+    """YSB-like: 100 keys, large batches -> LDS pre-aggregation kernel (forced or auto)."""
+    kw = dict(assigner="tumbling", size=10000, slide=10000, agg=agg)
+    keys, ts, vals, batches = random_stream(seed=9, n=400000, num_keys=100, n_batches=8, ts_step=1, agg=agg)
+    g, _, stats = run_gpu(kw, keys, ts, vals, batches, flags=flags, capacity_hint=100)
+    o, _ = run_oracle(oracle_lib, kw, keys, ts, vals, batches)
+    assert stats["preagg_batches"] > 0
+    assert _cmp(g, o, agg) == []
+
+
+def test_special_keys_and_timestamps(oracle_lib):
+    """Long.MIN_VALUE (the table's empty marker) and Long.MAX_VALUE as keys, negative
+    timestamps, duplicates."""
+    kw = dict(assigner="sliding", size=300, slide=100, offset=-30, agg="sum_i64")
+    keys = np.array([W.LONG_MIN, W.LONG_MAX, 0, -1, W.LONG_MIN, 7, W.LONG_MIN], np.int64)
+    ts = np.array([-1000, -999, -1, 0, -950, 5, 1], np.int64)
+    vals = np.array([1, 2, 3, 4, 5, 6, 7], np.int64)
+    batches = [(0, 4, -2000), (4, 7, -500)]
+    g, _, _ = run_gpu(kw, keys, ts, vals, batches)
+    o, _ = run_oracle(oracle_lib, kw, keys, ts, vals, batches)
+    assert compare(g, o, False) == []
+
+
+def test_double_ordering_min_max(oracle_lib):
+    """Double.compare order: NaN largest, -0.0 < 0.0 (Comparator.java:33-90)."""
+    for agg in ["min_f64", "max_f64"]:
+        kw = dict(assigner="tumbling", size=100, slide=100, agg=agg)
+        vals = np.array([0.0, -0.0, 1.5, np.nan, -np.inf, np.inf, -0.0, 0.0, np.nan, 2.0], np.float64)
+        keys = np.array([1, 1, 2, 2, 3, 3, 4, 4, 5, 5], np.int64)
+        ts = np.arange(10, dtype=np.int64)
+        batches = [(0, 10, 50)]
+        g, _, _ = run_gpu(kw, keys, ts, vals, batches)
+        o, _ = run_oracle(oracle_lib, kw, keys, ts, vals, batches)
+        # compare bit patterns except NaN payloads
+        gk = np.concatenate([x[0] for x in g]); gr = np.concatenate([x[3] for x in g]).view(np.float64)
+        ok = np.concatenate([x[0] for x in o]); orr = np.concatenate([x[3] for x in o]).view(np.float64)
+        gi, oi = np.argsort(gk), np.argsort(ok)
+        for a, b in zip(gr[gi], orr[oi]):
+            assert (np.isnan(a) and np.isnan(b)) or np.signbit(a) == np.signbit(b) and a == b
+
+
+def test_no_timestamp_fails_the_operator():
+    op = gpu_operator(dict(assigner="tumbling", size=1000, slide=1000, agg="count"))
+    with pytest.raises(N.GpuWinError) as ei:
+        op.process_batch(np.array([1], np.int64), np.array([W.LONG_MIN], np.int64), None)
+    assert ei.value.code == -6
+    op.close()
+
+
+def test_empty_batches_and_idle_watermarks():
+    op = gpu_operator(dict(assigner="sliding", size=1000, slide=500, agg="count"))
+    op.process_batch(np.zeros(0, np.int64), np.zeros(0, np.int64), None)
+    assert op.advance_watermark(10 ** 9) == 0
+    op.process_batch(np.array([5], np.int64), np.array([2 * 10 ** 9], np.int64), None)
+    assert op.advance_watermark(10 ** 9 + 5) == 0
+    assert op.advance_watermark(W.LONG_MAX) == 2
+    k, s, e, r = op.drain()
+    assert sorted(zip(s.tolist(), r.tolist())) == [(2 * 10 ** 9 - 500, 1), (2 * 10 ** 9, 1)]
+    op.close()
+
+
+def test_partial_drain():
+    op = gpu_operator(dict(assigner="tumbling", size=10, slide=10, agg="count"))
+    op.process_batch(np.arange(1000, dtype=np.int64), np.zeros(1000, np.int64), None)
+    op.advance_watermark(100)
+    import ctypes
+    got = ctypes.c_int64()
+    buf = np.empty(300, np.int64)
+    total = 0
+    while True:
+        rc = N.lib().gw_drain(op.handle, ctypes.c_void_p(buf.ctypes.data), None, None, None, 300, ctypes.byref(got))
+        total += got.value
+        if rc == 0:
+            break
+        assert rc == N.GW_E_OUTPUT_FULL
+    assert total == 1000
+    op.close()
+
+
+def test_device_ingest_torch():
+    import torch
+    op = gpu_operator(dict(assigner="tumbling", size=100, slide=100, agg="sum_i64"))
+    k = torch.arange(64, dtype=torch.int64, device="cuda") % 8
+    t = torch.arange(64, dtype=torch.int64, device="cuda")
+    v = torch.ones(64, dtype=torch.int64, device="cuda")
+    op.process_batch_device(k, t, v, stream=torch.cuda.current_stream().cuda_stream)
+    op.advance_watermark(1000)
+    kk, s, e, r = op.drain()
+    assert sorted(kk.tolist()) == list(range(8)) and r.tolist() == [8] * 8
+    op.close()
+
+
+def test_key_groups_and_partition_device(oracle_lib):
+    import ctypes
+    import torch
+    L, O = N.lib(), oracle_lib.lib()
+    n = 100000
+    rng = np.random.default_rng(1)
+    keys = rng.integers(-(1 << 62), 1 << 62, n).astype(np.int64)
+    ts = np.arange(n, dtype=np.int64)
+    vals = rng.integers(0, 100, n).astype(np.int64)
+    dk, dt, dv = (torch.from_numpy(x).cuda() for x in (keys, ts, vals))
+    kg = torch.empty(n, dtype=torch.int32, device="cuda")
+    ow = torch.empty(n, dtype=torch.int32, device="cuda")
+    P = lambda x: ctypes.c_void_p(x.data_ptr())
+    assert L.gw_key_groups_device(n, P(dk), None, 128, 8, P(kg), P(ow), None) == 0
+    torch.cuda.synchronize()
+    exp_kg = np.array([O.wo_assign_to_key_group(O.wo_long_hash(int(x)), 128) for x in keys[:5000]])
+    assert np.array_equal(kg.cpu().numpy()[:5000], exp_kg)
+    assert np.array_equal(ow.cpu().numpy(), kg.cpu().numpy() * 8 // 128)
+    for p in [1, 2, 8]:
+        ko, to, vo = torch.empty_like(dk), torch.empty_like(dt), torch.empty_like(dv)
+        counts = torch.empty(p, dtype=torch.int64, device="cuda")
+        scratch = torch.empty(L.gw_partition_scratch_bytes(n, p), dtype=torch.uint8, device="cuda")
+        assert L.gw_partition_device(n, P(dk), None, P(dt), P(dv), 128, p, P(ko), P(to), P(vo), P(counts),
+                                     P(scratch), None) == 0
+        torch.cuda.synchronize()
+        owner = kg.cpu().numpy().astype(np.int64) * p // 128
+        order = np.argsort(owner, kind="stable")
+        assert np.array_equal(counts.cpu().numpy(), np.bincount(owner, minlength=p))
+        assert np.array_equal(ko.cpu().numpy(), keys[order])
+        assert np.array_equal(to.cpu().numpy(), ts[order])
+        assert np.array_equal(vo.cpu().numpy(), vals[order])
+
+
+def test_q5_shape_size_independent_properties():
+    """Nexmark Q5 shape at scale (sliding 10 s / 2 s count over 2M keys, 20M events):
+    size-independent properties instead of the oracle — every record is counted in
+    exactly size/slide = 5 windows, every fired (key, window) is unique, and each
+    window's count equals the records of that key inside [start, end)."""
+    import torch
+    n, nk = 20_000_000, 2_000_000
+    g = torch.Generator(device="cuda").manual_seed(5)
+    keys = torch.randint(0, nk, (n,), device="cuda", dtype=torch.int64, generator=g)
+    ts = torch.arange(n, device="cuda", dtype=torch.int64) // 1000  # 1000 events / ms -> 2M per pane
+    op = gpu_operator(dict(assigner="sliding", size=10000, slide=2000, agg="count"), capacity_hint=nk)
+    step = 1_000_000
+    total = 0
+    kk = int(keys[123].item())
+    spot = []
+    for lo in range(0, n, step):
+        op.process_batch_device(keys[lo:lo + step], ts[lo:lo + step], None,
+                                stream=torch.cuda.current_stream().cuda_stream)
+        op.advance_watermark(int(ts[lo + step - 1].item()) - 1)
+        k, s, e, r = op.drain()
+        total += int(r.sum())
+        m = k == kk
+        spot.append((s[m], e[m], r[m]))
+        assert len(np.unique(k * 4096 + (s // 2000) % 4096)) == len(k)  # (key, window) unique
+    op.advance_watermark(W.LONG_MAX)
+    k, s, e, r = op.drain()
+    total += int(r.sum())
+    m = k == kk
+    spot.append((s[m], e[m], r[m]))
+    assert total == 5 * n
+    assert op.num_late_records_dropped == 0
+    kts = ts[(keys == kk).nonzero().flatten()].cpu().numpy()
+    ss = np.concatenate([x[0] for x in spot]); ee = np.concatenate([x[1] for x in spot])
+    cc = np.concatenate([x[2] for x in spot])
+    assert int(cc.sum()) == 5 * len(kts)
+    for st, en, c in zip(ss, ee, cc):
+        assert c == int(((kts >= st) & (kts < en)).sum())
+    op.close()
