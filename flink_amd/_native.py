@@ -80,6 +80,14 @@ def lib() -> ctypes.CDLL:
     global _lib
     if _lib is not None:
         return _lib
+    # One HIP runtime per process: torch bundles its own libamdhip64.so.7 (same SONAME as
+    # /opt/rocm's).  Whichever is loaded first serves both, and torch only initialises
+    # with its own, so import torch first when it is installed (plumbing only; the
+    # library itself has no torch dependency and binds whatever runtime is loaded).
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     if not os.path.exists(LIB_PATH):
         raise NativeLibraryError(
             f"{LIB_PATH} not found: build it with `python -m flink_amd.build` (hipcc, gfx950). "

@@ -24,18 +24,26 @@ struct TableView {
 };
 
 // Device-side counters, copied to pinned host memory after each launch sequence.
+// Hot counters are sharded (blockIdx % kShards) and updated once per block after a
+// wave + LDS reduction: same-address device atomics serialise at ~12 ns each on
+// MI355X (MI355X_MICROARCH.md "fanin"), so one counter per wave costs ms per launch.
+constexpr int kShards = 32;
+struct ShardCtr {
+    unsigned long long late, ins, flags, occ, cells, merges, pad0, pad1;  // 64 B
+};
 struct DevStatus {
-    unsigned long long used_slots;
-    unsigned long long n_deferred;
-    unsigned long long late;
-    unsigned long long flags;      // GW_DF_*
-    unsigned long long occ;        // pane-ring positions that may hold data
-    unsigned long long rows;       // output cursor
-    long long def_min_pane;        // min pane over the deferred list (reduction)
-    unsigned long long preagg_cells;
-    unsigned long long merges;     // session merges (M_b)
-    unsigned long long overflow;   // session slots that did not fit (retry list length)
+    unsigned long long used_slots;  // host view: sum of sh[].ins
+    unsigned long long n_deferred;  // deferred-list cursor (rare writers)
+    unsigned long long late;        // host view: sum of sh[].late
+    unsigned long long flags;       // host view: OR of sh[].flags
+    unsigned long long occ;         // host view: OR of sh[].occ (pane-ring positions with data)
+    unsigned long long rows;        // output cursor (one atomic per block flush)
+    long long def_min_pane;         // min pane over the deferred list (reduction)
+    unsigned long long preagg_cells;// host view: sum of sh[].cells
+    unsigned long long merges;      // host view: sum of sh[].merges (session merges, M_b)
+    unsigned long long overflow;    // session segments that did not fit (retry list length)
     unsigned long long pad[6];
+    ShardCtr sh[kShards];
 };
 #define GW_DF_NO_TS 1ull
 #define GW_DF_RANGE 2ull
@@ -68,6 +76,80 @@ __device__ __forceinline__ void wave_add(unsigned long long* ctr, unsigned long 
 __device__ __forceinline__ void wave_or(unsigned long long* ctr, unsigned long long v) {
     for (int o = 32; o > 0; o >>= 1) v |= __shfl_xor(v, o);
     if (__lane_id() == 0 && v) atomicOr(ctr, v);
+}
+
+__device__ __forceinline__ unsigned long long wave_sum(unsigned long long v) {
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+__device__ __forceinline__ unsigned long long wave_ior(unsigned long long v) {
+    for (int o = 32; o > 0; o >>= 1) v |= __shfl_xor(v, o);
+    return v;
+}
+
+// Block-level reduction of the per-thread counters, then ONE atomic per non-zero
+// field into this block's shard.  Every thread of the block must call it (uniformly).
+__device__ __forceinline__ void block_commit(DevStatus* st, unsigned long long late, unsigned long long ins,
+                                             unsigned long long flags, unsigned long long occ,
+                                             unsigned long long cells = 0, unsigned long long merges = 0) {
+    __shared__ unsigned long long red[16][6];
+    late = wave_sum(late); ins = wave_sum(ins); cells = wave_sum(cells); merges = wave_sum(merges);
+    flags = wave_ior(flags); occ = wave_ior(occ);
+    const int wave = threadIdx.x >> 6;
+    if (__lane_id() == 0) {
+        red[wave][0] = late; red[wave][1] = ins; red[wave][2] = flags;
+        red[wave][3] = occ; red[wave][4] = cells; red[wave][5] = merges;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const int nw = (blockDim.x + 63) >> 6;
+        unsigned long long v[6] = {0, 0, 0, 0, 0, 0};
+        for (int w = 0; w < nw; ++w) {
+            v[0] += red[w][0]; v[1] += red[w][1]; v[2] |= red[w][2];
+            v[3] |= red[w][3]; v[4] += red[w][4]; v[5] += red[w][5];
+        }
+        ShardCtr& sc = st->sh[blockIdx.x % kShards];
+        if (v[0]) atomicAdd(&sc.late, v[0]);
+        if (v[1]) atomicAdd(&sc.ins, v[1]);
+        if (v[2]) atomicOr(&sc.flags, v[2]);
+        if (v[3]) atomicOr(&sc.occ, v[3]);
+        if (v[4]) atomicAdd(&sc.cells, v[4]);
+        if (v[5]) atomicAdd(&sc.merges, v[5]);
+    }
+}
+
+// Fold the shards into the scalar host-view fields (host side, after a D2H copy).
+inline void fold_shards(DevStatus* h) {
+    unsigned long long late = 0, ins = 0, flags = 0, occ = 0, cells = 0, merges = 0;
+    for (int i = 0; i < kShards; ++i) {
+        late += h->sh[i].late; ins += h->sh[i].ins; flags |= h->sh[i].flags;
+        occ |= h->sh[i].occ; cells += h->sh[i].cells; merges += h->sh[i].merges;
+    }
+    h->late = late; h->used_slots = ins; h->flags = flags; h->occ = occ;
+    h->preagg_cells = cells; h->merges = merges;
+}
+
+// Fired-row staging in LDS: rows are appended with LDS atomics and flushed to the
+// global output with one device atomic per flush and coalesced stores.
+constexpr int kRowStage = 1024;
+struct RowStage {
+    long long k[kRowStage], s[kRowStage], e[kRowStage], r[kRowStage];
+    unsigned cnt;
+    unsigned long long base;
+};
+__device__ __forceinline__ void stage_flush(RowStage& rs, unsigned long long* cursor, int64_t* ok, int64_t* os,
+                                            int64_t* oe, int64_t* orr) {
+    __syncthreads();
+    const unsigned c = rs.cnt;
+    if (threadIdx.x == 0 && c) rs.base = atomicAdd(cursor, (unsigned long long)c);
+    __syncthreads();
+    const unsigned long long b = rs.base;
+    for (unsigned j = threadIdx.x; j < c; j += blockDim.x) {
+        ok[b + j] = rs.k[j]; os[b + j] = rs.s[j]; oe[b + j] = rs.e[j]; orr[b + j] = rs.r[j];
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) rs.cnt = 0;
+    __syncthreads();
 }
 
 // Exclusive wave scan of per-lane counts + one atomic per wave.

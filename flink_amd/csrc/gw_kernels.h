@@ -72,6 +72,7 @@ hipError_t launch_deferred_min(const int64_t* pane, int64_t n, DevStatus* st, hi
 hipError_t launch_fire(const FireArgs& a, hipStream_t s);
 hipError_t launch_evict(const EvictArgs& a, hipStream_t s);
 hipError_t launch_rehash(const TableView& o, const TableView& n, DevStatus* st, hipStream_t s);
+hipError_t launch_status_set(DevStatus* st, int word, unsigned long long v, int shard_field, hipStream_t s);
 hipError_t launch_count_live(const TableView& t, unsigned long long* out, hipStream_t s);
 
 // key groups / exchange (gw_keygroups.hip)

@@ -24,6 +24,8 @@
 // per-window state for every associative aggregate of the closed set.
 #include "gw_kernels.h"
 
+#include <algorithm>
+
 namespace gw {
 
 template <int AGG>
@@ -42,67 +44,147 @@ __global__ void __launch_bounds__(256) k_table_init(TableView t) {
     }
 }
 
-// Direct path: one HBM RMW (device-scope atomic) per in-ring record.
 template <int AGG>
+__device__ __forceinline__ constexpr bool uses_mask() {
+    return !(AGG == GW_COUNT || AGG == GW_AVG_I64 || AGG == GW_AVG_F64);
+}
+
+// Ring positions of a slot holding a non-null accumulator.  COUNT / AVG carry a
+// count in the cell, so presence is `count != 0` and ingest never touches word 1;
+// the other aggregates keep an explicit presence mask in word 1.
+template <int AGG>
+__device__ __forceinline__ uint64_t presence(const int64_t* s, int R, int W) {
+    if constexpr (uses_mask<AGG>()) {
+        return (uint64_t)s[1];
+    } else {
+        uint64_t m = 0;
+        for (int r = 0; r < R; ++r)
+            if (s[2 + r * W + (W - 1)] != 0) m |= 1ull << r;
+        return m;
+    }
+}
+__device__ __forceinline__ uint64_t presence_rt(const int64_t* s, const TableView& t) {
+    if (t.agg == GW_COUNT || t.agg == GW_AVG_I64 || t.agg == GW_AVG_F64) {
+        uint64_t m = 0;
+        for (int r = 0; r < t.ring; ++r)
+            if (s[2 + r * t.words + (t.words - 1)] != 0) m |= 1ull << r;
+        return m;
+    }
+    return (uint64_t)s[1];
+}
+
+// Continue a linear probe from `idx` (the first slot was already read as `k0`).
+__device__ __forceinline__ int64_t probe_from(const TableView& t, int64_t key, uint64_t idx, int64_t k0,
+                                              bool& inserted) {
+    inserted = false;
+    const uint64_t mask = (uint64_t)t.cap - 1;
+    int64_t k = k0;
+    for (int p = 0; p < kMaxProbe; ++p) {
+        int64_t* s = slot_ptr(t, (int64_t)idx);
+        if (p) k = *(volatile int64_t*)s;
+        if (k == key) return (int64_t)idx;
+        if (k == kEmptyKey) {
+            const unsigned long long prev = atomicCAS((unsigned long long*)s, (unsigned long long)kEmptyKey,
+                                                      (unsigned long long)key);
+            if (prev == (unsigned long long)kEmptyKey) { inserted = true; return (int64_t)idx; }
+            if ((int64_t)prev == key) return (int64_t)idx;
+        }
+        idx = (idx + 1) & mask;
+    }
+    return -1;
+}
+
+// Direct path: one device-scope atomic RMW into the record's (slot, pane) cell, plus
+// one presence-bit OR on the first touch of a (key, pane) for SUM/MIN/MAX.
+// U records per thread per iteration: their first probes are issued back to back so
+// each lane keeps U random 64-B line reads in flight (memory-level parallelism).
+template <int AGG, int U>
 __global__ void __launch_bounds__(256) k_ingest(IngestArgs a) {
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    const int64_t base0 = blockIdx.x * (int64_t)blockDim.x;
+    const int64_t tile = (int64_t)blockDim.x * U;
+    const int64_t stride = (int64_t)gridDim.x * tile;
     unsigned long long late = 0, ins = 0, flags = 0, occ = 0;
     const uint64_t R = (uint64_t)a.t.ring;
-    for (int64_t base = base0; base < a.n; base += stride) {
-        const int64_t i = base + threadIdx.x;
-        bool defer = false;
-        int64_t key = 0, pane = 0, c0 = 0, c1 = 0;
-        if (i < a.n) {
-            key = a.key[i];
-            const int64_t ts = a.ts[i];
-            const int64_t v = a.val ? a.val[i] : 0;
-            if (ts == INT64_MIN) {
-                flags |= GW_DF_NO_TS;
-            } else if (ts < a.t_late) {
-                if (a.late_exact) late++;
-                else flags |= GW_DF_RANGE;
-            } else {
-                const uint64_t q = udiv64((uint64_t)ts - (uint64_t)a.t_late, a.div);
-                record_cell(AGG, v, c0, c1);
-                const uint64_t rel = q - a.delta;
-                if (q >= a.delta && rel < R) {
-                    uint32_t pos = (uint32_t)a.b_pos + (uint32_t)rel;
-                    if (pos >= R) pos -= (uint32_t)R;
-                    bool inserted;
-                    const int64_t si = find_or_insert(a.t, key, inserted);
-                    ins += inserted;
-                    if (si < 0) {
-                        flags |= GW_DF_TABLE_FULL;
-                        defer = true;
-                        pane = a.p_late + (int64_t)q;
-                    } else {
-                        int64_t* s = slot_ptr(a.t, si);
-                        cell_atomic<AGG>(s + 2 + pos * (uint32_t)a.t.words, c0, c1);
-                        const unsigned long long bit = 1ull << pos;
-                        if (!(*(volatile unsigned long long*)(s + 1) & bit))
-                            atomicOr((unsigned long long*)(s + 1), bit);
-                        occ |= bit;
-                    }
+    const uint64_t tmask = (uint64_t)a.t.cap - 1;
+    const uint32_t W = (uint32_t)a.t.words;
+    for (int64_t base = blockIdx.x * tile; base < a.n; base += stride) {
+        int64_t key[U], c0[U], c1[U], pane[U], k0[U];
+        uint64_t idx[U];
+        uint32_t pos[U];
+        int state[U];  // 0 skip, 1 in ring, 2 defer
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t i = base + (int64_t)u * blockDim.x + threadIdx.x;
+            state[u] = 0;
+            key[u] = 0; c0[u] = 0; c1[u] = 0; pane[u] = 0; pos[u] = 0;
+            if (i < a.n) {
+                key[u] = a.key[i];
+                const int64_t ts = a.ts[i];
+                const int64_t v = a.val ? a.val[i] : 0;
+                if (ts == INT64_MIN) {
+                    flags |= GW_DF_NO_TS;
+                } else if (ts < a.t_late) {
+                    if (a.late_exact) late++;
+                    else flags |= GW_DF_RANGE;
                 } else {
-                    if (q > (uint64_t)(INT64_MAX - a.p_late)) flags |= GW_DF_RANGE;
-                    defer = true;
-                    pane = a.p_late + (int64_t)q;
+                    const uint64_t q = udiv64((uint64_t)ts - (uint64_t)a.t_late, a.div);
+                    record_cell(AGG, v, c0[u], c1[u]);
+                    const uint64_t rel = q - a.delta;
+                    pane[u] = a.p_late + (int64_t)q;
+                    if (q >= a.delta && rel < R) {
+                        uint32_t p = (uint32_t)a.b_pos + (uint32_t)rel;
+                        if (p >= R) p -= (uint32_t)R;
+                        pos[u] = p;
+                        state[u] = 1;
+                    } else {
+                        if (q > (uint64_t)(INT64_MAX - a.p_late)) flags |= GW_DF_RANGE;
+                        state[u] = 2;
+                    }
                 }
             }
         }
-        const unsigned long long off = wave_reserve(&a.st->n_deferred, defer);
-        if (defer) {
-            a.d_key[off] = key;
-            a.d_pane[off] = pane;
-            a.d_a0[off] = c0;
-            a.d_a1[off] = c1;
+        // first probes of all U records, issued together
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            idx[u] = key[u] == kEmptyKey ? (uint64_t)a.t.cap : (slot_hash(key[u]) & tmask);
+            k0[u] = state[u] == 1 ? *(volatile int64_t*)slot_ptr(a.t, (int64_t)idx[u]) : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (state[u] != 1) continue;
+            int64_t si;
+            if (key[u] == kEmptyKey) {
+                si = a.t.cap;  // sentinel slot of the key Long.MIN_VALUE
+            } else {
+                bool inserted;
+                si = probe_from(a.t, key[u], idx[u], k0[u], inserted);
+                ins += inserted;
+            }
+            if (si < 0) {
+                flags |= GW_DF_TABLE_FULL;
+                state[u] = 2;
+                continue;
+            }
+            int64_t* s = slot_ptr(a.t, si);
+            cell_atomic<AGG>(s + 2 + pos[u] * W, c0[u], c1[u]);
+            const unsigned long long bit = 1ull << pos[u];
+            if constexpr (uses_mask<AGG>()) {
+                if (!(*(volatile unsigned long long*)(s + 1) & bit)) atomicOr((unsigned long long*)(s + 1), bit);
+            }
+            occ |= bit;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const bool defer = state[u] == 2;
+            const unsigned long long off = wave_reserve(&a.st->n_deferred, defer);
+            if (defer) {
+                a.d_key[off] = key[u];
+                a.d_pane[off] = pane[u];
+                a.d_a0[off] = c0[u];
+                a.d_a1[off] = c1[u];
+            }
         }
     }
-    wave_add(&a.st->late, late);
-    wave_add(&a.st->used_slots, ins);
-    wave_or(&a.st->flags, flags);
-    wave_or(&a.st->occ, occ);
+    block_commit(a.st, late, ins, flags, occ);
 }
 
 // LDS pre-aggregation path (low key cardinality per batch, e.g. YSB's 100 campaigns):
@@ -188,8 +270,10 @@ __global__ void __launch_bounds__(256) k_ingest_preagg(IngestArgs a) {
                                 int64_t* s = slot_ptr(a.t, si);
                                 cell_atomic<AGG>(s + 2 + pos * (uint32_t)a.t.words, c0, c1);
                                 const unsigned long long bit = 1ull << pos;
-                                if (!(*(volatile unsigned long long*)(s + 1) & bit))
-                                    atomicOr((unsigned long long*)(s + 1), bit);
+                                if constexpr (uses_mask<AGG>()) {
+                                    if (!(*(volatile unsigned long long*)(s + 1) & bit))
+                                        atomicOr((unsigned long long*)(s + 1), bit);
+                                }
                             }
                         }
                     } else {
@@ -220,15 +304,13 @@ __global__ void __launch_bounds__(256) k_ingest_preagg(IngestArgs a) {
             if constexpr (AGG == GW_AVG_I64 || AGG == GW_AVG_F64) b1 = s_a1[j];
             cell_atomic<AGG>(s + 2 + pos * (uint32_t)a.t.words, s_a0[j], b1);
             const unsigned long long bit = 1ull << pos;
-            if (!(*(volatile unsigned long long*)(s + 1) & bit)) atomicOr((unsigned long long*)(s + 1), bit);
+            if constexpr (uses_mask<AGG>()) {
+                if (!(*(volatile unsigned long long*)(s + 1) & bit)) atomicOr((unsigned long long*)(s + 1), bit);
+            }
         }
         __syncthreads();
     }
-    wave_add(&a.st->late, late);
-    wave_add(&a.st->used_slots, ins);
-    wave_add(&a.st->preagg_cells, cells);
-    wave_or(&a.st->flags, flags);
-    wave_or(&a.st->occ, occ);
+    block_commit(a.st, late, ins, flags, occ, cells);
 }
 
 // Re-ingest parked partial aggregates whose pane now lies inside the ring.
@@ -260,8 +342,10 @@ __global__ void __launch_bounds__(256) k_merge_deferred(MergeArgs a) {
                     int64_t* s = slot_ptr(a.t, si);
                     cell_atomic<AGG>(s + 2 + pos * a.t.words, c0, c1);
                     const unsigned long long bit = 1ull << pos;
-                    if (!(*(volatile unsigned long long*)(s + 1) & bit))
-                        atomicOr((unsigned long long*)(s + 1), bit);
+                    if constexpr (uses_mask<AGG>()) {
+                        if (!(*(volatile unsigned long long*)(s + 1) & bit))
+                            atomicOr((unsigned long long*)(s + 1), bit);
+                    }
                     occ |= bit;
                 }
             } else {
@@ -276,9 +360,7 @@ __global__ void __launch_bounds__(256) k_merge_deferred(MergeArgs a) {
             a.d_a1[off] = c1;
         }
     }
-    wave_add(&a.st->used_slots, ins);
-    wave_or(&a.st->flags, flags);
-    wave_or(&a.st->occ, occ);
+    block_commit(a.st, 0, ins, flags, occ);
 }
 
 __global__ void __launch_bounds__(256) k_deferred_min(const int64_t* pane, int64_t n, DevStatus* st) {
@@ -295,45 +377,53 @@ __global__ void __launch_bounds__(256) k_deferred_min(const int64_t* pane, int64
 
 // Fire pass: one streaming sweep over all slots emits every (key, window) with a
 // non-null pane among the nwin windows of this pass, then retires the panes that no
-// later window covers (clearAllState).  Rows are compacted with one atomic per wave.
+// later window covers (clearAllState).  Each block sweeps a contiguous chunk; rows
+// are staged in LDS and flushed with one device atomic per 2048 rows (coalesced).
 template <int AGG>
 __global__ void __launch_bounds__(256) k_fire(FireArgs a) {
+    __shared__ RowStage rs;
     const int64_t nslots = a.t.cap + 1;
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     const int64_t id0 = identity0(AGG);
     const int W = a.t.words;
-    for (int64_t base = blockIdx.x * (int64_t)blockDim.x; base < nslots; base += stride) {
+    const int R = a.t.ring;
+    if (threadIdx.x == 0) rs.cnt = 0;
+    if (blockIdx.x == 0 && threadIdx.x < kShards) atomicAnd(&a.st->sh[threadIdx.x].occ, ~a.rmask);
+    __syncthreads();
+    const int64_t chunk = ((nslots + gridDim.x - 1) / gridDim.x + 255) / 256 * 256;
+    const int64_t c0 = blockIdx.x * chunk, c1 = min(nslots, c0 + chunk);
+    for (int64_t base = c0; base < c1; base += blockDim.x) {
         const int64_t i = base + threadIdx.x;
         int64_t key = kEmptyKey;
         uint64_t mask = 0;
         int64_t* s = nullptr;
-        if (i < nslots) {
+        if (i < c1) {
             s = slot_ptr(a.t, i);
             key = s[0];
-            mask = (uint64_t)s[1];
+            mask = presence<AGG>(s, R, W);
         }
         for (int w = 0; w < a.nwin; ++w) {
+            if (rs.cnt + blockDim.x > kRowStage) stage_flush(rs, &a.st->rows, a.o_key, a.o_start, a.o_end, a.o_res);
             uint64_t m = mask & a.wmask[w];
-            const bool emit = m != 0;
-            int64_t r0 = id0, r1 = 0;
-            while (m) {
-                const int pos = __ffsll((long long)m) - 1;
-                m &= m - 1;
-                const int64_t* c = s + 2 + pos * W;
-                fold_cell(AGG, r0, r1, c[0], W == 2 ? c[1] : 0);
-            }
-            const unsigned long long off = wave_reserve(&a.st->rows, emit);
-            if (emit) {
+            if (m) {
+                int64_t r0 = id0, r1 = 0;
+                while (m) {
+                    const int pos = __ffsll((long long)m) - 1;
+                    m &= m - 1;
+                    const int64_t* c = s + 2 + pos * W;
+                    fold_cell(AGG, r0, r1, c[0], W == 2 ? c[1] : 0);
+                }
+                const unsigned j = atomicAdd(&rs.cnt, 1u);
                 const int64_t st = a.start0 + (int64_t)w * a.slide;
-                a.o_key[off] = key;
-                a.o_start[off] = st;
-                a.o_end[off] = st + a.size;
-                a.o_res[off] = cell_result(AGG, r0, r1);
+                rs.k[j] = key;
+                rs.s[j] = st;
+                rs.e[j] = st + a.size;
+                rs.r[j] = cell_result(AGG, r0, r1);
             }
+            __syncthreads();
         }
         uint64_t m = mask & a.rmask;
         if (m) {
-            s[1] = (int64_t)(mask & ~a.rmask);
+            if constexpr (uses_mask<AGG>()) s[1] = (int64_t)(mask & ~a.rmask);
             while (m) {
                 const int pos = __ffsll((long long)m) - 1;
                 m &= m - 1;
@@ -342,6 +432,7 @@ __global__ void __launch_bounds__(256) k_fire(FireArgs a) {
             }
         }
     }
+    stage_flush(rs, &a.st->rows, a.o_key, a.o_start, a.o_end, a.o_res);
 }
 
 // Move the cells of ring positions `emask` to the deferred list (ring re-base down).
@@ -351,6 +442,7 @@ __global__ void __launch_bounds__(256) k_evict(EvictArgs a) {
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     const int64_t id0 = identity0(AGG);
     const int W = a.t.words;
+    if (blockIdx.x == 0 && threadIdx.x < kShards) atomicAnd(&a.st->sh[threadIdx.x].occ, ~a.emask);
     for (int64_t base = blockIdx.x * (int64_t)blockDim.x; base < nslots; base += stride) {
         const int64_t i = base + threadIdx.x;
         uint64_t m = 0;
@@ -359,11 +451,11 @@ __global__ void __launch_bounds__(256) k_evict(EvictArgs a) {
         if (i < nslots) {
             s = slot_ptr(a.t, i);
             key = s[0];
-            m = (uint64_t)s[1] & a.emask;
+            m = presence<AGG>(s, a.t.ring, W) & a.emask;
         }
         unsigned long long off = wave_reserve_n(&a.st->n_deferred, (unsigned)__popcll(m));
         if (m) {
-            s[1] = (int64_t)((uint64_t)s[1] & ~a.emask);
+            if constexpr (uses_mask<AGG>()) s[1] = (int64_t)((uint64_t)s[1] & ~a.emask);
             while (m) {
                 const int pos = __ffsll((long long)m) - 1;
                 m &= m - 1;
@@ -388,7 +480,7 @@ __global__ void __launch_bounds__(256) k_rehash(TableView o, TableView n, DevSta
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nslots;
          i += (int64_t)gridDim.x * blockDim.x) {
         const int64_t* s = slot_ptr(o, i);
-        if (s[1] == 0) continue;
+        if (presence_rt(s, o) == 0) continue;
         const int64_t key = i == o.cap ? kEmptyKey : s[0];
         bool inserted;
         const int64_t j = find_or_insert(n, key, inserted);
@@ -397,16 +489,24 @@ __global__ void __launch_bounds__(256) k_rehash(TableView o, TableView n, DevSta
         int64_t* d = slot_ptr(n, j);
         for (int w = 1; w < W; ++w) d[w] = s[w];
     }
-    wave_add(&st->used_slots, ins);
-    wave_or(&st->flags, flags);
+    block_commit(st, 0, ins, flags, 0);
 }
 
 __global__ void __launch_bounds__(256) k_count_live(TableView t, unsigned long long* out) {
     unsigned long long c = 0;
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i <= t.cap;
          i += (int64_t)gridDim.x * blockDim.x)
-        c += slot_ptr(t, i)[1] != 0;
+        c += presence_rt(slot_ptr(t, i), t) != 0;
     wave_add(out, c);
+}
+
+// Status word writes, ordered on the stream (no host sync).
+__global__ void k_status_set(DevStatus* st, int word, unsigned long long v, int shard_field) {
+    if (shard_field >= 0) {
+        if (threadIdx.x < kShards) reinterpret_cast<unsigned long long*>(&st->sh[threadIdx.x])[shard_field] = v;
+    } else if (threadIdx.x == 0) {
+        reinterpret_cast<unsigned long long*>(st)[word] = v;
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -428,9 +528,9 @@ __global__ void __launch_bounds__(256) k_count_live(TableView t, unsigned long l
     }
 
 static inline int grid_for(int64_t n, int per_thread = 1) {
-    int64_t g = (n / per_thread + 255) / 256;
+    int64_t g = ((n + per_thread - 1) / per_thread + 255) / 256;
     if (g < 1) g = 1;
-    if (g > 256 * 16) g = 256 * 16;  // 16 blocks per CU, grid-stride the rest
+    if (g > 256 * 8) g = 256 * 8;  // 8 blocks (32 waves) per CU, grid-stride the rest
     return (int)g;
 }
 
@@ -448,8 +548,8 @@ hipError_t launch_ingest(const IngestArgs& a, bool preagg, hipStream_t s) {
         GW_AGG_SWITCH(a.t.agg, L);
 #undef L
     } else {
-        const int g = grid_for(a.n);
-#define L(A) hipLaunchKernelGGL(k_ingest<A>, dim3(g), dim3(256), 0, s, a)
+        const int g = grid_for(a.n, 2);
+#define L(A) hipLaunchKernelGGL((k_ingest<A, 2>), dim3(g), dim3(256), 0, s, a)
         GW_AGG_SWITCH(a.t.agg, L);
 #undef L
     }
@@ -469,7 +569,8 @@ hipError_t launch_deferred_min(const int64_t* pane, int64_t n, DevStatus* st, hi
 }
 
 hipError_t launch_fire(const FireArgs& a, hipStream_t s) {
-#define L(A) hipLaunchKernelGGL(k_fire<A>, dim3(grid_for(a.t.cap + 1)), dim3(256), 0, s, a)
+    const int fg = (int)std::min<int64_t>(1024, std::max<int64_t>(1, (a.t.cap + 1 + 255) / 256));
+#define L(A) hipLaunchKernelGGL(k_fire<A>, dim3(fg), dim3(256), 0, s, a)
     GW_AGG_SWITCH(a.t.agg, L);
 #undef L
     return hipGetLastError();
@@ -479,6 +580,11 @@ hipError_t launch_evict(const EvictArgs& a, hipStream_t s) {
 #define L(A) hipLaunchKernelGGL(k_evict<A>, dim3(grid_for(a.t.cap + 1)), dim3(256), 0, s, a)
     GW_AGG_SWITCH(a.t.agg, L);
 #undef L
+    return hipGetLastError();
+}
+
+hipError_t launch_status_set(DevStatus* st, int word, unsigned long long v, int shard_field, hipStream_t s) {
+    hipLaunchKernelGGL(k_status_set, dim3(1), dim3(64), 0, s, st, word, v, shard_field);
     return hipGetLastError();
 }
 

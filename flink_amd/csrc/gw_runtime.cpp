@@ -155,9 +155,13 @@ struct gw_handle {
         if (e_ != hipSuccess) return fail(GW_E_DEVICE, "%s failed: %s", #x, hipGetErrorString(e_)); \
     } while (0)
 
+    bool dirty = true;  // device counters changed since the last refresh()
+
     int refresh() {
         HIPCHECK(hipMemcpyAsync(h_st, d_st, sizeof(DevStatus), hipMemcpyDeviceToHost, stream));
         HIPCHECK(hipStreamSynchronize(stream));
+        fold_shards(h_st);
+        dirty = false;
         if (timing) { t_ingest.resolve(); t_fire.resolve(); }
         if (h_st->flags & GW_DF_NO_TS)
             return fail(GW_E_NO_TIMESTAMP,
@@ -165,25 +169,28 @@ struct gw_handle {
                         "call 'DataStream.assignTimestampsAndWatermarks(...)'?");
         if (h_st->flags & GW_DF_RANGE)
             return fail(GW_E_RANGE, "record timestamp/pane outside the supported int64 window range");
+        occ = h_st->occ;
         stats.late_dropped = (int64_t)h_st->late;
         stats.live_keys = (int64_t)h_st->used_slots;
         stats.deferred = (int64_t)h_st->n_deferred;
         stats.session_merges = (int64_t)h_st->merges;
         return GW_OK;
     }
+    int ensure_fresh() { return dirty ? refresh() : GW_OK; }
+    // Write one scalar status word, ordered on the stream (no host sync).
     int set_field(size_t off, unsigned long long v) {
-        // small H2D write of one DevStatus word, ordered on the stream
-        unsigned long long* hv = reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(h_st) + off);
-        *hv = v;
-        HIPCHECK(hipMemcpyAsync(reinterpret_cast<char*>(d_st) + off, hv, 8, hipMemcpyHostToDevice, stream));
-        HIPCHECK(hipStreamSynchronize(stream));  // h_st reused as the source
+        *reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(h_st) + off) = v;
+        HIPCHECK(launch_status_set(d_st, (int)(off / 8), v, -1, stream));
         return GW_OK;
     }
-    int take_occ() {  // fold device ring occupancy into the host view and clear it
-        occ |= h_st->occ;
-        if (h_st->occ) return set_field(offsetof(DevStatus, occ), 0);
+    // Zero one field of every counter shard (field index within ShardCtr).
+    int zero_shards(int field) {
+        for (int i = 0; i < kShards; ++i) reinterpret_cast<unsigned long long*>(&h_st->sh[i])[field] = 0;
+        HIPCHECK(launch_status_set(d_st, 0, 0, field, stream));
+        dirty = true;
         return GW_OK;
     }
+    int take_occ() { occ = h_st->occ; return GW_OK; }
 
     // ---------------------------------------------------------------- memory
     int alloc_table(TableView& t, int64_t cap) {
@@ -255,7 +262,9 @@ struct gw_handle {
         TableView nt;
         int rc = alloc_table(nt, new_cap);
         if (rc) return rc;
-        if ((rc = set_field(offsetof(DevStatus, used_slots), 0))) return rc;
+        if ((rc = zero_shards(1))) return rc;                          // ins (used slots)
+        if (h_st->flags & GW_DF_TABLE_FULL)
+            if ((rc = zero_shards(2))) return rc;                      // flags
         HIPCHECK(launch_rehash(tv, nt, d_st, stream));
         HIPCHECK(hipStreamSynchronize(stream));
         HIPCHECK(hipFree(tv.base));
@@ -281,16 +290,11 @@ struct gw_handle {
         const bool full = (h_st->flags & GW_DF_TABLE_FULL) != 0;
         if (!full && (double)used <= 0.7 * (double)tv.cap) return GW_OK;
         const int64_t live = live_count();
+        // parked records that failed to insert are potential new keys
+        const int64_t pending = full ? std::max<int64_t>(incoming, (int64_t)h_st->n_deferred) : 0;
         int64_t want = std::max<int64_t>(tv.cap, 1024);
-        while ((double)live > 0.45 * (double)want || (full && want <= tv.cap)) want *= 2;
-        (void)incoming;
-        int rc = rehash(want);
-        if (rc) return rc;
-        if (full) {
-            unsigned long long f = h_st->flags & ~GW_DF_TABLE_FULL;
-            if ((rc = set_field(offsetof(DevStatus, flags), f))) return rc;
-        }
-        return GW_OK;
+        while ((double)(live + pending) > 0.5 * (double)want || (full && want <= tv.cap)) want *= 2;
+        return rehash(want);
     }
 
     // ---------------------------------------------------------------- pane mode
@@ -428,6 +432,7 @@ struct gw_handle {
                 HIPCHECK(launch_fire(f, stream));
             }
             stats.fires++;
+            dirty = true;
             occ &= ~rmask;
             fired_k = k_last + 1;
             if (B < fired_k * m) B = fired_k * m;
@@ -447,7 +452,7 @@ struct gw_handle {
 
     int ingest_pane(int64_t nrec, const int64_t* key, const int64_t* ts, const int64_t* val) {
         int rc;
-        if ((rc = refresh())) return rc;
+        if ((rc = ensure_fresh())) return rc;
         if ((rc = maybe_grow(nrec))) return rc;
         if ((rc = ensure_deferred((int64_t)h_st->n_deferred + nrec))) return rc;
         // first non-late pane: the first window not fired at the current watermark
@@ -494,8 +499,8 @@ struct gw_handle {
         }
         stats.events_in += nrec;
         stats.batches++;
-        if ((rc = refresh())) return rc;
-        if ((rc = take_occ())) return rc;
+        dirty = true;
+        if ((rc = refresh())) return rc;  // the one host sync of an ingest call
         if (h_st->flags & GW_DF_TABLE_FULL) {
             if ((rc = maybe_grow(0))) return rc;
             if ((rc = merge_deferred())) return rc;
@@ -513,15 +518,20 @@ struct gw_handle {
 
     int advance_pane(int64_t w, int64_t* rows_out) {
         int rc;
-        if ((rc = refresh())) return rc;
-        if ((rc = take_occ())) return rc;
+        if (rows_out) *rows_out = 0;
+        if (w <= wm) return GW_OK;
+        const i128 kt = k_for_wm(w);
+        if (kt < fired_k) {  // no window completes: nothing to launch (timer heap empty below w)
+            wm = w;
+            return GW_OK;
+        }
+        if ((rc = ensure_fresh())) return rc;
         const int64_t before = (int64_t)h_st->rows;
-        if (w > wm) {
-            const i128 kt = k_for_wm(w);
+        {
             if ((rc = fire_until(kt))) return rc;
             wm = w;
         }
-        if ((rc = refresh())) return rc;
+        if ((rc = ensure_fresh())) return rc;
         const int64_t fired = (int64_t)h_st->rows - before;
         stats.rows_fired += fired;
         if (rows_out) *rows_out = fired;

@@ -64,11 +64,19 @@ __global__ void __launch_bounds__(256) k_sess_minmax(const int64_t* ts, int64_t 
         lo = a < lo ? a : lo;
         hi = b > hi ? b : hi;
     }
-    if (__lane_id() == 0) {
+    __shared__ long long red[2][16];
+    const int wave = threadIdx.x >> 6;
+    if (__lane_id() == 0) { red[0][wave] = lo; red[1][wave] = hi; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < (int)(blockDim.x >> 6); ++w) {
+            lo = red[0][w] < lo ? red[0][w] : lo;
+            hi = red[1][w] > hi ? red[1][w] : hi;
+        }
         if (lo != INT64_MAX) atomicMin(&mm[0], lo);
         if (hi != INT64_MIN) atomicMax(&mm[1], hi);
     }
-    wave_or(&st->flags, flags);
+    block_commit(st, 0, 0, flags, 0);
 }
 
 __global__ void __launch_bounds__(256) k_sess_prep(const int64_t* key, const int64_t* ts, int64_t n, int64_t ts_min,
@@ -83,8 +91,7 @@ __global__ void __launch_bounds__(256) k_sess_prep(const int64_t* key, const int
         skey[i] = ((uint64_t)s << ts_bits) | (uint64_t)(ts[i] - ts_min);
         perm[i] = (uint32_t)i;
     }
-    wave_add(&st->used_slots, ins);
-    wave_or(&st->flags, flags);
+    block_commit(st, 0, ins, flags, 0);
 }
 
 struct Sess {
@@ -218,9 +225,10 @@ __device__ void seg_process(const SegArgs& a, int64_t i) {
         if (SW == 4) x[3] = cur_list[q].a1;
     }
     sp[1] = cnt;
-    if (late) atomicAdd(&a.st->late, late);
-    if (merges) atomicAdd(&a.st->merges, merges);
-    if (flags) atomicOr(&a.st->flags, flags);
+    ShardCtr& sc = a.st->sh[blockIdx.x % kShards];
+    if (late) atomicAdd(&sc.late, late);
+    if (merges) atomicAdd(&sc.merges, merges);
+    if (flags) atomicOr(&sc.flags, flags);
 }
 
 template <int AGG>
@@ -239,36 +247,52 @@ __global__ void __launch_bounds__(256) k_sess_segment(SegArgs a) {
 
 // Fire every in-flight session with end-1 <= wm (sessions in a slot are disjoint and
 // sorted, so the fired ones are a prefix), emit (key, start, end, result), purge.
+// Rows are staged in LDS, one row per thread per round, and flushed in bulk.
 template <int AGG>
 __global__ void __launch_bounds__(256) k_sess_fire(TableView t, int64_t wm, int64_t* o_key, int64_t* o_start,
                                                    int64_t* o_end, int64_t* o_res, DevStatus* st) {
+    __shared__ RowStage rs;
+    __shared__ int s_max;
     const int64_t nslots = t.cap + 1;
     const int SW = t.words;
-    for (int64_t base = blockIdx.x * (int64_t)blockDim.x; base < nslots; base += (int64_t)gridDim.x * blockDim.x) {
+    if (threadIdx.x == 0) rs.cnt = 0;
+    __syncthreads();
+    const int64_t chunk = ((nslots + gridDim.x - 1) / gridDim.x + 255) / 256 * 256;
+    const int64_t c0 = blockIdx.x * chunk, c1 = min(nslots, c0 + chunk);
+    for (int64_t base = c0; base < c1; base += blockDim.x) {
         const int64_t i = base + threadIdx.x;
         int64_t* s = nullptr;
         int cnt = 0, nf = 0;
-        if (i < nslots) {
+        if (i < c1) {
             s = slot_ptr(t, i);
             cnt = (int)s[1];
             while (nf < cnt && s[2 + nf * SW + 1] - 1 <= wm) ++nf;
         }
-        unsigned long long off = wave_reserve_n(&st->rows, (unsigned)nf);
-        if (nf) {
-            const int64_t key = s[0];
-            for (int q = 0; q < nf; ++q) {
+        if (threadIdx.x == 0) s_max = 0;
+        __syncthreads();
+        if (nf) atomicMax(&s_max, nf);
+        __syncthreads();
+        const int rounds = s_max;
+        __syncthreads();  // everyone has read s_max before thread 0 resets it
+        for (int q = 0; q < rounds; ++q) {
+            if (rs.cnt + blockDim.x > kRowStage) stage_flush(rs, &st->rows, o_key, o_start, o_end, o_res);
+            if (q < nf) {
                 const int64_t* x = s + 2 + q * SW;
-                o_key[off] = key;
-                o_start[off] = x[0];
-                o_end[off] = x[1];
-                o_res[off] = cell_result(AGG, x[2], SW == 4 ? x[3] : 0);
-                off++;
+                const unsigned j = atomicAdd(&rs.cnt, 1u);
+                rs.k[j] = s[0];
+                rs.s[j] = x[0];
+                rs.e[j] = x[1];
+                rs.r[j] = cell_result(AGG, x[2], SW == 4 ? x[3] : 0);
             }
+            __syncthreads();
+        }
+        if (nf) {
             for (int q = nf; q < cnt; ++q)
                 for (int w = 0; w < SW; ++w) s[2 + (q - nf) * SW + w] = s[2 + q * SW + w];
             s[1] = cnt - nf;
         }
     }
+    stage_flush(rs, &st->rows, o_key, o_start, o_end, o_res);
 }
 
 __global__ void __launch_bounds__(256) k_sess_rewiden(TableView o, TableView n) {
@@ -374,6 +398,7 @@ static std::pair<hipEvent_t, hipEvent_t> get_ev(SessionState* s) {
 int session_refresh(SessionState* s, std::string& err) {
     SCHECK(hipMemcpyAsync(s->h_st, s->d_st, sizeof(DevStatus), hipMemcpyDeviceToHost, s->stream));
     SCHECK(hipStreamSynchronize(s->stream));
+    fold_shards(s->h_st);
     if (s->timing) resolve_timers(s);
     if (s->h_st->flags & GW_DF_NO_TS) {
         err = "Record has Long.MIN_VALUE timestamp (= no timestamp marker). Did you forget to call "
@@ -463,7 +488,7 @@ static int rehash_sess(SessionState* s, int64_t new_cap, std::string& err) {
     TableView nt;
     int rc = alloc_sess_table(s, nt, new_cap, s->tv.ring, err);
     if (rc) return rc;
-    if ((rc = set_word(s, offsetof(DevStatus, used_slots), 0, err))) return rc;
+    SCHECK(launch_status_set(s->d_st, 0, 0, 1, s->stream));  // zero sh[].ins (used slots)
     SCHECK(launch_rehash(s->tv, nt, s->d_st, s->stream));
     SCHECK(hipStreamSynchronize(s->stream));
     hipFree(s->tv.base);
@@ -521,7 +546,7 @@ int session_ingest(SessionState* s, int64_t n, const int64_t* key, const int64_t
         if ((rc = session_refresh(s, err))) return rc;
         if (!(s->h_st->flags & GW_DF_TABLE_FULL)) break;
         if (attempt > 4) { err = "session state table full"; return GW_E_OOM; }
-        if ((rc = set_word(s, offsetof(DevStatus, flags), s->h_st->flags & ~GW_DF_TABLE_FULL, err))) return rc;
+        SCHECK(launch_status_set(s->d_st, 0, 0, 2, s->stream));  // zero sh[].flags
         if ((rc = rehash_sess(s, s->tv.cap * 2, err))) return rc;
         slot_bits++;
         if (ts_bits + slot_bits > 64) { err = "session sort key overflow"; return GW_E_UNSUPPORTED; }
@@ -594,9 +619,10 @@ int session_fire(SessionState* s, int64_t wm, int64_t* fired, std::string& err) 
     }
     auto ev = s->timing ? get_ev(s) : std::pair<hipEvent_t, hipEvent_t>{};
     if (s->timing) SCHECK(hipEventRecord(ev.first, s->stream));
-#define L(A)                                                                                                     \
-    hipLaunchKernelGGL(k_sess_fire<A>, dim3(grid_of(s->tv.cap + 1)), dim3(256), 0, s->stream, s->tv, wm, s->o_key, \
-                       s->o_start, s->o_end, s->o_res, s->d_st)
+    const unsigned fg = (unsigned)std::min<int64_t>(1024, std::max<int64_t>(1, (s->tv.cap + 1 + 255) / 256));
+#define L(A)                                                                                               \
+    hipLaunchKernelGGL(k_sess_fire<A>, dim3(fg), dim3(256), 0, s->stream, s->tv, wm, s->o_key, s->o_start, \
+                       s->o_end, s->o_res, s->d_st)
     GW_AGG_SWITCH(s->cfg.agg, L);
 #undef L
     SCHECK(hipGetLastError());
