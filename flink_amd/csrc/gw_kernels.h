@@ -66,7 +66,7 @@ struct EvictArgs {
 };
 
 hipError_t launch_table_init(const TableView& t, hipStream_t s);
-hipError_t launch_ingest(const IngestArgs& a, bool preagg, hipStream_t s);
+hipError_t launch_ingest(const IngestArgs& a, bool preagg, int unroll, hipStream_t s);
 hipError_t launch_merge_deferred(const MergeArgs& a, hipStream_t s);
 hipError_t launch_deferred_min(const int64_t* pane, int64_t n, DevStatus* st, hipStream_t s);
 hipError_t launch_fire(const FireArgs& a, hipStream_t s);

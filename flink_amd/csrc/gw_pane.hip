@@ -402,7 +402,10 @@ __global__ void __launch_bounds__(256) k_fire(FireArgs a) {
             mask = presence<AGG>(s, R, W);
         }
         for (int w = 0; w < a.nwin; ++w) {
-            if (rs.cnt + blockDim.x > kRowStage) stage_flush(rs, &a.st->rows, a.o_key, a.o_start, a.o_end, a.o_res);
+            // uniform flush decision: every thread reads rs.cnt before anyone appends
+            const bool flush = rs.cnt + blockDim.x > kRowStage;
+            __syncthreads();
+            if (flush) stage_flush(rs, &a.st->rows, a.o_key, a.o_start, a.o_end, a.o_res);
             uint64_t m = mask & a.wmask[w];
             if (m) {
                 int64_t r0 = id0, r1 = 0;
@@ -541,17 +544,29 @@ hipError_t launch_table_init(const TableView& t, hipStream_t s) {
     return hipGetLastError();
 }
 
-hipError_t launch_ingest(const IngestArgs& a, bool preagg, hipStream_t s) {
+hipError_t launch_ingest(const IngestArgs& a, bool preagg, int unroll, hipStream_t s) {
     if (preagg) {
         const int g = grid_for(a.n, kPreaggItems);
 #define L(A) hipLaunchKernelGGL(k_ingest_preagg<A>, dim3(g), dim3(256), 0, s, a)
         GW_AGG_SWITCH(a.t.agg, L);
 #undef L
     } else {
-        const int g = grid_for(a.n, 2);
-#define L(A) hipLaunchKernelGGL((k_ingest<A, 2>), dim3(g), dim3(256), 0, s, a)
-        GW_AGG_SWITCH(a.t.agg, L);
+        if (unroll == 4) {
+            const int g = grid_for(a.n, 4);
+#define L(A) hipLaunchKernelGGL((k_ingest<A, 4>), dim3(g), dim3(256), 0, s, a)
+            GW_AGG_SWITCH(a.t.agg, L);
 #undef L
+        } else if (unroll == 2) {
+            const int g = grid_for(a.n, 2);
+#define L(A) hipLaunchKernelGGL((k_ingest<A, 2>), dim3(g), dim3(256), 0, s, a)
+            GW_AGG_SWITCH(a.t.agg, L);
+#undef L
+        } else {
+            const int g = grid_for(a.n, 1);
+#define L(A) hipLaunchKernelGGL((k_ingest<A, 1>), dim3(g), dim3(256), 0, s, a)
+            GW_AGG_SWITCH(a.t.agg, L);
+#undef L
+        }
     }
     return hipGetLastError();
 }

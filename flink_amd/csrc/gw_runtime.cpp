@@ -9,6 +9,7 @@
 #include <algorithm>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
@@ -138,6 +139,7 @@ struct gw_handle {
     KernelTimer t_ingest, t_fire;
 
     SessionState* sess = nullptr;
+    int ingest_unroll = 2;  // records per thread per iteration of k_ingest (GW_INGEST_UNROLL)
 
     int fail(int code, const char* fmt, ...) {
         char buf[512];
@@ -491,11 +493,11 @@ struct gw_handle {
         if (timing) {
             auto ev = t_ingest.get();
             HIPCHECK(hipEventRecord(ev.first, stream));
-            HIPCHECK(launch_ingest(a, preagg, stream));
+            HIPCHECK(launch_ingest(a, preagg, ingest_unroll, stream));
             HIPCHECK(hipEventRecord(ev.second, stream));
             t_ingest.pending.push_back(ev);
         } else {
-            HIPCHECK(launch_ingest(a, preagg, stream));
+            HIPCHECK(launch_ingest(a, preagg, ingest_unroll, stream));
         }
         stats.events_in += nrec;
         stats.batches++;
@@ -596,6 +598,7 @@ int gw_create(const gw_config* cfg, gw_handle** out) {
     gw_handle* h = new (std::nothrow) gw_handle();
     if (!h) { g_create_error = "out of host memory"; return GW_E_OOM; }
     h->cfg = *cfg;
+    if (const char* u = getenv("GW_INGEST_UNROLL")) h->ingest_unroll = atoi(u);
     if (h->cfg.max_parallelism <= 0) h->cfg.max_parallelism = 128;
     if (h->cfg.parallelism <= 0) h->cfg.parallelism = 1;
     if (h->cfg.max_batch <= 0) h->cfg.max_batch = 1 << 20;

@@ -275,7 +275,9 @@ __global__ void __launch_bounds__(256) k_sess_fire(TableView t, int64_t wm, int6
         const int rounds = s_max;
         __syncthreads();  // everyone has read s_max before thread 0 resets it
         for (int q = 0; q < rounds; ++q) {
-            if (rs.cnt + blockDim.x > kRowStage) stage_flush(rs, &st->rows, o_key, o_start, o_end, o_res);
+            const bool flush = rs.cnt + blockDim.x > kRowStage;
+            __syncthreads();
+            if (flush) stage_flush(rs, &st->rows, o_key, o_start, o_end, o_res);
             if (q < nf) {
                 const int64_t* x = s + 2 + q * SW;
                 const unsigned j = atomicAdd(&rs.cnt, 1u);
