@@ -135,53 +135,30 @@ def main():
     op = W.GpuWindowOperator(W.SlidingEventTimeWindows.of(size, slide), agg, capacity_hint=max(K // world, 1024),
                              max_parallelism=maxp, parallelism=world, operator_index=rank, device=local,
                              flags=flags, max_batch=nb * 2).open()
-    op_stream = op.stream()
     cur = torch.cuda.current_stream().cuda_stream
 
-    # exchange buffers (multi-GPU)
-    if world > 1 and args.exchange == "a2a":
-        pk = torch.empty(nb, dtype=torch.int64, device=dev)
-        pt = torch.empty_like(pk)
-        pv = torch.empty_like(pk) if vals is not None else None
-        counts = torch.empty(world, dtype=torch.int64, device=dev)
-        rcounts = torch.empty_like(counts)
-        scratch = torch.empty(N.lib().gw_partition_scratch_bytes(nb, world), dtype=torch.uint8, device=dev)
-        rk = torch.empty(nb * 2, dtype=torch.int64, device=dev)
-        rt = torch.empty_like(rk)
-        rv = torch.empty_like(rk) if vals is not None else None
+    ex = None
+    if world > 1:
+        from flink_amd.exchange import KeyByExchange
+        ex = KeyByExchange(world, rank, max_parallelism=maxp, device=dev)
 
     exch_bytes = 0
-    d_b = []  # distinct (key, pane) accumulators per timed batch (rank-local)
 
     def step(b, timed):
         nonlocal exch_bytes
         lo, hi = b * nb, (b + 1) * nb
         k, t, v = keys[lo:hi], ts[lo:hi], (vals[lo:hi] if vals is not None else None)
-        if world > 1 and args.exchange == "a2a":
-            N.check(N.lib().gw_partition_device(nb, k.data_ptr(), None, t.data_ptr(),
-                                                v.data_ptr() if v is not None else None, maxp, world,
-                                                pk.data_ptr(), pt.data_ptr(),
-                                                pv.data_ptr() if v is not None else None,
-                                                counts.data_ptr(), scratch.data_ptr(), cur))
-            dist.all_to_all_single(rcounts, counts)
-            sc = counts.tolist()
-            rc = rcounts.tolist()
-            nrecv = sum(rc)
-            dist.all_to_all_single(rk[:nrecv], pk, rc, sc)
-            dist.all_to_all_single(rt[:nrecv], pt, rc, sc)
-            if v is not None:
-                dist.all_to_all_single(rv[:nrecv], pv, rc, sc)
-            k, t, v = rk[:nrecv], rt[:nrecv], (rv[:nrecv] if v is not None else None)
+        if ex is not None and args.exchange == "a2a":
+            pk, pt, pv, counts = ex.partition(k, t, v, stream=cur)
+            (k, t, v), n_recv = ex.exchange_partitioned([pk, pt, pv], counts)
             if timed:
-                exch_bytes += (nb - sc[rank]) * b_in
+                exch_bytes += (nb - int(counts[rank].item())) * b_in
         n = k.numel()
         N.check(N.lib().gw_ingest_device(op.handle, n, k.data_ptr(), None, t.data_ptr(),
                                          v.data_ptr() if v is not None else None, cur), op.handle)
         wm = wms[b]
-        if world > 1:
-            w = torch.tensor([wm], dtype=torch.int64, device=dev)
-            dist.all_reduce(w, op=dist.ReduceOp.MIN)  # StatusWatermarkValve: min over inputs
-            wm = int(w.item())
+        if ex is not None:
+            wm = ex.combine_watermark(wm)  # StatusWatermarkValve: min over inputs
         op.advance_watermark(wm)
         op.clear_rows()  # DiscardingSink
         return k, t
