@@ -1,0 +1,134 @@
+/*
+ * GpuWindowOperator — drop-in for WindowOperator on the keyed event-time aggregation path,
+ * backed by libgpuwin.so (MI355X).  NOT BUILT in this repository (no JDK in the build image);
+ * it shows the reference-side binding a Flink maintainer adds.  It fills the same slot as
+ * WindowOperator (flink-runtime/.../operators/windowing/WindowOperator.java:102): a
+ * OneInputStreamOperator inserted by WindowedStream via input.transform(...)
+ * (WindowedStream.java:233-240, DataStream.java:815-821).
+ *
+ * Records between two watermarks are appended to off-heap columns; processWatermark hands
+ * the batch to the GPU, advances event time, and emits the fired (key, window, result) rows
+ * BEFORE forwarding the watermark, as AbstractStreamOperator.processWatermark does
+ * (AbstractStreamOperator.java:690-703).
+ */
+package org.apache.flink.streaming.runtime.operators.windowing.gpu;
+
+import org.apache.flink.api.java.functions.KeySelector;
+import org.apache.flink.api.java.tuple.Tuple4;
+import org.apache.flink.streaming.api.operators.AbstractStreamOperator;
+import org.apache.flink.streaming.api.operators.BoundedOneInput;
+import org.apache.flink.streaming.api.operators.OneInputStreamOperator;
+import org.apache.flink.streaming.api.watermark.Watermark;
+import org.apache.flink.streaming.runtime.streamrecord.StreamRecord;
+import org.apache.flink.streaming.runtime.tasks.KeyContextHandler;
+
+import java.nio.ByteBuffer;
+import java.nio.ByteOrder;
+import java.util.function.ToDoubleFunction;
+import java.util.function.ToLongFunction;
+
+public class GpuWindowOperator<IN>
+        extends AbstractStreamOperator<Tuple4<Long, Long, Long, Object>>
+        implements OneInputStreamOperator<IN, Tuple4<Long, Long, Long, Object>>, BoundedOneInput,
+                KeyContextHandler {
+
+    static { System.loadLibrary("gpuwin_jni"); }
+
+    // gw_assigner / gw_trigger / gw_agg codes of include/gpuwin.h
+    private final int assigner, trigger, agg;
+    private final long size, slide, offset, gap, lateness;
+    private final KeySelector<IN, Long> keySelector;
+    private final ToLongFunction<IN> longValue;       // for integer aggregates
+    private final ToDoubleFunction<IN> doubleValue;   // for f64 aggregates
+    private final int batchCapacity;
+
+    private transient long handle;
+    private transient ByteBuffer keys, hashes, ts, values, oKey, oStart, oEnd, oRes;
+    private transient int n;
+
+    public GpuWindowOperator(int assigner, long size, long slide, long offset, long gap, long lateness,
+                             int trigger, int agg, KeySelector<IN, Long> keySelector,
+                             ToLongFunction<IN> longValue, ToDoubleFunction<IN> doubleValue, int batchCapacity) {
+        this.assigner = assigner; this.size = size; this.slide = slide; this.offset = offset;
+        this.gap = gap; this.lateness = lateness; this.trigger = trigger; this.agg = agg;
+        this.keySelector = keySelector; this.longValue = longValue; this.doubleValue = doubleValue;
+        this.batchCapacity = batchCapacity;
+    }
+
+    @Override
+    public boolean hasKeyContext() { return false; }  // no per-record setCurrentKey (RecordProcessorUtils.java:47-57)
+
+    @Override
+    public void open() throws Exception {
+        super.open();
+        int subtask = getRuntimeContext().getTaskInfo().getIndexOfThisSubtask();
+        int parallelism = getRuntimeContext().getTaskInfo().getNumberOfParallelSubtasks();
+        int maxP = getRuntimeContext().getTaskInfo().getMaxNumberOfParallelSubtasks();
+        int device = 0; // RuntimeContext.getExternalResourceInfos("gpu") with an amd-smi discovery script
+        handle = nativeCreate(assigner, trigger, size, slide, offset, gap, lateness, agg, maxP, parallelism,
+                              subtask, device, 1L << 24, batchCapacity);
+        keys = direct(8); hashes = direct(4); ts = direct(8); values = direct(8);
+        oKey = direct(8); oStart = direct(8); oEnd = direct(8); oRes = direct(8);
+    }
+
+    private ByteBuffer direct(int width) {
+        return ByteBuffer.allocateDirect(batchCapacity * width).order(ByteOrder.nativeOrder());
+    }
+
+    @Override
+    public void processElement(StreamRecord<IN> element) throws Exception {
+        IN v = element.getValue();
+        Long k = keySelector.getKey(v);
+        keys.putLong(n * 8, k);
+        hashes.putInt(n * 4, k.hashCode());                 // key group of the reference
+        ts.putLong(n * 8, element.getTimestamp());
+        if (doubleValue != null) values.putDouble(n * 8, doubleValue.applyAsDouble(v));
+        else if (longValue != null) values.putLong(n * 8, longValue.applyAsLong(v));
+        if (++n == batchCapacity) flush();
+    }
+
+    private void flush() {
+        if (n > 0) nativeIngest(handle, n, keys, hashes, ts, values);
+        n = 0;
+    }
+
+    @Override
+    public void processWatermark(Watermark mark) throws Exception {
+        flush();
+        nativeAdvanceWatermark(handle, mark.getTimestamp());
+        int got;
+        while ((got = nativeDrain(handle, oKey, oStart, oEnd, oRes, batchCapacity)) > 0) {
+            for (int i = 0; i < got; i++) {
+                long end = oEnd.getLong(i * 8);
+                Object res = agg == 2 || agg >= 5 && agg <= 8 ? (Object) oRes.getDouble(i * 8) : oRes.getLong(i * 8);
+                output.collect(new StreamRecord<>(
+                        Tuple4.of(oKey.getLong(i * 8), oStart.getLong(i * 8), end, res), end - 1));
+            }
+            if (got < batchCapacity) break;
+        }
+        super.processWatermark(mark);  // forward after the fired rows
+    }
+
+    @Override
+    public void endInput() throws Exception { processWatermark(Watermark.MAX_WATERMARK); }
+
+    @Override
+    public void close() throws Exception {
+        if (handle != 0) nativeDestroy(handle);
+        handle = 0;
+        super.close();
+    }
+
+    public long numLateRecordsDropped() { return nativeLateDropped(handle); }
+
+    private static native long nativeCreate(int assigner, int trigger, long size, long slide, long offset, long gap,
+                                            long lateness, int agg, int maxParallelism, int parallelism,
+                                            int subtask, int device, long capacityHint, long maxBatch);
+    private static native void nativeIngest(long h, int n, ByteBuffer keys, ByteBuffer keyHashes, ByteBuffer ts,
+                                            ByteBuffer values);
+    private static native long nativeAdvanceWatermark(long h, long wm);
+    private static native int nativeDrain(long h, ByteBuffer key, ByteBuffer start, ByteBuffer end, ByteBuffer result,
+                                          int cap);
+    private static native long nativeLateDropped(long h);
+    private static native void nativeDestroy(long h);
+}
