@@ -68,6 +68,8 @@ def parse():
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--preagg", choices=["auto", "force", "off"], default="auto")
+    ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
+                    help="nccl = RCCL over xGMI; gloo = host-staged rehearsal (several ranks may share one GPU)")
     return ap.parse_args()
 
 
@@ -79,12 +81,16 @@ def main():
     if world != args.gpus:
         if world == 1 and args.gpus > 1:
             raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run (one rank per GPU)")
+    local = local % max(torch.cuda.device_count(), 1)  # rehearsal: ranks may share a GPU
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
 
     from flink_amd import _native as N
     from flink_amd import windowing as W
@@ -184,7 +190,7 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if dist:
-        e = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        e = torch.tensor([elapsed], dtype=torch.float64, device=dev if args.dist_backend == "nccl" else "cpu")
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
     ingest_ms, ingest_launches = op.kernel_time_ms(0)
@@ -208,7 +214,8 @@ def main():
     achieved = per_launch / (ingest_ms / 1e3) / 1e9 if ingest_ms > 0 else 0.0
     pipeline_gbs = (ingest_bytes_total + fire_bytes_total) / elapsed / 1e9
 
-    tot = torch.tensor([events_rank, rows_rank], dtype=torch.int64, device=dev)
+    tot = torch.tensor([events_rank, rows_rank], dtype=torch.int64,
+                       device=dev if args.dist_backend == "nccl" else "cpu")
     if dist:
         dist.all_reduce(tot)
     events_all, rows_all = int(tot[0].item()), int(tot[1].item())
@@ -244,7 +251,7 @@ def main():
             "roofline": {
                 "bound": "hbm", "kernel": "k_ingest (pane RMW)",
                 "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                "frac": achieved / HBM_PEAK_GBS, "traffic": traffic_bytes(agg, nb),
                 "bytes_per_launch": per_launch, "avg_launch_ms": ingest_ms, "launches": ingest_launches,
                 "pipeline_achieved": pipeline_gbs, "pipeline_frac": pipeline_gbs / HBM_PEAK_GBS,
                 "fire_avg_launch_ms": fire_ms, "fire_launches": fire_launches,
@@ -259,6 +266,21 @@ def main():
     op.close()
     if dist:
         dist.destroy_process_group()
+
+
+def traffic_bytes(agg, nb):
+    """HBM bytes per k_ingest launch from the newest committed PMC pass of this workload
+    (profiles/<round>/traffic.json: FETCH_SIZE x2 + WRITE_SIZE, gfx950 corrections);
+    None when no pass matches this aggregate / batch size."""
+    import glob
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "traffic.json")), reverse=True):
+        try:
+            d = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        if d.get("agg") == agg and d.get("events_per_launch") == nb:
+            return d["traffic_bytes_per_launch"]
+    return None
 
 
 def cpu_baseline(args, keys, ts, vals, wms, nb, agg, size, slide):

@@ -56,6 +56,11 @@ class KeyByExchange:
                              ) -> Tuple[list, int]:
         """All-to-all of already partitioned columns (any backend: RCCL on GPU tensors,
         gloo on CPU tensors).  send_counts[d] = records for rank d."""
+        staged = dist.get_backend(self.group) == "gloo" and send_counts.is_cuda
+        if staged:  # rehearsal on one GPU: gloo moves host tensors only
+            dev = send_counts.device
+            send_counts = send_counts.cpu()
+            cols = [c.cpu() if c is not None else None for c in cols]
         recv_counts = torch.empty_like(send_counts)
         dist.all_to_all_single(recv_counts, send_counts, group=self.group)
         sc = send_counts.tolist()
@@ -68,7 +73,7 @@ class KeyByExchange:
                 continue
             r = torch.empty(total, dtype=c.dtype, device=c.device)
             dist.all_to_all_single(r, c, rc, sc, group=self.group)
-            out.append(r)
+            out.append(r.to(dev) if staged else r)
         return out, total
 
     def exchange(self, keys, ts, vals, key_hashes=None):
@@ -80,6 +85,8 @@ class KeyByExchange:
     def combine_watermark(self, wm: int) -> int:
         """Minimum over all ranks (StatusWatermarkValve)."""
         dev = self.device if self.device is not None else torch.device("cpu")
+        if dist.get_backend(self.group) == "gloo":
+            dev = torch.device("cpu")
         t = torch.tensor([wm], dtype=torch.int64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MIN, group=self.group)
         return int(t.item())
