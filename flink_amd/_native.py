@@ -30,6 +30,8 @@ DOUBLE_INPUT = {"sum_f64", "min_f64", "max_f64", "avg_f64"}
 FLAG_FORCE_LDS_PREAGG = 1
 FLAG_NO_LDS_PREAGG = 2
 FLAG_CHECK_KEY_GROUPS = 4
+FLAG_FORCE_REGION = 8
+FLAG_NO_REGION = 16
 
 EXPORTS = [
     "gw_create", "gw_destroy", "gw_last_error", "gw_abi_version", "gw_ingest", "gw_ingest_device",

@@ -1,8 +1,111 @@
-// gw_kernels.h — kernel argument blocks and launcher declarations (host <-> device).
+// gw_kernels.h — pane-table layout, kernel argument blocks and launcher declarations.
+//
+// Pane state table: `cap` slots in `nreg` regions of S = 2^log2S slots,
+// plus one sentinel region (slot index `cap`) for the key Long.MIN_VALUE, which doubles
+// as the empty marker.  A key's region is the top bits of its hash, its home slot the low
+// bits; linear probing stays inside the region.  Each region is stored SoA:
+//
+//     keys [S]                int64, kEmptyKey while free (set once by CAS)
+//     mask [S]                presence bits per ring cell (SUM/MIN/MAX only), 1/2/4/8
+//                             bytes per slot as the ring length R needs (Q5: R = 6, 1 B)
+//     cells[R][S][W]          pane accumulators, pane-major (W = 2 for AVG)
+//
+// so an ingest pass touches only the keys, the mask and the 1-2 pane arrays the batch
+// hits, each as one contiguous block per region (loaded into LDS and written back whole
+// by k_rgn_apply), and a fire pass streams every array coalesced.
 #pragma once
 #include "gw_device.h"
 
 namespace gw {
+
+struct PaneTable {
+    int64_t* base;
+    int64_t cap;           // slots = nreg << log2S (sentinel slot index = cap)
+    int64_t nreg;          // regions (power of two), + 1 sentinel region allocated
+    int64_t region_words;  // S + mask words + S * R * W
+    int32_t log2S;
+    int32_t log2nreg;
+    int32_t ring;          // R
+    int32_t words;         // W
+    int32_t agg;
+    int32_t has_mask;
+    int32_t mask_shift;    // log2 bytes of one slot's presence mask
+};
+
+GW_HD int64_t pt_S(const PaneTable& t) { return (int64_t)1 << t.log2S; }
+GW_HD int64_t* pt_region(const PaneTable& t, int64_t r) { return t.base + r * t.region_words; }
+GW_HD int64_t* pt_key(const PaneTable& t, int64_t g) {
+    return pt_region(t, g >> t.log2S) + (g & (pt_S(t) - 1));
+}
+// int64 words of one region's mask array (S >= 16, so always a whole, even number)
+GW_HD int64_t pt_mask_words(const PaneTable& t) { return t.has_mask ? (pt_S(t) << t.mask_shift) >> 3 : 0; }
+GW_HD uint8_t* pt_mask_base(const PaneTable& t, int64_t r) { return (uint8_t*)(pt_region(t, r) + pt_S(t)); }
+GW_HD int64_t* pt_cell(const PaneTable& t, int64_t g, int pos) {
+    const int64_t S = pt_S(t);
+    return pt_region(t, g >> t.log2S) + S + pt_mask_words(t) + ((int64_t)pos * S + (g & (S - 1))) * t.words;
+}
+// Presence mask of slot j in a region's mask array m (global or LDS).
+__device__ __forceinline__ uint64_t mask_get(const uint8_t* m, int64_t j, int shift) {
+    switch (shift) {
+    case 0: return m[j];
+    case 1: return ((const uint16_t*)m)[j];
+    case 2: return ((const uint32_t*)m)[j];
+    default: return ((const uint64_t*)m)[j];
+    }
+}
+__device__ __forceinline__ void mask_put(uint8_t* m, int64_t j, int shift, uint64_t v) {
+    switch (shift) {
+    case 0: m[j] = (uint8_t)v; break;
+    case 1: ((uint16_t*)m)[j] = (uint16_t)v; break;
+    case 2: ((uint32_t*)m)[j] = (uint32_t)v; break;
+    default: ((uint64_t*)m)[j] = v; break;
+    }
+}
+// Atomically set presence bit `pos` of slot j (32-bit atomic on the word holding it);
+// returns true if the bit was clear.
+__device__ __forceinline__ bool mask_set_bit(uint8_t* m, int64_t j, int shift, uint32_t pos) {
+    const uint64_t bit = ((uint64_t)j << (shift + 3)) + pos;
+    uint32_t* w = (uint32_t*)m + (bit >> 5);
+    const uint32_t b = 1u << (bit & 31);
+    if (*(volatile uint32_t*)w & b) return false;
+    return !(atomicOr(w, b) & b);
+}
+__device__ __forceinline__ uint64_t pt_mask_get(const PaneTable& t, int64_t g) {
+    return mask_get(pt_mask_base(t, g >> t.log2S), g & (pt_S(t) - 1), t.mask_shift);
+}
+__device__ __forceinline__ void pt_mask_put(const PaneTable& t, int64_t g, uint64_t v) {
+    mask_put(pt_mask_base(t, g >> t.log2S), g & (pt_S(t) - 1), t.mask_shift, v);
+}
+// region and home slot of a key hash (independent bit ranges)
+GW_HD int64_t pt_key_region(const PaneTable& t, uint64_t h) {
+    return t.log2nreg == 0 ? 0 : (int64_t)(h >> (64 - t.log2nreg));
+}
+GW_HD int64_t pt_home(const PaneTable& t, uint64_t h) { return (int64_t)(h & (uint64_t)(pt_S(t) - 1)); }
+
+// Find (or insert) the slot of `key` in its region; -1 if the probe limit is hit.
+__device__ __forceinline__ int64_t pt_find_or_insert(const PaneTable& t, int64_t key, bool& inserted) {
+    inserted = false;
+    if (key == kEmptyKey) return t.cap;
+    const uint64_t h = slot_hash(key);
+    const int64_t S = pt_S(t);
+    const int64_t r = pt_key_region(t, h);
+    int64_t* keys = pt_region(t, r);
+    int64_t j = pt_home(t, h);
+    const int lim = S < kMaxProbe ? (int)S : kMaxProbe;
+    for (int p = 0; p < lim; ++p) {
+        int64_t* kp = keys + j;
+        const int64_t k = *(volatile int64_t*)kp;
+        if (k == key) return (r << t.log2S) + j;
+        if (k == kEmptyKey) {
+            const unsigned long long prev = atomicCAS((unsigned long long*)kp, (unsigned long long)kEmptyKey,
+                                                      (unsigned long long)key);
+            if (prev == (unsigned long long)kEmptyKey) { inserted = true; return (r << t.log2S) + j; }
+            if ((int64_t)prev == key) return (r << t.log2S) + j;
+        }
+        j = (j + 1) & (S - 1);
+    }
+    return -1;
+}
 
 struct IngestArgs {
     const int64_t* key;
@@ -15,12 +118,30 @@ struct IngestArgs {
     UDiv64 div;         // division by the pane width g
     int32_t b_pos;      // B mod R
     int32_t late_exact; // 0: t_late was clamped at Long.MIN_VALUE (then ts < t_late is a range error)
-    TableView t;
+    PaneTable t;
     int64_t* d_key;     // deferred list (append at st->n_deferred)
     int64_t* d_pane;
     int64_t* d_a0;
     int64_t* d_a1;
     DevStatus* st;
+    // region path (k_part_*, k_rgn_apply)
+    int32_t d1_bits;       // region = (pass-1 bucket << d2_bits) | pass-2 bucket
+    int32_t d2_bits;       // 0: one pass (pass 1 writes e_* directly)
+    uint32_t* p_counts1;   // [tiles1][kPartBuckets] per-tile histogram -> column-exclusive offsets
+    uint32_t* p_counts2;   // [tiles2][kPartBuckets]
+    int64_t* p1_base;      // [2^d1 + 1] pass-1 bucket starts
+    int64_t* p2_tile0;     // [2^d1 + 1] first pass-2 tile of each pass-1 bucket
+    int64_t* p1_key;       // pass-1 output
+    int64_t* p1_a0;
+    int64_t* p1_a1;
+    uint8_t* p1_pos;
+    int64_t* rg_base;      // [nreg + 1] region bucket starts
+    int64_t* e_key;        // region-bucketed records
+    int64_t* e_a0;
+    int64_t* e_a1;
+    uint8_t* e_pos;
+    unsigned long long* batch_occ;  // ring positions this batch touches (for k_rgn_apply)
+    uint64_t ring_fresh;            // ring positions holding only identities (not in occ)
 };
 
 struct MergeArgs {
@@ -31,7 +152,7 @@ struct MergeArgs {
     int64_t n;
     int64_t b;          // ring base pane
     int32_t b_pos;
-    TableView t;
+    PaneTable t;
     int64_t* d_key;     // entries still outside the ring (append at st->n_deferred)
     int64_t* d_pane;
     int64_t* d_a0;
@@ -40,7 +161,7 @@ struct MergeArgs {
 };
 
 struct FireArgs {
-    TableView t;
+    PaneTable t;
     int32_t nwin;
     int64_t start0;     // start of the first window fired in this pass
     int64_t slide;
@@ -55,7 +176,7 @@ struct FireArgs {
 };
 
 struct EvictArgs {
-    TableView t;
+    PaneTable t;
     uint64_t emask;
     int64_t pane_of_pos[kMaxRing];
     int64_t* d_key;
@@ -65,15 +186,21 @@ struct EvictArgs {
     DevStatus* st;
 };
 
-hipError_t launch_table_init(const TableView& t, hipStream_t s);
-hipError_t launch_ingest(const IngestArgs& a, bool preagg, int unroll, hipStream_t s);
+constexpr int kPartTile = 4096;     // records per partition block (LDS-sorted)
+constexpr int kPartBuckets = 128;   // buckets per partition pass (<= 7 region bits)
+constexpr int kRgnMaxRegions = 16384;
+
+hipError_t launch_table_init(const PaneTable& t, hipStream_t s);
+// path: 0 direct atomics, 1 LDS pre-aggregation, 2 region (hist + scatter + apply)
+hipError_t launch_ingest(const IngestArgs& a, int path, int unroll, hipStream_t s);
+int64_t region_scratch_tiles(int64_t n);  // pass-1 tiles; pass 2 uses <= this + kPartBuckets
 hipError_t launch_merge_deferred(const MergeArgs& a, hipStream_t s);
 hipError_t launch_deferred_min(const int64_t* pane, int64_t n, DevStatus* st, hipStream_t s);
 hipError_t launch_fire(const FireArgs& a, hipStream_t s);
 hipError_t launch_evict(const EvictArgs& a, hipStream_t s);
-hipError_t launch_rehash(const TableView& o, const TableView& n, DevStatus* st, hipStream_t s);
+hipError_t launch_rehash(const PaneTable& o, const PaneTable& n, DevStatus* st, hipStream_t s);
 hipError_t launch_status_set(DevStatus* st, int word, unsigned long long v, int shard_field, hipStream_t s);
-hipError_t launch_count_live(const TableView& t, unsigned long long* out, hipStream_t s);
+hipError_t launch_count_live(const PaneTable& t, unsigned long long* out, hipStream_t s);
 
 // key groups / exchange (gw_keygroups.hip)
 hipError_t launch_key_groups(int64_t n, const int64_t* key, const int32_t* key_hash, int32_t max_p,

@@ -97,9 +97,19 @@ struct gw_handle {
     int R = 2;
     UDiv64 div{};
 
-    // state table
-    TableView tv{};
+    // state table (region-major SoA, gw_kernels.h)
+    PaneTable tv{};
     size_t table_bytes = 0;
+
+    // region-path scratch (k_part_*, k_rgn_apply)
+    uint32_t* p_counts = nullptr;  // pass-1 rows then pass-2 rows
+    int64_t p_counts_cap = 0;      // uint32 entries
+    int64_t* p_small = nullptr;    // p1_base | p2_tile0 (kPartBuckets + 1 each)
+    int64_t* rg_base = nullptr;
+    int64_t rg_base_cap = 0;       // int64 entries
+    int64_t* e_col[6] = {};        // e_key e_a0 e_a1 p1_key p1_a0 p1_a1
+    uint8_t* e_pos[2] = {};        // e_pos p1_pos
+    int64_t e_cap = 0;
 
     // event-time state
     int64_t wm = INT64_MIN;
@@ -140,6 +150,7 @@ struct gw_handle {
 
     SessionState* sess = nullptr;
     int ingest_unroll = 2;  // records per thread per iteration of k_ingest (GW_INGEST_UNROLL)
+    int64_t region_min_batch = 1 << 16;  // smallest batch for the region path (GW_REGION_MIN_BATCH)
 
     int fail(int code, const char* fmt, ...) {
         char buf[512];
@@ -195,12 +206,52 @@ struct gw_handle {
     int take_occ() { occ = h_st->occ; return GW_OK; }
 
     // ---------------------------------------------------------------- memory
-    int alloc_table(TableView& t, int64_t cap) {
+    // Region size S: one region's keys + mask + two pane arrays fit the LDS budget of
+    // k_rgn_apply (64 KB at S = 2048 for one-word cells).
+    static size_t pane_table_bytes(const PaneTable& t) { return (size_t)(t.nreg + 1) * (size_t)t.region_words * 8; }
+    int alloc_table(PaneTable& t, int64_t cap) {
         t = tv;
+        int64_t S = t.words == 2 ? 1024 : 2048;
+        if (S > cap) S = cap;
+        int l2s = 0;
+        while (((int64_t)1 << l2s) < S) ++l2s;
         t.cap = cap;
-        const size_t bytes = (size_t)(cap + 1) * (size_t)t.stride_w * 8;
-        HIPCHECK(hipMalloc((void**)&t.base, bytes));
+        t.log2S = l2s;
+        t.nreg = cap >> l2s;
+        int l2r = 0;
+        while (((int64_t)1 << l2r) < t.nreg) ++l2r;
+        t.log2nreg = l2r;
+        t.mask_shift = t.ring <= 8 ? 0 : t.ring <= 16 ? 1 : t.ring <= 32 ? 2 : 3;
+        t.region_words = S + pt_mask_words(t) + S * (int64_t)t.ring * t.words;
+        HIPCHECK(hipMalloc((void**)&t.base, pane_table_bytes(t)));
         HIPCHECK(launch_table_init(t, stream));
+        return GW_OK;
+    }
+    int ensure_region(int64_t n) {
+        const int64_t tiles1 = region_scratch_tiles(n);
+        const int64_t cnt = (2 * tiles1 + kPartBuckets) * kPartBuckets;
+        if (cnt > p_counts_cap) {
+            if (p_counts) { hipStreamSynchronize(stream); hipFree(p_counts); p_counts = nullptr; }
+            HIPCHECK(hipMalloc((void**)&p_counts, (size_t)cnt * 4));
+            p_counts_cap = cnt;
+        }
+        if (!p_small) HIPCHECK(hipMalloc((void**)&p_small, (size_t)2 * (kPartBuckets + 1) * 8));
+        if (tv.nreg + 1 > rg_base_cap) {
+            if (rg_base) { hipStreamSynchronize(stream); hipFree(rg_base); rg_base = nullptr; }
+            HIPCHECK(hipMalloc((void**)&rg_base, (size_t)(tv.nreg + 1) * 8));
+            rg_base_cap = tv.nreg + 1;
+        }
+        if (n > e_cap) {
+            hipStreamSynchronize(stream);
+            for (auto& p : e_col) { if (p) hipFree(p); p = nullptr; }
+            for (auto& p : e_pos) { if (p) hipFree(p); p = nullptr; }
+            for (int i = 0; i < 6; ++i) {
+                if ((i == 2 || i == 5) && tv.words != 2) continue;  // a1 only for AVG
+                HIPCHECK(hipMalloc((void**)&e_col[i], (size_t)n * 8));
+            }
+            for (auto& p : e_pos) HIPCHECK(hipMalloc((void**)&p, (size_t)n));
+            e_cap = n;
+        }
         return GW_OK;
     }
     int ensure_deferred(int64_t need) {
@@ -261,7 +312,7 @@ struct gw_handle {
 
     // Re-hash the live slots into a table of `new_cap` slots (drops dead keys).
     int rehash(int64_t new_cap) {
-        TableView nt;
+        PaneTable nt;
         int rc = alloc_table(nt, new_cap);
         if (rc) return rc;
         if ((rc = zero_shards(1))) return rc;                          // ins (used slots)
@@ -271,7 +322,7 @@ struct gw_handle {
         HIPCHECK(hipStreamSynchronize(stream));
         HIPCHECK(hipFree(tv.base));
         tv = nt;
-        table_bytes = (size_t)(nt.cap + 1) * (size_t)nt.stride_w * 8;
+        table_bytes = pane_table_bytes(nt);
         stats.rehashes++;
         if ((rc = refresh())) return rc;
         if (h_st->flags & GW_DF_TABLE_FULL) return fail(GW_E_OOM, "state table rehash overflow");
@@ -480,24 +531,46 @@ struct gw_handle {
         a.t = tv;
         a.d_key = dk[cur]; a.d_pane = dp[cur]; a.d_a0 = da0[cur]; a.d_a1 = da1[cur];
         a.st = d_st;
-        bool preagg;
-        if (cfg.flags & GW_FLAG_FORCE_LDS_PREAGG) preagg = true;
-        else if (cfg.flags & GW_FLAG_NO_LDS_PREAGG) preagg = false;
-        else {
-            const int64_t keys = std::max<int64_t>((int64_t)h_st->used_slots, cfg.capacity_hint > 0 ? 0 : 1);
-            const int64_t est = h_st->used_slots ? (int64_t)h_st->used_slots : cfg.capacity_hint;
-            preagg = est > 0 && nrec >= 8 * est;
-            (void)keys;
+        // path: LDS pre-aggregation when the batch repeats few keys many times; region
+        // bucketing when the batch is large against the table (its streaming passes cost
+        // ~48 B per slot, the direct path ~300 B of scattered traffic per record);
+        // otherwise direct atomics.
+        int path = 0;
+        const int64_t est = h_st->used_slots ? (int64_t)h_st->used_slots : cfg.capacity_hint;
+        if (cfg.flags & GW_FLAG_FORCE_LDS_PREAGG) path = 1;
+        else if (!(cfg.flags & GW_FLAG_NO_LDS_PREAGG) && est > 0 && nrec >= 8 * est) path = 1;
+        if (path == 0 && tv.nreg <= kRgnMaxRegions && !(cfg.flags & GW_FLAG_NO_REGION)) {
+            const bool big = nrec >= region_min_batch && nrec * 8 >= tv.cap;
+            if (big || (cfg.flags & GW_FLAG_FORCE_REGION)) path = 2;
         }
-        if (preagg) stats.preagg_batches++;
+        if (path == 1) stats.preagg_batches++;
+        if (path == 2) {
+            if ((rc = ensure_region(nrec))) return rc;
+            int l2 = 0;
+            while (((int64_t)1 << l2) < tv.nreg) ++l2;
+            a.d1_bits = std::min(l2, 7);
+            a.d2_bits = l2 - a.d1_bits;
+            const int64_t tiles1 = region_scratch_tiles(nrec);
+            a.p_counts1 = p_counts;
+            a.p_counts2 = p_counts + tiles1 * kPartBuckets;
+            a.p1_base = p_small;
+            a.p2_tile0 = p_small + kPartBuckets + 1;
+            a.rg_base = rg_base;
+            a.e_key = e_col[0]; a.e_a0 = e_col[1]; a.e_a1 = e_col[2];
+            a.p1_key = e_col[3]; a.p1_a0 = e_col[4]; a.p1_a1 = e_col[5];
+            a.e_pos = e_pos[0]; a.p1_pos = e_pos[1];
+            a.batch_occ = d_tmp + 1;
+            a.ring_fresh = ~occ;
+            HIPCHECK(hipMemsetAsync(d_tmp + 1, 0, 8, stream));
+        }
         if (timing) {
             auto ev = t_ingest.get();
             HIPCHECK(hipEventRecord(ev.first, stream));
-            HIPCHECK(launch_ingest(a, preagg, ingest_unroll, stream));
+            HIPCHECK(launch_ingest(a, path, ingest_unroll, stream));
             HIPCHECK(hipEventRecord(ev.second, stream));
             t_ingest.pending.push_back(ev);
         } else {
-            HIPCHECK(launch_ingest(a, preagg, ingest_unroll, stream));
+            HIPCHECK(launch_ingest(a, path, ingest_unroll, stream));
         }
         stats.events_in += nrec;
         stats.batches++;
@@ -599,6 +672,7 @@ int gw_create(const gw_config* cfg, gw_handle** out) {
     if (!h) { g_create_error = "out of host memory"; return GW_E_OOM; }
     h->cfg = *cfg;
     if (const char* u = getenv("GW_INGEST_UNROLL")) h->ingest_unroll = atoi(u);
+    if (const char* u = getenv("GW_REGION_MIN_BATCH")) h->region_min_batch = atoll(u);
     if (h->cfg.max_parallelism <= 0) h->cfg.max_parallelism = 128;
     if (h->cfg.parallelism <= 0) h->cfg.parallelism = 1;
     if (h->cfg.max_batch <= 0) h->cfg.max_batch = 1 << 20;
@@ -622,6 +696,7 @@ int gw_create(const gw_config* cfg, gw_handle** out) {
     const int words = cell_words(agg);
     h->tv.agg = agg;
     h->tv.words = words;
+    h->tv.has_mask = !(agg == GW_COUNT || agg == GW_AVG_I64 || agg == GW_AVG_F64);
     int64_t hint = cfg->capacity_hint > 0 ? cfg->capacity_hint : 1 << 16;
     int64_t cap = 1024;
     while ((double)cap * 0.7 < (double)hint) cap *= 2;
@@ -650,13 +725,12 @@ int gw_create(const gw_config* cfg, gw_handle** out) {
     if (R > kMaxRing) R = kMaxRing;
     h->R = R;
     h->tv.ring = R;
-    h->tv.stride_w = stride_w;
     h->div = make_udiv((uint64_t)h->g);
     h->fired_k = h->k_for_wm(INT64_MIN) + 1;
     h->B = h->fired_k * h->m;
     rc = h->alloc_table(h->tv, cap);
     if (rc) return bail(rc, h->err);
-    h->table_bytes = (size_t)(cap + 1) * (size_t)stride_w * 8;
+    h->table_bytes = gw_handle::pane_table_bytes(h->tv);
     rc = h->ensure_deferred(1 << 16);
     if (rc) return bail(rc, h->err);
     if ((e = hipStreamSynchronize(h->stream)) != hipSuccess)
@@ -675,6 +749,11 @@ int gw_destroy(gw_handle* h) {
     }
     if (h->o_key) { hipFree(h->o_key); hipFree(h->o_start); hipFree(h->o_end); hipFree(h->o_res); }
     if (h->h_stage) { hipHostFree(h->h_stage); hipFree(h->d_stage); hipFree(h->d_hash_stage); }
+    if (h->p_counts) hipFree(h->p_counts);
+    if (h->p_small) hipFree(h->p_small);
+    if (h->rg_base) hipFree(h->rg_base);
+    for (auto p : h->e_col) if (p) hipFree(p);
+    for (auto p : h->e_pos) if (p) hipFree(p);
     if (h->d_st) hipFree(h->d_st);
     if (h->d_tmp) hipFree(h->d_tmp);
     if (h->h_st) hipHostFree(h->h_st);

@@ -308,6 +308,25 @@ __global__ void __launch_bounds__(256) k_sess_rewiden(TableView o, TableView n) 
     }
 }
 
+// Re-hash slots with in-flight sessions into a fresh table (dead keys dropped).
+__global__ void __launch_bounds__(256) k_sess_rehash(TableView o, TableView n, DevStatus* st) {
+    unsigned long long ins = 0, flags = 0;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i <= o.cap; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t* s = slot_ptr(o, i);
+        if (s[1] == 0) continue;
+        const int64_t key = i == o.cap ? kEmptyKey : s[0];
+        bool inserted;
+        const int64_t j = find_or_insert(n, key, inserted);
+        if (j < 0) { flags |= GW_DF_TABLE_FULL; continue; }
+        ins += inserted;
+        int64_t* d = slot_ptr(n, j);
+        const int cnt = (int)s[1];
+        d[1] = cnt;
+        for (int w = 0; w < cnt * o.words; ++w) d[2 + w] = s[2 + w];
+    }
+    block_commit(st, 0, ins, flags, 0);
+}
+
 __global__ void __launch_bounds__(256) k_sess_init(TableView t) {
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i <= t.cap; i += (int64_t)gridDim.x * blockDim.x) {
         int64_t* s = slot_ptr(t, i);
@@ -491,7 +510,8 @@ static int rehash_sess(SessionState* s, int64_t new_cap, std::string& err) {
     int rc = alloc_sess_table(s, nt, new_cap, s->tv.ring, err);
     if (rc) return rc;
     SCHECK(launch_status_set(s->d_st, 0, 0, 1, s->stream));  // zero sh[].ins (used slots)
-    SCHECK(launch_rehash(s->tv, nt, s->d_st, s->stream));
+    hipLaunchKernelGGL(k_sess_rehash, dim3(grid_of(s->tv.cap + 1)), dim3(256), 0, s->stream, s->tv, nt, s->d_st);
+    SCHECK(hipGetLastError());
     SCHECK(hipStreamSynchronize(s->stream));
     hipFree(s->tv.base);
     s->tv = nt;

@@ -109,6 +109,8 @@ typedef struct gw_config {
 #define GW_FLAG_FORCE_LDS_PREAGG   1 /* always pre-aggregate in LDS before the HBM RMW  */
 #define GW_FLAG_NO_LDS_PREAGG      2 /* never pre-aggregate in LDS                       */
 #define GW_FLAG_CHECK_KEY_GROUPS   4 /* reject keys outside this subtask's key groups    */
+#define GW_FLAG_FORCE_REGION       8 /* always use the region-bucketed ingest path      */
+#define GW_FLAG_NO_REGION         16 /* never use the region-bucketed ingest path       */
 
 typedef struct gw_handle gw_handle;
 

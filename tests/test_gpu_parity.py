@@ -104,14 +104,59 @@ def test_random_stream_vs_oracle(oracle_lib, cfg, agg):
     kw = dict(cfg, agg=agg)
     keys, ts, vals, batches = random_stream(seed=zlib.crc32(f"{agg}{cfg}".encode()) & 0xffff, n=20000, num_keys=300,
                                             n_batches=25, agg=agg)
-    g, glate, _ = run_gpu(kw, keys, ts, vals, batches)
+    g, glate, _ = run_gpu(kw, keys, ts, vals, batches, flags=N.FLAG_NO_REGION)
+    o, olate = run_oracle(oracle_lib, kw, keys, ts, vals, batches)
+    assert glate == olate == 0
+    assert _cmp(g, o, agg) == []
+
+
+# Region-bucketed ingest (k_rgn_hist/scatter/apply): forced on every batch, with more
+# keys than one region holds so several regions and the LDS probe path are exercised.
+@pytest.mark.parametrize("agg", ALL_AGGS)
+@pytest.mark.parametrize("cfg", CONFIGS[:-1], ids=lambda c: "-".join(str(v) for v in c.values()))
+def test_region_path_vs_oracle(oracle_lib, cfg, agg):
+    kw = dict(cfg, agg=agg)
+    keys, ts, vals, batches = random_stream(seed=zlib.crc32(f"rgn{agg}{cfg}".encode()) & 0xffff, n=60000,
+                                            num_keys=20000, n_batches=12, ts_step=1, agg=agg)
+    g, glate, _ = run_gpu(kw, keys, ts, vals, batches, flags=N.FLAG_FORCE_REGION, capacity_hint=20000)
+    o, olate = run_oracle(oracle_lib, kw, keys, ts, vals, batches)
+    assert glate == olate == 0
+    assert _cmp(g, o, agg) == []
+
+
+@pytest.mark.parametrize("size,slide", [(1000, 50), (3000, 100)])
+@pytest.mark.parametrize("flags", [N.FLAG_NO_REGION, N.FLAG_FORCE_REGION], ids=["direct", "region"])
+@pytest.mark.parametrize("agg", ["sum_i64", "max_f64"])
+def test_long_pane_rings(oracle_lib, size, slide, flags, agg):
+    """size/slide = 20 and 30: pane rings of 22 and 38 cells, i.e. 4- and 8-byte
+    presence masks per slot (Q5's ring of 6 uses 1 byte)."""
+    kw = dict(assigner="sliding", size=size, slide=slide, agg=agg)
+    keys, ts, vals, batches = random_stream(seed=size + slide, n=30000, num_keys=2000, n_batches=10, ts_step=1,
+                                            agg=agg)
+    g, glate, _ = run_gpu(kw, keys, ts, vals, batches, flags=flags, capacity_hint=4000)
+    o, olate = run_oracle(oracle_lib, kw, keys, ts, vals, batches)
+    assert glate == olate == 0
+    assert _cmp(g, o, agg) == []
+
+
+@pytest.mark.parametrize("agg", ["count", "sum_i64", "min_f64", "avg_f64", "avg_i64"])
+@pytest.mark.parametrize("cfg", CONFIGS[:-1], ids=lambda c: "-".join(str(v) for v in c.values()))
+def test_region_two_pass_partition_vs_oracle(oracle_lib, cfg, agg):
+    """A table of 512 regions: the records are bucketed in two LDS-sorted passes
+    (7 + 2 region bits) before k_rgn_apply."""
+    kw = dict(cfg, agg=agg)
+    keys, ts, vals, batches = random_stream(seed=zlib.crc32(f"rgn2{agg}{cfg}".encode()) & 0xffff, n=80000,
+                                            num_keys=50000, n_batches=8, ts_step=1, agg=agg)
+    g, glate, stats = run_gpu(kw, keys, ts, vals, batches, flags=N.FLAG_FORCE_REGION, capacity_hint=600000)
+    assert stats["table_capacity"] == 1 << 20
     o, olate = run_oracle(oracle_lib, kw, keys, ts, vals, batches)
     assert glate == olate == 0
     assert _cmp(g, o, agg) == []
 
 
 @pytest.mark.parametrize("cfg", CONFIGS, ids=lambda c: "-".join(str(v) for v in c.values()))
-def test_late_records_dropped_like_reference(oracle_lib, cfg):
+@pytest.mark.parametrize("flags", [0, N.FLAG_FORCE_REGION], ids=["auto", "region"])
+def test_late_records_dropped_like_reference(oracle_lib, cfg, flags):
     """Disorder larger than the watermark lag: some records are late (isWindowLate /
     isElementLate, WindowOperator.java:609-624) and are dropped and counted; sessions
     with late records take the arrival-order replay path."""
@@ -119,7 +164,7 @@ def test_late_records_dropped_like_reference(oracle_lib, cfg):
     disorder = max(2500, 3 * cfg.get("size", 0))  # late = beyond the oldest unfired window
     keys, ts, vals, batches = random_stream(seed=11, n=20000, num_keys=50, n_batches=40, disorder=disorder,
                                             wm_lag=200, agg="sum_i64")
-    g, glate, _ = run_gpu(kw, keys, ts, vals, batches)
+    g, glate, _ = run_gpu(kw, keys, ts, vals, batches, flags=flags)
     o, olate = run_oracle(oracle_lib, kw, keys, ts, vals, batches)
     assert olate > 0
     assert glate == olate
@@ -127,7 +172,8 @@ def test_late_records_dropped_like_reference(oracle_lib, cfg):
 
 
 @pytest.mark.parametrize("cfg", CONFIGS[:-1], ids=lambda c: "-".join(str(v) for v in c.values()))
-def test_far_future_records_and_watermark_jumps(oracle_lib, cfg):
+@pytest.mark.parametrize("flags", [0, N.FLAG_FORCE_REGION], ids=["auto", "region"])
+def test_far_future_records_and_watermark_jumps(oracle_lib, cfg, flags):
     """Records far ahead of the pane ring are parked and merged when their windows
     come up; big watermark jumps fire many windows at once."""
     kw = dict(cfg, agg="count")
@@ -137,7 +183,7 @@ def test_far_future_records_and_watermark_jumps(oracle_lib, cfg):
     ts = rng.integers(0, 2_000_000, n).astype(np.int64)  # unordered over a wide span
     vals = np.zeros(n, np.int64)
     batches = [(0, 2000, -1), (2000, 4000, 100_000), (4000, 6000, 1_500_000)]
-    g, glate, _ = run_gpu(kw, keys, ts, vals, batches)
+    g, glate, _ = run_gpu(kw, keys, ts, vals, batches, flags=flags)
     o, olate = run_oracle(oracle_lib, kw, keys, ts, vals, batches)
     assert glate == olate
     assert compare(g, o, False) == []
@@ -168,10 +214,13 @@ def test_sessions_beyond_inline_limit_fail_loudly():
     op.close()
 
 
-def test_table_growth(oracle_lib):
+@pytest.mark.parametrize("flags", [N.FLAG_NO_REGION, N.FLAG_FORCE_REGION], ids=["direct", "region"])
+def test_table_growth(oracle_lib, flags):
+    """Far more keys than the capacity hint: probes / regions fill, records are parked,
+    the table re-hashes to a larger one and the parked records are merged back."""
     kw = dict(assigner="sliding", size=1000, slide=500, agg="sum_i64")
     keys, ts, vals, batches = random_stream(seed=2, n=200000, num_keys=150000, n_batches=10, agg="sum_i64")
-    g, _, stats = run_gpu(kw, keys, ts, vals, batches, capacity_hint=16)
+    g, _, stats = run_gpu(kw, keys, ts, vals, batches, capacity_hint=16, flags=flags)
     o, _ = run_oracle(oracle_lib, kw, keys, ts, vals, batches)
     assert stats["rehashes"] > 0
     assert compare(g, o, False) == []
@@ -189,7 +238,8 @@ def test_lds_preaggregation_low_cardinality(oracle_lib, agg, flags):
     assert _cmp(g, o, agg) == []
 
 
-def test_special_keys_and_timestamps(oracle_lib):
+@pytest.mark.parametrize("flags", [N.FLAG_NO_REGION, N.FLAG_FORCE_REGION], ids=["direct", "region"])
+def test_special_keys_and_timestamps(oracle_lib, flags):
     """Long.MIN_VALUE (the table's empty marker) and Long.MAX_VALUE as keys, negative
     timestamps, duplicates."""
     kw = dict(assigner="sliding", size=300, slide=100, offset=-30, agg="sum_i64")
@@ -197,7 +247,7 @@ def test_special_keys_and_timestamps(oracle_lib):
     ts = np.array([-1000, -999, -1, 0, -950, 5, 1], np.int64)
     vals = np.array([1, 2, 3, 4, 5, 6, 7], np.int64)
     batches = [(0, 4, -2000), (4, 7, -500)]
-    g, _, _ = run_gpu(kw, keys, ts, vals, batches)
+    g, _, _ = run_gpu(kw, keys, ts, vals, batches, flags=flags)
     o, _ = run_oracle(oracle_lib, kw, keys, ts, vals, batches)
     assert compare(g, o, False) == []
 
