@@ -187,8 +187,8 @@ struct EvictArgs {
 };
 
 constexpr int kPartTile = 4096;     // records per partition block (LDS-sorted)
-constexpr int kPartBuckets = 128;   // buckets per partition pass (<= 7 region bits)
-constexpr int kRgnMaxRegions = 16384;
+constexpr int kPartBuckets = 256;   // buckets per partition pass (<= 8 region bits)
+constexpr int kRgnMaxRegions = 65536;
 
 hipError_t launch_table_init(const PaneTable& t, hipStream_t s);
 // path: 0 direct atomics, 1 LDS pre-aggregation, 2 region (hist + scatter + apply)

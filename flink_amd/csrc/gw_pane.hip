@@ -304,7 +304,7 @@ __global__ void __launch_bounds__(256) k_ingest_preagg(IngestArgs a) {
 // region path
 // ---------------------------------------------------------------------------
 // In-ring records are bucketed by table region (the top log2nreg bits of the key
-// hash) in at most two stable-free counting passes of <= 128 buckets each: pass 1 on
+// hash) in at most two counting passes of <= 256 buckets each: pass 1 on
 // the top d1 region bits, pass 2 on the remaining d2 bits inside each pass-1 bucket.
 // Every pass sorts its 4096-record tile by bucket in LDS first and then writes each
 // bucket's run with consecutive lanes, so all HBM writes are whole-line streams
@@ -315,20 +315,27 @@ constexpr int kPartItems = kPartTile / kPartThreads;
 
 __device__ __forceinline__ int64_t rgn_of(const PaneTable& t, int64_t key) { return pt_key_region(t, slot_hash(key)); }
 
-// Exclusive scan of h[0..nb) (nb <= 128) into out[]; executed by wave 0.
-__device__ __forceinline__ void scan128(const uint32_t* h, uint32_t* out, int nb) {
+// Exclusive scan of h[0..nb) (nb <= 256) into out[]; executed by wave 0.
+__device__ __forceinline__ void scan_buckets(const uint32_t* h, uint32_t* out, int nb) {
     if (threadIdx.x >= 64) return;
     const int l = threadIdx.x;
-    const uint32_t v0 = 2 * l < nb ? h[2 * l] : 0u, v1 = 2 * l + 1 < nb ? h[2 * l + 1] : 0u;
-    const uint32_t s = v0 + v1;
-    uint32_t incl = s;
+    uint32_t v[4], sum = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        v[q] = 4 * l + q < nb ? h[4 * l + q] : 0u;
+        sum += v[q];
+    }
+    uint32_t incl = sum;
     for (int o = 1; o < 64; o <<= 1) {
         const uint32_t up = __shfl_up(incl, o);
         if (l >= o) incl += up;
     }
-    const uint32_t ex = incl - s;
-    if (2 * l < nb) out[2 * l] = ex;
-    if (2 * l + 1 < nb) out[2 * l + 1] = ex + v0;
+    uint32_t ex = incl - sum;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        if (4 * l + q < nb) out[4 * l + q] = ex;
+        ex += v[q];
+    }
 }
 
 // Pass-2 tile g -> its pass-1 bucket and record range (false: g beyond the last tile).
@@ -367,17 +374,35 @@ __global__ void __launch_bounds__(kPartThreads) k_part_hist(IngestArgs a) {
     __syncthreads();
     unsigned long long late = 0, flags = 0, occ = 0;
     const int64_t m2 = ((int64_t)1 << a.d2_bits) - 1;
-    for (int64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
+    // all of this thread's loads first (kPartItems in flight), then the LDS counts
+    int64_t kk[kPartItems], tt[kPartItems];
+#pragma unroll
+    for (int it = 0; it < kPartItems; ++it) {
+        const int64_t i = lo + it * kPartThreads + threadIdx.x;
+        kk[it] = 0;
+        tt[it] = INT64_MIN;
+        if (i < hi) {
+            if constexpr (PASS == 1) {
+                kk[it] = a.key[i];
+                tt[it] = a.ts[i];
+            } else {
+                kk[it] = a.p1_key[i];
+            }
+        }
+    }
+#pragma unroll
+    for (int it = 0; it < kPartItems; ++it) {
+        const int64_t i = lo + it * kPartThreads + threadIdx.x;
+        if (i >= hi) continue;
         if constexpr (PASS == 1) {
-            const int64_t key = a.key[i];
             uint32_t pos = 0;
             int64_t pane = 0, c0 = 0, c1 = 0;
-            if (classify<AGG>(a, a.ts[i], 0, pos, pane, c0, c1, late, flags) == REC_RING && key != kEmptyKey) {
-                atomicAdd(&lh[rgn_of(a.t, key) >> a.d2_bits], 1u);
+            if (classify<AGG>(a, tt[it], 0, pos, pane, c0, c1, late, flags) == REC_RING && kk[it] != kEmptyKey) {
+                atomicAdd(&lh[rgn_of(a.t, kk[it]) >> a.d2_bits], 1u);
                 occ |= 1ull << pos;
             }
         } else {
-            atomicAdd(&lh[rgn_of(a.t, a.p1_key[i]) & m2], 1u);
+            atomicAdd(&lh[rgn_of(a.t, kk[it]) & m2], 1u);
         }
     }
     if constexpr (PASS == 1) {  // one device atomic per block (same-address atomics serialise)
@@ -540,7 +565,7 @@ __global__ void __launch_bounds__(kPartThreads) k_part_scatter(IngestArgs a) {
         if (bk[it] >= 0) rank[it] = atomicAdd(&lh[bk[it]], 1u);
     }
     __syncthreads();
-    scan128(lh, ls, nb);
+    scan_buckets(lh, ls, nb);
     __syncthreads();
 #pragma unroll
     for (int it = 0; it < kPartItems; ++it) {
@@ -574,6 +599,10 @@ __device__ __forceinline__ void copy_words(long long* __restrict__ d, const long
     for (int64_t w = threadIdx.x; w < n2; w += blockDim.x) d2[w] = s2[w];
 }
 
+// Records per thread loaded in the prologue together with the region's state, so the
+// two latencies overlap (a region holds ~1200 records of a 10M batch at 8192 regions).
+constexpr int kApplyPre = 4;
+
 template <int AGG>
 __global__ void __launch_bounds__(512) k_rgn_apply(IngestArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -588,8 +617,8 @@ __global__ void __launch_bounds__(512) k_rgn_apply(IngestArgs a) {
     const int64_t MW = pt_mask_words(a.t);       // 0 unless M
     uint8_t* lmask = (uint8_t*)(lkeys + S);
     long long* lcell = lkeys + S + MW;           // [2][S][W]
-    int& s_ins = *(int*)(lcell + 2 * S * W);     // region keys / mask changed
-    int& s_mask = *((int*)(lcell + 2 * S * W) + 1);
+    // dirty 128-B lines of the key and mask arrays (S <= 2048: <= 128 key lines)
+    __shared__ uint32_t s_kdirty[4], s_mdirty[4];
     // the (up to) two pane positions this batch touches
     const unsigned long long bocc = *(volatile unsigned long long*)a.batch_occ;
     const int act0 = bocc ? __ffsll((long long)bocc) - 1 : -1;
@@ -598,6 +627,20 @@ __global__ void __launch_bounds__(512) k_rgn_apply(IngestArgs a) {
     int64_t* gkeys = pt_region(a.t, r);
     int64_t* gmask = gkeys + S;
     const int msh = a.t.mask_shift;
+    // prologue: this thread's first records + the region state, all loads in flight
+    int64_t pk[kApplyPre], p0[kApplyPre], p1[kApplyPre];
+    uint32_t pp[kApplyPre];
+#pragma unroll
+    for (int q = 0; q < kApplyPre; ++q) {
+        const int64_t e = lo + q * (int64_t)blockDim.x + threadIdx.x;
+        pk[q] = 0; p0[q] = 0; p1[q] = 1; pp[q] = 0;
+        if (e < hi) {
+            pk[q] = a.e_key[e];
+            p0[q] = a.e_a0[e];
+            if constexpr (AV) p1[q] = a.e_a1[e];
+            pp[q] = a.e_pos[e];
+        }
+    }
     copy_words(lkeys, (const long long*)gkeys, S);
     if constexpr (M) copy_words((long long*)lmask, (const long long*)gmask, MW);
     for (int ai = 0; ai < 2; ++ai) {
@@ -611,56 +654,85 @@ __global__ void __launch_bounds__(512) k_rgn_apply(IngestArgs a) {
             copy_words(dst, (const long long*)pt_cell(a.t, r << a.t.log2S, p), S * W);
         }
     }
-    if (threadIdx.x == 0) { s_ins = 0; s_mask = 0; }
+    if (threadIdx.x < 4) { s_kdirty[threadIdx.x] = 0; s_mdirty[threadIdx.x] = 0; }
     __syncthreads();
     unsigned long long ins = 0, flags = 0;
-    for (int64_t e0 = lo; e0 < hi; e0 += blockDim.x) {
+    auto apply_one = [&](int64_t key, int64_t c0, int64_t c1, uint32_t pos, int64_t& pane) -> bool {
+        int64_t j = pt_home(a.t, slot_hash(key));
+        int64_t found = -1;
+        for (int64_t p = 0; p < S; ++p) {
+            const long long k = lkeys[j];
+            if (k == key) { found = j; break; }
+            if (k == kEmptyKey) {
+                const unsigned long long prev = atomicCAS((unsigned long long*)&lkeys[j],
+                                                          (unsigned long long)kEmptyKey, (unsigned long long)key);
+                if (prev == (unsigned long long)kEmptyKey) {
+                    found = j;
+                    ins++;
+                    atomicOr(&s_kdirty[j >> 9], 1u << ((j >> 4) & 31));
+                    break;
+                }
+                if ((int64_t)prev == key) { found = j; break; }
+            }
+            j = (j + 1) & (S - 1);
+        }
+        if (found < 0) {  // region full: park the record, the host grows the table
+            flags |= GW_DF_TABLE_FULL;
+            const int64_t rel = ((int64_t)pos - a.b_pos + a.t.ring) % a.t.ring;
+            pane = a.p_late + (int64_t)a.delta + rel;
+            return true;
+        }
+        const int ai = (int)pos == act0 ? 0 : ((int)pos == act1 ? 1 : -1);
+        if (ai >= 0) {
+            long long* c = lcell + ((int64_t)ai * S + found) * W;
+            lds_cell_add<AGG>(c, c + (W == 2 ? 1 : 0), c0, c1);
+        } else {  // a third pane in one batch: device atomics on this region's cells
+            cell_atomic<AGG>(pt_cell(a.t, (r << a.t.log2S) + found, (int)pos), c0, c1);
+        }
+        if constexpr (M) {
+            if (mask_set_bit(lmask, found, msh, pos)) {
+                const int64_t line = (found << msh) >> 7;
+                atomicOr(&s_mdirty[line >> 5], 1u << (line & 31));
+            }
+        }
+        return false;
+    };
+#pragma unroll
+    for (int q = 0; q < kApplyPre; ++q) {
+        const int64_t e = lo + q * (int64_t)blockDim.x + threadIdx.x;
+        int64_t pane = 0;
+        const bool defer = e < hi && apply_one(pk[q], p0[q], p1[q], pp[q], pane);
+        defer_write(a, defer, pk[q], pane, p0[q], p1[q]);
+    }
+    for (int64_t e0 = lo + kApplyPre * (int64_t)blockDim.x; e0 < hi; e0 += blockDim.x) {
         const int64_t e = e0 + threadIdx.x;
         bool defer = false;
-        int64_t key = 0, pane = 0, c0 = 0, c1 = 0;
+        int64_t key = 0, pane = 0, c0 = 0, c1 = 1;
         if (e < hi) {
             key = a.e_key[e];
             c0 = a.e_a0[e];
             if constexpr (AV) c1 = a.e_a1[e];
-            else c1 = 1;
-            const uint32_t pos = a.e_pos[e];
-            int64_t j = pt_home(a.t, slot_hash(key));
-            int64_t found = -1;
-            for (int64_t p = 0; p < S; ++p) {
-                const long long k = lkeys[j];
-                if (k == key) { found = j; break; }
-                if (k == kEmptyKey) {
-                    const unsigned long long prev = atomicCAS((unsigned long long*)&lkeys[j],
-                                                              (unsigned long long)kEmptyKey, (unsigned long long)key);
-                    if (prev == (unsigned long long)kEmptyKey) { found = j; ins++; s_ins = 1; break; }
-                    if ((int64_t)prev == key) { found = j; break; }
-                }
-                j = (j + 1) & (S - 1);
-            }
-            if (found < 0) {  // region full: park the record, the host grows the table
-                flags |= GW_DF_TABLE_FULL;
-                defer = true;
-                const int64_t rel = ((int64_t)pos - a.b_pos + a.t.ring) % a.t.ring;
-                pane = a.p_late + (int64_t)a.delta + rel;
-            } else {
-                const int ai = (int)pos == act0 ? 0 : ((int)pos == act1 ? 1 : -1);
-                if (ai >= 0) {
-                    long long* c = lcell + ((int64_t)ai * S + found) * W;
-                    lds_cell_add<AGG>(c, c + (W == 2 ? 1 : 0), c0, c1);
-                } else {  // a third pane in one batch: device atomics on this region's cells
-                    cell_atomic<AGG>(pt_cell(a.t, (r << a.t.log2S) + found, (int)pos), c0, c1);
-                }
-                if constexpr (M) {
-                    if (mask_set_bit(lmask, found, msh, pos)) s_mask = 1;
-                }
-            }
+            defer = apply_one(key, c0, c1, a.e_pos[e], pane);
         }
         defer_write(a, defer, key, pane, c0, c1);
     }
     __syncthreads();
-    if (s_ins) copy_words((long long*)gkeys, lkeys, S);
+    // write back: dirty 128-B lines of keys / mask, every line of the active pane arrays
+    {
+        const long2* sk = reinterpret_cast<const long2*>(lkeys);
+        long2* dk = reinterpret_cast<long2*>(gkeys);
+        for (int64_t w = threadIdx.x; w < S / 2; w += blockDim.x) {
+            const int64_t line = w >> 3;
+            if (s_kdirty[line >> 5] & (1u << (line & 31))) dk[w] = sk[w];
+        }
+    }
     if constexpr (M) {
-        if (s_mask) copy_words((long long*)gmask, (const long long*)lmask, MW);
+        const long2* sm = reinterpret_cast<const long2*>(lmask);
+        long2* dm = reinterpret_cast<long2*>(gmask);
+        for (int64_t w = threadIdx.x; w < MW / 2; w += blockDim.x) {
+            const int64_t line = w >> 3;
+            if (s_mdirty[line >> 5] & (1u << (line & 31))) dm[w] = sm[w];
+        }
     }
     for (int ai = 0; ai < 2; ++ai) {
         const int p = ai ? act1 : act0;
@@ -914,7 +986,7 @@ hipError_t launch_ingest(const IngestArgs& a, int path, int unroll, hipStream_t 
         const int nb1 = 1 << a.d1_bits;
         const size_t part_lds = (size_t)kPartTile * 8 * (a.t.words == 2 ? 3 : 2) + 2 * kPartTile;
         const int64_t S = pt_S(a.t);
-        const size_t apply_lds = (size_t)(S + pt_mask_words(a.t)) * 8 + (size_t)2 * S * a.t.words * 8 + 16;
+        const size_t apply_lds = (size_t)(S + pt_mask_words(a.t)) * 8 + (size_t)2 * S * a.t.words * 8;
         int64_t* b1 = single ? a.rg_base : a.p1_base;
         // beyond the 64 KB default: opt in (gfx950 has 160 KB of LDS per CU)
 #define L(A)                                                                                                    \

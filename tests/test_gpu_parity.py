@@ -154,6 +154,18 @@ def test_region_two_pass_partition_vs_oracle(oracle_lib, cfg, agg):
     assert _cmp(g, o, agg) == []
 
 
+def test_region_partition_eight_bit_digits(oracle_lib):
+    """2^26 slots = 32768 regions: the two partition passes take 8 + 7 region bits."""
+    kw = dict(assigner="sliding", size=1000, slide=250, agg="sum_i64")
+    keys, ts, vals, batches = random_stream(seed=77, n=50000, num_keys=30000, n_batches=5, ts_step=1,
+                                            agg="sum_i64")
+    g, glate, stats = run_gpu(kw, keys, ts, vals, batches, flags=N.FLAG_FORCE_REGION, capacity_hint=40_000_000)
+    assert stats["table_capacity"] == 1 << 26
+    o, olate = run_oracle(oracle_lib, kw, keys, ts, vals, batches)
+    assert glate == olate == 0
+    assert compare(g, o, False) == []
+
+
 @pytest.mark.parametrize("cfg", CONFIGS, ids=lambda c: "-".join(str(v) for v in c.values()))
 @pytest.mark.parametrize("flags", [0, N.FLAG_FORCE_REGION], ids=["auto", "region"])
 def test_late_records_dropped_like_reference(oracle_lib, cfg, flags):
