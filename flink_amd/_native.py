@@ -32,10 +32,11 @@ FLAG_NO_LDS_PREAGG = 2
 FLAG_CHECK_KEY_GROUPS = 4
 FLAG_FORCE_REGION = 8
 FLAG_NO_REGION = 16
+FLAG_NO_BUFFER = 32
 
 EXPORTS = [
     "gw_create", "gw_destroy", "gw_last_error", "gw_abi_version", "gw_ingest", "gw_ingest_device",
-    "gw_advance_watermark", "gw_end_input", "gw_pending_rows", "gw_drain", "gw_rows_device",
+    "gw_advance_watermark", "gw_flush", "gw_end_input", "gw_pending_rows", "gw_drain", "gw_rows_device",
     "gw_clear_rows", "gw_late_dropped", "gw_get_stats", "gw_synchronize", "gw_stream",
     "gw_kernel_time_ms", "gw_enable_kernel_timing", "gw_java_long_hash", "gw_murmur_hash",
     "gw_key_group_for_hash", "gw_operator_for_key_group", "gw_default_max_parallelism",
@@ -68,7 +69,7 @@ class GwConfig(ctypes.Structure):
 class GwStats(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int64) for n in (
         "events_in", "late_dropped", "rows_fired", "live_keys", "table_capacity", "table_bytes",
-        "deferred", "batches", "fires", "rehashes", "preagg_batches", "session_merges")]
+        "deferred", "batches", "fires", "rehashes", "preagg_batches", "session_merges", "applies")]
 
     def as_dict(self):
         return {n: getattr(self, n) for n, _ in self._fields_}
@@ -108,6 +109,7 @@ def lib() -> ctypes.CDLL:
         "gw_ingest": (c_int, [p, i64, p, p, p, p]),
         "gw_ingest_device": (c_int, [p, i64, p, p, p, p, p]),
         "gw_advance_watermark": (c_int, [p, i64, P64]),
+        "gw_flush": (c_int, [p]),
         "gw_end_input": (c_int, [p, P64]),
         "gw_pending_rows": (c_int, [p, P64]),
         "gw_drain": (c_int, [p, p, p, p, p, i64, P64]),

@@ -42,7 +42,8 @@ struct DevStatus {
     unsigned long long preagg_cells;// host view: sum of sh[].cells
     unsigned long long merges;      // host view: sum of sh[].merges (session merges, M_b)
     unsigned long long overflow;    // session segments that did not fit (retry list length)
-    unsigned long long pad[6];
+    unsigned long long spills;      // region apply: records left in the buffer by full regions
+    unsigned long long pad[5];
     ShardCtr sh[kShards];
 };
 #define GW_DF_NO_TS 1ull

@@ -124,25 +124,37 @@ struct IngestArgs {
     int64_t* d_a0;
     int64_t* d_a1;
     DevStatus* st;
-    // region path (k_part_*, k_rgn_apply)
+    // region path (k_rgn_p1 / k_rgn_plan* / k_rgn_p2 / k_rgn_apply, gw_pane.hip)
     int32_t d1_bits;       // region = (pass-1 bucket << d2_bits) | pass-2 bucket
-    int32_t d2_bits;       // 0: one pass (pass 1 writes e_* directly)
-    uint32_t* p_counts1;   // [tiles1][kPartBuckets] per-tile histogram -> column-exclusive offsets
-    uint32_t* p_counts2;   // [tiles2][kPartBuckets]
-    int64_t* p1_base;      // [2^d1 + 1] pass-1 bucket starts
-    int64_t* p2_tile0;     // [2^d1 + 1] first pass-2 tile of each pass-1 bucket
-    int64_t* p1_key;       // pass-1 output
+    int32_t d2_bits;       // 0: single-pass table (apply reads the P1 tiles directly)
+    int64_t tile0;         // P1: buffer tile of this batch's first tile
+    int64_t ntiles;        // flush: buffer tiles in use
+    int64_t ngroups;       // flush: P1 tile groups (= P2 blocks per bucket)
+    int32_t p2_group;      // flush: P1 tiles per group (G)
+    int64_t* p1_key;       // P1 output: tile t at [t * kPartTile, ...), sorted by bucket
     int64_t* p1_a0;
     int64_t* p1_a1;
     uint8_t* p1_pos;
-    int64_t* rg_base;      // [nreg + 1] region bucket starts
-    int64_t* e_key;        // region-bucketed records
+    uint32_t* p1_row;      // [tile][kPartBuckets] (start << 16 | count) per bucket
+    uint32_t* p2_desc;     // [bucket][tile]  the same descriptors, transposed
+    int64_t* p2_off;       // [bucket * ngroups + group] sizes -> output starts within the bucket
+    int64_t* p2_roff;      // [bucket * ngroups + group] rounds -> first round within the bucket
+    int64_t* rbeg;         // [nb1 + 1] first P2 round of each bucket
+    int64_t* bk_off;       // [nb1 + 1] first P2 output record of each bucket
+    int64_t* e_key;        // P2 output, bucket-major, rounds sorted by region
     int64_t* e_a0;
     int64_t* e_a1;
     uint8_t* e_pos;
-    unsigned long long* batch_occ;  // ring positions this batch touches (for k_rgn_apply)
+    uint32_t* r_row;       // [round][kPartBuckets] (start << 16 | count) per region of the bucket
+    int64_t* r_base;       // [round] first record of the round
+    unsigned long long* batch_occ;  // ring positions the buffered records touch (for k_rgn_apply)
     uint64_t ring_fresh;            // ring positions holding only identities (not in occ)
 };
+
+constexpr int kPartTile = 4096;     // records per P1 tile / P2 round (LDS-sorted)
+constexpr int kPartBuckets = 256;   // descriptor row width (<= 8 region bits per pass)
+constexpr int kRgnMaxRegions = 65536;
+constexpr int kMaxGroup = 256;      // P1 tiles per P2 block (G = 7/8 of the pass-1 buckets)
 
 struct MergeArgs {
     const int64_t* i_key;
@@ -186,14 +198,16 @@ struct EvictArgs {
     DevStatus* st;
 };
 
-constexpr int kPartTile = 4096;     // records per partition block (LDS-sorted)
-constexpr int kPartBuckets = 256;   // buckets per partition pass (<= 8 region bits)
-constexpr int kRgnMaxRegions = 65536;
-
 hipError_t launch_table_init(const PaneTable& t, hipStream_t s);
-// path: 0 direct atomics, 1 LDS pre-aggregation, 2 region (hist + scatter + apply)
+// path: 0 direct atomics, 1 LDS pre-aggregation (the region path has its own launchers)
 hipError_t launch_ingest(const IngestArgs& a, int path, int unroll, hipStream_t s);
-int64_t region_scratch_tiles(int64_t n);  // pass-1 tiles; pass 2 uses <= this + kPartBuckets
+// region path: P1 over one batch (a.n records -> buffer tiles from a.tile0) ...
+hipError_t launch_region_p1(const IngestArgs& a, hipStream_t s);
+// ... and, per flush, plan + P2 (two-pass tables) + apply over a.ntiles buffer tiles
+hipError_t launch_region_flush(const IngestArgs& a, hipStream_t s);
+// ... and after a flush that filled regions: its spilled records -> the deferred list
+hipError_t launch_region_collect(const IngestArgs& a, hipStream_t s);
+int region_group(int d1_bits);  // G: P1 tiles per P2 block
 hipError_t launch_merge_deferred(const MergeArgs& a, hipStream_t s);
 hipError_t launch_deferred_min(const int64_t* pane, int64_t n, DevStatus* st, hipStream_t s);
 hipError_t launch_fire(const FireArgs& a, hipStream_t s);

@@ -301,19 +301,28 @@ __global__ void __launch_bounds__(256) k_ingest_preagg(IngestArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// region path
+// region path: tile-local two-level bucketing, then one workgroup per region
 // ---------------------------------------------------------------------------
-// In-ring records are bucketed by table region (the top log2nreg bits of the key
-// hash) in at most two counting passes of <= 256 buckets each: pass 1 on
-// the top d1 region bits, pass 2 on the remaining d2 bits inside each pass-1 bucket.
-// Every pass sorts its 4096-record tile by bucket in LDS first and then writes each
-// bucket's run with consecutive lanes, so all HBM writes are whole-line streams
-// (single scattered 8-B stores turn into partial-line read-modify-writes in HBM3E and
-// were measured at ~30 G stores/s).  k_rgn_apply then owns one region per workgroup.
+// In-ring records are bucketed by table region (the top log2nreg bits of the key hash)
+// without histogram passes:
+//   P1  (per watermark batch) one block per 4096-record tile classifies its records,
+//       sorts them in LDS by pass-1 bucket (top d1 region bits) and writes the tile
+//       back contiguously, plus one descriptor row: per bucket (start << 16 | count).
+//   P2  (per flush, two-pass tables) block (b1, j) gathers bucket b1's runs from a group
+//       of G P1 tiles, sorts them by the remaining d2 region bits in LDS and writes
+//       rounds of <= 4096 records, each with a descriptor row of its own.  Two small
+//       plan kernels place the blocks' outputs (bucket-major) and their rounds.
+//   apply  one workgroup per region gathers its runs (from the P2 rounds of its bucket,
+//       or straight from the P1 tiles of a single-pass table) and applies them to an
+//       LDS copy of the region's keys / mask / active pane arrays.
+// Every HBM access is a contiguous run: whole tiles, runs of ~32-64 records, and the
+// region state.  P1 segments of several watermark batches accumulate in the buffer and
+// P2 + apply run once per fire (gw_runtime.cpp flush_buffer).
 constexpr int kPartThreads = 512;
 constexpr int kPartItems = kPartTile / kPartThreads;
 
 __device__ __forceinline__ int64_t rgn_of(const PaneTable& t, int64_t key) { return pt_key_region(t, slot_hash(key)); }
+__device__ __forceinline__ uint32_t desc_pack(uint32_t start, uint32_t cnt) { return (start << 16) | cnt; }
 
 // Exclusive scan of h[0..nb) (nb <= 256) into out[]; executed by wave 0.
 __device__ __forceinline__ void scan_buckets(const uint32_t* h, uint32_t* out, int nb) {
@@ -338,256 +347,323 @@ __device__ __forceinline__ void scan_buckets(const uint32_t* h, uint32_t* out, i
     }
 }
 
-// Pass-2 tile g -> its pass-1 bucket and record range (false: g beyond the last tile).
-__device__ __forceinline__ bool pass2_tile(const IngestArgs& a, int64_t g, int& b1, int64_t& lo, int64_t& hi) {
-    const int nb1 = 1 << a.d1_bits;
-    if (g >= a.p2_tile0[nb1]) return false;
-    int l = 0, h = nb1 - 1;  // last bucket with tile0 <= g
-    while (l < h) {
-        const int mid = (l + h + 1) >> 1;
-        if (a.p2_tile0[mid] <= g) l = mid;
-        else h = mid - 1;
+// Exclusive block scan of cnt[0..n) (n <= 2 * blockDim.x, blockDim.x = 512) into pre[],
+// pre[n] = total.  Every thread calls it; ends with a barrier.
+__device__ __forceinline__ void block_scan2(const uint32_t* cnt, uint32_t* pre, int n, uint32_t* wsum) {
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const uint32_t a = 2 * t < n ? cnt[2 * t] : 0u, b = 2 * t + 1 < n ? cnt[2 * t + 1] : 0u;
+    uint32_t incl = a + b;
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t up = __shfl_up(incl, o);
+        if (lane >= o) incl += up;
     }
-    b1 = l;
-    lo = a.p1_base[l] + (g - a.p2_tile0[l]) * kPartTile;
-    hi = min(a.p1_base[l + 1], lo + (int64_t)kPartTile);
-    return true;
+    if (lane == 63) wsum[w] = incl;
+    __syncthreads();
+    uint32_t off = 0;
+    for (int q = 0; q < w; ++q) off += wsum[q];
+    const uint32_t ex = off + incl - (a + b);
+    if (2 * t < n) pre[2 * t] = ex;
+    if (2 * t + 1 < n) pre[2 * t + 1] = ex + a;
+    if (t == blockDim.x - 1) pre[n] = off + incl;
+    __syncthreads();
 }
 
-// Histogram of one tile: pass 1 over the input batch (classifying records), pass 2
-// over one pass-1 bucket.  counts[g][b] (stride kPartBuckets).
-template <int AGG, int PASS>
-__global__ void __launch_bounds__(kPartThreads) k_part_hist(IngestArgs a) {
-    __shared__ uint32_t lh[kPartBuckets];
+// Index i of the run holding record e: pre[i] <= e < pre[i + 1] (pre ascending, n runs).
+__device__ __forceinline__ int run_of(const uint32_t* pre, int n, uint32_t e) {
+    int l = 0, h = n - 1;
+    while (l < h) {
+        const int mid = (l + h + 1) >> 1;
+        if (pre[mid] <= e) l = mid;
+        else h = mid - 1;
+    }
+    return l;
+}
+
+// LDS image of one sorted tile: keys, accumulator words, ring positions, buckets.
+struct TileLds {
+    long long* k;
+    long long* a0;
+    long long* a1;
+    uint8_t* pos;
+    uint8_t* bk;
+};
+template <bool AV>
+__device__ __forceinline__ TileLds tile_lds(unsigned char* smem) {
+    TileLds s;
+    s.k = (long long*)smem;
+    s.a0 = s.k + kPartTile;
+    s.a1 = s.a0 + kPartTile;  // AV only
+    s.pos = (uint8_t*)(s.a0 + (AV ? 2 : 1) * kPartTile);
+    s.bk = s.pos + kPartTile;
+    return s;
+}
+
+// P1: one 4096-record tile of the batch -> buffer tile a.tile0 + blockIdx.x.
+template <int AGG>
+__global__ void __launch_bounds__(kPartThreads) k_rgn_p1(IngestArgs a) {
+    constexpr bool AV = AGG == GW_AVG_I64 || AGG == GW_AVG_F64;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const TileLds s = tile_lds<AV>(smem);
+    __shared__ uint32_t lh[kPartBuckets], ls[kPartBuckets];
     __shared__ unsigned long long s_occ;
     const int64_t g = blockIdx.x;
-    int64_t lo, hi;
-    int b1 = 0;
-    if constexpr (PASS == 1) {
-        lo = g * kPartTile;
-        hi = min(a.n, lo + (int64_t)kPartTile);
-    } else {
-        if (!pass2_tile(a, g, b1, lo, hi)) return;
-    }
+    const int64_t lo = g * kPartTile, hi = min(a.n, lo + (int64_t)kPartTile);
+    const int nb = 1 << a.d1_bits;
     for (int b = threadIdx.x; b < kPartBuckets; b += blockDim.x) lh[b] = 0;
     if (threadIdx.x == 0) s_occ = 0;
     __syncthreads();
     unsigned long long late = 0, flags = 0, occ = 0;
-    const int64_t m2 = ((int64_t)1 << a.d2_bits) - 1;
-    // all of this thread's loads first (kPartItems in flight), then the LDS counts
-    int64_t kk[kPartItems], tt[kPartItems];
-#pragma unroll
-    for (int it = 0; it < kPartItems; ++it) {
-        const int64_t i = lo + it * kPartThreads + threadIdx.x;
-        kk[it] = 0;
-        tt[it] = INT64_MIN;
-        if (i < hi) {
-            if constexpr (PASS == 1) {
-                kk[it] = a.key[i];
-                tt[it] = a.ts[i];
-            } else {
-                kk[it] = a.p1_key[i];
-            }
-        }
-    }
-#pragma unroll
-    for (int it = 0; it < kPartItems; ++it) {
-        const int64_t i = lo + it * kPartThreads + threadIdx.x;
-        if (i >= hi) continue;
-        if constexpr (PASS == 1) {
-            uint32_t pos = 0;
-            int64_t pane = 0, c0 = 0, c1 = 0;
-            if (classify<AGG>(a, tt[it], 0, pos, pane, c0, c1, late, flags) == REC_RING && kk[it] != kEmptyKey) {
-                atomicAdd(&lh[rgn_of(a.t, kk[it]) >> a.d2_bits], 1u);
-                occ |= 1ull << pos;
-            }
-        } else {
-            atomicAdd(&lh[rgn_of(a.t, kk[it]) & m2], 1u);
-        }
-    }
-    if constexpr (PASS == 1) {  // one device atomic per block (same-address atomics serialise)
-        occ = wave_ior(occ);
-        if (__lane_id() == 0 && occ) atomicOr(&s_occ, occ);
-    }
-    __syncthreads();
-    if (PASS == 1 && threadIdx.x == 0 && s_occ) atomicOr(a.batch_occ, s_occ);
-    uint32_t* row = (PASS == 1 ? a.p_counts1 : a.p_counts2) + g * kPartBuckets;
-    for (int b = threadIdx.x; b < kPartBuckets; b += blockDim.x) row[b] = lh[b];
-}
-
-// Pass-1 columns: for each bucket (one block) an exclusive scan over the tiles; the
-// bucket total goes to base[b].
-__global__ void __launch_bounds__(256) k_part_cols1(uint32_t* counts, int64_t tiles, int64_t* base) {
-    __shared__ uint32_t part[256];
-    const int b = blockIdx.x;
-    uint32_t carry = 0;
-    for (int64_t c = 0; c < tiles; c += 256) {
-        const int64_t t = c + threadIdx.x;
-        const uint32_t v = t < tiles ? counts[t * kPartBuckets + b] : 0u;
-        part[threadIdx.x] = v;
-        __syncthreads();
-        for (int o = 1; o < 256; o <<= 1) {
-            const uint32_t x = threadIdx.x >= (unsigned)o ? part[threadIdx.x - o] : 0u;
-            __syncthreads();
-            part[threadIdx.x] += x;
-            __syncthreads();
-        }
-        if (t < tiles) counts[t * kPartBuckets + b] = carry + part[threadIdx.x] - v;
-        carry += part[255];
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) base[b] = carry;
-}
-
-// Exclusive scan of base[0..n) in place (one block); base[n] = total.  Pass 1 also
-// lays out the pass-2 tiles: tile0[b] = first tile of bucket b, tile0[n] = tiles.
-__global__ void __launch_bounds__(1024) k_rgn_bases(int64_t* base, int64_t n, int64_t* tile0) {
-    __shared__ int64_t part[1024];
-    const int64_t per = (n + blockDim.x - 1) / blockDim.x;
-    const int64_t lo = threadIdx.x * per, hi = min(n, lo + per);
-    for (int round = 0; round < (tile0 ? 2 : 1); ++round) {
-        int64_t* arr = round ? tile0 : base;
-        if (round) {  // tiles per bucket from the scanned bases
-            for (int64_t i = lo; i < hi; ++i) tile0[i] = (base[i + 1] - base[i] + kPartTile - 1) / kPartTile;
-        }
-        int64_t s = 0;
-        for (int64_t i = lo; i < hi; ++i) s += arr[i];
-        part[threadIdx.x] = s;
-        __syncthreads();
-        for (int o = 1; o < 1024; o <<= 1) {
-            const int64_t v = threadIdx.x >= (unsigned)o ? part[threadIdx.x - o] : 0;
-            __syncthreads();
-            part[threadIdx.x] += v;
-            __syncthreads();
-        }
-        int64_t run = threadIdx.x ? part[threadIdx.x - 1] : 0;
-        for (int64_t i = lo; i < hi; ++i) {
-            const int64_t v = arr[i];
-            arr[i] = run;
-            run += v;
-        }
-        if (threadIdx.x == blockDim.x - 1) arr[n] = part[blockDim.x - 1];
-        __syncthreads();
-    }
-}
-
-// Pass-2 columns: one thread per region, exclusive scan over the tiles of its pass-1
-// bucket; region totals to rg_base[r] (scanned next by k_rgn_bases).
-__global__ void __launch_bounds__(256) k_part_cols2(IngestArgs a) {
-    const int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-    if (r >= a.t.nreg) return;
-    const int64_t b1 = r >> a.d2_bits, s = r & (((int64_t)1 << a.d2_bits) - 1);
-    uint32_t run = 0;
-    for (int64_t g = a.p2_tile0[b1]; g < a.p2_tile0[b1 + 1]; ++g) {
-        uint32_t* c = a.p_counts2 + g * kPartBuckets + s;
-        const uint32_t v = *c;
-        *c = run;
-        run += v;
-    }
-    a.rg_base[r] = run;
-}
-
-// Scatter one tile: classify (pass 1), rank each record inside its bucket with an LDS
-// atomic, place it in LDS in bucket order, then stream every bucket run out with
-// consecutive lanes.  Pass 1 also handles late / parked / sentinel-key records.
-template <int AGG, int PASS>
-__global__ void __launch_bounds__(kPartThreads) k_part_scatter(IngestArgs a) {
-    constexpr bool AV = AGG == GW_AVG_I64 || AGG == GW_AVG_F64;
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    long long* sk = (long long*)smem;
-    long long* sa0 = sk + kPartTile;
-    long long* sa1 = sa0 + kPartTile;                                   // AV only
-    uint8_t* sp = (uint8_t*)(sa0 + (AV ? 2 : 1) * kPartTile);
-    uint8_t* sb = sp + kPartTile;
-    __shared__ uint32_t lh[kPartBuckets], ls[kPartBuckets];
-    __shared__ int64_t lbase[kPartBuckets];
-    const int64_t g = blockIdx.x;
-    int64_t lo, hi;
-    int b1 = 0;
-    if constexpr (PASS == 1) {
-        lo = g * kPartTile;
-        hi = min(a.n, lo + (int64_t)kPartTile);
-    } else {
-        if (!pass2_tile(a, g, b1, lo, hi)) return;
-    }
-    const bool single = a.d2_bits == 0;
-    int64_t* o_key = (PASS == 2 || single) ? a.e_key : a.p1_key;
-    int64_t* o_a0 = (PASS == 2 || single) ? a.e_a0 : a.p1_a0;
-    int64_t* o_a1 = (PASS == 2 || single) ? a.e_a1 : a.p1_a1;
-    uint8_t* o_pos = (PASS == 2 || single) ? a.e_pos : a.p1_pos;
-    const uint32_t* crow = (PASS == 1 ? a.p_counts1 : a.p_counts2) + g * kPartBuckets;
-    const int nb = PASS == 1 ? (1 << a.d1_bits) : (1 << a.d2_bits);
-    for (int b = threadIdx.x; b < kPartBuckets; b += blockDim.x) {
-        lh[b] = 0;
-        if (b < nb) {
-            const int64_t* base = PASS == 1 ? (single ? a.rg_base : a.p1_base) : a.rg_base + ((int64_t)b1 << a.d2_bits);
-            lbase[b] = base[b] + crow[b];
-        }
-    }
-    __syncthreads();
-    unsigned long long late = 0, flags = 0, occ = 0;
-    const int64_t m2 = ((int64_t)1 << a.d2_bits) - 1;
-    int64_t key[kPartItems], c0[kPartItems], c1[kPartItems];
+    int64_t key[kPartItems], ts[kPartItems], val[kPartItems], c0[kPartItems], c1[kPartItems];
     uint32_t pos[kPartItems], rank[kPartItems];
     int bk[kPartItems];
+#pragma unroll
+    for (int it = 0; it < kPartItems; ++it) {  // all loads in flight first
+        const int64_t i = lo + it * kPartThreads + threadIdx.x;
+        key[it] = 0; ts[it] = 0; val[it] = 0;
+        if (i < hi) {
+            key[it] = a.key[i];
+            ts[it] = a.ts[i];
+            if (a.val) val[it] = a.val[i];
+        }
+    }
 #pragma unroll
     for (int it = 0; it < kPartItems; ++it) {
         const int64_t i = lo + it * kPartThreads + threadIdx.x;
         bk[it] = -1;
-        key[it] = 0; c0[it] = 0; c1[it] = 0; pos[it] = 0;
-        if constexpr (PASS == 1) {
-            int st = REC_SKIP;
-            int64_t pane = 0;
-            if (i < hi) {
-                key[it] = a.key[i];
-                st = classify<AGG>(a, a.ts[i], a.val ? a.val[i] : 0, pos[it], pane, c0[it], c1[it], late, flags);
-            }
-            if (st == REC_RING) {
-                if (key[it] == kEmptyKey) {  // sentinel slot: rare, straight atomics
-                    cell_atomic<AGG>(pt_cell(a.t, a.t.cap, pos[it]), c0[it], c1[it]);
-                    mask_set<AGG>(a.t, a.t.cap, pos[it]);
-                    occ |= 1ull << pos[it];
-                } else {
-                    bk[it] = (int)(rgn_of(a.t, key[it]) >> a.d2_bits);
-                    occ |= 1ull << pos[it];
-                }
-            }
-            defer_write(a, st == REC_DEFER, key[it], pane, c0[it], c1[it]);
-        } else {
-            if (i < hi) {
-                key[it] = a.p1_key[i];
-                c0[it] = a.p1_a0[i];
-                if constexpr (AV) c1[it] = a.p1_a1[i];
-                pos[it] = a.p1_pos[i];
-                bk[it] = (int)(rgn_of(a.t, key[it]) & m2);
+        c0[it] = 0; c1[it] = 0; pos[it] = 0;
+        int st = REC_SKIP;
+        int64_t pane = 0;
+        if (i < hi) st = classify<AGG>(a, ts[it], val[it], pos[it], pane, c0[it], c1[it], late, flags);
+        if (st == REC_RING) {
+            occ |= 1ull << pos[it];
+            if (key[it] == kEmptyKey) {  // sentinel slot: rare, straight atomics
+                cell_atomic<AGG>(pt_cell(a.t, a.t.cap, pos[it]), c0[it], c1[it]);
+                mask_set<AGG>(a.t, a.t.cap, pos[it]);
+            } else {
+                bk[it] = (int)(rgn_of(a.t, key[it]) >> a.d2_bits);
             }
         }
+        defer_write(a, st == REC_DEFER, key[it], pane, c0[it], c1[it]);
         if (bk[it] >= 0) rank[it] = atomicAdd(&lh[bk[it]], 1u);
     }
+    occ = wave_ior(occ);
+    if (__lane_id() == 0 && occ) atomicOr(&s_occ, occ);
     __syncthreads();
     scan_buckets(lh, ls, nb);
+    if (threadIdx.x == 0 && s_occ) atomicOr(a.batch_occ, s_occ);
     __syncthreads();
 #pragma unroll
     for (int it = 0; it < kPartItems; ++it) {
         if (bk[it] < 0) continue;
         const uint32_t j = ls[bk[it]] + rank[it];
-        sk[j] = key[it];
-        sa0[j] = c0[it];
-        if constexpr (AV) sa1[j] = c1[it];
-        sp[j] = (uint8_t)pos[it];
-        sb[j] = (uint8_t)bk[it];
+        s.k[j] = key[it];
+        s.a0[j] = c0[it];
+        if constexpr (AV) s.a1[j] = c1[it];
+        s.pos[j] = (uint8_t)pos[it];
     }
     __syncthreads();
     const uint32_t cnt = ls[nb - 1] + lh[nb - 1];
+    const int64_t tile = a.tile0 + g;
+    const int64_t base = tile * kPartTile;
     for (uint32_t j = threadIdx.x; j < cnt; j += blockDim.x) {
-        const int b = sb[j];
-        const int64_t dst = lbase[b] + (int64_t)(j - ls[b]);
-        o_key[dst] = sk[j];
-        o_a0[dst] = sa0[j];
-        if constexpr (AV) o_a1[dst] = sa1[j];
-        o_pos[dst] = sp[j];
+        a.p1_key[base + j] = s.k[j];
+        a.p1_a0[base + j] = s.a0[j];
+        if constexpr (AV) a.p1_a1[base + j] = s.a1[j];
+        a.p1_pos[base + j] = s.pos[j];
     }
-    if constexpr (PASS == 1) block_commit(a.st, late, 0, flags, occ);
+    for (int b = threadIdx.x; b < nb; b += blockDim.x) a.p1_row[tile * kPartBuckets + b] = desc_pack(ls[b], lh[b]);
+    block_commit(a.st, late, 0, flags, occ);
+}
+
+// Plan, step 1 (block j = tile group [j*G, (j+1)*G)): transpose the group's descriptor
+// rows into p2_desc[b][tile] and record each (bucket, group) block's size and rounds.
+constexpr int kColBatch = 16;
+__global__ void __launch_bounds__(256) k_rgn_plan1(IngestArgs a) {
+    const int b = threadIdx.x;
+    const int nb = 1 << a.d1_bits;
+    if (b >= nb) return;
+    const int64_t j = blockIdx.x;
+    const int64_t t0 = j * a.p2_group, t1 = min(a.ntiles, t0 + (int64_t)a.p2_group);
+    uint32_t size = 0;
+    for (int64_t t = t0; t < t1; t += kColBatch) {
+        uint32_t d[kColBatch];
+#pragma unroll
+        for (int q = 0; q < kColBatch; ++q) d[q] = a.p1_row[min(t + q, t1 - 1) * kPartBuckets + b];
+#pragma unroll
+        for (int q = 0; q < kColBatch; ++q) {
+            if (t + q < t1) {
+                a.p2_desc[(int64_t)b * a.ntiles + t + q] = d[q];
+                size += d[q] & 0xffffu;
+            }
+        }
+    }
+    const int64_t k = (int64_t)b * a.ngroups + j;
+    a.p2_off[k] = size;
+    a.p2_roff[k] = (size + kPartTile - 1) / kPartTile;
+}
+
+// Plan, step 2 (block b = pass-1 bucket b): exclusive scans of its blocks' sizes and
+// rounds over the groups (bucket-local); the bucket totals go to bk_off[b] / rbeg[b].
+__global__ void __launch_bounds__(256) k_rgn_plan2(IngestArgs a) {
+    __shared__ int64_t part[2][256];
+    const int64_t b = blockIdx.x;
+    const int64_t G = a.ngroups;
+    const int64_t per = (G + 255) / 256;
+    const int64_t lo = b * G + min(G, threadIdx.x * per), hi = b * G + min(G, (threadIdx.x + 1) * per);
+    int64_t s0 = 0, s1 = 0;
+    // loads in flight together: clamped (unconditional) addresses, values masked after
+    for (int64_t k = lo; k < hi; k += kColBatch) {
+        int64_t v0[kColBatch], v1[kColBatch];
+#pragma unroll
+        for (int q = 0; q < kColBatch; ++q) {
+            const int64_t x = min(k + q, hi - 1);
+            v0[q] = a.p2_off[x];
+            v1[q] = a.p2_roff[x];
+        }
+#pragma unroll
+        for (int q = 0; q < kColBatch; ++q) {
+            if (k + q < hi) { s0 += v0[q]; s1 += v1[q]; }
+        }
+    }
+    part[0][threadIdx.x] = s0;
+    part[1][threadIdx.x] = s1;
+    __syncthreads();
+    for (int o = 1; o < 256; o <<= 1) {
+        const int64_t v0 = threadIdx.x >= (unsigned)o ? part[0][threadIdx.x - o] : 0;
+        const int64_t v1 = threadIdx.x >= (unsigned)o ? part[1][threadIdx.x - o] : 0;
+        __syncthreads();
+        part[0][threadIdx.x] += v0;
+        part[1][threadIdx.x] += v1;
+        __syncthreads();
+    }
+    int64_t r0 = threadIdx.x ? part[0][threadIdx.x - 1] : 0, r1 = threadIdx.x ? part[1][threadIdx.x - 1] : 0;
+    for (int64_t k = lo; k < hi; k += kColBatch) {
+        int64_t v0[kColBatch], v1[kColBatch];
+#pragma unroll
+        for (int q = 0; q < kColBatch; ++q) {
+            const int64_t x = min(k + q, hi - 1);
+            v0[q] = a.p2_off[x];
+            v1[q] = a.p2_roff[x];
+        }
+#pragma unroll
+        for (int q = 0; q < kColBatch; ++q) {
+            if (k + q >= hi) break;
+            a.p2_off[k + q] = r0;
+            a.p2_roff[k + q] = r1;
+            r0 += v0[q];
+            r1 += v1[q];
+        }
+    }
+    if (threadIdx.x == 255) {
+        a.bk_off[b] = part[0][255];
+        a.rbeg[b] = part[1][255];
+    }
+}
+
+// Plan, step 3 (one block): bucket totals -> bucket starts (records bk_off[], rounds
+// rbeg[]), both exclusive with the grand total at [nb].
+__global__ void __launch_bounds__(256) k_rgn_plan3(IngestArgs a) {
+    __shared__ int64_t part[2][256];
+    const int nb = 1 << a.d1_bits;
+    const int b = threadIdx.x;
+    const int64_t v0 = b < nb ? a.bk_off[b] : 0, v1 = b < nb ? a.rbeg[b] : 0;
+    part[0][b] = v0;
+    part[1][b] = v1;
+    __syncthreads();
+    for (int o = 1; o < 256; o <<= 1) {
+        const int64_t x0 = b >= o ? part[0][b - o] : 0, x1 = b >= o ? part[1][b - o] : 0;
+        __syncthreads();
+        part[0][b] += x0;
+        part[1][b] += x1;
+        __syncthreads();
+    }
+    if (b < nb) {
+        a.bk_off[b] = part[0][b] - v0;
+        a.rbeg[b] = part[1][b] - v1;
+    }
+    if (b == 255) {
+        a.bk_off[nb] = part[0][255];
+        a.rbeg[nb] = part[1][255];
+    }
+}
+
+// P2: block (b1, j) -> rounds p2_roff[b1, j] ... of bucket b1, records at p2_off[b1, j].
+template <int AGG>
+__global__ void __launch_bounds__(kPartThreads) k_rgn_p2(IngestArgs a) {
+    constexpr bool AV = AGG == GW_AVG_I64 || AGG == GW_AVG_F64;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const TileLds s = tile_lds<AV>(smem);
+    __shared__ uint32_t lh[kPartBuckets], ls[kPartBuckets];
+    __shared__ uint32_t r_cnt[kMaxGroup], r_pre[kMaxGroup + 1], wsum[8];
+    __shared__ int64_t r_src[kMaxGroup];
+    const int64_t b1 = blockIdx.x / a.ngroups, j = blockIdx.x - b1 * a.ngroups;
+    const int64_t t0 = j * a.p2_group;
+    const int nt = (int)min((int64_t)a.p2_group, a.ntiles - t0);
+    const int nb2 = 1 << a.d2_bits;
+    const int64_t m2 = nb2 - 1;
+    for (int i = threadIdx.x; i < nt; i += blockDim.x) {
+        const uint32_t d = a.p2_desc[b1 * a.ntiles + t0 + i];
+        r_cnt[i] = d & 0xffffu;
+        r_src[i] = (t0 + i) * kPartTile + (d >> 16);
+    }
+    __syncthreads();
+    block_scan2(r_cnt, r_pre, nt, wsum);
+    const uint32_t total = r_pre[nt];
+    const int64_t k = b1 * a.ngroups + j;
+    const int64_t out0 = a.bk_off[b1] + a.p2_off[k], rnd0 = a.rbeg[b1] + a.p2_roff[k];
+    for (uint32_t e0 = 0; e0 < total; e0 += kPartTile) {
+        const uint32_t e1 = min(total, e0 + (uint32_t)kPartTile);
+        for (int b = threadIdx.x; b < kPartBuckets; b += blockDim.x) lh[b] = 0;
+        __syncthreads();
+        int64_t key[kPartItems], c0[kPartItems], c1[kPartItems];
+        uint32_t pos[kPartItems], rank[kPartItems];
+        int bk[kPartItems];
+#pragma unroll
+        for (int it = 0; it < kPartItems; ++it) {
+            const uint32_t e = e0 + it * kPartThreads + threadIdx.x;
+            key[it] = 0; c0[it] = 0; c1[it] = 0; pos[it] = 0;
+            bk[it] = -1;
+            if (e < e1) {
+                const int i = run_of(r_pre, nt, e);
+                const int64_t src = r_src[i] + (e - r_pre[i]);
+                key[it] = a.p1_key[src];
+                c0[it] = a.p1_a0[src];
+                if constexpr (AV) c1[it] = a.p1_a1[src];
+                pos[it] = a.p1_pos[src];
+                bk[it] = 0;
+            }
+        }
+#pragma unroll
+        for (int it = 0; it < kPartItems; ++it) {
+            if (bk[it] < 0) continue;
+            bk[it] = (int)(rgn_of(a.t, key[it]) & m2);
+            rank[it] = atomicAdd(&lh[bk[it]], 1u);
+        }
+        __syncthreads();
+        scan_buckets(lh, ls, nb2);
+        __syncthreads();
+#pragma unroll
+        for (int it = 0; it < kPartItems; ++it) {
+            if (bk[it] < 0) continue;
+            const uint32_t jj = ls[bk[it]] + rank[it];
+            s.k[jj] = key[it];
+            s.a0[jj] = c0[it];
+            if constexpr (AV) s.a1[jj] = c1[it];
+            s.pos[jj] = (uint8_t)pos[it];
+        }
+        __syncthreads();
+        const int64_t base = out0 + e0;
+        const int64_t rnd = rnd0 + e0 / kPartTile;
+        for (uint32_t jj = threadIdx.x; jj < e1 - e0; jj += blockDim.x) {
+            a.e_key[base + jj] = s.k[jj];
+            a.e_a0[base + jj] = s.a0[jj];
+            if constexpr (AV) a.e_a1[base + jj] = s.a1[jj];
+            a.e_pos[base + jj] = s.pos[jj];
+        }
+        for (int b = threadIdx.x; b < nb2; b += blockDim.x) a.r_row[rnd * kPartBuckets + b] = desc_pack(ls[b], lh[b]);
+        if (threadIdx.x == 0) a.r_base[rnd] = base;
+        __syncthreads();
+    }
 }
 
 // apply: one workgroup per region; keys / mask / up to two active pane arrays in LDS
@@ -599,27 +675,38 @@ __device__ __forceinline__ void copy_words(long long* __restrict__ d, const long
     for (int64_t w = threadIdx.x; w < n2; w += blockDim.x) d2[w] = s2[w];
 }
 
-// Records per thread loaded in the prologue together with the region's state, so the
-// two latencies overlap (a region holds ~1200 records of a 10M batch at 8192 regions).
-constexpr int kApplyPre = 4;
+constexpr int kApplyRuns = 128;  // run descriptors staged in LDS per step
+constexpr int kApplyGroup = 4;   // consecutive runs a wave walks as one sequence
+constexpr int kApplyUnroll = 4;  // records per lane with their loads in flight together
 
 template <int AGG>
 __global__ void __launch_bounds__(512) k_rgn_apply(IngestArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     constexpr bool M = uses_mask<AGG>();
     constexpr bool AV = AGG == GW_AVG_I64 || AGG == GW_AVG_F64;
+    __shared__ uint32_t r_cnt[kApplyRuns];
+    __shared__ int64_t r_src[kApplyRuns];
     const int64_t r = blockIdx.x;
-    const int64_t lo = a.rg_base[r], hi = a.rg_base[r + 1];
-    if (lo == hi) return;  // uniform: no records for this region in this batch
     const int64_t S = pt_S(a.t);
     const int W = a.t.words;
+    // this region's runs: rounds [rb, re) of its bucket, column col of their rows
+    const int64_t bucket = r >> a.d2_bits, col = r & (((int64_t)1 << a.d2_bits) - 1);
+    const bool single = a.d2_bits == 0;
+    const int64_t rb = single ? 0 : a.rbeg[bucket], re = single ? a.ntiles : a.rbeg[bucket + 1];
+    const int64_t ccol = single ? r : col;
+    const uint32_t* rows = single ? a.p1_row : a.r_row;
+    const int64_t* rk = single ? a.p1_key : a.e_key;
+    const int64_t* ra0 = single ? a.p1_a0 : a.e_a0;
+    const int64_t* ra1 = single ? a.p1_a1 : a.e_a1;
+    const uint8_t* rpos = single ? a.p1_pos : a.e_pos;
     long long* lkeys = (long long*)smem;
     const int64_t MW = pt_mask_words(a.t);       // 0 unless M
     uint8_t* lmask = (uint8_t*)(lkeys + S);
     long long* lcell = lkeys + S + MW;           // [2][S][W]
     // dirty 128-B lines of the key and mask arrays (S <= 2048: <= 128 key lines)
     __shared__ uint32_t s_kdirty[4], s_mdirty[4];
-    // the (up to) two pane positions this batch touches
+    __shared__ int s_any;
+    // the (up to) two pane positions this flush touches
     const unsigned long long bocc = *(volatile unsigned long long*)a.batch_occ;
     const int act0 = bocc ? __ffsll((long long)bocc) - 1 : -1;
     const unsigned long long rest = bocc & (bocc - 1);
@@ -627,20 +714,13 @@ __global__ void __launch_bounds__(512) k_rgn_apply(IngestArgs a) {
     int64_t* gkeys = pt_region(a.t, r);
     int64_t* gmask = gkeys + S;
     const int msh = a.t.mask_shift;
-    // prologue: this thread's first records + the region state, all loads in flight
-    int64_t pk[kApplyPre], p0[kApplyPre], p1[kApplyPre];
-    uint32_t pp[kApplyPre];
-#pragma unroll
-    for (int q = 0; q < kApplyPre; ++q) {
-        const int64_t e = lo + q * (int64_t)blockDim.x + threadIdx.x;
-        pk[q] = 0; p0[q] = 0; p1[q] = 1; pp[q] = 0;
-        if (e < hi) {
-            pk[q] = a.e_key[e];
-            p0[q] = a.e_a0[e];
-            if constexpr (AV) p1[q] = a.e_a1[e];
-            pp[q] = a.e_pos[e];
-        }
-    }
+    if (threadIdx.x == 0) s_any = 0;
+    // any record at all for this region?  (first step's descriptors; uniform exit)
+    __syncthreads();
+    for (int64_t i = rb + threadIdx.x; i < re; i += blockDim.x)
+        if (rows[i * kPartBuckets + ccol] & 0xffffu) { s_any = 1; break; }
+    __syncthreads();
+    if (!s_any) return;
     copy_words(lkeys, (const long long*)gkeys, S);
     if constexpr (M) copy_words((long long*)lmask, (const long long*)gmask, MW);
     for (int ai = 0; ai < 2; ++ai) {
@@ -655,9 +735,10 @@ __global__ void __launch_bounds__(512) k_rgn_apply(IngestArgs a) {
         }
     }
     if (threadIdx.x < 4) { s_kdirty[threadIdx.x] = 0; s_mdirty[threadIdx.x] = 0; }
-    __syncthreads();
-    unsigned long long ins = 0, flags = 0;
-    auto apply_one = [&](int64_t key, int64_t c0, int64_t c1, uint32_t pos, int64_t& pane) -> bool {
+    unsigned long long ins = 0, flags = 0, spills = 0;
+    // false: the region is full; the record stays in the buffer marked (pos | 0x80) and
+    // k_rgn_collect parks it on the deferred list once the host has room for it
+    auto apply_one = [&](int64_t key, int64_t c0, int64_t c1, uint32_t pos, int64_t x) -> bool {
         int64_t j = pt_home(a.t, slot_hash(key));
         int64_t found = -1;
         for (int64_t p = 0; p < S; ++p) {
@@ -676,17 +757,17 @@ __global__ void __launch_bounds__(512) k_rgn_apply(IngestArgs a) {
             }
             j = (j + 1) & (S - 1);
         }
-        if (found < 0) {  // region full: park the record, the host grows the table
+        if (found < 0) {  // region full: the host grows the table, then merges the spills
             flags |= GW_DF_TABLE_FULL;
-            const int64_t rel = ((int64_t)pos - a.b_pos + a.t.ring) % a.t.ring;
-            pane = a.p_late + (int64_t)a.delta + rel;
-            return true;
+            spills++;
+            const_cast<uint8_t*>(rpos)[x] = (uint8_t)(pos | 0x80u);
+            return false;
         }
         const int ai = (int)pos == act0 ? 0 : ((int)pos == act1 ? 1 : -1);
         if (ai >= 0) {
             long long* c = lcell + ((int64_t)ai * S + found) * W;
             lds_cell_add<AGG>(c, c + (W == 2 ? 1 : 0), c0, c1);
-        } else {  // a third pane in one batch: device atomics on this region's cells
+        } else {  // a third pane in one flush: device atomics on this region's cells
             cell_atomic<AGG>(pt_cell(a.t, (r << a.t.log2S) + found, (int)pos), c0, c1);
         }
         if constexpr (M) {
@@ -695,26 +776,62 @@ __global__ void __launch_bounds__(512) k_rgn_apply(IngestArgs a) {
                 atomicOr(&s_mdirty[line >> 5], 1u << (line & 31));
             }
         }
-        return false;
+        return true;
     };
-#pragma unroll
-    for (int q = 0; q < kApplyPre; ++q) {
-        const int64_t e = lo + q * (int64_t)blockDim.x + threadIdx.x;
-        int64_t pane = 0;
-        const bool defer = e < hi && apply_one(pk[q], p0[q], p1[q], pp[q], pane);
-        defer_write(a, defer, pk[q], pane, p0[q], p1[q]);
-    }
-    for (int64_t e0 = lo + kApplyPre * (int64_t)blockDim.x; e0 < hi; e0 += blockDim.x) {
-        const int64_t e = e0 + threadIdx.x;
-        bool defer = false;
-        int64_t key = 0, pane = 0, c0 = 0, c1 = 1;
-        if (e < hi) {
-            key = a.e_key[e];
-            c0 = a.e_a0[e];
-            if constexpr (AV) c1 = a.e_a1[e];
-            defer = apply_one(key, c0, c1, a.e_pos[e], pane);
+    // Runs go to waves round-robin; a wave's lanes cover 64 consecutive records of a run,
+    // and kApplyUnroll runs per wave have their loads in flight together.
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    for (int64_t c0r = rb; c0r < re; c0r += kApplyRuns) {
+        const int nr = (int)min((int64_t)kApplyRuns, re - c0r);
+        __syncthreads();  // previous step's descriptors fully consumed (and region state staged)
+        for (int i = threadIdx.x; i < nr; i += blockDim.x) {
+            const int64_t rnd = c0r + i;
+            const uint32_t d = rows[rnd * kPartBuckets + ccol];
+            r_cnt[i] = d & 0xffffu;
+            r_src[i] = (single ? rnd * kPartTile : a.r_base[rnd]) + (d >> 16);
         }
-        defer_write(a, defer, key, pane, c0, c1);
+        __syncthreads();
+        // a wave takes kApplyGroup consecutive runs and walks their records as one
+        // flattened sequence, kApplyUnroll records per lane per step (loads in flight
+        // together); the run of a record is found against the group's prefix in registers
+        for (int i0 = wave * kApplyGroup; i0 < nr; i0 += nw * kApplyGroup) {
+            uint32_t pre[kApplyGroup + 1];
+            int64_t src[kApplyGroup];
+            pre[0] = 0;
+#pragma unroll
+            for (int u = 0; u < kApplyGroup; ++u) {
+                const int i = i0 + u;
+                const uint32_t c = i < nr ? r_cnt[i] : 0u;
+                src[u] = i < nr ? r_src[i] : 0;
+                pre[u + 1] = pre[u] + c;
+            }
+            const uint32_t tot = pre[kApplyGroup];
+            for (uint32_t k = 0; k < tot; k += 64 * kApplyUnroll) {  // wave-uniform trip count
+                int64_t key[kApplyUnroll], v0[kApplyUnroll], v1[kApplyUnroll], xs[kApplyUnroll];
+                uint32_t ps[kApplyUnroll];
+                bool ok[kApplyUnroll];
+#pragma unroll
+                for (int q = 0; q < kApplyUnroll; ++q) {
+                    const uint32_t e = k + q * 64 + lane;
+                    ok[q] = e < tot;
+                    key[q] = 0; v0[q] = 0; v1[q] = 1; ps[q] = 0; xs[q] = 0;
+                    if (ok[q]) {
+                        int u = 0;
+#pragma unroll
+                        for (int w = 1; w < kApplyGroup; ++w) u += e >= pre[w];
+                        const int64_t x = src[u] + (e - pre[u]);
+                        xs[q] = x;
+                        key[q] = rk[x];
+                        v0[q] = ra0[x];
+                        if constexpr (AV) v1[q] = ra1[x];
+                        ps[q] = rpos[x];
+                    }
+                }
+#pragma unroll
+                for (int q = 0; q < kApplyUnroll; ++q)
+                    if (ok[q]) apply_one(key[q], v0[q], v1[q], ps[q], xs[q]);
+            }
+        }
     }
     __syncthreads();
     // write back: dirty 128-B lines of keys / mask, every line of the active pane arrays
@@ -739,7 +856,46 @@ __global__ void __launch_bounds__(512) k_rgn_apply(IngestArgs a) {
         if (p < 0) continue;
         copy_words((long long*)pt_cell(a.t, r << a.t.log2S, p), lcell + (int64_t)ai * S * W, S * W);
     }
+    spills = wave_sum(spills);
+    if (__lane_id() == 0 && spills) atomicAdd(&a.st->spills, spills);
     block_commit(a.st, 0, ins, flags, 0);
+}
+
+// After a flush that filled regions: park every spilled record (pos | 0x80 in the
+// buffer) on the deferred list; the host has made room for st->spills entries.
+template <int AGG>
+__global__ void __launch_bounds__(256) k_rgn_collect(IngestArgs a) {
+    const bool single = a.d2_bits == 0;
+    const int nb = 1 << a.d1_bits;
+    const int64_t n = single ? a.ntiles * kPartTile : a.bk_off[nb];
+    const int64_t* rk = single ? a.p1_key : a.e_key;
+    const int64_t* ra0 = single ? a.p1_a0 : a.e_a0;
+    const int64_t* ra1 = single ? a.p1_a1 : a.e_a1;
+    uint8_t* rpos = single ? a.p1_pos : a.e_pos;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t base = blockIdx.x * (int64_t)blockDim.x; base < n; base += stride) {
+        const int64_t i = base + threadIdx.x;
+        bool spill = false;
+        int64_t key = 0, pane = 0, c0 = 0, c1 = 0;
+        if (i < n) {
+            bool valid = true;
+            if (single) {  // tile-local records: [0, start + count of the last bucket)
+                const uint32_t d = a.p1_row[(i / kPartTile) * kPartBuckets + nb - 1];
+                valid = (i % kPartTile) < (int64_t)((d >> 16) + (d & 0xffffu));
+            }
+            const uint32_t pos = rpos[i];
+            if (valid && (pos & 0x80u)) {
+                spill = true;
+                rpos[i] = (uint8_t)(pos & 0x7fu);
+                key = rk[i];
+                c0 = ra0[i];
+                c1 = ra1 ? ra1[i] : 1;
+                const int64_t rel = ((int64_t)(pos & 0x7fu) - a.b_pos + a.t.ring) % a.t.ring;
+                pane = a.p_late + (int64_t)a.delta + rel;
+            }
+        }
+        defer_write(a, spill, key, pane, c0, c1);
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -964,8 +1120,6 @@ static inline int grid_for(int64_t n, int per_thread = 1) {
     return (int)g;
 }
 
-int64_t region_scratch_tiles(int64_t n) { return std::max<int64_t>(1, (n + kPartTile - 1) / kPartTile); }
-
 hipError_t launch_table_init(const PaneTable& t, hipStream_t s) {
 #define L(A) hipLaunchKernelGGL(k_table_init<A>, dim3(grid_for(t.cap + 1)), dim3(256), 0, s, t)
     GW_AGG_SWITCH(t.agg, L);
@@ -977,35 +1131,6 @@ hipError_t launch_ingest(const IngestArgs& a, int path, int unroll, hipStream_t 
     if (path == 1) {
         const int g = grid_for(a.n, kPreaggItems);
 #define L(A) hipLaunchKernelGGL(k_ingest_preagg<A>, dim3(g), dim3(256), 0, s, a)
-        GW_AGG_SWITCH(a.t.agg, L);
-#undef L
-    } else if (path == 2) {
-        const int64_t tiles1 = region_scratch_tiles(a.n);
-        const int64_t tiles2 = tiles1 + kPartBuckets;
-        const bool single = a.d2_bits == 0;
-        const int nb1 = 1 << a.d1_bits;
-        const size_t part_lds = (size_t)kPartTile * 8 * (a.t.words == 2 ? 3 : 2) + 2 * kPartTile;
-        const int64_t S = pt_S(a.t);
-        const size_t apply_lds = (size_t)(S + pt_mask_words(a.t)) * 8 + (size_t)2 * S * a.t.words * 8;
-        int64_t* b1 = single ? a.rg_base : a.p1_base;
-        // beyond the 64 KB default: opt in (gfx950 has 160 KB of LDS per CU)
-#define L(A)                                                                                                    \
-    hipFuncSetAttribute((const void*)k_part_scatter<A, 1>, hipFuncAttributeMaxDynamicSharedMemorySize,          \
-                        (int)part_lds);                                                                         \
-    hipFuncSetAttribute((const void*)k_part_scatter<A, 2>, hipFuncAttributeMaxDynamicSharedMemorySize,          \
-                        (int)part_lds);                                                                         \
-    hipFuncSetAttribute((const void*)k_rgn_apply<A>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)apply_lds); \
-    hipLaunchKernelGGL((k_part_hist<A, 1>), dim3((unsigned)tiles1), dim3(kPartThreads), 0, s, a);             \
-    hipLaunchKernelGGL(k_part_cols1, dim3(nb1), dim3(256), 0, s, a.p_counts1, tiles1, b1);                     \
-    hipLaunchKernelGGL(k_rgn_bases, dim3(1), dim3(1024), 0, s, b1, (int64_t)nb1, single ? nullptr : a.p2_tile0); \
-    hipLaunchKernelGGL((k_part_scatter<A, 1>), dim3((unsigned)tiles1), dim3(kPartThreads), part_lds, s, a);   \
-    if (!single) {                                                                                              \
-        hipLaunchKernelGGL((k_part_hist<A, 2>), dim3((unsigned)tiles2), dim3(kPartThreads), 0, s, a);         \
-        hipLaunchKernelGGL(k_part_cols2, dim3((unsigned)((a.t.nreg + 255) / 256)), dim3(256), 0, s, a);       \
-        hipLaunchKernelGGL(k_rgn_bases, dim3(1), dim3(1024), 0, s, a.rg_base, a.t.nreg, (int64_t*)nullptr);   \
-        hipLaunchKernelGGL((k_part_scatter<A, 2>), dim3((unsigned)tiles2), dim3(kPartThreads), part_lds, s, a); \
-    }                                                                                                           \
-    hipLaunchKernelGGL(k_rgn_apply<A>, dim3((unsigned)a.t.nreg), dim3(512), apply_lds, s, a)
         GW_AGG_SWITCH(a.t.agg, L);
 #undef L
     } else if (unroll == 4) {
@@ -1024,6 +1149,58 @@ hipError_t launch_ingest(const IngestArgs& a, int path, int unroll, hipStream_t 
         GW_AGG_SWITCH(a.t.agg, L);
 #undef L
     }
+    return hipGetLastError();
+}
+
+static size_t part_lds_bytes(const IngestArgs& a) {
+    return (size_t)kPartTile * 8 * (a.t.words == 2 ? 3 : 2) + 2 * kPartTile;
+}
+
+int region_group(int d1_bits) { return std::max(1, std::min(kMaxGroup, 7 * (1 << d1_bits) / 8)); }
+
+// Region path, P1 over one watermark batch: one block per 4096-record tile.
+hipError_t launch_region_p1(const IngestArgs& a, hipStream_t s) {
+    const int64_t tiles = (a.n + kPartTile - 1) / kPartTile;
+    if (tiles == 0) return hipSuccess;
+    const size_t part_lds = part_lds_bytes(a);
+    // beyond the 64 KB default: opt in (gfx950 has 160 KB of LDS per CU)
+#define L(A)                                                                                                    \
+    hipFuncSetAttribute((const void*)k_rgn_p1<A>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)part_lds);   \
+    hipLaunchKernelGGL(k_rgn_p1<A>, dim3((unsigned)tiles), dim3(kPartThreads), part_lds, s, a)
+    GW_AGG_SWITCH(a.t.agg, L);
+#undef L
+    return hipGetLastError();
+}
+
+// Region path, per flush over a.ntiles buffer tiles: plan + P2 (two-pass tables), then
+// one workgroup per region applies its runs.
+hipError_t launch_region_flush(const IngestArgs& a, hipStream_t s) {
+    const bool single = a.d2_bits == 0;
+    const size_t part_lds = part_lds_bytes(a);
+    const int64_t S = pt_S(a.t);
+    const size_t apply_lds = (size_t)(S + pt_mask_words(a.t)) * 8 + (size_t)2 * S * a.t.words * 8;
+    const int nb1 = 1 << a.d1_bits;
+    if (a.ntiles == 0) return hipSuccess;
+#define L(A)                                                                                                    \
+    hipFuncSetAttribute((const void*)k_rgn_p2<A>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)part_lds);   \
+    hipFuncSetAttribute((const void*)k_rgn_apply<A>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)apply_lds); \
+    if (!single) {                                                                                              \
+        hipLaunchKernelGGL(k_rgn_plan1, dim3((unsigned)a.ngroups), dim3(256), 0, s, a);                        \
+        hipLaunchKernelGGL(k_rgn_plan2, dim3((unsigned)nb1), dim3(256), 0, s, a);                              \
+        hipLaunchKernelGGL(k_rgn_plan3, dim3(1), dim3(256), 0, s, a);                                          \
+        hipLaunchKernelGGL(k_rgn_p2<A>, dim3((unsigned)(a.ngroups * nb1)), dim3(kPartThreads), part_lds, s, a); \
+    }                                                                                                           \
+    hipLaunchKernelGGL(k_rgn_apply<A>, dim3((unsigned)a.t.nreg), dim3(512), apply_lds, s, a)
+    GW_AGG_SWITCH(a.t.agg, L);
+#undef L
+    return hipGetLastError();
+}
+
+hipError_t launch_region_collect(const IngestArgs& a, hipStream_t s) {
+    const int64_t n = a.ntiles * kPartTile;  // upper bound of the buffer's records
+#define L(A) hipLaunchKernelGGL(k_rgn_collect<A>, dim3(grid_for(n)), dim3(256), 0, s, a)
+    GW_AGG_SWITCH(a.t.agg, L);
+#undef L
     return hipGetLastError();
 }
 

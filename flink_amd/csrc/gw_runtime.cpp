@@ -101,15 +101,26 @@ struct gw_handle {
     PaneTable tv{};
     size_t table_bytes = 0;
 
-    // region-path scratch (k_part_*, k_rgn_apply)
-    uint32_t* p_counts = nullptr;  // pass-1 rows then pass-2 rows
-    int64_t p_counts_cap = 0;      // uint32 entries
-    int64_t* p_small = nullptr;    // p1_base | p2_tile0 (kPartBuckets + 1 each)
-    int64_t* rg_base = nullptr;
-    int64_t rg_base_cap = 0;       // int64 entries
-    int64_t* e_col[6] = {};        // e_key e_a0 e_a1 p1_key p1_a0 p1_a1
-    uint8_t* e_pos[2] = {};        // e_pos p1_pos
-    int64_t e_cap = 0;
+    // Buffer of P1 tiles (k_rgn_p1) and the flush scratch (k_rgn_plan*, k_rgn_p2), sized
+    // in 4096-record tiles; every array below holds buf_cap tiles' worth.
+    int64_t* e_col[6] = {};         // e_key e_a0 e_a1 (P2 output) p1_key p1_a0 p1_a1 (P1 output)
+    uint8_t* e_pos[2] = {};         // e_pos p1_pos
+    uint32_t* p1_row = nullptr;     // [tile][kPartBuckets]
+    uint32_t* p2_desc = nullptr;    // [bucket][tile]
+    int64_t* p2_off = nullptr;      // [blocks + 1], blocks = buckets x groups <= 2 tiles + kPartBuckets
+    int64_t* p2_roff = nullptr;
+    int64_t* rbeg = nullptr;        // [kPartBuckets + 1] rounds | [kPartBuckets + 1] records (bk_off)
+    uint32_t* r_row = nullptr;      // [rounds][kPartBuckets], rounds <= tiles + blocks
+    int64_t* r_base = nullptr;      // [rounds]
+    int64_t buf_cap = 0;            // tiles
+    static int64_t max_blocks(int64_t tiles) { return 2 * tiles + kPartBuckets + 1; }
+    static int64_t max_rounds(int64_t tiles) { return tiles + max_blocks(tiles); }
+
+    // buffered region ingest: P1 segments waiting for P2 + apply
+    int nseg = 0;
+    int64_t buf_tiles = 0;          // tiles used by the waiting segments
+    uint64_t buf_fresh = 0;         // ring positions holding only identities at buffer start
+    int64_t buf_limit = (int64_t)1 << 27;  // records (GW_BUFFER_RECORDS)
 
     // event-time state
     int64_t wm = INT64_MIN;
@@ -146,7 +157,7 @@ struct gw_handle {
 
     gw_stats stats{};
     bool timing = false;
-    KernelTimer t_ingest, t_fire;
+    KernelTimer t_ingest, t_fire, t_apply;
 
     SessionState* sess = nullptr;
     int ingest_unroll = 2;  // records per thread per iteration of k_ingest (GW_INGEST_UNROLL)
@@ -175,7 +186,7 @@ struct gw_handle {
         HIPCHECK(hipStreamSynchronize(stream));
         fold_shards(h_st);
         dirty = false;
-        if (timing) { t_ingest.resolve(); t_fire.resolve(); }
+        if (timing) { t_ingest.resolve(); t_fire.resolve(); t_apply.resolve(); }
         if (h_st->flags & GW_DF_NO_TS)
             return fail(GW_E_NO_TIMESTAMP,
                         "Record has Long.MIN_VALUE timestamp (= no timestamp marker). Did you forget to "
@@ -228,36 +239,43 @@ struct gw_handle {
         HIPCHECK(launch_table_init(t, stream));
         return GW_OK;
     }
-    int ensure_region(int64_t n) {
-        const int64_t tiles1 = region_scratch_tiles(n);
-        const int64_t cnt = (2 * tiles1 + kPartBuckets) * kPartBuckets;
-        if (cnt > p_counts_cap) {
-            if (p_counts) { hipStreamSynchronize(stream); hipFree(p_counts); p_counts = nullptr; }
-            HIPCHECK(hipMalloc((void**)&p_counts, (size_t)cnt * 4));
-            p_counts_cap = cnt;
+    void free_region() {
+        for (auto& p : e_col) { if (p) hipFree(p); p = nullptr; }
+        for (auto& p : e_pos) { if (p) hipFree(p); p = nullptr; }
+        for (void** p : {(void**)&p1_row, (void**)&p2_desc, (void**)&p2_off, (void**)&p2_roff, (void**)&r_row,
+                         (void**)&r_base}) {
+            if (*p) hipFree(*p);
+            *p = nullptr;
         }
-        if (!p_small) HIPCHECK(hipMalloc((void**)&p_small, (size_t)2 * (kPartBuckets + 1) * 8));
-        if (tv.nreg + 1 > rg_base_cap) {
-            if (rg_base) { hipStreamSynchronize(stream); hipFree(rg_base); rg_base = nullptr; }
-            HIPCHECK(hipMalloc((void**)&rg_base, (size_t)(tv.nreg + 1) * 8));
-            rg_base_cap = tv.nreg + 1;
+        buf_cap = 0;
+    }
+    // Region buffer of >= need tiles (re-allocated to `want` tiles when too small; only
+    // with no segment waiting).
+    int ensure_region(int64_t need, int64_t want) {
+        if (!rbeg) HIPCHECK(hipMalloc((void**)&rbeg, (size_t)2 * (kPartBuckets + 1) * 8));  // rbeg | bk_off
+        if (need <= buf_cap) return GW_OK;
+        if (nseg) return fail(GW_E_STATE, "internal: region buffer re-allocated with %d segments waiting", nseg);
+        const int64_t cap = std::max(need, want);
+        const size_t recs = (size_t)cap * kPartTile;
+        hipStreamSynchronize(stream);
+        free_region();
+        for (int i = 0; i < 6; ++i) {
+            if ((i == 2 || i == 5) && tv.words != 2) continue;  // a1 only for AVG
+            HIPCHECK(hipMalloc((void**)&e_col[i], recs * 8));
         }
-        if (n > e_cap) {
-            hipStreamSynchronize(stream);
-            for (auto& p : e_col) { if (p) hipFree(p); p = nullptr; }
-            for (auto& p : e_pos) { if (p) hipFree(p); p = nullptr; }
-            for (int i = 0; i < 6; ++i) {
-                if ((i == 2 || i == 5) && tv.words != 2) continue;  // a1 only for AVG
-                HIPCHECK(hipMalloc((void**)&e_col[i], (size_t)n * 8));
-            }
-            for (auto& p : e_pos) HIPCHECK(hipMalloc((void**)&p, (size_t)n));
-            e_cap = n;
-        }
+        for (auto& p : e_pos) HIPCHECK(hipMalloc((void**)&p, recs));
+        HIPCHECK(hipMalloc((void**)&p1_row, (size_t)cap * kPartBuckets * 4));
+        HIPCHECK(hipMalloc((void**)&p2_desc, (size_t)cap * kPartBuckets * 4));
+        HIPCHECK(hipMalloc((void**)&p2_off, (size_t)max_blocks(cap) * 8));
+        HIPCHECK(hipMalloc((void**)&p2_roff, (size_t)max_blocks(cap) * 8));
+        HIPCHECK(hipMalloc((void**)&r_row, (size_t)max_rounds(cap) * kPartBuckets * 4));
+        HIPCHECK(hipMalloc((void**)&r_base, (size_t)max_rounds(cap) * 8));
+        buf_cap = cap;
         return GW_OK;
     }
     int ensure_deferred(int64_t need) {
         if (need <= def_cap) return GW_OK;
-        int64_t nc = std::max<int64_t>(need + need / 2, 1 << 16);
+        int64_t nc = std::max<int64_t>(need + (need > (1 << 24) ? need / 8 : need / 2), 1 << 16);
         for (int b = 0; b < 2; ++b) {
             int64_t* nk; int64_t* np; int64_t* n0; int64_t* n1;
             HIPCHECK(hipMalloc((void**)&nk, nc * 8));
@@ -340,6 +358,11 @@ struct gw_handle {
     }
     // Keep the load factor of the linear-probing table below 0.7.
     int maybe_grow(int64_t incoming) {
+        if (nseg) {  // waiting segments are bucketed for this table's regions: apply them first
+            if (!(h_st->flags & GW_DF_TABLE_FULL) && (double)h_st->used_slots <= 0.7 * (double)tv.cap) return GW_OK;
+            int rc = flush_buffer();  // refreshes the counters (and may grow by itself)
+            if (rc) return rc;
+        }
         const int64_t used = (int64_t)h_st->used_slots;
         const bool full = (h_st->flags & GW_DF_TABLE_FULL) != 0;
         if (!full && (double)used <= 0.7 * (double)tv.cap) return GW_OK;
@@ -356,6 +379,7 @@ struct gw_handle {
 
     int merge_deferred() {
         int rc;
+        if (nseg && (rc = flush_buffer())) return rc;  // the merge writes the table directly
         const int64_t nin = (int64_t)h_st->n_deferred;
         if (nin == 0) return GW_OK;
         for (int attempt = 0; attempt < 8; ++attempt) {
@@ -504,11 +528,9 @@ struct gw_handle {
         return floor_div((i128)w + 1 - (i128)size() - (i128)cfg.offset, (i128)slide());
     }
 
-    int ingest_pane(int64_t nrec, const int64_t* key, const int64_t* ts, const int64_t* val) {
-        int rc;
-        if ((rc = ensure_fresh())) return rc;
-        if ((rc = maybe_grow(nrec))) return rc;
-        if ((rc = ensure_deferred((int64_t)h_st->n_deferred + nrec))) return rc;
+    // Ingest arguments shared by every path: the lateness bound and the ring geometry
+    // at the current watermark.
+    int base_args(IngestArgs& a, int64_t nrec, const int64_t* key, const int64_t* ts, const int64_t* val) {
         // first non-late pane: the first window not fired at the current watermark
         const i128 p_late = fired_k * m;
         i128 t_late = (i128)cfg.offset + p_late * g;
@@ -521,7 +543,7 @@ struct gw_handle {
         }
         if (t_late > (i128)INT64_MAX) return fail(GW_E_RANGE, "watermark beyond the last representable window");
         if (B < pl) B = pl;
-        IngestArgs a{};
+        a = IngestArgs{};
         a.key = key; a.ts = ts; a.val = val; a.n = nrec;
         a.t_late = (int64_t)t_late;
         a.p_late = (int64_t)pl;
@@ -532,6 +554,77 @@ struct gw_handle {
         a.t = tv;
         a.d_key = dk[cur]; a.d_pane = dp[cur]; a.d_a0 = da0[cur]; a.d_a1 = da1[cur];
         a.st = d_st;
+        return GW_OK;
+    }
+
+    // Region arrays of the current table geometry.
+    void region_args(IngestArgs& a) {
+        int l2 = 0;
+        while (((int64_t)1 << l2) < tv.nreg) ++l2;
+        // <= 7 bits in P1 keeps ~32 records per bucket run of a 4096-record tile
+        a.d1_bits = l2 <= 14 ? std::min(l2, 7) : (l2 + 1) / 2;
+        a.d2_bits = l2 - a.d1_bits;
+        a.p1_key = e_col[3]; a.p1_a0 = e_col[4]; a.p1_a1 = e_col[5]; a.p1_pos = e_pos[1];
+        a.e_key = e_col[0]; a.e_a0 = e_col[1]; a.e_a1 = e_col[2]; a.e_pos = e_pos[0];
+        a.p1_row = p1_row;
+        a.p2_desc = p2_desc;
+        a.p2_off = p2_off;
+        a.p2_roff = p2_roff;
+        a.rbeg = rbeg;
+        a.bk_off = rbeg + kPartBuckets + 1;
+        a.r_row = r_row;
+        a.r_base = r_base;
+        a.batch_occ = d_tmp + 1;
+    }
+
+    // P2 + apply over every waiting segment (one fire's worth of batches).  Runs before
+    // any fire, rehash, merge or non-region ingest, so the table is exact whenever it is
+    // read.
+    int flush_buffer() {
+        if (!nseg) return GW_OK;
+        int rc;
+        IngestArgs a;
+        if ((rc = base_args(a, 0, nullptr, nullptr, nullptr))) return rc;
+        region_args(a);
+        a.ntiles = buf_tiles;
+        a.p2_group = region_group(a.d1_bits);
+        a.ngroups = (buf_tiles + a.p2_group - 1) / a.p2_group;
+        a.ring_fresh = buf_fresh;
+        nseg = 0;  // before any launch: the TABLE_FULL handling below may grow the table
+        buf_tiles = 0;
+        if (timing) {
+            auto ev = t_apply.get();
+            HIPCHECK(hipEventRecord(ev.first, stream));
+            HIPCHECK(launch_region_flush(a, stream));
+            HIPCHECK(hipEventRecord(ev.second, stream));
+            t_apply.pending.push_back(ev);
+        } else {
+            HIPCHECK(launch_region_flush(a, stream));
+        }
+        stats.applies++;
+        dirty = true;
+        if ((rc = refresh())) return rc;
+        if (h_st->spills) {  // full regions left records in the buffer: park them
+            if ((rc = ensure_deferred((int64_t)h_st->n_deferred + (int64_t)h_st->spills))) return rc;
+            if ((rc = set_field(offsetof(DevStatus, spills), 0))) return rc;
+            HIPCHECK(launch_region_collect(a, stream));
+            dirty = true;
+            if ((rc = refresh())) return rc;
+        }
+        if (h_st->flags & GW_DF_TABLE_FULL) {
+            if ((rc = maybe_grow(0))) return rc;
+            if ((rc = merge_deferred())) return rc;
+        }
+        return GW_OK;
+    }
+
+    int ingest_pane(int64_t nrec, const int64_t* key, const int64_t* ts, const int64_t* val) {
+        int rc;
+        if ((rc = ensure_fresh())) return rc;
+        if ((rc = maybe_grow(nrec))) return rc;
+        if ((rc = ensure_deferred((int64_t)h_st->n_deferred + nrec))) return rc;
+        IngestArgs a;
+        if ((rc = base_args(a, nrec, key, ts, val))) return rc;
         // path: LDS pre-aggregation when the batch repeats few keys many times; region
         // bucketing when the batch is large against the table (its streaming passes cost
         // ~48 B per slot, the direct path ~300 B of scattered traffic per record);
@@ -545,27 +638,43 @@ struct gw_handle {
             if (big || (cfg.flags & GW_FLAG_FORCE_REGION)) path = 2;
         }
         if (path == 1) stats.preagg_batches++;
-        if (path == 2) {
-            if ((rc = ensure_region(nrec))) return rc;
-            int l2 = 0;
-            while (((int64_t)1 << l2) < tv.nreg) ++l2;
-            // <= 7 bits per pass keeps >= 32 records per bucket run of a 4096-record tile
-            a.d1_bits = l2 <= 14 ? std::min(l2, 7) : (l2 + 1) / 2;
-            a.d2_bits = l2 - a.d1_bits;
-            const int64_t tiles1 = region_scratch_tiles(nrec);
-            a.p_counts1 = p_counts;
-            a.p_counts2 = p_counts + tiles1 * kPartBuckets;
-            a.p1_base = p_small;
-            a.p2_tile0 = p_small + kPartBuckets + 1;
-            a.rg_base = rg_base;
-            a.e_key = e_col[0]; a.e_a0 = e_col[1]; a.e_a1 = e_col[2];
-            a.p1_key = e_col[3]; a.p1_a0 = e_col[4]; a.p1_a1 = e_col[5];
-            a.e_pos = e_pos[0]; a.p1_pos = e_pos[1];
-            a.batch_occ = d_tmp + 1;
-            a.ring_fresh = ~occ;
-            HIPCHECK(hipMemsetAsync(d_tmp + 1, 0, 8, stream));
+        if (path != 2 && nseg) {  // the other paths write the table directly: apply first
+            if ((rc = flush_buffer())) return rc;
+            if ((rc = base_args(a, nrec, key, ts, val))) return rc;  // the table may have grown
         }
-        if (timing) {
+        if (path == 2) {
+            region_args(a);
+            // Two-pass tables buffer P1 segments across watermarks (P2 + apply once per
+            // fire); single-pass tables apply every batch.
+            const bool buffered = a.d2_bits > 0 && !(cfg.flags & GW_FLAG_NO_BUFFER);
+            const int64_t tiles = (nrec + kPartTile - 1) / kPartTile;
+            if (nseg && buf_tiles + tiles > buf_cap) {
+                if ((rc = flush_buffer())) return rc;
+                if ((rc = base_args(a, nrec, key, ts, val))) return rc;
+            }
+            const int64_t want =
+                buffered ? std::min(std::max<int64_t>(buf_limit / kPartTile, 1), std::max<int64_t>(16 * tiles, 256))
+                         : tiles;
+            if ((rc = ensure_region(buf_tiles + tiles, want))) return rc;
+            region_args(a);
+            a.tile0 = buf_tiles;
+            if (nseg == 0) {
+                HIPCHECK(hipMemsetAsync(d_tmp + 1, 0, 8, stream));
+                buf_fresh = ~occ;
+            }
+            if (timing) {
+                auto ev = t_ingest.get();
+                HIPCHECK(hipEventRecord(ev.first, stream));
+                HIPCHECK(launch_region_p1(a, stream));
+                HIPCHECK(hipEventRecord(ev.second, stream));
+                t_ingest.pending.push_back(ev);
+            } else {
+                HIPCHECK(launch_region_p1(a, stream));
+            }
+            nseg++;
+            buf_tiles += tiles;
+            if (!buffered && (rc = flush_buffer())) return rc;
+        } else if (timing) {
             auto ev = t_ingest.get();
             HIPCHECK(hipEventRecord(ev.first, stream));
             HIPCHECK(launch_ingest(a, path, ingest_unroll, stream));
@@ -603,6 +712,7 @@ struct gw_handle {
             return GW_OK;
         }
         if ((rc = ensure_fresh())) return rc;
+        if ((rc = flush_buffer())) return rc;  // buffered records first, then the timers
         const int64_t before = (int64_t)h_st->rows;
         {
             if ((rc = fire_until(kt))) return rc;
@@ -675,6 +785,7 @@ int gw_create(const gw_config* cfg, gw_handle** out) {
     h->cfg = *cfg;
     if (const char* u = getenv("GW_INGEST_UNROLL")) h->ingest_unroll = atoi(u);
     if (const char* u = getenv("GW_REGION_MIN_BATCH")) h->region_min_batch = atoll(u);
+    if (const char* u = getenv("GW_BUFFER_RECORDS")) h->buf_limit = std::max<int64_t>(atoll(u), 1);
     if (h->cfg.max_parallelism <= 0) h->cfg.max_parallelism = 128;
     if (h->cfg.parallelism <= 0) h->cfg.parallelism = 1;
     if (h->cfg.max_batch <= 0) h->cfg.max_batch = 1 << 20;
@@ -735,6 +846,8 @@ int gw_create(const gw_config* cfg, gw_handle** out) {
     h->table_bytes = gw_handle::pane_table_bytes(h->tv);
     rc = h->ensure_deferred(1 << 16);
     if (rc) return bail(rc, h->err);
+    rc = h->ensure_output(hint);  // one fired window per expected key, before the first fire
+    if (rc) return bail(rc, h->err);
     if ((e = hipStreamSynchronize(h->stream)) != hipSuccess)
         return bail(GW_E_DEVICE, std::string("init: ") + hipGetErrorString(e));
     *out = h;
@@ -751,16 +864,14 @@ int gw_destroy(gw_handle* h) {
     }
     if (h->o_key) { hipFree(h->o_key); hipFree(h->o_start); hipFree(h->o_end); hipFree(h->o_res); }
     if (h->h_stage) { hipHostFree(h->h_stage); hipFree(h->d_stage); hipFree(h->d_hash_stage); }
-    if (h->p_counts) hipFree(h->p_counts);
-    if (h->p_small) hipFree(h->p_small);
-    if (h->rg_base) hipFree(h->rg_base);
-    for (auto p : h->e_col) if (p) hipFree(p);
-    for (auto p : h->e_pos) if (p) hipFree(p);
+    h->free_region();
+    if (h->rbeg) hipFree(h->rbeg);
     if (h->d_st) hipFree(h->d_st);
     if (h->d_tmp) hipFree(h->d_tmp);
     if (h->h_st) hipHostFree(h->h_st);
     h->t_ingest.destroy();
     h->t_fire.destroy();
+    h->t_apply.destroy();
     if (h->stream) hipStreamDestroy(h->stream);
     delete h;
     return GW_OK;
@@ -840,6 +951,15 @@ int gw_advance_watermark(gw_handle* h, int64_t wm, int64_t* rows_fired) {
         return rc;
     }
     return h->advance_pane(wm, rows_fired);
+}
+
+int gw_flush(gw_handle* h) {
+    if (!h) return GW_E_INVALID;
+    if (h->failed) return h->fail(GW_E_STATE, "operator failed earlier: %s", h->err.c_str());
+    if (h->session) return GW_OK;
+    hipSetDevice(h->cfg.device);
+    int rc = h->ensure_fresh();
+    return rc ? rc : h->flush_buffer();
 }
 
 int gw_end_input(gw_handle* h, int64_t* rows_fired) { return gw_advance_watermark(h, INT64_MAX, rows_fired); }
@@ -956,7 +1076,7 @@ int gw_kernel_time_ms(gw_handle* h, int which, double* ms, int64_t* launches) {
     if (!h) return GW_E_INVALID;
     hipStreamSynchronize(h->stream);
     if (h->sess) return session_kernel_time(h->sess, which, ms, launches);
-    KernelTimer& t = which == 0 ? h->t_ingest : h->t_fire;
+    KernelTimer& t = which == 0 ? h->t_ingest : which == 1 ? h->t_fire : h->t_apply;
     t.resolve();
     if (ms) *ms = t.launches ? t.total_ms / (double)t.launches : 0.0;
     if (launches) *launches = t.launches;

@@ -363,6 +363,11 @@ class GpuWindowOperator:
         N.check(N.lib().gw_advance_watermark(self._h, int(wm), ctypes.byref(fired)), self._h)
         return fired.value
 
+    def flush(self):
+        """Apply every buffered record to the window state (gw_flush); firing does this
+        by itself, a snapshot or a timing boundary calls it explicitly."""
+        N.check(N.lib().gw_flush(self._h), self._h)
+
     def pending_rows(self) -> int:
         n = ctypes.c_int64(0)
         N.check(N.lib().gw_pending_rows(self._h, ctypes.byref(n)), self._h)

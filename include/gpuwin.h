@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define GW_ABI_VERSION 1
+#define GW_ABI_VERSION 2
 
 /* ---- status codes -------------------------------------------------------- */
 #define GW_OK              0
@@ -111,6 +111,8 @@ typedef struct gw_config {
 #define GW_FLAG_CHECK_KEY_GROUPS   4 /* reject keys outside this subtask's key groups    */
 #define GW_FLAG_FORCE_REGION       8 /* always use the region-bucketed ingest path      */
 #define GW_FLAG_NO_REGION         16 /* never use the region-bucketed ingest path       */
+#define GW_FLAG_NO_BUFFER         32 /* region path: apply every batch at once instead of
+                                        buffering pass-1 segments until the next fire    */
 
 typedef struct gw_handle gw_handle;
 
@@ -128,6 +130,7 @@ typedef struct gw_stats {
     int64_t rehashes;         /* table growths                                     */
     int64_t preagg_batches;   /* batches that used the LDS pre-aggregation kernel  */
     int64_t session_merges;   /* sessions merged away (M_b)                        */
+    int64_t applies;          /* region pass-2 + apply launches (buffer flushes)   */
 } gw_stats;
 
 /* ---- lifecycle ------------------------------------------------------------ */
@@ -156,6 +159,11 @@ int  gw_ingest_device(gw_handle* h, int64_t n, const int64_t* d_key, const int32
  * NULL) receives the number of rows this call produced.  Watermarks that do not
  * advance are ignored, as in InternalTimerServiceImpl.tryAdvanceWatermark. */
 int  gw_advance_watermark(gw_handle* h, int64_t wm, int64_t* rows_fired);
+/* Apply every buffered record to the window state now.  The region path buffers
+ * pass-1 segments of several watermark batches and applies them before the next fire
+ * by itself; gw_flush makes the state exact at any point, as a snapshot needs
+ * (StreamOperator.prepareSnapshotPreBarrier, RS/api/operators/StreamOperator.java:122). */
+int  gw_flush(gw_handle* h);
 /* Bounded input ended (BoundedOneInput.endInput) — equivalent to MAX_WATERMARK. */
 int  gw_end_input(gw_handle* h, int64_t* rows_fired);
 
@@ -176,8 +184,9 @@ int  gw_get_stats(const gw_handle* h, gw_stats* out);
 int  gw_synchronize(gw_handle* h);
 /* hipStream_t the handle launches on (for ordering / event timing by callers). */
 void* gw_stream(gw_handle* h);
-/* Average device duration (ms) of the last launch of each named kernel family,
- * measured with HIP events on the handle's stream.  which: 0 = ingest, 1 = fire. */
+/* Average device duration (ms) per launch of each kernel family since the last call,
+ * measured with HIP events on the handle's stream.  which: 0 = ingest (per batch;
+ * region path: pass 1), 1 = fire, 2 = region pass 2 + apply (per buffer flush). */
 int  gw_kernel_time_ms(gw_handle* h, int which, double* ms, int64_t* launches);
 int  gw_enable_kernel_timing(gw_handle* h, int enable);
 

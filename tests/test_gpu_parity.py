@@ -154,6 +154,93 @@ def test_region_two_pass_partition_vs_oracle(oracle_lib, cfg, agg):
     assert _cmp(g, o, agg) == []
 
 
+BUFFER_CFGS = [
+    dict(assigner="sliding", size=100_000, slide=50_000),    # ~50 batches per fire
+    dict(assigner="tumbling", size=200_000, slide=200_000),  # ~100 batches: the 64-segment cap flushes
+    dict(assigner="sliding", size=30_000, slide=20_000),     # pane 10 s: buffers span several panes
+]
+
+
+@pytest.mark.parametrize("agg", ["count", "sum_i64", "max_f64", "avg_f64"])
+@pytest.mark.parametrize("cfg", BUFFER_CFGS, ids=lambda c: "-".join(str(v) for v in c.values()))
+def test_region_buffered_segments_vs_oracle(oracle_lib, cfg, agg):
+    """Two-pass region table (512 regions): pass 1 of every watermark batch is buffered
+    as a segment and pass 2 + apply run once before the next fire (or when 64 segments
+    wait).  Same fired rows as the oracle at every watermark."""
+    kw = dict(cfg, agg=agg)
+    keys, ts, vals, batches = random_stream(seed=zlib.crc32(f"buf{agg}{cfg}".encode()) & 0xffff, n=150_000,
+                                            num_keys=40_000, n_batches=150, ts_step=1, agg=agg)
+    g, glate, stats = run_gpu(kw, keys, ts, vals, batches, flags=N.FLAG_FORCE_REGION, capacity_hint=600_000)
+    assert stats["table_capacity"] == 1 << 20
+    assert 0 < stats["applies"] < 150  # batches were buffered
+    o, olate = run_oracle(oracle_lib, kw, keys, ts, vals, batches)
+    assert glate == olate == 0
+    assert _cmp(g, o, agg) == []
+
+
+@pytest.mark.parametrize("agg", ["sum_i64", "avg_f64"])
+def test_region_two_pass_spills_and_growth(oracle_lib, agg):
+    """Far more keys than a two-pass table holds: full regions leave their records in
+    the buffer (spills), which are parked, the table grows, and they are merged back."""
+    kw = dict(assigner="tumbling", size=1_000_000, slide=1_000_000, agg=agg)
+    keys, ts, vals, batches = random_stream(seed=23, n=1_600_000, num_keys=1_200_000, n_batches=4, ts_step=1,
+                                            agg=agg)
+    g, glate, stats = run_gpu(kw, keys, ts, vals, batches, flags=N.FLAG_FORCE_REGION, capacity_hint=300_000)
+    assert stats["rehashes"] > 0
+    o, olate = run_oracle(oracle_lib, kw, keys, ts, vals, batches)
+    assert glate == olate == 0
+    assert _cmp(g, o, agg) == []
+
+
+def test_region_buffer_limit_flushes(oracle_lib, monkeypatch):
+    """A 5000-record buffer (GW_BUFFER_RECORDS) flushes every few 1000-record batches."""
+    monkeypatch.setenv("GW_BUFFER_RECORDS", "5000")
+    kw = dict(assigner="sliding", size=100_000, slide=50_000, agg="sum_i64")
+    keys, ts, vals, batches = random_stream(seed=31, n=100_000, num_keys=30_000, n_batches=100, ts_step=1)
+    g, glate, stats = run_gpu(kw, keys, ts, vals, batches, flags=N.FLAG_FORCE_REGION, capacity_hint=600_000)
+    assert stats["applies"] >= 20
+    o, olate = run_oracle(oracle_lib, kw, keys, ts, vals, batches)
+    assert glate == olate == 0
+    assert compare(g, o, False) == []
+
+
+def test_region_buffer_mixed_paths(oracle_lib):
+    """Large batches take the buffered region path, small ones the direct path, which
+    applies the waiting segments first."""
+    kw = dict(assigner="sliding", size=40_000, slide=20_000, agg="sum_i64")
+    sizes = [140_000, 900, 140_000, 140_000, 700, 2_000, 140_000, 500] * 2
+    n = sum(sizes)
+    keys, ts, vals, _ = random_stream(seed=17, n=n, num_keys=200_000, n_batches=1, ts_step=1)
+    ts = np.arange(n, dtype=np.int64) // 40 - np.random.default_rng(3).integers(0, 200, n)
+    batches, lo = [], 0
+    for s in sizes:
+        batches.append((lo, lo + s, int(ts[:lo + s].max()) - 201))
+        lo += s
+    g, glate, stats = run_gpu(kw, keys, ts, vals, batches, capacity_hint=600_000)
+    assert stats["table_capacity"] == 1 << 20
+    o, olate = run_oracle(oracle_lib, kw, keys, ts, vals, batches)
+    assert glate == olate == 0
+    assert compare(g, o, False) == []
+
+
+@pytest.mark.parametrize("cfg", CONFIGS[:-1], ids=lambda c: "-".join(str(v) for v in c.values()))
+@pytest.mark.parametrize("flags", [N.FLAG_FORCE_REGION, N.FLAG_FORCE_REGION | N.FLAG_NO_BUFFER],
+                         ids=["buffered", "unbuffered"])
+def test_region_two_pass_late_and_far_future(oracle_lib, cfg, flags):
+    """Late drops and parked far-future records on a two-pass (buffered) region table."""
+    kw = dict(cfg, agg="sum_i64")
+    keys, ts, vals, batches = random_stream(seed=12, n=30000, num_keys=3000, n_batches=40,
+                                            disorder=max(4000, 3 * cfg["size"]), wm_lag=200, agg="sum_i64")
+    rng = np.random.default_rng(4)
+    far = rng.choice(len(ts), 300, replace=False)
+    ts[far] += rng.integers(50_000, 2_000_000, 300)
+    g, glate, _ = run_gpu(kw, keys, ts, vals, batches, flags=flags, capacity_hint=600_000)
+    o, olate = run_oracle(oracle_lib, kw, keys, ts, vals, batches)
+    assert olate > 0
+    assert glate == olate
+    assert compare(g, o, False) == []
+
+
 def test_region_partition_eight_bit_digits(oracle_lib):
     """2^26 slots = 32768 regions: the two partition passes take 8 + 7 region bits."""
     kw = dict(assigner="sliding", size=1000, slide=250, agg="sum_i64")
