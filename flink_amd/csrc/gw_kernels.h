@@ -80,7 +80,14 @@ __device__ __forceinline__ void pt_mask_put(const PaneTable& t, int64_t g, uint6
 GW_HD int64_t pt_key_region(const PaneTable& t, uint64_t h) {
     return t.log2nreg == 0 ? 0 : (int64_t)(h >> (64 - t.log2nreg));
 }
-GW_HD int64_t pt_home(const PaneTable& t, uint64_t h) { return (int64_t)(h & (uint64_t)(pt_S(t) - 1)); }
+// The home slot is aligned to a group of kProbeGroup slots: linear probing then starts
+// on a 32-B group boundary, so k_rgn_apply compares a whole group of keys per LDS step
+// (one probe step for almost every key at the table's load) with the same slot order
+// as the scalar probes of the other kernels.
+constexpr int kProbeGroup = 4;
+GW_HD int64_t pt_home(const PaneTable& t, uint64_t h) {
+    return (int64_t)(h & (uint64_t)(pt_S(t) - 1) & ~(uint64_t)(kProbeGroup - 1));
+}
 
 // Find (or insert) the slot of `key` in its region; -1 if the probe limit is hit.
 __device__ __forceinline__ int64_t pt_find_or_insert(const PaneTable& t, int64_t key, bool& inserted) {

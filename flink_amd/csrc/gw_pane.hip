@@ -675,7 +675,8 @@ __device__ __forceinline__ void copy_words(long long* __restrict__ d, const long
     for (int64_t w = threadIdx.x; w < n2; w += blockDim.x) d2[w] = s2[w];
 }
 
-constexpr int kApplyRuns = 128;  // run descriptors staged in LDS per step
+constexpr int kApplyRuns = 256;  // run descriptors staged in LDS per step (<= blockDim)
+constexpr int kStageRegs = 8;    // 16-B state words per thread in the prologue (<= 4096 x 16 B)
 constexpr int kApplyGroup = 4;   // consecutive runs a wave walks as one sequence
 constexpr int kApplyUnroll = 4;  // records per lane with their loads in flight together
 
@@ -684,8 +685,7 @@ __global__ void __launch_bounds__(512) k_rgn_apply(IngestArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     constexpr bool M = uses_mask<AGG>();
     constexpr bool AV = AGG == GW_AVG_I64 || AGG == GW_AVG_F64;
-    __shared__ uint32_t r_cnt[kApplyRuns];
-    __shared__ int64_t r_src[kApplyRuns];
+    __shared__ uint32_t r_cnt[kApplyRuns], r_src[kApplyRuns];  // buffer offsets < 2^32 (gw_runtime.cpp)
     const int64_t r = blockIdx.x;
     const int64_t S = pt_S(a.t);
     const int W = a.t.words;
@@ -703,9 +703,8 @@ __global__ void __launch_bounds__(512) k_rgn_apply(IngestArgs a) {
     const int64_t MW = pt_mask_words(a.t);       // 0 unless M
     uint8_t* lmask = (uint8_t*)(lkeys + S);
     long long* lcell = lkeys + S + MW;           // [2][S][W]
-    // dirty 128-B lines of the key and mask arrays (S <= 2048: <= 128 key lines)
-    __shared__ uint32_t s_kdirty[4], s_mdirty[4];
-    __shared__ int s_any;
+    // dirty 128-B lines of the key array (S <= 2048: <= 128 lines)
+    __shared__ uint32_t s_kdirty[4];
     // the (up to) two pane positions this flush touches
     const unsigned long long bocc = *(volatile unsigned long long*)a.batch_occ;
     const int act0 = bocc ? __ffsll((long long)bocc) - 1 : -1;
@@ -714,37 +713,72 @@ __global__ void __launch_bounds__(512) k_rgn_apply(IngestArgs a) {
     int64_t* gkeys = pt_region(a.t, r);
     int64_t* gmask = gkeys + S;
     const int msh = a.t.mask_shift;
-    if (threadIdx.x == 0) s_any = 0;
-    // any record at all for this region?  (first step's descriptors; uniform exit)
-    __syncthreads();
-    for (int64_t i = rb + threadIdx.x; i < re; i += blockDim.x)
-        if (rows[i * kPartBuckets + ccol] & 0xffffu) { s_any = 1; break; }
-    __syncthreads();
-    if (!s_any) return;
-    copy_words(lkeys, (const long long*)gkeys, S);
-    if constexpr (M) copy_words((long long*)lmask, (const long long*)gmask, MW);
-    for (int ai = 0; ai < 2; ++ai) {
-        const int p = ai ? act1 : act0;
-        if (p < 0) continue;
-        long long* dst = lcell + (int64_t)ai * S * W;
-        if ((a.ring_fresh >> p) & 1) {  // position retired since its last use: all identity
-            const int64_t id0 = identity0(AGG);
-            for (int64_t w = threadIdx.x; w < S * W; w += blockDim.x) dst[w] = (W == 2 && (w & 1)) ? 0 : id0;
-        } else {
-            copy_words(dst, (const long long*)pt_cell(a.t, r << a.t.log2S, p), S * W);
-        }
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+
+    // Prologue: the first block of run descriptors and the whole region state (keys +
+    // mask, then each active pane array; a retired pane is the identity, not loaded) are
+    // loaded in one memory round trip, then staged into LDS.
+    const int nr0 = (int)min((int64_t)kApplyRuns, re - rb);
+    uint32_t d0 = 0;
+    int64_t base0 = 0;
+    if ((int)threadIdx.x < nr0) {
+        const int64_t rnd = rb + threadIdx.x;
+        d0 = rows[rnd * kPartBuckets + ccol];
+        base0 = single ? rnd * kPartTile : a.r_base[rnd];
     }
-    if (threadIdx.x < 4) { s_kdirty[threadIdx.x] = 0; s_mdirty[threadIdx.x] = 0; }
+    const int64_t nkm = (S + MW) / 2, np = S * W / 2;  // in 16-B units
+    const bool ld0 = act0 >= 0 && !((a.ring_fresh >> act0) & 1);
+    const bool ld1 = act1 >= 0 && !((a.ring_fresh >> act1) & 1);
+    const int64_t total2 = nkm + (act0 >= 0 ? np : 0) + (act1 >= 0 ? np : 0);
+    const long2* gkm2 = reinterpret_cast<const long2*>(gkeys);
+    const long2* gp0 = act0 >= 0 ? reinterpret_cast<const long2*>(pt_cell(a.t, r << a.t.log2S, act0)) : nullptr;
+    const long2* gp1 = act1 >= 0 ? reinterpret_cast<const long2*>(pt_cell(a.t, r << a.t.log2S, act1)) : nullptr;
+    const int64_t id0 = identity0(AGG);
+    const long2 ident = W == 2 ? long2{id0, 0} : long2{id0, id0};
+    long2 stage[kStageRegs];
+#pragma unroll
+    for (int q = 0; q < kStageRegs; ++q) {
+        const int64_t w = threadIdx.x + (int64_t)q * 512;
+        stage[q] = ident;
+        if (w < nkm) stage[q] = gkm2[w];
+        else if (w < nkm + np) { if (ld0) stage[q] = gp0[w - nkm]; }
+        else if (w < total2) { if (ld1) stage[q] = gp1[w - nkm - np]; }
+    }
+    // uniform exit for a region without records (its first descriptor block is empty)
+    const int any = __syncthreads_or((int)(d0 & 0xffffu)) || (re - rb > kApplyRuns);
+    if (!any) return;
+    long2* l2 = reinterpret_cast<long2*>(lkeys);
+#pragma unroll
+    for (int q = 0; q < kStageRegs; ++q) {
+        const int64_t w = threadIdx.x + (int64_t)q * 512;
+        if (w < total2) l2[w] = stage[q];
+    }
+    if ((int)threadIdx.x < nr0) {
+        r_cnt[threadIdx.x] = d0 & 0xffffu;
+        r_src[threadIdx.x] = (uint32_t)(base0 + (d0 >> 16));
+    }
+    if (threadIdx.x < 4) s_kdirty[threadIdx.x] = 0;
     unsigned long long ins = 0, flags = 0, spills = 0;
     // false: the region is full; the record stays in the buffer marked (pos | 0x80) and
     // k_rgn_collect parks it on the deferred list once the host has room for it
     auto apply_one = [&](int64_t key, int64_t c0, int64_t c1, uint32_t pos, int64_t x) -> bool {
-        int64_t j = pt_home(a.t, slot_hash(key));
+        // Probe one 4-key group (32 B) per step: the first slot holding the key or
+        // empty, in slot order, decides; an empty slot is claimed with a CAS (a lost race
+        // re-reads the same group).
+        int64_t g0 = pt_home(a.t, slot_hash(key));
         int64_t found = -1;
-        for (int64_t p = 0; p < S; ++p) {
-            const long long k = lkeys[j];
-            if (k == key) { found = j; break; }
-            if (k == kEmptyKey) {
+        for (int64_t p = 0; p < S;) {
+            const long2 k01 = *reinterpret_cast<const long2*>(&lkeys[g0]);
+            const long2 k23 = *reinterpret_cast<const long2*>(&lkeys[g0 + 2]);
+            const uint32_t hit = (uint32_t)(k01.x == key) | (uint32_t)(k01.y == key) << 1 |
+                                 (uint32_t)(k23.x == key) << 2 | (uint32_t)(k23.y == key) << 3;
+            const uint32_t emp = (uint32_t)(k01.x == kEmptyKey) | (uint32_t)(k01.y == kEmptyKey) << 1 |
+                                 (uint32_t)(k23.x == kEmptyKey) << 2 | (uint32_t)(k23.y == kEmptyKey) << 3;
+            const uint32_t m = hit | emp;
+            if (m) {
+                const int i = __ffs((int)m) - 1;
+                const int64_t j = g0 + i;
+                if ((hit >> i) & 1) { found = j; break; }
                 const unsigned long long prev = atomicCAS((unsigned long long*)&lkeys[j],
                                                           (unsigned long long)kEmptyKey, (unsigned long long)key);
                 if (prev == (unsigned long long)kEmptyKey) {
@@ -754,84 +788,163 @@ __global__ void __launch_bounds__(512) k_rgn_apply(IngestArgs a) {
                     break;
                 }
                 if ((int64_t)prev == key) { found = j; break; }
+                continue;  // another key took the slot: re-read this group
             }
-            j = (j + 1) & (S - 1);
+            g0 = (g0 + kProbeGroup) & (S - 1);
+            p += kProbeGroup;
         }
-        if (found < 0) {  // region full: the host grows the table, then merges the spills
+        // Rare cases leave the record in the buffer (no global memory op here, so the
+        // prefetched loads stay in flight): the region is full (the host grows the
+        // table), or the record's pane is a third ring position in this flush.  The
+        // spill pass below marks them for k_rgn_collect.
+        if (found < 0) {
             flags |= GW_DF_TABLE_FULL;
             spills++;
-            const_cast<uint8_t*>(rpos)[x] = (uint8_t)(pos | 0x80u);
             return false;
         }
         const int ai = (int)pos == act0 ? 0 : ((int)pos == act1 ? 1 : -1);
-        if (ai >= 0) {
+        if (ai < 0) {
+            spills++;
+            return false;
+        }
+        {
             long long* c = lcell + ((int64_t)ai * S + found) * W;
             lds_cell_add<AGG>(c, c + (W == 2 ? 1 : 0), c0, c1);
-        } else {  // a third pane in one flush: device atomics on this region's cells
-            cell_atomic<AGG>(pt_cell(a.t, (r << a.t.log2S) + found, (int)pos), c0, c1);
         }
-        if constexpr (M) {
-            if (mask_set_bit(lmask, found, msh, pos)) {
-                const int64_t line = (found << msh) >> 7;
-                atomicOr(&s_mdirty[line >> 5], 1u << (line & 31));
-            }
+        if constexpr (M) {  // presence bit: a non-returning LDS OR (the mask is written back whole)
+            const uint64_t bit = ((uint64_t)found << (msh + 3)) + pos;
+            atomicOr((uint32_t*)lmask + (bit >> 5), 1u << (bit & 31));
         }
         return true;
     };
-    // Runs go to waves round-robin; a wave's lanes cover 64 consecutive records of a run,
-    // and kApplyUnroll runs per wave have their loads in flight together.
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+
+    // Records: a wave takes kApplyGroup consecutive runs and walks their records as one
+    // flattened sequence, kApplyUnroll records per lane per step; the loads of the next
+    // step are issued before the current step is applied (one step of software
+    // pipelining), so a wave always has a step of loads in flight.
+    struct Grp {
+        uint32_t pre[kApplyGroup + 1];
+        uint32_t src[kApplyGroup];
+    };
+    struct Step {
+        int64_t key[kApplyUnroll], v0[kApplyUnroll], v1[kApplyUnroll];
+        uint32_t x[kApplyUnroll];
+        uint8_t ps[kApplyUnroll];
+        bool ok[kApplyUnroll];
+    };
     for (int64_t c0r = rb; c0r < re; c0r += kApplyRuns) {
         const int nr = (int)min((int64_t)kApplyRuns, re - c0r);
-        __syncthreads();  // previous step's descriptors fully consumed (and region state staged)
-        for (int i = threadIdx.x; i < nr; i += blockDim.x) {
-            const int64_t rnd = c0r + i;
-            const uint32_t d = rows[rnd * kPartBuckets + ccol];
-            r_cnt[i] = d & 0xffffu;
-            r_src[i] = (single ? rnd * kPartTile : a.r_base[rnd]) + (d >> 16);
+        if (c0r != rb) {
+            __syncthreads();  // previous block's descriptors fully consumed
+            for (int i = threadIdx.x; i < nr; i += blockDim.x) {
+                const int64_t rnd = c0r + i;
+                const uint32_t d = rows[rnd * kPartBuckets + ccol];
+                r_cnt[i] = d & 0xffffu;
+                r_src[i] = (uint32_t)((single ? rnd * kPartTile : a.r_base[rnd]) + (d >> 16));
+            }
         }
-        __syncthreads();
-        // a wave takes kApplyGroup consecutive runs and walks their records as one
-        // flattened sequence, kApplyUnroll records per lane per step (loads in flight
-        // together); the run of a record is found against the group's prefix in registers
-        for (int i0 = wave * kApplyGroup; i0 < nr; i0 += nw * kApplyGroup) {
-            uint32_t pre[kApplyGroup + 1];
-            int64_t src[kApplyGroup];
-            pre[0] = 0;
+        __syncthreads();  // descriptors (and, first time, the region state) in LDS
+        auto load_grp = [&](int i0, Grp& g) {
+            g.pre[0] = 0;
 #pragma unroll
             for (int u = 0; u < kApplyGroup; ++u) {
                 const int i = i0 + u;
-                const uint32_t c = i < nr ? r_cnt[i] : 0u;
-                src[u] = i < nr ? r_src[i] : 0;
-                pre[u + 1] = pre[u] + c;
+                g.pre[u + 1] = g.pre[u] + (i < nr ? r_cnt[i] : 0u);
+                g.src[u] = i < nr ? r_src[i] : 0u;
             }
-            const uint32_t tot = pre[kApplyGroup];
-            for (uint32_t k = 0; k < tot; k += 64 * kApplyUnroll) {  // wave-uniform trip count
-                int64_t key[kApplyUnroll], v0[kApplyUnroll], v1[kApplyUnroll], xs[kApplyUnroll];
-                uint32_t ps[kApplyUnroll];
-                bool ok[kApplyUnroll];
+        };
+        auto load_step = [&](const Grp& g, uint32_t k, Step& s) {
+            const uint32_t tot = g.pre[kApplyGroup];
 #pragma unroll
-                for (int q = 0; q < kApplyUnroll; ++q) {
-                    const uint32_t e = k + q * 64 + lane;
-                    ok[q] = e < tot;
-                    key[q] = 0; v0[q] = 0; v1[q] = 1; ps[q] = 0; xs[q] = 0;
-                    if (ok[q]) {
-                        int u = 0;
+            for (int q = 0; q < kApplyUnroll; ++q) {
+                const uint32_t e = k + q * 64 + lane;
+                s.ok[q] = e < tot;
+                uint32_t sb = g.src[0], sp = 0;  // static indices only: no scratch
 #pragma unroll
-                        for (int w = 1; w < kApplyGroup; ++w) u += e >= pre[w];
-                        const int64_t x = src[u] + (e - pre[u]);
-                        xs[q] = x;
-                        key[q] = rk[x];
-                        v0[q] = ra0[x];
-                        if constexpr (AV) v1[q] = ra1[x];
-                        ps[q] = rpos[x];
+                for (int w = 1; w < kApplyGroup; ++w) {
+                    if (e >= g.pre[w]) { sb = g.src[w]; sp = g.pre[w]; }
+                }
+                // unconditional loads (an idle lane reads record 0): no branch around them,
+                // so the compiler can count them and wait for exactly the ones it needs
+                const uint32_t x = s.ok[q] ? sb + (e - sp) : 0u;
+                s.x[q] = x;
+                s.key[q] = rk[x];
+                s.v0[q] = ra0[x];
+                s.v1[q] = 1;
+                if constexpr (AV) s.v1[q] = ra1[x];
+                s.ps[q] = rpos[x];
+            }
+        };
+        // next non-empty step after (i0, k) (k = ~0u: the first one), wave-uniform
+        auto advance = [&](int& i0, uint32_t& k, Grp& g) -> bool {
+            k = k == ~0u ? 0u : k + 64 * kApplyUnroll;
+            while (i0 < nr && k >= g.pre[kApplyGroup]) {
+                i0 += nw * kApplyGroup;
+                k = 0;
+                if (i0 < nr) load_grp(i0, g);
+            }
+            return i0 < nr;
+        };
+        int i0 = wave * kApplyGroup;
+        uint32_t k = ~0u;
+        Grp g;
+        if (i0 < nr) load_grp(i0, g);
+        Step cur;
+        bool live = advance(i0, k, g);
+        if (live) load_step(g, k, cur);
+        while (live) {
+            int i1 = i0;
+            uint32_t k1 = k;
+            Grp g1 = g;
+            const bool live1 = advance(i1, k1, g1);
+            Step nxt;
+            if (live1) load_step(g1, k1, nxt);
+#pragma unroll
+            for (int q = 0; q < kApplyUnroll; ++q)
+                if (cur.ok[q]) apply_one(cur.key[q], cur.v0[q], cur.v1[q], cur.ps[q], cur.x[q]);
+            cur = nxt;
+            i0 = i1;
+            k = k1;
+            g = g1;
+            live = live1;
+        }
+    }
+    // Spill pass (only in regions that had a spill): the final LDS key table says which
+    // records were not applied: their key is absent (the region was full; no slot ever
+    // frees up) or their ring position is not an active one.  Mark them (pos | 0x80).
+    if (__syncthreads_or(spills != 0)) {
+        unsigned long long marked = 0;
+        for (int64_t c0r = rb; c0r < re; c0r += kApplyRuns) {
+            const int nr = (int)min((int64_t)kApplyRuns, re - c0r);
+            __syncthreads();
+            for (int i = threadIdx.x; i < nr; i += blockDim.x) {
+                const int64_t rnd = c0r + i;
+                const uint32_t d = rows[rnd * kPartBuckets + ccol];
+                r_cnt[i] = d & 0xffffu;
+                r_src[i] = (uint32_t)((single ? rnd * kPartTile : a.r_base[rnd]) + (d >> 16));
+            }
+            __syncthreads();
+            for (int i = wave; i < nr; i += nw) {
+                for (uint32_t k = lane; k < r_cnt[i]; k += 64) {
+                    const uint32_t x = r_src[i] + k;
+                    const int64_t key = rk[x];
+                    const uint32_t pos = rpos[x];
+                    bool present = false;
+                    int64_t g0 = pt_home(a.t, slot_hash(key));
+                    for (int64_t p = 0; p < S; ++p) {
+                        const long long kk = lkeys[g0];
+                        if (kk == key) { present = true; break; }
+                        if (kk == kEmptyKey) break;
+                        g0 = (g0 + 1) & (S - 1);
+                    }
+                    if (!present || ((int)pos != act0 && (int)pos != act1)) {
+                        const_cast<uint8_t*>(rpos)[x] = (uint8_t)(pos | 0x80u);
+                        marked++;
                     }
                 }
-#pragma unroll
-                for (int q = 0; q < kApplyUnroll; ++q)
-                    if (ok[q]) apply_one(key[q], v0[q], v1[q], ps[q], xs[q]);
             }
         }
+        spills = marked;
     }
     __syncthreads();
     // write back: dirty 128-B lines of keys / mask, every line of the active pane arrays
@@ -843,14 +956,7 @@ __global__ void __launch_bounds__(512) k_rgn_apply(IngestArgs a) {
             if (s_kdirty[line >> 5] & (1u << (line & 31))) dk[w] = sk[w];
         }
     }
-    if constexpr (M) {
-        const long2* sm = reinterpret_cast<const long2*>(lmask);
-        long2* dm = reinterpret_cast<long2*>(gmask);
-        for (int64_t w = threadIdx.x; w < MW / 2; w += blockDim.x) {
-            const int64_t line = w >> 3;
-            if (s_mdirty[line >> 5] & (1u << (line & 31))) dm[w] = sm[w];
-        }
-    }
+    if constexpr (M) copy_words((long long*)gmask, (const long long*)lmask, MW);
     for (int ai = 0; ai < 2; ++ai) {
         const int p = ai ? act1 : act0;
         if (p < 0) continue;

@@ -24,6 +24,8 @@ namespace {
 
 thread_local std::string g_create_error;
 
+constexpr int64_t kMaxIngest = (int64_t)1 << 30;  // records per region-path batch / buffer
+
 typedef __int128 i128;
 
 i128 floor_div(i128 a, i128 b) {  // b > 0
@@ -604,12 +606,13 @@ struct gw_handle {
         stats.applies++;
         dirty = true;
         if ((rc = refresh())) return rc;
-        if (h_st->spills) {  // full regions left records in the buffer: park them
+        if (h_st->spills) {  // full regions / a third ring position left records: park them
             if ((rc = ensure_deferred((int64_t)h_st->n_deferred + (int64_t)h_st->spills))) return rc;
             if ((rc = set_field(offsetof(DevStatus, spills), 0))) return rc;
             HIPCHECK(launch_region_collect(a, stream));
             dirty = true;
             if ((rc = refresh())) return rc;
+            if (!(h_st->flags & GW_DF_TABLE_FULL) && (rc = merge_deferred())) return rc;
         }
         if (h_st->flags & GW_DF_TABLE_FULL) {
             if ((rc = maybe_grow(0))) return rc;
@@ -786,6 +789,7 @@ int gw_create(const gw_config* cfg, gw_handle** out) {
     if (const char* u = getenv("GW_INGEST_UNROLL")) h->ingest_unroll = atoi(u);
     if (const char* u = getenv("GW_REGION_MIN_BATCH")) h->region_min_batch = atoll(u);
     if (const char* u = getenv("GW_BUFFER_RECORDS")) h->buf_limit = std::max<int64_t>(atoll(u), 1);
+    h->buf_limit = std::min<int64_t>(h->buf_limit, kMaxIngest);  // buffer offsets stay below 2^32
     if (h->cfg.max_parallelism <= 0) h->cfg.max_parallelism = 128;
     if (h->cfg.parallelism <= 0) h->cfg.parallelism = 1;
     if (h->cfg.max_batch <= 0) h->cfg.max_batch = 1 << 20;
@@ -885,7 +889,13 @@ static int ingest_device_impl(gw_handle* h, int64_t n, const int64_t* key, const
         else if (rc == GW_E_DEVICE || rc == GW_E_NO_TIMESTAMP || rc == GW_E_RANGE) h->failed = true;
         return rc;
     }
-    return h->ingest_pane(n, key, ts, val);
+    // the region buffer indexes records with 32-bit offsets: split very large calls
+    for (int64_t off = 0; off < n; off += kMaxIngest) {
+        const int64_t c = std::min<int64_t>(kMaxIngest, n - off);
+        int rc = h->ingest_pane(c, key + off, ts + off, val ? val + off : nullptr);
+        if (rc) return rc;
+    }
+    return GW_OK;
 }
 
 int gw_ingest(gw_handle* h, int64_t n, const int64_t* key, const int32_t* key_hash, const int64_t* ts,
