@@ -34,6 +34,8 @@
 #include "gw_kernels.h"
 
 #include <algorithm>
+#include <mutex>
+#include <vector>
 
 namespace gw {
 
@@ -765,9 +767,11 @@ __global__ void __launch_bounds__(512) k_rgn_apply(IngestArgs a) {
         // Probe one 4-key group (32 B) per step: the first slot holding the key or
         // empty, in slot order, decides; an empty slot is claimed with a CAS (a lost race
         // re-reads the same group).
-        int64_t g0 = pt_home(a.t, slot_hash(key));
-        int64_t found = -1;
-        for (int64_t p = 0; p < S;) {
+        // 32-bit LDS indices (S <= 2048 slots)
+        const int Si = (int)S;
+        int g0 = (int)pt_home(a.t, slot_hash(key));
+        int found = -1;
+        for (int p = 0; p < Si;) {
             const long2 k01 = *reinterpret_cast<const long2*>(&lkeys[g0]);
             const long2 k23 = *reinterpret_cast<const long2*>(&lkeys[g0 + 2]);
             const uint32_t hit = (uint32_t)(k01.x == key) | (uint32_t)(k01.y == key) << 1 |
@@ -777,7 +781,7 @@ __global__ void __launch_bounds__(512) k_rgn_apply(IngestArgs a) {
             const uint32_t m = hit | emp;
             if (m) {
                 const int i = __ffs((int)m) - 1;
-                const int64_t j = g0 + i;
+                const int j = g0 + i;
                 if ((hit >> i) & 1) { found = j; break; }
                 const unsigned long long prev = atomicCAS((unsigned long long*)&lkeys[j],
                                                           (unsigned long long)kEmptyKey, (unsigned long long)key);
@@ -790,7 +794,7 @@ __global__ void __launch_bounds__(512) k_rgn_apply(IngestArgs a) {
                 if ((int64_t)prev == key) { found = j; break; }
                 continue;  // another key took the slot: re-read this group
             }
-            g0 = (g0 + kProbeGroup) & (S - 1);
+            g0 = (g0 + kProbeGroup) & (Si - 1);
             p += kProbeGroup;
         }
         // Rare cases leave the record in the buffer (no global memory op here, so the
@@ -808,11 +812,11 @@ __global__ void __launch_bounds__(512) k_rgn_apply(IngestArgs a) {
             return false;
         }
         {
-            long long* c = lcell + ((int64_t)ai * S + found) * W;
-            lds_cell_add<AGG>(c, c + (W == 2 ? 1 : 0), c0, c1);
+            long long* c = lcell + (ai * Si + found) * (AV ? 2 : 1);
+            lds_cell_add<AGG>(c, c + (AV ? 1 : 0), c0, c1);
         }
         if constexpr (M) {  // presence bit: a non-returning LDS OR (the mask is written back whole)
-            const uint64_t bit = ((uint64_t)found << (msh + 3)) + pos;
+            const uint32_t bit = ((uint32_t)found << (msh + 3)) + pos;
             atomicOr((uint32_t*)lmask + (bit >> 5), 1u << (bit & 31));
         }
         return true;
@@ -1258,6 +1262,18 @@ hipError_t launch_ingest(const IngestArgs& a, int path, int unroll, hipStream_t 
     return hipGetLastError();
 }
 
+// Opt a kernel in to more than 64 KB of dynamic LDS (gfx950 has 160 KB per CU) once per
+// size, not per launch: the attribute call costs host time on every ingest otherwise.
+static void lds_opt_in(const void* f, size_t bytes) {
+    static std::mutex mu;
+    static std::vector<std::pair<const void*, size_t>> done;
+    std::lock_guard<std::mutex> lock(mu);
+    for (auto& d : done)
+        if (d.first == f && d.second >= bytes) return;
+    hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+    done.emplace_back(f, bytes);
+}
+
 static size_t part_lds_bytes(const IngestArgs& a) {
     return (size_t)kPartTile * 8 * (a.t.words == 2 ? 3 : 2) + 2 * kPartTile;
 }
@@ -1271,7 +1287,7 @@ hipError_t launch_region_p1(const IngestArgs& a, hipStream_t s) {
     const size_t part_lds = part_lds_bytes(a);
     // beyond the 64 KB default: opt in (gfx950 has 160 KB of LDS per CU)
 #define L(A)                                                                                                    \
-    hipFuncSetAttribute((const void*)k_rgn_p1<A>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)part_lds);   \
+    lds_opt_in((const void*)k_rgn_p1<A>, part_lds);                                                            \
     hipLaunchKernelGGL(k_rgn_p1<A>, dim3((unsigned)tiles), dim3(kPartThreads), part_lds, s, a)
     GW_AGG_SWITCH(a.t.agg, L);
 #undef L
@@ -1288,8 +1304,8 @@ hipError_t launch_region_flush(const IngestArgs& a, hipStream_t s) {
     const int nb1 = 1 << a.d1_bits;
     if (a.ntiles == 0) return hipSuccess;
 #define L(A)                                                                                                    \
-    hipFuncSetAttribute((const void*)k_rgn_p2<A>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)part_lds);   \
-    hipFuncSetAttribute((const void*)k_rgn_apply<A>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)apply_lds); \
+    lds_opt_in((const void*)k_rgn_p2<A>, part_lds);                                                            \
+    lds_opt_in((const void*)k_rgn_apply<A>, apply_lds);                                                        \
     if (!single) {                                                                                              \
         hipLaunchKernelGGL(k_rgn_plan1, dim3((unsigned)a.ngroups), dim3(256), 0, s, a);                        \
         hipLaunchKernelGGL(k_rgn_plan2, dim3((unsigned)nb1), dim3(256), 0, s, a);                              \

@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -25,6 +26,28 @@ namespace {
 thread_local std::string g_create_error;
 
 constexpr int64_t kMaxIngest = (int64_t)1 << 30;  // records per region-path batch / buffer
+
+// Host-time profile of the ingest path (GW_HOST_PROFILE=1: printed by gw_destroy).
+struct HostProf {
+    bool on = getenv("GW_HOST_PROFILE") != nullptr;
+    double t[8] = {};
+    int64_t n[8] = {};
+    std::chrono::steady_clock::time_point last;
+    void mark() { if (on) last = std::chrono::steady_clock::now(); }
+    void lap(int i) {
+        if (!on) return;
+        auto now = std::chrono::steady_clock::now();
+        t[i] += std::chrono::duration<double, std::micro>(now - last).count();
+        n[i]++;
+        last = now;
+    }
+    void dump() {
+        if (!on) return;
+        static const char* names[8] = {"prep", "launch", "status-enqueue", "status-wait", "absorb", "api-entry", "-", "-"};
+        for (int i = 0; i < 8; ++i)
+            if (n[i]) fprintf(stderr, "[gw host] %-15s %8.2f us x %lld\n", names[i], t[i] / n[i], (long long)n[i]);
+    }
+};
 
 typedef __int128 i128;
 
@@ -160,6 +183,7 @@ struct gw_handle {
     gw_stats stats{};
     bool timing = false;
     KernelTimer t_ingest, t_fire, t_apply;
+    HostProf hp;
 
     SessionState* sess = nullptr;
     int ingest_unroll = 2;  // records per thread per iteration of k_ingest (GW_INGEST_UNROLL)
@@ -183,12 +207,68 @@ struct gw_handle {
 
     bool dirty = true;  // device counters changed since the last refresh()
 
+    // Lazy status (buffered region P1 only): after a P1 launch the status is copied
+    // asynchronously; the copy of batch b is read while batch b + 1 is already queued,
+    // so the GPU does not wait for the host between watermark batches.  h_st then lags
+    // by the last batch (`lazy`): decisions that need exact counters call refresh().
+    static constexpr int kAsync = 3;  // status copies in flight: absorb the one 2 batches old
+    DevStatus* h_st_async[kAsync] = {};
+    hipEvent_t st_ev[kAsync] = {};      // status copy done (side stream)
+    hipEvent_t p1_ev[kAsync] = {};      // P1 done (operator stream)
+    hipStream_t st_stream = nullptr;
+    bool async_pending[kAsync] = {};
+    uint64_t async_gen[kAsync] = {};
+    int64_t async_recs[kAsync] = {};    // records of the batch each copy follows
+    uint64_t hgen = 0;        // host writes to the status (a snapshot older than one is stale)
+    int async_slot = 0;
+    bool lazy = false;        // launches since the last exact status: region P1 only
+    int64_t lazy_recs = 0;    // records of those launches (bound on their deferred entries)
+
     int refresh() {
         HIPCHECK(hipMemcpyAsync(h_st, d_st, sizeof(DevStatus), hipMemcpyDeviceToHost, stream));
         HIPCHECK(hipStreamSynchronize(stream));
-        fold_shards(h_st);
+        for (auto& p : async_pending) p = false;  // older than this copy
+        lazy = false;
+        lazy_recs = 0;
         dirty = false;
         if (timing) { t_ingest.resolve(); t_fire.resolve(); t_apply.resolve(); }
+        return absorb();
+    }
+    // Queue an asynchronous status copy after the last launch; absorb the previous one
+    // (complete by now: this batch is queued behind it).
+    // The copy runs on a side stream after an event on the operator stream, so the next
+    // batch's P1 follows this one back-to-back; it may also see part of the next batch,
+    // which the bounds below allow (the counters only grow).
+    int lazy_status(int64_t nrec) {
+        const int s = async_slot;
+        hp.lap(1);
+        HIPCHECK(hipEventRecord(p1_ev[s], stream));
+        HIPCHECK(hipStreamWaitEvent(st_stream, p1_ev[s], 0));
+        HIPCHECK(hipMemcpyAsync(h_st_async[s], d_st, sizeof(DevStatus), hipMemcpyDeviceToHost, st_stream));
+        HIPCHECK(hipEventRecord(st_ev[s], st_stream));
+        async_pending[s] = true;
+        async_gen[s] = hgen;
+        async_recs[s] = nrec;
+        async_slot = (s + 1) % kAsync;
+        lazy = true;
+        lazy_recs += nrec;
+        const int o = async_slot;  // the oldest copy
+        hp.lap(2);
+        if (!async_pending[o]) return GW_OK;
+        async_pending[o] = false;
+        HIPCHECK(hipEventSynchronize(st_ev[o]));
+        hp.lap(3);
+        if (async_gen[o] != hgen) return GW_OK;  // the host changed the status since
+        memcpy(h_st, h_st_async[o], sizeof(DevStatus));
+        lazy_recs = 0;  // the batches after the absorbed copy are unaccounted for
+        for (int i = 0; i < kAsync; ++i)
+            if (async_pending[i]) lazy_recs += async_recs[i];
+        const int rc = absorb();
+        hp.lap(4);
+        return rc;
+    }
+    int absorb() {
+        fold_shards(h_st);
         if (h_st->flags & GW_DF_NO_TS)
             return fail(GW_E_NO_TIMESTAMP,
                         "Record has Long.MIN_VALUE timestamp (= no timestamp marker). Did you forget to "
@@ -202,15 +282,17 @@ struct gw_handle {
         stats.session_merges = (int64_t)h_st->merges;
         return GW_OK;
     }
-    int ensure_fresh() { return dirty ? refresh() : GW_OK; }
+    int ensure_fresh() { return dirty || lazy ? refresh() : GW_OK; }
     // Write one scalar status word, ordered on the stream (no host sync).
     int set_field(size_t off, unsigned long long v) {
+        hgen++;
         *reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(h_st) + off) = v;
         HIPCHECK(launch_status_set(d_st, (int)(off / 8), v, -1, stream));
         return GW_OK;
     }
     // Zero one field of every counter shard (field index within ShardCtr).
     int zero_shards(int field) {
+        hgen++;
         for (int i = 0; i < kShards; ++i) reinterpret_cast<unsigned long long*>(&h_st->sh[i])[field] = 0;
         HIPCHECK(launch_status_set(d_st, 0, 0, field, stream));
         dirty = true;
@@ -285,7 +367,8 @@ struct gw_handle {
             HIPCHECK(hipMalloc((void**)&n0, nc * 8));
             HIPCHECK(hipMalloc((void**)&n1, nc * 8));
             if (dk[b] && b == cur) {
-                const int64_t used = (int64_t)h_st->n_deferred;
+                // a lagging status does not know the last batch's entries: copy them all
+                const int64_t used = lazy ? def_cap : (int64_t)h_st->n_deferred;
                 if (used) {
                     HIPCHECK(hipMemcpyAsync(nk, dk[b], used * 8, hipMemcpyDeviceToDevice, stream));
                     HIPCHECK(hipMemcpyAsync(np, dp[b], used * 8, hipMemcpyDeviceToDevice, stream));
@@ -623,9 +706,9 @@ struct gw_handle {
 
     int ingest_pane(int64_t nrec, const int64_t* key, const int64_t* ts, const int64_t* val) {
         int rc;
-        if ((rc = ensure_fresh())) return rc;
+        if (dirty && (rc = refresh())) return rc;  // a lagging (lazy) status is fine here
         if ((rc = maybe_grow(nrec))) return rc;
-        if ((rc = ensure_deferred((int64_t)h_st->n_deferred + nrec))) return rc;
+        if ((rc = ensure_deferred((int64_t)h_st->n_deferred + lazy_recs + nrec))) return rc;
         IngestArgs a;
         if ((rc = base_args(a, nrec, key, ts, val))) return rc;
         // path: LDS pre-aggregation when the batch repeats few keys many times; region
@@ -665,6 +748,7 @@ struct gw_handle {
                 HIPCHECK(hipMemsetAsync(d_tmp + 1, 0, 8, stream));
                 buf_fresh = ~occ;
             }
+            hp.lap(0);
             if (timing) {
                 auto ev = t_ingest.get();
                 HIPCHECK(hipEventRecord(ev.first, stream));
@@ -688,13 +772,19 @@ struct gw_handle {
         }
         stats.events_in += nrec;
         stats.batches++;
+        if (path == 2 && nseg) {  // buffered P1: no host sync (it writes no table cell)
+            if ((rc = lazy_status(nrec))) return rc;
+            if (occ || !h_st->n_deferred) return GW_OK;
+        }
         dirty = true;
-        if ((rc = refresh())) return rc;  // the one host sync of an ingest call
+        if ((rc = refresh())) return rc;  // the host sync of an unbuffered ingest call
         if (h_st->flags & GW_DF_TABLE_FULL) {
             if ((rc = maybe_grow(0))) return rc;
             if ((rc = merge_deferred())) return rc;
         }
-        // An empty ring with parked records: jump the ring to the data.
+        // An empty ring with parked records: jump the ring to the data (the buffer holds
+        // no in-ring record then; apply it before the ring moves all the same).
+        if (!occ && h_st->n_deferred && nseg && (rc = flush_buffer())) return rc;
         if (!occ && h_st->n_deferred) {
             i128 dmin;
             if ((rc = deferred_min(dmin))) return rc;
@@ -808,6 +898,14 @@ int gw_create(const gw_config* cfg, gw_handle** out) {
         return bail(GW_E_DEVICE, std::string("status alloc: ") + hipGetErrorString(e));
     hipMemset(h->d_st, 0, sizeof(DevStatus));
     memset(h->h_st, 0, sizeof(DevStatus));
+    for (int i = 0; i < gw_handle::kAsync; ++i) {
+        if ((e = hipHostMalloc((void**)&h->h_st_async[i], sizeof(DevStatus), hipHostMallocDefault)) != hipSuccess ||
+            (e = hipEventCreateWithFlags(&h->st_ev[i], hipEventDisableTiming)) != hipSuccess ||
+            (e = hipEventCreateWithFlags(&h->p1_ev[i], hipEventDisableTiming)) != hipSuccess)
+            return bail(GW_E_DEVICE, std::string("status alloc: ") + hipGetErrorString(e));
+    }
+    if ((e = hipStreamCreateWithFlags(&h->st_stream, hipStreamNonBlocking)) != hipSuccess)
+        return bail(GW_E_DEVICE, std::string("hipStreamCreate: ") + hipGetErrorString(e));
 
     const int agg = cfg->agg;
     const int words = cell_words(agg);
@@ -860,7 +958,9 @@ int gw_create(const gw_config* cfg, gw_handle** out) {
 
 int gw_destroy(gw_handle* h) {
     if (!h) return GW_OK;
+    h->hp.dump();
     if (h->stream) hipStreamSynchronize(h->stream);
+    if (h->st_stream) hipStreamSynchronize(h->st_stream);  // a status copy may still read d_st
     if (h->sess) session_destroy(h->sess);
     if (h->tv.base) hipFree(h->tv.base);
     for (int b = 0; b < 2; ++b) {
@@ -873,6 +973,12 @@ int gw_destroy(gw_handle* h) {
     if (h->d_st) hipFree(h->d_st);
     if (h->d_tmp) hipFree(h->d_tmp);
     if (h->h_st) hipHostFree(h->h_st);
+    for (int i = 0; i < gw_handle::kAsync; ++i) {
+        if (h->h_st_async[i]) hipHostFree(h->h_st_async[i]);
+        if (h->st_ev[i]) hipEventDestroy(h->st_ev[i]);
+        if (h->p1_ev[i]) hipEventDestroy(h->p1_ev[i]);
+    }
+    if (h->st_stream) hipStreamDestroy(h->st_stream);
     h->t_ingest.destroy();
     h->t_fire.destroy();
     h->t_apply.destroy();
@@ -928,6 +1034,7 @@ int gw_ingest(gw_handle* h, int64_t n, const int64_t* key, const int32_t* key_ha
 int gw_ingest_device(gw_handle* h, int64_t n, const int64_t* d_key, const int32_t* d_key_hash,
                      const int64_t* d_ts, const void* d_value, void* stream) {
     if (!h) return GW_E_INVALID;
+    h->hp.mark();
     if (h->failed) return h->fail(GW_E_STATE, "operator failed earlier: %s", h->err.c_str());
     if (n < 0 || (n > 0 && (!d_key || !d_ts))) return h->fail(GW_E_INVALID, "null key/ts column");
     if (n > 0 && !d_value && h->cfg.agg != GW_COUNT) return h->fail(GW_E_INVALID, "value column required");
@@ -941,6 +1048,7 @@ int gw_ingest_device(gw_handle* h, int64_t n, const int64_t* d_key, const int32_
         hipEventDestroy(ev);
     }
     if (n == 0) return GW_OK;
+    h->hp.lap(5);
     return ingest_device_impl(h, n, d_key, d_ts, (const int64_t*)d_value);
 }
 
@@ -1042,6 +1150,7 @@ int gw_clear_rows(gw_handle* h) {
     if (!h) return GW_E_INVALID;
     h->rows_head = 0;
     if (h->session) return session_clear_rows(h->sess, h->err);
+    if (h->h_st->rows == 0) return GW_OK;  // rows only grow in a fire, which refreshes h_st
     return h->set_field(offsetof(DevStatus, rows), 0);
 }
 
