@@ -159,7 +159,7 @@ def main():
             pk, pt, pv, counts = ex.partition(k, t, v, stream=cur)
             (k, t, v), n_recv = ex.exchange_partitioned([pk, pt, pv], counts)
             if timed:
-                exch_bytes += (nb - int(counts[rank].item())) * b_in
+                exch_bytes += (nb - ex.last_send_counts[rank]) * b_in
         n = k.numel()
         N.check(N.lib().gw_ingest_device(op.handle, n, k.data_ptr(), None, t.data_ptr(),
                                          v.data_ptr() if v is not None else None, cur), op.handle)

@@ -29,6 +29,13 @@ class KeyByExchange:
         self.device = device
         self._scratch = None
         self._bufs = {}
+        # Watermarks are control-plane data: combining them over a host (gloo) group keeps
+        # the per-batch minimum off the GPU streams (an RCCL all-reduce + .item() would
+        # wait for the column all-to-all queued before it).
+        self._wm_group = None
+        if dist.is_initialized() and dist.get_backend(group) != "gloo":
+            self._wm_group = dist.new_group(backend="gloo")
+        self.last_send_counts: list = []
 
     # ---------------------------------------------------------------- partition
     def partition(self, keys: torch.Tensor, ts: torch.Tensor, vals: Optional[torch.Tensor],
@@ -65,6 +72,7 @@ class KeyByExchange:
         dist.all_to_all_single(recv_counts, send_counts, group=self.group)
         sc = send_counts.tolist()
         rc = recv_counts.tolist()
+        self.last_send_counts = sc
         total = int(sum(rc))
         out = []
         for c in cols:
@@ -83,12 +91,9 @@ class KeyByExchange:
 
     # ---------------------------------------------------------------- watermark
     def combine_watermark(self, wm: int) -> int:
-        """Minimum over all ranks (StatusWatermarkValve)."""
-        dev = self.device if self.device is not None else torch.device("cpu")
-        if dist.get_backend(self.group) == "gloo":
-            dev = torch.device("cpu")
-        t = torch.tensor([wm], dtype=torch.int64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MIN, group=self.group)
+        """Minimum over all ranks (StatusWatermarkValve), on a host (gloo) group."""
+        t = torch.tensor([wm], dtype=torch.int64)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN, group=self._wm_group if self._wm_group is not None else self.group)
         return int(t.item())
 
     def key_group_range(self):
