@@ -205,6 +205,25 @@ struct EvictArgs {
     DevStatus* st;
 };
 
+struct SnapArgs {
+    PaneTable t;
+    uint64_t occ;                  // ring positions that may hold data
+    int64_t pane_of_pos[kMaxRing]; // pane index held by each ring position
+    const int64_t* d_key;          // deferred list
+    const int64_t* d_pane;
+    const int64_t* d_a0;
+    const int64_t* d_a1;
+    int64_t n_def;
+    int32_t max_p, kg_lo, kg_hi;
+    int64_t* o_key;                // collected entries (append at *n_out)
+    int64_t* o_pane;
+    int64_t* o_a0;
+    int64_t* o_a1;
+    int32_t* o_kg;
+    unsigned long long* n_out;
+};
+hipError_t launch_snap_collect(const SnapArgs& a, hipStream_t s);
+
 hipError_t launch_table_init(const PaneTable& t, hipStream_t s);
 // path: 0 direct atomics, 1 LDS pre-aggregation (the region path has its own launchers)
 hipError_t launch_ingest(const IngestArgs& a, int path, int unroll, hipStream_t s);

@@ -1196,6 +1196,50 @@ __global__ void __launch_bounds__(256) k_count_live(PaneTable t, unsigned long l
     if (__lane_id() == 0 && c) atomicAdd(out, c);
 }
 
+// Snapshot (gw_snapshot): every non-null pane cell of the table and every deferred entry
+// whose key group lies in [kg_lo, kg_hi] -> (key, pane, a0, a1, kg) entries.
+template <int AGG>
+__global__ void __launch_bounds__(256) k_snap_collect(SnapArgs a) {
+    const int64_t nslots = a.t.cap + 1;
+    const int W = a.t.words;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    const int64_t total = nslots + a.n_def;
+    for (int64_t base = blockIdx.x * (int64_t)blockDim.x; base < total; base += stride) {
+        const int64_t i = base + threadIdx.x;
+        uint64_t m = 0;
+        int64_t key = 0;
+        int32_t kg = -1;
+        bool def = false;
+        if (i < nslots) {
+            key = i == a.t.cap ? kEmptyKey : *pt_key(a.t, i);
+            m = presence<AGG>(a.t, i) & a.occ;
+        } else if (i < total) {
+            key = a.d_key[i - nslots];
+            def = true;
+        }
+        if (m || def) {
+            kg = key_group_for_hash(java_long_hash(key), a.max_p);
+            if (kg < a.kg_lo || kg > a.kg_hi) { m = 0; def = false; }
+        }
+        const unsigned cnt = def ? 1u : (unsigned)__popcll(m);
+        unsigned long long off = wave_reserve_n(a.n_out, cnt);
+        if (def) {
+            const int64_t j = i - nslots;
+            a.o_key[off] = key; a.o_pane[off] = a.d_pane[j]; a.o_a0[off] = a.d_a0[j]; a.o_a1[off] = a.d_a1[j];
+            a.o_kg[off] = kg;
+        }
+        while (m) {
+            const int pos = __ffsll((long long)m) - 1;
+            m &= m - 1;
+            const int64_t* c = pt_cell(a.t, i, pos);
+            a.o_key[off] = key; a.o_pane[off] = a.pane_of_pos[pos];
+            a.o_a0[off] = c[0]; a.o_a1[off] = W == 2 ? c[1] : 0;
+            a.o_kg[off] = kg;
+            off++;
+        }
+    }
+}
+
 // Status word writes, ordered on the stream (no host sync).
 __global__ void k_status_set(DevStatus* st, int word, unsigned long long v, int shard_field) {
     if (shard_field >= 0) {
@@ -1355,6 +1399,13 @@ hipError_t launch_evict(const EvictArgs& a, hipStream_t s) {
 
 hipError_t launch_status_set(DevStatus* st, int word, unsigned long long v, int shard_field, hipStream_t s) {
     hipLaunchKernelGGL(k_status_set, dim3(1), dim3(64), 0, s, st, word, v, shard_field);
+    return hipGetLastError();
+}
+
+hipError_t launch_snap_collect(const SnapArgs& a, hipStream_t s) {
+#define L(A) hipLaunchKernelGGL(k_snap_collect<A>, dim3(grid_for(a.t.cap + 1 + a.n_def)), dim3(256), 0, s, a)
+    GW_AGG_SWITCH(a.t.agg, L);
+#undef L
     return hipGetLastError();
 }
 

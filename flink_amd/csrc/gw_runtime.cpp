@@ -795,6 +795,141 @@ struct gw_handle {
         return GW_OK;
     }
 
+    // ---------------------------------------------------------------- snapshot
+    // Blob (little-endian): SnapHeader, int64 kg_offsets[kg_hi - kg_lo + 2] (first entry
+    // of each key group), then SnapEntry entries sorted by key group.
+    struct SnapHeader {
+        char magic[4];
+        uint32_t version;
+        int32_t agg, assigner;
+        int64_t size, slide, offset, gap, pane;
+        int32_t max_parallelism, kg_lo, kg_hi, reserved;
+        int64_t fired_lo, fired_hi;  // first window not fired yet (int128): the timer state
+        int64_t entries;
+    };
+    bool restored = false;
+    struct SnapEntry {
+        int64_t key, pane, a0, a1;
+    };
+
+    int snapshot(int32_t kg_lo, int32_t kg_hi, void* buf, int64_t cap, int64_t* len) {
+        int rc;
+        if (kg_lo < 0 || kg_hi < kg_lo || kg_hi >= cfg.max_parallelism)
+            return fail(GW_E_INVALID, "key-group range [%d, %d] outside [0, %d)", kg_lo, kg_hi, cfg.max_parallelism);
+        if ((rc = ensure_fresh())) return rc;
+        if ((rc = flush_buffer())) return rc;  // prepareSnapshotPreBarrier: buffered records first
+        if ((rc = refresh())) return rc;
+        const int64_t n_def = (int64_t)h_st->n_deferred;
+        const int64_t bound = ((int64_t)h_st->used_slots + 1) * popcount(occ) + n_def;
+        std::vector<SnapEntry> ents;
+        std::vector<int32_t> kgs;
+        if (bound > 0) {
+            int64_t* d = nullptr;
+            HIPCHECK(hipMalloc((void**)&d, (size_t)bound * 36));
+            SnapArgs a{};
+            a.t = tv;
+            a.occ = occ;
+            for (i128 p = B; p < B + R; ++p) a.pane_of_pos[pos_of(p)] = (int64_t)p;
+            a.d_key = dk[cur]; a.d_pane = dp[cur]; a.d_a0 = da0[cur]; a.d_a1 = da1[cur];
+            a.n_def = n_def;
+            a.max_p = cfg.max_parallelism; a.kg_lo = kg_lo; a.kg_hi = kg_hi;
+            a.o_key = d; a.o_pane = d + bound; a.o_a0 = d + 2 * bound; a.o_a1 = d + 3 * bound;
+            a.o_kg = (int32_t*)(d + 4 * bound);
+            a.n_out = d_tmp + 2;  // 8-B aligned scratch word (64-bit atomic)
+            hipError_t e = hipMemsetAsync(a.n_out, 0, 8, stream);
+            if (e == hipSuccess) e = launch_snap_collect(a, stream);
+            unsigned long long n = 0;
+            if (e == hipSuccess) e = hipMemcpyAsync(&n, a.n_out, 8, hipMemcpyDeviceToHost, stream);
+            if (e == hipSuccess) e = hipStreamSynchronize(stream);
+            std::vector<int64_t> col[4];
+            if (e == hipSuccess) {
+                kgs.resize(n);
+                for (int c = 0; c < 4 && e == hipSuccess; ++c) {
+                    col[c].resize(n);
+                    if (n) e = hipMemcpy(col[c].data(), d + c * bound, n * 8, hipMemcpyDeviceToHost);
+                }
+                if (n && e == hipSuccess) e = hipMemcpy(kgs.data(), a.o_kg, n * 4, hipMemcpyDeviceToHost);
+            }
+            hipFree(d);
+            if (e != hipSuccess) return fail(GW_E_DEVICE, "snapshot: %s", hipGetErrorString(e));
+            ents.resize(n);
+            for (size_t i = 0; i < n; ++i) ents[i] = SnapEntry{col[0][i], col[1][i], col[2][i], col[3][i]};
+        }
+        // counting sort by key group
+        const int nk = kg_hi - kg_lo + 1;
+        std::vector<int64_t> offs(nk + 1, 0);
+        for (int32_t k : kgs) offs[k - kg_lo + 1]++;
+        for (int i = 0; i < nk; ++i) offs[i + 1] += offs[i];
+        const int64_t need = (int64_t)sizeof(SnapHeader) + (int64_t)(nk + 1) * 8 + (int64_t)ents.size() * 32;
+        *len = need;
+        if (!buf) return GW_OK;
+        if (cap < need) return fail(GW_E_OUTPUT_FULL, "snapshot needs %lld bytes", (long long)need);
+        SnapHeader hd{};
+        memcpy(hd.magic, "GWS1", 4);
+        hd.version = 1;
+        hd.agg = cfg.agg; hd.assigner = cfg.assigner;
+        hd.size = cfg.size; hd.slide = slide(); hd.offset = cfg.offset; hd.gap = cfg.gap; hd.pane = g;
+        hd.max_parallelism = cfg.max_parallelism; hd.kg_lo = kg_lo; hd.kg_hi = kg_hi;
+        hd.fired_lo = (int64_t)(uint64_t)fired_k;
+        hd.fired_hi = (int64_t)(fired_k >> 64);
+        hd.entries = (int64_t)ents.size();
+        char* out = (char*)buf;
+        memcpy(out, &hd, sizeof hd);
+        memcpy(out + sizeof hd, offs.data(), (nk + 1) * 8);
+        SnapEntry* oe = (SnapEntry*)(out + sizeof hd + (nk + 1) * 8);
+        std::vector<int64_t> fill(offs.begin(), offs.end() - 1);
+        for (size_t i = 0; i < ents.size(); ++i) oe[fill[kgs[i] - kg_lo]++] = ents[i];
+        return GW_OK;
+    }
+
+    // Restore: the entries become deferred partial aggregates and merge like parked
+    // records (exact for every aggregate); the watermark stays Long.MIN_VALUE, as in
+    // Flink after initializeState.
+    int restore(const void* buf, int64_t len) {
+        int rc;
+        if (!buf || len < (int64_t)sizeof(SnapHeader)) return fail(GW_E_INVALID, "snapshot blob too short");
+        SnapHeader hd;
+        memcpy(&hd, buf, sizeof hd);
+        if (memcmp(hd.magic, "GWS1", 4) != 0 || hd.version != 1) return fail(GW_E_INVALID, "not a gpuwin snapshot");
+        if (hd.agg != cfg.agg || hd.assigner != cfg.assigner || hd.size != cfg.size || hd.slide != slide() ||
+            hd.offset != cfg.offset || hd.pane != g || hd.max_parallelism != cfg.max_parallelism)
+            return fail(GW_E_INVALID, "snapshot of a different window / aggregate / max parallelism");
+        const int nk = hd.kg_hi - hd.kg_lo + 1;
+        const int64_t need = (int64_t)sizeof hd + (int64_t)(nk + 1) * 8 + hd.entries * 32;
+        if (nk <= 0 || hd.entries < 0 || len < need) return fail(GW_E_INVALID, "truncated snapshot blob");
+        // Windows fired before the snapshot stay fired (Flink restores no timer for them).
+        // Every blob restored into one handle must come from the same fired position.
+        const i128 fk = ((i128)hd.fired_hi << 64) | (i128)(uint64_t)hd.fired_lo;
+        if (!restored && stats.events_in == 0) {
+            if (fk > fired_k) fired_k = fk;
+            if (B < fired_k * m) B = fired_k * m;
+            restored = true;
+        } else if (fk != fired_k) {
+            return fail(GW_E_UNSUPPORTED, "snapshot blobs at different fired windows cannot be merged into one operator");
+        }
+        if (hd.entries == 0) return GW_OK;
+        if ((rc = ensure_fresh())) return rc;
+        if (nseg && (rc = flush_buffer())) return rc;
+        const int64_t nd = (int64_t)h_st->n_deferred;
+        if ((rc = ensure_deferred(nd + hd.entries))) return rc;
+        const SnapEntry* in = (const SnapEntry*)((const char*)buf + sizeof hd + (nk + 1) * 8);
+        std::vector<int64_t> col(hd.entries);
+        int64_t* dst[4] = {dk[cur], dp[cur], da0[cur], da1[cur]};
+        for (int c = 0; c < 4; ++c) {
+            for (int64_t i = 0; i < hd.entries; ++i) col[i] = (&in[i].key)[c];
+            HIPCHECK(hipMemcpy(dst[c] + nd, col.data(), hd.entries * 8, hipMemcpyHostToDevice));
+        }
+        if ((rc = set_field(offsetof(DevStatus, n_deferred), (unsigned long long)(nd + hd.entries)))) return rc;
+        dirty = true;
+        if ((rc = refresh())) return rc;
+        if (!occ) {  // nothing in the ring yet: start it at the oldest restored pane
+            i128 dmin;
+            if ((rc = deferred_min(dmin))) return rc;
+            B = std::max(fired_k * m, dmin);
+        }
+        return merge_deferred();
+    }
+
     int advance_pane(int64_t w, int64_t* rows_out) {
         int rc;
         if (rows_out) *rows_out = 0;
@@ -1078,6 +1213,22 @@ int gw_flush(gw_handle* h) {
     hipSetDevice(h->cfg.device);
     int rc = h->ensure_fresh();
     return rc ? rc : h->flush_buffer();
+}
+
+int gw_snapshot(gw_handle* h, int32_t kg_lo, int32_t kg_hi, void* buf, int64_t cap, int64_t* len) {
+    if (!h || !len) return GW_E_INVALID;
+    if (h->failed) return h->fail(GW_E_STATE, "operator failed earlier: %s", h->err.c_str());
+    if (h->session) return h->fail(GW_E_UNSUPPORTED, "snapshot of session windows is not yet supported");
+    hipSetDevice(h->cfg.device);
+    return h->snapshot(kg_lo, kg_hi, buf, cap, len);
+}
+
+int gw_restore(gw_handle* h, const void* buf, int64_t len) {
+    if (!h) return GW_E_INVALID;
+    if (h->failed) return h->fail(GW_E_STATE, "operator failed earlier: %s", h->err.c_str());
+    if (h->session) return h->fail(GW_E_UNSUPPORTED, "restore of session windows is not yet supported");
+    hipSetDevice(h->cfg.device);
+    return h->restore(buf, len);
 }
 
 int gw_end_input(gw_handle* h, int64_t* rows_fired) { return gw_advance_watermark(h, INT64_MAX, rows_fired); }

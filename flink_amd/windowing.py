@@ -368,6 +368,25 @@ class GpuWindowOperator:
         by itself, a snapshot or a timing boundary calls it explicitly."""
         N.check(N.lib().gw_flush(self._h), self._h)
 
+    # checkpointing ----------------------------------------------------------------
+    def snapshot_state(self, key_group_range=None) -> bytes:
+        """Keyed window state of the key groups [lo, hi] (default: all), as one blob
+        (StreamOperator.snapshotState; restore with initialize_state)."""
+        lo, hi = key_group_range if key_group_range is not None else (0, self.cfg.max_parallelism - 1)
+        n = ctypes.c_int64(0)
+        N.check(N.lib().gw_snapshot(self._h, lo, hi, None, 0, ctypes.byref(n)), self._h)
+        buf = ctypes.create_string_buffer(n.value)
+        N.check(N.lib().gw_snapshot(self._h, lo, hi, buf, n.value, ctypes.byref(n)), self._h)
+        return buf.raw[:n.value]
+
+    def initialize_state(self, blobs):
+        """Restore one or more snapshot blobs (e.g. the key-group ranges of several
+        subtasks after rescaling) before processing (StreamOperator.initializeState)."""
+        if isinstance(blobs, (bytes, bytearray)):
+            blobs = [blobs]
+        for b in blobs:
+            N.check(N.lib().gw_restore(self._h, bytes(b), len(b)), self._h)
+
     def pending_rows(self) -> int:
         n = ctypes.c_int64(0)
         N.check(N.lib().gw_pending_rows(self._h, ctypes.byref(n)), self._h)

@@ -164,6 +164,22 @@ int  gw_advance_watermark(gw_handle* h, int64_t wm, int64_t* rows_fired);
  * by itself; gw_flush makes the state exact at any point, as a snapshot needs
  * (StreamOperator.prepareSnapshotPreBarrier, RS/api/operators/StreamOperator.java:122). */
 int  gw_flush(gw_handle* h);
+/* ---- checkpoint / restore ------------------------------------------------ */
+/* Snapshot of the window state of key groups [kg_lo, kg_hi] (buffered records are
+ * applied first).  Replaces the keyed-state part of StreamOperator.snapshotState
+ * (RS/api/operators/StreamOperator.java:131; heap backend per key group:
+ * HeapSnapshotStrategy.java:97-154, CopyOnWriteStateMapSnapshot.writeState :127-149).
+ * The blob holds, per key group, (key, pane, accumulator) entries; panes are the
+ * operator's slices of width gcd(size, slide), so every aggregate restores exactly.
+ * Two calls: buf == NULL returns the size in *len; then a buffer of cap >= *len.
+ * Tumbling/sliding only (sessions: GW_E_UNSUPPORTED). */
+int  gw_snapshot(gw_handle* h, int32_t kg_lo, int32_t kg_hi, void* buf, int64_t cap, int64_t* len);
+/* Restore one snapshot blob (call once per key-group range, e.g. after rescaling) into a
+ * handle with the same assigner, aggregate and max parallelism
+ * (StreamOperator.initializeState, StreamOperator.java:139).  The watermark is not part
+ * of the state: like Flink after a restore it starts at Long.MIN_VALUE. */
+int  gw_restore(gw_handle* h, const void* buf, int64_t len);
+
 /* Bounded input ended (BoundedOneInput.endInput) — equivalent to MAX_WATERMARK. */
 int  gw_end_input(gw_handle* h, int64_t* rows_fired);
 

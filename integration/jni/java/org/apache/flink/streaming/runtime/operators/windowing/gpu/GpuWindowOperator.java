@@ -15,6 +15,11 @@ package org.apache.flink.streaming.runtime.operators.windowing.gpu;
 
 import org.apache.flink.api.java.functions.KeySelector;
 import org.apache.flink.api.java.tuple.Tuple4;
+import org.apache.flink.runtime.state.KeyGroupRange;
+import org.apache.flink.runtime.state.KeyGroupStatePartitionStreamProvider;
+import org.apache.flink.runtime.state.KeyedStateCheckpointOutputStream;
+import org.apache.flink.runtime.state.StateInitializationContext;
+import org.apache.flink.runtime.state.StateSnapshotContext;
 import org.apache.flink.streaming.api.operators.AbstractStreamOperator;
 import org.apache.flink.streaming.api.operators.BoundedOneInput;
 import org.apache.flink.streaming.api.operators.OneInputStreamOperator;
@@ -22,8 +27,12 @@ import org.apache.flink.streaming.api.watermark.Watermark;
 import org.apache.flink.streaming.runtime.streamrecord.StreamRecord;
 import org.apache.flink.streaming.runtime.tasks.KeyContextHandler;
 
+import java.io.DataInputStream;
+import java.io.DataOutputStream;
 import java.nio.ByteBuffer;
 import java.nio.ByteOrder;
+import java.util.ArrayList;
+import java.util.List;
 import java.util.function.ToDoubleFunction;
 import java.util.function.ToLongFunction;
 
@@ -45,6 +54,7 @@ public class GpuWindowOperator<IN>
     private transient long handle;
     private transient ByteBuffer keys, hashes, ts, values, oKey, oStart, oEnd, oRes;
     private transient int n;
+    private transient List<byte[]> restored;  // per-key-group blobs read in initializeState
 
     public GpuWindowOperator(int assigner, long size, long slide, long offset, long gap, long lateness,
                              int trigger, int agg, KeySelector<IN, Long> keySelector,
@@ -69,6 +79,48 @@ public class GpuWindowOperator<IN>
                               subtask, device, 1L << 24, batchCapacity);
         keys = direct(8); hashes = direct(4); ts = direct(8); values = direct(8);
         oKey = direct(8); oStart = direct(8); oEnd = direct(8); oRes = direct(8);
+        if (restored != null) {  // initializeState runs before open (StreamOperator.java:139)
+            for (byte[] blob : restored) nativeRestore(handle, blob);
+            restored = null;
+        }
+    }
+
+    // ---- checkpointing: raw keyed state, one blob per key group -------------------------
+    // (the heap backend also writes per key group: HeapSnapshotStrategy.java:97-154)
+
+    @Override
+    public void prepareSnapshotPreBarrier(long checkpointId) throws Exception {
+        flush();
+        nativeFlush(handle);  // buffered records into the window state
+    }
+
+    @Override
+    public void snapshotState(StateSnapshotContext context) throws Exception {
+        super.snapshotState(context);
+        KeyGroupRange range = getKeyedStateBackend().getKeyGroupRange();
+        byte[] all = nativeSnapshot(handle, range.getStartKeyGroup(), range.getEndKeyGroup());
+        KeyedStateCheckpointOutputStream out = context.getRawKeyedOperatorStateOutput();
+        for (int kg : range) {
+            out.startNewKeyGroup(kg);
+            byte[] part = nativeSliceKeyGroup(all, kg);
+            DataOutputStream dos = new DataOutputStream(out);
+            dos.writeInt(part.length);
+            dos.write(part);
+            dos.flush();
+        }
+    }
+
+    @Override
+    public void initializeState(StateInitializationContext context) throws Exception {
+        super.initializeState(context);
+        if (!context.isRestored()) return;
+        restored = new ArrayList<>();
+        for (KeyGroupStatePartitionStreamProvider p : context.getRawKeyedStateInputs()) {
+            DataInputStream in = new DataInputStream(p.getStream());
+            byte[] blob = new byte[in.readInt()];
+            in.readFully(blob);
+            restored.add(blob);
+        }
     }
 
     private ByteBuffer direct(int width) {
@@ -131,4 +183,8 @@ public class GpuWindowOperator<IN>
                                           int cap);
     private static native long nativeLateDropped(long h);
     private static native void nativeDestroy(long h);
+    private static native void nativeFlush(long h);
+    private static native byte[] nativeSnapshot(long h, int kgLo, int kgHi);
+    private static native byte[] nativeSliceKeyGroup(byte[] blob, int kg);
+    private static native void nativeRestore(long h, byte[] blob);
 }

@@ -9,6 +9,8 @@
  */
 #include <jni.h>
 #include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
 #include "gpuwin.h"
 
 #define CLS(n) Java_org_apache_flink_streaming_runtime_operators_windowing_gpu_GpuWindowOperator_##n
@@ -66,3 +68,65 @@ JNIEXPORT jlong JNICALL CLS(nativeLateDropped)(JNIEnv* env, jclass c, jlong h) {
 }
 
 JNIEXPORT void JNICALL CLS(nativeDestroy)(JNIEnv* env, jclass c, jlong h) { gw_destroy((gw_handle*)(intptr_t)h); }
+
+/* prepareSnapshotPreBarrier: apply every buffered record (gw_flush). */
+JNIEXPORT void JNICALL CLS(nativeFlush)(JNIEnv* env, jclass c, jlong h) {
+    fail(env, (gw_handle*)(intptr_t)h, gw_flush((gw_handle*)(intptr_t)h));
+}
+
+/* snapshotState: the window state of key groups [lo, hi] as one blob (gw_snapshot). */
+JNIEXPORT jbyteArray JNICALL CLS(nativeSnapshot)(JNIEnv* env, jclass c, jlong h, jint lo, jint hi) {
+    gw_handle* g = (gw_handle*)(intptr_t)h;
+    int64_t len = 0;
+    if (fail(env, g, gw_snapshot(g, lo, hi, 0, 0, &len)) < 0) return 0;
+    void* buf = malloc((size_t)len);
+    int rc = gw_snapshot(g, lo, hi, buf, len, &len);
+    jbyteArray out = 0;
+    if (rc == GW_OK) {
+        out = (*env)->NewByteArray(env, (jsize)len);
+        (*env)->SetByteArrayRegion(env, out, 0, (jsize)len, (const jbyte*)buf);
+    }
+    free(buf);
+    fail(env, g, rc);
+    return out;
+}
+
+/* The part of a [lo, hi] snapshot blob that belongs to key group kg, as a blob of its
+ * own (written per key group into the raw keyed state stream).  Layout: include/gpuwin.h
+ * gw_snapshot; header = 4 + 4 + 2*4 + 5*8 + 4*4 + 2*8 + 8 = 96 bytes, kg_lo at 60. */
+JNIEXPORT jbyteArray JNICALL CLS(nativeSliceKeyGroup)(JNIEnv* env, jclass c, jbyteArray blob, jint kg) {
+    const int HDR = 96, OFF_KGLO = 60, OFF_KGHI = 64, OFF_N = 88;
+    jsize len = (*env)->GetArrayLength(env, blob);
+    jbyte* b = (*env)->GetByteArrayElements(env, blob, 0);
+    int32_t lo, hi;
+    memcpy(&lo, b + OFF_KGLO, 4);
+    memcpy(&hi, b + OFF_KGHI, 4);
+    int64_t o0, o1;
+    memcpy(&o0, b + HDR + (int64_t)(kg - lo) * 8, 8);
+    memcpy(&o1, b + HDR + (int64_t)(kg - lo + 1) * 8, 8);
+    const int64_t n = o1 - o0, ent0 = HDR + (int64_t)(hi - lo + 2) * 8;
+    const jsize out_len = (jsize)(HDR + 16 + n * 32);
+    jbyteArray out = (*env)->NewByteArray(env, out_len);
+    jbyte* o = (*env)->GetByteArrayElements(env, out, 0);
+    memcpy(o, b, HDR);
+    memcpy(o + OFF_KGLO, &kg, 4);
+    memcpy(o + OFF_KGHI, &kg, 4);
+    memcpy(o + OFF_N, &n, 8);
+    const int64_t zero = 0;
+    memcpy(o + HDR, &zero, 8);
+    memcpy(o + HDR + 8, &n, 8);
+    if (n) memcpy(o + HDR + 16, b + ent0 + o0 * 32, (size_t)n * 32);
+    (*env)->ReleaseByteArrayElements(env, out, o, 0);
+    (*env)->ReleaseByteArrayElements(env, blob, b, JNI_ABORT);
+    (void)len;
+    return out;
+}
+
+/* initializeState: restore one key group's blob (gw_restore). */
+JNIEXPORT void JNICALL CLS(nativeRestore)(JNIEnv* env, jclass c, jlong h, jbyteArray blob) {
+    jsize len = (*env)->GetArrayLength(env, blob);
+    jbyte* b = (*env)->GetByteArrayElements(env, blob, 0);
+    int rc = gw_restore((gw_handle*)(intptr_t)h, b, len);
+    (*env)->ReleaseByteArrayElements(env, blob, b, JNI_ABORT);
+    fail(env, (gw_handle*)(intptr_t)h, rc);
+}

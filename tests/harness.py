@@ -54,6 +54,11 @@ def replay(test, make_backend, is_double=False):
         if op[0] == "e":
             _, k, v, ts = op
             be.process_element(keys.id(k), ts, v)
+        elif op[0] == "snapshot":
+            # testHarness.snapshot -> close -> new harness -> initializeState -> open
+            # (WindowOperatorTest.java:169-177); backends without it just continue
+            if hasattr(be, "snapshot_restore"):
+                be.snapshot_restore()
         elif op[0] == "w":
             _, wm, expected = op
             be.process_watermark(wm)

@@ -45,9 +45,22 @@ class GpuBackend:
         k, s, e, r = self.op.drain()
         return k, s, e, r.view(np.int64)
 
+    def snapshot_restore(self):
+        if self.kw["assigner"] == "session":
+            return  # session snapshots are not supported yet (GW_E_UNSUPPORTED)
+        if self.k:
+            self.op.process_batch(np.array(self.k, np.int64), np.array(self.t, np.int64),
+                                  np.array(self.v, np.int64))
+            self.k, self.t, self.v = [], [], []
+        blob = self.op.snapshot_state()
+        self.late_before = getattr(self, "late_before", 0) + self.op.num_late_records_dropped
+        self.op.close()
+        self.op = gpu_operator(self.kw)
+        self.op.initialize_state(blob)
+
     @property
     def late_dropped(self):
-        return self.op.num_late_records_dropped
+        return getattr(self, "late_before", 0) + self.op.num_late_records_dropped
 
 
 @pytest.mark.parametrize("test", load_golden("operator_harness.json")["tests"], ids=lambda t: t["name"])

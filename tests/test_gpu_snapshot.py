@@ -1,0 +1,124 @@
+"""Checkpoint / restore of the GPU window state: gw_snapshot /
+gw_restore per key-group range, checked against the CPU oracle run without any
+interruption (the reference's snapshot/restore is transparent to the output,
+WindowOperatorTest.java:169-177), including rescaling 2 -> 1 and 1 -> 2 subtasks."""
+import numpy as np
+import pytest
+
+from flink_amd import _native as N
+from flink_amd import windowing as W
+from tests.dist_worker import owners
+from tests.gpu_helpers import compare, gpu_operator, random_stream, run_oracle
+
+pytestmark = pytest.mark.gpu
+
+CFGS = [
+    dict(assigner="tumbling", size=1000, slide=1000),
+    dict(assigner="sliding", size=1000, slide=300, offset=-50),
+    dict(assigner="sliding", size=10000, slide=2000),
+]
+
+
+def _rows(op, outs):
+    k, s, e, r = op.drain()
+    outs.append((k, s, e, r.view(np.int64)))
+
+
+@pytest.mark.parametrize("agg", ["count", "sum_i64", "min_f64", "avg_f64"])
+@pytest.mark.parametrize("cfg", CFGS, ids=lambda c: "-".join(str(v) for v in c.values()))
+@pytest.mark.parametrize("flags", [N.FLAG_NO_REGION, N.FLAG_FORCE_REGION], ids=["direct", "region"])
+def test_snapshot_restore_mid_stream(oracle_lib, cfg, agg, flags):
+    kw = dict(cfg, agg=agg)
+    keys, ts, vals, batches = random_stream(seed=41, n=40000, num_keys=3000, n_batches=16, agg=agg)
+    opkw = dict(flags=flags, capacity_hint=600_000 if flags == N.FLAG_FORCE_REGION else 4096)
+    op = gpu_operator(kw, **opkw)
+    outs = []
+    for i, (lo, hi, wm) in enumerate(batches):
+        op.process_batch(keys[lo:hi], ts[lo:hi], vals[lo:hi])
+        if i in (5, 11):  # snapshot after the records, before the watermark
+            blob = op.snapshot_state()
+            op.close()
+            op = gpu_operator(kw, **opkw)
+            op.initialize_state(blob)
+        op.advance_watermark(wm)
+        _rows(op, outs)
+    op.advance_watermark(W.LONG_MAX)
+    _rows(op, outs)
+    op.close()
+    o, _ = run_oracle(oracle_lib, kw, keys, ts, vals, batches)
+    assert compare(outs, o, agg in ("sum_f64", "avg_f64")) == []
+
+
+@pytest.mark.parametrize("agg", ["sum_i64", "max_f64"])
+def test_rescale_two_to_one_and_one_to_two(oracle_lib, agg):
+    """Key groups move between subtasks (KeyGroupRangeAssignment.java:93-106): two
+    subtasks' snapshots restore into one, and one subtask's snapshot splits into two
+    key-group ranges restored into two subtasks."""
+    kw = dict(assigner="sliding", size=1000, slide=250, agg=agg)
+    keys, ts, vals, batches = random_stream(seed=5, n=30000, num_keys=2000, n_batches=12, agg=agg)
+    own2 = owners(keys, 128, 2)
+    cut = 6
+    o, _ = run_oracle(oracle_lib, kw, keys, ts, vals, batches)
+
+    def run(ops, own, phase_batches, outs_per_wm):
+        for j, (lo, hi, wm) in enumerate(phase_batches):
+            for r, op in enumerate(ops):
+                sel = np.arange(lo, hi)
+                if own is not None:
+                    sel = sel[own[lo:hi] == r]
+                op.process_batch(keys[sel], ts[sel], vals[sel])
+            got = []
+            for op in ops:
+                op.advance_watermark(wm)
+                k, s, e, rr = op.drain()
+                got.append((k, s, e, rr.view(np.int64)))
+            outs_per_wm.append(tuple(np.concatenate([g[c] for g in got]) for c in range(4)))
+
+    # 2 -> 1
+    ops = [W.GpuWindowOperator(W.SlidingEventTimeWindows.of(1000, 250), agg, capacity_hint=4096, parallelism=2,
+                               operator_index=r).open() for r in range(2)]
+    outs = []
+    run(ops, own2, batches[:cut], outs)
+    blobs = [op.snapshot_state(W.compute_key_group_range_for_operator_index(128, 2, r)) for r, op in enumerate(ops)]
+    for op in ops:
+        op.close()
+    one = gpu_operator(kw, capacity_hint=4096)
+    one.initialize_state(blobs)
+    run([one], None, batches[cut:], outs)
+    one.advance_watermark(W.LONG_MAX)
+    k, s, e, rr = one.drain()
+    outs.append((k, s, e, rr.view(np.int64)))
+    one.close()
+    assert compare(outs, o, False) == []
+
+    # 1 -> 2
+    one = gpu_operator(kw, capacity_hint=4096)
+    outs = []
+    run([one], None, batches[:cut], outs)
+    blobs = [one.snapshot_state(W.compute_key_group_range_for_operator_index(128, 2, r)) for r in range(2)]
+    one.close()
+    ops = [W.GpuWindowOperator(W.SlidingEventTimeWindows.of(1000, 250), agg, capacity_hint=4096, parallelism=2,
+                               operator_index=r).open() for r in range(2)]
+    for r, op in enumerate(ops):
+        op.initialize_state(blobs[r])
+    run(ops, own2, batches[cut:], outs)
+    last = []
+    for op in ops:
+        op.advance_watermark(W.LONG_MAX)
+        k, s, e, rr = op.drain()
+        last.append((k, s, e, rr.view(np.int64)))
+        op.close()
+    outs.append(tuple(np.concatenate([g[c] for g in last]) for c in range(4)))
+    assert compare(outs, o, False) == []
+
+
+def test_restore_rejects_other_config():
+    a = gpu_operator(dict(assigner="tumbling", size=100, slide=100, agg="sum_i64"))
+    a.process_batch(np.arange(10, dtype=np.int64), np.arange(10, dtype=np.int64), np.ones(10, np.int64))
+    blob = a.snapshot_state()
+    a.close()
+    b = gpu_operator(dict(assigner="tumbling", size=200, slide=200, agg="sum_i64"))
+    with pytest.raises(N.GpuWinError) as ei:
+        b.initialize_state(blob)
+    assert ei.value.code == -1
+    b.close()
