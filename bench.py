@@ -69,6 +69,8 @@ def parse():
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--preagg", choices=["auto", "force", "off"], default="auto")
+    ap.add_argument("--no-kernel-timing", action="store_true",
+                    help="no HIP events around the kernels (the roofline fields are then null)")
     ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
                     help="nccl = RCCL over xGMI; gloo = host-staged rehearsal (several ranks may share one GPU)")
     return ap.parse_args()
@@ -170,7 +172,7 @@ def main():
         op.clear_rows()  # DiscardingSink
         return k, t
 
-    op.enable_kernel_timing(True)
+    op.enable_kernel_timing(not args.no_kernel_timing)
     for b in range(args.warmup):
         step(b, False)
     op.flush()  # warmup batches still buffered are applied outside the timed region

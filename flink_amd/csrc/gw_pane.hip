@@ -678,7 +678,6 @@ __device__ __forceinline__ void copy_words(long long* __restrict__ d, const long
 }
 
 constexpr int kApplyRuns = 256;  // run descriptors staged in LDS per step (<= blockDim)
-constexpr int kStageRegs = 8;    // 16-B state words per thread in the prologue (<= 4096 x 16 B)
 constexpr int kApplyGroup = 4;   // consecutive runs a wave walks as one sequence
 constexpr int kApplyUnroll = 4;  // records per lane with their loads in flight together
 
@@ -737,24 +736,26 @@ __global__ void __launch_bounds__(512) k_rgn_apply(IngestArgs a) {
     const long2* gp1 = act1 >= 0 ? reinterpret_cast<const long2*>(pt_cell(a.t, r << a.t.log2S, act1)) : nullptr;
     const int64_t id0 = identity0(AGG);
     const long2 ident = W == 2 ? long2{id0, 0} : long2{id0, id0};
-    long2 stage[kStageRegs];
-#pragma unroll
-    for (int q = 0; q < kStageRegs; ++q) {
-        const int64_t w = threadIdx.x + (int64_t)q * 512;
-        stage[q] = ident;
-        if (w < nkm) stage[q] = gkm2[w];
-        else if (w < nkm + np) { if (ld0) stage[q] = gp0[w - nkm]; }
-        else if (w < total2) { if (ld1) stage[q] = gp1[w - nkm - np]; }
+    // LDS-DMA (global_load_lds_dwordx4): each wave copies 1-KB pieces of the state
+    // straight into LDS, 16 B per lane from a per-lane source, no VGPRs; a retired pane
+    // is written as identities instead.
+    long2* l2 = reinterpret_cast<long2*>(lkeys);
+    for (int64_t w0 = (int64_t)wave * 64; w0 < total2; w0 += (int64_t)nw * 64) {
+        const int64_t w = w0 + lane;
+        const long2* src = nullptr;
+        if (w < nkm) src = gkm2 + w;
+        else if (w < nkm + np) { if (ld0) src = gp0 + (w - nkm); }
+        else if (w < total2) { if (ld1) src = gp1 + (w - nkm - np); }
+        if (src)
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                             (__attribute__((address_space(3))) void*)(l2 + w0), 16, 0, 0);
+        else if (w < total2)
+            l2[w] = ident;
     }
-    // uniform exit for a region without records (its first descriptor block is empty)
+    // uniform exit for a region without records (its first descriptor block is empty);
+    // the barrier also waits for the LDS-DMA
     const int any = __syncthreads_or((int)(d0 & 0xffffu)) || (re - rb > kApplyRuns);
     if (!any) return;
-    long2* l2 = reinterpret_cast<long2*>(lkeys);
-#pragma unroll
-    for (int q = 0; q < kStageRegs; ++q) {
-        const int64_t w = threadIdx.x + (int64_t)q * 512;
-        if (w < total2) l2[w] = stage[q];
-    }
     if ((int)threadIdx.x < nr0) {
         r_cnt[threadIdx.x] = d0 & 0xffffu;
         r_src[threadIdx.x] = (uint32_t)(base0 + (d0 >> 16));
@@ -857,8 +858,8 @@ __global__ void __launch_bounds__(512) k_rgn_apply(IngestArgs a) {
                 g.src[u] = i < nr ? r_src[i] : 0u;
             }
         };
-        auto load_step = [&](const Grp& g, uint32_t k, Step& s) {
-            const uint32_t tot = g.pre[kApplyGroup];
+        auto load_step = [&](const Grp& g, uint32_t k, Step& s, bool live) {
+            const uint32_t tot = live ? g.pre[kApplyGroup] : 0u;
 #pragma unroll
             for (int q = 0; q < kApplyUnroll; ++q) {
                 const uint32_t e = k + q * 64 + lane;
@@ -893,24 +894,26 @@ __global__ void __launch_bounds__(512) k_rgn_apply(IngestArgs a) {
         uint32_t k = ~0u;
         Grp g;
         if (i0 < nr) load_grp(i0, g);
-        Step cur;
-        bool live = advance(i0, k, g);
-        if (live) load_step(g, k, cur);
-        while (live) {
-            int i1 = i0;
-            uint32_t k1 = k;
-            Grp g1 = g;
-            const bool live1 = advance(i1, k1, g1);
-            Step nxt;
-            if (live1) load_step(g1, k1, nxt);
+        // Two step buffers used in turn (no register copy of a step whose loads are still
+        // in flight, which would wait for them): while one step is applied, the other's
+        // loads are outstanding.  The loads are issued unconditionally, past the end as
+        // well, so the compiler can count the outstanding ones on every path.
+        auto apply_step = [&](const Step& c) {
 #pragma unroll
             for (int q = 0; q < kApplyUnroll; ++q)
-                if (cur.ok[q]) apply_one(cur.key[q], cur.v0[q], cur.v1[q], cur.ps[q], cur.x[q]);
-            cur = nxt;
-            i0 = i1;
-            k = k1;
-            g = g1;
-            live = live1;
+                if (c.ok[q]) apply_one(c.key[q], c.v0[q], c.v1[q], c.ps[q], c.x[q]);
+        };
+        Step sa, sb;
+        bool live = advance(i0, k, g);
+        load_step(g, k, sa, live);
+        while (live) {
+            live = advance(i0, k, g);
+            load_step(g, k, sb, live);
+            apply_step(sa);
+            if (!live) break;
+            live = advance(i0, k, g);
+            load_step(g, k, sa, live);
+            apply_step(sb);
         }
     }
     // Spill pass (only in regions that had a spill): the final LDS key table says which
