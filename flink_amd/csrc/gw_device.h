@@ -43,7 +43,8 @@ struct DevStatus {
     unsigned long long merges;      // host view: sum of sh[].merges (session merges, M_b)
     unsigned long long overflow;    // session segments that did not fit (retry list length)
     unsigned long long spills;      // region apply: records left in the buffer by full regions
-    unsigned long long pad[5];
+    unsigned long long n_refire;    // lateness > 0: re-fire list cursor (late records of fired windows)
+    unsigned long long pad[4];
     ShardCtr sh[kShards];
 };
 #define GW_DF_NO_TS 1ull

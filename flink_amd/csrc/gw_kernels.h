@@ -122,6 +122,14 @@ struct IngestArgs {
     int64_t t_late;     // first non-late timestamp (start of the first unfired window)
     int64_t p_late;     // its pane index
     uint64_t delta;     // ring base pane B - p_late (>= 0)
+    uint64_t q_refire;  // lateness > 0: panes p_late .. p_late + q_refire - 1 belong to fired,
+                        // not yet cleaned windows; their records go to the re-fire list
+    int64_t seq0;       // arrival number of record 0 of this call (re-fire order)
+    int64_t* rf_key;    // re-fire list (append at st->n_refire)
+    int64_t* rf_pane;
+    int64_t* rf_a0;
+    int64_t* rf_a1;
+    int64_t* rf_seq;
     UDiv64 div;         // division by the pane width g
     int32_t b_pos;      // B mod R
     int32_t late_exact; // 0: t_late was clamped at Long.MIN_VALUE (then ts < t_late is a range error)
@@ -194,6 +202,30 @@ struct FireArgs {
     DevStatus* st;
 };
 
+// Late records of fired, not yet cleaned windows (allowed lateness > 0), in (key, arrival)
+// order: each emits one row per such window it belongs to (EventTimeTrigger.onElement FIRE,
+// RS/api/windowing/triggers/EventTimeTrigger.java:37-45; WindowOperator.java:408-446).
+struct RefireArgs {
+    PaneTable t;
+    int64_t n;
+    const uint32_t* order;  // entry indices sorted by (key, seq)
+    const int64_t* rf_key;
+    const int64_t* rf_pane;
+    const int64_t* rf_a0;
+    const int64_t* rf_a1;
+    int64_t b;              // ring base pane
+    int32_t b_pos;
+    int32_t purging;        // PurgingTrigger: a late record's row holds the record alone
+    int64_t m, np;          // slide and size in panes
+    int64_t k_lo, k_hi;     // windows that re-fire: k_lo .. k_hi (not late, already fired)
+    int64_t offset, slide, size;
+    int64_t* o_key;
+    int64_t* o_start;
+    int64_t* o_end;
+    int64_t* o_res;
+    DevStatus* st;
+};
+
 struct EvictArgs {
     PaneTable t;
     uint64_t emask;
@@ -235,6 +267,10 @@ hipError_t launch_region_flush(const IngestArgs& a, hipStream_t s);
 hipError_t launch_region_collect(const IngestArgs& a, hipStream_t s);
 int region_group(int d1_bits);  // G: P1 tiles per P2 block
 hipError_t launch_merge_deferred(const MergeArgs& a, hipStream_t s);
+hipError_t launch_refire(const RefireArgs& a, hipStream_t s);
+// re-fire sort keys: mode 0 k[i] = seq[i] - seq_base, v[i] = i; mode 1 k[i] = key[v[i]]
+hipError_t launch_refire_keys(int mode, const int64_t* src, int64_t base, uint64_t* k, uint32_t* v, int64_t n,
+                              hipStream_t s);
 hipError_t launch_deferred_min(const int64_t* pane, int64_t n, DevStatus* st, hipStream_t s);
 hipError_t launch_fire(const FireArgs& a, hipStream_t s);
 hipError_t launch_evict(const EvictArgs& a, hipStream_t s);

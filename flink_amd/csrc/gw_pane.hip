@@ -65,8 +65,9 @@ __device__ __forceinline__ uint64_t presence_rt(const PaneTable& t, int64_t g) {
     return m;
 }
 
-// Per-record classification: late / parked (outside the pane ring) / in ring.
-enum { REC_SKIP = 0, REC_RING = 1, REC_DEFER = 2 };
+// Per-record classification: late / parked (outside the pane ring) / in ring / re-fire
+// (allowed lateness > 0: the pane belongs to a fired window that is not cleaned yet).
+enum { REC_SKIP = 0, REC_RING = 1, REC_DEFER = 2, REC_REFIRE = 3 };
 template <int AGG>
 __device__ __forceinline__ int classify(const IngestArgs& a, int64_t ts, int64_t v, uint32_t& pos, int64_t& pane,
                                         int64_t& c0, int64_t& c1, unsigned long long& late,
@@ -81,6 +82,7 @@ __device__ __forceinline__ int classify(const IngestArgs& a, int64_t ts, int64_t
     const uint64_t q = udiv64((uint64_t)ts - (uint64_t)a.t_late, a.div);
     record_cell(AGG, v, c0, c1);
     pane = a.p_late + (int64_t)q;
+    if (q < a.q_refire) return REC_REFIRE;
     const uint64_t rel = q - a.delta;
     if (q >= a.delta && rel < R) {
         uint32_t p = (uint32_t)a.b_pos + (uint32_t)rel;
@@ -107,6 +109,20 @@ __device__ __forceinline__ void defer_write(const IngestArgs& a, bool defer, int
         a.d_pane[off] = pane;
         a.d_a0[off] = c0;
         a.d_a1[off] = c1;
+    }
+}
+
+// Late record of a fired, not yet cleaned window: onto the re-fire list with its
+// arrival number (processed in order at the next watermark, k_refire).
+__device__ __forceinline__ void refire_write(const IngestArgs& a, bool rf, int64_t key, int64_t pane, int64_t c0,
+                                             int64_t c1, int64_t i) {
+    const unsigned long long off = wave_reserve(&a.st->n_refire, rf);
+    if (rf) {
+        a.rf_key[off] = key;
+        a.rf_pane[off] = pane;
+        a.rf_a0[off] = c0;
+        a.rf_a1[off] = c1;
+        a.rf_seq[off] = a.seq0 + i;
     }
 }
 
@@ -198,7 +214,11 @@ __global__ void __launch_bounds__(256) k_ingest(IngestArgs a) {
             occ |= 1ull << pos[u];
         }
 #pragma unroll
-        for (int u = 0; u < U; ++u) defer_write(a, state[u] == REC_DEFER, key[u], pane[u], c0[u], c1[u]);
+        for (int u = 0; u < U; ++u) {
+            defer_write(a, state[u] == REC_DEFER, key[u], pane[u], c0[u], c1[u]);
+            refire_write(a, state[u] == REC_REFIRE, key[u], pane[u], c0[u], c1[u],
+                         base + (int64_t)u * blockDim.x + threadIdx.x);
+        }
     }
     block_commit(a.st, late, ins, flags, occ);
 }
@@ -283,6 +303,7 @@ __global__ void __launch_bounds__(256) k_ingest_preagg(IngestArgs a) {
                 }
             }
             defer_write(a, state == REC_DEFER, key, pane, c0, c1);
+            refire_write(a, state == REC_REFIRE, key, pane, c0, c1, i);
         }
         __syncthreads();
         for (int j = threadIdx.x; j < kLdsCells; j += blockDim.x) {
@@ -446,6 +467,7 @@ __global__ void __launch_bounds__(kPartThreads) k_rgn_p1(IngestArgs a) {
             }
         }
         defer_write(a, st == REC_DEFER, key[it], pane, c0[it], c1[it]);
+        refire_write(a, st == REC_REFIRE, key[it], pane, c0[it], c1[it], i);
         if (bk[it] >= 0) rank[it] = atomicAdd(&lh[bk[it]], 1u);
     }
     occ = wave_ior(occ);
@@ -1058,6 +1080,102 @@ __global__ void __launch_bounds__(256) k_merge_deferred(MergeArgs a) {
     block_commit(a.st, 0, ins, flags, occ);
 }
 
+// ---------------------------------------------------------------------------
+// Allowed lateness > 0: rows of late records for fired, not yet cleaned windows
+// ---------------------------------------------------------------------------
+// Reference: WindowOperator.processElement :408-446 adds the record to every window
+// that is not late (cleanup time > watermark) and, because EventTimeTrigger.onElement
+// returns FIRE for a window whose max timestamp <= watermark (EventTimeTrigger.java:
+// 37-45), emits that window's contents right away; under PurgingTrigger the contents
+// are purged after each emission, so a late record's row holds that record alone.
+// Here the late records of one watermark interval are sorted by (key, arrival); one
+// thread per key walks them in arrival order, keeping a per-pane running fold on top
+// of the table's panes, and emits one row per (record, re-firing window).  The records
+// are merged into the table afterwards (k_merge_deferred).
+__device__ __forceinline__ int64_t pt_find_ro(const PaneTable& t, int64_t key) {
+    if (key == kEmptyKey) return t.cap;
+    const uint64_t h = slot_hash(key);
+    const int64_t S = pt_S(t);
+    const int64_t r = pt_key_region(t, h);
+    const int64_t* keys = pt_region(t, r);
+    int64_t j = pt_home(t, h);
+    const int lim = S < kMaxProbe ? (int)S : kMaxProbe;
+    for (int p = 0; p < lim; ++p) {
+        const int64_t k = keys[j];
+        if (k == key) return (r << t.log2S) + j;
+        if (k == kEmptyKey) return -1;
+        j = (j + 1) & (S - 1);
+    }
+    return -1;
+}
+
+__device__ __forceinline__ int64_t floor_div_d(int64_t a, int64_t b) {
+    const int64_t q = a / b;
+    return (a % b != 0 && ((a < 0) != (b < 0))) ? q - 1 : q;
+}
+
+template <int AGG>
+__global__ void __launch_bounds__(256) k_refire(RefireArgs a) {
+    const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (i >= a.n) return;
+    const int64_t key = a.rf_key[a.order[i]];
+    if (i > 0 && a.rf_key[a.order[i - 1]] == key) return;  // not the first record of its key
+    const int R = a.t.ring;
+    const int W = a.t.words;
+    const int64_t id0 = identity0(AGG);
+    const int64_t g = pt_find_ro(a.t, key);
+    const uint64_t mask = g >= 0 ? presence<AGG>(a.t, g) : 0;
+    int64_t run0[kMaxRing], run1[kMaxRing];  // this interval's late records per ring position
+    for (int q = 0; q < R; ++q) { run0[q] = id0; run1[q] = 0; }
+    for (int64_t j = i; j < a.n && a.rf_key[a.order[j]] == key; ++j) {
+        const uint32_t e = a.order[j];
+        const int64_t p = a.rf_pane[e], c0 = a.rf_a0[e], c1 = a.rf_a1[e];
+        const bool in_ring = p >= a.b && p - a.b < R;
+        int pos = 0;
+        if (in_ring) {
+            pos = a.b_pos + (int)(p - a.b);
+            if (pos >= R) pos -= R;
+            fold_cell(AGG, run0[pos], run1[pos], c0, c1);
+        }
+        const int64_t k0 = max(a.k_lo, floor_div_d(p - a.np, a.m) + 1), k1 = min(a.k_hi, floor_div_d(p, a.m));
+        for (int64_t k = k0; k <= k1; ++k) {
+            int64_t r0 = id0, r1 = 0;
+            if (a.purging) {
+                fold_cell(AGG, r0, r1, c0, c1);
+            } else {
+                for (int64_t q = k * a.m; q < k * a.m + a.np; ++q) {
+                    if (q < a.b || q - a.b >= R) continue;  // outside the ring: no data
+                    int qp = a.b_pos + (int)(q - a.b);
+                    if (qp >= R) qp -= R;
+                    if ((mask >> qp) & 1) {
+                        const int64_t* c = pt_cell(a.t, g, qp);
+                        fold_cell(AGG, r0, r1, c[0], W == 2 ? c[1] : 0);
+                    }
+                    fold_cell(AGG, r0, r1, run0[qp], run1[qp]);
+                }
+            }
+            const unsigned long long o = atomicAdd(&a.st->rows, 1ull);
+            const int64_t st = a.offset + k * a.slide;
+            a.o_key[o] = key;
+            a.o_start[o] = st;
+            a.o_end[o] = st + a.size;
+            a.o_res[o] = cell_result(AGG, r0, r1);
+        }
+    }
+}
+
+__global__ void __launch_bounds__(256) k_refire_keys(int mode, const int64_t* src, int64_t base, uint64_t* k,
+                                                     uint32_t* v, int64_t n) {
+    const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    if (mode == 0) {
+        k[i] = (uint64_t)(src[i] - base);
+        v[i] = (uint32_t)i;
+    } else {
+        k[i] = (uint64_t)src[v[i]];
+    }
+}
+
 __global__ void __launch_bounds__(256) k_deferred_min(const int64_t* pane, int64_t n, DevStatus* st) {
     long long m = INT64_MAX;
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n;
@@ -1377,6 +1495,21 @@ hipError_t launch_merge_deferred(const MergeArgs& a, hipStream_t s) {
 #define L(A) hipLaunchKernelGGL(k_merge_deferred<A>, dim3(grid_for(a.n)), dim3(256), 0, s, a)
     GW_AGG_SWITCH(a.t.agg, L);
 #undef L
+    return hipGetLastError();
+}
+
+hipError_t launch_refire(const RefireArgs& a, hipStream_t s) {
+    if (a.n == 0) return hipSuccess;
+#define L(A) hipLaunchKernelGGL(k_refire<A>, dim3((unsigned)((a.n + 255) / 256)), dim3(256), 0, s, a)
+    GW_AGG_SWITCH(a.t.agg, L);
+#undef L
+    return hipGetLastError();
+}
+
+hipError_t launch_refire_keys(int mode, const int64_t* src, int64_t base, uint64_t* k, uint32_t* v, int64_t n,
+                              hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_refire_keys, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, mode, src, base, k, v, n);
     return hipGetLastError();
 }
 

@@ -18,6 +18,7 @@
 
 #include "gw_kernels.h"
 #include "gw_session.h"
+#include "gw_sort.h"
 
 using namespace gw;
 
@@ -146,6 +147,16 @@ struct gw_handle {
     int64_t buf_tiles = 0;          // tiles used by the waiting segments
     uint64_t buf_fresh = 0;         // ring positions holding only identities at buffer start
     int64_t buf_limit = (int64_t)1 << 27;  // records (GW_BUFFER_RECORDS)
+
+    // allowed lateness > 0 (tumbling / sliding): late records of fired, not yet cleaned
+    // windows wait on the re-fire list until the next watermark (process_refire)
+    int64_t* rf[5] = {};            // key, pane, a0, a1, arrival number
+    int64_t rf_cap = 0;
+    int64_t rf_bound = 0;           // records ingested since the list was last processed
+    int64_t seq_ctr = 0;            // arrival number of the next record
+    int64_t rf_seq_base = 0;        // arrival number at the last processing
+    void* rf_sort = nullptr;        // sort keys / payloads / scratch
+    int64_t rf_sort_bytes = 0;
 
     // event-time state
     int64_t wm = INT64_MIN;
@@ -491,6 +502,139 @@ struct gw_handle {
         return GW_OK;
     }
 
+    int ensure_refire(int64_t need) {
+        if (need <= rf_cap) return GW_OK;
+        const int64_t nc = std::max<int64_t>(need + need / 2, 1 << 16);
+        const int64_t used = std::min(rf_bound, rf_cap);
+        for (int c = 0; c < 5; ++c) {
+            int64_t* nb;
+            HIPCHECK(hipMalloc((void**)&nb, nc * 8));
+            if (rf[c] && used) HIPCHECK(hipMemcpyAsync(nb, rf[c], used * 8, hipMemcpyDeviceToDevice, stream));
+            if (rf[c]) {
+                HIPCHECK(hipStreamSynchronize(stream));
+                hipFree(rf[c]);
+            }
+            rf[c] = nb;
+        }
+        rf_cap = nc;
+        return GW_OK;
+    }
+
+    // Window index bounds under allowed lateness (WindowOperator.cleanupTime :670-677,
+    // isWindowLate :609-612): window k is late at watermark w when max timestamp + lateness
+    // <= w (a cleanup time beyond Long.MAX_VALUE is Long.MAX_VALUE: late only at the last
+    // watermark, never cleaned), and its state is cleared by the cleanup timer once
+    // max timestamp + lateness <= w < Long.MAX_VALUE.
+    i128 k_for_wm128(i128 w) const { return floor_div(w + 1 - (i128)size() - (i128)cfg.offset, (i128)slide()); }
+    i128 late_k_at(int64_t w) const {  // first window that is not late
+        if (cfg.allowed_lateness == 0) return fired_k;
+        const i128 k = w == INT64_MAX ? k_for_wm(w) + 1 : k_for_wm128((i128)w - cfg.allowed_lateness) + 1;
+        return std::min(k, fired_k);
+    }
+    i128 clean_k_at(int64_t w) const {  // first window whose state is not cleared
+        if (cfg.allowed_lateness == 0) return k_for_wm(w) + 1;
+        return k_for_wm128(std::min<i128>(w, (i128)INT64_MAX - 1) - cfg.allowed_lateness) + 1;
+    }
+
+    // The re-fire list of the watermark interval that ends now: rows for every late
+    // record of a fired, not yet cleaned window (k_refire), then the records go into the
+    // table like parked ones.
+    int process_refire() {
+        if (!rf_bound) return GW_OK;
+        int rc;
+        if ((rc = refresh())) return rc;
+        const int64_t nrf = (int64_t)h_st->n_refire;
+        rf_bound = 0;
+        if (nrf) {
+            const int64_t span = seq_ctr - rf_seq_base;
+            const int seq_bits = span < ((int64_t)1 << 32) ? 32 : 64;
+            const int64_t kb = ((nrf * 8 + 255) / 256) * 256, vb = ((nrf * 4 + 255) / 256) * 256;
+            const int64_t need = 2 * kb + 2 * vb + radix_sort_scratch_bytes(nrf);
+            if (need > rf_sort_bytes) {
+                if (rf_sort) { HIPCHECK(hipStreamSynchronize(stream)); hipFree(rf_sort); }
+                HIPCHECK(hipMalloc(&rf_sort, need + need / 2));
+                rf_sort_bytes = need + need / 2;
+            }
+            char* base = (char*)rf_sort;
+            uint64_t* k0 = (uint64_t*)base;
+            uint64_t* k1 = (uint64_t*)(base + kb);
+            uint32_t* v0 = (uint32_t*)(base + 2 * kb);
+            uint32_t* v1 = (uint32_t*)(base + 2 * kb + vb);
+            void* scratch = base + 2 * kb + 2 * vb;
+            // (key, arrival) order: stable sort by arrival, then by key
+            int alt = 0;
+            HIPCHECK(launch_refire_keys(0, rf[4], rf_seq_base, k0, v0, nrf, stream));
+            HIPCHECK(radix_sort_pairs(k0, v0, k1, v1, nrf, seq_bits, scratch, stream, &alt));
+            uint64_t* ka = alt ? k0 : k1;  // the free key buffer
+            uint32_t* va = alt ? v1 : v0;  // the sorted payload
+            uint32_t* vo = alt ? v0 : v1;
+            HIPCHECK(launch_refire_keys(1, rf[0], 0, ka, va, nrf, stream));
+            uint64_t* kother = alt ? k1 : k0;
+            HIPCHECK(radix_sort_pairs(ka, va, kother, vo, nrf, 64, scratch, stream, &alt));
+            const uint32_t* order = alt ? vo : va;
+            const int64_t per_rec = (n + m - 1) / m;  // windows a pane belongs to
+            if ((rc = ensure_output((int64_t)h_st->rows + nrf * per_rec))) return rc;
+            RefireArgs r{};
+            r.t = tv;
+            r.n = nrf;
+            r.order = order;
+            r.rf_key = rf[0]; r.rf_pane = rf[1]; r.rf_a0 = rf[2]; r.rf_a1 = rf[3];
+            r.b = (int64_t)B;
+            r.b_pos = (int32_t)pos_of(B);
+            r.purging = cfg.trigger == GW_PURGING_EVENT_TIME_TRIGGER;
+            r.m = (int64_t)m;
+            r.np = (int64_t)n;
+            r.k_lo = (int64_t)late_k_at(wm);
+            r.k_hi = (int64_t)(fired_k - 1);
+            r.offset = cfg.offset;
+            r.slide = slide();
+            r.size = size();
+            r.o_key = o_key; r.o_start = o_start; r.o_end = o_end; r.o_res = o_res;
+            r.st = d_st;
+            HIPCHECK(launch_refire(r, stream));
+            // the records join their panes (windows that fire later fold them)
+            if ((rc = ensure_deferred((int64_t)h_st->n_deferred + nrf))) return rc;
+            MergeArgs a{};
+            a.i_key = rf[0]; a.i_pane = rf[1]; a.i_a0 = rf[2]; a.i_a1 = rf[3];
+            a.n = nrf;
+            a.b = (int64_t)B;
+            a.b_pos = (int32_t)pos_of(B);
+            a.t = tv;
+            a.d_key = dk[cur]; a.d_pane = dp[cur]; a.d_a0 = da0[cur]; a.d_a1 = da1[cur];
+            a.st = d_st;
+            HIPCHECK(launch_merge_deferred(a, stream));
+            if ((rc = set_field(offsetof(DevStatus, n_refire), 0))) return rc;
+            dirty = true;
+            if ((rc = refresh())) return rc;
+            if ((rc = take_occ())) return rc;
+            if (h_st->flags & GW_DF_TABLE_FULL) {
+                if ((rc = maybe_grow(0))) return rc;
+                if ((rc = merge_deferred())) return rc;
+            }
+        }
+        rf_seq_base = seq_ctr;
+        return GW_OK;
+    }
+
+    // Clear the ring panes below pane `upto` (their windows are fired and cleaned).
+    int retire_below(i128 upto) {
+        uint64_t rmask = 0;
+        for (i128 p = B; p < upto && p < B + R; ++p) rmask |= 1ull << pos_of(p);
+        rmask &= occ;
+        if (rmask) {
+            FireArgs f{};
+            f.t = tv;
+            f.nwin = 0;
+            f.rmask = rmask;
+            f.st = d_st;
+            HIPCHECK(launch_fire(f, stream));
+            occ &= ~rmask;
+            dirty = true;
+        }
+        if (B < upto) B = upto;
+        return GW_OK;
+    }
+
     // Lowest pane with data in the ring (or INT128 max).
     i128 ring_min() const {
         if (!occ) return ((i128)1) << 100;
@@ -543,8 +687,11 @@ struct gw_handle {
     static int popcount(uint64_t x) { return __builtin_popcountll(x); }
 
     // Fire every window k <= k_target (end-1 <= wm).
-    int fire_until(i128 k_target) {
+    int fire_until(i128 k_target, i128 c_target) {
         int rc;
+        const bool lat = cfg.allowed_lateness > 0;
+        // panes below both frontiers belong to fired windows that are cleaned now
+        if (lat && (rc = retire_below(std::min(fired_k, c_target) * m))) return rc;
         while (fired_k <= k_target) {
             i128 dmin;
             if ((rc = deferred_min(dmin))) return rc;
@@ -555,7 +702,8 @@ struct gw_handle {
             i128 k_first = floor_div(L - n, m) + 1;
             if (k_first < fired_k) k_first = fired_k;
             if (k_first > k_target) { fired_k = k_target + 1; break; }
-            if ((rc = rebase(k_first * m))) return rc;
+            // keep the retained panes of fired, not yet cleaned windows in the ring
+            if ((rc = rebase(lat ? std::min(k_first * m, L) : k_first * m))) return rc;
             if ((int64_t)h_st->n_deferred) {
                 if ((rc = merge_deferred())) return rc;
             }
@@ -578,8 +726,10 @@ struct gw_handle {
                 for (int j = 0; j < n; ++j) wm_ |= 1ull << pos_of(p0 + j);
                 f.wmask[w] = wm_;
             }
+            if (k_last < k_first) return fail(GW_E_STATE, "pane ring too short for the retained panes");
             uint64_t rmask = 0;
-            for (i128 p = B; p < (k_last + 1) * m && p < B + R; ++p) rmask |= 1ull << pos_of(p);
+            const i128 keep = lat ? std::min(k_last + 1, c_target) * m : (k_last + 1) * m;
+            for (i128 p = B; p < keep && p < B + R; ++p) rmask |= 1ull << pos_of(p);
             f.rmask = rmask;
             if ((rc = ensure_output((int64_t)h_st->rows + (int64_t)nwin * ((int64_t)h_st->used_slots + 1))))
                 return rc;
@@ -598,9 +748,10 @@ struct gw_handle {
             dirty = true;
             occ &= ~rmask;
             fired_k = k_last + 1;
-            if (B < fired_k * m) B = fired_k * m;
+            if (B < keep) B = keep;
             if ((rc = refresh())) return rc;
         }
+        if (lat) return retire_below(c_target * m);
         if (B < fired_k * m) B = fired_k * m;
         return GW_OK;
     }
@@ -616,8 +767,10 @@ struct gw_handle {
     // Ingest arguments shared by every path: the lateness bound and the ring geometry
     // at the current watermark.
     int base_args(IngestArgs& a, int64_t nrec, const int64_t* key, const int64_t* ts, const int64_t* val) {
-        // first non-late pane: the first window not fired at the current watermark
-        const i128 p_late = fired_k * m;
+        // first non-late pane: the first window that is not late at the current watermark
+        // (lateness 0: the first window not fired)
+        const i128 late_k = late_k_at(wm);
+        const i128 p_late = late_k * m;
         i128 t_late = (i128)cfg.offset + p_late * g;
         i128 pl = p_late;
         int exact = 1;
@@ -639,6 +792,15 @@ struct gw_handle {
         a.t = tv;
         a.d_key = dk[cur]; a.d_pane = dp[cur]; a.d_a0 = da0[cur]; a.d_a1 = da1[cur];
         a.st = d_st;
+        // panes up to the last one of the last fired window re-fire (lateness > 0)
+        const i128 hi = (fired_k - 1) * m + n - 1;
+        if (late_k < fired_k && hi >= pl) {
+            a.q_refire = (uint64_t)(hi - pl + 1);
+            a.seq0 = seq_ctr;
+            int rc;
+            if (nrec && (rc = ensure_refire(rf_bound + nrec))) return rc;
+            a.rf_key = rf[0]; a.rf_pane = rf[1]; a.rf_a0 = rf[2]; a.rf_a1 = rf[3]; a.rf_seq = rf[4];
+        }
         return GW_OK;
     }
 
@@ -772,6 +934,8 @@ struct gw_handle {
         }
         stats.events_in += nrec;
         stats.batches++;
+        seq_ctr += nrec;
+        if (a.q_refire) rf_bound += nrec;
         if (path == 2 && nseg) {  // buffered P1: no host sync (it writes no table cell)
             if ((rc = lazy_status(nrec))) return rc;
             if (occ || !h_st->n_deferred) return GW_OK;
@@ -788,8 +952,8 @@ struct gw_handle {
         if (!occ && h_st->n_deferred) {
             i128 dmin;
             if ((rc = deferred_min(dmin))) return rc;
-            const i128 lo = fired_k * m;
-            B = std::max(lo, dmin);
+            const i128 lo = late_k_at(wm) * m;
+            B = rf_bound ? lo : std::max(lo, dmin);  // pending re-fire records sit at >= lo
             if ((rc = merge_deferred())) return rc;
         }
         return GW_OK;
@@ -935,15 +1099,32 @@ struct gw_handle {
         if (rows_out) *rows_out = 0;
         if (w <= wm) return GW_OK;
         const i128 kt = k_for_wm(w);
-        if (kt < fired_k) {  // no window completes: nothing to launch (timer heap empty below w)
-            wm = w;
-            return GW_OK;
+        const i128 ct = clean_k_at(w);
+        int64_t before = 0;
+        if (cfg.allowed_lateness > 0) {
+            if ((rc = ensure_fresh())) return rc;
+            before = (int64_t)h_st->rows;
+            // rows of the interval's late records come before the timers' rows
+            if (rf_bound && (rc = process_refire())) return rc;
+            if (kt < fired_k && !(occ && ct * m > B)) {  // nothing fires, nothing is cleaned
+                wm = w;
+                if ((rc = ensure_fresh())) return rc;
+                const int64_t fired = (int64_t)h_st->rows - before;
+                stats.rows_fired += fired;
+                if (rows_out) *rows_out = fired;
+                return GW_OK;
+            }
+        } else {
+            if (kt < fired_k) {  // no window completes: nothing to launch (timer heap empty below w)
+                wm = w;
+                return GW_OK;
+            }
+            if ((rc = ensure_fresh())) return rc;
+            before = (int64_t)h_st->rows;
         }
-        if ((rc = ensure_fresh())) return rc;
         if ((rc = flush_buffer())) return rc;  // buffered records first, then the timers
-        const int64_t before = (int64_t)h_st->rows;
         {
-            if ((rc = fire_until(kt))) return rc;
+            if ((rc = fire_until(kt, ct))) return rc;
             wm = w;
         }
         if ((rc = ensure_fresh())) return rc;
@@ -995,8 +1176,8 @@ static int validate(const gw_config* c, std::string& why) {
         why = "unknown trigger";
         return GW_E_INVALID;
     }
-    if (c->allowed_lateness != 0) {
-        why = "allowed lateness > 0 is not yet supported on the GPU path";
+    if (c->allowed_lateness != 0 && c->assigner == GW_SESSION) {
+        why = "allowed lateness > 0 with session windows is not yet supported on the GPU path";
         return GW_E_UNSUPPORTED;
     }
     return GW_OK;
@@ -1070,6 +1251,15 @@ int gw_create(const gw_config* cfg, gw_handle** out) {
     if (need > kMaxRing)
         return bail(GW_E_UNSUPPORTED, "size/gcd(size,slide) + slide/gcd(size,slide) > 64 panes is not supported "
                                       "on the GPU path");
+    if (cfg->allowed_lateness > 0) {
+        // the panes of fired windows stay until their cleanup: ceil(lateness / slide) + 1
+        // more slides of the ring
+        const int64_t extra = cfg->allowed_lateness / slide + 2;
+        if (extra > kMaxRing || need + extra * h->m > kMaxRing)
+            return bail(GW_E_UNSUPPORTED, "allowed lateness spanning more than 64 panes of the ring is not "
+                                          "supported on the GPU path");
+        need += extra * h->m;
+    }
     int stride_w = (int)(((2 + need * words) + 7) / 8 * 8);
     int R = (stride_w - 2) / words;
     if (R > kMaxRing) R = kMaxRing;
@@ -1102,6 +1292,9 @@ int gw_destroy(gw_handle* h) {
         if (h->dk[b]) { hipFree(h->dk[b]); hipFree(h->dp[b]); hipFree(h->da0[b]); hipFree(h->da1[b]); }
     }
     if (h->o_key) { hipFree(h->o_key); hipFree(h->o_start); hipFree(h->o_end); hipFree(h->o_res); }
+    for (int c = 0; c < 5; ++c)
+        if (h->rf[c]) hipFree(h->rf[c]);
+    if (h->rf_sort) hipFree(h->rf_sort);
     if (h->h_stage) { hipHostFree(h->h_stage); hipFree(h->d_stage); hipFree(h->d_hash_stage); }
     h->free_region();
     if (h->rbeg) hipFree(h->rbeg);
@@ -1219,6 +1412,8 @@ int gw_snapshot(gw_handle* h, int32_t kg_lo, int32_t kg_hi, void* buf, int64_t c
     if (!h || !len) return GW_E_INVALID;
     if (h->failed) return h->fail(GW_E_STATE, "operator failed earlier: %s", h->err.c_str());
     if (h->session) return h->fail(GW_E_UNSUPPORTED, "snapshot of session windows is not yet supported");
+    if (h->cfg.allowed_lateness > 0)
+        return h->fail(GW_E_UNSUPPORTED, "snapshot with allowed lateness > 0 is not yet supported");
     hipSetDevice(h->cfg.device);
     return h->snapshot(kg_lo, kg_hi, buf, cap, len);
 }
@@ -1227,6 +1422,8 @@ int gw_restore(gw_handle* h, const void* buf, int64_t len) {
     if (!h) return GW_E_INVALID;
     if (h->failed) return h->fail(GW_E_STATE, "operator failed earlier: %s", h->err.c_str());
     if (h->session) return h->fail(GW_E_UNSUPPORTED, "restore of session windows is not yet supported");
+    if (h->cfg.allowed_lateness > 0)
+        return h->fail(GW_E_UNSUPPORTED, "restore with allowed lateness > 0 is not yet supported");
     hipSetDevice(h->cfg.device);
     return h->restore(buf, len);
 }

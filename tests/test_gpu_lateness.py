@@ -1,0 +1,131 @@
+"""GPU parity with allowed lateness > 0: windows keep their state
+until max timestamp + lateness (WindowOperator.cleanupTime, WindowOperator.java:670-677),
+a late record of a fired window that is not cleaned yet fires it again with the updated
+contents (EventTimeTrigger.onElement, EventTimeTrigger.java:37-45; WindowOperator.java:
+408-446), PurgingTrigger emits the late record alone, and records of cleaned windows are
+dropped and counted (isElementLate :620-624).  The CPU oracle (oracle/flink_oracle.c)
+replays the reference record by record; rows are compared per watermark as multisets."""
+import zlib
+
+import numpy as np
+import pytest
+
+from flink_amd import _native as N
+from tests.gpu_helpers import compare, gpu_operator, random_stream, run_gpu, run_oracle
+
+pytestmark = pytest.mark.gpu
+
+TOL_AGGS = {"sum_f64", "avg_f64"}
+
+CFGS = [
+    dict(assigner="tumbling", size=1000, slide=1000),
+    dict(assigner="tumbling", size=700, slide=700, offset=-300),
+    dict(assigner="sliding", size=1000, slide=250),
+    dict(assigner="sliding", size=1000, slide=300, offset=-50),
+    dict(assigner="sliding", size=10000, slide=2000),
+]
+
+
+def _cmp(g, o, agg):
+    return compare(g, o, agg in TOL_AGGS)
+
+
+def _late_stream(seed, agg, cfg, lateness, n=20000, num_keys=60, n_batches=40):
+    # disorder well beyond the watermark lag: records land in fired windows, some
+    # within the lateness, some beyond it
+    disorder = max(2500, 3 * cfg["size"]) + lateness
+    return random_stream(seed=seed, n=n, num_keys=num_keys, n_batches=n_batches, disorder=disorder, wm_lag=200,
+                         agg=agg)
+
+
+@pytest.mark.parametrize("agg", ["count", "sum_i64", "min_f64", "avg_f64", "sum_i32"])
+@pytest.mark.parametrize("lateness", [300, 2000])
+@pytest.mark.parametrize("cfg", CFGS, ids=lambda c: "-".join(str(v) for v in c.values()))
+@pytest.mark.parametrize("flags", [N.FLAG_NO_REGION, N.FLAG_FORCE_REGION], ids=["direct", "region"])
+def test_lateness_refires_vs_oracle(oracle_lib, cfg, lateness, agg, flags):
+    kw = dict(cfg, agg=agg, lateness=lateness)
+    keys, ts, vals, batches = _late_stream(zlib.crc32(f"lat{agg}{cfg}{lateness}".encode()) & 0xffff, agg, cfg,
+                                           lateness)
+    g, glate, _ = run_gpu(kw, keys, ts, vals, batches, flags=flags)
+    o, olate = run_oracle(oracle_lib, kw, keys, ts, vals, batches)
+    assert olate > 0
+    assert glate == olate
+    assert _cmp(g, o, agg) == []
+    # re-fires happened: more rows than (key, window) pairs
+    rows = sum(len(x[0]) for x in o)
+    pairs = len({(int(k), int(s)) for x in o for k, s in zip(x[0], x[1])})
+    assert rows > pairs
+
+
+@pytest.mark.parametrize("agg", ["sum_i64", "max_i64", "avg_i64"])
+@pytest.mark.parametrize("cfg", CFGS, ids=lambda c: "-".join(str(v) for v in c.values()))
+def test_lateness_purging_trigger_vs_oracle(oracle_lib, cfg, agg):
+    """PurgingTrigger: every re-fire row holds the late record alone."""
+    kw = dict(cfg, agg=agg, lateness=1500, trigger="purging_event_time")
+    keys, ts, vals, batches = _late_stream(zlib.crc32(f"purge{agg}{cfg}".encode()) & 0xffff, agg, cfg, 1500)
+    g, glate, _ = run_gpu(kw, keys, ts, vals, batches, flags=0)
+    o, olate = run_oracle(oracle_lib, kw, keys, ts, vals, batches)
+    assert glate == olate
+    assert _cmp(g, o, agg) == []
+
+
+@pytest.mark.parametrize("cfg", CFGS[:4], ids=lambda c: "-".join(str(v) for v in c.values()))
+@pytest.mark.parametrize("flags", [N.FLAG_FORCE_REGION, N.FLAG_FORCE_REGION | N.FLAG_NO_BUFFER],
+                         ids=["buffered", "unbuffered"])
+def test_lateness_two_pass_region_table(oracle_lib, cfg, flags):
+    """A two-pass (buffered) region table: late records leave the P1 buckets for the
+    re-fire list; far-future records are parked as before."""
+    kw = dict(cfg, agg="sum_i64", lateness=1200)
+    keys, ts, vals, batches = random_stream(seed=41, n=60000, num_keys=20000, n_batches=40,
+                                            disorder=max(4000, 3 * cfg["size"]), wm_lag=200, agg="sum_i64")
+    rng = np.random.default_rng(9)
+    far = rng.choice(len(ts), 300, replace=False)
+    ts[far] += rng.integers(50_000, 2_000_000, 300)
+    g, glate, _ = run_gpu(kw, keys, ts, vals, batches, flags=flags, capacity_hint=600_000)
+    o, olate = run_oracle(oracle_lib, kw, keys, ts, vals, batches)
+    assert glate == olate
+    assert compare(g, o, False) == []
+
+
+@pytest.mark.parametrize("flags", [0, N.FLAG_FORCE_REGION], ids=["auto", "region"])
+def test_lateness_watermark_jumps(oracle_lib, flags):
+    """Watermark jumps fire and clean many windows in one call; records land all over."""
+    kw = dict(assigner="sliding", size=1000, slide=250, agg="count", lateness=1700)
+    rng = np.random.default_rng(6)
+    n = 9000
+    keys = rng.integers(0, 40, n).astype(np.int64)
+    ts = rng.integers(0, 400_000, n).astype(np.int64)
+    vals = np.zeros(n, np.int64)
+    batches = [(0, 2000, -1), (2000, 4000, 50_000), (4000, 6000, 51_000), (6000, 7500, 200_000),
+               (7500, 9000, 200_900)]
+    g, glate, _ = run_gpu(kw, keys, ts, vals, batches, flags=flags)
+    o, olate = run_oracle(oracle_lib, kw, keys, ts, vals, batches)
+    assert glate == olate
+    assert compare(g, o, False) == []
+
+
+def test_lateness_preaggregation_path(oracle_lib):
+    """Few keys, many records per batch: the LDS pre-aggregation path with re-fires."""
+    kw = dict(assigner="tumbling", size=1000, slide=1000, agg="sum_i64", lateness=800)
+    keys, ts, vals, batches = random_stream(seed=3, n=40000, num_keys=5, n_batches=20, disorder=3000, wm_lag=200)
+    g, glate, stats = run_gpu(kw, keys, ts, vals, batches, flags=N.FLAG_FORCE_LDS_PREAGG)
+    o, olate = run_oracle(oracle_lib, kw, keys, ts, vals, batches)
+    assert stats["preagg_batches"] > 0
+    assert glate == olate
+    assert compare(g, o, False) == []
+
+
+def test_lateness_beyond_the_ring_is_unsupported():
+    with pytest.raises(N.GpuWinError) as ei:
+        gpu_operator(dict(assigner="sliding", size=1000, slide=100, agg="sum_i64", lateness=10_000))
+    assert ei.value.code == -2
+
+
+def test_lateness_snapshot_is_unsupported():
+    op = gpu_operator(dict(assigner="tumbling", size=1000, slide=1000, agg="sum_i64", lateness=500))
+    try:
+        with pytest.raises(N.GpuWinError) as ei:
+            op.snapshot_state()
+        assert ei.value.code == -2
+    finally:
+        op.close()
