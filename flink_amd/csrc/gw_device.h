@@ -44,9 +44,10 @@ struct DevStatus {
     unsigned long long overflow;    // session segments that did not fit (retry list length)
     unsigned long long spills;      // region apply: records left in the buffer by full regions
     unsigned long long n_refire;    // lateness > 0: re-fire list cursor (late records of fired windows)
-    unsigned long long pad[4];
+    unsigned long long pad[4];      // pad[kPubSeqWord]: stamp of a published host copy (never set on the device)
     ShardCtr sh[kShards];
 };
+constexpr int kPubSeqWord = 3;
 #define GW_DF_NO_TS 1ull
 #define GW_DF_RANGE 2ull
 #define GW_DF_TABLE_FULL 4ull

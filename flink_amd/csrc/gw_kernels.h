@@ -163,6 +163,8 @@ struct IngestArgs {
     uint32_t* r_row;       // [round][kPartBuckets] (start << 16 | count) per region of the bucket
     int64_t* r_base;       // [round] first record of the round
     unsigned long long* batch_occ;  // ring positions the buffered records touch (for k_rgn_apply)
+    DevStatus* st_host;             // buffered P1: pinned host slot k_publish_status copies the status into
+    unsigned long long st_seq;      //     and the stamp it writes last
     uint64_t ring_fresh;            // ring positions holding only identities (not in occ)
 };
 
@@ -261,6 +263,7 @@ hipError_t launch_table_init(const PaneTable& t, hipStream_t s);
 hipError_t launch_ingest(const IngestArgs& a, int path, int unroll, hipStream_t s);
 // region path: P1 over one batch (a.n records -> buffer tiles from a.tile0) ...
 hipError_t launch_region_p1(const IngestArgs& a, hipStream_t s);
+hipError_t launch_publish_status(const IngestArgs& a, hipStream_t s);
 // ... and, per flush, plan + P2 (two-pass tables) + apply over a.ntiles buffer tiles
 hipError_t launch_region_flush(const IngestArgs& a, hipStream_t s);
 // ... and after a flush that filled regions: its spilled records -> the deferred list

@@ -421,6 +421,25 @@ __device__ __forceinline__ TileLds tile_lds(unsigned char* smem) {
     return s;
 }
 
+// After a buffered P1 (same stream, one workgroup): copy the status block into the
+// host's pinned slot and stamp it with the launch's sequence number.  This replaces an
+// event + asynchronous copy on a side stream after every batch.  The slot stores are
+// system-scope and acknowledged (vmcnt) by every wave before the barrier that precedes
+// the stamp store, so no L2 write-back fence is needed.  (A last-arriver publish inside
+// P1 cost ~10 us per batch: a returning atomic per workgroup on the critical path.)
+__global__ void __launch_bounds__(256) k_publish_status(const DevStatus* st, DevStatus* host, unsigned long long seq) {
+    constexpr int kWords = (int)(sizeof(DevStatus) / 8);
+    const unsigned long long* src = reinterpret_cast<const unsigned long long*>(st);
+    unsigned long long* dst = reinterpret_cast<unsigned long long*>(host);
+    for (int i = threadIdx.x; i < kWords; i += blockDim.x)
+        if (i != kPubSeqWord + (int)(offsetof(DevStatus, pad) / 8))
+            __hip_atomic_store(&dst[i], src[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0)
+        __hip_atomic_store(&host->pad[kPubSeqWord], seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // P1: one 4096-record tile of the batch -> buffer tile a.tile0 + blockIdx.x.
 template <int AGG>
 __global__ void __launch_bounds__(kPartThreads) k_rgn_p1(IngestArgs a) {
@@ -1456,6 +1475,11 @@ hipError_t launch_region_p1(const IngestArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(k_rgn_p1<A>, dim3((unsigned)tiles), dim3(kPartThreads), part_lds, s, a)
     GW_AGG_SWITCH(a.t.agg, L);
 #undef L
+    return hipGetLastError();
+}
+
+hipError_t launch_publish_status(const IngestArgs& a, hipStream_t s) {
+    hipLaunchKernelGGL(k_publish_status, dim3(1), dim3(256), 0, s, a.st, a.st_host, a.st_seq);
     return hipGetLastError();
 }
 

@@ -7,7 +7,9 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
+#include <thread>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -218,15 +220,16 @@ struct gw_handle {
 
     bool dirty = true;  // device counters changed since the last refresh()
 
-    // Lazy status (buffered region P1 only): after a P1 launch the status is copied
-    // asynchronously; the copy of batch b is read while batch b + 1 is already queued,
-    // so the GPU does not wait for the host between watermark batches.  h_st then lags
-    // by the last batch (`lazy`): decisions that need exact counters call refresh().
-    static constexpr int kAsync = 3;  // status copies in flight: absorb the one 2 batches old
+    // Lazy status (buffered region P1 only): a one-workgroup kernel behind each P1 launch
+    // (k_publish_status, same stream) writes the status into a pinned host slot and
+    // stamps it with the launch's sequence number.  The host reads the slot of batch b
+    // while batch b + 1 is already queued, so the GPU does not wait for the host between watermark batches and
+    // the stream carries no event or copy between them.  h_st then lags by the last
+    // batches (`lazy`): decisions that need exact counters call refresh().
+    static constexpr int kAsync = 3;  // slots in flight: absorb the one 2 batches old
     DevStatus* h_st_async[kAsync] = {};
-    hipEvent_t st_ev[kAsync] = {};      // status copy done (side stream)
-    hipEvent_t p1_ev[kAsync] = {};      // P1 done (operator stream)
-    hipStream_t st_stream = nullptr;
+    uint64_t async_seq[kAsync] = {};
+    uint64_t pub_ctr = 0;
     bool async_pending[kAsync] = {};
     uint64_t async_gen[kAsync] = {};
     int64_t async_recs[kAsync] = {};    // records of the batch each copy follows
@@ -245,36 +248,53 @@ struct gw_handle {
         if (timing) { t_ingest.resolve(); t_fire.resolve(); t_apply.resolve(); }
         return absorb();
     }
-    // Queue an asynchronous status copy after the last launch; absorb the previous one
-    // (complete by now: this batch is queued behind it).
-    // The copy runs on a side stream after an event on the operator stream, so the next
-    // batch's P1 follows this one back-to-back; it may also see part of the next batch,
-    // which the bounds below allow (the counters only grow).
+    // Arm the status slot the next buffered P1 publishes into.
+    void arm_status(IngestArgs& a) {
+        const int s = async_slot;
+        volatile uint64_t* tag = (volatile uint64_t*)&h_st_async[s]->pad[kPubSeqWord];
+        *tag = 0;
+        a.st_host = h_st_async[s];
+        a.st_seq = async_seq[s] = ++pub_ctr;
+    }
+    // Wait until slot o carries its launch's stamp (the P1 has finished publishing).
+    int wait_published(int o) {
+        volatile uint64_t* tag = (volatile uint64_t*)&h_st_async[o]->pad[kPubSeqWord];
+        for (int64_t spin = 0; *tag != async_seq[o]; ++spin) {
+            if ((spin & 255) == 255) {
+                const hipError_t q = hipStreamQuery(stream);
+                if (q == hipSuccess && *tag != async_seq[o])
+                    return fail(GW_E_DEVICE, "status slot not published by the finished pass 1");
+                if (q != hipSuccess && q != hipErrorNotReady)
+                    return fail(GW_E_DEVICE, "pass 1 failed: %s", hipGetErrorString(q));
+                std::this_thread::yield();
+            }
+        }
+        std::atomic_thread_fence(std::memory_order_acquire);
+        return GW_OK;
+    }
+    // After a buffered P1 launch: absorb the slot published two launches ago.
     int lazy_status(int64_t nrec) {
         const int s = async_slot;
         hp.lap(1);
-        HIPCHECK(hipEventRecord(p1_ev[s], stream));
-        HIPCHECK(hipStreamWaitEvent(st_stream, p1_ev[s], 0));
-        HIPCHECK(hipMemcpyAsync(h_st_async[s], d_st, sizeof(DevStatus), hipMemcpyDeviceToHost, st_stream));
-        HIPCHECK(hipEventRecord(st_ev[s], st_stream));
         async_pending[s] = true;
         async_gen[s] = hgen;
         async_recs[s] = nrec;
         async_slot = (s + 1) % kAsync;
         lazy = true;
         lazy_recs += nrec;
-        const int o = async_slot;  // the oldest copy
+        const int o = async_slot;  // the oldest slot
         hp.lap(2);
         if (!async_pending[o]) return GW_OK;
         async_pending[o] = false;
-        HIPCHECK(hipEventSynchronize(st_ev[o]));
+        int rc;
+        if ((rc = wait_published(o))) return rc;
         hp.lap(3);
         if (async_gen[o] != hgen) return GW_OK;  // the host changed the status since
         memcpy(h_st, h_st_async[o], sizeof(DevStatus));
-        lazy_recs = 0;  // the batches after the absorbed copy are unaccounted for
+        lazy_recs = 0;  // the batches after the absorbed slot are unaccounted for
         for (int i = 0; i < kAsync; ++i)
             if (async_pending[i]) lazy_recs += async_recs[i];
-        const int rc = absorb();
+        rc = absorb();
         hp.lap(4);
         return rc;
     }
@@ -910,6 +930,7 @@ struct gw_handle {
                 HIPCHECK(hipMemsetAsync(d_tmp + 1, 0, 8, stream));
                 buf_fresh = ~occ;
             }
+            if (buffered) arm_status(a);
             hp.lap(0);
             if (timing) {
                 auto ev = t_ingest.get();
@@ -920,6 +941,7 @@ struct gw_handle {
             } else {
                 HIPCHECK(launch_region_p1(a, stream));
             }
+            if (buffered) HIPCHECK(launch_publish_status(a, stream));
             nseg++;
             buf_tiles += tiles;
             if (!buffered && (rc = flush_buffer())) return rc;
@@ -1215,13 +1237,11 @@ int gw_create(const gw_config* cfg, gw_handle** out) {
     hipMemset(h->d_st, 0, sizeof(DevStatus));
     memset(h->h_st, 0, sizeof(DevStatus));
     for (int i = 0; i < gw_handle::kAsync; ++i) {
-        if ((e = hipHostMalloc((void**)&h->h_st_async[i], sizeof(DevStatus), hipHostMallocDefault)) != hipSuccess ||
-            (e = hipEventCreateWithFlags(&h->st_ev[i], hipEventDisableTiming)) != hipSuccess ||
-            (e = hipEventCreateWithFlags(&h->p1_ev[i], hipEventDisableTiming)) != hipSuccess)
+        // coherent: the device's stores reach the host without a cache flush on either side
+        if ((e = hipHostMalloc((void**)&h->h_st_async[i], sizeof(DevStatus), hipHostMallocCoherent)) != hipSuccess)
             return bail(GW_E_DEVICE, std::string("status alloc: ") + hipGetErrorString(e));
+        memset(h->h_st_async[i], 0, sizeof(DevStatus));
     }
-    if ((e = hipStreamCreateWithFlags(&h->st_stream, hipStreamNonBlocking)) != hipSuccess)
-        return bail(GW_E_DEVICE, std::string("hipStreamCreate: ") + hipGetErrorString(e));
 
     const int agg = cfg->agg;
     const int words = cell_words(agg);
@@ -1285,7 +1305,6 @@ int gw_destroy(gw_handle* h) {
     if (!h) return GW_OK;
     h->hp.dump();
     if (h->stream) hipStreamSynchronize(h->stream);
-    if (h->st_stream) hipStreamSynchronize(h->st_stream);  // a status copy may still read d_st
     if (h->sess) session_destroy(h->sess);
     if (h->tv.base) hipFree(h->tv.base);
     for (int b = 0; b < 2; ++b) {
@@ -1301,12 +1320,8 @@ int gw_destroy(gw_handle* h) {
     if (h->d_st) hipFree(h->d_st);
     if (h->d_tmp) hipFree(h->d_tmp);
     if (h->h_st) hipHostFree(h->h_st);
-    for (int i = 0; i < gw_handle::kAsync; ++i) {
+    for (int i = 0; i < gw_handle::kAsync; ++i)
         if (h->h_st_async[i]) hipHostFree(h->h_st_async[i]);
-        if (h->st_ev[i]) hipEventDestroy(h->st_ev[i]);
-        if (h->p1_ev[i]) hipEventDestroy(h->p1_ev[i]);
-    }
-    if (h->st_stream) hipStreamDestroy(h->st_stream);
     h->t_ingest.destroy();
     h->t_fire.destroy();
     h->t_apply.destroy();
