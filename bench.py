@@ -165,8 +165,6 @@ def main():
         n = k.numel()
         N.check(N.lib().gw_ingest_device(op.handle, n, k.data_ptr(), None, t.data_ptr(),
                                          v.data_ptr() if v is not None else None, cur), op.handle)
-        if ex is not None and args.exchange == "a2a":
-            op.hold_until_consumed(k, t, v)  # exchange outputs: read later on the operator's stream
         wm = wms[b]
         if ex is not None:
             wm = ex.combine_watermark(wm)  # StatusWatermarkValve: min over inputs

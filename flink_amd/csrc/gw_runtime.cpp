@@ -118,6 +118,7 @@ struct gw_handle {
     std::string err;
     bool failed = false;
     hipStream_t stream = nullptr;
+    hipEvent_t ev_in = nullptr, ev_out = nullptr;  // gw_ingest_device ordering with the producer stream
     bool session = false;
 
     // pane geometry
@@ -1230,6 +1231,9 @@ int gw_create(const gw_config* cfg, gw_handle** out) {
     if (e != hipSuccess) return bail(GW_E_DEVICE, std::string("hipSetDevice: ") + hipGetErrorString(e));
     if ((e = hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking)) != hipSuccess)
         return bail(GW_E_DEVICE, std::string("hipStreamCreate: ") + hipGetErrorString(e));
+    if ((e = hipEventCreateWithFlags(&h->ev_in, hipEventDisableTiming)) != hipSuccess ||
+        (e = hipEventCreateWithFlags(&h->ev_out, hipEventDisableTiming)) != hipSuccess)
+        return bail(GW_E_DEVICE, std::string("hipEventCreate: ") + hipGetErrorString(e));
     if ((e = hipMalloc((void**)&h->d_st, sizeof(DevStatus))) != hipSuccess ||
         (e = hipMalloc((void**)&h->d_tmp, 64)) != hipSuccess ||
         (e = hipHostMalloc((void**)&h->h_st, sizeof(DevStatus), hipHostMallocDefault)) != hipSuccess)
@@ -1325,6 +1329,8 @@ int gw_destroy(gw_handle* h) {
     h->t_ingest.destroy();
     h->t_fire.destroy();
     h->t_apply.destroy();
+    if (h->ev_in) hipEventDestroy(h->ev_in);
+    if (h->ev_out) hipEventDestroy(h->ev_out);
     if (h->stream) hipStreamDestroy(h->stream);
     delete h;
     return GW_OK;
@@ -1383,16 +1389,24 @@ int gw_ingest_device(gw_handle* h, int64_t n, const int64_t* d_key, const int32_
     if (n > 0 && !d_value && h->cfg.agg != GW_COUNT) return h->fail(GW_E_INVALID, "value column required");
     (void)d_key_hash;
     hipSetDevice(h->cfg.device);
-    if (stream && (hipStream_t)stream != h->stream) {
-        hipEvent_t ev;
-        hipEventCreateWithFlags(&ev, hipEventDisableTiming);
-        hipEventRecord(ev, (hipStream_t)stream);
-        hipStreamWaitEvent(h->stream, ev, 0);
-        hipEventDestroy(ev);
+    // The producer stream (NULL = the default stream) wrote the columns; the handle's
+    // non-blocking stream reads them.  Order both ways: the reads after the writes, and
+    // whatever the producer stream does next (reusing or freeing the columns) after the
+    // reads, so a caching allocator on the producer side needs nothing more.
+    hipStream_t ps = (hipStream_t)stream;
+    const bool foreign = ps != h->stream;
+    if (foreign) {
+        hipEventRecord(h->ev_in, ps);
+        hipStreamWaitEvent(h->stream, h->ev_in, 0);
     }
     if (n == 0) return GW_OK;
     h->hp.lap(5);
-    return ingest_device_impl(h, n, d_key, d_ts, (const int64_t*)d_value);
+    int rc = ingest_device_impl(h, n, d_key, d_ts, (const int64_t*)d_value);
+    if (foreign) {
+        hipEventRecord(h->ev_out, h->stream);
+        hipStreamWaitEvent(ps, h->ev_out, 0);
+    }
+    return rc;
 }
 
 int gw_advance_watermark(gw_handle* h, int64_t wm, int64_t* rows_fired) {

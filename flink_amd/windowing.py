@@ -230,7 +230,6 @@ class GpuWindowOperator:
         c.device, c.flags, c.capacity_hint, c.max_batch = device, flags, capacity_hint, max_batch
         self.cfg = c
         self._h = None
-        self._torch_stream = None
         self._keys_in: dict = {}
         self._keys_out: list = []
         self._int_keys = True
@@ -349,20 +348,12 @@ class GpuWindowOperator:
         n = keys if isinstance(keys, int) else keys.numel()
         if isinstance(keys, int):
             raise ValueError("pass tensors, or use process_batch_device_ptr for raw pointers")
+        if stream is None:  # the columns were produced on PyTorch's current stream
+            import torch
+            stream = torch.cuda.current_stream(keys.device).cuda_stream
         rc = N.lib().gw_ingest_device(self._h, n, p(keys), None, p(timestamps), p(values),
                                       ctypes.c_void_p(stream) if stream else None)
         N.check(rc, self._h)
-        self.hold_until_consumed(keys, timestamps, values)
-
-    def hold_until_consumed(self, *tensors):
-        """The handle's stream reads device columns after gw_ingest_device returns: keep the
-        caching allocator from handing their memory out again before that work is done."""
-        import torch
-        if self._torch_stream is None:
-            self._torch_stream = torch.cuda.ExternalStream(self.stream(), device=torch.device("cuda", self.cfg.device))
-        for t in tensors:
-            if isinstance(t, torch.Tensor) and t.is_cuda:
-                t.record_stream(self._torch_stream)
 
     def process_batch_device_ptr(self, n: int, key_ptr: int, ts_ptr: int, val_ptr: Optional[int], stream=None):
         rc = N.lib().gw_ingest_device(self._h, n, ctypes.c_void_p(key_ptr), None, ctypes.c_void_p(ts_ptr),

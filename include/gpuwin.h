@@ -150,11 +150,11 @@ int  gw_abi_version(void);
 int  gw_ingest(gw_handle* h, int64_t n, const int64_t* key, const int32_t* key_hash,
                const int64_t* ts, const void* value);
 /* Same, with the columns already resident in device memory (d_* are device
- * pointers).  `stream` is a hipStream_t the inputs were produced on (NULL = the
- * handle's own stream); the call orders itself after it.  The columns are read
- * asynchronously on the handle's stream (gw_stream): the caller keeps them unchanged
- * until that work is done (order a reuse after gw_stream, or, from PyTorch,
- * record_stream the tensors on it). */
+ * pointers).  `stream` is the hipStream_t the inputs were produced on (NULL = the
+ * default stream).  The handle's stream (gw_stream) reads them after that stream's
+ * pending work, and the producer stream is made to wait for those reads, so the caller
+ * may reuse or free the columns in stream order on the producer stream (e.g. a PyTorch
+ * caching allocator) without further synchronisation. */
 int  gw_ingest_device(gw_handle* h, int64_t n, const int64_t* d_key, const int32_t* d_key_hash,
                       const int64_t* d_ts, const void* d_value, void* stream);
 /* Advance event time to wm: fire every window whose maxTimestamp (end-1) <= wm,
