@@ -41,7 +41,27 @@ EXPORTS = [
     "gw_kernel_time_ms", "gw_enable_kernel_timing", "gw_java_long_hash", "gw_murmur_hash",
     "gw_key_group_for_hash", "gw_operator_for_key_group", "gw_default_max_parallelism",
     "gw_key_groups_device", "gw_partition_scratch_bytes", "gw_partition_device",
+    "gw_decode_serialized", "gw_ingest_serialized", "gw_ingest_serialized_device",
 ]
+
+
+class GwRecordLayout(ctypes.Structure):
+    """gw_record_layout: the Tuple value type of the serialized records."""
+    _fields_ = [("nfields", ctypes.c_int32), ("key_field", ctypes.c_int32), ("value_field", ctypes.c_int32),
+                ("types", ctypes.c_char * 8)]
+
+
+class GwDecodeResult(ctypes.Structure):
+    _fields_ = [("records", ctypes.c_int64), ("watermarks", ctypes.c_int64), ("consumed", ctypes.c_int64),
+                ("skipped", ctypes.c_int64)]
+
+
+def record_layout(types: str, key_field: int, value_field: int = -1) -> GwRecordLayout:
+    """types: JVM type codes of the Tuple fields, e.g. "JJ" for Tuple2<Long, Long>."""
+    lay = GwRecordLayout()
+    lay.nfields, lay.key_field, lay.value_field = len(types), key_field, value_field
+    lay.types = types.encode()
+    return lay
 
 
 class NativeLibraryError(RuntimeError):
@@ -132,6 +152,10 @@ def lib() -> ctypes.CDLL:
         "gw_key_groups_device": (c_int, [i64, p, p, i32, i32, p, p, p]),
         "gw_partition_scratch_bytes": (i64, [i64, i32]),
         "gw_partition_device": (c_int, [i64, p, p, p, p, i32, i32, p, p, p, p, p, p]),
+        "gw_decode_serialized": (c_int, [p, i64, ctypes.POINTER(GwRecordLayout), p, p, p, i64, p, p, i64,
+                                         ctypes.POINTER(GwDecodeResult), p]),
+        "gw_ingest_serialized": (c_int, [p, p, i64, ctypes.POINTER(GwRecordLayout), P64, P64]),
+        "gw_ingest_serialized_device": (c_int, [p, p, i64, ctypes.POINTER(GwRecordLayout), p, P64, P64]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)

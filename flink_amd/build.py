@@ -17,7 +17,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "libgpuwin.so")
 OBJDIR = os.path.join(HERE, "_build")
-SOURCES = ["gw_pane.hip", "gw_keygroups.hip", "gw_sort.hip", "gw_session.hip", "gw_runtime.cpp"]
+SOURCES = ["gw_pane.hip", "gw_keygroups.hip", "gw_sort.hip", "gw_session.hip", "gw_netbuf.hip", "gw_runtime.cpp"]
 ARCH = os.environ.get("GW_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 CFLAGS = ["-O3", "-fPIC", "-std=c++17", "-munsafe-fp-atomics", f"--offload-arch={ARCH}",

@@ -19,6 +19,7 @@
 #include <vector>
 
 #include "gw_kernels.h"
+#include "gw_netbuf.h"
 #include "gw_session.h"
 #include "gw_sort.h"
 
@@ -119,6 +120,22 @@ struct gw_handle {
     bool failed = false;
     hipStream_t stream = nullptr;
     hipEvent_t ev_in = nullptr, ev_out = nullptr;  // gw_ingest_device ordering with the producer stream
+
+    // network-buffer ingest (gw_ingest_serialized*): grow-only device scratch, decoded
+    // columns, watermark list, pinned status and staging for host bytes
+    void* nb_scratch = nullptr;
+    int64_t nb_scratch_cap = 0;
+    int64_t* nb_cols = nullptr;  // key | ts | value, nb_rec_cap each
+    int64_t nb_rec_cap = 0;
+    int64_t* nb_wm = nullptr;    // position | value, nb_wm_cap each
+    int64_t nb_wm_cap = 0;
+    NbStatus* d_nbst = nullptr;
+    NbStatus* h_nbst = nullptr;  // pinned
+    int64_t* h_nbwm = nullptr;   // pinned, 2 * kNbWmHost
+    uint8_t* h_nbbytes = nullptr;
+    uint8_t* d_nbbytes = nullptr;
+    int64_t nb_bytes_cap = 0;
+    static constexpr int64_t kNbWmHost = 4096;
     bool session = false;
 
     // pane geometry
@@ -1329,6 +1346,14 @@ int gw_destroy(gw_handle* h) {
     h->t_ingest.destroy();
     h->t_fire.destroy();
     h->t_apply.destroy();
+    if (h->nb_scratch) hipFree(h->nb_scratch);
+    if (h->nb_cols) hipFree(h->nb_cols);
+    if (h->nb_wm) hipFree(h->nb_wm);
+    if (h->d_nbst) hipFree(h->d_nbst);
+    if (h->h_nbst) hipHostFree(h->h_nbst);
+    if (h->h_nbwm) hipHostFree(h->h_nbwm);
+    if (h->h_nbbytes) hipHostFree(h->h_nbbytes);
+    if (h->d_nbbytes) hipFree(h->d_nbbytes);
     if (h->ev_in) hipEventDestroy(h->ev_in);
     if (h->ev_out) hipEventDestroy(h->ev_out);
     if (h->stream) hipStreamDestroy(h->stream);
@@ -1407,6 +1432,225 @@ int gw_ingest_device(gw_handle* h, int64_t n, const int64_t* d_key, const int32_
         hipStreamWaitEvent(ps, h->ev_out, 0);
     }
     return rc;
+}
+
+// ---- network-buffer ingest ---------------------------------------------------
+// Validates the record layout (and, with agg >= 0, that the aggregated field's type
+// suits the aggregate: a Long/Integer/Short/Byte field for the integer aggregates, a
+// Double/Float field for the floating-point ones, as SumAggregator / ComparableAggregator
+// require a field of the result's type, RS/api/functions/aggregation/SumFunction.java).
+static int nb_layout(const gw_record_layout* lay, int agg, NbLayout& L, std::string& why) {
+    if (!lay) { why = "null record layout"; return GW_E_INVALID; }
+    if (lay->nfields < 1 || lay->nfields > GW_MAX_FIELDS) { why = "layout: 1..8 fields"; return GW_E_INVALID; }
+    int off[GW_MAX_FIELDS], vb = 0;
+    for (int i = 0; i < lay->nfields; ++i) {
+        const int w = nb_field_width(lay->types[i]);
+        if (w < 0) { why = std::string("layout: unknown type code '") + lay->types[i] + "'"; return GW_E_INVALID; }
+        off[i] = vb;
+        vb += w;
+    }
+    if (lay->key_field < 0 || lay->key_field >= lay->nfields || lay->types[lay->key_field] != 'J') {
+        why = "layout: the key field must be a Long ('J')";
+        return GW_E_INVALID;
+    }
+    if (lay->value_field < -1 || lay->value_field >= lay->nfields) { why = "layout: bad value field"; return GW_E_INVALID; }
+    L.vbytes = vb;
+    L.key_off = off[lay->key_field];
+    L.val_off = lay->value_field >= 0 ? off[lay->value_field] : 0;
+    L.val_type = lay->value_field >= 0 ? lay->types[lay->value_field] : 0;
+    if (agg < 0) return GW_OK;
+    if (agg == GW_COUNT) { L.val_type = 0; return GW_OK; }
+    if (!L.val_type) { why = "layout: the aggregate needs a value field"; return GW_E_INVALID; }
+    const char t = (char)L.val_type;
+    const bool fp = result_is_double(agg) && agg != GW_AVG_I64;
+    const bool ok = fp ? (t == 'D' || t == 'F') : (t == 'J' || t == 'I' || t == 'S' || t == 'B');
+    if (!ok) { why = std::string("layout: field type '") + t + "' does not match the aggregate"; return GW_E_INVALID; }
+    return GW_OK;
+}
+
+static int nb_status_code(const NbStatus& st, std::string& why) {
+    if (st.corrupt) { why = "Corrupt stream: unknown tag or element length (StreamElementSerializer)"; return GW_E_INVALID; }
+    if (st.unsupported) { why = "stream element longer than GW_MAX_ELEMENT bytes"; return GW_E_UNSUPPORTED; }
+    if (st.full) { why = "decoded records / watermarks exceed the output capacity"; return GW_E_OUTPUT_FULL; }
+    return GW_OK;
+}
+
+int gw_decode_serialized(const void* d_bytes, int64_t nbytes, const gw_record_layout* layout, int64_t* d_key,
+                         int64_t* d_ts, int64_t* d_value, int64_t rec_cap, int64_t* d_wm_pos, int64_t* d_wm_val,
+                         int64_t wm_cap, gw_decode_result* out, void* stream) {
+    NbLayout L{};
+    std::string why;
+    int rc = nb_layout(layout, -1, L, why);
+    if (rc) { g_create_error = why; return rc; }
+    if (nbytes < 0 || (nbytes > 0 && !d_bytes) || !out || ((uintptr_t)d_bytes & 3)) {
+        g_create_error = "bad byte buffer (device pointer, 4-byte aligned)";
+        return GW_E_INVALID;
+    }
+    if ((rec_cap > 0 && (!d_key || !d_ts)) || (wm_cap > 0 && (!d_wm_pos || !d_wm_val))) {
+        g_create_error = "null output column";
+        return GW_E_INVALID;
+    }
+    hipStream_t s = (hipStream_t)stream;
+    void* scratch = nullptr;
+    NbStatus* d_st = nullptr;
+    NbStatus hst{};
+    hipError_t e = hipMalloc(&scratch, (size_t)nb_scratch_bytes(nbytes));
+    if (e == hipSuccess) e = hipMalloc((void**)&d_st, sizeof(NbStatus));
+    if (e == hipSuccess)
+        e = launch_nb_decode((const uint8_t*)d_bytes, nbytes, L, d_key, d_ts, d_value, rec_cap, d_wm_pos, d_wm_val,
+                             wm_cap, scratch, d_st, s);
+    if (e == hipSuccess) e = hipMemcpyAsync(&hst, d_st, sizeof(NbStatus), hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (scratch) hipFree(scratch);
+    if (d_st) hipFree(d_st);
+    if (e != hipSuccess) { g_create_error = std::string("decode: ") + hipGetErrorString(e); return GW_E_DEVICE; }
+    out->records = hst.records;
+    out->watermarks = hst.watermarks;
+    out->consumed = hst.consumed;
+    out->skipped = (int64_t)hst.skipped;
+    rc = nb_status_code(hst, why);
+    if (rc) g_create_error = why;
+    return rc;
+}
+
+static int nb_ensure(gw_handle* h, int64_t nbytes, const NbLayout& L) {
+    auto grow = [&](void** p, int64_t& cap, int64_t want, int64_t unit) -> hipError_t {
+        if (want <= cap) return hipSuccess;
+        if (*p) hipFree(*p);
+        *p = nullptr;
+        cap = 0;
+        hipError_t e = hipMalloc(p, (size_t)(want * unit));
+        if (e == hipSuccess) cap = want;
+        return e;
+    };
+    const int64_t want = std::max<int64_t>(nbytes, 1 << 16);
+    // upper bounds: every element a record without timestamp / a watermark
+    const int64_t recs = want / (4 + 1 + L.vbytes) + 1, wms = want / 13 + 1;
+    hipError_t e = grow(&h->nb_scratch, h->nb_scratch_cap, nb_scratch_bytes(want), 1);
+    if (e == hipSuccess) e = grow((void**)&h->nb_cols, h->nb_rec_cap, recs, 24);
+    if (e == hipSuccess) e = grow((void**)&h->nb_wm, h->nb_wm_cap, wms, 16);
+    if (e == hipSuccess && !h->d_nbst) e = hipMalloc((void**)&h->d_nbst, sizeof(NbStatus));
+    if (e == hipSuccess && !h->h_nbst) e = hipHostMalloc((void**)&h->h_nbst, sizeof(NbStatus), hipHostMallocDefault);
+    if (e == hipSuccess && !h->h_nbwm)
+        e = hipHostMalloc((void**)&h->h_nbwm, 2 * gw_handle::kNbWmHost * 8, hipHostMallocDefault);
+    if (e != hipSuccess) return h->fail(GW_E_OOM, "network-buffer scratch: %s", hipGetErrorString(e));
+    return GW_OK;
+}
+
+// Decode on the handle's stream, then replay the channel: records between two watermarks
+// as one batch, each watermark as gw_advance_watermark (StreamTaskNetworkInput.processElement,
+// RS/runtime/io/AbstractStreamTaskNetworkInput.java:210-235; one channel's
+// StatusWatermarkValve forwards every advancing watermark, StatusWatermarkValve.java:153-185).
+static int nb_ingest_on_stream(gw_handle* h, const uint8_t* d_bytes, int64_t nbytes, const NbLayout& L,
+                               int64_t* consumed, int64_t* rows_fired) {
+    int rc = nb_ensure(h, nbytes, L);
+    if (rc) return rc;
+    int64_t* k = h->nb_cols;
+    int64_t* t = h->nb_cols + h->nb_rec_cap;
+    int64_t* v = h->nb_cols + 2 * h->nb_rec_cap;
+    int64_t* wp = h->nb_wm;
+    int64_t* wv = h->nb_wm + h->nb_wm_cap;
+    hipError_t e = launch_nb_decode(d_bytes, nbytes, L, k, t, L.val_type ? v : nullptr, h->nb_rec_cap, wp, wv,
+                                    h->nb_wm_cap, h->nb_scratch, h->d_nbst, h->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(h->h_nbst, h->d_nbst, sizeof(NbStatus), hipMemcpyDeviceToHost, h->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(h->h_nbwm, wp, gw_handle::kNbWmHost * 8, hipMemcpyDeviceToHost, h->stream);
+    if (e == hipSuccess)
+        e = hipMemcpyAsync(h->h_nbwm + gw_handle::kNbWmHost, wv, gw_handle::kNbWmHost * 8, hipMemcpyDeviceToHost,
+                           h->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+    if (e != hipSuccess) return h->fail(GW_E_DEVICE, "network-buffer decode: %s", hipGetErrorString(e));
+    const NbStatus st = *h->h_nbst;
+    std::string why;
+    rc = nb_status_code(st, why);
+    if (rc) {
+        h->fail(rc, "%s", why.c_str());
+        if (rc == GW_E_INVALID) h->failed = true;  // IOException: the task fails
+        return rc;
+    }
+    std::vector<int64_t> wpos, wval;
+    const int64_t nw = st.watermarks;
+    if (nw > gw_handle::kNbWmHost) {
+        wpos.resize(nw);
+        wval.resize(nw);
+        e = hipMemcpy(wpos.data(), wp, nw * 8, hipMemcpyDeviceToHost);
+        if (e == hipSuccess) e = hipMemcpy(wval.data(), wv, nw * 8, hipMemcpyDeviceToHost);
+        if (e != hipSuccess) return h->fail(GW_E_DEVICE, "watermark list: %s", hipGetErrorString(e));
+    } else {
+        wpos.assign(h->h_nbwm, h->h_nbwm + nw);
+        wval.assign(h->h_nbwm + gw_handle::kNbWmHost, h->h_nbwm + gw_handle::kNbWmHost + nw);
+    }
+    int64_t fired = 0, done = 0;
+    for (int64_t i = 0; i <= nw; ++i) {
+        const int64_t upto = i < nw ? wpos[i] : st.records;
+        if (upto > done) {
+            rc = ingest_device_impl(h, upto - done, k + done, t + done, L.val_type ? v + done : nullptr);
+            if (rc) return rc;
+            done = upto;
+        }
+        if (i < nw) {
+            int64_t f = 0;
+            rc = gw_advance_watermark(h, wval[i], &f);
+            if (rc) return rc;
+            fired += f;
+        }
+    }
+    if (consumed) *consumed = st.consumed;
+    if (rows_fired) *rows_fired = fired;
+    return GW_OK;
+}
+
+int gw_ingest_serialized_device(gw_handle* h, const void* d_bytes, int64_t nbytes, const gw_record_layout* layout,
+                                void* stream, int64_t* consumed, int64_t* rows_fired) {
+    if (!h) return GW_E_INVALID;
+    if (h->failed) return h->fail(GW_E_STATE, "operator failed earlier: %s", h->err.c_str());
+    NbLayout L{};
+    std::string why;
+    int rc = nb_layout(layout, h->cfg.agg, L, why);
+    if (rc) return h->fail(rc, "%s", why.c_str());
+    if (nbytes < 0 || (nbytes > 0 && !d_bytes) || ((uintptr_t)d_bytes & 3))
+        return h->fail(GW_E_INVALID, "bad byte buffer (device pointer, 4-byte aligned)");
+    if (consumed) *consumed = 0;
+    if (rows_fired) *rows_fired = 0;
+    if (nbytes == 0) return GW_OK;
+    hipSetDevice(h->cfg.device);
+    hipStream_t ps = (hipStream_t)stream;
+    if (ps != h->stream) {
+        hipEventRecord(h->ev_in, ps);
+        hipStreamWaitEvent(h->stream, h->ev_in, 0);
+    }
+    // the decode has read the bytes once this returns (it synchronises the handle's stream)
+    return nb_ingest_on_stream(h, (const uint8_t*)d_bytes, nbytes, L, consumed, rows_fired);
+}
+
+int gw_ingest_serialized(gw_handle* h, const void* bytes, int64_t nbytes, const gw_record_layout* layout,
+                         int64_t* consumed, int64_t* rows_fired) {
+    if (!h) return GW_E_INVALID;
+    if (h->failed) return h->fail(GW_E_STATE, "operator failed earlier: %s", h->err.c_str());
+    NbLayout L{};
+    std::string why;
+    int rc = nb_layout(layout, h->cfg.agg, L, why);
+    if (rc) return h->fail(rc, "%s", why.c_str());
+    if (nbytes < 0 || (nbytes > 0 && !bytes)) return h->fail(GW_E_INVALID, "null byte buffer");
+    if (consumed) *consumed = 0;
+    if (rows_fired) *rows_fired = 0;
+    if (nbytes == 0) return GW_OK;
+    hipSetDevice(h->cfg.device);
+    if (nbytes > h->nb_bytes_cap) {
+        if (h->h_nbbytes) { hipHostFree(h->h_nbbytes); hipFree(h->d_nbbytes); }
+        h->h_nbbytes = nullptr;
+        h->d_nbbytes = nullptr;
+        h->nb_bytes_cap = 0;
+        const int64_t cap = std::max<int64_t>(nbytes, 1 << 20);
+        hipError_t e = hipHostMalloc((void**)&h->h_nbbytes, (size_t)cap, hipHostMallocDefault);
+        if (e == hipSuccess) e = hipMalloc((void**)&h->d_nbbytes, (size_t)cap);
+        if (e != hipSuccess) return h->fail(GW_E_OOM, "network-buffer staging: %s", hipGetErrorString(e));
+        h->nb_bytes_cap = cap;
+    }
+    // the previous call synchronised the stream, so the pinned staging is free
+    memcpy(h->h_nbbytes, bytes, (size_t)nbytes);
+    hipError_t e = hipMemcpyAsync(h->d_nbbytes, h->h_nbbytes, (size_t)nbytes, hipMemcpyHostToDevice, h->stream);
+    if (e != hipSuccess) return h->fail(GW_E_DEVICE, "H2D: %s", hipGetErrorString(e));
+    return nb_ingest_on_stream(h, h->d_nbbytes, nbytes, L, consumed, rows_fired);
 }
 
 int gw_advance_watermark(gw_handle* h, int64_t wm, int64_t* rows_fired) {

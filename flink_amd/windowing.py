@@ -339,6 +339,44 @@ class GpuWindowOperator:
         rc = N.lib().gw_ingest(self._h, len(keys), _ptr(keys), _ptr(key_hashes), _ptr(timestamps), _ptr(values))
         N.check(rc, self._h)
 
+    # network-buffer surface -----------------------------------------------------------
+    def process_serialized(self, data: bytes, layout: "N.GwRecordLayout") -> tuple:
+        """Decode and process one input channel's serialized elements (records and
+        watermarks) on the GPU (gw_ingest_serialized).  Returns (consumed, rows_fired):
+        bytes past `consumed` belong to an element spanning into the next buffer and must
+        be passed again, prepended to it."""
+        consumed, fired = ctypes.c_int64(0), ctypes.c_int64(0)
+        buf = ctypes.create_string_buffer(bytes(data), len(data)) if data else None
+        N.check(N.lib().gw_ingest_serialized(self._h, buf, len(data), ctypes.byref(layout), ctypes.byref(consumed),
+                                             ctypes.byref(fired)), self._h)
+        return consumed.value, fired.value
+
+    def process_serialized_device(self, data, layout: "N.GwRecordLayout", stream=None) -> tuple:
+        """Same, with the bytes in a device uint8 tensor."""
+        if stream is None:
+            import torch
+            stream = torch.cuda.current_stream(data.device).cuda_stream
+        consumed, fired = ctypes.c_int64(0), ctypes.c_int64(0)
+        N.check(N.lib().gw_ingest_serialized_device(self._h, ctypes.c_void_p(data.data_ptr()), data.numel(),
+                                                    ctypes.byref(layout),
+                                                    ctypes.c_void_p(stream) if stream else None,
+                                                    ctypes.byref(consumed), ctypes.byref(fired)), self._h)
+        return consumed.value, fired.value
+
+    def process_buffers(self, buffers, layout: "N.GwRecordLayout") -> int:
+        """Feed network buffers in order, carrying a spanning record's bytes over to the next
+        buffer (SpanningWrapper).  Returns the rows fired."""
+        carry = b""
+        fired = 0
+        for b in buffers:
+            data = carry + bytes(b)
+            used, f = self.process_serialized(data, layout)
+            carry = data[used:]
+            fired += f
+        if carry:
+            raise N.GpuWinError(-1, f"{len(carry)} bytes of an incomplete element at the end of the input")
+        return fired
+
     def process_batch_device(self, keys, timestamps, values=None, stream=None):
         """Columns already in HBM (torch tensors or raw device pointers)."""
         def p(x):

@@ -183,6 +183,62 @@ int  gw_snapshot(gw_handle* h, int32_t kg_lo, int32_t kg_hi, void* buf, int64_t 
  * of the state: like Flink after a restore it starts at Long.MIN_VALUE. */
 int  gw_restore(gw_handle* h, const void* buf, int64_t len);
 
+/* ---- network-buffer ingest ----------------------------- */
+/* Layout of the record value: a Flink Tuple of fixed-width fields as TupleSerializer
+ * writes them (fields in order, no null markers; flink-core/.../api/java/typeutils/
+ * runtime/TupleSerializer.java:139-145), each field big-endian as DataOutputView
+ * writes it (LongSerializer.serialize = writeLong, DoubleSerializer = writeDouble,
+ * IntSerializer = writeInt, ...).  Type codes are JVM descriptors:
+ *   'J' long, 'D' double, 'I' int, 'F' float, 'S' short, 'B' byte, 'Z' boolean. */
+#define GW_MAX_FIELDS 8
+typedef struct gw_record_layout {
+    int32_t nfields;               /* fields of the Tuple (1..GW_MAX_FIELDS)             */
+    int32_t key_field;             /* index of the Long key field (keyBy(t -> t.fN))     */
+    int32_t value_field;           /* index of the aggregated field; -1 for GW_COUNT     */
+    char    types[GW_MAX_FIELDS];  /* type code per field                                */
+} gw_record_layout;
+
+/* Result of decoding one input channel's bytes. */
+typedef struct gw_decode_result {
+    int64_t records;    /* StreamRecords decoded (columns written)                         */
+    int64_t watermarks; /* Watermark elements (wm_pos/wm_val written)                      */
+    int64_t consumed;   /* bytes up to the end of the last complete element; the caller
+                           keeps the rest and prepends it to the next call (a record
+                           spanning network buffers, SpanningWrapper)                      */
+    int64_t skipped;    /* latency markers, stream status and record attributes            */
+} gw_decode_result;
+
+/* Decode the serialized stream elements of one input channel on the device.  The bytes
+ * are the concatenated payloads of the channel's network buffers: per element a 4-byte
+ * big-endian length, then StreamElementSerializer's tag and body
+ * (RecordWriter.serializeRecord, flink-runtime/.../io/network/api/writer/
+ * RecordWriter.java:144-156; StreamElementSerializer.serialize/deserialize,
+ * RS/runtime/streamrecord/StreamElementSerializer.java:163-225).  Records go to the
+ * columns (key, timestamp, value as 8-byte int64 / IEEE double bits; a record without
+ * timestamp gets Long.MIN_VALUE), watermarks to (wm_pos = number of records before it,
+ * wm_val).  Elements are at most GW_MAX_ELEMENT bytes long including the length word.
+ * Synchronous; allocates its own scratch.  GW_E_INVALID on a corrupt stream ("Corrupt
+ * stream, found tag"), GW_E_OUTPUT_FULL if rec_cap / wm_cap are too small. */
+#define GW_MAX_ELEMENT 64
+int  gw_decode_serialized(const void* d_bytes, int64_t nbytes, const gw_record_layout* layout,
+                          int64_t* d_key, int64_t* d_ts, int64_t* d_value, int64_t rec_cap,
+                          int64_t* d_wm_pos, int64_t* d_wm_val, int64_t wm_cap,
+                          gw_decode_result* out, void* stream);
+/* Decode and process one input channel's bytes on the operator: the records between
+ * two watermarks go through gw_ingest, each watermark through gw_advance_watermark —
+ * what StreamTaskNetworkInput.processElement does per element (RS/runtime/io/
+ * AbstractStreamTaskNetworkInput.java:152-175, processElement :205-230) with a single
+ * input channel's StatusWatermarkValve.  *consumed (may be NULL) as in
+ * gw_decode_result; *rows_fired (may be NULL) counts the rows the watermarks fired.
+ * One host synchronisation per call (the watermark positions): pass many buffers at
+ * once. */
+int  gw_ingest_serialized(gw_handle* h, const void* bytes, int64_t nbytes, const gw_record_layout* layout,
+                          int64_t* consumed, int64_t* rows_fired);
+/* Same, with the bytes in device memory, produced on `stream` (NULL = default stream). */
+int  gw_ingest_serialized_device(gw_handle* h, const void* d_bytes, int64_t nbytes,
+                                 const gw_record_layout* layout, void* stream, int64_t* consumed,
+                                 int64_t* rows_fired);
+
 /* Bounded input ended (BoundedOneInput.endInput) — equivalent to MAX_WATERMARK. */
 int  gw_end_input(gw_handle* h, int64_t* rows_fired);
 

@@ -997,3 +997,118 @@ int64_t wo_run_parallel(const gw_config* cfg, int threads, int64_t nb, const int
     free(args);
     return rc ? rc : rows;
 }
+
+/* ---------------------------------------------------------------------------
+ * Network-buffer decode, one input channel, sequential —
+ * the way the reference's record deserializer walks a buffer:
+ *   - length word: NonSpanningWrapper.readInt = getIntBigEndian
+ *     (flink-runtime/.../io/network/api/serialization/NonSpanningWrapper.java:142-144);
+ *     a record that does not fit the remaining bytes waits for the next buffer
+ *     (hasCompleteLength / canReadRecord :351-357, SpanningWrapper);
+ *   - element: StreamElementSerializer.deserialize
+ *     (RS/runtime/streamrecord/StreamElementSerializer.java:200-225): tag byte, then
+ *     REC_WITH_TIMESTAMP (0): long ts + value; REC_WITHOUT_TIMESTAMP (1): value;
+ *     WATERMARK (2): long; INTERNAL_WATERMARK (6): int subpartition + long;
+ *     STREAM_STATUS (4): int; LATENCY_MARKER (3): long, long, long, int;
+ *     RECORD_ATTRIBUTES (5): boolean; any other tag: "Corrupt stream" IOException;
+ *   - value: TupleSerializer.serialize writes the fields in order
+ *     (flink-core/.../api/java/typeutils/runtime/TupleSerializer.java:135-144), each
+ *     with its DataOutputView primitive (big-endian).
+ * A record without timestamp carries Long.MIN_VALUE (StreamRecord.getTimestamp).
+ * ------------------------------------------------------------------------- */
+static int field_width(char t) {
+    switch (t) {
+        case 'J': case 'D': return 8;
+        case 'I': case 'F': return 4;
+        case 'S': return 2;
+        case 'B': case 'Z': return 1;
+        default: return -1;
+    }
+}
+
+static uint64_t be_read(const uint8_t* p, int w) {
+    uint64_t v = 0;
+    for (int i = 0; i < w; i++) v = (v << 8) | p[i];
+    return v;
+}
+
+/* field -> the 8-byte value column: integral types sign-extended to int64,
+ * float widened to double (Java's float -> double conversion is exact). */
+static int64_t field_to_bits(char t, const uint8_t* p) {
+    uint64_t u = be_read(p, field_width(t));
+    switch (t) {
+        case 'J': case 'D': return (int64_t)u;
+        case 'I': return (int64_t)(int32_t)(uint32_t)u;
+        case 'S': return (int64_t)(int16_t)(uint16_t)u;
+        case 'B': return (int64_t)(int8_t)(uint8_t)u;
+        case 'Z': return (int64_t)(u != 0);
+        case 'F': {
+            uint32_t b = (uint32_t)u;
+            float f;
+            double d;
+            int64_t r;
+            memcpy(&f, &b, 4);
+            d = (double)f;
+            memcpy(&r, &d, 8);
+            return r;
+        }
+    }
+    return 0;
+}
+
+int wo_decode_stream(const uint8_t* buf, int64_t nbytes, const gw_record_layout* lay,
+                     int64_t* key, int64_t* ts, int64_t* value_bits, int64_t rec_cap,
+                     int64_t* wm_pos, int64_t* wm_val, int64_t wm_cap, gw_decode_result* out) {
+    if (!lay || lay->nfields < 1 || lay->nfields > GW_MAX_FIELDS) return GW_E_INVALID;
+    int off[GW_MAX_FIELDS], vbytes = 0;
+    for (int i = 0; i < lay->nfields; i++) {
+        int w = field_width(lay->types[i]);
+        if (w < 0) return GW_E_INVALID;
+        off[i] = vbytes;
+        vbytes += w;
+    }
+    if (lay->key_field < 0 || lay->key_field >= lay->nfields || lay->types[lay->key_field] != 'J')
+        return GW_E_INVALID;
+    if (lay->value_field >= lay->nfields) return GW_E_INVALID;
+    int64_t pos = 0, nr = 0, nw = 0, sk = 0;
+    while (pos + 4 <= nbytes) {
+        int64_t len = (int32_t)(uint32_t)be_read(buf + pos, 4);
+        if (len < 1) return GW_E_INVALID;
+        if (len + 4 > GW_MAX_ELEMENT) return GW_E_UNSUPPORTED; /* valid in Flink, beyond the GPU decoder */
+        if (pos + 4 + len > nbytes) break; /* spans into the next buffer */
+        const uint8_t* e = buf + pos + 4;
+        int tag = e[0];
+        if (tag == 0 || tag == 1) {
+            int hdr = tag == 0 ? 9 : 1;
+            if (len != hdr + vbytes) return GW_E_INVALID;
+            if (nr >= rec_cap) return GW_E_OUTPUT_FULL;
+            const uint8_t* v = e + hdr;
+            ts[nr] = tag == 0 ? (int64_t)be_read(e + 1, 8) : INT64_MIN;
+            key[nr] = (int64_t)be_read(v + off[lay->key_field], 8);
+            if (value_bits)
+                value_bits[nr] = lay->value_field >= 0
+                                     ? field_to_bits(lay->types[lay->value_field], v + off[lay->value_field])
+                                     : 0;
+            nr++;
+        } else if (tag == 2 || tag == 6) {
+            if (len != (tag == 2 ? 9 : 13)) return GW_E_INVALID;
+            if (nw >= wm_cap) return GW_E_OUTPUT_FULL;
+            wm_pos[nw] = nr;
+            wm_val[nw] = (int64_t)be_read(e + (tag == 2 ? 1 : 5), 8);
+            nw++;
+        } else if (tag == 3 || tag == 4 || tag == 5) {
+            if (len != (tag == 3 ? 29 : tag == 4 ? 5 : 2)) return GW_E_INVALID;
+            sk++;
+        } else {
+            return GW_E_INVALID;
+        }
+        pos += 4 + len;
+    }
+    if (out) {
+        out->records = nr;
+        out->watermarks = nw;
+        out->consumed = pos;
+        out->skipped = sk;
+    }
+    return GW_OK;
+}

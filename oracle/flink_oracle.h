@@ -73,6 +73,12 @@ int64_t wo_run_parallel(const gw_config* cfg, int threads, int64_t n_batches,
                         const int64_t* key, const int64_t* ts, const int64_t* value_bits,
                         int64_t* checksum, double* seconds);
 
+/* Sequential decode of one input channel's serialized stream elements (the GPU's
+ * gw_decode_serialized restated record by record). */
+int     wo_decode_stream(const uint8_t* buf, int64_t nbytes, const gw_record_layout* lay,
+                         int64_t* key, int64_t* ts, int64_t* value_bits, int64_t rec_cap,
+                         int64_t* wm_pos, int64_t* wm_val, int64_t wm_cap, gw_decode_result* out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -60,6 +60,35 @@ def make_config(assigner="tumbling", size=0, slide=0, offset=0, gap=0, lateness=
     return c
 
 
+class GwRecordLayout(ctypes.Structure):
+    """include/gpuwin.h gw_record_layout."""
+    _fields_ = [("nfields", ctypes.c_int32), ("key_field", ctypes.c_int32), ("value_field", ctypes.c_int32),
+                ("types", ctypes.c_char * 8)]
+
+
+class GwDecodeResult(ctypes.Structure):
+    _fields_ = [("records", ctypes.c_int64), ("watermarks", ctypes.c_int64), ("consumed", ctypes.c_int64),
+                ("skipped", ctypes.c_int64)]
+
+
+def decode_stream(data: bytes, types: str, key_field: int, value_field: int = -1):
+    """Sequential decode of one channel's serialized elements (wo_decode_stream).
+    Returns (rc, key, ts, value_bits, wm_pos, wm_val, result)."""
+    lay = GwRecordLayout()
+    lay.nfields, lay.key_field, lay.value_field = len(types), key_field, value_field
+    lay.types = types.encode()
+    n = len(data)
+    cap = n // 6 + 1
+    key, ts, val = (np.zeros(cap, dtype=np.int64) for _ in range(3))
+    wp, wv = np.zeros(cap, dtype=np.int64), np.zeros(cap, dtype=np.int64)
+    res = GwDecodeResult()
+    buf = np.frombuffer(data, dtype=np.uint8) if n else np.zeros(1, dtype=np.uint8)
+    rc = lib().wo_decode_stream(buf.ctypes.data, n, ctypes.byref(lay), key.ctypes.data, ts.ctypes.data,
+                                val.ctypes.data, cap, wp.ctypes.data, wv.ctypes.data, cap, ctypes.byref(res))
+    r, w = res.records, res.watermarks
+    return rc, key[:r], ts[:r], val[:r], wp[:w], wv[:w], res
+
+
 def build(force: bool = False) -> str:
     src = os.path.join(_HERE, "flink_oracle.c")
     if force or not os.path.exists(_LIB_PATH) or os.path.getmtime(_LIB_PATH) < os.path.getmtime(src):
@@ -97,6 +126,8 @@ def lib() -> ctypes.CDLL:
             ("wo_late_dropped", i64, [p]), ("wo_current_watermark", i64, [p]),
             ("wo_state_entries", i64, [p]), ("wo_timer_count", i64, [p]),
             ("wo_session_merges", i64, [p]), ("wo_last_error", ctypes.c_char_p, [p]),
+            ("wo_decode_stream", ctypes.c_int, [p, i64, ctypes.POINTER(GwRecordLayout), p, p, p, i64, p, p, i64,
+                                                 ctypes.POINTER(GwDecodeResult)]),
             ("wo_run_parallel", i64, [ctypes.POINTER(GwConfig), ctypes.c_int, i64, p, p, p, p, p,
                                        P64, ctypes.POINTER(ctypes.c_double)]),
         ]:
