@@ -7,7 +7,7 @@
 
 namespace gw {
 
-constexpr int kNbChunk = 4096;  // bytes per wave in the chain walk
+constexpr int kNbChunk = 1024;  // bytes per wave in the chain walk
 
 // The record value layout reduced to what the decoder needs (validated on the host).
 struct NbLayout {

@@ -19,72 +19,126 @@
 // per-chunk record / watermark counts into output offsets, and k_nb_decode walks each
 // chunk's true chain once more, out of LDS, and decodes its elements with all 64 lanes
 // (byte-swaps, tag dispatch, coalesced column stores).
+#include <cstdlib>
+
 #include "gw_kernels.h"
 #include "gw_netbuf.h"
 
 namespace gw {
 
-constexpr int kNbLanes = GW_MAX_ELEMENT;            // candidate entries per chunk (one per lane)
-constexpr int kNbWaves = 4;                         // chunks per block
-constexpr int kNbLds = kNbChunk + kNbLanes;         // chunk bytes + the overhang a length word may need
-constexpr int kNbMaxElems = kNbChunk / 6 + 2;       // shortest element: 4 + RecordAttributes(2)
+constexpr int kNbLanes = GW_MAX_ELEMENT;                 // candidate entries per chunk (one per lane)
+constexpr int kNbWaves = 4;                              // chunks per block
+constexpr int kNbWords = (kNbChunk + kNbLanes + 8) / 4;  // chunk + overhang + one spare dword, as dwords
+constexpr int kNbMaxElems = kNbChunk / 6 + 2;            // shortest element: 4 + RecordAttributes(2)
+constexpr int kNbScanBlock = 256;                        // chunks per k_nb_resolve block
 
-// lane state packed into the top byte of an exit word
+// walk state of a candidate lane, packed into the top bits of its exit word
 constexpr int kStNormal = 0, kStTail = 1, kStDead = 2, kStLong = 3;
 __device__ __forceinline__ int64_t nb_pack(int64_t pos, int st) { return pos | ((int64_t)st << 56); }
-__host__ __device__ __forceinline__ int64_t nb_pos(int64_t w) { return w & (((int64_t)1 << 56) - 1); }
-__host__ __device__ __forceinline__ int nb_state(int64_t w) { return (int)(w >> 56); }
+__device__ __forceinline__ int64_t nb_pos(int64_t w) { return w & (((int64_t)1 << 56) - 1); }
+__device__ __forceinline__ int nb_state(int64_t w) { return (int)(w >> 56); }
 constexpr int64_t kNonConv = -1;
 
-// Stage bytes [base, base + kNbLds) ∩ [0, nbytes) of the buffer into LDS (one wave).
-__device__ __forceinline__ void nb_stage(uint8_t* lds, const uint8_t* buf, int64_t base, int64_t nbytes) {
+// A wave's chunk in flight: bytes [base, base + 4*kNbWords) ∩ [0, nbytes) as dwords in
+// registers (kNbRegs per lane; bytes past the end read as 0), loaded one chunk ahead of
+// the walk so the HBM latency hides behind the LDS chain walk of the current chunk.
+constexpr int kNbRegs = (kNbWords + 63) / 64;
+__device__ __forceinline__ void nb_fetch(uint32_t (&r)[kNbRegs], const uint8_t* buf, int64_t base, int64_t nbytes) {
     const int lane = __lane_id();
-    const int64_t avail = nbytes - base < kNbLds ? nbytes - base : kNbLds;
-    const int words = (int)(avail >> 2);
+    const int64_t left = nbytes - base;
+    const int avail = left < 4 * kNbWords ? (int)left : 4 * kNbWords;
+    const int full = avail >> 2;
     const uint32_t* src = (const uint32_t*)(buf + base);  // base is a multiple of kNbChunk; buf 4-aligned
-    uint32_t* dst = (uint32_t*)lds;
-    for (int i = lane; i < words; i += 64) dst[i] = __builtin_nontemporal_load(src + i);
-    for (int i = words * 4 + lane; i < avail; i += 64) lds[i] = buf[base + i];
+#pragma unroll
+    for (int k = 0; k < kNbRegs; ++k) {
+        const int i = lane + 64 * k;
+        uint32_t v = 0;
+        if (i < full) {
+            v = __builtin_nontemporal_load(src + i);
+        } else if (i == full) {
+            for (int b = 0; b < (avail & 3); ++b) v |= (uint32_t)buf[base + 4 * i + b] << (8 * b);
+        }
+        r[k] = v;
+    }
+}
+__device__ __forceinline__ void nb_put(uint32_t* lds, const uint32_t (&r)[kNbRegs]) {
+    const int lane = __lane_id();
+#pragma unroll
+    for (int k = 0; k < kNbRegs; ++k) {
+        const int i = lane + 64 * k;
+        if (i < kNbWords) lds[i] = r[k];
+    }
 }
 
-__device__ __forceinline__ uint32_t lds_be32(const uint8_t* l, int p) {
-    return ((uint32_t)l[p] << 24) | ((uint32_t)l[p + 1] << 16) | ((uint32_t)l[p + 2] << 8) | (uint32_t)l[p + 3];
+// Little-endian dwords in LDS -> big-endian fields at any byte offset p.
+__device__ __forceinline__ uint32_t lds_le32(const uint32_t* w, int p) {
+    const int q = p >> 2;
+    return __builtin_amdgcn_alignbyte(w[q + 1], w[q], (uint32_t)(p & 3));
 }
-__device__ __forceinline__ uint64_t lds_be(const uint8_t* l, int p, int w) {
-    uint64_t v = 0;
-    for (int i = 0; i < w; ++i) v = (v << 8) | l[p + i];
-    return v;
+__device__ __forceinline__ uint32_t lds_be32(const uint32_t* w, int p) { return __builtin_bswap32(lds_le32(w, p)); }
+__device__ __forceinline__ uint32_t lds_byte(const uint32_t* w, int p) { return (w[p >> 2] >> (8 * (p & 3))) & 0xffu; }
+__device__ __forceinline__ uint64_t lds_be64(const uint32_t* w, int p) {
+    const int q = p >> 2;
+    const uint32_t r = (uint32_t)(p & 3);
+    const uint32_t w0 = w[q], w1 = w[q + 1], w2 = w[q + 2];
+    const uint64_t le = ((uint64_t)__builtin_amdgcn_alignbyte(w2, w1, r) << 32) | __builtin_amdgcn_alignbyte(w1, w0, r);
+    return __builtin_bswap64(le);
 }
 
-__global__ void __launch_bounds__(256) k_nb_walk(const uint8_t* buf, int64_t nbytes, int64_t nch, int64_t* exits,
-                                                 int32_t* cnt, int64_t* conv) {
-    __shared__ uint8_t lds[kNbWaves][kNbLds];
+// Pass 1: every candidate entry of every chunk, walked at once (lane = candidate offset).
+// Per lane: exit (relative position | state << 28) and (records | watermarks << 16).
+__global__ void __launch_bounds__(256) k_nb_walk(const uint8_t* buf, int64_t nbytes, int64_t nch, int32_t vbytes,
+                                                 uint32_t* exits, uint32_t* cnt, int64_t* conv) {
+    const int rec_ts = 9 + vbytes, rec_nots = 1 + vbytes;
+    __shared__ uint32_t lds[kNbWaves][kNbWords];
     const int w = threadIdx.x >> 6, lane = __lane_id();
-    const int64_t c = (int64_t)blockIdx.x * kNbWaves + w;
-    if (c >= nch) return;  // whole wave
+    const int64_t stride = (int64_t)gridDim.x * kNbWaves;
+    uint32_t pre[kNbRegs];
+    int64_t c = (int64_t)blockIdx.x * kNbWaves + w;
+    if (c < nch) nb_fetch(pre, buf, c * kNbChunk, nbytes);
+    for (; c < nch; c += stride) {
     const int64_t base = c * kNbChunk;
-    nb_stage(lds[w], buf, base, nbytes);
+    __builtin_amdgcn_wave_barrier();  // the previous chunk's LDS reads are done
+    nb_put(lds[w], pre);
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    const int64_t cend = base + kNbChunk < nbytes ? base + kNbChunk : nbytes;
-    int64_t pos = base + lane;
-    int nr = 0, nw = 0, st = kStNormal;
-    while (pos < cend) {
-        if (pos + 4 > nbytes) { st = kStTail; break; }
-        const int32_t len = (int32_t)lds_be32(lds[w], (int)(pos - base));
-        if (len < 1) { st = kStDead; break; }
-        if (len > kNbLanes - 4) { st = kStLong; break; }
-        if (pos + 4 + len > nbytes) { st = kStTail; break; }
-        const int tag = lds[w][pos - base + 4];
-        nr += tag <= 1;
-        nw += tag == 2 || tag == 6;
-        pos += 4 + len;
+    if (c + stride < nch) nb_fetch(pre, buf, (c + stride) * kNbChunk, nbytes);
+    const uint32_t* l = lds[w];
+    const int64_t left = nbytes - base;
+    const int rlim = left < kNbChunk + 4 * kNbLanes ? (int)left : kNbChunk + 4 * kNbLanes;  // binding only near the end
+    const int rend = rlim < kNbChunk ? rlim : kNbChunk;
+    // Branch-free step (one ds_read2 gives the length word and the tag): the loop runs as
+    // long as any candidate lane is alive, every lane steps in lockstep under a full exec
+    // mask, and the per-step VALU count stays small, which is what bounds this kernel.
+    int pos = lane, nr = 0, nw = 0, st = kStNormal;
+    bool run = pos < rend;
+    while (__ballot(run)) {
+        const int p = run ? pos : 0;
+        const uint32_t w0 = l[p >> 2], w1 = l[(p >> 2) + 1];
+        const uint32_t sh = (uint32_t)(p & 3);
+        const int32_t len = (int32_t)__builtin_bswap32(__builtin_amdgcn_alignbyte(w1, w0, sh));
+        const uint32_t tag = (w1 >> (8 * sh)) & 0xffu;
+        // a candidate lives only on elements whose length fits their tag (what k_nb_decode
+        // checks on the true chain): payload bytes that merely read as a plausible length
+        // rarely also carry the matching tag, so wrong chains die within a step or two
+        const int want = tag == 0u ? rec_ts : tag == 1u ? rec_nots : tag == 2u ? 9 : tag == 3u ? 29
+                       : tag == 4u ? 5 : tag == 5u ? 2 : tag == 6u ? 13 : -1;
+        const int ns = p + 4 > rlim ? kStTail
+                     : len < 1 ? kStDead
+                     : len > kNbLanes - 4 ? kStLong
+                     : p + 4 + len > rlim ? kStTail
+                     : len != want ? kStDead : kStNormal;
+        const bool adv = run && ns == kStNormal;
+        st = (run && !adv) ? ns : st;
+        nr += (adv && tag <= 1u) ? 1 : 0;
+        nw += (adv && (tag == 2u || tag == 6u)) ? 1 : 0;
+        pos = adv ? p + 4 + len : pos;
+        run = adv && pos < rend;
     }
-    const int64_t ex = nb_pack(pos, st);
-    exits[c * kNbLanes + lane] = ex;
-    cnt[(c * kNbLanes + lane) * 2] = nr;
-    cnt[(c * kNbLanes + lane) * 2 + 1] = nw;
+    exits[c * kNbLanes + lane] = (uint32_t)pos | ((uint32_t)st << 28);
+    cnt[c * kNbLanes + lane] = (uint32_t)nr | ((uint32_t)nw << 16);
     // unique exit over the live candidates (dead ones never hold the true entry)
+    const int64_t ex = nb_pack(base + pos, st);
     const bool live = st == kStNormal || st == kStTail;
     const unsigned long long lv = __ballot(live);
     int64_t cv = kNonConv;
@@ -96,55 +150,83 @@ __global__ void __launch_bounds__(256) k_nb_walk(const uint8_t* buf, int64_t nby
         cv = nb_pack(base, kStDead);
     }
     if (lane == 0) conv[c] = cv;
+    }
 }
 
-// One thread per chunk: its true entry, from the nearest earlier chunk with a unique exit.
-__global__ void __launch_bounds__(256) k_nb_resolve(int64_t nbytes, int64_t nch, const int64_t* exits,
-                                                    const int32_t* cnt, const int64_t* conv, int64_t* entry,
-                                                    int32_t* counts, NbStatus* st) {
-    const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= nch) return;
-    int64_t j = c - 1;
-    while (j >= 0 && conv[j] == kNonConv) --j;
-    int64_t e = j < 0 ? nb_pack(0, kStNormal) : conv[j];  // entry word of chunk j + 1
-    for (int64_t t = j + 1; t < c && nb_state(e) == kStNormal; ++t) {
-        const int64_t lane = nb_pos(e) - t * kNbChunk;
-        if (lane < 0 || lane >= kNbLanes) { e = nb_pack(nb_pos(e), kStDead); break; }
-        e = exits[t * kNbLanes + lane];
-    }
-    int32_t nr = 0, nw = 0;
-    int64_t ent = -1;
-    if (nb_state(e) == kStNormal) {
-        const int64_t p = nb_pos(e);
-        const int64_t lane = p - c * kNbChunk;
-        if (p >= nbytes) {
-            // the chain ended exactly at the end of the bytes: nothing starts here
-        } else if (lane < 0 || lane >= kNbLanes) {
-            atomicOr(&st->corrupt, 1ull);
-        } else {
-            ent = p;
-            const int64_t ex = exits[c * kNbLanes + lane];
-            nr = cnt[(c * kNbLanes + lane) * 2];
-            nw = cnt[(c * kNbLanes + lane) * 2 + 1];
-            const int s = nb_state(ex);
-            if (s == kStDead) atomicOr(&st->corrupt, 1ull);
-            if (s == kStLong) atomicOr(&st->unsupported, 1ull);
-            if (s == kStTail) st->consumed = nb_pos(ex);  // at most one chunk of the chain stops early
-            if (s == kStNormal && nb_pos(ex) >= nbytes) st->consumed = nbytes;
+__device__ __forceinline__ int64_t nb_exit_word(const uint32_t* exits, int64_t t, int64_t lane) {
+    const uint32_t x = exits[t * kNbLanes + lane];
+    return nb_pack(t * kNbChunk + (x & 0x0fffffffu), (int)(x >> 28));
+}
+
+// Pass 2: one thread per chunk finds its true entry from the nearest earlier chunk with a
+// unique exit, then the block scans the chunk counts (exclusive, block-local).
+__global__ void __launch_bounds__(kNbScanBlock) k_nb_resolve(int64_t nbytes, int64_t nch, const uint32_t* exits,
+                                                             const uint32_t* cnt, const int64_t* conv, int64_t* entry,
+                                                             int32_t* offs, long long* btot, NbStatus* st) {
+    __shared__ int wsum[kNbScanBlock / 64][2];
+    const int64_t c = (int64_t)blockIdx.x * kNbScanBlock + threadIdx.x;
+    int nr = 0, nw = 0;
+    if (c < nch) {
+        int64_t j = c - 1;
+        while (j >= 0 && conv[j] == kNonConv) --j;
+        if (j < c - 1) atomicAdd((unsigned long long*)&st->pad, (unsigned long long)(c - 1 - j));
+        int64_t e = j < 0 ? nb_pack(0, kStNormal) : conv[j];  // entry word of chunk j + 1
+        for (int64_t t = j + 1; t < c && nb_state(e) == kStNormal; ++t) {
+            const int64_t lane = nb_pos(e) - t * kNbChunk;
+            if (lane < 0 || lane >= kNbLanes) { e = nb_pack(nb_pos(e), kStDead); break; }
+            e = nb_exit_word(exits, t, lane);
         }
+        int64_t ent = -1;
+        if (nb_state(e) == kStNormal) {
+            const int64_t p = nb_pos(e);
+            const int64_t lane = p - c * kNbChunk;
+            if (p >= nbytes) {
+                // the chain ended exactly at the end of the bytes: nothing starts here
+            } else if (lane < 0 || lane >= kNbLanes) {
+                atomicOr(&st->corrupt, 1ull);
+            } else {
+                ent = p;
+                const int64_t ex = nb_exit_word(exits, c, lane);
+                const uint32_t cc = cnt[c * kNbLanes + lane];
+                nr = (int)(cc & 0xffffu);
+                nw = (int)(cc >> 16);
+                const int s = nb_state(ex);
+                if (s == kStDead) atomicOr(&st->corrupt, 1ull);
+                if (s == kStLong) atomicOr(&st->unsupported, 1ull);
+                if (s == kStTail) st->consumed = nb_pos(ex);  // at most one chunk of the chain stops early
+                if (s == kStNormal && nb_pos(ex) >= nbytes) st->consumed = nbytes;
+            }
+        }
+        entry[c] = ent;
     }
-    entry[c] = ent;
-    counts[2 * c] = nr;
-    counts[2 * c + 1] = nw;
+    // block-local exclusive scan of (nr, nw): wave prefix, then across the 4 waves
+    const int lane = __lane_id(), wv = threadIdx.x >> 6;
+    int ir = nr, iw = nw;
+    for (int o = 1; o < 64; o <<= 1) {
+        const int ur = __shfl_up(ir, o), uw = __shfl_up(iw, o);
+        if (lane >= o) { ir += ur; iw += uw; }
+    }
+    if (lane == 63) { wsum[wv][0] = ir; wsum[wv][1] = iw; }
+    __syncthreads();
+    int br = 0, bw = 0;
+    for (int k = 0; k < wv; ++k) { br += wsum[k][0]; bw += wsum[k][1]; }
+    if (c < nch) {
+        offs[2 * c] = br + ir - nr;
+        offs[2 * c + 1] = bw + iw - nw;
+    }
+    if (threadIdx.x == kNbScanBlock - 1) {
+        btot[2 * blockIdx.x] = br + ir;
+        btot[2 * blockIdx.x + 1] = bw + iw;
+    }
 }
 
-// Exclusive scan of the per-chunk (records, watermarks) counts; one block.
-__global__ void __launch_bounds__(1024) k_nb_scan(int64_t nch, const int32_t* counts, int64_t* offs, NbStatus* st) {
+// Pass 3: exclusive scan of the per-block totals (in place); one block.
+__global__ void __launch_bounds__(1024) k_nb_scan(int64_t nblk, long long* btot, NbStatus* st) {
     __shared__ long long part[1024][2];
-    const int64_t per = (nch + blockDim.x - 1) / blockDim.x;
-    const int64_t lo = threadIdx.x * per, hi = lo + per < nch ? lo + per : nch;
+    const int64_t per = (nblk + blockDim.x - 1) / blockDim.x;
+    const int64_t lo = threadIdx.x * per, hi = lo + per < nblk ? lo + per : nblk;
     long long r = 0, w = 0;
-    for (int64_t i = lo; i < hi; ++i) { r += counts[2 * i]; w += counts[2 * i + 1]; }
+    for (int64_t i = lo; i < hi; ++i) { r += btot[2 * i]; w += btot[2 * i + 1]; }
     part[threadIdx.x][0] = r;
     part[threadIdx.x][1] = w;
     __syncthreads();
@@ -162,62 +244,76 @@ __global__ void __launch_bounds__(1024) k_nb_scan(int64_t nch, const int32_t* co
     r = part[threadIdx.x][0];
     w = part[threadIdx.x][1];
     for (int64_t i = lo; i < hi; ++i) {
-        offs[2 * i] = r;
-        offs[2 * i + 1] = w;
-        r += counts[2 * i];
-        w += counts[2 * i + 1];
+        const long long x = btot[2 * i], y = btot[2 * i + 1];
+        btot[2 * i] = r;
+        btot[2 * i + 1] = w;
+        r += x;
+        w += y;
     }
 }
 
 // field -> 8-byte column word (integral: sign-extended int64; float: widened double)
-__device__ __forceinline__ int64_t nb_field(const uint8_t* l, int p, int type) {
+__device__ __forceinline__ int64_t nb_field(const uint32_t* l, int p, int type) {
     switch (type) {
-    case 'J': case 'D': return (int64_t)lds_be(l, p, 8);
-    case 'I': return (int64_t)(int32_t)(uint32_t)lds_be(l, p, 4);
-    case 'S': return (int64_t)(int16_t)(uint16_t)lds_be(l, p, 2);
-    case 'B': return (int64_t)(int8_t)l[p];
-    case 'Z': return (int64_t)(l[p] != 0);
-    case 'F': return f64_to_bits((double)__builtin_bit_cast(float, (uint32_t)lds_be(l, p, 4)));
+    case 'J': case 'D': return (int64_t)lds_be64(l, p);
+    case 'I': return (int64_t)(int32_t)lds_be32(l, p);
+    case 'S': return (int64_t)(int16_t)(uint16_t)(lds_be32(l, p) >> 16);
+    case 'B': return (int64_t)(int8_t)(uint8_t)lds_byte(l, p);
+    case 'Z': return (int64_t)(lds_byte(l, p) != 0);
+    case 'F': return f64_to_bits((double)__builtin_bit_cast(float, lds_be32(l, p)));
     default: return 0;
     }
 }
 
+// Pass 4: each chunk's true chain, walked once more out of LDS, decoded by all 64 lanes.
 __global__ void __launch_bounds__(256) k_nb_decode(const uint8_t* buf, int64_t nbytes, int64_t nch, NbLayout L,
-                                                   const int64_t* entry, const int64_t* offs, int64_t* key,
-                                                   int64_t* ts, int64_t* val, int64_t rec_cap, int64_t* wm_pos,
-                                                   int64_t* wm_val, int64_t wm_cap, NbStatus* st) {
-    __shared__ uint8_t lds[kNbWaves][kNbLds];
+                                                   const int64_t* entry, const int32_t* offs, const long long* btot,
+                                                   int64_t* key, int64_t* ts, int64_t* val, int64_t rec_cap,
+                                                   int64_t* wm_pos, int64_t* wm_val, int64_t wm_cap, NbStatus* st) {
+    __shared__ uint32_t lds[kNbWaves][kNbWords];
     __shared__ uint16_t starts[kNbWaves][kNbMaxElems];
     __shared__ int nelem[kNbWaves];
     const int w = threadIdx.x >> 6, lane = __lane_id();
-    const int64_t c = (int64_t)blockIdx.x * kNbWaves + w;
-    if (c >= nch) return;  // whole wave
+    const int64_t stride = (int64_t)gridDim.x * kNbWaves;
+    uint32_t pre[kNbRegs];
+    int64_t c = (int64_t)blockIdx.x * kNbWaves + w;
+    if (c < nch) nb_fetch(pre, buf, c * kNbChunk, nbytes);
+    for (; c < nch; c += stride) {
     const int64_t e0 = entry[c];
-    if (e0 < 0) return;
     const int64_t base = c * kNbChunk;
-    nb_stage(lds[w], buf, base, nbytes);
+    __builtin_amdgcn_wave_barrier();  // the previous chunk's LDS reads are done
+    nb_put(lds[w], pre);
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    const uint8_t* l = lds[w];
-    const int64_t cend = base + kNbChunk < nbytes ? base + kNbChunk : nbytes;
-    if (lane == 0) {  // the true chain (k_nb_walk proved every step of it is in bounds)
+    if (c + stride < nch) nb_fetch(pre, buf, (c + stride) * kNbChunk, nbytes);
+    if (e0 < 0) continue;
+    const uint32_t* l = lds[w];
+    const int64_t left = nbytes - base;
+    const int rlim = left < kNbChunk + 4 * kNbLanes ? (int)left : kNbChunk + 4 * kNbLanes;
+    const int rend = rlim < kNbChunk ? rlim : kNbChunk;
+    {  // the true chain, walked by the whole wave in lockstep (uniform addresses: LDS
+       // broadcasts), lane 0 recording the element starts
         int m = 0;
-        int64_t pos = e0;
-        for (; pos < cend && m < kNbMaxElems;) {
-            if (pos + 4 > nbytes) break;
-            const int32_t len = (int32_t)lds_be32(l, (int)(pos - base));
-            if (len < 1 || len > kNbLanes - 4 || pos + 4 + len > nbytes) break;
-            starts[w][m++] = (uint16_t)(pos - base);
+        int pos = (int)(e0 - base);
+        bool run = pos < rend;
+        while (run && m < kNbMaxElems) {
+            const uint32_t w0 = l[pos >> 2], w1 = l[(pos >> 2) + 1];
+            const int32_t len = (int32_t)__builtin_bswap32(__builtin_amdgcn_alignbyte(w1, w0, (uint32_t)(pos & 3)));
+            if (pos + 4 > rlim || len < 1 || len > kNbLanes - 4 || pos + 4 + len > rlim) break;
+            if (lane == 0) starts[w][m] = (uint16_t)pos;
+            ++m;
             pos += 4 + len;
+            run = pos < rend;
         }
         // more elements than valid ones of >= 6 bytes can make: lengths of 1 -> corrupt
-        if (m == kNbMaxElems && pos < cend) atomicOr(&st->corrupt, 1ull);
-        nelem[w] = m;
+        if (lane == 0 && m == kNbMaxElems && pos < rend) atomicOr(&st->corrupt, 1ull);
+        if (lane == 0) nelem[w] = m;
     }
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     const int m = nelem[w];
-    int64_t rbase = offs[2 * c], wbase = offs[2 * c + 1];
+    const int64_t blk = c / kNbScanBlock;
+    int64_t rbase = btot[2 * blk] + offs[2 * c], wbase = btot[2 * blk + 1] + offs[2 * c + 1];
     unsigned long long bad = 0, full = 0, skipped = 0;
     for (int i0 = 0; i0 < m; i0 += 64) {
         const int i = i0 + lane;
@@ -227,7 +323,7 @@ __global__ void __launch_bounds__(256) k_nb_decode(const uint8_t* buf, int64_t n
         if (i < m) {
             p = starts[w][i];
             len = (int)lds_be32(l, p);
-            tag = l[p + 4];
+            tag = (int)lds_byte(l, p + 4);
             if (tag == 0 || tag == 1) {
                 kind = 1;
                 ok = len == (tag == 0 ? 9 : 1) + L.vbytes;
@@ -250,8 +346,8 @@ __global__ void __launch_bounds__(256) k_nb_decode(const uint8_t* buf, int64_t n
             if (o < rec_cap) {
                 const int hdr = tag == 0 ? 9 : 1;
                 const int v = p + 4 + hdr;
-                ts[o] = tag == 0 ? (int64_t)lds_be(l, p + 5, 8) : INT64_MIN;
-                key[o] = (int64_t)lds_be(l, v + L.key_off, 8);
+                ts[o] = tag == 0 ? (int64_t)lds_be64(l, p + 5) : INT64_MIN;
+                key[o] = (int64_t)lds_be64(l, v + L.key_off);
                 if (val) val[o] = L.val_type ? nb_field(l, v + L.val_off, L.val_type) : 0;
             } else {
                 full = 1;
@@ -259,9 +355,9 @@ __global__ void __launch_bounds__(256) k_nb_decode(const uint8_t* buf, int64_t n
         } else if (kind == 2 && ok) {
             const int64_t o = wbase + __popcll(bw & below);
             if (o < wm_cap) {
-                // records of this chunk before the watermark: those of lower lanes and earlier rounds
+                // records before the watermark: all earlier chunks', earlier rounds', lower lanes'
                 wm_pos[o] = rbase + __popcll(br & below);
-                wm_val[o] = (int64_t)lds_be(l, p + (tag == 2 ? 5 : 9), 8);
+                wm_val[o] = (int64_t)lds_be64(l, p + (tag == 2 ? 5 : 9));
             } else {
                 full = 1;
             }
@@ -277,12 +373,14 @@ __global__ void __launch_bounds__(256) k_nb_decode(const uint8_t* buf, int64_t n
         if (full) atomicOr(&st->full, 1ull);
         if (skipped) atomicAdd(&st->skipped, skipped);
     }
+    }
 }
 
 int64_t nb_scratch_bytes(int64_t nbytes) {
     const int64_t nch = (nbytes + kNbChunk - 1) / kNbChunk;
-    // exits, per-lane counts, conv, entry, per-chunk counts, offsets, status
-    return nch * kNbLanes * 8 + nch * kNbLanes * 8 + nch * 8 + nch * 8 + nch * 8 + nch * 16 + 256;
+    const int64_t nblk = (nch + kNbScanBlock - 1) / kNbScanBlock;
+    // exits + counts per lane, conv + entry + offsets per chunk, block totals
+    return nch * kNbLanes * 8 + nch * 24 + nblk * 16 + 256;
 }
 
 hipError_t launch_nb_decode(const uint8_t* buf, int64_t nbytes, const NbLayout& L, int64_t* key, int64_t* ts,
@@ -291,20 +389,28 @@ hipError_t launch_nb_decode(const uint8_t* buf, int64_t nbytes, const NbLayout& 
     hipError_t e = hipMemsetAsync(d_st, 0, sizeof(NbStatus), s);
     if (e != hipSuccess || nbytes <= 0) return e;
     const int64_t nch = (nbytes + kNbChunk - 1) / kNbChunk;
+    const int64_t nblk = (nch + kNbScanBlock - 1) / kNbScanBlock;
     uint8_t* p = (uint8_t*)scratch;
-    int64_t* exits = (int64_t*)p;              p += nch * kNbLanes * 8;
-    int32_t* cnt = (int32_t*)p;                p += nch * kNbLanes * 8;
+    uint32_t* exits = (uint32_t*)p;            p += nch * kNbLanes * 4;
+    uint32_t* cnt = (uint32_t*)p;              p += nch * kNbLanes * 4;
     int64_t* conv = (int64_t*)p;               p += nch * 8;
     int64_t* entry = (int64_t*)p;              p += nch * 8;
-    int32_t* counts = (int32_t*)p;             p += nch * 8;
-    int64_t* offs = (int64_t*)p;
-    const unsigned gb = (unsigned)((nch + kNbWaves - 1) / kNbWaves);
-    hipLaunchKernelGGL(k_nb_walk, dim3(gb), dim3(256), 0, s, buf, nbytes, nch, exits, cnt, conv);
-    hipLaunchKernelGGL(k_nb_resolve, dim3((unsigned)((nch + 255) / 256)), dim3(256), 0, s, nbytes, nch, exits, cnt,
-                       conv, entry, counts, d_st);
-    hipLaunchKernelGGL(k_nb_scan, dim3(1), dim3(1024), 0, s, nch, counts, offs, d_st);
-    hipLaunchKernelGGL(k_nb_decode, dim3(gb), dim3(256), 0, s, buf, nbytes, nch, L, entry, offs, key, ts, val, rec_cap,
-                       wm_pos, wm_val, wm_cap, d_st);
+    int32_t* offs = (int32_t*)p;               p += nch * 8;
+    long long* btot = (long long*)p;
+    // a bounded grid of waves that loop over the chunks: a chunk is ~1 us of work, too
+    // little to pay for a workgroup dispatch each (GW_NB_GRID overrides, for sweeps)
+    int64_t gb = (nch + kNbWaves - 1) / kNbWaves;
+    static const int64_t cap = [] {
+        const char* e = getenv("GW_NB_GRID");
+        return e ? (int64_t)atoll(e) : (int64_t)4096;
+    }();
+    if (cap > 0 && gb > cap) gb = cap;
+    hipLaunchKernelGGL(k_nb_walk, dim3((unsigned)gb), dim3(256), 0, s, buf, nbytes, nch, L.vbytes, exits, cnt, conv);
+    hipLaunchKernelGGL(k_nb_resolve, dim3((unsigned)nblk), dim3(kNbScanBlock), 0, s, nbytes, nch, exits, cnt, conv,
+                       entry, offs, btot, d_st);
+    hipLaunchKernelGGL(k_nb_scan, dim3(1), dim3(1024), 0, s, nblk, btot, d_st);
+    hipLaunchKernelGGL(k_nb_decode, dim3((unsigned)gb), dim3(256), 0, s, buf, nbytes, nch, L, entry, offs, btot, key, ts, val,
+                       rec_cap, wm_pos, wm_val, wm_cap, d_st);
     return hipGetLastError();
 }
 
