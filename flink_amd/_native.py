@@ -18,7 +18,7 @@ ERRORS = {
 }
 GW_E_OUTPUT_FULL = -5
 
-ASSIGNERS = {"tumbling": 0, "sliding": 1, "session": 2}
+ASSIGNERS = {"tumbling": 0, "sliding": 1, "session": 2, "count_tumbling": 3, "count_sliding": 4}
 TRIGGERS = {"event_time": 0, "purging_event_time": 1}
 AGGS = {
     "count": 0, "sum_i64": 1, "sum_f64": 2, "min_i64": 3, "max_i64": 4,

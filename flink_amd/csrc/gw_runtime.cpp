@@ -1206,6 +1206,18 @@ static int validate(const gw_config* c, std::string& why) {
             why = "EventTimeSessionWindows parameters must satisfy 0 < size";
             return GW_E_INVALID;
         }
+    } else if (c->assigner == GW_COUNT_TUMBLING || c->assigner == GW_COUNT_SLIDING) {
+        const int64_t slide = c->assigner == GW_COUNT_SLIDING ? c->slide : c->size;
+        if (c->size <= 0 || slide <= 0) {
+            why = "count windows need size > 0 and slide > 0";
+            return GW_E_INVALID;
+        }
+        int64_t a = c->size, b = slide;
+        while (b) { const int64_t t = a % b; a = b; b = t; }
+        if (c->size / a > kMaxRing) {
+            why = "count window size / gcd(size, slide) > 64 panes is not supported on the GPU path";
+            return GW_E_UNSUPPORTED;
+        }
     } else {
         why = "unknown window assigner";
         return GW_E_INVALID;
@@ -1273,8 +1285,8 @@ int gw_create(const gw_config* cfg, gw_handle** out) {
     int64_t cap = 1024;
     while ((double)cap * 0.7 < (double)hint) cap *= 2;
 
-    if (cfg->assigner == GW_SESSION) {
-        h->session = true;
+    if (cfg->assigner == GW_SESSION || cfg->assigner == GW_COUNT_TUMBLING || cfg->assigner == GW_COUNT_SLIDING) {
+        h->session = true;  // the per-key slot path (session merging or count windows)
         rc = session_create(h->sess, *cfg, cap, h->stream, h->d_st, why);
         if (rc) return bail(rc, why);
         hipStreamSynchronize(h->stream);

@@ -357,6 +357,102 @@ static unsigned grid_of(int64_t n) {
     return (unsigned)g;
 }
 
+// --------------------------------------------------------------------------- count windows
+// KeyedStream.countWindow(size) / countWindow(size, slide) over GlobalWindows
+// (RS/api/datastream/KeyedStream.java:676-690): CountTrigger fires on the element that
+// brings the key's count to a multiple of the trigger count (CountTrigger.java:47-56);
+// the tumbling form purges (PurgingTrigger.onElement :44-48), the sliding form evicts
+// all but the newest `size` elements before the function (CountEvictor.java:50-85).
+//
+// MI355X design: the elements of a key are cut into count-panes of g = gcd(size, slide)
+// consecutive elements, so every fired window is exactly n = size/g whole panes (the
+// first windows of a key: all its panes so far) and every slide ends a pane.  A slot
+// holds [key][element count][ring of n pane accumulators]; a batch is grouped by slot
+// with the stable radix sort (arrival order kept inside a key) and each key's run is
+// folded in order by one thread, which emits a row at every multiple of the slide.
+struct CountGeom {
+    int64_t size, slide, g;
+};
+
+__global__ void __launch_bounds__(256) k_cnt_slot(TableView t, const int64_t* key, int64_t n, uint64_t* kslot,
+                                                  uint32_t* idx, DevStatus* st) {
+    unsigned long long ins = 0, flags = 0;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        bool inserted;
+        const int64_t j = find_or_insert(t, key[i], inserted);
+        if (j < 0) flags |= GW_DF_TABLE_FULL;
+        ins += inserted;
+        kslot[i] = j < 0 ? (uint64_t)t.cap + 1 : (uint64_t)j;  // cap + 1: parked, never applied
+        idx[i] = (uint32_t)i;
+    }
+    block_commit(st, 0, ins, flags, 0);
+}
+
+template <int AGG>
+__global__ void __launch_bounds__(256) k_cnt_apply(TableView t, CountGeom G, const uint64_t* ks, const uint32_t* perm,
+                                                   int64_t n, const int64_t* val, int64_t* ok, int64_t* os,
+                                                   int64_t* oe, int64_t* orr, DevStatus* st) {
+    constexpr int W = (AGG == GW_AVG_I64 || AGG == GW_AVG_F64) ? 2 : 1;
+    const int R = t.ring;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const uint64_t slot = ks[i];
+        if ((i > 0 && ks[i - 1] == slot) || slot > (uint64_t)t.cap) continue;  // not the head of a key's run
+        int64_t* sp = slot_ptr(t, (int64_t)slot);
+        int64_t* cells = sp + 2;
+        const int64_t key = sp[0];  // the sentinel slot's key word is Long.MIN_VALUE, its key
+        int64_t c = sp[1];
+        for (int64_t r = i; r < n && ks[r] == slot; ++r) {
+            int64_t a0, a1;
+            record_cell(AGG, val ? val[perm[r]] : 0, a0, a1);
+            int64_t* cell = cells + ((c / G.g) % R) * W;
+            if (c % G.g == 0) {  // first element of a pane: the ring cell starts over
+                cell[0] = a0;
+                if (W == 2) cell[1] = a1;
+            } else {
+                int64_t b0 = cell[0], b1 = W == 2 ? cell[1] : 0;
+                fold_cell(AGG, b0, b1, a0, a1);
+                cell[0] = b0;
+                if (W == 2) cell[1] = b1;
+            }
+            ++c;
+            if (c % G.slide == 0) {  // CountTrigger FIRE: the newest min(size, c) elements
+                const int64_t len = c < G.size ? c : G.size;
+                const int64_t p0 = (c - len) / G.g, p1 = c / G.g;
+                const int64_t* f = cells + (p0 % R) * W;
+                int64_t r0 = f[0], r1 = W == 2 ? f[1] : 0;
+                for (int64_t q = p0 + 1; q < p1; ++q) {
+                    const int64_t* e = cells + (q % R) * W;
+                    fold_cell(AGG, r0, r1, e[0], W == 2 ? e[1] : 0);
+                }
+                const unsigned long long o = atomicAdd(&st->rows, 1ull);
+                ok[o] = key;
+                os[o] = c - len;
+                oe[o] = c;
+                orr[o] = cell_result(AGG, r0, r1);
+            }
+        }
+        sp[1] = c;
+    }
+}
+
+__global__ void __launch_bounds__(256) k_cnt_rehash(TableView o, TableView nt, DevStatus* st) {
+    unsigned long long ins = 0, flags = 0;
+    const int words = o.ring * o.words;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i <= o.cap; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t* sp = slot_ptr(o, i);
+        if (sp[1] == 0) continue;  // every key in the table has counted an element
+        const int64_t key = i == o.cap ? kEmptyKey : sp[0];
+        bool inserted;
+        const int64_t j = find_or_insert(nt, key, inserted);
+        if (j < 0) { flags |= GW_DF_TABLE_FULL; continue; }
+        ins += inserted;
+        int64_t* d = slot_ptr(nt, j);
+        d[1] = sp[1];
+        for (int w = 0; w < words; ++w) d[2 + w] = sp[2 + w];
+    }
+    block_commit(st, 0, ins, flags, 0);
+}
+
 // --------------------------------------------------------------------------- host
 struct SessionState {
     gw_config cfg{};
@@ -381,6 +477,8 @@ struct SessionState {
     int64_t wm = INT64_MIN;
     gw_stats stats{};
     bool timing = false;
+    bool count_mode = false;  // GW_COUNT_TUMBLING / GW_COUNT_SLIDING (same slot table and row plumbing)
+    CountGeom cg{};
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pending[2], ev_pool;
     double t_total[2] = {0, 0};
     int64_t t_count[2] = {0, 0};
@@ -465,9 +563,22 @@ int session_create(SessionState*& out, const gw_config& cfg, int64_t cap, hipStr
     SCHECK(hipMalloc((void**)&s->d_mm, 16));
     SCHECK(hipMemset(s->d_st, 0, sizeof(DevStatus)));
     memset(s->h_st, 0, sizeof(DevStatus));
+    int rc;
+    if (cfg.assigner == GW_COUNT_TUMBLING || cfg.assigner == GW_COUNT_SLIDING) {
+        s->count_mode = true;
+        const int64_t size = cfg.size, slide = cfg.assigner == GW_COUNT_SLIDING ? cfg.slide : cfg.size;
+        int64_t a = size, b = slide;
+        while (b) { const int64_t t = a % b; a = b; b = t; }
+        s->cg = CountGeom{size, slide, a};
+        s->tv.words = cell_words(cfg.agg);
+        rc = alloc_sess_table(s, s->tv, cap, (int)(size / a), why);  // ring of size/g panes
+        if (rc) { session_destroy(s); return rc; }
+        out = s;
+        return GW_OK;
+    }
     // K so that the slot fills a 64-byte (sum/count/min/max) or 128-byte (avg) line
     const int K = s->tv.words == 3 ? 2 : 3;
-    int rc = alloc_sess_table(s, s->tv, cap, K, why);
+    rc = alloc_sess_table(s, s->tv, cap, K, why);
     if (rc) { session_destroy(s); return rc; }
     out = s;
     return GW_OK;
@@ -510,7 +621,10 @@ static int rehash_sess(SessionState* s, int64_t new_cap, std::string& err) {
     int rc = alloc_sess_table(s, nt, new_cap, s->tv.ring, err);
     if (rc) return rc;
     SCHECK(launch_status_set(s->d_st, 0, 0, 1, s->stream));  // zero sh[].ins (used slots)
-    hipLaunchKernelGGL(k_sess_rehash, dim3(grid_of(s->tv.cap + 1)), dim3(256), 0, s->stream, s->tv, nt, s->d_st);
+    if (s->count_mode)
+        hipLaunchKernelGGL(k_cnt_rehash, dim3(grid_of(s->tv.cap + 1)), dim3(256), 0, s->stream, s->tv, nt, s->d_st);
+    else
+        hipLaunchKernelGGL(k_sess_rehash, dim3(grid_of(s->tv.cap + 1)), dim3(256), 0, s->stream, s->tv, nt, s->d_st);
     SCHECK(hipGetLastError());
     SCHECK(hipStreamSynchronize(s->stream));
     hipFree(s->tv.base);
@@ -531,8 +645,65 @@ static int widen(SessionState* s, int newK, std::string& err) {
     return GW_OK;
 }
 
+static int ensure_rows(SessionState* s, int64_t need, std::string& err) {
+    if (need <= s->o_cap) return GW_OK;
+    const int64_t before = (int64_t)s->h_st->rows;
+    const int64_t c = std::max<int64_t>(need + need / 4, 1 << 16);
+    int64_t* nb[4];
+    for (int q = 0; q < 4; ++q) SCHECK(hipMalloc((void**)&nb[q], c * 8));
+    int64_t* old[4] = {s->o_key, s->o_start, s->o_end, s->o_res};
+    for (int q = 0; q < 4; ++q) {
+        if (old[q] && before) SCHECK(hipMemcpyAsync(nb[q], old[q], before * 8, hipMemcpyDeviceToDevice, s->stream));
+    }
+    SCHECK(hipStreamSynchronize(s->stream));
+    for (int q = 0; q < 4; ++q) hipFree(old[q]);
+    s->o_key = nb[0]; s->o_start = nb[1]; s->o_end = nb[2]; s->o_res = nb[3];
+    s->o_cap = c;
+    return GW_OK;
+}
+
+// Count windows: slot per record, stable grouping by slot, one in-order fold per key.
+static int count_ingest(SessionState* s, int64_t n, const int64_t* key, const int64_t* val, std::string& err) {
+    int rc;
+    if ((rc = session_refresh(s, err))) return rc;
+    if (n <= 0) return GW_OK;
+    if ((int64_t)n > (int64_t)0xffffffffLL) { err = "batch too large"; return GW_E_INVALID; }
+    if ((double)(s->h_st->used_slots + n) > 0.7 * (double)s->tv.cap) {
+        int64_t want = s->tv.cap;
+        while ((double)(s->h_st->used_slots + n) > 0.7 * (double)want) want *= 2;
+        if ((rc = rehash_sess(s, want, err))) return rc;
+    }
+    if ((rc = ensure_bufs(s, n, err))) return rc;
+    // every element fires at most one window
+    if ((rc = ensure_rows(s, (int64_t)s->h_st->rows + n, err))) return rc;
+    int slot_bits = 1;
+    while (slot_bits < 63 && ((uint64_t)(s->tv.cap + 1) >> slot_bits)) ++slot_bits;
+    auto ev = s->timing ? get_ev(s) : std::pair<hipEvent_t, hipEvent_t>{};
+    if (s->timing) SCHECK(hipEventRecord(ev.first, s->stream));
+    hipLaunchKernelGGL(k_cnt_slot, dim3(grid_of(n)), dim3(256), 0, s->stream, s->tv, key, n, s->k0, s->v0, s->d_st);
+    SCHECK(hipGetLastError());
+    int alt = 0;
+    SCHECK(radix_sort_pairs(s->k0, s->v0, s->k1, s->v1, n, slot_bits, s->scratch, s->stream, &alt));
+    const uint64_t* ks = alt ? s->k1 : s->k0;
+    const uint32_t* perm = alt ? s->v1 : s->v0;
+#define L(A)                                                                                             \
+    hipLaunchKernelGGL(k_cnt_apply<A>, dim3(grid_of(n)), dim3(256), 0, s->stream, s->tv, s->cg, ks, perm, n, \
+                       s->cfg.agg == GW_COUNT ? nullptr : val, s->o_key, s->o_start, s->o_end, s->o_res, s->d_st)
+    GW_AGG_SWITCH(s->cfg.agg, L);
+#undef L
+    SCHECK(hipGetLastError());
+    if (s->timing) {
+        SCHECK(hipEventRecord(ev.second, s->stream));
+        s->ev_pending[0].push_back(ev);
+    }
+    if ((rc = session_refresh(s, err))) return rc;
+    if (s->h_st->flags & GW_DF_TABLE_FULL) { err = "count-window state table overflow"; return GW_E_OOM; }
+    return GW_OK;
+}
+
 int session_ingest(SessionState* s, int64_t n, const int64_t* key, const int64_t* ts, const int64_t* val, int64_t wm,
                    std::string& err) {
+    if (s->count_mode) return count_ingest(s, n, key, val, err);
     int rc;
     if ((rc = session_refresh(s, err))) return rc;
     if (n <= 0) return GW_OK;
@@ -622,6 +793,11 @@ int session_ingest(SessionState* s, int64_t n, const int64_t* key, const int64_t
 }
 
 int session_fire(SessionState* s, int64_t wm, int64_t* fired, std::string& err) {
+    if (s->count_mode) {  // GlobalWindows: event time fires nothing (CountTrigger.onEventTime: CONTINUE)
+        s->wm = wm;
+        *fired = 0;
+        return GW_OK;
+    }
     int rc;
     if ((rc = session_refresh(s, err))) return rc;
     const int64_t before = (int64_t)s->h_st->rows;

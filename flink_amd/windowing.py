@@ -112,6 +112,28 @@ class EventTimeSessionWindows(WindowAssigner):
         return dict(assigner="session", gap=self.gap)
 
 
+class CountWindows(WindowAssigner):
+    """KeyedStream.countWindow(size[, slide]) — GlobalWindows with
+    PurgingTrigger(CountTrigger(size)), or CountEvictor(size) + CountTrigger(slide)
+    (RS/api/datastream/KeyedStream.java:676-690).  Rows are (key, first element ordinal,
+    end ordinal, result) and come out of process_batch itself."""
+    kind = "count"
+
+    def __init__(self, size: int, slide: Optional[int] = None):
+        if size <= 0 or (slide is not None and slide <= 0):
+            raise ValueError("count windows need size > 0 and slide > 0")
+        self.size, self.slide = int(size), (int(slide) if slide is not None else None)
+
+    @staticmethod
+    def of(size: int, slide: Optional[int] = None) -> "CountWindows":
+        return CountWindows(size, slide)
+
+    def config(self):
+        if self.slide is None:
+            return dict(assigner="count_tumbling", size=self.size, slide=self.size)
+        return dict(assigner="count_sliding", size=self.size, slide=self.slide)
+
+
 # ----------------------------------------------------------------------- triggers
 class EventTimeTrigger:
     name = "event_time"
@@ -554,6 +576,12 @@ class KeyedStream:
 
     def window(self, assigner: WindowAssigner) -> WindowedStream:
         return WindowedStream(self, assigner)
+
+    def count_window(self, size: int, slide: Optional[int] = None) -> WindowedStream:
+        """KeyedStream.countWindow (KeyedStream.java:676-690)."""
+        return WindowedStream(self, CountWindows(size, slide))
+
+    countWindow = count_window
 
 
 class DataStream:

@@ -64,7 +64,16 @@ extern "C" {
 typedef enum gw_assigner {
     GW_TUMBLING = 0, /* TumblingEventTimeWindows.of(size, offset)  (stagger ALIGNED)   */
     GW_SLIDING  = 1, /* SlidingEventTimeWindows.of(size, slide, offset)                */
-    GW_SESSION  = 2  /* EventTimeSessionWindows.withGap(gap)                           */
+    GW_SESSION  = 2, /* EventTimeSessionWindows.withGap(gap)                           */
+    /* Count windows over GlobalWindows, per key in arrival order;
+     * timestamps, watermarks and allowed lateness play no part (GlobalWindows is not an
+     * event-time assigner).  A row is (key, first element ordinal, end ordinal, result):
+     * the window holds the key's elements [start, end) in arrival order, counted from 0.
+     * Rows are produced by gw_ingest* itself (CountTrigger fires on the element). */
+    GW_COUNT_TUMBLING = 3, /* KeyedStream.countWindow(size): PurgingTrigger(CountTrigger(size))
+                              (RS/api/datastream/KeyedStream.java:676-678)                  */
+    GW_COUNT_SLIDING  = 4  /* KeyedStream.countWindow(size, slide): CountEvictor(size) +
+                              CountTrigger(slide) (KeyedStream.java:686-690)                */
 } gw_assigner;
 
 typedef enum gw_trigger {

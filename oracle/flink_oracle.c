@@ -134,6 +134,10 @@ int wo_validate(const gw_config* c) {
     } else if (c->assigner == GW_SESSION) {
         /* EventTimeSessionWindows ctor: sessionTimeout <= 0 -> IAE (:52-53) */
         if (c->gap <= 0) return GW_E_INVALID;
+    } else if (c->assigner == GW_COUNT_TUMBLING) {
+        if (c->size <= 0) return GW_E_INVALID;
+    } else if (c->assigner == GW_COUNT_SLIDING) {
+        if (c->size <= 0 || c->slide <= 0) return GW_E_INVALID;
     } else {
         return GW_E_INVALID;
     }
@@ -388,8 +392,21 @@ struct wo_op {
     int64_t nsets, cap_sets;
     int64_t *ok, *os, *oe, *orr;
     int64_t on, ocap, ohead;
+    map_t cmap;   /* count windows: (key,0,0,0) -> index into cws */
+    struct cw_s* cws;
+    int64_t ncws, cap_cws;
     char err[256];
 };
+
+/* Count-window state of one key: the GlobalWindow's contents (the element list the
+ * evicting operator keeps, EvictingWindowOperator's ListState) and the CountTrigger's
+ * ReducingState<Long> count (CountTrigger.java:39-40). */
+typedef struct cw_s {
+    int64_t trig;   /* CountTrigger count since its last FIRE                  */
+    int64_t total;  /* elements of this key so far (the row's end ordinal)     */
+    int64_t n, cap; /* window contents                                         */
+    int64_t* v;
+} cw_t;
 
 static void op_err(wo_op* op, const char* fmt, ...) {
     va_list ap;
@@ -742,7 +759,67 @@ static int mws_add_window(wo_op* op, int64_t key, mws_t* m, int64_t ns, int64_t 
 /* ------------------------------------------------------------------------ */
 /* WindowOperator.processElement (WindowOperator.java:293-447)                */
 /* ------------------------------------------------------------------------ */
+/* Count windows, element by element (GlobalWindows.assignWindows -> the single
+ * GlobalWindow, RS/api/windowing/assigners/GlobalWindows.java:50-53):
+ *  - countWindow(size) = PurgingTrigger(CountTrigger(size)) (KeyedStream.java:676-678):
+ *    the element joins the window state; CountTrigger.onElement (CountTrigger.java:47-56)
+ *    counts it and FIREs at count >= size, clearing its count; PurgingTrigger turns FIRE
+ *    into FIRE_AND_PURGE, so the window state is emitted and cleared
+ *    (WindowOperator.processElement :408-446, PurgingTrigger.onElement :44-48);
+ *  - countWindow(size, slide) = CountEvictor(size) + CountTrigger(slide)
+ *    (KeyedStream.java:686-690): on FIRE the evicting operator runs
+ *    CountEvictor.evictBefore, which drops the oldest elements beyond `size`
+ *    (CountEvictor.java:50-85), and emits the function over the rest
+ *    (EvictingWindowOperator.emitWindowContents :373-410); nothing is purged.
+ * The function folds the contents in arrival order (ReduceApplyWindowFunction /
+ * AggregateApplyWindowFunction), as acc_first/acc_add do.  GlobalWindows is not an
+ * event-time assigner, so nothing is ever late and MAX_WATERMARK fires nothing. */
+static int count_process_element(wo_op* op, int64_t key, int64_t v) {
+    int64_t k[4] = {key, 0, 0, 0};
+    int created = 0;
+    ment_t* m = map_upsert(&op->cmap, k, op->ncws, &created);
+    if (!m) { op_err(op, "out of memory"); return GW_E_OOM; }
+    if (created) {
+        if (op->ncws == op->cap_cws) {
+            int64_t nc = op->cap_cws ? op->cap_cws * 2 : 1024;
+            cw_t* nw = (cw_t*)realloc(op->cws, sizeof(cw_t) * (size_t)nc);
+            if (!nw) { op_err(op, "out of memory"); return GW_E_OOM; }
+            op->cws = nw;
+            op->cap_cws = nc;
+        }
+        memset(&op->cws[op->ncws], 0, sizeof(cw_t));
+        op->ncws++;
+    }
+    cw_t* w = &op->cws[m->v];
+    if (w->n == w->cap) {
+        int64_t nc = w->cap ? w->cap * 2 : 16;
+        int64_t* nv = (int64_t*)realloc(w->v, 8 * (size_t)nc);
+        if (!nv) { op_err(op, "out of memory"); return GW_E_OOM; }
+        w->v = nv;
+        w->cap = nc;
+    }
+    w->v[w->n++] = v;
+    w->total++;
+    const int sliding = op->c.assigner == GW_COUNT_SLIDING;
+    const int64_t max_count = sliding ? op->c.slide : op->c.size;
+    if (++w->trig < max_count) return GW_OK;
+    w->trig = 0; /* CountTrigger: count.clear() before FIRE */
+    if (sliding && w->n > op->c.size) {
+        int64_t drop = w->n - op->c.size;
+        memmove(w->v, w->v + drop, 8 * (size_t)(w->n - drop));
+        w->n -= drop;
+    }
+    acc_t a;
+    acc_first(&a, op->c.agg, w->v[0]);
+    for (int64_t i = 1; i < w->n; i++) acc_add(&a, op->c.agg, w->v[i]);
+    int rc = emit(op, key, w->total - w->n, w->total, &a);
+    if (!sliding) w->n = 0; /* FIRE_AND_PURGE */
+    return rc;
+}
+
 int wo_process_element(wo_op* op, int64_t key, int64_t ts, int64_t v) {
+    if (op->c.assigner == GW_COUNT_TUMBLING || op->c.assigner == GW_COUNT_SLIDING)
+        return count_process_element(op, key, v);
     int64_t ws[64], we[64];
     int64_t* pws = ws;
     int64_t* pwe = we;
@@ -873,7 +950,8 @@ wo_op* wo_create(const gw_config* cfg) {
     if (!op) return NULL;
     op->c = *cfg;
     op->wm = INT64_MIN;
-    if (map_init(&op->state, 1024) || map_init(&op->timers, 1024) || map_init(&op->sets, 256)) {
+    if (map_init(&op->state, 1024) || map_init(&op->timers, 1024) || map_init(&op->sets, 256) ||
+        map_init(&op->cmap, 1024)) {
         wo_destroy(op);
         return NULL;
     }
@@ -885,6 +963,9 @@ void wo_destroy(wo_op* op) {
     map_free(&op->state);
     map_free(&op->timers);
     map_free(&op->sets);
+    map_free(&op->cmap);
+    for (int64_t i = 0; i < op->ncws; i++) free(op->cws[i].v);
+    free(op->cws);
     for (int64_t i = 0; i < op->nsets; i++) free(op->msets[i].w);
     free(op->msets);
     free(op->accs);

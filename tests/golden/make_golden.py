@@ -206,4 +206,24 @@ ops_tests.append({
 })
 dump("operator_harness.json", {"tests": ops_tests})
 
+# Count windows: EvictingWindowOperatorTest.testCountTrigger (flink-streaming-java/src/test/
+# java/org/apache/flink/streaming/runtime/operators/windowing/EvictingWindowOperatorTest.java
+# :730-841): GlobalWindows + CountTrigger.of(2) + CountEvictor.of(4) = countWindow(4, 2),
+# SumReducer over Tuple2<String, Integer>.f1; every output carries Long.MAX_VALUE.  The
+# expected rows are checked as a multiset after each group of elements, as the test does
+# (assertOutputEqualsSorted).
+EWOT = ("flink-streaming-java/src/test/java/org/apache/flink/streaming/runtime/operators/windowing/"
+        "EvictingWindowOperatorTest.java")
+dump("count_windows.json", {"tests": [{
+    "name": "count_trigger_count_evictor", "source": EWOT + ":730-841",
+    "config": {"assigner": "count_sliding", "size": 4, "slide": 2, "agg": "sum_i32"},
+    "groups": [
+        {"elements": [["key2", 1], ["key2", 1], ["key1", 1], ["key1", 1], ["key1", 1],
+                      ["key2", 1], ["key2", 1], ["key2", 1]],
+         "expected": [["key2", 2], ["key2", 4], ["key1", 2]]},
+        {"elements": [["key1", 1], ["key2", 1]],
+         "expected": [["key1", 4], ["key2", 4]]},
+    ],
+}]})
+
 print("golden vectors written to", HERE)

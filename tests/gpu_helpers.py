@@ -16,6 +16,10 @@ def make_assigner(kw):
         return W.TumblingEventTimeWindows.of(kw["size"], kw.get("offset", 0))
     if kw["assigner"] == "sliding":
         return W.SlidingEventTimeWindows.of(kw["size"], kw["slide"], kw.get("offset", 0))
+    if kw["assigner"] == "count_tumbling":
+        return W.CountWindows.of(kw["size"])
+    if kw["assigner"] == "count_sliding":
+        return W.CountWindows.of(kw["size"], kw["slide"])
     return W.EventTimeSessionWindows.with_gap(kw["gap"])
 
 

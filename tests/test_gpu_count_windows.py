@@ -1,0 +1,97 @@
+"""Count windows on the GPU: countWindow(size) and
+countWindow(size, slide) through libgpuwin.so against the oracle (bit-exact for integer
+aggregates, 1e-6 relative for f64) and against the reference's golden vector
+(EvictingWindowOperatorTest.testCountTrigger)."""
+import numpy as np
+import pytest
+
+from flink_amd import _native as N
+from flink_amd import windowing as W
+from tests.gpu_helpers import compare, gpu_operator, random_stream
+from tests.test_count_windows_oracle import KEYS, golden
+
+pytestmark = pytest.mark.gpu
+
+
+def rows(op):
+    k, s, e, r = op.drain()
+    return k, s, e, r.view(np.int64)
+
+
+@pytest.mark.parametrize("case", golden(), ids=lambda c: c["name"])
+def test_gpu_count_windows_golden(case):
+    op = gpu_operator(case["config"])
+    got, expected = [], []
+    try:
+        for g in case["groups"]:
+            keys = np.array([KEYS[k] for k, _ in g["elements"]], dtype=np.int64)
+            vals = np.array([v for _, v in g["elements"]], dtype=np.int64)
+            op.process_batch(keys, np.zeros_like(keys), vals)
+            k, s, e, r = rows(op)
+            got += list(zip(k.tolist(), r.tolist()))
+            expected += [(KEYS[k], v) for k, v in g["expected"]]
+            assert sorted(got) == sorted(expected)
+        assert op.advance_watermark(W.LONG_MAX) == 0  # GlobalWindows: nothing fires on event time
+    finally:
+        op.close()
+
+
+def run_both(oracle_lib, kw, keys, vals, cuts, **opkw):
+    op = gpu_operator(kw, **opkw)
+    ora = oracle_lib.OracleOperator(oracle_lib.make_config(**kw))
+    vb = vals.view(np.int64) if vals.dtype == np.float64 else vals
+    g_out, o_out = [], []
+    try:
+        for lo, hi in zip(cuts[:-1], cuts[1:]):
+            op.process_batch(keys[lo:hi], np.zeros(hi - lo, dtype=np.int64), vals[lo:hi])
+            op.advance_watermark(int(hi))  # watermarks are no-ops for count windows
+            g_out.append(rows(op))
+            ora.process_batch(keys[lo:hi], np.zeros(hi - lo, dtype=np.int64), vb[lo:hi])
+            o_out.append(ora.drain())
+        stats = op.stats()
+    finally:
+        op.close()
+    return g_out, o_out, stats
+
+
+CONFIGS = [("count_tumbling", 5, 5), ("count_sliding", 4, 2), ("count_sliding", 250, 150),
+           ("count_sliding", 3, 5), ("count_tumbling", 1, 1), ("count_sliding", 64, 1)]
+AGGS = ["count", "sum_i64", "min_i64", "max_f64", "avg_f64", "sum_i32", "avg_i64", "sum_f64"]
+
+
+@pytest.mark.parametrize("assigner,size,slide", CONFIGS)
+@pytest.mark.parametrize("agg", AGGS)
+def test_gpu_count_windows_match_oracle(oracle_lib, assigner, size, slide, agg):
+    kw = dict(assigner=assigner, size=size, slide=slide, agg=agg)
+    n = 60000
+    keys, _, vals, _ = random_stream(size * 7 + slide, n, 300, 1, agg=agg)
+    rng = np.random.default_rng(slide)
+    keys[rng.random(n) < 0.2] = 7  # a hot key: one long in-order run per batch
+    cuts = [0, 1, 17, 5000, 5001, 31000, n]
+    g, o, stats = run_both(oracle_lib, kw, keys, vals, cuts, capacity_hint=16)  # grows the table
+    assert compare(g, o, agg in N.DOUBLE_RESULT) == []
+    assert stats["rehashes"] > 0
+
+
+def test_gpu_count_windows_special_keys(oracle_lib):
+    kw = dict(assigner="count_sliding", size=3, slide=2, agg="sum_i64")
+    keys = np.array([W.LONG_MIN, W.LONG_MAX, 0, -1] * 50, dtype=np.int64)
+    vals = np.arange(200, dtype=np.int64) * 1_000_000_007
+    g, o, _ = run_both(oracle_lib, kw, keys, vals, [0, 3, 100, 200])
+    assert compare(g, o, False) == []
+
+
+def test_gpu_window_word_count_shape(oracle_lib):
+    """WindowWordCount (flink-examples-streaming .../windowing/WindowWordCount.java:121-149):
+    tokens keyed by word (String.hashCode as the key), countWindow(250, 150).sum(1), on a
+    synthetic Zipf-distributed text (the example's text is not copied here)."""
+    rng = np.random.default_rng(3)
+    vocab = [f"w{i}" for i in range(2000)]
+    ranks = np.minimum(rng.zipf(1.3, 300_000), len(vocab)) - 1
+    words = [vocab[i] for i in ranks]
+    keys = np.array([W.java_string_hash(w) for w in words], dtype=np.int64)
+    vals = np.ones(len(keys), dtype=np.int64)
+    kw = dict(assigner="count_sliding", size=250, slide=150, agg="sum_i32")
+    g, o, _ = run_both(oracle_lib, kw, keys, vals, [0, 100_000, 200_000, 300_000])
+    assert compare(g, o, False) == []
+    assert sum(len(x[0]) for x in g) > 100
