@@ -69,6 +69,9 @@ def parse():
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--preagg", choices=["auto", "force", "off"], default="auto")
+    ap.add_argument("--producer-stream", choices=["auto", "torch", "handle"], default="auto",
+                    help="stream gw_ingest_device orders after: the exchange output's (torch) stream, or, "
+                         "for columns generated and synchronised before the clock starts, none (handle)")
     ap.add_argument("--no-kernel-timing", action="store_true",
                     help="no HIP events around the kernels (the roofline fields are then null)")
     ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
@@ -152,6 +155,12 @@ def main():
         ex = KeyByExchange(world, rank, max_parallelism=maxp, device=dev)
 
     exch_bytes = 0
+    # Exchanged columns are produced on torch's stream inside each step, so the ingest orders
+    # itself after it (and torch's stream after the read).  Columns generated in HBM before
+    # the clock starts (synchronised above) need no ordering: pass the handle's own stream.
+    exchanged = ex is not None and args.exchange == "a2a"
+    use_torch = args.producer_stream == "torch" or (args.producer_stream == "auto" and exchanged)
+    prod = cur if use_torch else op.stream()
 
     def step(b, timed):
         nonlocal exch_bytes
@@ -164,7 +173,7 @@ def main():
                 exch_bytes += (nb - ex.last_send_counts[rank]) * b_in
         n = k.numel()
         N.check(N.lib().gw_ingest_device(op.handle, n, k.data_ptr(), None, t.data_ptr(),
-                                         v.data_ptr() if v is not None else None, cur), op.handle)
+                                         v.data_ptr() if v is not None else None, prod), op.handle)
         wm = wms[b]
         if ex is not None:
             wm = ex.combine_watermark(wm)  # StatusWatermarkValve: min over inputs
