@@ -46,6 +46,29 @@ JNIEXPORT void JNICALL CLS(nativeIngest)(JNIEnv* env, jclass c, jlong h, jint n,
     fail(env, (gw_handle*)(intptr_t)h, gw_ingest((gw_handle*)(intptr_t)h, n, k, kh, t, v));
 }
 
+/* Network-buffer ingest: `bytes` is a direct ByteBuffer holding one input channel's
+ * serialized elements (the payload of its network buffers, in order); `types` the Tuple's
+ * field type codes ("JJ" for Tuple2<Long, Long>).  Returns the bytes consumed; the caller
+ * keeps the rest (an element spanning into the next buffer).  Rows fired by the channel's
+ * watermarks are drained as usual. */
+JNIEXPORT jlong JNICALL CLS(nativeIngestSerialized)(JNIEnv* env, jclass c, jlong h, jobject bytes, jlong n,
+                                                    jstring types, jint keyField, jint valueField) {
+    gw_record_layout lay;
+    memset(&lay, 0, sizeof(lay));
+    const char* t = (*env)->GetStringUTFChars(env, types, 0);
+    lay.nfields = (int32_t)strlen(t);
+    if (lay.nfields > GW_MAX_FIELDS) lay.nfields = GW_MAX_FIELDS + 1; /* rejected by gw_ingest_serialized */
+    memcpy(lay.types, t, lay.nfields <= GW_MAX_FIELDS ? (size_t)lay.nfields : 0);
+    (*env)->ReleaseStringUTFChars(env, types, t);
+    lay.key_field = keyField;
+    lay.value_field = valueField;
+    int64_t consumed = 0, rows = 0;
+    fail(env, (gw_handle*)(intptr_t)h,
+         gw_ingest_serialized((gw_handle*)(intptr_t)h, (*env)->GetDirectBufferAddress(env, bytes), n, &lay,
+                              &consumed, &rows));
+    return consumed;
+}
+
 JNIEXPORT jlong JNICALL CLS(nativeAdvanceWatermark)(JNIEnv* env, jclass c, jlong h, jlong wm) {
     int64_t rows = 0;
     fail(env, (gw_handle*)(intptr_t)h, gw_advance_watermark((gw_handle*)(intptr_t)h, wm, &rows));
