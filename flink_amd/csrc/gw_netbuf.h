@@ -24,7 +24,7 @@ struct NbStatus {
     unsigned long long skipped;      // latency markers, stream status, record attributes
     long long consumed;              // bytes up to the end of the last complete element
     long long records, watermarks;
-    long long pad;
+    unsigned long long walkback;     // chunk steps k_nb_resolve walked back over non-converged chunks
 };
 
 inline int nb_field_width(char t) {

@@ -169,7 +169,7 @@ __global__ void __launch_bounds__(kNbScanBlock) k_nb_resolve(int64_t nbytes, int
     if (c < nch) {
         int64_t j = c - 1;
         while (j >= 0 && conv[j] == kNonConv) --j;
-        if (j < c - 1) atomicAdd((unsigned long long*)&st->pad, (unsigned long long)(c - 1 - j));
+        if (j < c - 1) atomicAdd(&st->walkback, (unsigned long long)(c - 1 - j));
         int64_t e = j < 0 ? nb_pack(0, kStNormal) : conv[j];  // entry word of chunk j + 1
         for (int64_t t = j + 1; t < c && nb_state(e) == kStNormal; ++t) {
             const int64_t lane = nb_pos(e) - t * kNbChunk;

@@ -1516,28 +1516,6 @@ int gw_decode_serialized(const void* d_bytes, int64_t nbytes, const gw_record_la
     if (scratch) hipFree(scratch);
     if (d_st) hipFree(d_st);
     if (e != hipSuccess) { g_create_error = std::string("decode: ") + hipGetErrorString(e); return GW_E_DEVICE; }
-    if (getenv("GW_NB_DEBUG") && nbytes > 0) {
-        fprintf(stderr, "[gw] decode: %lld chunk walk-back steps, %lld records\n", (long long)hst.pad,
-                (long long)hst.records);
-        const int64_t nch = (nbytes + kNbChunk - 1) / kNbChunk;
-        std::vector<int64_t> conv(nch);
-        void* s2 = nullptr;
-        hipMalloc(&s2, (size_t)nb_scratch_bytes(nbytes));
-        NbStatus* d2 = nullptr;
-        hipMalloc((void**)&d2, sizeof(NbStatus));
-        launch_nb_decode((const uint8_t*)d_bytes, nbytes, L, d_key, d_ts, d_value, rec_cap, d_wm_pos, d_wm_val, wm_cap,
-                         s2, d2, s);
-        hipMemcpy(conv.data(), (char*)s2 + nch * GW_MAX_ELEMENT * 8, nch * 8, hipMemcpyDeviceToHost);
-        int64_t bad = 0;
-        for (int64_t c = 0; c < nch; ++c)
-            if (conv[c] == -1) {
-                if (bad < 8) fprintf(stderr, "[gw]   non-converged chunk %lld\n", (long long)c);
-                ++bad;
-            }
-        fprintf(stderr, "[gw]   %lld of %lld chunks non-converged\n", (long long)bad, (long long)nch);
-        hipFree(s2);
-        hipFree(d2);
-    }
     out->records = hst.records;
     out->watermarks = hst.watermarks;
     out->consumed = hst.consumed;
