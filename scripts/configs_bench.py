@@ -1,0 +1,162 @@
+"""Throughput of the BASELINE.json configs other than the headline (bench.py measures
+Nexmark Q5), one GPU, synthetic data generated in HBM, with the oracle ("port") timed on
+the host cores over a bounded prefix of the same stream.  One JSON line per config.
+
+    python scripts/configs_bench.py [--only ysb,q7,sessions,wordcount] [--steps 10]
+
+  wordcount  WindowWordCount (flink-examples-streaming .../windowing/WindowWordCount.java:
+             121-149): tokens keyed by word (String.hashCode of Zipf(1.1) words over a 50k
+             vocabulary), countWindow(250, 150).sum(1)
+  ysb        Yahoo Streaming Benchmark shape: 100 campaigns, 10 s tumbling count,
+             ts 1 ms per 100k events, disorder <= 50 ms, watermark every 200 ms
+  q7         Nexmark Q7/Q8 shape at one GPU: 10M keys, 10 s tumbling max(price)
+  sessions   event-time sessions, gap 10 s, avg(f64) over 12.5M keys (one GPU's share of
+             100M keys on 8 GPUs); keys come in four groups, each active 5 s out of 20 s, so
+             sessions close and fire
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from bench import MASK63, splitmix64  # noqa: E402
+from flink_amd import _native as N  # noqa: E402
+from flink_amd import windowing as W  # noqa: E402
+
+
+def gen(name, nb, steps, dev):
+    """Returns (assigner kwargs, agg, keys, ts, vals, watermarks)."""
+    n = nb * steps
+    idx = torch.arange(n, device=dev, dtype=torch.int64)
+    r = splitmix64(idx, 0x5EED0000 + {"wordcount": 1, "ysb": 2, "q7": 7, "sessions": 5}[name]) & MASK63
+    if name == "wordcount":
+        rng = np.random.default_rng(7)
+        vocab = 50_000
+        hashes = np.array([W.java_string_hash(f"word{i}") for i in range(vocab)], dtype=np.int64)
+        p = 1.0 / np.arange(1, vocab + 1) ** 1.1
+        cdf = torch.from_numpy(np.cumsum(p / p.sum())).to(dev)
+        u = (r % (1 << 53)).to(torch.float64) / float(1 << 53)
+        ranks = torch.searchsorted(cdf, u).clamp_(max=vocab - 1)
+        keys = torch.from_numpy(hashes).to(dev)[ranks]
+        ts = torch.zeros(n, dtype=torch.int64, device=dev)
+        vals = torch.ones(n, dtype=torch.int64, device=dev)
+        wms = [0] * steps
+        return dict(assigner="count_sliding", size=250, slide=150), "sum_i32", keys, ts, vals, wms
+    if name == "ysb":
+        keys = r % 100
+        base = idx // 100_000
+        ts = base - (splitmix64(idx, 77) & MASK63) % 51
+        wms = [int((b + 1) * nb // 100_000) - 50 - 1 for b in range(steps)]
+        return dict(assigner="tumbling", size=10_000), "count", keys, ts, None, wms
+    if name == "q7":
+        keys = r % 10_000_000
+        base = idx * 200 // nb
+        ts = base - (splitmix64(idx, 78) & MASK63) % 101
+        vals = (splitmix64(idx, 79) & MASK63) % 1_000_000
+        wms = [int((b + 1) * 200) - 100 - 1 for b in range(steps)]
+        return dict(assigner="tumbling", size=10_000), "max_i64", keys, ts, vals, wms
+    if name == "sessions":
+        K = 12_500_000
+        base = idx * 200 // nb
+        group = (base // 5000) % 4
+        keys = group * (K // 4) + r % (K // 4)
+        ts = base - (splitmix64(idx, 80) & MASK63) % 101
+        vals = ((splitmix64(idx, 81) & MASK63) % 1_000_000).to(torch.float64) / 1000.0
+        wms = [int((b + 1) * 200) - 100 - 1 for b in range(steps)]
+        return dict(assigner="session", gap=10_000), "avg_f64", keys, ts, vals.view(torch.int64), wms
+    raise ValueError(name)
+
+
+def run(name, args, dev):
+    nb = {"wordcount": 2_000_000, "ysb": 20_000_000, "q7": 10_000_000, "sessions": 10_000_000}[name]
+    n_timed = args.steps or {"wordcount": 10, "ysb": 60, "q7": 60, "sessions": 100}[name]
+    steps = args.warmup + n_timed
+    kw, agg, keys, ts, vals, wms = gen(name, nb, steps, dev)
+    torch.cuda.synchronize()
+    assigner = {"tumbling": lambda: W.TumblingEventTimeWindows.of(kw["size"]),
+                "session": lambda: W.EventTimeSessionWindows.with_gap(kw["gap"]),
+                "count_sliding": lambda: W.CountWindows.of(kw["size"], kw["slide"])}[kw["assigner"]]()
+    cap = {"wordcount": 1 << 16, "ysb": 1024, "q7": 10_000_000, "sessions": 12_500_000}[name]
+    op = W.GpuWindowOperator(assigner, agg, capacity_hint=cap, max_batch=nb * 2).open()
+    rows = 0
+
+    def step(b):
+        nonlocal rows
+        lo, hi = b * nb, (b + 1) * nb
+        N.check(N.lib().gw_ingest_device(op.handle, nb, keys[lo:hi].data_ptr(), None, ts[lo:hi].data_ptr(),
+                                         vals[lo:hi].data_ptr() if vals is not None else None, op.stream()),
+                op.handle)
+        rows += op.advance_watermark(wms[b])
+        rows += op.pending_rows() if kw["assigner"].startswith("count") else 0
+        op.clear_rows()
+
+    for b in range(args.warmup):
+        step(b)
+    op.flush()
+    torch.cuda.synchronize()
+    rows = 0
+    t0 = time.perf_counter()
+    for b in range(args.warmup, steps):
+        step(b)
+    op.flush()
+    op.synchronize()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    stats = op.stats()
+    op.close()
+    out = {"config": name, "window": kw, "aggregate": agg, "events_per_step": nb, "steps": n_timed,
+           "value": nb * n_timed / dt, "unit": "events/s", "ms_per_step": dt * 1e3 / n_timed,
+           "rows_fired": rows, "live_keys": stats.get("live_keys"), "data": "synthetic, generated in HBM"}
+    if not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(kw, agg, keys, ts, vals, wms, nb, args.cpu_seconds)
+    return out
+
+
+def cpu_baseline(kw, agg, keys, ts, vals, wms, nb, seconds):
+    from oracle import oracle as O
+    O.build()
+    threads = min(16, os.cpu_count() or 1)
+    cfg = O.make_config(agg=agg, max_parallelism=128, **kw)
+
+    def go(n_ev):
+        k = keys[:n_ev].cpu().numpy()
+        t = ts[:n_ev].cpu().numpy()
+        v = vals[:n_ev].cpu().numpy() if vals is not None else None
+        nbat = max(1, n_ev // nb)
+        per = n_ev // nbat
+        blen = np.full(nbat, per, np.int64)
+        wm = np.array(wms[:nbat], np.int64)
+        r, _, sec = O.run_parallel(cfg, threads, blen, wm, k[:per * nbat], t[:per * nbat],
+                                   v[:per * nbat] if v is not None else None)
+        return per * nbat, sec
+
+    n0, s0 = go(min(nb, 200_000))
+    target = int(n0 / max(s0, 1e-6) * seconds)
+    n, sec = go(max(min(target, keys.numel()), 10_000))
+    return {"value": n / sec, "unit": "events/s", "cores": threads, "kind": "port",
+            "sample": f"first {n} events of the GPU stream", "seconds": sec}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--only", default="wordcount,ysb,q7,sessions")
+    ap.add_argument("--steps", type=int, default=0,
+                    help="timed steps (0: per config, long enough that windows / sessions fire: "
+                         "wordcount 10, ysb and q7 60 (12 s of event time), sessions 100 (20 s))")
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--cpu-seconds", type=float, default=3.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    for name in args.only.split(","):
+        print(json.dumps(run(name, args, dev)), flush=True)
+
+
+if __name__ == "__main__":
+    main()
