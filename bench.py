@@ -76,6 +76,13 @@ def parse():
                     help="stream the step's torch work (exchange) runs on")
     ap.add_argument("--no-kernel-timing", action="store_true",
                     help="no HIP events around the kernels (the roofline fields are then null)")
+    ap.add_argument("--overlap", choices=["on", "off"], default="on",
+                    help="on: double-buffered receive columns, so batch b+1's partition and all-to-all "
+                         "run while the operator still aggregates batch b; off: every step ordered "
+                         "after the previous ingest's reads")
+    ap.add_argument("--checksum", action="store_true",
+                    help="drain the fired rows to the host and report an order-independent checksum "
+                         "(key, start, end, result) summed over ranks (a check, not a bench setting)")
     ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
                     help="nccl = RCCL over xGMI; gloo = host-staged rehearsal (several ranks may share one GPU)")
     return ap.parse_args()
@@ -161,12 +168,25 @@ def main():
         ex = KeyByExchange(world, rank, max_parallelism=maxp, device=dev)
 
     exch_bytes = 0
+    rows_sum = 0
     # Exchanged columns are produced on torch's stream inside each step, so the ingest orders
     # itself after it (and torch's stream after the read).  Columns generated in HBM before
     # the clock starts (synchronised above) need no ordering: pass the handle's own stream.
     exchanged = ex is not None and args.exchange == "a2a"
     use_torch = args.producer_stream == "torch" or (args.producer_stream == "auto" and exchanged)
     prod = cur if use_torch else op.stream()
+    # Overlapped exchange: two sets of receive columns used in turn.  The all-to-all of
+    # batch b writes set b%2 once the ingest of batch b-2 has read it (ev_read), and the
+    # ingest orders itself through a hand-off stream that nothing else uses, so the
+    # exchange stream never waits for the ingest of the batch just before it.
+    overlap = exchanged and args.overlap == "on" and args.producer_stream != "handle"
+    if overlap:
+        cap = nb * 2  # received records per step: ~nb for uniform keys (max_batch above)
+        ncols = 3 if vals is not None else 2
+        bufs = [[torch.empty(cap, dtype=torch.int64, device=dev) for _ in range(ncols)] + [None] * (3 - ncols)
+                for _ in range(2)]
+        handoff = torch.cuda.Stream(device=dev)
+        ev_read = [None, None]
 
     def step(b, timed):
         if not exchanged:  # nothing of the step runs on a torch stream
@@ -180,16 +200,27 @@ def main():
         k, t, v = keys[lo:hi], ts[lo:hi], (vals[lo:hi] if vals is not None else None)
         if ex is not None and args.exchange == "a2a":
             pk, pt, pv, counts = ex.partition(k, t, v, stream=cur)
-            (k, t, v), n_recv = ex.exchange_partitioned([pk, pt, pv], counts)
+            if overlap:
+                s = b % 2
+                (k, t, v), n_recv = ex.exchange_partitioned([pk, pt, pv], counts, out=bufs[s], out_ready=ev_read[s])
+                handoff.wait_event(side.record_event())
+            else:
+                (k, t, v), n_recv = ex.exchange_partitioned([pk, pt, pv], counts)
             if timed:
                 exch_bytes += (nb - ex.last_send_counts[rank]) * b_in
         n = k.numel()
         N.check(N.lib().gw_ingest_device(op.handle, n, k.data_ptr(), None, t.data_ptr(),
-                                         v.data_ptr() if v is not None else None, prod), op.handle)
+                                         v.data_ptr() if v is not None else None,
+                                         handoff.cuda_stream if overlap else prod), op.handle)
+        if overlap:
+            ev_read[b % 2] = handoff.record_event()  # the ingest's reads of set b%2 are done
         wm = wms[b]
         if ex is not None:
             wm = ex.combine_watermark(wm)  # StatusWatermarkValve: min over inputs
         op.advance_watermark(wm)
+        if args.checksum:
+            nonlocal rows_sum
+            rows_sum = (rows_sum + rows_checksum(op.drain())) % (1 << 56)
         op.clear_rows()  # DiscardingSink
         return k, t
 
@@ -246,11 +277,14 @@ def main():
     achieved = ingest_bytes_total / (pipe_ms_total / 1e3) / 1e9 if pipe_ms_total > 0 else 0.0
     pipeline_gbs = (ingest_bytes_total + fire_bytes_total) / elapsed / 1e9
 
-    tot = torch.tensor([events_rank, rows_rank], dtype=torch.int64,
+    if args.checksum:
+        rows_sum = (rows_sum + rows_checksum(op.drain())) % (1 << 56)
+    tot = torch.tensor([events_rank, rows_rank, rows_sum], dtype=torch.int64,
                        device=dev if args.dist_backend == "nccl" else "cpu")
     if dist:
         dist.all_reduce(tot)
     events_all, rows_all = int(tot[0].item()), int(tot[1].item())
+    rows_sum = int(tot[2].item()) % (1 << 56)
     value = events_all / elapsed
 
     # ------------------------------------------------------------ CPU baseline
@@ -295,12 +329,25 @@ def main():
             "rows_fired": rows_all,
             "cpu_baseline": cpu,
         }
+        if args.checksum:
+            out["rows_checksum"] = rows_sum
         if world > 1:
             out["exchange_gbs_per_gpu"] = exch_bytes / elapsed / 1e9
         print(json.dumps(out), flush=True)
     op.close()
     if dist:
         dist.destroy_process_group()
+
+
+def rows_checksum(rows) -> int:
+    """Order-independent checksum of fired rows: sum of a 64-bit mix of each (key, start,
+    end, result), mod 2^56 (results compared by their bit pattern)."""
+    k, s, e, r = (np.ascontiguousarray(c).view(np.uint64) for c in rows)
+    with np.errstate(over="ignore"):
+        h = k * np.uint64(0x9E3779B97F4A7C15) ^ s * np.uint64(0xBF58476D1CE4E5B9) \
+            ^ e * np.uint64(0x94D049BB133111EB) ^ r * np.uint64(0xD6E8FEB86659FD93)
+        h ^= h >> np.uint64(31)
+    return int((h & np.uint64((1 << 56) - 1)).astype(object).sum() % (1 << 56)) if h.size else 0
 
 
 def traffic_bytes(agg, nb):

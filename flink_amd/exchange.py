@@ -59,10 +59,17 @@ class KeyByExchange:
         return pk, pt, pv, counts
 
     # ---------------------------------------------------------------- exchange
-    def exchange_partitioned(self, cols: Sequence[Optional[torch.Tensor]], send_counts: torch.Tensor
-                             ) -> Tuple[list, int]:
+    def exchange_partitioned(self, cols: Sequence[Optional[torch.Tensor]], send_counts: torch.Tensor,
+                             out: Optional[Sequence[Optional[torch.Tensor]]] = None,
+                             out_ready: Optional[torch.cuda.Event] = None) -> Tuple[list, int]:
         """All-to-all of already partitioned columns (any backend: RCCL on GPU tensors,
-        gloo on CPU tensors).  send_counts[d] = records for rank d."""
+        gloo on CPU tensors).  send_counts[d] = records for rank d.
+
+        ``out`` (optional): persistent receive columns, one per input column, each with
+        capacity for the received records; the result columns are their leading slices.
+        ``out_ready``: an event the current stream waits for before the column exchange
+        writes into ``out`` (the consumer's read of the previous contents), so a caller can
+        double-buffer the receive side instead of ordering every step after the consumer."""
         staged = dist.get_backend(self.group) == "gloo" and send_counts.is_cuda
         if staged:  # rehearsal on one GPU: gloo moves host tensors only
             dev = send_counts.device
@@ -74,15 +81,27 @@ class KeyByExchange:
         rc = recv_counts.tolist()
         self.last_send_counts = sc
         total = int(sum(rc))
-        out = []
-        for c in cols:
+        if out is not None:
+            for c, o in zip(cols, out):
+                if c is not None and (o is None or o.numel() < total):
+                    raise ValueError(f"receive buffer holds {0 if o is None else o.numel()} records, "
+                                     f"the exchange delivers {total}")
+            if out_ready is not None:
+                torch.cuda.current_stream().wait_event(out_ready)
+        res = []
+        for i, c in enumerate(cols):
             if c is None:
-                out.append(None)
+                res.append(None)
                 continue
-            r = torch.empty(total, dtype=c.dtype, device=c.device)
+            if out is not None and not staged:
+                r = out[i][:total]
+            else:
+                r = torch.empty(total, dtype=c.dtype, device=c.device)
             dist.all_to_all_single(r, c, rc, sc, group=self.group)
-            out.append(r.to(dev) if staged else r)
-        return out, total
+            if staged:
+                r = out[i][:total].copy_(r) if out is not None else r.to(dev)
+            res.append(r)
+        return res, total
 
     def exchange(self, keys, ts, vals, key_hashes=None):
         pk, pt, pv, counts = self.partition(keys, ts, vals, key_hashes)
