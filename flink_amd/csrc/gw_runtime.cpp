@@ -1094,7 +1094,9 @@ struct gw_handle {
         if (!buf || len < (int64_t)sizeof(SnapHeader)) return fail(GW_E_INVALID, "snapshot blob too short");
         SnapHeader hd;
         memcpy(&hd, buf, sizeof hd);
-        if (memcmp(hd.magic, "GWS1", 4) != 0 || hd.version != 1) return fail(GW_E_INVALID, "not a gpuwin snapshot");
+        if (memcmp(hd.magic, "GWS1", 4) != 0 || (hd.version != 1 && hd.version != 2))
+            return fail(GW_E_INVALID, "not a gpuwin snapshot");
+        if (hd.version != 1) return fail(GW_E_INVALID, "snapshot of a different window / aggregate / max parallelism");
         if (hd.agg != cfg.agg || hd.assigner != cfg.assigner || hd.size != cfg.size || hd.slide != slide() ||
             hd.offset != cfg.offset || hd.pane != g || hd.max_parallelism != cfg.max_parallelism)
             return fail(GW_E_INVALID, "snapshot of a different window / aggregate / max parallelism");
@@ -1132,6 +1134,59 @@ struct gw_handle {
             B = std::max(fired_k * m, dmin);
         }
         return merge_deferred();
+    }
+
+    // Session windows: the blob (version 2) holds, per key group, every in-flight session
+    // as a 40-B (key, start, end, a0, a1) entry; no timer state (a session fires when the
+    // watermark passes end - 1, whichever handle holds it).
+    int snapshot_sessions(int32_t kg_lo, int32_t kg_hi, void* buf, int64_t cap, int64_t* len) {
+        int rc;
+        if (kg_lo < 0 || kg_hi < kg_lo || kg_hi >= cfg.max_parallelism)
+            return fail(GW_E_INVALID, "key-group range [%d, %d] outside [0, %d)", kg_lo, kg_hi, cfg.max_parallelism);
+        if ((rc = session_refresh(sess, err))) return fail(rc, "%s", err.c_str());
+        std::vector<int64_t> ent;
+        std::vector<int32_t> kgs;
+        if ((rc = session_collect(sess, kg_lo, kg_hi, ent, kgs, err))) return fail(rc, "%s", err.c_str());
+        const int nk = kg_hi - kg_lo + 1;
+        std::vector<int64_t> offs(nk + 1, 0);
+        for (int32_t k : kgs) offs[k - kg_lo + 1]++;
+        for (int i = 0; i < nk; ++i) offs[i + 1] += offs[i];
+        const int64_t need = (int64_t)sizeof(SnapHeader) + (int64_t)(nk + 1) * 8 + (int64_t)kgs.size() * 40;
+        *len = need;
+        if (!buf) return GW_OK;
+        if (cap < need) return fail(GW_E_OUTPUT_FULL, "snapshot needs %lld bytes", (long long)need);
+        SnapHeader hd{};
+        memcpy(hd.magic, "GWS1", 4);
+        hd.version = 2;
+        hd.agg = cfg.agg; hd.assigner = cfg.assigner;
+        hd.gap = cfg.gap;
+        hd.max_parallelism = cfg.max_parallelism; hd.kg_lo = kg_lo; hd.kg_hi = kg_hi;
+        hd.entries = (int64_t)kgs.size();
+        char* out = (char*)buf;
+        memcpy(out, &hd, sizeof hd);
+        memcpy(out + sizeof hd, offs.data(), (nk + 1) * 8);
+        int64_t* oe = (int64_t*)(out + sizeof hd + (nk + 1) * 8);
+        std::vector<int64_t> fill(offs.begin(), offs.end() - 1);
+        for (size_t i = 0; i < kgs.size(); ++i) memcpy(oe + 5 * fill[kgs[i] - kg_lo]++, &ent[5 * i], 40);
+        return GW_OK;
+    }
+
+    int restore_sessions(const void* buf, int64_t len) {
+        if (!buf || len < (int64_t)sizeof(SnapHeader)) return fail(GW_E_INVALID, "snapshot blob too short");
+        SnapHeader hd;
+        memcpy(&hd, buf, sizeof hd);
+        if (memcmp(hd.magic, "GWS1", 4) != 0 || (hd.version != 1 && hd.version != 2))
+            return fail(GW_E_INVALID, "not a gpuwin snapshot");
+        if (hd.version != 2 || hd.agg != cfg.agg || hd.assigner != cfg.assigner || hd.gap != cfg.gap ||
+            hd.max_parallelism != cfg.max_parallelism)
+            return fail(GW_E_INVALID, "snapshot of a different window / aggregate / max parallelism");
+        const int nk = hd.kg_hi - hd.kg_lo + 1;
+        const int64_t need = (int64_t)sizeof hd + (int64_t)(nk + 1) * 8 + hd.entries * 40;
+        if (nk <= 0 || hd.entries < 0 || len < need) return fail(GW_E_INVALID, "truncated snapshot blob");
+        const int64_t* in = (const int64_t*)((const char*)buf + sizeof hd + (nk + 1) * 8);
+        std::vector<int64_t> ent(in, in + hd.entries * 5);  // aligned copy
+        int rc = session_restore(sess, ent.data(), hd.entries, err);
+        return rc ? fail(rc, "%s", err.c_str()) : GW_OK;
     }
 
     int advance_pane(int64_t w, int64_t* rows_out) {
@@ -1696,20 +1751,24 @@ int gw_flush(gw_handle* h) {
 int gw_snapshot(gw_handle* h, int32_t kg_lo, int32_t kg_hi, void* buf, int64_t cap, int64_t* len) {
     if (!h || !len) return GW_E_INVALID;
     if (h->failed) return h->fail(GW_E_STATE, "operator failed earlier: %s", h->err.c_str());
-    if (h->session) return h->fail(GW_E_UNSUPPORTED, "snapshot of session windows is not yet supported");
+    if (h->session && h->cfg.assigner != GW_SESSION)
+        return h->fail(GW_E_UNSUPPORTED, "snapshot of count windows is not yet supported");
     if (h->cfg.allowed_lateness > 0)
         return h->fail(GW_E_UNSUPPORTED, "snapshot with allowed lateness > 0 is not yet supported");
     hipSetDevice(h->cfg.device);
+    if (h->session) return h->snapshot_sessions(kg_lo, kg_hi, buf, cap, len);
     return h->snapshot(kg_lo, kg_hi, buf, cap, len);
 }
 
 int gw_restore(gw_handle* h, const void* buf, int64_t len) {
     if (!h) return GW_E_INVALID;
     if (h->failed) return h->fail(GW_E_STATE, "operator failed earlier: %s", h->err.c_str());
-    if (h->session) return h->fail(GW_E_UNSUPPORTED, "restore of session windows is not yet supported");
+    if (h->session && h->cfg.assigner != GW_SESSION)
+        return h->fail(GW_E_UNSUPPORTED, "restore of count windows is not yet supported");
     if (h->cfg.allowed_lateness > 0)
         return h->fail(GW_E_UNSUPPORTED, "restore with allowed lateness > 0 is not yet supported");
     hipSetDevice(h->cfg.device);
+    if (h->session) return h->restore_sessions(buf, len);
     return h->restore(buf, len);
 }
 

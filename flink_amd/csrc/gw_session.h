@@ -1,6 +1,7 @@
 // gw_session.h — host interface of the event-time session-window path (gw_session.hip).
 #pragma once
 #include <string>
+#include <vector>
 
 #include "gw_device.h"
 
@@ -16,6 +17,11 @@ int session_ingest(SessionState* s, int64_t n, const int64_t* key, const int64_t
 int session_fire(SessionState* s, int64_t wm, int64_t* fired, std::string& err);
 void session_rows(SessionState* s, int64_t** k, int64_t** st, int64_t** en, int64_t** r, int64_t* total);
 int session_refresh(SessionState* s, std::string& err);
+// In-flight sessions of key groups [kg_lo, kg_hi] as (key, start, end, a0, a1) entries.
+int session_collect(SessionState* s, int32_t kg_lo, int32_t kg_hi, std::vector<int64_t>& ent,
+                    std::vector<int32_t>& kgs, std::string& err);
+// Insert n (key, start, end, a0, a1) session entries into the table.
+int session_restore(SessionState* s, const int64_t* ent, int64_t n, std::string& err);
 int session_clear_rows(SessionState* s, std::string& err);
 int64_t session_late(SessionState* s);
 void session_stats(SessionState* s, gw_stats* out);

@@ -335,6 +335,71 @@ __global__ void __launch_bounds__(256) k_sess_init(TableView t) {
     }
 }
 
+// Restore (gw_restore of a session snapshot): one thread per restored key.  The key's
+// restored sessions (sorted by start, disjoint) are swept together with the slot's
+// in-flight ones in start order and merged on inclusive intersection, exactly as
+// seg_process merges a batch; a fresh slot receives them unchanged.  A key whose
+// result exceeds the slot's K sessions is counted in st->overflow and left untouched.
+template <int AGG>
+__global__ void __launch_bounds__(256) k_sess_restore(TableView t, const int64_t* rk, const int64_t* roff,
+                                                      const int64_t* rs, int64_t n, DevStatus* st) {
+    unsigned long long ins = 0, flags = 0;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        bool inserted;
+        const int64_t slot = find_or_insert(t, rk[i], inserted);
+        ins += inserted;
+        if (slot < 0) { flags |= GW_DF_TABLE_FULL; continue; }
+        int64_t* sp = slot_ptr(t, slot);
+        const int SW = t.words, K = t.ring;
+        const int cnt = (int)sp[1];
+        Sess out[kMaxLocalSess];
+        int nout = 0, oi = 0;
+        int64_t r = roff[i];
+        const int64_t re = roff[i + 1];
+        bool have = false, ok = true;
+        Sess cur{0, 0, 0, 0};
+        while (oi < cnt || r < re) {
+            Sess item;
+            const int64_t* x = sp + 2 + oi * SW;
+            if (oi < cnt && (r >= re || x[0] <= rs[r * 4])) {
+                item = Sess{x[0], x[1], x[2], SW == 4 ? x[3] : 0};
+                ++oi;
+            } else {
+                item = Sess{rs[r * 4], rs[r * 4 + 1], rs[r * 4 + 2], rs[r * 4 + 3]};
+                ++r;
+            }
+            if (!have) {
+                cur = item;
+                have = true;
+            } else if (item.s <= cur.e) {
+                if (item.e > cur.e) cur.e = item.e;
+                fold_cell(AGG, cur.a0, cur.a1, item.a0, item.a1);
+            } else {
+                if (nout == K) { ok = false; break; }
+                out[nout++] = cur;
+                cur = item;
+            }
+        }
+        if (ok && have) {
+            if (nout == K) ok = false;
+            else out[nout++] = cur;
+        }
+        if (!ok) {
+            atomicAdd(&st->overflow, 1ull);
+            continue;
+        }
+        for (int q = 0; q < nout; ++q) {
+            int64_t* y = sp + 2 + q * SW;
+            y[0] = out[q].s;
+            y[1] = out[q].e;
+            y[2] = out[q].a0;
+            if (SW == 4) y[3] = out[q].a1;
+        }
+        sp[1] = nout;
+    }
+    block_commit(st, 0, ins, flags, 0);
+}
+
 #define GW_AGG_SWITCH(agg, CALL)                  \
     switch (agg) {                                \
     case GW_COUNT: CALL(GW_COUNT); break;         \
@@ -841,6 +906,102 @@ void session_rows(SessionState* s, int64_t** k, int64_t** st, int64_t** en, int6
 }
 
 int session_clear_rows(SessionState* s, std::string& err) { return set_word(s, offsetof(DevStatus, rows), 0, err); }
+
+// ---- snapshot / restore of in-flight sessions (gw_snapshot / gw_restore) -------------
+// The heap backend snapshots, per key group, every (key, window) state entry plus the
+// MergingWindowSet mapping (HeapSnapshotStrategy.java:97-154, MergingWindowSet.java:
+// 95-104 persistState); in-flight sessions are exactly that state here, one
+// (key, start, end, a0, a1) entry per session.
+int session_collect(SessionState* s, int32_t kg_lo, int32_t kg_hi, std::vector<int64_t>& ent,
+                    std::vector<int32_t>& kgs, std::string& err) {
+    SCHECK(hipStreamSynchronize(s->stream));
+    const TableView& t = s->tv;
+    const size_t words = (size_t)(t.cap + 1) * t.stride_w;
+    std::vector<int64_t> h(words);
+    SCHECK(hipMemcpy(h.data(), t.base, words * 8, hipMemcpyDeviceToHost));
+    const int SW = t.words;
+    for (int64_t i = 0; i <= t.cap; ++i) {
+        const int64_t* sp = h.data() + (size_t)i * t.stride_w;
+        const int cnt = (int)sp[1];
+        if (cnt <= 0) continue;
+        const int64_t key = i == t.cap ? kEmptyKey : sp[0];
+        const int32_t kg = key_group_for_hash(java_long_hash(key), s->cfg.max_parallelism);
+        if (kg < kg_lo || kg > kg_hi) continue;
+        for (int q = 0; q < cnt; ++q) {
+            const int64_t* x = sp + 2 + q * SW;
+            const int64_t e[5] = {key, x[0], x[1], x[2], SW == 4 ? x[3] : 0};
+            ent.insert(ent.end(), e, e + 5);
+            kgs.push_back(kg);
+        }
+    }
+    return GW_OK;
+}
+
+int session_restore(SessionState* s, const int64_t* ent, int64_t n, std::string& err) {
+    int rc;
+    if ((rc = session_refresh(s, err))) return rc;
+    if (n <= 0) return GW_OK;
+    std::vector<int64_t> ord(n);
+    for (int64_t i = 0; i < n; ++i) ord[i] = i;
+    std::sort(ord.begin(), ord.end(), [&](int64_t a, int64_t b) {
+        const int64_t* x = ent + a * 5;
+        const int64_t* y = ent + b * 5;
+        return x[0] != y[0] ? x[0] < y[0] : x[1] < y[1];
+    });
+    std::vector<int64_t> rk, roff, rs;
+    rs.reserve((size_t)n * 4);
+    int maxk = 0, run = 0;
+    for (int64_t j = 0; j < n; ++j) {
+        const int64_t* x = ent + ord[j] * 5;
+        if (j == 0 || x[0] != rk.back()) {
+            rk.push_back(x[0]);
+            roff.push_back(j);
+            run = 0;
+        }
+        maxk = std::max(maxk, ++run);
+        rs.insert(rs.end(), x + 1, x + 5);
+    }
+    roff.push_back(n);
+    const int64_t nk = (int64_t)rk.size();
+    if (maxk > kMaxLocalSess) {
+        err = "more than 32 in-flight sessions for one key is not supported on the GPU path";
+        return GW_E_UNSUPPORTED;
+    }
+    if (maxk > s->tv.ring) {
+        int newK = s->tv.ring;
+        while (newK < maxk) newK *= 2;
+        if ((rc = widen(s, std::min(newK, kMaxLocalSess), err))) return rc;
+    }
+    if ((double)(s->h_st->used_slots + nk) > 0.7 * (double)s->tv.cap) {
+        int64_t want = s->tv.cap;
+        while ((double)(s->h_st->used_slots + nk) > 0.7 * (double)want) want *= 2;
+        if ((rc = rehash_sess(s, want, err))) return rc;
+    }
+    int64_t *d_k = nullptr, *d_o = nullptr, *d_s = nullptr;
+    SCHECK(hipMalloc((void**)&d_k, nk * 8));
+    SCHECK(hipMalloc((void**)&d_o, (nk + 1) * 8));
+    SCHECK(hipMalloc((void**)&d_s, n * 32));
+    SCHECK(hipMemcpy(d_k, rk.data(), nk * 8, hipMemcpyHostToDevice));
+    SCHECK(hipMemcpy(d_o, roff.data(), (nk + 1) * 8, hipMemcpyHostToDevice));
+    SCHECK(hipMemcpy(d_s, rs.data(), n * 32, hipMemcpyHostToDevice));
+    if ((rc = set_word(s, offsetof(DevStatus, overflow), 0, err))) return rc;
+#define L(A) \
+    hipLaunchKernelGGL(k_sess_restore<A>, dim3(grid_of(nk)), dim3(256), 0, s->stream, s->tv, d_k, d_o, d_s, nk, s->d_st)
+    GW_AGG_SWITCH(s->cfg.agg, L);
+#undef L
+    SCHECK(hipGetLastError());
+    rc = session_refresh(s, err);
+    hipFree(d_k);
+    hipFree(d_o);
+    hipFree(d_s);
+    if (rc) return rc;
+    if (s->h_st->flags & GW_DF_TABLE_FULL) { err = "session state table full"; return GW_E_OOM; }
+    if (s->h_st->overflow) {
+        err = "restored sessions and in-flight sessions of one key exceed the slot's session list";
+        return GW_E_UNSUPPORTED;
+    }
+    return GW_OK;
+}
 
 int64_t session_late(SessionState* s) { return (int64_t)s->h_st->late; }
 

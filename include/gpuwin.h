@@ -183,8 +183,11 @@ int  gw_flush(gw_handle* h);
  * HeapSnapshotStrategy.java:97-154, CopyOnWriteStateMapSnapshot.writeState :127-149).
  * The blob holds, per key group, (key, pane, accumulator) entries; panes are the
  * operator's slices of width gcd(size, slide), so every aggregate restores exactly.
+ * Session windows: the blob (version 2) holds every in-flight session as a
+ * (key, start, end, accumulator) entry per key group -- the (key, window) state entries
+ * plus the merging window set of the heap backend (MergingWindowSet.java:95-104).
  * Two calls: buf == NULL returns the size in *len; then a buffer of cap >= *len.
- * Tumbling/sliding only (sessions: GW_E_UNSUPPORTED). */
+ * Count windows and allowed lateness > 0: GW_E_UNSUPPORTED. */
 int  gw_snapshot(gw_handle* h, int32_t kg_lo, int32_t kg_hi, void* buf, int64_t cap, int64_t* len);
 /* Restore one snapshot blob (call once per key-group range, e.g. after rescaling) into a
  * handle with the same assigner, aggregate and max parallelism

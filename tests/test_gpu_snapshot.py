@@ -122,3 +122,138 @@ def test_restore_rejects_other_config():
         b.initialize_state(blob)
     assert ei.value.code == -1
     b.close()
+
+
+# ------------------------------------------------------------------ session windows
+# The heap backend snapshots every (key, session window) state entry and the merging
+# window set per key group (HeapSnapshotStrategy.java:97-154, MergingWindowSet.java:95-104);
+# here every in-flight session is one (key, start, end, accumulator) entry of the blob.
+SESSION_AGGS = ["count", "sum_i64", "max_f64", "avg_f64", "avg_i64"]
+
+
+@pytest.mark.parametrize("agg", SESSION_AGGS)
+@pytest.mark.parametrize("gap", [100, 3000])
+def test_session_snapshot_restore_mid_stream(oracle_lib, agg, gap):
+    kw = dict(assigner="session", gap=gap, agg=agg)
+    keys, ts, vals, batches = random_stream(seed=43 + gap, n=20000, num_keys=300, n_batches=16, agg=agg)
+    op = gpu_operator(kw)
+    outs = []
+    for i, (lo, hi, wm) in enumerate(batches):
+        op.process_batch(keys[lo:hi], ts[lo:hi], vals[lo:hi])
+        if i in (4, 9, 13):  # snapshot after the records, before the watermark
+            blob = op.snapshot_state()
+            op.close()
+            op = gpu_operator(kw)
+            op.initialize_state(blob)
+        op.advance_watermark(wm)
+        _rows(op, outs)
+    op.advance_watermark(W.LONG_MAX)
+    _rows(op, outs)
+    op.close()
+    o, _ = run_oracle(oracle_lib, kw, keys, ts, vals, batches)
+    assert compare(outs, o, agg in ("sum_f64", "avg_f64")) == []
+
+
+@pytest.mark.parametrize("agg", ["sum_i64", "avg_f64"])
+def test_session_rescale_two_to_one_and_one_to_two(oracle_lib, agg):
+    """Session state moves with its key groups (KeyGroupRangeAssignment.java:93-106)."""
+    kw = dict(assigner="session", gap=3000, agg=agg)
+    keys, ts, vals, batches = random_stream(seed=17, n=20000, num_keys=500, n_batches=12, agg=agg)
+    own2 = owners(keys, 128, 2)
+    cut = 6
+    o, _ = run_oracle(oracle_lib, kw, keys, ts, vals, batches)
+    dbl = agg == "avg_f64"
+
+    def mk(p, r):
+        return W.GpuWindowOperator(W.EventTimeSessionWindows.with_gap(3000), agg, capacity_hint=1024, parallelism=p,
+                                   operator_index=r).open()
+
+    def run(ops, own, phase_batches, outs_per_wm):
+        for lo, hi, wm in phase_batches:
+            for r, op in enumerate(ops):
+                sel = np.arange(lo, hi)
+                if own is not None:
+                    sel = sel[own[lo:hi] == r]
+                op.process_batch(keys[sel], ts[sel], vals[sel])
+            got = []
+            for op in ops:
+                op.advance_watermark(wm)
+                k, s, e, rr = op.drain()
+                got.append((k, s, e, rr.view(np.int64)))
+            outs_per_wm.append(tuple(np.concatenate([g[c] for g in got]) for c in range(4)))
+
+    def finish(ops, outs):
+        last = []
+        for op in ops:
+            op.advance_watermark(W.LONG_MAX)
+            k, s, e, rr = op.drain()
+            last.append((k, s, e, rr.view(np.int64)))
+            op.close()
+        outs.append(tuple(np.concatenate([g[c] for g in last]) for c in range(4)))
+
+    # 2 -> 1
+    ops = [mk(2, r) for r in range(2)]
+    outs = []
+    run(ops, own2, batches[:cut], outs)
+    blobs = [op.snapshot_state(W.compute_key_group_range_for_operator_index(128, 2, r)) for r, op in enumerate(ops)]
+    for op in ops:
+        op.close()
+    one = mk(1, 0)
+    one.initialize_state(blobs)
+    run([one], None, batches[cut:], outs)
+    finish([one], outs)
+    assert compare(outs, o, dbl) == []
+
+    # 1 -> 2
+    one = mk(1, 0)
+    outs = []
+    run([one], None, batches[:cut], outs)
+    blobs = [one.snapshot_state(W.compute_key_group_range_for_operator_index(128, 2, r)) for r in range(2)]
+    one.close()
+    ops = [mk(2, r) for r in range(2)]
+    for r, op in enumerate(ops):
+        op.initialize_state(blobs[r])
+    run(ops, own2, batches[cut:], outs)
+    finish(ops, outs)
+    assert compare(outs, o, dbl) == []
+
+
+def test_session_restore_widens_for_many_sessions_per_key(oracle_lib):
+    """A key with more restored sessions than the slot's inline list widens it (K -> 32)."""
+    kw = dict(assigner="session", gap=10, agg="sum_i64")
+    keys = np.zeros(20, np.int64)
+    ts = np.arange(20, dtype=np.int64) * 1000  # 20 disjoint sessions of one key, none fired
+    vals = np.arange(20, dtype=np.int64)
+    batches = [(0, 20, -10**9)]
+    op = gpu_operator(kw)
+    op.process_batch(keys, ts, vals)
+    blob = op.snapshot_state()
+    op.close()
+    op = gpu_operator(kw)
+    op.initialize_state(blob)
+    outs = []
+    op.advance_watermark(-10**9)
+    _rows(op, outs)
+    op.advance_watermark(W.LONG_MAX)
+    _rows(op, outs)
+    op.close()
+    o, _ = run_oracle(oracle_lib, kw, keys, ts, vals, batches)
+    assert compare(outs, o, False) == []
+
+
+def test_session_and_pane_blobs_do_not_mix():
+    s = gpu_operator(dict(assigner="session", gap=100, agg="sum_i64"))
+    s.process_batch(np.arange(10, dtype=np.int64), np.arange(10, dtype=np.int64), np.ones(10, np.int64))
+    sblob = s.snapshot_state()
+    t = gpu_operator(dict(assigner="tumbling", size=100, slide=100, agg="sum_i64"))
+    t.process_batch(np.arange(10, dtype=np.int64), np.arange(10, dtype=np.int64), np.ones(10, np.int64))
+    tblob = t.snapshot_state()
+    for op, blob in ((t, sblob), (s, tblob)):
+        with pytest.raises(N.GpuWinError) as ei:
+            op.initialize_state(blob)
+        assert ei.value.code == -1
+    g = gpu_operator(dict(assigner="session", gap=200, agg="sum_i64"))
+    with pytest.raises(N.GpuWinError):
+        g.initialize_state(sblob)
+    for op in (s, t, g):
+        op.close()
