@@ -1094,7 +1094,7 @@ struct gw_handle {
         if (!buf || len < (int64_t)sizeof(SnapHeader)) return fail(GW_E_INVALID, "snapshot blob too short");
         SnapHeader hd;
         memcpy(&hd, buf, sizeof hd);
-        if (memcmp(hd.magic, "GWS1", 4) != 0 || (hd.version != 1 && hd.version != 2))
+        if (memcmp(hd.magic, "GWS1", 4) != 0 || hd.version < 1 || hd.version > 3)
             return fail(GW_E_INVALID, "not a gpuwin snapshot");
         if (hd.version != 1) return fail(GW_E_INVALID, "snapshot of a different window / aggregate / max parallelism");
         if (hd.agg != cfg.agg || hd.assigner != cfg.assigner || hd.size != cfg.size || hd.slide != slide() ||
@@ -1139,6 +1139,14 @@ struct gw_handle {
     // Session windows: the blob (version 2) holds, per key group, every in-flight session
     // as a 40-B (key, start, end, a0, a1) entry; no timer state (a session fires when the
     // watermark passes end - 1, whichever handle holds it).
+    // Session windows (blob version 2): every in-flight session as a (key, start, end,
+    // a0, a1) entry per key group -- the reference's (key, window) state entries plus its
+    // merging window set -- and no timer state (a session fires when the watermark passes
+    // end - 1, whichever handle holds it).  Count windows (version 3): per key, the
+    // element count and the ring of count-pane accumulators -- the CountTrigger count and
+    // the window contents the evicting operator keeps (EvictingWindowOperator.java:92-135).
+    uint32_t slot_blob_version() const { return cfg.assigner == GW_SESSION ? 2u : 3u; }
+
     int snapshot_sessions(int32_t kg_lo, int32_t kg_hi, void* buf, int64_t cap, int64_t* len) {
         int rc;
         if (kg_lo < 0 || kg_hi < kg_lo || kg_hi >= cfg.max_parallelism)
@@ -1147,27 +1155,29 @@ struct gw_handle {
         std::vector<int64_t> ent;
         std::vector<int32_t> kgs;
         if ((rc = session_collect(sess, kg_lo, kg_hi, ent, kgs, err))) return fail(rc, "%s", err.c_str());
+        const int64_t ew = session_entry_words(sess);
         const int nk = kg_hi - kg_lo + 1;
         std::vector<int64_t> offs(nk + 1, 0);
         for (int32_t k : kgs) offs[k - kg_lo + 1]++;
         for (int i = 0; i < nk; ++i) offs[i + 1] += offs[i];
-        const int64_t need = (int64_t)sizeof(SnapHeader) + (int64_t)(nk + 1) * 8 + (int64_t)kgs.size() * 40;
+        const int64_t need = (int64_t)sizeof(SnapHeader) + (int64_t)(nk + 1) * 8 + (int64_t)kgs.size() * ew * 8;
         *len = need;
         if (!buf) return GW_OK;
         if (cap < need) return fail(GW_E_OUTPUT_FULL, "snapshot needs %lld bytes", (long long)need);
         SnapHeader hd{};
         memcpy(hd.magic, "GWS1", 4);
-        hd.version = 2;
+        hd.version = slot_blob_version();
         hd.agg = cfg.agg; hd.assigner = cfg.assigner;
-        hd.gap = cfg.gap;
+        hd.size = cfg.size; hd.slide = cfg.slide; hd.gap = cfg.gap;
         hd.max_parallelism = cfg.max_parallelism; hd.kg_lo = kg_lo; hd.kg_hi = kg_hi;
+        hd.reserved = (int32_t)ew;
         hd.entries = (int64_t)kgs.size();
         char* out = (char*)buf;
         memcpy(out, &hd, sizeof hd);
         memcpy(out + sizeof hd, offs.data(), (nk + 1) * 8);
         int64_t* oe = (int64_t*)(out + sizeof hd + (nk + 1) * 8);
         std::vector<int64_t> fill(offs.begin(), offs.end() - 1);
-        for (size_t i = 0; i < kgs.size(); ++i) memcpy(oe + 5 * fill[kgs[i] - kg_lo]++, &ent[5 * i], 40);
+        for (size_t i = 0; i < kgs.size(); ++i) memcpy(oe + ew * fill[kgs[i] - kg_lo]++, &ent[ew * i], ew * 8);
         return GW_OK;
     }
 
@@ -1175,16 +1185,18 @@ struct gw_handle {
         if (!buf || len < (int64_t)sizeof(SnapHeader)) return fail(GW_E_INVALID, "snapshot blob too short");
         SnapHeader hd;
         memcpy(&hd, buf, sizeof hd);
-        if (memcmp(hd.magic, "GWS1", 4) != 0 || (hd.version != 1 && hd.version != 2))
+        if (memcmp(hd.magic, "GWS1", 4) != 0 || hd.version < 1 || hd.version > 3)
             return fail(GW_E_INVALID, "not a gpuwin snapshot");
-        if (hd.version != 2 || hd.agg != cfg.agg || hd.assigner != cfg.assigner || hd.gap != cfg.gap ||
-            hd.max_parallelism != cfg.max_parallelism)
+        const int64_t ew = session_entry_words(sess);
+        if (hd.version != slot_blob_version() || hd.agg != cfg.agg || hd.assigner != cfg.assigner ||
+            hd.gap != cfg.gap || hd.size != cfg.size || hd.slide != cfg.slide ||
+            hd.max_parallelism != cfg.max_parallelism || hd.reserved != (int32_t)ew)
             return fail(GW_E_INVALID, "snapshot of a different window / aggregate / max parallelism");
         const int nk = hd.kg_hi - hd.kg_lo + 1;
-        const int64_t need = (int64_t)sizeof hd + (int64_t)(nk + 1) * 8 + hd.entries * 40;
+        const int64_t need = (int64_t)sizeof hd + (int64_t)(nk + 1) * 8 + hd.entries * ew * 8;
         if (nk <= 0 || hd.entries < 0 || len < need) return fail(GW_E_INVALID, "truncated snapshot blob");
         const int64_t* in = (const int64_t*)((const char*)buf + sizeof hd + (nk + 1) * 8);
-        std::vector<int64_t> ent(in, in + hd.entries * 5);  // aligned copy
+        std::vector<int64_t> ent(in, in + hd.entries * ew);  // aligned copy
         int rc = session_restore(sess, ent.data(), hd.entries, err);
         return rc ? fail(rc, "%s", err.c_str()) : GW_OK;
     }
@@ -1751,8 +1763,6 @@ int gw_flush(gw_handle* h) {
 int gw_snapshot(gw_handle* h, int32_t kg_lo, int32_t kg_hi, void* buf, int64_t cap, int64_t* len) {
     if (!h || !len) return GW_E_INVALID;
     if (h->failed) return h->fail(GW_E_STATE, "operator failed earlier: %s", h->err.c_str());
-    if (h->session && h->cfg.assigner != GW_SESSION)
-        return h->fail(GW_E_UNSUPPORTED, "snapshot of count windows is not yet supported");
     if (h->cfg.allowed_lateness > 0)
         return h->fail(GW_E_UNSUPPORTED, "snapshot with allowed lateness > 0 is not yet supported");
     hipSetDevice(h->cfg.device);
@@ -1763,8 +1773,6 @@ int gw_snapshot(gw_handle* h, int32_t kg_lo, int32_t kg_hi, void* buf, int64_t c
 int gw_restore(gw_handle* h, const void* buf, int64_t len) {
     if (!h) return GW_E_INVALID;
     if (h->failed) return h->fail(GW_E_STATE, "operator failed earlier: %s", h->err.c_str());
-    if (h->session && h->cfg.assigner != GW_SESSION)
-        return h->fail(GW_E_UNSUPPORTED, "restore of count windows is not yet supported");
     if (h->cfg.allowed_lateness > 0)
         return h->fail(GW_E_UNSUPPORTED, "restore with allowed lateness > 0 is not yet supported");
     hipSetDevice(h->cfg.device);

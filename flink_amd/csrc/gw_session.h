@@ -17,10 +17,13 @@ int session_ingest(SessionState* s, int64_t n, const int64_t* key, const int64_t
 int session_fire(SessionState* s, int64_t wm, int64_t* fired, std::string& err);
 void session_rows(SessionState* s, int64_t** k, int64_t** st, int64_t** en, int64_t** r, int64_t* total);
 int session_refresh(SessionState* s, std::string& err);
-// In-flight sessions of key groups [kg_lo, kg_hi] as (key, start, end, a0, a1) entries.
+// State of key groups [kg_lo, kg_hi] as entries of session_entry_words() int64 each:
+// sessions (key, start, end, a0, a1) per in-flight session; count windows (key, element
+// count, ring of pane accumulators) per key.
+int session_entry_words(SessionState* s);
 int session_collect(SessionState* s, int32_t kg_lo, int32_t kg_hi, std::vector<int64_t>& ent,
                     std::vector<int32_t>& kgs, std::string& err);
-// Insert n (key, start, end, a0, a1) session entries into the table.
+// Insert n entries of session_entry_words() int64 (as session_collect writes them).
 int session_restore(SessionState* s, const int64_t* ent, int64_t n, std::string& err);
 int session_clear_rows(SessionState* s, std::string& err);
 int64_t session_late(SessionState* s);

@@ -518,6 +518,31 @@ __global__ void __launch_bounds__(256) k_cnt_rehash(TableView o, TableView nt, D
     block_commit(st, 0, ins, flags, 0);
 }
 
+// Restore of count-window state: one thread per entry (key, element count, ring of pane
+// accumulators), copied into the key's slot.  The slot geometry is a function of the
+// configuration (checked by the caller), so the copy is exact.  A key that already holds
+// state here is counted in st->overflow and left untouched (blobs of one key group are
+// never restored twice).
+__global__ void __launch_bounds__(256) k_cnt_restore(TableView t, const int64_t* ent, int64_t n, DevStatus* st) {
+    unsigned long long ins = 0, flags = 0;
+    const int words = t.ring * t.words;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t* e = ent + i * (2 + words);
+        bool inserted;
+        const int64_t j = find_or_insert(t, e[0], inserted);
+        if (j < 0) { flags |= GW_DF_TABLE_FULL; continue; }
+        ins += inserted;
+        int64_t* d = slot_ptr(t, j);
+        if (d[1] != 0) {
+            atomicAdd(&st->overflow, 1ull);
+            continue;
+        }
+        for (int w = 0; w < words; ++w) d[2 + w] = e[2 + w];
+        d[1] = e[1];
+    }
+    block_commit(st, 0, ins, flags, 0);
+}
+
 // --------------------------------------------------------------------------- host
 struct SessionState {
     gw_config cfg{};
@@ -922,11 +947,17 @@ int session_collect(SessionState* s, int32_t kg_lo, int32_t kg_hi, std::vector<i
     const int SW = t.words;
     for (int64_t i = 0; i <= t.cap; ++i) {
         const int64_t* sp = h.data() + (size_t)i * t.stride_w;
-        const int cnt = (int)sp[1];
-        if (cnt <= 0) continue;
+        if (sp[1] == 0) continue;
         const int64_t key = i == t.cap ? kEmptyKey : sp[0];
         const int32_t kg = key_group_for_hash(java_long_hash(key), s->cfg.max_parallelism);
         if (kg < kg_lo || kg > kg_hi) continue;
+        if (s->count_mode) {  // (key, element count, ring of pane accumulators)
+            ent.push_back(key);
+            ent.insert(ent.end(), sp + 1, sp + 2 + t.ring * SW);
+            kgs.push_back(kg);
+            continue;
+        }
+        const int cnt = (int)sp[1];
         for (int q = 0; q < cnt; ++q) {
             const int64_t* x = sp + 2 + q * SW;
             const int64_t e[5] = {key, x[0], x[1], x[2], SW == 4 ? x[3] : 0};
@@ -937,10 +968,38 @@ int session_collect(SessionState* s, int32_t kg_lo, int32_t kg_hi, std::vector<i
     return GW_OK;
 }
 
+int session_entry_words(SessionState* s) { return s->count_mode ? 2 + s->tv.ring * s->tv.words : 5; }
+
+static int count_restore(SessionState* s, const int64_t* ent, int64_t n, std::string& err) {
+    int rc;
+    if ((double)(s->h_st->used_slots + n) > 0.7 * (double)s->tv.cap) {
+        int64_t want = s->tv.cap;
+        while ((double)(s->h_st->used_slots + n) > 0.7 * (double)want) want *= 2;
+        if ((rc = rehash_sess(s, want, err))) return rc;
+    }
+    const int64_t bytes = n * session_entry_words(s) * 8;
+    int64_t* d = nullptr;
+    SCHECK(hipMalloc((void**)&d, bytes));
+    SCHECK(hipMemcpy(d, ent, bytes, hipMemcpyHostToDevice));
+    if ((rc = set_word(s, offsetof(DevStatus, overflow), 0, err))) return rc;
+    hipLaunchKernelGGL(k_cnt_restore, dim3(grid_of(n)), dim3(256), 0, s->stream, s->tv, d, n, s->d_st);
+    SCHECK(hipGetLastError());
+    rc = session_refresh(s, err);
+    hipFree(d);
+    if (rc) return rc;
+    if (s->h_st->flags & GW_DF_TABLE_FULL) { err = "count-window state table overflow"; return GW_E_OOM; }
+    if (s->h_st->overflow) {
+        err = "a restored key already holds count-window state in this operator";
+        return GW_E_UNSUPPORTED;
+    }
+    return GW_OK;
+}
+
 int session_restore(SessionState* s, const int64_t* ent, int64_t n, std::string& err) {
     int rc;
     if ((rc = session_refresh(s, err))) return rc;
     if (n <= 0) return GW_OK;
+    if (s->count_mode) return count_restore(s, ent, n, err);
     std::vector<int64_t> ord(n);
     for (int64_t i = 0; i < n; ++i) ord[i] = i;
     std::sort(ord.begin(), ord.end(), [&](int64_t a, int64_t b) {

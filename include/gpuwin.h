@@ -186,8 +186,10 @@ int  gw_flush(gw_handle* h);
  * Session windows: the blob (version 2) holds every in-flight session as a
  * (key, start, end, accumulator) entry per key group -- the (key, window) state entries
  * plus the merging window set of the heap backend (MergingWindowSet.java:95-104).
+ * Count windows (version 3): per key, the element count and the ring of count-pane
+ * accumulators (the CountTrigger count and the evicting operator's window contents).
  * Two calls: buf == NULL returns the size in *len; then a buffer of cap >= *len.
- * Count windows and allowed lateness > 0: GW_E_UNSUPPORTED. */
+ * Allowed lateness > 0: GW_E_UNSUPPORTED. */
 int  gw_snapshot(gw_handle* h, int32_t kg_lo, int32_t kg_hi, void* buf, int64_t cap, int64_t* len);
 /* Restore one snapshot blob (call once per key-group range, e.g. after rescaling) into a
  * handle with the same assigner, aggregate and max parallelism

@@ -95,3 +95,78 @@ def test_gpu_window_word_count_shape(oracle_lib):
     g, o, _ = run_both(oracle_lib, kw, keys, vals, [0, 100_000, 200_000, 300_000])
     assert compare(g, o, False) == []
     assert sum(len(x[0]) for x in g) > 100
+
+
+# ------------------------------------------------------------------ snapshot / restore
+# The reference checkpoints, per key group, the CountTrigger's count and the window
+# contents the evicting operator keeps (HeapSnapshotStrategy.java:97-154); here a key's
+# element count and its ring of count-pane accumulators are that state.
+@pytest.mark.parametrize("assigner,size,slide", [("count_tumbling", 5, 5), ("count_sliding", 250, 150),
+                                                 ("count_sliding", 3, 5)])
+@pytest.mark.parametrize("agg", ["count", "sum_i64", "max_f64", "avg_f64"])
+def test_gpu_count_windows_snapshot_restore(oracle_lib, assigner, size, slide, agg):
+    kw = dict(assigner=assigner, size=size, slide=slide, agg=agg)
+    n = 40000
+    keys, _, vals, _ = random_stream(size * 3 + slide, n, 300, 1, agg=agg)
+    keys[np.random.default_rng(1).random(n) < 0.1] = W.LONG_MIN  # the sentinel slot carries state too
+    cuts = [0, 9000, 9001, 23000, n]
+    g_out, o_out = [], []
+    ora = oracle_lib.OracleOperator(oracle_lib.make_config(**kw))
+    vb = vals.view(np.int64) if vals.dtype == np.float64 else vals
+    op = gpu_operator(kw, capacity_hint=64)
+    try:
+        for i, (lo, hi) in enumerate(zip(cuts[:-1], cuts[1:])):
+            if i:  # snapshot between every two batches, restore into a fresh operator
+                blob = op.snapshot_state()
+                op.close()
+                op = gpu_operator(kw, capacity_hint=16)
+                op.initialize_state(blob)
+            op.process_batch(keys[lo:hi], np.zeros(hi - lo, dtype=np.int64), vals[lo:hi])
+            g_out.append(rows(op))
+            ora.process_batch(keys[lo:hi], np.zeros(hi - lo, dtype=np.int64), vb[lo:hi])
+            o_out.append(ora.drain())
+    finally:
+        op.close()
+    assert compare(g_out, o_out, agg in N.DOUBLE_RESULT) == []
+
+
+def test_gpu_count_windows_rescale_two_to_one(oracle_lib):
+    from tests.dist_worker import owners
+    kw = dict(assigner="count_sliding", size=4, slide=2, agg="sum_i64")
+    n = 20000
+    keys, _, vals, _ = random_stream(9, n, 500, 1, agg="sum_i64")
+    own = owners(keys, 128, 2)
+    cut = 8000
+    mk = lambda p, r: W.GpuWindowOperator(W.CountWindows.of(4, 2), "sum_i64", capacity_hint=1024, parallelism=p,
+                                          operator_index=r).open()
+    ops = [mk(2, r) for r in range(2)]
+    got = []
+    for r, op in enumerate(ops):
+        sel = np.arange(cut)[own[:cut] == r]
+        op.process_batch(keys[sel], np.zeros(len(sel), np.int64), vals[sel])
+        got.append(rows(op))
+    blobs = [op.snapshot_state(W.compute_key_group_range_for_operator_index(128, 2, r)) for r, op in enumerate(ops)]
+    for op in ops:
+        op.close()
+    one = mk(1, 0)
+    one.initialize_state(blobs)
+    one.process_batch(keys[cut:], np.zeros(n - cut, np.int64), vals[cut:])
+    got.append(rows(one))
+    one.close()
+    ora = oracle_lib.OracleOperator(oracle_lib.make_config(**kw))
+    ora.process_batch(keys, np.zeros(n, np.int64), vals)
+    o = ora.drain()
+    g = tuple(np.concatenate([x[c] for x in got]) for c in range(4))
+    assert compare([g], [o], False) == []
+
+
+def test_gpu_count_window_blob_rejected_by_other_geometry():
+    a = gpu_operator(dict(assigner="count_sliding", size=4, slide=2, agg="sum_i64"))
+    a.process_batch(np.arange(10, dtype=np.int64), np.zeros(10, np.int64), np.ones(10, np.int64))
+    blob = a.snapshot_state()
+    b = gpu_operator(dict(assigner="count_sliding", size=6, slide=2, agg="sum_i64"))
+    with pytest.raises(N.GpuWinError) as ei:
+        b.initialize_state(blob)
+    assert ei.value.code == -1
+    a.close()
+    b.close()
