@@ -42,6 +42,11 @@ struct SegArgs {
     const int64_t* val;
     int64_t gap;
     int64_t wm;             // current watermark (all records of the batch see it)
+    int64_t lateness;       // allowed lateness (WindowOperator.allowedLateness)
+    int64_t* o_key;         // rows of windows an element fires at once (EventTimeTrigger.onElement
+    int64_t* o_start;       //   FIRE: window max timestamp <= watermark; lateness > 0 only)
+    int64_t* o_end;
+    int64_t* o_res;
     TableView t;            // ring = K sessions per slot, words = words per session
     const uint32_t* retry_in;
     int64_t n_retry_in;
@@ -96,7 +101,29 @@ __global__ void __launch_bounds__(256) k_sess_prep(const int64_t* key, const int
 
 struct Sess {
     int64_t s, e, a0, a1;
+    bool f;  // its event-time timer has fired (kept for allowed lateness until cleanup)
 };
+
+// Slot word 1: in-flight session count (low 32 bits) | fired bit per session (high 32).
+__device__ __forceinline__ int slot_cnt(int64_t w) { return (int)(uint32_t)(uint64_t)w; }
+__device__ __forceinline__ bool slot_fired(int64_t w, int q) { return ((uint64_t)w >> (32 + q)) & 1ull; }
+
+// WindowOperator.cleanupTime (:670-677, overflow -> Long.MAX_VALUE, never cleaned) <= wm
+__device__ __forceinline__ bool cleaned_at(int64_t end, int64_t lateness, int64_t wm) {
+    const int64_t mx = end - 1;
+    int64_t ct;
+    if (__builtin_add_overflow(mx, lateness, &ct)) ct = INT64_MAX;
+    return ct <= wm;
+}
+
+template <int AGG>
+__device__ __forceinline__ void emit_now(const SegArgs& a, int64_t key, const Sess& x) {
+    const unsigned long long at = atomicAdd(&a.st->rows, 1ull);
+    a.o_key[at] = key;
+    a.o_start[at] = x.s;
+    a.o_end[at] = x.e;
+    a.o_res[at] = cell_result(AGG, x.a0, x.a1);
+}
 
 template <int AGG>
 __device__ void seg_process(const SegArgs& a, int64_t i) {
@@ -108,10 +135,11 @@ __device__ void seg_process(const SegArgs& a, int64_t i) {
     const int SW = a.t.words;
     const int K = a.t.ring;
     Sess cur_list[kMaxLocalSess];
-    int cnt = (int)sp[1];
+    const int64_t w1 = sp[1];
+    int cnt = slot_cnt(w1);
     for (int q = 0; q < cnt; ++q) {
         const int64_t* x = sp + 2 + q * SW;
-        cur_list[q] = Sess{x[0], x[1], x[2], SW == 4 ? x[3] : 0};
+        cur_list[q] = Sess{x[0], x[1], x[2], SW == 4 ? x[3] : 0, slot_fired(w1, q)};
     }
     unsigned long long late = 0, merges = 0, flags = 0;
     const int64_t ts_first = a.ts_min + (int64_t)(a.skey[i] & tsmask);
@@ -136,7 +164,7 @@ __device__ void seg_process(const SegArgs& a, int64_t i) {
             } else {
                 int64_t c0, c1;
                 record_cell(AGG, a.val ? a.val[a.perm[e]] : 0, c0, c1);
-                item = Sess{te, te + a.gap, c0, c1};
+                item = Sess{te, te + a.gap, c0, c1, false};
                 is_old = false;
                 ++e;
             }
@@ -147,6 +175,7 @@ __device__ void seg_process(const SegArgs& a, int64_t i) {
             } else if (item.s <= cur.e) {
                 if (item.e > cur.e) cur.e = item.e;
                 fold_cell(AGG, cur.a0, cur.a1, item.a0, item.a1);
+                cur.f = cur.f && item.f;  // a merge with a new window re-arms the timer (its end > wm)
                 if (is_old && cur_has_state) merges++;
                 cur_has_state |= is_old;
             } else {
@@ -165,7 +194,23 @@ __device__ void seg_process(const SegArgs& a, int64_t i) {
             cnt = nout;
         }
     } else {
-        // Arrival-order replay (MergingWindowSet.addWindow per record).
+        // Arrival-order replay (MergingWindowSet.addWindow per record).  With allowed
+        // lateness an element may fire its window at once; those rows are written only in
+        // a second pass, once the first has shown that the result fits the slot (a slot
+        // that overflows is retried after widening and must not emit twice).
+        Sess init[kMaxLocalSess];
+        const int cnt0 = cnt;
+        const int passes = a.lateness > 0 ? 2 : 1;
+        for (int q = 0; q < cnt0 && passes == 2; ++q) init[q] = cur_list[q];
+        for (int pass = 0; pass < passes; ++pass) {
+        const bool emit = pass == 1;
+        if (emit) {
+            if (!ok || cnt > K) break;
+            for (int q = 0; q < cnt0; ++q) cur_list[q] = init[q];
+            cnt = cnt0;
+            late = 0;
+            merges = 0;
+        }
         int64_t last = -1;
         for (int64_t step = i; step < j && ok; ++step) {
             int64_t best = -1;
@@ -187,11 +232,12 @@ __device__ void seg_process(const SegArgs& a, int64_t i) {
             int64_t c0, c1;
             record_cell(AGG, a.val ? a.val[bp] : 0, c0, c1);
             if (lo < 0) {
-                if (we - 1 <= a.wm) { late++; continue; }  // isWindowLate -> retireWindow, dropped
+                if (cleaned_at(we, a.lateness, a.wm)) { late++; continue; }  // isWindowLate -> dropped
                 if (cnt == kMaxLocalSess) { ok = false; break; }
                 int q = cnt;
                 while (q > 0 && cur_list[q - 1].s > ws) { cur_list[q] = cur_list[q - 1]; --q; }
-                cur_list[q] = Sess{ws, we, c0, c1};
+                cur_list[q] = Sess{ws, we, c0, c1, we - 1 <= a.wm};
+                if (emit && cur_list[q].f) emit_now<AGG>(a, sp[0], cur_list[q]);  // onElement: FIRE
                 cnt++;
             } else {
                 Sess m = cur_list[lo];
@@ -203,11 +249,14 @@ __device__ void seg_process(const SegArgs& a, int64_t i) {
                 }
                 if (we > m.e) m.e = we;
                 fold_cell(AGG, m.a0, m.a1, c0, c1);
+                m.f = m.e - 1 <= a.wm;  // onElement FIRE, or onMerge registers the merged window's timer
+                if (emit && m.f) emit_now<AGG>(a, sp[0], m);
                 cur_list[lo] = m;
                 const int removed = hi - lo;
                 for (int q = hi + 1; q < cnt; ++q) cur_list[q - removed] = cur_list[q];
                 cnt -= removed;
             }
+        }
         }
     }
     if (!ok || cnt > K) {
@@ -217,14 +266,16 @@ __device__ void seg_process(const SegArgs& a, int64_t i) {
         atomicMax(&a.st->pad[1], (unsigned long long)(ok ? cnt : kMaxLocalSess + 1));
         return;
     }
+    uint64_t fired = 0;
     for (int q = 0; q < cnt; ++q) {
         int64_t* x = sp + 2 + q * SW;
         x[0] = cur_list[q].s;
         x[1] = cur_list[q].e;
         x[2] = cur_list[q].a0;
         if (SW == 4) x[3] = cur_list[q].a1;
+        fired |= (uint64_t)cur_list[q].f << q;
     }
-    sp[1] = cnt;
+    sp[1] = (int64_t)(((uint64_t)fired << 32) | (uint64_t)(uint32_t)cnt);
     ShardCtr& sc = a.st->sh[blockIdx.x % kShards];
     if (late) atomicAdd(&sc.late, late);
     if (merges) atomicAdd(&sc.merges, merges);
@@ -249,8 +300,8 @@ __global__ void __launch_bounds__(256) k_sess_segment(SegArgs a) {
 // sorted, so the fired ones are a prefix), emit (key, start, end, result), purge.
 // Rows are staged in LDS, one row per thread per round, and flushed in bulk.
 template <int AGG>
-__global__ void __launch_bounds__(256) k_sess_fire(TableView t, int64_t wm, int64_t* o_key, int64_t* o_start,
-                                                   int64_t* o_end, int64_t* o_res, DevStatus* st) {
+__global__ void __launch_bounds__(256) k_sess_fire(TableView t, int64_t wm, int64_t lateness, int64_t* o_key,
+                                                   int64_t* o_start, int64_t* o_end, int64_t* o_res, DevStatus* st) {
     __shared__ RowStage rs;
     __shared__ int s_max;
     const int64_t nslots = t.cap + 1;
@@ -262,11 +313,18 @@ __global__ void __launch_bounds__(256) k_sess_fire(TableView t, int64_t wm, int6
     for (int64_t base = c0; base < c1; base += blockDim.x) {
         const int64_t i = base + threadIdx.x;
         int64_t* s = nullptr;
-        int cnt = 0, nf = 0;
+        int cnt = 0, nf = 0, nc = 0;
+        int64_t w1 = 0;
         if (i < c1) {
             s = slot_ptr(t, i);
-            cnt = (int)s[1];
-            while (nf < cnt && s[2 + nf * SW + 1] - 1 <= wm) ++nf;
+            w1 = s[1];
+            cnt = slot_cnt(w1);
+            while (nf < cnt && s[2 + nf * SW + 1] - 1 <= wm) ++nf;  // due timers: a prefix (sorted, disjoint)
+            nc = nf;
+            if (lateness > 0) {  // cleanup timers (max timestamp + lateness) are a prefix of those
+                nc = 0;
+                while (nc < nf && cleaned_at(s[2 + nc * SW + 1], lateness, wm)) ++nc;
+            }
         }
         if (threadIdx.x == 0) s_max = 0;
         __syncthreads();
@@ -278,7 +336,7 @@ __global__ void __launch_bounds__(256) k_sess_fire(TableView t, int64_t wm, int6
             const bool flush = rs.cnt + blockDim.x > kRowStage;
             __syncthreads();
             if (flush) stage_flush(rs, &st->rows, o_key, o_start, o_end, o_res);
-            if (q < nf) {
+            if (q < nf && !slot_fired(w1, q)) {
                 const int64_t* x = s + 2 + q * SW;
                 const unsigned j = atomicAdd(&rs.cnt, 1u);
                 rs.k[j] = s[0];
@@ -289,9 +347,12 @@ __global__ void __launch_bounds__(256) k_sess_fire(TableView t, int64_t wm, int6
             __syncthreads();
         }
         if (nf) {
-            for (int q = nf; q < cnt; ++q)
-                for (int w = 0; w < SW; ++w) s[2 + (q - nf) * SW + w] = s[2 + q * SW + w];
-            s[1] = cnt - nf;
+            uint64_t fired = 0;
+            for (int q = nc; q < cnt; ++q) {
+                for (int w = 0; w < SW; ++w) s[2 + (q - nc) * SW + w] = s[2 + q * SW + w];
+                fired |= (uint64_t)(q < nf || slot_fired(w1, q)) << (q - nc);
+            }
+            s[1] = (int64_t)((fired << 32) | (uint64_t)(uint32_t)(cnt - nc));
         }
     }
     stage_flush(rs, &st->rows, o_key, o_start, o_end, o_res);
@@ -303,7 +364,7 @@ __global__ void __launch_bounds__(256) k_sess_rewiden(TableView o, TableView n) 
         int64_t* d = slot_ptr(n, i);
         d[0] = s[0];
         d[1] = s[1];
-        const int cnt = (int)s[1];
+        const int cnt = slot_cnt(s[1]);
         for (int w = 0; w < cnt * o.words; ++w) d[2 + w] = s[2 + w];
     }
 }
@@ -320,8 +381,8 @@ __global__ void __launch_bounds__(256) k_sess_rehash(TableView o, TableView n, D
         if (j < 0) { flags |= GW_DF_TABLE_FULL; continue; }
         ins += inserted;
         int64_t* d = slot_ptr(n, j);
-        const int cnt = (int)s[1];
-        d[1] = cnt;
+        const int cnt = slot_cnt(s[1]);
+        d[1] = s[1];
         for (int w = 0; w < cnt * o.words; ++w) d[2 + w] = s[2 + w];
     }
     block_commit(st, 0, ins, flags, 0);
@@ -845,7 +906,12 @@ int session_ingest(SessionState* s, int64_t n, const int64_t* key, const int64_t
     a.val = val;
     a.gap = s->cfg.gap;
     a.wm = wm;
+    a.lateness = s->cfg.allowed_lateness;
     a.st = s->d_st;
+    if (a.lateness > 0) {  // an element fires at most one window at once
+        if ((rc = ensure_rows(s, (int64_t)s->h_st->rows + n, err))) return rc;
+        a.o_key = s->o_key; a.o_start = s->o_start; a.o_end = s->o_end; a.o_res = s->o_res;
+    }
     uint32_t* rin = s->r0;
     uint32_t* rout = s->r1;
     int64_t n_retry = 0;
@@ -909,8 +975,8 @@ int session_fire(SessionState* s, int64_t wm, int64_t* fired, std::string& err) 
     if (s->timing) SCHECK(hipEventRecord(ev.first, s->stream));
     const unsigned fg = (unsigned)std::min<int64_t>(1024, std::max<int64_t>(1, (s->tv.cap + 1 + 255) / 256));
 #define L(A)                                                                                               \
-    hipLaunchKernelGGL(k_sess_fire<A>, dim3(fg), dim3(256), 0, s->stream, s->tv, wm, s->o_key, s->o_start, \
-                       s->o_end, s->o_res, s->d_st)
+    hipLaunchKernelGGL(k_sess_fire<A>, dim3(fg), dim3(256), 0, s->stream, s->tv, wm, s->cfg.allowed_lateness, \
+                       s->o_key, s->o_start, s->o_end, s->o_res, s->d_st)
     GW_AGG_SWITCH(s->cfg.agg, L);
 #undef L
     SCHECK(hipGetLastError());

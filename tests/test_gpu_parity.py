@@ -46,8 +46,8 @@ class GpuBackend:
         return k, s, e, r.view(np.int64)
 
     def snapshot_restore(self):
-        if self.kw["assigner"] == "session" or self.kw.get("lateness", 0) > 0:
-            return  # not supported yet (GW_E_UNSUPPORTED)
+        if self.kw.get("lateness", 0) > 0:
+            return  # snapshots with allowed lateness > 0: not supported yet (GW_E_UNSUPPORTED)
         if self.k:
             self.op.process_batch(np.array(self.k, np.int64), np.array(self.t, np.int64),
                                   np.array(self.v, np.int64))
