@@ -190,6 +190,36 @@ ops_tests.append({
             ["w", _start + 999, [["key2", 1, _start + 999, None, None]]]],
     "late": 0,
 })
+# Session windows and allowed lateness (gap 3 s, ReducedSessionWindowFunction emits
+# (key-sum, start, end)@end-1).  Rows a late element fires at once (EventTimeTrigger.onElement
+# FIRE) are checked at the next watermark with that watermark's rows.
+_sl_in = [["e", "key2", 1, 1000], ["w", 1999, []], ["e", "key2", 1, 2000], ["w", 4998, []],
+          ["e", "key2", 1, 4500], ["e", "key2", 1, 8500], ["w", 7400, []],
+          ["e", "key2", 1, 7000], ["w", 11501, [["key2", 5, 11499, 1000, 11500]]],
+          ["e", "key2", 1, 11600], ["w", 14600, [["key2", 1, 14599, 11600, 14600]]]]
+# testSideOutputDueToLatenessSessionZeroLateness (:2571-2668): the element at 10000 is late
+# (side output; counted as late_dropped here).
+ops_tests.append({"name": "session_lateness_zero", "source": WOT + ":2571-2668",
+                  "config": {"assigner": "session", "gap": 3000, "agg": "sum_i32"},
+                  "ops": _sl_in + [["e", "key2", 1, 10000], ["e", "key2", 1, 14500],
+                                   ["w", 20000, [["key2", 1, 17499, 14500, 17500]]], ["w", 100000, []]],
+                  "late": 1})
+# testNotSideOutputDueToLatenessSessionWithLateness (:2766-2879): lateness 10 ms; 10000
+# merges into the fired (11600, 14600) session and fires (10000, 14600) at once.
+ops_tests.append({"name": "session_lateness_10", "source": WOT + ":2766-2879",
+                  "config": {"assigner": "session", "gap": 3000, "agg": "sum_i32", "lateness": 10},
+                  "ops": _sl_in + [["e", "key2", 1, 10000], ["e", "key2", 1, 14500],
+                                   ["w", 20000, [["key2", 2, 14599, 10000, 14600],
+                                                 ["key2", 3, 17499, 10000, 17500]]], ["w", 100000, []]],
+                  "late": 0})
+# testNotSideOutputDueToLatenessSessionWithHugeLateness (:2984-3083): lateness 10 s; the
+# fired (1000, 11500) session is still kept, so 10000 merges everything into (1000, 14600).
+ops_tests.append({"name": "session_lateness_huge", "source": WOT + ":2984-3083",
+                  "config": {"assigner": "session", "gap": 3000, "agg": "sum_i32", "lateness": 10000},
+                  "ops": _sl_in + [["e", "key2", 1, 10000], ["e", "key2", 1, 14500],
+                                   ["w", 20000, [["key2", 7, 14599, 1000, 14600],
+                                                 ["key2", 8, 17499, 1000, 17500]]], ["w", 100000, []]],
+                  "late": 0})
 # SessionWindowing example (flink-examples-streaming SessionWindowing.java:58-69, gap 3 ms
 # at :94, sum(2)) with expected output SessionWindowingData.java:23-24.  The tuple's f1
 # (first element's timestamp) equals the session start for this input.
