@@ -1295,10 +1295,6 @@ static int validate(const gw_config* c, std::string& why) {
         why = "unknown trigger";
         return GW_E_INVALID;
     }
-    if (c->allowed_lateness != 0 && c->assigner == GW_SESSION && c->trigger == GW_PURGING_EVENT_TIME_TRIGGER) {
-        why = "allowed lateness > 0 with session windows and a purging trigger is not yet supported on the GPU path";
-        return GW_E_UNSUPPORTED;
-    }
     return GW_OK;
 }
 

@@ -43,6 +43,7 @@ struct SegArgs {
     int64_t gap;
     int64_t wm;             // current watermark (all records of the batch see it)
     int64_t lateness;       // allowed lateness (WindowOperator.allowedLateness)
+    int purge;              // PurgingTrigger with lateness > 0: a fired session keeps an empty state
     int64_t* o_key;         // rows of windows an element fires at once (EventTimeTrigger.onElement
     int64_t* o_start;       //   FIRE: window max timestamp <= watermark; lateness > 0 only)
     int64_t* o_end;
@@ -114,6 +115,15 @@ __device__ __forceinline__ bool cleaned_at(int64_t end, int64_t lateness, int64_
     int64_t ct;
     if (__builtin_add_overflow(mx, lateness, &ct)) ct = INT64_MAX;
     return ct <= wm;
+}
+
+// The empty state a purged session keeps (FIRE_AND_PURGE clears the contents, the window
+// stays in the merging window set until its cleanup time): the fold identity, with -0.0
+// for floating sums so that folding a single -0.0 keeps its sign.
+template <int AGG>
+__device__ __forceinline__ void purge_acc(int64_t& a0, int64_t& a1) {
+    a0 = AGG == GW_AVG_F64 ? (int64_t)0x8000000000000000ull : identity0(AGG);
+    a1 = 0;
 }
 
 template <int AGG>
@@ -237,7 +247,10 @@ __device__ void seg_process(const SegArgs& a, int64_t i) {
                 int q = cnt;
                 while (q > 0 && cur_list[q - 1].s > ws) { cur_list[q] = cur_list[q - 1]; --q; }
                 cur_list[q] = Sess{ws, we, c0, c1, we - 1 <= a.wm};
-                if (emit && cur_list[q].f) emit_now<AGG>(a, sp[0], cur_list[q]);  // onElement: FIRE
+                if (cur_list[q].f) {  // onElement: FIRE (PurgingTrigger: FIRE_AND_PURGE)
+                    if (emit) emit_now<AGG>(a, sp[0], cur_list[q]);
+                    if (a.purge) purge_acc<AGG>(cur_list[q].a0, cur_list[q].a1);
+                }
                 cnt++;
             } else {
                 Sess m = cur_list[lo];
@@ -250,7 +263,10 @@ __device__ void seg_process(const SegArgs& a, int64_t i) {
                 if (we > m.e) m.e = we;
                 fold_cell(AGG, m.a0, m.a1, c0, c1);
                 m.f = m.e - 1 <= a.wm;  // onElement FIRE, or onMerge registers the merged window's timer
-                if (emit && m.f) emit_now<AGG>(a, sp[0], m);
+                if (m.f) {
+                    if (emit) emit_now<AGG>(a, sp[0], m);
+                    if (a.purge) purge_acc<AGG>(m.a0, m.a1);
+                }
                 cur_list[lo] = m;
                 const int removed = hi - lo;
                 for (int q = hi + 1; q < cnt; ++q) cur_list[q - removed] = cur_list[q];
@@ -300,7 +316,7 @@ __global__ void __launch_bounds__(256) k_sess_segment(SegArgs a) {
 // sorted, so the fired ones are a prefix), emit (key, start, end, result), purge.
 // Rows are staged in LDS, one row per thread per round, and flushed in bulk.
 template <int AGG>
-__global__ void __launch_bounds__(256) k_sess_fire(TableView t, int64_t wm, int64_t lateness, int64_t* o_key,
+__global__ void __launch_bounds__(256) k_sess_fire(TableView t, int64_t wm, int64_t lateness, int purge, int64_t* o_key,
                                                    int64_t* o_start, int64_t* o_end, int64_t* o_res, DevStatus* st) {
     __shared__ RowStage rs;
     __shared__ int s_max;
@@ -351,6 +367,12 @@ __global__ void __launch_bounds__(256) k_sess_fire(TableView t, int64_t wm, int6
             for (int q = nc; q < cnt; ++q) {
                 for (int w = 0; w < SW; ++w) s[2 + (q - nc) * SW + w] = s[2 + q * SW + w];
                 fired |= (uint64_t)(q < nf || slot_fired(w1, q)) << (q - nc);
+                if (purge && q < nf && !slot_fired(w1, q)) {  // FIRE_AND_PURGE of a kept session
+                    int64_t z0, z1;
+                    purge_acc<AGG>(z0, z1);
+                    s[2 + (q - nc) * SW + 2] = z0;
+                    if (SW == 4) s[2 + (q - nc) * SW + 3] = z1;
+                }
             }
             s[1] = (int64_t)((fired << 32) | (uint64_t)(uint32_t)(cnt - nc));
         }
@@ -907,6 +929,7 @@ int session_ingest(SessionState* s, int64_t n, const int64_t* key, const int64_t
     a.gap = s->cfg.gap;
     a.wm = wm;
     a.lateness = s->cfg.allowed_lateness;
+    a.purge = a.lateness > 0 && s->cfg.trigger == GW_PURGING_EVENT_TIME_TRIGGER;
     a.st = s->d_st;
     if (a.lateness > 0) {  // an element fires at most one window at once
         if ((rc = ensure_rows(s, (int64_t)s->h_st->rows + n, err))) return rc;
@@ -976,6 +999,7 @@ int session_fire(SessionState* s, int64_t wm, int64_t* fired, std::string& err) 
     const unsigned fg = (unsigned)std::min<int64_t>(1024, std::max<int64_t>(1, (s->tv.cap + 1 + 255) / 256));
 #define L(A)                                                                                               \
     hipLaunchKernelGGL(k_sess_fire<A>, dim3(fg), dim3(256), 0, s->stream, s->tv, wm, s->cfg.allowed_lateness, \
+                       (int)(s->cfg.allowed_lateness > 0 && s->cfg.trigger == GW_PURGING_EVENT_TIME_TRIGGER), \
                        s->o_key, s->o_start, s->o_end, s->o_res, s->d_st)
     GW_AGG_SWITCH(s->cfg.agg, L);
 #undef L

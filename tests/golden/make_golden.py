@@ -220,6 +220,18 @@ ops_tests.append({"name": "session_lateness_huge", "source": WOT + ":2984-3083",
                                    ["w", 20000, [["key2", 7, 14599, 1000, 14600],
                                                  ["key2", 8, 17499, 1000, 17500]]], ["w", 100000, []]],
                   "late": 0})
+# testDropDueToLatenessSessionWithLatenessPurgingTrigger (:2670-2765) and
+# testNotSideOutputDueToLatenessSessionWithHugeLatenessPurgingTrigger (:2881-2983):
+# PurgingTrigger(EventTimeTrigger); a fired session keeps an empty state until cleanup.
+for _name, _src, _lat, _start in (("session_lateness_10_purging", ":2670-2765", 10, 10000),
+                                  ("session_lateness_huge_purging", ":2881-2983", 10000, 1000)):
+    ops_tests.append({"name": _name, "source": WOT + _src,
+                      "config": {"assigner": "session", "gap": 3000, "agg": "sum_i32", "lateness": _lat,
+                                 "trigger": "purging_event_time"},
+                      "ops": _sl_in + [["e", "key2", 1, 10000], ["e", "key2", 1, 14500],
+                                       ["w", 20000, [["key2", 1, 14599, _start, 14600],
+                                                     ["key2", 1, 17499, _start, 17500]]], ["w", 100000, []]],
+                      "late": 0})
 # SessionWindowing example (flink-examples-streaming SessionWindowing.java:58-69, gap 3 ms
 # at :94, sum(2)) with expected output SessionWindowingData.java:23-24.  The tuple's f1
 # (first element's timestamp) equals the session start for this input.

@@ -166,7 +166,15 @@ def test_session_lateness_many_sessions_per_key(oracle_lib):
     assert _cmp(g, o, "sum_i64") == []
 
 
-def test_session_lateness_purging_trigger_is_unsupported():
-    with pytest.raises(N.GpuWinError) as ei:
-        gpu_operator(dict(assigner="session", gap=100, agg="sum_i64", lateness=500, trigger="purging_event_time"))
-    assert ei.value.code == -2
+@pytest.mark.parametrize("agg", ["count", "sum_i64", "min_f64", "avg_f64"])
+@pytest.mark.parametrize("lateness", [300, 2000])
+def test_session_lateness_purging_trigger_vs_oracle(oracle_lib, lateness, agg):
+    """PurgingTrigger(EventTimeTrigger) with lateness: every firing purges, the session stays
+    (empty) in the merging window set until cleanup, and a later merge folds into nothing."""
+    kw = dict(assigner="session", gap=1500, agg=agg, lateness=lateness, trigger="purging_event_time")
+    keys, ts, vals, batches = random_stream(seed=zlib.crc32(f"slp{agg}{lateness}".encode()) & 0xffff, n=20000,
+                                            num_keys=60, n_batches=40, disorder=2500 + lateness, wm_lag=200, agg=agg)
+    g, glate, _ = run_gpu(kw, keys, ts, vals, batches)
+    o, olate = run_oracle(oracle_lib, kw, keys, ts, vals, batches)
+    assert glate == olate
+    assert _cmp(g, o, agg) == []
