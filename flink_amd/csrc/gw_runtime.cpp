@@ -1140,7 +1140,7 @@ struct gw_handle {
     // as a 40-B (key, start, end, a0, a1) entry; no timer state (a session fires when the
     // watermark passes end - 1, whichever handle holds it).
     // Session windows (blob version 2): every in-flight session as a (key, start, end,
-    // a0, a1) entry per key group -- the reference's (key, window) state entries plus its
+    // a0, a1, fired) entry per key group (fired: kept after firing, under allowed lateness) -- the reference's (key, window) state entries plus its
     // merging window set -- and no timer state (a session fires when the watermark passes
     // end - 1, whichever handle holds it).  Count windows (version 3): per key, the
     // element count and the ring of count-pane accumulators -- the CountTrigger count and
@@ -1759,8 +1759,8 @@ int gw_flush(gw_handle* h) {
 int gw_snapshot(gw_handle* h, int32_t kg_lo, int32_t kg_hi, void* buf, int64_t cap, int64_t* len) {
     if (!h || !len) return GW_E_INVALID;
     if (h->failed) return h->fail(GW_E_STATE, "operator failed earlier: %s", h->err.c_str());
-    if (h->cfg.allowed_lateness > 0)
-        return h->fail(GW_E_UNSUPPORTED, "snapshot with allowed lateness > 0 is not yet supported");
+    if (h->cfg.allowed_lateness > 0 && h->cfg.assigner != GW_SESSION)
+        return h->fail(GW_E_UNSUPPORTED, "snapshot with allowed lateness > 0 is not yet supported for time windows");
     hipSetDevice(h->cfg.device);
     if (h->session) return h->snapshot_sessions(kg_lo, kg_hi, buf, cap, len);
     return h->snapshot(kg_lo, kg_hi, buf, cap, len);
@@ -1769,8 +1769,8 @@ int gw_snapshot(gw_handle* h, int32_t kg_lo, int32_t kg_hi, void* buf, int64_t c
 int gw_restore(gw_handle* h, const void* buf, int64_t len) {
     if (!h) return GW_E_INVALID;
     if (h->failed) return h->fail(GW_E_STATE, "operator failed earlier: %s", h->err.c_str());
-    if (h->cfg.allowed_lateness > 0)
-        return h->fail(GW_E_UNSUPPORTED, "restore with allowed lateness > 0 is not yet supported");
+    if (h->cfg.allowed_lateness > 0 && h->cfg.assigner != GW_SESSION)
+        return h->fail(GW_E_UNSUPPORTED, "restore with allowed lateness > 0 is not yet supported for time windows");
     hipSetDevice(h->cfg.device);
     if (h->session) return h->restore_sessions(buf, len);
     return h->restore(buf, len);

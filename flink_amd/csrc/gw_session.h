@@ -18,7 +18,7 @@ int session_fire(SessionState* s, int64_t wm, int64_t* fired, std::string& err);
 void session_rows(SessionState* s, int64_t** k, int64_t** st, int64_t** en, int64_t** r, int64_t* total);
 int session_refresh(SessionState* s, std::string& err);
 // State of key groups [kg_lo, kg_hi] as entries of session_entry_words() int64 each:
-// sessions (key, start, end, a0, a1) per in-flight session; count windows (key, element
+// sessions (key, start, end, a0, a1, fired) per in-flight session; count windows (key, element
 // count, ring of pane accumulators) per key.
 int session_entry_words(SessionState* s);
 int session_collect(SessionState* s, int32_t kg_lo, int32_t kg_hi, std::vector<int64_t>& ent,

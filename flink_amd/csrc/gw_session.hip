@@ -434,7 +434,8 @@ __global__ void __launch_bounds__(256) k_sess_restore(TableView t, const int64_t
         if (slot < 0) { flags |= GW_DF_TABLE_FULL; continue; }
         int64_t* sp = slot_ptr(t, slot);
         const int SW = t.words, K = t.ring;
-        const int cnt = (int)sp[1];
+        const int64_t w1 = sp[1];
+        const int cnt = slot_cnt(w1);
         Sess out[kMaxLocalSess];
         int nout = 0, oi = 0;
         int64_t r = roff[i];
@@ -444,11 +445,11 @@ __global__ void __launch_bounds__(256) k_sess_restore(TableView t, const int64_t
         while (oi < cnt || r < re) {
             Sess item;
             const int64_t* x = sp + 2 + oi * SW;
-            if (oi < cnt && (r >= re || x[0] <= rs[r * 4])) {
-                item = Sess{x[0], x[1], x[2], SW == 4 ? x[3] : 0};
+            if (oi < cnt && (r >= re || x[0] <= rs[r * 5])) {
+                item = Sess{x[0], x[1], x[2], SW == 4 ? x[3] : 0, slot_fired(w1, oi)};
                 ++oi;
             } else {
-                item = Sess{rs[r * 4], rs[r * 4 + 1], rs[r * 4 + 2], rs[r * 4 + 3]};
+                item = Sess{rs[r * 5], rs[r * 5 + 1], rs[r * 5 + 2], rs[r * 5 + 3], rs[r * 5 + 4] != 0};
                 ++r;
             }
             if (!have) {
@@ -457,6 +458,7 @@ __global__ void __launch_bounds__(256) k_sess_restore(TableView t, const int64_t
             } else if (item.s <= cur.e) {
                 if (item.e > cur.e) cur.e = item.e;
                 fold_cell(AGG, cur.a0, cur.a1, item.a0, item.a1);
+                cur.f = cur.f && item.f;
             } else {
                 if (nout == K) { ok = false; break; }
                 out[nout++] = cur;
@@ -471,14 +473,16 @@ __global__ void __launch_bounds__(256) k_sess_restore(TableView t, const int64_t
             atomicAdd(&st->overflow, 1ull);
             continue;
         }
+        uint64_t fired = 0;
         for (int q = 0; q < nout; ++q) {
             int64_t* y = sp + 2 + q * SW;
             y[0] = out[q].s;
             y[1] = out[q].e;
             y[2] = out[q].a0;
             if (SW == 4) y[3] = out[q].a1;
+            fired |= (uint64_t)out[q].f << q;
         }
-        sp[1] = nout;
+        sp[1] = (int64_t)((fired << 32) | (uint64_t)(uint32_t)nout);
     }
     block_commit(st, 0, ins, flags, 0);
 }
@@ -1047,18 +1051,19 @@ int session_collect(SessionState* s, int32_t kg_lo, int32_t kg_hi, std::vector<i
             kgs.push_back(kg);
             continue;
         }
-        const int cnt = (int)sp[1];
+        const int cnt = (int)(uint32_t)(uint64_t)sp[1];
         for (int q = 0; q < cnt; ++q) {
             const int64_t* x = sp + 2 + q * SW;
-            const int64_t e[5] = {key, x[0], x[1], x[2], SW == 4 ? x[3] : 0};
-            ent.insert(ent.end(), e, e + 5);
+            const int64_t fired = (int64_t)(((uint64_t)sp[1] >> (32 + q)) & 1ull);  // kept under allowed lateness
+            const int64_t e[6] = {key, x[0], x[1], x[2], SW == 4 ? x[3] : 0, fired};
+            ent.insert(ent.end(), e, e + 6);
             kgs.push_back(kg);
         }
     }
     return GW_OK;
 }
 
-int session_entry_words(SessionState* s) { return s->count_mode ? 2 + s->tv.ring * s->tv.words : 5; }
+int session_entry_words(SessionState* s) { return s->count_mode ? 2 + s->tv.ring * s->tv.words : 6; }
 
 static int count_restore(SessionState* s, const int64_t* ent, int64_t n, std::string& err) {
     int rc;
@@ -1093,22 +1098,22 @@ int session_restore(SessionState* s, const int64_t* ent, int64_t n, std::string&
     std::vector<int64_t> ord(n);
     for (int64_t i = 0; i < n; ++i) ord[i] = i;
     std::sort(ord.begin(), ord.end(), [&](int64_t a, int64_t b) {
-        const int64_t* x = ent + a * 5;
-        const int64_t* y = ent + b * 5;
+        const int64_t* x = ent + a * 6;
+        const int64_t* y = ent + b * 6;
         return x[0] != y[0] ? x[0] < y[0] : x[1] < y[1];
     });
     std::vector<int64_t> rk, roff, rs;
-    rs.reserve((size_t)n * 4);
+    rs.reserve((size_t)n * 5);
     int maxk = 0, run = 0;
     for (int64_t j = 0; j < n; ++j) {
-        const int64_t* x = ent + ord[j] * 5;
+        const int64_t* x = ent + ord[j] * 6;
         if (j == 0 || x[0] != rk.back()) {
             rk.push_back(x[0]);
             roff.push_back(j);
             run = 0;
         }
         maxk = std::max(maxk, ++run);
-        rs.insert(rs.end(), x + 1, x + 5);
+        rs.insert(rs.end(), x + 1, x + 6);
     }
     roff.push_back(n);
     const int64_t nk = (int64_t)rk.size();
@@ -1129,10 +1134,10 @@ int session_restore(SessionState* s, const int64_t* ent, int64_t n, std::string&
     int64_t *d_k = nullptr, *d_o = nullptr, *d_s = nullptr;
     SCHECK(hipMalloc((void**)&d_k, nk * 8));
     SCHECK(hipMalloc((void**)&d_o, (nk + 1) * 8));
-    SCHECK(hipMalloc((void**)&d_s, n * 32));
+    SCHECK(hipMalloc((void**)&d_s, n * 40));
     SCHECK(hipMemcpy(d_k, rk.data(), nk * 8, hipMemcpyHostToDevice));
     SCHECK(hipMemcpy(d_o, roff.data(), (nk + 1) * 8, hipMemcpyHostToDevice));
-    SCHECK(hipMemcpy(d_s, rs.data(), n * 32, hipMemcpyHostToDevice));
+    SCHECK(hipMemcpy(d_s, rs.data(), n * 40, hipMemcpyHostToDevice));
     if ((rc = set_word(s, offsetof(DevStatus, overflow), 0, err))) return rc;
 #define L(A) \
     hipLaunchKernelGGL(k_sess_restore<A>, dim3(grid_of(nk)), dim3(256), 0, s->stream, s->tv, d_k, d_o, d_s, nk, s->d_st)

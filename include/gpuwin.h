@@ -189,7 +189,8 @@ int  gw_flush(gw_handle* h);
  * Count windows (version 3): per key, the element count and the ring of count-pane
  * accumulators (the CountTrigger count and the evicting operator's window contents).
  * Two calls: buf == NULL returns the size in *len; then a buffer of cap >= *len.
- * Allowed lateness > 0: GW_E_UNSUPPORTED. */
+ * Allowed lateness > 0 with tumbling/sliding windows: GW_E_UNSUPPORTED (sessions carry a
+ * fired flag per entry and snapshot under lateness). */
 int  gw_snapshot(gw_handle* h, int32_t kg_lo, int32_t kg_hi, void* buf, int64_t cap, int64_t* len);
 /* Restore one snapshot blob (call once per key-group range, e.g. after rescaling) into a
  * handle with the same assigner, aggregate and max parallelism

@@ -257,3 +257,37 @@ def test_session_and_pane_blobs_do_not_mix():
         g.initialize_state(sblob)
     for op in (s, t, g):
         op.close()
+
+
+@pytest.mark.parametrize("trigger", ["event_time", "purging_event_time"])
+@pytest.mark.parametrize("agg", ["sum_i64", "avg_f64", "min_f64"])
+def test_session_snapshot_with_lateness(oracle_lib, agg, trigger):
+    """Under allowed lateness a fired session stays until cleanup; its entry carries the
+    fired flag, so a restored handle neither fires it again nor forgets it for late merges."""
+    kw = dict(assigner="session", gap=1500, agg=agg, lateness=2000)
+    if trigger == "purging_event_time":
+        kw["trigger"] = trigger
+    keys, ts, vals, batches = random_stream(seed=91, n=20000, num_keys=60, n_batches=30, disorder=4500, wm_lag=200,
+                                            agg=agg)
+    op = gpu_operator(kw)
+    outs = []
+    for i, (lo, hi, wm) in enumerate(batches):
+        op.process_batch(keys[lo:hi], ts[lo:hi], vals[lo:hi])
+        pre = None
+        if i in (7, 15, 22):
+            pre = op.drain()  # rows late elements fired at once were emitted before the snapshot
+            blob = op.snapshot_state()
+            op.close()
+            op = gpu_operator(kw)
+            op.initialize_state(blob)
+        op.advance_watermark(wm)
+        _rows(op, outs)
+        if pre is not None:
+            outs[-1] = tuple(np.concatenate([p, q]) for p, q in zip((pre[0], pre[1], pre[2], pre[3].view(np.int64)),
+                                                                     outs[-1]))
+    op.advance_watermark(W.LONG_MAX)
+    _rows(op, outs)
+    op.close()
+    o, olate = run_oracle(oracle_lib, kw, keys, ts, vals, batches)
+    assert olate > 0
+    assert compare(outs, o, agg in ("sum_f64", "avg_f64")) == []
