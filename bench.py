@@ -68,6 +68,9 @@ def parse():
                     help="a2a: RCCL all-to-all keyBy exchange; none: each rank generates only its own key groups")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-host-fed", action="store_true",
+                    help="skip the host-fed leg (gw_ingest from host columns: pinned staging + H2D)")
+    ap.add_argument("--host-fed-steps", type=int, default=4)
     ap.add_argument("--preagg", choices=["auto", "force", "off"], default="auto")
     ap.add_argument("--producer-stream", choices=["auto", "torch", "handle"], default="auto",
                     help="stream gw_ingest_device orders after: the exchange output's (torch) stream, or, "
@@ -236,8 +239,20 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     last = t0
+    # Per fire cycle: a watermark that completes windows fires them and synchronises with
+    # the device (gw_advance_watermark), so the host clock at the return of such a step
+    # closes one cycle of batches + their fire.
+    cycles = []
+    cyc_t, cyc_steps, fires_seen = t0, 0, op.stats()["fires"]
     for b in range(args.warmup, steps_total):
         step(b, True)
+        cyc_steps += 1
+        f = op.stats()["fires"]
+        if f != fires_seen:
+            now = time.perf_counter()
+            cycles.append({"steps": cyc_steps, "ms": (now - cyc_t) * 1e3,
+                           "events_per_s": cyc_steps * nb / max(now - cyc_t, 1e-9)})
+            cyc_t, cyc_steps, fires_seen = now, 0, f
         if rank == 0 and time.perf_counter() - last > 30:
             last = time.perf_counter()
             log(f"step {b - args.warmup + 1}/{args.steps}")
@@ -246,6 +261,8 @@ def main():
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    if cyc_steps:
+        cycles.append({"steps": cyc_steps, "ms": (time.perf_counter() - cyc_t) * 1e3, "partial": True})
     if dist:
         e = torch.tensor([elapsed], dtype=torch.float64, device=dev if args.dist_backend == "nccl" else "cpu")
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
@@ -291,6 +308,9 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args, keys, ts, vals, wms, nb, agg, size, slide)
+    host_fed = None
+    if rank == 0 and world == 1 and not args.no_host_fed:
+        host_fed = host_fed_leg(args, W, keys, ts, vals, wms, nb, agg, size, slide, K, maxp, local)
 
     if rank == 0:
         out = {
@@ -327,6 +347,8 @@ def main():
                 "d_over_n": dsum / max(events_rank, 1),
             },
             "rows_fired": rows_all,
+            "fire_cycles": cycles,
+            "host_fed": host_fed,
             "cpu_baseline": cpu,
         }
         if args.checksum:
@@ -365,15 +387,76 @@ def traffic_bytes(agg, nb):
     return None
 
 
+def host_fed_leg(args, W, keys, ts, vals, wms, nb, agg, size, slide, K, maxp, local):
+    """The north star's host path: columns in (pageable) host memory -> gw_ingest, which
+    copies them into the handle's pinned staging and then over PCIe into HBM, then the
+    watermark.  A fresh operator over the first --host-fed-steps batches of the same stream;
+    PCIe-inclusive events/s (never the bench's `value`)."""
+    H = max(1, min(args.host_fed_steps, len(wms)))
+    hk = keys[:H * nb].cpu().numpy()
+    ht = ts[:H * nb].cpu().numpy()
+    hv = vals[:H * nb].cpu().numpy() if vals is not None else None
+    op = W.GpuWindowOperator(W.SlidingEventTimeWindows.of(size, slide), agg, capacity_hint=K,
+                             max_parallelism=maxp, device=local, max_batch=nb).open()
+    try:
+        op.process_batch(hk[:nb], ht[:nb], hv[:nb] if hv is not None else None)  # warm: staging allocation
+        op.advance_watermark(wms[0])
+        op.clear_rows()
+        op.synchronize()
+        t0 = time.perf_counter()
+        for b in range(1, H):
+            lo, hi = b * nb, (b + 1) * nb
+            op.process_batch(hk[lo:hi], ht[lo:hi], hv[lo:hi] if hv is not None else None)
+            op.advance_watermark(wms[b])
+            op.clear_rows()
+        op.flush()
+        op.synchronize()
+        sec = time.perf_counter() - t0
+    finally:
+        op.close()
+    n = (H - 1) * nb
+    return {"value": n / sec if n else None, "unit": "events/s", "batches": H - 1, "events": n,
+            "bytes_per_event_h2d": 16 if vals is None else 24,
+            "path": "gw_ingest (memcpy into pinned staging + hipMemcpyAsync H2D) + gw_advance_watermark"}
+
+
+def host_cores():
+    """Host cores this process can use: the CPUs it may run on, capped by the cgroup CPU
+    quota (a container's share of a bigger machine; os.cpu_count() reports the machine)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    note = f"sched_getaffinity={n}"
+    quota = None
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]  # cgroup v2
+        if q != "max":
+            quota = int(q) / int(p)
+    except (OSError, ValueError):
+        try:
+            q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+            p = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+            if q > 0:
+                quota = q / p
+        except (OSError, ValueError):
+            pass
+    if quota is not None:
+        note += f", cgroup cpu quota={quota:g}"
+        n = max(1, min(n, int(quota)))
+    return n, note
+
+
 def cpu_baseline(args, keys, ts, vals, wms, nb, agg, size, slide):
     """CPU restatement of Flink's operator (oracle/, 'port') on the host cores: one operator
-    per simulated subtask thread over a bounded prefix of the same stream."""
+    per simulated subtask thread over a bounded prefix of the same stream.  Parallelism =
+    the host CPUs this process may run on (parallelism = nproc)."""
     try:
         from oracle import oracle as O
         O.build()
     except Exception as e:  # noqa: BLE001
         return {"value": None, "unit": "events/s", "cores": 0, "kind": "port", "sample": f"unavailable: {e}"}
-    threads = min(16, os.cpu_count() or 1)
+    threads, cores_note = host_cores()
     cfg = O.make_config(assigner="sliding", size=size, slide=slide, agg=agg, max_parallelism=128)
 
     def run(nbatches, per_batch):
@@ -399,7 +482,7 @@ def cpu_baseline(args, keys, ts, vals, wms, nb, agg, size, slide):
         n, sec, rows = run(nbatches, nb)
         sample = f"first {nbatches} watermark batches ({n} events) of the GPU stream + final watermark"
     return {"value": n / sec, "unit": "events/s", "cores": threads, "kind": "port", "sample": sample,
-            "seconds": sec, "rows": rows}
+            "seconds": sec, "rows": rows, "nproc": os.cpu_count(), "cores_source": cores_note}
 
 
 if __name__ == "__main__":

@@ -1008,6 +1008,8 @@ typedef struct {
     int64_t nb;
     const int64_t *blen, *wm, *key, *ts, *val;
     int64_t rows, checksum;
+    int64_t* pw_rows;  /* optional [nb + 1]: rows fired per watermark (the last: MAX_WATERMARK) */
+    uint64_t* pw_cs;   /* optional [nb + 1]: order-independent checksum of those rows */
     int rc;
 } par_arg;
 
@@ -1036,10 +1038,13 @@ static void* par_main(void* p) {
         if (rc) { a->rc = rc; goto done; }
         int64_t n;
         while ((n = wo_drain(op, bk, bs, be, br, 1024)) > 0) {
+            uint64_t c = 0;
             for (int64_t i = 0; i < n; i++)
-                cs += (uint64_t)bk[i] * 0x9e3779b97f4a7c15ull ^ (uint64_t)bs[i] * 31u ^
-                      (uint64_t)be[i] * 17u ^ (uint64_t)br[i];
+                c += (uint64_t)bk[i] * 0x9e3779b97f4a7c15ull ^ (uint64_t)bs[i] * 31u ^
+                     (uint64_t)be[i] * 17u ^ (uint64_t)br[i];
+            cs += c;
             rows += n;
+            if (a->pw_rows) { a->pw_rows[b] += n; a->pw_cs[b] += c; }
         }
     }
 done:
@@ -1059,7 +1064,7 @@ int64_t wo_run_parallel(const gw_config* cfg, int threads, int64_t nb, const int
     struct timespec t0, t1;
     clock_gettime(CLOCK_MONOTONIC, &t0);
     for (int i = 0; i < threads; i++) {
-        args[i] = (par_arg){cfg, i, threads, nb, blen, wm, key, ts, val, 0, 0, 0};
+        args[i] = (par_arg){cfg, i, threads, nb, blen, wm, key, ts, val, 0, 0, NULL, NULL, 0};
         pthread_create(&th[i], NULL, par_main, &args[i]);
     }
     int64_t rows = 0;
@@ -1076,6 +1081,44 @@ int64_t wo_run_parallel(const gw_config* cfg, int threads, int64_t nb, const int
     if (checksum) *checksum = (int64_t)cs;
     free(th);
     free(args);
+    return rc ? rc : rows;
+}
+
+/* wo_run_parallel with per-watermark results: wm_rows[b] / wm_cs[b] (b = 0..nb, the last
+ * entry for the final MAX_WATERMARK) receive the number of rows each watermark fired over
+ * all subtasks and the sum of their row hashes (the checksum of wo_run_parallel, per
+ * watermark) -- what a GPU run's per-watermark output is compared against at full size. */
+int64_t wo_run_parallel_wm(const gw_config* cfg, int threads, int64_t nb, const int64_t* blen,
+                           const int64_t* wm, const int64_t* key, const int64_t* ts, const int64_t* val,
+                           int64_t* wm_rows, int64_t* wm_cs, double* seconds) {
+    if (threads < 1) threads = 1;
+    pthread_t* th = (pthread_t*)calloc((size_t)threads, sizeof(pthread_t));
+    par_arg* args = (par_arg*)calloc((size_t)threads, sizeof(par_arg));
+    int64_t* pr = (int64_t*)calloc((size_t)threads * (size_t)(nb + 1), sizeof(int64_t));
+    uint64_t* pc = (uint64_t*)calloc((size_t)threads * (size_t)(nb + 1), sizeof(uint64_t));
+    if (!th || !args || !pr || !pc) { free(th); free(args); free(pr); free(pc); return GW_E_OOM; }
+    struct timespec t0, t1;
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    for (int i = 0; i < threads; i++) {
+        args[i] = (par_arg){cfg, i, threads, nb, blen, wm, key, ts, val, 0, 0,
+                            pr + (size_t)i * (size_t)(nb + 1), pc + (size_t)i * (size_t)(nb + 1), 0};
+        pthread_create(&th[i], NULL, par_main, &args[i]);
+    }
+    int64_t rows = 0;
+    int rc = 0;
+    for (int64_t b = 0; b <= nb; b++) { wm_rows[b] = 0; wm_cs[b] = 0; }
+    for (int i = 0; i < threads; i++) {
+        pthread_join(th[i], NULL);
+        rows += args[i].rows;
+        if (args[i].rc) rc = args[i].rc;
+        for (int64_t b = 0; b <= nb; b++) {
+            wm_rows[b] += args[i].pw_rows[b];
+            wm_cs[b] = (int64_t)((uint64_t)wm_cs[b] + args[i].pw_cs[b]);
+        }
+    }
+    clock_gettime(CLOCK_MONOTONIC, &t1);
+    if (seconds) *seconds = (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
+    free(th); free(args); free(pr); free(pc);
     return rc ? rc : rows;
 }
 

@@ -130,6 +130,8 @@ def lib() -> ctypes.CDLL:
                                                  ctypes.POINTER(GwDecodeResult)]),
             ("wo_run_parallel", i64, [ctypes.POINTER(GwConfig), ctypes.c_int, i64, p, p, p, p, p,
                                        P64, ctypes.POINTER(ctypes.c_double)]),
+            ("wo_run_parallel_wm", i64, [ctypes.POINTER(GwConfig), ctypes.c_int, i64, p, p, p, p, p, p, p,
+                                          ctypes.POINTER(ctypes.c_double)]),
         ]:
             f = getattr(L, name)
             f.restype = res
@@ -219,3 +221,32 @@ def run_parallel(cfg: GwConfig, threads: int, batch_len, wm, key, ts, value_bits
     if rows < 0:
         raise OracleError(f"parallel oracle failed: {rows}")
     return rows, cs.value, sec.value
+
+
+def rows_hash_sum(k, s, e, r) -> int:
+    """The oracle's order-independent row checksum (wo_run_parallel): the sum over rows of
+    (key * 0x9e3779b97f4a7c15) ^ (start * 31) ^ (end * 17) ^ result, mod 2^64, as int64."""
+    k, s, e, r = (np.ascontiguousarray(c).view(np.uint64) for c in (k, s, e, r))
+    with np.errstate(over="ignore"):
+        h = (k * np.uint64(0x9E3779B97F4A7C15)) ^ (s * np.uint64(31)) ^ (e * np.uint64(17)) ^ r
+        tot = h.sum(dtype=np.uint64) if h.size else np.uint64(0)
+    return int(np.array(tot, dtype=np.uint64).view(np.int64))
+
+
+def run_parallel_wm(cfg: GwConfig, threads: int, batch_len, wm, key, ts, value_bits):
+    """run_parallel with per-watermark results: (rows[nb + 1], checksum[nb + 1], seconds),
+    the last entry for the final MAX_WATERMARK; checksum as rows_hash_sum."""
+    batch_len = np.ascontiguousarray(batch_len, dtype=np.int64)
+    wm = np.ascontiguousarray(wm, dtype=np.int64)
+    key = np.ascontiguousarray(key, dtype=np.int64)
+    ts = np.ascontiguousarray(ts, dtype=np.int64)
+    vb = None if value_bits is None else np.ascontiguousarray(value_bits).view(np.int64)
+    nb = len(batch_len)
+    rows = np.zeros(nb + 1, np.int64)
+    cs = np.zeros(nb + 1, np.int64)
+    sec = ctypes.c_double(0)
+    rc = lib().wo_run_parallel_wm(ctypes.byref(cfg), threads, nb, _p(batch_len), _p(wm), _p(key), _p(ts), _p(vb),
+                                  _p(rows), _p(cs), ctypes.byref(sec))
+    if rc < 0:
+        raise OracleError(f"parallel oracle failed: {rc}")
+    return rows, cs, sec.value
