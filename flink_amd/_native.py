@@ -36,7 +36,7 @@ FLAG_NO_BUFFER = 32
 
 EXPORTS = [
     "gw_create", "gw_destroy", "gw_last_error", "gw_abi_version", "gw_ingest", "gw_ingest_device",
-    "gw_advance_watermark", "gw_flush", "gw_snapshot", "gw_restore", "gw_end_input", "gw_pending_rows", "gw_drain", "gw_rows_device",
+    "gw_advance_watermark", "gw_flush", "gw_snapshot", "gw_restore", "gw_snapshot_slice", "gw_end_input", "gw_pending_rows", "gw_drain", "gw_rows_device",
     "gw_clear_rows", "gw_late_dropped", "gw_get_stats", "gw_synchronize", "gw_stream",
     "gw_kernel_time_ms", "gw_enable_kernel_timing", "gw_java_long_hash", "gw_murmur_hash",
     "gw_key_group_for_hash", "gw_operator_for_key_group", "gw_default_max_parallelism",
@@ -132,6 +132,7 @@ def lib() -> ctypes.CDLL:
         "gw_flush": (c_int, [p]),
         "gw_snapshot": (c_int, [p, i32, i32, p, i64, P64]),
         "gw_restore": (c_int, [p, p, i64]),
+        "gw_snapshot_slice": (c_int, [p, i64, i32, p, i64, P64]),
         "gw_end_input": (c_int, [p, P64]),
         "gw_pending_rows": (c_int, [p, P64]),
         "gw_drain": (c_int, [p, p, p, p, p, i64, P64]),
@@ -170,3 +171,13 @@ def check(rc: int, handle=None):
         msg = lib().gw_last_error(handle)
         raise GpuWinError(rc, msg.decode() if msg else "")
     return rc
+
+
+def snapshot_slice(blob: bytes, kg: int) -> bytes:
+    """The part of a gw_snapshot blob that belongs to key group kg, as a blob of its own
+    (gw_snapshot_slice: what GpuWindowOperator writes per key group)."""
+    n = ctypes.c_int64(0)
+    check(lib().gw_snapshot_slice(blob, len(blob), kg, None, 0, ctypes.byref(n)))
+    out = ctypes.create_string_buffer(n.value)
+    check(lib().gw_snapshot_slice(blob, len(blob), kg, out, n.value, ctypes.byref(n)))
+    return out.raw[:n.value]

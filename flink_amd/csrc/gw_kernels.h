@@ -285,6 +285,10 @@ hipError_t launch_count_live(const PaneTable& t, unsigned long long* out, hipStr
 hipError_t launch_key_groups(int64_t n, const int64_t* key, const int32_t* key_hash, int32_t max_p,
                              int32_t p, int32_t* kg, int32_t* owner, hipStream_t s);
 int64_t partition_scratch_bytes(int64_t n, int32_t p);
+// out[0] |= 1: a key_hash differs from Long.hashCode(key); out[1] = min(key group + 1) outside
+// [kg_lo, kg_hi] when check_range (out[1] must start at ~0)
+hipError_t launch_check_keys(int64_t n, const int64_t* key, const int32_t* key_hash, int32_t max_p, int32_t kg_lo,
+                             int32_t kg_hi, int check_range, unsigned long long* out, hipStream_t s);
 hipError_t launch_partition(int64_t n, const int64_t* key, const int32_t* key_hash, const int64_t* ts,
                             const int64_t* val, int32_t max_p, int32_t p, int64_t* key_out,
                             int64_t* ts_out, int64_t* val_out, int64_t* counts, void* scratch,

@@ -117,6 +117,43 @@ __global__ void __launch_bounds__(256) k_part_scatter(int64_t n, const int64_t* 
     }
 }
 
+// Ingest-side key checks (gw_ingest* with a key_hash column, or GW_FLAG_CHECK_KEY_GROUPS):
+//   out[0] |= 1 when a key_hash differs from Long.hashCode(key): the window state groups keys
+//          by Long.hashCode (snapshots, rescaling), so such a handle refuses to snapshot;
+//   out[1] = min over records of (key group + 1) outside [kg_lo, kg_hi] (0: none), which
+//          fails the batch like StateTable.getMapForKeyGroup (RR/state/heap/StateTable.java:
+//          325-333, KeyGroupRangeOffsets.newIllegalKeyGroupException).
+__global__ void __launch_bounds__(256) k_check_keys(int64_t n, const int64_t* key, const int32_t* key_hash,
+                                                    int32_t max_p, int32_t kg_lo, int32_t kg_hi, int check_range,
+                                                    unsigned long long* out) {
+    unsigned long long foreign = 0, bad = ~0ull;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int32_t lh = java_long_hash(key[i]);
+        const int32_t h = key_hash ? key_hash[i] : lh;
+        foreign |= (unsigned long long)(h != lh);
+        if (check_range) {
+            const int32_t g = key_group_for_hash(h, max_p);
+            if (g < kg_lo || g > kg_hi) bad = min(bad, (unsigned long long)g + 1);
+        }
+    }
+    foreign = wave_ior(foreign);
+    for (int o = 32; o > 0; o >>= 1) bad = min(bad, (unsigned long long)__shfl_xor(bad, o));
+    if (__lane_id() == 0) {
+        if (foreign) atomicOr(&out[0], 1ull);
+        if (bad != ~0ull) atomicMin(&out[1], bad);
+    }
+}
+
+hipError_t launch_check_keys(int64_t n, const int64_t* key, const int32_t* key_hash, int32_t max_p, int32_t kg_lo,
+                             int32_t kg_hi, int check_range, unsigned long long* out, hipStream_t s) {
+    int64_t g = (n + 255) / 256;
+    if (g < 1) g = 1;
+    if (g > 2048) g = 2048;
+    hipLaunchKernelGGL(k_check_keys, dim3((unsigned)g), dim3(256), 0, s, n, key, key_hash, max_p, kg_lo, kg_hi,
+                       check_range, out);
+    return hipGetLastError();
+}
+
 hipError_t launch_key_groups(int64_t n, const int64_t* key, const int32_t* key_hash, int32_t max_p,
                              int32_t p, int32_t* kg, int32_t* owner, hipStream_t s) {
     int64_t g = (n + 255) / 256;

@@ -29,7 +29,8 @@ namespace {
 
 thread_local std::string g_create_error;
 
-constexpr int64_t kMaxIngest = (int64_t)1 << 30;  // records per region-path batch / buffer
+constexpr int64_t kMaxIngest = (int64_t)1 << 30;
+constexpr uint32_t kSnapMaxVersion = 3;  // gw_handle::SnapHeader versions  // records per region-path batch / buffer
 
 // Host-time profile of the ingest path (GW_HOST_PROFILE=1: printed by gw_destroy).
 struct HostProf {
@@ -78,6 +79,23 @@ UDiv64 make_udiv(uint64_t d) {
     r.shift = l - 1;
     r.mode = 0;
     return r;
+}
+
+// Host copy into pinned staging, split over threads for large columns (one thread's memcpy
+// is well below the PCIe rate the H2D copy behind it reaches).
+void par_memcpy(void* dst, const void* src, size_t bytes) {
+    constexpr size_t kPer = (size_t)32 << 20;
+    const int nt = (int)std::min<size_t>(8, bytes / kPer);
+    if (nt <= 1) { memcpy(dst, src, bytes); return; }
+    std::vector<std::thread> th;
+    const size_t part = (bytes / nt + 63) & ~(size_t)63;
+    for (int i = 0; i < nt; ++i) {
+        const size_t lo = (size_t)i * part;
+        if (lo >= bytes) break;
+        const size_t len = std::min(part, bytes - lo);
+        th.emplace_back([=] { memcpy((char*)dst + lo, (const char*)src + lo, len); });
+    }
+    for (auto& t : th) t.join();
 }
 
 struct KernelTimer {
@@ -193,7 +211,11 @@ struct gw_handle {
     int cur = 0;
 
     // host-ingest staging
-    int64_t* h_stage = nullptr;  // pinned: key | ts | val
+    // Two pinned slots used in turn: a slot is refilled only after the H2D copy that read it
+    // has completed (ev_stage), so the host fills one slot while the other is in flight.
+    int64_t* h_stage[2] = {nullptr, nullptr};  // pinned: key | ts | val | hash (int32)
+    hipEvent_t ev_stage[2] = {nullptr, nullptr};
+    int stage_slot = 0;
     int64_t* d_stage = nullptr;  // device: key | ts | val
     int32_t* d_hash_stage = nullptr;
     int64_t stage_cap = 0;
@@ -217,6 +239,9 @@ struct gw_handle {
     HostProf hp;
 
     SessionState* sess = nullptr;
+    // key checks (gw_ingest* with key_hash, GW_FLAG_CHECK_KEY_GROUPS): device words, see k_check_keys
+    unsigned long long* d_chk = nullptr;
+    bool foreign_hash = false;  // a key_hash differed from Long.hashCode(key): no snapshots
     int ingest_unroll = 2;  // records per thread per iteration of k_ingest (GW_INGEST_UNROLL)
     int64_t region_min_batch = 1 << 16;  // smallest batch for the region path (GW_REGION_MIN_BATCH)
 
@@ -452,11 +477,27 @@ struct gw_handle {
         o_cap = nc;
         return GW_OK;
     }
+    void free_stage() {
+        for (int i = 0; i < 2; ++i) {
+            if (h_stage[i]) hipHostFree(h_stage[i]);
+            if (ev_stage[i]) hipEventDestroy(ev_stage[i]);
+            h_stage[i] = nullptr;
+            ev_stage[i] = nullptr;
+        }
+        if (d_stage) hipFree(d_stage);
+        if (d_hash_stage) hipFree(d_hash_stage);
+        d_stage = nullptr;
+        d_hash_stage = nullptr;
+        stage_cap = 0;
+    }
     int ensure_stage(int64_t n) {
         if (n <= stage_cap) return GW_OK;
-        if (h_stage) { hipHostFree(h_stage); hipFree(d_stage); hipFree(d_hash_stage); }
-        h_stage = nullptr;
-        HIPCHECK(hipHostMalloc((void**)&h_stage, (size_t)n * 24, hipHostMallocDefault));
+        HIPCHECK(hipStreamSynchronize(stream));  // no copy still reads the old buffers
+        free_stage();
+        for (int i = 0; i < 2; ++i) {
+            HIPCHECK(hipHostMalloc((void**)&h_stage[i], (size_t)n * 28, hipHostMallocDefault));
+            HIPCHECK(hipEventCreateWithFlags(&ev_stage[i], hipEventDisableTiming));
+        }
         HIPCHECK(hipMalloc((void**)&d_stage, (size_t)n * 24));
         HIPCHECK(hipMalloc((void**)&d_hash_stage, (size_t)n * 4));
         stage_cap = n;
@@ -999,6 +1040,33 @@ struct gw_handle {
         return GW_OK;
     }
 
+    // ---------------------------------------------------------------- key checks
+    // Synchronous: only callers that pass a key_hash column or set GW_FLAG_CHECK_KEY_GROUPS
+    // pay for it (the Java operator passes no hash for Long keys).
+    int check_keys(int64_t nrec, const int64_t* d_key, const int32_t* d_hash) {
+        const bool range = (cfg.flags & GW_FLAG_CHECK_KEY_GROUPS) != 0;
+        if (nrec == 0 || (!d_hash && !range)) return GW_OK;
+        if (!d_chk) HIPCHECK(hipMalloc((void**)&d_chk, 16));
+        const unsigned long long init[2] = {0ull, ~0ull};
+        HIPCHECK(hipMemcpyAsync(d_chk, init, 16, hipMemcpyHostToDevice, stream));
+        const int32_t mp = cfg.max_parallelism, p = cfg.parallelism, ix = cfg.operator_index;
+        const int32_t lo = (ix * mp + p - 1) / p, hi = ((ix + 1) * mp - 1) / p;  // KeyGroupRangeAssignment :93-106
+        HIPCHECK(launch_check_keys(nrec, d_key, d_hash, mp, lo, hi, range ? 1 : 0, d_chk, stream));
+        unsigned long long out[2];
+        HIPCHECK(hipMemcpyAsync(out, d_chk, 16, hipMemcpyDeviceToHost, stream));
+        HIPCHECK(hipStreamSynchronize(stream));
+        if (out[0]) foreign_hash = true;
+        if (out[1] != ~0ull) {
+            failed = true;
+            return fail(GW_E_INVALID,
+                        "Key group %d is not in KeyGroupRange{startKeyGroup=%d, endKeyGroup=%d}. Unless you're "
+                        "directly using low level state access APIs, this is most likely caused by "
+                        "non-deterministic shuffle key (hashCode and equals implementation).",
+                        (int)(out[1] - 1), lo, hi);
+        }
+        return GW_OK;
+    }
+
     // ---------------------------------------------------------------- snapshot
     // Blob (little-endian): SnapHeader, int64 kg_offsets[kg_hi - kg_lo + 2] (first entry
     // of each key group), then SnapEntry entries sorted by key group.
@@ -1410,7 +1478,7 @@ int gw_destroy(gw_handle* h) {
     for (int c = 0; c < 5; ++c)
         if (h->rf[c]) hipFree(h->rf[c]);
     if (h->rf_sort) hipFree(h->rf_sort);
-    if (h->h_stage) { hipHostFree(h->h_stage); hipFree(h->d_stage); hipFree(h->d_hash_stage); }
+    h->free_stage();
     h->free_region();
     if (h->rbeg) hipFree(h->rbeg);
     if (h->d_st) hipFree(h->d_st);
@@ -1421,6 +1489,7 @@ int gw_destroy(gw_handle* h) {
     h->t_ingest.destroy();
     h->t_fire.destroy();
     h->t_apply.destroy();
+    if (h->d_chk) hipFree(h->d_chk);
     if (h->nb_scratch) hipFree(h->nb_scratch);
     if (h->nb_cols) hipFree(h->nb_cols);
     if (h->nb_wm) hipFree(h->nb_wm);
@@ -1459,21 +1528,32 @@ int gw_ingest(gw_handle* h, int64_t n, const int64_t* key, const int32_t* key_ha
     if (h->failed) return h->fail(GW_E_STATE, "operator failed earlier: %s", h->err.c_str());
     if (n < 0 || (n > 0 && (!key || !ts))) return h->fail(GW_E_INVALID, "null key/ts column");
     if (n > 0 && !value && h->cfg.agg != GW_COUNT) return h->fail(GW_E_INVALID, "value column required");
-    (void)key_hash;
     hipSetDevice(h->cfg.device);
     const int64_t chunk = h->cfg.max_batch;
     for (int64_t off = 0; off < n; off += chunk) {
         const int64_t c = std::min(chunk, n - off);
         int rc = h->ensure_stage(c);
         if (rc) return rc;
-        memcpy(h->h_stage, key + off, (size_t)c * 8);
-        memcpy(h->h_stage + c, ts + off, (size_t)c * 8);
-        if (value) memcpy(h->h_stage + 2 * c, (const int64_t*)value + off, (size_t)c * 8);
+        const int slot = h->stage_slot;
+        h->stage_slot ^= 1;
+        int64_t* hs = h->h_stage[slot];
         {
-            hipError_t e = hipMemcpyAsync(h->d_stage, h->h_stage, (size_t)c * (value ? 24 : 16),
-                                          hipMemcpyHostToDevice, h->stream);
+            hipError_t e = hipEventSynchronize(h->ev_stage[slot]);  // the slot's previous H2D is done
+            if (e != hipSuccess) return h->fail(GW_E_DEVICE, "staging: %s", hipGetErrorString(e));
+        }
+        par_memcpy(hs, key + off, (size_t)c * 8);
+        par_memcpy(hs + c, ts + off, (size_t)c * 8);
+        if (value) par_memcpy(hs + 2 * c, (const int64_t*)value + off, (size_t)c * 8);
+        if (key_hash) memcpy(hs + 3 * c, key_hash + off, (size_t)c * 4);
+        {
+            hipError_t e = hipMemcpyAsync(h->d_stage, hs, (size_t)c * (value ? 24 : 16), hipMemcpyHostToDevice,
+                                          h->stream);
+            if (e == hipSuccess && key_hash)
+                e = hipMemcpyAsync(h->d_hash_stage, hs + 3 * c, (size_t)c * 4, hipMemcpyHostToDevice, h->stream);
+            if (e == hipSuccess) e = hipEventRecord(h->ev_stage[slot], h->stream);
             if (e != hipSuccess) return h->fail(GW_E_DEVICE, "H2D: %s", hipGetErrorString(e));
         }
+        if ((rc = h->check_keys(c, h->d_stage, key_hash ? h->d_hash_stage : nullptr))) return rc;
         rc = ingest_device_impl(h, c, h->d_stage, h->d_stage + c, value ? h->d_stage + 2 * c : nullptr);
         if (rc) return rc;
     }
@@ -1487,7 +1567,6 @@ int gw_ingest_device(gw_handle* h, int64_t n, const int64_t* d_key, const int32_
     if (h->failed) return h->fail(GW_E_STATE, "operator failed earlier: %s", h->err.c_str());
     if (n < 0 || (n > 0 && (!d_key || !d_ts))) return h->fail(GW_E_INVALID, "null key/ts column");
     if (n > 0 && !d_value && h->cfg.agg != GW_COUNT) return h->fail(GW_E_INVALID, "value column required");
-    (void)d_key_hash;
     hipSetDevice(h->cfg.device);
     // The producer stream (NULL = the default stream) wrote the columns; the handle's
     // non-blocking stream reads them.  Order both ways: the reads after the writes, and
@@ -1501,7 +1580,8 @@ int gw_ingest_device(gw_handle* h, int64_t n, const int64_t* d_key, const int32_
     }
     if (n == 0) return GW_OK;
     h->hp.lap(5);
-    int rc = ingest_device_impl(h, n, d_key, d_ts, (const int64_t*)d_value);
+    int rc = h->check_keys(n, d_key, d_key_hash);
+    if (rc == GW_OK) rc = ingest_device_impl(h, n, d_key, d_ts, (const int64_t*)d_value);
     if (foreign) {
         hipEventRecord(h->ev_out, h->stream);
         hipStreamWaitEvent(ps, h->ev_out, 0);
@@ -1761,6 +1841,9 @@ int gw_snapshot(gw_handle* h, int32_t kg_lo, int32_t kg_hi, void* buf, int64_t c
     if (h->failed) return h->fail(GW_E_STATE, "operator failed earlier: %s", h->err.c_str());
     if (h->cfg.allowed_lateness > 0 && h->cfg.assigner != GW_SESSION)
         return h->fail(GW_E_UNSUPPORTED, "snapshot with allowed lateness > 0 is not yet supported for time windows");
+    if (h->foreign_hash)
+        return h->fail(GW_E_UNSUPPORTED, "snapshot of a handle that ingested a key_hash different from "
+                                         "Long.hashCode(key): the state is grouped by Long.hashCode");
     hipSetDevice(h->cfg.device);
     if (h->session) return h->snapshot_sessions(kg_lo, kg_hi, buf, cap, len);
     return h->snapshot(kg_lo, kg_hi, buf, cap, len);
@@ -1774,6 +1857,50 @@ int gw_restore(gw_handle* h, const void* buf, int64_t len) {
     hipSetDevice(h->cfg.device);
     if (h->session) return h->restore_sessions(buf, len);
     return h->restore(buf, len);
+}
+
+// The blob layout is gw_handle::SnapHeader (96 bytes: kg_lo at 60, kg_hi at 64, reserved at
+// 68, entries at 88), kg_offsets[kg_hi - kg_lo + 2], then the entries; an entry is 32 bytes in
+// version 1 and `reserved` int64 words in every later version.
+int gw_snapshot_slice(const void* blob, int64_t len, int32_t kg, void* out, int64_t cap, int64_t* out_len) {
+    typedef gw_handle::SnapHeader H;
+    static_assert(sizeof(H) == 96, "snapshot header layout");
+    if (!blob || !out_len || len < (int64_t)sizeof(H)) { g_create_error = "snapshot blob too short"; return GW_E_INVALID; }
+    H hd;
+    memcpy(&hd, blob, sizeof hd);
+    if (memcmp(hd.magic, "GWS1", 4) != 0 || hd.version < 1 || hd.version > kSnapMaxVersion) {
+        g_create_error = "not a gpuwin snapshot";
+        return GW_E_INVALID;
+    }
+    const int64_t ew = hd.version == 1 ? 32 : (int64_t)hd.reserved * 8;
+    const int64_t nk = (int64_t)hd.kg_hi - hd.kg_lo + 1;
+    if (ew <= 0 || nk <= 0 || hd.entries < 0 || len < (int64_t)sizeof hd + (nk + 1) * 8 + hd.entries * ew) {
+        g_create_error = "truncated snapshot blob";
+        return GW_E_INVALID;
+    }
+    if (kg < hd.kg_lo || kg > hd.kg_hi) {
+        g_create_error = "key group outside the blob's key-group range";
+        return GW_E_INVALID;
+    }
+    const char* b = (const char*)blob;
+    int64_t o0, o1;
+    memcpy(&o0, b + sizeof hd + (kg - hd.kg_lo) * 8, 8);
+    memcpy(&o1, b + sizeof hd + (kg - hd.kg_lo + 1) * 8, 8);
+    if (o0 < 0 || o1 < o0 || o1 > hd.entries) { g_create_error = "corrupt snapshot offsets"; return GW_E_INVALID; }
+    const int64_t n = o1 - o0;
+    const int64_t need = (int64_t)sizeof hd + 16 + n * ew;
+    *out_len = need;
+    if (!out) return GW_OK;
+    if (cap < need) { g_create_error = "slice buffer too small"; return GW_E_OUTPUT_FULL; }
+    H oh = hd;
+    oh.kg_lo = oh.kg_hi = kg;
+    oh.entries = n;
+    char* o = (char*)out;
+    memcpy(o, &oh, sizeof oh);
+    const int64_t offs[2] = {0, n};
+    memcpy(o + sizeof oh, offs, 16);
+    if (n) memcpy(o + sizeof oh + 16, b + sizeof hd + (nk + 1) * 8 + o0 * ew, (size_t)(n * ew));
+    return GW_OK;
 }
 
 int gw_end_input(gw_handle* h, int64_t* rows_fired) { return gw_advance_watermark(h, INT64_MAX, rows_fired); }

@@ -198,6 +198,13 @@ int  gw_snapshot(gw_handle* h, int32_t kg_lo, int32_t kg_hi, void* buf, int64_t 
  * of the state: like Flink after a restore it starts at Long.MIN_VALUE. */
 int  gw_restore(gw_handle* h, const void* buf, int64_t len);
 
+/* The part of a gw_snapshot blob that belongs to key group kg, as a blob of its own (what
+ * GpuWindowOperator writes per key group into the raw keyed state stream, like the heap
+ * backend's per-key-group write, HeapSnapshotStrategy.java:97-154).  Pure host code; any
+ * blob version.  Two calls as gw_snapshot: out == NULL returns the size in *out_len.
+ * GW_E_INVALID for a corrupt blob or kg outside its key-group range (gw_last_error(NULL)). */
+int  gw_snapshot_slice(const void* blob, int64_t len, int32_t kg, void* out, int64_t cap, int64_t* out_len);
+
 /* ---- network-buffer ingest ----------------------------- */
 /* Layout of the record value: a Flink Tuple of fixed-width fields as TupleSerializer
  * writes them (fields in order, no null markers; flink-core/.../api/java/typeutils/

@@ -7,13 +7,28 @@
  * (WindowedStream.java:233-240, DataStream.java:815-821).
  *
  * Records between two watermarks are appended to off-heap columns; processWatermark hands
- * the batch to the GPU, advances event time, and emits the fired (key, window, result) rows
- * BEFORE forwarding the watermark, as AbstractStreamOperator.processWatermark does
- * (AbstractStreamOperator.java:690-703).
+ * the batch to the GPU, advances event time, and emits the fired rows BEFORE forwarding the
+ * watermark, as AbstractStreamOperator.processWatermark does (AbstractStreamOperator.java:
+ * 690-703).  Count windows fire on the element (CountTrigger.onElement), so their rows are
+ * emitted right after each batch is handed over.
+ *
+ * Output (OutputMode), with the record timestamp window.maxTimestamp() = end - 1
+ * (WindowOperator.emitWindowContents :575-580):
+ *   POSITIONAL     WindowedStream.sum/min/max(1) on Tuple2<Long, X>: the reduced Tuple2 (key,
+ *                  result) -- SumAggregator / ComparableAggregator keep the first element's
+ *                  other field, here the key (SumAggregator.java:66-76, ComparableAggregator.
+ *                  java:83-104).  Wider tuples carry fields the GPU does not hold: rejected at
+ *                  construction (use aggregate(...) instead).
+ *   AGGREGATE      WindowedStream.aggregate(AggregateFunction): getResult(acc) alone (Long for
+ *                  count, Double for avg), PassThroughWindowFunction.
+ *   KEYED_WINDOW   Tuple4 (key, window start, window end, result), what a ProcessWindowFunction
+ *                  emitting (key, window, result) produces.
  */
 package org.apache.flink.streaming.runtime.operators.windowing.gpu;
 
+import org.apache.flink.api.common.externalresource.ExternalResourceInfo;
 import org.apache.flink.api.java.functions.KeySelector;
+import org.apache.flink.api.java.tuple.Tuple2;
 import org.apache.flink.api.java.tuple.Tuple4;
 import org.apache.flink.runtime.state.KeyGroupRange;
 import org.apache.flink.runtime.state.KeyGroupStatePartitionStreamProvider;
@@ -37,14 +52,18 @@ import java.util.function.ToDoubleFunction;
 import java.util.function.ToLongFunction;
 
 public class GpuWindowOperator<IN>
-        extends AbstractStreamOperator<Tuple4<Long, Long, Long, Object>>
-        implements OneInputStreamOperator<IN, Tuple4<Long, Long, Long, Object>>, BoundedOneInput,
-                KeyContextHandler {
+        extends AbstractStreamOperator<Object>
+        implements OneInputStreamOperator<IN, Object>, BoundedOneInput, KeyContextHandler {
 
     static { System.loadLibrary("gpuwin_jni"); }
 
+    /** What one fired (key, window, result) row becomes (see the class comment). */
+    public enum OutputMode { POSITIONAL, AGGREGATE, KEYED_WINDOW }
+
     // gw_assigner / gw_trigger / gw_agg codes of include/gpuwin.h
+    private static final int GW_COUNT_TUMBLING = 3, GW_COUNT_SLIDING = 4;
     private final int assigner, trigger, agg;
+    private final OutputMode mode;
     private final long size, slide, offset, gap, lateness;
     private final KeySelector<IN, Long> keySelector;
     private final ToLongFunction<IN> longValue;       // for integer aggregates
@@ -52,17 +71,24 @@ public class GpuWindowOperator<IN>
     private final int batchCapacity;
 
     private transient long handle;
-    private transient ByteBuffer keys, hashes, ts, values, oKey, oStart, oEnd, oRes;
+    private transient ByteBuffer keys, ts, values, oKey, oStart, oEnd, oRes;
     private transient int n;
     private transient List<byte[]> restored;  // per-key-group blobs read in initializeState
 
+    /** inputArity: fields of the input Tuple (POSITIONAL needs 2: the Long key and the field). */
     public GpuWindowOperator(int assigner, long size, long slide, long offset, long gap, long lateness,
                              int trigger, int agg, KeySelector<IN, Long> keySelector,
-                             ToLongFunction<IN> longValue, ToDoubleFunction<IN> doubleValue, int batchCapacity) {
+                             ToLongFunction<IN> longValue, ToDoubleFunction<IN> doubleValue, int batchCapacity,
+                             OutputMode mode, int inputArity) {
+        if (mode == OutputMode.POSITIONAL && inputArity != 2) {
+            throw new IllegalArgumentException(
+                    "positional sum/min/max on the GPU keep only the key and the aggregated field: "
+                            + "the input must be a Tuple2<Long, X> (got arity " + inputArity + ")");
+        }
         this.assigner = assigner; this.size = size; this.slide = slide; this.offset = offset;
         this.gap = gap; this.lateness = lateness; this.trigger = trigger; this.agg = agg;
         this.keySelector = keySelector; this.longValue = longValue; this.doubleValue = doubleValue;
-        this.batchCapacity = batchCapacity;
+        this.batchCapacity = batchCapacity; this.mode = mode;
     }
 
     @Override
@@ -74,15 +100,24 @@ public class GpuWindowOperator<IN>
         int subtask = getRuntimeContext().getTaskInfo().getIndexOfThisSubtask();
         int parallelism = getRuntimeContext().getTaskInfo().getNumberOfParallelSubtasks();
         int maxP = getRuntimeContext().getTaskInfo().getMaxNumberOfParallelSubtasks();
-        int device = 0; // RuntimeContext.getExternalResourceInfos("gpu") with an amd-smi discovery script
+        int device = gpuIndex();
         handle = nativeCreate(assigner, trigger, size, slide, offset, gap, lateness, agg, maxP, parallelism,
                               subtask, device, 1L << 24, batchCapacity);
-        keys = direct(8); hashes = direct(4); ts = direct(8); values = direct(8);
+        keys = direct(8); ts = direct(8); values = direct(8);
         oKey = direct(8); oStart = direct(8); oEnd = direct(8); oRes = direct(8);
         if (restored != null) {  // initializeState runs before open (StreamOperator.java:139)
             for (byte[] blob : restored) nativeRestore(handle, blob);
             restored = null;
         }
+    }
+
+    /** The GPU this subtask was given: the "index" property of the first "gpu" external
+     *  resource (GPUDriver with integration/gpu-discovery/amd-gpu-discovery.sh), else 0. */
+    private int gpuIndex() {
+        for (ExternalResourceInfo info : getRuntimeContext().getExternalResourceInfos("gpu")) {
+            return info.getProperty("index").map(Integer::parseInt).orElse(0);
+        }
+        return 0;
     }
 
     // ---- checkpointing: raw keyed state, one blob per key group -------------------------
@@ -131,8 +166,7 @@ public class GpuWindowOperator<IN>
     public void processElement(StreamRecord<IN> element) throws Exception {
         IN v = element.getValue();
         Long k = keySelector.getKey(v);
-        keys.putLong(n * 8, k);
-        hashes.putInt(n * 4, k.hashCode());                 // key group of the reference
+        keys.putLong(n * 8, k);   // key group = murmur(Long.hashCode(k)), computed on the GPU
         ts.putLong(n * 8, element.getTimestamp());
         if (doubleValue != null) values.putDouble(n * 8, doubleValue.applyAsDouble(v));
         else if (longValue != null) values.putLong(n * 8, longValue.applyAsLong(v));
@@ -140,24 +174,38 @@ public class GpuWindowOperator<IN>
     }
 
     private void flush() {
-        if (n > 0) nativeIngest(handle, n, keys, hashes, ts, values);
+        // the key hash column is null: keys are Longs, whose hashCode the GPU computes
+        if (n > 0) nativeIngest(handle, n, keys, null, ts, values);
         n = 0;
+        // CountTrigger fires on the element: count-window rows exist right after the batch
+        if (assigner == GW_COUNT_TUMBLING || assigner == GW_COUNT_SLIDING) emitRows();
+    }
+
+    private void emitRows() {
+        int got;
+        while ((got = nativeDrain(handle, oKey, oStart, oEnd, oRes, batchCapacity)) > 0) {
+            for (int i = 0; i < got; i++) {
+                long key = oKey.getLong(i * 8), end = oEnd.getLong(i * 8);
+                Object res = agg == 2 || agg >= 5 && agg <= 8 ? (Object) oRes.getDouble(i * 8) : oRes.getLong(i * 8);
+                Object row;
+                switch (mode) {
+                    case POSITIONAL: row = Tuple2.of(key, res); break;
+                    case AGGREGATE: row = res; break;
+                    default: row = Tuple4.of(key, oStart.getLong(i * 8), end, res);
+                }
+                // count windows: GlobalWindow.maxTimestamp() = Long.MAX_VALUE
+                long tsOut = assigner == GW_COUNT_TUMBLING || assigner == GW_COUNT_SLIDING ? Long.MAX_VALUE : end - 1;
+                output.collect(new StreamRecord<>(row, tsOut));
+            }
+            if (got < batchCapacity) break;
+        }
     }
 
     @Override
     public void processWatermark(Watermark mark) throws Exception {
         flush();
         nativeAdvanceWatermark(handle, mark.getTimestamp());
-        int got;
-        while ((got = nativeDrain(handle, oKey, oStart, oEnd, oRes, batchCapacity)) > 0) {
-            for (int i = 0; i < got; i++) {
-                long end = oEnd.getLong(i * 8);
-                Object res = agg == 2 || agg >= 5 && agg <= 8 ? (Object) oRes.getDouble(i * 8) : oRes.getLong(i * 8);
-                output.collect(new StreamRecord<>(
-                        Tuple4.of(oKey.getLong(i * 8), oStart.getLong(i * 8), end, res), end - 1));
-            }
-            if (got < batchCapacity) break;
-        }
+        emitRows();
         super.processWatermark(mark);  // forward after the fired rows
     }
 

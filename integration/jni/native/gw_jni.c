@@ -114,34 +114,26 @@ JNIEXPORT jbyteArray JNICALL CLS(nativeSnapshot)(JNIEnv* env, jclass c, jlong h,
     return out;
 }
 
-/* The part of a [lo, hi] snapshot blob that belongs to key group kg, as a blob of its
- * own (written per key group into the raw keyed state stream).  Layout: include/gpuwin.h
- * gw_snapshot; header = 4 + 4 + 2*4 + 5*8 + 4*4 + 2*8 + 8 = 96 bytes, kg_lo at 60. */
+/* The part of a [lo, hi] snapshot blob that belongs to key group kg, as a blob of its own
+ * (written per key group into the raw keyed state stream).  gw_snapshot_slice reads the
+ * entry size from the blob header, so pane, session and count-window blobs all slice. */
 JNIEXPORT jbyteArray JNICALL CLS(nativeSliceKeyGroup)(JNIEnv* env, jclass c, jbyteArray blob, jint kg) {
-    const int HDR = 96, OFF_KGLO = 60, OFF_KGHI = 64, OFF_N = 88;
     jsize len = (*env)->GetArrayLength(env, blob);
     jbyte* b = (*env)->GetByteArrayElements(env, blob, 0);
-    int32_t lo, hi;
-    memcpy(&lo, b + OFF_KGLO, 4);
-    memcpy(&hi, b + OFF_KGHI, 4);
-    int64_t o0, o1;
-    memcpy(&o0, b + HDR + (int64_t)(kg - lo) * 8, 8);
-    memcpy(&o1, b + HDR + (int64_t)(kg - lo + 1) * 8, 8);
-    const int64_t n = o1 - o0, ent0 = HDR + (int64_t)(hi - lo + 2) * 8;
-    const jsize out_len = (jsize)(HDR + 16 + n * 32);
-    jbyteArray out = (*env)->NewByteArray(env, out_len);
-    jbyte* o = (*env)->GetByteArrayElements(env, out, 0);
-    memcpy(o, b, HDR);
-    memcpy(o + OFF_KGLO, &kg, 4);
-    memcpy(o + OFF_KGHI, &kg, 4);
-    memcpy(o + OFF_N, &n, 8);
-    const int64_t zero = 0;
-    memcpy(o + HDR, &zero, 8);
-    memcpy(o + HDR + 8, &n, 8);
-    if (n) memcpy(o + HDR + 16, b + ent0 + o0 * 32, (size_t)n * 32);
-    (*env)->ReleaseByteArrayElements(env, out, o, 0);
+    int64_t out_len = 0;
+    int rc = gw_snapshot_slice(b, len, kg, 0, 0, &out_len);
+    jbyteArray out = 0;
+    if (rc == GW_OK) {
+        void* tmp = malloc((size_t)out_len);
+        rc = tmp ? gw_snapshot_slice(b, len, kg, tmp, out_len, &out_len) : GW_E_OOM;
+        if (rc == GW_OK) {
+            out = (*env)->NewByteArray(env, (jsize)out_len);
+            (*env)->SetByteArrayRegion(env, out, 0, (jsize)out_len, (const jbyte*)tmp);
+        }
+        free(tmp);
+    }
     (*env)->ReleaseByteArrayElements(env, blob, b, JNI_ABORT);
-    (void)len;
+    fail(env, 0, rc);
     return out;
 }
 

@@ -291,3 +291,66 @@ def test_session_snapshot_with_lateness(oracle_lib, agg, trigger):
     o, olate = run_oracle(oracle_lib, kw, keys, ts, vals, batches)
     assert olate > 0
     assert compare(outs, o, agg in ("sum_f64", "avg_f64")) == []
+
+
+# ------------------------------------------------------ per-key-group blobs (JNI slicing)
+@pytest.mark.parametrize("kw", [
+    dict(assigner="sliding", size=1000, slide=250, agg="sum_i64"),
+    dict(assigner="session", gap=300, agg="avg_f64"),
+    dict(assigner="count_sliding", size=7, slide=3, agg="max_i64"),
+], ids=["pane", "session", "count"])
+def test_restore_from_per_key_group_slices(oracle_lib, kw):
+    """GpuWindowOperator.snapshotState writes one blob per key group (gw_snapshot_slice,
+    what nativeSliceKeyGroup calls); restoring all 128 slices equals restoring the blob."""
+    agg = kw["agg"]
+    keys, ts, vals, batches = random_stream(seed=29, n=20000, num_keys=700, n_batches=10, agg=agg)
+    op = gpu_operator(kw)
+    outs = []
+    for i, (lo, hi, wm) in enumerate(batches):
+        op.process_batch(keys[lo:hi], ts[lo:hi], vals[lo:hi])
+        if i == 4:
+            if kw["assigner"].startswith("count"):
+                _rows(op, outs)  # count windows fire on the element
+            blob = op.snapshot_state()
+            op.close()
+            slices = [N.snapshot_slice(blob, kg) for kg in range(128)]
+            assert sum(len(s) - 112 for s in slices) == len(blob) - 96 - 129 * 8
+            op = gpu_operator(kw)
+            op.initialize_state(slices)
+        op.advance_watermark(wm)
+        _rows(op, outs)
+        if kw["assigner"].startswith("count") and i == 4:
+            outs[-2:] = [tuple(np.concatenate([a, b]) for a, b in zip(outs[-2], outs[-1]))]
+    op.advance_watermark(W.LONG_MAX)
+    _rows(op, outs)
+    op.close()
+    o, _ = run_oracle(oracle_lib, kw, keys, ts, vals, batches)
+    assert compare(outs, o, agg == "avg_f64") == []
+
+
+def test_foreign_key_hash_refuses_snapshot_and_key_group_check():
+    """A key_hash column that differs from Long.hashCode(key) marks the handle (its state is
+    grouped by Long.hashCode, so it cannot snapshot); GW_FLAG_CHECK_KEY_GROUPS fails a batch
+    holding a key of another subtask (StateTable.getMapForKeyGroup, StateTable.java:325-333)."""
+    keys = np.arange(100, dtype=np.int64)
+    ts = np.arange(100, dtype=np.int64)
+    ones = np.ones(100, np.int64)
+    op = gpu_operator(dict(assigner="tumbling", size=50, slide=50, agg="sum_i64"))
+    lh = np.array([N.lib().gw_java_long_hash(int(k)) for k in keys], np.int32)
+    op.process_batch(keys, ts, ones, key_hashes=lh)  # Long.hashCode: fine
+    op.snapshot_state()
+    op.process_batch(keys, ts, ones, key_hashes=lh + 1)
+    with pytest.raises(N.GpuWinError) as ei:
+        op.snapshot_state()
+    assert ei.value.code == -2
+    op.close()
+    kgr = W.compute_key_group_range_for_operator_index(128, 2, 0)
+    mine = np.array([k for k in range(1000) if kgr[0] <= W.assign_to_key_group(k, 128) <= kgr[1]][:50], np.int64)
+    other = np.array([k for k in range(1000) if not kgr[0] <= W.assign_to_key_group(k, 128) <= kgr[1]][:1], np.int64)
+    op = W.GpuWindowOperator(W.TumblingEventTimeWindows.of(50), "sum_i64", parallelism=2, operator_index=0,
+                             flags=N.FLAG_CHECK_KEY_GROUPS, capacity_hint=1024).open()
+    op.process_batch(mine, np.arange(50, dtype=np.int64), np.ones(50, np.int64))
+    with pytest.raises(N.GpuWinError) as ei:
+        op.process_batch(np.concatenate([mine, other]), np.arange(51, dtype=np.int64), np.ones(51, np.int64))
+    assert ei.value.code == -1 and "is not in KeyGroupRange" in str(ei.value)
+    op.close()

@@ -1,0 +1,81 @@
+"""The JNI glue (integration/jni/native/gw_jni.c) compiled against a test-only JNI header and a
+fake JNIEnv (tests/jni/), then called from Python: the per-key-group slicing GpuWindowOperator
+.snapshotState uses, and the status -> Java exception mapping (GW_E_INVALID ->
+IllegalArgumentException, other errors -> RuntimeException with gw_last_error's text)."""
+import ctypes
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from flink_amd import _native as N
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+from test_snapshot_slice import make_blob  # noqa: E402
+
+CLS = "Java_org_apache_flink_streaming_runtime_operators_windowing_gpu_GpuWindowOperator_"
+
+
+@pytest.fixture(scope="module")
+def jni(tmp_path_factory):
+    N.lib()
+    out = str(tmp_path_factory.mktemp("jni") / "libgw_jni_test.so")
+    fl = os.path.join(ROOT, "flink_amd")
+    cmd = ["gcc", "-shared", "-fPIC", "-Wall", "-Wextra", "-Werror", "-Wno-unused-parameter",
+           "-I" + os.path.join(ROOT, "tests", "jni"), "-I" + os.path.join(ROOT, "include"),
+           os.path.join(ROOT, "integration", "jni", "native", "gw_jni.c"), os.path.join(ROOT, "tests", "jni", "fake_env.c"),
+           "-L" + fl, "-lgpuwin", "-Wl,-rpath," + fl, "-o", out]
+    subprocess.run(cmd, check=True, capture_output=True)
+    L = ctypes.CDLL(out)
+    p = ctypes.c_void_p
+    L.fake_env.restype = p
+    L.fake_bytes_new.restype = p
+    L.fake_bytes_new.argtypes = [p, ctypes.c_int32]
+    L.fake_bytes_len.argtypes = [p]
+    L.fake_bytes_data.restype = p
+    L.fake_bytes_data.argtypes = [p]
+    L.fake_bytes_free.argtypes = [p]
+    getattr(L, CLS + "nativeSliceKeyGroup").restype = p
+    getattr(L, CLS + "nativeSliceKeyGroup").argtypes = [p, p, p, ctypes.c_int32]
+    f = getattr(L, CLS + "nativeCreate")
+    f.restype = ctypes.c_int64
+    f.argtypes = [p, p] + [ctypes.c_int32, ctypes.c_int32] + [ctypes.c_int64] * 5 + [ctypes.c_int32] * 5 + \
+        [ctypes.c_int64] * 2
+    return L
+
+
+def exception(L):
+    c, m = ctypes.create_string_buffer(256), ctypes.create_string_buffer(1024)
+    return (c.value.decode(), m.value.decode()) if L.fake_exception(c, m, 256) else None
+
+
+@pytest.mark.parametrize("version,words", [(1, 4), (2, 6), (3, 10)])
+def test_native_slice_key_group_matches_library(jni, version, words):
+    blob, offs, ent = make_blob(version, words, 64, 95, lambda k: k % 4, seed=11)
+    env = jni.fake_env()
+    arr = jni.fake_bytes_new(blob, len(blob))
+    for kg in range(64, 96):
+        out = getattr(jni, CLS + "nativeSliceKeyGroup")(env, None, arr, kg)
+        assert exception(jni) is None
+        got = ctypes.string_at(jni.fake_bytes_data(out), jni.fake_bytes_len(out))
+        assert got == N.snapshot_slice(blob, kg)
+        i = kg - 64
+        assert np.array_equal(np.frombuffer(got[112:], np.int64).reshape(-1, words), ent[offs[i]:offs[i + 1]])
+        jni.fake_bytes_free(out)
+    # a key group outside the blob: IllegalArgumentException, no array
+    assert getattr(jni, CLS + "nativeSliceKeyGroup")(env, None, arr, 3) is None
+    exc = exception(jni)
+    assert exc is not None and exc[0] == "java/lang/IllegalArgumentException"
+    jni.fake_bytes_free(arr)
+
+
+def test_native_create_maps_status_to_java_exceptions(jni):
+    env = jni.fake_env()
+    create = getattr(jni, CLS + "nativeCreate")
+    # tumbling size 0: invalid in Flink (IllegalArgumentException)
+    assert create(env, None, 0, 0, 0, 0, 0, 0, 0, 1, 128, 1, 0, 0, 1 << 16, 1 << 16) == 0
+    exc = exception(jni)
+    assert exc is not None and exc[0] == "java/lang/IllegalArgumentException" and "abs(offset) < size" in exc[1]
