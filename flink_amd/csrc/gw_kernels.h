@@ -189,8 +189,28 @@ struct MergeArgs {
     DevStatus* st;
 };
 
+// Restored window state (allowed by a heap-layout snapshot, gw_restore): one entry per
+// restored (key, window) state entry of the reference, sorted by (key, window index), each
+// key's entries reachable from its slot through head[slot] (-1: none).  A restored window
+// fires as the fold of its accumulator and the panes of the records that arrived after the
+// restore.
+constexpr uint32_t kOvTimer = 1;  // its event-time timer (maxTimestamp) is pending
+constexpr uint32_t kOvDead = 2;   // its state was purged
+struct Overlay {
+    const int32_t* head;  // [cap + 1], nullptr when no restored state is left
+    const int64_t* key;
+    const int64_t* k;     // window index: start = offset + k * slide
+    const int64_t* a0;
+    const int64_t* a1;
+    uint32_t* flags;
+    int64_t n;
+    int32_t purge;        // fired windows lose their state (lateness 0 or PurgingTrigger)
+};
+
 struct FireArgs {
     PaneTable t;
+    Overlay ov;
+    int64_t k0;         // window index of the first window of this pass
     int32_t nwin;
     int64_t start0;     // start of the first window fired in this pass
     int64_t slide;
@@ -209,6 +229,7 @@ struct FireArgs {
 // RS/api/windowing/triggers/EventTimeTrigger.java:37-45; WindowOperator.java:408-446).
 struct RefireArgs {
     PaneTable t;
+    Overlay ov;
     int64_t n;
     const uint32_t* order;  // entry indices sorted by (key, seq)
     const int64_t* rf_key;
@@ -259,6 +280,8 @@ struct SnapArgs {
 hipError_t launch_snap_collect(const SnapArgs& a, hipStream_t s);
 
 hipError_t launch_table_init(const PaneTable& t, hipStream_t s);
+// Insert every overlay key into the table and point head[slot] at its first entry.
+hipError_t launch_overlay_attach(const PaneTable& t, const Overlay& ov, int32_t* head, DevStatus* st, hipStream_t s);
 // path: 0 direct atomics, 1 LDS pre-aggregation (the region path has its own launchers)
 hipError_t launch_ingest(const IngestArgs& a, int path, int unroll, hipStream_t s);
 // region path: P1 over one batch (a.n records -> buffer tiles from a.tile0) ...

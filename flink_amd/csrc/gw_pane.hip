@@ -1144,6 +1144,7 @@ __global__ void __launch_bounds__(256) k_refire(RefireArgs a) {
     const int64_t id0 = identity0(AGG);
     const int64_t g = pt_find_ro(a.t, key);
     const uint64_t mask = g >= 0 ? presence<AGG>(a.t, g) : 0;
+    const int64_t oh = (a.ov.head && g >= 0) ? a.ov.head[g] : -1;
     int64_t run0[kMaxRing], run1[kMaxRing];  // this interval's late records per ring position
     for (int q = 0; q < R; ++q) { run0[q] = id0; run1[q] = 0; }
     for (int64_t j = i; j < a.n && a.rf_key[a.order[j]] == key; ++j) {
@@ -1162,6 +1163,10 @@ __global__ void __launch_bounds__(256) k_refire(RefireArgs a) {
             if (a.purging) {
                 fold_cell(AGG, r0, r1, c0, c1);
             } else {
+                if (oh >= 0) {  // restored state of this fired window
+                    for (int64_t q = oh; q < a.ov.n && a.ov.key[q] == key && a.ov.k[q] <= k; ++q)
+                        if (a.ov.k[q] == k && !(a.ov.flags[q] & kOvDead)) fold_cell(AGG, r0, r1, a.ov.a0[q], a.ov.a1[q]);
+                }
                 for (int64_t q = k * a.m; q < k * a.m + a.np; ++q) {
                     if (q < a.b || q - a.b >= R) continue;  // outside the ring: no data
                     int qp = a.b_pos + (int)(q - a.b);
@@ -1229,16 +1234,35 @@ __global__ void __launch_bounds__(256) k_fire(FireArgs a) {
         int64_t key = kEmptyKey;
         uint64_t mask = 0;
         const bool live = g < c1;
+        int64_t oi = -1;  // this key's next restored-window entry
         if (live) {
             key = *pt_key(a.t, g);
             mask = presence<AGG>(a.t, g);
+            if (a.ov.head) oi = a.ov.head[g];
         }
         for (int w = 0; w < a.nwin; ++w) {
             const bool flush = rs.cnt + blockDim.x > kRowStage;  // uniform: read before any append
             __syncthreads();
             if (flush) stage_flush(rs, &a.st->rows, a.o_key, a.o_start, a.o_end, a.o_res);
             uint64_t m = mask & a.wmask[w];
-            if (m) {
+            bool ov_hit = false;
+            int64_t o0 = 0, o1 = 0;
+            if (oi >= 0) {  // restored state of (key, window): fires with its timer or with new records
+                const int64_t kk = a.k0 + w;
+                while (oi < a.ov.n && a.ov.key[oi] == key && a.ov.k[oi] < kk) ++oi;
+                if (oi < a.ov.n && a.ov.key[oi] == key && a.ov.k[oi] == kk) {
+                    const uint32_t f = a.ov.flags[oi];
+                    if (!(f & kOvDead) && (m || (f & kOvTimer))) {
+                        ov_hit = true;
+                        o0 = a.ov.a0[oi];
+                        o1 = a.ov.a1[oi];
+                        a.ov.flags[oi] = a.ov.purge ? kOvDead : (f & ~kOvTimer);
+                    }
+                } else if (oi >= a.ov.n || a.ov.key[oi] != key) {
+                    oi = -1;
+                }
+            }
+            if (m || ov_hit) {
                 int64_t r0 = id0, r1 = 0;
                 while (m) {
                     const int pos = __ffsll((long long)m) - 1;
@@ -1246,6 +1270,7 @@ __global__ void __launch_bounds__(256) k_fire(FireArgs a) {
                     const int64_t* c = pt_cell(a.t, g, pos);
                     fold_cell(AGG, r0, r1, c[0], W == 2 ? c[1] : 0);
                 }
+                if (ov_hit) fold_cell(AGG, r0, r1, o0, o1);
                 const unsigned j = atomicAdd(&rs.cnt, 1u);
                 const int64_t st = a.start0 + (int64_t)w * a.slide;
                 rs.k[j] = key;
@@ -1378,6 +1403,21 @@ __global__ void __launch_bounds__(256) k_snap_collect(SnapArgs a) {
             off++;
         }
     }
+}
+
+// Restore: every overlay key gets a slot (inserted with no pane data) and head[slot] points at
+// its first entry (entries sorted by key).
+__global__ void __launch_bounds__(256) k_overlay_attach(PaneTable t, Overlay ov, int32_t* head, DevStatus* st) {
+    unsigned long long ins = 0, flags = 0;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < ov.n; i += (int64_t)gridDim.x * blockDim.x) {
+        if (i > 0 && ov.key[i - 1] == ov.key[i]) continue;
+        bool inserted;
+        const int64_t g = pt_find_or_insert(t, ov.key[i], inserted);
+        if (g < 0) { flags |= GW_DF_TABLE_FULL; continue; }
+        ins += inserted;
+        head[g] = (int32_t)i;
+    }
+    block_commit(st, 0, ins, flags, 0);
 }
 
 // Status word writes, ordered on the stream (no host sync).
@@ -1566,6 +1606,12 @@ hipError_t launch_snap_collect(const SnapArgs& a, hipStream_t s) {
 #define L(A) hipLaunchKernelGGL(k_snap_collect<A>, dim3(grid_for(a.t.cap + 1 + a.n_def)), dim3(256), 0, s, a)
     GW_AGG_SWITCH(a.t.agg, L);
 #undef L
+    return hipGetLastError();
+}
+
+hipError_t launch_overlay_attach(const PaneTable& t, const Overlay& ov, int32_t* head, DevStatus* st, hipStream_t s) {
+    if (ov.n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_overlay_attach, dim3(grid_for(ov.n)), dim3(256), 0, s, t, ov, head, st);
     return hipGetLastError();
 }
 

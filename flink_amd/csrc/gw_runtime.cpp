@@ -30,7 +30,7 @@ namespace {
 thread_local std::string g_create_error;
 
 constexpr int64_t kMaxIngest = (int64_t)1 << 30;
-constexpr uint32_t kSnapMaxVersion = 3;  // gw_handle::SnapHeader versions  // records per region-path batch / buffer
+constexpr uint32_t kSnapMaxVersion = 4;  // gw_handle::SnapHeader versions  // records per region-path batch / buffer
 
 // Host-time profile of the ingest path (GW_HOST_PROFILE=1: printed by gw_destroy).
 struct HostProf {
@@ -520,7 +520,7 @@ struct gw_handle {
         stats.rehashes++;
         if ((rc = refresh())) return rc;
         if (h_st->flags & GW_DF_TABLE_FULL) return fail(GW_E_OOM, "state table rehash overflow");
-        return GW_OK;
+        return ov_attach();  // restored keys without new records are not live slots: re-insert
     }
     int64_t live_count() {
         hipMemsetAsync(d_tmp, 0, 8, stream);
@@ -541,7 +541,7 @@ struct gw_handle {
         const int64_t used = (int64_t)h_st->used_slots;
         const bool full = (h_st->flags & GW_DF_TABLE_FULL) != 0;
         if (!full && (double)used <= 0.7 * (double)tv.cap) return GW_OK;
-        const int64_t live = live_count();
+        const int64_t live = live_count() + ov_nkeys;
         // parked records that failed to insert are potential new keys
         const int64_t pending = full ? std::max<int64_t>(incoming, (int64_t)h_st->n_deferred) : 0;
         int64_t want = std::max<int64_t>(tv.cap, 1024);
@@ -655,6 +655,7 @@ struct gw_handle {
             if ((rc = ensure_output((int64_t)h_st->rows + nrf * per_rec))) return rc;
             RefireArgs r{};
             r.t = tv;
+            r.ov = ov_view();
             r.n = nrf;
             r.order = order;
             r.rf_key = rf[0]; r.rf_pane = rf[1]; r.rf_a0 = rf[2]; r.rf_a1 = rf[3];
@@ -775,7 +776,9 @@ struct gw_handle {
             i128 dmin;
             if ((rc = deferred_min(dmin))) return rc;
             const i128 rmin = ring_min();
-            const i128 L = std::min(rmin, dmin);
+            // restored windows whose timer is pending fire even without new records
+            const i128 omin = ov_n ? ov_pending_min() * (i128)m + (i128)n - 1 : ((i128)1) << 100;
+            const i128 L = std::min(std::min(rmin, dmin), omin);
             const i128 NONE = ((i128)1) << 100;
             if (L >= NONE) { fired_k = k_target + 1; break; }
             i128 k_first = floor_div(L - n, m) + 1;
@@ -791,6 +794,8 @@ struct gw_handle {
             const int nwin = (int)(k_last - k_first + 1);
             FireArgs f{};
             f.t = tv;
+            f.ov = ov_view();
+            f.k0 = (int64_t)k_first;
             f.nwin = nwin;
             const i128 start0 = (i128)cfg.offset + k_first * (i128)slide();
             const i128 endl = (i128)cfg.offset + k_last * (i128)slide() + size();
@@ -947,6 +952,7 @@ struct gw_handle {
 
     int ingest_pane(int64_t nrec, const int64_t* key, const int64_t* ts, const int64_t* val) {
         int rc;
+        if ((rc = ov_finalize())) return rc;
         if (dirty && (rc = refresh())) return rc;  // a lagging (lazy) status is fine here
         if ((rc = maybe_grow(nrec))) return rc;
         if ((rc = ensure_deferred((int64_t)h_st->n_deferred + lazy_recs + nrec))) return rc;
@@ -1068,32 +1074,191 @@ struct gw_handle {
     }
 
     // ---------------------------------------------------------------- snapshot
-    // Blob (little-endian): SnapHeader, int64 kg_offsets[kg_hi - kg_lo + 2] (first entry
-    // of each key group), then SnapEntry entries sorted by key group.
+    // Blob (little-endian): SnapHeader, int64 kg_offsets[kg_hi - kg_lo + 2], then the entries
+    // of each key group.  Versions: 2 session windows, 3 count windows (fixed-size entries of
+    // `reserved` int64 words, offsets in entries), 4 tumbling / sliding windows (the heap
+    // backend's per-key-group byte layout, offsets in bytes; see snapshot_heap).
     struct SnapHeader {
         char magic[4];
         uint32_t version;
         int32_t agg, assigner;
         int64_t size, slide, offset, gap, pane;
         int32_t max_parallelism, kg_lo, kg_hi, reserved;
-        int64_t fired_lo, fired_hi;  // first window not fired yet (int128): the timer state
-        int64_t entries;
-    };
-    bool restored = false;
-    struct SnapEntry {
-        int64_t key, pane, a0, a1;
+        int64_t fired_lo, fired_hi;
+        int64_t entries;  // entries (versions 2, 3) / payload bytes (version 4)
     };
 
-    int snapshot(int32_t kg_lo, int32_t kg_hi, void* buf, int64_t cap, int64_t* len) {
+    // -------------------------------------------- restored window state (the overlay)
+    // A heap-layout blob holds the reference's state per (key, window) and its timers.
+    // Windows overlap (sliding), so a window's accumulator cannot be split back into panes:
+    // it stays a window-level entry (gw_kernels.h Overlay) that k_fire / k_refire fold
+    // into the window's row together with the panes of the records that arrive after the
+    // restore.  The watermark restarts at Long.MIN_VALUE as in the reference
+    // (InternalTimerServiceImpl.java:72): nothing has fired, nothing is late.
+    struct OvEntry {
+        int64_t key, k, a0, a1;
+        uint32_t flags;
+    };
+    std::vector<OvEntry> ov_pending;  // restored, not yet on the device
+    int64_t* d_ov = nullptr;          // key | k | a0 | a1, ov_n each
+    uint32_t* d_ov_flags = nullptr;
+    int32_t* d_ov_head = nullptr;     // [tv.cap + 1]
+    int64_t ov_n = 0, ov_nkeys = 0;
+    i128 ov_max_k = 0;
+    std::vector<int64_t> ov_timer_ks;  // sorted window indices with a pending timer
+
+    Overlay ov_view() const {
+        Overlay o{};
+        if (!ov_n) return o;
+        o.head = d_ov_head;
+        o.key = d_ov; o.k = d_ov + ov_n; o.a0 = d_ov + 2 * ov_n; o.a1 = d_ov + 3 * ov_n;
+        o.flags = d_ov_flags;
+        o.n = ov_n;
+        o.purge = cfg.allowed_lateness == 0 || cfg.trigger == GW_PURGING_EVENT_TIME_TRIGGER;
+        return o;
+    }
+    void ov_free() {
+        if (d_ov) hipFree(d_ov);
+        if (d_ov_flags) hipFree(d_ov_flags);
+        if (d_ov_head) hipFree(d_ov_head);
+        d_ov = nullptr; d_ov_flags = nullptr; d_ov_head = nullptr;
+        ov_n = ov_nkeys = 0;
+        ov_timer_ks.clear();
+    }
+    // Slots of the overlay keys in the current table (after the restore and every rehash).
+    int ov_attach() {
+        if (!ov_n) return GW_OK;
+        if (d_ov_head) HIPCHECK(hipFree(d_ov_head));
+        HIPCHECK(hipMalloc((void**)&d_ov_head, (size_t)(tv.cap + 1) * 4));
+        HIPCHECK(hipMemsetAsync(d_ov_head, 0xff, (size_t)(tv.cap + 1) * 4, stream));
+        HIPCHECK(launch_overlay_attach(tv, ov_view(), d_ov_head, d_st, stream));
+        dirty = true;
+        int rc;
+        if ((rc = refresh())) return rc;
+        if (h_st->flags & GW_DF_TABLE_FULL) return fail(GW_E_OOM, "state table full attaching restored state");
+        return GW_OK;
+    }
+    // Move the restored entries to the device (first call after the restores).
+    int ov_finalize() {
+        if (ov_pending.empty()) return GW_OK;
+        auto& v = ov_pending;
+        std::sort(v.begin(), v.end(), [](const OvEntry& x, const OvEntry& y) {
+            return x.key != y.key ? x.key < y.key : x.k < y.k;
+        });
+        size_t w = 0;  // one entry per (key, window): merge repeats (the same key group twice)
+        for (size_t i = 0; i < v.size(); ++i) {
+            if (w && v[w - 1].key == v[i].key && v[w - 1].k == v[i].k) {
+                fold_cell(cfg.agg, v[w - 1].a0, v[w - 1].a1, v[i].a0, v[i].a1);
+                v[w - 1].flags |= v[i].flags;
+            } else {
+                v[w++] = v[i];
+            }
+        }
+        v.resize(w);
+        const int64_t n = (int64_t)w;
+        ov_free();
+        std::vector<int64_t> cols((size_t)n * 4);
+        std::vector<uint32_t> fl((size_t)n);
+        ov_nkeys = 0;
+        ov_max_k = v.empty() ? 0 : v[0].k;
+        for (int64_t i = 0; i < n; ++i) {
+            cols[i] = v[i].key; cols[n + i] = v[i].k; cols[2 * n + i] = v[i].a0; cols[3 * n + i] = v[i].a1;
+            fl[i] = v[i].flags;
+            if (v[i].flags & kOvTimer) ov_timer_ks.push_back(v[i].k);
+            if (i == 0 || v[i].key != v[i - 1].key) ov_nkeys++;
+            if (v[i].k > ov_max_k) ov_max_k = v[i].k;
+        }
+        std::sort(ov_timer_ks.begin(), ov_timer_ks.end());
+        ov_timer_ks.erase(std::unique(ov_timer_ks.begin(), ov_timer_ks.end()), ov_timer_ks.end());
+        ov_pending.clear();
+        if (!n) return GW_OK;
+        HIPCHECK(hipMalloc((void**)&d_ov, (size_t)n * 32));
+        HIPCHECK(hipMalloc((void**)&d_ov_flags, (size_t)n * 4));
+        HIPCHECK(hipMemcpy(d_ov, cols.data(), (size_t)n * 32, hipMemcpyHostToDevice));
+        HIPCHECK(hipMemcpy(d_ov_flags, fl.data(), (size_t)n * 4, hipMemcpyHostToDevice));
+        ov_n = n;
+        int rc;
+        // room for the restored keys before they get slots
+        if ((double)(h_st->used_slots + ov_nkeys) > 0.7 * (double)tv.cap) {
+            int64_t want = tv.cap;
+            while ((double)(h_st->used_slots + ov_nkeys) > 0.5 * (double)want) want *= 2;
+            if ((rc = rehash(want))) return rc;  // attaches
+            return GW_OK;
+        }
+        return ov_attach();
+    }
+    // Smallest window index >= fired_k whose restored timer is pending (or "none").
+    i128 ov_pending_min() const {
+        auto it = std::lower_bound(ov_timer_ks.begin(), ov_timer_ks.end(), (int64_t)std::max<i128>(fired_k, INT64_MIN));
+        return it == ov_timer_ks.end() ? ((i128)1) << 100 : (i128)*it;
+    }
+    // Every restored window is fired and cleaned: drop the overlay.
+    void ov_maybe_release(int64_t w) {
+        if (ov_n && clean_k_at(w) > ov_max_k && fired_k > ov_max_k) ov_free();
+    }
+
+    // Accumulator <-> cell words (the serializer's value, gw_common.h cells).
+    void acc_to_be(std::vector<uint8_t>& o, int64_t a0, int64_t a1) const {
+        switch (cfg.agg) {
+        case GW_SUM_I32: be32(o, (int32_t)(uint32_t)(uint64_t)a0); break;
+        case GW_MIN_F64: case GW_MAX_F64: be64(o, f64_from_order_key(a0)); break;
+        case GW_AVG_I64: case GW_AVG_F64: be64(o, a0); be64(o, a1); break;
+        default: be64(o, a0); break;
+        }
+    }
+    int acc_bytes() const {
+        return cfg.agg == GW_SUM_I32 ? 4 : (cfg.agg == GW_AVG_I64 || cfg.agg == GW_AVG_F64) ? 16 : 8;
+    }
+    void acc_from_be(const uint8_t* p, int64_t& a0, int64_t& a1) const {
+        a1 = 0;
+        switch (cfg.agg) {
+        case GW_SUM_I32: a0 = (int64_t)rd32(p); break;
+        case GW_MIN_F64: case GW_MAX_F64: a0 = f64_order_key(rd64(p)); break;
+        case GW_AVG_I64: case GW_AVG_F64: a0 = rd64(p); a1 = rd64(p + 8); break;
+        default: a0 = rd64(p); break;
+        }
+    }
+    static void be64(std::vector<uint8_t>& o, int64_t v) {
+        for (int i = 0; i < 8; ++i) o.push_back((uint8_t)((uint64_t)v >> (56 - 8 * i)));
+    }
+    static void be32(std::vector<uint8_t>& o, int32_t v) {
+        for (int i = 0; i < 4; ++i) o.push_back((uint8_t)((uint32_t)v >> (24 - 8 * i)));
+    }
+    static int64_t rd64(const uint8_t* p) {
+        uint64_t v = 0;
+        for (int i = 0; i < 8; ++i) v = (v << 8) | p[i];
+        return (int64_t)v;
+    }
+    static int32_t rd32(const uint8_t* p) {
+        uint32_t v = 0;
+        for (int i = 0; i < 4; ++i) v = (v << 8) | p[i];
+        return (int32_t)v;
+    }
+    i128 win_start(i128 k) const { return (i128)cfg.offset + k * (i128)slide(); }
+
+    // Heap-layout snapshot (version 4) of the tumbling / sliding window state: per key group,
+    // the reference's "window-contents" entries (window, key, accumulator) -- every (key,
+    // window) whose panes hold data, folded, plus the restored windows -- the (empty)
+    // merging window set, and the event-time timers (CopyOnWriteStateMapSnapshot.writeState
+    // :127-149, TimerSerializer.serialize :147-152, InternalTimerServiceImpl :350-360):
+    //   state:   windows not fired yet; under allowed lateness with EventTimeTrigger also the
+    //            fired windows that are not cleaned yet (WindowOperator.cleanupTime :670-677);
+    //   timers:  maxTimestamp for the windows not fired yet (EventTimeTrigger.onElement),
+    //            maxTimestamp + lateness for every window with state when lateness > 0
+    //            (registerCleanupTimer :631-643; with lateness 0 the two coincide).
+    int snapshot_heap(int32_t kg_lo, int32_t kg_hi, void* buf, int64_t cap, int64_t* len) {
         int rc;
         if (kg_lo < 0 || kg_hi < kg_lo || kg_hi >= cfg.max_parallelism)
             return fail(GW_E_INVALID, "key-group range [%d, %d] outside [0, %d)", kg_lo, kg_hi, cfg.max_parallelism);
+        if ((rc = ov_finalize())) return rc;
         if ((rc = ensure_fresh())) return rc;
         if ((rc = flush_buffer())) return rc;  // prepareSnapshotPreBarrier: buffered records first
+        if (rf_bound && (rc = process_refire())) return rc;  // late records of fired windows
         if ((rc = refresh())) return rc;
+        // (key, pane, a0, a1, kg) of every non-null pane cell and parked entry in range
         const int64_t n_def = (int64_t)h_st->n_deferred;
         const int64_t bound = ((int64_t)h_st->used_slots + 1) * popcount(occ) + n_def;
-        std::vector<SnapEntry> ents;
+        std::vector<int64_t> col[4];
         std::vector<int32_t> kgs;
         if (bound > 0) {
             int64_t* d = nullptr;
@@ -1107,13 +1272,12 @@ struct gw_handle {
             a.max_p = cfg.max_parallelism; a.kg_lo = kg_lo; a.kg_hi = kg_hi;
             a.o_key = d; a.o_pane = d + bound; a.o_a0 = d + 2 * bound; a.o_a1 = d + 3 * bound;
             a.o_kg = (int32_t*)(d + 4 * bound);
-            a.n_out = d_tmp + 2;  // 8-B aligned scratch word (64-bit atomic)
+            a.n_out = d_tmp + 2;
             hipError_t e = hipMemsetAsync(a.n_out, 0, 8, stream);
             if (e == hipSuccess) e = launch_snap_collect(a, stream);
             unsigned long long n = 0;
             if (e == hipSuccess) e = hipMemcpyAsync(&n, a.n_out, 8, hipMemcpyDeviceToHost, stream);
             if (e == hipSuccess) e = hipStreamSynchronize(stream);
-            std::vector<int64_t> col[4];
             if (e == hipSuccess) {
                 kgs.resize(n);
                 for (int c = 0; c < 4 && e == hipSuccess; ++c) {
@@ -1124,84 +1288,200 @@ struct gw_handle {
             }
             hipFree(d);
             if (e != hipSuccess) return fail(GW_E_DEVICE, "snapshot: %s", hipGetErrorString(e));
-            ents.resize(n);
-            for (size_t i = 0; i < n; ++i) ents[i] = SnapEntry{col[0][i], col[1][i], col[2][i], col[3][i]};
         }
-        // counting sort by key group
+        // the restored windows still holding state
+        std::vector<OvEntry> ov;
+        if (ov_n) {
+            std::vector<int64_t> oc((size_t)ov_n * 4);
+            std::vector<uint32_t> of((size_t)ov_n);
+            HIPCHECK(hipMemcpy(oc.data(), d_ov, (size_t)ov_n * 32, hipMemcpyDeviceToHost));
+            HIPCHECK(hipMemcpy(of.data(), d_ov_flags, (size_t)ov_n * 4, hipMemcpyDeviceToHost));
+            for (int64_t i = 0; i < ov_n; ++i) {
+                if (of[i] & kOvDead) continue;
+                const int32_t kg = key_group_for_hash(java_long_hash(oc[i]), cfg.max_parallelism);
+                if (kg < kg_lo || kg > kg_hi) continue;
+                ov.push_back(OvEntry{oc[i], oc[ov_n + i], oc[2 * ov_n + i], oc[3 * ov_n + i], of[i]});
+            }
+        }
+        const bool lat = cfg.allowed_lateness > 0;
+        const bool purging = cfg.trigger == GW_PURGING_EVENT_TIME_TRIGGER;
+        const i128 state_lo = (lat && !purging) ? std::min(clean_k_at(wm), fired_k) : fired_k;
+        // entries of one key group: panes sorted by (key, pane), overlay by (key, k)
         const int nk = kg_hi - kg_lo + 1;
+        std::vector<std::vector<int64_t>> by_kg(nk);  // indices into col
+        for (size_t i = 0; i < kgs.size(); ++i) by_kg[kgs[i] - kg_lo].push_back((int64_t)i);
+        std::vector<std::vector<OvEntry>> ov_kg(nk);
+        for (auto& e : ov) ov_kg[key_group_for_hash(java_long_hash(e.key), cfg.max_parallelism) - kg_lo].push_back(e);
+        std::vector<uint8_t> pay;
         std::vector<int64_t> offs(nk + 1, 0);
-        for (int32_t k : kgs) offs[k - kg_lo + 1]++;
-        for (int i = 0; i < nk; ++i) offs[i + 1] += offs[i];
-        const int64_t need = (int64_t)sizeof(SnapHeader) + (int64_t)(nk + 1) * 8 + (int64_t)ents.size() * 32;
+        const int64_t id0 = identity0(cfg.agg);
+        const i128 LMAX = INT64_MAX;
+        for (int g = 0; g < nk; ++g) {
+            offs[g] = (int64_t)pay.size();
+            auto& ix = by_kg[g];
+            std::sort(ix.begin(), ix.end(), [&](int64_t x, int64_t y) {
+                return col[0][x] != col[0][y] ? col[0][x] < col[0][y] : col[1][x] < col[1][y];
+            });
+            auto& oe = ov_kg[g];
+            std::sort(oe.begin(), oe.end(), [](const OvEntry& x, const OvEntry& y) {
+                return x.key != y.key ? x.key < y.key : x.k < y.k;
+            });
+            std::vector<uint8_t> st, tm;
+            int32_t nst = 0, ntm = 0;
+            size_t a = 0, b = 0;
+            while (a < ix.size() || b < oe.size()) {
+                // next key
+                int64_t key;
+                if (a < ix.size() && (b >= oe.size() || col[0][ix[a]] <= oe[b].key)) key = col[0][ix[a]];
+                else key = oe[b].key;
+                std::vector<std::pair<int64_t, std::pair<int64_t, int64_t>>> panes;  // pane -> cell
+                for (; a < ix.size() && col[0][ix[a]] == key; ++a) {
+                    const int64_t i = ix[a];
+                    if (!panes.empty() && panes.back().first == col[1][i]) {
+                        fold_cell(cfg.agg, panes.back().second.first, panes.back().second.second, col[2][i], col[3][i]);
+                    } else {
+                        panes.push_back({col[1][i], {col[2][i], col[3][i]}});
+                    }
+                }
+                std::vector<OvEntry> ok_;
+                for (; b < oe.size() && oe[b].key == key; ++b) ok_.push_back(oe[b]);
+                // the windows holding state: those covering a pane with data, and restored ones
+                std::vector<i128> ks;
+                for (auto& pp : panes) {
+                    const i128 p = pp.first;
+                    for (i128 k = floor_div(p - (i128)n, (i128)m) + 1; k <= floor_div(p, (i128)m); ++k) ks.push_back(k);
+                }
+                for (auto& e : ok_) ks.push_back(e.k);
+                std::sort(ks.begin(), ks.end());
+                ks.erase(std::unique(ks.begin(), ks.end()), ks.end());
+                size_t q = 0;
+                for (i128 k : ks) {
+                    if (k < state_lo) continue;
+                    int64_t r0 = id0, r1 = 0;
+                    bool any = false;
+                    const i128 p0 = k * (i128)m, p1 = p0 + (i128)n;
+                    for (auto& pp : panes)
+                        if (pp.first >= p0 && pp.first < p1) {
+                            fold_cell(cfg.agg, r0, r1, pp.second.first, pp.second.second);
+                            any = true;
+                        }
+                    bool timer = any && k >= fired_k;
+                    while (q < ok_.size() && ok_[q].k < k) ++q;
+                    if (q < ok_.size() && ok_[q].k == k) {
+                        fold_cell(cfg.agg, r0, r1, ok_[q].a0, ok_[q].a1);
+                        any = true;
+                        if ((ok_[q].flags & kOvTimer) && k >= fired_k) timer = true;
+                    }
+                    if (!any) continue;
+                    const i128 s0 = win_start(k), e0 = s0 + (i128)size();
+                    if (!fits64(s0) || !fits64(e0)) return fail(GW_E_RANGE, "window bounds overflow int64");
+                    be64(st, (int64_t)s0); be64(st, (int64_t)e0); be64(st, key);
+                    acc_to_be(st, r0, r1);
+                    nst++;
+                    const i128 mx = e0 - 1;
+                    if (timer) {
+                        be64(tm, (int64_t)((uint64_t)(int64_t)mx ^ 0x8000000000000000ull));
+                        be64(tm, key); be64(tm, (int64_t)s0); be64(tm, (int64_t)e0);
+                        ntm++;
+                    }
+                    const i128 ct = mx + (i128)cfg.allowed_lateness;
+                    if (lat && ct < LMAX) {
+                        be64(tm, (int64_t)((uint64_t)(int64_t)ct ^ 0x8000000000000000ull));
+                        be64(tm, key); be64(tm, (int64_t)s0); be64(tm, (int64_t)e0);
+                        ntm++;
+                    }
+                }
+            }
+            be32(pay, nst);
+            pay.insert(pay.end(), st.begin(), st.end());
+            be32(pay, 0);  // merging window set: none for tumbling / sliding windows
+            be32(pay, ntm);
+            pay.insert(pay.end(), tm.begin(), tm.end());
+        }
+        offs[nk] = (int64_t)pay.size();
+        const int64_t need = (int64_t)sizeof(SnapHeader) + (int64_t)(nk + 1) * 8 + (int64_t)pay.size();
         *len = need;
         if (!buf) return GW_OK;
         if (cap < need) return fail(GW_E_OUTPUT_FULL, "snapshot needs %lld bytes", (long long)need);
         SnapHeader hd{};
         memcpy(hd.magic, "GWS1", 4);
-        hd.version = 1;
+        hd.version = 4;
         hd.agg = cfg.agg; hd.assigner = cfg.assigner;
-        hd.size = cfg.size; hd.slide = slide(); hd.offset = cfg.offset; hd.gap = cfg.gap; hd.pane = g;
+        hd.size = cfg.size; hd.slide = slide(); hd.offset = cfg.offset; hd.gap = cfg.gap; hd.pane = 0;
         hd.max_parallelism = cfg.max_parallelism; hd.kg_lo = kg_lo; hd.kg_hi = kg_hi;
-        hd.fired_lo = (int64_t)(uint64_t)fired_k;
-        hd.fired_hi = (int64_t)(fired_k >> 64);
-        hd.entries = (int64_t)ents.size();
+        hd.entries = (int64_t)pay.size();
         char* out = (char*)buf;
         memcpy(out, &hd, sizeof hd);
         memcpy(out + sizeof hd, offs.data(), (nk + 1) * 8);
-        SnapEntry* oe = (SnapEntry*)(out + sizeof hd + (nk + 1) * 8);
-        std::vector<int64_t> fill(offs.begin(), offs.end() - 1);
-        for (size_t i = 0; i < ents.size(); ++i) oe[fill[kgs[i] - kg_lo]++] = ents[i];
+        if (!pay.empty()) memcpy(out + sizeof hd + (nk + 1) * 8, pay.data(), pay.size());
         return GW_OK;
     }
 
-    // Restore: the entries become deferred partial aggregates and merge like parked
-    // records (exact for every aggregate); the watermark stays Long.MIN_VALUE, as in
-    // Flink after initializeState.
-    int restore(const void* buf, int64_t len) {
-        int rc;
+    // Restore one heap-layout blob (any key-group range; several calls after rescaling).
+    // Only before the first record or watermark, as initializeState runs before processing.
+    int restore_heap(const void* buf, int64_t len) {
         if (!buf || len < (int64_t)sizeof(SnapHeader)) return fail(GW_E_INVALID, "snapshot blob too short");
         SnapHeader hd;
         memcpy(&hd, buf, sizeof hd);
-        if (memcmp(hd.magic, "GWS1", 4) != 0 || hd.version < 1 || hd.version > 3)
+        if (memcmp(hd.magic, "GWS1", 4) != 0 || hd.version < 1 || hd.version > kSnapMaxVersion)
             return fail(GW_E_INVALID, "not a gpuwin snapshot");
-        if (hd.version != 1) return fail(GW_E_INVALID, "snapshot of a different window / aggregate / max parallelism");
-        if (hd.agg != cfg.agg || hd.assigner != cfg.assigner || hd.size != cfg.size || hd.slide != slide() ||
-            hd.offset != cfg.offset || hd.pane != g || hd.max_parallelism != cfg.max_parallelism)
+        if (hd.version != 4 || hd.agg != cfg.agg || hd.assigner != cfg.assigner || hd.size != cfg.size ||
+            hd.slide != slide() || hd.offset != cfg.offset || hd.max_parallelism != cfg.max_parallelism)
             return fail(GW_E_INVALID, "snapshot of a different window / aggregate / max parallelism");
-        const int nk = hd.kg_hi - hd.kg_lo + 1;
-        const int64_t need = (int64_t)sizeof hd + (int64_t)(nk + 1) * 8 + hd.entries * 32;
-        if (nk <= 0 || hd.entries < 0 || len < need) return fail(GW_E_INVALID, "truncated snapshot blob");
-        // Windows fired before the snapshot stay fired (Flink restores no timer for them).
-        // Every blob restored into one handle must come from the same fired position.
-        const i128 fk = ((i128)hd.fired_hi << 64) | (i128)(uint64_t)hd.fired_lo;
-        if (!restored && stats.events_in == 0) {
-            if (fk > fired_k) fired_k = fk;
-            if (B < fired_k * m) B = fired_k * m;
-            restored = true;
-        } else if (fk != fired_k) {
-            return fail(GW_E_UNSUPPORTED, "snapshot blobs at different fired windows cannot be merged into one operator");
+        if (stats.events_in != 0 || wm != INT64_MIN)
+            return fail(GW_E_STATE, "restore after processing started (initializeState runs before the first record)");
+        const int64_t nk = (int64_t)hd.kg_hi - hd.kg_lo + 1;
+        const int64_t pay0 = (int64_t)sizeof hd + (nk + 1) * 8;
+        if (nk <= 0 || hd.entries < 0 || len < pay0 + hd.entries) return fail(GW_E_INVALID, "truncated snapshot blob");
+        const uint8_t* p = (const uint8_t*)buf + pay0;
+        const uint8_t* end = p + hd.entries;
+        const int ab = acc_bytes();
+        const size_t first = ov_pending.size();
+#define NEED(x) do { if (p + (x) > end) return fail(GW_E_INVALID, "truncated snapshot blob"); } while (0)
+        for (int64_t g = 0; g < nk; ++g) {
+            NEED(4);
+            const int32_t ns = rd32(p); p += 4;
+            const size_t base = ov_pending.size();
+            for (int32_t i = 0; i < ns; ++i) {
+                NEED(24 + ab);
+                const int64_t s0 = rd64(p), e0 = rd64(p + 8), key = rd64(p + 16);
+                const i128 k = floor_div((i128)s0 - cfg.offset, (i128)slide());
+                if (win_start(k) != (i128)s0 || (i128)s0 + size() != (i128)e0)
+                    return fail(GW_E_INVALID, "snapshot window [%lld, %lld) is not a window of this assigner",
+                                (long long)s0, (long long)e0);
+                OvEntry e{key, (int64_t)k, 0, 0, 0};
+                acc_from_be(p + 24, e.a0, e.a1);
+                ov_pending.push_back(e);
+                p += 24 + ab;
+            }
+            NEED(4);
+            if (rd32(p) != 0) return fail(GW_E_INVALID, "merging window set in a tumbling / sliding snapshot");
+            p += 4;
+            NEED(4);
+            const int32_t nt = rd32(p); p += 4;
+            NEED((int64_t)nt * 32);
+            // an event-time timer at the window's maxTimestamp: the window has not fired
+            std::sort(ov_pending.begin() + base, ov_pending.end(), [](const OvEntry& x, const OvEntry& y) {
+                return x.key != y.key ? x.key < y.key : x.k < y.k;
+            });
+            for (int32_t i = 0; i < nt; ++i, p += 32) {
+                const int64_t ts = (int64_t)((uint64_t)rd64(p) ^ 0x8000000000000000ull);
+                const int64_t key = rd64(p + 8), s0 = rd64(p + 16), e0 = rd64(p + 24);
+                if (ts != (int64_t)((uint64_t)e0 - 1)) continue;  // cleanup timer: implied by the state
+                const int64_t k = (int64_t)floor_div((i128)s0 - cfg.offset, (i128)slide());
+                auto it = std::lower_bound(ov_pending.begin() + base, ov_pending.end(), OvEntry{key, k, 0, 0, 0},
+                                           [](const OvEntry& x, const OvEntry& y) {
+                                               return x.key != y.key ? x.key < y.key : x.k < y.k;
+                                           });
+                if (it != ov_pending.end() && it->key == key && it->k == k) it->flags |= kOvTimer;
+            }
         }
-        if (hd.entries == 0) return GW_OK;
-        if ((rc = ensure_fresh())) return rc;
-        if (nseg && (rc = flush_buffer())) return rc;
-        const int64_t nd = (int64_t)h_st->n_deferred;
-        if ((rc = ensure_deferred(nd + hd.entries))) return rc;
-        const SnapEntry* in = (const SnapEntry*)((const char*)buf + sizeof hd + (nk + 1) * 8);
-        std::vector<int64_t> col(hd.entries);
-        int64_t* dst[4] = {dk[cur], dp[cur], da0[cur], da1[cur]};
-        for (int c = 0; c < 4; ++c) {
-            for (int64_t i = 0; i < hd.entries; ++i) col[i] = (&in[i].key)[c];
-            HIPCHECK(hipMemcpy(dst[c] + nd, col.data(), hd.entries * 8, hipMemcpyHostToDevice));
+#undef NEED
+        if (p != end) {
+            ov_pending.resize(first);
+            return fail(GW_E_INVALID, "snapshot blob has trailing bytes");
         }
-        if ((rc = set_field(offsetof(DevStatus, n_deferred), (unsigned long long)(nd + hd.entries)))) return rc;
-        dirty = true;
-        if ((rc = refresh())) return rc;
-        if (!occ) {  // nothing in the ring yet: start it at the oldest restored pane
-            i128 dmin;
-            if ((rc = deferred_min(dmin))) return rc;
-            B = std::max(fired_k * m, dmin);
-        }
-        return merge_deferred();
+        return GW_OK;
     }
 
     // Session windows: the blob (version 2) holds, per key group, every in-flight session
@@ -1273,6 +1553,7 @@ struct gw_handle {
         int rc;
         if (rows_out) *rows_out = 0;
         if (w <= wm) return GW_OK;
+        if ((rc = ov_finalize())) return rc;
         const i128 kt = k_for_wm(w);
         const i128 ct = clean_k_at(w);
         int64_t before = 0;
@@ -1306,6 +1587,7 @@ struct gw_handle {
         const int64_t fired = (int64_t)h_st->rows - before;
         stats.rows_fired += fired;
         if (rows_out) *rows_out = fired;
+        ov_maybe_release(w);
         return GW_OK;
     }
 };
@@ -1470,6 +1752,7 @@ int gw_destroy(gw_handle* h) {
     h->hp.dump();
     if (h->stream) hipStreamSynchronize(h->stream);
     if (h->sess) session_destroy(h->sess);
+    h->ov_free();
     if (h->tv.base) hipFree(h->tv.base);
     for (int b = 0; b < 2; ++b) {
         if (h->dk[b]) { hipFree(h->dk[b]); hipFree(h->dp[b]); hipFree(h->da0[b]); hipFree(h->da1[b]); }
@@ -1832,31 +2115,28 @@ int gw_flush(gw_handle* h) {
     if (h->failed) return h->fail(GW_E_STATE, "operator failed earlier: %s", h->err.c_str());
     if (h->session) return GW_OK;
     hipSetDevice(h->cfg.device);
-    int rc = h->ensure_fresh();
+    int rc = h->ov_finalize();
+    if (rc == GW_OK) rc = h->ensure_fresh();
     return rc ? rc : h->flush_buffer();
 }
 
 int gw_snapshot(gw_handle* h, int32_t kg_lo, int32_t kg_hi, void* buf, int64_t cap, int64_t* len) {
     if (!h || !len) return GW_E_INVALID;
     if (h->failed) return h->fail(GW_E_STATE, "operator failed earlier: %s", h->err.c_str());
-    if (h->cfg.allowed_lateness > 0 && h->cfg.assigner != GW_SESSION)
-        return h->fail(GW_E_UNSUPPORTED, "snapshot with allowed lateness > 0 is not yet supported for time windows");
     if (h->foreign_hash)
         return h->fail(GW_E_UNSUPPORTED, "snapshot of a handle that ingested a key_hash different from "
                                          "Long.hashCode(key): the state is grouped by Long.hashCode");
     hipSetDevice(h->cfg.device);
     if (h->session) return h->snapshot_sessions(kg_lo, kg_hi, buf, cap, len);
-    return h->snapshot(kg_lo, kg_hi, buf, cap, len);
+    return h->snapshot_heap(kg_lo, kg_hi, buf, cap, len);
 }
 
 int gw_restore(gw_handle* h, const void* buf, int64_t len) {
     if (!h) return GW_E_INVALID;
     if (h->failed) return h->fail(GW_E_STATE, "operator failed earlier: %s", h->err.c_str());
-    if (h->cfg.allowed_lateness > 0 && h->cfg.assigner != GW_SESSION)
-        return h->fail(GW_E_UNSUPPORTED, "restore with allowed lateness > 0 is not yet supported for time windows");
     hipSetDevice(h->cfg.device);
     if (h->session) return h->restore_sessions(buf, len);
-    return h->restore(buf, len);
+    return h->restore_heap(buf, len);
 }
 
 // The blob layout is gw_handle::SnapHeader (96 bytes: kg_lo at 60, kg_hi at 64, reserved at
@@ -1872,7 +2152,7 @@ int gw_snapshot_slice(const void* blob, int64_t len, int32_t kg, void* out, int6
         g_create_error = "not a gpuwin snapshot";
         return GW_E_INVALID;
     }
-    const int64_t ew = hd.version == 1 ? 32 : (int64_t)hd.reserved * 8;
+    const int64_t ew = hd.version == 1 ? 32 : hd.version >= 4 ? 1 : (int64_t)hd.reserved * 8;  // v4: bytes
     const int64_t nk = (int64_t)hd.kg_hi - hd.kg_lo + 1;
     if (ew <= 0 || nk <= 0 || hd.entries < 0 || len < (int64_t)sizeof hd + (nk + 1) * 8 + hd.entries * ew) {
         g_create_error = "truncated snapshot blob";

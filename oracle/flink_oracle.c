@@ -1000,6 +1000,259 @@ int64_t wo_session_merges(const wo_op* op) { return op->merges; }
 const char* wo_last_error(const wo_op* op) { return op ? op->err : "null operator"; }
 
 /* ------------------------------------------------------------------------ */
+/* Snapshot / restore in the heap backend's per-key-group layout              */
+/* ------------------------------------------------------------------------ */
+/* The keyed state of the reference's WindowOperator is written per key group
+ * (HeapSnapshotStrategy.java:97-154): for each registered state its
+ * CopyOnWriteStateMapSnapshot.writeState (:127-149) -- int n, then n x (namespace, key,
+ * state), each with its serializer (big-endian DataOutputView) -- and the event-time
+ * timers of the key group (InternalTimerServiceImpl.snapshotTimersForKeyGroup :350-360),
+ * each as TimerSerializer.serialize writes it (:147-152: flipSignBit(timestamp), key,
+ * namespace).  The blob (version 4, include/gpuwin.h gw_snapshot) carries per key group:
+ *   "window-contents":    int32 n; n x (window.start, window.end, key, accumulator)
+ *                         (TimeWindow.Serializer :159-169, LongSerializer, and the
+ *                         accumulator as LongSerializer / DoubleSerializer / IntSerializer /
+ *                         Tuple2(sum, count) for the closed set of aggregates);
+ *   "merging-window-set": int32 m; m x (key, int32 c, c x (window, state window)) -- the
+ *                         MergingWindowSet ListState<Tuple2<W, W>> of session windows
+ *                         (MergingWindowSet.persist :99-106); 0 for other assigners;
+ *   timers:               int32 t; t x (flipSignBit(ts), key, window.start, window.end).
+ * The watermark is not state: after a restore it is Long.MIN_VALUE
+ * (InternalTimerServiceImpl.java:72), so nothing restored is late until the next
+ * watermark. */
+typedef struct { uint8_t* p; int64_t n, cap; } wbuf;
+static void wb_put(wbuf* b, const void* src, int64_t n) {
+    if (b->p && b->n + n <= b->cap) memcpy(b->p + b->n, src, (size_t)n);
+    b->n += n;
+}
+static void wb_be64(wbuf* b, int64_t v) {
+    uint8_t x[8];
+    for (int i = 0; i < 8; i++) x[i] = (uint8_t)((uint64_t)v >> (56 - 8 * i));
+    wb_put(b, x, 8);
+}
+static void wb_be32(wbuf* b, int32_t v) {
+    uint8_t x[4];
+    for (int i = 0; i < 4; i++) x[i] = (uint8_t)((uint32_t)v >> (24 - 8 * i));
+    wb_put(b, x, 4);
+}
+static int64_t rd_be64(const uint8_t* p) {
+    uint64_t v = 0;
+    for (int i = 0; i < 8; i++) v = (v << 8) | p[i];
+    return (int64_t)v;
+}
+static int32_t rd_be32(const uint8_t* p) {
+    uint32_t v = 0;
+    for (int i = 0; i < 4; i++) v = (v << 8) | p[i];
+    return (int32_t)v;
+}
+static void wb_acc(wbuf* b, int agg, const acc_t* a) {
+    switch (agg) {
+    case GW_COUNT: wb_be64(b, a->c); break;
+    case GW_SUM_I32: wb_be32(b, (int32_t)a->i); break;
+    case GW_SUM_F64: case GW_MIN_F64: case GW_MAX_F64: wb_be64(b, d2bits(a->d)); break;
+    case GW_AVG_I64: wb_be64(b, a->i); wb_be64(b, a->c); break;
+    case GW_AVG_F64: wb_be64(b, d2bits(a->d)); wb_be64(b, a->c); break;
+    default: wb_be64(b, a->i); break;
+    }
+}
+int wo_acc_bytes(int agg) {
+    return agg == GW_SUM_I32 ? 4 : (agg == GW_AVG_I64 || agg == GW_AVG_F64) ? 16 : 8;
+}
+static void rd_acc(const uint8_t* p, int agg, acc_t* a) {
+    memset(a, 0, sizeof(*a));
+    switch (agg) {
+    case GW_COUNT: a->c = rd_be64(p); break;
+    case GW_SUM_I32: a->i = rd_be32(p); break;
+    case GW_SUM_F64: case GW_MIN_F64: case GW_MAX_F64: a->d = bits2d(rd_be64(p)); break;
+    case GW_AVG_I64: a->i = rd_be64(p); a->c = rd_be64(p + 8); break;
+    case GW_AVG_F64: a->d = bits2d(rd_be64(p)); a->c = rd_be64(p + 8); break;
+    default: a->i = rd_be64(p); break;
+    }
+}
+
+typedef struct { int32_t kg; int64_t k0, k1, k2, k3; int64_t v; } snap_ent;
+static int cmp_snap_ent(const void* a, const void* b) {
+    const snap_ent* x = (const snap_ent*)a;
+    const snap_ent* y = (const snap_ent*)b;
+    if (x->kg != y->kg) return x->kg < y->kg ? -1 : 1;
+    const int64_t xs[4] = {x->k0, x->k1, x->k2, x->k3}, ys[4] = {y->k0, y->k1, y->k2, y->k3};
+    for (int i = 0; i < 4; i++)
+        if (xs[i] != ys[i]) return xs[i] < ys[i] ? -1 : 1;
+    return 0;
+}
+static int32_t key_group_of(const wo_op* op, int64_t key) {
+    return wo_assign_to_key_group(wo_long_hash(key), op->c.max_parallelism > 0 ? op->c.max_parallelism : 128);
+}
+
+/* Returns the blob size; writes it when buf holds >= that many bytes. Negative on error. */
+int64_t wo_snapshot(wo_op* op, int32_t kg_lo, int32_t kg_hi, uint8_t* buf, int64_t cap) {
+    if (op->c.assigner == GW_COUNT_TUMBLING || op->c.assigner == GW_COUNT_SLIDING) return GW_E_UNSUPPORTED;
+    if (kg_lo < 0 || kg_hi < kg_lo) return GW_E_INVALID;
+    const int nk = kg_hi - kg_lo + 1;
+    /* gather (key group, sort key) for state entries, timers and merging sets */
+    int64_t ns = 0, nt = 0, nm = 0;
+    snap_ent* se = (snap_ent*)malloc(sizeof(snap_ent) * (size_t)(op->state.n + 1));
+    snap_ent* te = (snap_ent*)malloc(sizeof(snap_ent) * (size_t)(op->timers.n + 1));
+    snap_ent* me = (snap_ent*)malloc(sizeof(snap_ent) * (size_t)(op->nsets + 1));
+    if (!se || !te || !me) { free(se); free(te); free(me); return GW_E_OOM; }
+    for (int64_t i = 0; i < op->state.cap; i++) {
+        const ment_t* m = &op->state.e[i];
+        if (m->st != 1) continue;
+        int32_t kg = key_group_of(op, m->k[0]);
+        if (kg < kg_lo || kg > kg_hi) continue;
+        se[ns++] = (snap_ent){kg, m->k[0], m->k[1], m->k[2], 0, m->v};
+    }
+    for (int64_t i = 0; i < op->timers.cap; i++) {
+        const ment_t* m = &op->timers.e[i];
+        if (m->st != 1) continue;
+        int32_t kg = key_group_of(op, m->k[1]);
+        if (kg < kg_lo || kg > kg_hi) continue;
+        te[nt++] = (snap_ent){kg, m->k[1], m->k[2], m->k[3], m->k[0], 0}; /* (key, s, e, ts) */
+    }
+    for (int64_t i = 0; i < op->sets.cap; i++) {
+        const ment_t* m = &op->sets.e[i];
+        if (m->st != 1 || op->msets[m->v].n == 0) continue;
+        int32_t kg = key_group_of(op, m->k[0]);
+        if (kg < kg_lo || kg > kg_hi) continue;
+        me[nm++] = (snap_ent){kg, m->k[0], 0, 0, 0, m->v};
+    }
+    qsort(se, (size_t)ns, sizeof(snap_ent), cmp_snap_ent);
+    qsort(te, (size_t)nt, sizeof(snap_ent), cmp_snap_ent);
+    qsort(me, (size_t)nm, sizeof(snap_ent), cmp_snap_ent);
+    const int64_t hdr = 96, offs_at = hdr, pay0 = hdr + (int64_t)(nk + 1) * 8;
+    wbuf b = {buf, pay0, cap};
+    int64_t* offs = (int64_t*)calloc((size_t)nk + 1, sizeof(int64_t));
+    int64_t a = 0, t = 0, q = 0;
+    for (int g = 0; g < nk; g++) {
+        const int32_t kg = kg_lo + g;
+        offs[g] = b.n - pay0;
+        int64_t a1 = a, t1 = t, q1 = q;
+        while (a1 < ns && se[a1].kg == kg) a1++;
+        while (t1 < nt && te[t1].kg == kg) t1++;
+        while (q1 < nm && me[q1].kg == kg) q1++;
+        wb_be32(&b, (int32_t)(a1 - a));
+        for (; a < a1; a++) { /* namespace, key, state */
+            wb_be64(&b, se[a].k1); wb_be64(&b, se[a].k2); wb_be64(&b, se[a].k0);
+            wb_acc(&b, op->c.agg, &op->accs[se[a].v]);
+        }
+        wb_be32(&b, (int32_t)(q1 - q));
+        for (; q < q1; q++) {
+            const mws_t* w = &op->msets[me[q].v];
+            /* the list in (window start, end) order: the reference's list order is the
+             * mapping's iteration order, which carries no meaning */
+            int64_t* idx = (int64_t*)malloc(sizeof(int64_t) * 4 * (size_t)w->n);
+            memcpy(idx, w->w, sizeof(int64_t) * 4 * (size_t)w->n);
+            for (int i = 1; i < w->n; i++)
+                for (int j = i; j > 0 && (idx[4 * j] < idx[4 * j - 4] ||
+                                          (idx[4 * j] == idx[4 * j - 4] && idx[4 * j + 1] < idx[4 * j - 3])); j--)
+                    for (int c = 0; c < 4; c++) { int64_t x = idx[4 * j + c]; idx[4 * j + c] = idx[4 * j - 4 + c]; idx[4 * j - 4 + c] = x; }
+            wb_be64(&b, me[q].k0);
+            wb_be32(&b, w->n);
+            for (int i = 0; i < 4 * w->n; i++) wb_be64(&b, idx[i]);
+            free(idx);
+        }
+        wb_be32(&b, (int32_t)(t1 - t));
+        for (; t < t1; t++) { /* TimerSerializer: flipSignBit(ts), key, namespace */
+            wb_be64(&b, (int64_t)((uint64_t)te[t].k3 ^ 0x8000000000000000ull));
+            wb_be64(&b, te[t].k0); wb_be64(&b, te[t].k1); wb_be64(&b, te[t].k2);
+        }
+    }
+    offs[nk] = b.n - pay0;
+    const int64_t total = b.n;
+    if (buf && cap >= total) {
+        uint8_t h[96];
+        memset(h, 0, sizeof h);
+        memcpy(h, "GWS1", 4);
+        const uint32_t ver = 4;
+        const int64_t slide = op->c.assigner == GW_TUMBLING ? op->c.size : op->c.slide;
+        const int32_t i32s[2] = {op->c.agg, op->c.assigner};
+        const int64_t i64s[5] = {op->c.size, slide, op->c.offset, op->c.gap, 0};
+        const int32_t mp = op->c.max_parallelism > 0 ? op->c.max_parallelism : 128;
+        const int32_t i32b[4] = {mp, kg_lo, kg_hi, 0};
+        const int64_t tail[3] = {0, 0, offs[nk]};
+        memcpy(h + 4, &ver, 4);
+        memcpy(h + 8, i32s, 8);
+        memcpy(h + 16, i64s, 40);
+        memcpy(h + 56, i32b, 16);
+        memcpy(h + 72, tail, 24);
+        memcpy(buf, h, 96);
+        memcpy(buf + offs_at, offs, (size_t)(nk + 1) * 8);
+    }
+    free(offs); free(se); free(te); free(me);
+    return total;
+}
+
+/* Restore one blob (of any key-group range) into the operator: state entries, merging
+ * window sets and timers as the reference's restore reads them back; the watermark stays
+ * where it is (Long.MIN_VALUE for a fresh operator). */
+int wo_restore(wo_op* op, const uint8_t* buf, int64_t len) {
+    if (len < 96 || memcmp(buf, "GWS1", 4) != 0) { op_err(op, "not a snapshot blob"); return GW_E_INVALID; }
+    uint32_t ver; int32_t i32s[2], i32b[4]; int64_t i64s[5], tail[3];
+    memcpy(&ver, buf + 4, 4); memcpy(i32s, buf + 8, 8); memcpy(i64s, buf + 16, 40);
+    memcpy(i32b, buf + 56, 16); memcpy(tail, buf + 72, 24);
+    const int64_t slide = op->c.assigner == GW_TUMBLING ? op->c.size : op->c.slide;
+    const int32_t mp = op->c.max_parallelism > 0 ? op->c.max_parallelism : 128;
+    if (ver != 4 || i32s[0] != op->c.agg || i32s[1] != op->c.assigner || i64s[0] != op->c.size ||
+        i64s[1] != slide || i64s[2] != op->c.offset || i64s[3] != op->c.gap || i32b[0] != mp) {
+        op_err(op, "snapshot of a different window / aggregate / max parallelism");
+        return GW_E_INVALID;
+    }
+    const int nk = i32b[2] - i32b[1] + 1;
+    const int64_t pay0 = 96 + (int64_t)(nk + 1) * 8;
+    if (nk <= 0 || tail[2] < 0 || len < pay0 + tail[2]) { op_err(op, "truncated snapshot blob"); return GW_E_INVALID; }
+    const uint8_t* p = buf + pay0;
+    const uint8_t* end = p + tail[2];
+    const int ab = wo_acc_bytes(op->c.agg);
+#define NEED(x) do { if (p + (x) > end) { op_err(op, "truncated snapshot blob"); return GW_E_INVALID; } } while (0)
+    for (int g = 0; g < nk; g++) {
+        NEED(4);
+        int32_t n = rd_be32(p); p += 4;
+        for (int32_t i = 0; i < n; i++) {
+            NEED(24 + ab);
+            int64_t s = rd_be64(p), e = rd_be64(p + 8), key = rd_be64(p + 16);
+            acc_t a;
+            rd_acc(p + 24, op->c.agg, &a);
+            p += 24 + ab;
+            int64_t k[4] = {key, s, e, 0};
+            int created = 0;
+            ment_t* m = map_upsert(&op->state, k, -1, &created);
+            if (!m) return GW_E_OOM;
+            if (created) {
+                int64_t ai = acc_alloc(op);
+                if (ai < 0) return GW_E_OOM;
+                m = map_find(&op->state, k);
+                m->v = ai;
+                op->accs[ai] = a;
+            } else {
+                acc_merge(&op->accs[m->v], &a, op->c.agg);
+            }
+        }
+        NEED(4);
+        int32_t nm = rd_be32(p); p += 4;
+        for (int32_t i = 0; i < nm; i++) {
+            NEED(12);
+            int64_t key = rd_be64(p);
+            int32_t c = rd_be32(p + 8);
+            p += 12;
+            NEED((int64_t)c * 32);
+            mws_t* w = mws_get(op, key, 1);
+            for (int32_t j = 0; j < c; j++, p += 32)
+                mws_put(w, rd_be64(p), rd_be64(p + 8), rd_be64(p + 16), rd_be64(p + 24));
+        }
+        NEED(4);
+        int32_t t = rd_be32(p); p += 4;
+        for (int32_t i = 0; i < t; i++, p += 32) {
+            NEED(32);
+            int64_t ts = (int64_t)((uint64_t)rd_be64(p) ^ 0x8000000000000000ull);
+            int rc = tmr_register(op, rd_be64(p + 8), rd_be64(p + 16), rd_be64(p + 24), ts);
+            if (rc) return rc;
+        }
+    }
+#undef NEED
+    return GW_OK;
+}
+
+/* ------------------------------------------------------------------------ */
 /* multi-threaded CPU baseline: one operator per simulated subtask            */
 /* ------------------------------------------------------------------------ */
 typedef struct {

@@ -63,6 +63,14 @@ int64_t wo_timer_count(const wo_op* op);
 int64_t wo_session_merges(const wo_op* op);
 const char* wo_last_error(const wo_op* op);
 
+/* Keyed state of key groups [kg_lo, kg_hi] in the heap backend's per-key-group layout
+ * (blob version 4 of include/gpuwin.h gw_snapshot).  Returns the size; writes the blob
+ * when cap is large enough.  wo_restore reads one blob back (state, merging window sets,
+ * timers); the watermark is not part of it. */
+int64_t wo_snapshot(wo_op* op, int32_t kg_lo, int32_t kg_hi, uint8_t* buf, int64_t cap);
+int     wo_restore(wo_op* op, const uint8_t* buf, int64_t len);
+int     wo_acc_bytes(int agg);
+
 /* Multi-threaded CPU baseline: `threads` operator instances, each owning the key
  * groups of one subtask (computeKeyGroupRangeForOperatorIndex), like a Flink job
  * at parallelism = threads.  Runs the whole stream: batches of batch_len records,

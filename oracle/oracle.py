@@ -130,6 +130,8 @@ def lib() -> ctypes.CDLL:
                                                  ctypes.POINTER(GwDecodeResult)]),
             ("wo_run_parallel", i64, [ctypes.POINTER(GwConfig), ctypes.c_int, i64, p, p, p, p, p,
                                        P64, ctypes.POINTER(ctypes.c_double)]),
+            ("wo_snapshot", i64, [p, i32, i32, p, i64]), ("wo_restore", ctypes.c_int, [p, p, i64]),
+            ("wo_acc_bytes", ctypes.c_int, [ctypes.c_int]),
             ("wo_run_parallel_wm", i64, [ctypes.POINTER(GwConfig), ctypes.c_int, i64, p, p, p, p, p, p, p,
                                           ctypes.POINTER(ctypes.c_double)]),
         ]:
@@ -193,6 +195,24 @@ class OracleOperator:
         got = lib().wo_drain(self._h, _p(k), _p(s), _p(e), _p(r), n)
         assert got == n
         return k, s, e, r
+
+    def snapshot(self, key_group_range=None) -> bytes:
+        """Keyed state of key groups [lo, hi] (default all) in the heap backend's per-key-group
+        layout (blob version 4; oracle/flink_oracle.c wo_snapshot)."""
+        lo, hi = key_group_range if key_group_range is not None else (0, (self.cfg.max_parallelism or 128) - 1)
+        n = lib().wo_snapshot(self._h, lo, hi, None, 0)
+        if n < 0:
+            raise OracleError(f"snapshot failed: {n}")
+        buf = ctypes.create_string_buffer(n)
+        m = lib().wo_snapshot(self._h, lo, hi, buf, n)
+        assert m == n
+        return buf.raw[:n]
+
+    def restore(self, blobs):
+        if isinstance(blobs, (bytes, bytearray)):
+            blobs = [blobs]
+        for b in blobs:
+            self._check(lib().wo_restore(self._h, bytes(b), len(b)))
 
     @property
     def late_dropped(self) -> int:

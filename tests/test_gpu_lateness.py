@@ -121,16 +121,6 @@ def test_lateness_beyond_the_ring_is_unsupported():
     assert ei.value.code == -2
 
 
-def test_lateness_snapshot_is_unsupported():
-    op = gpu_operator(dict(assigner="tumbling", size=1000, slide=1000, agg="sum_i64", lateness=500))
-    try:
-        with pytest.raises(N.GpuWinError) as ei:
-            op.snapshot_state()
-        assert ei.value.code == -2
-    finally:
-        op.close()
-
-
 # ------------------------------------------------------------------ session windows
 # Merging windows with allowed lateness (WindowOperator.java:303-403 merging branch):
 # a session keeps its state until max timestamp + lateness; a late element that lands in
