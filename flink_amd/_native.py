@@ -33,11 +33,12 @@ FLAG_CHECK_KEY_GROUPS = 4
 FLAG_FORCE_REGION = 8
 FLAG_NO_REGION = 16
 FLAG_NO_BUFFER = 32
+FLAG_LATE_SIDE_OUTPUT = 64
 
 EXPORTS = [
     "gw_create", "gw_destroy", "gw_last_error", "gw_abi_version", "gw_ingest", "gw_ingest_device",
     "gw_advance_watermark", "gw_flush", "gw_snapshot", "gw_restore", "gw_snapshot_slice", "gw_end_input", "gw_pending_rows", "gw_drain", "gw_rows_device",
-    "gw_clear_rows", "gw_late_dropped", "gw_get_stats", "gw_synchronize", "gw_stream",
+    "gw_clear_rows", "gw_late_dropped", "gw_pending_late", "gw_drain_late", "gw_get_stats", "gw_synchronize", "gw_stream",
     "gw_kernel_time_ms", "gw_enable_kernel_timing", "gw_java_long_hash", "gw_murmur_hash",
     "gw_key_group_for_hash", "gw_operator_for_key_group", "gw_default_max_parallelism",
     "gw_key_groups_device", "gw_partition_scratch_bytes", "gw_partition_device",
@@ -140,6 +141,8 @@ def lib() -> ctypes.CDLL:
                                    ctypes.POINTER(p), P64]),
         "gw_clear_rows": (c_int, [p]),
         "gw_late_dropped": (i64, [p]),
+        "gw_pending_late": (c_int, [p, P64]),
+        "gw_drain_late": (c_int, [p, p, p, p, i64, P64]),
         "gw_get_stats": (c_int, [p, ctypes.POINTER(GwStats)]),
         "gw_synchronize": (c_int, [p]),
         "gw_stream": (p, [p]),

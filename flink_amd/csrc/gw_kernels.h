@@ -125,6 +125,9 @@ struct IngestArgs {
     uint64_t q_refire;  // lateness > 0: panes p_late .. p_late + q_refire - 1 belong to fired,
                         // not yet cleaned windows; their records go to the re-fire list
     int64_t seq0;       // arrival number of record 0 of this call (re-fire order)
+    int64_t* lo_key;    // late side output (WindowOperator.sideOutput :587-588), append at
+    int64_t* lo_ts;     //   st->n_late_out; nullptr: late records are counted and dropped
+    int64_t* lo_val;
     int64_t* rf_key;    // re-fire list (append at st->n_refire)
     int64_t* rf_pane;
     int64_t* rf_a0;

@@ -67,15 +67,16 @@ __device__ __forceinline__ uint64_t presence_rt(const PaneTable& t, int64_t g) {
 
 // Per-record classification: late / parked (outside the pane ring) / in ring / re-fire
 // (allowed lateness > 0: the pane belongs to a fired window that is not cleaned yet).
-enum { REC_SKIP = 0, REC_RING = 1, REC_DEFER = 2, REC_REFIRE = 3 };
+enum { REC_SKIP = 0, REC_RING = 1, REC_DEFER = 2, REC_REFIRE = 3, REC_LATE = 4 };
 template <int AGG>
 __device__ __forceinline__ int classify(const IngestArgs& a, int64_t ts, int64_t v, uint32_t& pos, int64_t& pane,
                                         int64_t& c0, int64_t& c1, unsigned long long& late,
                                         unsigned long long& flags) {
     if (ts == INT64_MIN) { flags |= GW_DF_NO_TS; return REC_SKIP; }
-    if (ts < a.t_late) {
-        if (a.late_exact) late++;
-        else flags |= GW_DF_RANGE;
+    if (ts < a.t_late) {  // every window of the record is late: isSkippedElement && isElementLate
+        if (!a.late_exact) { flags |= GW_DF_RANGE; return REC_SKIP; }
+        if (a.lo_key) return REC_LATE;  // sideOutputLateData: the record goes to the side output
+        late++;                         // numLateRecordsDropped (WindowOperator.java:440-446)
         return REC_SKIP;
     }
     const uint64_t R = (uint64_t)a.t.ring;
@@ -109,6 +110,17 @@ __device__ __forceinline__ void defer_write(const IngestArgs& a, bool defer, int
         a.d_pane[off] = pane;
         a.d_a0[off] = c0;
         a.d_a1[off] = c1;
+    }
+}
+
+// Late record with a late-data side output: the record itself, as processElement passes it
+// to sideOutput (WindowOperator.java:440-446, 587-588).
+__device__ __forceinline__ void late_write(const IngestArgs& a, bool lo, int64_t key, int64_t i) {
+    const unsigned long long off = wave_reserve(&a.st->n_late_out, lo);
+    if (lo) {
+        a.lo_key[off] = key;
+        a.lo_ts[off] = a.ts[i];
+        a.lo_val[off] = a.val ? a.val[i] : 0;
     }
 }
 
@@ -218,6 +230,7 @@ __global__ void __launch_bounds__(256) k_ingest(IngestArgs a) {
             defer_write(a, state[u] == REC_DEFER, key[u], pane[u], c0[u], c1[u]);
             refire_write(a, state[u] == REC_REFIRE, key[u], pane[u], c0[u], c1[u],
                          base + (int64_t)u * blockDim.x + threadIdx.x);
+            if (a.lo_key) late_write(a, state[u] == REC_LATE, key[u], base + (int64_t)u * blockDim.x + threadIdx.x);
         }
     }
     block_commit(a.st, late, ins, flags, occ);
@@ -304,6 +317,7 @@ __global__ void __launch_bounds__(256) k_ingest_preagg(IngestArgs a) {
             }
             defer_write(a, state == REC_DEFER, key, pane, c0, c1);
             refire_write(a, state == REC_REFIRE, key, pane, c0, c1, i);
+            if (a.lo_key) late_write(a, state == REC_LATE, key, i);
         }
         __syncthreads();
         for (int j = threadIdx.x; j < kLdsCells; j += blockDim.x) {
@@ -487,6 +501,7 @@ __global__ void __launch_bounds__(kPartThreads) k_rgn_p1(IngestArgs a) {
         }
         defer_write(a, st == REC_DEFER, key[it], pane, c0[it], c1[it]);
         refire_write(a, st == REC_REFIRE, key[it], pane, c0[it], c1[it], i);
+        if (a.lo_key) late_write(a, st == REC_LATE, key[it], i);
         if (bk[it] >= 0) rank[it] = atomicAdd(&lh[bk[it]], 1u);
     }
     occ = wave_ior(occ);

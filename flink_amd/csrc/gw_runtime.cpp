@@ -196,6 +196,12 @@ struct gw_handle {
     void* rf_sort = nullptr;        // sort keys / payloads / scratch
     int64_t rf_sort_bytes = 0;
 
+    // late-data side output (GW_FLAG_LATE_SIDE_OUTPUT): key | ts | value, [lo_head, n_late_out) pending
+    int64_t* lo_buf[3] = {nullptr, nullptr, nullptr};
+    int64_t lo_cap = 0, lo_head = 0;
+    int64_t lo_bound = 0;  // records ingested since the buffer was last emptied (bounds n_late_out)
+    bool late_out() const { return (cfg.flags & GW_FLAG_LATE_SIDE_OUTPUT) != 0; }
+
     // event-time state
     int64_t wm = INT64_MIN;
     i128 fired_k = 0;  // first window index not yet fired
@@ -599,6 +605,26 @@ struct gw_handle {
         return GW_OK;
     }
 
+    int ensure_late(int64_t need) {
+        if (need <= lo_cap) return GW_OK;
+        int rc;
+        if ((rc = refresh())) return rc;  // exact n_late_out before copying
+        const int64_t used = (int64_t)h_st->n_late_out;
+        const int64_t nc = std::max<int64_t>(need + need / 2, 1 << 16);
+        for (int c = 0; c < 3; ++c) {
+            int64_t* nb;
+            HIPCHECK(hipMalloc((void**)&nb, nc * 8));
+            if (lo_buf[c] && used) HIPCHECK(hipMemcpyAsync(nb, lo_buf[c], used * 8, hipMemcpyDeviceToDevice, stream));
+            if (lo_buf[c]) {
+                HIPCHECK(hipStreamSynchronize(stream));
+                hipFree(lo_buf[c]);
+            }
+            lo_buf[c] = nb;
+        }
+        lo_cap = nc;
+        return GW_OK;
+    }
+
     // Window index bounds under allowed lateness (WindowOperator.cleanupTime :670-677,
     // isWindowLate :609-612): window k is late at watermark w when max timestamp + lateness
     // <= w (a cleanup time beyond Long.MAX_VALUE is Long.MAX_VALUE: late only at the last
@@ -877,6 +903,11 @@ struct gw_handle {
         a.d_key = dk[cur]; a.d_pane = dp[cur]; a.d_a0 = da0[cur]; a.d_a1 = da1[cur];
         a.st = d_st;
         // panes up to the last one of the last fired window re-fire (lateness > 0)
+        if (late_out() && exact) {
+            int rc;
+            if (nrec && (rc = ensure_late(lo_bound + nrec))) return rc;
+            a.lo_key = lo_buf[0]; a.lo_ts = lo_buf[1]; a.lo_val = lo_buf[2];
+        }
         const i128 hi = (fired_k - 1) * m + n - 1;
         if (late_k < fired_k && hi >= pl) {
             a.q_refire = (uint64_t)(hi - pl + 1);
@@ -1022,6 +1053,7 @@ struct gw_handle {
         stats.events_in += nrec;
         stats.batches++;
         seq_ctr += nrec;
+        if (a.lo_key) lo_bound += nrec;
         if (a.q_refire) rf_bound += nrec;
         if (path == 2 && nseg) {  // buffered P1: no host sync (it writes no table cell)
             if ((rc = lazy_status(nrec))) return rc;
@@ -1760,6 +1792,8 @@ int gw_destroy(gw_handle* h) {
     if (h->o_key) { hipFree(h->o_key); hipFree(h->o_start); hipFree(h->o_end); hipFree(h->o_res); }
     for (int c = 0; c < 5; ++c)
         if (h->rf[c]) hipFree(h->rf[c]);
+    for (int c = 0; c < 3; ++c)
+        if (h->lo_buf[c]) hipFree(h->lo_buf[c]);
     if (h->rf_sort) hipFree(h->rf_sort);
     h->free_stage();
     h->free_region();
@@ -2255,6 +2289,45 @@ int gw_clear_rows(gw_handle* h) {
     if (h->session) return session_clear_rows(h->sess, h->err);
     if (h->h_st->rows == 0) return GW_OK;  // rows only grow in a fire, which refreshes h_st
     return h->set_field(offsetof(DevStatus, rows), 0);
+}
+
+int gw_pending_late(gw_handle* h, int64_t* n) {
+    if (!h || !n) return GW_E_INVALID;
+    *n = 0;
+    if (!(h->cfg.flags & GW_FLAG_LATE_SIDE_OUTPUT)) return GW_OK;
+    if (h->session) return session_pending_late(h->sess, n, h->err);
+    int rc = h->refresh();
+    if (rc) return rc;
+    *n = (int64_t)h->h_st->n_late_out - h->lo_head;
+    return GW_OK;
+}
+
+int gw_drain_late(gw_handle* h, int64_t* key, int64_t* ts, void* value, int64_t cap, int64_t* n) {
+    if (!h || !n) return GW_E_INVALID;
+    *n = 0;
+    if (!(h->cfg.flags & GW_FLAG_LATE_SIDE_OUTPUT)) return GW_OK;
+    hipSetDevice(h->cfg.device);
+    if (h->session) return session_drain_late(h->sess, key, ts, (int64_t*)value, cap, n, h->err);
+    int64_t pending;
+    int rc = gw_pending_late(h, &pending);
+    if (rc) return rc;
+    const int64_t c = std::min(cap, pending), o = h->lo_head;
+    int64_t* dst[3] = {key, ts, (int64_t*)value};
+    for (int q = 0; q < 3 && c > 0; ++q) {
+        if (!dst[q]) continue;
+        hipError_t e = hipMemcpyAsync(dst[q], h->lo_buf[q] + o, c * 8, hipMemcpyDeviceToHost, h->stream);
+        if (e != hipSuccess) return h->fail(GW_E_DEVICE, "D2H late records: %s", hipGetErrorString(e));
+    }
+    hipError_t e = hipStreamSynchronize(h->stream);
+    if (e != hipSuccess) return h->fail(GW_E_DEVICE, "D2H late records: %s", hipGetErrorString(e));
+    *n = c;
+    h->lo_head += c;
+    if (c == pending) {  // emptied: restart the buffer
+        h->lo_head = 0;
+        h->lo_bound = 0;
+        if (h->h_st->n_late_out && (rc = h->set_field(offsetof(DevStatus, n_late_out), 0))) return rc;
+    }
+    return c < pending ? GW_E_OUTPUT_FULL : GW_OK;
 }
 
 int64_t gw_late_dropped(const gw_handle* h) {

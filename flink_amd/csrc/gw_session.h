@@ -27,6 +27,9 @@ int session_collect(SessionState* s, int32_t kg_lo, int32_t kg_hi, std::vector<i
 int session_restore(SessionState* s, const int64_t* ent, int64_t n, std::string& err);
 int session_clear_rows(SessionState* s, std::string& err);
 int64_t session_late(SessionState* s);
+int session_pending_late(SessionState* s, int64_t* n, std::string& err);
+int session_drain_late(SessionState* s, int64_t* key, int64_t* ts, int64_t* val, int64_t cap, int64_t* n,
+                       std::string& err);
 void session_stats(SessionState* s, gw_stats* out);
 void session_enable_timing(SessionState* s, bool on);
 int session_kernel_time(SessionState* s, int which, double* ms, int64_t* launches);

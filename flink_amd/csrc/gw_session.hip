@@ -49,6 +49,11 @@ struct SegArgs {
     int64_t* o_end;
     int64_t* o_res;
     TableView t;            // ring = K sessions per slot, words = words per session
+    const int64_t* ts;      // the batch's columns (late side output)
+    const int64_t* key;
+    int64_t* lo_key;        // late side output (GW_FLAG_LATE_SIDE_OUTPUT), append at st->n_late_out;
+    int64_t* lo_ts;         //   nullptr: late elements are counted (numLateRecordsDropped)
+    int64_t* lo_val;
     const uint32_t* retry_in;
     int64_t n_retry_in;
     uint32_t* retry_out;    // appended at st->overflow
@@ -210,7 +215,7 @@ __device__ void seg_process(const SegArgs& a, int64_t i) {
         // that overflows is retried after widening and must not emit twice).
         Sess init[kMaxLocalSess];
         const int cnt0 = cnt;
-        const int passes = a.lateness > 0 ? 2 : 1;
+        const int passes = (a.lateness > 0 || a.lo_key) ? 2 : 1;
         for (int q = 0; q < cnt0 && passes == 2; ++q) init[q] = cur_list[q];
         for (int pass = 0; pass < passes; ++pass) {
         const bool emit = pass == 1;
@@ -242,7 +247,16 @@ __device__ void seg_process(const SegArgs& a, int64_t i) {
             int64_t c0, c1;
             record_cell(AGG, a.val ? a.val[bp] : 0, c0, c1);
             if (lo < 0) {
-                if (cleaned_at(we, a.lateness, a.wm)) { late++; continue; }  // isWindowLate -> dropped
+                if (cleaned_at(we, a.lateness, a.wm)) {  // isWindowLate: skipped, and the element is late
+                    if (!a.lo_key) { late++; continue; }
+                    if (emit) {  // sideOutput(element) (WindowOperator.java:440-446, 587-588)
+                        const unsigned long long o = atomicAdd(&a.st->n_late_out, 1ull);
+                        a.lo_key[o] = a.key[bp];
+                        a.lo_ts[o] = a.ts[bp];
+                        a.lo_val[o] = a.val ? a.val[bp] : 0;
+                    }
+                    continue;
+                }
                 if (cnt == kMaxLocalSess) { ok = false; break; }
                 int q = cnt;
                 while (q > 0 && cur_list[q - 1].s > ws) { cur_list[q] = cur_list[q - 1]; --q; }
@@ -656,6 +670,8 @@ struct SessionState {
     bool timing = false;
     bool count_mode = false;  // GW_COUNT_TUMBLING / GW_COUNT_SLIDING (same slot table and row plumbing)
     CountGeom cg{};
+    int64_t* lo_buf[3] = {nullptr, nullptr, nullptr};  // late side output: key | ts | value
+    int64_t lo_cap = 0, lo_head = 0;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pending[2], ev_pool;
     double t_total[2] = {0, 0};
     int64_t t_count[2] = {0, 0};
@@ -771,6 +787,7 @@ void session_destroy(SessionState* s) {
     hipFree(s->k0); hipFree(s->k1); hipFree(s->v0); hipFree(s->v1); hipFree(s->r0); hipFree(s->r1);
     hipFree(s->scratch);
     hipFree(s->o_key); hipFree(s->o_start); hipFree(s->o_end); hipFree(s->o_res);
+    for (auto* p : s->lo_buf) hipFree(p);
     for (int w = 0; w < 2; ++w) for (auto& p : s->ev_pending[w]) s->ev_pool.push_back(p);
     for (auto& p : s->ev_pool) { hipEventDestroy(p.first); hipEventDestroy(p.second); }
     delete s;
@@ -837,6 +854,48 @@ static int ensure_rows(SessionState* s, int64_t need, std::string& err) {
     s->o_key = nb[0]; s->o_start = nb[1]; s->o_end = nb[2]; s->o_res = nb[3];
     s->o_cap = c;
     return GW_OK;
+}
+
+static int ensure_late(SessionState* s, int64_t need, std::string& err) {
+    if (need <= s->lo_cap) return GW_OK;
+    const int64_t used = (int64_t)s->h_st->n_late_out;  // exact: the session path is synchronous
+    const int64_t c = std::max<int64_t>(need + need / 2, 1 << 16);
+    for (int q = 0; q < 3; ++q) {
+        int64_t* nb;
+        SCHECK(hipMalloc((void**)&nb, c * 8));
+        if (s->lo_buf[q] && used) SCHECK(hipMemcpyAsync(nb, s->lo_buf[q], used * 8, hipMemcpyDeviceToDevice, s->stream));
+        SCHECK(hipStreamSynchronize(s->stream));
+        hipFree(s->lo_buf[q]);
+        s->lo_buf[q] = nb;
+    }
+    s->lo_cap = c;
+    return GW_OK;
+}
+
+int session_pending_late(SessionState* s, int64_t* n, std::string& err) {
+    int rc = session_refresh(s, err);
+    if (rc) return rc;
+    *n = (int64_t)s->h_st->n_late_out - s->lo_head;
+    return GW_OK;
+}
+
+int session_drain_late(SessionState* s, int64_t* key, int64_t* ts, int64_t* val, int64_t cap, int64_t* n,
+                       std::string& err) {
+    int64_t pending;
+    int rc = session_pending_late(s, &pending, err);
+    if (rc) return rc;
+    const int64_t c = std::min(cap, pending), o = s->lo_head;
+    int64_t* dst[3] = {key, ts, val};
+    for (int q = 0; q < 3 && c > 0; ++q)
+        if (dst[q]) SCHECK(hipMemcpyAsync(dst[q], s->lo_buf[q] + o, c * 8, hipMemcpyDeviceToHost, s->stream));
+    SCHECK(hipStreamSynchronize(s->stream));
+    *n = c;
+    s->lo_head += c;
+    if (c == pending) {
+        s->lo_head = 0;
+        if ((rc = set_word(s, offsetof(DevStatus, n_late_out), 0, err))) return rc;
+    }
+    return c < pending ? GW_E_OUTPUT_FULL : GW_OK;
 }
 
 // Count windows: slot per record, stable grouping by slot, one in-order fold per key.
@@ -938,6 +997,12 @@ int session_ingest(SessionState* s, int64_t n, const int64_t* key, const int64_t
     if (a.lateness > 0) {  // an element fires at most one window at once
         if ((rc = ensure_rows(s, (int64_t)s->h_st->rows + n, err))) return rc;
         a.o_key = s->o_key; a.o_start = s->o_start; a.o_end = s->o_end; a.o_res = s->o_res;
+    }
+    a.ts = ts;
+    a.key = key;
+    if (s->cfg.flags & GW_FLAG_LATE_SIDE_OUTPUT) {
+        if ((rc = ensure_late(s, (int64_t)s->h_st->n_late_out + n, err))) return rc;
+        a.lo_key = s->lo_buf[0]; a.lo_ts = s->lo_buf[1]; a.lo_val = s->lo_buf[2];
     }
     uint32_t* rin = s->r0;
     uint32_t* rout = s->r1;

@@ -481,6 +481,18 @@ class GpuWindowOperator:
         N.check(rc, self._h)
         return [x.value for x in p], n.value
 
+    def drain_late(self):
+        """The late-data side output (flags=FLAG_LATE_SIDE_OUTPUT, WindowedStream.sideOutputLateData):
+        the late records since the last call, as (key, timestamp, value bits) numpy columns."""
+        n = ctypes.c_int64(0)
+        N.check(N.lib().gw_pending_late(self._h, ctypes.byref(n)), self._h)
+        k, t, v = (np.empty(n.value, np.int64) for _ in range(3))
+        got = ctypes.c_int64(0)
+        if n.value:
+            N.check(N.lib().gw_drain_late(self._h, _ptr(k), _ptr(t), _ptr(v), n.value, ctypes.byref(got)), self._h)
+            assert got.value == n.value
+        return k, t, v
+
     @property
     def num_late_records_dropped(self) -> int:
         return N.lib().gw_late_dropped(self._h)

@@ -122,6 +122,8 @@ typedef struct gw_config {
 #define GW_FLAG_NO_REGION         16 /* never use the region-bucketed ingest path       */
 #define GW_FLAG_NO_BUFFER         32 /* region path: apply every batch at once instead of
                                         buffering pass-1 segments until the next fire    */
+#define GW_FLAG_LATE_SIDE_OUTPUT  64 /* WindowedStream.sideOutputLateData: late records go to
+                                        gw_drain_late instead of numLateRecordsDropped    */
 
 typedef struct gw_handle gw_handle;
 
@@ -277,6 +279,15 @@ int  gw_rows_device(gw_handle* h, const int64_t** d_key, const int64_t** d_start
 int  gw_clear_rows(gw_handle* h);
 
 int64_t gw_late_dropped(const gw_handle* h);
+/* Late-data side output (GW_FLAG_LATE_SIDE_OUTPUT; WindowedStream.sideOutputLateData, RS/api/
+ * datastream/WindowedStream.java): the records WindowOperator.processElement skips as late
+ * (isSkippedElement && isElementLate, WindowOperator.java:440-446) are kept, as the element
+ * itself (key, timestamp, value bits), instead of being counted in numLateRecordsDropped, and
+ * handed out here (sideOutput :587-588).  A record is pending from the ingest call that saw
+ * it; gw_drain_late copies up to cap records and removes them (GW_E_OUTPUT_FULL if more
+ * remain).  Without the flag both report 0 records. */
+int  gw_pending_late(gw_handle* h, int64_t* n);
+int  gw_drain_late(gw_handle* h, int64_t* key, int64_t* ts, void* value, int64_t cap, int64_t* n);
 int  gw_get_stats(const gw_handle* h, gw_stats* out);
 int  gw_synchronize(gw_handle* h);
 /* hipStream_t the handle launches on (for ordering / event timing by callers). */

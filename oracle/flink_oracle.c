@@ -392,6 +392,8 @@ struct wo_op {
     int64_t nsets, cap_sets;
     int64_t *ok, *os, *oe, *orr;
     int64_t on, ocap, ohead;
+    int64_t *lk, *lt, *lv;  /* late side output (GW_FLAG_LATE_SIDE_OUTPUT): the elements themselves */
+    int64_t ln, lcap;
     map_t cmap;   /* count windows: (key,0,0,0) -> index into cws */
     struct cw_s* cws;
     int64_t ncws, cap_cws;
@@ -881,7 +883,23 @@ int wo_process_element(wo_op* op, int64_t key, int64_t ts, int64_t v) {
             if (rc == GW_OK) rc = register_cleanup_timer(op, key, pws[w], pwe[w]);
         }
     }
-    if (rc == GW_OK && skipped && is_element_late(op, ts)) op->late++;
+    /* WindowOperator.java:440-446: a skipped late element goes to the late-data side output
+     * when one is set (sideOutput :587-588), else it is counted in numLateRecordsDropped */
+    if (rc == GW_OK && skipped && is_element_late(op, ts)) {
+        if (op->c.flags & GW_FLAG_LATE_SIDE_OUTPUT) {
+            if (op->ln == op->lcap) {
+                int64_t nc = op->lcap ? op->lcap * 2 : 256;
+                op->lk = (int64_t*)realloc(op->lk, 8 * (size_t)nc);
+                op->lt = (int64_t*)realloc(op->lt, 8 * (size_t)nc);
+                op->lv = (int64_t*)realloc(op->lv, 8 * (size_t)nc);
+                op->lcap = nc;
+            }
+            op->lk[op->ln] = key; op->lt[op->ln] = ts; op->lv[op->ln] = v;
+            op->ln++;
+        } else {
+            op->late++;
+        }
+    }
 out:
     if (pws != ws) free(pws);
     return rc;
@@ -972,7 +990,19 @@ void wo_destroy(wo_op* op) {
     free(op->freel);
     free(op->heap);
     free(op->ok); free(op->os); free(op->oe); free(op->orr);
+    free(op->lk); free(op->lt); free(op->lv);
     free(op);
+}
+
+int64_t wo_late_output_count(const wo_op* op) { return op->ln; }
+int64_t wo_drain_late(wo_op* op, int64_t* key, int64_t* ts, int64_t* v, int64_t cap) {
+    int64_t n = op->ln < cap ? op->ln : cap;
+    for (int64_t i = 0; i < n; i++) { key[i] = op->lk[i]; ts[i] = op->lt[i]; v[i] = op->lv[i]; }
+    memmove(op->lk, op->lk + n, 8 * (size_t)(op->ln - n));
+    memmove(op->lt, op->lt + n, 8 * (size_t)(op->ln - n));
+    memmove(op->lv, op->lv + n, 8 * (size_t)(op->ln - n));
+    op->ln -= n;
+    return n;
 }
 
 int64_t wo_output_count(const wo_op* op) { return op->on - op->ohead; }

@@ -57,6 +57,9 @@ int64_t wo_output_count(const wo_op* op);
 int64_t wo_drain(wo_op* op, int64_t* key, int64_t* start, int64_t* end, int64_t* result_bits,
                  int64_t cap);
 int64_t wo_late_dropped(const wo_op* op);
+/* Late-data side output (config flag GW_FLAG_LATE_SIDE_OUTPUT): the skipped late elements. */
+int64_t wo_late_output_count(const wo_op* op);
+int64_t wo_drain_late(wo_op* op, int64_t* key, int64_t* ts, int64_t* value_bits, int64_t cap);
 int64_t wo_current_watermark(const wo_op* op);
 int64_t wo_state_entries(const wo_op* op);
 int64_t wo_timer_count(const wo_op* op);

@@ -123,7 +123,8 @@ def lib() -> ctypes.CDLL:
             ("wo_process_batch", ctypes.c_int, [p, i64, p, p, p]),
             ("wo_process_watermark", ctypes.c_int, [p, i64]),
             ("wo_output_count", i64, [p]), ("wo_drain", i64, [p, p, p, p, p, i64]),
-            ("wo_late_dropped", i64, [p]), ("wo_current_watermark", i64, [p]),
+            ("wo_late_dropped", i64, [p]), ("wo_late_output_count", i64, [p]),
+            ("wo_drain_late", i64, [p, p, p, p, i64]), ("wo_current_watermark", i64, [p]),
             ("wo_state_entries", i64, [p]), ("wo_timer_count", i64, [p]),
             ("wo_session_merges", i64, [p]), ("wo_last_error", ctypes.c_char_p, [p]),
             ("wo_decode_stream", ctypes.c_int, [p, i64, ctypes.POINTER(GwRecordLayout), p, p, p, i64, p, p, i64,
@@ -217,6 +218,14 @@ class OracleOperator:
     @property
     def late_dropped(self) -> int:
         return lib().wo_late_dropped(self._h)
+
+    def drain_late(self):
+        """The late-data side output so far: (key, ts, value_bits) columns."""
+        n = lib().wo_late_output_count(self._h)
+        k, t, v = (np.empty(n, np.int64) for _ in range(3))
+        got = lib().wo_drain_late(self._h, _p(k), _p(t), _p(v), n)
+        assert got == n
+        return k, t, v
 
     @property
     def state_entries(self) -> int:

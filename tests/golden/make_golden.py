@@ -177,6 +177,7 @@ ops_tests.append({
             ["e", "key2", 1, 1997], ["w", 6000, [["key2", 1, 1999, None, None]]],
             ["e", "key2", 1, 1998], ["w", 7000, []]],
     "late": 1,
+    "side": [["key2", 1, 1998]],  # lateOutputTag set (:2066-2067), lateExpected (:2118)
 })
 # testCleanupTimeOverflow (:2139-2248): Tumbling 1000 ms, lateness 2000,
 # ts = Long.MAX_VALUE - 1750 -> window [MAX-1807, MAX-807), maxTs = MAX - 808.
@@ -203,7 +204,7 @@ ops_tests.append({"name": "session_lateness_zero", "source": WOT + ":2571-2668",
                   "config": {"assigner": "session", "gap": 3000, "agg": "sum_i32"},
                   "ops": _sl_in + [["e", "key2", 1, 10000], ["e", "key2", 1, 14500],
                                    ["w", 20000, [["key2", 1, 17499, 14500, 17500]]], ["w", 100000, []]],
-                  "late": 1})
+                  "late": 1, "side": [["key2", 1, 10000]]})
 # testNotSideOutputDueToLatenessSessionWithLateness (:2766-2879): lateness 10 ms; 10000
 # merges into the fired (11600, 14600) session and fires (10000, 14600) at once.
 ops_tests.append({"name": "session_lateness_10", "source": WOT + ":2766-2879",
@@ -211,7 +212,7 @@ ops_tests.append({"name": "session_lateness_10", "source": WOT + ":2766-2879",
                   "ops": _sl_in + [["e", "key2", 1, 10000], ["e", "key2", 1, 14500],
                                    ["w", 20000, [["key2", 2, 14599, 10000, 14600],
                                                  ["key2", 3, 17499, 10000, 17500]]], ["w", 100000, []]],
-                  "late": 0})
+                  "late": 0, "side": []})
 # testNotSideOutputDueToLatenessSessionWithHugeLateness (:2984-3083): lateness 10 s; the
 # fired (1000, 11500) session is still kept, so 10000 merges everything into (1000, 14600).
 ops_tests.append({"name": "session_lateness_huge", "source": WOT + ":2984-3083",
@@ -219,7 +220,7 @@ ops_tests.append({"name": "session_lateness_huge", "source": WOT + ":2984-3083",
                   "ops": _sl_in + [["e", "key2", 1, 10000], ["e", "key2", 1, 14500],
                                    ["w", 20000, [["key2", 7, 14599, 1000, 14600],
                                                  ["key2", 8, 17499, 1000, 17500]]], ["w", 100000, []]],
-                  "late": 0})
+                  "late": 0, "side": []})
 # testDropDueToLatenessSessionWithLatenessPurgingTrigger (:2670-2765) and
 # testNotSideOutputDueToLatenessSessionWithHugeLatenessPurgingTrigger (:2881-2983):
 # PurgingTrigger(EventTimeTrigger); a fired session keeps an empty state until cleanup.
@@ -231,7 +232,43 @@ for _name, _src, _lat, _start in (("session_lateness_10_purging", ":2670-2765", 
                       "ops": _sl_in + [["e", "key2", 1, 10000], ["e", "key2", 1, 14500],
                                        ["w", 20000, [["key2", 1, 14599, _start, 14600],
                                                      ["key2", 1, 17499, _start, 17500]]], ["w", 100000, []]],
-                      "late": 0})
+                      "late": 0, **({"side": []} if _lat == 10000 else {})})
+# Late-data side output (WindowedStream.sideOutputLateData; WindowOperator.java:440-446):
+# "side" lists the records the side output holds [key, value, timestamp]; without the side
+# output they are counted in numLateRecordsDropped ("late").
+# testSideOutputDueToLatenessTumbling (:2249-2346): Tumbling 2 s, lateness 0, SumReducer.
+ops_tests.append({
+    "name": "side_output_tumbling", "source": WOT + ":2249-2346",
+    "config": {"assigner": "tumbling", "size": 2000, "agg": "sum_i32"},
+    "ops": [["e", "key2", 1, 1000], ["w", 1985, []],
+            ["e", "key2", 1, 1980], ["w", 1999, [["key2", 2, 1999, None, None]]],
+            ["e", "key2", 1, 1998], ["e", "key2", 1, 2001], ["w", 2999, []],
+            ["w", 3999, [["key2", 1, 3999, None, None]]]],
+    "late": 1, "side": [["key2", 1, 1998]],
+})
+# testSideOutputDueToLatenessSliding (:2348-2462): Sliding 3 s / 1 s, lateness 0; the 2400
+# elements still fall into the windows ending at 3999 and 4999 (not skipped).
+ops_tests.append({
+    "name": "side_output_sliding", "source": WOT + ":2348-2462",
+    "config": {"assigner": "sliding", "size": 3000, "slide": 1000, "agg": "sum_i32"},
+    "ops": [["e", "key2", 1, 1000], ["w", 1999, [["key2", 1, 1999, None, None]]],
+            ["e", "key2", 1, 2000], ["w", 3000, [["key2", 2, 2999, None, None]]],
+            ["e", "key1", 1, 3001], ["e", "key2", 1, 2400], ["e", "key2", 1, 2400], ["e", "key1", 1, 3001],
+            ["e", "key2", 1, 3900],
+            ["w", 6000, [["key2", 5, 3999, None, None], ["key1", 2, 3999, None, None],
+                         ["key2", 4, 4999, None, None], ["key1", 2, 4999, None, None],
+                         ["key2", 1, 5999, None, None], ["key1", 2, 5999, None, None]]],
+            ["e", "key1", 1, 3001], ["w", 25000, []]],
+    "late": 1, "side": [["key1", 1, 3001]],
+})
+# testSideOutputDueToLatenessSessionZeroLatenessPurgingTrigger (:2465-2569): gap 3 s,
+# lateness 0, PurgingTrigger(EventTimeTrigger).
+ops_tests.append({"name": "side_output_session_zero_lateness_purging", "source": WOT + ":2465-2569",
+                  "config": {"assigner": "session", "gap": 3000, "agg": "sum_i32",
+                             "trigger": "purging_event_time"},
+                  "ops": _sl_in + [["e", "key2", 1, 10000], ["e", "key2", 1, 10100], ["e", "key2", 1, 14500],
+                                   ["w", 20000, [["key2", 1, 17499, 14500, 17500]]], ["w", 100000, []]],
+                  "late": 2, "side": [["key2", 1, 10000], ["key2", 1, 10100]]})
 # SessionWindowing example (flink-examples-streaming SessionWindowing.java:58-69, gap 3 ms
 # at :94, sum(2)) with expected output SessionWindowingData.java:23-24.  The tuple's f1
 # (first element's timestamp) equals the session start for this input.

@@ -44,10 +44,13 @@ def bits_to_result(bits, is_double):
     return int(bits)
 
 
-def replay(test, make_backend, is_double=False):
-    """Drive a backend through one golden harness test; returns list of mismatches."""
+def replay(test, make_backend, is_double=False, side_output=False):
+    """Drive a backend through one golden harness test; returns list of mismatches.
+    side_output: run with the late-data side output (WindowedStream.sideOutputLateData) and
+    compare it with the test's "side" records; without it those records are counted in
+    numLateRecordsDropped ("late")."""
     keys = KeyDictionary()
-    be = make_backend(test["config"])
+    be = make_backend(test["config"], side_output=side_output) if side_output else make_backend(test["config"])
     errors = []
     pin_window = any(row[3] is not None for op in test["ops"] if op[0] == "w" for row in op[2])
     for op in test["ops"]:
@@ -70,7 +73,15 @@ def replay(test, make_backend, is_double=False):
             e_cmp = sorted(tuple(x)[:n_] for x in expected)
             if g_cmp != e_cmp:
                 errors.append(f"wm {wm}: got {g_cmp} expected {e_cmp}")
-    if be.late_dropped != test.get("late", 0):
+    if side_output:
+        k, t, v = be.drain_late()
+        got = sorted((keys.names[int(k[i])], int(v[i]), int(t[i])) for i in range(len(k)))
+        exp = sorted(tuple(x) for x in test["side"])
+        if got != exp:
+            errors.append(f"side output {got} expected {exp}")
+        if be.late_dropped != 0:
+            errors.append(f"late_dropped {be.late_dropped} != 0 with a side output")
+    elif be.late_dropped != test.get("late", 0):
         errors.append(f"late_dropped {be.late_dropped} != {test.get('late', 0)}")
     return errors
 

@@ -168,3 +168,50 @@ def test_session_lateness_purging_trigger_vs_oracle(oracle_lib, lateness, agg):
     o, olate = run_oracle(oracle_lib, kw, keys, ts, vals, batches)
     assert glate == olate
     assert _cmp(g, o, agg) == []
+
+
+# ------------------------------------------------------------------ late-data side output
+# WindowedStream.sideOutputLateData: a skipped late element goes to the side output instead
+# of numLateRecordsDropped (WindowOperator.java:440-446, sideOutput :587-588).  Rows and the
+# side output are compared with the oracle per watermark; nothing is counted as dropped.
+@pytest.mark.parametrize("agg", ["sum_i64", "avg_f64"])
+@pytest.mark.parametrize("kw", [
+    dict(assigner="tumbling", size=1000, slide=1000),
+    dict(assigner="sliding", size=1000, slide=300, offset=-50),
+    dict(assigner="sliding", size=1000, slide=250, lateness=700),
+    dict(assigner="session", gap=300),
+    dict(assigner="session", gap=800, lateness=500),
+], ids=lambda c: "-".join(str(v) for v in c.values()))
+@pytest.mark.parametrize("flags", [0, N.FLAG_FORCE_REGION], ids=["auto", "region"])
+def test_late_side_output_vs_oracle(oracle_lib, kw, agg, flags):
+    if flags and kw["assigner"] == "session":
+        pytest.skip("sessions have one ingest path")
+    o = oracle_lib
+    kw = dict(kw, agg=agg)
+    keys, ts, vals, batches = random_stream(seed=zlib.crc32(f"so{kw}".encode()) & 0xffff, n=20000, num_keys=80,
+                                            n_batches=30, disorder=4000, wm_lag=200, agg=agg)
+    op = gpu_operator(kw, flags=flags | N.FLAG_LATE_SIDE_OUTPUT)
+    ora = o.OracleOperator(o.make_config(**kw, flags=N.FLAG_LATE_SIDE_OUTPUT))
+    vb = vals.view(np.int64) if vals.dtype == np.float64 else vals
+    g_rows, o_rows, g_side, o_side = [], [], [], []
+    for lo, hi, wm in batches:
+        op.process_batch(keys[lo:hi], ts[lo:hi], vals[lo:hi])
+        op.advance_watermark(wm)
+        k, s, e, r = op.drain()
+        g_rows.append((k, s, e, r.view(np.int64)))
+        g_side.append(op.drain_late())
+        ora.process_batch(keys[lo:hi], ts[lo:hi], vb[lo:hi])
+        ora.process_watermark(wm)
+        o_rows.append(ora.drain())
+        o_side.append(ora.drain_late())
+    assert op.num_late_records_dropped == 0 and ora.late_dropped == 0
+    assert _cmp(g_rows, o_rows, agg) == []
+    n_side = 0
+    for b, (gs, os_) in enumerate(zip(g_side, o_side)):
+        got = sorted(zip(*[c.tolist() for c in gs]))
+        exp = sorted(zip(*[c.tolist() for c in os_]))
+        assert got == exp, f"side output differs at watermark #{b}"
+        n_side += len(exp)
+    assert n_side > 0
+    op.close()
+    ora.close()

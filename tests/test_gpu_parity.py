@@ -26,9 +26,11 @@ def _cmp(gpu, ora, agg):
 
 # ------------------------------------------------------------------ golden vectors
 class GpuBackend:
-    def __init__(self, cfg):
+    def __init__(self, cfg, side_output=False):
         self.kw = config_kwargs(cfg)
-        self.op = gpu_operator(self.kw)
+        self.flags = N.FLAG_LATE_SIDE_OUTPUT if side_output else 0
+        self.op = gpu_operator(self.kw, flags=self.flags)
+        self.side = []
         self.k, self.t, self.v = [], [], []
 
     def process_element(self, k, ts, v):
@@ -46,17 +48,21 @@ class GpuBackend:
         return k, s, e, r.view(np.int64)
 
     def snapshot_restore(self):
-        if self.kw.get("lateness", 0) > 0:
-            return  # snapshots with allowed lateness > 0: not supported yet (GW_E_UNSUPPORTED)
         if self.k:
             self.op.process_batch(np.array(self.k, np.int64), np.array(self.t, np.int64),
                                   np.array(self.v, np.int64))
             self.k, self.t, self.v = [], [], []
         blob = self.op.snapshot_state()
         self.late_before = getattr(self, "late_before", 0) + self.op.num_late_records_dropped
+        if self.flags:
+            self.side.append(self.op.drain_late())
         self.op.close()
-        self.op = gpu_operator(self.kw)
+        self.op = gpu_operator(self.kw, flags=self.flags)
         self.op.initialize_state(blob)
+
+    def drain_late(self):
+        parts = self.side + [self.op.drain_late()]
+        return tuple(np.concatenate([p[c] for p in parts]) for c in range(3))
 
     @property
     def late_dropped(self):
@@ -66,6 +72,8 @@ class GpuBackend:
 @pytest.mark.parametrize("test", load_golden("operator_harness.json")["tests"], ids=lambda t: t["name"])
 def test_golden_harness_vectors(test):
     assert replay(test, GpuBackend) == []
+    if "side" in test:  # the reference test's own setting: late records on the side output
+        assert replay(test, GpuBackend, side_output=True) == []
 
 
 @pytest.mark.parametrize("assigner,size,slide", [("tumbling", 1000, 1000), ("sliding", 1000, 100)])

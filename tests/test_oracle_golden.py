@@ -5,6 +5,7 @@ import ctypes
 import numpy as np
 import pytest
 
+N_FLAG_LATE_SIDE_OUTPUT = 64  # include/gpuwin.h GW_FLAG_LATE_SIDE_OUTPUT
 from tests.harness import itcase_expected_sum, itcase_stream, load_golden, replay, config_kwargs
 
 
@@ -119,8 +120,9 @@ def test_operator_harness_vectors(oracle_lib, test):
     o = oracle_lib
 
     class Backend:
-        def __init__(self, cfg):
-            self.op = o.OracleOperator(o.make_config(**config_kwargs(cfg)))
+        def __init__(self, cfg, side_output=False):
+            self.op = o.OracleOperator(o.make_config(**config_kwargs(cfg),
+                                                     flags=N_FLAG_LATE_SIDE_OUTPUT if side_output else 0))
 
         def process_element(self, k, ts, v):
             self.op.process_element(k, ts, v)
@@ -135,7 +137,12 @@ def test_operator_harness_vectors(oracle_lib, test):
         def late_dropped(self):
             return self.op.late_dropped
 
+        def drain_late(self):
+            return self.op.drain_late()
+
     assert replay(test, Backend) == []
+    if "side" in test:  # the reference test's own setting: the late records on the side output
+        assert replay(test, Backend, side_output=True) == []
 
 
 @pytest.mark.parametrize("assigner,size,slide", [("tumbling", 1000, 1000), ("sliding", 1000, 100)])
