@@ -1148,8 +1148,11 @@ __device__ __forceinline__ int64_t floor_div_d(int64_t a, int64_t b) {
     return (a % b != 0 && ((a < 0) != (b < 0))) ? q - 1 : q;
 }
 
+constexpr int kRefireThreads = 64;
 template <int AGG>
-__global__ void __launch_bounds__(256) k_refire(RefireArgs a) {
+__global__ void __launch_bounds__(kRefireThreads) k_refire(RefireArgs a) {
+    // this interval's late records per ring position, per thread: LDS [R][threads] x 2
+    extern __shared__ int64_t rf_lds[];
     const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
     if (i >= a.n) return;
     const int64_t key = a.rf_key[a.order[i]];
@@ -1160,8 +1163,9 @@ __global__ void __launch_bounds__(256) k_refire(RefireArgs a) {
     const int64_t g = pt_find_ro(a.t, key);
     const uint64_t mask = g >= 0 ? presence<AGG>(a.t, g) : 0;
     const int64_t oh = (a.ov.head && g >= 0) ? a.ov.head[g] : -1;
-    int64_t run0[kMaxRing], run1[kMaxRing];  // this interval's late records per ring position
-    for (int q = 0; q < R; ++q) { run0[q] = id0; run1[q] = 0; }
+    int64_t* run0 = rf_lds + threadIdx.x;  // run0[q * kRefireThreads]
+    int64_t* run1 = rf_lds + R * kRefireThreads + threadIdx.x;
+    for (int q = 0; q < R; ++q) { run0[q * kRefireThreads] = id0; run1[q * kRefireThreads] = 0; }
     for (int64_t j = i; j < a.n && a.rf_key[a.order[j]] == key; ++j) {
         const uint32_t e = a.order[j];
         const int64_t p = a.rf_pane[e], c0 = a.rf_a0[e], c1 = a.rf_a1[e];
@@ -1170,7 +1174,7 @@ __global__ void __launch_bounds__(256) k_refire(RefireArgs a) {
         if (in_ring) {
             pos = a.b_pos + (int)(p - a.b);
             if (pos >= R) pos -= R;
-            fold_cell(AGG, run0[pos], run1[pos], c0, c1);
+            fold_cell(AGG, run0[pos * kRefireThreads], run1[pos * kRefireThreads], c0, c1);
         }
         const int64_t k0 = max(a.k_lo, floor_div_d(p - a.np, a.m) + 1), k1 = min(a.k_hi, floor_div_d(p, a.m));
         for (int64_t k = k0; k <= k1; ++k) {
@@ -1190,7 +1194,7 @@ __global__ void __launch_bounds__(256) k_refire(RefireArgs a) {
                         const int64_t* c = pt_cell(a.t, g, qp);
                         fold_cell(AGG, r0, r1, c[0], W == 2 ? c[1] : 0);
                     }
-                    fold_cell(AGG, r0, r1, run0[qp], run1[qp]);
+                    fold_cell(AGG, r0, r1, run0[qp * kRefireThreads], run1[qp * kRefireThreads]);
                 }
             }
             const unsigned long long o = atomicAdd(&a.st->rows, 1ull);
@@ -1579,7 +1583,9 @@ hipError_t launch_merge_deferred(const MergeArgs& a, hipStream_t s) {
 
 hipError_t launch_refire(const RefireArgs& a, hipStream_t s) {
     if (a.n == 0) return hipSuccess;
-#define L(A) hipLaunchKernelGGL(k_refire<A>, dim3((unsigned)((a.n + 255) / 256)), dim3(256), 0, s, a)
+    const size_t lds = (size_t)2 * a.t.ring * kRefireThreads * 8;
+#define L(A) hipLaunchKernelGGL(k_refire<A>, dim3((unsigned)((a.n + kRefireThreads - 1) / kRefireThreads)), \
+                                dim3(kRefireThreads), lds, s, a)
     GW_AGG_SWITCH(a.t.agg, L);
 #undef L
     return hipGetLastError();

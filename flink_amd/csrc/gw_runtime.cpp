@@ -1663,8 +1663,8 @@ static int validate(const gw_config* c, std::string& why) {
         }
         int64_t a = c->size, b = slide;
         while (b) { const int64_t t = a % b; a = b; b = t; }
-        if (c->size / a > kMaxRing) {
-            why = "count window size / gcd(size, slide) > 64 panes is not supported on the GPU path";
+        if (c->size / a > 4096) {
+            why = "count window size / gcd(size, slide) > 4096 panes is not supported on the GPU path";
             return GW_E_UNSUPPORTED;
         }
     } else {

@@ -1,4 +1,4 @@
-// gw_session.hip — event-time session windows (gap merge) on gfx950.
+// gw_session.hip — event-time session windows (gap merge) and count windows on gfx950.
 //
 // Reference semantics (paths relative to the Flink tree):
 //   EventTimeSessionWindows.assignWindows -> [ts, ts + gap)
@@ -7,19 +7,19 @@
 //     (RS/api/windowing/windows/TimeWindow.java:116-123,208-254)
 //   MergingWindowSet.addWindow (RS/runtime/operators/windowing/MergingWindowSet.java:153-224)
 //   WindowOperator.processElement merging branch incl. "drop if the window is already
-//     late" (RS/runtime/operators/windowing/WindowOperator.java:303-403)
+//     late" (RS/runtime/operators/windowing/WindowOperator.java:303-403, 440-446)
 //   AbstractHeapMergingState.mergeNamespaces (RR/state/heap/AbstractHeapMergingState.java:65-91)
 //   EventTimeTrigger + onEventTime: a session fires once when end-1 <= watermark.
 //
-// MI355X design: per watermark batch, records are grouped by (state
-// slot, timestamp) with a hand-written radix sort; each slot's sorted records are
-// swept against its in-flight sessions (<= K kept inline in the 64/128-byte slot).
-// Without late records the result of the reference's record-at-a-time merging is the
-// set of connected components of all windows (inclusive intersection), which a
-// sorted sweep computes in one pass.  If a slot's batch holds a record whose own
-// window is already late, the reference's outcome depends on arrival order (a late
-// window is dropped unless it touches an in-flight session at that moment), so that
-// slot is replayed record by record in arrival order.
+// MI355X design: per watermark batch every record finds its key's slot,
+// a stable radix sort by slot (rocPRIM) groups each key's records in ARRIVAL order, and one
+// thread per key replays them through MergingWindowSet.addWindow semantics -- the
+// reference's own record-at-a-time order, so late records, immediate firings and merges
+// behave exactly as in the reference, with no separate replay path.  The thread keeps the
+// key's in-flight sessions in its LDS lane (kLaneSess sessions); a key's sessions live
+// inline in its slot of the main table (K1 = 2 / 3 per slot).  A key with more in-flight
+// sessions moves to the wide table (one slot per such key, K2 sessions each, K2 doubled as
+// needed): its runs are replayed there in global memory.  No per-key session limit.
 #include "gw_kernels.h"
 #include "gw_session.h"
 #include "gw_sort.h"
@@ -29,89 +29,52 @@
 #include <cstdio>
 #include <vector>
 
+#include <rocprim/device/device_radix_sort.hpp>
+
 namespace gw {
 
-constexpr int kMaxLocalSess = 32;
+constexpr int kLaneSess = 8;        // sessions a thread replays in LDS
+constexpr int kSegThreads = 128;
+constexpr int kWideWords = 5;       // wide-table session: start, end, a0, a1, fired
+constexpr uint64_t kBigMeta = 1ull << 31;  // main-table slot word 1: the key lives in the wide table
 
 struct SegArgs {
-    const uint64_t* skey;   // sorted (slot << ts_bits) | (ts - ts_min)
-    const uint32_t* perm;   // original record index
+    const uint32_t* slot;   // sorted main-table slot of each record
+    const uint32_t* perm;   // its arrival index (stable sort: arrival order within a slot)
     int64_t n;
-    int ts_bits;
-    int64_t ts_min;
+    const int64_t* key;
+    const int64_t* ts;
     const int64_t* val;
     int64_t gap;
     int64_t wm;             // current watermark (all records of the batch see it)
     int64_t lateness;       // allowed lateness (WindowOperator.allowedLateness)
-    int purge;              // PurgingTrigger with lateness > 0: a fired session keeps an empty state
+    int purge;              // PurgingTrigger: a fired session keeps an empty state until cleanup
     int64_t* o_key;         // rows of windows an element fires at once (EventTimeTrigger.onElement
     int64_t* o_start;       //   FIRE: window max timestamp <= watermark; lateness > 0 only)
     int64_t* o_end;
     int64_t* o_res;
-    TableView t;            // ring = K sessions per slot, words = words per session
-    const int64_t* ts;      // the batch's columns (late side output)
-    const int64_t* key;
-    int64_t* lo_key;        // late side output (GW_FLAG_LATE_SIDE_OUTPUT), append at st->n_late_out;
-    int64_t* lo_ts;         //   nullptr: late elements are counted (numLateRecordsDropped)
+    int64_t* lo_key;        // late side output (GW_FLAG_LATE_SIDE_OUTPUT), append at st->n_late_out
+    int64_t* lo_ts;
     int64_t* lo_val;
-    const uint32_t* retry_in;
-    int64_t n_retry_in;
-    uint32_t* retry_out;    // appended at st->overflow
+    TableView t;            // main table: ring = K1 sessions per slot, words = words per session
+    TableView w;            // wide table: ring = K2, words = kWideWords
+    uint32_t* punt;         // main pass: runs for the wide table (append at st->overflow)
+    int64_t* mig;           // main pass: finished lists of more than K1 sessions (append at st->pad[0])
+    const uint32_t* runs;   // wide pass: run heads to replay
+    int64_t n_runs;
+    uint32_t* retry;        // wide pass: runs that did not fit K2 (append at st->overflow)
     DevStatus* st;
 };
 
-__global__ void __launch_bounds__(256) k_sess_minmax(const int64_t* ts, int64_t n, long long* mm,
-                                                     DevStatus* st) {
-    long long lo = INT64_MAX, hi = INT64_MIN;
-    unsigned long long flags = 0;
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-        const long long t = ts[i];
-        if (t == INT64_MIN) { flags |= GW_DF_NO_TS; continue; }
-        lo = t < lo ? t : lo;
-        hi = t > hi ? t : hi;
-    }
-    for (int o = 32; o > 0; o >>= 1) {
-        long long a = __shfl_xor(lo, o), b = __shfl_xor(hi, o);
-        lo = a < lo ? a : lo;
-        hi = b > hi ? b : hi;
-    }
-    __shared__ long long red[2][16];
-    const int wave = threadIdx.x >> 6;
-    if (__lane_id() == 0) { red[0][wave] = lo; red[1][wave] = hi; }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        for (int w = 1; w < (int)(blockDim.x >> 6); ++w) {
-            lo = red[0][w] < lo ? red[0][w] : lo;
-            hi = red[1][w] > hi ? red[1][w] : hi;
-        }
-        if (lo != INT64_MAX) atomicMin(&mm[0], lo);
-        if (hi != INT64_MIN) atomicMax(&mm[1], hi);
-    }
-    block_commit(st, 0, 0, flags, 0);
-}
-
-__global__ void __launch_bounds__(256) k_sess_prep(const int64_t* key, const int64_t* ts, int64_t n, int64_t ts_min,
-                                                   int ts_bits, TableView t, uint64_t* skey, uint32_t* perm,
-                                                   DevStatus* st) {
-    unsigned long long ins = 0, flags = 0;
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-        bool inserted;
-        int64_t s = find_or_insert(t, key[i], inserted);
-        ins += inserted;
-        if (s < 0) { flags |= GW_DF_TABLE_FULL; s = 0; }
-        skey[i] = ((uint64_t)s << ts_bits) | (uint64_t)(ts[i] - ts_min);
-        perm[i] = (uint32_t)i;
-    }
-    block_commit(st, 0, ins, flags, 0);
-}
-
 struct Sess {
     int64_t s, e, a0, a1;
-    bool f;  // its event-time timer has fired (kept for allowed lateness until cleanup)
+    int64_t f;  // its event-time timer has fired (kept for allowed lateness until cleanup)
 };
 
-// Slot word 1: in-flight session count (low 32 bits) | fired bit per session (high 32).
-__device__ __forceinline__ int slot_cnt(int64_t w) { return (int)(uint32_t)(uint64_t)w; }
+// Main-table slot word 1: in-flight session count (low 31 bits), kBigMeta, fired bit per
+// session (high 32 bits).
+__device__ __forceinline__ int slot_cnt(int64_t w) { return (int)((uint64_t)w & 0x7fffffffull); }
+__device__ __forceinline__ bool slot_big(int64_t w) { return ((uint64_t)w & kBigMeta) != 0; }
 __device__ __forceinline__ bool slot_fired(int64_t w, int q) { return ((uint64_t)w >> (32 + q)) & 1ull; }
 
 // WindowOperator.cleanupTime (:670-677, overflow -> Long.MAX_VALUE, never cleaned) <= wm
@@ -140,194 +103,261 @@ __device__ __forceinline__ void emit_now(const SegArgs& a, int64_t key, const Se
     a.o_res[at] = cell_result(AGG, x.a0, x.a1);
 }
 
+// A session list (sorted by start, disjoint) in LDS or in a wide-table slot: SoA with a
+// stride between fields, so both live in the same code.
+struct SessList {
+    int64_t* p;     // field f of session q at p[f * fs + q * qs]
+    int fs, qs;
+};
+__device__ __forceinline__ Sess sl_get(const SessList& l, int q) {
+    const int64_t* x = l.p + q * l.qs;
+    return Sess{x[0], x[l.fs], x[2 * l.fs], x[3 * l.fs], x[4 * l.fs]};
+}
+__device__ __forceinline__ void sl_put(const SessList& l, int q, const Sess& v) {
+    int64_t* x = l.p + q * l.qs;
+    x[0] = v.s; x[l.fs] = v.e; x[2 * l.fs] = v.a0; x[3 * l.fs] = v.a1; x[4 * l.fs] = v.f;
+}
+
+// MergingWindowSet.addWindow + WindowOperator.processElement (merging branch) for one
+// element: the window [ts, ts + gap) merges with every session it intersects (inclusive);
+// a window that merges with nothing and is already late is skipped (late: counted or sent
+// to the side output); a merged or new window whose max timestamp <= watermark fires at
+// once (EventTimeTrigger.onElement FIRE; PurgingTrigger purges), otherwise its timer is
+// (re-)armed.  Returns false if a new session does not fit `cap`.
 template <int AGG>
-__device__ void seg_process(const SegArgs& a, int64_t i) {
-    const uint64_t tsmask = (a.ts_bits >= 64) ? ~0ull : ((1ull << a.ts_bits) - 1ull);
-    const int64_t slot = (int64_t)(a.skey[i] >> a.ts_bits);
-    int64_t j = i + 1;
-    while (j < a.n && (int64_t)(a.skey[j] >> a.ts_bits) == slot) ++j;
-    int64_t* sp = slot_ptr(a.t, slot);
-    const int SW = a.t.words;
-    const int K = a.t.ring;
-    Sess cur_list[kMaxLocalSess];
-    const int64_t w1 = sp[1];
-    int cnt = slot_cnt(w1);
+__device__ __forceinline__ bool add_element(const SegArgs& a, const SessList& l, int& cnt, int cap, int64_t key,
+                                            int64_t idx, unsigned long long& late, unsigned long long& merges,
+                                            unsigned long long& flags) {
+    const int64_t ts = a.ts[idx];
+    int64_t we;
+    if (__builtin_add_overflow(ts, a.gap, &we)) { flags |= GW_DF_RANGE; return true; }
+    const int64_t ws = ts;
+    int lo = -1, hi = -1;
     for (int q = 0; q < cnt; ++q) {
-        const int64_t* x = sp + 2 + q * SW;
-        cur_list[q] = Sess{x[0], x[1], x[2], SW == 4 ? x[3] : 0, slot_fired(w1, q)};
+        const int64_t s = l.p[q * l.qs], e = l.p[l.fs + q * l.qs];
+        if (s <= we && e >= ws) {
+            if (lo < 0) lo = q;
+            hi = q;
+        }
     }
+    int64_t c0, c1;
+    record_cell(AGG, a.val ? a.val[idx] : 0, c0, c1);
+    if (lo < 0) {
+        if (cleaned_at(we, a.lateness, a.wm)) {  // isWindowLate: skipped; the element is late
+            if (!a.lo_key) {
+                late++;
+            } else {  // sideOutput(element) (WindowOperator.java:440-446, 587-588)
+                const unsigned long long o = atomicAdd(&a.st->n_late_out, 1ull);
+                a.lo_key[o] = key;
+                a.lo_ts[o] = ts;
+                a.lo_val[o] = a.val ? a.val[idx] : 0;
+            }
+            return true;
+        }
+        if (cnt == cap) return false;
+        int q = cnt;
+        while (q > 0 && l.p[(q - 1) * l.qs] > ws) {
+            sl_put(l, q, sl_get(l, q - 1));
+            --q;
+        }
+        Sess x{ws, we, c0, c1, (int64_t)(we - 1 <= a.wm)};
+        if (x.f) {  // onElement: FIRE (PurgingTrigger: FIRE_AND_PURGE)
+            emit_now<AGG>(a, key, x);
+            if (a.purge) purge_acc<AGG>(x.a0, x.a1);
+        }
+        sl_put(l, q, x);
+        cnt++;
+        return true;
+    }
+    Sess m = sl_get(l, lo);
+    if (ws < m.s) m.s = ws;
+    for (int q = lo + 1; q <= hi; ++q) {
+        const Sess y = sl_get(l, q);
+        if (y.e > m.e) m.e = y.e;
+        fold_cell(AGG, m.a0, m.a1, y.a0, y.a1);
+        merges++;
+    }
+    if (we > m.e) m.e = we;
+    fold_cell(AGG, m.a0, m.a1, c0, c1);
+    m.f = m.e - 1 <= a.wm;  // onElement FIRE, or onMerge registers the merged window's timer
+    if (m.f) {
+        emit_now<AGG>(a, key, m);
+        if (a.purge) purge_acc<AGG>(m.a0, m.a1);
+    }
+    sl_put(l, lo, m);
+    const int removed = hi - lo;
+    for (int q = hi + 1; q < cnt; ++q) sl_put(l, q - removed, sl_get(l, q));
+    cnt -= removed;
+    return true;
+}
+
+// Main pass: one thread per key's run.  The run's elements replay against the key's
+// inline sessions in the thread's LDS lane; a run that could need more than kLaneSess
+// sessions, or a key already in the wide table, goes to the wide pass.
+template <int AGG>
+__global__ void __launch_bounds__(kSegThreads) k_sess_segment(SegArgs a) {
+    __shared__ int64_t lane[5 * kLaneSess * kSegThreads];
+    const SessList l{lane + threadIdx.x, kLaneSess * kSegThreads, kSegThreads};
     unsigned long long late = 0, merges = 0, flags = 0;
-    const int64_t ts_first = a.ts_min + (int64_t)(a.skey[i] & tsmask);
-    bool ok = true;
-    if ((uint64_t)ts_first > (uint64_t)INT64_MAX - (uint64_t)a.gap && ts_first > 0) flags |= GW_DF_RANGE;
-    const bool any_late = ts_first + a.gap - 1 <= a.wm;  // sorted by ts: the first is the earliest
-    if (!any_late) {
-        // Sweep old sessions and the batch's windows in start order; merge on inclusive intersect.
-        Sess out[kMaxLocalSess];
-        int nout = 0, oi = 0;
-        int64_t e = i;
-        bool have = false;
-        bool cur_has_state = false;
-        Sess cur{0, 0, 0, 0};
-        while (oi < cnt || e < j) {
-            Sess item;
-            bool is_old;
-            const int64_t te = e < j ? a.ts_min + (int64_t)(a.skey[e] & tsmask) : INT64_MAX;
-            if (oi < cnt && (e >= j || cur_list[oi].s <= te)) {
-                item = cur_list[oi++];
-                is_old = true;
-            } else {
-                int64_t c0, c1;
-                record_cell(AGG, a.val ? a.val[a.perm[e]] : 0, c0, c1);
-                item = Sess{te, te + a.gap, c0, c1, false};
-                is_old = false;
-                ++e;
-            }
-            if (!have) {
-                cur = item;
-                have = true;
-                cur_has_state = is_old;
-            } else if (item.s <= cur.e) {
-                if (item.e > cur.e) cur.e = item.e;
-                fold_cell(AGG, cur.a0, cur.a1, item.a0, item.a1);
-                cur.f = cur.f && item.f;  // a merge with a new window re-arms the timer (its end > wm)
-                if (is_old && cur_has_state) merges++;
-                cur_has_state |= is_old;
-            } else {
-                if (nout == kMaxLocalSess) { ok = false; break; }
-                out[nout++] = cur;
-                cur = item;
-                cur_has_state = is_old;
-            }
-        }
-        if (ok && have) {
-            if (nout == kMaxLocalSess) ok = false;
-            else out[nout++] = cur;
-        }
-        if (ok) {
-            for (int q = 0; q < nout; ++q) cur_list[q] = out[q];
-            cnt = nout;
-        }
-    } else {
-        // Arrival-order replay (MergingWindowSet.addWindow per record).  With allowed
-        // lateness an element may fire its window at once; those rows are written only in
-        // a second pass, once the first has shown that the result fits the slot (a slot
-        // that overflows is retried after widening and must not emit twice).
-        Sess init[kMaxLocalSess];
-        const int cnt0 = cnt;
-        const int passes = (a.lateness > 0 || a.lo_key) ? 2 : 1;
-        for (int q = 0; q < cnt0 && passes == 2; ++q) init[q] = cur_list[q];
-        for (int pass = 0; pass < passes; ++pass) {
-        const bool emit = pass == 1;
-        if (emit) {
-            if (!ok || cnt > K) break;
-            for (int q = 0; q < cnt0; ++q) cur_list[q] = init[q];
-            cnt = cnt0;
-            late = 0;
-            merges = 0;
-        }
-        int64_t last = -1;
-        for (int64_t step = i; step < j && ok; ++step) {
-            int64_t best = -1;
-            uint32_t bp = 0xffffffffu;
-            for (int64_t x = i; x < j; ++x) {
-                const uint32_t p = a.perm[x];
-                if ((int64_t)p > last && p < bp) { bp = p; best = x; }
-            }
-            last = bp;
-            const int64_t ts = a.ts_min + (int64_t)(a.skey[best] & tsmask);
-            const int64_t ws = ts, we = ts + a.gap;
-            int lo = -1, hi = -1;
+    const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (i < a.n && (i == 0 || a.slot[i - 1] != a.slot[i])) {
+        const uint32_t slot = a.slot[i];
+        int64_t j = i + 1;
+        while (j < a.n && a.slot[j] == slot) ++j;
+        int64_t* sp = slot_ptr(a.t, (int64_t)slot);
+        const int64_t w1 = sp[1];
+        const int SW = a.t.words;
+        int cnt = slot_cnt(w1);
+        if (slot_big(w1) || cnt + (j - i) > kLaneSess) {
+            const unsigned long long at = atomicAdd(&a.st->overflow, 1ull);
+            a.punt[at] = (uint32_t)i;
+        } else {
             for (int q = 0; q < cnt; ++q) {
-                if (cur_list[q].s <= we && cur_list[q].e >= ws) {
-                    if (lo < 0) lo = q;
-                    hi = q;
-                }
+                const int64_t* x = sp + 2 + q * SW;
+                sl_put(l, q, Sess{x[0], x[1], x[2], SW == 4 ? x[3] : 0, (int64_t)slot_fired(w1, q)});
             }
-            int64_t c0, c1;
-            record_cell(AGG, a.val ? a.val[bp] : 0, c0, c1);
-            if (lo < 0) {
-                if (cleaned_at(we, a.lateness, a.wm)) {  // isWindowLate: skipped, and the element is late
-                    if (!a.lo_key) { late++; continue; }
-                    if (emit) {  // sideOutput(element) (WindowOperator.java:440-446, 587-588)
-                        const unsigned long long o = atomicAdd(&a.st->n_late_out, 1ull);
-                        a.lo_key[o] = a.key[bp];
-                        a.lo_ts[o] = a.ts[bp];
-                        a.lo_val[o] = a.val ? a.val[bp] : 0;
-                    }
-                    continue;
+            const int64_t key = sp[0];  // the sentinel slot's key word is Long.MIN_VALUE, its key
+            for (int64_t r = i; r < j; ++r) add_element<AGG>(a, l, cnt, kLaneSess, key, a.perm[r], late, merges, flags);
+            if (cnt <= a.t.ring) {
+                uint64_t fired = 0;
+                for (int q = 0; q < cnt; ++q) {
+                    const Sess v = sl_get(l, q);
+                    int64_t* x = sp + 2 + q * SW;
+                    x[0] = v.s; x[1] = v.e; x[2] = v.a0;
+                    if (SW == 4) x[3] = v.a1;
+                    fired |= (uint64_t)(v.f != 0) << q;
                 }
-                if (cnt == kMaxLocalSess) { ok = false; break; }
-                int q = cnt;
-                while (q > 0 && cur_list[q - 1].s > ws) { cur_list[q] = cur_list[q - 1]; --q; }
-                cur_list[q] = Sess{ws, we, c0, c1, we - 1 <= a.wm};
-                if (cur_list[q].f) {  // onElement: FIRE (PurgingTrigger: FIRE_AND_PURGE)
-                    if (emit) emit_now<AGG>(a, sp[0], cur_list[q]);
-                    if (a.purge) purge_acc<AGG>(cur_list[q].a0, cur_list[q].a1);
+                sp[1] = (int64_t)((fired << 32) | (uint64_t)(uint32_t)cnt);
+            } else {  // more sessions than the slot holds: the finished list moves to the wide table
+                const unsigned long long at = atomicAdd(&a.st->pad[0], 1ull);
+                int64_t* m = a.mig + at * (2 + kWideWords * kLaneSess);
+                m[0] = (int64_t)slot;
+                m[1] = cnt;
+                for (int q = 0; q < cnt; ++q) {
+                    const Sess v = sl_get(l, q);
+                    int64_t* x = m + 2 + q * kWideWords;
+                    x[0] = v.s; x[1] = v.e; x[2] = v.a0; x[3] = v.a1; x[4] = v.f;
                 }
-                cnt++;
-            } else {
-                Sess m = cur_list[lo];
-                if (ws < m.s) m.s = ws;
-                for (int q = lo + 1; q <= hi; ++q) {
-                    if (cur_list[q].e > m.e) m.e = cur_list[q].e;
-                    fold_cell(AGG, m.a0, m.a1, cur_list[q].a0, cur_list[q].a1);
-                    merges++;
-                }
-                if (we > m.e) m.e = we;
-                fold_cell(AGG, m.a0, m.a1, c0, c1);
-                m.f = m.e - 1 <= a.wm;  // onElement FIRE, or onMerge registers the merged window's timer
-                if (m.f) {
-                    if (emit) emit_now<AGG>(a, sp[0], m);
-                    if (a.purge) purge_acc<AGG>(m.a0, m.a1);
-                }
-                cur_list[lo] = m;
-                const int removed = hi - lo;
-                for (int q = hi + 1; q < cnt; ++q) cur_list[q - removed] = cur_list[q];
-                cnt -= removed;
+                atomicMax(&a.st->pad[1], (unsigned long long)cnt);
             }
         }
+    }
+    late = wave_sum(late);
+    merges = wave_sum(merges);
+    flags = wave_ior(flags);
+    if (__lane_id() == 0) {
+        ShardCtr& sc = a.st->sh[blockIdx.x % kShards];
+        if (late) atomicAdd(&sc.late, late);
+        if (merges) atomicAdd(&sc.merges, merges);
+        if (flags) atomicOr(&sc.flags, flags);
+    }
+}
+
+// The key of main-table slot g moves to the wide table: a wide slot with its sessions.
+__device__ __forceinline__ int64_t wide_slot_of(const TableView& w, int64_t key, unsigned long long& flags) {
+    bool inserted;
+    const int64_t g2 = find_or_insert(w, key, inserted);
+    if (g2 < 0) flags |= GW_DF_TABLE_FULL;
+    return g2;
+}
+
+// Finished lists of the main pass -> the wide table.
+__global__ void __launch_bounds__(256) k_sess_migrate(TableView t, TableView w, const int64_t* mig, int64_t n,
+                                                      DevStatus* st) {
+    unsigned long long flags = 0, ins = 0;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t* m = mig + i * (2 + kWideWords * kLaneSess);
+        int64_t* sp = slot_ptr(t, m[0]);
+        const int64_t key = m[0] == t.cap ? kEmptyKey : sp[0];
+        bool inserted;
+        const int64_t g2 = find_or_insert(w, key, inserted);
+        if (g2 < 0) { flags |= GW_DF_TABLE_FULL; continue; }
+        ins += inserted;
+        int64_t* d = slot_ptr(w, g2);
+        const int cnt = (int)m[1];
+        for (int x = 0; x < cnt * kWideWords; ++x) d[2 + x] = m[2 + x];
+        d[1] = cnt;
+        sp[1] = (int64_t)kBigMeta;
+    }
+    flags = wave_ior(flags);
+    ins = wave_sum(ins);
+    if (__lane_id() == 0) {
+        if (flags) atomicOr(&st->sh[blockIdx.x % kShards].flags, flags);
+        if (ins) atomicAdd(&st->pad[2], ins);  // wide-table slots in use
+    }
+}
+
+// Wide pass: one thread per punted run, against the key's wide slot in global memory.  A
+// key not yet wide moves there first.  A run that could exceed K2 sessions is left for a
+// retry after the host widens the table (nothing is written or emitted for it).
+template <int AGG>
+__global__ void __launch_bounds__(256) k_sess_wide(SegArgs a) {
+    unsigned long long late = 0, merges = 0, flags = 0, ins = 0;
+    for (int64_t r0 = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r0 < a.n_runs;
+         r0 += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t i = a.runs[r0];
+        const uint32_t slot = a.slot[i];
+        int64_t j = i + 1;
+        while (j < a.n && a.slot[j] == slot) ++j;
+        int64_t* sp = slot_ptr(a.t, (int64_t)slot);
+        const int64_t key = (int64_t)slot == a.t.cap ? kEmptyKey : sp[0];
+        bool inserted;
+        const int64_t g2 = find_or_insert(a.w, key, inserted);
+        if (g2 < 0) {
+            flags |= GW_DF_TABLE_FULL;
+            const unsigned long long at = atomicAdd(&a.st->overflow, 1ull);
+            a.retry[at] = (uint32_t)i;
+            continue;
         }
+        ins += inserted;
+        int64_t* d = slot_ptr(a.w, g2);
+        const int64_t w1 = sp[1];
+        if (!slot_big(w1)) {  // move the inline sessions over
+            const int c1 = slot_cnt(w1), SW = a.t.words;
+            for (int q = 0; q < c1; ++q) {
+                const int64_t* x = sp + 2 + q * SW;
+                int64_t* y = d + 2 + q * kWideWords;
+                y[0] = x[0]; y[1] = x[1]; y[2] = x[2]; y[3] = SW == 4 ? x[3] : 0; y[4] = slot_fired(w1, q);
+            }
+            d[1] = c1;
+            sp[1] = (int64_t)kBigMeta;
+        }
+        int cnt = (int)d[1];
+        if (cnt + (j - i) > a.w.ring) {
+            atomicMax(&a.st->pad[1], (unsigned long long)(cnt + (j - i)));
+            const unsigned long long at = atomicAdd(&a.st->overflow, 1ull);
+            a.retry[at] = (uint32_t)i;
+            continue;
+        }
+        const SessList l{d + 2, 1, kWideWords};
+        for (int64_t r = i; r < j; ++r) add_element<AGG>(a, l, cnt, a.w.ring, key, a.perm[r], late, merges, flags);
+        d[1] = cnt;
     }
-    if (!ok || cnt > K) {
-        // does not fit the slot: leave the slot untouched, retry after widening
-        const unsigned long long at = atomicAdd(&a.st->overflow, 1ull);
-        a.retry_out[at] = (uint32_t)i;
-        atomicMax(&a.st->pad[1], (unsigned long long)(ok ? cnt : kMaxLocalSess + 1));
-        return;
-    }
-    uint64_t fired = 0;
-    for (int q = 0; q < cnt; ++q) {
-        int64_t* x = sp + 2 + q * SW;
-        x[0] = cur_list[q].s;
-        x[1] = cur_list[q].e;
-        x[2] = cur_list[q].a0;
-        if (SW == 4) x[3] = cur_list[q].a1;
-        fired |= (uint64_t)cur_list[q].f << q;
-    }
-    sp[1] = (int64_t)(((uint64_t)fired << 32) | (uint64_t)(uint32_t)cnt);
     ShardCtr& sc = a.st->sh[blockIdx.x % kShards];
     if (late) atomicAdd(&sc.late, late);
     if (merges) atomicAdd(&sc.merges, merges);
     if (flags) atomicOr(&sc.flags, flags);
+    if (ins) atomicAdd(&a.st->pad[2], ins);
 }
 
-template <int AGG>
-__global__ void __launch_bounds__(256) k_sess_segment(SegArgs a) {
-    if (a.retry_in) {
-        for (int64_t r = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r < a.n_retry_in;
-             r += (int64_t)gridDim.x * blockDim.x)
-            seg_process<AGG>(a, (int64_t)a.retry_in[r]);
-        return;
+__global__ void __launch_bounds__(256) k_sess_prep(const int64_t* key, const int64_t* ts, int64_t n, TableView t,
+                                                   uint32_t* slot, uint32_t* perm, DevStatus* st) {
+    unsigned long long ins = 0, flags = 0;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        if (ts && ts[i] == INT64_MIN) flags |= GW_DF_NO_TS;
+        bool inserted;
+        int64_t s = find_or_insert(t, key[i], inserted);
+        ins += inserted;
+        if (s < 0) { flags |= GW_DF_TABLE_FULL; s = 0; }
+        slot[i] = (uint32_t)s;
+        perm[i] = (uint32_t)i;
     }
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < a.n; i += (int64_t)gridDim.x * blockDim.x) {
-        if (i > 0 && (a.skey[i] >> a.ts_bits) == (a.skey[i - 1] >> a.ts_bits)) continue;
-        seg_process<AGG>(a, i);
-    }
+    block_commit(st, 0, ins, flags, 0);
 }
 
 // Fire every in-flight session with end-1 <= wm (sessions in a slot are disjoint and
-// sorted, so the fired ones are a prefix), emit (key, start, end, result), purge.
+// sorted, so the fired ones are a prefix), emit (key, start, end, result), drop the
+// cleaned prefix (WindowOperator.onEventTime :450-494 / clearAllState :560-571).
 // Rows are staged in LDS, one row per thread per round, and flushed in bulk.
 template <int AGG>
 __global__ void __launch_bounds__(256) k_sess_fire(TableView t, int64_t wm, int64_t lateness, int purge, int64_t* o_key,
@@ -348,7 +378,7 @@ __global__ void __launch_bounds__(256) k_sess_fire(TableView t, int64_t wm, int6
         if (i < c1) {
             s = slot_ptr(t, i);
             w1 = s[1];
-            cnt = slot_cnt(w1);
+            cnt = slot_big(w1) ? 0 : slot_cnt(w1);  // wide keys: k_sess_fire_wide
             while (nf < cnt && s[2 + nf * SW + 1] - 1 <= wm) ++nf;  // due timers: a prefix (sorted, disjoint)
             nc = nf;
             if (lateness > 0) {  // cleanup timers (max timestamp + lateness) are a prefix of those
@@ -394,19 +424,44 @@ __global__ void __launch_bounds__(256) k_sess_fire(TableView t, int64_t wm, int6
     stage_flush(rs, &st->rows, o_key, o_start, o_end, o_res);
 }
 
-__global__ void __launch_bounds__(256) k_sess_rewiden(TableView o, TableView n) {
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i <= o.cap; i += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t* s = slot_ptr(o, i);
-        int64_t* d = slot_ptr(n, i);
-        d[0] = s[0];
-        d[1] = s[1];
-        const int cnt = slot_cnt(s[1]);
-        for (int w = 0; w < cnt * o.words; ++w) d[2 + w] = s[2 + w];
+// The same for the wide table (one thread per wide slot; few keys).
+template <int AGG>
+__global__ void __launch_bounds__(256) k_sess_fire_wide(TableView w, int64_t wm, int64_t lateness, int purge,
+                                                        int64_t* o_key, int64_t* o_start, int64_t* o_end,
+                                                        int64_t* o_res, DevStatus* st) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i <= w.cap; i += (int64_t)gridDim.x * blockDim.x) {
+        int64_t* s = slot_ptr(w, i);
+        const int cnt = (int)s[1];
+        if (cnt <= 0) continue;
+        int nf = 0, nc = 0;
+        while (nf < cnt && s[2 + nf * kWideWords + 1] - 1 <= wm) ++nf;
+        nc = nf;
+        if (lateness > 0) {
+            nc = 0;
+            while (nc < nf && cleaned_at(s[2 + nc * kWideWords + 1], lateness, wm)) ++nc;
+        }
+        const int64_t key = i == w.cap ? kEmptyKey : s[0];
+        for (int q = 0; q < nf; ++q) {
+            int64_t* x = s + 2 + q * kWideWords;
+            if (x[4]) continue;
+            const unsigned long long o = atomicAdd(&st->rows, 1ull);
+            o_key[o] = key; o_start[o] = x[0]; o_end[o] = x[1]; o_res[o] = cell_result(AGG, x[2], x[3]);
+            x[4] = 1;
+            if (purge) purge_acc<AGG>(x[2], x[3]);
+        }
+        if (nc) {
+            for (int q = nc; q < cnt; ++q)
+                for (int f = 0; f < kWideWords; ++f) s[2 + (q - nc) * kWideWords + f] = s[2 + q * kWideWords + f];
+            s[1] = cnt - nc;
+        }
     }
 }
 
-// Re-hash slots with in-flight sessions into a fresh table (dead keys dropped).
-__global__ void __launch_bounds__(256) k_sess_rehash(TableView o, TableView n, DevStatus* st) {
+// Re-hash slots holding state into a fresh table (dead keys dropped): main table (word 1 =
+// count | fired bits | kBigMeta), wide table (word 1 = count), count windows (word 1 =
+// element count).
+__global__ void __launch_bounds__(256) k_sess_rehash(TableView o, TableView n, int words_per_slot, DevStatus* st,
+                                                     int ins_field) {
     unsigned long long ins = 0, flags = 0;
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i <= o.cap; i += (int64_t)gridDim.x * blockDim.x) {
         const int64_t* s = slot_ptr(o, i);
@@ -417,11 +472,19 @@ __global__ void __launch_bounds__(256) k_sess_rehash(TableView o, TableView n, D
         if (j < 0) { flags |= GW_DF_TABLE_FULL; continue; }
         ins += inserted;
         int64_t* d = slot_ptr(n, j);
-        const int cnt = slot_cnt(s[1]);
         d[1] = s[1];
-        for (int w = 0; w < cnt * o.words; ++w) d[2 + w] = s[2 + w];
+        const int nw = words_per_slot < 0 ? (int)s[1] * o.words : words_per_slot;
+        for (int w = 0; w < nw; ++w) d[2 + w] = s[2 + w];
     }
-    block_commit(st, 0, ins, flags, 0);
+    ins = wave_sum(ins);
+    flags = wave_ior(flags);
+    if (__lane_id() == 0) {
+        if (flags) atomicOr(&st->sh[blockIdx.x % kShards].flags, flags);
+        if (ins) {
+            if (ins_field < 0) atomicAdd(&st->pad[2], ins);
+            else atomicAdd(&st->sh[blockIdx.x % kShards].ins, ins);
+        }
+    }
 }
 
 __global__ void __launch_bounds__(256) k_sess_init(TableView t) {
@@ -432,73 +495,46 @@ __global__ void __launch_bounds__(256) k_sess_init(TableView t) {
     }
 }
 
-// Restore (gw_restore of a session snapshot): one thread per restored key.  The key's
-// restored sessions (sorted by start, disjoint) are swept together with the slot's
-// in-flight ones in start order and merged on inclusive intersection, exactly as
-// seg_process merges a batch; a fresh slot receives them unchanged.  A key whose
-// result exceeds the slot's K sessions is counted in st->overflow and left untouched.
-template <int AGG>
-__global__ void __launch_bounds__(256) k_sess_restore(TableView t, const int64_t* rk, const int64_t* roff,
+// Restore (gw_restore of a session snapshot): one thread per restored key.  A key with at
+// most K1 restored sessions goes inline into its main slot; a key with more goes to the
+// wide table (its main slot marked).  A key that already holds sessions here is counted in
+// st->overflow and left untouched (blobs of one key group are never restored twice).
+__global__ void __launch_bounds__(256) k_sess_restore(TableView t, TableView w, const int64_t* rk, const int64_t* roff,
                                                       const int64_t* rs, int64_t n, DevStatus* st) {
-    unsigned long long ins = 0, flags = 0;
+    unsigned long long ins = 0, flags = 0, ins2 = 0;
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
         bool inserted;
         const int64_t slot = find_or_insert(t, rk[i], inserted);
         ins += inserted;
         if (slot < 0) { flags |= GW_DF_TABLE_FULL; continue; }
         int64_t* sp = slot_ptr(t, slot);
-        const int SW = t.words, K = t.ring;
-        const int64_t w1 = sp[1];
-        const int cnt = slot_cnt(w1);
-        Sess out[kMaxLocalSess];
-        int nout = 0, oi = 0;
-        int64_t r = roff[i];
-        const int64_t re = roff[i + 1];
-        bool have = false, ok = true;
-        Sess cur{0, 0, 0, 0};
-        while (oi < cnt || r < re) {
-            Sess item;
-            const int64_t* x = sp + 2 + oi * SW;
-            if (oi < cnt && (r >= re || x[0] <= rs[r * 5])) {
-                item = Sess{x[0], x[1], x[2], SW == 4 ? x[3] : 0, slot_fired(w1, oi)};
-                ++oi;
-            } else {
-                item = Sess{rs[r * 5], rs[r * 5 + 1], rs[r * 5 + 2], rs[r * 5 + 3], rs[r * 5 + 4] != 0};
-                ++r;
+        if (sp[1] != 0) { atomicAdd(&st->overflow, 1ull); continue; }
+        const int64_t r0 = roff[i], cnt = roff[i + 1] - r0;
+        if (cnt <= t.ring) {
+            const int SW = t.words;
+            uint64_t fired = 0;
+            for (int q = 0; q < cnt; ++q) {
+                const int64_t* x = rs + (r0 + q) * 5;
+                int64_t* y = sp + 2 + q * SW;
+                y[0] = x[0]; y[1] = x[1]; y[2] = x[2];
+                if (SW == 4) y[3] = x[3];
+                fired |= (uint64_t)(x[4] != 0) << q;
             }
-            if (!have) {
-                cur = item;
-                have = true;
-            } else if (item.s <= cur.e) {
-                if (item.e > cur.e) cur.e = item.e;
-                fold_cell(AGG, cur.a0, cur.a1, item.a0, item.a1);
-                cur.f = cur.f && item.f;
-            } else {
-                if (nout == K) { ok = false; break; }
-                out[nout++] = cur;
-                cur = item;
-            }
+            sp[1] = (int64_t)((fired << 32) | (uint64_t)cnt);
+        } else {
+            const int64_t g2 = find_or_insert(w, rk[i], inserted);
+            if (g2 < 0) { flags |= GW_DF_TABLE_FULL; continue; }
+            ins2 += inserted;
+            int64_t* d = slot_ptr(w, g2);
+            if (d[1] != 0) { atomicAdd(&st->overflow, 1ull); continue; }
+            for (int64_t x = 0; x < cnt * kWideWords; ++x) d[2 + x] = rs[r0 * 5 + x];
+            d[1] = cnt;
+            sp[1] = (int64_t)kBigMeta;
         }
-        if (ok && have) {
-            if (nout == K) ok = false;
-            else out[nout++] = cur;
-        }
-        if (!ok) {
-            atomicAdd(&st->overflow, 1ull);
-            continue;
-        }
-        uint64_t fired = 0;
-        for (int q = 0; q < nout; ++q) {
-            int64_t* y = sp + 2 + q * SW;
-            y[0] = out[q].s;
-            y[1] = out[q].e;
-            y[2] = out[q].a0;
-            if (SW == 4) y[3] = out[q].a1;
-            fired |= (uint64_t)out[q].f << q;
-        }
-        sp[1] = (int64_t)((fired << 32) | (uint64_t)(uint32_t)nout);
     }
     block_commit(st, 0, ins, flags, 0);
+    ins2 = wave_sum(ins2);
+    if (__lane_id() == 0 && ins2) atomicAdd(&st->pad[2], ins2);
 }
 
 #define GW_AGG_SWITCH(agg, CALL)                  \
@@ -534,40 +570,47 @@ static unsigned grid_of(int64_t n) {
 // consecutive elements, so every fired window is exactly n = size/g whole panes (the
 // first windows of a key: all its panes so far) and every slide ends a pane.  A slot
 // holds [key][element count][ring of n pane accumulators]; a batch is grouped by slot
-// with the stable radix sort (arrival order kept inside a key) and each key's run is
-// folded in order by one thread, which emits a row at every multiple of the slide.
+// with the stable radix sort (arrival order kept inside a key).  A key's run is folded in
+// order by one thread; a hot key's long run (WindowWordCount's frequent words) by a whole
+// workgroup: one thread per pane folds the pane's elements, then one thread per firing
+// folds the window's n panes.
 struct CountGeom {
     int64_t size, slide, g;
 };
+constexpr int kCntLongRun = 512;   // runs longer than this get a workgroup
+constexpr int kCntChunk = 256;     // panes per workgroup step
 
-__global__ void __launch_bounds__(256) k_cnt_slot(TableView t, const int64_t* key, int64_t n, uint64_t* kslot,
-                                                  uint32_t* idx, DevStatus* st) {
-    unsigned long long ins = 0, flags = 0;
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-        bool inserted;
-        const int64_t j = find_or_insert(t, key[i], inserted);
-        if (j < 0) flags |= GW_DF_TABLE_FULL;
-        ins += inserted;
-        kslot[i] = j < 0 ? (uint64_t)t.cap + 1 : (uint64_t)j;  // cap + 1: parked, never applied
-        idx[i] = (uint32_t)i;
-    }
-    block_commit(st, 0, ins, flags, 0);
+template <int AGG>
+__device__ __forceinline__ void cnt_emit(DevStatus* st, int64_t* ok, int64_t* os, int64_t* oe, int64_t* orr, int64_t key,
+                                         int64_t c, int64_t len, int64_t r0, int64_t r1) {
+    const unsigned long long o = atomicAdd(&st->rows, 1ull);
+    ok[o] = key;
+    os[o] = c - len;
+    oe[o] = c;
+    orr[o] = cell_result(AGG, r0, r1);
 }
 
 template <int AGG>
-__global__ void __launch_bounds__(256) k_cnt_apply(TableView t, CountGeom G, const uint64_t* ks, const uint32_t* perm,
+__global__ void __launch_bounds__(256) k_cnt_apply(TableView t, CountGeom G, const uint32_t* ks, const uint32_t* perm,
                                                    int64_t n, const int64_t* val, int64_t* ok, int64_t* os,
-                                                   int64_t* oe, int64_t* orr, DevStatus* st) {
+                                                   int64_t* oe, int64_t* orr, uint32_t* longs, DevStatus* st) {
     constexpr int W = (AGG == GW_AVG_I64 || AGG == GW_AVG_F64) ? 2 : 1;
     const int R = t.ring;
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-        const uint64_t slot = ks[i];
-        if ((i > 0 && ks[i - 1] == slot) || slot > (uint64_t)t.cap) continue;  // not the head of a key's run
+        const uint32_t slot = ks[i];
+        if (i > 0 && ks[i - 1] == slot) continue;  // not the head of a key's run
+        int64_t j = i + 1;
+        while (j < n && ks[j] == slot && j - i <= kCntLongRun) ++j;
+        if (j - i > kCntLongRun) {  // a hot key: k_cnt_long
+            const unsigned long long at = atomicAdd(&st->overflow, 1ull);
+            longs[at] = (uint32_t)i;
+            continue;
+        }
         int64_t* sp = slot_ptr(t, (int64_t)slot);
         int64_t* cells = sp + 2;
         const int64_t key = sp[0];  // the sentinel slot's key word is Long.MIN_VALUE, its key
         int64_t c = sp[1];
-        for (int64_t r = i; r < n && ks[r] == slot; ++r) {
+        for (int64_t r = i; r < j; ++r) {
             int64_t a0, a1;
             record_cell(AGG, val ? val[perm[r]] : 0, a0, a1);
             int64_t* cell = cells + ((c / G.g) % R) * W;
@@ -590,33 +633,124 @@ __global__ void __launch_bounds__(256) k_cnt_apply(TableView t, CountGeom G, con
                     const int64_t* e = cells + (q % R) * W;
                     fold_cell(AGG, r0, r1, e[0], W == 2 ? e[1] : 0);
                 }
-                const unsigned long long o = atomicAdd(&st->rows, 1ull);
-                ok[o] = key;
-                os[o] = c - len;
-                oe[o] = c;
-                orr[o] = cell_result(AGG, r0, r1);
+                cnt_emit<AGG>(st, ok, os, oe, orr, key, c, len, r0, r1);
             }
         }
         sp[1] = c;
     }
 }
 
-__global__ void __launch_bounds__(256) k_cnt_rehash(TableView o, TableView nt, DevStatus* st) {
-    unsigned long long ins = 0, flags = 0;
-    const int words = o.ring * o.words;
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i <= o.cap; i += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t* sp = slot_ptr(o, i);
-        if (sp[1] == 0) continue;  // every key in the table has counted an element
-        const int64_t key = i == o.cap ? kEmptyKey : sp[0];
-        bool inserted;
-        const int64_t j = find_or_insert(nt, key, inserted);
-        if (j < 0) { flags |= GW_DF_TABLE_FULL; continue; }
-        ins += inserted;
-        int64_t* d = slot_ptr(nt, j);
-        d[1] = sp[1];
-        for (int w = 0; w < words; ++w) d[2 + w] = sp[2 + w];
+// A hot key's run: one workgroup.  Panes are folded kCntChunk at a time (one thread per
+// pane, its <= g elements in arrival order); each firing in the step folds its n panes,
+// from the step's LDS values, the previous step's last n-1 panes (LDS) or the key's ring
+// (panes before the run).  The ring keeps the key's last n panes.
+template <int AGG>
+__global__ void __launch_bounds__(256) k_cnt_long(TableView t, CountGeom G, const uint32_t* ks, const uint32_t* perm,
+                                                  int64_t n, const int64_t* val, int64_t* ok, int64_t* os,
+                                                  int64_t* oe, int64_t* orr, const uint32_t* longs, DevStatus* st) {
+    constexpr int W = (AGG == GW_AVG_I64 || AGG == GW_AVG_F64) ? 2 : 1;
+    const int R = t.ring;  // = n panes per window; the LDS tail keeps the R panes before the step
+    const int nt = R;
+    extern __shared__ int64_t lds[];  // [2][nt + kCntChunk] pane values + [2][nt] copy space
+    int64_t* v0 = lds;
+    int64_t* v1 = lds + nt + kCntChunk;
+    int64_t* t0 = lds + 2 * (nt + kCntChunk);
+    int64_t* t1 = t0 + nt;
+    const int64_t i = longs[blockIdx.x];
+    const uint32_t slot = ks[i];
+    __shared__ int64_t s_j;
+    if (threadIdx.x == 0) {
+        int64_t j = i + 1;
+        while (j < n && ks[j] == slot) ++j;
+        s_j = j;
     }
-    block_commit(st, 0, ins, flags, 0);
+    __syncthreads();
+    const int64_t L = s_j - i;
+    int64_t* sp = slot_ptr(t, (int64_t)slot);
+    int64_t* cells = sp + 2;
+    const int64_t key = sp[0];
+    const int64_t c0 = sp[1];
+    const int64_t g = G.g;
+    const int64_t pf = c0 / g, pe = (c0 + L - 1) / g;  // panes the run touches
+    // pane q's value while panes [P0, P0 + kCntChunk) are the current step and the tail
+    // v[0, nt) holds panes [tail_end - nt, tail_end) (tail_end = P0 during a step)
+    auto pane_val = [&](int64_t q, int64_t P0, int64_t tail_end, int64_t& a, int64_t& b) {
+        if (q >= P0) {
+            a = v0[nt + (q - P0)]; b = v1[nt + (q - P0)];
+        } else if (q >= pf && q >= tail_end - nt) {
+            a = v0[q - (tail_end - nt)]; b = v1[q - (tail_end - nt)];
+        } else {
+            const int64_t* e = cells + (q % R) * W;
+            a = e[0]; b = W == 2 ? e[1] : 0;
+        }
+    };
+    for (int64_t P0 = pf; P0 <= pe; P0 += kCntChunk) {
+        const int64_t P = P0 + threadIdx.x;
+        if (threadIdx.x < kCntChunk && P <= pe) {
+            const int64_t o_lo = max(P * g, c0), o_hi = min((P + 1) * g, c0 + L);
+            int64_t a0, a1;
+            int64_t o = o_lo;
+            if (o_lo > P * g) {  // the pane began before the run: its ring cell
+                const int64_t* e = cells + (P % R) * W;
+                a0 = e[0];
+                a1 = W == 2 ? e[1] : 0;
+            } else {
+                record_cell(AGG, val ? val[perm[i + (o - c0)]] : 0, a0, a1);
+                ++o;
+            }
+            for (; o < o_hi; ++o) {
+                int64_t b0, b1;
+                record_cell(AGG, val ? val[perm[i + (o - c0)]] : 0, b0, b1);
+                fold_cell(AGG, a0, a1, b0, b1);
+            }
+            v0[nt + threadIdx.x] = a0;
+            v1[nt + threadIdx.x] = a1;
+        }
+        __syncthreads();
+        // firings in this step: count c = f * slide with c - 1 in the step's panes
+        const int64_t lo = max(c0 + 1, P0 * g + 1), hi = min(c0 + L, (P0 + kCntChunk) * g);
+        const int64_t f0 = (lo + G.slide - 1) / G.slide;
+        const int64_t f1 = hi / G.slide;
+        for (int64_t f = f0 + threadIdx.x; f <= f1; f += blockDim.x) {
+            const int64_t c = f * G.slide;
+            const int64_t len = c < G.size ? c : G.size;
+            const int64_t p0 = (c - len) / g, p1 = c / g;
+            int64_t r0, r1;
+            pane_val(p0, P0, P0, r0, r1);
+            for (int64_t q = p0 + 1; q < p1; ++q) {
+                int64_t b0, b1;
+                pane_val(q, P0, P0, b0, b1);
+                fold_cell(AGG, r0, r1, b0, b1);
+            }
+            cnt_emit<AGG>(st, ok, os, oe, orr, key, c, len, r0, r1);
+        }
+        // the R panes before the next step (after the last step: the run's last R panes)
+        const int64_t tail_end = min(P0 + kCntChunk, pe + 1);
+        for (int q = threadIdx.x; q < nt; q += blockDim.x) {
+            int64_t a = 0, b = 0;
+            pane_val(tail_end - nt + q, P0, P0, a, b);
+            t0[q] = a;
+            t1[q] = b;
+        }
+        __syncthreads();
+        for (int q = threadIdx.x; q < nt; q += blockDim.x) {
+            v0[q] = t0[q];
+            v1[q] = t1[q];
+        }
+        __syncthreads();
+    }
+    // ring: the run's last R panes (older panes keep their cells)
+    for (int q = threadIdx.x; q < R; q += blockDim.x) {
+        const int64_t P = pe - q;
+        if (P < pf) continue;
+        int64_t a, b;
+        pane_val(P, pe + 1, pe + 1, a, b);
+        int64_t* e = cells + (P % R) * W;
+        e[0] = a;
+        if (W == 2) e[1] = b;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) sp[1] = c0 + L;
 }
 
 // Restore of count-window state: one thread per entry (key, element count, ring of pane
@@ -648,30 +782,30 @@ __global__ void __launch_bounds__(256) k_cnt_restore(TableView t, const int64_t*
 struct SessionState {
     gw_config cfg{};
     hipStream_t stream = nullptr;
-    TableView tv{};
+    TableView tv{};          // main table (sessions: K1 inline; count windows: the pane ring)
+    TableView wv{};          // wide table (sessions of keys with more than K1 in flight)
     DevStatus* d_st = nullptr;
     DevStatus* h_st = nullptr;
-    long long* d_mm = nullptr;
-    uint64_t* k0 = nullptr;
-    uint64_t* k1 = nullptr;
-    uint32_t* v0 = nullptr;
-    uint32_t* v1 = nullptr;
-    uint32_t* r0 = nullptr;
+    uint32_t* slot[2] = {nullptr, nullptr};  // per record: slot (sort keys, double buffer)
+    uint32_t* perm[2] = {nullptr, nullptr};  // per record: arrival index (sort values)
+    uint32_t* r0 = nullptr;  // punted / retried run heads
     uint32_t* r1 = nullptr;
-    void* scratch = nullptr;
+    int64_t* mig = nullptr;  // migration lists (main pass -> wide table)
+    void* sort_tmp = nullptr;
+    size_t sort_tmp_bytes = 0;
     int64_t buf_cap = 0;
     int64_t* o_key = nullptr;
     int64_t* o_start = nullptr;
     int64_t* o_end = nullptr;
     int64_t* o_res = nullptr;
     int64_t o_cap = 0;
+    int64_t* lo_buf[3] = {nullptr, nullptr, nullptr};  // late side output: key | ts | value
+    int64_t lo_cap = 0, lo_head = 0;
     int64_t wm = INT64_MIN;
     gw_stats stats{};
     bool timing = false;
     bool count_mode = false;  // GW_COUNT_TUMBLING / GW_COUNT_SLIDING (same slot table and row plumbing)
     CountGeom cg{};
-    int64_t* lo_buf[3] = {nullptr, nullptr, nullptr};  // late side output: key | ts | value
-    int64_t lo_cap = 0, lo_head = 0;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_pending[2], ev_pool;
     double t_total[2] = {0, 0};
     int64_t t_count[2] = {0, 0};
@@ -732,11 +866,13 @@ static int set_word(SessionState* s, size_t off, unsigned long long v, std::stri
     return GW_OK;
 }
 
-static int alloc_sess_table(SessionState* s, TableView& t, int64_t cap, int K, std::string& err) {
+// ring = sessions (or count panes) per slot, words = int64 words each
+static int alloc_table(SessionState* s, TableView& t, int64_t cap, int ring, int words, std::string& err) {
     t = s->tv;
     t.cap = cap;
-    t.ring = K;
-    t.stride_w = (int)(((2 + K * t.words) + 7) / 8 * 8);
+    t.ring = ring;
+    t.words = words;
+    t.stride_w = (int)(((2 + ring * words) + 7) / 8 * 8);
     SCHECK(hipMalloc((void**)&t.base, (size_t)(cap + 1) * t.stride_w * 8));
     hipLaunchKernelGGL(k_sess_init, dim3(grid_of(cap + 1)), dim3(256), 0, s->stream, t);
     SCHECK(hipGetLastError());
@@ -749,11 +885,10 @@ int session_create(SessionState*& out, const gw_config& cfg, int64_t cap, hipStr
     s->cfg = cfg;
     s->stream = stream;
     s->tv.agg = cfg.agg;
-    s->tv.words = cell_words(cfg.agg) == 2 ? 4 : 3;
+    s->wv.agg = cfg.agg;
     std::string& err = why;
     SCHECK(hipMalloc((void**)&s->d_st, sizeof(DevStatus)));
     SCHECK(hipHostMalloc((void**)&s->h_st, sizeof(DevStatus), hipHostMallocDefault));
-    SCHECK(hipMalloc((void**)&s->d_mm, 16));
     SCHECK(hipMemset(s->d_st, 0, sizeof(DevStatus)));
     memset(s->h_st, 0, sizeof(DevStatus));
     int rc;
@@ -763,15 +898,15 @@ int session_create(SessionState*& out, const gw_config& cfg, int64_t cap, hipStr
         int64_t a = size, b = slide;
         while (b) { const int64_t t = a % b; a = b; b = t; }
         s->cg = CountGeom{size, slide, a};
-        s->tv.words = cell_words(cfg.agg);
-        rc = alloc_sess_table(s, s->tv, cap, (int)(size / a), why);  // ring of size/g panes
+        rc = alloc_table(s, s->tv, cap, (int)(size / a), cell_words(cfg.agg), why);  // ring of size/g panes
         if (rc) { session_destroy(s); return rc; }
         out = s;
         return GW_OK;
     }
-    // K so that the slot fills a 64-byte (sum/count/min/max) or 128-byte (avg) line
-    const int K = s->tv.words == 3 ? 2 : 3;
-    rc = alloc_sess_table(s, s->tv, cap, K, why);
+    // K1 so that the slot fills a 64-byte (sum/count/min/max) or 128-byte (avg) line
+    const int words = cell_words(cfg.agg) == 2 ? 4 : 3;
+    rc = alloc_table(s, s->tv, cap, words == 3 ? 2 : 3, words, why);
+    if (rc == GW_OK) rc = alloc_table(s, s->wv, 1024, 16, kWideWords, why);
     if (rc) { session_destroy(s); return rc; }
     out = s;
     return GW_OK;
@@ -781,11 +916,12 @@ void session_destroy(SessionState* s) {
     if (!s) return;
     hipStreamSynchronize(s->stream);
     hipFree(s->tv.base);
+    hipFree(s->wv.base);
     hipFree(s->d_st);
     hipHostFree(s->h_st);
-    hipFree(s->d_mm);
-    hipFree(s->k0); hipFree(s->k1); hipFree(s->v0); hipFree(s->v1); hipFree(s->r0); hipFree(s->r1);
-    hipFree(s->scratch);
+    for (int q = 0; q < 2; ++q) { hipFree(s->slot[q]); hipFree(s->perm[q]); }
+    hipFree(s->r0); hipFree(s->r1); hipFree(s->mig);
+    hipFree(s->sort_tmp);
     hipFree(s->o_key); hipFree(s->o_start); hipFree(s->o_end); hipFree(s->o_res);
     for (auto* p : s->lo_buf) hipFree(p);
     for (int w = 0; w < 2; ++w) for (auto& p : s->ev_pending[w]) s->ev_pool.push_back(p);
@@ -796,47 +932,73 @@ void session_destroy(SessionState* s) {
 static int ensure_bufs(SessionState* s, int64_t n, std::string& err) {
     if (n <= s->buf_cap) return GW_OK;
     const int64_t c = std::max<int64_t>(n + n / 4, 1 << 16);
-    hipStreamSynchronize(s->stream);
-    hipFree(s->k0); hipFree(s->k1); hipFree(s->v0); hipFree(s->v1); hipFree(s->r0); hipFree(s->r1);
-    hipFree(s->scratch);
-    SCHECK(hipMalloc((void**)&s->k0, c * 8));
-    SCHECK(hipMalloc((void**)&s->k1, c * 8));
-    SCHECK(hipMalloc((void**)&s->v0, c * 4));
-    SCHECK(hipMalloc((void**)&s->v1, c * 4));
+    SCHECK(hipStreamSynchronize(s->stream));
+    for (int q = 0; q < 2; ++q) { hipFree(s->slot[q]); hipFree(s->perm[q]); }
+    hipFree(s->r0); hipFree(s->r1); hipFree(s->mig); hipFree(s->sort_tmp);
+    s->mig = nullptr;
+    for (int q = 0; q < 2; ++q) {
+        SCHECK(hipMalloc((void**)&s->slot[q], c * 4));
+        SCHECK(hipMalloc((void**)&s->perm[q], c * 4));
+    }
     SCHECK(hipMalloc((void**)&s->r0, c * 4));
     SCHECK(hipMalloc((void**)&s->r1, c * 4));
-    SCHECK(hipMalloc((void**)&s->scratch, radix_sort_scratch_bytes(c)));
+    if (!s->count_mode) SCHECK(hipMalloc((void**)&s->mig, (size_t)c * (2 + kWideWords * kLaneSess) * 8));
+    rocprim::double_buffer<uint32_t> kb(s->slot[0], s->slot[1]), vb(s->perm[0], s->perm[1]);
+    size_t bytes = 0;
+    SCHECK(rocprim::radix_sort_pairs(nullptr, bytes, kb, vb, (size_t)c, 0, 32, s->stream));
+    SCHECK(hipMalloc(&s->sort_tmp, bytes));
+    s->sort_tmp_bytes = bytes;
     s->buf_cap = c;
     return GW_OK;
 }
 
-static int rehash_sess(SessionState* s, int64_t new_cap, std::string& err) {
-    TableView nt;
-    int rc = alloc_sess_table(s, nt, new_cap, s->tv.ring, err);
-    if (rc) return rc;
-    SCHECK(launch_status_set(s->d_st, 0, 0, 1, s->stream));  // zero sh[].ins (used slots)
-    if (s->count_mode)
-        hipLaunchKernelGGL(k_cnt_rehash, dim3(grid_of(s->tv.cap + 1)), dim3(256), 0, s->stream, s->tv, nt, s->d_st);
-    else
-        hipLaunchKernelGGL(k_sess_rehash, dim3(grid_of(s->tv.cap + 1)), dim3(256), 0, s->stream, s->tv, nt, s->d_st);
-    SCHECK(hipGetLastError());
-    SCHECK(hipStreamSynchronize(s->stream));
-    hipFree(s->tv.base);
-    s->tv = nt;
-    s->stats.rehashes++;
-    return session_refresh(s, err);
+// Records of the batch, grouped by slot in arrival order: stable LSD radix sort of (slot,
+// arrival index) over the slot bits.  Returns the sorted buffers.
+static int sort_by_slot(SessionState* s, int64_t n, int64_t cap, const uint32_t** sk, const uint32_t** sp,
+                        std::string& err) {
+    int bits = 1;
+    while (bits < 32 && ((uint64_t)(cap + 1) >> bits)) ++bits;
+    rocprim::double_buffer<uint32_t> kb(s->slot[0], s->slot[1]), vb(s->perm[0], s->perm[1]);
+    size_t bytes = s->sort_tmp_bytes;
+    SCHECK(rocprim::radix_sort_pairs(s->sort_tmp, bytes, kb, vb, (size_t)n, 0, bits, s->stream));
+    *sk = kb.current();
+    *sp = vb.current();
+    return GW_OK;
 }
 
-static int widen(SessionState* s, int newK, std::string& err) {
+// Grow a table to new_cap slots (and/or new ring): rehash its state into a fresh table.
+static int regrow(SessionState* s, TableView& t, int64_t new_cap, int new_ring, bool wide, std::string& err) {
     TableView nt;
-    int rc = alloc_sess_table(s, nt, s->tv.cap, newK, err);
+    int rc = alloc_table(s, nt, new_cap, new_ring, t.words, err);
     if (rc) return rc;
-    hipLaunchKernelGGL(k_sess_rewiden, dim3(grid_of(s->tv.cap + 1)), dim3(256), 0, s->stream, s->tv, nt);
+    if (wide) {
+        SCHECK(launch_status_set(s->d_st, offsetof(DevStatus, pad[2]) / 8, 0, -1, s->stream));
+    } else {
+        SCHECK(launch_status_set(s->d_st, 0, 0, 1, s->stream));  // zero sh[].ins (used slots)
+    }
+    const int wps = s->count_mode ? t.ring * t.words : (wide ? -1 : t.ring * t.words);
+    hipLaunchKernelGGL(k_sess_rehash, dim3(grid_of(t.cap + 1)), dim3(256), 0, s->stream, t, nt, wps, s->d_st,
+                       wide ? -1 : 1);
     SCHECK(hipGetLastError());
     SCHECK(hipStreamSynchronize(s->stream));
-    hipFree(s->tv.base);
-    s->tv = nt;
+    hipFree(t.base);
+    t = nt;
+    s->stats.rehashes++;
+    rc = session_refresh(s, err);
+    if (rc) return rc;
+    if (s->h_st->flags & GW_DF_TABLE_FULL) { err = "session state table rehash overflow"; return GW_E_OOM; }
     return GW_OK;
+}
+
+// Room for `add` more wide keys (load <= 0.7) and lists of `need` sessions.
+static int ensure_wide(SessionState* s, int64_t add, int64_t need, std::string& err) {
+    const int64_t used = (int64_t)s->h_st->pad[2];
+    int64_t cap = s->wv.cap;
+    while ((double)(used + add) > 0.7 * (double)cap) cap *= 2;
+    int ring = s->wv.ring;
+    while (ring < need) ring *= 2;
+    if (cap == s->wv.cap && ring == s->wv.ring) return GW_OK;
+    return regrow(s, s->wv, cap, ring, true, err);
 }
 
 static int ensure_rows(SessionState* s, int64_t need, std::string& err) {
@@ -898,36 +1060,72 @@ int session_drain_late(SessionState* s, int64_t* key, int64_t* ts, int64_t* val,
     return c < pending ? GW_E_OUTPUT_FULL : GW_OK;
 }
 
+// Slot per record and the stable grouping by slot (both modes).  Grows the main table to
+// keep its load below 0.7 for `n` possible new keys.
+static int group_records(SessionState* s, int64_t n, const int64_t* key, const int64_t* ts, const uint32_t** sk,
+                         const uint32_t** sp, std::string& err) {
+    int rc;
+    if ((double)(s->h_st->used_slots + n) > 0.7 * (double)s->tv.cap &&
+        ((double)s->h_st->used_slots > 0.7 * (double)s->tv.cap ||
+         (double)(s->h_st->used_slots + n) > 0.95 * (double)s->tv.cap)) {
+        int64_t want = s->tv.cap;
+        while ((double)(s->h_st->used_slots + n) > 0.7 * (double)want) want *= 2;
+        if ((rc = regrow(s, s->tv, want, s->tv.ring, false, err))) return rc;
+    }
+    if ((rc = ensure_bufs(s, n, err))) return rc;
+    for (int attempt = 0;; ++attempt) {
+        hipLaunchKernelGGL(k_sess_prep, dim3(grid_of(n)), dim3(256), 0, s->stream, key, ts, n, s->tv, s->slot[0],
+                           s->perm[0], s->d_st);
+        if ((rc = session_refresh(s, err))) return rc;
+        if (!(s->h_st->flags & GW_DF_TABLE_FULL)) break;
+        if (attempt > 4) { err = "session state table full"; return GW_E_OOM; }
+        SCHECK(launch_status_set(s->d_st, 0, 0, 2, s->stream));  // zero sh[].flags
+        if ((rc = regrow(s, s->tv, s->tv.cap * 2, s->tv.ring, false, err))) return rc;
+    }
+    return sort_by_slot(s, n, s->tv.cap, sk, sp, err);
+}
+
+// Count windows: short runs one thread each, hot keys' long runs one workgroup each.
+static int launch_count_apply(SessionState* s, const uint32_t* ks, const uint32_t* perm, int64_t n, const int64_t* val,
+                              std::string& err) {
+    int rc;
+    if ((rc = set_word(s, offsetof(DevStatus, overflow), 0, err))) return rc;
+    const int64_t* v = s->cfg.agg == GW_COUNT ? nullptr : val;
+#define L(A)                                                                                               \
+    hipLaunchKernelGGL(k_cnt_apply<A>, dim3(grid_of(n)), dim3(256), 0, s->stream, s->tv, s->cg, ks, perm, n, v, \
+                       s->o_key, s->o_start, s->o_end, s->o_res, s->r0, s->d_st)
+    GW_AGG_SWITCH(s->cfg.agg, L);
+#undef L
+    SCHECK(hipGetLastError());
+    if ((rc = session_refresh(s, err))) return rc;
+    const int64_t nl = (int64_t)s->h_st->overflow;
+    if (!nl) return GW_OK;
+    const size_t lds = (size_t)2 * (2 * s->tv.ring + kCntChunk) * 8;
+#define L(A)                                                                                                  \
+    if (lds > 65536) SCHECK(hipFuncSetAttribute((const void*)k_cnt_long<A>,                                   \
+                                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));       \
+    hipLaunchKernelGGL(k_cnt_long<A>, dim3((unsigned)nl), dim3(kCntChunk), lds, s->stream, s->tv, s->cg, ks, perm, \
+                       n, v, s->o_key, s->o_start, s->o_end, s->o_res, s->r0, s->d_st)
+    GW_AGG_SWITCH(s->cfg.agg, L);
+#undef L
+    SCHECK(hipGetLastError());
+    return GW_OK;
+}
+
 // Count windows: slot per record, stable grouping by slot, one in-order fold per key.
 static int count_ingest(SessionState* s, int64_t n, const int64_t* key, const int64_t* val, std::string& err) {
     int rc;
     if ((rc = session_refresh(s, err))) return rc;
     if (n <= 0) return GW_OK;
-    if ((int64_t)n > (int64_t)0xffffffffLL) { err = "batch too large"; return GW_E_INVALID; }
-    if ((double)(s->h_st->used_slots + n) > 0.7 * (double)s->tv.cap) {
-        int64_t want = s->tv.cap;
-        while ((double)(s->h_st->used_slots + n) > 0.7 * (double)want) want *= 2;
-        if ((rc = rehash_sess(s, want, err))) return rc;
-    }
-    if ((rc = ensure_bufs(s, n, err))) return rc;
+    if ((int64_t)n > (int64_t)0x7fffffffLL) { err = "batch too large"; return GW_E_INVALID; }
     // every element fires at most one window
     if ((rc = ensure_rows(s, (int64_t)s->h_st->rows + n, err))) return rc;
-    int slot_bits = 1;
-    while (slot_bits < 63 && ((uint64_t)(s->tv.cap + 1) >> slot_bits)) ++slot_bits;
     auto ev = s->timing ? get_ev(s) : std::pair<hipEvent_t, hipEvent_t>{};
     if (s->timing) SCHECK(hipEventRecord(ev.first, s->stream));
-    hipLaunchKernelGGL(k_cnt_slot, dim3(grid_of(n)), dim3(256), 0, s->stream, s->tv, key, n, s->k0, s->v0, s->d_st);
-    SCHECK(hipGetLastError());
-    int alt = 0;
-    SCHECK(radix_sort_pairs(s->k0, s->v0, s->k1, s->v1, n, slot_bits, s->scratch, s->stream, &alt));
-    const uint64_t* ks = alt ? s->k1 : s->k0;
-    const uint32_t* perm = alt ? s->v1 : s->v0;
-#define L(A)                                                                                             \
-    hipLaunchKernelGGL(k_cnt_apply<A>, dim3(grid_of(n)), dim3(256), 0, s->stream, s->tv, s->cg, ks, perm, n, \
-                       s->cfg.agg == GW_COUNT ? nullptr : val, s->o_key, s->o_start, s->o_end, s->o_res, s->d_st)
-    GW_AGG_SWITCH(s->cfg.agg, L);
-#undef L
-    SCHECK(hipGetLastError());
+    const uint32_t* ks;
+    const uint32_t* perm;
+    if ((rc = group_records(s, n, key, nullptr, &ks, &perm, err))) return rc;
+    if ((rc = launch_count_apply(s, ks, perm, n, val, err))) return rc;
     if (s->timing) {
         SCHECK(hipEventRecord(ev.second, s->stream));
         s->ev_pending[0].push_back(ev);
@@ -943,51 +1141,14 @@ int session_ingest(SessionState* s, int64_t n, const int64_t* key, const int64_t
     int rc;
     if ((rc = session_refresh(s, err))) return rc;
     if (n <= 0) return GW_OK;
-    if ((int64_t)n > (int64_t)0xffffffffLL) { err = "batch too large"; return GW_E_INVALID; }
-    // keep the linear-probing load below 0.7 (worst case: every record a new key)
-    if ((double)s->h_st->used_slots > 0.7 * (double)s->tv.cap ||
-        (double)(s->h_st->used_slots + n) > 0.95 * (double)s->tv.cap) {
-        int64_t want = s->tv.cap;
-        while ((double)(s->h_st->used_slots + n) > 0.7 * (double)want) want *= 2;
-        if ((rc = rehash_sess(s, want, err))) return rc;
-    }
-    if ((rc = ensure_bufs(s, n, err))) return rc;
-    const long long init_mm[2] = {INT64_MAX, INT64_MIN};
-    SCHECK(hipMemcpyAsync(s->d_mm, init_mm, 16, hipMemcpyHostToDevice, s->stream));
-    hipLaunchKernelGGL(k_sess_minmax, dim3(grid_of(n)), dim3(256), 0, s->stream, ts, n, s->d_mm, s->d_st);
-    long long mm[2];
-    SCHECK(hipMemcpyAsync(mm, s->d_mm, 16, hipMemcpyDeviceToHost, s->stream));
-    if ((rc = session_refresh(s, err))) return rc;
-    const uint64_t span = (uint64_t)mm[1] - (uint64_t)mm[0];
-    int ts_bits = 1;
-    while (ts_bits < 64 && (span >> ts_bits)) ++ts_bits;
-    int slot_bits = 1;
-    while (slot_bits < 63 && ((uint64_t)(s->tv.cap) >> slot_bits)) ++slot_bits;
-    if (ts_bits + slot_bits > 64) {
-        err = "session batch spans too many milliseconds for the (slot, ts) sort key";
-        return GW_E_UNSUPPORTED;
-    }
+    if ((int64_t)n > (int64_t)0x7fffffffLL) { err = "batch too large"; return GW_E_INVALID; }
     auto ev = s->timing ? get_ev(s) : std::pair<hipEvent_t, hipEvent_t>{};
     if (s->timing) SCHECK(hipEventRecord(ev.first, s->stream));
-    for (int attempt = 0;; ++attempt) {
-        hipLaunchKernelGGL(k_sess_prep, dim3(grid_of(n)), dim3(256), 0, s->stream, key, ts, n, (int64_t)mm[0], ts_bits,
-                           s->tv, s->k0, s->v0, s->d_st);
-        if ((rc = session_refresh(s, err))) return rc;
-        if (!(s->h_st->flags & GW_DF_TABLE_FULL)) break;
-        if (attempt > 4) { err = "session state table full"; return GW_E_OOM; }
-        SCHECK(launch_status_set(s->d_st, 0, 0, 2, s->stream));  // zero sh[].flags
-        if ((rc = rehash_sess(s, s->tv.cap * 2, err))) return rc;
-        slot_bits++;
-        if (ts_bits + slot_bits > 64) { err = "session sort key overflow"; return GW_E_UNSUPPORTED; }
-    }
-    int alt = 0;
-    SCHECK(radix_sort_pairs(s->k0, s->v0, s->k1, s->v1, n, ts_bits + slot_bits, s->scratch, s->stream, &alt));
     SegArgs a{};
-    a.skey = alt ? s->k1 : s->k0;
-    a.perm = alt ? s->v1 : s->v0;
+    if ((rc = group_records(s, n, key, ts, &a.slot, &a.perm, err))) return rc;
     a.n = n;
-    a.ts_bits = ts_bits;
-    a.ts_min = mm[0];
+    a.key = key;
+    a.ts = ts;
     a.val = val;
     a.gap = s->cfg.gap;
     a.wm = wm;
@@ -998,39 +1159,57 @@ int session_ingest(SessionState* s, int64_t n, const int64_t* key, const int64_t
         if ((rc = ensure_rows(s, (int64_t)s->h_st->rows + n, err))) return rc;
         a.o_key = s->o_key; a.o_start = s->o_start; a.o_end = s->o_end; a.o_res = s->o_res;
     }
-    a.ts = ts;
-    a.key = key;
     if (s->cfg.flags & GW_FLAG_LATE_SIDE_OUTPUT) {
         if ((rc = ensure_late(s, (int64_t)s->h_st->n_late_out + n, err))) return rc;
         a.lo_key = s->lo_buf[0]; a.lo_ts = s->lo_buf[1]; a.lo_val = s->lo_buf[2];
     }
+    // main pass
+    if ((rc = set_word(s, offsetof(DevStatus, overflow), 0, err))) return rc;
+    if ((rc = set_word(s, offsetof(DevStatus, pad[0]), 0, err))) return rc;
+    if ((rc = set_word(s, offsetof(DevStatus, pad[1]), 0, err))) return rc;
+    a.t = s->tv;
+    a.w = s->wv;
+    a.punt = s->r0;
+    a.mig = s->mig;
+    const unsigned gs = (unsigned)((n + kSegThreads - 1) / kSegThreads);
+#define L(A) hipLaunchKernelGGL(k_sess_segment<A>, dim3(gs), dim3(kSegThreads), 0, s->stream, a)
+    GW_AGG_SWITCH(s->cfg.agg, L);
+#undef L
+    SCHECK(hipGetLastError());
+    if ((rc = session_refresh(s, err))) return rc;
+    const int64_t n_mig = (int64_t)s->h_st->pad[0];
+    int64_t n_punt = (int64_t)s->h_st->overflow;
+    if (n_mig) {  // finished lists of more than K1 sessions move to the wide table
+        if ((rc = ensure_wide(s, n_mig, (int64_t)s->h_st->pad[1], err))) return rc;
+        hipLaunchKernelGGL(k_sess_migrate, dim3(grid_of(n_mig)), dim3(256), 0, s->stream, s->tv, s->wv, s->mig, n_mig,
+                           s->d_st);
+        SCHECK(hipGetLastError());
+        if ((rc = session_refresh(s, err))) return rc;
+        if (s->h_st->flags & GW_DF_TABLE_FULL) { err = "session wide table full"; return GW_E_OOM; }
+    }
+    // wide pass over the punted runs; runs that do not fit K2 retry after widening
     uint32_t* rin = s->r0;
     uint32_t* rout = s->r1;
-    int64_t n_retry = 0;
-    for (int pass = 0;; ++pass) {
+    for (int pass = 0; n_punt > 0; ++pass) {
+        if (pass > 40) { err = "session wide table did not converge"; return GW_E_DEVICE; }
+        if ((rc = ensure_wide(s, n_punt, 0, err))) return rc;
         if ((rc = set_word(s, offsetof(DevStatus, overflow), 0, err))) return rc;
         if ((rc = set_word(s, offsetof(DevStatus, pad[1]), 0, err))) return rc;
         a.t = s->tv;
-        a.retry_in = pass ? rin : nullptr;
-        a.n_retry_in = n_retry;
-        a.retry_out = rout;
-        const unsigned g = pass ? grid_of(n_retry) : grid_of(n);
-#define L(A) hipLaunchKernelGGL(k_sess_segment<A>, dim3(g), dim3(256), 0, s->stream, a)
+        a.w = s->wv;
+        a.runs = rin;
+        a.n_runs = n_punt;
+        a.retry = rout;
+#define L(A) hipLaunchKernelGGL(k_sess_wide<A>, dim3(grid_of(n_punt)), dim3(256), 0, s->stream, a)
         GW_AGG_SWITCH(s->cfg.agg, L);
 #undef L
         SCHECK(hipGetLastError());
         if ((rc = session_refresh(s, err))) return rc;
-        if (!s->h_st->overflow) break;
-        const unsigned long long need = s->h_st->pad[1];
-        if (need > (unsigned long long)kMaxLocalSess || pass > 8) {
-            err = "more than 32 in-flight sessions for one key in one batch is not supported on the GPU path";
-            return GW_E_UNSUPPORTED;
+        n_punt = (int64_t)s->h_st->overflow;
+        if (n_punt) {
+            SCHECK(launch_status_set(s->d_st, 0, 0, 2, s->stream));  // zero sh[].flags (TABLE_FULL of the wide table)
+            if ((rc = ensure_wide(s, n_punt, (int64_t)s->h_st->pad[1], err))) return rc;
         }
-        int newK = s->tv.ring;
-        while ((unsigned long long)newK < need) newK *= 2;
-        if (newK > kMaxLocalSess) newK = kMaxLocalSess;
-        if ((rc = widen(s, newK, err))) return rc;
-        n_retry = (int64_t)s->h_st->overflow;
         std::swap(rin, rout);
     }
     if (s->timing) {
@@ -1049,27 +1228,19 @@ int session_fire(SessionState* s, int64_t wm, int64_t* fired, std::string& err) 
     int rc;
     if ((rc = session_refresh(s, err))) return rc;
     const int64_t before = (int64_t)s->h_st->rows;
-    const int64_t need = before + (int64_t)(s->h_st->used_slots + 1) * s->tv.ring;
-    if (need > s->o_cap) {
-        const int64_t c = std::max<int64_t>(need + need / 4, 1 << 16);
-        int64_t* nb[4];
-        for (int q = 0; q < 4; ++q) SCHECK(hipMalloc((void**)&nb[q], c * 8));
-        int64_t* old[4] = {s->o_key, s->o_start, s->o_end, s->o_res};
-        for (int q = 0; q < 4; ++q) {
-            if (old[q] && before) SCHECK(hipMemcpyAsync(nb[q], old[q], before * 8, hipMemcpyDeviceToDevice, s->stream));
-        }
-        SCHECK(hipStreamSynchronize(s->stream));
-        for (int q = 0; q < 4; ++q) hipFree(old[q]);
-        s->o_key = nb[0]; s->o_start = nb[1]; s->o_end = nb[2]; s->o_res = nb[3];
-        s->o_cap = c;
-    }
+    const int64_t need = before + (int64_t)(s->h_st->used_slots + 1) * s->tv.ring +
+                         (int64_t)(s->h_st->pad[2] + 1) * s->wv.ring;
+    if ((rc = ensure_rows(s, need, err))) return rc;
     auto ev = s->timing ? get_ev(s) : std::pair<hipEvent_t, hipEvent_t>{};
     if (s->timing) SCHECK(hipEventRecord(ev.first, s->stream));
     const unsigned fg = (unsigned)std::min<int64_t>(1024, std::max<int64_t>(1, (s->tv.cap + 1 + 255) / 256));
+    const int purge = (int)(s->cfg.allowed_lateness > 0 && s->cfg.trigger == GW_PURGING_EVENT_TIME_TRIGGER);
 #define L(A)                                                                                               \
     hipLaunchKernelGGL(k_sess_fire<A>, dim3(fg), dim3(256), 0, s->stream, s->tv, wm, s->cfg.allowed_lateness, \
-                       (int)(s->cfg.allowed_lateness > 0 && s->cfg.trigger == GW_PURGING_EVENT_TIME_TRIGGER), \
-                       s->o_key, s->o_start, s->o_end, s->o_res, s->d_st)
+                       purge, s->o_key, s->o_start, s->o_end, s->o_res, s->d_st);                          \
+    if (s->h_st->pad[2])                                                                                    \
+    hipLaunchKernelGGL(k_sess_fire_wide<A>, dim3(grid_of(s->wv.cap + 1)), dim3(256), 0, s->stream, s->wv, wm, \
+                       s->cfg.allowed_lateness, purge, s->o_key, s->o_start, s->o_end, s->o_res, s->d_st)
     GW_AGG_SWITCH(s->cfg.agg, L);
 #undef L
     SCHECK(hipGetLastError());
@@ -1095,34 +1266,42 @@ int session_clear_rows(SessionState* s, std::string& err) { return set_word(s, o
 // The heap backend snapshots, per key group, every (key, window) state entry plus the
 // MergingWindowSet mapping (HeapSnapshotStrategy.java:97-154, MergingWindowSet.java:
 // 95-104 persistState); in-flight sessions are exactly that state here, one
-// (key, start, end, a0, a1) entry per session.
+// (key, start, end, a0, a1, fired) entry per session.
 int session_collect(SessionState* s, int32_t kg_lo, int32_t kg_hi, std::vector<int64_t>& ent,
                     std::vector<int32_t>& kgs, std::string& err) {
     SCHECK(hipStreamSynchronize(s->stream));
-    const TableView& t = s->tv;
-    const size_t words = (size_t)(t.cap + 1) * t.stride_w;
-    std::vector<int64_t> h(words);
-    SCHECK(hipMemcpy(h.data(), t.base, words * 8, hipMemcpyDeviceToHost));
-    const int SW = t.words;
-    for (int64_t i = 0; i <= t.cap; ++i) {
-        const int64_t* sp = h.data() + (size_t)i * t.stride_w;
-        if (sp[1] == 0) continue;
-        const int64_t key = i == t.cap ? kEmptyKey : sp[0];
-        const int32_t kg = key_group_for_hash(java_long_hash(key), s->cfg.max_parallelism);
-        if (kg < kg_lo || kg > kg_hi) continue;
-        if (s->count_mode) {  // (key, element count, ring of pane accumulators)
-            ent.push_back(key);
-            ent.insert(ent.end(), sp + 1, sp + 2 + t.ring * SW);
-            kgs.push_back(kg);
-            continue;
-        }
-        const int cnt = (int)(uint32_t)(uint64_t)sp[1];
-        for (int q = 0; q < cnt; ++q) {
-            const int64_t* x = sp + 2 + q * SW;
-            const int64_t fired = (int64_t)(((uint64_t)sp[1] >> (32 + q)) & 1ull);  // kept under allowed lateness
-            const int64_t e[6] = {key, x[0], x[1], x[2], SW == 4 ? x[3] : 0, fired};
-            ent.insert(ent.end(), e, e + 6);
-            kgs.push_back(kg);
+    for (int tab = 0; tab < (s->count_mode ? 1 : 2); ++tab) {
+        const TableView& t = tab ? s->wv : s->tv;
+        const size_t words = (size_t)(t.cap + 1) * t.stride_w;
+        std::vector<int64_t> h(words);
+        SCHECK(hipMemcpy(h.data(), t.base, words * 8, hipMemcpyDeviceToHost));
+        const int SW = t.words;
+        for (int64_t i = 0; i <= t.cap; ++i) {
+            const int64_t* sp = h.data() + (size_t)i * t.stride_w;
+            if (sp[1] == 0) continue;
+            if (tab == 0 && !s->count_mode && ((uint64_t)sp[1] & kBigMeta)) continue;  // in the wide table
+            const int64_t key = i == t.cap ? kEmptyKey : sp[0];
+            const int32_t kg = key_group_for_hash(java_long_hash(key), s->cfg.max_parallelism);
+            if (kg < kg_lo || kg > kg_hi) continue;
+            if (s->count_mode) {  // (key, element count, ring of pane accumulators)
+                ent.push_back(key);
+                ent.insert(ent.end(), sp + 1, sp + 2 + t.ring * SW);
+                kgs.push_back(kg);
+                continue;
+            }
+            const int cnt = tab ? (int)sp[1] : (int)((uint64_t)sp[1] & 0x7fffffffull);
+            for (int q = 0; q < cnt; ++q) {
+                const int64_t* x = sp + 2 + q * SW;
+                int64_t e[6];
+                if (tab) {
+                    e[0] = key; e[1] = x[0]; e[2] = x[1]; e[3] = x[2]; e[4] = x[3]; e[5] = x[4] != 0;
+                } else {
+                    const int64_t fired = (int64_t)(((uint64_t)sp[1] >> (32 + q)) & 1ull);  // kept under lateness
+                    e[0] = key; e[1] = x[0]; e[2] = x[1]; e[3] = x[2]; e[4] = SW == 4 ? x[3] : 0; e[5] = fired;
+                }
+                ent.insert(ent.end(), e, e + 6);
+                kgs.push_back(kg);
+            }
         }
     }
     return GW_OK;
@@ -1135,7 +1314,7 @@ static int count_restore(SessionState* s, const int64_t* ent, int64_t n, std::st
     if ((double)(s->h_st->used_slots + n) > 0.7 * (double)s->tv.cap) {
         int64_t want = s->tv.cap;
         while ((double)(s->h_st->used_slots + n) > 0.7 * (double)want) want *= 2;
-        if ((rc = rehash_sess(s, want, err))) return rc;
+        if ((rc = regrow(s, s->tv, want, s->tv.ring, false, err))) return rc;
     }
     const int64_t bytes = n * session_entry_words(s) * 8;
     int64_t* d = nullptr;
@@ -1169,10 +1348,11 @@ int session_restore(SessionState* s, const int64_t* ent, int64_t n, std::string&
     });
     std::vector<int64_t> rk, roff, rs;
     rs.reserve((size_t)n * 5);
-    int maxk = 0, run = 0;
+    int64_t maxk = 0, run = 0, wide = 0;
     for (int64_t j = 0; j < n; ++j) {
         const int64_t* x = ent + ord[j] * 6;
         if (j == 0 || x[0] != rk.back()) {
+            if (j && run > s->tv.ring) wide++;
             rk.push_back(x[0]);
             roff.push_back(j);
             run = 0;
@@ -1180,21 +1360,14 @@ int session_restore(SessionState* s, const int64_t* ent, int64_t n, std::string&
         maxk = std::max(maxk, ++run);
         rs.insert(rs.end(), x + 1, x + 6);
     }
+    if (run > s->tv.ring) wide++;
     roff.push_back(n);
     const int64_t nk = (int64_t)rk.size();
-    if (maxk > kMaxLocalSess) {
-        err = "more than 32 in-flight sessions for one key is not supported on the GPU path";
-        return GW_E_UNSUPPORTED;
-    }
-    if (maxk > s->tv.ring) {
-        int newK = s->tv.ring;
-        while (newK < maxk) newK *= 2;
-        if ((rc = widen(s, std::min(newK, kMaxLocalSess), err))) return rc;
-    }
+    if (wide && (rc = ensure_wide(s, wide, maxk, err))) return rc;
     if ((double)(s->h_st->used_slots + nk) > 0.7 * (double)s->tv.cap) {
         int64_t want = s->tv.cap;
         while ((double)(s->h_st->used_slots + nk) > 0.7 * (double)want) want *= 2;
-        if ((rc = rehash_sess(s, want, err))) return rc;
+        if ((rc = regrow(s, s->tv, want, s->tv.ring, false, err))) return rc;
     }
     int64_t *d_k = nullptr, *d_o = nullptr, *d_s = nullptr;
     SCHECK(hipMalloc((void**)&d_k, nk * 8));
@@ -1204,10 +1377,8 @@ int session_restore(SessionState* s, const int64_t* ent, int64_t n, std::string&
     SCHECK(hipMemcpy(d_o, roff.data(), (nk + 1) * 8, hipMemcpyHostToDevice));
     SCHECK(hipMemcpy(d_s, rs.data(), n * 40, hipMemcpyHostToDevice));
     if ((rc = set_word(s, offsetof(DevStatus, overflow), 0, err))) return rc;
-#define L(A) \
-    hipLaunchKernelGGL(k_sess_restore<A>, dim3(grid_of(nk)), dim3(256), 0, s->stream, s->tv, d_k, d_o, d_s, nk, s->d_st)
-    GW_AGG_SWITCH(s->cfg.agg, L);
-#undef L
+    hipLaunchKernelGGL(k_sess_restore, dim3(grid_of(nk)), dim3(256), 0, s->stream, s->tv, s->wv, d_k, d_o, d_s, nk,
+                       s->d_st);
     SCHECK(hipGetLastError());
     rc = session_refresh(s, err);
     hipFree(d_k);
@@ -1216,7 +1387,7 @@ int session_restore(SessionState* s, const int64_t* ent, int64_t n, std::string&
     if (rc) return rc;
     if (s->h_st->flags & GW_DF_TABLE_FULL) { err = "session state table full"; return GW_E_OOM; }
     if (s->h_st->overflow) {
-        err = "restored sessions and in-flight sessions of one key exceed the slot's session list";
+        err = "a restored key already holds sessions in this operator (key group restored twice)";
         return GW_E_UNSUPPORTED;
     }
     return GW_OK;
@@ -1228,7 +1399,7 @@ void session_stats(SessionState* s, gw_stats* out) {
     out->late_dropped = (int64_t)s->h_st->late;
     out->live_keys = (int64_t)s->h_st->used_slots;
     out->table_capacity = s->tv.cap;
-    out->table_bytes = (int64_t)(s->tv.cap + 1) * s->tv.stride_w * 8;
+    out->table_bytes = (int64_t)(s->tv.cap + 1) * s->tv.stride_w * 8 + (int64_t)(s->wv.cap + 1) * s->wv.stride_w * 8;
     out->session_merges = (int64_t)s->h_st->merges;
     out->fires = s->stats.fires;
     out->rehashes = s->stats.rehashes;

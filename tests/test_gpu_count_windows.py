@@ -55,7 +55,8 @@ def run_both(oracle_lib, kw, keys, vals, cuts, **opkw):
 
 
 CONFIGS = [("count_tumbling", 5, 5), ("count_sliding", 4, 2), ("count_sliding", 250, 150),
-           ("count_sliding", 3, 5), ("count_tumbling", 1, 1), ("count_sliding", 64, 1)]
+           ("count_sliding", 3, 5), ("count_tumbling", 1, 1), ("count_sliding", 64, 1),
+           ("count_sliding", 300, 1), ("count_sliding", 1000, 999), ("count_sliding", 7, 3)]
 AGGS = ["count", "sum_i64", "min_i64", "max_f64", "avg_f64", "sum_i32", "avg_i64", "sum_f64"]
 
 

@@ -305,8 +305,8 @@ def test_far_future_records_and_watermark_jumps(oracle_lib, cfg, flags):
 
 
 def test_sessions_many_in_flight_per_key(oracle_lib):
-    """Up to 32 in-flight sessions per key: the slot widens its inline session list
-    (K = 2 -> 4 -> ... -> 32) and results stay exact."""
+    """Many in-flight sessions per key: keys beyond the slot's inline sessions move to the wide
+    table (K2 = 16 -> 32 -> ...) and results stay exact."""
     kw = dict(assigner="session", gap=100, agg="sum_i64")
     rng = np.random.default_rng(8)
     n = 3000
@@ -320,13 +320,28 @@ def test_sessions_many_in_flight_per_key(oracle_lib):
     assert compare(g, o, False) == []
 
 
-def test_sessions_beyond_inline_limit_fail_loudly():
-    op = gpu_operator(dict(assigner="session", gap=10, agg="count"))
-    ts = np.arange(40, dtype=np.int64) * 1000  # 40 disjoint sessions of one key, none fired
-    with pytest.raises(N.GpuWinError) as ei:
-        op.process_batch(np.zeros(40, np.int64), ts, None)
-    assert ei.value.code == -2
-    op.close()
+@pytest.mark.parametrize("lateness", [0, 5_000_000])
+@pytest.mark.parametrize("agg", ["count", "avg_f64"])
+def test_sessions_hundreds_in_flight_for_one_key(oracle_lib, lateness, agg):
+    """One key with hundreds of in-flight sessions (no per-key limit): 700 disjoint sessions,
+    then merges that bridge some of them, fired in steps; with allowed lateness the fired
+    sessions stay in the merging window set within the lateness horizon and late elements
+    merge into them (EventTimeTrigger.onElement FIRE)."""
+    kw = dict(assigner="session", gap=10, agg=agg, lateness=lateness)
+    rng = np.random.default_rng(12)
+    ts0 = np.arange(700, dtype=np.int64) * 1000
+    ts1 = rng.choice(ts0, 200) + 15          # bridge sessions t and t + 1000? no: extend them
+    ts2 = rng.integers(0, 700_000, 300).astype(np.int64)
+    ts = np.concatenate([ts0, ts1, ts2])
+    keys = np.zeros(len(ts), np.int64)
+    keys[::9] = 1
+    vals = rng.uniform(0, 100, len(ts)) if agg == "avg_f64" else np.zeros(len(ts), np.int64)
+    batches = [(0, 700, -1), (700, 900, 200_000), (900, 1200, 400_000)]
+    g, glate, _ = run_gpu(kw, keys, ts, vals, batches)
+    o, olate = run_oracle(oracle_lib, kw, keys, ts, vals, batches)
+    assert glate == olate
+    assert compare(g, o, agg == "avg_f64") == []
+    assert sum(len(x[0]) for x in o) > 500
 
 
 @pytest.mark.parametrize("flags", [N.FLAG_NO_REGION, N.FLAG_FORCE_REGION], ids=["direct", "region"])

@@ -219,7 +219,7 @@ def test_session_rescale_two_to_one_and_one_to_two(oracle_lib, agg):
 
 
 def test_session_restore_widens_for_many_sessions_per_key(oracle_lib):
-    """A key with more restored sessions than the slot's inline list widens it (K -> 32)."""
+    """A key with more restored sessions than the slot's inline list goes to the wide table."""
     kw = dict(assigner="session", gap=10, agg="sum_i64")
     keys = np.zeros(20, np.int64)
     ts = np.arange(20, dtype=np.int64) * 1000  # 20 disjoint sessions of one key, none fired
