@@ -33,7 +33,7 @@
 
 namespace gw {
 
-constexpr int kLaneSess = 8;        // sessions a thread replays in LDS
+constexpr int kLaneSess = 4;        // sessions a thread replays in LDS
 constexpr int kSegThreads = 128;
 constexpr int kWideWords = 5;       // wide-table session: start, end, a0, a1, fired
 constexpr uint64_t kBigMeta = 1ull << 31;  // main-table slot word 1: the key lives in the wide table
@@ -85,6 +85,37 @@ __device__ __forceinline__ bool cleaned_at(int64_t end, int64_t lateness, int64_
     return ct <= wm;
 }
 
+// The watermark at which a session needs the fire sweep: its timer (max timestamp) while it
+// has not fired, its cleanup time once it has (kept for allowed lateness).
+__device__ __forceinline__ int64_t due_time(int64_t end, bool fired, int64_t lateness) {
+    const int64_t mx = end - 1;
+    if (!fired) return mx;
+    int64_t ct;
+    if (__builtin_add_overflow(mx, lateness, &ct)) ct = INT64_MAX;
+    return ct;
+}
+
+// Per slot, the earliest due time of its sessions (INT64_MAX: none, or the key lives in the
+// wide table), in a dense array after the slots: the fire sweep reads 8 bytes per slot and
+// touches only the slots with something due.
+__device__ __forceinline__ int64_t* due_of(const TableView& t) { return t.base + (t.cap + 1) * (int64_t)t.stride_w; }
+
+__device__ __forceinline__ int64_t inline_due(const int64_t* sp, int SW, int64_t lateness) {
+    const int64_t w1 = sp[1];
+    if (slot_big(w1)) return INT64_MAX;
+    int64_t m = INT64_MAX;
+    for (int q = 0, c = slot_cnt(w1); q < c; ++q) m = min(m, due_time(sp[2 + q * SW + 1], slot_fired(w1, q), lateness));
+    return m;
+}
+__device__ __forceinline__ int64_t wide_due(const int64_t* sp, int64_t lateness) {
+    int64_t m = INT64_MAX;
+    for (int q = 0, c = (int)sp[1]; q < c; ++q) {
+        const int64_t* x = sp + 2 + q * kWideWords;
+        m = min(m, due_time(x[1], x[4] != 0, lateness));
+    }
+    return m;
+}
+
 // The empty state a purged session keeps (FIRE_AND_PURGE clears the contents, the window
 // stays in the merging window set until its cleanup time): the fold identity, with -0.0
 // for floating sums so that folding a single -0.0 keeps its sign.
@@ -123,11 +154,12 @@ __device__ __forceinline__ void sl_put(const SessList& l, int q, const Sess& v) 
 // a window that merges with nothing and is already late is skipped (late: counted or sent
 // to the side output); a merged or new window whose max timestamp <= watermark fires at
 // once (EventTimeTrigger.onElement FIRE; PurgingTrigger purges), otherwise its timer is
-// (re-)armed.  Returns false if a new session does not fit `cap`.
+// (re-)armed.  Returns false if a new session does not fit `cap`.  `dry`: no rows and no
+// side output are written (a trial replay that may be abandoned).
 template <int AGG>
 __device__ __forceinline__ bool add_element(const SegArgs& a, const SessList& l, int& cnt, int cap, int64_t key,
                                             int64_t idx, unsigned long long& late, unsigned long long& merges,
-                                            unsigned long long& flags) {
+                                            unsigned long long& flags, bool dry = false) {
     const int64_t ts = a.ts[idx];
     int64_t we;
     if (__builtin_add_overflow(ts, a.gap, &we)) { flags |= GW_DF_RANGE; return true; }
@@ -146,7 +178,7 @@ __device__ __forceinline__ bool add_element(const SegArgs& a, const SessList& l,
         if (cleaned_at(we, a.lateness, a.wm)) {  // isWindowLate: skipped; the element is late
             if (!a.lo_key) {
                 late++;
-            } else {  // sideOutput(element) (WindowOperator.java:440-446, 587-588)
+            } else if (!dry) {  // sideOutput(element) (WindowOperator.java:440-446, 587-588)
                 const unsigned long long o = atomicAdd(&a.st->n_late_out, 1ull);
                 a.lo_key[o] = key;
                 a.lo_ts[o] = ts;
@@ -162,7 +194,7 @@ __device__ __forceinline__ bool add_element(const SegArgs& a, const SessList& l,
         }
         Sess x{ws, we, c0, c1, (int64_t)(we - 1 <= a.wm)};
         if (x.f) {  // onElement: FIRE (PurgingTrigger: FIRE_AND_PURGE)
-            emit_now<AGG>(a, key, x);
+            if (!dry) emit_now<AGG>(a, key, x);
             if (a.purge) purge_acc<AGG>(x.a0, x.a1);
         }
         sl_put(l, q, x);
@@ -181,7 +213,7 @@ __device__ __forceinline__ bool add_element(const SegArgs& a, const SessList& l,
     fold_cell(AGG, m.a0, m.a1, c0, c1);
     m.f = m.e - 1 <= a.wm;  // onElement FIRE, or onMerge registers the merged window's timer
     if (m.f) {
-        emit_now<AGG>(a, key, m);
+        if (!dry) emit_now<AGG>(a, key, m);
         if (a.purge) purge_acc<AGG>(m.a0, m.a1);
     }
     sl_put(l, lo, m);
@@ -192,8 +224,11 @@ __device__ __forceinline__ bool add_element(const SegArgs& a, const SessList& l,
 }
 
 // Main pass: one thread per key's run.  The run's elements replay against the key's
-// inline sessions in the thread's LDS lane; a run that could need more than kLaneSess
-// sessions, or a key already in the wide table, goes to the wide pass.
+// inline sessions in the thread's LDS lane.  A run that could need more than kLaneSess
+// sessions is first replayed dry (no rows, no side output); only if the list really
+// outgrows the lane, or the key is already in the wide table, does it go to the wide pass.
+// Without allowed lateness and side output a replay has no effects beyond the slot, so
+// the dry replay is the real one.
 template <int AGG>
 __global__ void __launch_bounds__(kSegThreads) k_sess_segment(SegArgs a) {
     __shared__ int64_t lane[5 * kLaneSess * kSegThreads];
@@ -207,27 +242,45 @@ __global__ void __launch_bounds__(kSegThreads) k_sess_segment(SegArgs a) {
         int64_t* sp = slot_ptr(a.t, (int64_t)slot);
         const int64_t w1 = sp[1];
         const int SW = a.t.words;
-        int cnt = slot_cnt(w1);
-        if (slot_big(w1) || cnt + (j - i) > kLaneSess) {
-            const unsigned long long at = atomicAdd(&a.st->overflow, 1ull);
-            a.punt[at] = (uint32_t)i;
-        } else {
+        const int64_t key = sp[0];  // the sentinel slot's key word is Long.MIN_VALUE, its key
+        auto load = [&](int& cnt) {
+            cnt = slot_cnt(w1);
             for (int q = 0; q < cnt; ++q) {
                 const int64_t* x = sp + 2 + q * SW;
                 sl_put(l, q, Sess{x[0], x[1], x[2], SW == 4 ? x[3] : 0, (int64_t)slot_fired(w1, q)});
             }
-            const int64_t key = sp[0];  // the sentinel slot's key word is Long.MIN_VALUE, its key
-            for (int64_t r = i; r < j; ++r) add_element<AGG>(a, l, cnt, kLaneSess, key, a.perm[r], late, merges, flags);
+        };
+        int cnt = 0;
+        bool ok = !slot_big(w1), done = false;
+        if (ok && slot_cnt(w1) + (j - i) > kLaneSess) {  // could outgrow the lane: dry replay
+            const unsigned long long l0 = late, m0 = merges;
+            load(cnt);
+            for (int64_t r = i; r < j && ok; ++r)
+                ok = add_element<AGG>(a, l, cnt, kLaneSess, key, a.perm[r], late, merges, flags, true);
+            done = ok && a.lateness == 0 && !a.lo_key;
+            if (!done) { late = l0; merges = m0; }
+        }
+        if (!ok) {
+            const unsigned long long at = atomicAdd(&a.st->overflow, 1ull);
+            a.punt[at] = (uint32_t)i;
+        } else {
+            if (!done) {
+                load(cnt);
+                for (int64_t r = i; r < j; ++r) add_element<AGG>(a, l, cnt, kLaneSess, key, a.perm[r], late, merges, flags);
+            }
             if (cnt <= a.t.ring) {
                 uint64_t fired = 0;
+                int64_t due = INT64_MAX;
                 for (int q = 0; q < cnt; ++q) {
                     const Sess v = sl_get(l, q);
                     int64_t* x = sp + 2 + q * SW;
                     x[0] = v.s; x[1] = v.e; x[2] = v.a0;
                     if (SW == 4) x[3] = v.a1;
                     fired |= (uint64_t)(v.f != 0) << q;
+                    due = min(due, due_time(v.e, v.f != 0, a.lateness));
                 }
                 sp[1] = (int64_t)((fired << 32) | (uint64_t)(uint32_t)cnt);
+                due_of(a.t)[slot] = due;
             } else {  // more sessions than the slot holds: the finished list moves to the wide table
                 const unsigned long long at = atomicAdd(&a.st->pad[0], 1ull);
                 int64_t* m = a.mig + at * (2 + kWideWords * kLaneSess);
@@ -263,7 +316,7 @@ __device__ __forceinline__ int64_t wide_slot_of(const TableView& w, int64_t key,
 
 // Finished lists of the main pass -> the wide table.
 __global__ void __launch_bounds__(256) k_sess_migrate(TableView t, TableView w, const int64_t* mig, int64_t n,
-                                                      DevStatus* st) {
+                                                      int64_t lateness, DevStatus* st) {
     unsigned long long flags = 0, ins = 0;
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
         const int64_t* m = mig + i * (2 + kWideWords * kLaneSess);
@@ -277,7 +330,9 @@ __global__ void __launch_bounds__(256) k_sess_migrate(TableView t, TableView w, 
         const int cnt = (int)m[1];
         for (int x = 0; x < cnt * kWideWords; ++x) d[2 + x] = m[2 + x];
         d[1] = cnt;
+        due_of(w)[g2] = wide_due(d, lateness);
         sp[1] = (int64_t)kBigMeta;
+        due_of(t)[m[0]] = INT64_MAX;
     }
     flags = wave_ior(flags);
     ins = wave_sum(ins);
@@ -297,8 +352,11 @@ __global__ void __launch_bounds__(256) k_sess_wide(SegArgs a) {
          r0 += (int64_t)gridDim.x * blockDim.x) {
         const int64_t i = a.runs[r0];
         const uint32_t slot = a.slot[i];
-        int64_t j = i + 1;
-        while (j < a.n && a.slot[j] == slot) ++j;
+        int64_t j = i + 1, hi = a.n;  // sorted by slot: the run ends at the first other slot
+        while (j < hi) {
+            const int64_t mid = (j + hi) >> 1;
+            if (a.slot[mid] == slot) j = mid + 1; else hi = mid;
+        }
         int64_t* sp = slot_ptr(a.t, (int64_t)slot);
         const int64_t key = (int64_t)slot == a.t.cap ? kEmptyKey : sp[0];
         bool inserted;
@@ -321,6 +379,7 @@ __global__ void __launch_bounds__(256) k_sess_wide(SegArgs a) {
             }
             d[1] = c1;
             sp[1] = (int64_t)kBigMeta;
+            due_of(a.t)[slot] = INT64_MAX;
         }
         int cnt = (int)d[1];
         if (cnt + (j - i) > a.w.ring) {
@@ -332,6 +391,7 @@ __global__ void __launch_bounds__(256) k_sess_wide(SegArgs a) {
         const SessList l{d + 2, 1, kWideWords};
         for (int64_t r = i; r < j; ++r) add_element<AGG>(a, l, cnt, a.w.ring, key, a.perm[r], late, merges, flags);
         d[1] = cnt;
+        due_of(a.w)[g2] = wide_due(d, a.lateness);
     }
     ShardCtr& sc = a.st->sh[blockIdx.x % kShards];
     if (late) atomicAdd(&sc.late, late);
@@ -375,7 +435,7 @@ __global__ void __launch_bounds__(256) k_sess_fire(TableView t, int64_t wm, int6
         int64_t* s = nullptr;
         int cnt = 0, nf = 0, nc = 0;
         int64_t w1 = 0;
-        if (i < c1) {
+        if (i < c1 && due_of(t)[i] <= wm) {
             s = slot_ptr(t, i);
             w1 = s[1];
             cnt = slot_big(w1) ? 0 : slot_cnt(w1);  // wide keys: k_sess_fire_wide
@@ -419,6 +479,7 @@ __global__ void __launch_bounds__(256) k_sess_fire(TableView t, int64_t wm, int6
                 }
             }
             s[1] = (int64_t)((fired << 32) | (uint64_t)(uint32_t)(cnt - nc));
+            due_of(t)[i] = inline_due(s, SW, lateness);
         }
     }
     stage_flush(rs, &st->rows, o_key, o_start, o_end, o_res);
@@ -430,6 +491,7 @@ __global__ void __launch_bounds__(256) k_sess_fire_wide(TableView w, int64_t wm,
                                                         int64_t* o_key, int64_t* o_start, int64_t* o_end,
                                                         int64_t* o_res, DevStatus* st) {
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i <= w.cap; i += (int64_t)gridDim.x * blockDim.x) {
+        if (due_of(w)[i] > wm) continue;
         int64_t* s = slot_ptr(w, i);
         const int cnt = (int)s[1];
         if (cnt <= 0) continue;
@@ -454,6 +516,7 @@ __global__ void __launch_bounds__(256) k_sess_fire_wide(TableView w, int64_t wm,
                 for (int f = 0; f < kWideWords; ++f) s[2 + (q - nc) * kWideWords + f] = s[2 + q * kWideWords + f];
             s[1] = cnt - nc;
         }
+        due_of(w)[i] = wide_due(s, lateness);
     }
 }
 
@@ -475,6 +538,7 @@ __global__ void __launch_bounds__(256) k_sess_rehash(TableView o, TableView n, i
         d[1] = s[1];
         const int nw = words_per_slot < 0 ? (int)s[1] * o.words : words_per_slot;
         for (int w = 0; w < nw; ++w) d[2 + w] = s[2 + w];
+        due_of(n)[j] = due_of(o)[i];
     }
     ins = wave_sum(ins);
     flags = wave_ior(flags);
@@ -492,6 +556,7 @@ __global__ void __launch_bounds__(256) k_sess_init(TableView t) {
         int64_t* s = slot_ptr(t, i);
         s[0] = kEmptyKey;
         s[1] = 0;
+        due_of(t)[i] = INT64_MAX;
     }
 }
 
@@ -500,7 +565,7 @@ __global__ void __launch_bounds__(256) k_sess_init(TableView t) {
 // wide table (its main slot marked).  A key that already holds sessions here is counted in
 // st->overflow and left untouched (blobs of one key group are never restored twice).
 __global__ void __launch_bounds__(256) k_sess_restore(TableView t, TableView w, const int64_t* rk, const int64_t* roff,
-                                                      const int64_t* rs, int64_t n, DevStatus* st) {
+                                                      const int64_t* rs, int64_t n, int64_t lateness, DevStatus* st) {
     unsigned long long ins = 0, flags = 0, ins2 = 0;
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
         bool inserted;
@@ -521,6 +586,7 @@ __global__ void __launch_bounds__(256) k_sess_restore(TableView t, TableView w, 
                 fired |= (uint64_t)(x[4] != 0) << q;
             }
             sp[1] = (int64_t)((fired << 32) | (uint64_t)cnt);
+            due_of(t)[slot] = inline_due(sp, SW, lateness);
         } else {
             const int64_t g2 = find_or_insert(w, rk[i], inserted);
             if (g2 < 0) { flags |= GW_DF_TABLE_FULL; continue; }
@@ -529,7 +595,9 @@ __global__ void __launch_bounds__(256) k_sess_restore(TableView t, TableView w, 
             if (d[1] != 0) { atomicAdd(&st->overflow, 1ull); continue; }
             for (int64_t x = 0; x < cnt * kWideWords; ++x) d[2 + x] = rs[r0 * 5 + x];
             d[1] = cnt;
+            due_of(w)[g2] = wide_due(d, lateness);
             sp[1] = (int64_t)kBigMeta;
+            due_of(t)[slot] = INT64_MAX;
         }
     }
     block_commit(st, 0, ins, flags, 0);
@@ -571,14 +639,13 @@ static unsigned grid_of(int64_t n) {
 // first windows of a key: all its panes so far) and every slide ends a pane.  A slot
 // holds [key][element count][ring of n pane accumulators]; a batch is grouped by slot
 // with the stable radix sort (arrival order kept inside a key).  A key's run is folded in
-// order by one thread; a hot key's long run (WindowWordCount's frequent words) by a whole
-// workgroup: one thread per pane folds the pane's elements, then one thread per firing
+// order by one thread; a hot key's long run (WindowWordCount's frequent words) across the
+// GPU: one thread or wave per pane folds the pane's elements, then one thread per firing
 // folds the window's n panes.
 struct CountGeom {
     int64_t size, slide, g;
 };
-constexpr int kCntLongRun = 512;   // runs longer than this get a workgroup
-constexpr int kCntChunk = 256;     // panes per workgroup step
+constexpr int kCntLongRun = 256;   // longer runs are spread over panes and firings
 
 template <int AGG>
 __device__ __forceinline__ void cnt_emit(DevStatus* st, int64_t* ok, int64_t* os, int64_t* oe, int64_t* orr, int64_t key,
@@ -640,117 +707,138 @@ __global__ void __launch_bounds__(256) k_cnt_apply(TableView t, CountGeom G, con
     }
 }
 
-// A hot key's run: one workgroup.  Panes are folded kCntChunk at a time (one thread per
-// pane, its <= g elements in arrival order); each firing in the step folds its n panes,
-// from the step's LDS values, the previous step's last n-1 panes (LDS) or the key's ring
-// (panes before the run).  The ring keeps the key's last n panes.
-template <int AGG>
-__global__ void __launch_bounds__(256) k_cnt_long(TableView t, CountGeom G, const uint32_t* ks, const uint32_t* perm,
-                                                  int64_t n, const int64_t* val, int64_t* ok, int64_t* os,
-                                                  int64_t* oe, int64_t* orr, const uint32_t* longs, DevStatus* st) {
-    constexpr int W = (AGG == GW_AVG_I64 || AGG == GW_AVG_F64) ? 2 : 1;
-    const int R = t.ring;  // = n panes per window; the LDS tail keeps the R panes before the step
-    const int nt = R;
-    extern __shared__ int64_t lds[];  // [2][nt + kCntChunk] pane values + [2][nt] copy space
-    int64_t* v0 = lds;
-    int64_t* v1 = lds + nt + kCntChunk;
-    int64_t* t0 = lds + 2 * (nt + kCntChunk);
-    int64_t* t1 = t0 + nt;
-    const int64_t i = longs[blockIdx.x];
+// Hot keys' long runs: spread over the whole GPU in three launches.  A plan row per run
+// (arrival start i, length L, element count c0 before the batch, slot) and exclusive
+// prefix sums of its panes [c0/g, (c0+L-1)/g] and firings (counts c = f*slide in
+// (c0, c0+L]) give every pane and every firing a global index:
+//   k_cnt_panes  one thread (g < 16) or one wave per pane folds the pane's elements (the
+//                first pane starts from its ring cell when it began before the batch);
+//   k_cnt_fires  one thread per firing folds its n panes from the pane values or, for
+//                panes before the batch, the key's ring;
+//   k_cnt_ring   the run's last n panes go back to the ring, the count to the slot.
+enum { kPlanI, kPlanL, kPlanC0, kPlanSlot, kPlanWords = 4 };
+
+__global__ void __launch_bounds__(256) k_cnt_long_info(TableView t, const uint32_t* ks, int64_t n,
+                                                       const uint32_t* longs, int64_t nl, int64_t* plan) {
+    const int64_t l = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (l >= nl) return;
+    const int64_t i = longs[l];
     const uint32_t slot = ks[i];
-    __shared__ int64_t s_j;
-    if (threadIdx.x == 0) {
-        int64_t j = i + 1;
-        while (j < n && ks[j] == slot) ++j;
-        s_j = j;
+    int64_t lo = i + 1, hi = n;  // ks is sorted: the run ends at the first other slot
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (ks[mid] == slot) lo = mid + 1; else hi = mid;
     }
-    __syncthreads();
-    const int64_t L = s_j - i;
-    int64_t* sp = slot_ptr(t, (int64_t)slot);
-    int64_t* cells = sp + 2;
-    const int64_t key = sp[0];
-    const int64_t c0 = sp[1];
+    int64_t* p = plan + l * kPlanWords;
+    p[kPlanI] = i;
+    p[kPlanL] = lo - i;
+    p[kPlanC0] = slot_ptr(t, (int64_t)slot)[1];
+    p[kPlanSlot] = slot;
+}
+
+// largest l in [0, nl) with off[l] <= x
+__device__ __forceinline__ int64_t plan_find(const int64_t* off, int64_t nl, int64_t x) {
+    int64_t lo = 0, hi = nl - 1;
+    while (lo < hi) {
+        const int64_t mid = (lo + hi + 1) >> 1;
+        if (off[mid] <= x) lo = mid; else hi = mid - 1;
+    }
+    return lo;
+}
+
+template <int AGG, bool WAVE>
+__global__ void __launch_bounds__(256) k_cnt_panes(TableView t, CountGeom G, const uint32_t* perm, const int64_t* val,
+                                                   const int64_t* plan, const int64_t* poff, int64_t nl,
+                                                   int64_t np, int64_t* tmp) {
+    constexpr int W = (AGG == GW_AVG_I64 || AGG == GW_AVG_F64) ? 2 : 1;
+    const int64_t tid = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    const int64_t gp = WAVE ? tid / 64 : tid;
+    const int lane = WAVE ? (int)(threadIdx.x & 63) : 0;
+    if (gp >= np) return;  // WAVE: whole waves leave together
+    const int64_t l = plan_find(poff, nl, gp);
+    const int64_t* p = plan + l * kPlanWords;
+    const int64_t i = p[kPlanI], L = p[kPlanL], c0 = p[kPlanC0];
     const int64_t g = G.g;
-    const int64_t pf = c0 / g, pe = (c0 + L - 1) / g;  // panes the run touches
-    // pane q's value while panes [P0, P0 + kCntChunk) are the current step and the tail
-    // v[0, nt) holds panes [tail_end - nt, tail_end) (tail_end = P0 during a step)
-    auto pane_val = [&](int64_t q, int64_t P0, int64_t tail_end, int64_t& a, int64_t& b) {
-        if (q >= P0) {
-            a = v0[nt + (q - P0)]; b = v1[nt + (q - P0)];
-        } else if (q >= pf && q >= tail_end - nt) {
-            a = v0[q - (tail_end - nt)]; b = v1[q - (tail_end - nt)];
-        } else {
-            const int64_t* e = cells + (q % R) * W;
-            a = e[0]; b = W == 2 ? e[1] : 0;
+    const int64_t q = c0 / g + (gp - poff[l]);
+    const int64_t o_lo = max(q * g, c0), o_hi = min((q + 1) * g, c0 + L);
+    int64_t a0 = 0, a1 = 0;
+    bool has = false;
+    if (lane == 0 && o_lo > q * g) {  // the pane began before the batch: its ring cell
+        const int64_t* e = slot_ptr(t, p[kPlanSlot]) + 2 + (q % t.ring) * W;
+        a0 = e[0];
+        a1 = W == 2 ? e[1] : 0;
+        has = true;
+    }
+    for (int64_t o = o_lo + lane; o < o_hi; o += WAVE ? 64 : 1) {
+        int64_t b0, b1;
+        record_cell(AGG, val ? val[perm[i + (o - c0)]] : 0, b0, b1);
+        if (has) fold_cell(AGG, a0, a1, b0, b1); else { a0 = b0; a1 = b1; has = true; }
+    }
+    if (WAVE) {
+        for (int s = 1; s < 64; s <<= 1) {
+            const int64_t b0 = __shfl_xor(a0, s), b1 = __shfl_xor(a1, s);
+            const bool bh = __shfl_xor((int)has, s) != 0;
+            if (bh) {
+                if (has) fold_cell(AGG, a0, a1, b0, b1); else { a0 = b0; a1 = b1; has = true; }
+            }
         }
+    }
+    if (lane == 0) {
+        tmp[gp * W] = a0;
+        if (W == 2) tmp[gp * W + 1] = a1;
+    }
+}
+
+template <int AGG>
+__global__ void __launch_bounds__(256) k_cnt_fires(TableView t, CountGeom G, const int64_t* plan, const int64_t* poff,
+                                                   const int64_t* foff, int64_t nl, int64_t nf, const int64_t* tmp,
+                                                   int64_t* ok, int64_t* os, int64_t* oe, int64_t* orr, DevStatus* st) {
+    constexpr int W = (AGG == GW_AVG_I64 || AGG == GW_AVG_F64) ? 2 : 1;
+    const int64_t gf = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (gf >= nf) return;
+    const int64_t l = plan_find(foff, nl, gf);
+    const int64_t* p = plan + l * kPlanWords;
+    const int64_t c0 = p[kPlanC0], g = G.g;
+    const int64_t pf = c0 / g;
+    const int64_t* sp = slot_ptr(t, p[kPlanSlot]);
+    const int64_t* cells = sp + 2;
+    const int64_t* pv = tmp + poff[l] * W;
+    const int64_t c = (c0 / G.slide + 1 + (gf - foff[l])) * G.slide;
+    const int64_t len = c < G.size ? c : G.size;
+    const int64_t p0 = (c - len) / g, p1 = c / g;
+    auto pane = [&](int64_t q, int64_t& a, int64_t& b) {
+        const int64_t* e = q >= pf ? pv + (q - pf) * W : cells + (q % t.ring) * W;
+        a = e[0];
+        b = W == 2 ? e[1] : 0;
     };
-    for (int64_t P0 = pf; P0 <= pe; P0 += kCntChunk) {
-        const int64_t P = P0 + threadIdx.x;
-        if (threadIdx.x < kCntChunk && P <= pe) {
-            const int64_t o_lo = max(P * g, c0), o_hi = min((P + 1) * g, c0 + L);
-            int64_t a0, a1;
-            int64_t o = o_lo;
-            if (o_lo > P * g) {  // the pane began before the run: its ring cell
-                const int64_t* e = cells + (P % R) * W;
-                a0 = e[0];
-                a1 = W == 2 ? e[1] : 0;
-            } else {
-                record_cell(AGG, val ? val[perm[i + (o - c0)]] : 0, a0, a1);
-                ++o;
-            }
-            for (; o < o_hi; ++o) {
-                int64_t b0, b1;
-                record_cell(AGG, val ? val[perm[i + (o - c0)]] : 0, b0, b1);
-                fold_cell(AGG, a0, a1, b0, b1);
-            }
-            v0[nt + threadIdx.x] = a0;
-            v1[nt + threadIdx.x] = a1;
-        }
-        __syncthreads();
-        // firings in this step: count c = f * slide with c - 1 in the step's panes
-        const int64_t lo = max(c0 + 1, P0 * g + 1), hi = min(c0 + L, (P0 + kCntChunk) * g);
-        const int64_t f0 = (lo + G.slide - 1) / G.slide;
-        const int64_t f1 = hi / G.slide;
-        for (int64_t f = f0 + threadIdx.x; f <= f1; f += blockDim.x) {
-            const int64_t c = f * G.slide;
-            const int64_t len = c < G.size ? c : G.size;
-            const int64_t p0 = (c - len) / g, p1 = c / g;
-            int64_t r0, r1;
-            pane_val(p0, P0, P0, r0, r1);
-            for (int64_t q = p0 + 1; q < p1; ++q) {
-                int64_t b0, b1;
-                pane_val(q, P0, P0, b0, b1);
-                fold_cell(AGG, r0, r1, b0, b1);
-            }
-            cnt_emit<AGG>(st, ok, os, oe, orr, key, c, len, r0, r1);
-        }
-        // the R panes before the next step (after the last step: the run's last R panes)
-        const int64_t tail_end = min(P0 + kCntChunk, pe + 1);
-        for (int q = threadIdx.x; q < nt; q += blockDim.x) {
-            int64_t a = 0, b = 0;
-            pane_val(tail_end - nt + q, P0, P0, a, b);
-            t0[q] = a;
-            t1[q] = b;
-        }
-        __syncthreads();
-        for (int q = threadIdx.x; q < nt; q += blockDim.x) {
-            v0[q] = t0[q];
-            v1[q] = t1[q];
-        }
-        __syncthreads();
+    int64_t r0, r1;
+    pane(p0, r0, r1);
+    for (int64_t q = p0 + 1; q < p1; ++q) {
+        int64_t b0, b1;
+        pane(q, b0, b1);
+        fold_cell(AGG, r0, r1, b0, b1);
     }
-    // ring: the run's last R panes (older panes keep their cells)
-    for (int q = threadIdx.x; q < R; q += blockDim.x) {
-        const int64_t P = pe - q;
-        if (P < pf) continue;
-        int64_t a, b;
-        pane_val(P, pe + 1, pe + 1, a, b);
-        int64_t* e = cells + (P % R) * W;
-        e[0] = a;
-        if (W == 2) e[1] = b;
+    cnt_emit<AGG>(st, ok, os, oe, orr, sp[0], c, len, r0, r1);
+}
+
+__global__ void __launch_bounds__(256) k_cnt_ring(TableView t, CountGeom G, const int64_t* plan, const int64_t* poff,
+                                                  int64_t nl, const int64_t* tmp) {
+    const int R = t.ring, W = t.words;
+    const int64_t x = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (x >= nl * R) return;
+    const int64_t l = x / R;
+    const int q = (int)(x % R);
+    const int64_t* p = plan + l * kPlanWords;
+    const int64_t c0 = p[kPlanC0], L = p[kPlanL];
+    const int64_t pf = c0 / G.g, pe = (c0 + L - 1) / G.g;
+    int64_t* sp = slot_ptr(t, p[kPlanSlot]);
+    const int64_t P = pe - q;
+    if (P >= pf) {
+        const int64_t* v = tmp + (poff[l] + (P - pf)) * W;
+        int64_t* e = sp + 2 + (P % R) * W;
+        for (int w = 0; w < W; ++w) e[w] = v[w];
     }
-    __syncthreads();
-    if (threadIdx.x == 0) sp[1] = c0 + L;
+    if (q == 0) sp[1] = c0 + L;
 }
 
 // Restore of count-window state: one thread per entry (key, element count, ring of pane
@@ -791,6 +879,10 @@ struct SessionState {
     uint32_t* r0 = nullptr;  // punted / retried run heads
     uint32_t* r1 = nullptr;
     int64_t* mig = nullptr;  // migration lists (main pass -> wide table)
+    int64_t* cnt_plan = nullptr;  // count windows: long-run plan rows + pane / firing offsets
+    int64_t cnt_plan_cap = 0;
+    int64_t* cnt_tmp = nullptr;   // count windows: pane values of the long runs
+    int64_t cnt_tmp_cap = 0;
     void* sort_tmp = nullptr;
     size_t sort_tmp_bytes = 0;
     int64_t buf_cap = 0;
@@ -873,7 +965,7 @@ static int alloc_table(SessionState* s, TableView& t, int64_t cap, int ring, int
     t.ring = ring;
     t.words = words;
     t.stride_w = (int)(((2 + ring * words) + 7) / 8 * 8);
-    SCHECK(hipMalloc((void**)&t.base, (size_t)(cap + 1) * t.stride_w * 8));
+    SCHECK(hipMalloc((void**)&t.base, (size_t)(cap + 1) * (t.stride_w + 1) * 8));  // slots + due times
     hipLaunchKernelGGL(k_sess_init, dim3(grid_of(cap + 1)), dim3(256), 0, s->stream, t);
     SCHECK(hipGetLastError());
     return GW_OK;
@@ -921,6 +1013,7 @@ void session_destroy(SessionState* s) {
     hipHostFree(s->h_st);
     for (int q = 0; q < 2; ++q) { hipFree(s->slot[q]); hipFree(s->perm[q]); }
     hipFree(s->r0); hipFree(s->r1); hipFree(s->mig);
+    hipFree(s->cnt_plan); hipFree(s->cnt_tmp);
     hipFree(s->sort_tmp);
     hipFree(s->o_key); hipFree(s->o_start); hipFree(s->o_end); hipFree(s->o_res);
     for (auto* p : s->lo_buf) hipFree(p);
@@ -1100,14 +1193,57 @@ static int launch_count_apply(SessionState* s, const uint32_t* ks, const uint32_
     if ((rc = session_refresh(s, err))) return rc;
     const int64_t nl = (int64_t)s->h_st->overflow;
     if (!nl) return GW_OK;
-    const size_t lds = (size_t)2 * (2 * s->tv.ring + kCntChunk) * 8;
-#define L(A)                                                                                                  \
-    if (lds > 65536) SCHECK(hipFuncSetAttribute((const void*)k_cnt_long<A>,                                   \
-                                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));       \
-    hipLaunchKernelGGL(k_cnt_long<A>, dim3((unsigned)nl), dim3(kCntChunk), lds, s->stream, s->tv, s->cg, ks, perm, \
-                       n, v, s->o_key, s->o_start, s->o_end, s->o_res, s->r0, s->d_st)
+    // plan rows of the long runs -> host: pane and firing offsets -> the three launches
+    const int64_t pw = nl * kPlanWords + 2 * (nl + 1);
+    if (pw > s->cnt_plan_cap) {
+        hipFree(s->cnt_plan);
+        s->cnt_plan_cap = std::max<int64_t>(pw * 2, 4096);
+        SCHECK(hipMalloc((void**)&s->cnt_plan, s->cnt_plan_cap * 8));
+    }
+    hipLaunchKernelGGL(k_cnt_long_info, dim3(grid_of(nl)), dim3(256), 0, s->stream, s->tv, ks, n, s->r0, nl,
+                       s->cnt_plan);
+    SCHECK(hipGetLastError());
+    std::vector<int64_t> h((size_t)pw);
+    SCHECK(hipMemcpyAsync(h.data(), s->cnt_plan, nl * kPlanWords * 8, hipMemcpyDeviceToHost, s->stream));
+    SCHECK(hipStreamSynchronize(s->stream));
+    int64_t* poff = h.data() + nl * kPlanWords;
+    int64_t* foff = poff + nl + 1;
+    const CountGeom& G = s->cg;
+    poff[0] = foff[0] = 0;
+    for (int64_t l = 0; l < nl; ++l) {
+        const int64_t* p = h.data() + l * kPlanWords;
+        const int64_t c0 = p[kPlanC0], L = p[kPlanL];
+        poff[l + 1] = poff[l] + (c0 + L - 1) / G.g - c0 / G.g + 1;
+        foff[l + 1] = foff[l] + (c0 + L) / G.slide - c0 / G.slide;
+    }
+    const int64_t np = poff[nl], nf = foff[nl];
+    SCHECK(hipMemcpyAsync(s->cnt_plan + nl * kPlanWords, poff, 2 * (nl + 1) * 8, hipMemcpyHostToDevice, s->stream));
+    const int W = s->tv.words;
+    if (np * W > s->cnt_tmp_cap) {
+        SCHECK(hipStreamSynchronize(s->stream));
+        hipFree(s->cnt_tmp);
+        s->cnt_tmp_cap = std::max<int64_t>(np * W + np * W / 2, 1 << 16);
+        SCHECK(hipMalloc((void**)&s->cnt_tmp, s->cnt_tmp_cap * 8));
+    }
+    const int64_t* dpo = s->cnt_plan + nl * kPlanWords;
+    const int64_t* dfo = dpo + nl + 1;
+    const bool wave = G.g >= 16;
+    const unsigned pg = (unsigned)((np * (wave ? 64 : 1) + 255) / 256);
+#define L(A)                                                                                                   \
+    if (wave)                                                                                                  \
+        hipLaunchKernelGGL((k_cnt_panes<A, true>), dim3(pg), dim3(256), 0, s->stream, s->tv, G, perm, v, s->cnt_plan, \
+                           dpo, nl, np, s->cnt_tmp);                                                           \
+    else                                                                                                       \
+        hipLaunchKernelGGL((k_cnt_panes<A, false>), dim3(pg), dim3(256), 0, s->stream, s->tv, G, perm, v,      \
+                           s->cnt_plan, dpo, nl, np, s->cnt_tmp);                                              \
+    if (nf > 0)                                                                                                \
+        hipLaunchKernelGGL(k_cnt_fires<A>, dim3((unsigned)((nf + 255) / 256)), dim3(256), 0, s->stream, s->tv, G, \
+                           s->cnt_plan, dpo, dfo, nl, nf, s->cnt_tmp, s->o_key, s->o_start, s->o_end, s->o_res, \
+                           s->d_st)
     GW_AGG_SWITCH(s->cfg.agg, L);
 #undef L
+    hipLaunchKernelGGL(k_cnt_ring, dim3((unsigned)((nl * s->tv.ring + 255) / 256)), dim3(256), 0, s->stream, s->tv, G,
+                       s->cnt_plan, dpo, nl, s->cnt_tmp);
     SCHECK(hipGetLastError());
     return GW_OK;
 }
@@ -1182,7 +1318,7 @@ int session_ingest(SessionState* s, int64_t n, const int64_t* key, const int64_t
     if (n_mig) {  // finished lists of more than K1 sessions move to the wide table
         if ((rc = ensure_wide(s, n_mig, (int64_t)s->h_st->pad[1], err))) return rc;
         hipLaunchKernelGGL(k_sess_migrate, dim3(grid_of(n_mig)), dim3(256), 0, s->stream, s->tv, s->wv, s->mig, n_mig,
-                           s->d_st);
+                           s->cfg.allowed_lateness, s->d_st);
         SCHECK(hipGetLastError());
         if ((rc = session_refresh(s, err))) return rc;
         if (s->h_st->flags & GW_DF_TABLE_FULL) { err = "session wide table full"; return GW_E_OOM; }
@@ -1378,7 +1514,7 @@ int session_restore(SessionState* s, const int64_t* ent, int64_t n, std::string&
     SCHECK(hipMemcpy(d_s, rs.data(), n * 40, hipMemcpyHostToDevice));
     if ((rc = set_word(s, offsetof(DevStatus, overflow), 0, err))) return rc;
     hipLaunchKernelGGL(k_sess_restore, dim3(grid_of(nk)), dim3(256), 0, s->stream, s->tv, s->wv, d_k, d_o, d_s, nk,
-                       s->d_st);
+                       s->cfg.allowed_lateness, s->d_st);
     SCHECK(hipGetLastError());
     rc = session_refresh(s, err);
     hipFree(d_k);
