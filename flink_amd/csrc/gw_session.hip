@@ -33,7 +33,7 @@
 
 namespace gw {
 
-constexpr int kLaneSess = 4;        // sessions a thread replays in LDS
+constexpr int kLaneSess = 3;        // sessions a thread replays in LDS
 constexpr int kSegThreads = 128;
 constexpr int kWideWords = 5;       // wide-table session: start, end, a0, a1, fired
 constexpr uint64_t kBigMeta = 1ull << 31;  // main-table slot word 1: the key lives in the wide table
@@ -45,6 +45,7 @@ struct SegArgs {
     const int64_t* key;
     const int64_t* ts;
     const int64_t* val;
+    const int64_t* rec;     // (ts, value) per record in arrival order, 16-B aligned: one gather per record
     int64_t gap;
     int64_t wm;             // current watermark (all records of the batch see it)
     int64_t lateness;       // allowed lateness (WindowOperator.allowedLateness)
@@ -160,7 +161,9 @@ template <int AGG>
 __device__ __forceinline__ bool add_element(const SegArgs& a, const SessList& l, int& cnt, int cap, int64_t key,
                                             int64_t idx, unsigned long long& late, unsigned long long& merges,
                                             unsigned long long& flags, bool dry = false) {
-    const int64_t ts = a.ts[idx];
+    struct alignas(16) TsVal { int64_t ts, v; };
+    const TsVal tv = reinterpret_cast<const TsVal*>(a.rec)[idx];
+    const int64_t ts = tv.ts;
     int64_t we;
     if (__builtin_add_overflow(ts, a.gap, &we)) { flags |= GW_DF_RANGE; return true; }
     const int64_t ws = ts;
@@ -173,7 +176,7 @@ __device__ __forceinline__ bool add_element(const SegArgs& a, const SessList& l,
         }
     }
     int64_t c0, c1;
-    record_cell(AGG, a.val ? a.val[idx] : 0, c0, c1);
+    record_cell(AGG, tv.v, c0, c1);
     if (lo < 0) {
         if (cleaned_at(we, a.lateness, a.wm)) {  // isWindowLate: skipped; the element is late
             if (!a.lo_key) {
@@ -182,7 +185,7 @@ __device__ __forceinline__ bool add_element(const SegArgs& a, const SessList& l,
                 const unsigned long long o = atomicAdd(&a.st->n_late_out, 1ull);
                 a.lo_key[o] = key;
                 a.lo_ts[o] = ts;
-                a.lo_val[o] = a.val ? a.val[idx] : 0;
+                a.lo_val[o] = tv.v;
             }
             return true;
         }
@@ -230,75 +233,93 @@ __device__ __forceinline__ bool add_element(const SegArgs& a, const SessList& l,
 // Without allowed lateness and side output a replay has no effects beyond the slot, so
 // the dry replay is the real one.
 template <int AGG>
+__device__ __forceinline__ void seg_run(const SegArgs& a, const SessList& l, int64_t i, unsigned long long& late,
+                                        unsigned long long& merges, unsigned long long& flags) {
+    const uint32_t slot = a.slot[i];
+    int64_t j = i + 1;
+    while (j < a.n && a.slot[j] == slot) ++j;
+    int64_t* sp = slot_ptr(a.t, (int64_t)slot);
+    const int64_t w1 = sp[1];
+    const int SW = a.t.words;
+    const int64_t key = sp[0];  // the sentinel slot's key word is Long.MIN_VALUE, its key
+    bool ok = !slot_big(w1);
+    bool dry = ok && slot_cnt(w1) + (j - i) > kLaneSess;  // could outgrow the lane
+    const bool effects = a.lateness > 0 || a.lo_key;
+    const unsigned long long l0 = late, m0 = merges;
+    int cnt = 0;
+    while (ok) {  // at most two replays: dry, then (with effects) the real one
+        cnt = slot_cnt(w1);
+        for (int q = 0; q < cnt; ++q) {
+            const int64_t* x = sp + 2 + q * SW;
+            sl_put(l, q, Sess{x[0], x[1], x[2], SW == 4 ? x[3] : 0, (int64_t)slot_fired(w1, q)});
+        }
+        for (int64_t r = i; r < j && ok; ++r)
+            ok = add_element<AGG>(a, l, cnt, kLaneSess, key, a.perm[r], late, merges, flags, dry);
+        if (!ok || !dry || !effects) break;
+        dry = false;
+        late = l0;
+        merges = m0;
+    }
+    if (!ok) {
+        late = l0;
+        merges = m0;
+        const unsigned long long at = atomicAdd(&a.st->overflow, 1ull);
+        a.punt[at] = (uint32_t)i;
+        return;
+    }
+    if (cnt <= a.t.ring) {
+        uint64_t fired = 0;
+        int64_t due = INT64_MAX;
+        for (int q = 0; q < cnt; ++q) {
+            const Sess v = sl_get(l, q);
+            int64_t* x = sp + 2 + q * SW;
+            x[0] = v.s; x[1] = v.e; x[2] = v.a0;
+            if (SW == 4) x[3] = v.a1;
+            fired |= (uint64_t)(v.f != 0) << q;
+            due = min(due, due_time(v.e, v.f != 0, a.lateness));
+        }
+        sp[1] = (int64_t)((fired << 32) | (uint64_t)(uint32_t)cnt);
+        due_of(a.t)[slot] = due;
+    } else {  // more sessions than the slot holds: the finished list moves to the wide table
+        const unsigned long long at = atomicAdd(&a.st->pad[0], 1ull);
+        int64_t* m = a.mig + at * (2 + kWideWords * kLaneSess);
+        m[0] = (int64_t)slot;
+        m[1] = cnt;
+        for (int q = 0; q < cnt; ++q) {
+            const Sess v = sl_get(l, q);
+            int64_t* x = m + 2 + q * kWideWords;
+            x[0] = v.s; x[1] = v.e; x[2] = v.a0; x[3] = v.a1; x[4] = v.f;
+        }
+        atomicMax(&a.st->pad[1], (unsigned long long)cnt);
+    }
+}
+
+// Each wave takes kSegChunk consecutive records, compacts their run heads into LDS with
+// ballots, and replays the heads 64 at a time: every lane owns a run (about one record in
+// three starts a run), not one lane per record.
+constexpr int kSegChunk = 512;
+template <int AGG>
 __global__ void __launch_bounds__(kSegThreads) k_sess_segment(SegArgs a) {
     __shared__ int64_t lane[5 * kLaneSess * kSegThreads];
+    __shared__ uint32_t heads[kSegThreads / 64][kSegChunk];
     const SessList l{lane + threadIdx.x, kLaneSess * kSegThreads, kSegThreads};
     unsigned long long late = 0, merges = 0, flags = 0;
-    const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-    if (i < a.n && (i == 0 || a.slot[i - 1] != a.slot[i])) {
-        const uint32_t slot = a.slot[i];
-        int64_t j = i + 1;
-        while (j < a.n && a.slot[j] == slot) ++j;
-        int64_t* sp = slot_ptr(a.t, (int64_t)slot);
-        const int64_t w1 = sp[1];
-        const int SW = a.t.words;
-        const int64_t key = sp[0];  // the sentinel slot's key word is Long.MIN_VALUE, its key
-        auto load = [&](int& cnt) {
-            cnt = slot_cnt(w1);
-            for (int q = 0; q < cnt; ++q) {
-                const int64_t* x = sp + 2 + q * SW;
-                sl_put(l, q, Sess{x[0], x[1], x[2], SW == 4 ? x[3] : 0, (int64_t)slot_fired(w1, q)});
-            }
-        };
-        int cnt = 0;
-        bool ok = !slot_big(w1), done = false;
-        if (ok && slot_cnt(w1) + (j - i) > kLaneSess) {  // could outgrow the lane: dry replay
-            const unsigned long long l0 = late, m0 = merges;
-            load(cnt);
-            for (int64_t r = i; r < j && ok; ++r)
-                ok = add_element<AGG>(a, l, cnt, kLaneSess, key, a.perm[r], late, merges, flags, true);
-            done = ok && a.lateness == 0 && !a.lo_key;
-            if (!done) { late = l0; merges = m0; }
-        }
-        if (!ok) {
-            const unsigned long long at = atomicAdd(&a.st->overflow, 1ull);
-            a.punt[at] = (uint32_t)i;
-        } else {
-            if (!done) {
-                load(cnt);
-                for (int64_t r = i; r < j; ++r) add_element<AGG>(a, l, cnt, kLaneSess, key, a.perm[r], late, merges, flags);
-            }
-            if (cnt <= a.t.ring) {
-                uint64_t fired = 0;
-                int64_t due = INT64_MAX;
-                for (int q = 0; q < cnt; ++q) {
-                    const Sess v = sl_get(l, q);
-                    int64_t* x = sp + 2 + q * SW;
-                    x[0] = v.s; x[1] = v.e; x[2] = v.a0;
-                    if (SW == 4) x[3] = v.a1;
-                    fired |= (uint64_t)(v.f != 0) << q;
-                    due = min(due, due_time(v.e, v.f != 0, a.lateness));
-                }
-                sp[1] = (int64_t)((fired << 32) | (uint64_t)(uint32_t)cnt);
-                due_of(a.t)[slot] = due;
-            } else {  // more sessions than the slot holds: the finished list moves to the wide table
-                const unsigned long long at = atomicAdd(&a.st->pad[0], 1ull);
-                int64_t* m = a.mig + at * (2 + kWideWords * kLaneSess);
-                m[0] = (int64_t)slot;
-                m[1] = cnt;
-                for (int q = 0; q < cnt; ++q) {
-                    const Sess v = sl_get(l, q);
-                    int64_t* x = m + 2 + q * kWideWords;
-                    x[0] = v.s; x[1] = v.e; x[2] = v.a0; x[3] = v.a1; x[4] = v.f;
-                }
-                atomicMax(&a.st->pad[1], (unsigned long long)cnt);
-            }
-        }
+    const int w = threadIdx.x >> 6, ln = threadIdx.x & 63;
+    const int64_t base = (blockIdx.x * (int64_t)(kSegThreads / 64) + w) * kSegChunk;
+    int nh = 0;
+    for (int c = 0; c < kSegChunk; c += 64) {
+        const int64_t i = base + c + ln;
+        const bool h = i < a.n && (i == 0 || a.slot[i - 1] != a.slot[i]);
+        const uint64_t b = __ballot(h);
+        if (h) heads[w][nh + __popcll(b & ((1ull << ln) - 1ull))] = (uint32_t)(i - base);
+        nh += __popcll(b);
     }
+    __syncthreads();
+    for (int q = ln; q < nh; q += 64) seg_run<AGG>(a, l, base + heads[w][q], late, merges, flags);
     late = wave_sum(late);
     merges = wave_sum(merges);
     flags = wave_ior(flags);
-    if (__lane_id() == 0) {
+    if (ln == 0) {
         ShardCtr& sc = a.st->sh[blockIdx.x % kShards];
         if (late) atomicAdd(&sc.late, late);
         if (merges) atomicAdd(&sc.merges, merges);
@@ -400,9 +421,15 @@ __global__ void __launch_bounds__(256) k_sess_wide(SegArgs a) {
     if (ins) atomicAdd(&a.st->pad[2], ins);
 }
 
-__global__ void __launch_bounds__(256) k_sess_prep(const int64_t* key, const int64_t* ts, int64_t n, TableView t,
-                                                   uint32_t* slot, uint32_t* perm, DevStatus* st) {
+__global__ void __launch_bounds__(256) k_sess_prep(const int64_t* key, const int64_t* ts, const int64_t* val, int64_t n,
+                                                   TableView t, uint32_t* slot, uint32_t* perm, int64_t* rec,
+                                                   DevStatus* st) {
     unsigned long long ins = 0, flags = 0;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {  // the main pass's counters (nothing reads them before it)
+        st->overflow = 0;
+        st->pad[0] = 0;
+        st->pad[1] = 0;
+    }
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
         if (ts && ts[i] == INT64_MIN) flags |= GW_DF_NO_TS;
         bool inserted;
@@ -411,31 +438,88 @@ __global__ void __launch_bounds__(256) k_sess_prep(const int64_t* key, const int
         if (s < 0) { flags |= GW_DF_TABLE_FULL; s = 0; }
         slot[i] = (uint32_t)s;
         perm[i] = (uint32_t)i;
+        if (rec) {
+            rec[2 * i] = ts[i];
+            rec[2 * i + 1] = val ? val[i] : 0;
+        }
     }
     block_commit(st, 0, ins, flags, 0);
 }
 
-// Fire every in-flight session with end-1 <= wm (sessions in a slot are disjoint and
-// sorted, so the fired ones are a prefix), emit (key, start, end, result), drop the
-// cleaned prefix (WindowOperator.onEventTime :450-494 / clearAllState :560-571).
-// Rows are staged in LDS, one row per thread per round, and flushed in bulk.
+// Fire sweep, part 1: stream the due array (8 B per slot) and list the slots with
+// something due at `wm` -- a small fraction: the sessions that close at this watermark.
+// Each workgroup scans one contiguous chunk with 16-B loads (4 per lane in flight),
+// collects its hits in LDS and reserves list space with one atomic at the end.
+constexpr int kDueBuf = 4096;
+__global__ void __launch_bounds__(256) k_sess_due_scan(TableView t, int64_t wm, uint32_t* list, DevStatus* st) {
+    __shared__ uint32_t buf[kDueBuf];
+    __shared__ unsigned cnt;
+    __shared__ unsigned long long gbase;
+    const int64_t nslots = t.cap + 1;
+    const int64_t* due = due_of(t);
+    constexpr int kStep = 256 * 2 * 4;  // slots per workgroup iteration
+    const int64_t chunk = ((nslots + gridDim.x - 1) / gridDim.x + kStep - 1) / kStep * kStep;
+    const int64_t lo = blockIdx.x * chunk, hi = min(nslots, lo + chunk);
+    if (threadIdx.x == 0) cnt = 0;
+    __syncthreads();
+    auto hit = [&](int64_t i) {
+        const unsigned p = atomicAdd(&cnt, 1u);
+        if (p < kDueBuf) {
+            buf[p] = (uint32_t)i;
+        } else {  // a watermark that makes most slots due: straight to the list
+            list[atomicAdd(&st->n_refire, 1ull)] = (uint32_t)i;
+        }
+    };
+    for (int64_t b = lo; b < hi; b += kStep) {
+        int64_t d[8];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int64_t i = b + u * 512 + 2 * threadIdx.x;
+            if (i + 1 < hi) {
+                const longlong2 x = *reinterpret_cast<const longlong2*>(due + i);
+                d[2 * u] = x.x;
+                d[2 * u + 1] = x.y;
+            } else {
+                d[2 * u] = i < hi ? due[i] : INT64_MAX;
+                d[2 * u + 1] = INT64_MAX;
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int64_t i = b + u * 512 + 2 * threadIdx.x;
+            if (d[2 * u] <= wm && i < hi) hit(i);
+            if (d[2 * u + 1] <= wm && i + 1 < hi) hit(i + 1);
+        }
+    }
+    __syncthreads();
+    const unsigned c = min(cnt, (unsigned)kDueBuf);
+    if (threadIdx.x == 0 && c) gbase = atomicAdd(&st->n_refire, (unsigned long long)c);
+    __syncthreads();
+    for (unsigned j = threadIdx.x; j < c; j += blockDim.x) list[gbase + j] = buf[j];
+}
+
+// Part 2: one thread per listed slot fires its due sessions (a prefix: sorted, disjoint),
+// emits (key, start, end, result), drops the cleaned prefix (WindowOperator.onEventTime
+// :450-494 / clearAllState :560-571), and recomputes the slot's due time.  Rows are staged
+// in LDS, one row per thread per round, and flushed in bulk.
 template <int AGG>
-__global__ void __launch_bounds__(256) k_sess_fire(TableView t, int64_t wm, int64_t lateness, int purge, int64_t* o_key,
-                                                   int64_t* o_start, int64_t* o_end, int64_t* o_res, DevStatus* st) {
+__global__ void __launch_bounds__(256) k_sess_fire(TableView t, const uint32_t* list, int64_t wm, int64_t lateness,
+                                                   int purge, int64_t* o_key, int64_t* o_start, int64_t* o_end,
+                                                   int64_t* o_res, DevStatus* st) {
     __shared__ RowStage rs;
     __shared__ int s_max;
-    const int64_t nslots = t.cap + 1;
+    const int64_t nl = (int64_t)st->n_refire;
     const int SW = t.words;
     if (threadIdx.x == 0) rs.cnt = 0;
     __syncthreads();
-    const int64_t chunk = ((nslots + gridDim.x - 1) / gridDim.x + 255) / 256 * 256;
-    const int64_t c0 = blockIdx.x * chunk, c1 = min(nslots, c0 + chunk);
-    for (int64_t base = c0; base < c1; base += blockDim.x) {
-        const int64_t i = base + threadIdx.x;
+    for (int64_t base = blockIdx.x * (int64_t)blockDim.x; base < nl; base += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t x_i = base + threadIdx.x;
         int64_t* s = nullptr;
+        int64_t i = 0;
         int cnt = 0, nf = 0, nc = 0;
         int64_t w1 = 0;
-        if (i < c1 && due_of(t)[i] <= wm) {
+        if (x_i < nl) {
+            i = list[x_i];
             s = slot_ptr(t, i);
             w1 = s[1];
             cnt = slot_big(w1) ? 0 : slot_cnt(w1);  // wide keys: k_sess_fire_wide
@@ -645,7 +729,7 @@ static unsigned grid_of(int64_t n) {
 struct CountGeom {
     int64_t size, slide, g;
 };
-constexpr int kCntLongRun = 256;   // longer runs are spread over panes and firings
+constexpr int kCntLongRun = 16;    // longer runs are spread over panes and firings
 
 template <int AGG>
 __device__ __forceinline__ void cnt_emit(DevStatus* st, int64_t* ok, int64_t* os, int64_t* oe, int64_t* orr, int64_t key,
@@ -718,8 +802,9 @@ __global__ void __launch_bounds__(256) k_cnt_apply(TableView t, CountGeom G, con
 //   k_cnt_ring   the run's last n panes go back to the ring, the count to the slot.
 enum { kPlanI, kPlanL, kPlanC0, kPlanSlot, kPlanWords = 4 };
 
-__global__ void __launch_bounds__(256) k_cnt_long_info(TableView t, const uint32_t* ks, int64_t n,
-                                                       const uint32_t* longs, int64_t nl, int64_t* plan) {
+__global__ void __launch_bounds__(256) k_cnt_long_info(TableView t, CountGeom G, const uint32_t* ks, int64_t n,
+                                                       const uint32_t* longs, int64_t nl, int64_t* plan,
+                                                       int64_t* poff, int64_t* foff) {
     const int64_t l = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
     if (l >= nl) return;
     const int64_t i = longs[l];
@@ -732,8 +817,38 @@ __global__ void __launch_bounds__(256) k_cnt_long_info(TableView t, const uint32
     int64_t* p = plan + l * kPlanWords;
     p[kPlanI] = i;
     p[kPlanL] = lo - i;
-    p[kPlanC0] = slot_ptr(t, (int64_t)slot)[1];
+    const int64_t c0 = slot_ptr(t, (int64_t)slot)[1], L = lo - i;
+    p[kPlanC0] = c0;
     p[kPlanSlot] = slot;
+    poff[l] = (c0 + L - 1) / G.g - c0 / G.g + 1;  // panes and firings of the run (scanned next)
+    foff[l] = (c0 + L) / G.slide - c0 / G.slide;
+}
+
+// Exclusive prefix sums of the runs' pane and firing counts, in place (one workgroup;
+// off[nl] = the total).
+__global__ void __launch_bounds__(1024) k_cnt_plan_scan(int64_t* poff, int64_t* foff, int64_t nl) {
+    __shared__ int64_t sp[1024], sf[1024];
+    const int64_t per = (nl + 1023) / 1024;
+    const int64_t b = threadIdx.x * per, e = min(nl, b + per);
+    int64_t tp = 0, tf = 0;
+    for (int64_t x = b; x < e; ++x) { tp += poff[x]; tf += foff[x]; }
+    sp[threadIdx.x] = tp;
+    sf[threadIdx.x] = tf;
+    __syncthreads();
+    for (int o = 1; o < 1024; o <<= 1) {  // Hillis-Steele inclusive scan
+        const int64_t ap = threadIdx.x >= o ? sp[threadIdx.x - o] : 0, af = threadIdx.x >= o ? sf[threadIdx.x - o] : 0;
+        __syncthreads();
+        sp[threadIdx.x] += ap;
+        sf[threadIdx.x] += af;
+        __syncthreads();
+    }
+    int64_t rp = sp[threadIdx.x] - tp, rf = sf[threadIdx.x] - tf;
+    for (int64_t x = b; x < e; ++x) {
+        const int64_t cp = poff[x], cf = foff[x];
+        poff[x] = rp; foff[x] = rf;
+        rp += cp; rf += cf;
+    }
+    if (threadIdx.x == 1023) { poff[nl] = sp[1023]; foff[nl] = sf[1023]; }
 }
 
 // largest l in [0, nl) with off[l] <= x
@@ -749,12 +864,12 @@ __device__ __forceinline__ int64_t plan_find(const int64_t* off, int64_t nl, int
 template <int AGG, bool WAVE>
 __global__ void __launch_bounds__(256) k_cnt_panes(TableView t, CountGeom G, const uint32_t* perm, const int64_t* val,
                                                    const int64_t* plan, const int64_t* poff, int64_t nl,
-                                                   int64_t np, int64_t* tmp) {
+                                                   int64_t* tmp) {
     constexpr int W = (AGG == GW_AVG_I64 || AGG == GW_AVG_F64) ? 2 : 1;
     const int64_t tid = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
     const int64_t gp = WAVE ? tid / 64 : tid;
     const int lane = WAVE ? (int)(threadIdx.x & 63) : 0;
-    if (gp >= np) return;  // WAVE: whole waves leave together
+    if (gp >= poff[nl]) return;  // the grid is an upper bound; WAVE: whole waves leave together
     const int64_t l = plan_find(poff, nl, gp);
     const int64_t* p = plan + l * kPlanWords;
     const int64_t i = p[kPlanI], L = p[kPlanL], c0 = p[kPlanC0];
@@ -791,11 +906,11 @@ __global__ void __launch_bounds__(256) k_cnt_panes(TableView t, CountGeom G, con
 
 template <int AGG>
 __global__ void __launch_bounds__(256) k_cnt_fires(TableView t, CountGeom G, const int64_t* plan, const int64_t* poff,
-                                                   const int64_t* foff, int64_t nl, int64_t nf, const int64_t* tmp,
+                                                   const int64_t* foff, int64_t nl, const int64_t* tmp,
                                                    int64_t* ok, int64_t* os, int64_t* oe, int64_t* orr, DevStatus* st) {
     constexpr int W = (AGG == GW_AVG_I64 || AGG == GW_AVG_F64) ? 2 : 1;
     const int64_t gf = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-    if (gf >= nf) return;
+    if (gf >= foff[nl]) return;  // the grid is an upper bound
     const int64_t l = plan_find(foff, nl, gf);
     const int64_t* p = plan + l * kPlanWords;
     const int64_t c0 = p[kPlanC0], g = G.g;
@@ -879,6 +994,10 @@ struct SessionState {
     uint32_t* r0 = nullptr;  // punted / retried run heads
     uint32_t* r1 = nullptr;
     int64_t* mig = nullptr;  // migration lists (main pass -> wide table)
+    int64_t* rec = nullptr;  // sessions: (ts, value) per record
+    bool fresh = false;      // h_st matches the device (nothing launched since the last refresh)
+    uint32_t* due_list = nullptr;  // fire sweep: main-table slots with something due
+    int64_t due_list_cap = 0;
     int64_t* cnt_plan = nullptr;  // count windows: long-run plan rows + pane / firing offsets
     int64_t cnt_plan_cap = 0;
     int64_t* cnt_tmp = nullptr;   // count windows: pane values of the long runs
@@ -937,6 +1056,7 @@ int session_refresh(SessionState* s, std::string& err) {
     SCHECK(hipMemcpyAsync(s->h_st, s->d_st, sizeof(DevStatus), hipMemcpyDeviceToHost, s->stream));
     SCHECK(hipStreamSynchronize(s->stream));
     fold_shards(s->h_st);
+    s->fresh = false;
     if (s->timing) resolve_timers(s);
     if (s->h_st->flags & GW_DF_NO_TS) {
         err = "Record has Long.MIN_VALUE timestamp (= no timestamp marker). Did you forget to call "
@@ -947,6 +1067,22 @@ int session_refresh(SessionState* s, std::string& err) {
         err = "session window end overflows int64";
         return GW_E_RANGE;
     }
+    s->fresh = true;
+    return GW_OK;
+}
+
+// Entry of a call that launches work: the host view is refreshed unless nothing ran on the
+// device since the last refresh (the ingest and fire calls end with one).
+static int begin_launch(SessionState* s, std::string& err) {
+    int rc = s->fresh ? GW_OK : session_refresh(s, err);
+    s->fresh = false;
+    return rc;
+}
+
+// Zero a device status word without a host round trip (host view updated alike).
+static int zero_word_async(SessionState* s, size_t off, std::string& err) {
+    *reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(s->h_st) + off) = 0;
+    SCHECK(hipMemsetAsync(reinterpret_cast<char*>(s->d_st) + off, 0, 8, s->stream));
     return GW_OK;
 }
 
@@ -995,10 +1131,10 @@ int session_create(SessionState*& out, const gw_config& cfg, int64_t cap, hipStr
         out = s;
         return GW_OK;
     }
-    // K1 so that the slot fills a 64-byte (sum/count/min/max) or 128-byte (avg) line
+    // K1 so that the slot is one 64-byte line: 2 sessions (sum/count/min/max), 1 (avg)
     const int words = cell_words(cfg.agg) == 2 ? 4 : 3;
-    rc = alloc_table(s, s->tv, cap, words == 3 ? 2 : 3, words, why);
-    if (rc == GW_OK) rc = alloc_table(s, s->wv, 1024, 16, kWideWords, why);
+    rc = alloc_table(s, s->tv, cap, words == 3 ? 2 : 1, words, why);
+    if (rc == GW_OK) rc = alloc_table(s, s->wv, 1024, 4, kWideWords, why);
     if (rc) { session_destroy(s); return rc; }
     out = s;
     return GW_OK;
@@ -1012,8 +1148,8 @@ void session_destroy(SessionState* s) {
     hipFree(s->d_st);
     hipHostFree(s->h_st);
     for (int q = 0; q < 2; ++q) { hipFree(s->slot[q]); hipFree(s->perm[q]); }
-    hipFree(s->r0); hipFree(s->r1); hipFree(s->mig);
-    hipFree(s->cnt_plan); hipFree(s->cnt_tmp);
+    hipFree(s->r0); hipFree(s->r1); hipFree(s->mig); hipFree(s->rec);
+    hipFree(s->cnt_plan); hipFree(s->cnt_tmp); hipFree(s->due_list);
     hipFree(s->sort_tmp);
     hipFree(s->o_key); hipFree(s->o_start); hipFree(s->o_end); hipFree(s->o_res);
     for (auto* p : s->lo_buf) hipFree(p);
@@ -1027,8 +1163,9 @@ static int ensure_bufs(SessionState* s, int64_t n, std::string& err) {
     const int64_t c = std::max<int64_t>(n + n / 4, 1 << 16);
     SCHECK(hipStreamSynchronize(s->stream));
     for (int q = 0; q < 2; ++q) { hipFree(s->slot[q]); hipFree(s->perm[q]); }
-    hipFree(s->r0); hipFree(s->r1); hipFree(s->mig); hipFree(s->sort_tmp);
+    hipFree(s->r0); hipFree(s->r1); hipFree(s->mig); hipFree(s->sort_tmp); hipFree(s->rec);
     s->mig = nullptr;
+    s->rec = nullptr;
     for (int q = 0; q < 2; ++q) {
         SCHECK(hipMalloc((void**)&s->slot[q], c * 4));
         SCHECK(hipMalloc((void**)&s->perm[q], c * 4));
@@ -1036,6 +1173,7 @@ static int ensure_bufs(SessionState* s, int64_t n, std::string& err) {
     SCHECK(hipMalloc((void**)&s->r0, c * 4));
     SCHECK(hipMalloc((void**)&s->r1, c * 4));
     if (!s->count_mode) SCHECK(hipMalloc((void**)&s->mig, (size_t)c * (2 + kWideWords * kLaneSess) * 8));
+    if (!s->count_mode) SCHECK(hipMalloc((void**)&s->rec, (size_t)c * 16));
     rocprim::double_buffer<uint32_t> kb(s->slot[0], s->slot[1]), vb(s->perm[0], s->perm[1]);
     size_t bytes = 0;
     SCHECK(rocprim::radix_sort_pairs(nullptr, bytes, kb, vb, (size_t)c, 0, 32, s->stream));
@@ -1155,8 +1293,8 @@ int session_drain_late(SessionState* s, int64_t* key, int64_t* ts, int64_t* val,
 
 // Slot per record and the stable grouping by slot (both modes).  Grows the main table to
 // keep its load below 0.7 for `n` possible new keys.
-static int group_records(SessionState* s, int64_t n, const int64_t* key, const int64_t* ts, const uint32_t** sk,
-                         const uint32_t** sp, std::string& err) {
+static int group_records(SessionState* s, int64_t n, const int64_t* key, const int64_t* ts, const int64_t* val,
+                         const uint32_t** sk, const uint32_t** sp, std::string& err) {
     int rc;
     if ((double)(s->h_st->used_slots + n) > 0.7 * (double)s->tv.cap &&
         ((double)s->h_st->used_slots > 0.7 * (double)s->tv.cap ||
@@ -1167,8 +1305,8 @@ static int group_records(SessionState* s, int64_t n, const int64_t* key, const i
     }
     if ((rc = ensure_bufs(s, n, err))) return rc;
     for (int attempt = 0;; ++attempt) {
-        hipLaunchKernelGGL(k_sess_prep, dim3(grid_of(n)), dim3(256), 0, s->stream, key, ts, n, s->tv, s->slot[0],
-                           s->perm[0], s->d_st);
+        hipLaunchKernelGGL(k_sess_prep, dim3(grid_of(n)), dim3(256), 0, s->stream, key, ts, val, n, s->tv, s->slot[0],
+                           s->perm[0], s->count_mode ? nullptr : s->rec, s->d_st);
         if ((rc = session_refresh(s, err))) return rc;
         if (!(s->h_st->flags & GW_DF_TABLE_FULL)) break;
         if (attempt > 4) { err = "session state table full"; return GW_E_OOM; }
@@ -1182,7 +1320,7 @@ static int group_records(SessionState* s, int64_t n, const int64_t* key, const i
 static int launch_count_apply(SessionState* s, const uint32_t* ks, const uint32_t* perm, int64_t n, const int64_t* val,
                               std::string& err) {
     int rc;
-    if ((rc = set_word(s, offsetof(DevStatus, overflow), 0, err))) return rc;
+    if ((rc = zero_word_async(s, offsetof(DevStatus, overflow), err))) return rc;
     const int64_t* v = s->cfg.agg == GW_COUNT ? nullptr : val;
 #define L(A)                                                                                               \
     hipLaunchKernelGGL(k_cnt_apply<A>, dim3(grid_of(n)), dim3(256), 0, s->stream, s->tv, s->cg, ks, perm, n, v, \
@@ -1193,53 +1331,41 @@ static int launch_count_apply(SessionState* s, const uint32_t* ks, const uint32_
     if ((rc = session_refresh(s, err))) return rc;
     const int64_t nl = (int64_t)s->h_st->overflow;
     if (!nl) return GW_OK;
-    // plan rows of the long runs -> host: pane and firing offsets -> the three launches
+    // plan rows of the long runs, their pane / firing offsets (device scan), then the three
+    // launches over upper bounds of the pane and firing counts (no host round trip)
     const int64_t pw = nl * kPlanWords + 2 * (nl + 1);
     if (pw > s->cnt_plan_cap) {
+        SCHECK(hipStreamSynchronize(s->stream));
         hipFree(s->cnt_plan);
         s->cnt_plan_cap = std::max<int64_t>(pw * 2, 4096);
         SCHECK(hipMalloc((void**)&s->cnt_plan, s->cnt_plan_cap * 8));
     }
-    hipLaunchKernelGGL(k_cnt_long_info, dim3(grid_of(nl)), dim3(256), 0, s->stream, s->tv, ks, n, s->r0, nl,
-                       s->cnt_plan);
-    SCHECK(hipGetLastError());
-    std::vector<int64_t> h((size_t)pw);
-    SCHECK(hipMemcpyAsync(h.data(), s->cnt_plan, nl * kPlanWords * 8, hipMemcpyDeviceToHost, s->stream));
-    SCHECK(hipStreamSynchronize(s->stream));
-    int64_t* poff = h.data() + nl * kPlanWords;
-    int64_t* foff = poff + nl + 1;
     const CountGeom& G = s->cg;
-    poff[0] = foff[0] = 0;
-    for (int64_t l = 0; l < nl; ++l) {
-        const int64_t* p = h.data() + l * kPlanWords;
-        const int64_t c0 = p[kPlanC0], L = p[kPlanL];
-        poff[l + 1] = poff[l] + (c0 + L - 1) / G.g - c0 / G.g + 1;
-        foff[l + 1] = foff[l] + (c0 + L) / G.slide - c0 / G.slide;
-    }
-    const int64_t np = poff[nl], nf = foff[nl];
-    SCHECK(hipMemcpyAsync(s->cnt_plan + nl * kPlanWords, poff, 2 * (nl + 1) * 8, hipMemcpyHostToDevice, s->stream));
+    int64_t* dpo = s->cnt_plan + nl * kPlanWords;
+    int64_t* dfo = dpo + nl + 1;
+    hipLaunchKernelGGL(k_cnt_long_info, dim3(grid_of(nl)), dim3(256), 0, s->stream, s->tv, G, ks, n, s->r0, nl,
+                       s->cnt_plan, dpo, dfo);
+    hipLaunchKernelGGL(k_cnt_plan_scan, dim3(1), dim3(1024), 0, s->stream, dpo, dfo, nl);
+    const int64_t np_max = n / G.g + 2 * nl, nf_max = n / G.slide + nl;
     const int W = s->tv.words;
-    if (np * W > s->cnt_tmp_cap) {
+    if (np_max * W > s->cnt_tmp_cap) {
         SCHECK(hipStreamSynchronize(s->stream));
         hipFree(s->cnt_tmp);
-        s->cnt_tmp_cap = std::max<int64_t>(np * W + np * W / 2, 1 << 16);
+        s->cnt_tmp_cap = std::max<int64_t>(np_max * W + np_max * W / 2, 1 << 16);
         SCHECK(hipMalloc((void**)&s->cnt_tmp, s->cnt_tmp_cap * 8));
     }
-    const int64_t* dpo = s->cnt_plan + nl * kPlanWords;
-    const int64_t* dfo = dpo + nl + 1;
     const bool wave = G.g >= 16;
-    const unsigned pg = (unsigned)((np * (wave ? 64 : 1) + 255) / 256);
+    const unsigned pg = (unsigned)((np_max * (wave ? 64 : 1) + 255) / 256);
 #define L(A)                                                                                                   \
     if (wave)                                                                                                  \
         hipLaunchKernelGGL((k_cnt_panes<A, true>), dim3(pg), dim3(256), 0, s->stream, s->tv, G, perm, v, s->cnt_plan, \
-                           dpo, nl, np, s->cnt_tmp);                                                           \
+                           dpo, nl, s->cnt_tmp);                                                               \
     else                                                                                                       \
         hipLaunchKernelGGL((k_cnt_panes<A, false>), dim3(pg), dim3(256), 0, s->stream, s->tv, G, perm, v,      \
-                           s->cnt_plan, dpo, nl, np, s->cnt_tmp);                                              \
-    if (nf > 0)                                                                                                \
-        hipLaunchKernelGGL(k_cnt_fires<A>, dim3((unsigned)((nf + 255) / 256)), dim3(256), 0, s->stream, s->tv, G, \
-                           s->cnt_plan, dpo, dfo, nl, nf, s->cnt_tmp, s->o_key, s->o_start, s->o_end, s->o_res, \
-                           s->d_st)
+                           s->cnt_plan, dpo, nl, s->cnt_tmp);                                                  \
+    if (nf_max > 0)                                                                                            \
+        hipLaunchKernelGGL(k_cnt_fires<A>, dim3((unsigned)((nf_max + 255) / 256)), dim3(256), 0, s->stream, s->tv, G, \
+                           s->cnt_plan, dpo, dfo, nl, s->cnt_tmp, s->o_key, s->o_start, s->o_end, s->o_res, s->d_st)
     GW_AGG_SWITCH(s->cfg.agg, L);
 #undef L
     hipLaunchKernelGGL(k_cnt_ring, dim3((unsigned)((nl * s->tv.ring + 255) / 256)), dim3(256), 0, s->stream, s->tv, G,
@@ -1251,7 +1377,7 @@ static int launch_count_apply(SessionState* s, const uint32_t* ks, const uint32_
 // Count windows: slot per record, stable grouping by slot, one in-order fold per key.
 static int count_ingest(SessionState* s, int64_t n, const int64_t* key, const int64_t* val, std::string& err) {
     int rc;
-    if ((rc = session_refresh(s, err))) return rc;
+    if ((rc = begin_launch(s, err))) return rc;
     if (n <= 0) return GW_OK;
     if ((int64_t)n > (int64_t)0x7fffffffLL) { err = "batch too large"; return GW_E_INVALID; }
     // every element fires at most one window
@@ -1260,7 +1386,7 @@ static int count_ingest(SessionState* s, int64_t n, const int64_t* key, const in
     if (s->timing) SCHECK(hipEventRecord(ev.first, s->stream));
     const uint32_t* ks;
     const uint32_t* perm;
-    if ((rc = group_records(s, n, key, nullptr, &ks, &perm, err))) return rc;
+    if ((rc = group_records(s, n, key, nullptr, nullptr, &ks, &perm, err))) return rc;
     if ((rc = launch_count_apply(s, ks, perm, n, val, err))) return rc;
     if (s->timing) {
         SCHECK(hipEventRecord(ev.second, s->stream));
@@ -1275,13 +1401,14 @@ int session_ingest(SessionState* s, int64_t n, const int64_t* key, const int64_t
                    std::string& err) {
     if (s->count_mode) return count_ingest(s, n, key, val, err);
     int rc;
-    if ((rc = session_refresh(s, err))) return rc;
+    if ((rc = begin_launch(s, err))) return rc;
     if (n <= 0) return GW_OK;
     if ((int64_t)n > (int64_t)0x7fffffffLL) { err = "batch too large"; return GW_E_INVALID; }
     auto ev = s->timing ? get_ev(s) : std::pair<hipEvent_t, hipEvent_t>{};
     if (s->timing) SCHECK(hipEventRecord(ev.first, s->stream));
     SegArgs a{};
-    if ((rc = group_records(s, n, key, ts, &a.slot, &a.perm, err))) return rc;
+    if ((rc = group_records(s, n, key, ts, val, &a.slot, &a.perm, err))) return rc;
+    a.rec = s->rec;
     a.n = n;
     a.key = key;
     a.ts = ts;
@@ -1300,14 +1427,14 @@ int session_ingest(SessionState* s, int64_t n, const int64_t* key, const int64_t
         a.lo_key = s->lo_buf[0]; a.lo_ts = s->lo_buf[1]; a.lo_val = s->lo_buf[2];
     }
     // main pass
-    if ((rc = set_word(s, offsetof(DevStatus, overflow), 0, err))) return rc;
-    if ((rc = set_word(s, offsetof(DevStatus, pad[0]), 0, err))) return rc;
-    if ((rc = set_word(s, offsetof(DevStatus, pad[1]), 0, err))) return rc;
+    // st->overflow, pad[0], pad[1] were zeroed by k_sess_prep
+    s->h_st->overflow = s->h_st->pad[0] = s->h_st->pad[1] = 0;
     a.t = s->tv;
     a.w = s->wv;
     a.punt = s->r0;
     a.mig = s->mig;
-    const unsigned gs = (unsigned)((n + kSegThreads - 1) / kSegThreads);
+    const int64_t per_block = (int64_t)kSegChunk * (kSegThreads / 64);
+    const unsigned gs = (unsigned)((n + per_block - 1) / per_block);
 #define L(A) hipLaunchKernelGGL(k_sess_segment<A>, dim3(gs), dim3(kSegThreads), 0, s->stream, a)
     GW_AGG_SWITCH(s->cfg.agg, L);
 #undef L
@@ -1329,8 +1456,8 @@ int session_ingest(SessionState* s, int64_t n, const int64_t* key, const int64_t
     for (int pass = 0; n_punt > 0; ++pass) {
         if (pass > 40) { err = "session wide table did not converge"; return GW_E_DEVICE; }
         if ((rc = ensure_wide(s, n_punt, 0, err))) return rc;
-        if ((rc = set_word(s, offsetof(DevStatus, overflow), 0, err))) return rc;
-        if ((rc = set_word(s, offsetof(DevStatus, pad[1]), 0, err))) return rc;
+        if ((rc = zero_word_async(s, offsetof(DevStatus, overflow), err))) return rc;
+        if ((rc = zero_word_async(s, offsetof(DevStatus, pad[1]), err))) return rc;
         a.t = s->tv;
         a.w = s->wv;
         a.runs = rin;
@@ -1362,7 +1489,7 @@ int session_fire(SessionState* s, int64_t wm, int64_t* fired, std::string& err) 
         return GW_OK;
     }
     int rc;
-    if ((rc = session_refresh(s, err))) return rc;
+    if ((rc = begin_launch(s, err))) return rc;
     const int64_t before = (int64_t)s->h_st->rows;
     const int64_t need = before + (int64_t)(s->h_st->used_slots + 1) * s->tv.ring +
                          (int64_t)(s->h_st->pad[2] + 1) * s->wv.ring;
@@ -1370,10 +1497,19 @@ int session_fire(SessionState* s, int64_t wm, int64_t* fired, std::string& err) 
     auto ev = s->timing ? get_ev(s) : std::pair<hipEvent_t, hipEvent_t>{};
     if (s->timing) SCHECK(hipEventRecord(ev.first, s->stream));
     const unsigned fg = (unsigned)std::min<int64_t>(1024, std::max<int64_t>(1, (s->tv.cap + 1 + 255) / 256));
+    if (s->due_list_cap < s->tv.cap + 1) {
+        hipFree(s->due_list);
+        s->due_list = nullptr;
+        SCHECK(hipMalloc((void**)&s->due_list, (size_t)(s->tv.cap + 1) * 4));
+        s->due_list_cap = s->tv.cap + 1;
+    }
+    if ((rc = zero_word_async(s, offsetof(DevStatus, n_refire), err))) return rc;  // due-list cursor
+    const unsigned sg = (unsigned)std::min<int64_t>(2048, std::max<int64_t>(1, (s->tv.cap + 1) / 2048));
+    hipLaunchKernelGGL(k_sess_due_scan, dim3(sg), dim3(256), 0, s->stream, s->tv, wm, s->due_list, s->d_st);
     const int purge = (int)(s->cfg.allowed_lateness > 0 && s->cfg.trigger == GW_PURGING_EVENT_TIME_TRIGGER);
 #define L(A)                                                                                               \
-    hipLaunchKernelGGL(k_sess_fire<A>, dim3(fg), dim3(256), 0, s->stream, s->tv, wm, s->cfg.allowed_lateness, \
-                       purge, s->o_key, s->o_start, s->o_end, s->o_res, s->d_st);                          \
+    hipLaunchKernelGGL(k_sess_fire<A>, dim3(fg), dim3(256), 0, s->stream, s->tv, s->due_list, wm,            \
+                       s->cfg.allowed_lateness, purge, s->o_key, s->o_start, s->o_end, s->o_res, s->d_st); \
     if (s->h_st->pad[2])                                                                                    \
     hipLaunchKernelGGL(k_sess_fire_wide<A>, dim3(grid_of(s->wv.cap + 1)), dim3(256), 0, s->stream, s->wv, wm, \
                        s->cfg.allowed_lateness, purge, s->o_key, s->o_start, s->o_end, s->o_res, s->d_st)
