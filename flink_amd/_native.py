@@ -43,7 +43,10 @@ EXPORTS = [
     "gw_key_group_for_hash", "gw_operator_for_key_group", "gw_default_max_parallelism",
     "gw_key_groups_device", "gw_partition_scratch_bytes", "gw_partition_device",
     "gw_decode_serialized", "gw_ingest_serialized", "gw_ingest_serialized_device",
+    "gw_exchange_unique_id", "gw_exchange_create", "gw_exchange_destroy", "gw_exchange_batch",
+    "gw_exchange_min_watermark", "gw_exchange_last_error",
 ]
+EXCHANGE_ID_BYTES = 128
 
 
 class GwRecordLayout(ctypes.Structure):
@@ -160,6 +163,13 @@ def lib() -> ctypes.CDLL:
                                          ctypes.POINTER(GwDecodeResult), p]),
         "gw_ingest_serialized": (c_int, [p, p, i64, ctypes.POINTER(GwRecordLayout), P64, P64]),
         "gw_ingest_serialized_device": (c_int, [p, p, i64, ctypes.POINTER(GwRecordLayout), p, P64, P64]),
+        "gw_exchange_unique_id": (c_int, [p]),
+        "gw_exchange_create": (c_int, [ctypes.POINTER(p), i32, i32, p, i32, i32]),
+        "gw_exchange_destroy": (None, [p]),
+        "gw_exchange_batch": (c_int, [p, i64, p, p, p, p, P64, ctypes.POINTER(p), ctypes.POINTER(p),
+                                      ctypes.POINTER(p), ctypes.POINTER(p), p]),
+        "gw_exchange_min_watermark": (c_int, [p, i64, P64, p]),
+        "gw_exchange_last_error": (ctypes.c_char_p, [p]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)

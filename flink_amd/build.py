@@ -3,7 +3,7 @@
     python -m flink_amd.build [--force] [--jobs N]
 
 Sources: flink_amd/csrc/*.hip (kernels) + gw_runtime.cpp (host runtime + C ABI of
-include/gpuwin.h).  No torch in the library: it links only the HIP runtime.
+include/gpuwin.h).  No torch in the library: it links the HIP runtime and RCCL (gw_exchange.cpp).
 """
 from __future__ import annotations
 
@@ -17,7 +17,9 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "libgpuwin.so")
 OBJDIR = os.path.join(HERE, "_build")
-SOURCES = ["gw_pane.hip", "gw_keygroups.hip", "gw_sort.hip", "gw_session.hip", "gw_netbuf.hip", "gw_runtime.cpp"]
+SOURCES = ["gw_pane.hip", "gw_keygroups.hip", "gw_sort.hip", "gw_session.hip", "gw_netbuf.hip", "gw_runtime.cpp",
+           "gw_exchange.cpp"]
+ROCM_LIB = os.environ.get("ROCM_PATH", "/opt/rocm") + "/lib"
 ARCH = os.environ.get("GW_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 CFLAGS = ["-O3", "-fPIC", "-std=c++17", "-munsafe-fp-atomics", f"--offload-arch={ARCH}",
@@ -58,7 +60,8 @@ def build(force: bool = False, jobs: int = 4, verbose: bool = False) -> str:
         raise RuntimeError("hipcc failed:\n" + "\n".join(errors))
     objs = [o for o, _ in results]
     if force or _stale(OUT, objs):
-        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", OUT, *objs]
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", OUT, *objs, f"-L{ROCM_LIB}", "-lrccl",
+               f"-Wl,-rpath,{ROCM_LIB}"]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")

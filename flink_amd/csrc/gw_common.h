@@ -71,6 +71,17 @@ GW_HD uint64_t slot_hash(int64_t key) {
     x ^= x >> 33;
     return x;
 }
+// Its inverse (each step of the 64-bit finalizer is a bijection: xor-shifts by >= 32 are
+// self-inverse, the multipliers are odd): the compact region-path records carry the hash
+// and the apply recovers the key from it.
+GW_HD int64_t slot_unhash(uint64_t x) {
+    x ^= x >> 33;
+    x *= 0x9cb4b2f8129337dbull;  // 0xc4ceb9fe1a85ec53^-1 mod 2^64
+    x ^= x >> 33;
+    x *= 0x4f74430c22a54005ull;  // 0xff51afd7ed558ccd^-1 mod 2^64
+    x ^= x >> 33;
+    return (int64_t)x;
+}
 
 // ---------------------------------------------------------------------------
 // Double ordering (Double.compare: NaN largest and canonical, -0.0 < 0.0) as a

@@ -45,6 +45,7 @@ struct DevStatus {
     unsigned long long spills;      // region apply: records left in the buffer by full regions
     unsigned long long n_refire;    // lateness > 0: re-fire list cursor (late records of fired windows)
     unsigned long long n_late_out;  // late side output cursor (GW_FLAG_LATE_SIDE_OUTPUT)
+    unsigned long long wide_vals;   // compact region records: values beyond 32 bits sent to the deferred list
     unsigned long long pad[4];      // pad[kPubSeqWord]: stamp of a published host copy (never set on the device)
     ShardCtr sh[kShards];
 };

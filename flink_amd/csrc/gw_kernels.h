@@ -145,6 +145,7 @@ struct IngestArgs {
     // region path (k_rgn_p1 / k_rgn_plan* / k_rgn_p2 / k_rgn_apply, gw_pane.hip)
     int32_t d1_bits;       // region = (pass-1 bucket << d2_bits) | pass-2 bucket
     int32_t d2_bits;       // 0: single-pass table (apply reads the P1 tiles directly)
+    int32_t cmp;           // compact records (integer aggregates): hash word + 32-bit value
     int64_t tile0;         // P1: buffer tile of this batch's first tile
     int64_t ntiles;        // flush: buffer tiles in use
     int64_t ngroups;       // flush: P1 tile groups (= P2 blocks per bucket)
@@ -318,6 +319,6 @@ hipError_t launch_check_keys(int64_t n, const int64_t* key, const int32_t* key_h
 hipError_t launch_partition(int64_t n, const int64_t* key, const int32_t* key_hash, const int64_t* ts,
                             const int64_t* val, int32_t max_p, int32_t p, int64_t* key_out,
                             int64_t* ts_out, int64_t* val_out, int64_t* counts, void* scratch,
-                            hipStream_t s);
+                            hipStream_t s, int32_t* hash_out = nullptr);
 
 }  // namespace gw

@@ -80,7 +80,7 @@ __global__ void __launch_bounds__(1024) k_part_scan(uint32_t* block_counts, int6
 __global__ void __launch_bounds__(256) k_part_scatter(int64_t n, const int64_t* key, const int32_t* key_hash,
                                                       const int64_t* ts, const int64_t* val, int32_t max_p,
                                                       int32_t p, const int64_t* offsets, int64_t* key_out,
-                                                      int64_t* ts_out, int64_t* val_out) {
+                                                      int64_t* ts_out, int64_t* val_out, int32_t* hash_out) {
     __shared__ int64_t cursor[kPartMaxDest];
     __shared__ uint32_t wave_cnt[4][kPartMaxDest];
     const int lane = __lane_id();
@@ -109,6 +109,7 @@ __global__ void __launch_bounds__(256) k_part_scatter(int64_t n, const int64_t* 
             key_out[pos] = key[i];
             ts_out[pos] = ts[i];
             if (val) val_out[pos] = val[i];
+            if (hash_out) hash_out[pos] = key_hash[i];
         }
         __syncthreads();
         for (int dd = threadIdx.x; dd < p; dd += blockDim.x)
@@ -175,7 +176,7 @@ int64_t partition_scratch_bytes(int64_t n, int32_t p) {
 
 hipError_t launch_partition(int64_t n, const int64_t* key, const int32_t* key_hash, const int64_t* ts,
                             const int64_t* val, int32_t max_p, int32_t p, int64_t* key_out, int64_t* ts_out,
-                            int64_t* val_out, int64_t* counts, void* scratch, hipStream_t s) {
+                            int64_t* val_out, int64_t* counts, void* scratch, hipStream_t s, int32_t* hash_out) {
     if (p < 1 || p > kPartMaxDest) return hipErrorInvalidValue;
     const int64_t nb = part_blocks(n);
     uint32_t* bc = (uint32_t*)scratch;
@@ -183,7 +184,7 @@ hipError_t launch_partition(int64_t n, const int64_t* key, const int32_t* key_ha
     hipLaunchKernelGGL(k_part_hist, dim3((unsigned)nb), dim3(256), 0, s, n, key, key_hash, max_p, p, bc);
     hipLaunchKernelGGL(k_part_scan, dim3(1), dim3(1024), 0, s, bc, nb, p, off, counts);
     hipLaunchKernelGGL(k_part_scatter, dim3((unsigned)nb), dim3(256), 0, s, n, key, key_hash, ts, val, max_p, p,
-                       off, key_out, ts_out, val_out);
+                       off, key_out, ts_out, val_out, key_hash ? hash_out : nullptr);
     return hipGetLastError();
 }
 

@@ -361,6 +361,27 @@ constexpr int kPartItems = kPartTile / kPartThreads;
 __device__ __forceinline__ int64_t rgn_of(const PaneTable& t, int64_t key) { return pt_key_region(t, slot_hash(key)); }
 __device__ __forceinline__ uint32_t desc_pack(uint32_t start, uint32_t cnt) { return (start << 16) | cnt; }
 
+// Compact records (integer aggregates; the host enables them when R <= 2^(d1-1)): 12 B per
+// record instead of 17 (8 for COUNT).  The 64-bit word is the key's hash with its top d1
+// bits -- the pass-1 bucket, known from where the record sits -- replaced by the ring
+// position, bit 63 marking a spill; the value is 32 bits (wider values go to the deferred
+// list in P1).  The hash is a bijection (slot_unhash), so the apply recovers the key.
+template <int AGG>
+__device__ __forceinline__ constexpr bool cmp_agg() {
+    return AGG == GW_COUNT || AGG == GW_SUM_I64 || AGG == GW_SUM_I32 || AGG == GW_MIN_I64 || AGG == GW_MAX_I64 ||
+           AGG == GW_AVG_I64;
+}
+__device__ __forceinline__ uint64_t cmp_pack(uint64_t h, uint32_t pos, int d1) {
+    const int sh = 64 - d1;
+    return (h & ((1ull << sh) - 1ull)) | ((uint64_t)pos << sh);
+}
+__device__ __forceinline__ uint64_t cmp_hash(uint64_t w, uint64_t bucket, int d1) {
+    const int sh = 64 - d1;
+    return (bucket << sh) | (w & ((1ull << sh) - 1ull));
+}
+__device__ __forceinline__ uint32_t cmp_pos(uint64_t w, int d1) { return (uint32_t)((w << 1) >> (65 - d1)); }
+constexpr uint64_t kCmpSpill = 1ull << 63;
+
 // Exclusive scan of h[0..nb) (nb <= 256) into out[]; executed by wave 0.
 __device__ __forceinline__ void scan_buckets(const uint32_t* h, uint32_t* out, int nb) {
     if (threadIdx.x >= 64) return;
@@ -455,11 +476,14 @@ __global__ void __launch_bounds__(256) k_publish_status(const DevStatus* st, Dev
 }
 
 // P1: one 4096-record tile of the batch -> buffer tile a.tile0 + blockIdx.x.
-template <int AGG>
+template <int AGG, bool CMP>
 __global__ void __launch_bounds__(kPartThreads) k_rgn_p1(IngestArgs a) {
-    constexpr bool AV = AGG == GW_AVG_I64 || AGG == GW_AVG_F64;
+    constexpr bool C = CMP && cmp_agg<AGG>();
+    constexpr bool AV = !C && (AGG == GW_AVG_I64 || AGG == GW_AVG_F64);
+    constexpr bool ACC = !(C && AGG == GW_COUNT);  // COUNT records carry no value
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const TileLds s = tile_lds<AV>(smem);
+    int32_t* s_v32 = reinterpret_cast<int32_t*>(s.a0);  // C: 32-bit values
     __shared__ uint32_t lh[kPartBuckets], ls[kPartBuckets];
     __shared__ unsigned long long s_occ;
     const int64_t g = blockIdx.x;
@@ -468,7 +492,7 @@ __global__ void __launch_bounds__(kPartThreads) k_rgn_p1(IngestArgs a) {
     for (int b = threadIdx.x; b < kPartBuckets; b += blockDim.x) lh[b] = 0;
     if (threadIdx.x == 0) s_occ = 0;
     __syncthreads();
-    unsigned long long late = 0, flags = 0, occ = 0;
+    unsigned long long late = 0, flags = 0, occ = 0, wide = 0;
     int64_t key[kPartItems], ts[kPartItems], val[kPartItems], c0[kPartItems], c1[kPartItems];
     uint32_t pos[kPartItems], rank[kPartItems];
     int bk[kPartItems];
@@ -490,13 +514,19 @@ __global__ void __launch_bounds__(kPartThreads) k_rgn_p1(IngestArgs a) {
         int st = REC_SKIP;
         int64_t pane = 0;
         if (i < hi) st = classify<AGG>(a, ts[it], val[it], pos[it], pane, c0[it], c1[it], late, flags);
+        if (C && ACC && st == REC_RING && (c0[it] < INT32_MIN || c0[it] > INT32_MAX)) {
+            st = REC_DEFER;  // beyond the compact record's 32-bit value: exact via the deferred list
+            wide++;
+        }
         if (st == REC_RING) {
             occ |= 1ull << pos[it];
             if (key[it] == kEmptyKey) {  // sentinel slot: rare, straight atomics
                 cell_atomic<AGG>(pt_cell(a.t, a.t.cap, pos[it]), c0[it], c1[it]);
                 mask_set<AGG>(a.t, a.t.cap, pos[it]);
             } else {
-                bk[it] = (int)(rgn_of(a.t, key[it]) >> a.d2_bits);
+                const uint64_t h = slot_hash(key[it]);
+                bk[it] = (int)(pt_key_region(a.t, h) >> a.d2_bits);
+                if constexpr (C) key[it] = (int64_t)cmp_pack(h, pos[it], a.d1_bits);  // key -> word
             }
         }
         defer_write(a, st == REC_DEFER, key[it], pane, c0[it], c1[it]);
@@ -515,9 +545,13 @@ __global__ void __launch_bounds__(kPartThreads) k_rgn_p1(IngestArgs a) {
         if (bk[it] < 0) continue;
         const uint32_t j = ls[bk[it]] + rank[it];
         s.k[j] = key[it];
-        s.a0[j] = c0[it];
-        if constexpr (AV) s.a1[j] = c1[it];
-        s.pos[j] = (uint8_t)pos[it];
+        if constexpr (C) {
+            if constexpr (ACC) s_v32[j] = (int32_t)c0[it];
+        } else {
+            s.a0[j] = c0[it];
+            if constexpr (AV) s.a1[j] = c1[it];
+            s.pos[j] = (uint8_t)pos[it];
+        }
     }
     __syncthreads();
     const uint32_t cnt = ls[nb - 1] + lh[nb - 1];
@@ -525,11 +559,19 @@ __global__ void __launch_bounds__(kPartThreads) k_rgn_p1(IngestArgs a) {
     const int64_t base = tile * kPartTile;
     for (uint32_t j = threadIdx.x; j < cnt; j += blockDim.x) {
         a.p1_key[base + j] = s.k[j];
-        a.p1_a0[base + j] = s.a0[j];
-        if constexpr (AV) a.p1_a1[base + j] = s.a1[j];
-        a.p1_pos[base + j] = s.pos[j];
+        if constexpr (C) {
+            if constexpr (ACC) reinterpret_cast<int32_t*>(a.p1_a0)[base + j] = s_v32[j];
+        } else {
+            a.p1_a0[base + j] = s.a0[j];
+            if constexpr (AV) a.p1_a1[base + j] = s.a1[j];
+            a.p1_pos[base + j] = s.pos[j];
+        }
     }
     for (int b = threadIdx.x; b < nb; b += blockDim.x) a.p1_row[tile * kPartBuckets + b] = desc_pack(ls[b], lh[b]);
+    if constexpr (C && ACC) {
+        wide = wave_sum(wide);
+        if (__lane_id() == 0 && wide) atomicAdd(&a.st->wide_vals, wide);
+    }
     block_commit(a.st, late, 0, flags, occ);
 }
 
@@ -646,11 +688,15 @@ __global__ void __launch_bounds__(256) k_rgn_plan3(IngestArgs a) {
 }
 
 // P2: block (b1, j) -> rounds p2_roff[b1, j] ... of bucket b1, records at p2_off[b1, j].
-template <int AGG>
+template <int AGG, bool CMP>
 __global__ void __launch_bounds__(kPartThreads) k_rgn_p2(IngestArgs a) {
-    constexpr bool AV = AGG == GW_AVG_I64 || AGG == GW_AVG_F64;
+    constexpr bool C = CMP && cmp_agg<AGG>();
+    constexpr bool AV = !C && (AGG == GW_AVG_I64 || AGG == GW_AVG_F64);
+    constexpr bool ACC = !(C && AGG == GW_COUNT);
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const TileLds s = tile_lds<AV>(smem);
+    int32_t* s_v32 = reinterpret_cast<int32_t*>(s.a0);
+    const int lr_sh = 64 - (a.d1_bits + a.d2_bits);  // C: region bits of the hash word
     __shared__ uint32_t lh[kPartBuckets], ls[kPartBuckets];
     __shared__ uint32_t r_cnt[kMaxGroup], r_pre[kMaxGroup + 1], wsum[8];
     __shared__ int64_t r_src[kMaxGroup];
@@ -685,16 +731,20 @@ __global__ void __launch_bounds__(kPartThreads) k_rgn_p2(IngestArgs a) {
                 const int i = run_of(r_pre, nt, e);
                 const int64_t src = r_src[i] + (e - r_pre[i]);
                 key[it] = a.p1_key[src];
-                c0[it] = a.p1_a0[src];
-                if constexpr (AV) c1[it] = a.p1_a1[src];
-                pos[it] = a.p1_pos[src];
+                if constexpr (C) {
+                    if constexpr (ACC) c0[it] = reinterpret_cast<const int32_t*>(a.p1_a0)[src];
+                } else {
+                    c0[it] = a.p1_a0[src];
+                    if constexpr (AV) c1[it] = a.p1_a1[src];
+                    pos[it] = a.p1_pos[src];
+                }
                 bk[it] = 0;
             }
         }
 #pragma unroll
         for (int it = 0; it < kPartItems; ++it) {
             if (bk[it] < 0) continue;
-            bk[it] = (int)(rgn_of(a.t, key[it]) & m2);
+            bk[it] = C ? (int)(((uint64_t)key[it] >> lr_sh) & (uint64_t)m2) : (int)(rgn_of(a.t, key[it]) & m2);
             rank[it] = atomicAdd(&lh[bk[it]], 1u);
         }
         __syncthreads();
@@ -705,18 +755,26 @@ __global__ void __launch_bounds__(kPartThreads) k_rgn_p2(IngestArgs a) {
             if (bk[it] < 0) continue;
             const uint32_t jj = ls[bk[it]] + rank[it];
             s.k[jj] = key[it];
-            s.a0[jj] = c0[it];
-            if constexpr (AV) s.a1[jj] = c1[it];
-            s.pos[jj] = (uint8_t)pos[it];
+            if constexpr (C) {
+                if constexpr (ACC) s_v32[jj] = (int32_t)c0[it];
+            } else {
+                s.a0[jj] = c0[it];
+                if constexpr (AV) s.a1[jj] = c1[it];
+                s.pos[jj] = (uint8_t)pos[it];
+            }
         }
         __syncthreads();
         const int64_t base = out0 + e0;
         const int64_t rnd = rnd0 + e0 / kPartTile;
         for (uint32_t jj = threadIdx.x; jj < e1 - e0; jj += blockDim.x) {
             a.e_key[base + jj] = s.k[jj];
-            a.e_a0[base + jj] = s.a0[jj];
-            if constexpr (AV) a.e_a1[base + jj] = s.a1[jj];
-            a.e_pos[base + jj] = s.pos[jj];
+            if constexpr (C) {
+                if constexpr (ACC) reinterpret_cast<int32_t*>(a.e_a0)[base + jj] = s_v32[jj];
+            } else {
+                a.e_a0[base + jj] = s.a0[jj];
+                if constexpr (AV) a.e_a1[base + jj] = s.a1[jj];
+                a.e_pos[base + jj] = s.pos[jj];
+            }
         }
         for (int b = threadIdx.x; b < nb2; b += blockDim.x) a.r_row[rnd * kPartBuckets + b] = desc_pack(ls[b], lh[b]);
         if (threadIdx.x == 0) a.r_base[rnd] = base;
@@ -737,11 +795,13 @@ constexpr int kApplyRuns = 256;  // run descriptors staged in LDS per step (<= b
 constexpr int kApplyGroup = 4;   // consecutive runs a wave walks as one sequence
 constexpr int kApplyUnroll = 4;  // records per lane with their loads in flight together
 
-template <int AGG>
+template <int AGG, bool CMP>
 __global__ void __launch_bounds__(512) k_rgn_apply(IngestArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     constexpr bool M = uses_mask<AGG>();
-    constexpr bool AV = AGG == GW_AVG_I64 || AGG == GW_AVG_F64;
+    constexpr bool C = CMP && cmp_agg<AGG>();
+    constexpr bool AV = AGG == GW_AVG_I64 || AGG == GW_AVG_F64;  // (C: a1 = 1, not stored)
+    constexpr bool ACC = !(C && AGG == GW_COUNT);
     __shared__ uint32_t r_cnt[kApplyRuns], r_src[kApplyRuns];  // buffer offsets < 2^32 (gw_runtime.cpp)
     const int64_t r = blockIdx.x;
     const int64_t S = pt_S(a.t);
@@ -756,6 +816,8 @@ __global__ void __launch_bounds__(512) k_rgn_apply(IngestArgs a) {
     const int64_t* ra0 = single ? a.p1_a0 : a.e_a0;
     const int64_t* ra1 = single ? a.p1_a1 : a.e_a1;
     const uint8_t* rpos = single ? a.p1_pos : a.e_pos;
+    const int32_t* rv32 = reinterpret_cast<const int32_t*>(ra0);  // C: 32-bit values
+    const uint64_t bucket_id = (uint64_t)bucket;                 // C: the hash's top d1 bits
     long long* lkeys = (long long*)smem;
     const int64_t MW = pt_mask_words(a.t);       // 0 unless M
     uint8_t* lmask = (uint8_t*)(lkeys + S);
@@ -820,13 +882,13 @@ __global__ void __launch_bounds__(512) k_rgn_apply(IngestArgs a) {
     unsigned long long ins = 0, flags = 0, spills = 0;
     // false: the region is full; the record stays in the buffer marked (pos | 0x80) and
     // k_rgn_collect parks it on the deferred list once the host has room for it
-    auto apply_one = [&](int64_t key, int64_t c0, int64_t c1, uint32_t pos, int64_t x) -> bool {
+    auto apply_one = [&](int64_t key, uint64_t h, int64_t c0, int64_t c1, uint32_t pos) -> bool {
         // Probe one 4-key group (32 B) per step: the first slot holding the key or
         // empty, in slot order, decides; an empty slot is claimed with a CAS (a lost race
         // re-reads the same group).
         // 32-bit LDS indices (S <= 2048 slots)
         const int Si = (int)S;
-        int g0 = (int)pt_home(a.t, slot_hash(key));
+        int g0 = (int)pt_home(a.t, h);
         int found = -1;
         for (int p = 0; p < Si;) {
             const long2 k01 = *reinterpret_cast<const long2*>(&lkeys[g0]);
@@ -889,7 +951,6 @@ __global__ void __launch_bounds__(512) k_rgn_apply(IngestArgs a) {
     };
     struct Step {
         int64_t key[kApplyUnroll], v0[kApplyUnroll], v1[kApplyUnroll];
-        uint32_t x[kApplyUnroll];
         uint8_t ps[kApplyUnroll];
         bool ok[kApplyUnroll];
     };
@@ -928,12 +989,16 @@ __global__ void __launch_bounds__(512) k_rgn_apply(IngestArgs a) {
                 // unconditional loads (an idle lane reads record 0): no branch around them,
                 // so the compiler can count them and wait for exactly the ones it needs
                 const uint32_t x = s.ok[q] ? sb + (e - sp) : 0u;
-                s.x[q] = x;
                 s.key[q] = rk[x];
-                s.v0[q] = ra0[x];
                 s.v1[q] = 1;
-                if constexpr (AV) s.v1[q] = ra1[x];
-                s.ps[q] = rpos[x];
+                if constexpr (C) {
+                    s.v0[q] = ACC ? (int64_t)rv32[x] : 1;
+                    s.ps[q] = 0;  // in the word
+                } else {
+                    s.v0[q] = ra0[x];
+                    if constexpr (AV) s.v1[q] = ra1[x];
+                    s.ps[q] = rpos[x];
+                }
             }
         };
         // next non-empty step after (i0, k) (k = ~0u: the first one), wave-uniform
@@ -956,8 +1021,15 @@ __global__ void __launch_bounds__(512) k_rgn_apply(IngestArgs a) {
         // well, so the compiler can count the outstanding ones on every path.
         auto apply_step = [&](const Step& c) {
 #pragma unroll
-            for (int q = 0; q < kApplyUnroll; ++q)
-                if (c.ok[q]) apply_one(c.key[q], c.v0[q], c.v1[q], c.ps[q], c.x[q]);
+            for (int q = 0; q < kApplyUnroll; ++q) {
+                if (!c.ok[q]) continue;
+                if constexpr (C) {
+                    const uint64_t h = cmp_hash((uint64_t)c.key[q], bucket_id, a.d1_bits);
+                    apply_one(slot_unhash(h), h, c.v0[q], c.v1[q], cmp_pos((uint64_t)c.key[q], a.d1_bits));
+                } else {
+                    apply_one(c.key[q], slot_hash(c.key[q]), c.v0[q], c.v1[q], c.ps[q]);
+                }
+            }
         };
         Step sa, sb;
         bool live = advance(i0, k, g);
@@ -990,10 +1062,19 @@ __global__ void __launch_bounds__(512) k_rgn_apply(IngestArgs a) {
             for (int i = wave; i < nr; i += nw) {
                 for (uint32_t k = lane; k < r_cnt[i]; k += 64) {
                     const uint32_t x = r_src[i] + k;
-                    const int64_t key = rk[x];
-                    const uint32_t pos = rpos[x];
+                    int64_t key = rk[x];
+                    uint32_t pos;
+                    uint64_t h;
+                    if constexpr (C) {
+                        h = cmp_hash((uint64_t)key, bucket_id, a.d1_bits);
+                        pos = cmp_pos((uint64_t)key, a.d1_bits);
+                        key = slot_unhash(h);
+                    } else {
+                        pos = rpos[x];
+                        h = slot_hash(key);
+                    }
                     bool present = false;
-                    int64_t g0 = pt_home(a.t, slot_hash(key));
+                    int64_t g0 = pt_home(a.t, h);
                     for (int64_t p = 0; p < S; ++p) {
                         const long long kk = lkeys[g0];
                         if (kk == key) { present = true; break; }
@@ -1001,7 +1082,8 @@ __global__ void __launch_bounds__(512) k_rgn_apply(IngestArgs a) {
                         g0 = (g0 + 1) & (S - 1);
                     }
                     if (!present || ((int)pos != act0 && (int)pos != act1)) {
-                        const_cast<uint8_t*>(rpos)[x] = (uint8_t)(pos | 0x80u);
+                        if constexpr (C) const_cast<int64_t*>(rk)[x] = (int64_t)((uint64_t)rk[x] | kCmpSpill);
+                        else const_cast<uint8_t*>(rpos)[x] = (uint8_t)(pos | 0x80u);
                         marked++;
                     }
                 }
@@ -1028,6 +1110,46 @@ __global__ void __launch_bounds__(512) k_rgn_apply(IngestArgs a) {
     spills = wave_sum(spills);
     if (__lane_id() == 0 && spills) atomicAdd(&a.st->spills, spills);
     block_commit(a.st, 0, ins, flags, 0);
+}
+
+// The same for compact records: the spill mark is bit 63 of the word, and the key comes
+// back from the hash, whose top bits are the record's bucket -- so one workgroup per
+// region walks the region's runs as the apply does.
+template <int AGG>
+__global__ void __launch_bounds__(256) k_rgn_collect_cmp(IngestArgs a) {
+    constexpr bool ACC = AGG != GW_COUNT;
+    const int64_t r = blockIdx.x;
+    const int64_t bucket = r >> a.d2_bits, col = r & (((int64_t)1 << a.d2_bits) - 1);
+    const bool single = a.d2_bits == 0;
+    const int64_t rb = single ? 0 : a.rbeg[bucket], re = single ? a.ntiles : a.rbeg[bucket + 1];
+    const int64_t ccol = single ? r : col;
+    const uint32_t* rows = single ? a.p1_row : a.r_row;
+    int64_t* rk = single ? a.p1_key : a.e_key;
+    const int32_t* rv32 = reinterpret_cast<const int32_t*>(single ? a.p1_a0 : a.e_a0);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    for (int64_t rnd = rb + wave; rnd < re; rnd += nw) {  // a wave per run: uniform loop bounds
+        const uint32_t d = rows[rnd * kPartBuckets + ccol];
+        const uint32_t cnt = d & 0xffffu;
+        const int64_t src = (single ? rnd * kPartTile : a.r_base[rnd]) + (d >> 16);
+        for (uint32_t k0 = 0; k0 < cnt; k0 += 64) {
+            const uint32_t k = k0 + lane;
+            bool spill = false;
+            int64_t key = 0, pane = 0, c0 = 0;
+            if (k < cnt) {
+                const uint64_t w = (uint64_t)rk[src + k];
+                if (w & kCmpSpill) {
+                    spill = true;
+                    rk[src + k] = (int64_t)(w & ~kCmpSpill);
+                    key = slot_unhash(cmp_hash(w, (uint64_t)bucket, a.d1_bits));
+                    const uint32_t pos = cmp_pos(w, a.d1_bits);
+                    c0 = ACC ? (int64_t)rv32[src + k] : 1;
+                    const int64_t rel = ((int64_t)pos - a.b_pos + a.t.ring) % a.t.ring;
+                    pane = a.p_late + (int64_t)a.delta + rel;
+                }
+            }
+            defer_write(a, spill, key, pane, c0, 1);
+        }
+    }
 }
 
 // After a flush that filled regions: park every spilled record (pos | 0x80 in the
@@ -1239,6 +1361,9 @@ __global__ void __launch_bounds__(256) k_deferred_min(const int64_t* pane, int64
 // with the identity unconditionally (full-line coalesced stores).
 template <int AGG>
 __global__ void __launch_bounds__(256) k_fire(FireArgs a) {
+    // kFireU slots per thread per step: their key / presence loads, then their cell loads,
+    // are issued together (a sweep is latency-bound with one dependent chain per lane)
+    constexpr int kFireU = 4;
     __shared__ RowStage rs;
     const int64_t nslots = a.t.cap + 1;
     const int64_t id0 = identity0(AGG);
@@ -1246,70 +1371,92 @@ __global__ void __launch_bounds__(256) k_fire(FireArgs a) {
     if (threadIdx.x == 0) rs.cnt = 0;
     if (blockIdx.x == 0 && threadIdx.x < kShards) atomicAnd(&a.st->sh[threadIdx.x].occ, ~a.rmask);
     __syncthreads();
-    const int64_t chunk = ((nslots + gridDim.x - 1) / gridDim.x + 255) / 256 * 256;
+    const int64_t step = (int64_t)blockDim.x * kFireU;
+    const int64_t chunk = ((nslots + gridDim.x - 1) / gridDim.x + step - 1) / step * step;
     const int64_t c0 = blockIdx.x * chunk, c1 = min(nslots, c0 + chunk);
-    for (int64_t base = c0; base < c1; base += blockDim.x) {
-        const int64_t g = base + threadIdx.x;
-        int64_t key = kEmptyKey;
-        uint64_t mask = 0;
-        const bool live = g < c1;
-        int64_t oi = -1;  // this key's next restored-window entry
-        if (live) {
-            key = *pt_key(a.t, g);
-            mask = presence<AGG>(a.t, g);
-            if (a.ov.head) oi = a.ov.head[g];
+    for (int64_t base = c0; base < c1; base += step) {
+        int64_t key[kFireU], oi[kFireU];
+        uint64_t mask[kFireU];
+#pragma unroll
+        for (int u = 0; u < kFireU; ++u) {
+            const int64_t g = base + u * (int64_t)blockDim.x + threadIdx.x;
+            key[u] = kEmptyKey;
+            mask[u] = 0;
+            oi[u] = -1;  // this key's next restored-window entry
+            if (g < c1) {
+                key[u] = *pt_key(a.t, g);
+                mask[u] = presence<AGG>(a.t, g);
+                if (a.ov.head) oi[u] = a.ov.head[g];
+            }
         }
         for (int w = 0; w < a.nwin; ++w) {
-            const bool flush = rs.cnt + blockDim.x > kRowStage;  // uniform: read before any append
+            const bool flush = rs.cnt + kFireU * blockDim.x > kRowStage;  // uniform: read before any append
             __syncthreads();
             if (flush) stage_flush(rs, &a.st->rows, a.o_key, a.o_start, a.o_end, a.o_res);
-            uint64_t m = mask & a.wmask[w];
-            bool ov_hit = false;
-            int64_t o0 = 0, o1 = 0;
-            if (oi >= 0) {  // restored state of (key, window): fires with its timer or with new records
-                const int64_t kk = a.k0 + w;
-                while (oi < a.ov.n && a.ov.key[oi] == key && a.ov.k[oi] < kk) ++oi;
-                if (oi < a.ov.n && a.ov.key[oi] == key && a.ov.k[oi] == kk) {
-                    const uint32_t f = a.ov.flags[oi];
-                    if (!(f & kOvDead) && (m || (f & kOvTimer))) {
-                        ov_hit = true;
-                        o0 = a.ov.a0[oi];
-                        o1 = a.ov.a1[oi];
-                        a.ov.flags[oi] = a.ov.purge ? kOvDead : (f & ~kOvTimer);
+            int64_t r0[kFireU], r1[kFireU];
+            bool emit[kFireU];
+#pragma unroll
+            for (int u = 0; u < kFireU; ++u) {
+                const int64_t g = base + u * (int64_t)blockDim.x + threadIdx.x;
+                uint64_t m = mask[u] & a.wmask[w];
+                bool ov_hit = false;
+                int64_t o0 = 0, o1 = 0;
+                if (oi[u] >= 0) {  // restored state of (key, window): fires with its timer or with new records
+                    const int64_t kk = a.k0 + w;
+                    int64_t x = oi[u];
+                    while (x < a.ov.n && a.ov.key[x] == key[u] && a.ov.k[x] < kk) ++x;
+                    if (x < a.ov.n && a.ov.key[x] == key[u] && a.ov.k[x] == kk) {
+                        const uint32_t f = a.ov.flags[x];
+                        if (!(f & kOvDead) && (m || (f & kOvTimer))) {
+                            ov_hit = true;
+                            o0 = a.ov.a0[x];
+                            o1 = a.ov.a1[x];
+                            a.ov.flags[x] = a.ov.purge ? kOvDead : (f & ~kOvTimer);
+                        }
+                    } else if (x >= a.ov.n || a.ov.key[x] != key[u]) {
+                        x = -1;
                     }
-                } else if (oi >= a.ov.n || a.ov.key[oi] != key) {
-                    oi = -1;
+                    oi[u] = x;
                 }
-            }
-            if (m || ov_hit) {
-                int64_t r0 = id0, r1 = 0;
+                emit[u] = m || ov_hit;
+                r0[u] = id0;
+                r1[u] = 0;
                 while (m) {
                     const int pos = __ffsll((long long)m) - 1;
                     m &= m - 1;
                     const int64_t* c = pt_cell(a.t, g, pos);
-                    fold_cell(AGG, r0, r1, c[0], W == 2 ? c[1] : 0);
+                    fold_cell(AGG, r0[u], r1[u], c[0], W == 2 ? c[1] : 0);
                 }
-                if (ov_hit) fold_cell(AGG, r0, r1, o0, o1);
+                if (ov_hit) fold_cell(AGG, r0[u], r1[u], o0, o1);
+            }
+            const int64_t st = a.start0 + (int64_t)w * a.slide;
+#pragma unroll
+            for (int u = 0; u < kFireU; ++u) {
+                if (!emit[u]) continue;
                 const unsigned j = atomicAdd(&rs.cnt, 1u);
-                const int64_t st = a.start0 + (int64_t)w * a.slide;
-                rs.k[j] = key;
+                rs.k[j] = key[u];
                 rs.s[j] = st;
                 rs.e[j] = st + a.size;
-                rs.r[j] = cell_result(AGG, r0, r1);
+                rs.r[j] = cell_result(AGG, r0[u], r1[u]);
             }
             __syncthreads();
         }
-        if (live && a.rmask) {
-            if constexpr (uses_mask<AGG>()) {
-                if (mask & a.rmask) pt_mask_put(a.t, g, mask & ~a.rmask);
-            }
-            uint64_t m = a.rmask;
-            while (m) {
-                const int pos = __ffsll((long long)m) - 1;
-                m &= m - 1;
-                int64_t* c = pt_cell(a.t, g, pos);
-                c[0] = id0;
-                if (W == 2) c[1] = 0;
+        if (a.rmask) {
+#pragma unroll
+            for (int u = 0; u < kFireU; ++u) {
+                const int64_t g = base + u * (int64_t)blockDim.x + threadIdx.x;
+                if (g >= c1) continue;
+                if constexpr (uses_mask<AGG>()) {
+                    if (mask[u] & a.rmask) pt_mask_put(a.t, g, mask[u] & ~a.rmask);
+                }
+                uint64_t m = a.rmask;
+                while (m) {
+                    const int pos = __ffsll((long long)m) - 1;
+                    m &= m - 1;
+                    int64_t* c = pt_cell(a.t, g, pos);
+                    c[0] = id0;
+                    if (W == 2) c[1] = 0;
+                }
             }
         }
     }
@@ -1518,6 +1665,7 @@ static void lds_opt_in(const void* f, size_t bytes) {
 }
 
 static size_t part_lds_bytes(const IngestArgs& a) {
+    if (a.cmp) return (size_t)kPartTile * 12;  // hash word + 32-bit value
     return (size_t)kPartTile * 8 * (a.t.words == 2 ? 3 : 2) + 2 * kPartTile;
 }
 
@@ -1530,8 +1678,13 @@ hipError_t launch_region_p1(const IngestArgs& a, hipStream_t s) {
     const size_t part_lds = part_lds_bytes(a);
     // beyond the 64 KB default: opt in (gfx950 has 160 KB of LDS per CU)
 #define L(A)                                                                                                    \
-    lds_opt_in((const void*)k_rgn_p1<A>, part_lds);                                                            \
-    hipLaunchKernelGGL(k_rgn_p1<A>, dim3((unsigned)tiles), dim3(kPartThreads), part_lds, s, a)
+    if (a.cmp) {                                                                                                \
+        lds_opt_in((const void*)k_rgn_p1<A, true>, part_lds);                                                  \
+        hipLaunchKernelGGL((k_rgn_p1<A, true>), dim3((unsigned)tiles), dim3(kPartThreads), part_lds, s, a);    \
+    } else {                                                                                                    \
+        lds_opt_in((const void*)k_rgn_p1<A, false>, part_lds);                                                 \
+        hipLaunchKernelGGL((k_rgn_p1<A, false>), dim3((unsigned)tiles), dim3(kPartThreads), part_lds, s, a);   \
+    }
     GW_AGG_SWITCH(a.t.agg, L);
 #undef L
     return hipGetLastError();
@@ -1551,24 +1704,36 @@ hipError_t launch_region_flush(const IngestArgs& a, hipStream_t s) {
     const size_t apply_lds = (size_t)(S + pt_mask_words(a.t)) * 8 + (size_t)2 * S * a.t.words * 8;
     const int nb1 = 1 << a.d1_bits;
     if (a.ntiles == 0) return hipSuccess;
-#define L(A)                                                                                                    \
-    lds_opt_in((const void*)k_rgn_p2<A>, part_lds);                                                            \
-    lds_opt_in((const void*)k_rgn_apply<A>, apply_lds);                                                        \
+#define L2(A, CM)                                                                                               \
+    lds_opt_in((const void*)k_rgn_p2<A, CM>, part_lds);                                                       \
+    lds_opt_in((const void*)k_rgn_apply<A, CM>, apply_lds);                                                   \
     if (!single) {                                                                                              \
         hipLaunchKernelGGL(k_rgn_plan1, dim3((unsigned)a.ngroups), dim3(256), 0, s, a);                        \
         hipLaunchKernelGGL(k_rgn_plan2, dim3((unsigned)nb1), dim3(256), 0, s, a);                              \
         hipLaunchKernelGGL(k_rgn_plan3, dim3(1), dim3(256), 0, s, a);                                          \
-        hipLaunchKernelGGL(k_rgn_p2<A>, dim3((unsigned)(a.ngroups * nb1)), dim3(kPartThreads), part_lds, s, a); \
+        hipLaunchKernelGGL((k_rgn_p2<A, CM>), dim3((unsigned)(a.ngroups * nb1)), dim3(kPartThreads), part_lds, s, \
+                           a);                                                                                  \
     }                                                                                                           \
-    hipLaunchKernelGGL(k_rgn_apply<A>, dim3((unsigned)a.t.nreg), dim3(512), apply_lds, s, a)
+    hipLaunchKernelGGL((k_rgn_apply<A, CM>), dim3((unsigned)a.t.nreg), dim3(512), apply_lds, s, a)
+#define L(A)            \
+    if (a.cmp) {        \
+        L2(A, true);    \
+    } else {            \
+        L2(A, false);   \
+    }
     GW_AGG_SWITCH(a.t.agg, L);
 #undef L
+#undef L2
     return hipGetLastError();
 }
 
 hipError_t launch_region_collect(const IngestArgs& a, hipStream_t s) {
     const int64_t n = a.ntiles * kPartTile;  // upper bound of the buffer's records
-#define L(A) hipLaunchKernelGGL(k_rgn_collect<A>, dim3(grid_for(n)), dim3(256), 0, s, a)
+#define L(A)                                                                                         \
+    if (a.cmp)                                                                                       \
+        hipLaunchKernelGGL(k_rgn_collect_cmp<A>, dim3((unsigned)a.t.nreg), dim3(256), 0, s, a);     \
+    else                                                                                             \
+        hipLaunchKernelGGL(k_rgn_collect<A>, dim3(grid_for(n)), dim3(256), 0, s, a)
     GW_AGG_SWITCH(a.t.agg, L);
 #undef L
     return hipGetLastError();
@@ -1604,7 +1769,8 @@ hipError_t launch_deferred_min(const int64_t* pane, int64_t n, DevStatus* st, hi
 }
 
 hipError_t launch_fire(const FireArgs& a, hipStream_t s) {
-    const int fg = (int)std::min<int64_t>(1024, std::max<int64_t>(1, (a.t.cap + 1 + 255) / 256));
+    // 5 workgroups per CU fit (32 KB row stage each): one resident wave of blocks
+    const int fg = (int)std::min<int64_t>(5 * 256, std::max<int64_t>(1, (a.t.cap + 1 + 1023) / 1024));
 #define L(A) hipLaunchKernelGGL(k_fire<A>, dim3(fg), dim3(256), 0, s, a)
     GW_AGG_SWITCH(a.t.agg, L);
 #undef L

@@ -184,6 +184,9 @@ struct gw_handle {
     int nseg = 0;
     int64_t buf_tiles = 0;          // tiles used by the waiting segments
     uint64_t buf_fresh = 0;         // ring positions holding only identities at buffer start
+    bool buf_cmp = false;           // the waiting segments use compact records (fixed per window)
+    int64_t buf_recs = 0;           // records of the waiting segments
+    bool cmp_off = false;           // compact records turned off: too many values beyond 32 bits
     int64_t buf_limit = (int64_t)1 << 27;  // records (GW_BUFFER_RECORDS)
 
     // allowed lateness > 0 (tumbling / sliding): late records of fired, not yet cleaned
@@ -937,6 +940,17 @@ struct gw_handle {
         a.r_row = r_row;
         a.r_base = r_base;
         a.batch_occ = d_tmp + 1;
+        a.cmp = buf_cmp ? 1 : 0;
+    }
+
+    // Compact region records (gw_pane.hip cmp_pack): integer aggregates whose ring
+    // positions fit below the pass-1 bucket bits (R <= 2^(d1-1)).
+    bool compact_ok(int d1_bits) const {
+        const int agg = cfg.agg;
+        const bool int_agg = agg == GW_COUNT || agg == GW_SUM_I64 || agg == GW_SUM_I32 || agg == GW_MIN_I64 ||
+                             agg == GW_MAX_I64 || agg == GW_AVG_I64;
+        static const bool env_off = getenv("GW_NO_COMPACT") != nullptr;
+        return int_agg && !cmp_off && !env_off && d1_bits >= 2 && (int64_t)tv.ring <= ((int64_t)1 << (d1_bits - 1));
     }
 
     // P2 + apply over every waiting segment (one fire's worth of batches).  Runs before
@@ -952,8 +966,10 @@ struct gw_handle {
         a.p2_group = region_group(a.d1_bits);
         a.ngroups = (buf_tiles + a.p2_group - 1) / a.p2_group;
         a.ring_fresh = buf_fresh;
+        const int64_t window_recs = buf_recs;
         nseg = 0;  // before any launch: the TABLE_FULL handling below may grow the table
         buf_tiles = 0;
+        buf_recs = 0;
         if (timing) {
             auto ev = t_apply.get();
             HIPCHECK(hipEventRecord(ev.first, stream));
@@ -966,6 +982,10 @@ struct gw_handle {
         stats.applies++;
         dirty = true;
         if ((rc = refresh())) return rc;
+        if (h_st->wide_vals) {  // values beyond 32 bits went the deferred way: keep it rare
+            if (h_st->wide_vals * 64 > (unsigned long long)window_recs) cmp_off = true;
+            if ((rc = set_field(offsetof(DevStatus, wide_vals), 0))) return rc;
+        }
         if (h_st->spills) {  // full regions / a third ring position left records: park them
             if ((rc = ensure_deferred((int64_t)h_st->n_deferred + (int64_t)h_st->spills))) return rc;
             if ((rc = set_field(offsetof(DevStatus, spills), 0))) return rc;
@@ -1025,7 +1045,9 @@ struct gw_handle {
             if (nseg == 0) {
                 HIPCHECK(hipMemsetAsync(d_tmp + 1, 0, 8, stream));
                 buf_fresh = ~occ;
+                buf_cmp = compact_ok(a.d1_bits);
             }
+            a.cmp = buf_cmp ? 1 : 0;
             if (buffered) arm_status(a);
             hp.lap(0);
             if (timing) {
@@ -1040,6 +1062,7 @@ struct gw_handle {
             if (buffered) HIPCHECK(launch_publish_status(a, stream));
             nseg++;
             buf_tiles += tiles;
+            buf_recs += nrec;
             if (!buffered && (rc = flush_buffer())) return rc;
         } else if (timing) {
             auto ev = t_ingest.get();

@@ -119,3 +119,71 @@ class KeyByExchange:
         start = (self.rank * self.maxp + self.p - 1) // self.p
         end = ((self.rank + 1) * self.maxp - 1) // self.p
         return start, end
+
+
+class NativeKeyByExchange:
+    """The same exchange through libgpuwin's own RCCL communicator (gw_exchange_*,
+    include/gpuwin.h): the C-ABI path a JVM task drives.  torch.distributed, when
+    initialized, only carries the 128-byte communicator id from rank 0 to the others
+    (a JVM job would use its own rendezvous)."""
+
+    def __init__(self, parallelism: int, rank: int, max_parallelism: int = 128, device: int = 0,
+                 uid: Optional[bytes] = None, group=None):
+        import ctypes
+        if not (1 <= parallelism <= max_parallelism):
+            raise ValueError("Maximum parallelism must not be smaller than parallelism.")
+        L = N.lib()
+        if uid is None:
+            buf = ctypes.create_string_buffer(N.EXCHANGE_ID_BYTES)
+            if rank == 0:
+                N.check(L.gw_exchange_unique_id(buf))
+            if parallelism > 1:
+                obj = [buf.raw if rank == 0 else None]
+                dist.broadcast_object_list(obj, src=0, group=group)
+                buf = ctypes.create_string_buffer(obj[0], N.EXCHANGE_ID_BYTES)
+        else:
+            buf = ctypes.create_string_buffer(uid, N.EXCHANGE_ID_BYTES)
+        h = ctypes.c_void_p()
+        rc = L.gw_exchange_create(ctypes.byref(h), parallelism, rank, buf, device, max_parallelism)
+        if rc != N.GW_OK:
+            raise N.GpuWinError(rc, "gw_exchange_create failed")
+        self._h = h
+        self.p, self.rank, self.maxp, self.device = parallelism, rank, max_parallelism, device
+
+    def close(self):
+        if getattr(self, "_h", None):
+            N.lib().gw_exchange_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc):
+        if rc != N.GW_OK:
+            msg = N.lib().gw_exchange_last_error(self._h)
+            raise N.GpuWinError(rc, msg.decode() if msg else "")
+
+    def exchange(self, keys: torch.Tensor, ts: torch.Tensor, vals: Optional[torch.Tensor] = None,
+                 key_hashes: Optional[torch.Tensor] = None, stream=None):
+        """-> (n, key_ptr, ts_ptr, value_ptr, key_hash_ptr): device pointers of the records
+        this rank owns, in the exchange's receive columns (valid until the next-but-one call);
+        feed them to GpuWindowOperator.process_batch_device_ptr."""
+        import ctypes
+        s = stream if stream is not None else torch.cuda.current_stream(keys.device).cuda_stream
+        ptr = lambda t: t.data_ptr() if t is not None else None
+        n_out = ctypes.c_int64()
+        ok, oh, ot, ov = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p()
+        self._check(N.lib().gw_exchange_batch(self._h, keys.numel(), ptr(keys), ptr(key_hashes), ptr(ts), ptr(vals),
+                                              ctypes.byref(n_out), ctypes.byref(ok), ctypes.byref(oh),
+                                              ctypes.byref(ot), ctypes.byref(ov), s))
+        return n_out.value, ok.value, ot.value, ov.value, oh.value
+
+    def combine_watermark(self, wm: int, stream=None) -> int:
+        import ctypes
+        out = ctypes.c_int64()
+        s = stream if stream is not None else torch.cuda.current_stream().cuda_stream
+        self._check(N.lib().gw_exchange_min_watermark(self._h, int(wm), ctypes.byref(out), s))
+        return out.value

@@ -319,6 +319,38 @@ int  gw_partition_device(int64_t n, const int64_t* d_key, const int32_t* d_key_h
                          int64_t* d_key_out, int64_t* d_ts_out, void* d_value_out,
                          int64_t* d_counts, void* d_scratch, void* stream);
 
+/* ---- keyBy exchange over RCCL (one process per GPU) ------------------------
+ * Replaces the network shuffle behind KeyGroupStreamPartitioner.selectChannel
+ * (flink-runtime/.../streaming/runtime/partitioner/KeyGroupStreamPartitioner.java:55-64)
+ * and RecordWriter.emit (flink-runtime/.../io/network/api/writer/RecordWriter.java:
+ * 104-110): per watermark batch, the device partition above, an RCCL all-to-all of the
+ * per-destination counts, then one grouped ncclSend/ncclRecv per column and peer over
+ * xGMI.  The watermark combine of StatusWatermarkValve.inputWatermark (minimum over the
+ * input channels, flink-streaming-java/.../watermarkstatus/StatusWatermarkValve.java:
+ * 153-185) is an RCCL all-reduce(MIN).
+ *
+ * gw_exchange_unique_id: rank 0 creates the 128-byte communicator id; the caller hands it
+ * to every rank out of band (the JobManager / a TCP rendezvous), each rank calls
+ * gw_exchange_create with it.  gw_exchange_batch: d_key/d_ts (d_value, d_key_hash may be
+ * NULL) hold this rank's n records; the *n_out records this rank owns arrive in receive
+ * columns owned by the exchange (*d_*_out; NULL for an absent input column), valid until
+ * the next-but-one call (two receive sets used in turn, so the ingest of one batch may
+ * overlap the exchange of the next on another stream).  All ranks call it for every batch
+ * (n may be 0).  It waits for the counts (one small device->host copy), then enqueues the
+ * column exchange on `stream`. */
+#define GW_EXCHANGE_ID_BYTES 128
+typedef struct gw_exchange gw_exchange;
+int  gw_exchange_unique_id(void* id);
+int  gw_exchange_create(gw_exchange** out, int32_t nranks, int32_t rank, const void* id, int32_t device,
+                        int32_t max_parallelism);
+void gw_exchange_destroy(gw_exchange* ex);
+int  gw_exchange_batch(gw_exchange* ex, int64_t n, const int64_t* d_key, const int32_t* d_key_hash,
+                       const int64_t* d_ts, const int64_t* d_value, int64_t* n_out, const int64_t** d_key_out,
+                       const int32_t** d_key_hash_out, const int64_t** d_ts_out, const int64_t** d_value_out,
+                       void* stream);
+int  gw_exchange_min_watermark(gw_exchange* ex, int64_t wm, int64_t* out, void* stream);
+const char* gw_exchange_last_error(const gw_exchange* ex);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,85 @@
+"""libgpuwin's native keyBy exchange (gw_exchange_*, RCCL) on the box's one GPU: a
+world-size-1 communicator (RCCL refuses two ranks on one device), so every record comes
+back to rank 0 -- the partition, the count all-to-all, the grouped send/receive of every
+column, the receive-set rotation and the watermark all-reduce all run; the ranks > 1 data
+path is the same code with more peers (the 2-rank product test uses gloo instead,
+tests/test_gpu_multirank.py).  The received batch, fed to the operator, fires what the
+oracle fires."""
+import numpy as np
+import pytest
+import torch
+
+from flink_amd import windowing as W
+from flink_amd.exchange import NativeKeyByExchange
+from gpu_helpers import compare, random_stream
+
+pytestmark = pytest.mark.gpu
+
+
+class _Dev:
+    """__cuda_array_interface__ view of a device pointer (the exchange's receive column)."""
+
+    def __init__(self, ptr, n, typestr):
+        self.__cuda_array_interface__ = {"shape": (n,), "typestr": typestr, "data": (ptr, False), "version": 2}
+
+
+def dev_view(ptr, n, typestr="<i8"):
+    return torch.as_tensor(_Dev(ptr, n, typestr), device="cuda")
+
+
+def test_exchange_round_trip_and_watermark():
+    ex = NativeKeyByExchange(1, 0)
+    rng = np.random.default_rng(1)
+    for n in (0, 1, 1000, 300_000, 17):
+        k = torch.from_numpy(rng.integers(-(1 << 62), 1 << 62, n).astype(np.int64)).cuda()
+        t = torch.from_numpy(rng.integers(0, 1 << 40, n).astype(np.int64)).cuda()
+        v = torch.from_numpy(rng.integers(-(1 << 40), 1 << 40, n).astype(np.int64)).cuda()
+        h = torch.from_numpy(rng.integers(-(1 << 31), (1 << 31) - 1, n).astype(np.int32)).cuda()
+        m, pk, pt, pv, ph = ex.exchange(k, t, v, key_hashes=h)
+        torch.cuda.synchronize()
+        assert m == n
+        if n:
+            # one destination: the stable partition keeps arrival order
+            assert torch.equal(dev_view(pk, n), k)
+            assert torch.equal(dev_view(pt, n), t)
+            assert torch.equal(dev_view(pv, n), v)
+            assert torch.equal(dev_view(ph, n, "<i4"), h)
+        m2, qk, qt, qv, qh = ex.exchange(k, t, None)
+        assert m2 == n and qv is None and qh is None
+        if n:
+            assert qk != pk  # the next call uses the other receive set
+    assert ex.combine_watermark(12345) == 12345
+    assert ex.combine_watermark(W.LONG_MIN) == W.LONG_MIN
+    ex.close()
+
+
+def test_exchanged_batches_fire_like_the_oracle(oracle_lib):
+    kw = dict(assigner="sliding", size=1000, slide=250, agg="sum_i64")
+    keys, ts, vals, batches = random_stream(31, 60000, 2000, 12)
+    ex = NativeKeyByExchange(1, 0)
+    op = W.GpuWindowOperator(W.SlidingEventTimeWindows.of(1000, 250), "sum_i64", capacity_hint=4096).open()
+    ora = oracle_lib.OracleOperator(oracle_lib.make_config(**kw))
+    g, o = [], []
+    s = op.stream()
+    for lo, hi, wm in batches:
+        k = torch.from_numpy(keys[lo:hi]).cuda()
+        t = torch.from_numpy(ts[lo:hi]).cuda()
+        v = torch.from_numpy(vals[lo:hi]).cuda()
+        torch.cuda.synchronize()
+        n, pk, pt, pv, _ = ex.exchange(k, t, v, stream=s)
+        op.process_batch_device_ptr(n, pk, pt, pv, stream=s)
+        op.advance_watermark(ex.combine_watermark(wm, stream=s))
+        kk, ss, ee, rr = op.drain()
+        g.append((kk, ss, ee, rr.view(np.int64)))
+        ora.process_batch(keys[lo:hi], ts[lo:hi], vals[lo:hi])
+        ora.process_watermark(wm)
+        o.append(ora.drain())
+    op.advance_watermark(W.LONG_MAX)
+    kk, ss, ee, rr = op.drain()
+    g.append((kk, ss, ee, rr.view(np.int64)))
+    ora.process_watermark(W.LONG_MAX)
+    o.append(ora.drain())
+    assert compare(g, o, False) == []
+    op.close()
+    ora.close()
+    ex.close()
