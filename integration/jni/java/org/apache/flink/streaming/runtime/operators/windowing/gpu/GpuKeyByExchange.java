@@ -1,0 +1,60 @@
+package org.apache.flink.streaming.runtime.operators.windowing.gpu;
+
+import java.nio.ByteBuffer;
+import java.nio.ByteOrder;
+
+/**
+ * The keyBy shuffle of a GPU window job through libgpuwin's RCCL communicator
+ * (include/gpuwin.h gw_exchange_*): replaces KeyGroupStreamPartitioner.selectChannel
+ * (KeyGroupStreamPartitioner.java:55-64) + RecordWriter + the Netty transport for the
+ * columns of one watermark batch, and StatusWatermarkValve's minimum over channels.
+ * One instance per subtask / GPU; every subtask calls {@link #batch} once per batch.
+ * Subtask 0 creates the communicator id ({@link #uniqueId}); the job ships it to the
+ * others (e.g. through the operator coordinator) before {@link #open}.
+ */
+public final class GpuKeyByExchange implements AutoCloseable {
+    public static final int ID_BYTES = 128;
+
+    private long handle;
+    private final ByteBuffer out = ByteBuffer.allocateDirect(5 * 8).order(ByteOrder.nativeOrder());
+
+    public static byte[] uniqueId() {
+        ByteBuffer id = ByteBuffer.allocateDirect(ID_BYTES);
+        nativeUniqueId(id);
+        byte[] b = new byte[ID_BYTES];
+        id.get(b);
+        return b;
+    }
+
+    public GpuKeyByExchange open(int parallelism, int subtask, byte[] id, int device, int maxParallelism) {
+        ByteBuffer b = ByteBuffer.allocateDirect(ID_BYTES);
+        b.put(id).flip();
+        handle = nativeCreate(parallelism, subtask, b, device, maxParallelism);
+        return this;
+    }
+
+    /** Device columns in (addresses; 0 = absent); returns {n, key, keyHash, ts, value} of the
+     *  records this subtask owns, in the exchange's receive columns (valid until the
+     *  next-but-one call), ready for GpuWindowOperator's device ingest. */
+    public long[] batch(long n, long keyPtr, long hashPtr, long tsPtr, long valuePtr, long stream) {
+        nativeBatch(handle, n, keyPtr, hashPtr, tsPtr, valuePtr, stream, out);
+        long[] r = new long[5];
+        for (int i = 0; i < 5; i++) r[i] = out.getLong(8 * i);
+        return r;
+    }
+
+    public long minWatermark(long wm, long stream) { return nativeMinWatermark(handle, wm, stream); }
+
+    @Override
+    public void close() {
+        if (handle != 0) nativeDestroy(handle);
+        handle = 0;
+    }
+
+    private static native void nativeUniqueId(ByteBuffer id);
+    private static native long nativeCreate(int nranks, int rank, ByteBuffer id, int device, int maxParallelism);
+    private static native void nativeDestroy(long h);
+    private static native void nativeBatch(long h, long n, long keyPtr, long hashPtr, long tsPtr, long valuePtr,
+                                           long stream, ByteBuffer out);
+    private static native long nativeMinWatermark(long h, long wm, long stream);
+}

@@ -41,6 +41,7 @@ import org.apache.flink.streaming.api.operators.OneInputStreamOperator;
 import org.apache.flink.streaming.api.watermark.Watermark;
 import org.apache.flink.streaming.runtime.streamrecord.StreamRecord;
 import org.apache.flink.streaming.runtime.tasks.KeyContextHandler;
+import org.apache.flink.util.OutputTag;
 
 import java.io.DataInputStream;
 import java.io.DataOutputStream;
@@ -74,6 +75,8 @@ public class GpuWindowOperator<IN>
     private transient ByteBuffer keys, ts, values, oKey, oStart, oEnd, oRes;
     private transient int n;
     private transient List<byte[]> restored;  // per-key-group blobs read in initializeState
+    private OutputTag<Tuple2<Long, Object>> lateDataTag;  // sideOutputLateData (null: count and drop)
+    private transient ByteBuffer lKey, lTs, lVal;
 
     /** inputArity: fields of the input Tuple (POSITIONAL needs 2: the Long key and the field). */
     public GpuWindowOperator(int assigner, long size, long slide, long offset, long gap, long lateness,
@@ -91,6 +94,13 @@ public class GpuWindowOperator<IN>
         this.batchCapacity = batchCapacity; this.mode = mode;
     }
 
+    /** WindowedStream.sideOutputLateData (WindowOperator.java:440-446, 587-588) for a Tuple2<Long, X>
+     *  input: skipped late elements come back as (key, value) with their timestamp. */
+    public GpuWindowOperator<IN> withLateDataOutput(OutputTag<Tuple2<Long, Object>> tag) {
+        this.lateDataTag = tag;
+        return this;
+    }
+
     @Override
     public boolean hasKeyContext() { return false; }  // no per-record setCurrentKey (RecordProcessorUtils.java:47-57)
 
@@ -101,8 +111,10 @@ public class GpuWindowOperator<IN>
         int parallelism = getRuntimeContext().getTaskInfo().getNumberOfParallelSubtasks();
         int maxP = getRuntimeContext().getTaskInfo().getMaxNumberOfParallelSubtasks();
         int device = gpuIndex();
+        final int flags = lateDataTag != null ? 64 /* GW_FLAG_LATE_SIDE_OUTPUT */ : 0;
         handle = nativeCreate(assigner, trigger, size, slide, offset, gap, lateness, agg, maxP, parallelism,
-                              subtask, device, 1L << 24, batchCapacity);
+                              subtask, device, flags, 1L << 24, batchCapacity);
+        if (lateDataTag != null) { lKey = direct(8); lTs = direct(8); lVal = direct(8); }
         keys = direct(8); ts = direct(8); values = direct(8);
         oKey = direct(8); oStart = direct(8); oEnd = direct(8); oRes = direct(8);
         if (restored != null) {  // initializeState runs before open (StreamOperator.java:139)
@@ -177,6 +189,7 @@ public class GpuWindowOperator<IN>
         // the key hash column is null: keys are Longs, whose hashCode the GPU computes
         if (n > 0) nativeIngest(handle, n, keys, null, ts, values);
         n = 0;
+        if (lateDataTag != null) emitLate();
         // CountTrigger fires on the element: count-window rows exist right after the batch
         if (assigner == GW_COUNT_TUMBLING || assigner == GW_COUNT_SLIDING) emitRows();
     }
@@ -196,6 +209,17 @@ public class GpuWindowOperator<IN>
                 // count windows: GlobalWindow.maxTimestamp() = Long.MAX_VALUE
                 long tsOut = assigner == GW_COUNT_TUMBLING || assigner == GW_COUNT_SLIDING ? Long.MAX_VALUE : end - 1;
                 output.collect(new StreamRecord<>(row, tsOut));
+            }
+            if (got < batchCapacity) break;
+        }
+    }
+
+    private void emitLate() {
+        int got;
+        while ((got = nativeDrainLate(handle, lKey, lTs, lVal, batchCapacity)) > 0) {
+            for (int i = 0; i < got; i++) {
+                Object v = doubleValue != null ? (Object) lVal.getDouble(i * 8) : lVal.getLong(i * 8);
+                output.collect(lateDataTag, new StreamRecord<>(Tuple2.of(lKey.getLong(i * 8), v), lTs.getLong(i * 8)));
             }
             if (got < batchCapacity) break;
         }
@@ -223,7 +247,7 @@ public class GpuWindowOperator<IN>
 
     private static native long nativeCreate(int assigner, int trigger, long size, long slide, long offset, long gap,
                                             long lateness, int agg, int maxParallelism, int parallelism,
-                                            int subtask, int device, long capacityHint, long maxBatch);
+                                            int subtask, int device, int flags, long capacityHint, long maxBatch);
     private static native void nativeIngest(long h, int n, ByteBuffer keys, ByteBuffer keyHashes, ByteBuffer ts,
                                             ByteBuffer values);
     private static native long nativeAdvanceWatermark(long h, long wm);
@@ -235,4 +259,7 @@ public class GpuWindowOperator<IN>
     private static native byte[] nativeSnapshot(long h, int kgLo, int kgHi);
     private static native byte[] nativeSliceKeyGroup(byte[] blob, int kg);
     private static native void nativeRestore(long h, byte[] blob);
+    private static native int nativeDrainLate(long h, ByteBuffer key, ByteBuffer ts, ByteBuffer value, int cap);
+    /** The keyBy exchange's receive columns (GpuKeyByExchange.batch) straight into the operator. */
+    static native void nativeIngestDevice(long h, long n, long keyPtr, long hashPtr, long tsPtr, long valuePtr);
 }

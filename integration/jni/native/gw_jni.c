@@ -27,9 +27,9 @@ static jint fail(JNIEnv* env, gw_handle* h, int rc) {
 JNIEXPORT jlong JNICALL CLS(nativeCreate)(JNIEnv* env, jclass c, jint assigner, jint trigger, jlong size,
                                           jlong slide, jlong offset, jlong gap, jlong lateness, jint agg,
                                           jint maxParallelism, jint parallelism, jint subtask, jint device,
-                                          jlong capacityHint, jlong maxBatch) {
+                                          jint flags, jlong capacityHint, jlong maxBatch) {
     gw_config cfg = {assigner, trigger, size, slide, offset, gap, lateness, agg, maxParallelism,
-                     parallelism, subtask, device, 0, capacityHint, maxBatch};
+                     parallelism, subtask, device, flags, capacityHint, maxBatch};
     gw_handle* h = 0;
     int rc = gw_create(&cfg, &h);
     if (rc) { fail(env, 0, rc); return 0; }
@@ -144,4 +144,80 @@ JNIEXPORT void JNICALL CLS(nativeRestore)(JNIEnv* env, jclass c, jlong h, jbyteA
     int rc = gw_restore((gw_handle*)(intptr_t)h, b, len);
     (*env)->ReleaseByteArrayElements(env, blob, b, JNI_ABORT);
     fail(env, (gw_handle*)(intptr_t)h, rc);
+}
+
+/* Device-resident ingest (gw_ingest_device): the columns the keyBy exchange delivered
+ * (GpuKeyByExchange.batch), as raw device addresses; 0 = absent column. */
+JNIEXPORT void JNICALL CLS(nativeIngestDevice)(JNIEnv* env, jclass c, jlong h, jlong n, jlong keyPtr, jlong hashPtr,
+                                               jlong tsPtr, jlong valuePtr) {
+    gw_handle* g = (gw_handle*)(intptr_t)h;
+    fail(env, g, gw_ingest_device(g, n, (const int64_t*)(intptr_t)keyPtr, (const int32_t*)(intptr_t)hashPtr,
+                                  (const int64_t*)(intptr_t)tsPtr, (const void*)(intptr_t)valuePtr, gw_stream(g)));
+}
+
+/* sideOutputLateData: up to cap late records into direct buffers (key, timestamp, value);
+ * returns how many were copied (more may remain: call again). */
+JNIEXPORT jint JNICALL CLS(nativeDrainLate)(JNIEnv* env, jclass c, jlong h, jobject key, jobject ts, jobject value,
+                                            jint cap) {
+    gw_handle* g = (gw_handle*)(intptr_t)h;
+    int64_t n = 0;
+    int rc = gw_drain_late(g, (*env)->GetDirectBufferAddress(env, key), (*env)->GetDirectBufferAddress(env, ts),
+                           value ? (*env)->GetDirectBufferAddress(env, value) : 0, cap, &n);
+    fail(env, g, rc);
+    return (jint)n;
+}
+
+/* ---- GpuKeyByExchange: the keyBy shuffle through libgpuwin's RCCL communicator ---- */
+#define XCLS(n) Java_org_apache_flink_streaming_runtime_operators_windowing_gpu_GpuKeyByExchange_##n
+
+static jint fail_ex(JNIEnv* env, gw_exchange* x, int rc) {
+    if (rc < 0) {
+        jclass ex = (*env)->FindClass(env, rc == GW_E_INVALID ? "java/lang/IllegalArgumentException"
+                                                             : "java/lang/RuntimeException");
+        (*env)->ThrowNew(env, ex, x ? gw_exchange_last_error(x) : "gw_exchange: invalid argument or device error");
+    }
+    return rc;
+}
+
+/* Rank 0: the communicator id into a direct buffer of GW_EXCHANGE_ID_BYTES bytes (shipped to
+ * the other subtasks through the job's own channel). */
+JNIEXPORT void JNICALL XCLS(nativeUniqueId)(JNIEnv* env, jclass c, jobject id) {
+    fail_ex(env, 0, gw_exchange_unique_id((*env)->GetDirectBufferAddress(env, id)));
+}
+
+JNIEXPORT jlong JNICALL XCLS(nativeCreate)(JNIEnv* env, jclass c, jint nranks, jint rank, jobject id, jint device,
+                                           jint maxParallelism) {
+    gw_exchange* x = 0;
+    int rc = gw_exchange_create(&x, nranks, rank, (*env)->GetDirectBufferAddress(env, id), device, maxParallelism);
+    if (rc) { fail_ex(env, 0, rc); return 0; }
+    return (jlong)(intptr_t)x;
+}
+
+JNIEXPORT void JNICALL XCLS(nativeDestroy)(JNIEnv* env, jclass c, jlong x) {
+    gw_exchange_destroy((gw_exchange*)(intptr_t)x);
+}
+
+/* One batch: device columns in (raw addresses, 0 = absent); `out` is a direct buffer of 5
+ * longs receiving {records received, key, key hash, timestamp, value} device addresses. */
+JNIEXPORT void JNICALL XCLS(nativeBatch)(JNIEnv* env, jclass c, jlong x, jlong n, jlong keyPtr, jlong hashPtr,
+                                         jlong tsPtr, jlong valuePtr, jlong stream, jobject out) {
+    int64_t* o = (*env)->GetDirectBufferAddress(env, out);
+    const int64_t *k = 0, *t = 0, *v = 0;
+    const int32_t* kh = 0;
+    int rc = gw_exchange_batch((gw_exchange*)(intptr_t)x, n, (const int64_t*)(intptr_t)keyPtr,
+                               (const int32_t*)(intptr_t)hashPtr, (const int64_t*)(intptr_t)tsPtr,
+                               (const int64_t*)(intptr_t)valuePtr, &o[0], &k, &kh, &t, &v, (void*)(intptr_t)stream);
+    o[1] = (int64_t)(intptr_t)k;
+    o[2] = (int64_t)(intptr_t)kh;
+    o[3] = (int64_t)(intptr_t)t;
+    o[4] = (int64_t)(intptr_t)v;
+    fail_ex(env, (gw_exchange*)(intptr_t)x, rc);
+}
+
+/* StatusWatermarkValve: the minimum of the subtasks' watermarks. */
+JNIEXPORT jlong JNICALL XCLS(nativeMinWatermark)(JNIEnv* env, jclass c, jlong x, jlong wm, jlong stream) {
+    int64_t out = wm;
+    fail_ex(env, (gw_exchange*)(intptr_t)x,
+            gw_exchange_min_watermark((gw_exchange*)(intptr_t)x, wm, &out, (void*)(intptr_t)stream));
+    return out;
 }

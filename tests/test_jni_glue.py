@@ -42,7 +42,7 @@ def jni(tmp_path_factory):
     getattr(L, CLS + "nativeSliceKeyGroup").argtypes = [p, p, p, ctypes.c_int32]
     f = getattr(L, CLS + "nativeCreate")
     f.restype = ctypes.c_int64
-    f.argtypes = [p, p] + [ctypes.c_int32, ctypes.c_int32] + [ctypes.c_int64] * 5 + [ctypes.c_int32] * 5 + \
+    f.argtypes = [p, p] + [ctypes.c_int32, ctypes.c_int32] + [ctypes.c_int64] * 5 + [ctypes.c_int32] * 6 + \
         [ctypes.c_int64] * 2
     return L
 
@@ -76,6 +76,25 @@ def test_native_create_maps_status_to_java_exceptions(jni):
     env = jni.fake_env()
     create = getattr(jni, CLS + "nativeCreate")
     # tumbling size 0: invalid in Flink (IllegalArgumentException)
-    assert create(env, None, 0, 0, 0, 0, 0, 0, 0, 1, 128, 1, 0, 0, 1 << 16, 1 << 16) == 0
+    assert create(env, None, 0, 0, 0, 0, 0, 0, 0, 1, 128, 1, 0, 0, 0, 1 << 16, 1 << 16) == 0
     exc = exception(jni)
     assert exc is not None and exc[0] == "java/lang/IllegalArgumentException" and "abs(offset) < size" in exc[1]
+
+
+XCLS = "Java_org_apache_flink_streaming_runtime_operators_windowing_gpu_GpuKeyByExchange_"
+
+
+def test_exchange_glue_maps_invalid_arguments(jni):
+    """GpuKeyByExchange.nativeCreate with an impossible layout (rank outside the ranks, or
+    max parallelism below the parallelism) fails before touching a device and raises
+    IllegalArgumentException, as KeyGroupRangeAssignment's checks do."""
+    p = ctypes.c_void_p
+    create = getattr(jni, XCLS + "nativeCreate")
+    create.restype = ctypes.c_int64
+    create.argtypes = [p, p, ctypes.c_int32, ctypes.c_int32, p, ctypes.c_int32, ctypes.c_int32]
+    env = jni.fake_env()
+    idbuf = ctypes.create_string_buffer(128)
+    for nranks, rank, maxp in ((2, 2, 128), (0, 0, 128), (4, 0, 2)):
+        assert create(env, None, nranks, rank, ctypes.cast(idbuf, p), 0, maxp) == 0
+        exc = exception(jni)
+        assert exc is not None and exc[0] == "java/lang/IllegalArgumentException"
