@@ -501,9 +501,9 @@ __global__ void __launch_bounds__(kPartThreads) k_rgn_p1(IngestArgs a) {
         const int64_t i = lo + it * kPartThreads + threadIdx.x;
         key[it] = 0; ts[it] = 0; val[it] = 0;
         if (i < hi) {
-            key[it] = a.key[i];
-            ts[it] = a.ts[i];
-            if (a.val) val[it] = a.val[i];
+            key[it] = __builtin_nontemporal_load(a.key + i);  // read once: keep it out of the caches
+            ts[it] = __builtin_nontemporal_load(a.ts + i);
+            if (a.val) val[it] = __builtin_nontemporal_load(a.val + i);
         }
     }
 #pragma unroll
@@ -558,9 +558,9 @@ __global__ void __launch_bounds__(kPartThreads) k_rgn_p1(IngestArgs a) {
     const int64_t tile = a.tile0 + g;
     const int64_t base = tile * kPartTile;
     for (uint32_t j = threadIdx.x; j < cnt; j += blockDim.x) {
-        a.p1_key[base + j] = s.k[j];
+        __builtin_nontemporal_store((int64_t)s.k[j], a.p1_key + base + j);  // read back a flush later
         if constexpr (C) {
-            if constexpr (ACC) reinterpret_cast<int32_t*>(a.p1_a0)[base + j] = s_v32[j];
+            if constexpr (ACC) __builtin_nontemporal_store(s_v32[j], reinterpret_cast<int32_t*>(a.p1_a0) + base + j);
         } else {
             a.p1_a0[base + j] = s.a0[j];
             if constexpr (AV) a.p1_a1[base + j] = s.a1[j];
@@ -767,9 +767,9 @@ __global__ void __launch_bounds__(kPartThreads) k_rgn_p2(IngestArgs a) {
         const int64_t base = out0 + e0;
         const int64_t rnd = rnd0 + e0 / kPartTile;
         for (uint32_t jj = threadIdx.x; jj < e1 - e0; jj += blockDim.x) {
-            a.e_key[base + jj] = s.k[jj];
+            __builtin_nontemporal_store((int64_t)s.k[jj], a.e_key + base + jj);
             if constexpr (C) {
-                if constexpr (ACC) reinterpret_cast<int32_t*>(a.e_a0)[base + jj] = s_v32[jj];
+                if constexpr (ACC) __builtin_nontemporal_store(s_v32[jj], reinterpret_cast<int32_t*>(a.e_a0) + base + jj);
             } else {
                 a.e_a0[base + jj] = s.a0[jj];
                 if constexpr (AV) a.e_a1[base + jj] = s.a1[jj];
@@ -1361,9 +1361,6 @@ __global__ void __launch_bounds__(256) k_deferred_min(const int64_t* pane, int64
 // with the identity unconditionally (full-line coalesced stores).
 template <int AGG>
 __global__ void __launch_bounds__(256) k_fire(FireArgs a) {
-    // kFireU slots per thread per step: their key / presence loads, then their cell loads,
-    // are issued together (a sweep is latency-bound with one dependent chain per lane)
-    constexpr int kFireU = 4;
     __shared__ RowStage rs;
     const int64_t nslots = a.t.cap + 1;
     const int64_t id0 = identity0(AGG);
@@ -1371,92 +1368,70 @@ __global__ void __launch_bounds__(256) k_fire(FireArgs a) {
     if (threadIdx.x == 0) rs.cnt = 0;
     if (blockIdx.x == 0 && threadIdx.x < kShards) atomicAnd(&a.st->sh[threadIdx.x].occ, ~a.rmask);
     __syncthreads();
-    const int64_t step = (int64_t)blockDim.x * kFireU;
-    const int64_t chunk = ((nslots + gridDim.x - 1) / gridDim.x + step - 1) / step * step;
+    const int64_t chunk = ((nslots + gridDim.x - 1) / gridDim.x + 255) / 256 * 256;
     const int64_t c0 = blockIdx.x * chunk, c1 = min(nslots, c0 + chunk);
-    for (int64_t base = c0; base < c1; base += step) {
-        int64_t key[kFireU], oi[kFireU];
-        uint64_t mask[kFireU];
-#pragma unroll
-        for (int u = 0; u < kFireU; ++u) {
-            const int64_t g = base + u * (int64_t)blockDim.x + threadIdx.x;
-            key[u] = kEmptyKey;
-            mask[u] = 0;
-            oi[u] = -1;  // this key's next restored-window entry
-            if (g < c1) {
-                key[u] = *pt_key(a.t, g);
-                mask[u] = presence<AGG>(a.t, g);
-                if (a.ov.head) oi[u] = a.ov.head[g];
-            }
+    for (int64_t base = c0; base < c1; base += blockDim.x) {
+        const int64_t g = base + threadIdx.x;
+        int64_t key = kEmptyKey;
+        uint64_t mask = 0;
+        const bool live = g < c1;
+        int64_t oi = -1;  // this key's next restored-window entry
+        if (live) {
+            key = *pt_key(a.t, g);
+            mask = presence<AGG>(a.t, g);
+            if (a.ov.head) oi = a.ov.head[g];
         }
         for (int w = 0; w < a.nwin; ++w) {
-            const bool flush = rs.cnt + kFireU * blockDim.x > kRowStage;  // uniform: read before any append
+            const bool flush = rs.cnt + blockDim.x > kRowStage;  // uniform: read before any append
             __syncthreads();
             if (flush) stage_flush(rs, &a.st->rows, a.o_key, a.o_start, a.o_end, a.o_res);
-            int64_t r0[kFireU], r1[kFireU];
-            bool emit[kFireU];
-#pragma unroll
-            for (int u = 0; u < kFireU; ++u) {
-                const int64_t g = base + u * (int64_t)blockDim.x + threadIdx.x;
-                uint64_t m = mask[u] & a.wmask[w];
-                bool ov_hit = false;
-                int64_t o0 = 0, o1 = 0;
-                if (oi[u] >= 0) {  // restored state of (key, window): fires with its timer or with new records
-                    const int64_t kk = a.k0 + w;
-                    int64_t x = oi[u];
-                    while (x < a.ov.n && a.ov.key[x] == key[u] && a.ov.k[x] < kk) ++x;
-                    if (x < a.ov.n && a.ov.key[x] == key[u] && a.ov.k[x] == kk) {
-                        const uint32_t f = a.ov.flags[x];
-                        if (!(f & kOvDead) && (m || (f & kOvTimer))) {
-                            ov_hit = true;
-                            o0 = a.ov.a0[x];
-                            o1 = a.ov.a1[x];
-                            a.ov.flags[x] = a.ov.purge ? kOvDead : (f & ~kOvTimer);
-                        }
-                    } else if (x >= a.ov.n || a.ov.key[x] != key[u]) {
-                        x = -1;
+            uint64_t m = mask & a.wmask[w];
+            bool ov_hit = false;
+            int64_t o0 = 0, o1 = 0;
+            if (oi >= 0) {  // restored state of (key, window): fires with its timer or with new records
+                const int64_t kk = a.k0 + w;
+                while (oi < a.ov.n && a.ov.key[oi] == key && a.ov.k[oi] < kk) ++oi;
+                if (oi < a.ov.n && a.ov.key[oi] == key && a.ov.k[oi] == kk) {
+                    const uint32_t f = a.ov.flags[oi];
+                    if (!(f & kOvDead) && (m || (f & kOvTimer))) {
+                        ov_hit = true;
+                        o0 = a.ov.a0[oi];
+                        o1 = a.ov.a1[oi];
+                        a.ov.flags[oi] = a.ov.purge ? kOvDead : (f & ~kOvTimer);
                     }
-                    oi[u] = x;
+                } else if (oi >= a.ov.n || a.ov.key[oi] != key) {
+                    oi = -1;
                 }
-                emit[u] = m || ov_hit;
-                r0[u] = id0;
-                r1[u] = 0;
+            }
+            if (m || ov_hit) {
+                int64_t r0 = id0, r1 = 0;
                 while (m) {
                     const int pos = __ffsll((long long)m) - 1;
                     m &= m - 1;
                     const int64_t* c = pt_cell(a.t, g, pos);
-                    fold_cell(AGG, r0[u], r1[u], c[0], W == 2 ? c[1] : 0);
+                    fold_cell(AGG, r0, r1, c[0], W == 2 ? c[1] : 0);
                 }
-                if (ov_hit) fold_cell(AGG, r0[u], r1[u], o0, o1);
-            }
-            const int64_t st = a.start0 + (int64_t)w * a.slide;
-#pragma unroll
-            for (int u = 0; u < kFireU; ++u) {
-                if (!emit[u]) continue;
+                if (ov_hit) fold_cell(AGG, r0, r1, o0, o1);
                 const unsigned j = atomicAdd(&rs.cnt, 1u);
-                rs.k[j] = key[u];
+                const int64_t st = a.start0 + (int64_t)w * a.slide;
+                rs.k[j] = key;
                 rs.s[j] = st;
                 rs.e[j] = st + a.size;
-                rs.r[j] = cell_result(AGG, r0[u], r1[u]);
+                rs.r[j] = cell_result(AGG, r0, r1);
             }
             __syncthreads();
         }
-        if (a.rmask) {
-#pragma unroll
-            for (int u = 0; u < kFireU; ++u) {
-                const int64_t g = base + u * (int64_t)blockDim.x + threadIdx.x;
-                if (g >= c1) continue;
-                if constexpr (uses_mask<AGG>()) {
-                    if (mask[u] & a.rmask) pt_mask_put(a.t, g, mask[u] & ~a.rmask);
-                }
-                uint64_t m = a.rmask;
-                while (m) {
-                    const int pos = __ffsll((long long)m) - 1;
-                    m &= m - 1;
-                    int64_t* c = pt_cell(a.t, g, pos);
-                    c[0] = id0;
-                    if (W == 2) c[1] = 0;
-                }
+        if (live && a.rmask) {
+            if constexpr (uses_mask<AGG>()) {
+                if (mask & a.rmask) pt_mask_put(a.t, g, mask & ~a.rmask);
+            }
+            uint64_t m = a.rmask;
+            while (m) {
+                const int pos = __ffsll((long long)m) - 1;
+                m &= m - 1;
+                int64_t* c = pt_cell(a.t, g, pos);
+                c[0] = id0;
+                if (W == 2) c[1] = 0;
             }
         }
     }
@@ -1769,8 +1744,7 @@ hipError_t launch_deferred_min(const int64_t* pane, int64_t n, DevStatus* st, hi
 }
 
 hipError_t launch_fire(const FireArgs& a, hipStream_t s) {
-    // 5 workgroups per CU fit (32 KB row stage each): one resident wave of blocks
-    const int fg = (int)std::min<int64_t>(5 * 256, std::max<int64_t>(1, (a.t.cap + 1 + 1023) / 1024));
+    const int fg = (int)std::min<int64_t>(1024, std::max<int64_t>(1, (a.t.cap + 1 + 255) / 256));
 #define L(A) hipLaunchKernelGGL(k_fire<A>, dim3(fg), dim3(256), 0, s, a)
     GW_AGG_SWITCH(a.t.agg, L);
 #undef L
