@@ -25,6 +25,7 @@
 #include "gw_sort.h"
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <cstdio>
 #include <vector>
@@ -65,6 +66,7 @@ struct SegArgs {
     int64_t n_runs;
     uint32_t* retry;        // wide pass: runs that did not fit K2 (append at st->overflow)
     DevStatus* st;
+    int gshift;             // records are grouped by slot >> gshift (the sort skips the low bits)
 };
 
 struct Sess {
@@ -232,18 +234,18 @@ __device__ __forceinline__ bool add_element(const SegArgs& a, const SessList& l,
 // outgrows the lane, or the key is already in the wide table, does it go to the wide pass.
 // Without allowed lateness and side output a replay has no effects beyond the slot, so
 // the dry replay is the real one.
+// One key's records among the group [i, j) (those whose slot is `slot`, L of them, the first
+// at i), in arrival order.
 template <int AGG>
-__device__ __forceinline__ void seg_run(const SegArgs& a, const SessList& l, int64_t i, unsigned long long& late,
-                                        unsigned long long& merges, unsigned long long& flags) {
-    const uint32_t slot = a.slot[i];
-    int64_t j = i + 1;
-    while (j < a.n && a.slot[j] == slot) ++j;
+__device__ __forceinline__ void seg_slot(const SegArgs& a, const SessList& l, int64_t i, int64_t j, uint32_t slot,
+                                         int64_t L, unsigned long long& late, unsigned long long& merges,
+                                         unsigned long long& flags) {
     int64_t* sp = slot_ptr(a.t, (int64_t)slot);
     const int64_t w1 = sp[1];
     const int SW = a.t.words;
     const int64_t key = sp[0];  // the sentinel slot's key word is Long.MIN_VALUE, its key
     bool ok = !slot_big(w1);
-    bool dry = ok && slot_cnt(w1) + (j - i) > kLaneSess;  // could outgrow the lane
+    bool dry = ok && slot_cnt(w1) + L > kLaneSess;  // could outgrow the lane
     const bool effects = a.lateness > 0 || a.lo_key;
     const unsigned long long l0 = late, m0 = merges;
     int cnt = 0;
@@ -254,7 +256,7 @@ __device__ __forceinline__ void seg_run(const SegArgs& a, const SessList& l, int
             sl_put(l, q, Sess{x[0], x[1], x[2], SW == 4 ? x[3] : 0, (int64_t)slot_fired(w1, q)});
         }
         for (int64_t r = i; r < j && ok; ++r)
-            ok = add_element<AGG>(a, l, cnt, kLaneSess, key, a.perm[r], late, merges, flags, dry);
+            if (a.slot[r] == slot) ok = add_element<AGG>(a, l, cnt, kLaneSess, key, a.perm[r], late, merges, flags, dry);
         if (!ok || !dry || !effects) break;
         dry = false;
         late = l0;
@@ -264,7 +266,7 @@ __device__ __forceinline__ void seg_run(const SegArgs& a, const SessList& l, int
         late = l0;
         merges = m0;
         const unsigned long long at = atomicAdd(&a.st->overflow, 1ull);
-        a.punt[at] = (uint32_t)i;
+        a.punt[at] = (uint32_t)i;  // the wide pass replays this slot's records from i to the group's end
         return;
     }
     if (cnt <= a.t.ring) {
@@ -294,9 +296,44 @@ __device__ __forceinline__ void seg_run(const SegArgs& a, const SessList& l, int
     }
 }
 
-// Each wave takes kSegChunk consecutive records, compacts their run heads into LDS with
-// ballots, and replays the heads 64 at a time: every lane owns a run (about one record in
-// three starts a run), not one lane per record.
+// Main pass: one thread per key's run.  The radix sort groups records by slot >> gshift
+// (it skips the low bits: one pass fewer on large tables), so a group interleaves the runs
+// of at most 2^gshift slots, each in arrival order.  A work item is the first record of a
+// slot in its group; its thread replays that slot's records of the group against the
+// key's inline sessions in its LDS lane.  A run that could need more than kLaneSess
+// sessions is first replayed dry (no rows, no side output); only if the list really
+// outgrows the lane, or the key is already in the wide table, does it go to the wide
+// pass.  Without allowed lateness and side output a replay has no effects beyond the
+// slot, so the dry replay is the real one.
+__device__ __forceinline__ bool seg_is_item(const SegArgs& a, int64_t i) {
+    if (i >= a.n) return false;
+    if (i == 0) return true;
+    const uint32_t slot = a.slot[i], grp = slot >> a.gshift;
+    if ((a.slot[i - 1] >> a.gshift) != grp) return true;  // a group head
+    for (int64_t q = i - 1; q >= 0; --q) {  // an earlier record of the slot in the group?
+        const uint32_t x = a.slot[q];
+        if (x == slot) return false;
+        if ((x >> a.gshift) != grp) break;
+    }
+    return true;
+}
+
+template <int AGG>
+__device__ __forceinline__ void seg_run(const SegArgs& a, const SessList& l, int64_t i, unsigned long long& late,
+                                        unsigned long long& merges, unsigned long long& flags) {
+    const uint32_t slot = a.slot[i], grp = slot >> a.gshift;
+    int64_t j = i + 1, L = 1;
+    for (; j < a.n; ++j) {
+        const uint32_t x = a.slot[j];
+        if ((x >> a.gshift) != grp) break;
+        L += x == slot;
+    }
+    seg_slot<AGG>(a, l, i, j, slot, L, late, merges, flags);
+}
+
+// Each wave takes kSegChunk consecutive records, compacts their work items into LDS with
+// ballots, and replays them 64 at a time: every lane owns a run (about one record in
+// three starts one), not one lane per record.
 constexpr int kSegChunk = 512;
 template <int AGG>
 __global__ void __launch_bounds__(kSegThreads) k_sess_segment(SegArgs a) {
@@ -309,7 +346,7 @@ __global__ void __launch_bounds__(kSegThreads) k_sess_segment(SegArgs a) {
     int nh = 0;
     for (int c = 0; c < kSegChunk; c += 64) {
         const int64_t i = base + c + ln;
-        const bool h = i < a.n && (i == 0 || a.slot[i - 1] != a.slot[i]);
+        const bool h = seg_is_item(a, i);
         const uint64_t b = __ballot(h);
         if (h) heads[w][nh + __popcll(b & ((1ull << ln) - 1ull))] = (uint32_t)(i - base);
         nh += __popcll(b);
@@ -371,13 +408,16 @@ __global__ void __launch_bounds__(256) k_sess_wide(SegArgs a) {
     unsigned long long late = 0, merges = 0, flags = 0, ins = 0;
     for (int64_t r0 = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; r0 < a.n_runs;
          r0 += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t i = a.runs[r0];
+        const int64_t i = a.runs[r0];  // the slot's first record in its group
         const uint32_t slot = a.slot[i];
-        int64_t j = i + 1, hi = a.n;  // sorted by slot: the run ends at the first other slot
+        const uint32_t grp = slot >> a.gshift;
+        int64_t j = i + 1, hi = a.n;  // sorted by group: the group ends at the first other group
         while (j < hi) {
             const int64_t mid = (j + hi) >> 1;
-            if (a.slot[mid] == slot) j = mid + 1; else hi = mid;
+            if ((a.slot[mid] >> a.gshift) == grp) j = mid + 1; else hi = mid;
         }
+        int64_t L = 0;
+        for (int64_t q = i; q < j; ++q) L += a.slot[q] == slot;
         int64_t* sp = slot_ptr(a.t, (int64_t)slot);
         const int64_t key = (int64_t)slot == a.t.cap ? kEmptyKey : sp[0];
         bool inserted;
@@ -403,14 +443,15 @@ __global__ void __launch_bounds__(256) k_sess_wide(SegArgs a) {
             due_of(a.t)[slot] = INT64_MAX;
         }
         int cnt = (int)d[1];
-        if (cnt + (j - i) > a.w.ring) {
-            atomicMax(&a.st->pad[1], (unsigned long long)(cnt + (j - i)));
+        if (cnt + L > a.w.ring) {
+            atomicMax(&a.st->pad[1], (unsigned long long)(cnt + L));
             const unsigned long long at = atomicAdd(&a.st->overflow, 1ull);
             a.retry[at] = (uint32_t)i;
             continue;
         }
         const SessList l{d + 2, 1, kWideWords};
-        for (int64_t r = i; r < j; ++r) add_element<AGG>(a, l, cnt, a.w.ring, key, a.perm[r], late, merges, flags);
+        for (int64_t r = i; r < j; ++r)
+            if (a.slot[r] == slot) add_element<AGG>(a, l, cnt, a.w.ring, key, a.perm[r], late, merges, flags);
         d[1] = cnt;
         due_of(a.w)[g2] = wide_due(d, a.lateness);
     }
@@ -996,6 +1037,7 @@ struct SessionState {
     int64_t* mig = nullptr;  // migration lists (main pass -> wide table)
     int64_t* rec = nullptr;  // sessions: (ts, value) per record
     bool fresh = false;      // h_st matches the device (nothing launched since the last refresh)
+    int gshift = 0;          // sessions: the last sort grouped records by slot >> gshift
     uint32_t* due_list = nullptr;  // fire sweep: main-table slots with something due
     int64_t due_list_cap = 0;
     int64_t* cnt_plan = nullptr;  // count windows: long-run plan rows + pane / firing offsets
@@ -1189,9 +1231,17 @@ static int sort_by_slot(SessionState* s, int64_t n, int64_t cap, const uint32_t*
                         std::string& err) {
     int bits = 1;
     while (bits < 32 && ((uint64_t)(cap + 1) >> bits)) ++bits;
+    // sessions may group by slot >> gshift so that the sort covers fewer bits (passes of 8);
+    // the replay then separates the <= 2^gshift slots of a group (count windows need whole
+    // slots).  Measured on 12.5M keys (26 slot bits): 24-bit groups save 80 us of sort but
+    // cost 180 us of replay, so the default sorts whole slots; GW_SESSION_SORT_BITS sets
+    // the cap (the tests force 4-bit groups)
+    int sort_bits = 32;
+    if (const char* e = getenv("GW_SESSION_SORT_BITS")) sort_bits = std::max(1, atoi(e));
+    s->gshift = s->count_mode ? 0 : std::min(4, std::max(0, bits - sort_bits));
     rocprim::double_buffer<uint32_t> kb(s->slot[0], s->slot[1]), vb(s->perm[0], s->perm[1]);
     size_t bytes = s->sort_tmp_bytes;
-    SCHECK(rocprim::radix_sort_pairs(s->sort_tmp, bytes, kb, vb, (size_t)n, 0, bits, s->stream));
+    SCHECK(rocprim::radix_sort_pairs(s->sort_tmp, bytes, kb, vb, (size_t)n, s->gshift, bits, s->stream));
     *sk = kb.current();
     *sp = vb.current();
     return GW_OK;
@@ -1409,6 +1459,7 @@ int session_ingest(SessionState* s, int64_t n, const int64_t* key, const int64_t
     SegArgs a{};
     if ((rc = group_records(s, n, key, ts, val, &a.slot, &a.perm, err))) return rc;
     a.rec = s->rec;
+    a.gshift = s->gshift;
     a.n = n;
     a.key = key;
     a.ts = ts;
