@@ -9,7 +9,8 @@ import ctypes
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libgpuwin.so")
+# GW_LIB_PATH: an experiment build of the same library (flink_amd.build --define ... --out ...)
+LIB_PATH = os.environ.get("GW_LIB_PATH") or os.path.join(HERE, "libgpuwin.so")
 
 GW_OK = 0
 ERRORS = {

@@ -39,44 +39,48 @@ def _stale(target, deps):
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def _compile(src, force):
-    obj = os.path.join(OBJDIR, src + ".o")
+def _compile(src, force, defines=(), objdir=OBJDIR):
+    obj = os.path.join(objdir, src + ".o")
     deps = [os.path.join(CSRC, src)] + _headers()
     if not force and not _stale(obj, deps):
         return obj, None
-    cmd = [HIPCC, *CFLAGS, "-x", "hip", "-c", os.path.join(CSRC, src), "-o", obj]
+    cmd = [HIPCC, *CFLAGS, *[f"-D{d}" for d in defines], "-x", "hip", "-c", os.path.join(CSRC, src), "-o", obj]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         return obj, f"{' '.join(cmd)}\n{r.stdout}\n{r.stderr}"
     return obj, None
 
 
-def build(force: bool = False, jobs: int = 4, verbose: bool = False) -> str:
-    os.makedirs(OBJDIR, exist_ok=True)
+def build(force: bool = False, jobs: int = 4, verbose: bool = False, defines=(), out: str = OUT) -> str:
+    """defines/out: experiment builds (-D knobs into another .so, loaded through GW_LIB_PATH)."""
+    objdir = OBJDIR if not defines else os.path.join(OBJDIR, "exp_" + os.path.basename(out).replace(".so", ""))
+    os.makedirs(objdir, exist_ok=True)
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
-        results = list(ex.map(lambda s: _compile(s, force), SOURCES))
+        results = list(ex.map(lambda s: _compile(s, force or bool(defines), defines, objdir), SOURCES))
     errors = [e for _, e in results if e]
     if errors:
         raise RuntimeError("hipcc failed:\n" + "\n".join(errors))
     objs = [o for o, _ in results]
-    if force or _stale(OUT, objs):
-        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", OUT, *objs, f"-L{ROCM_LIB}", "-lrccl",
+    if force or defines or _stale(out, objs):
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out, *objs, f"-L{ROCM_LIB}", "-lrccl",
                f"-Wl,-rpath,{ROCM_LIB}"]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
     if verbose:
-        print(OUT)
-    return OUT
+        print(out)
+    return out
 
 
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--force", action="store_true")
     ap.add_argument("--jobs", type=int, default=4)
+    ap.add_argument("--define", action="append", default=[], help="experiment build: -D knob (needs --out)")
+    ap.add_argument("--out", default=OUT)
     args = ap.parse_args()
     try:
-        build(args.force, args.jobs, verbose=True)
+        build(args.force, args.jobs, verbose=True, defines=args.define, out=os.path.abspath(args.out))
     except RuntimeError as e:
         print(e, file=sys.stderr)
         sys.exit(1)

@@ -31,6 +31,7 @@
 //           atomics on the state; every HBM access is a contiguous stream.
 //   direct  (small batches)  k_ingest: one device-scope atomic per record.
 //   preagg  (few keys)       k_ingest_preagg: LDS combine per (slot, pane), then atomics.
+#include <type_traits>
 #include "gw_kernels.h"
 
 #include <algorithm>
@@ -476,8 +477,20 @@ __global__ void __launch_bounds__(256) k_publish_status(const DevStatus* st, Dev
 }
 
 // P1: one 4096-record tile of the batch -> buffer tile a.tile0 + blockIdx.x.
+// GW_P1_WAVES / GW_APPLY_WAVES: minimum waves per SIMD the register allocation must allow
+// (6 = 3 workgroups of 512 per CU, as many as the LDS allows, at <= 80 VGPRs)
+#ifdef GW_P1_WAVES
+#define GW_P1_ATTR __attribute__((amdgpu_waves_per_eu(GW_P1_WAVES)))
+#else
+#define GW_P1_ATTR
+#endif
+#ifdef GW_APPLY_WAVES
+#define GW_APPLY_ATTR __attribute__((amdgpu_waves_per_eu(GW_APPLY_WAVES)))
+#else
+#define GW_APPLY_ATTR
+#endif
 template <int AGG, bool CMP>
-__global__ void __launch_bounds__(kPartThreads) k_rgn_p1(IngestArgs a) {
+__global__ void __launch_bounds__(kPartThreads) GW_P1_ATTR k_rgn_p1(IngestArgs a) {
     constexpr bool C = CMP && cmp_agg<AGG>();
     constexpr bool AV = !C && (AGG == GW_AVG_I64 || AGG == GW_AVG_F64);
     constexpr bool ACC = !(C && AGG == GW_COUNT);  // COUNT records carry no value
@@ -493,9 +506,13 @@ __global__ void __launch_bounds__(kPartThreads) k_rgn_p1(IngestArgs a) {
     if (threadIdx.x == 0) s_occ = 0;
     __syncthreads();
     unsigned long long late = 0, flags = 0, occ = 0, wide = 0;
-    int64_t key[kPartItems], ts[kPartItems], val[kPartItems], c0[kPartItems], c1[kPartItems];
-    uint32_t pos[kPartItems], rank[kPartItems];
-    int bk[kPartItems];
+    // Registers per record after classification: the key (compact: the hash word), the
+    // value (32 bits for compact records), and bucket << 16 | rank in one word (~0: none).
+    using V0 = std::conditional_t<C, int32_t, int64_t>;
+    int64_t key[kPartItems], ts[kPartItems], val[kPartItems];
+    V0 c0[kPartItems];
+    int64_t c1[kPartItems];
+    uint32_t pos[kPartItems], br[kPartItems];
 #pragma unroll
     for (int it = 0; it < kPartItems; ++it) {  // all loads in flight first
         const int64_t i = lo + it * kPartThreads + threadIdx.x;
@@ -509,30 +526,34 @@ __global__ void __launch_bounds__(kPartThreads) k_rgn_p1(IngestArgs a) {
 #pragma unroll
     for (int it = 0; it < kPartItems; ++it) {
         const int64_t i = lo + it * kPartThreads + threadIdx.x;
-        bk[it] = -1;
-        c0[it] = 0; c1[it] = 0; pos[it] = 0;
+        int bk = -1;
+        int64_t v0 = 0, v1 = 0;
+        uint32_t ps = 0;
         int st = REC_SKIP;
         int64_t pane = 0;
-        if (i < hi) st = classify<AGG>(a, ts[it], val[it], pos[it], pane, c0[it], c1[it], late, flags);
-        if (C && ACC && st == REC_RING && (c0[it] < INT32_MIN || c0[it] > INT32_MAX)) {
+        if (i < hi) st = classify<AGG>(a, ts[it], val[it], ps, pane, v0, v1, late, flags);
+        if (C && ACC && st == REC_RING && (v0 < INT32_MIN || v0 > INT32_MAX)) {
             st = REC_DEFER;  // beyond the compact record's 32-bit value: exact via the deferred list
             wide++;
         }
         if (st == REC_RING) {
-            occ |= 1ull << pos[it];
+            occ |= 1ull << ps;
             if (key[it] == kEmptyKey) {  // sentinel slot: rare, straight atomics
-                cell_atomic<AGG>(pt_cell(a.t, a.t.cap, pos[it]), c0[it], c1[it]);
-                mask_set<AGG>(a.t, a.t.cap, pos[it]);
+                cell_atomic<AGG>(pt_cell(a.t, a.t.cap, ps), v0, v1);
+                mask_set<AGG>(a.t, a.t.cap, ps);
             } else {
                 const uint64_t h = slot_hash(key[it]);
-                bk[it] = (int)(pt_key_region(a.t, h) >> a.d2_bits);
-                if constexpr (C) key[it] = (int64_t)cmp_pack(h, pos[it], a.d1_bits);  // key -> word
+                bk = (int)(pt_key_region(a.t, h) >> a.d2_bits);
+                if constexpr (C) key[it] = (int64_t)cmp_pack(h, ps, a.d1_bits);  // key -> word
             }
         }
-        defer_write(a, st == REC_DEFER, key[it], pane, c0[it], c1[it]);
-        refire_write(a, st == REC_REFIRE, key[it], pane, c0[it], c1[it], i);
+        defer_write(a, st == REC_DEFER, key[it], pane, v0, v1);
+        refire_write(a, st == REC_REFIRE, key[it], pane, v0, v1, i);
         if (a.lo_key) late_write(a, st == REC_LATE, key[it], i);
-        if (bk[it] >= 0) rank[it] = atomicAdd(&lh[bk[it]], 1u);
+        c0[it] = (V0)v0;
+        c1[it] = v1;
+        pos[it] = ps;
+        br[it] = bk >= 0 ? ((uint32_t)bk << 16) | atomicAdd(&lh[bk], 1u) : ~0u;
     }
     occ = wave_ior(occ);
     if (__lane_id() == 0 && occ) atomicOr(&s_occ, occ);
@@ -542,11 +563,11 @@ __global__ void __launch_bounds__(kPartThreads) k_rgn_p1(IngestArgs a) {
     __syncthreads();
 #pragma unroll
     for (int it = 0; it < kPartItems; ++it) {
-        if (bk[it] < 0) continue;
-        const uint32_t j = ls[bk[it]] + rank[it];
+        if (br[it] == ~0u) continue;
+        const uint32_t j = ls[br[it] >> 16] + (br[it] & 0xffffu);
         s.k[j] = key[it];
         if constexpr (C) {
-            if constexpr (ACC) s_v32[j] = (int32_t)c0[it];
+            if constexpr (ACC) s_v32[j] = c0[it];
         } else {
             s.a0[j] = c0[it];
             if constexpr (AV) s.a1[j] = c1[it];
@@ -791,12 +812,22 @@ __device__ __forceinline__ void copy_words(long long* __restrict__ d, const long
     for (int64_t w = threadIdx.x; w < n2; w += blockDim.x) d2[w] = s2[w];
 }
 
+#ifndef GW_APPLY_THREADS
+#define GW_APPLY_THREADS 512
+#endif
+#ifndef GW_APPLY_GROUP
+#define GW_APPLY_GROUP 4
+#endif
+#ifndef GW_APPLY_UNROLL
+#define GW_APPLY_UNROLL 4
+#endif
+constexpr int kApplyThreads = GW_APPLY_THREADS;
 constexpr int kApplyRuns = 256;  // run descriptors staged in LDS per step (<= blockDim)
-constexpr int kApplyGroup = 4;   // consecutive runs a wave walks as one sequence
-constexpr int kApplyUnroll = 4;  // records per lane with their loads in flight together
+constexpr int kApplyGroup = GW_APPLY_GROUP;   // consecutive runs a wave walks as one sequence
+constexpr int kApplyUnroll = GW_APPLY_UNROLL;  // records per lane with their loads in flight together
 
 template <int AGG, bool CMP>
-__global__ void __launch_bounds__(512) k_rgn_apply(IngestArgs a) {
+__global__ void __launch_bounds__(kApplyThreads) GW_APPLY_ATTR k_rgn_apply(IngestArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     constexpr bool M = uses_mask<AGG>();
     constexpr bool C = CMP && cmp_agg<AGG>();
@@ -1025,7 +1056,11 @@ __global__ void __launch_bounds__(512) k_rgn_apply(IngestArgs a) {
                 if (!c.ok[q]) continue;
                 if constexpr (C) {
                     const uint64_t h = cmp_hash((uint64_t)c.key[q], bucket_id, a.d1_bits);
+#ifdef GW_EXP_NO_UNHASH
+                    apply_one((int64_t)h, h, c.v0[q], c.v1[q], cmp_pos((uint64_t)c.key[q], a.d1_bits));
+#else
                     apply_one(slot_unhash(h), h, c.v0[q], c.v1[q], cmp_pos((uint64_t)c.key[q], a.d1_bits));
+#endif
                 } else {
                     apply_one(c.key[q], slot_hash(c.key[q]), c.v0[q], c.v1[q], c.ps[q]);
                 }
@@ -1438,6 +1473,163 @@ __global__ void __launch_bounds__(256) k_fire(FireArgs a) {
     stage_flush(rs, &a.st->rows, a.o_key, a.o_start, a.o_end, a.o_res);
 }
 
+// Fire sweep without restored-window overlay, for passes whose windows cover at most
+// kFirePos ring positions (every sliding/tumbling fire of a ring of <= 8 panes; Nexmark Q5:
+// 5 of 6).  Each thread takes U slots per step and issues every load of the step at
+// once -- keys, presence masks and the cells of all covered positions, unconditionally
+// and coalesced -- so a wave keeps U * (2 + positions) loads in flight instead of one
+// dependent chain per slot.  Presence picks the cells to fold in registers (mask bit, or
+// the count word for COUNT / AVG; an absent cell is never folded).  Rows are compacted
+// per wave with ballots and staged in LDS as (key, result, window); a block reserves its
+// staged rows in the output with one device atomic per kFireStage rows.  Same rows,
+// same retire as k_fire (row order within a fire is unspecified for both).
+constexpr int kFirePos = 8;
+constexpr int kFireStage = 2048;
+constexpr int kFireThreads = 256;
+template <int AGG, int U>
+__global__ void __launch_bounds__(kFireThreads) k_fire_sweep(FireArgs a) {
+    constexpr bool M = uses_mask<AGG>();
+    constexpr bool AV = AGG == GW_AVG_I64 || AGG == GW_AVG_F64;
+    constexpr int NW = kFireThreads / 64;
+    __shared__ long long s_k[kFireStage], s_r[kFireStage];
+    __shared__ uint8_t s_w[kFireStage];
+    __shared__ unsigned s_wave[NW];
+    __shared__ unsigned s_cnt;
+    __shared__ unsigned long long s_base;
+    const int64_t nslots = a.t.cap + 1;
+    const int64_t id0 = identity0(AGG);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (threadIdx.x == 0) s_cnt = 0;
+    if (blockIdx.x == 0 && threadIdx.x < kShards) atomicAnd(&a.st->sh[threadIdx.x].occ, ~a.rmask);
+    // the ring positions this pass folds (uniform)
+    uint64_t need = 0;
+    for (int w = 0; w < a.nwin; ++w) need |= a.wmask[w];
+    int posl[kFirePos];
+    int np = 0;
+#pragma unroll
+    for (int q = 0; q < kFirePos; ++q) {
+        posl[q] = need ? __ffsll((long long)need) - 1 : 0;
+        if (need) { need &= need - 1; np = q + 1; }
+    }
+    const int64_t S = pt_S(a.t);
+    const int64_t MW = pt_mask_words(a.t);
+    auto flush = [&]() {  // every thread; ends with s_cnt == 0
+        __syncthreads();
+        const unsigned c = s_cnt;
+        if (threadIdx.x == 0 && c) s_base = atomicAdd(&a.st->rows, (unsigned long long)c);
+        __syncthreads();
+        const unsigned long long b = s_base;
+        for (unsigned j = threadIdx.x; j < c; j += kFireThreads) {
+            const int64_t st = a.start0 + (int64_t)s_w[j] * a.slide;
+            a.o_key[b + j] = s_k[j];
+            a.o_start[b + j] = st;
+            a.o_end[b + j] = st + a.size;
+            a.o_res[b + j] = s_r[j];
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) s_cnt = 0;
+        __syncthreads();
+    };
+    __syncthreads();
+    const int64_t tile = (int64_t)kFireThreads * U;
+    for (int64_t base = (int64_t)blockIdx.x * tile; base < nslots; base += (int64_t)gridDim.x * tile) {
+        int64_t key[U], c0[U][kFirePos], c1[U][kFirePos];
+        uint64_t mask[U];
+        bool live[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {  // all loads of the step in flight together
+            const int64_t g0 = base + u * kFireThreads + threadIdx.x;
+            live[u] = g0 < nslots;
+            const int64_t g = live[u] ? g0 : nslots - 1;
+            int64_t* rg = pt_region(a.t, g >> a.t.log2S);
+            const int64_t j = g & (S - 1);
+            key[u] = rg[j];
+            mask[u] = M ? mask_get((const uint8_t*)(rg + S), j, a.t.mask_shift) : 0;
+            const int64_t* cells = rg + S + MW;
+#pragma unroll
+            for (int q = 0; q < kFirePos; ++q) {
+                c0[u][q] = id0;
+                c1[u][q] = 0;
+                if (q < np) {
+                    const int64_t* c = cells + ((int64_t)posl[q] * S + j) * (AV ? 2 : 1);
+                    c0[u][q] = c[0];
+                    if constexpr (AV) c1[u][q] = c[1];
+                }
+            }
+        }
+        for (int w = 0; w < a.nwin; ++w) {
+            const uint64_t wm = a.wmask[w];
+            int64_t res[U];
+            uint64_t bal[U];
+            unsigned tot = 0;
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                int64_t r0 = id0, r1 = 0;
+                bool any = false;
+#pragma unroll
+                for (int q = 0; q < kFirePos; ++q) {
+                    if (q < np && ((wm >> posl[q]) & 1)) {
+                        const bool pres = M ? ((mask[u] >> posl[q]) & 1) != 0 : (AV ? c1[u][q] : c0[u][q]) != 0;
+                        if (pres) {
+                            fold_cell(AGG, r0, r1, c0[u][q], c1[u][q]);
+                            any = true;
+                        }
+                    }
+                }
+                any = any && live[u];
+                res[u] = cell_result(AGG, r0, r1);
+                bal[u] = __ballot(any);
+                tot += (unsigned)__popcll(bal[u]);
+            }
+            if (lane == 0) s_wave[wave] = tot;
+            __syncthreads();
+            unsigned woff = 0, btot = 0;
+#pragma unroll
+            for (int q = 0; q < NW; ++q) {
+                const unsigned v = s_wave[q];
+                woff += q < wave ? v : 0u;
+                btot += v;
+            }
+            if (s_cnt + btot > (unsigned)kFireStage) flush();  // uniform
+            else __syncthreads();  // everyone has read s_wave and s_cnt
+            unsigned o = s_cnt + woff;
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                if ((bal[u] >> lane) & 1) {
+                    const unsigned j = o + (unsigned)__popcll(bal[u] & ((1ull << lane) - 1ull));
+                    s_k[j] = key[u];
+                    s_r[j] = res[u];
+                    s_w[j] = (uint8_t)w;
+                }
+                o += (unsigned)__popcll(bal[u]);
+            }
+            __syncthreads();
+            if (threadIdx.x == 0) s_cnt += btot;
+        }
+        if (a.rmask) {  // clearAllState of the panes no later window covers
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                if (!live[u]) continue;
+                const int64_t g = base + u * kFireThreads + threadIdx.x;
+                int64_t* rg = pt_region(a.t, g >> a.t.log2S);
+                const int64_t j = g & (S - 1);
+                if constexpr (M) {
+                    if (mask[u] & a.rmask) mask_put((uint8_t*)(rg + S), j, a.t.mask_shift, mask[u] & ~a.rmask);
+                }
+                uint64_t m = a.rmask;
+                while (m) {
+                    const int pos = __ffsll((long long)m) - 1;
+                    m &= m - 1;
+                    int64_t* c = rg + S + MW + ((int64_t)pos * S + j) * (AV ? 2 : 1);
+                    c[0] = id0;
+                    if constexpr (AV) c[1] = 0;
+                }
+            }
+        }
+    }
+    flush();
+}
+
 // Move the cells of ring positions `emask` to the deferred list (ring re-base down).
 template <int AGG>
 __global__ void __launch_bounds__(256) k_evict(EvictArgs a) {
@@ -1689,7 +1881,7 @@ hipError_t launch_region_flush(const IngestArgs& a, hipStream_t s) {
         hipLaunchKernelGGL((k_rgn_p2<A, CM>), dim3((unsigned)(a.ngroups * nb1)), dim3(kPartThreads), part_lds, s, \
                            a);                                                                                  \
     }                                                                                                           \
-    hipLaunchKernelGGL((k_rgn_apply<A, CM>), dim3((unsigned)a.t.nreg), dim3(512), apply_lds, s, a)
+    hipLaunchKernelGGL((k_rgn_apply<A, CM>), dim3((unsigned)a.t.nreg), dim3(kApplyThreads), apply_lds, s, a)
 #define L(A)            \
     if (a.cmp) {        \
         L2(A, true);    \
@@ -1744,6 +1936,28 @@ hipError_t launch_deferred_min(const int64_t* pane, int64_t n, DevStatus* st, hi
 }
 
 hipError_t launch_fire(const FireArgs& a, hipStream_t s) {
+    uint64_t need = 0;
+    for (int w = 0; w < a.nwin; ++w) need |= a.wmask[w];
+    const bool sweep = a.ov.head == nullptr && __builtin_popcountll(need) <= kFirePos && a.nwin <= 255;
+#ifdef GW_EXP_FIRE_SWEEP
+    if (sweep) {
+#else
+    if (false && sweep) {  // measured slower than k_fire on Q5 (0.37 vs 0.30 ms per fire)
+#endif
+        // 4 slots per thread (2 for the two-word AVG cells); ~4 blocks per CU
+        const bool av = a.t.agg == GW_AVG_I64 || a.t.agg == GW_AVG_F64;
+#ifndef GW_FIRE_U
+#define GW_FIRE_U 4
+#endif
+        const int64_t tile = (int64_t)kFireThreads * (av ? 2 : GW_FIRE_U);
+        const int fg = (int)std::min<int64_t>(1024, std::max<int64_t>(1, (a.t.cap + 1 + tile - 1) / tile));
+#define L(A)                                                                                              \
+    if (av) hipLaunchKernelGGL((k_fire_sweep<A, 2>), dim3(fg), dim3(kFireThreads), 0, s, a);             \
+    else hipLaunchKernelGGL((k_fire_sweep<A, GW_FIRE_U>), dim3(fg), dim3(kFireThreads), 0, s, a)
+        GW_AGG_SWITCH(a.t.agg, L);
+#undef L
+        return hipGetLastError();
+    }
     const int fg = (int)std::min<int64_t>(1024, std::max<int64_t>(1, (a.t.cap + 1 + 255) / 256));
 #define L(A) hipLaunchKernelGGL(k_fire<A>, dim3(fg), dim3(256), 0, s, a)
     GW_AGG_SWITCH(a.t.agg, L);

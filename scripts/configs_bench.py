@@ -7,8 +7,13 @@ the host cores over a bounded prefix of the same stream.  One JSON line per conf
   wordcount  WindowWordCount (flink-examples-streaming .../windowing/WindowWordCount.java:
              121-149): tokens keyed by word (String.hashCode of Zipf(1.1) words over a 50k
              vocabulary), countWindow(250, 150).sum(1)
-  ysb        Yahoo Streaming Benchmark shape: 100 campaigns, 10 s tumbling count,
-             ts 1 ms per 100k events, disorder <= 50 ms, watermark every 200 ms
+  ysb        Yahoo Streaming Benchmark shape (streaming-benchmarks AdvertisingTopologyNative):
+             events (ad_id, event_type, event_time) over 1000 ads of 100 campaigns (10 ads
+             each), filter(event_type == "view") (1/3 of the events), project + join
+             ad_id -> campaign_id (the Redis lookup, a device gather here), keyBy(campaign)
+             10 s tumbling count; ts 1 ms per 100k events, disorder <= 50 ms, watermark every
+             200 ms.  The filter and the join run on the GPU inside the timed region; `value`
+             counts raw events (before the filter), `operator_events` the window operator's
   q7         Nexmark Q7/Q8 shape at one GPU: 10M keys, 10 s tumbling max(price)
   sessions   event-time sessions, gap 10 s, avg(f64) over 12.5M keys (one GPU's share of
              100M keys on 8 GPUs); keys come in four groups, each active 5 s out of 20 s, so
@@ -49,11 +54,16 @@ def gen(name, nb, steps, dev):
         wms = [0] * steps
         return dict(assigner="count_sliding", size=250, slide=150), "sum_i32", keys, ts, vals, wms
     if name == "ysb":
-        keys = r % 100
+        # raw events: ad index into the 1000-ad table and event type (0 = view, 1 = click,
+        # 2 = purchase); the campaign ids are random 64-bit ids like YSB's UUIDs
+        ad = r % 1000
+        etype = (splitmix64(idx, 76) & MASK63) % 3
         base = idx // 100_000
         ts = base - (splitmix64(idx, 77) & MASK63) % 51
         wms = [int((b + 1) * nb // 100_000) - 50 - 1 for b in range(steps)]
-        return dict(assigner="tumbling", size=10_000), "count", keys, ts, None, wms
+        campaigns = splitmix64(torch.arange(100, device=dev, dtype=torch.int64), 0xCA11) & MASK63
+        ad_campaign = campaigns.repeat_interleave(10)  # ad i belongs to campaign i // 10
+        return dict(assigner="tumbling", size=10_000), "count", (ad, etype, ad_campaign), ts, None, wms
     if name == "q7":
         keys = r % 10_000_000
         base = idx * 200 // nb
@@ -85,13 +95,30 @@ def run(name, args, dev):
     cap = {"wordcount": 1 << 16, "ysb": 1024, "q7": 10_000_000, "sessions": 12_500_000}[name]
     op = W.GpuWindowOperator(assigner, agg, capacity_hint=cap, max_batch=nb * 2).open()
     rows = 0
+    op_events = 0
+    ysb = name == "ysb"
+    if ysb:
+        ad, etype, ad_campaign = keys
+        side = torch.cuda.Stream(device=dev)
 
     def step(b):
-        nonlocal rows
+        nonlocal rows, op_events
         lo, hi = b * nb, (b + 1) * nb
-        N.check(N.lib().gw_ingest_device(op.handle, nb, keys[lo:hi].data_ptr(), None, ts[lo:hi].data_ptr(),
-                                         vals[lo:hi].data_ptr() if vals is not None else None, op.stream()),
-                op.handle)
+        if ysb:  # filter(view) -> project -> join(ad -> campaign), on a torch stream
+            with torch.cuda.stream(side):
+                view = etype[lo:hi] == 0
+                k = ad_campaign[ad[lo:hi][view]]
+                t = ts[lo:hi][view]
+            n = k.numel()
+            side.synchronize()
+            N.check(N.lib().gw_ingest_device(op.handle, n, k.data_ptr(), None, t.data_ptr(), None, op.stream()),
+                    op.handle)
+            op_events += n
+        else:
+            N.check(N.lib().gw_ingest_device(op.handle, nb, keys[lo:hi].data_ptr(), None, ts[lo:hi].data_ptr(),
+                                             vals[lo:hi].data_ptr() if vals is not None else None, op.stream()),
+                    op.handle)
+            op_events += nb
         rows += op.advance_watermark(wms[b])
         rows += op.pending_rows() if kw["assigner"].startswith("count") else 0
         op.clear_rows()
@@ -101,6 +128,7 @@ def run(name, args, dev):
     op.flush()
     torch.cuda.synchronize()
     rows = 0
+    op_events = 0
     t0 = time.perf_counter()
     for b in range(args.warmup, steps):
         step(b)
@@ -112,16 +140,29 @@ def run(name, args, dev):
     op.close()
     out = {"config": name, "window": kw, "aggregate": agg, "events_per_step": nb, "steps": n_timed,
            "value": nb * n_timed / dt, "unit": "events/s", "ms_per_step": dt * 1e3 / n_timed,
+           "operator_events_per_s": op_events / dt,
            "rows_fired": rows, "live_keys": stats.get("live_keys"), "data": "synthetic, generated in HBM"}
+    if ysb:
+        out["pipeline"] = "filter(event_type == view) + join(ad_id -> campaign_id) on the GPU, then the operator"
     if not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(kw, agg, keys, ts, vals, wms, nb, args.cpu_seconds)
+        if ysb:  # the oracle times the window operator on the filtered, joined stream
+            ad, etype, ad_campaign = keys
+            view = etype == 0
+            keys_o, ts_o = ad_campaign[ad[view]], ts[view]
+            cum = torch.cumsum(view.view(-1, nb).sum(1), 0).tolist()
+            nb_o = int(cum[0])  # first batch's size (batches are ~nb/3 each)
+            out["cpu_baseline"] = cpu_baseline(kw, agg, keys_o, ts_o, None, wms, nb_o, args.cpu_seconds)
+            out["cpu_baseline"]["note"] = "oracle operator over the filtered + joined stream, events after the filter"
+        else:
+            out["cpu_baseline"] = cpu_baseline(kw, agg, keys, ts, vals, wms, nb, args.cpu_seconds)
     return out
 
 
 def cpu_baseline(kw, agg, keys, ts, vals, wms, nb, seconds):
     from oracle import oracle as O
+    from bench import host_cores
     O.build()
-    threads = min(16, os.cpu_count() or 1)
+    threads = host_cores()[0]
     cfg = O.make_config(agg=agg, max_parallelism=128, **kw)
 
     def go(n_ev):
