@@ -10,9 +10,10 @@
 //
 // The element chain is a linked list (each length says where the next element starts),
 // which the reference walks one element at a time.  Here it is split into chunks of
-// kNbChunk bytes.  The first element that starts in chunk c starts within GW_MAX_ELEMENT
-// (= 64) bytes of the chunk start, so a wave per chunk walks all 64 candidate entries at
-// once, one per lane (k_nb_walk).  Wrong candidates read payload bytes as lengths and
+// kNbChunk bytes.  The first element that starts in chunk c starts within the longest
+// element (NL = 64 bytes, or 128 = GW_MAX_ELEMENT for layouts whose records are longer)
+// of the chunk start, so a wave per chunk walks all NL candidate entries at once, one or
+// two per lane (k_nb_walk).  Wrong candidates read payload bytes as lengths and
 // die, or land on a real element start and merge with the true chain, so almost every
 // chunk ends with one exit whatever its entry was.  k_nb_resolve then finds each chunk's
 // true entry from the nearest chunk before it whose exit is unique, k_nb_scan turns the
@@ -26,11 +27,14 @@
 
 namespace gw {
 
-constexpr int kNbLanes = GW_MAX_ELEMENT;                 // candidate entries per chunk (one per lane)
+// NL: candidate entries per chunk = the longest element (64, or GW_MAX_ELEMENT = 128 when
+// the record layout's elements exceed 64 bytes); NL / 64 candidates per lane.
 constexpr int kNbWaves = 4;                              // chunks per block
-constexpr int kNbWords = (kNbChunk + kNbLanes + 8) / 4;  // chunk + overhang + one spare dword, as dwords
+template <int NL>
+constexpr int nb_words() { return (kNbChunk + NL + 8) / 4; }  // chunk + overhang + one spare dword
 constexpr int kNbMaxElems = kNbChunk / 6 + 2;            // shortest element: 4 + RecordAttributes(2)
 constexpr int kNbScanBlock = 256;                        // chunks per k_nb_resolve block
+constexpr int kNbMaxLanes = GW_MAX_ELEMENT;              // scratch sizing: the widest walk
 
 // walk state of a candidate lane, packed into the top bits of its exit word
 constexpr int kStNormal = 0, kStTail = 1, kStDead = 2, kStLong = 3;
@@ -42,8 +46,12 @@ constexpr int64_t kNonConv = -1;
 // A wave's chunk in flight: bytes [base, base + 4*kNbWords) ∩ [0, nbytes) as dwords in
 // registers (kNbRegs per lane; bytes past the end read as 0), loaded one chunk ahead of
 // the walk so the HBM latency hides behind the LDS chain walk of the current chunk.
-constexpr int kNbRegs = (kNbWords + 63) / 64;
-__device__ __forceinline__ void nb_fetch(uint32_t (&r)[kNbRegs], const uint8_t* buf, int64_t base, int64_t nbytes) {
+template <int NL>
+constexpr int nb_regs() { return (nb_words<NL>() + 63) / 64; }
+template <int NL>
+__device__ __forceinline__ void nb_fetch(uint32_t (&r)[nb_regs<NL>()], const uint8_t* buf, int64_t base,
+                                         int64_t nbytes) {
+    constexpr int kNbWords = nb_words<NL>(), kNbRegs = nb_regs<NL>();
     const int lane = __lane_id();
     const int64_t left = nbytes - base;
     const int avail = left < 4 * kNbWords ? (int)left : 4 * kNbWords;
@@ -61,7 +69,9 @@ __device__ __forceinline__ void nb_fetch(uint32_t (&r)[kNbRegs], const uint8_t* 
         r[k] = v;
     }
 }
-__device__ __forceinline__ void nb_put(uint32_t* lds, const uint32_t (&r)[kNbRegs]) {
+template <int NL>
+__device__ __forceinline__ void nb_put(uint32_t* lds, const uint32_t (&r)[nb_regs<NL>()]) {
+    constexpr int kNbWords = nb_words<NL>(), kNbRegs = nb_regs<NL>();
     const int lane = __lane_id();
 #pragma unroll
     for (int k = 0; k < kNbRegs; ++k) {
@@ -85,32 +95,40 @@ __device__ __forceinline__ uint64_t lds_be64(const uint32_t* w, int p) {
     return __builtin_bswap64(le);
 }
 
-// Pass 1: every candidate entry of every chunk, walked at once (lane = candidate offset).
-// Per lane: exit (relative position | state << 28) and (records | watermarks << 16).
+// Pass 1: every candidate entry of every chunk, walked at once (lane = candidate offset,
+// plus 64 for the second candidate of a lane when NL = 128).
+// Per candidate: exit (relative position | state << 28) and (records | watermarks << 16).
+template <int NL>
 __global__ void __launch_bounds__(256) k_nb_walk(const uint8_t* buf, int64_t nbytes, int64_t nch, int32_t vbytes,
                                                  uint32_t* exits, uint32_t* cnt, int64_t* conv) {
+    constexpr int kNbWords = nb_words<NL>(), kNbRegs = nb_regs<NL>(), CPL = NL / 64;
     const int rec_ts = 9 + vbytes, rec_nots = 1 + vbytes;
     __shared__ uint32_t lds[kNbWaves][kNbWords];
     const int w = threadIdx.x >> 6, lane = __lane_id();
     const int64_t stride = (int64_t)gridDim.x * kNbWaves;
     uint32_t pre[kNbRegs];
     int64_t c = (int64_t)blockIdx.x * kNbWaves + w;
-    if (c < nch) nb_fetch(pre, buf, c * kNbChunk, nbytes);
+    if (c < nch) nb_fetch<NL>(pre, buf, c * kNbChunk, nbytes);
     for (; c < nch; c += stride) {
     const int64_t base = c * kNbChunk;
     __builtin_amdgcn_wave_barrier();  // the previous chunk's LDS reads are done
-    nb_put(lds[w], pre);
+    nb_put<NL>(lds[w], pre);
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    if (c + stride < nch) nb_fetch(pre, buf, (c + stride) * kNbChunk, nbytes);
+    if (c + stride < nch) nb_fetch<NL>(pre, buf, (c + stride) * kNbChunk, nbytes);
     const uint32_t* l = lds[w];
     const int64_t left = nbytes - base;
-    const int rlim = left < kNbChunk + 4 * kNbLanes ? (int)left : kNbChunk + 4 * kNbLanes;  // binding only near the end
+    const int rlim = left < kNbChunk + 4 * NL ? (int)left : kNbChunk + 4 * NL;  // binding only near the end
     const int rend = rlim < kNbChunk ? rlim : kNbChunk;
+    int64_t ex[CPL];
+    bool live[CPL];
+#pragma unroll
+    for (int k = 0; k < CPL; ++k) {
     // Branch-free step (one ds_read2 gives the length word and the tag): the loop runs as
     // long as any candidate lane is alive, every lane steps in lockstep under a full exec
     // mask, and the per-step VALU count stays small, which is what bounds this kernel.
-    int pos = lane, nr = 0, nw = 0, st = kStNormal;
+    const int cand = lane + 64 * k;
+    int pos = cand, nr = 0, nw = 0, st = kStNormal;
     bool run = pos < rend;
     while (__ballot(run)) {
         const int p = run ? pos : 0;
@@ -123,9 +141,12 @@ __global__ void __launch_bounds__(256) k_nb_walk(const uint8_t* buf, int64_t nby
         // rarely also carry the matching tag, so wrong chains die within a step or two
         const int want = tag == 0u ? rec_ts : tag == 1u ? rec_nots : tag == 2u ? 9 : tag == 3u ? 29
                        : tag == 4u ? 5 : tag == 5u ? 2 : tag == 6u ? 13 : -1;
+        // beyond GW_MAX_ELEMENT: unsupported; longer than NL but within it: no element of
+        // this layout is that long, so the length cannot match its tag (dead: corrupt on
+        // the true chain) -- the same order of checks as the oracle's decoder
         const int ns = p + 4 > rlim ? kStTail
                      : len < 1 ? kStDead
-                     : len > kNbLanes - 4 ? kStLong
+                     : len > GW_MAX_ELEMENT - 4 ? kStLong
                      : p + 4 + len > rlim ? kStTail
                      : len != want ? kStDead : kStNormal;
         const bool adv = run && ns == kStNormal;
@@ -135,31 +156,42 @@ __global__ void __launch_bounds__(256) k_nb_walk(const uint8_t* buf, int64_t nby
         pos = adv ? p + 4 + len : pos;
         run = adv && pos < rend;
     }
-    exits[c * kNbLanes + lane] = (uint32_t)pos | ((uint32_t)st << 28);
-    cnt[c * kNbLanes + lane] = (uint32_t)nr | ((uint32_t)nw << 16);
+    exits[c * NL + cand] = (uint32_t)pos | ((uint32_t)st << 28);
+    cnt[c * NL + cand] = (uint32_t)nr | ((uint32_t)nw << 16);
+    ex[k] = nb_pack(base + pos, st);
+    live[k] = st == kStNormal || st == kStTail;
+    }
     // unique exit over the live candidates (dead ones never hold the true entry)
-    const int64_t ex = nb_pack(base + pos, st);
-    const bool live = st == kStNormal || st == kStTail;
-    const unsigned long long lv = __ballot(live);
-    int64_t cv = kNonConv;
-    if (lv) {
-        const int first = __ffsll((long long)lv) - 1;
-        const int64_t ref = __shfl(ex, first);
-        if (__ballot(live && ex != ref) == 0) cv = ref;
-    } else {
-        cv = nb_pack(base, kStDead);
+    int64_t ref = 0;
+    bool have = false;
+#pragma unroll
+    for (int k = 0; k < CPL && !have; ++k) {
+        const unsigned long long lv = __ballot(live[k]);
+        if (lv) {
+            ref = __shfl(ex[k], __ffsll((long long)lv) - 1);
+            have = true;
+        }
+    }
+    int64_t cv = nb_pack(base, kStDead);
+    if (have) {
+        bool diff = false;
+#pragma unroll
+        for (int k = 0; k < CPL; ++k) diff = diff || __ballot(live[k] && ex[k] != ref) != 0;
+        cv = diff ? kNonConv : ref;
     }
     if (lane == 0) conv[c] = cv;
     }
 }
 
+template <int NL>
 __device__ __forceinline__ int64_t nb_exit_word(const uint32_t* exits, int64_t t, int64_t lane) {
-    const uint32_t x = exits[t * kNbLanes + lane];
+    const uint32_t x = exits[t * NL + lane];
     return nb_pack(t * kNbChunk + (x & 0x0fffffffu), (int)(x >> 28));
 }
 
 // Pass 2: one thread per chunk finds its true entry from the nearest earlier chunk with a
 // unique exit, then the block scans the chunk counts (exclusive, block-local).
+template <int NL>
 __global__ void __launch_bounds__(kNbScanBlock) k_nb_resolve(int64_t nbytes, int64_t nch, const uint32_t* exits,
                                                              const uint32_t* cnt, const int64_t* conv, int64_t* entry,
                                                              int32_t* offs, long long* btot, NbStatus* st) {
@@ -173,8 +205,8 @@ __global__ void __launch_bounds__(kNbScanBlock) k_nb_resolve(int64_t nbytes, int
         int64_t e = j < 0 ? nb_pack(0, kStNormal) : conv[j];  // entry word of chunk j + 1
         for (int64_t t = j + 1; t < c && nb_state(e) == kStNormal; ++t) {
             const int64_t lane = nb_pos(e) - t * kNbChunk;
-            if (lane < 0 || lane >= kNbLanes) { e = nb_pack(nb_pos(e), kStDead); break; }
-            e = nb_exit_word(exits, t, lane);
+            if (lane < 0 || lane >= NL) { e = nb_pack(nb_pos(e), kStDead); break; }
+            e = nb_exit_word<NL>(exits, t, lane);
         }
         int64_t ent = -1;
         if (nb_state(e) == kStNormal) {
@@ -182,12 +214,12 @@ __global__ void __launch_bounds__(kNbScanBlock) k_nb_resolve(int64_t nbytes, int
             const int64_t lane = p - c * kNbChunk;
             if (p >= nbytes) {
                 // the chain ended exactly at the end of the bytes: nothing starts here
-            } else if (lane < 0 || lane >= kNbLanes) {
+            } else if (lane < 0 || lane >= NL) {
                 atomicOr(&st->corrupt, 1ull);
             } else {
                 ent = p;
-                const int64_t ex = nb_exit_word(exits, c, lane);
-                const uint32_t cc = cnt[c * kNbLanes + lane];
+                const int64_t ex = nb_exit_word<NL>(exits, c, lane);
+                const uint32_t cc = cnt[c * NL + lane];
                 nr = (int)(cc & 0xffffu);
                 nw = (int)(cc >> 16);
                 const int s = nb_state(ex);
@@ -266,10 +298,12 @@ __device__ __forceinline__ int64_t nb_field(const uint32_t* l, int p, int type) 
 }
 
 // Pass 4: each chunk's true chain, walked once more out of LDS, decoded by all 64 lanes.
+template <int NL>
 __global__ void __launch_bounds__(256) k_nb_decode(const uint8_t* buf, int64_t nbytes, int64_t nch, NbLayout L,
                                                    const int64_t* entry, const int32_t* offs, const long long* btot,
                                                    int64_t* key, int64_t* ts, int64_t* val, int64_t rec_cap,
                                                    int64_t* wm_pos, int64_t* wm_val, int64_t wm_cap, NbStatus* st) {
+    constexpr int kNbWords = nb_words<NL>(), kNbRegs = nb_regs<NL>();
     __shared__ uint32_t lds[kNbWaves][kNbWords];
     __shared__ uint16_t starts[kNbWaves][kNbMaxElems];
     __shared__ int nelem[kNbWaves];
@@ -277,19 +311,19 @@ __global__ void __launch_bounds__(256) k_nb_decode(const uint8_t* buf, int64_t n
     const int64_t stride = (int64_t)gridDim.x * kNbWaves;
     uint32_t pre[kNbRegs];
     int64_t c = (int64_t)blockIdx.x * kNbWaves + w;
-    if (c < nch) nb_fetch(pre, buf, c * kNbChunk, nbytes);
+    if (c < nch) nb_fetch<NL>(pre, buf, c * kNbChunk, nbytes);
     for (; c < nch; c += stride) {
     const int64_t e0 = entry[c];
     const int64_t base = c * kNbChunk;
     __builtin_amdgcn_wave_barrier();  // the previous chunk's LDS reads are done
-    nb_put(lds[w], pre);
+    nb_put<NL>(lds[w], pre);
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    if (c + stride < nch) nb_fetch(pre, buf, (c + stride) * kNbChunk, nbytes);
+    if (c + stride < nch) nb_fetch<NL>(pre, buf, (c + stride) * kNbChunk, nbytes);
     if (e0 < 0) continue;
     const uint32_t* l = lds[w];
     const int64_t left = nbytes - base;
-    const int rlim = left < kNbChunk + 4 * kNbLanes ? (int)left : kNbChunk + 4 * kNbLanes;
+    const int rlim = left < kNbChunk + 4 * NL ? (int)left : kNbChunk + 4 * NL;
     const int rend = rlim < kNbChunk ? rlim : kNbChunk;
     {  // the true chain, walked by the whole wave in lockstep (uniform addresses: LDS
        // broadcasts), lane 0 recording the element starts
@@ -299,7 +333,7 @@ __global__ void __launch_bounds__(256) k_nb_decode(const uint8_t* buf, int64_t n
         while (run && m < kNbMaxElems) {
             const uint32_t w0 = l[pos >> 2], w1 = l[(pos >> 2) + 1];
             const int32_t len = (int32_t)__builtin_bswap32(__builtin_amdgcn_alignbyte(w1, w0, (uint32_t)(pos & 3)));
-            if (pos + 4 > rlim || len < 1 || len > kNbLanes - 4 || pos + 4 + len > rlim) break;
+            if (pos + 4 > rlim || len < 1 || len > NL - 4 || pos + 4 + len > rlim) break;
             if (lane == 0) starts[w][m] = (uint16_t)pos;
             ++m;
             pos += 4 + len;
@@ -380,7 +414,7 @@ int64_t nb_scratch_bytes(int64_t nbytes) {
     const int64_t nch = (nbytes + kNbChunk - 1) / kNbChunk;
     const int64_t nblk = (nch + kNbScanBlock - 1) / kNbScanBlock;
     // exits + counts per lane, conv + entry + offsets per chunk, block totals
-    return nch * kNbLanes * 8 + nch * 24 + nblk * 16 + 256;
+    return nch * kNbMaxLanes * 8 + nch * 24 + nblk * 16 + 256;
 }
 
 hipError_t launch_nb_decode(const uint8_t* buf, int64_t nbytes, const NbLayout& L, int64_t* key, int64_t* ts,
@@ -391,8 +425,8 @@ hipError_t launch_nb_decode(const uint8_t* buf, int64_t nbytes, const NbLayout& 
     const int64_t nch = (nbytes + kNbChunk - 1) / kNbChunk;
     const int64_t nblk = (nch + kNbScanBlock - 1) / kNbScanBlock;
     uint8_t* p = (uint8_t*)scratch;
-    uint32_t* exits = (uint32_t*)p;            p += nch * kNbLanes * 4;
-    uint32_t* cnt = (uint32_t*)p;              p += nch * kNbLanes * 4;
+    uint32_t* exits = (uint32_t*)p;            p += nch * kNbMaxLanes * 4;
+    uint32_t* cnt = (uint32_t*)p;              p += nch * kNbMaxLanes * 4;
     int64_t* conv = (int64_t*)p;               p += nch * 8;
     int64_t* entry = (int64_t*)p;              p += nch * 8;
     int32_t* offs = (int32_t*)p;               p += nch * 8;
@@ -405,12 +439,23 @@ hipError_t launch_nb_decode(const uint8_t* buf, int64_t nbytes, const NbLayout& 
         return e ? (int64_t)atoll(e) : (int64_t)4096;
     }();
     if (cap > 0 && gb > cap) gb = cap;
-    hipLaunchKernelGGL(k_nb_walk, dim3((unsigned)gb), dim3(256), 0, s, buf, nbytes, nch, L.vbytes, exits, cnt, conv);
-    hipLaunchKernelGGL(k_nb_resolve, dim3((unsigned)nblk), dim3(kNbScanBlock), 0, s, nbytes, nch, exits, cnt, conv,
-                       entry, offs, btot, d_st);
-    hipLaunchKernelGGL(k_nb_scan, dim3(1), dim3(1024), 0, s, nblk, btot, d_st);
-    hipLaunchKernelGGL(k_nb_decode, dim3((unsigned)gb), dim3(256), 0, s, buf, nbytes, nch, L, entry, offs, btot, key, ts, val,
-                       rec_cap, wm_pos, wm_val, wm_cap, d_st);
+    // candidates per chunk: the longest element this layout can produce (a record with a
+    // timestamp: 4 + 1 + 8 + vbytes; the other tags are at most 33 bytes)
+    const bool wide = 13 + L.vbytes > 64;
+#define NB_LAUNCH(NL)                                                                                              \
+    hipLaunchKernelGGL(k_nb_walk<NL>, dim3((unsigned)gb), dim3(256), 0, s, buf, nbytes, nch, L.vbytes, exits, cnt, \
+                       conv);                                                                                      \
+    hipLaunchKernelGGL(k_nb_resolve<NL>, dim3((unsigned)nblk), dim3(kNbScanBlock), 0, s, nbytes, nch, exits, cnt,  \
+                       conv, entry, offs, btot, d_st);                                                             \
+    hipLaunchKernelGGL(k_nb_scan, dim3(1), dim3(1024), 0, s, nblk, btot, d_st);                                    \
+    hipLaunchKernelGGL(k_nb_decode<NL>, dim3((unsigned)gb), dim3(256), 0, s, buf, nbytes, nch, L, entry, offs, btot, \
+                       key, ts, val, rec_cap, wm_pos, wm_val, wm_cap, d_st)
+    if (wide) {
+        NB_LAUNCH(GW_MAX_ELEMENT);
+    } else {
+        NB_LAUNCH(64);
+    }
+#undef NB_LAUNCH
     return hipGetLastError();
 }
 

@@ -243,7 +243,7 @@ typedef struct gw_decode_result {
  * wm_val).  Elements are at most GW_MAX_ELEMENT bytes long including the length word.
  * Synchronous; allocates its own scratch.  GW_E_INVALID on a corrupt stream ("Corrupt
  * stream, found tag"), GW_E_OUTPUT_FULL if rec_cap / wm_cap are too small. */
-#define GW_MAX_ELEMENT 64
+#define GW_MAX_ELEMENT 128
 int  gw_decode_serialized(const void* d_bytes, int64_t nbytes, const gw_record_layout* layout,
                           int64_t* d_key, int64_t* d_ts, int64_t* d_value, int64_t rec_cap,
                           int64_t* d_wm_pos, int64_t* d_wm_val, int64_t wm_cap,

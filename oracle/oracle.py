@@ -90,8 +90,9 @@ def decode_stream(data: bytes, types: str, key_field: int, value_field: int = -1
 
 
 def build(force: bool = False) -> str:
-    src = os.path.join(_HERE, "flink_oracle.c")
-    if force or not os.path.exists(_LIB_PATH) or os.path.getmtime(_LIB_PATH) < os.path.getmtime(src):
+    deps = [os.path.join(_HERE, f) for f in ("flink_oracle.c", "flink_oracle.h", "Makefile")]
+    deps.append(os.path.join(os.path.dirname(_HERE), "include", "gpuwin.h"))
+    if force or not os.path.exists(_LIB_PATH) or os.path.getmtime(_LIB_PATH) < max(map(os.path.getmtime, deps)):
         subprocess.run(["make", "-C", _HERE, "-s"], check=True)
     return _LIB_PATH
 

@@ -93,7 +93,11 @@ def test_decode_errors():
     bad_tag = struct.pack(">i", 9) + bytes([9]) + b"\0" * 8
     assert gpu_decode(good + bad_tag + good, "JJ", 0, 1)[0] == -1
     assert gpu_decode(good + NB.record((1, 2, 3), "JJJ", 3), "JJ", 0, 1)[0] == -1
-    assert gpu_decode(good + NB.record(tuple(range(7)), "JJJJJJJ", 1) + good, "JJ", 0, 1)[0] == -2
+    assert gpu_decode(good + NB.record(tuple(range(7)), "JJJJJJJ", 1) + good, "JJ", 0, 1)[0] == -1
+    assert gpu_decode(good + NB.record(tuple(range(15)), "J" * 15, 1) + good, "JJ", 0, 1)[0] == -2
+    wide = NB.record(tuple(range(8)), "J" * 8, 3) * 300
+    assert gpu_decode(wide + NB.record(tuple(range(15)), "J" * 15, 1) + wide, "J" * 8, 0, 1)[0] == -2
+    assert gpu_decode(wide + NB.record((1, 2), "JJ", 3) + wide, "J" * 8, 0, 1)[0] == -1
     assert gpu_decode(good, "JJ", 0, 1, rec_cap=100)[0] == -5
     assert gpu_decode(good + NB.watermark(5) * 3, "JJ", 0, 1, wm_cap=2)[0] == -5
 

@@ -82,7 +82,9 @@ def random_elements(rng, n, types, key_field, value_field, p_wm=0.05, p_other=0.
     return b"".join(out)
 
 
-LAYOUTS = [("JJ", 0, 1), ("JD", 0, 1), ("IJJ", 1, 2), ("JI", 0, 1), ("SJFB", 1, 2), ("JZDJ", 0, 3), ("JJ", 1, -1)]
+# the last two: elements of 77 and 73 bytes (beyond 64: the two-candidates-per-lane walk)
+LAYOUTS = [("JJ", 0, 1), ("JD", 0, 1), ("IJJ", 1, 2), ("JI", 0, 1), ("SJFB", 1, 2), ("JZDJ", 0, 3), ("JJ", 1, -1),
+           ("JJJJJJJJ", 3, 7), ("IJJJJJJD", 1, 7)]
 
 
 @pytest.mark.parametrize("types,kf,vf", LAYOUTS)
@@ -115,8 +117,11 @@ def test_corrupt_and_unsupported(oracle_lib):
     bad_tag = struct.pack(">i", 9) + bytes([9]) + b"\0" * 8
     assert oracle_lib.decode_stream(good + bad_tag, "JJ", 0, 1)[0] == -1      # Corrupt stream, found tag
     assert oracle_lib.decode_stream(good + NB.record((1, 2, 3), "JJJ", 3), "JJ", 0, 1)[0] == -1  # length
-    too_long = NB.record(tuple(range(7)), "JJJJJJJ", 1)
-    assert oracle_lib.decode_stream(too_long, "JJJJJJJ", 0, 1)[0] == -2       # > GW_MAX_ELEMENT
+    too_long = NB.record(tuple(range(15)), "J" * 15, 1)                            # 133 bytes
+    assert oracle_lib.decode_stream(too_long, "JJ", 0, 1)[0] == -2            # > GW_MAX_ELEMENT
+    wide = NB.record(tuple(range(8)), "J" * 8, 1)                                 # 77 bytes
+    assert oracle_lib.decode_stream(wide, "J" * 8, 0, 1)[0] == 0
+    assert oracle_lib.decode_stream(wide, "JJ", 0, 1)[0] == -1                # length does not fit the layout
     assert oracle_lib.decode_stream(struct.pack(">i", 0), "JJ", 0, 1)[0] == -1
 
 
