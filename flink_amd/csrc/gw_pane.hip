@@ -910,10 +910,18 @@ __global__ void __launch_bounds__(kApplyThreads) GW_APPLY_ATTR k_rgn_apply(Inges
         r_src[threadIdx.x] = (uint32_t)(base0 + (d0 >> 16));
     }
     if (threadIdx.x < 4) s_kdirty[threadIdx.x] = 0;
+    // The LDS key array holds the keys' 64-bit hashes while the records apply (slot_hash is
+    // a bijection; a free slot holds the hash of the empty marker, a key that never lives
+    // in a normal slot): a compact record's word gives the hash without unhashing, and
+    // only the dirty key lines are unhashed on the way back.  (The first barrier of the run
+    // loop below orders this pass before any probe.)
+    const long long kEmptyH = (long long)slot_hash(kEmptyKey);
+    for (int j = threadIdx.x; j < (int)S; j += blockDim.x) lkeys[j] = (long long)slot_hash(lkeys[j]);
     unsigned long long ins = 0, flags = 0, spills = 0;
     // false: the region is full; the record stays in the buffer marked (pos | 0x80) and
     // k_rgn_collect parks it on the deferred list once the host has room for it
-    auto apply_one = [&](int64_t key, uint64_t h, int64_t c0, int64_t c1, uint32_t pos) -> bool {
+    auto apply_one = [&](uint64_t h, int64_t c0, int64_t c1, uint32_t pos) -> bool {
+        const long long key = (long long)h;
         // Probe one 4-key group (32 B) per step: the first slot holding the key or
         // empty, in slot order, decides; an empty slot is claimed with a CAS (a lost race
         // re-reads the same group).
@@ -926,16 +934,16 @@ __global__ void __launch_bounds__(kApplyThreads) GW_APPLY_ATTR k_rgn_apply(Inges
             const long2 k23 = *reinterpret_cast<const long2*>(&lkeys[g0 + 2]);
             const uint32_t hit = (uint32_t)(k01.x == key) | (uint32_t)(k01.y == key) << 1 |
                                  (uint32_t)(k23.x == key) << 2 | (uint32_t)(k23.y == key) << 3;
-            const uint32_t emp = (uint32_t)(k01.x == kEmptyKey) | (uint32_t)(k01.y == kEmptyKey) << 1 |
-                                 (uint32_t)(k23.x == kEmptyKey) << 2 | (uint32_t)(k23.y == kEmptyKey) << 3;
+            const uint32_t emp = (uint32_t)(k01.x == kEmptyH) | (uint32_t)(k01.y == kEmptyH) << 1 |
+                                 (uint32_t)(k23.x == kEmptyH) << 2 | (uint32_t)(k23.y == kEmptyH) << 3;
             const uint32_t m = hit | emp;
             if (m) {
                 const int i = __ffs((int)m) - 1;
                 const int j = g0 + i;
                 if ((hit >> i) & 1) { found = j; break; }
                 const unsigned long long prev = atomicCAS((unsigned long long*)&lkeys[j],
-                                                          (unsigned long long)kEmptyKey, (unsigned long long)key);
-                if (prev == (unsigned long long)kEmptyKey) {
+                                                          (unsigned long long)kEmptyH, (unsigned long long)key);
+                if (prev == (unsigned long long)kEmptyH) {
                     found = j;
                     ins++;
                     atomicOr(&s_kdirty[j >> 9], 1u << ((j >> 4) & 31));
@@ -1056,13 +1064,9 @@ __global__ void __launch_bounds__(kApplyThreads) GW_APPLY_ATTR k_rgn_apply(Inges
                 if (!c.ok[q]) continue;
                 if constexpr (C) {
                     const uint64_t h = cmp_hash((uint64_t)c.key[q], bucket_id, a.d1_bits);
-#ifdef GW_EXP_NO_UNHASH
-                    apply_one((int64_t)h, h, c.v0[q], c.v1[q], cmp_pos((uint64_t)c.key[q], a.d1_bits));
-#else
-                    apply_one(slot_unhash(h), h, c.v0[q], c.v1[q], cmp_pos((uint64_t)c.key[q], a.d1_bits));
-#endif
+                    apply_one(h, c.v0[q], c.v1[q], cmp_pos((uint64_t)c.key[q], a.d1_bits));
                 } else {
-                    apply_one(c.key[q], slot_hash(c.key[q]), c.v0[q], c.v1[q], c.ps[q]);
+                    apply_one(slot_hash(c.key[q]), c.v0[q], c.v1[q], c.ps[q]);
                 }
             }
         };
@@ -1103,7 +1107,6 @@ __global__ void __launch_bounds__(kApplyThreads) GW_APPLY_ATTR k_rgn_apply(Inges
                     if constexpr (C) {
                         h = cmp_hash((uint64_t)key, bucket_id, a.d1_bits);
                         pos = cmp_pos((uint64_t)key, a.d1_bits);
-                        key = slot_unhash(h);
                     } else {
                         pos = rpos[x];
                         h = slot_hash(key);
@@ -1112,8 +1115,8 @@ __global__ void __launch_bounds__(kApplyThreads) GW_APPLY_ATTR k_rgn_apply(Inges
                     int64_t g0 = pt_home(a.t, h);
                     for (int64_t p = 0; p < S; ++p) {
                         const long long kk = lkeys[g0];
-                        if (kk == key) { present = true; break; }
-                        if (kk == kEmptyKey) break;
+                        if (kk == (long long)h) { present = true; break; }
+                        if (kk == kEmptyH) break;
                         g0 = (g0 + 1) & (S - 1);
                     }
                     if (!present || ((int)pos != act0 && (int)pos != act1)) {
@@ -1133,7 +1136,10 @@ __global__ void __launch_bounds__(kApplyThreads) GW_APPLY_ATTR k_rgn_apply(Inges
         long2* dk = reinterpret_cast<long2*>(gkeys);
         for (int64_t w = threadIdx.x; w < S / 2; w += blockDim.x) {
             const int64_t line = w >> 3;
-            if (s_kdirty[line >> 5] & (1u << (line & 31))) dk[w] = sk[w];
+            if (s_kdirty[line >> 5] & (1u << (line & 31))) {
+                const long2 v = sk[w];
+                dk[w] = long2{slot_unhash((uint64_t)v.x), slot_unhash((uint64_t)v.y)};
+            }
         }
     }
     if constexpr (M) copy_words((long long*)gmask, (const long long*)lmask, MW);
