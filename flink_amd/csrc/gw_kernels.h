@@ -137,6 +137,13 @@ struct IngestArgs {
     int32_t b_pos;      // B mod R
     int32_t late_exact; // 0: t_late was clamped at Long.MIN_VALUE (then ts < t_late is a range error)
     PaneTable t;
+    // window class of a composite handle (gw_runtime.cpp, rings beyond kMaxRing): this
+    // operator holds the windows k = j (mod J) of slide `cls_slide`, offset `cls_off`; a late
+    // record is counted / side-output only by the class of its last window
+    int64_t cls_slide;
+    int64_t cls_off;
+    int32_t cls_J;      // 0 or 1: not a window class
+    int32_t cls_j;
     int64_t* d_key;     // deferred list (append at st->n_deferred)
     int64_t* d_pane;
     int64_t* d_a0;

@@ -66,6 +66,11 @@ __device__ __forceinline__ uint64_t presence_rt(const PaneTable& t, int64_t g) {
     return m;
 }
 
+__device__ __forceinline__ int64_t floor_div_d(int64_t a, int64_t b) {
+    const int64_t q = a / b;
+    return (a % b != 0 && ((a < 0) != (b < 0))) ? q - 1 : q;
+}
+
 // Per-record classification: late / parked (outside the pane ring) / in ring / re-fire
 // (allowed lateness > 0: the pane belongs to a fired window that is not cleaned yet).
 enum { REC_SKIP = 0, REC_RING = 1, REC_DEFER = 2, REC_REFIRE = 3, REC_LATE = 4 };
@@ -76,6 +81,13 @@ __device__ __forceinline__ int classify(const IngestArgs& a, int64_t ts, int64_t
     if (ts == INT64_MIN) { flags |= GW_DF_NO_TS; return REC_SKIP; }
     if (ts < a.t_late) {  // every window of the record is late: isSkippedElement && isElementLate
         if (!a.late_exact) { flags |= GW_DF_RANGE; return REC_SKIP; }
+        if (a.cls_J > 1) {  // window class: only the class of the record's last window reports it
+            // (wrapping subtraction: timestamps within |offset| of Long.MIN_VALUE wrap as in Java)
+            const int64_t k = floor_div_d((int64_t)((uint64_t)ts - (uint64_t)a.cls_off), a.cls_slide);
+            int64_t c = k % a.cls_J;
+            if (c < 0) c += a.cls_J;
+            if (c != a.cls_j) return REC_SKIP;
+        }
         if (a.lo_key) return REC_LATE;  // sideOutputLateData: the record goes to the side output
         late++;                         // numLateRecordsDropped (WindowOperator.java:440-446)
         return REC_SKIP;
@@ -1306,10 +1318,7 @@ __device__ __forceinline__ int64_t pt_find_ro(const PaneTable& t, int64_t key) {
     return -1;
 }
 
-__device__ __forceinline__ int64_t floor_div_d(int64_t a, int64_t b) {
-    const int64_t q = a / b;
-    return (a % b != 0 && ((a < 0) != (b < 0))) ? q - 1 : q;
-}
+
 
 constexpr int kRefireThreads = 64;
 template <int AGG>

@@ -137,6 +137,15 @@ struct gw_handle {
     std::string err;
     bool failed = false;
     hipStream_t stream = nullptr;
+    // Window-class composite (sliding windows whose pane ring exceeds kMaxRing): J child
+    // operators, child j holding the windows k = j (mod J) -- a sliding assigner of slide
+    // J * slide and offset offset + j * slide -- on one shared stream; rows gathered by
+    // gw_rows_device wait in c_* until drained.
+    std::vector<gw_handle*> kids;
+    bool shared_stream = false;      // the stream belongs to another handle
+    int64_t cls_J = 0, cls_j = 0, cls_slide = 0, cls_off = 0;  // a child's class
+    int64_t *c_key = nullptr, *c_start = nullptr, *c_end = nullptr, *c_res = nullptr;
+    int64_t c_cap = 0, c_rows = 0, c_head = 0;
     hipEvent_t ev_in = nullptr, ev_out = nullptr;  // gw_ingest_device ordering with the producer stream
 
     // network-buffer ingest (gw_ingest_serialized*): grow-only device scratch, decoded
@@ -903,6 +912,7 @@ struct gw_handle {
         a.b_pos = (int32_t)pos_of(B);
         a.late_exact = exact;
         a.t = tv;
+        a.cls_J = (int32_t)cls_J; a.cls_j = (int32_t)cls_j; a.cls_slide = cls_slide; a.cls_off = cls_off;
         a.d_key = dk[cur]; a.d_pane = dp[cur]; a.d_a0 = da0[cur]; a.d_a1 = da1[cur];
         a.st = d_st;
         // panes up to the last one of the last fired window re-fire (lateness > 0)
@@ -1703,6 +1713,61 @@ static int validate(const gw_config* c, std::string& why) {
     return GW_OK;
 }
 
+// Ring positions a sliding (or tumbling: slide = size) assigner needs: the n panes of the
+// oldest unfired window + at least one slide ahead, plus, with allowed lateness, the panes
+// of fired windows kept until their cleanup (ceil(lateness / slide) + 1 more slides).
+static int64_t ring_need(int64_t size, int64_t slide, int64_t lateness) {
+    const int64_t g = gcd64(size, slide), m = slide / g, n = size / g;
+    if (n > kMaxRing || m > kMaxRing) return kMaxRing + 1;
+    int64_t need = n + std::max<int64_t>(m, 1);
+    if (lateness > 0) {
+        const int64_t extra = lateness / slide + 2;
+        if (extra > kMaxRing || need + extra * m > kMaxRing) return kMaxRing + 1;
+        need += extra * m;
+    }
+    return need;
+}
+// The fewest window classes J whose assigner (size, J * slide) fits the ring, 0 if none
+// below 4096 does (or J * slide overflows).
+static int64_t class_count(int64_t size, int64_t slide, int64_t lateness) {
+    for (int64_t J = 2; J <= 4096; ++J) {
+        if (slide > INT64_MAX / J) return 0;
+        if (ring_need(size, slide * J, lateness) <= kMaxRing) return J;
+    }
+    return 0;
+}
+// A composite handle h (its cfg set): J children on child 0's stream.
+static int make_composite(gw_handle* h, int64_t J) {
+    const gw_config& c = h->cfg;
+    if (h->stream) {  // the composite launches nothing of its own
+        hipStreamSynchronize(h->stream);
+        hipStreamDestroy(h->stream);
+        h->stream = nullptr;
+    }
+    for (int64_t j = 0; j < J; ++j) {
+        gw_config k = c;
+        k.slide = c.slide * J;
+        k.offset = c.offset + j * c.slide;  // in (-slide, J * slide): |offset'| < slide'
+        gw_handle* kid = nullptr;
+        int rc = gw_create(&k, &kid);
+        if (rc) return rc;
+        kid->cls_J = J;
+        kid->cls_j = j;
+        kid->cls_slide = c.slide;
+        kid->cls_off = c.offset;
+        if (j > 0) {  // one stream for all: the children's launches stay in issue order
+            hipStreamSynchronize(kid->stream);
+            hipStreamDestroy(kid->stream);
+            kid->stream = h->kids[0]->stream;
+            kid->shared_stream = true;
+        }
+        h->kids.push_back(kid);
+    }
+    h->stream = h->kids[0]->stream;
+    h->shared_stream = true;
+    return GW_OK;
+}
+
 int gw_create(const gw_config* cfg, gw_handle** out) {
     if (!cfg || !out) { g_create_error = "null argument"; return GW_E_INVALID; }
     *out = nullptr;
@@ -1768,18 +1833,20 @@ int gw_create(const gw_config* cfg, gw_handle** out) {
     h->n = size / h->g;
     // ring: n panes of the oldest unfired window + at least one pane ahead, filling
     // the slot up to the next 64-byte line
-    int64_t need = h->n + std::max<int64_t>(h->m, 1);
-    if (need > kMaxRing)
-        return bail(GW_E_UNSUPPORTED, "size/gcd(size,slide) + slide/gcd(size,slide) > 64 panes is not supported "
-                                      "on the GPU path");
-    if (cfg->allowed_lateness > 0) {
-        // the panes of fired windows stay until their cleanup: ceil(lateness / slide) + 1
-        // more slides of the ring
-        const int64_t extra = cfg->allowed_lateness / slide + 2;
-        if (extra > kMaxRing || need + extra * h->m > kMaxRing)
-            return bail(GW_E_UNSUPPORTED, "allowed lateness spanning more than 64 panes of the ring is not "
-                                          "supported on the GPU path");
-        need += extra * h->m;
+    int64_t need = ring_need(size, slide, cfg->allowed_lateness);
+    if (need > kMaxRing) {
+        // more panes than one ring holds: split the windows into J classes (k mod J), each a
+        // sliding assigner of slide J * slide whose ring fits (gcd(size, J * slide) grows)
+        const int64_t J = cfg->assigner == GW_SLIDING ? class_count(size, slide, cfg->allowed_lateness) : 0;
+        if (J == 0)
+            return bail(GW_E_UNSUPPORTED, cfg->allowed_lateness > 0
+                                              ? "allowed lateness spanning more than 64 panes of the ring is not "
+                                                "supported on the GPU path"
+                                              : "no split of the windows into classes fits a ring of 64 panes");
+        rc = make_composite(h, J);
+        if (rc) return bail(rc, g_create_error);
+        *out = h;
+        return GW_OK;
     }
     int stride_w = (int)(((2 + need * words) + 7) / 8 * 8);
     int R = (stride_w - 2) / words;
@@ -1804,6 +1871,12 @@ int gw_create(const gw_config* cfg, gw_handle** out) {
 
 int gw_destroy(gw_handle* h) {
     if (!h) return GW_OK;
+    if (!h->kids.empty()) {
+        for (size_t j = h->kids.size(); j-- > 0;) gw_destroy(h->kids[j]);  // child 0 owns the stream
+        h->kids.clear();
+        h->stream = nullptr;
+        if (h->c_key) { hipFree(h->c_key); hipFree(h->c_start); hipFree(h->c_end); hipFree(h->c_res); }
+    }
     h->hp.dump();
     if (h->stream) hipStreamSynchronize(h->stream);
     if (h->sess) session_destroy(h->sess);
@@ -1840,7 +1913,7 @@ int gw_destroy(gw_handle* h) {
     if (h->d_nbbytes) hipFree(h->d_nbbytes);
     if (h->ev_in) hipEventDestroy(h->ev_in);
     if (h->ev_out) hipEventDestroy(h->ev_out);
-    if (h->stream) hipStreamDestroy(h->stream);
+    if (h->stream && !h->shared_stream) hipStreamDestroy(h->stream);
     delete h;
     return GW_OK;
 }
@@ -1862,9 +1935,26 @@ static int ingest_device_impl(gw_handle* h, int64_t n, const int64_t* key, const
     return GW_OK;
 }
 
+// ---- window-class composite: every call goes to each child, results are combined ----
+static int kid_rc(gw_handle* h, gw_handle* kid, int rc) {
+    return rc == GW_OK ? GW_OK : h->fail(rc, "%s", kid->err.c_str());
+}
+#define FOR_KIDS(call)                                                                   \
+    do {                                                                                 \
+        for (gw_handle* k_ : h->kids) {                                                  \
+            gw_handle* kid = k_;                                                         \
+            const int rc_ = (call);                                                      \
+            if (rc_ != GW_OK && rc_ != GW_E_OUTPUT_FULL) return kid_rc(h, kid, rc_);      \
+        }                                                                                \
+    } while (0)
+
 int gw_ingest(gw_handle* h, int64_t n, const int64_t* key, const int32_t* key_hash, const int64_t* ts,
               const void* value) {
     if (!h) return GW_E_INVALID;
+    if (!h->kids.empty()) {
+        FOR_KIDS(gw_ingest(kid, n, key, key_hash, ts, value));
+        return GW_OK;
+    }
     if (h->failed) return h->fail(GW_E_STATE, "operator failed earlier: %s", h->err.c_str());
     if (n < 0 || (n > 0 && (!key || !ts))) return h->fail(GW_E_INVALID, "null key/ts column");
     if (n > 0 && !value && h->cfg.agg != GW_COUNT) return h->fail(GW_E_INVALID, "value column required");
@@ -1903,6 +1993,10 @@ int gw_ingest(gw_handle* h, int64_t n, const int64_t* key, const int32_t* key_ha
 int gw_ingest_device(gw_handle* h, int64_t n, const int64_t* d_key, const int32_t* d_key_hash,
                      const int64_t* d_ts, const void* d_value, void* stream) {
     if (!h) return GW_E_INVALID;
+    if (!h->kids.empty()) {  // the children share one stream: order after the producer once
+        FOR_KIDS(gw_ingest_device(kid, n, d_key, d_key_hash, d_ts, d_value, stream));
+        return GW_OK;
+    }
     h->hp.mark();
     if (h->failed) return h->fail(GW_E_STATE, "operator failed earlier: %s", h->err.c_str());
     if (n < 0 || (n > 0 && (!d_key || !d_ts))) return h->fail(GW_E_INVALID, "null key/ts column");
@@ -2097,6 +2191,17 @@ static int nb_ingest_on_stream(gw_handle* h, const uint8_t* d_bytes, int64_t nby
 int gw_ingest_serialized_device(gw_handle* h, const void* d_bytes, int64_t nbytes, const gw_record_layout* layout,
                                 void* stream, int64_t* consumed, int64_t* rows_fired) {
     if (!h) return GW_E_INVALID;
+    if (!h->kids.empty()) {  // each child decodes the channel (same bytes consumed by all)
+        int64_t sum = 0;
+        for (gw_handle* kid : h->kids) {
+            int64_t f = 0;
+            const int rc = gw_ingest_serialized_device(kid, d_bytes, nbytes, layout, stream, consumed, &f);
+            if (rc) return kid_rc(h, kid, rc);
+            sum += f;
+        }
+        if (rows_fired) *rows_fired = sum;
+        return GW_OK;
+    }
     if (h->failed) return h->fail(GW_E_STATE, "operator failed earlier: %s", h->err.c_str());
     NbLayout L{};
     std::string why;
@@ -2120,6 +2225,17 @@ int gw_ingest_serialized_device(gw_handle* h, const void* d_bytes, int64_t nbyte
 int gw_ingest_serialized(gw_handle* h, const void* bytes, int64_t nbytes, const gw_record_layout* layout,
                          int64_t* consumed, int64_t* rows_fired) {
     if (!h) return GW_E_INVALID;
+    if (!h->kids.empty()) {
+        int64_t sum = 0;
+        for (gw_handle* kid : h->kids) {
+            int64_t f = 0;
+            const int rc = gw_ingest_serialized(kid, bytes, nbytes, layout, consumed, &f);
+            if (rc) return kid_rc(h, kid, rc);
+            sum += f;
+        }
+        if (rows_fired) *rows_fired = sum;
+        return GW_OK;
+    }
     if (h->failed) return h->fail(GW_E_STATE, "operator failed earlier: %s", h->err.c_str());
     NbLayout L{};
     std::string why;
@@ -2150,6 +2266,18 @@ int gw_ingest_serialized(gw_handle* h, const void* bytes, int64_t nbytes, const 
 
 int gw_advance_watermark(gw_handle* h, int64_t wm, int64_t* rows_fired) {
     if (!h) return GW_E_INVALID;
+    if (!h->kids.empty()) {
+        int64_t sum = 0;
+        for (gw_handle* kid : h->kids) {
+            int64_t f = 0;
+            const int rc = gw_advance_watermark(kid, wm, &f);
+            if (rc) return kid_rc(h, kid, rc);
+            sum += f;
+        }
+        h->stats.rows_fired += sum;
+        if (rows_fired) *rows_fired = sum;
+        return GW_OK;
+    }
     if (h->failed) return h->fail(GW_E_STATE, "operator failed earlier: %s", h->err.c_str());
     hipSetDevice(h->cfg.device);
     if (h->session) {
@@ -2169,6 +2297,10 @@ int gw_advance_watermark(gw_handle* h, int64_t wm, int64_t* rows_fired) {
 
 int gw_flush(gw_handle* h) {
     if (!h) return GW_E_INVALID;
+    if (!h->kids.empty()) {
+        FOR_KIDS(gw_flush(kid));
+        return GW_OK;
+    }
     if (h->failed) return h->fail(GW_E_STATE, "operator failed earlier: %s", h->err.c_str());
     if (h->session) return GW_OK;
     hipSetDevice(h->cfg.device);
@@ -2179,6 +2311,9 @@ int gw_flush(gw_handle* h) {
 
 int gw_snapshot(gw_handle* h, int32_t kg_lo, int32_t kg_hi, void* buf, int64_t cap, int64_t* len) {
     if (!h || !len) return GW_E_INVALID;
+    if (!h->kids.empty())
+        return h->fail(GW_E_UNSUPPORTED, "snapshot of sliding windows split into %d window classes (a pane ring "
+                                         "beyond 64 panes) is not supported yet", (int)h->kids.size());
     if (h->failed) return h->fail(GW_E_STATE, "operator failed earlier: %s", h->err.c_str());
     if (h->foreign_hash)
         return h->fail(GW_E_UNSUPPORTED, "snapshot of a handle that ingested a key_hash different from "
@@ -2190,6 +2325,9 @@ int gw_snapshot(gw_handle* h, int32_t kg_lo, int32_t kg_hi, void* buf, int64_t c
 
 int gw_restore(gw_handle* h, const void* buf, int64_t len) {
     if (!h) return GW_E_INVALID;
+    if (!h->kids.empty())
+        return h->fail(GW_E_UNSUPPORTED, "restore into sliding windows split into %d window classes (a pane ring "
+                                         "beyond 64 panes) is not supported yet", (int)h->kids.size());
     if (h->failed) return h->fail(GW_E_STATE, "operator failed earlier: %s", h->err.c_str());
     hipSetDevice(h->cfg.device);
     if (h->session) return h->restore_sessions(buf, len);
@@ -2253,6 +2391,17 @@ static void rows_view(gw_handle* h, int64_t** k, int64_t** s, int64_t** e, int64
 
 int gw_pending_rows(gw_handle* h, int64_t* n) {
     if (!h || !n) return GW_E_INVALID;
+    if (!h->kids.empty()) {
+        int64_t sum = h->c_rows - h->c_head;
+        for (gw_handle* kid : h->kids) {
+            int64_t p = 0;
+            const int rc = gw_pending_rows(kid, &p);
+            if (rc) return kid_rc(h, kid, rc);
+            sum += p;
+        }
+        *n = sum;
+        return GW_OK;
+    }
     int rc = h->session ? session_refresh(h->sess, h->err) : h->refresh();
     if (rc) return rc;
     int64_t *k, *s, *e, *r, total;
@@ -2264,6 +2413,38 @@ int gw_pending_rows(gw_handle* h, int64_t* n) {
 int gw_drain(gw_handle* h, int64_t* key, int64_t* start, int64_t* end, void* result, int64_t cap,
              int64_t* n) {
     if (!h || !n) return GW_E_INVALID;
+    if (!h->kids.empty()) {  // the gathered rows first, then each child's
+        int64_t got = 0;
+        auto at = [&](int64_t* p) { return p ? p + got : nullptr; };
+        const int64_t c = std::min(cap, h->c_rows - h->c_head);
+        if (c > 0) {
+            hipError_t e = hipSuccess;
+            const int64_t o = h->c_head;
+            if (key) e = hipMemcpyAsync(key, h->c_key + o, c * 8, hipMemcpyDeviceToHost, h->stream);
+            if (start && e == hipSuccess) e = hipMemcpyAsync(start, h->c_start + o, c * 8, hipMemcpyDeviceToHost, h->stream);
+            if (end && e == hipSuccess) e = hipMemcpyAsync(end, h->c_end + o, c * 8, hipMemcpyDeviceToHost, h->stream);
+            if (result && e == hipSuccess)
+                e = hipMemcpyAsync(result, h->c_res + o, c * 8, hipMemcpyDeviceToHost, h->stream);
+            if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+            if (e != hipSuccess) return h->fail(GW_E_DEVICE, "D2H rows: %s", hipGetErrorString(e));
+            h->c_head += c;
+            got += c;
+            if (h->c_head == h->c_rows) h->c_head = h->c_rows = 0;
+        }
+        for (gw_handle* kid : h->kids) {
+            if (got == cap) break;
+            int64_t g = 0;
+            const int rc = gw_drain(kid, at(key), at(start), at(end), result ? (void*)((int64_t*)result + got) : nullptr,
+                                    cap - got, &g);
+            if (rc && rc != GW_E_OUTPUT_FULL) return kid_rc(h, kid, rc);
+            got += g;
+        }
+        *n = got;
+        int64_t left = 0;
+        const int rc = gw_pending_rows(h, &left);
+        if (rc) return rc;
+        return left ? GW_E_OUTPUT_FULL : GW_OK;
+    }
     int64_t pending;
     int rc = gw_pending_rows(h, &pending);
     if (rc) return rc;
@@ -2292,6 +2473,56 @@ int gw_drain(gw_handle* h, int64_t* key, int64_t* start, int64_t* end, void* res
 int gw_rows_device(gw_handle* h, const int64_t** d_key, const int64_t** d_start, const int64_t** d_end,
                    const void** d_result, int64_t* n) {
     if (!h) return GW_E_INVALID;
+    if (!h->kids.empty()) {  // gather the children's pending rows behind the waiting ones
+        int64_t add = 0;
+        for (gw_handle* kid : h->kids) {
+            int64_t p = 0;
+            const int rc = gw_pending_rows(kid, &p);
+            if (rc) return kid_rc(h, kid, rc);
+            add += p;
+        }
+        if (h->c_rows + add > h->c_cap) {
+            const int64_t cap = std::max<int64_t>(h->c_rows + add, 2 * h->c_cap);
+            int64_t* nb[4] = {nullptr, nullptr, nullptr, nullptr};
+            for (int q = 0; q < 4; ++q) {
+                hipError_t e = hipMalloc((void**)&nb[q], (size_t)cap * 8);
+                if (e != hipSuccess) {
+                    for (int r = 0; r < q; ++r) hipFree(nb[r]);
+                    return h->fail(GW_E_OOM, "composite row buffer: %s", hipGetErrorString(e));
+                }
+            }
+            int64_t* old[4] = {h->c_key, h->c_start, h->c_end, h->c_res};
+            const int64_t live = h->c_rows - h->c_head;
+            for (int q = 0; q < 4; ++q) {
+                if (old[q] && live) hipMemcpyAsync(nb[q], old[q] + h->c_head, live * 8, hipMemcpyDeviceToDevice, h->stream);
+                if (old[q]) { hipStreamSynchronize(h->stream); hipFree(old[q]); }
+            }
+            h->c_key = nb[0]; h->c_start = nb[1]; h->c_end = nb[2]; h->c_res = nb[3];
+            h->c_cap = cap;
+            h->c_rows = live;
+            h->c_head = 0;
+        }
+        for (gw_handle* kid : h->kids) {
+            const int64_t* k[4];
+            int64_t p = 0;
+            int rc = gw_rows_device(kid, &k[0], &k[1], &k[2], (const void**)&k[3], &p);
+            if (rc) return kid_rc(h, kid, rc);
+            int64_t* dst[4] = {h->c_key, h->c_start, h->c_end, h->c_res};
+            for (int q = 0; q < 4 && p > 0; ++q) {
+                hipError_t e = hipMemcpyAsync(dst[q] + h->c_rows, k[q], p * 8, hipMemcpyDeviceToDevice, h->stream);
+                if (e != hipSuccess) return h->fail(GW_E_DEVICE, "gather rows: %s", hipGetErrorString(e));
+            }
+            h->c_rows += p;
+            if ((rc = gw_clear_rows(kid))) return kid_rc(h, kid, rc);
+        }
+        const int64_t o = h->c_head;
+        if (d_key) *d_key = h->c_key ? h->c_key + o : nullptr;
+        if (d_start) *d_start = h->c_start ? h->c_start + o : nullptr;
+        if (d_end) *d_end = h->c_end ? h->c_end + o : nullptr;
+        if (d_result) *d_result = h->c_res ? h->c_res + o : nullptr;
+        if (n) *n = h->c_rows - h->c_head;
+        return GW_OK;
+    }
     int64_t pending;
     int rc = gw_pending_rows(h, &pending);
     if (rc) return rc;
@@ -2308,6 +2539,11 @@ int gw_rows_device(gw_handle* h, const int64_t** d_key, const int64_t** d_start,
 
 int gw_clear_rows(gw_handle* h) {
     if (!h) return GW_E_INVALID;
+    if (!h->kids.empty()) {
+        h->c_rows = h->c_head = 0;
+        FOR_KIDS(gw_clear_rows(kid));
+        return GW_OK;
+    }
     h->rows_head = 0;
     if (h->session) return session_clear_rows(h->sess, h->err);
     if (h->h_st->rows == 0) return GW_OK;  // rows only grow in a fire, which refreshes h_st
@@ -2317,6 +2553,15 @@ int gw_clear_rows(gw_handle* h) {
 int gw_pending_late(gw_handle* h, int64_t* n) {
     if (!h || !n) return GW_E_INVALID;
     *n = 0;
+    if (!h->kids.empty()) {
+        for (gw_handle* kid : h->kids) {
+            int64_t p = 0;
+            const int rc = gw_pending_late(kid, &p);
+            if (rc) return kid_rc(h, kid, rc);
+            *n += p;
+        }
+        return GW_OK;
+    }
     if (!(h->cfg.flags & GW_FLAG_LATE_SIDE_OUTPUT)) return GW_OK;
     if (h->session) return session_pending_late(h->sess, n, h->err);
     int rc = h->refresh();
@@ -2328,6 +2573,22 @@ int gw_pending_late(gw_handle* h, int64_t* n) {
 int gw_drain_late(gw_handle* h, int64_t* key, int64_t* ts, void* value, int64_t cap, int64_t* n) {
     if (!h || !n) return GW_E_INVALID;
     *n = 0;
+    if (!h->kids.empty()) {  // each late record is reported by one child (its last window's class)
+        int64_t got = 0;
+        for (gw_handle* kid : h->kids) {
+            if (got == cap) break;
+            int64_t g = 0;
+            const int rc = gw_drain_late(kid, key ? key + got : nullptr, ts ? ts + got : nullptr,
+                                         value ? (void*)((int64_t*)value + got) : nullptr, cap - got, &g);
+            if (rc && rc != GW_E_OUTPUT_FULL) return kid_rc(h, kid, rc);
+            got += g;
+        }
+        *n = got;
+        int64_t left = 0;
+        const int rc = gw_pending_late(h, &left);
+        if (rc) return rc;
+        return left ? GW_E_OUTPUT_FULL : GW_OK;
+    }
     if (!(h->cfg.flags & GW_FLAG_LATE_SIDE_OUTPUT)) return GW_OK;
     hipSetDevice(h->cfg.device);
     if (h->session) return session_drain_late(h->sess, key, ts, (int64_t*)value, cap, n, h->err);
@@ -2355,12 +2616,37 @@ int gw_drain_late(gw_handle* h, int64_t* key, int64_t* ts, void* value, int64_t 
 
 int64_t gw_late_dropped(const gw_handle* h) {
     if (!h) return 0;
+    if (!h->kids.empty()) {
+        int64_t sum = 0;
+        for (const gw_handle* kid : h->kids) sum += gw_late_dropped(kid);
+        return sum;
+    }
     if (h->session) return session_late(h->sess);
     return (int64_t)h->h_st->late;
 }
 
 int gw_get_stats(const gw_handle* h, gw_stats* out) {
     if (!h || !out) return GW_E_INVALID;
+    if (!h->kids.empty()) {  // records: as one operator sees them; state: summed over the classes
+        gw_stats t{};
+        for (size_t j = 0; j < h->kids.size(); ++j) {
+            gw_stats k{};
+            gw_get_stats(h->kids[j], &k);
+            if (j == 0) { t.events_in = k.events_in; t.batches = k.batches; }
+            t.late_dropped += k.late_dropped;
+            t.rows_fired += k.rows_fired;
+            t.live_keys = std::max(t.live_keys, k.live_keys);
+            t.table_capacity += k.table_capacity;
+            t.table_bytes += k.table_bytes;
+            t.deferred += k.deferred;
+            t.fires += k.fires;
+            t.rehashes += k.rehashes;
+            t.preagg_batches += k.preagg_batches;
+            t.applies += k.applies;
+        }
+        *out = t;
+        return GW_OK;
+    }
     *out = h->stats;
     if (h->session) {
         session_stats(h->sess, out);
@@ -2376,6 +2662,10 @@ int gw_get_stats(const gw_handle* h, gw_stats* out) {
 
 int gw_synchronize(gw_handle* h) {
     if (!h) return GW_E_INVALID;
+    if (!h->kids.empty()) {
+        FOR_KIDS(gw_synchronize(kid));
+        return GW_OK;
+    }
     hipError_t e = hipStreamSynchronize(h->stream);
     if (e != hipSuccess) return h->fail(GW_E_DEVICE, "sync: %s", hipGetErrorString(e));
     return GW_OK;
@@ -2385,6 +2675,7 @@ void* gw_stream(gw_handle* h) { return h ? (void*)h->stream : nullptr; }
 
 int gw_enable_kernel_timing(gw_handle* h, int enable) {
     if (!h) return GW_E_INVALID;
+    for (gw_handle* kid : h->kids) gw_enable_kernel_timing(kid, enable);
     h->timing = enable != 0;
     if (h->sess) session_enable_timing(h->sess, h->timing);
     return GW_OK;
@@ -2392,6 +2683,20 @@ int gw_enable_kernel_timing(gw_handle* h, int enable) {
 
 int gw_kernel_time_ms(gw_handle* h, int which, double* ms, int64_t* launches) {
     if (!h) return GW_E_INVALID;
+    if (!h->kids.empty()) {  // per launch of child 0: the classes' device time together
+        double total = 0;
+        int64_t l0 = 0;
+        for (size_t j = 0; j < h->kids.size(); ++j) {
+            double m = 0;
+            int64_t l = 0;
+            gw_kernel_time_ms(h->kids[j], which, &m, &l);
+            total += m * (double)l;
+            if (j == 0) l0 = l;
+        }
+        if (ms) *ms = l0 ? total / (double)l0 : 0.0;
+        if (launches) *launches = l0;
+        return GW_OK;
+    }
     hipStreamSynchronize(h->stream);
     if (h->sess) return session_kernel_time(h->sess, which, ms, launches);
     KernelTimer& t = which == 0 ? h->t_ingest : which == 1 ? h->t_fire : h->t_apply;

@@ -1,0 +1,142 @@
+"""Sliding windows whose pane ring exceeds 64 positions (size/gcd + slide/gcd > 64, or allowed
+lateness spanning more panes than the ring holds): the handle splits the windows into J
+classes k = j (mod J), each an operator with slide J * slide and offset offset + j * slide
+(gw_runtime.cpp make_composite), and combines their rows, late counts and side outputs.
+
+Parity against the oracle, which keeps one state per (key, window) as the reference's
+WindowOperator does (WindowOperator.java:293-494; SlidingEventTimeWindows.assignWindows
+:77-90 assigns size/slide windows per record).  A late record is counted (or side-output)
+once: by the class of its last window, the one whose lateness decides the reference's
+isSkippedElement && isElementLate (WindowOperator.java:440-446)."""
+import ctypes
+import zlib
+
+import numpy as np
+import pytest
+
+from flink_amd import _native as N
+from tests.gpu_helpers import compare, gpu_operator, random_stream, run_gpu, run_oracle
+
+pytestmark = pytest.mark.gpu
+
+DOUBLE = {"sum_f64", "avg_f64", "avg_i64", "min_f64", "max_f64"}
+
+CONFIGS = [
+    dict(assigner="sliding", size=1000, slide=10),                 # n = 100: 2 classes
+    dict(assigner="sliding", size=7000, slide=60, offset=-25),     # gcd 20, n = 350: 10 classes
+    dict(assigner="sliding", size=3000, slide=40),                 # n = 75: 2 classes
+    dict(assigner="sliding", size=1000, slide=100, lateness=10_000),  # lateness over 102 panes
+]
+
+
+def _classes(kw):
+    size, slide, lat = kw["size"], kw["slide"], kw.get("lateness", 0)
+
+    def need(sl):
+        g = np.gcd(size, sl)
+        n, m = size // g, sl // g
+        r = n + max(m, 1)
+        if lat:
+            extra = lat // sl + 2
+            r += extra * m
+        return r
+
+    if need(slide) <= 64:
+        return 1
+    return next(J for J in range(2, 4097) if need(slide * J) <= 64)
+
+
+@pytest.mark.parametrize("agg", ["sum_i64", "count", "max_i64", "avg_f64", "sum_f64"])
+@pytest.mark.parametrize("kw", CONFIGS, ids=lambda c: "-".join(str(v) for v in c.values()))
+@pytest.mark.parametrize("flags", [0, N.FLAG_FORCE_REGION], ids=["auto", "region"])
+def test_window_classes_vs_oracle(oracle_lib, kw, agg, flags):
+    kw = dict(kw, agg=agg)
+    assert _classes(kw) > 1
+    lat = kw.get("lateness", 0)
+    keys, ts, vals, batches = random_stream(seed=zlib.crc32(f"wc{kw}".encode()) & 0xffff, n=12000, num_keys=60,
+                                            n_batches=24, ts_step=3, disorder=600 if lat else 250,
+                                            wm_lag=250, agg=agg)
+    g, glate, stats = run_gpu(kw, keys, ts, vals, batches, flags=flags)
+    o, olate = run_oracle(oracle_lib, kw, keys, ts, vals, batches)
+    assert glate == olate
+    assert compare(g, o, agg in DOUBLE) == []
+    assert stats["events_in"] == len(keys)
+    if lat:
+        assert glate > 0 or sum(len(x[0]) for x in o) > 0
+
+
+def test_window_classes_side_output(oracle_lib):
+    """Each late record reaches the side output once, from the class of its last window."""
+    kw = dict(assigner="sliding", size=1000, slide=10, agg="sum_i64")
+    o = oracle_lib
+    keys, ts, vals, batches = random_stream(seed=91, n=15000, num_keys=50, n_batches=25, ts_step=3,
+                                            disorder=3000, wm_lag=200)
+    op = gpu_operator(kw, flags=N.FLAG_LATE_SIDE_OUTPUT)
+    ora = o.OracleOperator(o.make_config(**kw, flags=N.FLAG_LATE_SIDE_OUTPUT))
+    n_side = 0
+    for b, (lo, hi, wm) in enumerate(batches):
+        op.process_batch(keys[lo:hi], ts[lo:hi], vals[lo:hi])
+        op.advance_watermark(wm)
+        ora.process_batch(keys[lo:hi], ts[lo:hi], vals[lo:hi])
+        ora.process_watermark(wm)
+        k, s, e, r = op.drain()
+        assert compare([(k, s, e, r.view(np.int64))], [ora.drain()], False) == [], f"rows at watermark #{b}"
+        got = sorted(zip(*[c.tolist() for c in op.drain_late()]))
+        exp = sorted(zip(*[c.tolist() for c in ora.drain_late()]))
+        assert got == exp, f"side output at watermark #{b}"
+        n_side += len(exp)
+    assert n_side > 0 and op.num_late_records_dropped == 0
+    op.close()
+    ora.close()
+
+
+def _d2h(ptr, n):
+    """n int64 words at a device pointer -> numpy (hipMemcpy of the runtime torch loaded)."""
+    import torch  # noqa: F401  (one HIP runtime per process: torch's)
+    hip = ctypes.CDLL("libamdhip64.so.7")
+    out = np.empty(n, np.int64)
+    if n:
+        assert hip.hipMemcpy(ctypes.c_void_p(out.ctypes.data), ctypes.c_void_p(ptr), ctypes.c_size_t(n * 8), 2) == 0
+    return out
+
+
+def test_window_classes_rows_device_and_stats(oracle_lib):
+    """gw_rows_device gathers the classes' rows into one device view (what a device-side
+    consumer reads); gw_drain then returns the same rows; stats count each record once."""
+    kw = dict(assigner="sliding", size=2000, slide=20, agg="count")
+    keys, ts, vals, batches = random_stream(seed=5, n=8000, num_keys=30, n_batches=8, ts_step=5, disorder=100,
+                                            wm_lag=150, agg="count")
+    op = gpu_operator(kw)
+    got = []
+    for lo, hi, wm in batches:
+        op.process_batch(keys[lo:hi], ts[lo:hi], None)
+        op.advance_watermark(wm)
+        ptrs, n = op.rows_device()
+        op.synchronize()
+        view = [_d2h(p, n) for p in ptrs]
+        k, s, e, r = op.drain()
+        assert len(k) == n
+        a = np.lexsort((view[2], view[1], view[0]))
+        b = np.lexsort((e, s, k))
+        for x, y in zip(view, (k, s, e, r.view(np.int64))):
+            assert np.array_equal(x[a], y[b])
+        got.append((k, s, e, r.view(np.int64)))
+    o, _ = run_oracle(oracle_lib, kw, keys, ts, vals, batches, final_wm=None)
+    assert compare(got, o, False) == []
+    assert op.stats()["events_in"] == len(keys)
+    op.close()
+
+
+def test_window_classes_snapshot_unsupported():
+    op = gpu_operator(dict(assigner="sliding", size=1000, slide=10, agg="sum_i64"))
+    op.process_batch(np.array([1, 2], np.int64), np.array([5, 9], np.int64), np.array([3, 4], np.int64))
+    with pytest.raises(N.GpuWinError) as ei:
+        op.snapshot_state()
+    assert ei.value.code == -2
+    op.close()
+
+
+def test_tumbling_lateness_beyond_the_ring_is_unsupported():
+    with pytest.raises(N.GpuWinError) as ei:
+        gpu_operator(dict(assigner="tumbling", size=100, agg="sum_i64", lateness=10_000))
+    assert ei.value.code == -2
