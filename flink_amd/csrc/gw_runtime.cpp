@@ -16,6 +16,7 @@
 #include <cstring>
 #include <new>
 #include <string>
+#include <tuple>
 #include <vector>
 
 #include "gw_kernels.h"
@@ -2309,11 +2310,141 @@ int gw_flush(gw_handle* h) {
     return rc ? rc : h->flush_buffer();
 }
 
+// Window-class composite snapshots: the children's heap-layout blobs merged per key group
+// (their (window, key, state) entries and timers are disjoint by window), under the
+// composite's own assigner header; restore splits each key group's entries and timers by
+// the class of their window.  Layout per key group (snapshot_heap): be32 n + n entries of
+// (start, end, key, state), be32 0 (no merging window set), be32 t + t timers of 32 bytes.
+typedef gw_handle::SnapHeader SnapHdr;
+static int comp_snapshot(gw_handle* h, int32_t kg_lo, int32_t kg_hi, void* buf, int64_t cap, int64_t* len) {
+    const int64_t nk = (int64_t)kg_hi - kg_lo + 1;
+    if (kg_lo < 0 || nk <= 0) return h->fail(GW_E_INVALID, "bad key-group range");
+    const int64_t eb = 24 + h->kids[0]->acc_bytes();
+    std::vector<std::vector<uint8_t>> blobs(h->kids.size());
+    for (size_t j = 0; j < h->kids.size(); ++j) {
+        int64_t l = 0;
+        int rc = gw_snapshot(h->kids[j], kg_lo, kg_hi, nullptr, 0, &l);
+        if (rc) return kid_rc(h, h->kids[j], rc);
+        blobs[j].resize((size_t)l);
+        if ((rc = gw_snapshot(h->kids[j], kg_lo, kg_hi, blobs[j].data(), l, &l))) return kid_rc(h, h->kids[j], rc);
+    }
+    std::vector<uint8_t> pay;
+    std::vector<int64_t> offs(nk + 1, 0);
+    const int64_t hb = (int64_t)sizeof(SnapHdr) + (nk + 1) * 8;
+    for (int64_t g = 0; g < nk; ++g) {
+        offs[g] = (int64_t)pay.size();
+        // entries in snapshot_heap's order: by key, then window; timers by key, window, time
+        std::vector<std::pair<std::pair<int64_t, int64_t>, const uint8_t*>> st;
+        std::vector<std::pair<std::tuple<int64_t, int64_t, uint64_t>, const uint8_t*>> tm;
+        for (auto& b : blobs) {
+            int64_t o0;
+            memcpy(&o0, b.data() + sizeof(SnapHdr) + g * 8, 8);
+            const uint8_t* p = b.data() + hb + o0;
+            const int32_t n = gw_handle::rd32(p);
+            p += 4;
+            for (int32_t i = 0; i < n; ++i, p += eb) st.push_back({{gw_handle::rd64(p + 16), gw_handle::rd64(p)}, p});
+            p += 4;  // the empty merging window set
+            const int32_t t = gw_handle::rd32(p);
+            p += 4;
+            for (int32_t i = 0; i < t; ++i, p += 32)
+                tm.push_back({{gw_handle::rd64(p + 8), gw_handle::rd64(p + 16), (uint64_t)gw_handle::rd64(p)}, p});
+        }
+        std::sort(st.begin(), st.end(), [](const auto& x, const auto& y) { return x.first < y.first; });
+        std::sort(tm.begin(), tm.end(), [](const auto& x, const auto& y) { return x.first < y.first; });
+        gw_handle::be32(pay, (int32_t)st.size());
+        for (auto& e : st) pay.insert(pay.end(), e.second, e.second + eb);
+        gw_handle::be32(pay, 0);
+        gw_handle::be32(pay, (int32_t)tm.size());
+        for (auto& e : tm) pay.insert(pay.end(), e.second, e.second + 32);
+    }
+    offs[nk] = (int64_t)pay.size();
+    const int64_t need = hb + (int64_t)pay.size();
+    *len = need;
+    if (!buf) return GW_OK;
+    if (cap < need) return h->fail(GW_E_OUTPUT_FULL, "snapshot needs %lld bytes", (long long)need);
+    SnapHdr hd;
+    memcpy(&hd, blobs[0].data(), sizeof hd);
+    hd.slide = h->cfg.slide;
+    hd.offset = h->cfg.offset;
+    hd.entries = (int64_t)pay.size();
+    char* out = (char*)buf;
+    memcpy(out, &hd, sizeof hd);
+    memcpy(out + sizeof hd, offs.data(), (size_t)(nk + 1) * 8);
+    if (!pay.empty()) memcpy(out + hb, pay.data(), pay.size());
+    return GW_OK;
+}
+
+static int comp_restore(gw_handle* h, const void* buf, int64_t len) {
+    if (!buf || len < (int64_t)sizeof(SnapHdr)) return h->fail(GW_E_INVALID, "snapshot blob too short");
+    SnapHdr hd;
+    memcpy(&hd, buf, sizeof hd);
+    if (memcmp(hd.magic, "GWS1", 4) != 0 || hd.version != 4 || hd.agg != h->cfg.agg ||
+        hd.assigner != h->cfg.assigner || hd.size != h->cfg.size || hd.slide != h->cfg.slide ||
+        hd.offset != h->cfg.offset || hd.max_parallelism != h->cfg.max_parallelism)
+        return h->fail(GW_E_INVALID, "snapshot of a different window / aggregate / max parallelism");
+    const int64_t nk = (int64_t)hd.kg_hi - hd.kg_lo + 1;
+    const int64_t hb = (int64_t)sizeof hd + (nk + 1) * 8;
+    if (nk <= 0 || hd.entries < 0 || len < hb + hd.entries) return h->fail(GW_E_INVALID, "truncated snapshot blob");
+    const int64_t J = (int64_t)h->kids.size(), eb = 24 + h->kids[0]->acc_bytes();
+    const uint8_t* p = (const uint8_t*)buf + hb;
+    const uint8_t* end = p + hd.entries;
+    auto cls = [&](int64_t s0) {  // window class of a window start
+        const int64_t k = (int64_t)floor_div((i128)s0 - h->cfg.offset, (i128)h->cfg.slide);
+        return (size_t)(((k % J) + J) % J);
+    };
+    std::vector<std::vector<uint8_t>> pay(J);
+    std::vector<std::vector<int64_t>> offs(J, std::vector<int64_t>(nk + 1, 0));
+    for (int64_t g = 0; g < nk; ++g) {
+        std::vector<std::vector<uint8_t>> st(J), tm(J);
+        std::vector<int32_t> nst(J, 0), ntm(J, 0);
+        if (p + 4 > end) return h->fail(GW_E_INVALID, "truncated snapshot blob");
+        const int32_t n = gw_handle::rd32(p);
+        p += 4;
+        if (n < 0 || p + (int64_t)n * eb + 8 > end) return h->fail(GW_E_INVALID, "truncated snapshot blob");
+        for (int32_t i = 0; i < n; ++i, p += eb) {
+            const size_t j = cls(gw_handle::rd64(p));
+            st[j].insert(st[j].end(), p, p + eb);
+            nst[j]++;
+        }
+        if (gw_handle::rd32(p) != 0) return h->fail(GW_E_INVALID, "merging window set in a sliding snapshot");
+        p += 4;
+        const int32_t t = gw_handle::rd32(p);
+        p += 4;
+        if (t < 0 || p + (int64_t)t * 32 > end) return h->fail(GW_E_INVALID, "truncated snapshot blob");
+        for (int32_t i = 0; i < t; ++i, p += 32) {
+            const size_t j = cls(gw_handle::rd64(p + 16));  // (timestamp, key, start, end)
+            tm[j].insert(tm[j].end(), p, p + 32);
+            ntm[j]++;
+        }
+        for (int64_t j = 0; j < J; ++j) {
+            offs[j][g] = (int64_t)pay[j].size();
+            gw_handle::be32(pay[j], nst[j]);
+            pay[j].insert(pay[j].end(), st[j].begin(), st[j].end());
+            gw_handle::be32(pay[j], 0);
+            gw_handle::be32(pay[j], ntm[j]);
+            pay[j].insert(pay[j].end(), tm[j].begin(), tm[j].end());
+        }
+    }
+    if (p != end) return h->fail(GW_E_INVALID, "snapshot blob has trailing bytes");
+    for (int64_t j = 0; j < J; ++j) {
+        offs[j][nk] = (int64_t)pay[j].size();
+        SnapHdr kh = hd;
+        kh.slide = h->kids[j]->cfg.slide;
+        kh.offset = h->kids[j]->cfg.offset;
+        kh.entries = (int64_t)pay[j].size();
+        std::vector<uint8_t> blob(sizeof kh + (nk + 1) * 8 + pay[j].size());
+        memcpy(blob.data(), &kh, sizeof kh);
+        memcpy(blob.data() + sizeof kh, offs[j].data(), (size_t)(nk + 1) * 8);
+        if (!pay[j].empty()) memcpy(blob.data() + sizeof kh + (nk + 1) * 8, pay[j].data(), pay[j].size());
+        const int rc = gw_restore(h->kids[j], blob.data(), (int64_t)blob.size());
+        if (rc) return kid_rc(h, h->kids[j], rc);
+    }
+    return GW_OK;
+}
+
 int gw_snapshot(gw_handle* h, int32_t kg_lo, int32_t kg_hi, void* buf, int64_t cap, int64_t* len) {
     if (!h || !len) return GW_E_INVALID;
-    if (!h->kids.empty())
-        return h->fail(GW_E_UNSUPPORTED, "snapshot of sliding windows split into %d window classes (a pane ring "
-                                         "beyond 64 panes) is not supported yet", (int)h->kids.size());
+    if (!h->kids.empty()) return comp_snapshot(h, kg_lo, kg_hi, buf, cap, len);
     if (h->failed) return h->fail(GW_E_STATE, "operator failed earlier: %s", h->err.c_str());
     if (h->foreign_hash)
         return h->fail(GW_E_UNSUPPORTED, "snapshot of a handle that ingested a key_hash different from "
@@ -2325,9 +2456,7 @@ int gw_snapshot(gw_handle* h, int32_t kg_lo, int32_t kg_hi, void* buf, int64_t c
 
 int gw_restore(gw_handle* h, const void* buf, int64_t len) {
     if (!h) return GW_E_INVALID;
-    if (!h->kids.empty())
-        return h->fail(GW_E_UNSUPPORTED, "restore into sliding windows split into %d window classes (a pane ring "
-                                         "beyond 64 panes) is not supported yet", (int)h->kids.size());
+    if (!h->kids.empty()) return comp_restore(h, buf, len);
     if (h->failed) return h->fail(GW_E_STATE, "operator failed earlier: %s", h->err.c_str());
     hipSetDevice(h->cfg.device);
     if (h->session) return h->restore_sessions(buf, len);

@@ -127,13 +127,58 @@ def test_window_classes_rows_device_and_stats(oracle_lib):
     op.close()
 
 
-def test_window_classes_snapshot_unsupported():
-    op = gpu_operator(dict(assigner="sliding", size=1000, slide=10, agg="sum_i64"))
-    op.process_batch(np.array([1, 2], np.int64), np.array([5, 9], np.int64), np.array([3, 4], np.int64))
-    with pytest.raises(N.GpuWinError) as ei:
-        op.snapshot_state()
-    assert ei.value.code == -2
+SNAP_CFGS = [
+    dict(assigner="sliding", size=1000, slide=10),
+    dict(assigner="sliding", size=1000, slide=100, lateness=10_000),
+]
+
+
+@pytest.mark.parametrize("agg", ["sum_i64", "avg_f64", "count"])
+@pytest.mark.parametrize("cfg", SNAP_CFGS, ids=lambda c: "-".join(str(v) for v in c.values()))
+def test_window_classes_snapshot_equals_oracle(oracle_lib, cfg, agg):
+    """The classes' blobs merged per key group equal the oracle's heap-layout snapshot of the
+    same stream: (window, key) entries, accumulators and timers."""
+    from test_gpu_restore import feed_gpu, feed_oracle, same_state
+    kw = dict(cfg, agg=agg)
+    keys, ts, vals, batches = random_stream(31, 9000, 120, 10, ts_step=3, disorder=1500, wm_lag=300, agg=agg)
+    op = gpu_operator(kw, capacity_hint=4096)
+    ora = oracle_lib.OracleOperator(oracle_lib.make_config(**kw))
+    go, oo = [], []
+    feed_gpu(op, keys, ts, vals, batches[:6], go)
+    feed_oracle(ora, keys, ts, vals, batches[:6], oo)
+    same_state(op.snapshot_state(), ora.snapshot(), agg)
+    assert compare(go, oo, agg in DOUBLE) == []
     op.close()
+    ora.close()
+
+
+@pytest.mark.parametrize("agg", ["sum_i64", "avg_f64"])
+@pytest.mark.parametrize("cfg", SNAP_CFGS, ids=lambda c: "-".join(str(v) for v in c.values()))
+@pytest.mark.parametrize("writer", ["oracle", "gpu"])
+def test_window_classes_restore(oracle_lib, cfg, agg, writer):
+    """A blob written by either side restores into the classes (split by window class) and
+    into the oracle; records of fired windows arriving before the first watermark re-fire
+    them (the watermark restarts at Long.MIN_VALUE) and both continue identically."""
+    from test_gpu_restore import feed_gpu, feed_oracle, resume
+    o = oracle_lib
+    kw = dict(cfg, agg=agg)
+    keys, ts, vals, batches = random_stream(37, 9000, 120, 10, ts_step=3, disorder=1500, wm_lag=300, agg=agg)
+    cut = 5
+    if writer == "gpu":
+        op = gpu_operator(kw, capacity_hint=4096)
+        feed_gpu(op, keys, ts, vals, batches[:cut], [])
+        blob = op.snapshot_state()
+        op.close()
+    else:
+        op = o.OracleOperator(o.make_config(**kw))
+        feed_oracle(op, keys, ts, vals, batches[:cut], [])
+        blob = op.snapshot()
+        op.close()
+    old = np.arange(0, batches[1][1], 5)
+    g, glate, _ = resume("gpu", o, kw, blob, keys, ts, vals, batches[cut:], old)
+    r, rlate, _ = resume("oracle", o, kw, blob, keys, ts, vals, batches[cut:], old)
+    assert compare(g, r, agg in DOUBLE) == []
+    assert glate == rlate
 
 
 def test_tumbling_lateness_beyond_the_ring_is_unsupported():
