@@ -185,3 +185,33 @@ def test_tumbling_lateness_beyond_the_ring_is_unsupported():
     with pytest.raises(N.GpuWinError) as ei:
         gpu_operator(dict(assigner="tumbling", size=100, agg="sum_i64", lateness=10_000))
     assert ei.value.code == -2
+
+
+def test_window_classes_network_buffers(oracle_lib):
+    """A window-class handle fed network buffers: every class decodes the channel; the rows
+    equal the oracle operator fed the decoded channel."""
+    from test_gpu_netbuf import channel_stream, drained, oracle_channel
+    from flink_amd import netbuf as NB
+    from flink_amd import windowing as W
+    kw, types, kf, vf = dict(assigner="sliding", size=1500, slide=15, agg="sum_i64"), "JJ", 0, 1
+    data = channel_stream(kw, types, kf, vf, seed=17, n=20000, nb=8, n_keys=200)
+    exp = oracle_channel(oracle_lib, kw, data, types, kf, vf)
+    op = gpu_operator(kw)
+    try:
+        op.process_buffers(NB.split_buffers(data, 4093), N.record_layout(types, kf, vf))
+        op.advance_watermark(W.LONG_MAX)
+        got = drained(op)
+    finally:
+        op.close()
+    assert compare([got], [exp], False) == []
+
+
+@pytest.mark.parametrize("agg", ["sum_i32", "min_f64"])
+def test_window_classes_purging_trigger_with_lateness(oracle_lib, agg):
+    kw = dict(assigner="sliding", size=1200, slide=20, lateness=400, trigger="purging_event_time", agg=agg)
+    keys, ts, vals, batches = random_stream(seed=23, n=10000, num_keys=40, n_batches=20, ts_step=3, disorder=800,
+                                            wm_lag=200, agg=agg)
+    g, glate, _ = run_gpu(kw, keys, ts, vals, batches)
+    o, olate = run_oracle(oracle_lib, kw, keys, ts, vals, batches)
+    assert glate == olate
+    assert compare(g, o, agg in DOUBLE) == []
