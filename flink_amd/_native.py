@@ -35,6 +35,7 @@ FLAG_FORCE_REGION = 8
 FLAG_NO_REGION = 16
 FLAG_NO_BUFFER = 32
 FLAG_LATE_SIDE_OUTPUT = 64
+FLAG_FIRST_ELEMENT = 128
 
 EXPORTS = [
     "gw_create", "gw_destroy", "gw_last_error", "gw_abi_version", "gw_ingest", "gw_ingest_device",
@@ -46,6 +47,7 @@ EXPORTS = [
     "gw_decode_serialized", "gw_ingest_serialized", "gw_ingest_serialized_device",
     "gw_exchange_unique_id", "gw_exchange_create", "gw_exchange_destroy", "gw_exchange_batch",
     "gw_exchange_min_watermark", "gw_exchange_last_error",
+    "gw_ingest_payload", "gw_ingest_payload_device", "gw_drain_payload",
 ]
 EXCHANGE_ID_BYTES = 128
 
@@ -141,6 +143,9 @@ def lib() -> ctypes.CDLL:
         "gw_end_input": (c_int, [p, P64]),
         "gw_pending_rows": (c_int, [p, P64]),
         "gw_drain": (c_int, [p, p, p, p, p, i64, P64]),
+        "gw_ingest_payload": (c_int, [p, i64, p, p, p, p, p]),
+        "gw_ingest_payload_device": (c_int, [p, i64, p, p, p, p, p, p]),
+        "gw_drain_payload": (c_int, [p, p, p, p, p, p, i64, P64]),
         "gw_rows_device": (c_int, [p, ctypes.POINTER(p), ctypes.POINTER(p), ctypes.POINTER(p),
                                    ctypes.POINTER(p), P64]),
         "gw_clear_rows": (c_int, [p]),

@@ -19,6 +19,7 @@
 #include <tuple>
 #include <vector>
 
+#include "gw_first.h"
 #include "gw_kernels.h"
 #include "gw_netbuf.h"
 #include "gw_session.h"
@@ -147,6 +148,23 @@ struct gw_handle {
     int64_t cls_J = 0, cls_j = 0, cls_slide = 0, cls_off = 0;  // a child's class
     int64_t *c_key = nullptr, *c_start = nullptr, *c_end = nullptr, *c_res = nullptr;
     int64_t c_cap = 0, c_rows = 0, c_head = 0;
+    // First-element handle (GW_FLAG_FIRST_ELEMENT, gw_first.hip): kids[0] folds the aggregate,
+    // kids[1] the MIN of each record's arrival sequence; the payload log keeps every record's
+    // payload (a ring indexed by sequence) until all windows that could hold it are cleaned.
+    bool fe = false;
+    int64_t fe_seq = 0;                                 // sequence of the next record
+    int64_t* fe_log = nullptr;
+    int64_t fe_log_cap = 0, fe_log_base = 0;            // live sequences [fe_log_base, fe_seq)
+    int64_t* fe_seqbuf = nullptr;
+    int64_t fe_seqbuf_cap = 0;
+    int64_t* fe_maxts = nullptr;                        // per batch (ring of kFeBatches): largest ts
+    std::vector<std::pair<int64_t, int64_t>> fe_batches; // (sequence end, ring slot) not yet released
+    int64_t fe_batch_no = 0;
+    int64_t* c_pay = nullptr;
+    void* fe_scratch = nullptr;
+    size_t fe_scratch_bytes = 0;
+    int32_t* fe_bad = nullptr;
+    static constexpr int64_t kFeBatches = 1 << 16;
     hipEvent_t ev_in = nullptr, ev_out = nullptr;  // gw_ingest_device ordering with the producer stream
 
     // network-buffer ingest (gw_ingest_serialized*): grow-only device scratch, decoded
@@ -1769,6 +1787,34 @@ static int make_composite(gw_handle* h, int64_t J) {
     return GW_OK;
 }
 
+// A first-element handle h (its cfg set): kids[0] the aggregate, kids[1] MIN(sequence).
+static int make_first_element(gw_handle* h) {
+    if (h->stream) {  // kernels of its own (sequence, payload log, join) run on kids[0]'s stream
+        hipStreamSynchronize(h->stream);
+        hipStreamDestroy(h->stream);
+        h->stream = nullptr;
+    }
+    gw_config a = h->cfg, b = h->cfg;
+    a.flags &= ~GW_FLAG_FIRST_ELEMENT;
+    b.flags &= ~(GW_FLAG_FIRST_ELEMENT | GW_FLAG_LATE_SIDE_OUTPUT);
+    b.agg = GW_MIN_I64;
+    for (const gw_config* c : {&a, &b}) {
+        gw_handle* kid = nullptr;
+        const int rc = gw_create(c, &kid);
+        if (rc) return rc;
+        h->kids.push_back(kid);
+    }
+    h->fe = true;
+    h->stream = h->kids[0]->stream;
+    h->shared_stream = true;
+    if (hipMalloc((void**)&h->fe_maxts, (size_t)gw_handle::kFeBatches * 8) != hipSuccess ||
+        hipMalloc((void**)&h->fe_bad, 4) != hipSuccess) {
+        g_create_error = "first-element buffers: out of device memory";
+        return GW_E_OOM;
+    }
+    return GW_OK;
+}
+
 int gw_create(const gw_config* cfg, gw_handle** out) {
     if (!cfg || !out) { g_create_error = "null argument"; return GW_E_INVALID; }
     *out = nullptr;
@@ -1820,10 +1866,23 @@ int gw_create(const gw_config* cfg, gw_handle** out) {
     while ((double)cap * 0.7 < (double)hint) cap *= 2;
 
     if (cfg->assigner == GW_SESSION || cfg->assigner == GW_COUNT_TUMBLING || cfg->assigner == GW_COUNT_SLIDING) {
+        if (cfg->flags & GW_FLAG_FIRST_ELEMENT)
+            return bail(GW_E_UNSUPPORTED, "first-element rows are for tumbling and sliding event-time windows");
         h->session = true;  // the per-key slot path (session merging or count windows)
         rc = session_create(h->sess, *cfg, cap, h->stream, h->d_st, why);
         if (rc) return bail(rc, why);
         hipStreamSynchronize(h->stream);
+        *out = h;
+        return GW_OK;
+    }
+    if (cfg->flags & GW_FLAG_FIRST_ELEMENT) {
+        if (cfg->trigger != GW_EVENT_TIME_TRIGGER)
+            return bail(GW_E_UNSUPPORTED, "first-element rows with PurgingTrigger are not supported");
+        const int a = cfg->agg;
+        if (a == GW_COUNT || a == GW_AVG_I64 || a == GW_AVG_F64)
+            return bail(GW_E_INVALID, "first-element rows are for the positional aggregates sum / min / max");
+        rc = make_first_element(h);
+        if (rc) return bail(rc, g_create_error);
         *out = h;
         return GW_OK;
     }
@@ -1877,6 +1936,12 @@ int gw_destroy(gw_handle* h) {
         h->kids.clear();
         h->stream = nullptr;
         if (h->c_key) { hipFree(h->c_key); hipFree(h->c_start); hipFree(h->c_end); hipFree(h->c_res); }
+        if (h->c_pay) hipFree(h->c_pay);
+        if (h->fe_log) hipFree(h->fe_log);
+        if (h->fe_seqbuf) hipFree(h->fe_seqbuf);
+        if (h->fe_maxts) hipFree(h->fe_maxts);
+        if (h->fe_bad) hipFree(h->fe_bad);
+        if (h->fe_scratch) hipFree(h->fe_scratch);
     }
     h->hp.dump();
     if (h->stream) hipStreamSynchronize(h->stream);
@@ -1949,9 +2014,202 @@ static int kid_rc(gw_handle* h, gw_handle* kid, int rc) {
         }                                                                                \
     } while (0)
 
+// ---- first-element handle (GW_FLAG_FIRST_ELEMENT, gw_first.hip) ----------------------
+// Row buffers of the joined rows (key, start, end, result, payload) for `need` rows in all.
+static int fe_reserve_rows(gw_handle* h, int64_t need) {
+    if (need <= h->c_cap) return GW_OK;
+    const int64_t cap = std::max<int64_t>(need, 2 * h->c_cap);
+    int64_t* nb[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
+    for (int q = 0; q < 5; ++q) {
+        if (hipMalloc((void**)&nb[q], (size_t)cap * 8) != hipSuccess) {
+            for (int r = 0; r < q; ++r) hipFree(nb[r]);
+            return h->fail(GW_E_OOM, "first-element row buffer: out of device memory");
+        }
+    }
+    int64_t* old[5] = {h->c_key, h->c_start, h->c_end, h->c_res, h->c_pay};
+    const int64_t live = h->c_rows - h->c_head;
+    for (int q = 0; q < 5; ++q)
+        if (old[q] && live) hipMemcpyAsync(nb[q], old[q] + h->c_head, live * 8, hipMemcpyDeviceToDevice, h->stream);
+    hipStreamSynchronize(h->stream);
+    for (int q = 0; q < 5; ++q)
+        if (old[q]) hipFree(old[q]);
+    h->c_key = nb[0]; h->c_start = nb[1]; h->c_end = nb[2]; h->c_res = nb[3]; h->c_pay = nb[4];
+    h->c_cap = cap;
+    h->c_rows = live;
+    h->c_head = 0;
+    return GW_OK;
+}
+
+// The rows both operators fired, joined by (key, window start) with the payload of the
+// window's first element, appended to the c_* rows; then the payloads no window can need
+// any more leave the log.
+static int fe_gather(gw_handle* h, int64_t wm) {
+    gw_handle *A = h->kids[0], *B = h->kids[1];
+    int64_t na = 0, nb = 0;
+    int rc = gw_pending_rows(A, &na);
+    if (rc) return kid_rc(h, A, rc);
+    if ((rc = gw_pending_rows(B, &nb))) return kid_rc(h, B, rc);
+    if (na != nb) return h->fail(GW_E_STATE, "first-element rows out of step (%lld vs %lld)", (long long)na, (long long)nb);
+    if (na > 0) {
+        const int64_t *ak, *as, *ae, *bk, *bs, *be;
+        const void *ar, *br;
+        int64_t x = 0;
+        if ((rc = gw_rows_device(A, &ak, &as, &ae, &ar, &x))) return kid_rc(h, A, rc);
+        if ((rc = gw_rows_device(B, &bk, &bs, &be, &br, &x))) return kid_rc(h, B, rc);
+        if ((rc = fe_reserve_rows(h, h->c_rows + na))) return rc;
+        const size_t need = fe_join_scratch_bytes(na);
+        if (need > h->fe_scratch_bytes) {
+            if (h->fe_scratch) hipFree(h->fe_scratch);
+            h->fe_scratch = nullptr;
+            h->fe_scratch_bytes = 0;
+            if (hipMalloc(&h->fe_scratch, need) != hipSuccess) return h->fail(GW_E_OOM, "first-element join scratch");
+            h->fe_scratch_bytes = need;
+        }
+        const int64_t o = h->c_rows;
+        hipError_t e = hipMemsetAsync(h->fe_bad, 0, 4, h->stream);
+        if (e == hipSuccess)
+            e = fe_join(na, ak, as, ae, (const int64_t*)ar, bk, bs, (const int64_t*)br, h->fe_log, h->fe_log_base,
+                        h->fe_log_cap, h->c_key + o, h->c_start + o, h->c_end + o, h->c_res + o, h->c_pay + o,
+                        h->fe_scratch, h->fe_scratch_bytes, h->fe_bad, h->stream);
+        int32_t bad = 0;
+        if (e == hipSuccess) e = hipMemcpyAsync(&bad, h->fe_bad, 4, hipMemcpyDeviceToHost, h->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+        if (e != hipSuccess) return h->fail(GW_E_DEVICE, "first-element join: %s", hipGetErrorString(e));
+        if (bad) return h->fail(GW_E_STATE, "first-element join: %s", bad & 1 ? "rows differ" : "payload released");
+        h->c_rows += na;
+        if ((rc = gw_clear_rows(A))) return kid_rc(h, A, rc);
+        if ((rc = gw_clear_rows(B))) return kid_rc(h, B, rc);
+    }
+    // release: a batch whose largest timestamp's windows are all cleaned (maxTs + size - 1 +
+    // lateness <= wm: WindowOperator.cleanupTime) can hold no first element any more
+    if (!h->fe_batches.empty()) {
+        std::vector<int64_t> mx(h->fe_batches.size());
+        for (size_t i = 0; i < mx.size(); ++i)
+            if (hipMemcpy(&mx[i], h->fe_maxts + h->fe_batches[i].second, 8, hipMemcpyDeviceToHost) != hipSuccess)
+                return h->fail(GW_E_DEVICE, "first-element log");
+        size_t q = 0;
+        for (; q < mx.size(); ++q) {
+            const i128 ct = (i128)mx[q] + (i128)h->cfg.size - 1 + (i128)h->cfg.allowed_lateness;
+            if (mx[q] != INT64_MIN && ct > (i128)wm) break;
+            h->fe_log_base = h->fe_batches[q].first;
+        }
+        h->fe_batches.erase(h->fe_batches.begin(), h->fe_batches.begin() + q);
+    }
+    return GW_OK;
+}
+
+int gw_ingest_payload_device(gw_handle* h, int64_t n, const int64_t* d_key, const int32_t* d_key_hash,
+                             const int64_t* d_ts, const void* d_value, const int64_t* d_payload, void* stream) {
+    if (!h) return GW_E_INVALID;
+    if (!h->fe) return h->fail(GW_E_INVALID, "gw_ingest_payload*: not a GW_FLAG_FIRST_ELEMENT handle");
+    if (h->failed) return h->fail(GW_E_STATE, "operator failed earlier: %s", h->err.c_str());
+    if (n < 0 || (n > 0 && (!d_key || !d_ts || !d_value || !d_payload)))
+        return h->fail(GW_E_INVALID, "null key/ts/value/payload column");
+    hipSetDevice(h->cfg.device);
+    hipStream_t s = h->stream, ps = (hipStream_t)stream;
+    if (ps != s) {
+        hipEventRecord(h->ev_in, ps);
+        hipStreamWaitEvent(s, h->ev_in, 0);
+    }
+    if (n == 0) return GW_OK;
+    // arrival sequence of the batch's records (kids[1] folds its minimum per window)
+    if (n > h->fe_seqbuf_cap) {
+        hipStreamSynchronize(s);
+        if (h->fe_seqbuf) hipFree(h->fe_seqbuf);
+        h->fe_seqbuf = nullptr;
+        h->fe_seqbuf_cap = 0;
+        if (hipMalloc((void**)&h->fe_seqbuf, (size_t)n * 8) != hipSuccess) return h->fail(GW_E_OOM, "sequence buffer");
+        h->fe_seqbuf_cap = n;
+    }
+    hipError_t e = fe_iota64(h->fe_seqbuf, n, h->fe_seq, s);
+    // payload log: a ring of the live sequences [fe_log_base, fe_seq + n)
+    const int64_t need = h->fe_seq + n - h->fe_log_base;
+    if (e == hipSuccess && need > h->fe_log_cap) {
+        const int64_t ncap = std::max<int64_t>(2 * need, 1 << 20);
+        int64_t* nl = nullptr;
+        if (hipMalloc((void**)&nl, (size_t)ncap * 8) != hipSuccess) return h->fail(GW_E_OOM, "payload log");
+        if (h->fe_log) e = fe_log_regrow(h->fe_log, h->fe_log_cap, nl, ncap, h->fe_log_base, h->fe_seq, s);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        if (h->fe_log) hipFree(h->fe_log);
+        h->fe_log = nl;
+        h->fe_log_cap = ncap;
+    }
+    if (e == hipSuccess) e = fe_log_append(h->fe_log, h->fe_log_cap, h->fe_seq, d_payload, n, s);
+    if ((int64_t)h->fe_batches.size() >= gw_handle::kFeBatches - 1)
+        return h->fail(GW_E_STATE, "first-element log: too many batches without a watermark");
+    const int64_t slot = h->fe_batch_no % gw_handle::kFeBatches;
+    if (e == hipSuccess) e = fe_iota64(h->fe_maxts + slot, 1, INT64_MIN, s);
+    if (e == hipSuccess) e = fe_max_ts(d_ts, n, h->fe_maxts + slot, s);
+    if (e != hipSuccess) return h->fail(GW_E_DEVICE, "first-element ingest: %s", hipGetErrorString(e));
+    h->fe_batches.push_back({h->fe_seq + n, slot});
+    h->fe_batch_no++;
+    int rc = gw_ingest_device(h->kids[0], n, d_key, d_key_hash, d_ts, d_value, (void*)s);
+    if (rc) return kid_rc(h, h->kids[0], rc);
+    if ((rc = gw_ingest_device(h->kids[1], n, d_key, d_key_hash, d_ts, h->fe_seqbuf, (void*)s)))
+        return kid_rc(h, h->kids[1], rc);
+    h->fe_seq += n;
+    if (ps != s) {
+        hipEventRecord(h->ev_out, s);
+        hipStreamWaitEvent(ps, h->ev_out, 0);
+    }
+    return GW_OK;
+}
+
+int gw_ingest_payload(gw_handle* h, int64_t n, const int64_t* key, const int32_t* key_hash, const int64_t* ts,
+                      const void* value, const int64_t* payload) {
+    if (!h) return GW_E_INVALID;
+    if (!h->fe) return h->fail(GW_E_INVALID, "gw_ingest_payload*: not a GW_FLAG_FIRST_ELEMENT handle");
+    if (n < 0 || (n > 0 && (!key || !ts || !value || !payload)))
+        return h->fail(GW_E_INVALID, "null key/ts/value/payload column");
+    if (n == 0) return GW_OK;
+    hipSetDevice(h->cfg.device);
+    // host columns: one device copy of each (synchronous), then the device path
+    int64_t* d = nullptr;
+    int32_t* dh = nullptr;
+    if (hipMalloc((void**)&d, (size_t)n * 32) != hipSuccess) return h->fail(GW_E_OOM, "payload staging");
+    if (key_hash && hipMalloc((void**)&dh, (size_t)n * 4) != hipSuccess) {
+        hipFree(d);
+        return h->fail(GW_E_OOM, "payload staging");
+    }
+    hipError_t e = hipMemcpyAsync(d, key, n * 8, hipMemcpyHostToDevice, h->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(d + n, ts, n * 8, hipMemcpyHostToDevice, h->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(d + 2 * n, value, n * 8, hipMemcpyHostToDevice, h->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(d + 3 * n, payload, n * 8, hipMemcpyHostToDevice, h->stream);
+    if (e == hipSuccess && dh) e = hipMemcpyAsync(dh, key_hash, n * 4, hipMemcpyHostToDevice, h->stream);
+    int rc = e == hipSuccess ? gw_ingest_payload_device(h, n, d, dh, d + n, d + 2 * n, d + 3 * n, h->stream)
+                             : h->fail(GW_E_DEVICE, "H2D: %s", hipGetErrorString(e));
+    hipStreamSynchronize(h->stream);
+    hipFree(d);
+    if (dh) hipFree(dh);
+    return rc;
+}
+
+int gw_drain_payload(gw_handle* h, int64_t* key, int64_t* start, int64_t* end, void* result, int64_t* payload,
+                     int64_t cap, int64_t* n) {
+    if (!h || !n) return GW_E_INVALID;
+    *n = 0;
+    if (!h->fe) return h->fail(GW_E_INVALID, "gw_drain_payload: not a GW_FLAG_FIRST_ELEMENT handle");
+    const int64_t c = std::min(cap, h->c_rows - h->c_head);
+    if (c > 0) {
+        const int64_t o = h->c_head;
+        int64_t* dst[5] = {key, start, end, (int64_t*)result, payload};
+        int64_t* src[5] = {h->c_key, h->c_start, h->c_end, h->c_res, h->c_pay};
+        hipError_t e = hipSuccess;
+        for (int q = 0; q < 5 && e == hipSuccess; ++q)
+            if (dst[q]) e = hipMemcpyAsync(dst[q], src[q] + o, c * 8, hipMemcpyDeviceToHost, h->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+        if (e != hipSuccess) return h->fail(GW_E_DEVICE, "D2H rows: %s", hipGetErrorString(e));
+        h->c_head += c;
+        if (h->c_head == h->c_rows) h->c_head = h->c_rows = 0;
+    }
+    *n = c;
+    return h->c_rows - h->c_head > 0 ? GW_E_OUTPUT_FULL : GW_OK;
+}
+
 int gw_ingest(gw_handle* h, int64_t n, const int64_t* key, const int32_t* key_hash, const int64_t* ts,
               const void* value) {
     if (!h) return GW_E_INVALID;
+    if (h->fe) return h->fail(GW_E_INVALID, "GW_FLAG_FIRST_ELEMENT handle: records need their payload (gw_ingest_payload)");
     if (!h->kids.empty()) {
         FOR_KIDS(gw_ingest(kid, n, key, key_hash, ts, value));
         return GW_OK;
@@ -1994,6 +2252,8 @@ int gw_ingest(gw_handle* h, int64_t n, const int64_t* key, const int32_t* key_ha
 int gw_ingest_device(gw_handle* h, int64_t n, const int64_t* d_key, const int32_t* d_key_hash,
                      const int64_t* d_ts, const void* d_value, void* stream) {
     if (!h) return GW_E_INVALID;
+    if (h->fe)
+        return h->fail(GW_E_INVALID, "GW_FLAG_FIRST_ELEMENT handle: records need their payload (gw_ingest_payload_device)");
     if (!h->kids.empty()) {  // the children share one stream: order after the producer once
         FOR_KIDS(gw_ingest_device(kid, n, d_key, d_key_hash, d_ts, d_value, stream));
         return GW_OK;
@@ -2192,6 +2452,7 @@ static int nb_ingest_on_stream(gw_handle* h, const uint8_t* d_bytes, int64_t nby
 int gw_ingest_serialized_device(gw_handle* h, const void* d_bytes, int64_t nbytes, const gw_record_layout* layout,
                                 void* stream, int64_t* consumed, int64_t* rows_fired) {
     if (!h) return GW_E_INVALID;
+    if (h->fe) return h->fail(GW_E_UNSUPPORTED, "network-buffer ingest of first-element rows is not supported");
     if (!h->kids.empty()) {  // each child decodes the channel (same bytes consumed by all)
         int64_t sum = 0;
         for (gw_handle* kid : h->kids) {
@@ -2226,6 +2487,7 @@ int gw_ingest_serialized_device(gw_handle* h, const void* d_bytes, int64_t nbyte
 int gw_ingest_serialized(gw_handle* h, const void* bytes, int64_t nbytes, const gw_record_layout* layout,
                          int64_t* consumed, int64_t* rows_fired) {
     if (!h) return GW_E_INVALID;
+    if (h->fe) return h->fail(GW_E_UNSUPPORTED, "network-buffer ingest of first-element rows is not supported");
     if (!h->kids.empty()) {
         int64_t sum = 0;
         for (gw_handle* kid : h->kids) {
@@ -2267,6 +2529,18 @@ int gw_ingest_serialized(gw_handle* h, const void* bytes, int64_t nbytes, const 
 
 int gw_advance_watermark(gw_handle* h, int64_t wm, int64_t* rows_fired) {
     if (!h) return GW_E_INVALID;
+    if (h->fe) {  // both operators fire the same windows; join their rows now, while the log holds them
+        int64_t f = 0;
+        for (gw_handle* kid : h->kids) {
+            const int rc = gw_advance_watermark(kid, wm, kid == h->kids[0] ? &f : nullptr);
+            if (rc) return kid_rc(h, kid, rc);
+        }
+        const int rc = fe_gather(h, wm);
+        if (rc) return rc;
+        h->stats.rows_fired += f;
+        if (rows_fired) *rows_fired = f;
+        return GW_OK;
+    }
     if (!h->kids.empty()) {
         int64_t sum = 0;
         for (gw_handle* kid : h->kids) {
@@ -2444,6 +2718,7 @@ static int comp_restore(gw_handle* h, const void* buf, int64_t len) {
 
 int gw_snapshot(gw_handle* h, int32_t kg_lo, int32_t kg_hi, void* buf, int64_t cap, int64_t* len) {
     if (!h || !len) return GW_E_INVALID;
+    if (h->fe) return h->fail(GW_E_UNSUPPORTED, "snapshots of first-element rows are not supported");
     if (!h->kids.empty()) return comp_snapshot(h, kg_lo, kg_hi, buf, cap, len);
     if (h->failed) return h->fail(GW_E_STATE, "operator failed earlier: %s", h->err.c_str());
     if (h->foreign_hash)
@@ -2456,6 +2731,7 @@ int gw_snapshot(gw_handle* h, int32_t kg_lo, int32_t kg_hi, void* buf, int64_t c
 
 int gw_restore(gw_handle* h, const void* buf, int64_t len) {
     if (!h) return GW_E_INVALID;
+    if (h->fe) return h->fail(GW_E_UNSUPPORTED, "snapshots of first-element rows are not supported");
     if (!h->kids.empty()) return comp_restore(h, buf, len);
     if (h->failed) return h->fail(GW_E_STATE, "operator failed earlier: %s", h->err.c_str());
     hipSetDevice(h->cfg.device);
@@ -2520,6 +2796,10 @@ static void rows_view(gw_handle* h, int64_t** k, int64_t** s, int64_t** e, int64
 
 int gw_pending_rows(gw_handle* h, int64_t* n) {
     if (!h || !n) return GW_E_INVALID;
+    if (h->fe) {  // rows are joined at every watermark
+        *n = h->c_rows - h->c_head;
+        return GW_OK;
+    }
     if (!h->kids.empty()) {
         int64_t sum = h->c_rows - h->c_head;
         for (gw_handle* kid : h->kids) {
@@ -2542,6 +2822,7 @@ int gw_pending_rows(gw_handle* h, int64_t* n) {
 int gw_drain(gw_handle* h, int64_t* key, int64_t* start, int64_t* end, void* result, int64_t cap,
              int64_t* n) {
     if (!h || !n) return GW_E_INVALID;
+    if (h->fe) return gw_drain_payload(h, key, start, end, result, nullptr, cap, n);
     if (!h->kids.empty()) {  // the gathered rows first, then each child's
         int64_t got = 0;
         auto at = [&](int64_t* p) { return p ? p + got : nullptr; };
@@ -2602,6 +2883,15 @@ int gw_drain(gw_handle* h, int64_t* key, int64_t* start, int64_t* end, void* res
 int gw_rows_device(gw_handle* h, const int64_t** d_key, const int64_t** d_start, const int64_t** d_end,
                    const void** d_result, int64_t* n) {
     if (!h) return GW_E_INVALID;
+    if (h->fe) {
+        const int64_t o = h->c_head;
+        if (d_key) *d_key = h->c_key ? h->c_key + o : nullptr;
+        if (d_start) *d_start = h->c_start ? h->c_start + o : nullptr;
+        if (d_end) *d_end = h->c_end ? h->c_end + o : nullptr;
+        if (d_result) *d_result = h->c_res ? h->c_res + o : nullptr;
+        if (n) *n = h->c_rows - h->c_head;
+        return GW_OK;
+    }
     if (!h->kids.empty()) {  // gather the children's pending rows behind the waiting ones
         int64_t add = 0;
         for (gw_handle* kid : h->kids) {
@@ -2682,6 +2972,7 @@ int gw_clear_rows(gw_handle* h) {
 int gw_pending_late(gw_handle* h, int64_t* n) {
     if (!h || !n) return GW_E_INVALID;
     *n = 0;
+    if (h->fe) return gw_pending_late(h->kids[0], n);
     if (!h->kids.empty()) {
         for (gw_handle* kid : h->kids) {
             int64_t p = 0;
@@ -2702,6 +2993,7 @@ int gw_pending_late(gw_handle* h, int64_t* n) {
 int gw_drain_late(gw_handle* h, int64_t* key, int64_t* ts, void* value, int64_t cap, int64_t* n) {
     if (!h || !n) return GW_E_INVALID;
     *n = 0;
+    if (h->fe) return gw_drain_late(h->kids[0], key, ts, value, cap, n);
     if (!h->kids.empty()) {  // each late record is reported by one child (its last window's class)
         int64_t got = 0;
         for (gw_handle* kid : h->kids) {
@@ -2745,6 +3037,7 @@ int gw_drain_late(gw_handle* h, int64_t* key, int64_t* ts, void* value, int64_t 
 
 int64_t gw_late_dropped(const gw_handle* h) {
     if (!h) return 0;
+    if (h->fe) return gw_late_dropped(h->kids[0]);
     if (!h->kids.empty()) {
         int64_t sum = 0;
         for (const gw_handle* kid : h->kids) sum += gw_late_dropped(kid);
@@ -2756,6 +3049,14 @@ int64_t gw_late_dropped(const gw_handle* h) {
 
 int gw_get_stats(const gw_handle* h, gw_stats* out) {
     if (!h || !out) return GW_E_INVALID;
+    if (h->fe) {
+        gw_get_stats(h->kids[0], out);
+        gw_stats b{};
+        gw_get_stats(h->kids[1], &b);
+        out->table_bytes += b.table_bytes;
+        out->rows_fired = h->stats.rows_fired;
+        return GW_OK;
+    }
     if (!h->kids.empty()) {  // records: as one operator sees them; state: summed over the classes
         gw_stats t{};
         for (size_t j = 0; j < h->kids.size(); ++j) {

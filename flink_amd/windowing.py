@@ -361,6 +361,45 @@ class GpuWindowOperator:
         rc = N.lib().gw_ingest(self._h, len(keys), _ptr(keys), _ptr(key_hashes), _ptr(timestamps), _ptr(values))
         N.check(rc, self._h)
 
+    # first-element rows (flags=FLAG_FIRST_ELEMENT) ------------------------------------
+    def process_batch_payload(self, keys, timestamps, values, payload, key_hashes=None):
+        """Records with a 64-bit payload each (the Tuple's non-aggregated fields, packed by the
+        caller); rows carry the payload of their window's first element in arrival order, as
+        SumAggregator / ComparableAggregator keep it (gw_ingest_payload)."""
+        keys = np.ascontiguousarray(keys, dtype=np.int64)
+        timestamps = np.ascontiguousarray(timestamps, dtype=np.int64)
+        values = np.ascontiguousarray(values)
+        values = values.view(np.int64) if values.dtype == np.float64 else values.astype(np.int64, copy=False)
+        payload = np.ascontiguousarray(payload, dtype=np.int64)
+        if key_hashes is not None:
+            key_hashes = np.ascontiguousarray(key_hashes, dtype=np.int32)
+        if not (len(keys) == len(timestamps) == len(values) == len(payload)):
+            raise ValueError("column lengths differ")
+        N.check(N.lib().gw_ingest_payload(self._h, len(keys), _ptr(keys), _ptr(key_hashes), _ptr(timestamps),
+                                          _ptr(values), _ptr(payload)), self._h)
+
+    def process_batch_payload_device(self, keys, timestamps, values, payload, stream=None):
+        """Same, with torch device columns produced on `stream` (default: torch's current)."""
+        if stream is None:
+            import torch
+            stream = torch.cuda.current_stream(keys.device).cuda_stream
+        p = [ctypes.c_void_p(x.data_ptr()) for x in (keys, timestamps, values, payload)]
+        N.check(N.lib().gw_ingest_payload_device(self._h, keys.numel(), p[0], None, p[1], p[2], p[3],
+                                                 ctypes.c_void_p(stream) if stream else None), self._h)
+
+    def drain_payload(self):
+        """All pending rows as numpy (key, start, end, result, payload) columns."""
+        n = self.pending_rows()
+        k, s, e, r, pl = (np.empty(n, np.int64) for _ in range(5))
+        got = ctypes.c_int64(0)
+        if n:
+            N.check(N.lib().gw_drain_payload(self._h, _ptr(k), _ptr(s), _ptr(e), _ptr(r), _ptr(pl), n,
+                                             ctypes.byref(got)), self._h)
+            assert got.value == n
+        if self.is_double_out:
+            r = r.view(np.float64)
+        return k, s, e, r, pl
+
     # network-buffer surface -----------------------------------------------------------
     def process_serialized(self, data: bytes, layout: "N.GwRecordLayout") -> tuple:
         """Decode and process one input channel's serialized elements (records and

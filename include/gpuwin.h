@@ -124,6 +124,12 @@ typedef struct gw_config {
                                         buffering pass-1 segments until the next fire    */
 #define GW_FLAG_LATE_SIDE_OUTPUT  64 /* WindowedStream.sideOutputLateData: late records go to
                                         gw_drain_late instead of numLateRecordsDropped    */
+#define GW_FLAG_FIRST_ELEMENT    128 /* positional sum/min/max (WindowedStream.sum(i) etc.):
+                                        records carry a 64-bit payload (the tuple's other
+                                        fields, packed by the caller) and every row carries the
+                                        payload of its window's first element in arrival
+                                        order (gw_ingest_payload*, gw_drain_payload);
+                                        tumbling / sliding windows with EventTimeTrigger    */
 
 typedef struct gw_handle gw_handle;
 
@@ -270,6 +276,17 @@ int  gw_end_input(gw_handle* h, int64_t* rows_fired);
 int  gw_pending_rows(gw_handle* h, int64_t* n);
 /* Copy up to cap pending rows (key, window start, window end, result) to host
  * arrays and remove them.  Returns GW_E_OUTPUT_FULL if rows remain. */
+/* GW_FLAG_FIRST_ELEMENT handles: the batch with each record's payload (SumAggregator /
+ * ComparableAggregator keep the first element's other fields, RS/api/functions/aggregation/
+ * SumAggregator.java:66-76, ComparableAggregator.java:83-104), and rows with the payload of
+ * their window's first element.  gw_ingest / gw_ingest_device return GW_E_INVALID on such
+ * handles; gw_drain drains the rows without the payload. */
+int  gw_ingest_payload(gw_handle* h, int64_t n, const int64_t* key, const int32_t* key_hash, const int64_t* ts,
+                       const void* value, const int64_t* payload);
+int  gw_ingest_payload_device(gw_handle* h, int64_t n, const int64_t* d_key, const int32_t* d_key_hash,
+                              const int64_t* d_ts, const void* d_value, const int64_t* d_payload, void* stream);
+int  gw_drain_payload(gw_handle* h, int64_t* key, int64_t* start, int64_t* end, void* result, int64_t* payload,
+                      int64_t cap, int64_t* n);
 int  gw_drain(gw_handle* h, int64_t* key, int64_t* start, int64_t* end, void* result,
               int64_t cap, int64_t* n);
 /* Zero-copy device view of the pending rows (for a device-side consumer). */

@@ -14,11 +14,13 @@
  *
  * Output (OutputMode), with the record timestamp window.maxTimestamp() = end - 1
  * (WindowOperator.emitWindowContents :575-580):
- *   POSITIONAL     WindowedStream.sum/min/max(1) on Tuple2<Long, X>: the reduced Tuple2 (key,
- *                  result) -- SumAggregator / ComparableAggregator keep the first element's
- *                  other field, here the key (SumAggregator.java:66-76, ComparableAggregator.
- *                  java:83-104).  Wider tuples carry fields the GPU does not hold: rejected at
- *                  construction (use aggregate(...) instead).
+ *   POSITIONAL     WindowedStream.sum/min/max(i): the window's first element (arrival order)
+ *                  with field i replaced by the result -- SumAggregator / ComparableAggregator
+ *                  keep the first element's other fields (SumAggregator.java:66-76,
+ *                  ComparableAggregator.java:83-104).  Tuple2<Long, X>: (key, result).  Wider
+ *                  tuples: the handle runs with GW_FLAG_FIRST_ELEMENT, each element's payload is
+ *                  its arrival sequence, the elements wait in an ElementLog until no window can
+ *                  reach them, and each row's payload picks its first element.
  *   AGGREGATE      WindowedStream.aggregate(AggregateFunction): getResult(acc) alone (Long for
  *                  count, Double for avg), PassThroughWindowFunction.
  *   KEYED_WINDOW   Tuple4 (key, window start, window end, result), what a ProcessWindowFunction
@@ -28,6 +30,7 @@ package org.apache.flink.streaming.runtime.operators.windowing.gpu;
 
 import org.apache.flink.api.common.externalresource.ExternalResourceInfo;
 import org.apache.flink.api.java.functions.KeySelector;
+import org.apache.flink.api.java.tuple.Tuple;
 import org.apache.flink.api.java.tuple.Tuple2;
 import org.apache.flink.api.java.tuple.Tuple4;
 import org.apache.flink.runtime.state.KeyGroupRange;
@@ -47,6 +50,7 @@ import java.io.DataInputStream;
 import java.io.DataOutputStream;
 import java.nio.ByteBuffer;
 import java.nio.ByteOrder;
+import java.util.ArrayDeque;
 import java.util.ArrayList;
 import java.util.List;
 import java.util.function.ToDoubleFunction;
@@ -70,6 +74,7 @@ public class GpuWindowOperator<IN>
     private final ToLongFunction<IN> longValue;       // for integer aggregates
     private final ToDoubleFunction<IN> doubleValue;   // for f64 aggregates
     private final int batchCapacity;
+    private final int inputArity, positionalField;
 
     private transient long handle;
     private transient ByteBuffer keys, ts, values, oKey, oStart, oEnd, oRes;
@@ -77,17 +82,27 @@ public class GpuWindowOperator<IN>
     private transient List<byte[]> restored;  // per-key-group blobs read in initializeState
     private OutputTag<Tuple2<Long, Object>> lateDataTag;  // sideOutputLateData (null: count and drop)
     private transient ByteBuffer lKey, lTs, lVal;
+    // positional on Tuple3+: payload column (arrival sequence), the elements by sequence, and
+    // per batch (sequence end, max timestamp) for releasing them
+    private transient ByteBuffer payload, oPay;
+    private transient ElementLog<IN> elements;
+    private transient ArrayDeque<long[]> batches;
+    private transient long batchMaxTs;
 
-    /** inputArity: fields of the input Tuple (POSITIONAL needs 2: the Long key and the field). */
+    /** inputArity: fields of the input Tuple; positionalField: the aggregated field of a
+     *  POSITIONAL sum/min/max (the result replaces it in the emitted tuple). */
     public GpuWindowOperator(int assigner, long size, long slide, long offset, long gap, long lateness,
                              int trigger, int agg, KeySelector<IN, Long> keySelector,
                              ToLongFunction<IN> longValue, ToDoubleFunction<IN> doubleValue, int batchCapacity,
-                             OutputMode mode, int inputArity) {
-        if (mode == OutputMode.POSITIONAL && inputArity != 2) {
+                             OutputMode mode, int inputArity, int positionalField) {
+        if (mode == OutputMode.POSITIONAL && inputArity > 2
+                && (assigner > 1 /* tumbling, sliding */ || trigger != 0 /* EventTimeTrigger */)) {
             throw new IllegalArgumentException(
-                    "positional sum/min/max on the GPU keep only the key and the aggregated field: "
-                            + "the input must be a Tuple2<Long, X> (got arity " + inputArity + ")");
+                    "positional sum/min/max on Tuple3+ runs on tumbling / sliding event-time windows with "
+                            + "EventTimeTrigger (GW_FLAG_FIRST_ELEMENT); use aggregate(...) otherwise");
         }
+        this.inputArity = inputArity;
+        this.positionalField = positionalField;
         this.assigner = assigner; this.size = size; this.slide = slide; this.offset = offset;
         this.gap = gap; this.lateness = lateness; this.trigger = trigger; this.agg = agg;
         this.keySelector = keySelector; this.longValue = longValue; this.doubleValue = doubleValue;
@@ -111,10 +126,17 @@ public class GpuWindowOperator<IN>
         int parallelism = getRuntimeContext().getTaskInfo().getNumberOfParallelSubtasks();
         int maxP = getRuntimeContext().getTaskInfo().getMaxNumberOfParallelSubtasks();
         int device = gpuIndex();
-        final int flags = lateDataTag != null ? 64 /* GW_FLAG_LATE_SIDE_OUTPUT */ : 0;
+        final int flags = (lateDataTag != null ? 64 /* GW_FLAG_LATE_SIDE_OUTPUT */ : 0)
+                | (wide() ? 128 /* GW_FLAG_FIRST_ELEMENT */ : 0);
         handle = nativeCreate(assigner, trigger, size, slide, offset, gap, lateness, agg, maxP, parallelism,
                               subtask, device, flags, 1L << 24, batchCapacity);
         if (lateDataTag != null) { lKey = direct(8); lTs = direct(8); lVal = direct(8); }
+        if (wide()) {
+            payload = direct(8); oPay = direct(8);
+            elements = new ElementLog<>();
+            batches = new ArrayDeque<>();
+            batchMaxTs = Long.MIN_VALUE;
+        }
         keys = direct(8); ts = direct(8); values = direct(8);
         oKey = direct(8); oStart = direct(8); oEnd = direct(8); oRes = direct(8);
         if (restored != null) {  // initializeState runs before open (StreamOperator.java:139)
@@ -182,12 +204,36 @@ public class GpuWindowOperator<IN>
         ts.putLong(n * 8, element.getTimestamp());
         if (doubleValue != null) values.putDouble(n * 8, doubleValue.applyAsDouble(v));
         else if (longValue != null) values.putLong(n * 8, longValue.applyAsLong(v));
+        if (wide()) {
+            payload.putLong(n * 8, elements.append(v));
+            batchMaxTs = Math.max(batchMaxTs, element.getTimestamp());
+        }
         if (++n == batchCapacity) flush();
+    }
+
+    private boolean wide() { return mode == OutputMode.POSITIONAL && inputArity > 2; }
+
+    /** The first element with the aggregated field replaced by the result, in the field's own type. */
+    private Object positionalRow(IN first, Object res) {
+        Tuple t = ((Tuple) first).copy();
+        Object f = t.getField(positionalField);
+        if (f instanceof Integer) res = (int) (long) (Long) res;
+        else if (f instanceof Short) res = (short) (long) (Long) res;
+        else if (f instanceof Byte) res = (byte) (long) (Long) res;
+        else if (f instanceof Float) res = (float) (double) (Double) res;
+        t.setField(res, positionalField);
+        return t;
     }
 
     private void flush() {
         // the key hash column is null: keys are Longs, whose hashCode the GPU computes
-        if (n > 0) nativeIngest(handle, n, keys, null, ts, values);
+        if (n > 0 && wide()) {
+            nativeIngestPayload(handle, n, keys, ts, values, payload);
+            batches.addLast(new long[] {elements.end(), batchMaxTs});
+            batchMaxTs = Long.MIN_VALUE;
+        } else if (n > 0) {
+            nativeIngest(handle, n, keys, null, ts, values);
+        }
         n = 0;
         if (lateDataTag != null) emitLate();
         // CountTrigger fires on the element: count-window rows exist right after the batch
@@ -196,13 +242,16 @@ public class GpuWindowOperator<IN>
 
     private void emitRows() {
         int got;
-        while ((got = nativeDrain(handle, oKey, oStart, oEnd, oRes, batchCapacity)) > 0) {
+        while ((got = wide() ? nativeDrainPayload(handle, oKey, oStart, oEnd, oRes, oPay, batchCapacity)
+                             : nativeDrain(handle, oKey, oStart, oEnd, oRes, batchCapacity)) > 0) {
             for (int i = 0; i < got; i++) {
                 long key = oKey.getLong(i * 8), end = oEnd.getLong(i * 8);
                 Object res = agg == 2 || agg >= 5 && agg <= 8 ? (Object) oRes.getDouble(i * 8) : oRes.getLong(i * 8);
                 Object row;
                 switch (mode) {
-                    case POSITIONAL: row = Tuple2.of(key, res); break;
+                    case POSITIONAL:
+                        row = wide() ? positionalRow(elements.get(oPay.getLong(i * 8)), res) : Tuple2.of(key, res);
+                        break;
                     case AGGREGATE: row = res; break;
                     default: row = Tuple4.of(key, oStart.getLong(i * 8), end, res);
                 }
@@ -230,7 +279,51 @@ public class GpuWindowOperator<IN>
         flush();
         nativeAdvanceWatermark(handle, mark.getTimestamp());
         emitRows();
+        if (wide()) releaseElements(mark.getTimestamp());
         super.processWatermark(mark);  // forward after the fired rows
+    }
+
+    /** A batch's elements leave the log once every window they could fall in is cleaned up
+     *  (maxTs + size - 1 + allowed lateness <= watermark: WindowOperator.cleanupTime), the rule
+     *  the native payload log releases by. */
+    private void releaseElements(long wm) {
+        while (!batches.isEmpty()) {
+            long[] b = batches.peekFirst();
+            long ct = b[1] + (size - 1);
+            ct = ct < b[1] ? Long.MAX_VALUE : ct;  // saturate like the window's cleanup time
+            ct = ct + lateness < ct ? Long.MAX_VALUE : ct + lateness;
+            if (b[1] != Long.MIN_VALUE && ct > wm) break;
+            elements.releaseUpTo(b[0]);
+            batches.pollFirst();
+        }
+    }
+
+    /** Elements by arrival sequence, a growable ring: append at the end, release from the start. */
+    private static final class ElementLog<T> {
+        private Object[] ring = new Object[1024];
+        private long start, end;
+
+        long append(T v) {
+            if (end - start == ring.length) {
+                Object[] r = new Object[ring.length * 2];
+                for (long q = start; q < end; q++) r[(int) (q % r.length)] = ring[(int) (q % ring.length)];
+                ring = r;
+            }
+            ring[(int) (end % ring.length)] = v;
+            return end++;
+        }
+
+        @SuppressWarnings("unchecked")
+        T get(long seq) {
+            if (seq < start || seq >= end) throw new IllegalStateException("element " + seq + " was released");
+            return (T) ring[(int) (seq % ring.length)];
+        }
+
+        long end() { return end; }
+
+        void releaseUpTo(long seqEnd) {
+            for (; start < seqEnd; start++) ring[(int) (start % ring.length)] = null;
+        }
     }
 
     @Override
@@ -253,6 +346,10 @@ public class GpuWindowOperator<IN>
     private static native long nativeAdvanceWatermark(long h, long wm);
     private static native int nativeDrain(long h, ByteBuffer key, ByteBuffer start, ByteBuffer end, ByteBuffer result,
                                           int cap);
+    private static native void nativeIngestPayload(long h, int n, ByteBuffer keys, ByteBuffer ts, ByteBuffer values,
+                                                   ByteBuffer payload);
+    private static native int nativeDrainPayload(long h, ByteBuffer key, ByteBuffer start, ByteBuffer end,
+                                                 ByteBuffer result, ByteBuffer payload, int cap);
     private static native long nativeLateDropped(long h);
     private static native void nativeDestroy(long h);
     private static native void nativeFlush(long h);

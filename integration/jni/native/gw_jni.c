@@ -86,6 +86,29 @@ JNIEXPORT jint JNICALL CLS(nativeDrain)(JNIEnv* env, jclass c, jlong h, jobject 
     return (jint)n;
 }
 
+/* Positional sum/min/max on Tuple3+ (GW_FLAG_FIRST_ELEMENT): the batch with a payload column
+ * (the operator's arrival sequence of each element) ... */
+JNIEXPORT void JNICALL CLS(nativeIngestPayload)(JNIEnv* env, jclass c, jlong h, jint n, jobject keys, jobject ts,
+                                                jobject values, jobject payload) {
+    gw_handle* g = (gw_handle*)(intptr_t)h;
+    fail(env, g, gw_ingest_payload(g, n, (*env)->GetDirectBufferAddress(env, keys), 0,
+                                   (*env)->GetDirectBufferAddress(env, ts), (*env)->GetDirectBufferAddress(env, values),
+                                   (*env)->GetDirectBufferAddress(env, payload)));
+}
+
+/* ... and rows with their window's first-element payload: up to cap rows into five direct
+ * buffers; returns the count (more may remain). */
+JNIEXPORT jint JNICALL CLS(nativeDrainPayload)(JNIEnv* env, jclass c, jlong h, jobject key, jobject start,
+                                               jobject end, jobject result, jobject payload, jint cap) {
+    gw_handle* g = (gw_handle*)(intptr_t)h;
+    int64_t n = 0;
+    int rc = gw_drain_payload(g, (*env)->GetDirectBufferAddress(env, key), (*env)->GetDirectBufferAddress(env, start),
+                              (*env)->GetDirectBufferAddress(env, end), (*env)->GetDirectBufferAddress(env, result),
+                              (*env)->GetDirectBufferAddress(env, payload), cap, &n);
+    fail(env, g, rc);
+    return (jint)n;
+}
+
 JNIEXPORT jlong JNICALL CLS(nativeLateDropped)(JNIEnv* env, jclass c, jlong h) {
     return gw_late_dropped((gw_handle*)(intptr_t)h);
 }

@@ -98,3 +98,65 @@ def test_exchange_glue_maps_invalid_arguments(jni):
         assert create(env, None, nranks, rank, ctypes.cast(idbuf, p), 0, maxp) == 0
         exc = exception(jni)
         assert exc is not None and exc[0] == "java/lang/IllegalArgumentException"
+
+
+def _payload_fns(jni):
+    p, i32, i64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64
+    ing = getattr(jni, CLS + "nativeIngestPayload")
+    ing.restype = None
+    ing.argtypes = [p, p, i64, i32, p, p, p, p]
+    dr = getattr(jni, CLS + "nativeDrainPayload")
+    dr.restype = i32
+    dr.argtypes = [p, p, i64, p, p, p, p, p, i32]
+    adv = getattr(jni, CLS + "nativeAdvanceWatermark")
+    adv.restype = i64
+    adv.argtypes = [p, p, i64, i64]
+    return ing, dr, adv
+
+
+def test_payload_glue_null_handle(jni):
+    """nativeIngestPayload on no handle: gw_ingest_payload's GW_E_INVALID -> IllegalArgumentException."""
+    ing, _, _ = _payload_fns(jni)
+    env = jni.fake_env()
+    col = np.zeros(4, np.int64)
+    ing(env, None, 0, 4, col.ctypes.data, col.ctypes.data, col.ctypes.data, col.ctypes.data)
+    exc = exception(jni)
+    assert exc is not None and exc[0] == "java/lang/IllegalArgumentException"
+
+
+@pytest.mark.gpu
+def test_payload_glue_positional_rows(jni):
+    """GpuWindowOperator's Tuple3+ positional path through the glue on a GPU: payload = arrival
+    sequence, each row's payload = the sequence of its window's first element (min over the
+    window's records in arrival order), result = the window's sum."""
+    ing, dr, adv = _payload_fns(jni)
+    env = jni.fake_env()
+    create = getattr(jni, CLS + "nativeCreate")
+    h = create(env, None, 0, 0, 100, 0, 0, 0, 0, 1, 128, 1, 0, 0, N.FLAG_FIRST_ELEMENT, 1 << 16, 1 << 16)
+    assert h and exception(jni) is None
+    rng = np.random.default_rng(3)
+    n = 5000
+    keys = rng.integers(0, 50, n).astype(np.int64)
+    ts = rng.integers(0, 1000, n).astype(np.int64)
+    vals = rng.integers(-1000, 1000, n).astype(np.int64)
+    seq = np.arange(n, dtype=np.int64)
+    try:
+        ing(env, None, h, n, keys.ctypes.data, ts.ctypes.data, vals.ctypes.data, seq.ctypes.data)
+        assert exception(jni) is None
+        fired = adv(env, None, h, (1 << 63) - 1)
+        assert exception(jni) is None
+        cols = [np.zeros(fired, np.int64) for _ in range(5)]
+        got = dr(env, None, h, *[c.ctypes.data for c in cols], fired)
+        assert got == fired and exception(jni) is None
+    finally:
+        getattr(jni, CLS + "nativeDestroy")(env, None, ctypes.c_int64(h))
+    exp = {}
+    for i in range(n):
+        w = (int(keys[i]), int(ts[i]) // 100 * 100)
+        s, first = exp.get(w, (0, i))
+        exp[w] = (s + int(vals[i]), first)
+    k, s, e, r, pl = cols
+    assert len(k) == len(exp)
+    for j in range(len(k)):
+        assert (int(r[j]), int(pl[j])) == exp[(int(k[j]), int(s[j]))]
+        assert e[j] == s[j] + 100
