@@ -144,6 +144,12 @@ struct IngestArgs {
     int64_t cls_off;
     int32_t cls_J;      // 0 or 1: not a window class
     int32_t cls_j;
+    // size < slide (gw_runtime.cpp: pane width = slide, one pane per window): a record whose
+    // offset in its pane is >= gap_size lies between two windows and belongs to none
+    int64_t gap_w;      // pane width (= slide) when gap_size > 0
+    int64_t gap_size;   // window size, 0: no gaps
+    int64_t gap_late;   // a record in a gap is late iff ts <= gap_late (= watermark - lateness:
+                        // isElementLate, WindowOperator.java:620-623)
     int64_t* d_key;     // deferred list (append at st->n_deferred)
     int64_t* d_pane;
     int64_t* d_a0;

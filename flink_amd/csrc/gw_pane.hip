@@ -81,6 +81,12 @@ __device__ __forceinline__ int classify(const IngestArgs& a, int64_t ts, int64_t
     if (ts == INT64_MIN) { flags |= GW_DF_NO_TS; return REC_SKIP; }
     if (ts < a.t_late) {  // every window of the record is late: isSkippedElement && isElementLate
         if (!a.late_exact) { flags |= GW_DF_RANGE; return REC_SKIP; }
+        if (a.gap_size) {  // t_late is a pane boundary: the record's offset into its pane
+            const uint64_t r = ((uint64_t)a.t_late - (uint64_t)ts) % (uint64_t)a.gap_w;
+            const uint64_t off = r ? (uint64_t)a.gap_w - r : 0;
+            // no window: isSkippedElement, and late only by its own timestamp
+            if (off >= (uint64_t)a.gap_size && ts > a.gap_late) return REC_SKIP;
+        }
         if (a.cls_J > 1) {  // window class: only the class of the record's last window reports it
             // (wrapping subtraction: timestamps within |offset| of Long.MIN_VALUE wrap as in Java)
             const int64_t k = floor_div_d((int64_t)((uint64_t)ts - (uint64_t)a.cls_off), a.cls_slide);
@@ -94,6 +100,10 @@ __device__ __forceinline__ int classify(const IngestArgs& a, int64_t ts, int64_t
     }
     const uint64_t R = (uint64_t)a.t.ring;
     const uint64_t q = udiv64((uint64_t)ts - (uint64_t)a.t_late, a.div);
+    // between two windows (size < slide): assignWindows gives the record no window and it is
+    // not late, so processElement does nothing with it
+    if (a.gap_size && (uint64_t)ts - (uint64_t)a.t_late - q * (uint64_t)a.gap_w >= (uint64_t)a.gap_size)
+        return REC_SKIP;
     record_cell(AGG, v, c0, c1);
     pane = a.p_late + (int64_t)q;
     if (q < a.q_refire) return REC_REFIRE;

@@ -186,6 +186,7 @@ struct gw_handle {
 
     // pane geometry
     int64_t g = 1, m = 1, n = 1;
+    int64_t gap_size = 0;  // size < slide: panes of width slide, records past `size` into one are skipped
     int R = 2;
     UDiv64 div{};
 
@@ -932,6 +933,11 @@ struct gw_handle {
         a.late_exact = exact;
         a.t = tv;
         a.cls_J = (int32_t)cls_J; a.cls_j = (int32_t)cls_j; a.cls_slide = cls_slide; a.cls_off = cls_off;
+        a.gap_w = g; a.gap_size = gap_size;
+        {
+            const i128 gl = (i128)wm - (i128)cfg.allowed_lateness;
+            a.gap_late = gl < (i128)INT64_MIN ? INT64_MIN : (int64_t)gl;
+        }
         a.d_key = dk[cur]; a.d_pane = dp[cur]; a.d_a0 = da0[cur]; a.d_a1 = da1[cur];
         a.st = d_st;
         // panes up to the last one of the last fired window re-fire (lateness > 0)
@@ -1735,8 +1741,18 @@ static int validate(const gw_config* c, std::string& why) {
 // Ring positions a sliding (or tumbling: slide = size) assigner needs: the n panes of the
 // oldest unfired window + at least one slide ahead, plus, with allowed lateness, the panes
 // of fired windows kept until their cleanup (ceil(lateness / slide) + 1 more slides).
+// Pane geometry (width g, n panes per window, m per slide): g = gcd(size, slide), except for
+// size < slide, where a pane is one slide with the window at its start and the rest a gap.
+static void pane_geometry(int64_t size, int64_t slide, int64_t& g, int64_t& n, int64_t& m) {
+    if (size < slide) {
+        g = slide; n = 1; m = 1;
+    } else {
+        g = gcd64(size, slide); n = size / g; m = slide / g;
+    }
+}
 static int64_t ring_need(int64_t size, int64_t slide, int64_t lateness) {
-    const int64_t g = gcd64(size, slide), m = slide / g, n = size / g;
+    int64_t g, n, m;
+    pane_geometry(size, slide, g, n, m);
     if (n > kMaxRing || m > kMaxRing) return kMaxRing + 1;
     int64_t need = n + std::max<int64_t>(m, 1);
     if (lateness > 0) {
@@ -1755,9 +1771,14 @@ static int64_t class_count(int64_t size, int64_t slide, int64_t lateness) {
     }
     return 0;
 }
-// A composite handle h (its cfg set): J children on child 0's stream.
+// A composite handle h (its cfg set): J children on child 0's stream.  Tumbling windows split
+// the same way: class j is a sliding assigner (size, J * size, offset + j * size).
 static int make_composite(gw_handle* h, int64_t J) {
-    const gw_config& c = h->cfg;
+    gw_config c = h->cfg;
+    if (c.assigner == GW_TUMBLING) {
+        c.assigner = GW_SLIDING;
+        c.slide = c.size;
+    }
     if (h->stream) {  // the composite launches nothing of its own
         hipStreamSynchronize(h->stream);
         hipStreamDestroy(h->stream);
@@ -1888,16 +1909,15 @@ int gw_create(const gw_config* cfg, gw_handle** out) {
     }
     const int64_t size = cfg->size;
     const int64_t slide = cfg->assigner == GW_TUMBLING ? cfg->size : cfg->slide;
-    h->g = gcd64(size, slide);
-    h->m = slide / h->g;
-    h->n = size / h->g;
+    pane_geometry(size, slide, h->g, h->n, h->m);
+    h->gap_size = size < slide ? size : 0;
     // ring: n panes of the oldest unfired window + at least one pane ahead, filling
     // the slot up to the next 64-byte line
     int64_t need = ring_need(size, slide, cfg->allowed_lateness);
     if (need > kMaxRing) {
         // more panes than one ring holds: split the windows into J classes (k mod J), each a
         // sliding assigner of slide J * slide whose ring fits (gcd(size, J * slide) grows)
-        const int64_t J = cfg->assigner == GW_SLIDING ? class_count(size, slide, cfg->allowed_lateness) : 0;
+        const int64_t J = class_count(size, slide, cfg->allowed_lateness);
         if (J == 0)
             return bail(GW_E_UNSUPPORTED, cfg->allowed_lateness > 0
                                               ? "allowed lateness spanning more than 64 panes of the ring is not "
@@ -2590,6 +2610,7 @@ int gw_flush(gw_handle* h) {
 // the class of their window.  Layout per key group (snapshot_heap): be32 n + n entries of
 // (start, end, key, state), be32 0 (no merging window set), be32 t + t timers of 32 bytes.
 typedef gw_handle::SnapHeader SnapHdr;
+static int64_t comp_slide(const gw_handle* h) { return h->cfg.assigner == GW_TUMBLING ? h->cfg.size : h->cfg.slide; }
 static int comp_snapshot(gw_handle* h, int32_t kg_lo, int32_t kg_hi, void* buf, int64_t cap, int64_t* len) {
     const int64_t nk = (int64_t)kg_hi - kg_lo + 1;
     if (kg_lo < 0 || nk <= 0) return h->fail(GW_E_INVALID, "bad key-group range");
@@ -2638,7 +2659,8 @@ static int comp_snapshot(gw_handle* h, int32_t kg_lo, int32_t kg_hi, void* buf, 
     if (cap < need) return h->fail(GW_E_OUTPUT_FULL, "snapshot needs %lld bytes", (long long)need);
     SnapHdr hd;
     memcpy(&hd, blobs[0].data(), sizeof hd);
-    hd.slide = h->cfg.slide;
+    hd.assigner = h->cfg.assigner;
+    hd.slide = comp_slide(h);
     hd.offset = h->cfg.offset;
     hd.entries = (int64_t)pay.size();
     char* out = (char*)buf;
@@ -2653,7 +2675,7 @@ static int comp_restore(gw_handle* h, const void* buf, int64_t len) {
     SnapHdr hd;
     memcpy(&hd, buf, sizeof hd);
     if (memcmp(hd.magic, "GWS1", 4) != 0 || hd.version != 4 || hd.agg != h->cfg.agg ||
-        hd.assigner != h->cfg.assigner || hd.size != h->cfg.size || hd.slide != h->cfg.slide ||
+        hd.assigner != h->cfg.assigner || hd.size != h->cfg.size || hd.slide != comp_slide(h) ||
         hd.offset != h->cfg.offset || hd.max_parallelism != h->cfg.max_parallelism)
         return h->fail(GW_E_INVALID, "snapshot of a different window / aggregate / max parallelism");
     const int64_t nk = (int64_t)hd.kg_hi - hd.kg_lo + 1;
@@ -2663,7 +2685,7 @@ static int comp_restore(gw_handle* h, const void* buf, int64_t len) {
     const uint8_t* p = (const uint8_t*)buf + hb;
     const uint8_t* end = p + hd.entries;
     auto cls = [&](int64_t s0) {  // window class of a window start
-        const int64_t k = (int64_t)floor_div((i128)s0 - h->cfg.offset, (i128)h->cfg.slide);
+        const int64_t k = (int64_t)floor_div((i128)s0 - h->cfg.offset, (i128)comp_slide(h));
         return (size_t)(((k % J) + J) % J);
     };
     std::vector<std::vector<uint8_t>> pay(J);
@@ -2703,6 +2725,7 @@ static int comp_restore(gw_handle* h, const void* buf, int64_t len) {
     for (int64_t j = 0; j < J; ++j) {
         offs[j][nk] = (int64_t)pay[j].size();
         SnapHdr kh = hd;
+        kh.assigner = h->kids[j]->cfg.assigner;
         kh.slide = h->kids[j]->cfg.slide;
         kh.offset = h->kids[j]->cfg.offset;
         kh.entries = (int64_t)pay[j].size();

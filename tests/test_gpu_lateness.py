@@ -115,14 +115,6 @@ def test_lateness_preaggregation_path(oracle_lib):
     assert compare(g, o, False) == []
 
 
-def test_lateness_beyond_the_ring_is_unsupported():
-    # tumbling windows cannot be split into window classes (tests/test_gpu_window_classes.py
-    # covers the sliding case, which is)
-    with pytest.raises(N.GpuWinError) as ei:
-        gpu_operator(dict(assigner="tumbling", size=100, agg="sum_i64", lateness=10_000))
-    assert ei.value.code == -2
-
-
 # ------------------------------------------------------------------ session windows
 # Merging windows with allowed lateness (WindowOperator.java:303-403 merging branch):
 # a session keeps its state until max timestamp + lateness; a late element that lands in

@@ -26,15 +26,19 @@ CONFIGS = [
     dict(assigner="sliding", size=7000, slide=60, offset=-25),     # gcd 20, n = 350: 10 classes
     dict(assigner="sliding", size=3000, slide=40),                 # n = 75: 2 classes
     dict(assigner="sliding", size=1000, slide=100, lateness=10_000),  # lateness over 102 panes
+    dict(assigner="tumbling", size=100, lateness=10_000),           # 102 windows of lateness: 3 classes
+    dict(assigner="tumbling", size=60, offset=-7, lateness=5_000),  # 85 windows: 2 classes
+    dict(assigner="sliding", size=300, slide=100, lateness=20_000), # classes of slide >= size (gapped)
 ]
 
 
 def _classes(kw):
-    size, slide, lat = kw["size"], kw["slide"], kw.get("lateness", 0)
+    size, lat = kw["size"], kw.get("lateness", 0)
+    slide = kw.get("slide", size)
 
     def need(sl):
-        g = np.gcd(size, sl)
-        n, m = size // g, sl // g
+        g = sl if size < sl else np.gcd(size, sl)  # size < slide: one pane per slide (gapped)
+        n, m = (1, 1) if size < sl else (size // g, sl // g)
         r = n + max(m, 1)
         if lat:
             extra = lat // sl + 2
@@ -130,6 +134,7 @@ def test_window_classes_rows_device_and_stats(oracle_lib):
 SNAP_CFGS = [
     dict(assigner="sliding", size=1000, slide=10),
     dict(assigner="sliding", size=1000, slide=100, lateness=10_000),
+    dict(assigner="tumbling", size=100, lateness=10_000),
 ]
 
 
@@ -181,10 +186,53 @@ def test_window_classes_restore(oracle_lib, cfg, agg, writer):
     assert glate == rlate
 
 
-def test_tumbling_lateness_beyond_the_ring_is_unsupported():
+def test_lateness_beyond_4096_classes_is_unsupported():
+    # tumbling windows of 1 ms with ~1e9 windows of lateness: no split into <= 4096 classes fits
     with pytest.raises(N.GpuWinError) as ei:
-        gpu_operator(dict(assigner="tumbling", size=100, agg="sum_i64", lateness=10_000))
+        gpu_operator(dict(assigner="tumbling", size=1, agg="sum_i64", lateness=10 ** 9))
     assert ei.value.code == -2
+
+
+GAPPED = [
+    dict(assigner="sliding", size=30, slide=100),
+    dict(assigner="sliding", size=70, slide=250, offset=-40),
+    dict(assigner="sliding", size=30, slide=100, lateness=1_500),
+]
+
+
+@pytest.mark.parametrize("agg", ["sum_i64", "count", "min_f64"])
+@pytest.mark.parametrize("kw", GAPPED, ids=lambda c: "-".join(str(v) for v in c.values()))
+@pytest.mark.parametrize("flags", [0, N.FLAG_FORCE_REGION, N.FLAG_LATE_SIDE_OUTPUT], ids=["auto", "region", "side"])
+def test_sliding_with_gaps_vs_oracle(oracle_lib, kw, agg, flags):
+    """size < slide (SlidingEventTimeWindows allows it): one pane per slide, the window at its
+    start; a record in the gap gets no window (assignWindows returns none) and is dropped
+    silently unless it is late (isSkippedElement && isElementLate, WindowOperator.java:440-446)."""
+    kw = dict(kw, agg=agg)
+    lat = kw.get("lateness", 0)
+    keys, ts, vals, batches = random_stream(seed=zlib.crc32(f"gap{kw}".encode()) & 0xffff, n=15000, num_keys=70,
+                                            n_batches=20, ts_step=3, disorder=900 if lat else 400, wm_lag=250,
+                                            agg=agg)
+    if flags == N.FLAG_LATE_SIDE_OUTPUT:
+        op = gpu_operator(kw, flags=flags)
+        ora = oracle_lib.OracleOperator(oracle_lib.make_config(**kw, flags=flags))
+        for b, (lo, hi, wm) in enumerate(batches):
+            op.process_batch(keys[lo:hi], ts[lo:hi], vals[lo:hi])
+            op.advance_watermark(wm)
+            vb = vals.view(np.int64) if vals.dtype == np.float64 else vals
+            ora.process_batch(keys[lo:hi], ts[lo:hi], vb[lo:hi])
+            ora.process_watermark(wm)
+            k, s, e, r = op.drain()
+            assert compare([(k, s, e, r.view(np.int64))], [ora.drain()], agg in DOUBLE) == []
+            got = sorted(zip(*[c.tolist() for c in op.drain_late()]))
+            exp = sorted(zip(*[c.tolist() for c in ora.drain_late()]))
+            assert got == exp, f"side output at watermark #{b}"
+        op.close()
+        ora.close()
+        return
+    g, glate, stats = run_gpu(kw, keys, ts, vals, batches, flags=flags)
+    o, olate = run_oracle(oracle_lib, kw, keys, ts, vals, batches)
+    assert glate == olate
+    assert compare(g, o, agg in DOUBLE) == []
 
 
 def test_window_classes_network_buffers(oracle_lib):
