@@ -74,14 +74,14 @@ __device__ __forceinline__ int64_t floor_div_d(int64_t a, int64_t b) {
 // Per-record classification: late / parked (outside the pane ring) / in ring / re-fire
 // (allowed lateness > 0: the pane belongs to a fired window that is not cleaned yet).
 enum { REC_SKIP = 0, REC_RING = 1, REC_DEFER = 2, REC_REFIRE = 3, REC_LATE = 4 };
-template <int AGG>
+template <int AGG, bool GAP = true>
 __device__ __forceinline__ int classify(const IngestArgs& a, int64_t ts, int64_t v, uint32_t& pos, int64_t& pane,
                                         int64_t& c0, int64_t& c1, unsigned long long& late,
                                         unsigned long long& flags) {
     if (ts == INT64_MIN) { flags |= GW_DF_NO_TS; return REC_SKIP; }
     if (ts < a.t_late) {  // every window of the record is late: isSkippedElement && isElementLate
         if (!a.late_exact) { flags |= GW_DF_RANGE; return REC_SKIP; }
-        if (a.gap_size) {  // t_late is a pane boundary: the record's offset into its pane
+        if (GAP && a.gap_size) {  // t_late is a pane boundary: the record's offset into its pane
             const uint64_t r = ((uint64_t)a.t_late - (uint64_t)ts) % (uint64_t)a.gap_w;
             const uint64_t off = r ? (uint64_t)a.gap_w - r : 0;
             // no window: isSkippedElement, and late only by its own timestamp
@@ -102,7 +102,7 @@ __device__ __forceinline__ int classify(const IngestArgs& a, int64_t ts, int64_t
     const uint64_t q = udiv64((uint64_t)ts - (uint64_t)a.t_late, a.div);
     // between two windows (size < slide): assignWindows gives the record no window and it is
     // not late, so processElement does nothing with it
-    if (a.gap_size && (uint64_t)ts - (uint64_t)a.t_late - q * (uint64_t)a.gap_w >= (uint64_t)a.gap_size)
+    if (GAP && a.gap_size && (uint64_t)ts - (uint64_t)a.t_late - q * (uint64_t)a.gap_w >= (uint64_t)a.gap_size)
         return REC_SKIP;
     record_cell(AGG, v, c0, c1);
     pane = a.p_late + (int64_t)q;
@@ -511,7 +511,7 @@ __global__ void __launch_bounds__(256) k_publish_status(const DevStatus* st, Dev
 #else
 #define GW_APPLY_ATTR
 #endif
-template <int AGG, bool CMP>
+template <int AGG, bool CMP, bool GAP>
 __global__ void __launch_bounds__(kPartThreads) GW_P1_ATTR k_rgn_p1(IngestArgs a) {
     constexpr bool C = CMP && cmp_agg<AGG>();
     constexpr bool AV = !C && (AGG == GW_AVG_I64 || AGG == GW_AVG_F64);
@@ -553,7 +553,7 @@ __global__ void __launch_bounds__(kPartThreads) GW_P1_ATTR k_rgn_p1(IngestArgs a
         uint32_t ps = 0;
         int st = REC_SKIP;
         int64_t pane = 0;
-        if (i < hi) st = classify<AGG>(a, ts[it], val[it], ps, pane, v0, v1, late, flags);
+        if (i < hi) st = classify<AGG, GAP>(a, ts[it], val[it], ps, pane, v0, v1, late, flags);
         if (C && ACC && st == REC_RING && (v0 < INT32_MIN || v0 > INT32_MAX)) {
             st = REC_DEFER;  // beyond the compact record's 32-bit value: exact via the deferred list
             wide++;
@@ -1869,13 +1869,20 @@ hipError_t launch_region_p1(const IngestArgs& a, hipStream_t s) {
     if (tiles == 0) return hipSuccess;
     const size_t part_lds = part_lds_bytes(a);
     // beyond the 64 KB default: opt in (gfx950 has 160 KB of LDS per CU)
+    // the gap test (size < slide) only in a variant of its own: it costs the hot pass ~3%
 #define L(A)                                                                                                    \
-    if (a.cmp) {                                                                                                \
-        lds_opt_in((const void*)k_rgn_p1<A, true>, part_lds);                                                  \
-        hipLaunchKernelGGL((k_rgn_p1<A, true>), dim3((unsigned)tiles), dim3(kPartThreads), part_lds, s, a);    \
+    if (a.gap_size) {                                                                                           \
+        lds_opt_in((const void*)k_rgn_p1<A, false, true>, part_lds);                                           \
+        hipLaunchKernelGGL((k_rgn_p1<A, false, true>), dim3((unsigned)tiles), dim3(kPartThreads), part_lds, s, \
+                           a);                                                                                  \
+    } else if (a.cmp) {                                                                                         \
+        lds_opt_in((const void*)k_rgn_p1<A, true, false>, part_lds);                                           \
+        hipLaunchKernelGGL((k_rgn_p1<A, true, false>), dim3((unsigned)tiles), dim3(kPartThreads), part_lds, s, \
+                           a);                                                                                  \
     } else {                                                                                                    \
-        lds_opt_in((const void*)k_rgn_p1<A, false>, part_lds);                                                 \
-        hipLaunchKernelGGL((k_rgn_p1<A, false>), dim3((unsigned)tiles), dim3(kPartThreads), part_lds, s, a);   \
+        lds_opt_in((const void*)k_rgn_p1<A, false, false>, part_lds);                                          \
+        hipLaunchKernelGGL((k_rgn_p1<A, false, false>), dim3((unsigned)tiles), dim3(kPartThreads), part_lds,   \
+                           s, a);                                                                               \
     }
     GW_AGG_SWITCH(a.t.agg, L);
 #undef L

@@ -985,7 +985,8 @@ struct gw_handle {
         const bool int_agg = agg == GW_COUNT || agg == GW_SUM_I64 || agg == GW_SUM_I32 || agg == GW_MIN_I64 ||
                              agg == GW_MAX_I64 || agg == GW_AVG_I64;
         static const bool env_off = getenv("GW_NO_COMPACT") != nullptr;
-        return int_agg && !cmp_off && !env_off && d1_bits >= 2 && (int64_t)tv.ring <= ((int64_t)1 << (d1_bits - 1));
+        // gapped panes (size < slide) use the wide pass 1, the one instantiated with the gap test
+        return int_agg && !cmp_off && !env_off && !gap_size && d1_bits >= 2 && (int64_t)tv.ring <= ((int64_t)1 << (d1_bits - 1));
     }
 
     // P2 + apply over every waiting segment (one fire's worth of batches).  Runs before
