@@ -7,7 +7,10 @@
 
 namespace gw {
 
-constexpr int kNbChunk = 1024;  // bytes per wave in the chain walk
+#ifndef GW_NB_CHUNK
+#define GW_NB_CHUNK 1024
+#endif
+constexpr int kNbChunk = GW_NB_CHUNK;  // bytes per wave in the chain walk
 
 // The record value layout reduced to what the decoder needs (validated on the host).
 struct NbLayout {
@@ -25,6 +28,7 @@ struct NbStatus {
     long long consumed;              // bytes up to the end of the last complete element
     long long records, watermarks;
     unsigned long long walkback;     // chunk steps k_nb_resolve walked back over non-converged chunks
+    unsigned long long fallback;     // chunks whose candidates disagreed after the sync window
 };
 
 inline int nb_field_width(char t) {

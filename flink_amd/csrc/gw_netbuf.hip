@@ -35,6 +35,10 @@ constexpr int nb_words() { return (kNbChunk + NL + 8) / 4; }  // chunk + overhan
 constexpr int kNbMaxElems = kNbChunk / 6 + 2;            // shortest element: 4 + RecordAttributes(2)
 constexpr int kNbScanBlock = 256;                        // chunks per k_nb_resolve block
 constexpr int kNbMaxLanes = GW_MAX_ELEMENT;              // scratch sizing: the widest walk
+constexpr int kNbMaskWords = kNbChunk / 32;              // element-start mask words per chunk
+// sync window: bytes of a chunk the candidates walk before checking that they agree
+template <int NL>
+constexpr int nb_sync_bytes() { return NL == 64 ? 256 : 512; }
 
 // walk state of a candidate lane, packed into the top bits of its exit word
 constexpr int kStNormal = 0, kStTail = 1, kStDead = 2, kStLong = 3;
@@ -95,41 +99,11 @@ __device__ __forceinline__ uint64_t lds_be64(const uint32_t* w, int p) {
     return __builtin_bswap64(le);
 }
 
-// Pass 1: every candidate entry of every chunk, walked at once (lane = candidate offset,
-// plus 64 for the second candidate of a lane when NL = 128).
-// Per candidate: exit (relative position | state << 28) and (records | watermarks << 16).
-template <int NL>
-__global__ void __launch_bounds__(256) k_nb_walk(const uint8_t* buf, int64_t nbytes, int64_t nch, int32_t vbytes,
-                                                 uint32_t* exits, uint32_t* cnt, int64_t* conv) {
-    constexpr int kNbWords = nb_words<NL>(), kNbRegs = nb_regs<NL>(), CPL = NL / 64;
-    const int rec_ts = 9 + vbytes, rec_nots = 1 + vbytes;
-    __shared__ uint32_t lds[kNbWaves][kNbWords];
-    const int w = threadIdx.x >> 6, lane = __lane_id();
-    const int64_t stride = (int64_t)gridDim.x * kNbWaves;
-    uint32_t pre[kNbRegs];
-    int64_t c = (int64_t)blockIdx.x * kNbWaves + w;
-    if (c < nch) nb_fetch<NL>(pre, buf, c * kNbChunk, nbytes);
-    for (; c < nch; c += stride) {
-    const int64_t base = c * kNbChunk;
-    __builtin_amdgcn_wave_barrier();  // the previous chunk's LDS reads are done
-    nb_put<NL>(lds[w], pre);
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    if (c + stride < nch) nb_fetch<NL>(pre, buf, (c + stride) * kNbChunk, nbytes);
-    const uint32_t* l = lds[w];
-    const int64_t left = nbytes - base;
-    const int rlim = left < kNbChunk + 4 * NL ? (int)left : kNbChunk + 4 * NL;  // binding only near the end
-    const int rend = rlim < kNbChunk ? rlim : kNbChunk;
-    int64_t ex[CPL];
-    bool live[CPL];
-#pragma unroll
-    for (int k = 0; k < CPL; ++k) {
-    // Branch-free step (one ds_read2 gives the length word and the tag): the loop runs as
-    // long as any candidate lane is alive, every lane steps in lockstep under a full exec
-    // mask, and the per-step VALU count stays small, which is what bounds this kernel.
-    const int cand = lane + 64 * k;
-    int pos = cand, nr = 0, nw = 0, st = kStNormal;
-    bool run = pos < rend;
+// One candidate's walk from its state (pos, counts, st) while pos < H, out of LDS.
+// Branch-free step (one ds_read2 gives the length word and the tag): every lane steps in
+// lockstep under a full exec mask, and the per-step VALU count stays small.
+__device__ __forceinline__ void nb_walk_lane(const uint32_t* l, int H, int rlim, int rec_ts, int rec_nots, bool run,
+                                             int& pos, int& nr, int& nw, int& st) {
     while (__ballot(run)) {
         const int p = run ? pos : 0;
         const uint32_t w0 = l[p >> 2], w1 = l[(p >> 2) + 1];
@@ -154,12 +128,116 @@ __global__ void __launch_bounds__(256) k_nb_walk(const uint8_t* buf, int64_t nby
         nr += (adv && tag <= 1u) ? 1 : 0;
         nw += (adv && (tag == 2u || tag == 6u)) ? 1 : 0;
         pos = adv ? p + 4 + len : pos;
-        run = adv && pos < rend;
+        run = adv && pos < H;
     }
-    exits[c * NL + cand] = (uint32_t)pos | ((uint32_t)st << 28);
-    cnt[c * NL + cand] = (uint32_t)nr | ((uint32_t)nw << 16);
-    ex[k] = nb_pack(base + pos, st);
-    live[k] = st == kStNormal || st == kStTail;
+}
+
+// Pass 1: every candidate entry of every chunk (lane = candidate offset, plus 64 for the
+// second candidate of a lane when NL = 128), walked at once -- but only through a short
+// sync window of the chunk's first kNbSync bytes.  Wrong candidates die or merge within
+// a step or two, so at the window's end the live candidates almost always stand on one
+// element start P of the true chain (whatever the entry): then the chunk records P
+// (sync), each candidate's (P or its death, counts up to P), and k_nb_tail walks P to the
+// chunk's end with one thread.  Otherwise (a payload that mimics a chain for longer, the
+// stream's last chunk) the wave loads the whole chunk and walks on to its end, as before.
+// Per candidate: exit (relative position | state << 28) and (records | watermarks << 16).
+template <int NL>
+__global__ void __launch_bounds__(256) k_nb_walk(const uint8_t* buf, int64_t nbytes, int64_t nch, int32_t vbytes,
+                                                 uint32_t* exits, uint32_t* cnt, int64_t* conv, int64_t* sync,
+                                                 NbStatus* nst) {
+    constexpr int kNbWords = nb_words<NL>(), CPL = NL / 64;
+    constexpr int kSyncRegs = nb_sync_bytes<NL>() / 256, kSync = nb_sync_bytes<NL>() - 8;
+    const int rec_ts = 9 + vbytes, rec_nots = 1 + vbytes;
+    __shared__ uint32_t lds[kNbWaves][kNbWords];
+    const int w = threadIdx.x >> 6, lane = __lane_id();
+    const int64_t stride = (int64_t)gridDim.x * kNbWaves;
+    uint32_t pre[kSyncRegs];
+    auto fetch_window = [&](int64_t b) {  // the sync window's dwords (bytes past the end read as 0)
+        const int64_t left = nbytes - b;
+        const uint32_t* src = (const uint32_t*)(buf + b);
+#pragma unroll
+        for (int k = 0; k < kSyncRegs; ++k) {
+            const int i = lane + 64 * k;
+            uint32_t v = 0;
+            if (4 * (int64_t)i + 4 <= left) {
+                v = __builtin_nontemporal_load(src + i);
+            } else {
+                for (int q = 0; q < 4; ++q)
+                    if (4 * (int64_t)i + q < left) v |= (uint32_t)buf[b + 4 * i + q] << (8 * q);
+            }
+            pre[k] = v;
+        }
+    };
+    int64_t c = (int64_t)blockIdx.x * kNbWaves + w;
+    if (c < nch) fetch_window(c * kNbChunk);
+    for (; c < nch; c += stride) {
+    const int64_t base = c * kNbChunk;
+    __builtin_amdgcn_wave_barrier();  // the previous chunk's LDS reads are done
+#pragma unroll
+    for (int k = 0; k < kSyncRegs; ++k) lds[w][lane + 64 * k] = pre[k];
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (c + stride < nch) fetch_window((c + stride) * kNbChunk);
+    const uint32_t* l = lds[w];
+    const int64_t left = nbytes - base;
+    const int rlim = left < kNbChunk + 4 * NL ? (int)left : kNbChunk + 4 * NL;  // binding only near the end
+    const int rend = rlim < kNbChunk ? rlim : kNbChunk;
+    const bool windowed = rend > kSync;
+    const int H = windowed ? kSync : rend;
+    int pos[CPL], nr[CPL], nw[CPL], st[CPL];
+#pragma unroll
+    for (int k = 0; k < CPL; ++k) {
+        pos[k] = lane + 64 * k; nr[k] = 0; nw[k] = 0; st[k] = kStNormal;
+        nb_walk_lane(l, H, rlim, rec_ts, rec_nots, pos[k] < H, pos[k], nr[k], nw[k], st[k]);
+    }
+    // converged: every live candidate stopped normally on the same position
+    bool conv_ok = windowed;
+    int P = -1;
+    if (windowed) {
+        unsigned long long anyl = 0;
+#pragma unroll
+        for (int k = 0; k < CPL; ++k) anyl |= __ballot(st[k] == kStNormal || st[k] == kStTail);
+        if (!anyl) {
+            conv_ok = false;  // no live candidate: dead everywhere (the full walk changes nothing)
+        } else {
+#pragma unroll
+            for (int k = 0; k < CPL; ++k) {
+                const unsigned long long lv = __ballot(st[k] == kStNormal);
+                if (P < 0 && lv) P = __shfl(pos[k], __ffsll((long long)lv) - 1);
+            }
+            bool diff = false;
+#pragma unroll
+            for (int k = 0; k < CPL; ++k)
+                diff = diff || __ballot(st[k] == kStTail || (st[k] == kStNormal && pos[k] != P)) != 0;
+            conv_ok = !diff && P >= 0;
+        }
+    }
+    if (windowed && !conv_ok) {  // walk on to the chunk's end out of the whole chunk
+        if (lane == 0) atomicAdd(&nst->fallback, 1ull);
+        uint32_t full[nb_regs<NL>()];
+        nb_fetch<NL>(full, buf, base, nbytes);
+        __builtin_amdgcn_wave_barrier();
+        nb_put<NL>(lds[w], full);
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+        for (int k = 0; k < CPL; ++k)
+            nb_walk_lane(l, rend, rlim, rec_ts, rec_nots, st[k] == kStNormal && pos[k] < rend, pos[k], nr[k], nw[k],
+                         st[k]);
+    }
+    int64_t ex[CPL];
+    bool live[CPL];
+#pragma unroll
+    for (int k = 0; k < CPL; ++k) {
+        const int cand = lane + 64 * k;
+        exits[c * NL + cand] = (uint32_t)pos[k] | ((uint32_t)st[k] << 28);
+        cnt[c * NL + cand] = (uint32_t)nr[k] | ((uint32_t)nw[k] << 16);
+        ex[k] = nb_pack(base + pos[k], st[k]);
+        live[k] = st[k] == kStNormal || st[k] == kStTail;
+    }
+    if (conv_ok) {  // k_nb_tail finishes the chain from P and writes conv[c]
+        if (lane == 0) sync[c] = base + P;
+        continue;
     }
     // unique exit over the live candidates (dead ones never hold the true entry)
     int64_t ref = 0;
@@ -179,21 +257,97 @@ __global__ void __launch_bounds__(256) k_nb_walk(const uint8_t* buf, int64_t nby
         for (int k = 0; k < CPL; ++k) diff = diff || __ballot(live[k] && ex[k] != ref) != 0;
         cv = diff ? kNonConv : ref;
     }
-    if (lane == 0) conv[c] = cv;
+    if (lane == 0) {
+        conv[c] = cv;
+        sync[c] = -1;
+    }
     }
 }
 
+// Pass 1b: one thread per synced chunk walks the true chain from its sync point P to the
+// chunk's end (global loads; each thread streams through its own chunk), the exit and the
+// record / watermark counts of [P, exit) -> conv[c], tcnt[c], the element starts -> tmask.
 template <int NL>
-__device__ __forceinline__ int64_t nb_exit_word(const uint32_t* exits, int64_t t, int64_t lane) {
+__global__ void __launch_bounds__(256) k_nb_tail(const uint8_t* buf, int64_t nbytes, int64_t nch, int32_t vbytes,
+                                                 const int64_t* sync, int64_t* conv, uint32_t* tcnt,
+                                                 uint32_t* tmask) {
+    // element starts of [P, exit) as a bit mask per chunk (kNbMaskWords words), which
+    // k_nb_decode expands with all lanes instead of walking the chain again; staged in LDS
+    // (one row per thread, padded against bank conflicts) and written out coalesced
+    constexpr int kRow = kNbMaskWords + 1;
+    __shared__ uint32_t lm[256 * kRow];
+    const int rec_ts = 9 + vbytes, rec_nots = 1 + vbytes;
+    const int tid = threadIdx.x;
+    for (int64_t c0 = (int64_t)blockIdx.x * 256; c0 < nch; c0 += (int64_t)gridDim.x * 256) {
+        const int64_t c = c0 + tid;
+        uint32_t* mk = lm + tid * kRow;
+        const int64_t s0 = c < nch ? sync[c] : -1;
+        if (s0 >= 0) {
+            const int64_t base = c * kNbChunk;
+            const int64_t left = nbytes - base;
+            const int rlim = left < kNbChunk + 4 * NL ? (int)left : kNbChunk + 4 * NL;
+            const int rend = rlim < kNbChunk ? rlim : kNbChunk;
+            const uint8_t* b = buf + base;
+            int pos = (int)(s0 - base), nr = 0, nw = 0, st = kStNormal, mw = 0;
+            uint32_t cur = 0;
+            while (pos < rend) {
+                if (pos + 4 > rlim) { st = kStTail; break; }
+                int32_t len;
+                uint32_t tag;
+                const int q = pos & ~3;
+                if ((int64_t)q + 8 <= left) {  // one 8-byte load holds the length word and the tag
+                    const uint2 d = *(const uint2*)(b + q);
+                    const uint32_t sh = (uint32_t)(pos & 3);
+                    len = (int32_t)__builtin_bswap32(__builtin_amdgcn_alignbyte(d.y, d.x, sh));
+                    tag = (d.y >> (8 * sh)) & 0xffu;
+                } else {
+                    len = (int32_t)(((uint32_t)b[pos] << 24) | ((uint32_t)b[pos + 1] << 16) |
+                                    ((uint32_t)b[pos + 2] << 8) | (uint32_t)b[pos + 3]);
+                    tag = pos + 4 < left ? b[pos + 4] : 0u;
+                }
+                const int want = tag == 0u ? rec_ts : tag == 1u ? rec_nots : tag == 2u ? 9 : tag == 3u ? 29
+                               : tag == 4u ? 5 : tag == 5u ? 2 : tag == 6u ? 13 : -1;
+                const int ns = len < 1 ? kStDead
+                             : len > GW_MAX_ELEMENT - 4 ? kStLong
+                             : pos + 4 + len > rlim ? kStTail
+                             : len != want ? kStDead : kStNormal;
+                if (ns != kStNormal) { st = ns; break; }
+                nr += tag <= 1u ? 1 : 0;
+                nw += (tag == 2u || tag == 6u) ? 1 : 0;
+                for (; mw < (pos >> 5); ++mw, cur = 0) mk[mw] = cur;
+                cur |= 1u << (pos & 31);
+                pos += 4 + len;
+            }
+            for (; mw < kNbMaskWords; ++mw, cur = 0) mk[mw] = cur;
+            conv[c] = nb_pack(base + pos, st);
+            tcnt[c] = (uint32_t)nr | ((uint32_t)nw << 16);
+        } else {
+            for (int k = 0; k < kNbMaskWords; ++k) mk[k] = 0;
+        }
+        __syncthreads();
+        const int64_t nrow = nch - c0 < 256 ? nch - c0 : 256;
+        for (int j = tid; j < nrow * kNbMaskWords; j += 256)
+            tmask[c0 * kNbMaskWords + j] = lm[(j / kNbMaskWords) * kRow + j % kNbMaskWords];
+        __syncthreads();
+    }
+}
+
+// A candidate's exit from chunk t: its walk's end, or for a synced chunk whose candidate
+// reached the sync point, the tail walk's end.
+template <int NL>
+__device__ __forceinline__ int64_t nb_exit_word(const uint32_t* exits, const int64_t* sync, const int64_t* conv,
+                                                int64_t t, int64_t lane) {
     const uint32_t x = exits[t * NL + lane];
-    return nb_pack(t * kNbChunk + (x & 0x0fffffffu), (int)(x >> 28));
+    const int64_t e = nb_pack(t * kNbChunk + (x & 0x0fffffffu), (int)(x >> 28));
+    return (sync[t] >= 0 && e == nb_pack(sync[t], kStNormal)) ? conv[t] : e;
 }
 
 // Pass 2: one thread per chunk finds its true entry from the nearest earlier chunk with a
 // unique exit, then the block scans the chunk counts (exclusive, block-local).
 template <int NL>
 __global__ void __launch_bounds__(kNbScanBlock) k_nb_resolve(int64_t nbytes, int64_t nch, const uint32_t* exits,
-                                                             const uint32_t* cnt, const int64_t* conv, int64_t* entry,
+                                                             const uint32_t* cnt, const int64_t* conv,
+                                                             const int64_t* sync, const uint32_t* tcnt, int64_t* entry,
                                                              int32_t* offs, long long* btot, NbStatus* st) {
     __shared__ int wsum[kNbScanBlock / 64][2];
     const int64_t c = (int64_t)blockIdx.x * kNbScanBlock + threadIdx.x;
@@ -206,7 +360,7 @@ __global__ void __launch_bounds__(kNbScanBlock) k_nb_resolve(int64_t nbytes, int
         for (int64_t t = j + 1; t < c && nb_state(e) == kStNormal; ++t) {
             const int64_t lane = nb_pos(e) - t * kNbChunk;
             if (lane < 0 || lane >= NL) { e = nb_pack(nb_pos(e), kStDead); break; }
-            e = nb_exit_word<NL>(exits, t, lane);
+            e = nb_exit_word<NL>(exits, sync, conv, t, lane);
         }
         int64_t ent = -1;
         if (nb_state(e) == kStNormal) {
@@ -218,10 +372,16 @@ __global__ void __launch_bounds__(kNbScanBlock) k_nb_resolve(int64_t nbytes, int
                 atomicOr(&st->corrupt, 1ull);
             } else {
                 ent = p;
-                const int64_t ex = nb_exit_word<NL>(exits, c, lane);
+                const int64_t ex = nb_exit_word<NL>(exits, sync, conv, c, lane);
                 const uint32_t cc = cnt[c * NL + lane];
                 nr = (int)(cc & 0xffffu);
                 nw = (int)(cc >> 16);
+                const uint32_t x = exits[c * NL + lane];
+                if (sync[c] >= 0 && nb_pack(c * kNbChunk + (x & 0x0fffffffu), (int)(x >> 28)) ==
+                                        nb_pack(sync[c], kStNormal)) {
+                    nr += (int)(tcnt[c] & 0xffffu);
+                    nw += (int)(tcnt[c] >> 16);
+                }
                 const int s = nb_state(ex);
                 if (s == kStDead) atomicOr(&st->corrupt, 1ull);
                 if (s == kStLong) atomicOr(&st->unsupported, 1ull);
@@ -301,6 +461,7 @@ __device__ __forceinline__ int64_t nb_field(const uint32_t* l, int p, int type) 
 template <int NL>
 __global__ void __launch_bounds__(256) k_nb_decode(const uint8_t* buf, int64_t nbytes, int64_t nch, NbLayout L,
                                                    const int64_t* entry, const int32_t* offs, const long long* btot,
+                                                   const int64_t* sync, const uint32_t* tmask,
                                                    int64_t* key, int64_t* ts, int64_t* val, int64_t rec_cap,
                                                    int64_t* wm_pos, int64_t* wm_val, int64_t wm_cap, NbStatus* st) {
     constexpr int kNbWords = nb_words<NL>(), kNbRegs = nb_regs<NL>();
@@ -326,11 +487,13 @@ __global__ void __launch_bounds__(256) k_nb_decode(const uint8_t* buf, int64_t n
     const int rlim = left < kNbChunk + 4 * NL ? (int)left : kNbChunk + 4 * NL;
     const int rend = rlim < kNbChunk ? rlim : kNbChunk;
     {  // the true chain, walked by the whole wave in lockstep (uniform addresses: LDS
-       // broadcasts), lane 0 recording the element starts
+       // broadcasts), lane 0 recording the element starts -- for a synced chunk only up to
+       // its sync point P: the starts from P on come from k_nb_tail's mask
         int m = 0;
         int pos = (int)(e0 - base);
+        const int P = sync[c] >= 0 ? (int)(sync[c] - base) : -1;
         bool run = pos < rend;
-        while (run && m < kNbMaxElems) {
+        while (run && m < kNbMaxElems && pos != P) {
             const uint32_t w0 = l[pos >> 2], w1 = l[(pos >> 2) + 1];
             const int32_t len = (int32_t)__builtin_bswap32(__builtin_amdgcn_alignbyte(w1, w0, (uint32_t)(pos & 3)));
             if (pos + 4 > rlim || len < 1 || len > NL - 4 || pos + 4 + len > rlim) break;
@@ -338,6 +501,25 @@ __global__ void __launch_bounds__(256) k_nb_decode(const uint8_t* buf, int64_t n
             ++m;
             pos += 4 + len;
             run = pos < rend;
+        }
+        if (run && pos == P) {  // expand the mask: lane k < kNbMaskWords holds word k
+            uint32_t word = lane < kNbMaskWords ? tmask[c * kNbMaskWords + lane] : 0u;
+            const int nb = __popc(word);
+            int incl = nb;
+            for (int o = 1; o < 64; o <<= 1) {
+                const int u = __shfl_up(incl, o);
+                if (lane >= o) incl += u;
+            }
+            int at = m + incl - nb;
+            while (word) {
+                const int bit = __ffs(word) - 1;
+                word &= word - 1;
+                if (at < kNbMaxElems) starts[w][at] = (uint16_t)(lane * 32 + bit);
+                ++at;
+            }
+            m += __shfl(incl, 63);
+            pos = rend;  // (the tail's own end state was resolved by k_nb_resolve)
+            if (m > kNbMaxElems) m = kNbMaxElems;
         }
         // more elements than valid ones of >= 6 bytes can make: lengths of 1 -> corrupt
         if (lane == 0 && m == kNbMaxElems && pos < rend) atomicOr(&st->corrupt, 1ull);
@@ -414,7 +596,7 @@ int64_t nb_scratch_bytes(int64_t nbytes) {
     const int64_t nch = (nbytes + kNbChunk - 1) / kNbChunk;
     const int64_t nblk = (nch + kNbScanBlock - 1) / kNbScanBlock;
     // exits + counts per lane, conv + entry + offsets per chunk, block totals
-    return nch * kNbMaxLanes * 8 + nch * 24 + nblk * 16 + 256;
+    return nch * kNbMaxLanes * 8 + nch * (40 + 4 * kNbMaskWords) + nblk * 16 + 256;
 }
 
 hipError_t launch_nb_decode(const uint8_t* buf, int64_t nbytes, const NbLayout& L, int64_t* key, int64_t* ts,
@@ -430,6 +612,9 @@ hipError_t launch_nb_decode(const uint8_t* buf, int64_t nbytes, const NbLayout& 
     int64_t* conv = (int64_t*)p;               p += nch * 8;
     int64_t* entry = (int64_t*)p;              p += nch * 8;
     int32_t* offs = (int32_t*)p;               p += nch * 8;
+    int64_t* sync = (int64_t*)p;               p += nch * 8;
+    uint32_t* tcnt = (uint32_t*)p;             p += nch * 8;
+    uint32_t* tmask = (uint32_t*)p;            p += nch * 4 * kNbMaskWords;
     long long* btot = (long long*)p;
     // a bounded grid of waves that loop over the chunks: a chunk is ~1 us of work, too
     // little to pay for a workgroup dispatch each (GW_NB_GRID overrides, for sweeps)
@@ -439,17 +624,27 @@ hipError_t launch_nb_decode(const uint8_t* buf, int64_t nbytes, const NbLayout& 
         return e ? (int64_t)atoll(e) : (int64_t)4096;
     }();
     if (cap > 0 && gb > cap) gb = cap;
+    // tail walks: a grid of 512 blocks looping over the chunks (measured: 128 blocks 160 us,
+    // 256 98 us, 512 86 us, 1024 86 us per 10M Q5 records)
+    static const int64_t tcap = [] {
+        const char* e = getenv("GW_NB_TAIL_GRID");
+        return e ? (int64_t)atoll(e) : (int64_t)512;
+    }();
+    int64_t tb = (nch + 255) / 256;
+    if (tcap > 0 && tb > tcap) tb = tcap;
     // candidates per chunk: the longest element this layout can produce (a record with a
     // timestamp: 4 + 1 + 8 + vbytes; the other tags are at most 33 bytes)
     const bool wide = 13 + L.vbytes > 64;
 #define NB_LAUNCH(NL)                                                                                              \
     hipLaunchKernelGGL(k_nb_walk<NL>, dim3((unsigned)gb), dim3(256), 0, s, buf, nbytes, nch, L.vbytes, exits, cnt, \
-                       conv);                                                                                      \
+                       conv, sync, d_st);                                                                          \
+    hipLaunchKernelGGL(k_nb_tail<NL>, dim3((unsigned)tb), dim3(256), 0, s, buf, nbytes, nch,                       \
+                       L.vbytes, sync, conv, tcnt, tmask);                                                         \
     hipLaunchKernelGGL(k_nb_resolve<NL>, dim3((unsigned)nblk), dim3(kNbScanBlock), 0, s, nbytes, nch, exits, cnt,  \
-                       conv, entry, offs, btot, d_st);                                                             \
+                       conv, sync, tcnt, entry, offs, btot, d_st);                                                 \
     hipLaunchKernelGGL(k_nb_scan, dim3(1), dim3(1024), 0, s, nblk, btot, d_st);                                    \
     hipLaunchKernelGGL(k_nb_decode<NL>, dim3((unsigned)gb), dim3(256), 0, s, buf, nbytes, nch, L, entry, offs, btot, \
-                       key, ts, val, rec_cap, wm_pos, wm_val, wm_cap, d_st)
+                       sync, tmask, key, ts, val, rec_cap, wm_pos, wm_val, wm_cap, d_st)
     if (wide) {
         NB_LAUNCH(GW_MAX_ELEMENT);
     } else {

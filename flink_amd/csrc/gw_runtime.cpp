@@ -2340,6 +2340,8 @@ static int nb_layout(const gw_record_layout* lay, int agg, NbLayout& L, std::str
 }
 
 static int nb_status_code(const NbStatus& st, std::string& why) {
+    static const bool dbg = getenv("GW_NB_DEBUG") != nullptr;
+    if (dbg) fprintf(stderr, "gw netbuf: fallback %llu walkback %llu\n", st.fallback, st.walkback);
     if (st.corrupt) { why = "Corrupt stream: unknown tag or element length (StreamElementSerializer)"; return GW_E_INVALID; }
     if (st.unsupported) { why = "stream element longer than GW_MAX_ELEMENT bytes"; return GW_E_UNSUPPORTED; }
     if (st.full) { why = "decoded records / watermarks exceed the output capacity"; return GW_E_OUTPUT_FULL; }
