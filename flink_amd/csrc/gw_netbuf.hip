@@ -37,8 +37,11 @@ constexpr int kNbScanBlock = 256;                        // chunks per k_nb_reso
 constexpr int kNbMaxLanes = GW_MAX_ELEMENT;              // scratch sizing: the widest walk
 constexpr int kNbMaskWords = kNbChunk / 32;              // element-start mask words per chunk
 // sync window: bytes of a chunk the candidates walk before checking that they agree
+#ifndef GW_NB_SYNC
+#define GW_NB_SYNC 96  // measured per 10M Q5 records: 256 B 204 us, 128 B 125 us, 96 B 98 us (8 fallbacks)
+#endif
 template <int NL>
-constexpr int nb_sync_bytes() { return NL == 64 ? 256 : 512; }
+constexpr int nb_sync_bytes() { return NL == 64 ? GW_NB_SYNC : 2 * GW_NB_SYNC; }
 
 // walk state of a candidate lane, packed into the top bits of its exit word
 constexpr int kStNormal = 0, kStTail = 1, kStDead = 2, kStLong = 3;
@@ -113,8 +116,11 @@ __device__ __forceinline__ void nb_walk_lane(const uint32_t* l, int H, int rlim,
         // a candidate lives only on elements whose length fits their tag (what k_nb_decode
         // checks on the true chain): payload bytes that merely read as a plausible length
         // rarely also carry the matching tag, so wrong chains die within a step or two
-        const int want = tag == 0u ? rec_ts : tag == 1u ? rec_nots : tag == 2u ? 9 : tag == 3u ? 29
-                       : tag == 4u ? 5 : tag == 5u ? 2 : tag == 6u ? 13 : -1;
+        // the length each tag's element must have, as bytes of two words (tag 7: 255, which
+        // no element reaches: GW_MAX_ELEMENT)
+        const uint32_t lut = (tag & 4u) ? (5u | 2u << 8 | 13u << 16 | 255u << 24)
+                                        : ((uint32_t)rec_ts | (uint32_t)rec_nots << 8 | 9u << 16 | 29u << 24);
+        const int want = tag < 8u ? (int)((lut >> (8 * (tag & 3u))) & 0xffu) : -1;
         // beyond GW_MAX_ELEMENT: unsupported; longer than NL but within it: no element of
         // this layout is that long, so the length cannot match its tag (dead: corrupt on
         // the true chain) -- the same order of checks as the oracle's decoder
@@ -146,7 +152,8 @@ __global__ void __launch_bounds__(256) k_nb_walk(const uint8_t* buf, int64_t nby
                                                  uint32_t* exits, uint32_t* cnt, int64_t* conv, int64_t* sync,
                                                  NbStatus* nst) {
     constexpr int kNbWords = nb_words<NL>(), CPL = NL / 64;
-    constexpr int kSyncRegs = nb_sync_bytes<NL>() / 256, kSync = nb_sync_bytes<NL>() - 8;
+    constexpr int kSyncWords = nb_sync_bytes<NL>() / 4, kSyncRegs = (kSyncWords + 63) / 64;
+    constexpr int kSync = nb_sync_bytes<NL>() - 8;
     const int rec_ts = 9 + vbytes, rec_nots = 1 + vbytes;
     __shared__ uint32_t lds[kNbWaves][kNbWords];
     const int w = threadIdx.x >> 6, lane = __lane_id();
@@ -159,7 +166,8 @@ __global__ void __launch_bounds__(256) k_nb_walk(const uint8_t* buf, int64_t nby
         for (int k = 0; k < kSyncRegs; ++k) {
             const int i = lane + 64 * k;
             uint32_t v = 0;
-            if (4 * (int64_t)i + 4 <= left) {
+            if (i >= kSyncWords) {
+            } else if (4 * (int64_t)i + 4 <= left) {
                 v = __builtin_nontemporal_load(src + i);
             } else {
                 for (int q = 0; q < 4; ++q)
@@ -174,7 +182,8 @@ __global__ void __launch_bounds__(256) k_nb_walk(const uint8_t* buf, int64_t nby
     const int64_t base = c * kNbChunk;
     __builtin_amdgcn_wave_barrier();  // the previous chunk's LDS reads are done
 #pragma unroll
-    for (int k = 0; k < kSyncRegs; ++k) lds[w][lane + 64 * k] = pre[k];
+    for (int k = 0; k < kSyncRegs; ++k)
+        if (lane + 64 * k < kSyncWords) lds[w][lane + 64 * k] = pre[k];
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     if (c + stride < nch) fetch_window((c + stride) * kNbChunk);
@@ -471,16 +480,35 @@ __global__ void __launch_bounds__(256) k_nb_decode(const uint8_t* buf, int64_t n
     const int w = threadIdx.x >> 6, lane = __lane_id();
     const int64_t stride = (int64_t)gridDim.x * kNbWaves;
     uint32_t pre[kNbRegs];
+    // the next chunk's entry, sync point, mask word and output offsets load with its bytes
+    int64_t pe0 = -1, psy = -1, prb = 0, pwb = 0;
+    uint32_t pmw = 0;
+    auto fetch_meta = [&](int64_t cc) {
+        pe0 = entry[cc];
+        psy = sync[cc];
+        pmw = lane < kNbMaskWords ? tmask[cc * kNbMaskWords + lane] : 0u;
+        const int64_t blk = cc / kNbScanBlock;
+        prb = btot[2 * blk] + offs[2 * cc];
+        pwb = btot[2 * blk + 1] + offs[2 * cc + 1];
+    };
     int64_t c = (int64_t)blockIdx.x * kNbWaves + w;
-    if (c < nch) nb_fetch<NL>(pre, buf, c * kNbChunk, nbytes);
+    if (c < nch) {
+        nb_fetch<NL>(pre, buf, c * kNbChunk, nbytes);
+        fetch_meta(c);
+    }
     for (; c < nch; c += stride) {
-    const int64_t e0 = entry[c];
+    const int64_t e0 = pe0, sy = psy;
+    const uint32_t mword = pmw;
+    int64_t rbase = prb, wbase = pwb;
     const int64_t base = c * kNbChunk;
     __builtin_amdgcn_wave_barrier();  // the previous chunk's LDS reads are done
     nb_put<NL>(lds[w], pre);
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    if (c + stride < nch) nb_fetch<NL>(pre, buf, (c + stride) * kNbChunk, nbytes);
+    if (c + stride < nch) {
+        nb_fetch<NL>(pre, buf, (c + stride) * kNbChunk, nbytes);
+        fetch_meta(c + stride);
+    }
     if (e0 < 0) continue;
     const uint32_t* l = lds[w];
     const int64_t left = nbytes - base;
@@ -491,7 +519,7 @@ __global__ void __launch_bounds__(256) k_nb_decode(const uint8_t* buf, int64_t n
        // its sync point P: the starts from P on come from k_nb_tail's mask
         int m = 0;
         int pos = (int)(e0 - base);
-        const int P = sync[c] >= 0 ? (int)(sync[c] - base) : -1;
+        const int P = sy >= 0 ? (int)(sy - base) : -1;
         bool run = pos < rend;
         while (run && m < kNbMaxElems && pos != P) {
             const uint32_t w0 = l[pos >> 2], w1 = l[(pos >> 2) + 1];
@@ -503,7 +531,7 @@ __global__ void __launch_bounds__(256) k_nb_decode(const uint8_t* buf, int64_t n
             run = pos < rend;
         }
         if (run && pos == P) {  // expand the mask: lane k < kNbMaskWords holds word k
-            uint32_t word = lane < kNbMaskWords ? tmask[c * kNbMaskWords + lane] : 0u;
+            uint32_t word = mword;
             const int nb = __popc(word);
             int incl = nb;
             for (int o = 1; o < 64; o <<= 1) {
@@ -528,8 +556,6 @@ __global__ void __launch_bounds__(256) k_nb_decode(const uint8_t* buf, int64_t n
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     const int m = nelem[w];
-    const int64_t blk = c / kNbScanBlock;
-    int64_t rbase = btot[2 * blk] + offs[2 * c], wbase = btot[2 * blk + 1] + offs[2 * c + 1];
     unsigned long long bad = 0, full = 0, skipped = 0;
     for (int i0 = 0; i0 < m; i0 += 64) {
         const int i = i0 + lane;
