@@ -158,7 +158,13 @@ struct gw_handle {
     int64_t* fe_seqbuf = nullptr;
     int64_t fe_seqbuf_cap = 0;
     int64_t* fe_maxts = nullptr;                        // per batch (ring of kFeBatches): largest ts
-    std::vector<std::pair<int64_t, int64_t>> fe_batches; // (sequence end, ring slot) not yet released
+    struct FeBatch {
+        int64_t seq_end;  // sequences of the batch end here
+        int64_t slot;     // its max timestamp in fe_maxts[slot] until fetched
+        int64_t max_ts;   // fetched max timestamp
+        bool known;
+    };
+    std::vector<FeBatch> fe_batches;  // not yet released, in arrival order
     int64_t fe_batch_no = 0;
     int64_t* c_pay = nullptr;
     void* fe_scratch = nullptr;
@@ -2104,17 +2110,36 @@ static int fe_gather(gw_handle* h, int64_t wm) {
     // release: a batch whose largest timestamp's windows are all cleaned (maxTs + size - 1 +
     // lateness <= wm: WindowOperator.cleanupTime) can hold no first element any more
     if (!h->fe_batches.empty()) {
-        std::vector<int64_t> mx(h->fe_batches.size());
-        for (size_t i = 0; i < mx.size(); ++i)
-            if (hipMemcpy(&mx[i], h->fe_maxts + h->fe_batches[i].second, 8, hipMemcpyDeviceToHost) != hipSuccess)
+        bool any = false;  // each batch's max timestamp crosses to the host once
+        for (auto& b : h->fe_batches) {
+            if (b.known) continue;
+            if (hipMemcpyAsync(&b.max_ts, h->fe_maxts + b.slot, 8, hipMemcpyDeviceToHost, h->stream) != hipSuccess)
                 return h->fail(GW_E_DEVICE, "first-element log");
+            b.known = any = true;
+        }
+        if (any && hipStreamSynchronize(h->stream) != hipSuccess) return h->fail(GW_E_DEVICE, "first-element log");
         size_t q = 0;
-        for (; q < mx.size(); ++q) {
-            const i128 ct = (i128)mx[q] + (i128)h->cfg.size - 1 + (i128)h->cfg.allowed_lateness;
-            if (mx[q] != INT64_MIN && ct > (i128)wm) break;
-            h->fe_log_base = h->fe_batches[q].first;
+        for (; q < h->fe_batches.size(); ++q) {
+            const int64_t mx = h->fe_batches[q].max_ts;
+            const i128 ct = (i128)mx + (i128)h->cfg.size - 1 + (i128)h->cfg.allowed_lateness;
+            if (mx != INT64_MIN && ct > (i128)wm) break;
+            h->fe_log_base = h->fe_batches[q].seq_end;
         }
         h->fe_batches.erase(h->fe_batches.begin(), h->fe_batches.begin() + q);
+        // a long lateness keeps many batches: merge neighbours (the later end, the larger
+        // max timestamp -- released no earlier than either) so the list stays short
+        if (h->fe_batches.size() > 1024) {
+            std::vector<gw_handle::FeBatch> m;
+            for (size_t i = 0; i < h->fe_batches.size(); i += 2) {
+                gw_handle::FeBatch b = h->fe_batches[i];
+                if (i + 1 < h->fe_batches.size()) {
+                    b.seq_end = h->fe_batches[i + 1].seq_end;
+                    b.max_ts = std::max(b.max_ts, h->fe_batches[i + 1].max_ts);
+                }
+                m.push_back(b);
+            }
+            h->fe_batches.swap(m);
+        }
     }
     return GW_OK;
 }
@@ -2162,7 +2187,7 @@ int gw_ingest_payload_device(gw_handle* h, int64_t n, const int64_t* d_key, cons
     if (e == hipSuccess) e = fe_iota64(h->fe_maxts + slot, 1, INT64_MIN, s);
     if (e == hipSuccess) e = fe_max_ts(d_ts, n, h->fe_maxts + slot, s);
     if (e != hipSuccess) return h->fail(GW_E_DEVICE, "first-element ingest: %s", hipGetErrorString(e));
-    h->fe_batches.push_back({h->fe_seq + n, slot});
+    h->fe_batches.push_back({h->fe_seq + n, slot, INT64_MIN, false});
     h->fe_batch_no++;
     int rc = gw_ingest_device(h->kids[0], n, d_key, d_key_hash, d_ts, d_value, (void*)s);
     if (rc) return kid_rc(h, h->kids[0], rc);
