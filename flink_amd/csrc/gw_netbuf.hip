@@ -61,9 +61,14 @@ __device__ __forceinline__ void nb_fetch(uint32_t (&r)[nb_regs<NL>()], const uin
     constexpr int kNbWords = nb_words<NL>(), kNbRegs = nb_regs<NL>();
     const int lane = __lane_id();
     const int64_t left = nbytes - base;
+    const uint32_t* src = (const uint32_t*)(buf + base);  // base is a multiple of kNbChunk; buf 4-aligned
+    if (left >= 4 * (int64_t)(64 * kNbRegs)) {  // the whole register window is in range (wave-uniform)
+#pragma unroll
+        for (int k = 0; k < kNbRegs; ++k) r[k] = __builtin_nontemporal_load(src + lane + 64 * k);
+        return;
+    }
     const int avail = left < 4 * kNbWords ? (int)left : 4 * kNbWords;
     const int full = avail >> 2;
-    const uint32_t* src = (const uint32_t*)(buf + base);  // base is a multiple of kNbChunk; buf 4-aligned
 #pragma unroll
     for (int k = 0; k < kNbRegs; ++k) {
         const int i = lane + 64 * k;
@@ -162,6 +167,12 @@ __global__ void __launch_bounds__(256) k_nb_walk(const uint8_t* buf, int64_t nby
     auto fetch_window = [&](int64_t b) {  // the sync window's dwords (bytes past the end read as 0)
         const int64_t left = nbytes - b;
         const uint32_t* src = (const uint32_t*)(buf + b);
+        if (left >= 4 * (int64_t)(64 * kSyncRegs)) {  // in range (wave-uniform)
+#pragma unroll
+            for (int k = 0; k < kSyncRegs; ++k)
+                pre[k] = lane + 64 * k < kSyncWords ? __builtin_nontemporal_load(src + lane + 64 * k) : 0u;
+            return;
+        }
 #pragma unroll
         for (int k = 0; k < kSyncRegs; ++k) {
             const int i = lane + 64 * k;
@@ -582,7 +593,7 @@ __global__ void __launch_bounds__(256) k_nb_decode(const uint8_t* buf, int64_t n
         }
         const unsigned long long below = (1ull << lane) - 1ull;
         const unsigned long long br = __ballot(kind == 1), bw = __ballot(kind == 2);
-        skipped += kind == 3;
+        skipped += (unsigned long long)__popcll(__ballot(kind == 3));  // wave-uniform
         if (kind == 1 && ok) {
             const int64_t o = rbase + __popcll(br & below);
             if (o < rec_cap) {
@@ -607,9 +618,8 @@ __global__ void __launch_bounds__(256) k_nb_decode(const uint8_t* buf, int64_t n
         rbase += __popcll(br);
         wbase += __popcll(bw);
     }
-    bad = wave_ior(bad);
-    full = wave_ior(full);
-    skipped = wave_sum(skipped);
+    bad = __ballot(bad != 0) != 0;  // one ballot each instead of a wave reduction
+    full = __ballot(full != 0) != 0;
     if (lane == 0) {
         if (bad) atomicOr(&st->corrupt, 1ull);
         if (full) atomicOr(&st->full, 1ull);
