@@ -38,7 +38,8 @@ constexpr int kNbMaxLanes = GW_MAX_ELEMENT;              // scratch sizing: the 
 constexpr int kNbMaskWords = kNbChunk / 32;              // element-start mask words per chunk
 // sync window: bytes of a chunk the candidates walk before checking that they agree
 #ifndef GW_NB_SYNC
-#define GW_NB_SYNC 96  // measured per 10M Q5 records: 256 B 204 us, 128 B 125 us, 96 B 98 us (8 fallbacks)
+#define GW_NB_SYNC 80  // walk per 10M Q5 records: 256 B 204 us, 128 B 125 us, 96 B 98 us (8 fallback chunks),
+                       // 80 B 91 us (55), 72 B 89 us (191)
 #endif
 template <int NL>
 constexpr int nb_sync_bytes() { return NL == 64 ? GW_NB_SYNC : 2 * GW_NB_SYNC; }
