@@ -14,7 +14,7 @@ for tag in "$@"; do
     base) lib=$R/flink_amd/libgpuwin.so ;;
     *) lib=$R/flink_amd/libgpuwin_$tag.so ;;
   esac
-  (cd /tmp && export ${envs//,/ } && GW_LIB_PATH=$lib timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $R/$O/$tag -o run --output-format csv -- python -u $R/scripts/netbuf_bench.py --mode decode > $R/$O/$tag.json 2> $R/$O/$tag.err) || { echo "$tag failed"; tail -5 $O/$tag.err; exit 1; }
+  (cd /tmp && { [ -z "$envs" ] || export ${envs//,/ }; } && GW_LIB_PATH=$lib timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $R/$O/$tag -o run --output-format csv -- python -u $R/scripts/netbuf_bench.py --mode decode > $R/$O/$tag.json 2> $R/$O/$tag.err) || { echo "$tag failed"; tail -5 $O/$tag.err; exit 1; }
   python3 - "$O/$tag" "$tag" <<'PY'
 import csv, glob, sys
 f = glob.glob(sys.argv[1] + "/**/run_kernel_stats.csv", recursive=True)[0]
