@@ -31,17 +31,26 @@ __global__ void k_fe_gather_key(const int64_t* src, const uint32_t* idx, int64_t
         dst[i] = src[idx[i]];
 }
 
-__global__ void k_fe_max(const int64_t* ts, int64_t n, int64_t* out) {
+// The batch's largest timestamp: wave then block reduction, one device atomic per block
+// (a small grid: thousands of atomics on one address serialise at the memory side).
+__global__ void __launch_bounds__(256) k_fe_max(const int64_t* ts, int64_t n, int64_t* out) {
+    __shared__ int64_t wmax[4];
     int64_t m = INT64_MIN;
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
         m = max(m, ts[i]);
     for (int o = 32; o > 0; o >>= 1) m = max(m, (int64_t)__shfl_xor(m, o));
-    if (__lane_id() == 0 && m != INT64_MIN) atomicMax((long long*)out, (long long)m);
+    if (__lane_id() == 0) wmax[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        m = max(max(wmax[0], wmax[1]), max(wmax[2], wmax[3]));
+        if (m != INT64_MIN) atomicMax((long long*)out, (long long)m);
+    }
 }
 
-__global__ void k_fe_append(int64_t* log, int64_t cap, int64_t pos, const int64_t* src, int64_t n) {
+// n payloads to log positions [at, at + n) (the host splits a ring wrap into two calls)
+__global__ void k_fe_append(int64_t* log, int64_t at, const int64_t* src, int64_t n) {
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-        log[(pos + i) % cap] = src[i];
+        log[at + i] = src[i];
 }
 
 // Row i of the join: A's row pa[i] and B's row pb[i] (both sorted by (key, start)).
@@ -147,7 +156,8 @@ hipError_t fe_iota64(int64_t* d, int64_t n, int64_t base, hipStream_t s) {
 
 hipError_t fe_max_ts(const int64_t* ts, int64_t n, int64_t* out, hipStream_t s) {
     if (n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_fe_max, dim3(grid_n(n)), dim3(256), 0, s, ts, n, out);
+    const unsigned g = (unsigned)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 1024));
+    hipLaunchKernelGGL(k_fe_max, dim3(g), dim3(256), 0, s, ts, n, out);
     return hipGetLastError();
 }
 
@@ -160,7 +170,9 @@ hipError_t fe_log_regrow(const int64_t* o, int64_t ocap, int64_t* d, int64_t nca
 
 hipError_t fe_log_append(int64_t* log, int64_t cap, int64_t pos, const int64_t* src, int64_t n, hipStream_t s) {
     if (n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_fe_append, dim3(grid_n(n)), dim3(256), 0, s, log, cap, pos, src, n);
+    const int64_t at = pos % cap, n1 = std::min(n, cap - at);  // up to the ring's end, then from 0
+    hipLaunchKernelGGL(k_fe_append, dim3(grid_n(n1)), dim3(256), 0, s, log, at, src, n1);
+    if (n > n1) hipLaunchKernelGGL(k_fe_append, dim3(grid_n(n - n1)), dim3(256), 0, s, log, (int64_t)0, src + n1, n - n1);
     return hipGetLastError();
 }
 

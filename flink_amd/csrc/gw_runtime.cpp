@@ -165,6 +165,7 @@ struct gw_handle {
         bool known;
     };
     std::vector<FeBatch> fe_batches;  // not yet released, in arrival order
+    int64_t fe_wm = INT64_MIN;        // the last watermark (release decisions)
     int64_t fe_batch_no = 0;
     int64_t* c_pay = nullptr;
     void* fe_scratch = nullptr;
@@ -2070,7 +2071,7 @@ static int fe_reserve_rows(gw_handle* h, int64_t need) {
 // The rows both operators fired, joined by (key, window start) with the payload of the
 // window's first element, appended to the c_* rows; then the payloads no window can need
 // any more leave the log.
-static int fe_gather(gw_handle* h, int64_t wm) {
+static int fe_gather(gw_handle* h) {
     gw_handle *A = h->kids[0], *B = h->kids[1];
     int64_t na = 0, nb = 0;
     int rc = gw_pending_rows(A, &na);
@@ -2107,8 +2108,15 @@ static int fe_gather(gw_handle* h, int64_t wm) {
         if ((rc = gw_clear_rows(A))) return kid_rc(h, A, rc);
         if ((rc = gw_clear_rows(B))) return kid_rc(h, B, rc);
     }
-    // release: a batch whose largest timestamp's windows are all cleaned (maxTs + size - 1 +
-    // lateness <= wm: WindowOperator.cleanupTime) can hold no first element any more
+    return GW_OK;
+}
+
+// Release the payloads no window can need any more: a batch whose largest timestamp's
+// windows are all cleaned (maxTs + size - 1 + lateness <= wm: WindowOperator.cleanupTime).
+// Runs after a fire (cleanup happens then) and when the log would have to grow, so a
+// watermark that fires nothing costs no host synchronisation.
+static int fe_release(gw_handle* h) {
+    const int64_t wm = h->fe_wm;
     if (!h->fe_batches.empty()) {
         bool any = false;  // each batch's max timestamp crosses to the host once
         for (auto& b : h->fe_batches) {
@@ -2169,6 +2177,10 @@ int gw_ingest_payload_device(gw_handle* h, int64_t n, const int64_t* d_key, cons
     }
     hipError_t e = fe_iota64(h->fe_seqbuf, n, h->fe_seq, s);
     // payload log: a ring of the live sequences [fe_log_base, fe_seq + n)
+    if (h->fe_seq + n - h->fe_log_base > h->fe_log_cap || (int64_t)h->fe_batches.size() >= gw_handle::kFeBatches - 1) {
+        const int rc = fe_release(h);
+        if (rc) return rc;
+    }
     const int64_t need = h->fe_seq + n - h->fe_log_base;
     if (e == hipSuccess && need > h->fe_log_cap) {
         const int64_t ncap = std::max<int64_t>(2 * need, 1 << 20);
@@ -2583,8 +2595,12 @@ int gw_advance_watermark(gw_handle* h, int64_t wm, int64_t* rows_fired) {
             const int rc = gw_advance_watermark(kid, wm, kid == h->kids[0] ? &f : nullptr);
             if (rc) return kid_rc(h, kid, rc);
         }
-        const int rc = fe_gather(h, wm);
-        if (rc) return rc;
+        if (wm > h->fe_wm) h->fe_wm = wm;
+        if (f > 0) {  // both operators fired the same windows: join them, then release
+            int rc = fe_gather(h);
+            if (rc == GW_OK) rc = fe_release(h);
+            if (rc) return rc;
+        }
         h->stats.rows_fired += f;
         if (rows_fired) *rows_fired = f;
         return GW_OK;
