@@ -10,6 +10,8 @@
 // side by start, then by key -- and B's minimum sequence indexes the payload log (the other
 // fields of every record, packed by the caller into one 64-bit word, kept until all windows
 // that could hold the record are cleaned).
+#include <algorithm>
+
 #include <rocprim/device/device_radix_sort.hpp>
 
 #include "gw_first.h"
