@@ -160,3 +160,18 @@ def test_payload_glue_positional_rows(jni):
     for j in range(len(k)):
         assert (int(r[j]), int(pl[j])) == exp[(int(k[j]), int(s[j]))]
         assert e[j] == s[j] + 100
+
+
+def test_java_natives_have_jni_entry_points():
+    """Every `native` method GpuWindowOperator.java / GpuKeyByExchange.java declares has its
+    JNI function in gw_jni.c (the names the JVM binds: Java_<class path>_<method>)."""
+    import re
+    jdir = os.path.join(ROOT, "integration", "jni", "java", "org", "apache", "flink", "streaming", "runtime",
+                        "operators", "windowing", "gpu")
+    csrc = open(os.path.join(ROOT, "integration", "jni", "native", "gw_jni.c")).read()
+    for cls, macro in (("GpuWindowOperator", "CLS"), ("GpuKeyByExchange", "XCLS")):
+        src = open(os.path.join(jdir, cls + ".java")).read()
+        natives = set(re.findall(r"\bnative\s+[\w\[\]<>]+\s+(native\w+)\s*\(", src))
+        assert natives, cls
+        defined = set(re.findall(macro + r"\((native\w+)\)", csrc))
+        assert natives <= defined, f"{cls}: no JNI function for {sorted(natives - defined)}"
