@@ -112,7 +112,7 @@ __device__ __forceinline__ uint64_t lds_be64(const uint32_t* w, int p) {
 // Branch-free step (one ds_read2 gives the length word and the tag): every lane steps in
 // lockstep under a full exec mask, and the per-step VALU count stays small.
 __device__ __forceinline__ void nb_walk_lane(const uint32_t* l, int H, int rlim, int rec_ts, int rec_nots, bool run,
-                                             int& pos, int& nr, int& nw, int& st) {
+                                             int& pos, uint32_t& cnt, int& st) {
     while (__ballot(run)) {
         const int p = run ? pos : 0;
         const uint32_t w0 = l[p >> 2], w1 = l[(p >> 2) + 1];
@@ -137,8 +137,10 @@ __device__ __forceinline__ void nb_walk_lane(const uint32_t* l, int H, int rlim,
                      : len != want ? kStDead : kStNormal;
         const bool adv = run && ns == kStNormal;
         st = (run && !adv) ? ns : st;
-        nr += (adv && tag <= 1u) ? 1 : 0;
-        nw += (adv && (tag == 2u || tag == 6u)) ? 1 : 0;
+        // records | watermarks << 16 in one word: 2-bit class per tag (0, 1: record; 2, 6:
+        // watermark; 3-5: skipped), from a packed table
+        const uint32_t cls = (0x2025u >> (2 * (tag & 7u))) & 3u;
+        cnt += adv ? ((cls & 1u) | ((cls & 2u) << 15)) : 0u;
         pos = adv ? p + 4 + len : pos;
         run = adv && pos < H;
     }
@@ -205,11 +207,12 @@ __global__ void __launch_bounds__(256) k_nb_walk(const uint8_t* buf, int64_t nby
     const int rend = rlim < kNbChunk ? rlim : kNbChunk;
     const bool windowed = rend > kSync;
     const int H = windowed ? kSync : rend;
-    int pos[CPL], nr[CPL], nw[CPL], st[CPL];
+    int pos[CPL], st[CPL];
+    uint32_t cn[CPL];
 #pragma unroll
     for (int k = 0; k < CPL; ++k) {
-        pos[k] = lane + 64 * k; nr[k] = 0; nw[k] = 0; st[k] = kStNormal;
-        nb_walk_lane(l, H, rlim, rec_ts, rec_nots, pos[k] < H, pos[k], nr[k], nw[k], st[k]);
+        pos[k] = lane + 64 * k; cn[k] = 0; st[k] = kStNormal;
+        nb_walk_lane(l, H, rlim, rec_ts, rec_nots, pos[k] < H, pos[k], cn[k], st[k]);
     }
     // converged: every live candidate stopped normally on the same position
     bool conv_ok = windowed;
@@ -243,8 +246,7 @@ __global__ void __launch_bounds__(256) k_nb_walk(const uint8_t* buf, int64_t nby
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 #pragma unroll
         for (int k = 0; k < CPL; ++k)
-            nb_walk_lane(l, rend, rlim, rec_ts, rec_nots, st[k] == kStNormal && pos[k] < rend, pos[k], nr[k], nw[k],
-                         st[k]);
+            nb_walk_lane(l, rend, rlim, rec_ts, rec_nots, st[k] == kStNormal && pos[k] < rend, pos[k], cn[k], st[k]);
     }
     int64_t ex[CPL];
     bool live[CPL];
@@ -252,7 +254,7 @@ __global__ void __launch_bounds__(256) k_nb_walk(const uint8_t* buf, int64_t nby
     for (int k = 0; k < CPL; ++k) {
         const int cand = lane + 64 * k;
         exits[c * NL + cand] = (uint32_t)pos[k] | ((uint32_t)st[k] << 28);
-        cnt[c * NL + cand] = (uint32_t)nr[k] | ((uint32_t)nw[k] << 16);
+        cnt[c * NL + cand] = cn[k];
         ex[k] = nb_pack(base + pos[k], st[k]);
         live[k] = st[k] == kStNormal || st[k] == kStTail;
     }
