@@ -48,6 +48,7 @@ EXPORTS = [
     "gw_exchange_unique_id", "gw_exchange_create", "gw_exchange_destroy", "gw_exchange_batch",
     "gw_exchange_min_watermark", "gw_exchange_last_error",
     "gw_ingest_payload", "gw_ingest_payload_device", "gw_drain_payload",
+    "gw_snapshot_keys", "gw_snapshot_remap_keys",
 ]
 EXCHANGE_ID_BYTES = 128
 
@@ -140,6 +141,8 @@ def lib() -> ctypes.CDLL:
         "gw_snapshot": (c_int, [p, i32, i32, p, i64, P64]),
         "gw_restore": (c_int, [p, p, i64]),
         "gw_snapshot_slice": (c_int, [p, i64, i32, p, i64, P64]),
+        "gw_snapshot_keys": (c_int, [p, i64, p, i64, P64]),
+        "gw_snapshot_remap_keys": (c_int, [p, i64, p, p, i64]),
         "gw_end_input": (c_int, [p, P64]),
         "gw_pending_rows": (c_int, [p, P64]),
         "gw_drain": (c_int, [p, p, p, p, p, i64, P64]),
@@ -200,3 +203,24 @@ def snapshot_slice(blob: bytes, kg: int) -> bytes:
     out = ctypes.create_string_buffer(n.value)
     check(lib().gw_snapshot_slice(blob, len(blob), kg, out, n.value, ctypes.byref(n)))
     return out.raw[:n.value]
+
+
+def snapshot_keys(blob: bytes):
+    """The distinct keys (int64 ids) a snapshot blob names, ascending (gw_snapshot_keys)."""
+    import numpy as np
+    n = ctypes.c_int64(0)
+    check(lib().gw_snapshot_keys(blob, len(blob), None, 0, ctypes.byref(n)))
+    out = np.empty(n.value, np.int64)
+    if n.value:
+        check(lib().gw_snapshot_keys(blob, len(blob), out.ctypes.data, n.value, ctypes.byref(n)))
+    return out
+
+
+def snapshot_remap_keys(blob: bytes, mapping: dict) -> bytes:
+    """A copy of blob with every key k in mapping replaced by mapping[k] (gw_snapshot_remap_keys)."""
+    import numpy as np
+    buf = ctypes.create_string_buffer(bytes(blob), len(blob))
+    src = np.asarray(sorted(mapping), dtype=np.int64)
+    dst = np.asarray([mapping[int(k)] for k in src], dtype=np.int64)
+    check(lib().gw_snapshot_remap_keys(buf, len(blob), src.ctypes.data, dst.ctypes.data, len(src)))
+    return buf.raw[:len(blob)]

@@ -334,4 +334,23 @@ hipError_t launch_partition(int64_t n, const int64_t* key, const int32_t* key_ha
                             int64_t* ts_out, int64_t* val_out, int64_t* counts, void* scratch,
                             hipStream_t s, int32_t* hash_out = nullptr);
 
+// Key -> Java hashCode of the keys a handle was fed with a key_hash column (String,
+// Integer, ... keys mapped to int64 ids by the caller).  The heap backend files a key's
+// state under the key group of key.hashCode() (KeyGroupRangeAssignment.java:63-66), so a
+// snapshot needs the hash of every key holding state.  Open addressing, linear probing;
+// key[cap] / hash[cap] hold the key INT64_MIN (key[cap] = 1 once present, else 0).
+struct KeyHashMap {
+    int64_t* key = nullptr;
+    int32_t* hash = nullptr;
+    int64_t cap = 0;  // power of two; 0: no map yet
+};
+// Insert (key, hash) pairs (first hash wins); out[0] += keys inserted.  A second launch
+// with verify = 1 counts in out[1] the records whose hash differs from the stored one.
+hipError_t launch_khmap_insert(const KeyHashMap& m, int64_t n, const int64_t* key, const int32_t* hash, int verify,
+                               unsigned long long* out, hipStream_t s);
+// p[0..n) = v
+hipError_t launch_fill64(int64_t* p, int64_t n, int64_t v, hipStream_t s);
+// Every entry of `from` into the empty map `to`.
+hipError_t launch_khmap_rehash(const KeyHashMap& from, const KeyHashMap& to, hipStream_t s);
+
 }  // namespace gw

@@ -155,6 +155,98 @@ hipError_t launch_check_keys(int64_t n, const int64_t* key, const int32_t* key_h
     return hipGetLastError();
 }
 
+// ---- key -> Java hashCode map (KeyHashMap, gw_kernels.h) --------------------------------
+__device__ __forceinline__ int64_t khm_slot(const KeyHashMap& m, int64_t k) {
+    return (int64_t)(slot_hash(k) & (uint64_t)(m.cap - 1));
+}
+
+__global__ void __launch_bounds__(256) k_khmap_insert(KeyHashMap m, int64_t n, const int64_t* key, const int32_t* hash,
+                                                      int verify, unsigned long long* out) {
+    unsigned long long ins = 0, bad = 0;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t k = key[i];
+        const int32_t h = hash[i];
+        if (k == kEmptyKey) {  // the sentinel key has the extra slot
+            if (verify) bad += m.hash[m.cap] != h;
+            else if (atomicCAS((unsigned long long*)&m.key[m.cap], 0ull, 1ull) == 0ull) { m.hash[m.cap] = h; ins++; }
+            continue;
+        }
+        for (int64_t s = khm_slot(m, k);; s = (s + 1) & (m.cap - 1)) {
+            const int64_t cur = m.key[s];
+            if (cur == k) {
+                if (verify) bad += m.hash[s] != h;
+                break;
+            }
+            if (verify) {
+                if (cur == kEmptyKey) { bad++; break; }  // (cannot happen after the insert pass)
+                continue;
+            }
+            if (cur != kEmptyKey) continue;
+            const unsigned long long prev =
+                atomicCAS((unsigned long long*)&m.key[s], (unsigned long long)kEmptyKey, (unsigned long long)k);
+            if (prev == (unsigned long long)kEmptyKey) {
+                m.hash[s] = h;  // records of one key carry one hash: concurrent writers agree
+                ins++;
+                break;
+            }
+            if ((int64_t)prev == k) break;
+        }
+    }
+    ins = wave_sum(ins);
+    bad = wave_sum(bad);
+    if (__lane_id() == 0) {
+        if (ins) atomicAdd(&out[0], ins);
+        if (bad) atomicAdd(&out[1], bad);
+    }
+}
+
+__global__ void __launch_bounds__(256) k_khmap_rehash(KeyHashMap f, KeyHashMap t) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < f.cap; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t k = f.key[i];
+        if (k == kEmptyKey) continue;
+        for (int64_t s = khm_slot(t, k);; s = (s + 1) & (t.cap - 1)) {
+            if (atomicCAS((unsigned long long*)&t.key[s], (unsigned long long)kEmptyKey, (unsigned long long)k) ==
+                (unsigned long long)kEmptyKey) {
+                t.hash[s] = f.hash[i];
+                break;
+            }
+        }
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        t.key[t.cap] = f.key[f.cap];
+        t.hash[t.cap] = f.hash[f.cap];
+    }
+}
+
+__global__ void __launch_bounds__(256) k_fill64(int64_t* p, int64_t n, int64_t v) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) p[i] = v;
+}
+
+hipError_t launch_fill64(int64_t* p, int64_t n, int64_t v, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    int64_t g = (n + 255) / 256;
+    if (g > 4096) g = 4096;
+    hipLaunchKernelGGL(k_fill64, dim3((unsigned)g), dim3(256), 0, s, p, n, v);
+    return hipGetLastError();
+}
+
+hipError_t launch_khmap_insert(const KeyHashMap& m, int64_t n, const int64_t* key, const int32_t* hash, int verify,
+                               unsigned long long* out, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    int64_t g = (n + 255) / 256;
+    if (g > 4096) g = 4096;
+    hipLaunchKernelGGL(k_khmap_insert, dim3((unsigned)g), dim3(256), 0, s, m, n, key, hash, verify, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_khmap_rehash(const KeyHashMap& from, const KeyHashMap& to, hipStream_t s) {
+    int64_t g = (from.cap + 255) / 256;
+    if (g < 1) g = 1;
+    if (g > 4096) g = 4096;
+    hipLaunchKernelGGL(k_khmap_rehash, dim3((unsigned)g), dim3(256), 0, s, from, to);
+    return hipGetLastError();
+}
+
 hipError_t launch_key_groups(int64_t n, const int64_t* key, const int32_t* key_hash, int32_t max_p,
                              int32_t p, int32_t* kg, int32_t* owner, hipStream_t s) {
     int64_t g = (n + 255) / 256;

@@ -32,7 +32,8 @@ namespace {
 thread_local std::string g_create_error;
 
 constexpr int64_t kMaxIngest = (int64_t)1 << 30;
-constexpr uint32_t kSnapMaxVersion = 4;  // gw_handle::SnapHeader versions  // records per region-path batch / buffer
+constexpr uint32_t kSnapMaxVersion = 4;  // gw_handle::SnapHeader versions
+constexpr int64_t kSnapKeyHashes = 1;    // SnapHeader::flags
 
 // Host-time profile of the ingest path (GW_HOST_PROFILE=1: printed by gw_destroy).
 struct HostProf {
@@ -286,7 +287,7 @@ struct gw_handle {
     SessionState* sess = nullptr;
     // key checks (gw_ingest* with key_hash, GW_FLAG_CHECK_KEY_GROUPS): device words, see k_check_keys
     unsigned long long* d_chk = nullptr;
-    bool foreign_hash = false;  // a key_hash differed from Long.hashCode(key): no snapshots
+    bool foreign_hash = false;  // a key_hash differed from Long.hashCode(key) (keys are caller ids)
     int ingest_unroll = 2;  // records per thread per iteration of k_ingest (GW_INGEST_UNROLL)
     int64_t region_min_batch = 1 << 16;  // smallest batch for the region path (GW_REGION_MIN_BATCH)
 
@@ -1150,15 +1151,26 @@ struct gw_handle {
     int check_keys(int64_t nrec, const int64_t* d_key, const int32_t* d_hash) {
         const bool range = (cfg.flags & GW_FLAG_CHECK_KEY_GROUPS) != 0;
         if (nrec == 0 || (!d_hash && !range)) return GW_OK;
-        if (!d_chk) HIPCHECK(hipMalloc((void**)&d_chk, 16));
-        const unsigned long long init[2] = {0ull, ~0ull};
-        HIPCHECK(hipMemcpyAsync(d_chk, init, 16, hipMemcpyHostToDevice, stream));
+        if (!d_chk) HIPCHECK(hipMalloc((void**)&d_chk, 32));
+        const unsigned long long init[4] = {0ull, ~0ull, 0ull, 0ull};
+        HIPCHECK(hipMemcpyAsync(d_chk, init, 32, hipMemcpyHostToDevice, stream));
         const int32_t mp = cfg.max_parallelism, p = cfg.parallelism, ix = cfg.operator_index;
         const int32_t lo = (ix * mp + p - 1) / p, hi = ((ix + 1) * mp - 1) / p;  // KeyGroupRangeAssignment :93-106
         HIPCHECK(launch_check_keys(nrec, d_key, d_hash, mp, lo, hi, range ? 1 : 0, d_chk, stream));
-        unsigned long long out[2];
-        HIPCHECK(hipMemcpyAsync(out, d_chk, 16, hipMemcpyDeviceToHost, stream));
+        if (d_hash) {  // remember each key's hash: snapshots file its state under that key group
+            int rc = khm_reserve(nrec);
+            if (rc) return rc;
+            HIPCHECK(launch_khmap_insert(khm, nrec, d_key, d_hash, 0, d_chk + 2, stream));
+            HIPCHECK(launch_khmap_insert(khm, nrec, d_key, d_hash, 1, d_chk + 2, stream));
+        }
+        unsigned long long out[4];
+        HIPCHECK(hipMemcpyAsync(out, d_chk, 32, hipMemcpyDeviceToHost, stream));
         HIPCHECK(hipStreamSynchronize(stream));
+        khm_used += (int64_t)out[2];
+        if (out[3]) {
+            failed = true;
+            return fail(GW_E_INVALID, "a key arrived with two different key hashes (hashCode is not deterministic)");
+        }
         if (out[0]) foreign_hash = true;
         if (out[1] != ~0ull) {
             failed = true;
@@ -1171,16 +1183,106 @@ struct gw_handle {
         return GW_OK;
     }
 
+    // ------------------------------------------------- key -> Java hashCode (KeyHashMap)
+    KeyHashMap khm{};
+    int64_t khm_used = 0;  // keys in khm
+    void khm_free() {
+        if (khm.key) hipFree(khm.key);
+        if (khm.hash) hipFree(khm.hash);
+        khm = KeyHashMap{};
+        khm_used = 0;
+    }
+    // Room for `more` new keys at load <= 0.5 (grows by rehashing).
+    int khm_reserve(int64_t more) {
+        if (khm.cap && 2 * (khm_used + more) <= khm.cap) return GW_OK;
+        int64_t cap = khm.cap ? khm.cap : 1 << 12;
+        while (2 * (khm_used + more) > cap) cap *= 2;
+        KeyHashMap n;
+        n.cap = cap;
+        if (hipMalloc((void**)&n.key, (size_t)(cap + 1) * 8) != hipSuccess ||
+            hipMalloc((void**)&n.hash, (size_t)(cap + 1) * 4) != hipSuccess) {
+            if (n.key) hipFree(n.key);
+            return fail(GW_E_OOM, "key-hash map: out of device memory");
+        }
+        HIPCHECK(launch_fill64(n.key, cap, kEmptyKey, stream));
+        HIPCHECK(hipMemsetAsync(n.key + cap, 0, 8, stream));
+        HIPCHECK(hipMemsetAsync(n.hash + cap, 0, 4, stream));
+        if (khm.cap) HIPCHECK(launch_khmap_rehash(khm, n, stream));
+        HIPCHECK(hipStreamSynchronize(stream));
+        const int64_t used = khm_used;
+        khm_free();
+        khm = n;
+        khm_used = used;
+        return GW_OK;
+    }
+    // Host copy of the map, sorted by key, for key groups at snapshot time.
+    struct KhmHost {
+        std::vector<std::pair<int64_t, int32_t>> kv;
+        bool has_min = false;
+        int32_t min_hash = 0;
+        bool on() const { return has_min || !kv.empty(); }
+        int32_t hash(int64_t key) const {
+            if (key == kEmptyKey) return has_min ? min_hash : java_long_hash(key);
+            auto it = std::lower_bound(kv.begin(), kv.end(), std::make_pair(key, INT32_MIN));
+            return it != kv.end() && it->first == key ? it->second : java_long_hash(key);
+        }
+    };
+    int khm_host(KhmHost& out) {
+        out = KhmHost{};
+        if (!khm_used) return GW_OK;
+        std::vector<int64_t> k((size_t)khm.cap + 1);
+        std::vector<int32_t> h((size_t)khm.cap + 1);
+        HIPCHECK(hipStreamSynchronize(stream));
+        HIPCHECK(hipMemcpy(k.data(), khm.key, k.size() * 8, hipMemcpyDeviceToHost));
+        HIPCHECK(hipMemcpy(h.data(), khm.hash, h.size() * 4, hipMemcpyDeviceToHost));
+        out.kv.reserve((size_t)khm_used);
+        for (int64_t i = 0; i < khm.cap; ++i)
+            if (k[i] != kEmptyKey) out.kv.push_back({k[i], h[i]});
+        std::sort(out.kv.begin(), out.kv.end());
+        out.has_min = k[khm.cap] != 0;
+        out.min_hash = h[khm.cap];
+        return GW_OK;
+    }
+    // (key, hash) pairs of a restored blob into the map.
+    int khm_insert_host(const std::vector<int64_t>& keys, const std::vector<int32_t>& hashes) {
+        const int64_t n = (int64_t)keys.size();
+        if (!n) return GW_OK;
+        int rc = khm_reserve(n);
+        if (rc) return rc;
+        int64_t* dk_ = nullptr;
+        int32_t* dh_ = nullptr;
+        if (!d_chk) HIPCHECK(hipMalloc((void**)&d_chk, 32));
+        HIPCHECK(hipMalloc((void**)&dk_, (size_t)n * 8));
+        HIPCHECK(hipMalloc((void**)&dh_, (size_t)n * 4));
+        HIPCHECK(hipMemcpy(dk_, keys.data(), (size_t)n * 8, hipMemcpyHostToDevice));
+        HIPCHECK(hipMemcpy(dh_, hashes.data(), (size_t)n * 4, hipMemcpyHostToDevice));
+        const unsigned long long init[4] = {0ull, ~0ull, 0ull, 0ull};
+        HIPCHECK(hipMemcpyAsync(d_chk, init, 32, hipMemcpyHostToDevice, stream));
+        HIPCHECK(launch_khmap_insert(khm, n, dk_, dh_, 0, d_chk + 2, stream));
+        HIPCHECK(launch_khmap_insert(khm, n, dk_, dh_, 1, d_chk + 2, stream));
+        unsigned long long out[4];
+        HIPCHECK(hipMemcpyAsync(out, d_chk, 32, hipMemcpyDeviceToHost, stream));
+        HIPCHECK(hipStreamSynchronize(stream));
+        hipFree(dk_);
+        hipFree(dh_);
+        khm_used += (int64_t)out[2];
+        if (out[3]) return fail(GW_E_INVALID, "snapshot: a key with two different key hashes");
+        return GW_OK;
+    }
+
     // ---------------------------------------------------------------- snapshot
     // Blob (little-endian): SnapHeader, int64 kg_offsets[kg_hi - kg_lo + 2], then the entries
     // of each key group.  Versions: 2 session windows, 3 count windows (fixed-size entries of
     // `reserved` int64 words, offsets in entries), 4 tumbling / sliding windows (the heap
     // backend's per-key-group byte layout, offsets in bytes; see snapshot_heap).
+    // flags: kSnapKeyHashes -- the keys came with a key_hash column (String, Integer, ...
+    // keys as caller ids): each state entry carries the key's Java hashCode after the key
+    // (version 4: be32 after the be64 key; versions 2 / 3: one more int64 word at the end).
     struct SnapHeader {
         char magic[4];
         uint32_t version;
         int32_t agg, assigner;
-        int64_t size, slide, offset, gap, pane;
+        int64_t size, slide, offset, gap, flags;
         int32_t max_parallelism, kg_lo, kg_hi, reserved;
         int64_t fired_lo, fired_hi;
         int64_t entries;  // entries (versions 2, 3) / payload bytes (version 4)
@@ -1353,6 +1455,10 @@ struct gw_handle {
         if ((rc = flush_buffer())) return rc;  // prepareSnapshotPreBarrier: buffered records first
         if (rf_bound && (rc = process_refire())) return rc;  // late records of fired windows
         if ((rc = refresh())) return rc;
+        KhmHost kh;  // keys fed with a key_hash: their key group comes from that hash
+        if ((rc = khm_host(kh))) return rc;
+        const bool hashed = kh.on();
+        auto kg_of = [&](int64_t key) { return key_group_for_hash(kh.hash(key), cfg.max_parallelism); };
         // (key, pane, a0, a1, kg) of every non-null pane cell and parked entry in range
         const int64_t n_def = (int64_t)h_st->n_deferred;
         const int64_t bound = ((int64_t)h_st->used_slots + 1) * popcount(occ) + n_def;
@@ -1367,7 +1473,9 @@ struct gw_handle {
             for (i128 p = B; p < B + R; ++p) a.pane_of_pos[pos_of(p)] = (int64_t)p;
             a.d_key = dk[cur]; a.d_pane = dp[cur]; a.d_a0 = da0[cur]; a.d_a1 = da1[cur];
             a.n_def = n_def;
-            a.max_p = cfg.max_parallelism; a.kg_lo = kg_lo; a.kg_hi = kg_hi;
+            a.max_p = cfg.max_parallelism;
+            a.kg_lo = hashed ? 0 : kg_lo;  // hashed keys: every entry, key groups on the host
+            a.kg_hi = hashed ? cfg.max_parallelism - 1 : kg_hi;
             a.o_key = d; a.o_pane = d + bound; a.o_a0 = d + 2 * bound; a.o_a1 = d + 3 * bound;
             a.o_kg = (int32_t*)(d + 4 * bound);
             a.n_out = d_tmp + 2;
@@ -1386,6 +1494,17 @@ struct gw_handle {
             }
             hipFree(d);
             if (e != hipSuccess) return fail(GW_E_DEVICE, "snapshot: %s", hipGetErrorString(e));
+            if (hashed) {  // key groups from the keys' own hashes, then the range filter
+                size_t w = 0;
+                for (size_t i = 0; i < kgs.size(); ++i) {
+                    const int32_t g = kg_of(col[0][i]);
+                    if (g < kg_lo || g > kg_hi) continue;
+                    for (int c = 0; c < 4; ++c) col[c][w] = col[c][i];
+                    kgs[w++] = g;
+                }
+                kgs.resize(w);
+                for (int c = 0; c < 4; ++c) col[c].resize(w);
+            }
         }
         // the restored windows still holding state
         std::vector<OvEntry> ov;
@@ -1396,7 +1515,7 @@ struct gw_handle {
             HIPCHECK(hipMemcpy(of.data(), d_ov_flags, (size_t)ov_n * 4, hipMemcpyDeviceToHost));
             for (int64_t i = 0; i < ov_n; ++i) {
                 if (of[i] & kOvDead) continue;
-                const int32_t kg = key_group_for_hash(java_long_hash(oc[i]), cfg.max_parallelism);
+                const int32_t kg = kg_of(oc[i]);
                 if (kg < kg_lo || kg > kg_hi) continue;
                 ov.push_back(OvEntry{oc[i], oc[ov_n + i], oc[2 * ov_n + i], oc[3 * ov_n + i], of[i]});
             }
@@ -1409,7 +1528,7 @@ struct gw_handle {
         std::vector<std::vector<int64_t>> by_kg(nk);  // indices into col
         for (size_t i = 0; i < kgs.size(); ++i) by_kg[kgs[i] - kg_lo].push_back((int64_t)i);
         std::vector<std::vector<OvEntry>> ov_kg(nk);
-        for (auto& e : ov) ov_kg[key_group_for_hash(java_long_hash(e.key), cfg.max_parallelism) - kg_lo].push_back(e);
+        for (auto& e : ov) ov_kg[kg_of(e.key) - kg_lo].push_back(e);
         std::vector<uint8_t> pay;
         std::vector<int64_t> offs(nk + 1, 0);
         const int64_t id0 = identity0(cfg.agg);
@@ -1474,6 +1593,7 @@ struct gw_handle {
                     const i128 s0 = win_start(k), e0 = s0 + (i128)size();
                     if (!fits64(s0) || !fits64(e0)) return fail(GW_E_RANGE, "window bounds overflow int64");
                     be64(st, (int64_t)s0); be64(st, (int64_t)e0); be64(st, key);
+                    if (hashed) be32(st, kh.hash(key));
                     acc_to_be(st, r0, r1);
                     nst++;
                     const i128 mx = e0 - 1;
@@ -1505,7 +1625,8 @@ struct gw_handle {
         memcpy(hd.magic, "GWS1", 4);
         hd.version = 4;
         hd.agg = cfg.agg; hd.assigner = cfg.assigner;
-        hd.size = cfg.size; hd.slide = slide(); hd.offset = cfg.offset; hd.gap = cfg.gap; hd.pane = 0;
+        hd.size = cfg.size; hd.slide = slide(); hd.offset = cfg.offset; hd.gap = cfg.gap;
+        hd.flags = hashed ? kSnapKeyHashes : 0;
         hd.max_parallelism = cfg.max_parallelism; hd.kg_lo = kg_lo; hd.kg_hi = kg_hi;
         hd.entries = (int64_t)pay.size();
         char* out = (char*)buf;
@@ -1530,27 +1651,34 @@ struct gw_handle {
             return fail(GW_E_STATE, "restore after processing started (initializeState runs before the first record)");
         const int64_t nk = (int64_t)hd.kg_hi - hd.kg_lo + 1;
         const int64_t pay0 = (int64_t)sizeof hd + (nk + 1) * 8;
-        if (nk <= 0 || hd.entries < 0 || len < pay0 + hd.entries) return fail(GW_E_INVALID, "truncated snapshot blob");
+        if (nk <= 0 || hd.entries < 0 || len < pay0 || hd.entries > len - pay0) return fail(GW_E_INVALID, "truncated snapshot blob");
         const uint8_t* p = (const uint8_t*)buf + pay0;
         const uint8_t* end = p + hd.entries;
         const int ab = acc_bytes();
+        const int hb = (hd.flags & kSnapKeyHashes) ? 4 : 0;
         const size_t first = ov_pending.size();
-#define NEED(x) do { if (p + (x) > end) return fail(GW_E_INVALID, "truncated snapshot blob"); } while (0)
+        std::vector<int64_t> hkeys;  // (key, hash) of a hashed blob's entries
+        std::vector<int32_t> hvals;
+#define NEED(x) do { if ((int64_t)(x) > end - p) return fail(GW_E_INVALID, "truncated snapshot blob"); } while (0)
         for (int64_t g = 0; g < nk; ++g) {
             NEED(4);
             const int32_t ns = rd32(p); p += 4;
             const size_t base = ov_pending.size();
             for (int32_t i = 0; i < ns; ++i) {
-                NEED(24 + ab);
+                NEED(24 + hb + ab);
                 const int64_t s0 = rd64(p), e0 = rd64(p + 8), key = rd64(p + 16);
                 const i128 k = floor_div((i128)s0 - cfg.offset, (i128)slide());
                 if (win_start(k) != (i128)s0 || (i128)s0 + size() != (i128)e0)
                     return fail(GW_E_INVALID, "snapshot window [%lld, %lld) is not a window of this assigner",
                                 (long long)s0, (long long)e0);
                 OvEntry e{key, (int64_t)k, 0, 0, 0};
-                acc_from_be(p + 24, e.a0, e.a1);
+                if (hb) {
+                    hkeys.push_back(key);
+                    hvals.push_back(rd32(p + 24));
+                }
+                acc_from_be(p + 24 + hb, e.a0, e.a1);
                 ov_pending.push_back(e);
-                p += 24 + ab;
+                p += 24 + hb + ab;
             }
             NEED(4);
             if (rd32(p) != 0) return fail(GW_E_INVALID, "merging window set in a tumbling / sliding snapshot");
@@ -1579,7 +1707,7 @@ struct gw_handle {
             ov_pending.resize(first);
             return fail(GW_E_INVALID, "snapshot blob has trailing bytes");
         }
-        return GW_OK;
+        return khm_insert_host(hkeys, hvals);
     }
 
     // Session windows: the blob (version 2) holds, per key group, every in-flight session
@@ -1598,10 +1726,26 @@ struct gw_handle {
         if (kg_lo < 0 || kg_hi < kg_lo || kg_hi >= cfg.max_parallelism)
             return fail(GW_E_INVALID, "key-group range [%d, %d] outside [0, %d)", kg_lo, kg_hi, cfg.max_parallelism);
         if ((rc = session_refresh(sess, err))) return fail(rc, "%s", err.c_str());
+        KhmHost kh;
+        if ((rc = khm_host(kh))) return rc;
+        const bool hashed = kh.on();
         std::vector<int64_t> ent;
         std::vector<int32_t> kgs;
-        if ((rc = session_collect(sess, kg_lo, kg_hi, ent, kgs, err))) return fail(rc, "%s", err.c_str());
-        const int64_t ew = session_entry_words(sess);
+        if ((rc = session_collect(sess, kg_lo, kg_hi, ent, kgs, err,
+                                  hashed ? std::function<int32_t(int64_t)>([&](int64_t k) { return kh.hash(k); })
+                                         : std::function<int32_t(int64_t)>())))
+            return fail(rc, "%s", err.c_str());
+        const int64_t ew0 = session_entry_words(sess);
+        if (hashed) {  // each entry gets the key's hash as one more word
+            std::vector<int64_t> w;
+            w.reserve(ent.size() / ew0 * (ew0 + 1));
+            for (size_t i = 0; i < ent.size(); i += ew0) {
+                w.insert(w.end(), ent.begin() + i, ent.begin() + i + ew0);
+                w.push_back((int64_t)kh.hash(ent[i]));
+            }
+            ent.swap(w);
+        }
+        const int64_t ew = ew0 + (hashed ? 1 : 0);
         const int nk = kg_hi - kg_lo + 1;
         std::vector<int64_t> offs(nk + 1, 0);
         for (int32_t k : kgs) offs[k - kg_lo + 1]++;
@@ -1617,6 +1761,7 @@ struct gw_handle {
         hd.size = cfg.size; hd.slide = cfg.slide; hd.gap = cfg.gap;
         hd.max_parallelism = cfg.max_parallelism; hd.kg_lo = kg_lo; hd.kg_hi = kg_hi;
         hd.reserved = (int32_t)ew;
+        hd.flags = hashed ? kSnapKeyHashes : 0;
         hd.entries = (int64_t)kgs.size();
         char* out = (char*)buf;
         memcpy(out, &hd, sizeof hd);
@@ -1633,18 +1778,34 @@ struct gw_handle {
         memcpy(&hd, buf, sizeof hd);
         if (memcmp(hd.magic, "GWS1", 4) != 0 || hd.version < 1 || hd.version > 3)
             return fail(GW_E_INVALID, "not a gpuwin snapshot");
-        const int64_t ew = session_entry_words(sess);
+        const bool hashed = (hd.flags & kSnapKeyHashes) != 0;
+        const int64_t ew0 = session_entry_words(sess), ew = ew0 + (hashed ? 1 : 0);
         if (hd.version != slot_blob_version() || hd.agg != cfg.agg || hd.assigner != cfg.assigner ||
             hd.gap != cfg.gap || hd.size != cfg.size || hd.slide != cfg.slide ||
             hd.max_parallelism != cfg.max_parallelism || hd.reserved != (int32_t)ew)
             return fail(GW_E_INVALID, "snapshot of a different window / aggregate / max parallelism");
-        const int nk = hd.kg_hi - hd.kg_lo + 1;
-        const int64_t need = (int64_t)sizeof hd + (int64_t)(nk + 1) * 8 + hd.entries * ew * 8;
-        if (nk <= 0 || hd.entries < 0 || len < need) return fail(GW_E_INVALID, "truncated snapshot blob");
-        const int64_t* in = (const int64_t*)((const char*)buf + sizeof hd + (nk + 1) * 8);
-        std::vector<int64_t> ent(in, in + hd.entries * ew);  // aligned copy
+        const int64_t nk = (int64_t)hd.kg_hi - hd.kg_lo + 1;
+        const int64_t hdr = (int64_t)sizeof hd + (nk + 1) * 8;
+        if (nk <= 0 || hd.entries < 0 || len < hdr || hd.entries > (len - hdr) / (ew * 8))
+            return fail(GW_E_INVALID, "truncated snapshot blob");
+        const int64_t* in = (const int64_t*)((const char*)buf + hdr);
+        std::vector<int64_t> ent, hkeys;
+        std::vector<int32_t> hvals;
+        ent.reserve((size_t)(hd.entries * ew0));
+        for (int64_t i = 0; i < hd.entries; ++i) {  // aligned copy without the hash words
+            const size_t at = ent.size();
+            ent.resize(at + (size_t)ew0);
+            memcpy(ent.data() + at, (const char*)in + i * ew * 8, (size_t)ew0 * 8);
+            if (hashed) {
+                int64_t hw;
+                memcpy(&hw, (const char*)in + (i * ew + ew0) * 8, 8);
+                hkeys.push_back(ent[at]);
+                hvals.push_back((int32_t)hw);
+            }
+        }
         int rc = session_restore(sess, ent.data(), hd.entries, err);
-        return rc ? fail(rc, "%s", err.c_str()) : GW_OK;
+        if (rc) return fail(rc, "%s", err.c_str());
+        return khm_insert_host(hkeys, hvals);
     }
 
     int advance_pane(int64_t w, int64_t* rows_out) {
@@ -1973,6 +2134,7 @@ int gw_destroy(gw_handle* h) {
     }
     h->hp.dump();
     if (h->stream) hipStreamSynchronize(h->stream);
+    h->khm_free();
     if (h->sess) session_destroy(h->sess);
     h->ov_free();
     if (h->tv.base) hipFree(h->tv.base);
@@ -2084,6 +2246,12 @@ static int fe_gather(gw_handle* h) {
         int64_t x = 0;
         if ((rc = gw_rows_device(A, &ak, &as, &ae, &ar, &x))) return kid_rc(h, A, rc);
         if ((rc = gw_rows_device(B, &bk, &bs, &be, &br, &x))) return kid_rc(h, B, rc);
+        if (B->stream != h->stream) {
+            // B (e.g. a window-class composite) gathers its rows on its own stream: the join
+            // on h's stream reads them only after those copies
+            if (hipEventRecord(h->ev_out, B->stream) != hipSuccess || hipStreamWaitEvent(h->stream, h->ev_out, 0) != hipSuccess)
+                return h->fail(GW_E_DEVICE, "first-element join: stream ordering");
+        }
         if ((rc = fe_reserve_rows(h, h->c_rows + na))) return rc;
         const size_t need = fe_join_scratch_bytes(na);
         if (need > h->fe_scratch_bytes) {
@@ -2658,15 +2826,21 @@ static int64_t comp_slide(const gw_handle* h) { return h->cfg.assigner == GW_TUM
 static int comp_snapshot(gw_handle* h, int32_t kg_lo, int32_t kg_hi, void* buf, int64_t cap, int64_t* len) {
     const int64_t nk = (int64_t)kg_hi - kg_lo + 1;
     if (kg_lo < 0 || nk <= 0) return h->fail(GW_E_INVALID, "bad key-group range");
-    const int64_t eb = 24 + h->kids[0]->acc_bytes();
     std::vector<std::vector<uint8_t>> blobs(h->kids.size());
+    int64_t flags = -1;
     for (size_t j = 0; j < h->kids.size(); ++j) {
         int64_t l = 0;
         int rc = gw_snapshot(h->kids[j], kg_lo, kg_hi, nullptr, 0, &l);
         if (rc) return kid_rc(h, h->kids[j], rc);
         blobs[j].resize((size_t)l);
         if ((rc = gw_snapshot(h->kids[j], kg_lo, kg_hi, blobs[j].data(), l, &l))) return kid_rc(h, h->kids[j], rc);
+        SnapHdr kh;
+        memcpy(&kh, blobs[j].data(), sizeof kh);
+        if (flags >= 0 && kh.flags != flags) return h->fail(GW_E_STATE, "window classes disagree on key hashes");
+        flags = kh.flags;
     }
+    // every class sees every batch, so all or none carry key hashes
+    const int64_t eb = 24 + ((flags & kSnapKeyHashes) ? 4 : 0) + h->kids[0]->acc_bytes();
     std::vector<uint8_t> pay;
     std::vector<int64_t> offs(nk + 1, 0);
     const int64_t hb = (int64_t)sizeof(SnapHdr) + (nk + 1) * 8;
@@ -2724,8 +2898,10 @@ static int comp_restore(gw_handle* h, const void* buf, int64_t len) {
         return h->fail(GW_E_INVALID, "snapshot of a different window / aggregate / max parallelism");
     const int64_t nk = (int64_t)hd.kg_hi - hd.kg_lo + 1;
     const int64_t hb = (int64_t)sizeof hd + (nk + 1) * 8;
-    if (nk <= 0 || hd.entries < 0 || len < hb + hd.entries) return h->fail(GW_E_INVALID, "truncated snapshot blob");
-    const int64_t J = (int64_t)h->kids.size(), eb = 24 + h->kids[0]->acc_bytes();
+    if (nk <= 0 || hd.entries < 0 || len < hb || hd.entries > len - hb)
+        return h->fail(GW_E_INVALID, "truncated snapshot blob");
+    const int64_t J = (int64_t)h->kids.size();
+    const int64_t eb = 24 + ((hd.flags & kSnapKeyHashes) ? 4 : 0) + h->kids[0]->acc_bytes();
     const uint8_t* p = (const uint8_t*)buf + hb;
     const uint8_t* end = p + hd.entries;
     auto cls = [&](int64_t s0) {  // window class of a window start
@@ -2737,10 +2913,10 @@ static int comp_restore(gw_handle* h, const void* buf, int64_t len) {
     for (int64_t g = 0; g < nk; ++g) {
         std::vector<std::vector<uint8_t>> st(J), tm(J);
         std::vector<int32_t> nst(J, 0), ntm(J, 0);
-        if (p + 4 > end) return h->fail(GW_E_INVALID, "truncated snapshot blob");
+        if (end - p < 4) return h->fail(GW_E_INVALID, "truncated snapshot blob");
         const int32_t n = gw_handle::rd32(p);
         p += 4;
-        if (n < 0 || p + (int64_t)n * eb + 8 > end) return h->fail(GW_E_INVALID, "truncated snapshot blob");
+        if (n < 0 || (int64_t)n * eb + 8 > end - p) return h->fail(GW_E_INVALID, "truncated snapshot blob");
         for (int32_t i = 0; i < n; ++i, p += eb) {
             const size_t j = cls(gw_handle::rd64(p));
             st[j].insert(st[j].end(), p, p + eb);
@@ -2750,7 +2926,7 @@ static int comp_restore(gw_handle* h, const void* buf, int64_t len) {
         p += 4;
         const int32_t t = gw_handle::rd32(p);
         p += 4;
-        if (t < 0 || p + (int64_t)t * 32 > end) return h->fail(GW_E_INVALID, "truncated snapshot blob");
+        if (t < 0 || (int64_t)t * 32 > end - p) return h->fail(GW_E_INVALID, "truncated snapshot blob");
         for (int32_t i = 0; i < t; ++i, p += 32) {
             const size_t j = cls(gw_handle::rd64(p + 16));  // (timestamp, key, start, end)
             tm[j].insert(tm[j].end(), p, p + 32);
@@ -2788,9 +2964,6 @@ int gw_snapshot(gw_handle* h, int32_t kg_lo, int32_t kg_hi, void* buf, int64_t c
     if (h->fe) return h->fail(GW_E_UNSUPPORTED, "snapshots of first-element rows are not supported");
     if (!h->kids.empty()) return comp_snapshot(h, kg_lo, kg_hi, buf, cap, len);
     if (h->failed) return h->fail(GW_E_STATE, "operator failed earlier: %s", h->err.c_str());
-    if (h->foreign_hash)
-        return h->fail(GW_E_UNSUPPORTED, "snapshot of a handle that ingested a key_hash different from "
-                                         "Long.hashCode(key): the state is grouped by Long.hashCode");
     hipSetDevice(h->cfg.device);
     if (h->session) return h->snapshot_sessions(kg_lo, kg_hi, buf, cap, len);
     return h->snapshot_heap(kg_lo, kg_hi, buf, cap, len);
@@ -2821,7 +2994,8 @@ int gw_snapshot_slice(const void* blob, int64_t len, int32_t kg, void* out, int6
     }
     const int64_t ew = hd.version == 1 ? 32 : hd.version >= 4 ? 1 : (int64_t)hd.reserved * 8;  // v4: bytes
     const int64_t nk = (int64_t)hd.kg_hi - hd.kg_lo + 1;
-    if (ew <= 0 || nk <= 0 || hd.entries < 0 || len < (int64_t)sizeof hd + (nk + 1) * 8 + hd.entries * ew) {
+    if (ew <= 0 || nk <= 0 || hd.entries < 0 || len < (int64_t)sizeof hd + (nk + 1) * 8 ||
+        hd.entries > (len - (int64_t)sizeof hd - (nk + 1) * 8) / ew) {
         g_create_error = "truncated snapshot blob";
         return GW_E_INVALID;
     }
@@ -2847,6 +3021,100 @@ int gw_snapshot_slice(const void* blob, int64_t len, int32_t kg, void* out, int6
     const int64_t offs[2] = {0, n};
     memcpy(o + sizeof oh, offs, 16);
     if (n) memcpy(o + sizeof oh + 16, b + sizeof hd + (nk + 1) * 8 + o0 * ew, (size_t)(n * ew));
+    return GW_OK;
+}
+
+extern "C++" {
+// Calls f(p, big_endian) for the key field of every entry, merging-set key and timer of a
+// version 2-4 blob; false for a corrupt blob.
+template <class F>
+static bool blob_keys(const uint8_t* b, int64_t len, F&& f) {
+    typedef gw_handle::SnapHeader H;
+    H hd;
+    if (!b || len < (int64_t)sizeof hd) return false;
+    memcpy(&hd, b, sizeof hd);
+    if (memcmp(hd.magic, "GWS1", 4) != 0 || hd.version < 2 || hd.version > kSnapMaxVersion) return false;
+    const int64_t nk = (int64_t)hd.kg_hi - hd.kg_lo + 1;
+    const int64_t pay0 = (int64_t)sizeof hd + (nk + 1) * 8;
+    if (nk <= 0 || hd.entries < 0 || len < pay0) return false;
+    const uint8_t* p = b + pay0;
+    if (hd.version < 4) {  // fixed entries of `reserved` int64 words, key first
+        const int64_t ew = (int64_t)hd.reserved * 8;
+        if (ew <= 0 || hd.entries > (len - pay0) / ew) return false;
+        for (int64_t i = 0; i < hd.entries; ++i) f(p + i * ew, false);
+        return true;
+    }
+    if (hd.entries > len - pay0) return false;
+    const uint8_t* end = p + hd.entries;
+    const int64_t eb = 24 + ((hd.flags & kSnapKeyHashes) ? 4 : 0) +
+                       (hd.agg == GW_SUM_I32 ? 4 : (hd.agg == GW_AVG_I64 || hd.agg == GW_AVG_F64) ? 16 : 8);
+    for (int64_t g = 0; g < nk; ++g) {
+        if (end - p < 4) return false;
+        const int32_t n = gw_handle::rd32(p);
+        p += 4;
+        if (n < 0 || (int64_t)n * eb + 4 > end - p) return false;
+        for (int32_t i = 0; i < n; ++i, p += eb) f(p + 16, true);
+        const int32_t m = gw_handle::rd32(p);
+        p += 4;
+        if (m < 0) return false;
+        for (int32_t i = 0; i < m; ++i) {  // merging window sets: (key, be32 c, c x 32 B)
+            if (end - p < 12) return false;
+            const int32_t c = gw_handle::rd32(p + 8);
+            if (c < 0 || (int64_t)c * 32 > end - p - 12) return false;
+            f(p, true);
+            p += 12 + (int64_t)c * 32;
+        }
+        if (end - p < 4) return false;
+        const int32_t t = gw_handle::rd32(p);
+        p += 4;
+        if (t < 0 || (int64_t)t * 32 > end - p) return false;
+        for (int32_t i = 0; i < t; ++i, p += 32) f(p + 8, true);
+    }
+    return p == end;
+}
+
+static int64_t key_at(const uint8_t* p, bool be) {
+    if (be) return gw_handle::rd64(p);
+    int64_t k;
+    memcpy(&k, p, 8);
+    return k;
+}
+
+}  // extern "C++"
+
+int gw_snapshot_keys(const void* blob, int64_t len, int64_t* keys, int64_t cap, int64_t* n) {
+    if (!n) return GW_E_INVALID;
+    std::vector<int64_t> ks;
+    if (!blob_keys((const uint8_t*)blob, len, [&](const uint8_t* p, bool be) { ks.push_back(key_at(p, be)); })) {
+        g_create_error = "corrupt snapshot blob";
+        return GW_E_INVALID;
+    }
+    std::sort(ks.begin(), ks.end());
+    ks.erase(std::unique(ks.begin(), ks.end()), ks.end());
+    *n = (int64_t)ks.size();
+    if (!keys) return GW_OK;
+    if (cap < *n) { g_create_error = "key buffer too small"; return GW_E_OUTPUT_FULL; }
+    if (!ks.empty()) memcpy(keys, ks.data(), ks.size() * 8);
+    return GW_OK;
+}
+
+int gw_snapshot_remap_keys(void* blob, int64_t len, const int64_t* from, const int64_t* to, int64_t n) {
+    if (n < 0 || (n > 0 && (!from || !to))) { g_create_error = "null key map"; return GW_E_INVALID; }
+    for (int64_t i = 1; i < n; ++i)
+        if (from[i] <= from[i - 1]) { g_create_error = "remap keys: from[] not ascending"; return GW_E_INVALID; }
+    const bool ok = blob_keys((const uint8_t*)blob, len, [&](const uint8_t* cp, bool be) {
+        uint8_t* p = const_cast<uint8_t*>(cp);
+        const int64_t k = key_at(p, be);
+        const int64_t* it = std::lower_bound(from, from + n, k);
+        if (it == from + n || *it != k) return;
+        const int64_t v = to[it - from];
+        if (be) {
+            for (int i = 0; i < 8; ++i) p[i] = (uint8_t)((uint64_t)v >> (56 - 8 * i));
+        } else {
+            memcpy(p, &v, 8);
+        }
+    });
+    if (!ok) { g_create_error = "corrupt snapshot blob"; return GW_E_INVALID; }
     return GW_OK;
 }
 

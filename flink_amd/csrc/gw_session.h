@@ -1,5 +1,6 @@
 // gw_session.h — host interface of the event-time session-window path (gw_session.hip).
 #pragma once
+#include <functional>
 #include <string>
 #include <vector>
 
@@ -21,8 +22,10 @@ int session_refresh(SessionState* s, std::string& err);
 // sessions (key, start, end, a0, a1, fired) per in-flight session; count windows (key, element
 // count, ring of pane accumulators) per key.
 int session_entry_words(SessionState* s);
+// hash_of: the Java hashCode of a key (empty: Long.hashCode).
 int session_collect(SessionState* s, int32_t kg_lo, int32_t kg_hi, std::vector<int64_t>& ent,
-                    std::vector<int32_t>& kgs, std::string& err);
+                    std::vector<int32_t>& kgs, std::string& err,
+                    const std::function<int32_t(int64_t)>& hash_of = nullptr);
 // Insert n entries of session_entry_words() int64 (as session_collect writes them).
 int session_restore(SessionState* s, const int64_t* ent, int64_t n, std::string& err);
 int session_clear_rows(SessionState* s, std::string& err);

@@ -1591,7 +1591,7 @@ int session_clear_rows(SessionState* s, std::string& err) { return set_word(s, o
 // 95-104 persistState); in-flight sessions are exactly that state here, one
 // (key, start, end, a0, a1, fired) entry per session.
 int session_collect(SessionState* s, int32_t kg_lo, int32_t kg_hi, std::vector<int64_t>& ent,
-                    std::vector<int32_t>& kgs, std::string& err) {
+                    std::vector<int32_t>& kgs, std::string& err, const std::function<int32_t(int64_t)>& hash_of) {
     SCHECK(hipStreamSynchronize(s->stream));
     for (int tab = 0; tab < (s->count_mode ? 1 : 2); ++tab) {
         const TableView& t = tab ? s->wv : s->tv;
@@ -1604,7 +1604,7 @@ int session_collect(SessionState* s, int32_t kg_lo, int32_t kg_hi, std::vector<i
             if (sp[1] == 0) continue;
             if (tab == 0 && !s->count_mode && ((uint64_t)sp[1] & kBigMeta)) continue;  // in the wide table
             const int64_t key = i == t.cap ? kEmptyKey : sp[0];
-            const int32_t kg = key_group_for_hash(java_long_hash(key), s->cfg.max_parallelism);
+            const int32_t kg = key_group_for_hash(hash_of ? hash_of(key) : java_long_hash(key), s->cfg.max_parallelism);
             if (kg < kg_lo || kg > kg_hi) continue;
             if (s->count_mode) {  // (key, element count, ring of pane accumulators)
                 ent.push_back(key);

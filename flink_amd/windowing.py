@@ -254,6 +254,7 @@ class GpuWindowOperator:
         self._h = None
         self._keys_in: dict = {}
         self._keys_out: list = []
+        self._hash_out: list = []  # key.hashCode() per dictionary id (gw_ingest key_hash)
         self._int_keys = True
         self._buf_k: List[int] = []
         self._buf_t: List[int] = []
@@ -293,6 +294,9 @@ class GpuWindowOperator:
 
     # keys --------------------------------------------------------------------
     def _encode_key(self, key) -> int:
+        """Long keys go to the GPU as they are (the device computes Long.hashCode); any
+        other key type gets a dictionary id, and its key.hashCode() travels in the key_hash
+        column so key groups, snapshots and rescaling follow the key's own hash."""
         if isinstance(key, int) and not isinstance(key, bool) and LONG_MIN <= key <= LONG_MAX and self._int_keys \
                 and not self._keys_out:
             return key
@@ -302,6 +306,7 @@ class GpuWindowOperator:
             kid = len(self._keys_out)
             self._keys_in[key] = kid
             self._keys_out.append(key)
+            self._hash_out.append(java_hash(key))
         return kid
 
     def _decode_key(self, kid: int):
@@ -324,7 +329,8 @@ class GpuWindowOperator:
         else:
             v = np.asarray(self._buf_v, dtype=np.int64)
         self._buf_k, self._buf_t, self._buf_v = [], [], []
-        self.process_batch(k, t, v)
+        h = None if self._int_keys else np.asarray(self._hash_out, dtype=np.int32)[k]
+        self.process_batch(k, t, v, key_hashes=h)
 
     def process_watermark(self, wm):
         ts = wm.timestamp if isinstance(wm, Watermark) else int(wm)
@@ -483,11 +489,32 @@ class GpuWindowOperator:
 
     def initialize_state(self, blobs):
         """Restore one or more snapshot blobs (e.g. the key-group ranges of several
-        subtasks after rescaling) before processing (StreamOperator.initializeState)."""
+        subtasks after rescaling) before processing (StreamOperator.initializeState).
+        A keyed snapshot (snapshot_state_keyed) gets its keys re-encoded through this
+        operator's dictionary first."""
         if isinstance(blobs, (bytes, bytearray)):
             blobs = [blobs]
         for b in blobs:
-            N.check(N.lib().gw_restore(self._h, bytes(b), len(b)), self._h)
+            b = bytes(b)
+            if b[:4] == KEYED_MAGIC:
+                b = self._rekey(b)
+            N.check(N.lib().gw_restore(self._h, b, len(b)), self._h)
+
+    def snapshot_state_keyed(self, key_group_range=None) -> bytes:
+        """snapshot_state plus the real keys behind the dictionary ids its entries name, as
+        GpuWindowOperator.snapshotState writes them through the key serializer: any
+        operator (another process, another dictionary) restores it."""
+        blob = self.snapshot_state(key_group_range)
+        ids = N.snapshot_keys(blob)
+        return pack_keyed_snapshot(blob, {int(i): self._decode_key(int(i)) for i in ids})
+
+    def _rekey(self, wrapped: bytes) -> bytes:
+        blob, keys = unpack_keyed_snapshot(wrapped)
+        if self._int_keys and all(isinstance(k, int) for k in keys.values()) and not self._keys_out:
+            return N.snapshot_remap_keys(blob, {i: k for i, k in keys.items()})
+        if not self._keys_out:
+            self._int_keys = False
+        return N.snapshot_remap_keys(blob, {i: self._encode_key(k) for i, k in keys.items()})
 
     def pending_rows(self) -> int:
         n = ctypes.c_int64(0)
@@ -660,6 +687,47 @@ class StreamExecutionEnvironment:
     def from_elements(self, elements: Iterable) -> DataStream:
         self.elements = list(elements)
         return DataStream(self)
+
+
+# Keyed snapshot: a gw_snapshot blob plus its key table (id -> key), what the Java operator
+# writes per key group (the blob, then the keys through the key serializer).
+KEYED_MAGIC = b"GWK1"
+
+
+def pack_keyed_snapshot(blob: bytes, keys: dict) -> bytes:
+    out = [KEYED_MAGIC, struct.pack("<qq", len(blob), len(keys)), blob]
+    for kid, key in sorted(keys.items()):
+        if isinstance(key, str):
+            tag, body = b"s", key.encode("utf-8")
+        elif isinstance(key, bool):
+            tag, body = b"z", b"\x01" if key else b"\x00"
+        elif isinstance(key, int):
+            tag, body = b"j", struct.pack("<q", key)
+        else:
+            raise TypeError(f"unsupported key type {type(key).__name__}")
+        out.append(struct.pack("<q", kid) + tag + struct.pack("<i", len(body)) + body)
+    return b"".join(out)
+
+
+def unpack_keyed_snapshot(data: bytes):
+    if data[:4] != KEYED_MAGIC:
+        raise ValueError("not a keyed snapshot")
+    nb, nk = struct.unpack_from("<qq", data, 4)
+    p = 20
+    blob = data[p:p + nb]
+    p += nb
+    keys = {}
+    for _ in range(nk):
+        kid, = struct.unpack_from("<q", data, p)
+        tag = data[p + 8:p + 9]
+        ln, = struct.unpack_from("<i", data, p + 9)
+        body = data[p + 13:p + 13 + ln]
+        p += 13 + ln
+        keys[kid] = body.decode("utf-8") if tag == b"s" else (body == b"\x01" if tag == b"z" else
+                                                               struct.unpack("<q", body)[0])
+    if p != len(data):
+        raise ValueError("trailing bytes in a keyed snapshot")
+    return blob, keys
 
 
 def result_value(bits: int, is_double: bool):

@@ -187,18 +187,29 @@ int  gw_flush(gw_handle* h);
 /* ---- checkpoint / restore ------------------------------------------------ */
 /* Snapshot of the window state of key groups [kg_lo, kg_hi] (buffered records are
  * applied first).  Replaces the keyed-state part of StreamOperator.snapshotState
- * (RS/api/operators/StreamOperator.java:131; heap backend per key group:
- * HeapSnapshotStrategy.java:97-154, CopyOnWriteStateMapSnapshot.writeState :127-149).
- * The blob holds, per key group, (key, pane, accumulator) entries; panes are the
- * operator's slices of width gcd(size, slide), so every aggregate restores exactly.
- * Session windows: the blob (version 2) holds every in-flight session as a
- * (key, start, end, accumulator) entry per key group -- the (key, window) state entries
- * plus the merging window set of the heap backend (MergingWindowSet.java:95-104).
- * Count windows (version 3): per key, the element count and the ring of count-pane
- * accumulators (the CountTrigger count and the evicting operator's window contents).
- * Two calls: buf == NULL returns the size in *len; then a buffer of cap >= *len.
- * Allowed lateness > 0 with tumbling/sliding windows: GW_E_UNSUPPORTED (sessions carry a
- * fired flag per entry and snapshot under lateness). */
+ * (RS/api/operators/StreamOperator.java:131) in the heap backend's per-key-group layout
+ * (HeapSnapshotStrategy.java:97-154).  The blob is a 96-byte header (magic "GWS1",
+ * version, window, aggregate, max parallelism, key-group range, flags), int64
+ * kg_offsets[kg_hi - kg_lo + 2], then per key group:
+ *   version 4 (tumbling / sliding windows, also under allowed lateness and PurgingTrigger;
+ *   big-endian like DataOutputView): be32 n + n "window-contents" entries
+ *   (window.start, window.end, key, [be32 key hash,] state) as
+ *   CopyOnWriteStateMapSnapshot.writeState writes them (:127-149; one entry per (key,
+ *   window) holding state: not fired, or fired and kept until its cleanup time), be32 0
+ *   (no merging window set), be32 t + t event-time timers (flipSignBit(ts), key, start,
+ *   end) as TimerSerializer.serialize writes them (:147-152; the window's maxTimestamp
+ *   and, under lateness, its cleanup time);
+ *   version 2 (session windows): every in-flight session as (key, start, end, a0, a1,
+ *   fired) int64 words -- the (key, window) state plus the merging window set
+ *   (MergingWindowSet.java:95-104);
+ *   version 3 (count windows): per key (key, element count, ring of count-pane
+ *   accumulators): the CountTrigger count and the evicting operator's window contents.
+ * Keys fed with a key_hash column (String, Integer, ... keys as caller ids) are filed
+ * under the key group of that hash (KeyGroupRangeAssignment.java:63-66), and the blob
+ * carries each entry's key hash (header flags bit 0: a be32 after the key in version 4,
+ * one more int64 word per entry in versions 2 and 3).  A window-class composite writes
+ * its classes' entries merged per key group.  Two calls: buf == NULL returns the size in
+ * *len; then a buffer of cap >= *len. */
 int  gw_snapshot(gw_handle* h, int32_t kg_lo, int32_t kg_hi, void* buf, int64_t cap, int64_t* len);
 /* Restore one snapshot blob (call once per key-group range, e.g. after rescaling) into a
  * handle with the same assigner, aggregate and max parallelism
@@ -212,6 +223,16 @@ int  gw_restore(gw_handle* h, const void* buf, int64_t len);
  * blob version.  Two calls as gw_snapshot: out == NULL returns the size in *out_len.
  * GW_E_INVALID for a corrupt blob or kg outside its key-group range (gw_last_error(NULL)). */
 int  gw_snapshot_slice(const void* blob, int64_t len, int32_t kg, void* out, int64_t cap, int64_t* out_len);
+
+/* The distinct keys a blob's entries and timers name, ascending, into keys[cap]; *n gets
+ * their number (keys == NULL: only the count).  With gw_snapshot_remap_keys this is what a
+ * caller that maps its keys to int64 ids (GpuWindowOperator<IN, K> for non-Long K) needs
+ * to write the real keys beside the blob (through the key serializer) and to restore them
+ * under the ids of another process.  Pure host code; GW_E_INVALID for a corrupt blob. */
+int  gw_snapshot_keys(const void* blob, int64_t len, int64_t* keys, int64_t cap, int64_t* n);
+/* Rewrite in place every key of the blob found in from[0..n) (ascending) to the matching
+ * to[i]; key hashes stay.  GW_E_INVALID for a corrupt blob or unsorted from[]. */
+int  gw_snapshot_remap_keys(void* blob, int64_t len, const int64_t* from, const int64_t* to, int64_t n);
 
 /* ---- network-buffer ingest ----------------------------- */
 /* Layout of the record value: a Flink Tuple of fixed-width fields as TupleSerializer

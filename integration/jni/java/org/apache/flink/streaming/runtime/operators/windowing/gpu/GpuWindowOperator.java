@@ -25,6 +25,15 @@
  *                  count, Double for avg), PassThroughWindowFunction.
  *   KEYED_WINDOW   Tuple4 (key, window start, window end, result), what a ProcessWindowFunction
  *                  emitting (key, window, result) produces.
+ *
+ * Keys (K, as WindowOperator<K, ...> at WindowOperator.java:102): Long keys go to the GPU as
+ * they are, and the device computes Long.hashCode.  Any other key type (String, Integer,
+ * POJOs) gets an int64 id from a KeyDictionary, and key.hashCode() travels in the keyHashes
+ * column: key groups, snapshots and rescaling follow the key's own hash
+ * (KeyGroupRangeAssignment.java:63-66), and GW_FLAG_CHECK_KEY_GROUPS verifies every batch
+ * against this subtask's key-group range.  Snapshots write the blob per key group, then each
+ * key its entries name through the key serializer; a restore maps those keys to this
+ * subtask's ids (gw_snapshot_remap_keys) before gw_restore.
  */
 package org.apache.flink.streaming.runtime.operators.windowing.gpu;
 
@@ -52,11 +61,17 @@ import java.nio.ByteBuffer;
 import java.nio.ByteOrder;
 import java.util.ArrayDeque;
 import java.util.ArrayList;
+import java.util.HashMap;
 import java.util.List;
+import java.util.Map;
+
+import org.apache.flink.api.common.typeutils.TypeSerializer;
+import org.apache.flink.core.memory.DataInputViewStreamWrapper;
+import org.apache.flink.core.memory.DataOutputViewStreamWrapper;
 import java.util.function.ToDoubleFunction;
 import java.util.function.ToLongFunction;
 
-public class GpuWindowOperator<IN>
+public class GpuWindowOperator<IN, K>
         extends AbstractStreamOperator<Object>
         implements OneInputStreamOperator<IN, Object>, BoundedOneInput, KeyContextHandler {
 
@@ -70,17 +85,21 @@ public class GpuWindowOperator<IN>
     private final int assigner, trigger, agg;
     private final OutputMode mode;
     private final long size, slide, offset, gap, lateness;
-    private final KeySelector<IN, Long> keySelector;
+    private final KeySelector<IN, K> keySelector;
     private final ToLongFunction<IN> longValue;       // for integer aggregates
     private final ToDoubleFunction<IN> doubleValue;   // for f64 aggregates
     private final int batchCapacity;
     private final int inputArity, positionalField;
 
     private transient long handle;
-    private transient ByteBuffer keys, ts, values, oKey, oStart, oEnd, oRes;
+    private transient ByteBuffer keys, keyHashes, ts, values, oKey, oStart, oEnd, oRes;
     private transient int n;
     private transient List<byte[]> restored;  // per-key-group blobs read in initializeState
-    private OutputTag<Tuple2<Long, Object>> lateDataTag;  // sideOutputLateData (null: count and drop)
+    private transient List<Map<Long, K>> restoredKeys;  // their key tables (non-Long keys)
+    private transient KeyDictionary<K> dict;  // null while every key so far is a Long
+    private transient boolean longKeys;       // decided by the first key
+    private transient boolean keyModeKnown;
+    private OutputTag<Tuple2<Object, Object>> lateDataTag;  // sideOutputLateData (null: count and drop)
     private transient ByteBuffer lKey, lTs, lVal;
     // positional on Tuple3+: payload column (arrival sequence), the elements by sequence, and
     // per batch (sequence end, max timestamp) for releasing them
@@ -92,7 +111,7 @@ public class GpuWindowOperator<IN>
     /** inputArity: fields of the input Tuple; positionalField: the aggregated field of a
      *  POSITIONAL sum/min/max (the result replaces it in the emitted tuple). */
     public GpuWindowOperator(int assigner, long size, long slide, long offset, long gap, long lateness,
-                             int trigger, int agg, KeySelector<IN, Long> keySelector,
+                             int trigger, int agg, KeySelector<IN, K> keySelector,
                              ToLongFunction<IN> longValue, ToDoubleFunction<IN> doubleValue, int batchCapacity,
                              OutputMode mode, int inputArity, int positionalField) {
         if (mode == OutputMode.POSITIONAL && inputArity > 2
@@ -111,7 +130,7 @@ public class GpuWindowOperator<IN>
 
     /** WindowedStream.sideOutputLateData (WindowOperator.java:440-446, 587-588) for a Tuple2<Long, X>
      *  input: skipped late elements come back as (key, value) with their timestamp. */
-    public GpuWindowOperator<IN> withLateDataOutput(OutputTag<Tuple2<Long, Object>> tag) {
+    public GpuWindowOperator<IN, K> withLateDataOutput(OutputTag<Tuple2<Object, Object>> tag) {
         this.lateDataTag = tag;
         return this;
     }
@@ -127,7 +146,8 @@ public class GpuWindowOperator<IN>
         int maxP = getRuntimeContext().getTaskInfo().getMaxNumberOfParallelSubtasks();
         int device = gpuIndex();
         final int flags = (lateDataTag != null ? 64 /* GW_FLAG_LATE_SIDE_OUTPUT */ : 0)
-                | (wide() ? 128 /* GW_FLAG_FIRST_ELEMENT */ : 0);
+                | (wide() ? 128 /* GW_FLAG_FIRST_ELEMENT */ : 0)
+                | (parallelism > 1 ? 4 /* GW_FLAG_CHECK_KEY_GROUPS: a foreign key fails the batch */ : 0);
         handle = nativeCreate(assigner, trigger, size, slide, offset, gap, lateness, agg, maxP, parallelism,
                               subtask, device, flags, 1L << 24, batchCapacity);
         if (lateDataTag != null) { lKey = direct(8); lTs = direct(8); lVal = direct(8); }
@@ -137,12 +157,32 @@ public class GpuWindowOperator<IN>
             batches = new ArrayDeque<>();
             batchMaxTs = Long.MIN_VALUE;
         }
-        keys = direct(8); ts = direct(8); values = direct(8);
+        keys = direct(8); keyHashes = direct(4); ts = direct(8); values = direct(8);
         oKey = direct(8); oStart = direct(8); oEnd = direct(8); oRes = direct(8);
         if (restored != null) {  // initializeState runs before open (StreamOperator.java:139)
-            for (byte[] blob : restored) nativeRestore(handle, blob);
+            for (int i = 0; i < restored.size(); i++) {
+                byte[] blob = restored.get(i);
+                Map<Long, K> table = restoredKeys.get(i);
+                if (table != null) {  // the blob's key ids -> this subtask's dictionary ids
+                    long[] from = nativeSnapshotKeys(blob);
+                    long[] to = new long[from.length];
+                    for (int j = 0; j < from.length; j++) to[j] = dictionary().idOf(table.get(from[j]));
+                    nativeRemapKeys(blob, from, to);
+                }
+                nativeRestore(handle, blob);
+            }
             restored = null;
+            restoredKeys = null;
         }
+    }
+
+    private KeyDictionary<K> dictionary() {
+        if (dict == null) {
+            dict = new KeyDictionary<>();
+            longKeys = false;
+            keyModeKnown = true;
+        }
+        return dict;
     }
 
     /** The GPU this subtask was given: the "index" property of the first "gpu" external
@@ -169,12 +209,23 @@ public class GpuWindowOperator<IN>
         KeyGroupRange range = getKeyedStateBackend().getKeyGroupRange();
         byte[] all = nativeSnapshot(handle, range.getStartKeyGroup(), range.getEndKeyGroup());
         KeyedStateCheckpointOutputStream out = context.getRawKeyedOperatorStateOutput();
+        @SuppressWarnings("unchecked")
+        TypeSerializer<K> keySer = (TypeSerializer<K>) getKeyedStateBackend().getKeySerializer();
         for (int kg : range) {
             out.startNewKeyGroup(kg);
             byte[] part = nativeSliceKeyGroup(all, kg);
             DataOutputStream dos = new DataOutputStream(out);
             dos.writeInt(part.length);
             dos.write(part);
+            // the keys behind the ids, through the key serializer (none for Long keys)
+            long[] ids = dict != null ? nativeSnapshotKeys(part) : new long[0];
+            dos.writeBoolean(dict != null);
+            dos.writeInt(ids.length);
+            DataOutputViewStreamWrapper view = new DataOutputViewStreamWrapper(dos);
+            for (long id : ids) {
+                dos.writeLong(id);
+                keySer.serialize(dict.keyOf(id), view);
+            }
             dos.flush();
         }
     }
@@ -184,11 +235,23 @@ public class GpuWindowOperator<IN>
         super.initializeState(context);
         if (!context.isRestored()) return;
         restored = new ArrayList<>();
+        restoredKeys = new ArrayList<>();
+        @SuppressWarnings("unchecked")
+        TypeSerializer<K> keySer = (TypeSerializer<K>) getKeyedStateBackend().getKeySerializer();
         for (KeyGroupStatePartitionStreamProvider p : context.getRawKeyedStateInputs()) {
             DataInputStream in = new DataInputStream(p.getStream());
             byte[] blob = new byte[in.readInt()];
             in.readFully(blob);
             restored.add(blob);
+            boolean keyed = in.readBoolean();
+            int nk = in.readInt();
+            Map<Long, K> table = keyed ? new HashMap<>() : null;
+            DataInputViewStreamWrapper view = new DataInputViewStreamWrapper(in);
+            for (int j = 0; j < nk; j++) {
+                long id = in.readLong();
+                table.put(id, keySer.deserialize(view));
+            }
+            restoredKeys.add(table);
         }
     }
 
@@ -199,8 +262,17 @@ public class GpuWindowOperator<IN>
     @Override
     public void processElement(StreamRecord<IN> element) throws Exception {
         IN v = element.getValue();
-        Long k = keySelector.getKey(v);
-        keys.putLong(n * 8, k);   // key group = murmur(Long.hashCode(k)), computed on the GPU
+        K k = keySelector.getKey(v);
+        if (!keyModeKnown) {
+            longKeys = k instanceof Long;
+            keyModeKnown = true;
+        }
+        if (longKeys) {
+            keys.putLong(n * 8, (Long) k);   // key group = murmur(Long.hashCode(k)), computed on the GPU
+        } else {
+            keys.putLong(n * 8, dictionary().idOf(k));
+            keyHashes.putInt(n * 4, k.hashCode());  // KeyGroupRangeAssignment.assignToKeyGroup(key, ..)
+        }
         ts.putLong(n * 8, element.getTimestamp());
         if (doubleValue != null) values.putDouble(n * 8, doubleValue.applyAsDouble(v));
         else if (longValue != null) values.putLong(n * 8, longValue.applyAsLong(v));
@@ -226,13 +298,14 @@ public class GpuWindowOperator<IN>
     }
 
     private void flush() {
-        // the key hash column is null: keys are Longs, whose hashCode the GPU computes
+        // Long keys: no key hash column, the GPU computes Long.hashCode; others: ids + hashCode()
+        ByteBuffer kh = longKeys ? null : keyHashes;
         if (n > 0 && wide()) {
-            nativeIngestPayload(handle, n, keys, ts, values, payload);
+            nativeIngestPayload(handle, n, keys, kh, ts, values, payload);
             batches.addLast(new long[] {elements.end(), batchMaxTs});
             batchMaxTs = Long.MIN_VALUE;
         } else if (n > 0) {
-            nativeIngest(handle, n, keys, null, ts, values);
+            nativeIngest(handle, n, keys, kh, ts, values);
         }
         n = 0;
         if (lateDataTag != null) emitLate();
@@ -245,7 +318,8 @@ public class GpuWindowOperator<IN>
         while ((got = wide() ? nativeDrainPayload(handle, oKey, oStart, oEnd, oRes, oPay, batchCapacity)
                              : nativeDrain(handle, oKey, oStart, oEnd, oRes, batchCapacity)) > 0) {
             for (int i = 0; i < got; i++) {
-                long key = oKey.getLong(i * 8), end = oEnd.getLong(i * 8);
+                long end = oEnd.getLong(i * 8);
+                Object key = key(oKey.getLong(i * 8));
                 Object res = agg == 2 || agg >= 5 && agg <= 8 ? (Object) oRes.getDouble(i * 8) : oRes.getLong(i * 8);
                 Object row;
                 switch (mode) {
@@ -263,12 +337,15 @@ public class GpuWindowOperator<IN>
         }
     }
 
+    /** The key of a fired row: the Long itself, or the dictionary's key for an id. */
+    private Object key(long id) { return dict == null ? (Object) id : dict.keyOf(id); }
+
     private void emitLate() {
         int got;
         while ((got = nativeDrainLate(handle, lKey, lTs, lVal, batchCapacity)) > 0) {
             for (int i = 0; i < got; i++) {
                 Object v = doubleValue != null ? (Object) lVal.getDouble(i * 8) : lVal.getLong(i * 8);
-                output.collect(lateDataTag, new StreamRecord<>(Tuple2.of(lKey.getLong(i * 8), v), lTs.getLong(i * 8)));
+                output.collect(lateDataTag, new StreamRecord<>(Tuple2.of(key(lKey.getLong(i * 8)), v), lTs.getLong(i * 8)));
             }
             if (got < batchCapacity) break;
         }
@@ -296,6 +373,24 @@ public class GpuWindowOperator<IN>
             elements.releaseUpTo(b[0]);
             batches.pollFirst();
         }
+    }
+
+    /** Non-Long keys <-> dense int64 ids (the GPU keys), with each key's hashCode. */
+    static final class KeyDictionary<T> {
+        private final HashMap<T, Long> ids = new HashMap<>();
+        private final ArrayList<T> keys = new ArrayList<>();
+
+        long idOf(T key) {
+            Long id = ids.get(key);
+            if (id == null) {
+                id = (long) keys.size();
+                ids.put(key, id);
+                keys.add(key);
+            }
+            return id;
+        }
+
+        T keyOf(long id) { return keys.get((int) id); }
     }
 
     /** Elements by arrival sequence, a growable ring: append at the end, release from the start. */
@@ -346,8 +441,8 @@ public class GpuWindowOperator<IN>
     private static native long nativeAdvanceWatermark(long h, long wm);
     private static native int nativeDrain(long h, ByteBuffer key, ByteBuffer start, ByteBuffer end, ByteBuffer result,
                                           int cap);
-    private static native void nativeIngestPayload(long h, int n, ByteBuffer keys, ByteBuffer ts, ByteBuffer values,
-                                                   ByteBuffer payload);
+    private static native void nativeIngestPayload(long h, int n, ByteBuffer keys, ByteBuffer keyHashes, ByteBuffer ts,
+                                                   ByteBuffer values, ByteBuffer payload);
     private static native int nativeDrainPayload(long h, ByteBuffer key, ByteBuffer start, ByteBuffer end,
                                                  ByteBuffer result, ByteBuffer payload, int cap);
     private static native long nativeLateDropped(long h);
@@ -356,7 +451,11 @@ public class GpuWindowOperator<IN>
     private static native byte[] nativeSnapshot(long h, int kgLo, int kgHi);
     private static native byte[] nativeSliceKeyGroup(byte[] blob, int kg);
     private static native void nativeRestore(long h, byte[] blob);
+    private static native long[] nativeSnapshotKeys(byte[] blob);
+    private static native void nativeRemapKeys(byte[] blob, long[] from, long[] to);
     private static native int nativeDrainLate(long h, ByteBuffer key, ByteBuffer ts, ByteBuffer value, int cap);
-    /** The keyBy exchange's receive columns (GpuKeyByExchange.batch) straight into the operator. */
-    static native void nativeIngestDevice(long h, long n, long keyPtr, long hashPtr, long tsPtr, long valuePtr);
+    /** The keyBy exchange's receive columns (GpuKeyByExchange.batch, produced on `stream`)
+     *  straight into the operator. */
+    static native void nativeIngestDevice(long h, long n, long keyPtr, long hashPtr, long tsPtr, long valuePtr,
+                                          long stream);
 }

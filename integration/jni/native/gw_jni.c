@@ -88,10 +88,11 @@ JNIEXPORT jint JNICALL CLS(nativeDrain)(JNIEnv* env, jclass c, jlong h, jobject 
 
 /* Positional sum/min/max on Tuple3+ (GW_FLAG_FIRST_ELEMENT): the batch with a payload column
  * (the operator's arrival sequence of each element) ... */
-JNIEXPORT void JNICALL CLS(nativeIngestPayload)(JNIEnv* env, jclass c, jlong h, jint n, jobject keys, jobject ts,
-                                                jobject values, jobject payload) {
+JNIEXPORT void JNICALL CLS(nativeIngestPayload)(JNIEnv* env, jclass c, jlong h, jint n, jobject keys,
+                                                jobject keyHashes, jobject ts, jobject values, jobject payload) {
     gw_handle* g = (gw_handle*)(intptr_t)h;
-    fail(env, g, gw_ingest_payload(g, n, (*env)->GetDirectBufferAddress(env, keys), 0,
+    fail(env, g, gw_ingest_payload(g, n, (*env)->GetDirectBufferAddress(env, keys),
+                                   keyHashes ? (*env)->GetDirectBufferAddress(env, keyHashes) : 0,
                                    (*env)->GetDirectBufferAddress(env, ts), (*env)->GetDirectBufferAddress(env, values),
                                    (*env)->GetDirectBufferAddress(env, payload)));
 }
@@ -170,12 +171,53 @@ JNIEXPORT void JNICALL CLS(nativeRestore)(JNIEnv* env, jclass c, jlong h, jbyteA
 }
 
 /* Device-resident ingest (gw_ingest_device): the columns the keyBy exchange delivered
- * (GpuKeyByExchange.batch), as raw device addresses; 0 = absent column. */
+ * (GpuKeyByExchange.batch), as raw device addresses; 0 = absent column.  `stream` is the
+ * stream that produced them (the exchange's): the handle's stream waits for it before
+ * reading, and it waits for those reads before the exchange reuses the receive set. */
 JNIEXPORT void JNICALL CLS(nativeIngestDevice)(JNIEnv* env, jclass c, jlong h, jlong n, jlong keyPtr, jlong hashPtr,
-                                               jlong tsPtr, jlong valuePtr) {
+                                               jlong tsPtr, jlong valuePtr, jlong stream) {
     gw_handle* g = (gw_handle*)(intptr_t)h;
     fail(env, g, gw_ingest_device(g, n, (const int64_t*)(intptr_t)keyPtr, (const int32_t*)(intptr_t)hashPtr,
-                                  (const int64_t*)(intptr_t)tsPtr, (const void*)(intptr_t)valuePtr, gw_stream(g)));
+                                  (const int64_t*)(intptr_t)tsPtr, (const void*)(intptr_t)valuePtr,
+                                  (void*)(intptr_t)stream));
+}
+
+/* The key ids a key group's blob names (gw_snapshot_keys): snapshotState writes the real key
+ * of each through the key serializer after the blob. */
+JNIEXPORT jlongArray JNICALL CLS(nativeSnapshotKeys)(JNIEnv* env, jclass c, jbyteArray blob) {
+    jsize len = (*env)->GetArrayLength(env, blob);
+    jbyte* b = (*env)->GetByteArrayElements(env, blob, 0);
+    int64_t n = 0;
+    int rc = gw_snapshot_keys(b, len, 0, 0, &n);
+    jlongArray out = 0;
+    if (rc == GW_OK) {
+        int64_t* tmp = (int64_t*)malloc((size_t)(n > 0 ? n : 1) * 8);
+        rc = tmp ? gw_snapshot_keys(b, len, tmp, n, &n) : GW_E_OOM;
+        if (rc == GW_OK) {
+            out = (*env)->NewLongArray(env, (jsize)n);
+            (*env)->SetLongArrayRegion(env, out, 0, (jsize)n, (const jlong*)tmp);
+        }
+        free(tmp);
+    }
+    (*env)->ReleaseByteArrayElements(env, blob, b, JNI_ABORT);
+    fail(env, 0, rc);
+    return out;
+}
+
+/* initializeState: the restored blob's key ids -> this subtask's ids (ascending `from`),
+ * rewritten in place (gw_snapshot_remap_keys). */
+JNIEXPORT void JNICALL CLS(nativeRemapKeys)(JNIEnv* env, jclass c, jbyteArray blob, jlongArray from, jlongArray to) {
+    jsize len = (*env)->GetArrayLength(env, blob);
+    jsize n = (*env)->GetArrayLength(env, from);
+    jbyte* b = (*env)->GetByteArrayElements(env, blob, 0);
+    jlong* f = (*env)->GetLongArrayElements(env, from, 0);
+    jlong* t = (*env)->GetLongArrayElements(env, to, 0);
+    int rc = (*env)->GetArrayLength(env, to) == n ? gw_snapshot_remap_keys(b, len, (const int64_t*)f, (const int64_t*)t, n)
+                                                   : GW_E_INVALID;
+    (*env)->ReleaseLongArrayElements(env, to, t, JNI_ABORT);
+    (*env)->ReleaseLongArrayElements(env, from, f, JNI_ABORT);
+    (*env)->ReleaseByteArrayElements(env, blob, b, rc == GW_OK ? 0 : JNI_ABORT);  /* 0: copy back */
+    fail(env, 0, rc);
 }
 
 /* sideOutputLateData: up to cap late records into direct buffers (key, timestamp, value);

@@ -395,6 +395,7 @@ struct wo_op {
     int64_t *lk, *lt, *lv;  /* late side output (GW_FLAG_LATE_SIDE_OUTPUT): the elements themselves */
     int64_t ln, lcap;
     map_t cmap;   /* count windows: (key,0,0,0) -> index into cws */
+    map_t khash;  /* (key,0,0,0) -> key.hashCode() of keys given a hash (wo_set_key_hashes) */
     struct cw_s* cws;
     int64_t ncws, cap_cws;
     char err[256];
@@ -969,7 +970,7 @@ wo_op* wo_create(const gw_config* cfg) {
     op->c = *cfg;
     op->wm = INT64_MIN;
     if (map_init(&op->state, 1024) || map_init(&op->timers, 1024) || map_init(&op->sets, 256) ||
-        map_init(&op->cmap, 1024)) {
+        map_init(&op->cmap, 1024) || map_init(&op->khash, 64)) {
         wo_destroy(op);
         return NULL;
     }
@@ -982,6 +983,7 @@ void wo_destroy(wo_op* op) {
     map_free(&op->timers);
     map_free(&op->sets);
     map_free(&op->cmap);
+    map_free(&op->khash);
     for (int64_t i = 0; i < op->ncws; i++) free(op->cws[i].v);
     free(op->cws);
     for (int64_t i = 0; i < op->nsets; i++) free(op->msets[i].w);
@@ -1110,8 +1112,29 @@ static int cmp_snap_ent(const void* a, const void* b) {
         if (xs[i] != ys[i]) return xs[i] < ys[i] ? -1 : 1;
     return 0;
 }
+/* The key's Java hashCode: the one given with wo_set_key_hashes (the caller's key ids stand
+ * for String / Integer / ... keys), else Long.hashCode. */
+static int32_t key_hash_of(const wo_op* op, int64_t key) {
+    if (op->khash.n) {
+        const int64_t k[4] = {key, 0, 0, 0};
+        const ment_t* m = map_find(&op->khash, k);
+        if (m) return (int32_t)m->v;
+    }
+    return wo_long_hash(key);
+}
 static int32_t key_group_of(const wo_op* op, int64_t key) {
-    return wo_assign_to_key_group(wo_long_hash(key), op->c.max_parallelism > 0 ? op->c.max_parallelism : 128);
+    return wo_assign_to_key_group(key_hash_of(op, key), op->c.max_parallelism > 0 ? op->c.max_parallelism : 128);
+}
+
+int wo_set_key_hashes(wo_op* op, int64_t n, const int64_t* key, const int32_t* hash) {
+    for (int64_t i = 0; i < n; i++) {
+        const int64_t k[4] = {key[i], 0, 0, 0};
+        int created = 0;
+        ment_t* m = map_upsert(&op->khash, k, hash[i], &created);
+        if (!m) return GW_E_OOM;
+        if (!created && m->v != hash[i]) { op_err(op, "a key with two different key hashes"); return GW_E_INVALID; }
+    }
+    return GW_OK;
 }
 
 /* Returns the blob size; writes it when buf holds >= that many bytes. Negative on error. */
@@ -1119,6 +1142,7 @@ int64_t wo_snapshot(wo_op* op, int32_t kg_lo, int32_t kg_hi, uint8_t* buf, int64
     if (op->c.assigner == GW_COUNT_TUMBLING || op->c.assigner == GW_COUNT_SLIDING) return GW_E_UNSUPPORTED;
     if (kg_lo < 0 || kg_hi < kg_lo) return GW_E_INVALID;
     const int nk = kg_hi - kg_lo + 1;
+    const int hashed = op->khash.n > 0; /* header flags bit 0: entries carry the key hash */
     /* gather (key group, sort key) for state entries, timers and merging sets */
     int64_t ns = 0, nt = 0, nm = 0;
     snap_ent* se = (snap_ent*)malloc(sizeof(snap_ent) * (size_t)(op->state.n + 1));
@@ -1161,8 +1185,9 @@ int64_t wo_snapshot(wo_op* op, int32_t kg_lo, int32_t kg_hi, uint8_t* buf, int64
         while (t1 < nt && te[t1].kg == kg) t1++;
         while (q1 < nm && me[q1].kg == kg) q1++;
         wb_be32(&b, (int32_t)(a1 - a));
-        for (; a < a1; a++) { /* namespace, key, state */
+        for (; a < a1; a++) { /* namespace, key, [key hash,] state */
             wb_be64(&b, se[a].k1); wb_be64(&b, se[a].k2); wb_be64(&b, se[a].k0);
+            if (hashed) wb_be32(&b, key_hash_of(op, se[a].k0));
             wb_acc(&b, op->c.agg, &op->accs[se[a].v]);
         }
         wb_be32(&b, (int32_t)(q1 - q));
@@ -1196,7 +1221,7 @@ int64_t wo_snapshot(wo_op* op, int32_t kg_lo, int32_t kg_hi, uint8_t* buf, int64
         const uint32_t ver = 4;
         const int64_t slide = op->c.assigner == GW_TUMBLING ? op->c.size : op->c.slide;
         const int32_t i32s[2] = {op->c.agg, op->c.assigner};
-        const int64_t i64s[5] = {op->c.size, slide, op->c.offset, op->c.gap, 0};
+        const int64_t i64s[5] = {op->c.size, slide, op->c.offset, op->c.gap, hashed ? 1 : 0};
         const int32_t mp = op->c.max_parallelism > 0 ? op->c.max_parallelism : 128;
         const int32_t i32b[4] = {mp, kg_lo, kg_hi, 0};
         const int64_t tail[3] = {0, 0, offs[nk]};
@@ -1229,20 +1254,26 @@ int wo_restore(wo_op* op, const uint8_t* buf, int64_t len) {
     }
     const int nk = i32b[2] - i32b[1] + 1;
     const int64_t pay0 = 96 + (int64_t)(nk + 1) * 8;
-    if (nk <= 0 || tail[2] < 0 || len < pay0 + tail[2]) { op_err(op, "truncated snapshot blob"); return GW_E_INVALID; }
+    if (nk <= 0 || tail[2] < 0 || len < pay0 || tail[2] > len - pay0) { op_err(op, "truncated snapshot blob"); return GW_E_INVALID; }
     const uint8_t* p = buf + pay0;
     const uint8_t* end = p + tail[2];
     const int ab = wo_acc_bytes(op->c.agg);
-#define NEED(x) do { if (p + (x) > end) { op_err(op, "truncated snapshot blob"); return GW_E_INVALID; } } while (0)
+    const int hb = (i64s[4] & 1) ? 4 : 0;
+#define NEED(x) do { if ((int64_t)(x) > end - p) { op_err(op, "truncated snapshot blob"); return GW_E_INVALID; } } while (0)
     for (int g = 0; g < nk; g++) {
         NEED(4);
         int32_t n = rd_be32(p); p += 4;
         for (int32_t i = 0; i < n; i++) {
-            NEED(24 + ab);
+            NEED(24 + hb + ab);
             int64_t s = rd_be64(p), e = rd_be64(p + 8), key = rd_be64(p + 16);
+            if (hb) {
+                const int32_t kh = rd_be32(p + 24);
+                const int rc = wo_set_key_hashes(op, 1, &key, &kh);
+                if (rc) return rc;
+            }
             acc_t a;
-            rd_acc(p + 24, op->c.agg, &a);
-            p += 24 + ab;
+            rd_acc(p + 24 + hb, op->c.agg, &a);
+            p += 24 + hb + ab;
             int64_t k[4] = {key, s, e, 0};
             int created = 0;
             ment_t* m = map_upsert(&op->state, k, -1, &created);

@@ -52,6 +52,9 @@ int     wo_process_element(wo_op* op, int64_t key, int64_t ts, int64_t value_bit
 int     wo_process_batch(wo_op* op, int64_t n, const int64_t* key, const int64_t* ts,
                          const int64_t* value_bits);
 int     wo_process_watermark(wo_op* op, int64_t wm);
+/* key.hashCode() of keys the caller maps to int64 ids (String, Integer, ... keys): their key
+ * group, and the key hash a snapshot entry carries, follow it (default Long.hashCode). */
+int     wo_set_key_hashes(wo_op* op, int64_t n, const int64_t* key, const int32_t* hash);
 int64_t wo_output_count(const wo_op* op);
 /* Copies and removes up to cap rows. result is 8 bytes per row (int64 or double). */
 int64_t wo_drain(wo_op* op, int64_t* key, int64_t* start, int64_t* end, int64_t* result_bits,

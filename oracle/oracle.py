@@ -123,6 +123,7 @@ def lib() -> ctypes.CDLL:
             ("wo_process_element", ctypes.c_int, [p, i64, i64, i64]),
             ("wo_process_batch", ctypes.c_int, [p, i64, p, p, p]),
             ("wo_process_watermark", ctypes.c_int, [p, i64]),
+            ("wo_set_key_hashes", ctypes.c_int, [p, i64, p, p]),
             ("wo_output_count", i64, [p]), ("wo_drain", i64, [p, p, p, p, p, i64]),
             ("wo_late_dropped", i64, [p]), ("wo_late_output_count", i64, [p]),
             ("wo_drain_late", i64, [p, p, p, p, i64]), ("wo_current_watermark", i64, [p]),
@@ -189,6 +190,13 @@ class OracleOperator:
 
     def process_watermark(self, wm: int):
         self._check(lib().wo_process_watermark(self._h, wm))
+
+    def set_key_hashes(self, key: np.ndarray, hashes: np.ndarray):
+        """key.hashCode() of caller key ids (String / Integer / ... keys): key groups and the
+        snapshot's key hashes follow it."""
+        key = np.ascontiguousarray(key, dtype=np.int64)
+        hashes = np.ascontiguousarray(hashes, dtype=np.int32)
+        self._check(lib().wo_set_key_hashes(self._h, len(key), _p(key), _p(hashes)))
 
     def drain(self):
         n = lib().wo_output_count(self._h)

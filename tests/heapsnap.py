@@ -10,11 +10,12 @@ ACC_BYTES = {"sum_i32": 4, "avg_i64": 16, "avg_f64": 16}
 
 
 def parse(blob: bytes, agg: str):
-    """-> dict kg -> {"state": [(start, end, key, acc...)], "sets": [(key, ((w, sw), ...))],
+    """-> dict kg -> {"state": [(start, end, key, acc..., [key hash])], "sets": [(key, ((w, sw), ...))],
     "timers": [(ts, key, start, end)]}; acc as raw big-endian ints (doubles by their bits)."""
     h = HDR.unpack(blob[:96])
     assert h[0] == b"GWS1" and h[1] == 4, h[:2]
     kg_lo, kg_hi, nbytes = h[10], h[11], h[15]
+    hb = 4 if h[8] & 1 else 0  # flags: entries carry the key's hash after the key
     nk = kg_hi - kg_lo + 1
     offs = struct.unpack(f"<{nk + 1}q", blob[96:96 + 8 * (nk + 1)])
     pay = blob[96 + 8 * (nk + 1):]
@@ -27,8 +28,10 @@ def parse(blob: bytes, agg: str):
         state = []
         for _ in range(n):
             s, e, k = struct.unpack_from(">qqq", pay, p); p += 24
+            kh = struct.unpack_from(">i", pay, p) if hb else ()
+            p += hb
             acc = struct.unpack_from(">i" if ab == 4 else (">qq" if ab == 16 else ">q"), pay, p); p += ab
-            state.append((s, e, k) + acc)
+            state.append((s, e, k) + acc + kh)
         m, = struct.unpack_from(">i", pay, p); p += 4
         sets = []
         for _ in range(m):

@@ -36,8 +36,24 @@ static void f_set_region(JNIEnv* e, jbyteArray a, jsize s, jsize n, const jbyte*
     memcpy(((fake_bytes*)a)->data + s, src, (size_t)n);
 }
 
+/* long[]: the same length-first layout, so GetArrayLength serves both */
+typedef struct { jsize len; jlong data[]; } fake_longs;
+static jlong* f_longs(JNIEnv* e, jlongArray a, jboolean* c) { (void)e; if (c) *c = 0; return ((fake_longs*)a)->data; }
+static void f_rel_longs(JNIEnv* e, jlongArray a, jlong* p, jint m) { (void)e; (void)a; (void)p; (void)m; }
+static jlongArray f_new_longs(JNIEnv* e, jsize n) {
+    (void)e;
+    fake_longs* b = (fake_longs*)calloc(1, sizeof(fake_longs) + (size_t)n * 8);
+    b->len = n;
+    return (jlongArray)b;
+}
+static void f_set_longs(JNIEnv* e, jlongArray a, jsize s, jsize n, const jlong* src) {
+    (void)e;
+    memcpy(((fake_longs*)a)->data + s, src, (size_t)n * 8);
+}
+
 static const struct JNINativeInterface_ g_table = {f_find_class, f_throw_new, f_direct, f_utf, f_rel_utf,
-                                                   f_len, f_bytes, f_rel_bytes, f_new_bytes, f_set_region};
+                                                   f_len, f_bytes, f_rel_bytes, f_new_bytes, f_set_region,
+                                                   f_longs, f_rel_longs, f_new_longs, f_set_longs};
 static JNIEnv g_env = &g_table;
 
 JNIEnv* fake_env(void) { return &g_env; }
@@ -58,3 +74,9 @@ int fake_exception(char* cls, char* msg, int cap) {
     g_exc = 0;
     return had;
 }
+jlongArray fake_longs_new(const jlong* data, jsize n) {
+    jlongArray a = f_new_longs(&g_env, n);
+    memcpy(((fake_longs*)a)->data, data, (size_t)n * 8);
+    return a;
+}
+const jlong* fake_longs_data(jlongArray a) { return ((fake_longs*)a)->data; }

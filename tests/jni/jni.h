@@ -15,6 +15,7 @@ typedef jobject jclass;
 typedef jobject jstring;
 typedef jobject jarray;
 typedef jarray jbyteArray;
+typedef jarray jlongArray;
 #define JNIEXPORT __attribute__((visibility("default")))
 #define JNICALL
 #define JNI_ABORT 2
@@ -31,5 +32,9 @@ struct JNINativeInterface_ {
     void (*ReleaseByteArrayElements)(JNIEnv* env, jbyteArray array, jbyte* elems, jint mode);
     jbyteArray (*NewByteArray)(JNIEnv* env, jsize len);
     void (*SetByteArrayRegion)(JNIEnv* env, jbyteArray array, jsize start, jsize len, const jbyte* buf);
+    jlong* (*GetLongArrayElements)(JNIEnv* env, jlongArray array, jboolean* isCopy);
+    void (*ReleaseLongArrayElements)(JNIEnv* env, jlongArray array, jlong* elems, jint mode);
+    jlongArray (*NewLongArray)(JNIEnv* env, jsize len);
+    void (*SetLongArrayRegion)(JNIEnv* env, jlongArray array, jsize start, jsize len, const jlong* buf);
 };
 #endif

@@ -9,6 +9,7 @@ from flink_amd import _native as N
 from flink_amd import windowing as W
 from tests.dist_worker import owners
 from tests.gpu_helpers import compare, gpu_operator, random_stream, run_oracle
+from tests.heapsnap import parse
 
 pytestmark = pytest.mark.gpu
 
@@ -328,21 +329,26 @@ def test_restore_from_per_key_group_slices(oracle_lib, kw):
     assert compare(outs, o, agg == "avg_f64") == []
 
 
-def test_foreign_key_hash_refuses_snapshot_and_key_group_check():
-    """A key_hash column that differs from Long.hashCode(key) marks the handle (its state is
-    grouped by Long.hashCode, so it cannot snapshot); GW_FLAG_CHECK_KEY_GROUPS fails a batch
-    holding a key of another subtask (StateTable.getMapForKeyGroup, StateTable.java:325-333)."""
+def test_foreign_key_hash_files_state_by_that_hash_and_key_group_check():
+    """A key_hash column (keys as caller ids for String / Integer / ... keys) files each
+    key's state under the key group of that hash (KeyGroupRangeAssignment.java:63-66) and the
+    blob carries it; a key arriving with a second, different hash fails the handle;
+    GW_FLAG_CHECK_KEY_GROUPS fails a batch holding a key of another subtask
+    (StateTable.getMapForKeyGroup, StateTable.java:325-333)."""
     keys = np.arange(100, dtype=np.int64)
     ts = np.arange(100, dtype=np.int64)
     ones = np.ones(100, np.int64)
     op = gpu_operator(dict(assigner="tumbling", size=50, slide=50, agg="sum_i64"))
     lh = np.array([N.lib().gw_java_long_hash(int(k)) for k in keys], np.int32)
-    op.process_batch(keys, ts, ones, key_hashes=lh)  # Long.hashCode: fine
-    op.snapshot_state()
-    op.process_batch(keys, ts, ones, key_hashes=lh + 1)
+    fh = lh * 7 + 1  # not Long.hashCode
+    op.process_batch(keys, ts, ones, key_hashes=fh)
+    got = parse(op.snapshot_state(), "sum_i64")
+    for kg, sec in got.items():
+        for s_, e_, k, acc, kh in sec["state"]:
+            assert kh == fh[k] and N.lib().gw_key_group_for_hash(int(kh), 128) == kg
     with pytest.raises(N.GpuWinError) as ei:
-        op.snapshot_state()
-    assert ei.value.code == -2
+        op.process_batch(keys, ts, ones, key_hashes=fh + 1)
+    assert ei.value.code == -1 and "two different key hashes" in str(ei.value)
     op.close()
     kgr = W.compute_key_group_range_for_operator_index(128, 2, 0)
     mine = np.array([k for k in range(1000) if kgr[0] <= W.assign_to_key_group(k, 128) <= kgr[1]][:50], np.int64)

@@ -104,7 +104,7 @@ def _payload_fns(jni):
     p, i32, i64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64
     ing = getattr(jni, CLS + "nativeIngestPayload")
     ing.restype = None
-    ing.argtypes = [p, p, i64, i32, p, p, p, p]
+    ing.argtypes = [p, p, i64, i32, p, p, p, p, p]
     dr = getattr(jni, CLS + "nativeDrainPayload")
     dr.restype = i32
     dr.argtypes = [p, p, i64, p, p, p, p, p, i32]
@@ -119,7 +119,7 @@ def test_payload_glue_null_handle(jni):
     ing, _, _ = _payload_fns(jni)
     env = jni.fake_env()
     col = np.zeros(4, np.int64)
-    ing(env, None, 0, 4, col.ctypes.data, col.ctypes.data, col.ctypes.data, col.ctypes.data)
+    ing(env, None, 0, 4, col.ctypes.data, None, col.ctypes.data, col.ctypes.data, col.ctypes.data)
     exc = exception(jni)
     assert exc is not None and exc[0] == "java/lang/IllegalArgumentException"
 
@@ -141,7 +141,7 @@ def test_payload_glue_positional_rows(jni):
     vals = rng.integers(-1000, 1000, n).astype(np.int64)
     seq = np.arange(n, dtype=np.int64)
     try:
-        ing(env, None, h, n, keys.ctypes.data, ts.ctypes.data, vals.ctypes.data, seq.ctypes.data)
+        ing(env, None, h, n, keys.ctypes.data, None, ts.ctypes.data, vals.ctypes.data, seq.ctypes.data)
         assert exception(jni) is None
         fired = adv(env, None, h, (1 << 63) - 1)
         assert exception(jni) is None
@@ -175,3 +175,105 @@ def test_java_natives_have_jni_entry_points():
         assert natives, cls
         defined = set(re.findall(macro + r"\((native\w+)\)", csrc))
         assert natives <= defined, f"{cls}: no JNI function for {sorted(natives - defined)}"
+
+
+def _key_fns(jni):
+    p = ctypes.c_void_p
+    ks = getattr(jni, CLS + "nativeSnapshotKeys")
+    ks.restype = p
+    ks.argtypes = [p, p, p]
+    rm = getattr(jni, CLS + "nativeRemapKeys")
+    rm.restype = None
+    rm.argtypes = [p, p, p, p, p]
+    jni.fake_longs_new.restype = p
+    jni.fake_longs_new.argtypes = [p, ctypes.c_int32]
+    jni.fake_longs_data.restype = p
+    jni.fake_longs_data.argtypes = [p]
+    return ks, rm
+
+
+def test_key_table_glue_on_a_reference_snapshot(jni):
+    """snapshotState's key table and initializeState's remap through the glue, on the
+    reference's own reduce-event-time snapshot (String keys, tests/refsnap.py)."""
+    from flink_amd.windowing import java_string_hash
+    from tests import heapsnap, refsnap
+    ks, rm = _key_fns(jni)
+    ref = refsnap.parse(open(refsnap.migration_fixtures()["2.1"], "rb").read())
+    blob = refsnap.to_gpuwin_blob(ref, {"key1": 0, "key2": 1}, java_string_hash, N.AGGS["sum_i32"],
+                                  N.ASSIGNERS["tumbling"], 3000, 3000)
+    env = jni.fake_env()
+    arr = jni.fake_bytes_new(blob, len(blob))
+    ids = ks(env, None, arr)
+    assert exception(jni) is None and jni.fake_bytes_len(ids) == 2
+    assert list(np.ctypeslib.as_array(ctypes.cast(jni.fake_longs_data(ids), ctypes.POINTER(ctypes.c_int64)),
+                                      (2,))) == [0, 1]
+    frm = np.array([0, 1], np.int64)
+    to = np.array([41, 7], np.int64)
+    fa, ta = jni.fake_longs_new(frm.ctypes.data, 2), jni.fake_longs_new(to.ctypes.data, 2)
+    rm(env, None, arr, fa, ta)
+    assert exception(jni) is None
+    moved = ctypes.string_at(jni.fake_bytes_data(arr), len(blob))
+    st = heapsnap.parse(moved, "sum_i32")[0]["state"]
+    assert sorted(k for _, _, k, _, _ in st) == [7, 7, 41]
+    # from[] not ascending: IllegalArgumentException
+    rm(env, None, arr, ta, fa)
+    exc = exception(jni)
+    assert exc is not None and exc[0] == "java/lang/IllegalArgumentException"
+    for a in (arr, ids, fa, ta):
+        jni.fake_bytes_free(a)
+
+
+@pytest.mark.gpu
+def test_ingest_glue_with_key_hashes(jni):
+    """nativeIngest with a keyHashes column (String keys as dictionary ids, as the Java operator
+    passes them): state is filed under the key group of String.hashCode -- the snapshot blob
+    carries the hashes -- and with GW_FLAG_CHECK_KEY_GROUPS a subtask rejects a foreign key."""
+    from flink_amd.windowing import assign_to_key_group, java_string_hash, compute_key_group_range_for_operator_index
+    from tests import heapsnap
+    p, i32, i64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64
+    ing = getattr(jni, CLS + "nativeIngest")
+    ing.restype = None
+    ing.argtypes = [p, p, i64, i32, p, p, p, p]
+    adv = getattr(jni, CLS + "nativeAdvanceWatermark")
+    adv.restype = i64
+    adv.argtypes = [p, p, i64, i64]
+    snap = getattr(jni, CLS + "nativeSnapshot")
+    snap.restype = p
+    snap.argtypes = [p, p, i64, i32, i32]
+    create = getattr(jni, CLS + "nativeCreate")
+    env = jni.fake_env()
+    words = [f"word{i}" for i in range(300)]
+    lo, hi = compute_key_group_range_for_operator_index(128, 2, 1)
+    mine = [w for w in words if lo <= assign_to_key_group(w, 128) <= hi]
+    other = [w for w in words if not lo <= assign_to_key_group(w, 128) <= hi]
+    h = create(env, None, 0, 0, 1000, 0, 0, 0, 0, 1, 128, 2, 1, 0, N.FLAG_CHECK_KEY_GROUPS, 1 << 12, 1 << 16)
+    assert h and exception(jni) is None
+    try:
+        n = 4000
+        rng = np.random.default_rng(8)
+        sel = rng.integers(0, len(mine), n)
+        keys = sel.astype(np.int64)
+        hashes = np.array([java_string_hash(mine[i]) for i in sel], np.int32)
+        ts = rng.integers(0, 1500, n).astype(np.int64)
+        vals = rng.integers(-50, 50, n).astype(np.int64)
+        ing(env, None, h, n, keys.ctypes.data, hashes.ctypes.data, ts.ctypes.data, vals.ctypes.data)
+        assert exception(jni) is None
+        blob_arr = snap(env, None, h, lo, hi)
+        assert exception(jni) is None
+        blob = ctypes.string_at(jni.fake_bytes_data(blob_arr), jni.fake_bytes_len(blob_arr))
+        jni.fake_bytes_free(blob_arr)
+        parsed = heapsnap.parse(blob, "sum_i64")
+        seen = 0
+        for kg, sec in parsed.items():
+            for s, e, k, acc, kh in sec["state"]:
+                assert kh == java_string_hash(mine[k]) and assign_to_key_group(mine[k], 128) == kg
+                seen += 1
+        assert seen > 0
+        # a key of the other subtask: the batch fails (IllegalArgumentException text of the reference)
+        bad = np.array([0], np.int64)
+        bh = np.array([java_string_hash(other[0])], np.int32)
+        ing(env, None, h, 1, bad.ctypes.data, bh.ctypes.data, ts.ctypes.data, vals.ctypes.data)
+        exc = exception(jni)
+        assert exc is not None and "is not in KeyGroupRange" in exc[1]
+    finally:
+        getattr(jni, CLS + "nativeDestroy")(env, None, ctypes.c_int64(h))
