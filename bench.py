@@ -66,7 +66,7 @@ def parse():
     ap.add_argument("--disorder-ms", type=int, default=100)
     ap.add_argument("--exchange", choices=["a2a", "none"], default="a2a",
                     help="a2a: RCCL all-to-all keyBy exchange; none: each rank generates only its own key groups")
-    ap.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu-baseline-seconds", type=float, default=20.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-host-fed", action="store_true",
                     help="skip the host-fed leg (gw_ingest from host columns: pinned staging + H2D)")
@@ -166,7 +166,15 @@ def main():
     cur = side.cuda_stream
 
     ex = None
-    if world > 1:
+    native_ex = False
+    if world > 1 and args.exchange == "a2a" and args.dist_backend == "nccl":
+        # the product path: libgpuwin's own RCCL exchange (gw_exchange_*), what a JVM task
+        # drives; torch.distributed only ships its communicator id and times the run
+        from flink_amd.exchange import NativeKeyByExchange
+        ex = NativeKeyByExchange(world, rank, max_parallelism=maxp, device=local)
+        native_ex = True
+    elif world > 1:
+        # gloo rehearsal (several ranks may share one GPU): the torch.distributed exchange
         from flink_amd.exchange import KeyByExchange
         ex = KeyByExchange(world, rank, max_parallelism=maxp, device=dev)
 
@@ -182,7 +190,7 @@ def main():
     # batch b writes set b%2 once the ingest of batch b-2 has read it (ev_read), and the
     # ingest orders itself through a hand-off stream that nothing else uses, so the
     # exchange stream never waits for the ingest of the batch just before it.
-    overlap = exchanged and args.overlap == "on" and args.producer_stream != "handle"
+    overlap = exchanged and not native_ex and args.overlap == "on" and args.producer_stream != "handle"
     if overlap:
         cap = nb * 2  # received records per step: ~nb for uniform keys (max_batch above)
         ncols = 3 if vals is not None else 2
@@ -198,9 +206,22 @@ def main():
             return step_on_side(b, timed)
 
     def step_on_side(b, timed):
-        nonlocal exch_bytes
+        nonlocal exch_bytes, rows_sum
         lo, hi = b * nb, (b + 1) * nb
         k, t, v = keys[lo:hi], ts[lo:hi], (vals[lo:hi] if vals is not None else None)
+        if native_ex:
+            # partition + one all-to-all of (count, watermark, columns) + one host wait +
+            # grouped send/receive, all on `cur`; the ingest orders through the receive set's
+            # hand-off stream, so the next batch's exchange overlaps this batch's aggregation
+            n, pk, pt, pv, _, wmin, ist = ex.exchange(k, t, v, stream=cur, wm=wms[b])
+            if timed:
+                exch_bytes += (nb - int(ex.counts()[0][rank])) * b_in
+            N.check(N.lib().gw_ingest_device(op.handle, n, pk, None, pt, pv, ist), op.handle)
+            op.advance_watermark(wmin)
+            if args.checksum:
+                rows_sum = (rows_sum + rows_checksum(op.drain())) % (1 << 56)
+            op.clear_rows()  # DiscardingSink
+            return None
         if ex is not None and args.exchange == "a2a":
             pk, pt, pv, counts = ex.partition(k, t, v, stream=cur)
             if overlap:
@@ -222,7 +243,6 @@ def main():
             wm = ex.combine_watermark(wm)  # StatusWatermarkValve: min over inputs
         op.advance_watermark(wm)
         if args.checksum:
-            nonlocal rows_sum
             rows_sum = (rows_sum + rows_checksum(op.drain())) % (1 << 56)
         op.clear_rows()  # DiscardingSink
         return k, t
@@ -355,6 +375,9 @@ def main():
             out["rows_checksum"] = rows_sum
         if world > 1:
             out["exchange_gbs_per_gpu"] = exch_bytes / elapsed / 1e9
+            out["exchange_path"] = ("gw_exchange_batch (libgpuwin RCCL: partition, one all-to-all of "
+                                    "(count, watermark, columns), one host wait, grouped send/recv per batch)"
+                                    if native_ex else "torch.distributed KeyByExchange (gloo rehearsal)")
         print(json.dumps(out), flush=True)
     op.close()
     if dist:
@@ -449,8 +472,10 @@ def host_cores():
 
 def cpu_baseline(args, keys, ts, vals, wms, nb, agg, size, slide):
     """CPU restatement of Flink's operator (oracle/, 'port') on the host cores: one operator
-    per simulated subtask thread over a bounded prefix of the same stream.  Parallelism =
-    the host CPUs this process may run on (parallelism = nproc)."""
+    per simulated subtask thread over the first watermark batches of the same stream, at the
+    stream's own cadence (each batch followed by its watermark, no final MAX_WATERMARK: what
+    the GPU's timed steps do).  Parallelism = the host CPUs this process may run on
+    (parallelism = nproc)."""
     try:
         from oracle import oracle as O
         O.build()
@@ -467,20 +492,17 @@ def cpu_baseline(args, keys, ts, vals, wms, nb, agg, size, slide):
         blen = np.full(nbatches, per_batch, np.int64)
         wm = np.array(wms[:nbatches], np.int64) if per_batch == nb else \
             np.array([int(t[(b + 1) * per_batch - 1]) - args.disorder_ms - 1 for b in range(nbatches)], np.int64)
-        rows, _, sec = O.run_parallel(cfg, threads, blen, wm, k, t, v)
+        rows, _, sec = O.run_parallel(cfg, threads, blen, wm, k, t, v, final_watermark=False)
         return n, sec, rows
 
-    # calibrate on 1/50 of a step, then size the sample for ~cpu_baseline_seconds
+    # calibrate on 1/50 of a step, then size the sample for ~cpu_baseline_seconds in whole
+    # watermark batches of the stream (at least one)
     n0, s0, _ = run(1, max(nb // 50, 10000))
     rate0 = n0 / max(s0, 1e-6)
-    target = int(rate0 * args.cpu_baseline_seconds)
-    nbatches = max(1, min(len(wms), target // nb))
-    if target < nb:
-        n, sec, rows = run(1, max(target, 10000))
-        sample = f"first {n} events of the GPU stream as one batch + final watermark"
-    else:
-        n, sec, rows = run(nbatches, nb)
-        sample = f"first {nbatches} watermark batches ({n} events) of the GPU stream + final watermark"
+    nbatches = max(1, min(len(wms), int(round(rate0 * args.cpu_baseline_seconds / nb))))
+    n, sec, rows = run(nbatches, nb)
+    sample = (f"first {nbatches} watermark batches ({n} events) of the GPU stream, each followed by its "
+              f"watermark (no final MAX_WATERMARK), {rows} rows fired")
     return {"value": n / sec, "unit": "events/s", "cores": threads, "kind": "port", "sample": sample,
             "seconds": sec, "rows": rows, "nproc": os.cpu_count(), "cores_source": cores_note}
 

@@ -36,10 +36,19 @@ struct gw_exchange {
     int32_t* recv_hash[2] = {nullptr, nullptr};
     int64_t recv_cap[2] = {0, 0};
     int turn = 0;
-    int64_t* d_counts = nullptr;  // [2][nranks]: send counts | receive counts
-    int64_t* h_counts = nullptr;  // pinned copy
+    // One all-to-all message per peer and batch: (records for it, watermark, column mask).
+    // d_msg: [nranks][kMsg] send | [nranks][kMsg] receive; h_msg its pinned copy.
+    static constexpr int kMsg = 3;
+    int64_t* d_counts = nullptr;  // [nranks] partition counts
+    int64_t* d_msg = nullptr;
+    int64_t* h_msg = nullptr;
     int64_t* d_wm = nullptr;
     int64_t* h_wm = nullptr;
+    std::vector<int64_t> last_send, last_recv;
+    // per receive set: the hand-off stream the ingest orders on, and its "reads done" event
+    hipStream_t handoff[2] = {nullptr, nullptr};
+    hipEvent_t ev_recv[2] = {nullptr, nullptr}, ev_free[2] = {nullptr, nullptr};
+    bool set_used[2] = {false, false};
     std::string err;
 };
 
@@ -85,11 +94,22 @@ int gw_exchange_create(gw_exchange** out, int32_t nranks, int32_t rank, const vo
     ncclUniqueId u;
     memcpy(&u, id, sizeof(u));
     if (ncclCommInitRank(&ex->comm, nranks, u, rank) != ncclSuccess) return bail(GW_E_DEVICE);
-    if (hipMalloc((void**)&ex->d_counts, (size_t)2 * nranks * 8 + 16) != hipSuccess) return bail(GW_E_OOM);
-    if (hipHostMalloc((void**)&ex->h_counts, (size_t)2 * nranks * 8 + 16, hipHostMallocDefault) != hipSuccess)
+    const size_t words = (size_t)nranks * (1 + 2 * gw_exchange::kMsg) + 2;
+    if (hipMalloc((void**)&ex->d_counts, words * 8) != hipSuccess) return bail(GW_E_OOM);
+    if (hipHostMalloc((void**)&ex->h_msg, (size_t)(2 * gw_exchange::kMsg * nranks + 2) * 8, hipHostMallocDefault) !=
+        hipSuccess)
         return bail(GW_E_OOM);
-    ex->d_wm = ex->d_counts + 2 * nranks;
-    ex->h_wm = ex->h_counts + 2 * nranks;
+    ex->d_msg = ex->d_counts + nranks;
+    ex->d_wm = ex->d_msg + 2 * gw_exchange::kMsg * nranks;
+    ex->h_wm = ex->h_msg + 2 * gw_exchange::kMsg * nranks;
+    for (int q = 0; q < 2; ++q) {
+        if (hipStreamCreateWithFlags(&ex->handoff[q], hipStreamNonBlocking) != hipSuccess ||
+            hipEventCreateWithFlags(&ex->ev_recv[q], hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&ex->ev_free[q], hipEventDisableTiming) != hipSuccess)
+            return bail(GW_E_DEVICE);
+    }
+    ex->last_send.assign(nranks, 0);
+    ex->last_recv.assign(nranks, 0);
     *out = ex;
     return GW_OK;
 }
@@ -103,19 +123,25 @@ void gw_exchange_destroy(gw_exchange* ex) {
     hipFree(ex->part_hash);
     for (int q = 0; q < 2; ++q) { hipFree(ex->recv[q]); hipFree(ex->recv_hash[q]); }
     hipFree(ex->d_counts);
-    hipHostFree(ex->h_counts);
+    hipHostFree(ex->h_msg);
+    for (int q = 0; q < 2; ++q) {
+        if (ex->handoff[q]) hipStreamDestroy(ex->handoff[q]);
+        if (ex->ev_recv[q]) hipEventDestroy(ex->ev_recv[q]);
+        if (ex->ev_free[q]) hipEventDestroy(ex->ev_free[q]);
+    }
     delete ex;
 }
 
 const char* gw_exchange_last_error(const gw_exchange* ex) { return ex ? ex->err.c_str() : ""; }
 
 int gw_exchange_batch(gw_exchange* ex, int64_t n, const int64_t* d_key, const int32_t* d_key_hash,
-                      const int64_t* d_ts, const int64_t* d_value, int64_t* n_out, const int64_t** d_key_out,
-                      const int32_t** d_key_hash_out, const int64_t** d_ts_out, const int64_t** d_value_out,
-                      void* stream) {
+                      const int64_t* d_ts, const int64_t* d_value, int64_t wm, int64_t* n_out,
+                      const int64_t** d_key_out, const int32_t** d_key_hash_out, const int64_t** d_ts_out,
+                      const int64_t** d_value_out, int64_t* wm_out, void** ingest_stream, void* stream) {
     if (!ex || n < 0 || !n_out || !d_key_out || !d_ts_out || (n > 0 && (!d_key || !d_ts))) return GW_E_INVALID;
     hipStream_t s = (hipStream_t)stream;
     const int P = ex->nranks;
+    constexpr int M = gw_exchange::kMsg;
     // 1. stable device partition by owner subtask
     if (n > ex->part_cap) {
         EX_HIP(hipStreamSynchronize(s));
@@ -145,18 +171,34 @@ int gw_exchange_batch(gw_exchange* ex, int64_t n, const int64_t* d_key, const in
     } else {
         EX_HIP(hipMemsetAsync(ex->d_counts, 0, (size_t)P * 8, s));
     }
-    // 2. counts: all-to-all of one int64 per peer, then to the host (the receive sizes)
-    EX_NCCL(ncclAllToAll(ex->d_counts, ex->d_counts + P, 1, ncclInt64, ex->comm, s));
-    EX_HIP(hipMemcpyAsync(ex->h_counts, ex->d_counts, (size_t)2 * P * 8, hipMemcpyDeviceToHost, s));
+    // 2. one message per peer: (count, watermark, columns); all-to-all, then one host wait
+    const int64_t cols_mask = (d_value ? 1 : 0) | (d_key_hash ? 2 : 0);
+    EX_HIP(launch_exchange_message(ex->d_counts, P, wm, cols_mask, ex->d_msg, s));
+    EX_NCCL(ncclAllToAll(ex->d_msg, ex->d_msg + M * P, M, ncclInt64, ex->comm, s));
+    EX_HIP(hipMemcpyAsync(ex->h_msg, ex->d_msg, (size_t)2 * M * P * 8, hipMemcpyDeviceToHost, s));
     EX_HIP(hipStreamSynchronize(s));
-    const int64_t* sc = ex->h_counts;
-    const int64_t* rc = ex->h_counts + P;
-    int64_t total = 0;
-    for (int q = 0; q < P; ++q) total += rc[q];
-    // 3. this turn's receive set, grown to the batch (the stream is idle here)
+    const int64_t* sm = ex->h_msg;
+    const int64_t* rm = ex->h_msg + M * P;
+    int64_t total = 0, wmin = wm;
+    bool cols_agree = true;
+    for (int q = 0; q < P; ++q) {
+        ex->last_send[q] = sm[M * q];
+        ex->last_recv[q] = rm[M * q];
+        total += rm[M * q];
+        wmin = std::min(wmin, rm[M * q + 1]);
+        cols_agree &= rm[M * q + 2] == cols_mask;
+    }
+    // every rank sees every rank's mask: all of them fail here together, before any send
+    if (!cols_agree) return ex_fail(ex, GW_E_INVALID, "gw_exchange_batch: ranks pass different columns");
+    // 3. this turn's receive set: free once the ingest two batches ago has read it
     const int u = ex->turn;
     ex->turn ^= 1;
+    if (ex->set_used[u]) {  // everything queued on its hand-off stream so far: the ingest's reads
+        EX_HIP(hipEventRecord(ex->ev_free[u], ex->handoff[u]));
+        EX_HIP(hipStreamWaitEvent(s, ex->ev_free[u], 0));
+    }
     if (total > ex->recv_cap[u]) {
+        EX_HIP(hipStreamSynchronize(s));
         hipFree(ex->recv[u]);
         hipFree(ex->recv_hash[u]);
         ex->recv[u] = nullptr;
@@ -170,29 +212,49 @@ int gw_exchange_batch(gw_exchange* ex, int64_t n, const int64_t* d_key, const in
     int64_t* rt = rk + ex->recv_cap[u];
     int64_t* rv = rt + ex->recv_cap[u];
     int32_t* rh = ex->recv_hash[u];
-    // 4. columns: grouped point-to-point send / receive per peer
+    // 4. columns: grouped point-to-point send / receive per peer (the group is always closed)
     struct Col { const void* src; void* dst; ncclDataType_t t; size_t w; };
     const Col cols[4] = {{pk, rk, ncclInt64, 8},
                          {pt, rt, ncclInt64, 8},
                          {d_value ? pv : nullptr, rv, ncclInt64, 8},
                          {d_key_hash ? ex->part_hash : nullptr, rh, ncclInt32, 4}};
     EX_NCCL(ncclGroupStart());
+    ncclResult_t r = ncclSuccess;
     for (const Col& c : cols) {
         if (!c.src) continue;
         int64_t so = 0, ro = 0;
-        for (int q = 0; q < P; ++q) {
-            if (sc[q]) EX_NCCL(ncclSend((const char*)c.src + so * c.w, (size_t)sc[q], c.t, q, ex->comm, s));
-            if (rc[q]) EX_NCCL(ncclRecv((char*)c.dst + ro * c.w, (size_t)rc[q], c.t, q, ex->comm, s));
-            so += sc[q];
-            ro += rc[q];
+        for (int q = 0; q < P && r == ncclSuccess; ++q) {
+            if (sm[M * q]) r = ncclSend((const char*)c.src + so * c.w, (size_t)sm[M * q], c.t, q, ex->comm, s);
+            if (r == ncclSuccess && rm[M * q])
+                r = ncclRecv((char*)c.dst + ro * c.w, (size_t)rm[M * q], c.t, q, ex->comm, s);
+            so += sm[M * q];
+            ro += rm[M * q];
         }
     }
-    EX_NCCL(ncclGroupEnd());
+    const ncclResult_t re = ncclGroupEnd();
+    if (r != ncclSuccess) return ex_fail(ex, GW_E_DEVICE, std::string("ncclSend/ncclRecv: ") + ncclGetErrorString(r));
+    if (re != ncclSuccess) return ex_fail(ex, GW_E_DEVICE, std::string("ncclGroupEnd: ") + ncclGetErrorString(re));
+    // 5. hand-off: the ingest of this set orders after the receives on handoff[u] (and makes
+    // handoff[u] wait for its reads); the exchange that reuses the set waits for handoff[u]
+    EX_HIP(hipEventRecord(ex->ev_recv[u], s));
+    EX_HIP(hipStreamWaitEvent(ex->handoff[u], ex->ev_recv[u], 0));
+    ex->set_used[u] = true;
     *n_out = total;
     *d_key_out = rk;
     *d_ts_out = rt;
     if (d_value_out) *d_value_out = d_value ? rv : nullptr;
     if (d_key_hash_out) *d_key_hash_out = d_key_hash ? rh : nullptr;
+    if (wm_out) *wm_out = wmin;
+    if (ingest_stream) *ingest_stream = (void*)ex->handoff[u];
+    return GW_OK;
+}
+
+int gw_exchange_counts(const gw_exchange* ex, int64_t* send, int64_t* recv) {
+    if (!ex) return GW_E_INVALID;
+    for (int q = 0; q < ex->nranks; ++q) {
+        if (send) send[q] = ex->last_send[q];
+        if (recv) recv[q] = ex->last_recv[q];
+    }
     return GW_OK;
 }
 

@@ -350,6 +350,9 @@ hipError_t launch_khmap_insert(const KeyHashMap& m, int64_t n, const int64_t* ke
                                unsigned long long* out, hipStream_t s);
 // p[0..n) = v
 hipError_t launch_fill64(int64_t* p, int64_t n, int64_t v, hipStream_t s);
+// keyBy exchange message per peer q: msg[3q..3q+2] = (counts[q], wm, cols)
+hipError_t launch_exchange_message(const int64_t* counts, int32_t p, int64_t wm, int64_t cols, int64_t* msg,
+                                   hipStream_t s);
 // Every entry of `from` into the empty map `to`.
 hipError_t launch_khmap_rehash(const KeyHashMap& from, const KeyHashMap& to, hipStream_t s);
 

@@ -230,6 +230,21 @@ hipError_t launch_fill64(int64_t* p, int64_t n, int64_t v, hipStream_t s) {
     return hipGetLastError();
 }
 
+__global__ void __launch_bounds__(256) k_exchange_message(const int64_t* counts, int32_t p, int64_t wm, int64_t cols,
+                                                          int64_t* msg) {
+    for (int q = threadIdx.x; q < p; q += blockDim.x) {
+        msg[3 * q] = counts[q];
+        msg[3 * q + 1] = wm;
+        msg[3 * q + 2] = cols;
+    }
+}
+
+hipError_t launch_exchange_message(const int64_t* counts, int32_t p, int64_t wm, int64_t cols, int64_t* msg,
+                                   hipStream_t s) {
+    hipLaunchKernelGGL(k_exchange_message, dim3(1), dim3(256), 0, s, counts, p, wm, cols, msg);
+    return hipGetLastError();
+}
+
 hipError_t launch_khmap_insert(const KeyHashMap& m, int64_t n, const int64_t* key, const int32_t* hash, int verify,
                                unsigned long long* out, hipStream_t s) {
     if (n <= 0) return hipSuccess;

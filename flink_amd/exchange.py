@@ -167,19 +167,29 @@ class NativeKeyByExchange:
             raise N.GpuWinError(rc, msg.decode() if msg else "")
 
     def exchange(self, keys: torch.Tensor, ts: torch.Tensor, vals: Optional[torch.Tensor] = None,
-                 key_hashes: Optional[torch.Tensor] = None, stream=None):
-        """-> (n, key_ptr, ts_ptr, value_ptr, key_hash_ptr): device pointers of the records
-        this rank owns, in the exchange's receive columns (valid until the next-but-one call);
-        feed them to GpuWindowOperator.process_batch_device_ptr."""
+                 key_hashes: Optional[torch.Tensor] = None, stream=None, wm: int = -(1 << 63)):
+        """One watermark batch (gw_exchange_batch): -> (n, key_ptr, ts_ptr, value_ptr, key_hash_ptr,
+        min watermark over the ranks, ingest stream).  The pointers are device columns of the
+        records this rank owns (valid until the next-but-one call); pass the ingest stream as
+        the producer stream of gw_ingest_device (GpuWindowOperator.process_batch_device_ptr)."""
         import ctypes
         s = stream if stream is not None else torch.cuda.current_stream(keys.device).cuda_stream
         ptr = lambda t: t.data_ptr() if t is not None else None
-        n_out = ctypes.c_int64()
-        ok, oh, ot, ov = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p()
+        n_out, wm_out = ctypes.c_int64(), ctypes.c_int64()
+        ok, oh, ot, ov, ist = (ctypes.c_void_p() for _ in range(5))
         self._check(N.lib().gw_exchange_batch(self._h, keys.numel(), ptr(keys), ptr(key_hashes), ptr(ts), ptr(vals),
-                                              ctypes.byref(n_out), ctypes.byref(ok), ctypes.byref(oh),
-                                              ctypes.byref(ot), ctypes.byref(ov), s))
-        return n_out.value, ok.value, ot.value, ov.value, oh.value
+                                              int(wm), ctypes.byref(n_out), ctypes.byref(ok), ctypes.byref(oh),
+                                              ctypes.byref(ot), ctypes.byref(ov), ctypes.byref(wm_out),
+                                              ctypes.byref(ist), s))
+        return n_out.value, ok.value, ot.value, ov.value, oh.value, wm_out.value, ist.value
+
+    def counts(self):
+        """(send, receive) record counts per peer of the last batch."""
+        import ctypes
+        import numpy as np
+        sc, rc = np.zeros(self.p, np.int64), np.zeros(self.p, np.int64)
+        self._check(N.lib().gw_exchange_counts(self._h, sc.ctypes.data, rc.ctypes.data))
+        return sc, rc
 
     def combine_watermark(self, wm: int, stream=None) -> int:
         import ctypes

@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define GW_ABI_VERSION 2
+#define GW_ABI_VERSION 3
 
 /* ---- status codes -------------------------------------------------------- */
 #define GW_OK              0
@@ -369,13 +369,23 @@ int  gw_partition_device(int64_t n, const int64_t* d_key, const int32_t* d_key_h
  *
  * gw_exchange_unique_id: rank 0 creates the 128-byte communicator id; the caller hands it
  * to every rank out of band (the JobManager / a TCP rendezvous), each rank calls
- * gw_exchange_create with it.  gw_exchange_batch: d_key/d_ts (d_value, d_key_hash may be
- * NULL) hold this rank's n records; the *n_out records this rank owns arrive in receive
- * columns owned by the exchange (*d_*_out; NULL for an absent input column), valid until
- * the next-but-one call (two receive sets used in turn, so the ingest of one batch may
- * overlap the exchange of the next on another stream).  All ranks call it for every batch
- * (n may be 0).  It waits for the counts (one small device->host copy), then enqueues the
- * column exchange on `stream`. */
+ * gw_exchange_create with it.
+ *
+ * gw_exchange_batch: d_key/d_ts (d_value, d_key_hash may be NULL) hold this rank's n records
+ * of one watermark batch and wm the watermark its source emitted after them.  One RCCL
+ * all-to-all carries, per peer, (record count, watermark, column presence); the host waits
+ * for it once (one device->host copy: the only host synchronisation of the batch), checks
+ * that every rank sends the same columns (GW_E_INVALID otherwise, on every rank), then
+ * enqueues one grouped ncclSend/ncclRecv per column and peer on `stream`.  Out: the *n_out
+ * records this rank owns in receive columns owned by the exchange (*d_*_out; NULL for an
+ * absent column), valid until the next-but-one call (two receive sets used in turn);
+ * *wm_out = the minimum of the ranks' watermarks (StatusWatermarkValve); *ingest_stream = a
+ * hand-off stream of this receive set, ordered after the receives: pass it as the producer
+ * stream of gw_ingest_device, whose "producer waits for my reads" ordering then lands on
+ * the hand-off stream, so the exchange of the next batch never waits for this batch's
+ * ingest, only the reuse of this receive set two batches later does.  All ranks call it
+ * for every batch (n may be 0).  gw_exchange_counts: the last batch's per-peer send and
+ * receive record counts (nranks each; either may be NULL). */
 #define GW_EXCHANGE_ID_BYTES 128
 typedef struct gw_exchange gw_exchange;
 int  gw_exchange_unique_id(void* id);
@@ -383,9 +393,10 @@ int  gw_exchange_create(gw_exchange** out, int32_t nranks, int32_t rank, const v
                         int32_t max_parallelism);
 void gw_exchange_destroy(gw_exchange* ex);
 int  gw_exchange_batch(gw_exchange* ex, int64_t n, const int64_t* d_key, const int32_t* d_key_hash,
-                       const int64_t* d_ts, const int64_t* d_value, int64_t* n_out, const int64_t** d_key_out,
-                       const int32_t** d_key_hash_out, const int64_t** d_ts_out, const int64_t** d_value_out,
-                       void* stream);
+                       const int64_t* d_ts, const int64_t* d_value, int64_t wm, int64_t* n_out,
+                       const int64_t** d_key_out, const int32_t** d_key_hash_out, const int64_t** d_ts_out,
+                       const int64_t** d_value_out, int64_t* wm_out, void** ingest_stream, void* stream);
+int  gw_exchange_counts(const gw_exchange* ex, int64_t* send, int64_t* recv);
 int  gw_exchange_min_watermark(gw_exchange* ex, int64_t wm, int64_t* out, void* stream);
 const char* gw_exchange_last_error(const gw_exchange* ex);
 

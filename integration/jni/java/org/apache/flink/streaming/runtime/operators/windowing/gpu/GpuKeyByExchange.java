@@ -16,7 +16,7 @@ public final class GpuKeyByExchange implements AutoCloseable {
     public static final int ID_BYTES = 128;
 
     private long handle;
-    private final ByteBuffer out = ByteBuffer.allocateDirect(5 * 8).order(ByteOrder.nativeOrder());
+    private final ByteBuffer out = ByteBuffer.allocateDirect(7 * 8).order(ByteOrder.nativeOrder());
 
     public static byte[] uniqueId() {
         ByteBuffer id = ByteBuffer.allocateDirect(ID_BYTES);
@@ -33,13 +33,16 @@ public final class GpuKeyByExchange implements AutoCloseable {
         return this;
     }
 
-    /** Device columns in (addresses; 0 = absent); returns {n, key, keyHash, ts, value} of the
-     *  records this subtask owns, in the exchange's receive columns (valid until the
-     *  next-but-one call), ready for GpuWindowOperator's device ingest. */
-    public long[] batch(long n, long keyPtr, long hashPtr, long tsPtr, long valuePtr, long stream) {
-        nativeBatch(handle, n, keyPtr, hashPtr, tsPtr, valuePtr, stream, out);
-        long[] r = new long[5];
-        for (int i = 0; i < 5; i++) r[i] = out.getLong(8 * i);
+    /** One watermark batch: device columns in (addresses; 0 = absent) and the watermark the
+     *  source emitted after them.  Returns {n, key, keyHash, ts, value, minWatermark,
+     *  ingestStream}: the records this subtask owns, in the exchange's receive columns (valid
+     *  until the next-but-one call), the minimum watermark over the subtasks
+     *  (StatusWatermarkValve, carried by the same all-to-all as the counts: one host wait per
+     *  batch), and the stream to hand to GpuWindowOperator.nativeIngestDevice. */
+    public long[] batch(long n, long keyPtr, long hashPtr, long tsPtr, long valuePtr, long watermark, long stream) {
+        nativeBatch(handle, n, keyPtr, hashPtr, tsPtr, valuePtr, watermark, stream, out);
+        long[] r = new long[7];
+        for (int i = 0; i < 7; i++) r[i] = out.getLong(8 * i);
         return r;
     }
 
@@ -55,6 +58,6 @@ public final class GpuKeyByExchange implements AutoCloseable {
     private static native long nativeCreate(int nranks, int rank, ByteBuffer id, int device, int maxParallelism);
     private static native void nativeDestroy(long h);
     private static native void nativeBatch(long h, long n, long keyPtr, long hashPtr, long tsPtr, long valuePtr,
-                                           long stream, ByteBuffer out);
+                                           long watermark, long stream, ByteBuffer out);
     private static native long nativeMinWatermark(long h, long wm, long stream);
 }

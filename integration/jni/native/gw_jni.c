@@ -262,20 +262,25 @@ JNIEXPORT void JNICALL XCLS(nativeDestroy)(JNIEnv* env, jclass c, jlong x) {
     gw_exchange_destroy((gw_exchange*)(intptr_t)x);
 }
 
-/* One batch: device columns in (raw addresses, 0 = absent); `out` is a direct buffer of 5
- * longs receiving {records received, key, key hash, timestamp, value} device addresses. */
+/* One watermark batch: device columns in (raw addresses, 0 = absent) and the watermark the
+ * source emitted after them; `out` is a direct buffer of 7 longs receiving {records received,
+ * key, key hash, timestamp, value device addresses, minimum watermark over the subtasks, the
+ * ingest stream to pass to nativeIngestDevice}. */
 JNIEXPORT void JNICALL XCLS(nativeBatch)(JNIEnv* env, jclass c, jlong x, jlong n, jlong keyPtr, jlong hashPtr,
-                                         jlong tsPtr, jlong valuePtr, jlong stream, jobject out) {
+                                         jlong tsPtr, jlong valuePtr, jlong wm, jlong stream, jobject out) {
     int64_t* o = (*env)->GetDirectBufferAddress(env, out);
     const int64_t *k = 0, *t = 0, *v = 0;
     const int32_t* kh = 0;
+    void* ist = 0;
     int rc = gw_exchange_batch((gw_exchange*)(intptr_t)x, n, (const int64_t*)(intptr_t)keyPtr,
                                (const int32_t*)(intptr_t)hashPtr, (const int64_t*)(intptr_t)tsPtr,
-                               (const int64_t*)(intptr_t)valuePtr, &o[0], &k, &kh, &t, &v, (void*)(intptr_t)stream);
+                               (const int64_t*)(intptr_t)valuePtr, wm, &o[0], &k, &kh, &t, &v, &o[5], &ist,
+                               (void*)(intptr_t)stream);
     o[1] = (int64_t)(intptr_t)k;
     o[2] = (int64_t)(intptr_t)kh;
     o[3] = (int64_t)(intptr_t)t;
     o[4] = (int64_t)(intptr_t)v;
+    o[6] = (int64_t)(intptr_t)ist;
     fail_ex(env, (gw_exchange*)(intptr_t)x, rc);
 }
 

@@ -1325,6 +1325,7 @@ typedef struct {
     int64_t* pw_rows;  /* optional [nb + 1]: rows fired per watermark (the last: MAX_WATERMARK) */
     uint64_t* pw_cs;   /* optional [nb + 1]: order-independent checksum of those rows */
     int rc;
+    int no_final;      /* 1: no MAX_WATERMARK after the last batch (the stream's own cadence) */
 } par_arg;
 
 static void* par_main(void* p) {
@@ -1339,6 +1340,7 @@ static void* par_main(void* p) {
     int64_t* be = bs + 1024;
     int64_t* br = be + 1024;
     for (int64_t b = 0; b <= a->nb; b++) {
+        if (b == a->nb && a->no_final) break;
         if (b < a->nb) {
             for (int64_t i = off; i < off + a->blen[b]; i++) {
                 int32_t kg = wo_assign_to_key_group(wo_long_hash(a->key[i]), maxp);
@@ -1369,16 +1371,16 @@ done:
     return NULL;
 }
 
-int64_t wo_run_parallel(const gw_config* cfg, int threads, int64_t nb, const int64_t* blen,
-                        const int64_t* wm, const int64_t* key, const int64_t* ts,
-                        const int64_t* val, int64_t* checksum, double* seconds) {
+static int64_t run_parallel(const gw_config* cfg, int threads, int64_t nb, const int64_t* blen,
+                            const int64_t* wm, const int64_t* key, const int64_t* ts,
+                            const int64_t* val, int no_final, int64_t* checksum, double* seconds) {
     if (threads < 1) threads = 1;
     pthread_t* th = (pthread_t*)calloc((size_t)threads, sizeof(pthread_t));
     par_arg* args = (par_arg*)calloc((size_t)threads, sizeof(par_arg));
     struct timespec t0, t1;
     clock_gettime(CLOCK_MONOTONIC, &t0);
     for (int i = 0; i < threads; i++) {
-        args[i] = (par_arg){cfg, i, threads, nb, blen, wm, key, ts, val, 0, 0, NULL, NULL, 0};
+        args[i] = (par_arg){cfg, i, threads, nb, blen, wm, key, ts, val, 0, 0, NULL, NULL, 0, no_final};
         pthread_create(&th[i], NULL, par_main, &args[i]);
     }
     int64_t rows = 0;
@@ -1398,6 +1400,20 @@ int64_t wo_run_parallel(const gw_config* cfg, int threads, int64_t nb, const int
     return rc ? rc : rows;
 }
 
+int64_t wo_run_parallel(const gw_config* cfg, int threads, int64_t nb, const int64_t* blen,
+                        const int64_t* wm, const int64_t* key, const int64_t* ts,
+                        const int64_t* val, int64_t* checksum, double* seconds) {
+    return run_parallel(cfg, threads, nb, blen, wm, key, ts, val, 0, checksum, seconds);
+}
+
+/* The same without the final MAX_WATERMARK: the batches at the stream's own watermark cadence
+ * only (what a bench's timed steps do). */
+int64_t wo_run_parallel_stream(const gw_config* cfg, int threads, int64_t nb, const int64_t* blen,
+                               const int64_t* wm, const int64_t* key, const int64_t* ts,
+                               const int64_t* val, int64_t* checksum, double* seconds) {
+    return run_parallel(cfg, threads, nb, blen, wm, key, ts, val, 1, checksum, seconds);
+}
+
 /* wo_run_parallel with per-watermark results: wm_rows[b] / wm_cs[b] (b = 0..nb, the last
  * entry for the final MAX_WATERMARK) receive the number of rows each watermark fired over
  * all subtasks and the sum of their row hashes (the checksum of wo_run_parallel, per
@@ -1415,7 +1431,7 @@ int64_t wo_run_parallel_wm(const gw_config* cfg, int threads, int64_t nb, const 
     clock_gettime(CLOCK_MONOTONIC, &t0);
     for (int i = 0; i < threads; i++) {
         args[i] = (par_arg){cfg, i, threads, nb, blen, wm, key, ts, val, 0, 0,
-                            pr + (size_t)i * (size_t)(nb + 1), pc + (size_t)i * (size_t)(nb + 1), 0};
+                            pr + (size_t)i * (size_t)(nb + 1), pc + (size_t)i * (size_t)(nb + 1), 0, 0};
         pthread_create(&th[i], NULL, par_main, &args[i]);
     }
     int64_t rows = 0;

@@ -86,6 +86,12 @@ int64_t wo_run_parallel(const gw_config* cfg, int threads, int64_t n_batches,
                         const int64_t* batch_len, const int64_t* wm,
                         const int64_t* key, const int64_t* ts, const int64_t* value_bits,
                         int64_t* checksum, double* seconds);
+/* The same without the final MAX_WATERMARK: only the stream's own watermarks (the cadence a
+ * benchmark's timed steps run at). */
+int64_t wo_run_parallel_stream(const gw_config* cfg, int threads, int64_t n_batches,
+                               const int64_t* batch_len, const int64_t* wm,
+                               const int64_t* key, const int64_t* ts, const int64_t* value_bits,
+                               int64_t* checksum, double* seconds);
 /* The same, per watermark: wm_rows[b] / wm_cs[b] for b = 0..n_batches (the last entry is
  * the final MAX_WATERMARK) hold the rows that watermark fired over all subtasks and the
  * sum of their row hashes, (key * 0x9e3779b97f4a7c15) ^ (start * 31) ^ (end * 17) ^ result

@@ -133,6 +133,8 @@ def lib() -> ctypes.CDLL:
                                                  ctypes.POINTER(GwDecodeResult)]),
             ("wo_run_parallel", i64, [ctypes.POINTER(GwConfig), ctypes.c_int, i64, p, p, p, p, p,
                                        P64, ctypes.POINTER(ctypes.c_double)]),
+            ("wo_run_parallel_stream", i64, [ctypes.POINTER(GwConfig), ctypes.c_int, i64, p, p, p, p, p,
+                                              P64, ctypes.POINTER(ctypes.c_double)]),
             ("wo_snapshot", i64, [p, i32, i32, p, i64]), ("wo_restore", ctypes.c_int, [p, p, i64]),
             ("wo_acc_bytes", ctypes.c_int, [ctypes.c_int]),
             ("wo_run_parallel_wm", i64, [ctypes.POINTER(GwConfig), ctypes.c_int, i64, p, p, p, p, p, p, p,
@@ -245,8 +247,9 @@ class OracleOperator:
         return lib().wo_session_merges(self._h)
 
 
-def run_parallel(cfg: GwConfig, threads: int, batch_len, wm, key, ts, value_bits):
-    """Multi-threaded CPU baseline (one operator per simulated Flink subtask)."""
+def run_parallel(cfg: GwConfig, threads: int, batch_len, wm, key, ts, value_bits, final_watermark=True):
+    """Multi-threaded CPU baseline (one operator per simulated Flink subtask); without
+    final_watermark only the stream's own watermarks run (no MAX_WATERMARK at the end)."""
     batch_len = np.ascontiguousarray(batch_len, dtype=np.int64)
     wm = np.ascontiguousarray(wm, dtype=np.int64)
     key = np.ascontiguousarray(key, dtype=np.int64)
@@ -254,8 +257,9 @@ def run_parallel(cfg: GwConfig, threads: int, batch_len, wm, key, ts, value_bits
     vb = None if value_bits is None else np.ascontiguousarray(value_bits).view(np.int64)
     cs = ctypes.c_int64(0)
     sec = ctypes.c_double(0)
-    rows = lib().wo_run_parallel(ctypes.byref(cfg), threads, len(batch_len), _p(batch_len),
-                                 _p(wm), _p(key), _p(ts), _p(vb), ctypes.byref(cs), ctypes.byref(sec))
+    fn = lib().wo_run_parallel if final_watermark else lib().wo_run_parallel_stream
+    rows = fn(ctypes.byref(cfg), threads, len(batch_len), _p(batch_len), _p(wm), _p(key), _p(ts), _p(vb),
+              ctypes.byref(cs), ctypes.byref(sec))
     if rows < 0:
         raise OracleError(f"parallel oracle failed: {rows}")
     return rows, cs.value, sec.value

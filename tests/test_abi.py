@@ -30,7 +30,7 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_abi_version():
-    assert N.lib().gw_abi_version() == 2
+    assert N.lib().gw_abi_version() == 3
 
 
 def test_config_struct_layout_matches_header():

@@ -35,7 +35,10 @@ def test_exchange_round_trip_and_watermark():
         t = torch.from_numpy(rng.integers(0, 1 << 40, n).astype(np.int64)).cuda()
         v = torch.from_numpy(rng.integers(-(1 << 40), 1 << 40, n).astype(np.int64)).cuda()
         h = torch.from_numpy(rng.integers(-(1 << 31), (1 << 31) - 1, n).astype(np.int32)).cuda()
-        m, pk, pt, pv, ph = ex.exchange(k, t, v, key_hashes=h)
+        m, pk, pt, pv, ph, wmo, ist = ex.exchange(k, t, v, key_hashes=h, wm=n * 7)
+        assert wmo == n * 7 and ist  # one rank: the watermark comes back; a hand-off stream
+        sc, rc = ex.counts()
+        assert list(sc) == [n] and list(rc) == [n]
         torch.cuda.synchronize()
         assert m == n
         if n:
@@ -44,10 +47,10 @@ def test_exchange_round_trip_and_watermark():
             assert torch.equal(dev_view(pt, n), t)
             assert torch.equal(dev_view(pv, n), v)
             assert torch.equal(dev_view(ph, n, "<i4"), h)
-        m2, qk, qt, qv, qh = ex.exchange(k, t, None)
+        m2, qk, qt, qv, qh, _, ist2 = ex.exchange(k, t, None)
         assert m2 == n and qv is None and qh is None
         if n:
-            assert qk != pk  # the next call uses the other receive set
+            assert qk != pk and ist2 != ist  # the next call uses the other receive set
     assert ex.combine_watermark(12345) == 12345
     assert ex.combine_watermark(W.LONG_MIN) == W.LONG_MIN
     ex.close()
@@ -60,15 +63,17 @@ def test_exchanged_batches_fire_like_the_oracle(oracle_lib):
     op = W.GpuWindowOperator(W.SlidingEventTimeWindows.of(1000, 250), "sum_i64", capacity_hint=4096).open()
     ora = oracle_lib.OracleOperator(oracle_lib.make_config(**kw))
     g, o = [], []
-    s = op.stream()
+    xs = torch.cuda.Stream()  # the exchange's own stream; the ingest orders through the hand-off
+    s = xs.cuda_stream
     for lo, hi, wm in batches:
         k = torch.from_numpy(keys[lo:hi]).cuda()
         t = torch.from_numpy(ts[lo:hi]).cuda()
         v = torch.from_numpy(vals[lo:hi]).cuda()
         torch.cuda.synchronize()
-        n, pk, pt, pv, _ = ex.exchange(k, t, v, stream=s)
-        op.process_batch_device_ptr(n, pk, pt, pv, stream=s)
-        op.advance_watermark(ex.combine_watermark(wm, stream=s))
+        n, pk, pt, pv, _, wmin, ist = ex.exchange(k, t, v, stream=s, wm=wm)
+        op.process_batch_device_ptr(n, pk, pt, pv, stream=ist)
+        assert wmin == wm
+        op.advance_watermark(wmin)
         kk, ss, ee, rr = op.drain()
         g.append((kk, ss, ee, rr.view(np.int64)))
         ora.process_batch(keys[lo:hi], ts[lo:hi], vals[lo:hi])

@@ -270,7 +270,7 @@ def test_ingest_glue_with_key_hashes(jni):
                 seen += 1
         assert seen > 0
         # a key of the other subtask: the batch fails (IllegalArgumentException text of the reference)
-        bad = np.array([0], np.int64)
+        bad = np.array([10 ** 6], np.int64)  # a new id (id 0 already has its own hash)
         bh = np.array([java_string_hash(other[0])], np.int32)
         ing(env, None, h, 1, bad.ctypes.data, bh.ctypes.data, ts.ctypes.data, vals.ctypes.data)
         exc = exception(jni)
