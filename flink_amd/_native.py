@@ -36,6 +36,7 @@ FLAG_NO_REGION = 16
 FLAG_NO_BUFFER = 32
 FLAG_LATE_SIDE_OUTPUT = 64
 FLAG_FIRST_ELEMENT = 128
+FLAG_NO_NARROW = 256
 
 EXPORTS = [
     "gw_create", "gw_destroy", "gw_last_error", "gw_abi_version", "gw_ingest", "gw_ingest_device",
@@ -97,7 +98,8 @@ class GwConfig(ctypes.Structure):
 class GwStats(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int64) for n in (
         "events_in", "late_dropped", "rows_fired", "live_keys", "table_capacity", "table_bytes",
-        "deferred", "batches", "fires", "rehashes", "preagg_batches", "session_merges", "applies")]
+        "deferred", "batches", "fires", "rehashes", "preagg_batches", "session_merges", "applies",
+        "region_format")]
 
     def as_dict(self):
         return {n: getattr(self, n) for n, _ in self._fields_}

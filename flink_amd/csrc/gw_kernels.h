@@ -158,7 +158,8 @@ struct IngestArgs {
     // region path (k_rgn_p1 / k_rgn_plan* / k_rgn_p2 / k_rgn_apply, gw_pane.hip)
     int32_t d1_bits;       // region = (pass-1 bucket << d2_bits) | pass-2 bucket
     int32_t d2_bits;       // 0: single-pass table (apply reads the P1 tiles directly)
-    int32_t cmp;           // compact records (integer aggregates): hash word + 32-bit value
+    int32_t fmt;           // region record format (gw_pane.hip): 0 wide, 1 compact (hash word +
+                           // 32-bit value), 2 narrow (32-bit key + 28-bit value; 4 B for COUNT)
     int64_t tile0;         // P1: buffer tile of this batch's first tile
     int64_t ntiles;        // flush: buffer tiles in use
     int64_t ngroups;       // flush: P1 tile groups (= P2 blocks per bucket)

@@ -405,6 +405,28 @@ __device__ __forceinline__ uint64_t cmp_hash(uint64_t w, uint64_t bucket, int d1
 __device__ __forceinline__ uint32_t cmp_pos(uint64_t w, int d1) { return (uint32_t)((w << 1) >> (65 - d1)); }
 constexpr uint64_t kCmpSpill = 1ull << 63;
 
+// Record formats of the region buffer (IngestArgs::fmt, fixed per flush window by the host):
+// wide (key, acc word(s), ring position byte), compact (hash word + 32-bit value, above) and
+// narrow -- integer aggregates whose keys fit 32 bits (28 for COUNT) and values 28 bits
+// signed, ring positions < 8: the key itself, no hash, in 8 B (4 B for COUNT):
+//   8 B:  lo32 = key, hi32 = value << 4 | spill << 3 | ring position
+//   4 B:  key << 4 | spill << 3 | ring position                      (COUNT)
+// P2 and the apply recompute the key's hash (region bits, home slot) from it.  A record that
+// does not fit goes to the deferred list (exact); past 1/64 of a window's records the
+// handle drops to compact records at its next window.
+constexpr int kFmtWide = 0, kFmtCmp = 1, kFmtNar = 2;
+constexpr int64_t kNarKeyLimit = 1ll << 32, kNarCountKeyLimit = 1ll << 28, kNarValLimit = 1ll << 27;
+__device__ __forceinline__ uint64_t nar_pack(int64_t key, int64_t v, uint32_t pos) {
+    return (uint64_t)(uint32_t)key | ((uint64_t)(((uint32_t)(int32_t)v << 4) | pos) << 32);
+}
+__device__ __forceinline__ uint32_t nar_pack32(int64_t key, uint32_t pos) { return ((uint32_t)key << 4) | pos; }
+__device__ __forceinline__ int64_t nar_key(uint64_t r) { return (int64_t)(uint32_t)r; }
+__device__ __forceinline__ int64_t nar_key32(uint32_t r) { return (int64_t)(r >> 4); }
+__device__ __forceinline__ uint32_t nar_pos(uint32_t low_bits) { return low_bits & 7u; }
+__device__ __forceinline__ bool nar_spilled(uint32_t low_bits) { return (low_bits >> 3) & 1u; }
+__device__ __forceinline__ int64_t nar_val(uint64_t r) { return (int64_t)((int32_t)(uint32_t)(r >> 32) >> 4); }
+constexpr uint32_t kNarSpill = 8u;  // in the low bits of hi32 (8 B) or of the record (4 B)
+
 // Exclusive scan of h[0..nb) (nb <= 256) into out[]; executed by wave 0.
 __device__ __forceinline__ void scan_buckets(const uint32_t* h, uint32_t* out, int nb) {
     if (threadIdx.x >= 64) return;
@@ -511,14 +533,17 @@ __global__ void __launch_bounds__(256) k_publish_status(const DevStatus* st, Dev
 #else
 #define GW_APPLY_ATTR
 #endif
-template <int AGG, bool CMP, bool GAP>
+template <int AGG, int FMT, bool GAP>
 __global__ void __launch_bounds__(kPartThreads) GW_P1_ATTR k_rgn_p1(IngestArgs a) {
-    constexpr bool C = CMP && cmp_agg<AGG>();
-    constexpr bool AV = !C && (AGG == GW_AVG_I64 || AGG == GW_AVG_F64);
+    constexpr bool C = FMT == kFmtCmp && cmp_agg<AGG>();
+    constexpr bool NR = FMT == kFmtNar && cmp_agg<AGG>();
+    constexpr bool N4 = NR && AGG == GW_COUNT;  // 4-byte narrow records
+    constexpr bool AV = !C && !NR && (AGG == GW_AVG_I64 || AGG == GW_AVG_F64);
     constexpr bool ACC = !(C && AGG == GW_COUNT);  // COUNT records carry no value
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const TileLds s = tile_lds<AV>(smem);
     int32_t* s_v32 = reinterpret_cast<int32_t*>(s.a0);  // C: 32-bit values
+    uint32_t* s_r32 = reinterpret_cast<uint32_t*>(s.k);  // N4: the records
     __shared__ uint32_t lh[kPartBuckets], ls[kPartBuckets];
     __shared__ unsigned long long s_occ;
     const int64_t g = blockIdx.x;
@@ -558,6 +583,12 @@ __global__ void __launch_bounds__(kPartThreads) GW_P1_ATTR k_rgn_p1(IngestArgs a
             st = REC_DEFER;  // beyond the compact record's 32-bit value: exact via the deferred list
             wide++;
         }
+        if (NR && st == REC_RING &&
+            ((uint64_t)key[it] >= (uint64_t)(N4 ? kNarCountKeyLimit : kNarKeyLimit) ||
+             (!N4 && (v0 < -kNarValLimit || v0 >= kNarValLimit)))) {
+            st = REC_DEFER;  // beyond the narrow record: exact via the deferred list
+            wide++;
+        }
         if (st == REC_RING) {
             occ |= 1ull << ps;
             if (key[it] == kEmptyKey) {  // sentinel slot: rare, straight atomics
@@ -567,6 +598,7 @@ __global__ void __launch_bounds__(kPartThreads) GW_P1_ATTR k_rgn_p1(IngestArgs a
                 const uint64_t h = slot_hash(key[it]);
                 bk = (int)(pt_key_region(a.t, h) >> a.d2_bits);
                 if constexpr (C) key[it] = (int64_t)cmp_pack(h, ps, a.d1_bits);  // key -> word
+                if constexpr (NR) key[it] = N4 ? (int64_t)nar_pack32(key[it], ps) : (int64_t)nar_pack(key[it], v0, ps);
             }
         }
         defer_write(a, st == REC_DEFER, key[it], pane, v0, v1);
@@ -587,7 +619,12 @@ __global__ void __launch_bounds__(kPartThreads) GW_P1_ATTR k_rgn_p1(IngestArgs a
     for (int it = 0; it < kPartItems; ++it) {
         if (br[it] == ~0u) continue;
         const uint32_t j = ls[br[it] >> 16] + (br[it] & 0xffffu);
+        if constexpr (N4) {
+            s_r32[j] = (uint32_t)key[it];
+            continue;
+        }
         s.k[j] = key[it];
+        if constexpr (NR) continue;
         if constexpr (C) {
             if constexpr (ACC) s_v32[j] = c0[it];
         } else {
@@ -601,7 +638,12 @@ __global__ void __launch_bounds__(kPartThreads) GW_P1_ATTR k_rgn_p1(IngestArgs a
     const int64_t tile = a.tile0 + g;
     const int64_t base = tile * kPartTile;
     for (uint32_t j = threadIdx.x; j < cnt; j += blockDim.x) {
+        if constexpr (N4) {
+            __builtin_nontemporal_store(s_r32[j], reinterpret_cast<uint32_t*>(a.p1_key) + base + j);
+            continue;
+        }
         __builtin_nontemporal_store((int64_t)s.k[j], a.p1_key + base + j);  // read back a flush later
+        if constexpr (NR) continue;
         if constexpr (C) {
             if constexpr (ACC) __builtin_nontemporal_store(s_v32[j], reinterpret_cast<int32_t*>(a.p1_a0) + base + j);
         } else {
@@ -611,7 +653,7 @@ __global__ void __launch_bounds__(kPartThreads) GW_P1_ATTR k_rgn_p1(IngestArgs a
         }
     }
     for (int b = threadIdx.x; b < nb; b += blockDim.x) a.p1_row[tile * kPartBuckets + b] = desc_pack(ls[b], lh[b]);
-    if constexpr (C && ACC) {
+    if constexpr ((C && ACC) || NR) {
         wide = wave_sum(wide);
         if (__lane_id() == 0 && wide) atomicAdd(&a.st->wide_vals, wide);
     }
@@ -731,14 +773,17 @@ __global__ void __launch_bounds__(256) k_rgn_plan3(IngestArgs a) {
 }
 
 // P2: block (b1, j) -> rounds p2_roff[b1, j] ... of bucket b1, records at p2_off[b1, j].
-template <int AGG, bool CMP>
+template <int AGG, int FMT>
 __global__ void __launch_bounds__(kPartThreads) k_rgn_p2(IngestArgs a) {
-    constexpr bool C = CMP && cmp_agg<AGG>();
-    constexpr bool AV = !C && (AGG == GW_AVG_I64 || AGG == GW_AVG_F64);
+    constexpr bool C = FMT == kFmtCmp && cmp_agg<AGG>();
+    constexpr bool NR = FMT == kFmtNar && cmp_agg<AGG>();
+    constexpr bool N4 = NR && AGG == GW_COUNT;
+    constexpr bool AV = !C && !NR && (AGG == GW_AVG_I64 || AGG == GW_AVG_F64);
     constexpr bool ACC = !(C && AGG == GW_COUNT);
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const TileLds s = tile_lds<AV>(smem);
     int32_t* s_v32 = reinterpret_cast<int32_t*>(s.a0);
+    uint32_t* s_r32 = reinterpret_cast<uint32_t*>(s.k);
     const int lr_sh = 64 - (a.d1_bits + a.d2_bits);  // C: region bits of the hash word
     __shared__ uint32_t lh[kPartBuckets], ls[kPartBuckets];
     __shared__ uint32_t r_cnt[kMaxGroup], r_pre[kMaxGroup + 1], wsum[8];
@@ -773,8 +818,9 @@ __global__ void __launch_bounds__(kPartThreads) k_rgn_p2(IngestArgs a) {
             if (e < e1) {
                 const int i = run_of(r_pre, nt, e);
                 const int64_t src = r_src[i] + (e - r_pre[i]);
-                key[it] = a.p1_key[src];
-                if constexpr (C) {
+                key[it] = N4 ? (int64_t)reinterpret_cast<const uint32_t*>(a.p1_key)[src] : a.p1_key[src];
+                if constexpr (NR) {
+                } else if constexpr (C) {
                     if constexpr (ACC) c0[it] = reinterpret_cast<const int32_t*>(a.p1_a0)[src];
                 } else {
                     c0[it] = a.p1_a0[src];
@@ -787,7 +833,12 @@ __global__ void __launch_bounds__(kPartThreads) k_rgn_p2(IngestArgs a) {
 #pragma unroll
         for (int it = 0; it < kPartItems; ++it) {
             if (bk[it] < 0) continue;
-            bk[it] = C ? (int)(((uint64_t)key[it] >> lr_sh) & (uint64_t)m2) : (int)(rgn_of(a.t, key[it]) & m2);
+            if constexpr (NR) {  // the key's hash gives its region
+                const int64_t k = N4 ? nar_key32((uint32_t)key[it]) : nar_key((uint64_t)key[it]);
+                bk[it] = (int)((slot_hash(k) >> lr_sh) & (uint64_t)m2);
+            } else {
+                bk[it] = C ? (int)(((uint64_t)key[it] >> lr_sh) & (uint64_t)m2) : (int)(rgn_of(a.t, key[it]) & m2);
+            }
             rank[it] = atomicAdd(&lh[bk[it]], 1u);
         }
         __syncthreads();
@@ -797,7 +848,12 @@ __global__ void __launch_bounds__(kPartThreads) k_rgn_p2(IngestArgs a) {
         for (int it = 0; it < kPartItems; ++it) {
             if (bk[it] < 0) continue;
             const uint32_t jj = ls[bk[it]] + rank[it];
+            if constexpr (N4) {
+                s_r32[jj] = (uint32_t)key[it];
+                continue;
+            }
             s.k[jj] = key[it];
+            if constexpr (NR) continue;
             if constexpr (C) {
                 if constexpr (ACC) s_v32[jj] = (int32_t)c0[it];
             } else {
@@ -810,7 +866,12 @@ __global__ void __launch_bounds__(kPartThreads) k_rgn_p2(IngestArgs a) {
         const int64_t base = out0 + e0;
         const int64_t rnd = rnd0 + e0 / kPartTile;
         for (uint32_t jj = threadIdx.x; jj < e1 - e0; jj += blockDim.x) {
+            if constexpr (N4) {
+                __builtin_nontemporal_store(s_r32[jj], reinterpret_cast<uint32_t*>(a.e_key) + base + jj);
+                continue;
+            }
             __builtin_nontemporal_store((int64_t)s.k[jj], a.e_key + base + jj);
+            if constexpr (NR) continue;
             if constexpr (C) {
                 if constexpr (ACC) __builtin_nontemporal_store(s_v32[jj], reinterpret_cast<int32_t*>(a.e_a0) + base + jj);
             } else {
@@ -848,11 +909,13 @@ constexpr int kApplyRuns = 256;  // run descriptors staged in LDS per step (<= b
 constexpr int kApplyGroup = GW_APPLY_GROUP;   // consecutive runs a wave walks as one sequence
 constexpr int kApplyUnroll = GW_APPLY_UNROLL;  // records per lane with their loads in flight together
 
-template <int AGG, bool CMP>
+template <int AGG, int FMT>
 __global__ void __launch_bounds__(kApplyThreads) GW_APPLY_ATTR k_rgn_apply(IngestArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     constexpr bool M = uses_mask<AGG>();
-    constexpr bool C = CMP && cmp_agg<AGG>();
+    constexpr bool C = FMT == kFmtCmp && cmp_agg<AGG>();
+    constexpr bool NR = FMT == kFmtNar && cmp_agg<AGG>();
+    constexpr bool N4 = NR && AGG == GW_COUNT;
     constexpr bool AV = AGG == GW_AVG_I64 || AGG == GW_AVG_F64;  // (C: a1 = 1, not stored)
     constexpr bool ACC = !(C && AGG == GW_COUNT);
     __shared__ uint32_t r_cnt[kApplyRuns], r_src[kApplyRuns];  // buffer offsets < 2^32 (gw_runtime.cpp)
@@ -870,6 +933,7 @@ __global__ void __launch_bounds__(kApplyThreads) GW_APPLY_ATTR k_rgn_apply(Inges
     const int64_t* ra1 = single ? a.p1_a1 : a.e_a1;
     const uint8_t* rpos = single ? a.p1_pos : a.e_pos;
     const int32_t* rv32 = reinterpret_cast<const int32_t*>(ra0);  // C: 32-bit values
+    const uint32_t* rk32 = reinterpret_cast<const uint32_t*>(rk);  // N4: 4-byte records
     const uint64_t bucket_id = (uint64_t)bucket;                 // C: the hash's top d1 bits
     long long* lkeys = (long long*)smem;
     const int64_t MW = pt_mask_words(a.t);       // 0 unless M
@@ -1050,9 +1114,12 @@ __global__ void __launch_bounds__(kApplyThreads) GW_APPLY_ATTR k_rgn_apply(Inges
                 // unconditional loads (an idle lane reads record 0): no branch around them,
                 // so the compiler can count them and wait for exactly the ones it needs
                 const uint32_t x = s.ok[q] ? sb + (e - sp) : 0u;
-                s.key[q] = rk[x];
+                s.key[q] = N4 ? (int64_t)rk32[x] : rk[x];
                 s.v1[q] = 1;
-                if constexpr (C) {
+                if constexpr (NR) {
+                    s.v0[q] = 1;  // decoded in apply_step
+                    s.ps[q] = 0;
+                } else if constexpr (C) {
                     s.v0[q] = ACC ? (int64_t)rv32[x] : 1;
                     s.ps[q] = 0;  // in the word
                 } else {
@@ -1080,15 +1147,56 @@ __global__ void __launch_bounds__(kApplyThreads) GW_APPLY_ATTR k_rgn_apply(Inges
         // in flight, which would wait for them): while one step is applied, the other's
         // loads are outstanding.  The loads are issued unconditionally, past the end as
         // well, so the compiler can count the outstanding ones on every path.
+        // Fast path first: every record's home group (4 hashes, 32 B) is read with all the
+        // step's LDS loads in flight together; a record whose key sits in its home group and
+        // whose pane is active -- nearly all of them once the keys are in -- adds at once.
+        // The rest (an insert, a key displaced beyond its group, a spill) take the generic
+        // probe.  The table never holds an empty slot before a key in the key's probe order,
+        // so a key found in its home group is exactly the slot the generic probe would pick.
         auto apply_step = [&](const Step& c) {
+            uint64_t h[kApplyUnroll];
+            uint32_t ps[kApplyUnroll];
+            int g[kApplyUnroll];
+            long2 ka[kApplyUnroll], kb[kApplyUnroll];
+            int64_t v0[kApplyUnroll];
+#pragma unroll
+            for (int q = 0; q < kApplyUnroll; ++q) {
+                v0[q] = c.v0[q];
+                if constexpr (NR) {
+                    const uint64_t r = (uint64_t)c.key[q];
+                    h[q] = slot_hash(N4 ? nar_key32((uint32_t)r) : nar_key(r));
+                    ps[q] = nar_pos(N4 ? (uint32_t)r : (uint32_t)(r >> 32));
+                    if constexpr (!N4) v0[q] = nar_val(r);
+                } else if constexpr (C) {
+                    h[q] = cmp_hash((uint64_t)c.key[q], bucket_id, a.d1_bits);
+                    ps[q] = cmp_pos((uint64_t)c.key[q], a.d1_bits);
+                } else {
+                    h[q] = slot_hash(c.key[q]);
+                    ps[q] = c.ps[q];
+                }
+                g[q] = (int)pt_home(a.t, h[q]);
+            }
+#pragma unroll
+            for (int q = 0; q < kApplyUnroll; ++q) {
+                ka[q] = *reinterpret_cast<const long2*>(&lkeys[g[q]]);
+                kb[q] = *reinterpret_cast<const long2*>(&lkeys[g[q] + 2]);
+            }
 #pragma unroll
             for (int q = 0; q < kApplyUnroll; ++q) {
                 if (!c.ok[q]) continue;
-                if constexpr (C) {
-                    const uint64_t h = cmp_hash((uint64_t)c.key[q], bucket_id, a.d1_bits);
-                    apply_one(h, c.v0[q], c.v1[q], cmp_pos((uint64_t)c.key[q], a.d1_bits));
+                const long long key = (long long)h[q];
+                const int i = ka[q].x == key ? 0 : ka[q].y == key ? 1 : kb[q].x == key ? 2 : kb[q].y == key ? 3 : -1;
+                const int ai = (int)ps[q] == act0 ? 0 : ((int)ps[q] == act1 ? 1 : -1);
+                if (i >= 0 && ai >= 0) {
+                    const int found = g[q] + i;
+                    long long* cl = lcell + (ai * (int)S + found) * (AV ? 2 : 1);
+                    lds_cell_add<AGG>(cl, cl + (AV ? 1 : 0), v0[q], c.v1[q]);
+                    if constexpr (M) {
+                        const uint32_t bit = ((uint32_t)found << (msh + 3)) + ps[q];
+                        atomicOr((uint32_t*)lmask + (bit >> 5), 1u << (bit & 31));
+                    }
                 } else {
-                    apply_one(slot_hash(c.key[q]), c.v0[q], c.v1[q], c.ps[q]);
+                    apply_one(h[q], v0[q], c.v1[q], ps[q]);
                 }
             }
         };
@@ -1123,10 +1231,14 @@ __global__ void __launch_bounds__(kApplyThreads) GW_APPLY_ATTR k_rgn_apply(Inges
             for (int i = wave; i < nr; i += nw) {
                 for (uint32_t k = lane; k < r_cnt[i]; k += 64) {
                     const uint32_t x = r_src[i] + k;
-                    int64_t key = rk[x];
+                    int64_t key = N4 ? (int64_t)rk32[x] : rk[x];
                     uint32_t pos;
                     uint64_t h;
-                    if constexpr (C) {
+                    if constexpr (NR) {
+                        const uint64_t r = (uint64_t)key;
+                        h = slot_hash(N4 ? nar_key32((uint32_t)r) : nar_key(r));
+                        pos = nar_pos(N4 ? (uint32_t)r : (uint32_t)(r >> 32));
+                    } else if constexpr (C) {
                         h = cmp_hash((uint64_t)key, bucket_id, a.d1_bits);
                         pos = cmp_pos((uint64_t)key, a.d1_bits);
                     } else {
@@ -1142,7 +1254,9 @@ __global__ void __launch_bounds__(kApplyThreads) GW_APPLY_ATTR k_rgn_apply(Inges
                         g0 = (g0 + 1) & (S - 1);
                     }
                     if (!present || ((int)pos != act0 && (int)pos != act1)) {
-                        if constexpr (C) const_cast<int64_t*>(rk)[x] = (int64_t)((uint64_t)rk[x] | kCmpSpill);
+                        if constexpr (N4) const_cast<uint32_t*>(rk32)[x] = rk32[x] | kNarSpill;
+                        else if constexpr (NR) const_cast<int64_t*>(rk)[x] = (int64_t)((uint64_t)rk[x] | ((uint64_t)kNarSpill << 32));
+                        else if constexpr (C) const_cast<int64_t*>(rk)[x] = (int64_t)((uint64_t)rk[x] | kCmpSpill);
                         else const_cast<uint8_t*>(rpos)[x] = (uint8_t)(pos | 0x80u);
                         marked++;
                     }
@@ -1207,6 +1321,45 @@ __global__ void __launch_bounds__(256) k_rgn_collect_cmp(IngestArgs a) {
                     const uint32_t pos = cmp_pos(w, a.d1_bits);
                     c0 = ACC ? (int64_t)rv32[src + k] : 1;
                     const int64_t rel = ((int64_t)pos - a.b_pos + a.t.ring) % a.t.ring;
+                    pane = a.p_late + (int64_t)a.delta + rel;
+                }
+            }
+            defer_write(a, spill, key, pane, c0, 1);
+        }
+    }
+}
+
+// The same for narrow records (spill bit next to the ring position; the key is the record's).
+template <int AGG>
+__global__ void __launch_bounds__(256) k_rgn_collect_nar(IngestArgs a) {
+    constexpr bool N4 = AGG == GW_COUNT;
+    const int64_t r = blockIdx.x;
+    const int64_t bucket = r >> a.d2_bits, col = r & (((int64_t)1 << a.d2_bits) - 1);
+    const bool single = a.d2_bits == 0;
+    const int64_t rb = single ? 0 : a.rbeg[bucket], re = single ? a.ntiles : a.rbeg[bucket + 1];
+    const int64_t ccol = single ? r : col;
+    const uint32_t* rows = single ? a.p1_row : a.r_row;
+    int64_t* rk = single ? a.p1_key : a.e_key;
+    uint32_t* rk32 = reinterpret_cast<uint32_t*>(rk);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    for (int64_t rnd = rb + wave; rnd < re; rnd += nw) {  // a wave per run: uniform loop bounds
+        const uint32_t d = rows[rnd * kPartBuckets + ccol];
+        const uint32_t cnt = d & 0xffffu;
+        const int64_t src = (single ? rnd * kPartTile : a.r_base[rnd]) + (d >> 16);
+        for (uint32_t k0 = 0; k0 < cnt; k0 += 64) {
+            const uint32_t k = k0 + lane;
+            bool spill = false;
+            int64_t key = 0, pane = 0, c0 = 0;
+            if (k < cnt) {
+                const uint64_t w = N4 ? (uint64_t)rk32[src + k] : (uint64_t)rk[src + k];
+                const uint32_t lo = N4 ? (uint32_t)w : (uint32_t)(w >> 32);
+                if (nar_spilled(lo)) {
+                    spill = true;
+                    if (N4) rk32[src + k] = (uint32_t)w & ~kNarSpill;
+                    else rk[src + k] = (int64_t)(w & ~((uint64_t)kNarSpill << 32));
+                    key = N4 ? nar_key32((uint32_t)w) : nar_key(w);
+                    c0 = N4 ? 1 : nar_val(w);
+                    const int64_t rel = ((int64_t)nar_pos(lo) - a.b_pos + a.t.ring) % a.t.ring;
                     pane = a.p_late + (int64_t)a.delta + rel;
                 }
             }
@@ -1857,7 +2010,8 @@ static void lds_opt_in(const void* f, size_t bytes) {
 }
 
 static size_t part_lds_bytes(const IngestArgs& a) {
-    if (a.cmp) return (size_t)kPartTile * 12;  // hash word + 32-bit value
+    if (a.fmt == kFmtNar) return (size_t)kPartTile * (a.t.agg == GW_COUNT ? 4 : 8);
+    if (a.fmt == kFmtCmp) return (size_t)kPartTile * 12;  // hash word + 32-bit value
     return (size_t)kPartTile * 8 * (a.t.words == 2 ? 3 : 2) + 2 * kPartTile;
 }
 
@@ -1870,22 +2024,22 @@ hipError_t launch_region_p1(const IngestArgs& a, hipStream_t s) {
     const size_t part_lds = part_lds_bytes(a);
     // beyond the 64 KB default: opt in (gfx950 has 160 KB of LDS per CU)
     // the gap test (size < slide) only in a variant of its own: it costs the hot pass ~3%
-#define L(A)                                                                                                    \
-    if (a.gap_size) {                                                                                           \
-        lds_opt_in((const void*)k_rgn_p1<A, false, true>, part_lds);                                           \
-        hipLaunchKernelGGL((k_rgn_p1<A, false, true>), dim3((unsigned)tiles), dim3(kPartThreads), part_lds, s, \
-                           a);                                                                                  \
-    } else if (a.cmp) {                                                                                         \
-        lds_opt_in((const void*)k_rgn_p1<A, true, false>, part_lds);                                           \
-        hipLaunchKernelGGL((k_rgn_p1<A, true, false>), dim3((unsigned)tiles), dim3(kPartThreads), part_lds, s, \
-                           a);                                                                                  \
-    } else {                                                                                                    \
-        lds_opt_in((const void*)k_rgn_p1<A, false, false>, part_lds);                                          \
-        hipLaunchKernelGGL((k_rgn_p1<A, false, false>), dim3((unsigned)tiles), dim3(kPartThreads), part_lds,   \
-                           s, a);                                                                               \
+#define P1L(A, F, G)                                                                                            \
+    lds_opt_in((const void*)k_rgn_p1<A, F, G>, part_lds);                                                      \
+    hipLaunchKernelGGL((k_rgn_p1<A, F, G>), dim3((unsigned)tiles), dim3(kPartThreads), part_lds, s, a)
+#define L(A)                                  \
+    if (a.gap_size) {                         \
+        P1L(A, kFmtWide, true);               \
+    } else if (a.fmt == kFmtNar) {            \
+        P1L(A, kFmtNar, false);               \
+    } else if (a.fmt == kFmtCmp) {            \
+        P1L(A, kFmtCmp, false);               \
+    } else {                                  \
+        P1L(A, kFmtWide, false);              \
     }
     GW_AGG_SWITCH(a.t.agg, L);
 #undef L
+#undef P1L
     return hipGetLastError();
 }
 
@@ -1914,11 +2068,13 @@ hipError_t launch_region_flush(const IngestArgs& a, hipStream_t s) {
                            a);                                                                                  \
     }                                                                                                           \
     hipLaunchKernelGGL((k_rgn_apply<A, CM>), dim3((unsigned)a.t.nreg), dim3(kApplyThreads), apply_lds, s, a)
-#define L(A)            \
-    if (a.cmp) {        \
-        L2(A, true);    \
-    } else {            \
-        L2(A, false);   \
+#define L(A)                        \
+    if (a.fmt == kFmtNar) {         \
+        L2(A, kFmtNar);             \
+    } else if (a.fmt == kFmtCmp) {  \
+        L2(A, kFmtCmp);             \
+    } else {                        \
+        L2(A, kFmtWide);            \
     }
     GW_AGG_SWITCH(a.t.agg, L);
 #undef L
@@ -1929,7 +2085,9 @@ hipError_t launch_region_flush(const IngestArgs& a, hipStream_t s) {
 hipError_t launch_region_collect(const IngestArgs& a, hipStream_t s) {
     const int64_t n = a.ntiles * kPartTile;  // upper bound of the buffer's records
 #define L(A)                                                                                         \
-    if (a.cmp)                                                                                       \
+    if (a.fmt == kFmtNar)                                                                            \
+        hipLaunchKernelGGL(k_rgn_collect_nar<A>, dim3((unsigned)a.t.nreg), dim3(256), 0, s, a);     \
+    else if (a.fmt == kFmtCmp)                                                                       \
         hipLaunchKernelGGL(k_rgn_collect_cmp<A>, dim3((unsigned)a.t.nreg), dim3(256), 0, s, a);     \
     else                                                                                             \
         hipLaunchKernelGGL(k_rgn_collect<A>, dim3(grid_for(n)), dim3(256), 0, s, a)

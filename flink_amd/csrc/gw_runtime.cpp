@@ -221,9 +221,11 @@ struct gw_handle {
     int nseg = 0;
     int64_t buf_tiles = 0;          // tiles used by the waiting segments
     uint64_t buf_fresh = 0;         // ring positions holding only identities at buffer start
-    bool buf_cmp = false;           // the waiting segments use compact records (fixed per window)
+    int buf_fmt = 0;                // record format of the waiting segments (fixed per window):
+                                    // 0 wide, 1 compact, 2 narrow (gw_pane.hip kFmt*)
     int64_t buf_recs = 0;           // records of the waiting segments
     bool cmp_off = false;           // compact records turned off: too many values beyond 32 bits
+    bool nar_off = false;           // narrow records turned off: too many keys / values beyond them
     int64_t buf_limit = (int64_t)1 << 27;  // records (GW_BUFFER_RECORDS)
 
     // allowed lateness > 0 (tumbling / sliding): late records of fired, not yet cleaned
@@ -279,7 +281,7 @@ struct gw_handle {
     DevStatus* h_st = nullptr;
     unsigned long long* d_tmp = nullptr;
 
-    gw_stats stats{};
+    gw_stats stats{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, -1};
     bool timing = false;
     KernelTimer t_ingest, t_fire, t_apply;
     HostProf hp;
@@ -983,7 +985,7 @@ struct gw_handle {
         a.r_row = r_row;
         a.r_base = r_base;
         a.batch_occ = d_tmp + 1;
-        a.cmp = buf_cmp ? 1 : 0;
+        a.fmt = buf_fmt;
     }
 
     // Compact region records (gw_pane.hip cmp_pack): integer aggregates whose ring
@@ -995,6 +997,13 @@ struct gw_handle {
         static const bool env_off = getenv("GW_NO_COMPACT") != nullptr;
         // gapped panes (size < slide) use the wide pass 1, the one instantiated with the gap test
         return int_agg && !cmp_off && !env_off && !gap_size && d1_bits >= 2 && (int64_t)tv.ring <= ((int64_t)1 << (d1_bits - 1));
+    }
+    // Narrow records (32-bit keys, 28-bit values, ring positions < 8) where compact ones fit
+    // and no window has overflowed them yet (GW_NO_NARROW turns them off).
+    int region_fmt(int d1_bits) const {
+        if (!compact_ok(d1_bits)) return 0;
+        static const bool nar_env_off = getenv("GW_NO_NARROW") != nullptr;
+        return (!nar_off && !nar_env_off && !(cfg.flags & GW_FLAG_NO_NARROW) && tv.ring <= 8) ? 2 : 1;
     }
 
     // P2 + apply over every waiting segment (one fire's worth of batches).  Runs before
@@ -1026,8 +1035,11 @@ struct gw_handle {
         stats.applies++;
         dirty = true;
         if ((rc = refresh())) return rc;
-        if (h_st->wide_vals) {  // values beyond 32 bits went the deferred way: keep it rare
-            if (h_st->wide_vals * 64 > (unsigned long long)window_recs) cmp_off = true;
+        if (h_st->wide_vals) {  // records beyond the window's format went the deferred way: keep it rare
+            if (h_st->wide_vals * 64 > (unsigned long long)window_recs) {
+                if (a.fmt == 2) nar_off = true;
+                else cmp_off = true;
+            }
             if ((rc = set_field(offsetof(DevStatus, wide_vals), 0))) return rc;
         }
         if (h_st->spills) {  // full regions / a third ring position left records: park them
@@ -1089,9 +1101,10 @@ struct gw_handle {
             if (nseg == 0) {
                 HIPCHECK(hipMemsetAsync(d_tmp + 1, 0, 8, stream));
                 buf_fresh = ~occ;
-                buf_cmp = compact_ok(a.d1_bits);
+                buf_fmt = region_fmt(a.d1_bits);
             }
-            a.cmp = buf_cmp ? 1 : 0;
+            a.fmt = buf_fmt;
+            stats.region_format = buf_fmt;
             if (buffered) arm_status(a);
             hp.lap(0);
             if (timing) {
@@ -3408,6 +3421,7 @@ int gw_get_stats(const gw_handle* h, gw_stats* out) {
             t.rehashes += k.rehashes;
             t.preagg_batches += k.preagg_batches;
             t.applies += k.applies;
+            t.region_format = k.region_format;
         }
         *out = t;
         return GW_OK;

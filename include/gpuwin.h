@@ -124,6 +124,7 @@ typedef struct gw_config {
                                         buffering pass-1 segments until the next fire    */
 #define GW_FLAG_LATE_SIDE_OUTPUT  64 /* WindowedStream.sideOutputLateData: late records go to
                                         gw_drain_late instead of numLateRecordsDropped    */
+#define GW_FLAG_NO_NARROW        256 /* region path: never narrow records (compact or wide only) */
 #define GW_FLAG_FIRST_ELEMENT    128 /* positional sum/min/max (WindowedStream.sum(i) etc.):
                                         records carry a 64-bit payload (the tuple's other
                                         fields, packed by the caller) and every row carries the
@@ -148,6 +149,9 @@ typedef struct gw_stats {
     int64_t preagg_batches;   /* batches that used the LDS pre-aggregation kernel  */
     int64_t session_merges;   /* sessions merged away (M_b)                        */
     int64_t applies;          /* region pass-2 + apply launches (buffer flushes)   */
+    int64_t region_format;    /* record format of the last region flush window: 0 wide,
+                                 1 compact (hash word + 32-bit value), 2 narrow (32-bit
+                                 key + 28-bit value; 4 B for COUNT); -1 none yet       */
 } gw_stats;
 
 /* ---- lifecycle ------------------------------------------------------------ */
