@@ -49,7 +49,7 @@ EXPORTS = [
     "gw_exchange_unique_id", "gw_exchange_create", "gw_exchange_destroy", "gw_exchange_batch",
     "gw_exchange_min_watermark", "gw_exchange_last_error", "gw_exchange_counts",
     "gw_ingest_payload", "gw_ingest_payload_device", "gw_drain_payload",
-    "gw_snapshot_keys", "gw_snapshot_remap_keys",
+    "gw_snapshot_keys", "gw_snapshot_remap_keys", "gw_snapshot_payloads", "gw_snapshot_remap_payloads",
 ]
 EXCHANGE_ID_BYTES = 128
 
@@ -145,6 +145,8 @@ def lib() -> ctypes.CDLL:
         "gw_snapshot_slice": (c_int, [p, i64, i32, p, i64, P64]),
         "gw_snapshot_keys": (c_int, [p, i64, p, i64, P64]),
         "gw_snapshot_remap_keys": (c_int, [p, i64, p, p, i64]),
+        "gw_snapshot_payloads": (c_int, [p, i64, p, i64, P64, P64]),
+        "gw_snapshot_remap_payloads": (c_int, [p, i64, p, p, i64]),
         "gw_end_input": (c_int, [p, P64]),
         "gw_pending_rows": (c_int, [p, P64]),
         "gw_drain": (c_int, [p, p, p, p, p, i64, P64]),

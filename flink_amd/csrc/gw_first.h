@@ -21,6 +21,8 @@ hipError_t fe_max_ts(const int64_t* ts, int64_t n, int64_t* out, hipStream_t s);
 // Copy the live sequences [base, end) of a log ring of ocap words into one of ncap words.
 hipError_t fe_log_regrow(const int64_t* o, int64_t ocap, int64_t* d, int64_t ncap, int64_t base, int64_t end,
                          hipStream_t s);
+// out[i] = log[seq[i] mod cap] (the payloads of a snapshot's first elements).
+hipError_t fe_log_gather(const int64_t* log, int64_t cap, const int64_t* seq, int64_t n, int64_t* out, hipStream_t s);
 // Append n payload words at log position pos (a ring of cap words).
 hipError_t fe_log_append(int64_t* log, int64_t cap, int64_t pos, const int64_t* src, int64_t n, hipStream_t s);
 }  // namespace gw

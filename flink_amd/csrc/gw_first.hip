@@ -78,6 +78,11 @@ __global__ void k_fe_zip(int64_t n, const uint32_t* pa, const uint32_t* pb, cons
     }
 }
 
+__global__ void k_fe_gather_log(const int64_t* log, int64_t cap, const int64_t* seq, int64_t n, int64_t* out) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        out[i] = log[seq[i] % cap];
+}
+
 // Copy the live log [base, end) from a ring of ocap words into a ring of ncap words.
 __global__ void k_fe_recopy(const int64_t* o, int64_t ocap, int64_t* d, int64_t ncap, int64_t base, int64_t end) {
     for (int64_t q = base + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; q < end; q += (int64_t)gridDim.x * blockDim.x)
@@ -87,6 +92,12 @@ __global__ void k_fe_recopy(const int64_t* o, int64_t ocap, int64_t* d, int64_t 
 static unsigned grid_n(int64_t n) {
     int64_t g = (n + 255) / 256;
     return (unsigned)std::max<int64_t>(1, std::min<int64_t>(g, 4096));
+}
+
+hipError_t fe_log_gather(const int64_t* log, int64_t cap, const int64_t* seq, int64_t n, int64_t* out, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_fe_gather_log, dim3(grid_n(n)), dim3(256), 0, s, log, cap, seq, n, out);
+    return hipGetLastError();
 }
 
 size_t fe_join_scratch_bytes(int64_t n) {

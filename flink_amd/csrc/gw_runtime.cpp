@@ -34,6 +34,7 @@ thread_local std::string g_create_error;
 constexpr int64_t kMaxIngest = (int64_t)1 << 30;
 constexpr uint32_t kSnapMaxVersion = 4;  // gw_handle::SnapHeader versions
 constexpr int64_t kSnapKeyHashes = 1;    // SnapHeader::flags
+constexpr int64_t kSnapFirstElement = 2; // SnapHeader::flags: v4 entries end with the first element's payload
 
 // Host-time profile of the ingest path (GW_HOST_PROFILE=1: printed by gw_destroy).
 struct HostProf {
@@ -2333,6 +2334,30 @@ static int fe_release(gw_handle* h) {
     return GW_OK;
 }
 
+// Room in the payload log (a ring of the live sequences [fe_log_base, fe_seq + n)) for n
+// more sequences: release what no window needs any more, then grow.
+static int fe_log_reserve(gw_handle* h, int64_t n) {
+    hipStream_t s = h->stream;
+    if (h->fe_seq + n - h->fe_log_base > h->fe_log_cap || (int64_t)h->fe_batches.size() >= gw_handle::kFeBatches - 1) {
+        const int rc = fe_release(h);
+        if (rc) return rc;
+    }
+    const int64_t need = h->fe_seq + n - h->fe_log_base;
+    if (need > h->fe_log_cap) {
+        const int64_t ncap = std::max<int64_t>(2 * need, 1 << 20);
+        int64_t* nl = nullptr;
+        if (hipMalloc((void**)&nl, (size_t)ncap * 8) != hipSuccess) return h->fail(GW_E_OOM, "payload log");
+        hipError_t e = hipSuccess;
+        if (h->fe_log) e = fe_log_regrow(h->fe_log, h->fe_log_cap, nl, ncap, h->fe_log_base, h->fe_seq, s);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        if (h->fe_log) hipFree(h->fe_log);
+        h->fe_log = nl;
+        h->fe_log_cap = ncap;
+        if (e != hipSuccess) return h->fail(GW_E_DEVICE, "payload log: %s", hipGetErrorString(e));
+    }
+    return GW_OK;
+}
+
 int gw_ingest_payload_device(gw_handle* h, int64_t n, const int64_t* d_key, const int32_t* d_key_hash,
                              const int64_t* d_ts, const void* d_value, const int64_t* d_payload, void* stream) {
     if (!h) return GW_E_INVALID;
@@ -2357,23 +2382,11 @@ int gw_ingest_payload_device(gw_handle* h, int64_t n, const int64_t* d_key, cons
         h->fe_seqbuf_cap = n;
     }
     hipError_t e = fe_iota64(h->fe_seqbuf, n, h->fe_seq, s);
-    // payload log: a ring of the live sequences [fe_log_base, fe_seq + n)
-    if (h->fe_seq + n - h->fe_log_base > h->fe_log_cap || (int64_t)h->fe_batches.size() >= gw_handle::kFeBatches - 1) {
-        const int rc = fe_release(h);
+    if (e == hipSuccess) {
+        const int rc = fe_log_reserve(h, n);
         if (rc) return rc;
+        e = fe_log_append(h->fe_log, h->fe_log_cap, h->fe_seq, d_payload, n, s);
     }
-    const int64_t need = h->fe_seq + n - h->fe_log_base;
-    if (e == hipSuccess && need > h->fe_log_cap) {
-        const int64_t ncap = std::max<int64_t>(2 * need, 1 << 20);
-        int64_t* nl = nullptr;
-        if (hipMalloc((void**)&nl, (size_t)ncap * 8) != hipSuccess) return h->fail(GW_E_OOM, "payload log");
-        if (h->fe_log) e = fe_log_regrow(h->fe_log, h->fe_log_cap, nl, ncap, h->fe_log_base, h->fe_seq, s);
-        if (e == hipSuccess) e = hipStreamSynchronize(s);
-        if (h->fe_log) hipFree(h->fe_log);
-        h->fe_log = nl;
-        h->fe_log_cap = ncap;
-    }
-    if (e == hipSuccess) e = fe_log_append(h->fe_log, h->fe_log_cap, h->fe_seq, d_payload, n, s);
     if ((int64_t)h->fe_batches.size() >= gw_handle::kFeBatches - 1)
         return h->fail(GW_E_STATE, "first-element log: too many batches without a watermark");
     const int64_t slot = h->fe_batch_no % gw_handle::kFeBatches;
@@ -2972,9 +2985,194 @@ static int comp_restore(gw_handle* h, const void* buf, int64_t len) {
     return GW_OK;
 }
 
+#define HIPCHECK_H(h, x)                                                                                  \
+    do {                                                                                                  \
+        hipError_t e_ = (x);                                                                              \
+        if (e_ != hipSuccess) return (h)->fail(GW_E_DEVICE, "%s failed: %s", #x, hipGetErrorString(e_)); \
+    } while (0)
+
+// ---- first-element handles: one heap-layout blob for both operators -------------------
+// The reference keeps one reduced Tuple per (key, window): the window's first element with
+// the aggregated field replaced (HeapReducingState.java:90-97, SumAggregator /
+// ComparableAggregator).  The blob holds exactly that per entry: (window, key, [hash],
+// aggregate, payload of the first element) with flags |= kSnapFirstElement, and kids[0]'s
+// timers.  A restore gives the restored first elements new arrival sequences: their payloads
+// go to the log, kids[1] gets (window, key, new sequence) entries.
+static int fe_snapshot(gw_handle* h, int32_t kg_lo, int32_t kg_hi, void* buf, int64_t cap, int64_t* len) {
+    gw_handle *A = h->kids[0], *B = h->kids[1];
+    std::vector<uint8_t> ba, bb;
+    for (auto pr : {std::make_pair(A, &ba), std::make_pair(B, &bb)}) {
+        int64_t l = 0;
+        int rc = gw_snapshot(pr.first, kg_lo, kg_hi, nullptr, 0, &l);
+        if (rc) return kid_rc(h, pr.first, rc);
+        pr.second->resize((size_t)l);
+        if ((rc = gw_snapshot(pr.first, kg_lo, kg_hi, pr.second->data(), l, &l))) return kid_rc(h, pr.first, rc);
+    }
+    SnapHdr ha, hb;
+    memcpy(&ha, ba.data(), sizeof ha);
+    memcpy(&hb, bb.data(), sizeof hb);
+    if (ha.version != 4 || hb.version != 4 || ha.flags != hb.flags)
+        return h->fail(GW_E_STATE, "first-element snapshot: the operators' blobs differ");
+    const int64_t nk = (int64_t)kg_hi - kg_lo + 1, hdr = (int64_t)sizeof(SnapHdr) + (nk + 1) * 8;
+    const int kb = (ha.flags & kSnapKeyHashes) ? 4 : 0;
+    const int64_t ea = 24 + kb + A->acc_bytes(), eb = 24 + kb + 8;  // B: MIN_I64 of the sequence
+    // pass 1: the sequences of every entry's first element, in entry order
+    std::vector<int64_t> seqs;
+    struct Sec { const uint8_t *sa, *sb, *ta; int32_t n, t; };
+    std::vector<Sec> secs((size_t)nk);
+    for (int64_t g = 0; g < nk; ++g) {
+        int64_t oa, ob;
+        memcpy(&oa, ba.data() + sizeof(SnapHdr) + g * 8, 8);
+        memcpy(&ob, bb.data() + sizeof(SnapHdr) + g * 8, 8);
+        const uint8_t* pa = ba.data() + hdr + oa;
+        const uint8_t* pb = bb.data() + hdr + ob;
+        Sec sc{};
+        sc.n = gw_handle::rd32(pa);
+        if (gw_handle::rd32(pb) != sc.n) return h->fail(GW_E_STATE, "first-element snapshot: entries differ");
+        sc.sa = pa + 4;
+        sc.sb = pb + 4;
+        for (int32_t i = 0; i < sc.n; ++i) {
+            const uint8_t* xa = sc.sa + i * ea;
+            const uint8_t* xb = sc.sb + i * eb;
+            if (memcmp(xa, xb, 24 + kb) != 0) return h->fail(GW_E_STATE, "first-element snapshot: entries differ");
+            seqs.push_back(gw_handle::rd64(xb + 24 + kb));
+        }
+        sc.ta = sc.sa + sc.n * ea + 4;  // past the (empty) merging window set
+        sc.t = gw_handle::rd32(sc.ta);
+        sc.ta += 4;
+        secs[g] = sc;
+    }
+    std::vector<int64_t> pays(seqs.size());
+    if (!seqs.empty()) {
+        for (int64_t q : seqs)
+            if (q < h->fe_log_base || q >= h->fe_seq) return h->fail(GW_E_STATE, "first-element snapshot: payload released");
+        int64_t* d = nullptr;
+        HIPCHECK_H(h, hipMalloc((void**)&d, seqs.size() * 16));
+        hipError_t e = hipMemcpyAsync(d, seqs.data(), seqs.size() * 8, hipMemcpyHostToDevice, h->stream);
+        if (e == hipSuccess) e = fe_log_gather(h->fe_log, h->fe_log_cap, d, (int64_t)seqs.size(), d + seqs.size(), h->stream);
+        if (e == hipSuccess) e = hipMemcpyAsync(pays.data(), d + seqs.size(), seqs.size() * 8, hipMemcpyDeviceToHost, h->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+        hipFree(d);
+        if (e != hipSuccess) return h->fail(GW_E_DEVICE, "first-element snapshot: %s", hipGetErrorString(e));
+    }
+    // pass 2: the blob
+    std::vector<uint8_t> pay;
+    std::vector<int64_t> offs(nk + 1, 0);
+    size_t q = 0;
+    for (int64_t g = 0; g < nk; ++g) {
+        const Sec& sc = secs[g];
+        offs[g] = (int64_t)pay.size();
+        gw_handle::be32(pay, sc.n);
+        for (int32_t i = 0; i < sc.n; ++i) {
+            const uint8_t* xa = sc.sa + i * ea;
+            pay.insert(pay.end(), xa, xa + ea);
+            gw_handle::be64(pay, pays[q++]);
+        }
+        gw_handle::be32(pay, 0);
+        gw_handle::be32(pay, sc.t);
+        pay.insert(pay.end(), sc.ta, sc.ta + (size_t)sc.t * 32);
+    }
+    offs[nk] = (int64_t)pay.size();
+    *len = hdr + (int64_t)pay.size();
+    if (!buf) return GW_OK;
+    if (cap < *len) return h->fail(GW_E_OUTPUT_FULL, "snapshot needs %lld bytes", (long long)*len);
+    SnapHdr hd = ha;
+    hd.agg = h->cfg.agg;
+    hd.flags |= kSnapFirstElement;
+    hd.entries = (int64_t)pay.size();
+    char* out = (char*)buf;
+    memcpy(out, &hd, sizeof hd);
+    memcpy(out + sizeof hd, offs.data(), (size_t)(nk + 1) * 8);
+    if (!pay.empty()) memcpy(out + hdr, pay.data(), pay.size());
+    return GW_OK;
+}
+
+static int fe_restore(gw_handle* h, const void* buf, int64_t len) {
+    if (!buf || len < (int64_t)sizeof(SnapHdr)) return h->fail(GW_E_INVALID, "snapshot blob too short");
+    SnapHdr hd;
+    memcpy(&hd, buf, sizeof hd);
+    if (memcmp(hd.magic, "GWS1", 4) != 0 || hd.version != 4 || !(hd.flags & kSnapFirstElement) || hd.agg != h->cfg.agg)
+        return h->fail(GW_E_INVALID, "not a first-element snapshot of this aggregate");
+    gw_handle *A = h->kids[0], *B = h->kids[1];
+    const int64_t nk = (int64_t)hd.kg_hi - hd.kg_lo + 1, hdr = (int64_t)sizeof hd + (nk + 1) * 8;
+    if (nk <= 0 || hd.entries < 0 || len < hdr || hd.entries > len - hdr)
+        return h->fail(GW_E_INVALID, "truncated snapshot blob");
+    const int kb = (hd.flags & kSnapKeyHashes) ? 4 : 0;
+    const int64_t ea = 24 + kb + A->acc_bytes(), ef = ea + 8;
+    const uint8_t* p = (const uint8_t*)buf + hdr;
+    const uint8_t* end = p + hd.entries;
+    std::vector<uint8_t> pa, pb;
+    std::vector<int64_t> oa(nk + 1), ob(nk + 1), pays;
+    int64_t max_end = INT64_MIN;
+    const int64_t seq0 = h->fe_seq;
+    for (int64_t g = 0; g < nk; ++g) {
+        oa[g] = (int64_t)pa.size();
+        ob[g] = (int64_t)pb.size();
+        if (end - p < 4) return h->fail(GW_E_INVALID, "truncated snapshot blob");
+        const int32_t n = gw_handle::rd32(p);
+        p += 4;
+        if (n < 0 || (int64_t)n * ef + 8 > end - p) return h->fail(GW_E_INVALID, "truncated snapshot blob");
+        gw_handle::be32(pa, n);
+        gw_handle::be32(pb, n);
+        for (int32_t i = 0; i < n; ++i, p += ef) {
+            pa.insert(pa.end(), p, p + ea);
+            pb.insert(pb.end(), p, p + 24 + kb);
+            gw_handle::be64(pb, seq0 + (int64_t)pays.size());  // the restored first element's new sequence
+            pays.push_back(gw_handle::rd64(p + ea));
+            max_end = std::max(max_end, gw_handle::rd64(p + 8));
+        }
+        if (gw_handle::rd32(p) != 0) return h->fail(GW_E_INVALID, "merging window set in a first-element snapshot");
+        p += 4;
+        const int32_t t = gw_handle::rd32(p);
+        p += 4;
+        if (t < 0 || (int64_t)t * 32 > end - p) return h->fail(GW_E_INVALID, "truncated snapshot blob");
+        for (std::vector<uint8_t>* v : {&pa, &pb}) {
+            gw_handle::be32(*v, 0);
+            gw_handle::be32(*v, t);
+            v->insert(v->end(), p, p + (size_t)t * 32);
+        }
+        p += (size_t)t * 32;
+    }
+    if (p != end) return h->fail(GW_E_INVALID, "snapshot blob has trailing bytes");
+    oa[nk] = (int64_t)pa.size();
+    ob[nk] = (int64_t)pb.size();
+    // the payloads enter the log as one batch released once every restored window is cleaned
+    const int64_t m = (int64_t)pays.size();
+    if (m) {
+        int rc = fe_log_reserve(h, m);
+        if (rc) return rc;
+        int64_t* d = nullptr;
+        HIPCHECK_H(h, hipMalloc((void**)&d, (size_t)m * 8));
+        hipError_t e = hipMemcpy(d, pays.data(), (size_t)m * 8, hipMemcpyHostToDevice);
+        if (e == hipSuccess) e = fe_log_append(h->fe_log, h->fe_log_cap, h->fe_seq, d, m, h->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+        hipFree(d);
+        if (e != hipSuccess) return h->fail(GW_E_DEVICE, "first-element restore: %s", hipGetErrorString(e));
+        h->fe_seq += m;
+        // released like a batch whose records reach the latest restored window: maxTs + size - 1 = its end - 1
+        h->fe_batches.push_back({h->fe_seq, 0, max_end - h->cfg.size, true});
+    }
+    for (int w = 0; w < 2; ++w) {
+        std::vector<uint8_t>& pl = w ? pb : pa;
+        std::vector<int64_t>& of = w ? ob : oa;
+        SnapHdr kh = hd;
+        kh.flags &= ~kSnapFirstElement;
+        kh.agg = w ? GW_MIN_I64 : h->cfg.agg;
+        kh.entries = (int64_t)pl.size();
+        std::vector<uint8_t> blob(sizeof kh + (size_t)(nk + 1) * 8 + pl.size());
+        memcpy(blob.data(), &kh, sizeof kh);
+        memcpy(blob.data() + sizeof kh, of.data(), (size_t)(nk + 1) * 8);
+        if (!pl.empty()) memcpy(blob.data() + sizeof kh + (nk + 1) * 8, pl.data(), pl.size());
+        gw_handle* kid = w ? B : A;
+        const int rc = gw_restore(kid, blob.data(), (int64_t)blob.size());
+        if (rc) return kid_rc(h, kid, rc);
+    }
+    return GW_OK;
+}
+
 int gw_snapshot(gw_handle* h, int32_t kg_lo, int32_t kg_hi, void* buf, int64_t cap, int64_t* len) {
     if (!h || !len) return GW_E_INVALID;
-    if (h->fe) return h->fail(GW_E_UNSUPPORTED, "snapshots of first-element rows are not supported");
+    if (h->fe) return fe_snapshot(h, kg_lo, kg_hi, buf, cap, len);
     if (!h->kids.empty()) return comp_snapshot(h, kg_lo, kg_hi, buf, cap, len);
     if (h->failed) return h->fail(GW_E_STATE, "operator failed earlier: %s", h->err.c_str());
     hipSetDevice(h->cfg.device);
@@ -2984,7 +3182,7 @@ int gw_snapshot(gw_handle* h, int32_t kg_lo, int32_t kg_hi, void* buf, int64_t c
 
 int gw_restore(gw_handle* h, const void* buf, int64_t len) {
     if (!h) return GW_E_INVALID;
-    if (h->fe) return h->fail(GW_E_UNSUPPORTED, "snapshots of first-element rows are not supported");
+    if (h->fe) return fe_restore(h, buf, len);
     if (!h->kids.empty()) return comp_restore(h, buf, len);
     if (h->failed) return h->fail(GW_E_STATE, "operator failed earlier: %s", h->err.c_str());
     hipSetDevice(h->cfg.device);
@@ -3059,7 +3257,7 @@ static bool blob_keys(const uint8_t* b, int64_t len, F&& f) {
     }
     if (hd.entries > len - pay0) return false;
     const uint8_t* end = p + hd.entries;
-    const int64_t eb = 24 + ((hd.flags & kSnapKeyHashes) ? 4 : 0) +
+    const int64_t eb = 24 + ((hd.flags & kSnapKeyHashes) ? 4 : 0) + ((hd.flags & kSnapFirstElement) ? 8 : 0) +
                        (hd.agg == GW_SUM_I32 ? 4 : (hd.agg == GW_AVG_I64 || hd.agg == GW_AVG_F64) ? 16 : 8);
     for (int64_t g = 0; g < nk; ++g) {
         if (end - p < 4) return false;
@@ -3094,6 +3292,77 @@ static int64_t key_at(const uint8_t* p, bool be) {
 }
 
 }  // extern "C++"
+
+extern "C++" {
+// Calls f(payload field, window end) for every entry of a first-element blob; false for a
+// corrupt blob or one without payloads.
+template <class F>
+static bool blob_payloads(const uint8_t* b, int64_t len, F&& f) {
+    typedef gw_handle::SnapHeader H;
+    H hd;
+    if (!b || len < (int64_t)sizeof hd) return false;
+    memcpy(&hd, b, sizeof hd);
+    if (memcmp(hd.magic, "GWS1", 4) != 0 || hd.version != 4 || !(hd.flags & kSnapFirstElement)) return false;
+    const int64_t acc = hd.agg == GW_SUM_I32 ? 4 : (hd.agg == GW_AVG_I64 || hd.agg == GW_AVG_F64) ? 16 : 8;
+    const int64_t at = 24 + ((hd.flags & kSnapKeyHashes) ? 4 : 0) + acc, eb = at + 8;
+    const int64_t nk = (int64_t)hd.kg_hi - hd.kg_lo + 1, pay0 = (int64_t)sizeof hd + (nk + 1) * 8;
+    if (nk <= 0 || hd.entries < 0 || len < pay0 || hd.entries > len - pay0) return false;
+    const uint8_t* p = b + pay0;
+    const uint8_t* end = p + hd.entries;
+    for (int64_t g = 0; g < nk; ++g) {
+        if (end - p < 4) return false;
+        const int32_t n = gw_handle::rd32(p);
+        p += 4;
+        if (n < 0 || (int64_t)n * eb + 8 > end - p) return false;
+        for (int32_t i = 0; i < n; ++i, p += eb) f(p + at, gw_handle::rd64(p + 8));
+        p += 4;  // (empty) merging window set
+        const int32_t t = gw_handle::rd32(p);
+        p += 4;
+        if (t < 0 || (int64_t)t * 32 > end - p) return false;
+        p += (int64_t)t * 32;
+    }
+    return p == end;
+}
+
+}  // extern "C++"
+
+int gw_snapshot_payloads(const void* blob, int64_t len, int64_t* payloads, int64_t cap, int64_t* n,
+                         int64_t* max_window_end) {
+    if (!n) return GW_E_INVALID;
+    std::vector<int64_t> ps;
+    int64_t mx = INT64_MIN;
+    if (!blob_payloads((const uint8_t*)blob, len, [&](const uint8_t* p, int64_t e) {
+            ps.push_back(gw_handle::rd64(p));
+            mx = std::max(mx, e);
+        })) {
+        g_create_error = "not a first-element snapshot blob";
+        return GW_E_INVALID;
+    }
+    std::sort(ps.begin(), ps.end());
+    ps.erase(std::unique(ps.begin(), ps.end()), ps.end());
+    *n = (int64_t)ps.size();
+    if (max_window_end) *max_window_end = mx;
+    if (!payloads) return GW_OK;
+    if (cap < *n) { g_create_error = "payload buffer too small"; return GW_E_OUTPUT_FULL; }
+    if (!ps.empty()) memcpy(payloads, ps.data(), ps.size() * 8);
+    return GW_OK;
+}
+
+int gw_snapshot_remap_payloads(void* blob, int64_t len, const int64_t* from, const int64_t* to, int64_t n) {
+    if (n < 0 || (n > 0 && (!from || !to))) { g_create_error = "null payload map"; return GW_E_INVALID; }
+    for (int64_t i = 1; i < n; ++i)
+        if (from[i] <= from[i - 1]) { g_create_error = "remap payloads: from[] not ascending"; return GW_E_INVALID; }
+    const bool ok = blob_payloads((const uint8_t*)blob, len, [&](const uint8_t* cp, int64_t) {
+        uint8_t* p = const_cast<uint8_t*>(cp);
+        const int64_t v = gw_handle::rd64(p);
+        const int64_t* it = std::lower_bound(from, from + n, v);
+        if (it == from + n || *it != v) return;
+        const int64_t w = to[it - from];
+        for (int i = 0; i < 8; ++i) p[i] = (uint8_t)((uint64_t)w >> (56 - 8 * i));
+    });
+    if (!ok) { g_create_error = "not a first-element snapshot blob"; return GW_E_INVALID; }
+    return GW_OK;
+}
 
 int gw_snapshot_keys(const void* blob, int64_t len, int64_t* keys, int64_t cap, int64_t* n) {
     if (!n) return GW_E_INVALID;

@@ -237,6 +237,15 @@ int  gw_snapshot_keys(const void* blob, int64_t len, int64_t* keys, int64_t cap,
 /* Rewrite in place every key of the blob found in from[0..n) (ascending) to the matching
  * to[i]; key hashes stay.  GW_E_INVALID for a corrupt blob or unsorted from[]. */
 int  gw_snapshot_remap_keys(void* blob, int64_t len, const int64_t* from, const int64_t* to, int64_t n);
+/* First-element handles (GW_FLAG_FIRST_ELEMENT): their blob's version-4 entries end with the
+ * be64 payload of the window's first element (header flags bit 1).  gw_snapshot_payloads
+ * lists the distinct payloads ascending (payloads == NULL: only the count) and the latest
+ * window end among the entries -- what the caller needs to write the elements beside the
+ * blob and to keep them after a restore until those windows are cleaned;
+ * gw_snapshot_remap_payloads rewrites them to a restoring process's own ids. */
+int  gw_snapshot_payloads(const void* blob, int64_t len, int64_t* payloads, int64_t cap, int64_t* n,
+                          int64_t* max_window_end);
+int  gw_snapshot_remap_payloads(void* blob, int64_t len, const int64_t* from, const int64_t* to, int64_t n);
 
 /* ---- network-buffer ingest ----------------------------- */
 /* Layout of the record value: a Flink Tuple of fixed-width fields as TupleSerializer

@@ -90,12 +90,14 @@ public class GpuWindowOperator<IN, K>
     private final ToDoubleFunction<IN> doubleValue;   // for f64 aggregates
     private final int batchCapacity;
     private final int inputArity, positionalField;
+    private TypeSerializer<IN> inputSerializer;  // Tuple3+ positional: writes the first elements of a snapshot
 
     private transient long handle;
     private transient ByteBuffer keys, keyHashes, ts, values, oKey, oStart, oEnd, oRes;
     private transient int n;
     private transient List<byte[]> restored;  // per-key-group blobs read in initializeState
     private transient List<Map<Long, K>> restoredKeys;  // their key tables (non-Long keys)
+    private transient List<Map<Long, IN>> restoredElements;  // their first elements (Tuple3+ positional)
     private transient KeyDictionary<K> dict;  // null while every key so far is a Long
     private transient boolean longKeys;       // decided by the first key
     private transient boolean keyModeKnown;
@@ -128,6 +130,13 @@ public class GpuWindowOperator<IN, K>
         this.batchCapacity = batchCapacity; this.mode = mode;
     }
 
+    /** The input type's serializer (TypeInformation.createSerializer): a Tuple3+ positional
+     *  operator writes each window's first element with it when it checkpoints. */
+    public GpuWindowOperator<IN, K> withInputSerializer(TypeSerializer<IN> serializer) {
+        this.inputSerializer = serializer;
+        return this;
+    }
+
     /** WindowedStream.sideOutputLateData (WindowOperator.java:440-446, 587-588) for a Tuple2<Long, X>
      *  input: skipped late elements come back as (key, value) with their timestamp. */
     public GpuWindowOperator<IN, K> withLateDataOutput(OutputTag<Tuple2<Object, Object>> tag) {
@@ -151,6 +160,11 @@ public class GpuWindowOperator<IN, K>
         handle = nativeCreate(assigner, trigger, size, slide, offset, gap, lateness, agg, maxP, parallelism,
                               subtask, device, flags, 1L << 24, batchCapacity);
         if (lateDataTag != null) { lKey = direct(8); lTs = direct(8); lVal = direct(8); }
+        if (wide() && inputSerializer == null && getExecutionConfig() != null
+                && getContainingTask().getConfiguration().isCheckpointingEnabled()) {
+            throw new IllegalStateException("positional sum/min/max on Tuple3+ with checkpointing needs "
+                    + "withInputSerializer(...): the snapshot writes each window's first element");
+        }
         if (wide()) {
             payload = direct(8); oPay = direct(8);
             elements = new ElementLog<>();
@@ -169,10 +183,21 @@ public class GpuWindowOperator<IN, K>
                     for (int j = 0; j < from.length; j++) to[j] = dictionary().idOf(table.get(from[j]));
                     nativeRemapKeys(blob, from, to);
                 }
+                Map<Long, IN> firsts = restoredElements.get(i);
+                if (firsts != null) {  // the first elements join this subtask's ElementLog
+                    long[] maxEnd = new long[1];
+                    long[] from = nativeSnapshotPayloads(blob, maxEnd);
+                    long[] to = new long[from.length];
+                    for (int j = 0; j < from.length; j++) to[j] = elements.append(firsts.get(from[j]));
+                    nativeRemapPayloads(blob, from, to);
+                    // kept until the latest restored window is cleaned: maxTs + size - 1 = its end - 1
+                    batches.addLast(new long[] {elements.end(), maxEnd[0] - size});
+                }
                 nativeRestore(handle, blob);
             }
             restored = null;
             restoredKeys = null;
+            restoredElements = null;
         }
     }
 
@@ -226,6 +251,13 @@ public class GpuWindowOperator<IN, K>
                 dos.writeLong(id);
                 keySer.serialize(dict.keyOf(id), view);
             }
+            // Tuple3+ positional: each window's first element (the reduced Tuple's other fields)
+            long[] firsts = wide() ? nativeSnapshotPayloads(part, new long[1]) : new long[0];
+            dos.writeInt(firsts.length);
+            for (long seq : firsts) {
+                dos.writeLong(seq);
+                inputSerializer.serialize(elements.get(seq), view);
+            }
             dos.flush();
         }
     }
@@ -236,6 +268,7 @@ public class GpuWindowOperator<IN, K>
         if (!context.isRestored()) return;
         restored = new ArrayList<>();
         restoredKeys = new ArrayList<>();
+        restoredElements = new ArrayList<>();
         @SuppressWarnings("unchecked")
         TypeSerializer<K> keySer = (TypeSerializer<K>) getKeyedStateBackend().getKeySerializer();
         for (KeyGroupStatePartitionStreamProvider p : context.getRawKeyedStateInputs()) {
@@ -252,6 +285,13 @@ public class GpuWindowOperator<IN, K>
                 table.put(id, keySer.deserialize(view));
             }
             restoredKeys.add(table);
+            int ne = in.readInt();
+            Map<Long, IN> firsts = ne > 0 ? new HashMap<>() : null;
+            for (int j = 0; j < ne; j++) {
+                long seq = in.readLong();
+                firsts.put(seq, inputSerializer.deserialize(view));
+            }
+            restoredElements.add(firsts);
         }
     }
 
@@ -453,6 +493,8 @@ public class GpuWindowOperator<IN, K>
     private static native void nativeRestore(long h, byte[] blob);
     private static native long[] nativeSnapshotKeys(byte[] blob);
     private static native void nativeRemapKeys(byte[] blob, long[] from, long[] to);
+    private static native long[] nativeSnapshotPayloads(byte[] blob, long[] maxEnd);
+    private static native void nativeRemapPayloads(byte[] blob, long[] from, long[] to);
     private static native int nativeDrainLate(long h, ByteBuffer key, ByteBuffer ts, ByteBuffer value, int cap);
     /** The keyBy exchange's receive columns (GpuKeyByExchange.batch, produced on `stream`)
      *  straight into the operator. */

@@ -232,6 +232,46 @@ JNIEXPORT jint JNICALL CLS(nativeDrainLate)(JNIEnv* env, jclass c, jlong h, jobj
     return (jint)n;
 }
 
+/* First-element blobs: the payloads (ElementLog ids) their entries name, ascending, and in
+ * maxEnd[0] the latest window end (gw_snapshot_payloads). */
+JNIEXPORT jlongArray JNICALL CLS(nativeSnapshotPayloads)(JNIEnv* env, jclass c, jbyteArray blob, jlongArray maxEnd) {
+    jsize len = (*env)->GetArrayLength(env, blob);
+    jbyte* b = (*env)->GetByteArrayElements(env, blob, 0);
+    int64_t n = 0, mx = 0;
+    int rc = gw_snapshot_payloads(b, len, 0, 0, &n, &mx);
+    jlongArray out = 0;
+    if (rc == GW_OK) {
+        int64_t* tmp = (int64_t*)malloc((size_t)(n > 0 ? n : 1) * 8);
+        rc = tmp ? gw_snapshot_payloads(b, len, tmp, n, &n, &mx) : GW_E_OOM;
+        if (rc == GW_OK) {
+            out = (*env)->NewLongArray(env, (jsize)n);
+            (*env)->SetLongArrayRegion(env, out, 0, (jsize)n, (const jlong*)tmp);
+            (*env)->SetLongArrayRegion(env, maxEnd, 0, 1, (const jlong*)&mx);
+        }
+        free(tmp);
+    }
+    (*env)->ReleaseByteArrayElements(env, blob, b, JNI_ABORT);
+    fail(env, 0, rc);
+    return out;
+}
+
+/* ... and rewritten to this subtask's ElementLog ids (ascending `from`), in place. */
+JNIEXPORT void JNICALL CLS(nativeRemapPayloads)(JNIEnv* env, jclass c, jbyteArray blob, jlongArray from,
+                                                jlongArray to) {
+    jsize len = (*env)->GetArrayLength(env, blob);
+    jsize n = (*env)->GetArrayLength(env, from);
+    jbyte* b = (*env)->GetByteArrayElements(env, blob, 0);
+    jlong* f = (*env)->GetLongArrayElements(env, from, 0);
+    jlong* t = (*env)->GetLongArrayElements(env, to, 0);
+    int rc = (*env)->GetArrayLength(env, to) == n
+                 ? gw_snapshot_remap_payloads(b, len, (const int64_t*)f, (const int64_t*)t, n)
+                 : GW_E_INVALID;
+    (*env)->ReleaseLongArrayElements(env, to, t, JNI_ABORT);
+    (*env)->ReleaseLongArrayElements(env, from, f, JNI_ABORT);
+    (*env)->ReleaseByteArrayElements(env, blob, b, rc == GW_OK ? 0 : JNI_ABORT);
+    fail(env, 0, rc);
+}
+
 /* ---- GpuKeyByExchange: the keyBy shuffle through libgpuwin's RCCL communicator ---- */
 #define XCLS(n) Java_org_apache_flink_streaming_runtime_operators_windowing_gpu_GpuKeyByExchange_##n
 

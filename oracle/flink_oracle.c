@@ -1326,7 +1326,29 @@ typedef struct {
     uint64_t* pw_cs;   /* optional [nb + 1]: order-independent checksum of those rows */
     int rc;
     int no_final;      /* 1: no MAX_WATERMARK after the last batch (the stream's own cadence) */
+    int keep_rows;     /* 1: keep every row (rk.. / rwm, nrows of rcap) */
+    int64_t *rk, *rs, *re, *rr;
+    int32_t* rwm;
+    int64_t nrows, rcap;
 } par_arg;
+
+static int keep_row_buf(par_arg* a, int64_t more) {
+    if (a->nrows + more <= a->rcap) return 0;
+    int64_t cap = a->rcap ? a->rcap : 1 << 16;
+    while (cap < a->nrows + more) cap *= 2;
+    int64_t* b[4] = {a->rk, a->rs, a->re, a->rr};
+    for (int c = 0; c < 4; c++) {
+        int64_t* nb = (int64_t*)realloc(b[c], (size_t)cap * 8);
+        if (!nb) return GW_E_OOM;
+        b[c] = nb;
+    }
+    a->rk = b[0]; a->rs = b[1]; a->re = b[2]; a->rr = b[3];
+    int32_t* w = (int32_t*)realloc(a->rwm, (size_t)cap * 4);
+    if (!w) return GW_E_OOM;
+    a->rwm = w;
+    a->rcap = cap;
+    return 0;
+}
 
 static void* par_main(void* p) {
     par_arg* a = (par_arg*)p;
@@ -1361,6 +1383,15 @@ static void* par_main(void* p) {
             cs += c;
             rows += n;
             if (a->pw_rows) { a->pw_rows[b] += n; a->pw_cs[b] += c; }
+            if (a->keep_rows) {
+                if (keep_row_buf(a, n)) { a->rc = GW_E_OOM; goto done; }
+                memcpy(a->rk + a->nrows, bk, (size_t)n * 8);
+                memcpy(a->rs + a->nrows, bs, (size_t)n * 8);
+                memcpy(a->re + a->nrows, be, (size_t)n * 8);
+                memcpy(a->rr + a->nrows, br, (size_t)n * 8);
+                for (int64_t i = 0; i < n; i++) a->rwm[a->nrows + i] = (int32_t)b;
+                a->nrows += n;
+            }
         }
     }
 done:
@@ -1380,7 +1411,7 @@ static int64_t run_parallel(const gw_config* cfg, int threads, int64_t nb, const
     struct timespec t0, t1;
     clock_gettime(CLOCK_MONOTONIC, &t0);
     for (int i = 0; i < threads; i++) {
-        args[i] = (par_arg){cfg, i, threads, nb, blen, wm, key, ts, val, 0, 0, NULL, NULL, 0, no_final};
+        args[i] = (par_arg){cfg, i, threads, nb, blen, wm, key, ts, val, 0, 0, NULL, NULL, 0, no_final, 0, NULL, NULL, NULL, NULL, NULL, 0, 0};
         pthread_create(&th[i], NULL, par_main, &args[i]);
     }
     int64_t rows = 0;
@@ -1431,7 +1462,7 @@ int64_t wo_run_parallel_wm(const gw_config* cfg, int threads, int64_t nb, const 
     clock_gettime(CLOCK_MONOTONIC, &t0);
     for (int i = 0; i < threads; i++) {
         args[i] = (par_arg){cfg, i, threads, nb, blen, wm, key, ts, val, 0, 0,
-                            pr + (size_t)i * (size_t)(nb + 1), pc + (size_t)i * (size_t)(nb + 1), 0, 0};
+                            pr + (size_t)i * (size_t)(nb + 1), pc + (size_t)i * (size_t)(nb + 1), 0, 0, 0, NULL, NULL, NULL, NULL, NULL, 0, 0};
         pthread_create(&th[i], NULL, par_main, &args[i]);
     }
     int64_t rows = 0;
@@ -1450,6 +1481,52 @@ int64_t wo_run_parallel_wm(const gw_config* cfg, int threads, int64_t nb, const 
     if (seconds) *seconds = (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
     free(th); free(args); free(pr); free(pc);
     return rc ? rc : rows;
+}
+
+/* wo_run_parallel keeping every fired row: (key, start, end, result bits, watermark index)
+ * into the caller's arrays of cap rows (the last watermark index nb = MAX_WATERMARK).
+ * Returns the number of rows, GW_E_OUTPUT_FULL (nothing written) if more than cap. */
+int64_t wo_run_parallel_rows(const gw_config* cfg, int threads, int64_t nb, const int64_t* blen,
+                             const int64_t* wm, const int64_t* key, const int64_t* ts, const int64_t* val,
+                             int64_t cap, int64_t* ok, int64_t* os, int64_t* oe, int64_t* orr, int32_t* owm,
+                             double* seconds) {
+    if (threads < 1) threads = 1;
+    pthread_t* th = (pthread_t*)calloc((size_t)threads, sizeof(pthread_t));
+    par_arg* args = (par_arg*)calloc((size_t)threads, sizeof(par_arg));
+    if (!th || !args) { free(th); free(args); return GW_E_OOM; }
+    struct timespec t0, t1;
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    for (int i = 0; i < threads; i++) {
+        memset(&args[i], 0, sizeof(par_arg));
+        args[i].cfg = cfg; args[i].idx = i; args[i].threads = threads; args[i].nb = nb; args[i].blen = blen;
+        args[i].wm = wm; args[i].key = key; args[i].ts = ts; args[i].val = val; args[i].keep_rows = 1;
+        pthread_create(&th[i], NULL, par_main, &args[i]);
+    }
+    int64_t total = 0;
+    int rc = 0;
+    for (int i = 0; i < threads; i++) {
+        pthread_join(th[i], NULL);
+        total += args[i].nrows;
+        if (args[i].rc) rc = args[i].rc;
+    }
+    clock_gettime(CLOCK_MONOTONIC, &t1);
+    if (seconds) *seconds = (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
+    if (!rc && total > cap) rc = GW_E_OUTPUT_FULL;
+    int64_t at = 0;
+    for (int i = 0; i < threads; i++) {
+        par_arg* a = &args[i];
+        if (!rc && a->nrows) {
+            memcpy(ok + at, a->rk, (size_t)a->nrows * 8);
+            memcpy(os + at, a->rs, (size_t)a->nrows * 8);
+            memcpy(oe + at, a->re, (size_t)a->nrows * 8);
+            memcpy(orr + at, a->rr, (size_t)a->nrows * 8);
+            memcpy(owm + at, a->rwm, (size_t)a->nrows * 4);
+            at += a->nrows;
+        }
+        free(a->rk); free(a->rs); free(a->re); free(a->rr); free(a->rwm);
+    }
+    free(th); free(args);
+    return rc ? rc : total;
 }
 
 /* ---------------------------------------------------------------------------

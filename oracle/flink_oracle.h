@@ -92,6 +92,13 @@ int64_t wo_run_parallel_stream(const gw_config* cfg, int threads, int64_t n_batc
                                const int64_t* batch_len, const int64_t* wm,
                                const int64_t* key, const int64_t* ts, const int64_t* value_bits,
                                int64_t* checksum, double* seconds);
+/* The same keeping every fired row (key, start, end, result bits, watermark index b; nb for
+ * the final MAX_WATERMARK) in caller arrays of cap rows; GW_E_OUTPUT_FULL beyond cap. */
+int64_t wo_run_parallel_rows(const gw_config* cfg, int threads, int64_t n_batches,
+                             const int64_t* batch_len, const int64_t* wm,
+                             const int64_t* key, const int64_t* ts, const int64_t* value_bits,
+                             int64_t cap, int64_t* o_key, int64_t* o_start, int64_t* o_end, int64_t* o_res,
+                             int32_t* o_wm, double* seconds);
 /* The same, per watermark: wm_rows[b] / wm_cs[b] for b = 0..n_batches (the last entry is
  * the final MAX_WATERMARK) hold the rows that watermark fired over all subtasks and the
  * sum of their row hashes, (key * 0x9e3779b97f4a7c15) ^ (start * 31) ^ (end * 17) ^ result

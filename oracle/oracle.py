@@ -135,6 +135,8 @@ def lib() -> ctypes.CDLL:
                                        P64, ctypes.POINTER(ctypes.c_double)]),
             ("wo_run_parallel_stream", i64, [ctypes.POINTER(GwConfig), ctypes.c_int, i64, p, p, p, p, p,
                                               P64, ctypes.POINTER(ctypes.c_double)]),
+            ("wo_run_parallel_rows", i64, [ctypes.POINTER(GwConfig), ctypes.c_int, i64, p, p, p, p, p, i64,
+                                            p, p, p, p, p, ctypes.POINTER(ctypes.c_double)]),
             ("wo_snapshot", i64, [p, i32, i32, p, i64]), ("wo_restore", ctypes.c_int, [p, p, i64]),
             ("wo_acc_bytes", ctypes.c_int, [ctypes.c_int]),
             ("wo_run_parallel_wm", i64, [ctypes.POINTER(GwConfig), ctypes.c_int, i64, p, p, p, p, p, p, p,
@@ -292,3 +294,21 @@ def run_parallel_wm(cfg: GwConfig, threads: int, batch_len, wm, key, ts, value_b
     if rc < 0:
         raise OracleError(f"parallel oracle failed: {rc}")
     return rows, cs, sec.value
+
+
+def run_parallel_rows(cfg: GwConfig, threads: int, batch_len, wm, key, ts, value_bits, cap: int):
+    """run_parallel keeping every fired row: (key, start, end, result bits, watermark index)
+    numpy columns (index len(batch_len) = the final MAX_WATERMARK), seconds."""
+    batch_len = np.ascontiguousarray(batch_len, dtype=np.int64)
+    wm = np.ascontiguousarray(wm, dtype=np.int64)
+    key = np.ascontiguousarray(key, dtype=np.int64)
+    ts = np.ascontiguousarray(ts, dtype=np.int64)
+    vb = None if value_bits is None else np.ascontiguousarray(value_bits).view(np.int64)
+    k, s, e, r = (np.empty(cap, np.int64) for _ in range(4))
+    w = np.empty(cap, np.int32)
+    sec = ctypes.c_double(0)
+    n = lib().wo_run_parallel_rows(ctypes.byref(cfg), threads, len(batch_len), _p(batch_len), _p(wm), _p(key),
+                                   _p(ts), _p(vb), cap, _p(k), _p(s), _p(e), _p(r), _p(w), ctypes.byref(sec))
+    if n < 0:
+        raise OracleError(f"parallel oracle failed: {n}")
+    return k[:n], s[:n], e[:n], r[:n], w[:n], sec.value

@@ -126,8 +126,6 @@ def test_first_element_rejections():
     try:
         with pytest.raises(N.GpuWinError):
             op.process_batch(np.zeros(4, np.int64), np.zeros(4, np.int64), np.zeros(4, np.int64))
-        with pytest.raises(N.GpuWinError):
-            op.snapshot_state()
     finally:
         op.close()
     plain = gpu_operator(dict(assigner="tumbling", size=100, agg="sum_i64"))
@@ -142,3 +140,46 @@ def test_first_element_rejections():
                dict(assigner="session", gap=100, agg="sum_i64")):
         with pytest.raises((N.GpuWinError, ValueError)):
             gpu_operator(kw, flags=N.FLAG_FIRST_ELEMENT)
+
+
+@pytest.mark.parametrize("kw,agg", [(CONFIGS[0], "sum_i64"), (CONFIGS[2], "max_f64"), (CONFIGS[3], "min_i64"),
+                                    (CONFIGS[4], "sum_i64")],
+                         ids=["tumbling-sum", "sliding-max-f64", "window-classes-min", "sliding-lateness-sum"])
+def test_first_element_snapshot_restore(oracle_lib, kw, agg):
+    """A first-element handle snapshots (window, key, aggregate, first element's payload) per
+    (key, window) -- the reference's reduced Tuple, HeapReducingState.java:90-97 -- and a fresh
+    handle restored from it (through per-key-group slices) continues like the uninterrupted
+    operator: same rows, same first elements."""
+    kw = dict(kw, agg=agg)
+    lat = kw.get("lateness", 0)
+    keys, ts, vals, batches = random_stream(seed=91, n=24000, num_keys=150, n_batches=24, ts_step=3,
+                                            disorder=240, wm_lag=250, agg=agg)
+    payload = np.random.default_rng(92).integers(-(1 << 62), 1 << 62, len(keys)).astype(np.int64)
+    o, _ = _expected(oracle_lib, kw, keys, ts, vals, payload, batches)
+    cut = 11
+    a = gpu_operator(kw, flags=N.FLAG_FIRST_ELEMENT)
+    outs = []
+    try:
+        for lo, hi, wm in batches[:cut]:
+            a.process_batch_payload(keys[lo:hi], ts[lo:hi], vals[lo:hi], payload[lo:hi])
+            a.advance_watermark(wm)
+            outs.append(a.drain_payload())
+        blob = a.snapshot_state()
+    finally:
+        a.close()
+    b = gpu_operator(kw, flags=N.FLAG_FIRST_ELEMENT)
+    try:
+        b.initialize_state([N.snapshot_slice(blob, kg) for kg in range(128)])
+        for lo, hi, wm in batches[cut:]:
+            b.process_batch_payload(keys[lo:hi], ts[lo:hi], vals[lo:hi], payload[lo:hi])
+            b.advance_watermark(wm)
+            outs.append(b.drain_payload())
+        b.advance_watermark(W.LONG_MAX)
+        outs.append(b.drain_payload())
+    finally:
+        b.close()
+    g = []
+    for k, s, e, r, p in outs:
+        i = np.lexsort((e, s, k))
+        g.append((k[i], s[i], e[i], r.view(np.int64)[i], p[i]))
+    _check(g, o, agg.endswith("f64"))

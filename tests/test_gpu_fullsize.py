@@ -4,14 +4,15 @@ Each test drives libgpuwin.so through the C ABI over a stream of the config's re
 compares the rows of EVERY watermark with the CPU oracle (oracle/flink_oracle.c):
 
 * Nexmark Q5 (sliding 10 s / 2 s over 10M keys, 100M events, a watermark every 200 ms of
-  event time): the oracle runs the whole stream (wo_run_parallel_wm, one operator per
-  simulated subtask) and the rows of each watermark are compared by count and by an
-  order-independent checksum; a 1/32 key sample is also compared row by row.
-* Q7-style tumbling 10 s max over 10M keys, 100M events: 1/32 key sample row by row, plus
-  the full-stream invariants below.
+  event time), sum and count: the oracle runs the whole stream (wo_run_parallel_wm, one
+  operator per simulated subtask) and the rows of each watermark are compared by count and
+  by an order-independent checksum; a 1/32 key sample is also compared row by row.
+* Q7-style tumbling 10 s max over 10M keys, 100M events: the same full per-watermark count
+  and checksum, the 1/32 key sample row by row, and the full-stream invariants below.
 * Event-time sessions (gap 10 s) with avg over f64 at 12.5M keys (one GPU's share of
-  BASELINE's 100M keys over 8 GPUs), ~110M events: 1/64 key sample row by row (f64 within
-  1e-6 relative), plus the invariants.
+  BASELINE's 100M keys over 8 GPUs), ~110M events: every row of every watermark against the
+  oracle's (wo_run_parallel_rows): key, start and end exactly, the average within 1e-6
+  relative; plus the 1/64 key sample and the invariants.
 
 Keys are independent in the reference (WindowOperator keeps state per key, late drops depend
 only on the watermark), so a key sample run through the oracle on the sampled keys' records
@@ -70,10 +71,10 @@ def row_hash_sum(rows):
     return rows_hash_sum(*rows)
 
 
-def run_gpu_rows(kw, keys, ts, vals, nb, wms, capacity_hint, sample):
+def run_gpu_rows(kw, keys, ts, vals, nb, wms, capacity_hint, sample, keep_all=False):
     """Drive the GPU operator over device columns in batches of nb records; per watermark
-    (the last entry: MAX_WATERMARK) return (rows, checksum, sampled rows) and check that
-    (key, window) is unique."""
+    (the last entry: MAX_WATERMARK) return (rows, checksum, sampled rows -- or every row with
+    keep_all) and check that (key, window) is unique."""
     import torch
     op = gpu_operator(kw, capacity_hint=capacity_hint, max_batch=nb)
     stream = torch.cuda.current_stream().cuda_stream
@@ -96,8 +97,11 @@ def run_gpu_rows(kw, keys, ts, vals, nb, wms, capacity_hint, sample):
                 assert not np.any((ks[1:] == ks[:-1]) & (ss[1:] == ss[:-1])), f"duplicate (key, window) at wm #{b}"
             if kw["agg"] == "count":
                 total_result += int(r.sum())
-            m = sample(k)
-            samp.append((k[m], s[m], e[m], r[m]))
+            if keep_all:
+                samp.append((k, s, e, r))
+            else:
+                m = sample(k)
+                samp.append((k[m], s[m], e[m], r[m]))
         late = op.num_late_records_dropped
     finally:
         op.close()
@@ -125,7 +129,7 @@ Q7 = dict(assigner="tumbling", size=10_000, slide=10_000)
 
 
 @pytest.mark.timeout(600)
-@pytest.mark.parametrize("agg,full_oracle", [("sum_i64", True), ("count", False)])
+@pytest.mark.parametrize("agg,full_oracle", [("sum_i64", True), ("count", True)])
 def test_q5_10m_keys_100m_events(oracle_lib, agg, full_oracle):
     """Nexmark Q5 at its BASELINE size: 10M keys, 100M events (20M per 2-s pane, 50
     watermark batches, 5 windows fire during the stream, the rest at MAX_WATERMARK)."""
@@ -180,6 +184,12 @@ def test_q7_tumbling_max_10m_keys(oracle_lib):
     assert olate == 0
     errs = compare(samp, ora, False)
     assert not errs, errs[:5]
+    # every watermark's rows over all 10M keys: count + checksum
+    rows, cs, sec = oracle_lib.run_parallel_wm(oracle_lib.make_config(**kw), THREADS, np.full(len(wms), nb),
+                                               np.array(wms, np.int64), keys_np, ts_np, vals_np)
+    assert list(rows) == counts
+    bad = [b for b in range(len(counts)) if int(cs[b]) != sums[b]]
+    assert not bad, f"checksum differs at watermarks {bad[:10]}"
 
 
 def session_stream(num_keys, gap, seed):
@@ -231,14 +241,20 @@ def test_sessions_avg_f64_12m_keys(oracle_lib):
     run_max = torch.cummax(tsh, dim=0).values.cpu().numpy()
     wms = [int(x) - 200 - 1 for x in run_max]  # lag 200 ms > jitter: no record is late
     kw = dict(assigner="session", gap=gap, agg="avg_f64")
-    sample = lambda k: (k % 64) == 9
-    counts, sums, samp, _, late = run_gpu_rows(kw, keys, ts, vals, nb, wms, K, sample)
+    counts, sums, allrows, _, late = run_gpu_rows(kw, keys, ts, vals, nb, wms, K, None, keep_all=True)
     assert late == 0
     keys_np, ts_np, vals_np = keys.cpu().numpy(), ts.cpu().numpy(), vals.cpu().numpy()
     del keys, ts, vals
     assert sum(counts) >= len(np.unique(keys_np))  # at least one session per key
-    mask = sample(keys_np)
-    ora, olate = oracle_sample(oracle_lib, kw, keys_np, ts_np, vals_np, nb, wms, mask)
-    assert olate == 0
-    errs = compare([(k, s, e, r) for k, s, e, r in samp], ora, True)
+    # every row of every watermark against the full oracle (f64 averages within 1e-6)
+    ok_, os_, oe_, or_, ow_, sec = oracle_lib.run_parallel_rows(
+        oracle_lib.make_config(**kw), THREADS, np.full(len(wms), nb), np.array(wms, np.int64), keys_np, ts_np,
+        vals_np, n + 1024)
+    ora = []
+    order = np.argsort(ow_, kind="stable")
+    bounds = np.searchsorted(ow_[order], np.arange(len(wms) + 2))
+    for b in range(len(wms) + 1):
+        sel = order[bounds[b]:bounds[b + 1]]
+        ora.append((ok_[sel], os_[sel], oe_[sel], or_[sel]))
+    errs = compare(allrows, ora, True)
     assert not errs, errs[:5]

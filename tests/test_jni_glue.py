@@ -277,3 +277,50 @@ def test_ingest_glue_with_key_hashes(jni):
         assert exc is not None and "is not in KeyGroupRange" in exc[1]
     finally:
         getattr(jni, CLS + "nativeDestroy")(env, None, ctypes.c_int64(h))
+
+
+def _fe_blob(entries, agg="sum_i64", kg=0):
+    """A first-element blob (flags bit 1): entries (start, end, key, acc, payload), no timers."""
+    import struct
+    pay = struct.pack(">i", len(entries))
+    for s, e, k, a, p in entries:
+        pay += struct.pack(">qqqqq", s, e, k, a, p)
+    pay += struct.pack(">ii", 0, 0)
+    hdr = struct.pack("<4sIii5q4i3q", b"GWS1", 4, N.AGGS[agg], N.ASSIGNERS["tumbling"], 100, 100, 0, 0, 2,
+                      128, kg, kg, 0, 0, 0, len(pay))
+    return hdr + struct.pack("<2q", 0, len(pay)) + pay
+
+
+def test_payload_table_glue(jni):
+    """snapshotState's first-element table and initializeState's payload remap through the glue
+    (gw_snapshot_payloads / gw_snapshot_remap_payloads)."""
+    p = ctypes.c_void_p
+    sp = getattr(jni, CLS + "nativeSnapshotPayloads")
+    sp.restype = p
+    sp.argtypes = [p, p, p, p]
+    rp = getattr(jni, CLS + "nativeRemapPayloads")
+    rp.restype = None
+    rp.argtypes = [p, p, p, p, p]
+    _key_fns(jni)
+    blob = _fe_blob([(0, 100, 5, 7, 41), (100, 200, 5, 9, 12), (0, 100, 6, 1, 41)])
+    env = jni.fake_env()
+    arr = jni.fake_bytes_new(blob, len(blob))
+    mx = jni.fake_longs_new(np.zeros(1, np.int64).ctypes.data, 1)
+    out = sp(env, None, arr, mx)
+    assert exception(jni) is None and jni.fake_bytes_len(out) == 2
+    L = lambda a, n: list(np.ctypeslib.as_array(ctypes.cast(jni.fake_longs_data(a), ctypes.POINTER(ctypes.c_int64)), (n,)))
+    assert L(out, 2) == [12, 41] and L(mx, 1) == [200]
+    frm, to = np.array([12, 41], np.int64), np.array([3, 4], np.int64)
+    fa, ta = jni.fake_longs_new(frm.ctypes.data, 2), jni.fake_longs_new(to.ctypes.data, 2)
+    rp(env, None, arr, fa, ta)
+    assert exception(jni) is None
+    moved = ctypes.string_at(jni.fake_bytes_data(arr), len(blob))
+    assert moved == _fe_blob([(0, 100, 5, 7, 4), (100, 200, 5, 9, 3), (0, 100, 6, 1, 4)])
+    # a blob without payloads: IllegalArgumentException
+    plain = bytearray(blob)
+    plain[48:56] = (0).to_bytes(8, "little")
+    parr = jni.fake_bytes_new(bytes(plain), len(plain))
+    assert sp(env, None, parr, mx) is None
+    assert exception(jni)[0] == "java/lang/IllegalArgumentException"
+    for a in (arr, out, mx, fa, ta, parr):
+        jni.fake_bytes_free(a)
