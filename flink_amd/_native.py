@@ -99,7 +99,7 @@ class GwStats(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int64) for n in (
         "events_in", "late_dropped", "rows_fired", "live_keys", "table_capacity", "table_bytes",
         "deferred", "batches", "fires", "rehashes", "preagg_batches", "session_merges", "applies",
-        "region_format")]
+        "region_format", "session_punted", "session_slow")]
 
     def as_dict(self):
         return {n: getattr(self, n) for n, _ in self._fields_}

@@ -999,12 +999,20 @@ struct gw_handle {
         // gapped panes (size < slide) use the wide pass 1, the one instantiated with the gap test
         return int_agg && !cmp_off && !env_off && !gap_size && d1_bits >= 2 && (int64_t)tv.ring <= ((int64_t)1 << (d1_bits - 1));
     }
-    // Narrow records (32-bit keys, 28-bit values, ring positions < 8) where compact ones fit
-    // and no window has overflowed them yet (GW_NO_NARROW turns them off).
+    // Narrow records (32-bit keys, 28-bit values, ring positions < 8) for integer aggregates
+    // whose windows have not overflowed them yet (GW_NO_NARROW turns them off).  They keep
+    // the ring position beside the key, so unlike compact records they need no spare
+    // pass-1 bucket bits (small single-pass tables under allowed lateness take them too).
     int region_fmt(int d1_bits) const {
-        if (!compact_ok(d1_bits)) return 0;
+        const int agg = cfg.agg;
+        const bool int_agg = agg == GW_COUNT || agg == GW_SUM_I64 || agg == GW_SUM_I32 || agg == GW_MIN_I64 ||
+                             agg == GW_MAX_I64 || agg == GW_AVG_I64;
         static const bool nar_env_off = getenv("GW_NO_NARROW") != nullptr;
-        return (!nar_off && !nar_env_off && !(cfg.flags & GW_FLAG_NO_NARROW) && tv.ring <= 8) ? 2 : 1;
+        static const bool cmp_env_off = getenv("GW_NO_COMPACT") != nullptr;
+        if (int_agg && !gap_size && !cmp_env_off && !nar_off && !nar_env_off && !(cfg.flags & GW_FLAG_NO_NARROW) &&
+            tv.ring <= 8)
+            return 2;
+        return compact_ok(d1_bits) ? 1 : 0;
     }
 
     // P2 + apply over every waiting segment (one fire's worth of batches).  Runs before

@@ -38,6 +38,7 @@ constexpr int kLaneSess = 3;        // sessions a thread replays in LDS
 constexpr int kSegThreads = 128;
 constexpr int kWideWords = 5;       // wide-table session: start, end, a0, a1, fired
 constexpr uint64_t kBigMeta = 1ull << 31;  // main-table slot word 1: the key lives in the wide table
+constexpr uint64_t kPuntMeta = 1ull << 30; // ... the key's later records of this batch go to the punt list
 
 struct SegArgs {
     const uint32_t* slot;   // sorted main-table slot of each record
@@ -67,6 +68,18 @@ struct SegArgs {
     uint32_t* retry;        // wide pass: runs that did not fit K2 (append at st->overflow)
     DevStatus* st;
     int gshift;             // records are grouped by slot >> gshift (the sort skips the low bits)
+    // region-partitioned ingest (k_sp_part / k_sp_group / k_sp_keys)
+    const int64_t* p_key;   // pass-1 output, tile-major, bucket runs inside each tile (SoA)
+    const int64_t* p_ts;
+    const int64_t* p_val;
+    const uint32_t* col;    // [bucket][tile] run descriptors (start << 16 | count)
+    int64_t ntiles;
+    int lcap, bb;           // log2(table capacity), bucket bits (bucket = home >> (lcap - bb))
+    int exp;                // GW_SP_EXP: measurement variants of k_sp_keys (0: none)
+    uint32_t* slow;         // home slots for k_sp_slow (bucket << 14 | head), append at st->spills
+    int64_t* pu_key;        // punted records (arrival order per key), append at st->overflow
+    int64_t* pu_ts;
+    int64_t* pu_val;
 };
 
 struct Sess {
@@ -76,7 +89,7 @@ struct Sess {
 
 // Main-table slot word 1: in-flight session count (low 31 bits), kBigMeta, fired bit per
 // session (high 32 bits).
-__device__ __forceinline__ int slot_cnt(int64_t w) { return (int)((uint64_t)w & 0x7fffffffull); }
+__device__ __forceinline__ int slot_cnt(int64_t w) { return (int)((uint64_t)w & 0x3fffffffull); }
 __device__ __forceinline__ bool slot_big(int64_t w) { return ((uint64_t)w & kBigMeta) != 0; }
 __device__ __forceinline__ bool slot_fired(int64_t w, int q) { return ((uint64_t)w >> (32 + q)) & 1ull; }
 
@@ -160,12 +173,10 @@ __device__ __forceinline__ void sl_put(const SessList& l, int q, const Sess& v) 
 // (re-)armed.  Returns false if a new session does not fit `cap`.  `dry`: no rows and no
 // side output are written (a trial replay that may be abandoned).
 template <int AGG>
-__device__ __forceinline__ bool add_element(const SegArgs& a, const SessList& l, int& cnt, int cap, int64_t key,
-                                            int64_t idx, unsigned long long& late, unsigned long long& merges,
-                                            unsigned long long& flags, bool dry = false) {
-    struct alignas(16) TsVal { int64_t ts, v; };
-    const TsVal tv = reinterpret_cast<const TsVal*>(a.rec)[idx];
-    const int64_t ts = tv.ts;
+__device__ __forceinline__ bool add_element_tv(const SegArgs& a, const SessList& l, int& cnt, int cap, int64_t key,
+                                               int64_t ts, int64_t value, unsigned long long& late,
+                                               unsigned long long& merges, unsigned long long& flags, bool dry) {
+    struct { int64_t ts, v; } tv{ts, value};
     int64_t we;
     if (__builtin_add_overflow(ts, a.gap, &we)) { flags |= GW_DF_RANGE; return true; }
     const int64_t ws = ts;
@@ -226,6 +237,16 @@ __device__ __forceinline__ bool add_element(const SegArgs& a, const SessList& l,
     for (int q = hi + 1; q < cnt; ++q) sl_put(l, q - removed, sl_get(l, q));
     cnt -= removed;
     return true;
+}
+
+// The same for element `idx` of the batch, read from the (ts, value) pairs of k_sess_prep.
+template <int AGG>
+__device__ __forceinline__ bool add_element(const SegArgs& a, const SessList& l, int& cnt, int cap, int64_t key,
+                                            int64_t idx, unsigned long long& late, unsigned long long& merges,
+                                            unsigned long long& flags, bool dry = false) {
+    struct alignas(16) TsVal { int64_t ts, v; };
+    const TsVal tv = reinterpret_cast<const TsVal*>(a.rec)[idx];
+    return add_element_tv<AGG>(a, l, cnt, cap, key, tv.ts, tv.v, late, merges, flags, dry);
 }
 
 // Main pass: one thread per key's run.  The run's elements replay against the key's
@@ -485,6 +506,661 @@ __global__ void __launch_bounds__(256) k_sess_prep(const int64_t* key, const int
         }
     }
     block_commit(st, 0, ins, flags, 0);
+}
+
+// ---------------------------------------------------------- region-partitioned ingest
+// The default session ingest.  Four launches per batch, no device-wide sort:
+//  * k_sp_part: one workgroup per 4096-record tile hashes every key to its home slot and
+//    writes the tile's records grouped by bucket (the top bb bits of the home slot), one run
+//    per bucket, stable (arrival order inside a run); one descriptor row per tile.
+//  * k_sp_transpose: descriptor rows -> one column per bucket.
+//  * k_sp_group: one workgroup per bucket concatenates the bucket's runs in tile order -- the
+//    bucket's records in arrival order -- and sorts them in LDS by (home slot, arrival) with a
+//    stable radix sort; it writes the order and one head per home slot.
+//  * k_sp_keys: one thread per home slot finds or inserts the key (the probe the sort path's
+//    k_sess_prep makes, here on the line the replay needs anyway) and replays the slot's
+//    records through MergingWindowSet.addWindow semantics (add_element_tv), all of the
+//    batch's records of a key in arrival order.
+// A key that needs the wide table (more in-flight sessions than the lane holds, or already
+// wide) or finds no slot, and every key of a bucket with more than kGrpCap records, is
+// punted: its records go to a punt list in arrival order, which the sort path (k_sess_prep
+// ... k_sess_wide) replays after the launch.
+constexpr int kSessionRegionDefault = 0;  // until it outruns the sort path on the sessions config
+constexpr int kSpTile = 4096;
+constexpr int kSpThreads = 1024;
+constexpr int kSpWaveRecs = kSpTile / (kSpThreads / 64);  // records of one wave (a contiguous chunk)
+constexpr int kSpItems = kSpWaveRecs / 64;
+constexpr int kSpMaxBuckets = 1024;
+constexpr size_t kSpPartLds = (size_t)kSpTile * 3 * 8 + (size_t)(kSpThreads / 64) * kSpMaxBuckets * 2;
+
+// Pass 1.  Wave w owns the tile's records [w*256, (w+1)*256) (item it of lane l: w*256 +
+// it*64 + l), so arrival order is (wave, item, lane).  Ranks within a bucket are stable:
+// lanes of one bucket find each other with bb ballots, a leader per bucket bumps the wave's
+// private counter, and a block scan over (bucket, wave) turns the counters into offsets.
+__global__ void __launch_bounds__(kSpThreads) k_sp_part(const int64_t* key, const int64_t* ts, const int64_t* val,
+                                                        int64_t n, int64_t cap, int lcap, int bb, int64_t* o_key,
+                                                        int64_t* o_ts, int64_t* o_val, uint32_t* row, DevStatus* st) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    int64_t* s_key = reinterpret_cast<int64_t*>(smem);
+    int64_t* s_ts = s_key + kSpTile;
+    int64_t* s_val = s_ts + kSpTile;
+    uint16_t* wcnt = reinterpret_cast<uint16_t*>(s_val + kSpTile);  // [wave][bucket]
+    __shared__ uint32_t lh[kSpMaxBuckets], ls[kSpMaxBuckets];
+    __shared__ uint32_t wsum[kSpThreads / 64];
+    const int nb = 1 << bb, sh = lcap - bb;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int64_t tile = blockIdx.x;
+    const int64_t lo = tile * kSpTile, hi = min(n, lo + (int64_t)kSpTile);
+    for (int e = tid; e < (kSpThreads / 64) * nb; e += blockDim.x) wcnt[(e / nb) * kSpMaxBuckets + e % nb] = 0;
+    int64_t k[kSpItems], t[kSpItems], v[kSpItems];
+#pragma unroll
+    for (int it = 0; it < kSpItems; ++it) {  // all loads in flight first
+        const int64_t i = lo + w * kSpWaveRecs + it * 64 + lane;
+        k[it] = 0; t[it] = 0; v[it] = 0;
+        if (i < hi) {
+            k[it] = __builtin_nontemporal_load(key + i);
+            t[it] = __builtin_nontemporal_load(ts + i);
+            if (val) v[it] = __builtin_nontemporal_load(val + i);
+        }
+    }
+    __syncthreads();
+    unsigned long long flags = 0;
+    uint16_t* my = wcnt + w * kSpMaxBuckets;
+    uint32_t bk[kSpItems], rk[kSpItems];
+#pragma unroll
+    for (int it = 0; it < kSpItems; ++it) {
+        const int64_t i = lo + w * kSpWaveRecs + it * 64 + lane;
+        const bool ok = i < hi;
+        if (ok && t[it] == INT64_MIN) flags |= GW_DF_NO_TS;
+        const uint32_t b = !ok ? 0u
+                           : k[it] == kEmptyKey ? (uint32_t)(nb - 1)
+                                                : (uint32_t)((slot_hash(k[it]) & (uint64_t)(cap - 1)) >> sh);
+        uint64_t peers = __ballot(ok);
+        for (int q = 0; q < bb; ++q) {
+            const uint64_t m = __ballot(ok && ((b >> q) & 1u));
+            peers &= ((b >> q) & 1u) ? m : ~m;
+        }
+        uint32_t old = 0;
+        const int leader = ok ? __ffsll((long long)peers) - 1 : 0;
+        if (ok && lane == leader) {
+            old = my[b];
+            my[b] = (uint16_t)(old + __popcll(peers));
+        }
+        old = __shfl(old, leader);
+        bk[it] = ok ? b : ~0u;
+        rk[it] = old + (uint32_t)__popcll(peers & ((1ull << lane) - 1ull));
+    }
+    __syncthreads();
+    {  // bucket totals, exclusive scan over buckets, then per-(wave, bucket) offsets in place
+        uint32_t x = 0;
+        if (tid < nb)
+            for (int q = 0; q < kSpThreads / 64; ++q) x += wcnt[q * kSpMaxBuckets + tid];
+        uint32_t incl = x;
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t up = __shfl_up(incl, o);
+            if (lane >= o) incl += up;
+        }
+        if (lane == 63) wsum[w] = incl;
+        __syncthreads();
+        uint32_t off = 0;
+        for (int q = 0; q < w; ++q) off += wsum[q];
+        if (tid < nb) {
+            ls[tid] = off + incl - x;
+            lh[tid] = x;
+            uint32_t r = off + incl - x;
+            for (int q = 0; q < kSpThreads / 64; ++q) {
+                const uint32_t c = wcnt[q * kSpMaxBuckets + tid];
+                wcnt[q * kSpMaxBuckets + tid] = (uint16_t)r;
+                r += c;
+            }
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int it = 0; it < kSpItems; ++it) {
+        if (bk[it] == ~0u) continue;
+        const uint32_t j = my[bk[it]] + rk[it];
+        s_key[j] = k[it];
+        s_ts[j] = t[it];
+        s_val[j] = v[it];
+    }
+    __syncthreads();
+    const int64_t base = tile * kSpTile;
+    const int cnt = (int)(hi - lo);
+    for (int j = tid; j < cnt; j += blockDim.x) {  // read back by the replay: default cache policy
+        o_key[base + j] = s_key[j];
+        o_ts[base + j] = s_ts[j];
+        o_val[base + j] = s_val[j];
+    }
+    for (int b = tid; b < nb; b += blockDim.x) row[tile * nb + b] = (ls[b] << 16) | lh[b];
+    block_commit(st, 0, 0, flags, 0);
+}
+
+// Descriptor rows [tile][bucket] -> columns [bucket][tile] (64 x 64 blocks through LDS).
+__global__ void __launch_bounds__(256) k_sp_transpose(const uint32_t* row, uint32_t* col, int64_t ntiles, int nb) {
+    __shared__ uint32_t tt[64][65];
+    const int64_t t0 = (int64_t)blockIdx.x * 64;
+    const int b0 = blockIdx.y * 64;
+    for (int e = threadIdx.x; e < 64 * 64; e += blockDim.x) {
+        const int tl = e >> 6, bl = e & 63;
+        const int64_t t = t0 + tl;
+        tt[tl][bl] = (t < ntiles && b0 + bl < nb) ? row[t * nb + b0 + bl] : 0u;
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < 64 * 64; e += blockDim.x) {
+        const int bl = e >> 6, tl = e & 63;
+        const int64_t t = t0 + tl;
+        if (t < ntiles && b0 + bl < nb) col[(int64_t)(b0 + bl) * ntiles + t] = tt[tl][bl];
+    }
+}
+
+// Session words per slot: start, end, acc (+ count for averages).
+template <int AGG>
+__device__ __forceinline__ constexpr int sess_words() {
+    return (AGG == GW_AVG_I64 || AGG == GW_AVG_F64) ? 4 : 3;
+}
+
+// Grouping (k_sp_group): one workgroup per bucket sorts the bucket's records of the batch by
+// (local home slot, arrival) in LDS -- a stable two-pass radix sort over the home bits of
+// 32-bit keys (home << 14 | position) -- and writes the buffer offsets in that order plus
+// one head per home slot.  A bucket holds at most kGrpCap records; the records of a bucket
+// with more (a hot key, a batch far above the table's design size) go to the punt list.
+constexpr int kGrpCap = 16384;
+constexpr int kGrpPosBits = 14;
+constexpr int kGrpThreads = 1024;
+constexpr int kGrpItems = kGrpCap / kGrpThreads;     // per thread per radix pass
+constexpr int kGrpWaveRecs = kGrpCap / (kGrpThreads / 64);
+constexpr int kGrpMaxHomeBits = 31 - kGrpPosBits - 1;  // + the sentinel's code
+constexpr int kGrpBins = 512;
+constexpr size_t kGrpLds = (size_t)kGrpCap * 4 * 2 + (size_t)(kGrpThreads / 64) * kGrpBins * 2;
+
+// One stable LSD radix pass over x[0..n) -> y, digit = (v >> sh) & (2^db - 1), db <= 9.
+// Wave w owns positions [w*kGrpWaveRecs, (w+1)*kGrpWaveRecs) (item it of lane l at
+// w*kGrpWaveRecs + it*64 + l), so (wave, item, lane) is the input order; lanes of one digit
+// find each other with db ballots, and a leader per digit bumps the wave's counter.
+__device__ __forceinline__ void grp_radix_pass(const uint32_t* x, uint32_t* y, int n, int sh, int db,
+                                               uint16_t* wcnt, uint32_t* wsum) {
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int nbins = 1 << db;
+    for (int e = tid; e < (kGrpThreads / 64) * kGrpBins; e += blockDim.x) wcnt[e] = 0;
+    __syncthreads();
+    uint16_t* my = wcnt + w * kGrpBins;
+    uint32_t v[kGrpItems], rk[kGrpItems];
+#pragma unroll
+    for (int it = 0; it < kGrpItems; ++it) {
+        const int pos = w * kGrpWaveRecs + it * 64 + lane;
+        const bool ok = pos < n;
+        v[it] = ok ? x[pos] : 0u;
+        const uint32_t d = (v[it] >> sh) & (uint32_t)(nbins - 1);
+        uint64_t peers = __ballot(ok);
+        if (!peers) { rk[it] = 0; continue; }  // wave-uniform
+        for (int q = 0; q < db; ++q) {
+            const uint64_t m = __ballot(ok && ((d >> q) & 1u));
+            peers &= ((d >> q) & 1u) ? m : ~m;
+        }
+        uint32_t old = 0;
+        const int leader = ok ? __ffsll((long long)peers) - 1 : 0;
+        if (ok && lane == leader) {
+            old = my[d];
+            my[d] = (uint16_t)(old + __popcll(peers));
+        }
+        old = __shfl(old, leader);
+        rk[it] = old + (uint32_t)__popcll(peers & ((1ull << lane) - 1ull));
+    }
+    __syncthreads();
+    {  // digit totals -> exclusive scan over digits -> per-(wave, digit) offsets in place
+        const int per = kGrpBins / kGrpThreads > 0 ? kGrpBins / kGrpThreads : 1;
+        (void)per;
+        uint32_t tot = 0;
+        if (tid < nbins)
+            for (int q = 0; q < kGrpThreads / 64; ++q) tot += wcnt[q * kGrpBins + tid];
+        uint32_t incl = tot;
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t up = __shfl_up(incl, o);
+            if (lane >= o) incl += up;
+        }
+        if (lane == 63) wsum[w] = incl;
+        __syncthreads();
+        uint32_t off = 0;
+        for (int q = 0; q < w; ++q) off += wsum[q];
+        if (tid < nbins) {
+            uint32_t r = off + incl - tot;
+            for (int q = 0; q < kGrpThreads / 64; ++q) {
+                const uint32_t c = wcnt[q * kGrpBins + tid];
+                wcnt[q * kGrpBins + tid] = (uint16_t)r;
+                r += c;
+            }
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int it = 0; it < kGrpItems; ++it) {
+        const int pos = w * kGrpWaveRecs + it * 64 + lane;
+        if (pos < n) y[my[(v[it] >> sh) & (uint32_t)(nbins - 1)] + rk[it]] = v[it];
+    }
+    __syncthreads();
+}
+
+// grid: one workgroup per bucket.  Outputs per bucket b (at b * kGrpCap): the bucket's
+// records in (home, arrival) order -- sk[] keys, sts[] timestamps, sv[] values -- and shd[]
+// heads (sorted index | local home << 14); grp_n[2b] = records, grp_n[2b+1] = heads (both 0
+// for an oversize bucket, whose records went to the punt list).
+__global__ void __launch_bounds__(kGrpThreads) k_sp_group(SegArgs a, int64_t* skey, int64_t* sts, int64_t* sval,
+                                                          uint32_t* shd, uint32_t* grp_n) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    uint32_t* ka = reinterpret_cast<uint32_t*>(smem);
+    uint32_t* kb = ka + kGrpCap;
+    uint16_t* wcnt = reinterpret_cast<uint16_t*>(kb + kGrpCap);
+    __shared__ uint32_t wsum[kGrpThreads / 64];
+    __shared__ uint32_t s_tot, s_nh;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int64_t b = blockIdx.x;
+    const uint32_t* col = a.col + b * a.ntiles;
+    const int sh = a.lcap - a.bb;
+    const uint64_t hmask = ((uint64_t)1 << sh) - 1;
+    const uint32_t sent = 1u << sh;
+    // records of the bucket; an oversize bucket's records all go to the punt list (arrival
+    // order), which the sort path replays: its keys are disjoint from the other buckets'
+    {
+        uint32_t c = 0;
+        for (int64_t t = tid; t < a.ntiles; t += blockDim.x) c += col[t] & 0xffffu;
+        c = (uint32_t)wave_sum(c);
+        if (lane == 0) wsum[w] = c;
+        __syncthreads();
+        if (tid == 0) {
+            uint32_t tot = 0;
+            for (int q = 0; q < kGrpThreads / 64; ++q) tot += wsum[q];
+            s_tot = tot;
+            s_nh = tot > (uint32_t)kGrpCap ? (uint32_t)atomicAdd(&a.st->overflow, (unsigned long long)tot) : 0u;
+        }
+        __syncthreads();
+    }
+    const uint32_t n = s_tot;
+    const bool over = n > (uint32_t)kGrpCap;
+    const uint32_t pbase = s_nh;
+    int64_t* ko = skey + b * kGrpCap;
+    int64_t* to = sts + b * kGrpCap;
+    int64_t* vo = sval + b * kGrpCap;
+    // Walks the bucket's runs in tile order (arrival order): thread t takes tiles [3t, 3t + 3)
+    // of each chunk of 3 * kGrpThreads tiles, 8 records at a time with their loads issued
+    // together; fn(position, key, buffer offset).
+    auto walk = [&](bool full, auto&& fn) {
+        uint32_t running = 0;
+        for (int64_t c0 = 0; c0 < a.ntiles; c0 += 3 * kGrpThreads) {
+            uint32_t d[3], sum = 0;
+#pragma unroll
+            for (int q = 0; q < 3; ++q) {
+                const int64_t t = c0 + 3 * tid + q;
+                d[q] = t < a.ntiles ? col[t] : 0u;
+                sum += d[q] & 0xffffu;
+            }
+            uint32_t incl = sum;
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t up = __shfl_up(incl, o);
+                if (lane >= o) incl += up;
+            }
+            if (lane == 63) wsum[w] = incl;
+            __syncthreads();
+            uint32_t pre = running + incl - sum, tot = 0;
+            for (int q = 0; q < kGrpThreads / 64; ++q) {
+                if (q < w) pre += wsum[q];
+                tot += wsum[q];
+            }
+            const uint32_t c0n = d[0] & 0xffffu, c1n = d[1] & 0xffffu;
+            uint32_t s3[3];
+#pragma unroll
+            for (int q = 0; q < 3; ++q) s3[q] = (uint32_t)((c0 + 3 * tid + q) * kSpTile + (d[q] >> 16));
+            for (uint32_t u0 = 0; u0 < sum; u0 += 8) {
+                uint32_t sv[8];
+                int64_t kk[8], tt[8], vv[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const uint32_t uu = u0 + u;
+                    sv[u] = uu < c0n ? s3[0] + uu : uu < c0n + c1n ? s3[1] + (uu - c0n) : s3[2] + (uu - c0n - c1n);
+                    const bool in = uu < sum;
+                    kk[u] = in ? a.p_key[sv[u]] : 0;
+                    tt[u] = in && full ? a.p_ts[sv[u]] : 0;
+                    vv[u] = in && full ? a.p_val[sv[u]] : 0;
+                }
+#pragma unroll
+                for (int u = 0; u < 8; ++u)
+                    if (u0 + u < sum) fn(pre + u0 + u, kk[u], tt[u], vv[u]);
+            }
+            running += tot;
+            __syncthreads();  // wsum is rewritten by the next chunk
+        }
+    };
+    if (over) {
+        walk(true, [&](uint32_t pos, int64_t k, int64_t t, int64_t v) {
+            a.pu_key[pbase + pos] = k;
+            a.pu_ts[pbase + pos] = t;
+            a.pu_val[pbase + pos] = v;
+        });
+        if (tid == 0) { grp_n[2 * b] = 0; grp_n[2 * b + 1] = 0; }
+        return;
+    }
+    walk(false, [&](uint32_t pos, int64_t k, int64_t, int64_t) {
+        const uint32_t lh = k == kEmptyKey ? sent : (uint32_t)(slot_hash(k) & hmask);
+        ka[pos] = (lh << kGrpPosBits) | pos;
+    });
+    // home bits [kGrpPosBits, kGrpPosBits + sh + 1): two passes
+    const int hb = sh + 1, db0 = (hb + 1) / 2, db1 = hb - db0;
+    grp_radix_pass(ka, kb, (int)n, kGrpPosBits, db0, wcnt, wsum);
+    const uint32_t* fin = kb;
+    uint32_t* inv = ka;
+    if (db1 > 0) {
+        grp_radix_pass(kb, ka, (int)n, kGrpPosBits + db0, db1, wcnt, wsum);
+        fin = ka;
+        inv = kb;
+    }
+    // sorted index of every position, then the records to their sorted places (the bucket's
+    // 3 x 128 KB of output stays in L2 while the workgroup fills it)
+    for (uint32_t i = tid; i < n; i += blockDim.x) inv[fin[i] & ((1u << kGrpPosBits) - 1u)] = i;
+    __syncthreads();
+    walk(true, [&](uint32_t pos, int64_t k, int64_t t, int64_t v) {
+        const uint32_t i = inv[pos];
+        ko[i] = k;
+        to[i] = t;
+        vo[i] = v;
+    });
+    uint32_t* ho = shd + b * kGrpCap;
+    uint32_t nh = 0;  // heads in sorted order: ordered compaction per chunk (waves, then lanes)
+    for (uint32_t i0 = 0; i0 < n; i0 += blockDim.x) {
+        const uint32_t i = i0 + tid;
+        bool h = false;
+        uint32_t x = 0;
+        if (i < n) {
+            x = fin[i];
+            h = i == 0 || (fin[i - 1] >> kGrpPosBits) != (x >> kGrpPosBits);
+        }
+        const uint64_t bal = __ballot(h);
+        if (lane == 0) wsum[w] = (uint32_t)__popcll(bal);
+        __syncthreads();
+        uint32_t base = nh, tot = 0;
+        for (int q = 0; q < kGrpThreads / 64; ++q) {
+            if (q < w) base += wsum[q];
+            tot += wsum[q];
+        }
+        if (h) ho[base + __popcll(bal & ((1ull << lane) - 1ull))] = i | ((x >> kGrpPosBits) << kGrpPosBits);
+        nh += tot;
+        __syncthreads();  // wsum is rewritten by the next chunk
+    }
+    if (tid == 0) { grp_n[2 * b] = n; grp_n[2 * b + 1] = nh; }
+}
+
+// The key's list after a replay (cnt sessions in the lane) -> its slot, or to the migration
+// list when it outgrew the slot (the key's later records of the batch then punt until the
+// migration).
+template <int AGG>
+__device__ __forceinline__ void sp_store(const SegArgs& a, const SessList& l, int cnt, int64_t slot, int64_t* sp,
+                                         int64_t w1) {
+    constexpr int SW = sess_words<AGG>();
+    if (cnt <= a.t.ring) {
+        uint64_t fired = 0;
+        int64_t due = INT64_MAX;
+        for (int q = 0; q < cnt; ++q) {
+            const Sess v = sl_get(l, q);
+            int64_t* x = sp + 2 + q * SW;
+            x[0] = v.s; x[1] = v.e; x[2] = v.a0;
+            if (SW == 4) x[3] = v.a1;
+            fired |= (uint64_t)(v.f != 0) << q;
+            due = min(due, due_time(v.e, v.f != 0, a.lateness));
+        }
+        sp[1] = (int64_t)((fired << 32) | (uint64_t)(uint32_t)cnt);
+        due_of(a.t)[slot] = due;
+    } else {
+        const unsigned long long at = atomicAdd(&a.st->pad[0], 1ull);
+        int64_t* m = a.mig + at * (2 + kWideWords * kLaneSess);
+        m[0] = slot;
+        m[1] = cnt;
+        for (int q = 0; q < cnt; ++q) {
+            const Sess v = sl_get(l, q);
+            int64_t* x = m + 2 + q * kWideWords;
+            x[0] = v.s; x[1] = v.e; x[2] = v.a0; x[3] = v.a1; x[4] = v.f;
+        }
+        atomicMax(&a.st->pad[1], (unsigned long long)cnt);
+        sp[1] = (int64_t)((uint64_t)w1 | kPuntMeta);
+    }
+}
+
+// One key's records among the home slot's run [r0, f) of the sorted records (r0 holds one
+// of them; the others are the run's records with this key), in arrival order, against the
+// key's slot -- seg_slot's replay, with the punt list instead of the wide pass.
+template <int AGG>
+__device__ __forceinline__ void sp_key(const SegArgs& a, const SessList& l, int64_t key, uint32_t r0, uint32_t f,
+                                       const int64_t* sk, const int64_t* sts, const int64_t* sv,
+                                       unsigned long long& late, unsigned long long& merges,
+                                       unsigned long long& flags, unsigned long long& ins) {
+    constexpr int SW = sess_words<AGG>();
+    int64_t L = 0;
+    for (uint32_t q = r0; q < f; ++q) L += sk[q] == key;
+    bool inserted;
+    const int64_t slot = find_or_insert(a.t, key, inserted);
+    int64_t* sp = slot >= 0 ? slot_ptr(a.t, slot) : nullptr;
+    if (sp) ins += inserted;
+    const int64_t w1 = sp ? sp[1] : 0;
+    bool ok = sp && !((uint64_t)w1 & (kBigMeta | kPuntMeta));
+    bool dry = ok && slot_cnt(w1) + L > kLaneSess;  // could outgrow the lane
+    const bool effects = a.lateness > 0 || a.lo_key;
+    const unsigned long long l0 = late, m0 = merges;
+    int cnt = 0;
+    while (ok) {  // at most two replays: dry, then (with effects) the real one
+        cnt = slot_cnt(w1);
+        for (int q = 0; q < cnt; ++q) {
+            const int64_t* x = sp + 2 + q * SW;
+            sl_put(l, q, Sess{x[0], x[1], x[2], SW == 4 ? x[3] : 0, (int64_t)slot_fired(w1, q)});
+        }
+        for (uint32_t q = r0; q < f && ok; ++q)
+            if (sk[q] == key)
+                ok = add_element_tv<AGG>(a, l, cnt, kLaneSess, key, sts[q], sv[q], late, merges, flags, dry);
+        if (!ok || !dry || !effects) break;
+        dry = false;
+        late = l0;
+        merges = m0;
+    }
+    if (!ok) {  // punt the key's records of the batch (kPuntMeta: also any that come after)
+        late = l0;
+        merges = m0;
+        unsigned long long at = atomicAdd(&a.st->overflow, (unsigned long long)L);
+        for (uint32_t q = r0; q < f; ++q) {
+            if (sk[q] != key) continue;
+            a.pu_key[at] = key;
+            a.pu_ts[at] = sts[q];
+            a.pu_val[at] = sv[q];
+            ++at;
+        }
+        if (sp) sp[1] = (int64_t)((uint64_t)w1 | kPuntMeta);
+        return;
+    }
+    sp_store<AGG>(a, l, cnt, slot, sp, w1);
+}
+
+// Replay: one thread per home slot of the batch (grid: kGrpCap / 256 x buckets); a run's
+// records are contiguous in the sorted arrays, so neighbouring threads read neighbouring runs.
+// The thread loads its home slot's line with its first kSpFast records.  A run of one key
+// that finds its slot within kSpProbe lines of the home slot (or claims a free one there)
+// replays from registers, kSpFast records at a time; the rest take sp_key (longer probes,
+// several keys per home slot, the wide table, a list that could outgrow the lane under
+// allowed lateness or the side output).
+constexpr int kSpKeyThreads = 256;
+constexpr int kSpFast = 8;
+constexpr int kSpProbe = 4;
+template <int AGG>
+__global__ void __launch_bounds__(kSpKeyThreads) k_sp_keys(SegArgs a, const int64_t* skey, const int64_t* sts,
+                                                           const int64_t* sval, const uint32_t* shd,
+                                                           const uint32_t* grp_n) {
+    constexpr int SW = sess_words<AGG>();
+    constexpr uint32_t pm = (1u << kGrpPosBits) - 1u;
+    __shared__ int64_t lane[5 * kLaneSess * kSpKeyThreads];
+    const SessList l{lane + threadIdx.x, kLaneSess * kSpKeyThreads, kSpKeyThreads};
+    const int64_t b = blockIdx.y;
+    const uint32_t n = grp_n[2 * b], nh = grp_n[2 * b + 1];
+    if ((uint32_t)blockIdx.x * kSpKeyThreads >= nh) return;  // block-uniform
+    const uint32_t j = blockIdx.x * kSpKeyThreads + threadIdx.x;
+    const int sh = a.lcap - a.bb;
+    const uint32_t sent = 1u << sh;
+    const bool effects = a.lateness > 0 || a.lo_key;
+    unsigned long long late = 0, merges = 0, flags = 0, ins = 0;
+    if (j < nh) {
+        const int64_t* sk = skey + b * kGrpCap;
+        const int64_t* st = sts + b * kGrpCap;
+        const int64_t* sv = sval + b * kGrpCap;
+        const uint32_t h = shd[b * kGrpCap + j];
+        const uint32_t e = h & pm, lh = h >> kGrpPosBits;
+        const uint32_t f = j + 1 < nh ? (shd[b * kGrpCap + j + 1] & pm) : n;
+        const uint32_t L = f - e;
+        const bool sentinel = lh == sent;
+        int64_t slot = sentinel ? a.t.cap : ((b << sh) | (int64_t)lh);
+        int64_t cur[8], rk[kSpFast], rt[kSpFast], rv[kSpFast];
+// (macros, not lambdas: a lambda capturing these arrays by reference would put them in scratch)
+#define SP_LOAD_LINE(sl)                                                                   \
+    do {                                                                                   \
+        const longlong2* p_ = reinterpret_cast<const longlong2*>(slot_ptr(a.t, (sl)));     \
+        _Pragma("unroll") for (int x_ = 0; x_ < 4; ++x_) {                                 \
+            const longlong2 y_ = p_[x_];                                                   \
+            cur[2 * x_] = y_.x;                                                            \
+            cur[2 * x_ + 1] = y_.y;                                                        \
+        }                                                                                  \
+    } while (0)
+#define SP_LOAD_RECS(c)  /* records [c, c + kSpFast) of the run (clamped) */              \
+    do {                                                                                   \
+        _Pragma("unroll") for (int u_ = 0; u_ < kSpFast; ++u_) {                           \
+            const uint32_t q_ = (c) + u_ < f ? (c) + u_ : e;                               \
+            rk[u_] = sk[q_];                                                               \
+            rt[u_] = st[q_];                                                               \
+            rv[u_] = sv[q_];                                                               \
+        }                                                                                  \
+    } while (0)
+        SP_LOAD_LINE(slot);
+        SP_LOAD_RECS(e);
+        const int64_t key = rk[0];
+        bool one = true;  // every record of the run has this key
+        for (uint32_t c = e;;) {
+#pragma unroll
+            for (int u = 1; u < kSpFast; ++u) one = one && (c + u >= f || rk[u] == key);
+            c += kSpFast;
+            if (c >= f || !one) break;
+            SP_LOAD_RECS(c);
+            one = one && rk[0] == key;
+        }
+        if (L > (uint32_t)kSpFast) SP_LOAD_RECS(e);
+        // the key's slot: its home slot's line, or up to kSpProbe - 1 lines further
+        bool found = sentinel;
+        for (int pr = 0; pr < kSpProbe && !found && one; ++pr) {
+            if (cur[0] == key) { found = true; break; }
+            if (cur[0] == kEmptyKey) {
+                const unsigned long long prev = atomicCAS((unsigned long long*)slot_ptr(a.t, slot),
+                                                          (unsigned long long)kEmptyKey, (unsigned long long)key);
+                if (prev == (unsigned long long)kEmptyKey) {  // a new key: an empty slot has word 1 == 0
+                    found = true;
+                    ins++;
+                    cur[1] = 0;
+                    break;
+                }
+                if ((int64_t)prev == key) { found = true; SP_LOAD_LINE(slot); break; }
+            }
+            slot = (slot + 1) & (a.t.cap - 1);
+            SP_LOAD_LINE(slot);
+        }
+        const int64_t w1 = cur[1];
+        const bool fast = found && one && !((uint64_t)w1 & (kBigMeta | kPuntMeta)) &&
+                          (!effects || slot_cnt(w1) + L <= kLaneSess);
+        if (fast) {  // the run replays from registers against the loaded line
+            int64_t* sp = slot_ptr(a.t, slot);
+            int cnt = slot_cnt(w1);
+#pragma unroll
+            for (int q = 0; q < (8 - 2) / SW; ++q)
+                if (q < cnt)
+                    sl_put(l, q, Sess{cur[2 + q * SW], cur[3 + q * SW], cur[4 + q * SW], SW == 4 ? cur[5 + q * SW] : 0,
+                                      (int64_t)slot_fired(w1, q)});
+            const unsigned long long l0 = late, m0 = merges;
+            bool ok = true;
+            for (uint32_t c = e; c < f && ok; c += kSpFast) {
+                if (c != e) SP_LOAD_RECS(c);
+                const int m = (int)min((uint32_t)kSpFast, f - c);
+                for (int u = 0; u < m && ok; ++u) {
+                    int64_t t = rt[0], v = rv[0];  // record u by selects (static indices: no scratch)
+#pragma unroll
+                    for (int x = 1; x < kSpFast; ++x) {
+                        t = u == x ? rt[x] : t;
+                        v = u == x ? rv[x] : v;
+                    }
+                    ok = add_element_tv<AGG>(a, l, cnt, kLaneSess, key, t, v, late, merges, flags, false);
+                }
+            }
+            if (ok) {
+                sp_store<AGG>(a, l, cnt, slot, sp, w1);
+            } else {  // outgrew the lane (no effects were written): punt the run
+                late = l0;
+                merges = m0;
+                const unsigned long long at = atomicAdd(&a.st->overflow, (unsigned long long)L);
+                for (uint32_t q = 0; q < L; ++q) {
+                    a.pu_key[at + q] = key;
+                    a.pu_ts[at + q] = st[e + q];
+                    a.pu_val[at + q] = sv[e + q];
+                }
+                sp[1] = (int64_t)((uint64_t)w1 | kPuntMeta);
+            }
+        } else {  // k_sp_slow replays it (a dense launch: no divergence against the fast runs)
+            const uint64_t bal = __ballot(true);
+            unsigned long long at = 0;
+            const int ld = __ffsll((long long)bal) - 1;
+            if (__lane_id() == ld) at = atomicAdd(&a.st->spills, (unsigned long long)__popcll(bal));
+            at = __shfl(at, ld);
+            a.slow[at + __popcll(bal & ((1ull << __lane_id()) - 1ull))] = ((uint32_t)b << kGrpPosBits) | j;
+        }
+#undef SP_LOAD_LINE
+#undef SP_LOAD_RECS
+    }
+    block_commit(a.st, late, ins, flags, 0, 0, merges);
+}
+
+// The home slots k_sp_keys left (a.slow, st->spills of them): every key of the slot's run in
+// order of its first record through sp_key (probe, several keys, the wide table, the dry
+// replay under allowed lateness or the side output).
+template <int AGG>
+__global__ void __launch_bounds__(kSpKeyThreads) k_sp_slow(SegArgs a, const int64_t* skey, const int64_t* sts,
+                                                           const int64_t* sval, const uint32_t* shd,
+                                                           const uint32_t* grp_n) {
+    constexpr uint32_t pm = (1u << kGrpPosBits) - 1u;
+    __shared__ int64_t lane[5 * kLaneSess * kSpKeyThreads];
+    const SessList l{lane + threadIdx.x, kLaneSess * kSpKeyThreads, kSpKeyThreads};
+    const uint64_t ns = a.st->spills;
+    unsigned long long late = 0, merges = 0, flags = 0, ins = 0;
+    for (uint64_t x = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; x < ns; x += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t id = a.slow[x];
+        const int64_t b = id >> kGrpPosBits;
+        const uint32_t j = id & pm;
+        const uint32_t n = grp_n[2 * b], nh = grp_n[2 * b + 1];
+        const int64_t* sk = skey + b * kGrpCap;
+        const int64_t* st = sts + b * kGrpCap;
+        const int64_t* sv = sval + b * kGrpCap;
+        const uint32_t e = shd[b * kGrpCap + j] & pm;
+        const uint32_t f = j + 1 < nh ? (shd[b * kGrpCap + j + 1] & pm) : n;
+        for (uint32_t r = e; r < f;) {
+            const int64_t kr = sk[r];
+            sp_key<AGG>(a, l, kr, r, f, sk, st, sv, late, merges, flags, ins);
+            uint32_t nx = f;
+            for (uint32_t q = r + 1; q < f && nx == f; ++q) {
+                const int64_t kq = sk[q];
+                bool seen = false;
+                for (uint32_t z = e; z < q && !seen; ++z) seen = sk[z] == kq;
+                if (!seen) nx = q;
+            }
+            r = nx;
+        }
+    }
+    block_commit(a.st, late, ins, flags, 0, 0, merges);
+}
+
+// After a replay with punts: clear the punt marks before the sort path replays the list.
+__global__ void __launch_bounds__(256) k_sp_unpunt(TableView t, const int64_t* pk, int64_t n) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t slot = find_slot(t, pk[i]);
+        if (slot < 0) continue;
+        int64_t* sp = slot_ptr(t, slot);
+        if ((uint64_t)sp[1] & kPuntMeta) atomicAnd((unsigned long long*)(sp + 1), ~(unsigned long long)kPuntMeta);
+    }
 }
 
 // Fire sweep, part 1: stream the due array (8 B per slot) and list the slots with
@@ -1036,6 +1712,13 @@ struct SessionState {
     uint32_t* r1 = nullptr;
     int64_t* mig = nullptr;  // migration lists (main pass -> wide table)
     int64_t* rec = nullptr;  // sessions: (ts, value) per record
+    // region-partitioned ingest (k_sp_*): pass-1 records (SoA), descriptor rows / columns,
+    // punted records
+    int64_t* sp_col3 = nullptr;  // key | ts | value, sp_cap each
+    uint32_t* sp_row = nullptr;  // sp_desc_cap each: rows, then columns
+    int64_t* pu_col3 = nullptr;  // punted key | ts | value, sp_cap each
+    uint32_t* sp_grp = nullptr;  // grouping: sorted keys | timestamps | values (int64), heads (u32), counts
+    int64_t sp_cap = 0, sp_desc_cap = 0, sp_grp_cap = 0;
     bool fresh = false;      // h_st matches the device (nothing launched since the last refresh)
     int gshift = 0;          // sessions: the last sort grouped records by slot >> gshift
     uint32_t* due_list = nullptr;  // fire sweep: main-table slots with something due
@@ -1193,6 +1876,7 @@ void session_destroy(SessionState* s) {
     hipFree(s->r0); hipFree(s->r1); hipFree(s->mig); hipFree(s->rec);
     hipFree(s->cnt_plan); hipFree(s->cnt_tmp); hipFree(s->due_list);
     hipFree(s->sort_tmp);
+    hipFree(s->sp_col3); hipFree(s->sp_row); hipFree(s->pu_col3); hipFree(s->sp_grp);
     hipFree(s->o_key); hipFree(s->o_start); hipFree(s->o_end); hipFree(s->o_res);
     for (auto* p : s->lo_buf) hipFree(p);
     for (int w = 0; w < 2; ++w) for (auto& p : s->ev_pending[w]) s->ev_pool.push_back(p);
@@ -1447,23 +2131,11 @@ static int count_ingest(SessionState* s, int64_t n, const int64_t* key, const in
     return GW_OK;
 }
 
-int session_ingest(SessionState* s, int64_t n, const int64_t* key, const int64_t* ts, const int64_t* val, int64_t wm,
-                   std::string& err) {
-    if (s->count_mode) return count_ingest(s, n, key, val, err);
+// The fields of a main-pass launch that both ingest paths share; reserves output room
+// (rows fired at once under allowed lateness, the late side output).
+static int seg_common(SessionState* s, SegArgs& a, int64_t n, int64_t wm, std::string& err) {
     int rc;
-    if ((rc = begin_launch(s, err))) return rc;
-    if (n <= 0) return GW_OK;
-    if ((int64_t)n > (int64_t)0x7fffffffLL) { err = "batch too large"; return GW_E_INVALID; }
-    auto ev = s->timing ? get_ev(s) : std::pair<hipEvent_t, hipEvent_t>{};
-    if (s->timing) SCHECK(hipEventRecord(ev.first, s->stream));
-    SegArgs a{};
-    if ((rc = group_records(s, n, key, ts, val, &a.slot, &a.perm, err))) return rc;
-    a.rec = s->rec;
-    a.gshift = s->gshift;
     a.n = n;
-    a.key = key;
-    a.ts = ts;
-    a.val = val;
     a.gap = s->cfg.gap;
     a.wm = wm;
     a.lateness = s->cfg.allowed_lateness;
@@ -1477,13 +2149,43 @@ int session_ingest(SessionState* s, int64_t n, const int64_t* key, const int64_t
         if ((rc = ensure_late(s, (int64_t)s->h_st->n_late_out + n, err))) return rc;
         a.lo_key = s->lo_buf[0]; a.lo_ts = s->lo_buf[1]; a.lo_val = s->lo_buf[2];
     }
-    // main pass
-    // st->overflow, pad[0], pad[1] were zeroed by k_sess_prep
-    s->h_st->overflow = s->h_st->pad[0] = s->h_st->pad[1] = 0;
     a.t = s->tv;
     a.w = s->wv;
-    a.punt = s->r0;
     a.mig = s->mig;
+    return GW_OK;
+}
+
+// Finished lists of more than K1 sessions (st->pad[0] of them) move to the wide table.
+static int run_migrate(SessionState* s, std::string& err) {
+    int rc;
+    const int64_t n_mig = (int64_t)s->h_st->pad[0];
+    if (!n_mig) return GW_OK;
+    if ((rc = ensure_wide(s, n_mig, (int64_t)s->h_st->pad[1], err))) return rc;
+    hipLaunchKernelGGL(k_sess_migrate, dim3(grid_of(n_mig)), dim3(256), 0, s->stream, s->tv, s->wv, s->mig, n_mig,
+                       s->cfg.allowed_lateness, s->d_st);
+    SCHECK(hipGetLastError());
+    if ((rc = session_refresh(s, err))) return rc;
+    if (s->h_st->flags & GW_DF_TABLE_FULL) { err = "session wide table full"; return GW_E_OOM; }
+    return GW_OK;
+}
+
+// Sort path: slot per record (k_sess_prep), stable radix sort by slot, one thread per key run
+// (k_sess_segment), migrations, then the wide pass over punted runs.  Replays the punt list
+// of the region path, and is the whole ingest under GW_SESSION_PATH=sort.
+static int ingest_sorted(SessionState* s, int64_t n, const int64_t* key, const int64_t* ts, const int64_t* val,
+                         int64_t wm, std::string& err) {
+    int rc;
+    SegArgs a{};
+    if ((rc = group_records(s, n, key, ts, val, &a.slot, &a.perm, err))) return rc;
+    a.rec = s->rec;
+    a.gshift = s->gshift;
+    a.key = key;
+    a.ts = ts;
+    a.val = val;
+    if ((rc = seg_common(s, a, n, wm, err))) return rc;
+    // main pass (st->overflow, pad[0], pad[1] were zeroed by k_sess_prep)
+    s->h_st->overflow = s->h_st->pad[0] = s->h_st->pad[1] = 0;
+    a.punt = s->r0;
     const int64_t per_block = (int64_t)kSegChunk * (kSegThreads / 64);
     const unsigned gs = (unsigned)((n + per_block - 1) / per_block);
 #define L(A) hipLaunchKernelGGL(k_sess_segment<A>, dim3(gs), dim3(kSegThreads), 0, s->stream, a)
@@ -1491,16 +2193,8 @@ int session_ingest(SessionState* s, int64_t n, const int64_t* key, const int64_t
 #undef L
     SCHECK(hipGetLastError());
     if ((rc = session_refresh(s, err))) return rc;
-    const int64_t n_mig = (int64_t)s->h_st->pad[0];
     int64_t n_punt = (int64_t)s->h_st->overflow;
-    if (n_mig) {  // finished lists of more than K1 sessions move to the wide table
-        if ((rc = ensure_wide(s, n_mig, (int64_t)s->h_st->pad[1], err))) return rc;
-        hipLaunchKernelGGL(k_sess_migrate, dim3(grid_of(n_mig)), dim3(256), 0, s->stream, s->tv, s->wv, s->mig, n_mig,
-                           s->cfg.allowed_lateness, s->d_st);
-        SCHECK(hipGetLastError());
-        if ((rc = session_refresh(s, err))) return rc;
-        if (s->h_st->flags & GW_DF_TABLE_FULL) { err = "session wide table full"; return GW_E_OOM; }
-    }
+    if ((rc = run_migrate(s, err))) return rc;
     // wide pass over the punted runs; runs that do not fit K2 retry after widening
     uint32_t* rin = s->r0;
     uint32_t* rout = s->r1;
@@ -1526,6 +2220,142 @@ int session_ingest(SessionState* s, int64_t n, const int64_t* key, const int64_t
         }
         std::swap(rin, rout);
     }
+    return GW_OK;
+}
+
+static void sp_opt_in() {
+    static bool done = false;
+    if (!done) {
+        hipFuncSetAttribute((const void*)k_sp_part, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kSpPartLds);
+        hipFuncSetAttribute((const void*)k_sp_group, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kGrpLds);
+        done = true;
+    }
+}
+
+// Region path (k_sp_part / k_sp_transpose / k_sp_group / k_sp_keys), then migrations, then the sort
+// path over the punted records.
+static int ingest_region(SessionState* s, int64_t n, const int64_t* key, const int64_t* ts, const int64_t* val,
+                         int64_t wm, std::string& err) {
+    int rc;
+    // room for n new keys, as group_records keeps it: every key of the batch finds a slot
+    // within the probe limit unless the table is nearly full (the punt list takes those)
+    if ((double)(s->h_st->used_slots + n) > 0.7 * (double)s->tv.cap &&
+        ((double)s->h_st->used_slots > 0.7 * (double)s->tv.cap ||
+         (double)(s->h_st->used_slots + n) > 0.95 * (double)s->tv.cap)) {
+        int64_t want = s->tv.cap;
+        while ((double)(s->h_st->used_slots + n) > 0.7 * (double)want) want *= 2;
+        if ((rc = regrow(s, s->tv, want, s->tv.ring, false, err))) return rc;
+    }
+    if ((rc = ensure_bufs(s, n, err))) return rc;  // the migration list
+    int lcap = 0;
+    while (((int64_t)1 << lcap) < s->tv.cap) ++lcap;
+    int bb = std::min(lcap, 10);
+    if (lcap - bb > kGrpMaxHomeBits) bb = lcap - kGrpMaxHomeBits;  // the sort key's home bits
+    if (bb > 10) return ingest_sorted(s, n, key, ts, val, wm, err);  // beyond 2^26 slots
+    const int nb = 1 << bb;
+    const int64_t ntiles = (n + kSpTile - 1) / kSpTile;
+    const int64_t recs = ntiles * kSpTile;
+    if (recs > s->sp_cap || (int64_t)nb * kGrpCap > s->sp_grp_cap || ntiles * nb > s->sp_desc_cap) {
+        SCHECK(hipStreamSynchronize(s->stream));
+        if (recs > s->sp_cap) {
+            hipFree(s->sp_col3); hipFree(s->pu_col3);
+            s->sp_col3 = nullptr; s->pu_col3 = nullptr;
+            const int64_t c = std::max<int64_t>(recs + recs / 4, kSpTile * 16);
+            SCHECK(hipMalloc((void**)&s->sp_col3, (size_t)c * 24));
+            SCHECK(hipMalloc((void**)&s->pu_col3, (size_t)c * 28));  // + the slow-slot list (u32)
+            s->sp_cap = c;
+        }
+        if ((int64_t)nb * kGrpCap > s->sp_grp_cap) {
+            hipFree(s->sp_grp);
+            s->sp_grp = nullptr;
+            const int64_t c = (int64_t)nb * kGrpCap;
+            SCHECK(hipMalloc((void**)&s->sp_grp, (size_t)(7 * c + 2 * nb) * 4));  // sorted records (24 B), heads
+            s->sp_grp_cap = c;
+        }
+        if (ntiles * nb > s->sp_desc_cap) {
+            hipFree(s->sp_row);
+            s->sp_row = nullptr;
+            const int64_t c = std::max<int64_t>((ntiles + ntiles / 4 + 16) * nb, 1 << 16);
+            SCHECK(hipMalloc((void**)&s->sp_row, (size_t)c * 2 * 4));
+            s->sp_desc_cap = c;
+        }
+    }
+    const int64_t C = s->sp_cap, G = s->sp_grp_cap;
+    int64_t* pk = s->sp_col3;
+    uint32_t* row = s->sp_row;
+    uint32_t* col = s->sp_row + s->sp_desc_cap;
+    int64_t* skey = reinterpret_cast<int64_t*>(s->sp_grp);
+    int64_t* sts = skey + G;
+    int64_t* sval = sts + G;
+    uint32_t* shd = reinterpret_cast<uint32_t*>(sval + G);
+    uint32_t* grp_n = shd + G;
+    sp_opt_in();
+    if ((rc = zero_word_async(s, offsetof(DevStatus, overflow), err))) return rc;
+    if ((rc = zero_word_async(s, offsetof(DevStatus, pad[0]), err))) return rc;
+    if ((rc = zero_word_async(s, offsetof(DevStatus, pad[1]), err))) return rc;
+    hipLaunchKernelGGL(k_sp_part, dim3((unsigned)ntiles), dim3(kSpThreads), kSpPartLds, s->stream, key, ts, val, n,
+                       s->tv.cap, lcap, bb, pk, pk + C, pk + 2 * C, row, s->d_st);
+    hipLaunchKernelGGL(k_sp_transpose, dim3((unsigned)((ntiles + 63) / 64), (unsigned)((nb + 63) / 64)), dim3(256), 0,
+                       s->stream, row, col, ntiles, nb);
+    SCHECK(hipGetLastError());
+    SegArgs a{};
+    if ((rc = seg_common(s, a, n, wm, err))) return rc;
+    a.p_key = pk;
+    a.p_ts = pk + C;
+    a.p_val = pk + 2 * C;
+    a.col = col;
+    a.ntiles = ntiles;
+    a.lcap = lcap;
+    a.bb = bb;
+    a.pu_key = s->pu_col3;
+    a.pu_ts = s->pu_col3 + C;
+    a.pu_val = s->pu_col3 + 2 * C;
+    static const int sp_exp = getenv("GW_SP_EXP") ? atoi(getenv("GW_SP_EXP")) : 0;
+    a.exp = sp_exp;
+    hipLaunchKernelGGL(k_sp_group, dim3((unsigned)nb), dim3(kGrpThreads), kGrpLds, s->stream, a, skey, sts, sval, shd,
+                       grp_n);
+    a.slow = reinterpret_cast<uint32_t*>(s->pu_col3 + 3 * C);
+    if ((rc = zero_word_async(s, offsetof(DevStatus, spills), err))) return rc;
+#define L(A)                                                                                                   \
+    hipLaunchKernelGGL(k_sp_keys<A>, dim3((unsigned)(kGrpCap / kSpKeyThreads), (unsigned)nb), dim3(kSpKeyThreads), 0, \
+                       s->stream, a, skey, sts, sval, shd, grp_n);                                              \
+    hipLaunchKernelGGL(k_sp_slow<A>, dim3(1024), dim3(kSpKeyThreads), 0, s->stream, a, skey, sts, sval, shd, grp_n)
+    GW_AGG_SWITCH(s->cfg.agg, L);
+#undef L
+    SCHECK(hipGetLastError());
+    if ((rc = session_refresh(s, err))) return rc;
+    const int64_t n_punt = (int64_t)s->h_st->overflow;
+    s->stats.session_punted += n_punt;
+    if (sp_exp)
+        fprintf(stderr, "[sp_keys] slow home slots %llu of batch %lld, punted %lld\n",
+                (unsigned long long)s->h_st->spills, (long long)n, (long long)n_punt);
+    s->stats.session_slow += (int64_t)s->h_st->spills;
+    if ((rc = run_migrate(s, err))) return rc;
+    if (!n_punt) return GW_OK;
+    hipLaunchKernelGGL(k_sp_unpunt, dim3(grid_of(n_punt)), dim3(256), 0, s->stream, s->tv, a.pu_key, n_punt);
+    SCHECK(hipGetLastError());
+    return ingest_sorted(s, n_punt, a.pu_key, a.pu_ts, a.pu_val, wm, err);
+}
+
+// GW_SESSION_PATH=region|sort picks the ingest path (GW_SESSION_SORT_BITS, the sort path's
+// group tests, implies sort).
+static bool region_ingest_enabled() {
+    const char* p = getenv("GW_SESSION_PATH");
+    if (p) return strcmp(p, "sort") != 0;
+    return getenv("GW_SESSION_SORT_BITS") ? false : kSessionRegionDefault != 0;
+}
+
+int session_ingest(SessionState* s, int64_t n, const int64_t* key, const int64_t* ts, const int64_t* val, int64_t wm,
+                   std::string& err) {
+    if (s->count_mode) return count_ingest(s, n, key, val, err);
+    int rc;
+    if ((rc = begin_launch(s, err))) return rc;
+    if (n <= 0) return GW_OK;
+    if ((int64_t)n > (int64_t)0x7fffffffLL) { err = "batch too large"; return GW_E_INVALID; }
+    auto ev = s->timing ? get_ev(s) : std::pair<hipEvent_t, hipEvent_t>{};
+    if (s->timing) SCHECK(hipEventRecord(ev.first, s->stream));
+    rc = region_ingest_enabled() ? ingest_region(s, n, key, ts, val, wm, err) : ingest_sorted(s, n, key, ts, val, wm, err);
+    if (rc) return rc;
     if (s->timing) {
         SCHECK(hipEventRecord(ev.second, s->stream));
         s->ev_pending[0].push_back(ev);
@@ -1726,6 +2556,8 @@ void session_stats(SessionState* s, gw_stats* out) {
     out->session_merges = (int64_t)s->h_st->merges;
     out->fires = s->stats.fires;
     out->rehashes = s->stats.rehashes;
+    out->session_punted = s->stats.session_punted;
+    out->session_slow = s->stats.session_slow;
 }
 
 void session_enable_timing(SessionState* s, bool on) { s->timing = on; }

@@ -65,7 +65,7 @@ def run(oracle_lib, kw, keys, ts, vals, batches, capacity_hint, flags=0):
 
 
 CFGS = [dict(assigner="tumbling", size=1000, slide=1000), dict(assigner="sliding", size=2000, slide=500),
-        dict(assigner="sliding", size=1500, slide=500, lateness=700)]
+        dict(assigner="sliding", size=1500, slide=500, lateness=300)]  # ring 6 <= 8
 AGGS = ["count", "sum_i64", "sum_i32", "min_i64", "max_i64", "avg_i64"]
 
 
@@ -88,7 +88,9 @@ def test_records_beyond_narrow_are_exact(oracle_lib, odd, frac, agg):
     g, o, fmts = run(oracle_lib, kw, keys, ts, vals, batches, 1 << 19)
     assert compare(g, o, agg == "avg_i64") == []
     if frac > 0.1 and not (odd == "val" and agg == "count"):
-        assert fmts[0] == 2 and fmts[-1] == 1  # too many misfits: compact records from the next window
+        # too many misfits: compact records from the next window (and wide ones after that
+        # when the values do not fit compact records' 32 bits either)
+        assert fmts[0] == 2 and 1 in fmts and fmts[-1] == (0 if odd == "val" else 1)
 
 
 def test_narrow_spills_and_growth(oracle_lib):
