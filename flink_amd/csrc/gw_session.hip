@@ -69,9 +69,8 @@ struct SegArgs {
     DevStatus* st;
     int gshift;             // records are grouped by slot >> gshift (the sort skips the low bits)
     // region-partitioned ingest (k_sp_part / k_sp_group / k_sp_keys)
-    const int64_t* p_key;   // pass-1 output, tile-major, bucket runs inside each tile (SoA)
-    const int64_t* p_ts;
-    const int64_t* p_val;
+    const int64_t* p_key;   // pass-1 output, tile-major, bucket runs inside each tile: keys
+    const longlong2* p_tv;  //   and (timestamp, value) pairs
     const uint32_t* col;    // [bucket][tile] run descriptors (start << 16 | count)
     int64_t ntiles;
     int lcap, bb;           // log2(table capacity), bucket bits (bucket = home >> (lcap - bb))
@@ -539,7 +538,7 @@ constexpr size_t kSpPartLds = (size_t)kSpTile * 3 * 8 + (size_t)(kSpThreads / 64
 // private counter, and a block scan over (bucket, wave) turns the counters into offsets.
 __global__ void __launch_bounds__(kSpThreads) k_sp_part(const int64_t* key, const int64_t* ts, const int64_t* val,
                                                         int64_t n, int64_t cap, int lcap, int bb, int64_t* o_key,
-                                                        int64_t* o_ts, int64_t* o_val, uint32_t* row, DevStatus* st) {
+                                                        longlong2* o_tv, uint32_t* row, DevStatus* st) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     int64_t* s_key = reinterpret_cast<int64_t*>(smem);
     int64_t* s_ts = s_key + kSpTile;
@@ -627,10 +626,9 @@ __global__ void __launch_bounds__(kSpThreads) k_sp_part(const int64_t* key, cons
     __syncthreads();
     const int64_t base = tile * kSpTile;
     const int cnt = (int)(hi - lo);
-    for (int j = tid; j < cnt; j += blockDim.x) {  // read back by the replay: default cache policy
+    for (int j = tid; j < cnt; j += blockDim.x) {  // read back by the grouping and the replay
         o_key[base + j] = s_key[j];
-        o_ts[base + j] = s_ts[j];
-        o_val[base + j] = s_val[j];
+        o_tv[base + j] = longlong2{s_ts[j], s_val[j]};
     }
     for (int b = tid; b < nb; b += blockDim.x) row[tile * nb + b] = (ls[b] << 16) | lh[b];
     block_commit(st, 0, 0, flags, 0);
@@ -741,12 +739,12 @@ __device__ __forceinline__ void grp_radix_pass(const uint32_t* x, uint32_t* y, i
     __syncthreads();
 }
 
-// grid: one workgroup per bucket.  Outputs per bucket b (at b * kGrpCap): the bucket's
-// records in (home, arrival) order -- sk[] keys, sts[] timestamps, sv[] values -- and shd[]
-// heads (sorted index | local home << 14); grp_n[2b] = records, grp_n[2b+1] = heads (both 0
-// for an oversize bucket, whose records went to the punt list).
-__global__ void __launch_bounds__(kGrpThreads) k_sp_group(SegArgs a, int64_t* skey, int64_t* sts, int64_t* sval,
-                                                          uint32_t* shd, uint32_t* grp_n) {
+// grid: one workgroup per bucket.  Outputs per bucket b (at b * kGrpCap): perm[] the
+// pass-1 buffer offsets of the bucket's records in (home, arrival) order, shd[] heads (sorted
+// index | local home << 14); grp_n[2b] = records, grp_n[2b+1] = heads (both 0 for an
+// oversize bucket, whose records went to the punt list).  gsrc: scratch, offset by position.
+__global__ void __launch_bounds__(kGrpThreads) k_sp_group(SegArgs a, uint32_t* gsrc, uint32_t* perm, uint32_t* shd,
+                                                          uint32_t* grp_n) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     uint32_t* ka = reinterpret_cast<uint32_t*>(smem);
     uint32_t* kb = ka + kGrpCap;
@@ -759,6 +757,7 @@ __global__ void __launch_bounds__(kGrpThreads) k_sp_group(SegArgs a, int64_t* sk
     const int sh = a.lcap - a.bb;
     const uint64_t hmask = ((uint64_t)1 << sh) - 1;
     const uint32_t sent = 1u << sh;
+    uint32_t* gs = gsrc + b * kGrpCap;
     // records of the bucket; an oversize bucket's records all go to the punt list (arrival
     // order), which the sort path replays: its keys are disjoint from the other buckets'
     {
@@ -778,91 +777,75 @@ __global__ void __launch_bounds__(kGrpThreads) k_sp_group(SegArgs a, int64_t* sk
     const uint32_t n = s_tot;
     const bool over = n > (uint32_t)kGrpCap;
     const uint32_t pbase = s_nh;
-    int64_t* ko = skey + b * kGrpCap;
-    int64_t* to = sts + b * kGrpCap;
-    int64_t* vo = sval + b * kGrpCap;
-    // Walks the bucket's runs in tile order (arrival order): thread t takes tiles [3t, 3t + 3)
-    // of each chunk of 3 * kGrpThreads tiles, 8 records at a time with their loads issued
-    // together; fn(position, key, buffer offset).
-    auto walk = [&](bool full, auto&& fn) {
-        uint32_t running = 0;
-        for (int64_t c0 = 0; c0 < a.ntiles; c0 += 3 * kGrpThreads) {
-            uint32_t d[3], sum = 0;
+    // the bucket's runs in tile order (arrival order): thread t takes tiles [3t, 3t + 3) of each
+    // chunk of 3 * kGrpThreads tiles, 8 records at a time with their loads issued together
+    uint32_t running = 0;
+    for (int64_t c0 = 0; c0 < a.ntiles; c0 += 3 * kGrpThreads) {
+        uint32_t d[3], sum = 0;
 #pragma unroll
-            for (int q = 0; q < 3; ++q) {
-                const int64_t t = c0 + 3 * tid + q;
-                d[q] = t < a.ntiles ? col[t] : 0u;
-                sum += d[q] & 0xffffu;
-            }
-            uint32_t incl = sum;
-            for (int o = 1; o < 64; o <<= 1) {
-                const uint32_t up = __shfl_up(incl, o);
-                if (lane >= o) incl += up;
-            }
-            if (lane == 63) wsum[w] = incl;
-            __syncthreads();
-            uint32_t pre = running + incl - sum, tot = 0;
-            for (int q = 0; q < kGrpThreads / 64; ++q) {
-                if (q < w) pre += wsum[q];
-                tot += wsum[q];
-            }
-            const uint32_t c0n = d[0] & 0xffffu, c1n = d[1] & 0xffffu;
-            uint32_t s3[3];
-#pragma unroll
-            for (int q = 0; q < 3; ++q) s3[q] = (uint32_t)((c0 + 3 * tid + q) * kSpTile + (d[q] >> 16));
-            for (uint32_t u0 = 0; u0 < sum; u0 += 8) {
-                uint32_t sv[8];
-                int64_t kk[8], tt[8], vv[8];
-#pragma unroll
-                for (int u = 0; u < 8; ++u) {
-                    const uint32_t uu = u0 + u;
-                    sv[u] = uu < c0n ? s3[0] + uu : uu < c0n + c1n ? s3[1] + (uu - c0n) : s3[2] + (uu - c0n - c1n);
-                    const bool in = uu < sum;
-                    kk[u] = in ? a.p_key[sv[u]] : 0;
-                    tt[u] = in && full ? a.p_ts[sv[u]] : 0;
-                    vv[u] = in && full ? a.p_val[sv[u]] : 0;
-                }
-#pragma unroll
-                for (int u = 0; u < 8; ++u)
-                    if (u0 + u < sum) fn(pre + u0 + u, kk[u], tt[u], vv[u]);
-            }
-            running += tot;
-            __syncthreads();  // wsum is rewritten by the next chunk
+        for (int q = 0; q < 3; ++q) {
+            const int64_t t = c0 + 3 * tid + q;
+            d[q] = t < a.ntiles ? col[t] : 0u;
+            sum += d[q] & 0xffffu;
         }
-    };
+        uint32_t incl = sum;
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t up = __shfl_up(incl, o);
+            if (lane >= o) incl += up;
+        }
+        if (lane == 63) wsum[w] = incl;
+        __syncthreads();
+        uint32_t pre = running + incl - sum, tot = 0;
+        for (int q = 0; q < kGrpThreads / 64; ++q) {
+            if (q < w) pre += wsum[q];
+            tot += wsum[q];
+        }
+        const uint32_t c0n = d[0] & 0xffffu, c1n = d[1] & 0xffffu;
+        uint32_t s3[3];
+#pragma unroll
+        for (int q = 0; q < 3; ++q) s3[q] = (uint32_t)((c0 + 3 * tid + q) * kSpTile + (d[q] >> 16));
+        for (uint32_t u0 = 0; u0 < sum; u0 += 8) {
+            uint32_t sv[8];
+            int64_t kk[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const uint32_t uu = u0 + u;
+                sv[u] = uu < c0n ? s3[0] + uu : uu < c0n + c1n ? s3[1] + (uu - c0n) : s3[2] + (uu - c0n - c1n);
+                kk[u] = uu < sum ? a.p_key[sv[u]] : 0;
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const uint32_t uu = u0 + u;
+                if (uu >= sum) break;
+                const uint32_t pos = pre + uu;
+                if (over) {
+                    const longlong2 tv = a.p_tv[sv[u]];
+                    a.pu_key[pbase + pos] = kk[u];
+                    a.pu_ts[pbase + pos] = tv.x;
+                    a.pu_val[pbase + pos] = tv.y;
+                } else {
+                    const uint32_t lh = kk[u] == kEmptyKey ? sent : (uint32_t)(slot_hash(kk[u]) & hmask);
+                    ka[pos] = (lh << kGrpPosBits) | pos;
+                    gs[pos] = sv[u];
+                }
+            }
+        }
+        running += tot;
+        __syncthreads();  // wsum is rewritten by the next chunk
+    }
     if (over) {
-        walk(true, [&](uint32_t pos, int64_t k, int64_t t, int64_t v) {
-            a.pu_key[pbase + pos] = k;
-            a.pu_ts[pbase + pos] = t;
-            a.pu_val[pbase + pos] = v;
-        });
         if (tid == 0) { grp_n[2 * b] = 0; grp_n[2 * b + 1] = 0; }
         return;
     }
-    walk(false, [&](uint32_t pos, int64_t k, int64_t, int64_t) {
-        const uint32_t lh = k == kEmptyKey ? sent : (uint32_t)(slot_hash(k) & hmask);
-        ka[pos] = (lh << kGrpPosBits) | pos;
-    });
     // home bits [kGrpPosBits, kGrpPosBits + sh + 1): two passes
     const int hb = sh + 1, db0 = (hb + 1) / 2, db1 = hb - db0;
     grp_radix_pass(ka, kb, (int)n, kGrpPosBits, db0, wcnt, wsum);
     const uint32_t* fin = kb;
-    uint32_t* inv = ka;
     if (db1 > 0) {
         grp_radix_pass(kb, ka, (int)n, kGrpPosBits + db0, db1, wcnt, wsum);
         fin = ka;
-        inv = kb;
     }
-    // sorted index of every position, then the records to their sorted places (the bucket's
-    // 3 x 128 KB of output stays in L2 while the workgroup fills it)
-    for (uint32_t i = tid; i < n; i += blockDim.x) inv[fin[i] & ((1u << kGrpPosBits) - 1u)] = i;
-    __syncthreads();
-    walk(true, [&](uint32_t pos, int64_t k, int64_t t, int64_t v) {
-        const uint32_t i = inv[pos];
-        ko[i] = k;
-        to[i] = t;
-        vo[i] = v;
-    });
+    uint32_t* po = perm + b * kGrpCap;
     uint32_t* ho = shd + b * kGrpCap;
     uint32_t nh = 0;  // heads in sorted order: ordered compaction per chunk (waves, then lanes)
     for (uint32_t i0 = 0; i0 < n; i0 += blockDim.x) {
@@ -871,6 +854,7 @@ __global__ void __launch_bounds__(kGrpThreads) k_sp_group(SegArgs a, int64_t* sk
         uint32_t x = 0;
         if (i < n) {
             x = fin[i];
+            po[i] = gs[x & ((1u << kGrpPosBits) - 1u)];
             h = i == 0 || (fin[i - 1] >> kGrpPosBits) != (x >> kGrpPosBits);
         }
         const uint64_t bal = __ballot(h);
@@ -923,17 +907,17 @@ __device__ __forceinline__ void sp_store(const SegArgs& a, const SessList& l, in
     }
 }
 
-// One key's records among the home slot's run [r0, f) of the sorted records (r0 holds one
-// of them; the others are the run's records with this key), in arrival order, against the
-// key's slot -- seg_slot's replay, with the punt list instead of the wide pass.
+// One key's records among the home slot's run [r0, f) of the sorted order (pr: pass-1
+// offsets; r0 holds one of them, the others are the run's records with this key), in
+// arrival order, against the key's slot -- seg_slot's replay, with the punt list instead of
+// the wide pass.
 template <int AGG>
 __device__ __forceinline__ void sp_key(const SegArgs& a, const SessList& l, int64_t key, uint32_t r0, uint32_t f,
-                                       const int64_t* sk, const int64_t* sts, const int64_t* sv,
-                                       unsigned long long& late, unsigned long long& merges,
+                                       const uint32_t* pr, unsigned long long& late, unsigned long long& merges,
                                        unsigned long long& flags, unsigned long long& ins) {
     constexpr int SW = sess_words<AGG>();
     int64_t L = 0;
-    for (uint32_t q = r0; q < f; ++q) L += sk[q] == key;
+    for (uint32_t q = r0; q < f; ++q) L += a.p_key[pr[q]] == key;
     bool inserted;
     const int64_t slot = find_or_insert(a.t, key, inserted);
     int64_t* sp = slot >= 0 ? slot_ptr(a.t, slot) : nullptr;
@@ -950,9 +934,12 @@ __device__ __forceinline__ void sp_key(const SegArgs& a, const SessList& l, int6
             const int64_t* x = sp + 2 + q * SW;
             sl_put(l, q, Sess{x[0], x[1], x[2], SW == 4 ? x[3] : 0, (int64_t)slot_fired(w1, q)});
         }
-        for (uint32_t q = r0; q < f && ok; ++q)
-            if (sk[q] == key)
-                ok = add_element_tv<AGG>(a, l, cnt, kLaneSess, key, sts[q], sv[q], late, merges, flags, dry);
+        for (uint32_t q = r0; q < f && ok; ++q) {
+            const uint32_t o = pr[q];
+            if (a.p_key[o] != key) continue;
+            const longlong2 tv = a.p_tv[o];
+            ok = add_element_tv<AGG>(a, l, cnt, kLaneSess, key, tv.x, tv.y, late, merges, flags, dry);
+        }
         if (!ok || !dry || !effects) break;
         dry = false;
         late = l0;
@@ -963,10 +950,12 @@ __device__ __forceinline__ void sp_key(const SegArgs& a, const SessList& l, int6
         merges = m0;
         unsigned long long at = atomicAdd(&a.st->overflow, (unsigned long long)L);
         for (uint32_t q = r0; q < f; ++q) {
-            if (sk[q] != key) continue;
+            const uint32_t o = pr[q];
+            if (a.p_key[o] != key) continue;
+            const longlong2 tv = a.p_tv[o];
             a.pu_key[at] = key;
-            a.pu_ts[at] = sts[q];
-            a.pu_val[at] = sv[q];
+            a.pu_ts[at] = tv.x;
+            a.pu_val[at] = tv.y;
             ++at;
         }
         if (sp) sp[1] = (int64_t)((uint64_t)w1 | kPuntMeta);
@@ -975,43 +964,69 @@ __device__ __forceinline__ void sp_key(const SegArgs& a, const SessList& l, int6
     sp_store<AGG>(a, l, cnt, slot, sp, w1);
 }
 
-// Replay: one thread per home slot of the batch (grid: kGrpCap / 256 x buckets); a run's
-// records are contiguous in the sorted arrays, so neighbouring threads read neighbouring runs.
-// The thread loads its home slot's line with its first kSpFast records.  A run of one key
-// that finds its slot within kSpProbe lines of the home slot (or claims a free one there)
-// replays from registers, kSpFast records at a time; the rest take sp_key (longer probes,
-// several keys per home slot, the wide table, a list that could outgrow the lane under
-// allowed lateness or the side output).
+// Every key of a home slot's run [e, f), in order of its first record (several keys per home
+// slot are rare), through sp_key.
+template <int AGG>
+__device__ __forceinline__ void sp_run(const SegArgs& a, const SessList& l, uint32_t e, uint32_t f, const uint32_t* pr,
+                                       unsigned long long& late, unsigned long long& merges,
+                                       unsigned long long& flags, unsigned long long& ins) {
+    for (uint32_t r = e; r < f;) {
+        sp_key<AGG>(a, l, a.p_key[pr[r]], r, f, pr, late, merges, flags, ins);
+        uint32_t nx = f;
+        for (uint32_t q = r + 1; q < f && nx == f; ++q) {
+            const int64_t kq = a.p_key[pr[q]];
+            bool seen = false;
+            for (uint32_t z = e; z < q && !seen; ++z) seen = a.p_key[pr[z]] == kq;
+            if (!seen) nx = q;
+        }
+        r = nx;
+    }
+}
+
+// Replay: one thread per home slot.  A persistent grid (a multiple of 8 workgroups): the
+// workgroups with blockIdx % 8 == x walk the buckets b == x (mod 8) and deal their chunks of
+// 256 heads round-robin among themselves -- under the round-robin placement of
+// workgroups on the 8 XCDs (speed only, never correctness) a bucket's pass-1 lines are read
+// into one L2 and its records gathered from there.  The thread loads its home slot's line
+// with the offsets of its first kSpFast records, then their keys and (timestamp, value)
+// pairs.  A run of one key that finds its slot within kSpProbe lines of the home slot (or
+// claims a free one there) replays from registers, kSpFast records at a time; the rest go on
+// the slow list for k_sp_slow (longer probes, several keys per home slot, the wide table, a
+// list that could outgrow the lane under allowed lateness or the side output).
 constexpr int kSpKeyThreads = 256;
 constexpr int kSpFast = 8;
 constexpr int kSpProbe = 4;
 template <int AGG>
-__global__ void __launch_bounds__(kSpKeyThreads) k_sp_keys(SegArgs a, const int64_t* skey, const int64_t* sts,
-                                                           const int64_t* sval, const uint32_t* shd,
-                                                           const uint32_t* grp_n) {
+__global__ void __launch_bounds__(kSpKeyThreads) k_sp_keys(SegArgs a, const uint32_t* perm, const uint32_t* shd,
+                                                           const uint32_t* grp_n, int nb) {
     constexpr int SW = sess_words<AGG>();
     constexpr uint32_t pm = (1u << kGrpPosBits) - 1u;
     __shared__ int64_t lane[5 * kLaneSess * kSpKeyThreads];
     const SessList l{lane + threadIdx.x, kLaneSess * kSpKeyThreads, kSpKeyThreads};
-    const int64_t b = blockIdx.y;
-    const uint32_t n = grp_n[2 * b], nh = grp_n[2 * b + 1];
-    if ((uint32_t)blockIdx.x * kSpKeyThreads >= nh) return;  // block-uniform
-    const uint32_t j = blockIdx.x * kSpKeyThreads + threadIdx.x;
     const int sh = a.lcap - a.bb;
     const uint32_t sent = 1u << sh;
     const bool effects = a.lateness > 0 || a.lo_key;
+    const int xg = blockIdx.x & 7, per = gridDim.x >> 3, me = blockIdx.x >> 3;
     unsigned long long late = 0, merges = 0, flags = 0, ins = 0;
-    if (j < nh) {
-        const int64_t* sk = skey + b * kGrpCap;
-        const int64_t* st = sts + b * kGrpCap;
-        const int64_t* sv = sval + b * kGrpCap;
-        const uint32_t h = shd[b * kGrpCap + j];
-        const uint32_t e = h & pm, lh = h >> kGrpPosBits;
-        const uint32_t f = j + 1 < nh ? (shd[b * kGrpCap + j + 1] & pm) : n;
-        const uint32_t L = f - e;
-        const bool sentinel = lh == sent;
-        int64_t slot = sentinel ? a.t.cap : ((b << sh) | (int64_t)lh);
-        int64_t cur[8], rk[kSpFast], rt[kSpFast], rv[kSpFast];
+    uint32_t base = 0;  // chunks of this XCD group's earlier buckets: chunk g goes to workgroup g % per
+    for (int64_t b = xg; b < nb; b += 8) {
+        const uint32_t n = grp_n[2 * b], nh = grp_n[2 * b + 1];
+        const uint32_t* pr = perm + b * kGrpCap;
+        const uint32_t* hd = shd + b * kGrpCap;
+        const uint32_t nch = (nh + kSpKeyThreads - 1) / kSpKeyThreads;
+        const uint32_t c0 = (uint32_t)((me - (int)(base % (uint32_t)per) + per) % per);
+        base += nch;
+        for (uint32_t c = c0; c < nch; c += per) {
+            const uint32_t j = c * kSpKeyThreads + threadIdx.x;
+            if (j >= nh) continue;
+            const uint32_t h = hd[j];
+            const uint32_t e = h & pm, lh = h >> kGrpPosBits;
+            const uint32_t f = j + 1 < nh ? (hd[j + 1] & pm) : n;
+            const uint32_t L = f - e;
+            const bool sentinel = lh == sent;
+            int64_t slot = sentinel ? a.t.cap : ((b << sh) | (int64_t)lh);
+            int64_t cur[8], rk[kSpFast], rt[kSpFast], rv[kSpFast];
+            uint32_t ro[kSpFast];
 // (macros, not lambdas: a lambda capturing these arrays by reference would put them in scratch)
 #define SP_LOAD_LINE(sl)                                                                   \
     do {                                                                                   \
@@ -1022,105 +1037,117 @@ __global__ void __launch_bounds__(kSpKeyThreads) k_sp_keys(SegArgs a, const int6
             cur[2 * x_ + 1] = y_.y;                                                        \
         }                                                                                  \
     } while (0)
-#define SP_LOAD_RECS(c)  /* records [c, c + kSpFast) of the run (clamped) */              \
+#define SP_LOAD_OFFS(c)  /* pass-1 offsets of records [c, c + kSpFast) of the run (clamped) */ \
+    do {                                                                                   \
+        _Pragma("unroll") for (int u_ = 0; u_ < kSpFast; ++u_) ro[u_] = pr[(c) + u_ < f ? (c) + u_ : e]; \
+    } while (0)
+#define SP_LOAD_RECS()                                                                     \
     do {                                                                                   \
         _Pragma("unroll") for (int u_ = 0; u_ < kSpFast; ++u_) {                           \
-            const uint32_t q_ = (c) + u_ < f ? (c) + u_ : e;                               \
-            rk[u_] = sk[q_];                                                               \
-            rt[u_] = st[q_];                                                               \
-            rv[u_] = sv[q_];                                                               \
+            rk[u_] = a.p_key[ro[u_]];                                                      \
+            const longlong2 tv_ = a.p_tv[ro[u_]];                                          \
+            rt[u_] = tv_.x;                                                                \
+            rv[u_] = tv_.y;                                                                \
         }                                                                                  \
     } while (0)
-        SP_LOAD_LINE(slot);
-        SP_LOAD_RECS(e);
-        const int64_t key = rk[0];
-        bool one = true;  // every record of the run has this key
-        for (uint32_t c = e;;) {
-#pragma unroll
-            for (int u = 1; u < kSpFast; ++u) one = one && (c + u >= f || rk[u] == key);
-            c += kSpFast;
-            if (c >= f || !one) break;
-            SP_LOAD_RECS(c);
-            one = one && rk[0] == key;
-        }
-        if (L > (uint32_t)kSpFast) SP_LOAD_RECS(e);
-        // the key's slot: its home slot's line, or up to kSpProbe - 1 lines further
-        bool found = sentinel;
-        for (int pr = 0; pr < kSpProbe && !found && one; ++pr) {
-            if (cur[0] == key) { found = true; break; }
-            if (cur[0] == kEmptyKey) {
-                const unsigned long long prev = atomicCAS((unsigned long long*)slot_ptr(a.t, slot),
-                                                          (unsigned long long)kEmptyKey, (unsigned long long)key);
-                if (prev == (unsigned long long)kEmptyKey) {  // a new key: an empty slot has word 1 == 0
-                    found = true;
-                    ins++;
-                    cur[1] = 0;
-                    break;
-                }
-                if ((int64_t)prev == key) { found = true; SP_LOAD_LINE(slot); break; }
-            }
-            slot = (slot + 1) & (a.t.cap - 1);
             SP_LOAD_LINE(slot);
-        }
-        const int64_t w1 = cur[1];
-        const bool fast = found && one && !((uint64_t)w1 & (kBigMeta | kPuntMeta)) &&
-                          (!effects || slot_cnt(w1) + L <= kLaneSess);
-        if (fast) {  // the run replays from registers against the loaded line
-            int64_t* sp = slot_ptr(a.t, slot);
-            int cnt = slot_cnt(w1);
+            SP_LOAD_OFFS(e);
+            SP_LOAD_RECS();
+            const int64_t key = rk[0];
+            bool one = true;  // every record of the run has this key
+            for (uint32_t q = e;;) {
 #pragma unroll
-            for (int q = 0; q < (8 - 2) / SW; ++q)
-                if (q < cnt)
-                    sl_put(l, q, Sess{cur[2 + q * SW], cur[3 + q * SW], cur[4 + q * SW], SW == 4 ? cur[5 + q * SW] : 0,
-                                      (int64_t)slot_fired(w1, q)});
-            const unsigned long long l0 = late, m0 = merges;
-            bool ok = true;
-            for (uint32_t c = e; c < f && ok; c += kSpFast) {
-                if (c != e) SP_LOAD_RECS(c);
-                const int m = (int)min((uint32_t)kSpFast, f - c);
-                for (int u = 0; u < m && ok; ++u) {
-                    int64_t t = rt[0], v = rv[0];  // record u by selects (static indices: no scratch)
-#pragma unroll
-                    for (int x = 1; x < kSpFast; ++x) {
-                        t = u == x ? rt[x] : t;
-                        v = u == x ? rv[x] : v;
+                for (int u = 1; u < kSpFast; ++u) one = one && (q + u >= f || rk[u] == key);
+                q += kSpFast;
+                if (q >= f || !one) break;
+                SP_LOAD_OFFS(q);
+                SP_LOAD_RECS();
+                one = one && rk[0] == key;
+            }
+            if (L > (uint32_t)kSpFast) {
+                SP_LOAD_OFFS(e);
+                SP_LOAD_RECS();
+            }
+            // the key's slot: its home slot's line, or up to kSpProbe - 1 lines further
+            bool found = sentinel;
+            for (int pr_ = 0; pr_ < kSpProbe && !found && one; ++pr_) {
+                if (cur[0] == key) { found = true; break; }
+                if (cur[0] == kEmptyKey) {
+                    const unsigned long long prev = atomicCAS((unsigned long long*)slot_ptr(a.t, slot),
+                                                              (unsigned long long)kEmptyKey, (unsigned long long)key);
+                    if (prev == (unsigned long long)kEmptyKey) {  // a new key: an empty slot has word 1 == 0
+                        found = true;
+                        ins++;
+                        cur[1] = 0;
+                        break;
                     }
-                    ok = add_element_tv<AGG>(a, l, cnt, kLaneSess, key, t, v, late, merges, flags, false);
+                    if ((int64_t)prev == key) { found = true; SP_LOAD_LINE(slot); break; }
                 }
+                slot = (slot + 1) & (a.t.cap - 1);
+                SP_LOAD_LINE(slot);
             }
-            if (ok) {
-                sp_store<AGG>(a, l, cnt, slot, sp, w1);
-            } else {  // outgrew the lane (no effects were written): punt the run
-                late = l0;
-                merges = m0;
-                const unsigned long long at = atomicAdd(&a.st->overflow, (unsigned long long)L);
-                for (uint32_t q = 0; q < L; ++q) {
-                    a.pu_key[at + q] = key;
-                    a.pu_ts[at + q] = st[e + q];
-                    a.pu_val[at + q] = sv[e + q];
+            const int64_t w1 = cur[1];
+            const bool fast = found && one && !((uint64_t)w1 & (kBigMeta | kPuntMeta)) &&
+                              (!effects || slot_cnt(w1) + L <= kLaneSess);
+            if (fast) {  // the run replays from registers against the loaded line
+                int64_t* sp = slot_ptr(a.t, slot);
+                int cnt = slot_cnt(w1);
+#pragma unroll
+                for (int q = 0; q < (8 - 2) / SW; ++q)
+                    if (q < cnt)
+                        sl_put(l, q, Sess{cur[2 + q * SW], cur[3 + q * SW], cur[4 + q * SW],
+                                          SW == 4 ? cur[5 + q * SW] : 0, (int64_t)slot_fired(w1, q)});
+                const unsigned long long l0 = late, m0 = merges;
+                bool ok = true;
+                for (uint32_t q = e; q < f && ok; q += kSpFast) {
+                    if (q != e) {
+                        SP_LOAD_OFFS(q);
+                        SP_LOAD_RECS();
+                    }
+                    const int m = (int)min((uint32_t)kSpFast, f - q);
+                    for (int u = 0; u < m && ok; ++u) {
+                        int64_t t = rt[0], v = rv[0];  // record u by selects (static indices: no scratch)
+#pragma unroll
+                        for (int x = 1; x < kSpFast; ++x) {
+                            t = u == x ? rt[x] : t;
+                            v = u == x ? rv[x] : v;
+                        }
+                        ok = add_element_tv<AGG>(a, l, cnt, kLaneSess, key, t, v, late, merges, flags, false);
+                    }
                 }
-                sp[1] = (int64_t)((uint64_t)w1 | kPuntMeta);
+                if (ok) {
+                    sp_store<AGG>(a, l, cnt, slot, sp, w1);
+                } else {  // outgrew the lane (no effects were written): punt the run
+                    late = l0;
+                    merges = m0;
+                    const unsigned long long at = atomicAdd(&a.st->overflow, (unsigned long long)L);
+                    for (uint32_t q = 0; q < L; ++q) {
+                        const longlong2 tv = a.p_tv[pr[e + q]];
+                        a.pu_key[at + q] = key;
+                        a.pu_ts[at + q] = tv.x;
+                        a.pu_val[at + q] = tv.y;
+                    }
+                    sp[1] = (int64_t)((uint64_t)w1 | kPuntMeta);
+                }
+            } else {  // k_sp_slow replays it (a dense launch: no divergence against the fast runs)
+                const uint64_t bal = __ballot(true);
+                unsigned long long at = 0;
+                const int ld = __ffsll((long long)bal) - 1;
+                if (__lane_id() == ld) at = atomicAdd(&a.st->spills, (unsigned long long)__popcll(bal));
+                at = __shfl(at, ld);
+                a.slow[at + __popcll(bal & ((1ull << __lane_id()) - 1ull))] = ((uint32_t)b << kGrpPosBits) | j;
             }
-        } else {  // k_sp_slow replays it (a dense launch: no divergence against the fast runs)
-            const uint64_t bal = __ballot(true);
-            unsigned long long at = 0;
-            const int ld = __ffsll((long long)bal) - 1;
-            if (__lane_id() == ld) at = atomicAdd(&a.st->spills, (unsigned long long)__popcll(bal));
-            at = __shfl(at, ld);
-            a.slow[at + __popcll(bal & ((1ull << __lane_id()) - 1ull))] = ((uint32_t)b << kGrpPosBits) | j;
-        }
 #undef SP_LOAD_LINE
+#undef SP_LOAD_OFFS
 #undef SP_LOAD_RECS
+        }
     }
     block_commit(a.st, late, ins, flags, 0, 0, merges);
 }
 
-// The home slots k_sp_keys left (a.slow, st->spills of them): every key of the slot's run in
-// order of its first record through sp_key (probe, several keys, the wide table, the dry
-// replay under allowed lateness or the side output).
+// The home slots k_sp_keys left (a.slow, st->spills of them) through sp_run.
 template <int AGG>
-__global__ void __launch_bounds__(kSpKeyThreads) k_sp_slow(SegArgs a, const int64_t* skey, const int64_t* sts,
-                                                           const int64_t* sval, const uint32_t* shd,
+__global__ void __launch_bounds__(kSpKeyThreads) k_sp_slow(SegArgs a, const uint32_t* perm, const uint32_t* shd,
                                                            const uint32_t* grp_n) {
     constexpr uint32_t pm = (1u << kGrpPosBits) - 1u;
     __shared__ int64_t lane[5 * kLaneSess * kSpKeyThreads];
@@ -1132,23 +1159,9 @@ __global__ void __launch_bounds__(kSpKeyThreads) k_sp_slow(SegArgs a, const int6
         const int64_t b = id >> kGrpPosBits;
         const uint32_t j = id & pm;
         const uint32_t n = grp_n[2 * b], nh = grp_n[2 * b + 1];
-        const int64_t* sk = skey + b * kGrpCap;
-        const int64_t* st = sts + b * kGrpCap;
-        const int64_t* sv = sval + b * kGrpCap;
         const uint32_t e = shd[b * kGrpCap + j] & pm;
         const uint32_t f = j + 1 < nh ? (shd[b * kGrpCap + j + 1] & pm) : n;
-        for (uint32_t r = e; r < f;) {
-            const int64_t kr = sk[r];
-            sp_key<AGG>(a, l, kr, r, f, sk, st, sv, late, merges, flags, ins);
-            uint32_t nx = f;
-            for (uint32_t q = r + 1; q < f && nx == f; ++q) {
-                const int64_t kq = sk[q];
-                bool seen = false;
-                for (uint32_t z = e; z < q && !seen; ++z) seen = sk[z] == kq;
-                if (!seen) nx = q;
-            }
-            r = nx;
-        }
+        sp_run<AGG>(a, l, e, f, perm + b * kGrpCap, late, merges, flags, ins);
     }
     block_commit(a.st, late, ins, flags, 0, 0, merges);
 }
@@ -1717,8 +1730,9 @@ struct SessionState {
     int64_t* sp_col3 = nullptr;  // key | ts | value, sp_cap each
     uint32_t* sp_row = nullptr;  // sp_desc_cap each: rows, then columns
     int64_t* pu_col3 = nullptr;  // punted key | ts | value, sp_cap each
-    uint32_t* sp_grp = nullptr;  // grouping: sorted keys | timestamps | values (int64), heads (u32), counts
+    uint32_t* sp_grp = nullptr;  // grouping: offsets by position | offsets in order | heads, counts
     int64_t sp_cap = 0, sp_desc_cap = 0, sp_grp_cap = 0;
+    int sp_key_grid = 0;
     bool fresh = false;      // h_st matches the device (nothing launched since the last refresh)
     int gshift = 0;          // sessions: the last sort grouped records by slot >> gshift
     uint32_t* due_list = nullptr;  // fire sweep: main-table slots with something due
@@ -2223,7 +2237,16 @@ static int ingest_sorted(SessionState* s, int64_t n, const int64_t* key, const i
     return GW_OK;
 }
 
-static void sp_opt_in() {
+static void sp_opt_in(SessionState* s) {
+    if (!s->sp_key_grid) {  // persistent replay grid: the resident workgroups, a multiple of 8
+        int dev = 0, cus = 0, per = 0;
+        hipGetDevice(&dev);
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+#define L(A) hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void*)k_sp_keys<A>, kSpKeyThreads, 0)
+        GW_AGG_SWITCH(s->cfg.agg, L);
+#undef L
+        s->sp_key_grid = std::max(8, (std::max(cus, 1) * std::max(per, 1)) / 8 * 8);
+    }
     static bool done = false;
     if (!done) {
         hipFuncSetAttribute((const void*)k_sp_part, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kSpPartLds);
@@ -2269,7 +2292,7 @@ static int ingest_region(SessionState* s, int64_t n, const int64_t* key, const i
             hipFree(s->sp_grp);
             s->sp_grp = nullptr;
             const int64_t c = (int64_t)nb * kGrpCap;
-            SCHECK(hipMalloc((void**)&s->sp_grp, (size_t)(7 * c + 2 * nb) * 4));  // sorted records (24 B), heads
+            SCHECK(hipMalloc((void**)&s->sp_grp, (size_t)(3 * c + 2 * nb) * 4));  // offsets by position, order, heads
             s->sp_grp_cap = c;
         }
         if (ntiles * nb > s->sp_desc_cap) {
@@ -2284,25 +2307,23 @@ static int ingest_region(SessionState* s, int64_t n, const int64_t* key, const i
     int64_t* pk = s->sp_col3;
     uint32_t* row = s->sp_row;
     uint32_t* col = s->sp_row + s->sp_desc_cap;
-    int64_t* skey = reinterpret_cast<int64_t*>(s->sp_grp);
-    int64_t* sts = skey + G;
-    int64_t* sval = sts + G;
-    uint32_t* shd = reinterpret_cast<uint32_t*>(sval + G);
+    uint32_t* gsrc = s->sp_grp;
+    uint32_t* perm = gsrc + G;
+    uint32_t* shd = perm + G;
     uint32_t* grp_n = shd + G;
-    sp_opt_in();
+    sp_opt_in(s);
     if ((rc = zero_word_async(s, offsetof(DevStatus, overflow), err))) return rc;
     if ((rc = zero_word_async(s, offsetof(DevStatus, pad[0]), err))) return rc;
     if ((rc = zero_word_async(s, offsetof(DevStatus, pad[1]), err))) return rc;
     hipLaunchKernelGGL(k_sp_part, dim3((unsigned)ntiles), dim3(kSpThreads), kSpPartLds, s->stream, key, ts, val, n,
-                       s->tv.cap, lcap, bb, pk, pk + C, pk + 2 * C, row, s->d_st);
+                       s->tv.cap, lcap, bb, pk, reinterpret_cast<longlong2*>(pk + C), row, s->d_st);
     hipLaunchKernelGGL(k_sp_transpose, dim3((unsigned)((ntiles + 63) / 64), (unsigned)((nb + 63) / 64)), dim3(256), 0,
                        s->stream, row, col, ntiles, nb);
     SCHECK(hipGetLastError());
     SegArgs a{};
     if ((rc = seg_common(s, a, n, wm, err))) return rc;
     a.p_key = pk;
-    a.p_ts = pk + C;
-    a.p_val = pk + 2 * C;
+    a.p_tv = reinterpret_cast<const longlong2*>(pk + C);
     a.col = col;
     a.ntiles = ntiles;
     a.lcap = lcap;
@@ -2312,14 +2333,13 @@ static int ingest_region(SessionState* s, int64_t n, const int64_t* key, const i
     a.pu_val = s->pu_col3 + 2 * C;
     static const int sp_exp = getenv("GW_SP_EXP") ? atoi(getenv("GW_SP_EXP")) : 0;
     a.exp = sp_exp;
-    hipLaunchKernelGGL(k_sp_group, dim3((unsigned)nb), dim3(kGrpThreads), kGrpLds, s->stream, a, skey, sts, sval, shd,
-                       grp_n);
+    hipLaunchKernelGGL(k_sp_group, dim3((unsigned)nb), dim3(kGrpThreads), kGrpLds, s->stream, a, gsrc, perm, shd, grp_n);
     a.slow = reinterpret_cast<uint32_t*>(s->pu_col3 + 3 * C);
     if ((rc = zero_word_async(s, offsetof(DevStatus, spills), err))) return rc;
 #define L(A)                                                                                                   \
-    hipLaunchKernelGGL(k_sp_keys<A>, dim3((unsigned)(kGrpCap / kSpKeyThreads), (unsigned)nb), dim3(kSpKeyThreads), 0, \
-                       s->stream, a, skey, sts, sval, shd, grp_n);                                              \
-    hipLaunchKernelGGL(k_sp_slow<A>, dim3(1024), dim3(kSpKeyThreads), 0, s->stream, a, skey, sts, sval, shd, grp_n)
+    hipLaunchKernelGGL(k_sp_keys<A>, dim3((unsigned)s->sp_key_grid), dim3(kSpKeyThreads), 0, s->stream, a, perm, shd, \
+                       grp_n, nb);                                                                              \
+    hipLaunchKernelGGL(k_sp_slow<A>, dim3(1024), dim3(kSpKeyThreads), 0, s->stream, a, perm, shd, grp_n)
     GW_AGG_SWITCH(s->cfg.agg, L);
 #undef L
     SCHECK(hipGetLastError());
