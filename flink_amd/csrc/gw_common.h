@@ -61,26 +61,20 @@ GW_HD int32_t key_group_for_hash(int32_t h, int32_t max_p) { return murmur_hash(
 GW_HD int32_t operator_for_key_group(int32_t max_p, int32_t p, int32_t kg) { return kg * p / max_p; }
 
 // State-table hash (this library's own; independent of the key-group hash so that
-// the slots of one key group are spread over the whole table).
+// the slots of one key group are spread over the whole table): a multiply by the 64-bit
+// golden ratio (the region is the product's top bits, Fibonacci hashing), then an xor-shift
+// that folds the top half into the bottom one (the home slot is the low bits).  Both steps
+// are bijections; one 64-bit multiply instead of the murmur finalizer's two, since every
+// region-path record hashes in each pass.
 GW_HD uint64_t slot_hash(int64_t key) {
-    uint64_t x = (uint64_t)key;
-    x ^= x >> 33;
-    x *= 0xff51afd7ed558ccdull;
-    x ^= x >> 33;
-    x *= 0xc4ceb9fe1a85ec53ull;
-    x ^= x >> 33;
-    return x;
+    uint64_t x = (uint64_t)key * 0x9e3779b97f4a7c15ull;
+    return x ^ (x >> 32);
 }
-// Its inverse (each step of the 64-bit finalizer is a bijection: xor-shifts by >= 32 are
-// self-inverse, the multipliers are odd): the compact region-path records carry the hash
-// and the apply recovers the key from it.
+// Its inverse: the xor-shift by 32 is self-inverse, the multiplier odd.  The compact
+// region-path records carry the hash and the apply recovers the key from it.
 GW_HD int64_t slot_unhash(uint64_t x) {
-    x ^= x >> 33;
-    x *= 0x9cb4b2f8129337dbull;  // 0xc4ceb9fe1a85ec53^-1 mod 2^64
-    x ^= x >> 33;
-    x *= 0x4f74430c22a54005ull;  // 0xff51afd7ed558ccd^-1 mod 2^64
-    x ^= x >> 33;
-    return (int64_t)x;
+    x ^= x >> 32;
+    return (int64_t)(x * 0xf1de83e19937733dull);  // 0x9e3779b97f4a7c15^-1 mod 2^64
 }
 
 // ---------------------------------------------------------------------------

@@ -378,7 +378,10 @@ __global__ void __launch_bounds__(256) k_ingest_preagg(IngestArgs a) {
 // Every HBM access is a contiguous run: whole tiles, runs of ~32-64 records, and the
 // region state.  P1 segments of several watermark batches accumulate in the buffer and
 // P2 + apply run once per fire (gw_runtime.cpp flush_buffer).
-constexpr int kPartThreads = 512;
+#ifndef GW_PART_THREADS
+#define GW_PART_THREADS 512
+#endif
+constexpr int kPartThreads = GW_PART_THREADS;
 constexpr int kPartItems = kPartTile / kPartThreads;
 
 __device__ __forceinline__ int64_t rgn_of(const PaneTable& t, int64_t key) { return pt_key_region(t, slot_hash(key)); }
@@ -786,7 +789,7 @@ __global__ void __launch_bounds__(kPartThreads) k_rgn_p2(IngestArgs a) {
     uint32_t* s_r32 = reinterpret_cast<uint32_t*>(s.k);
     const int lr_sh = 64 - (a.d1_bits + a.d2_bits);  // C: region bits of the hash word
     __shared__ uint32_t lh[kPartBuckets], ls[kPartBuckets];
-    __shared__ uint32_t r_cnt[kMaxGroup], r_pre[kMaxGroup + 1], wsum[8];
+    __shared__ uint32_t r_cnt[kMaxGroup], r_pre[kMaxGroup + 1], wsum[kPartThreads / 64];
     __shared__ int64_t r_src[kMaxGroup];
     const int64_t b1 = blockIdx.x / a.ngroups, j = blockIdx.x - b1 * a.ngroups;
     const int64_t t0 = j * a.p2_group;
@@ -908,6 +911,7 @@ constexpr int kApplyThreads = GW_APPLY_THREADS;
 constexpr int kApplyRuns = 256;  // run descriptors staged in LDS per step (<= blockDim)
 constexpr int kApplyGroup = GW_APPLY_GROUP;   // consecutive runs a wave walks as one sequence
 constexpr int kApplyUnroll = GW_APPLY_UNROLL;  // records per lane with their loads in flight together
+constexpr int kApplyQ = 128;                   // per-wave queue of records that missed their home group
 
 template <int AGG, int FMT>
 __global__ void __launch_bounds__(kApplyThreads) GW_APPLY_ATTR k_rgn_apply(IngestArgs a) {
@@ -939,6 +943,16 @@ __global__ void __launch_bounds__(kApplyThreads) GW_APPLY_ATTR k_rgn_apply(Inges
     const int64_t MW = pt_mask_words(a.t);       // 0 unless M
     uint8_t* lmask = (uint8_t*)(lkeys + S);
     long long* lcell = lkeys + S + MW;           // [2][S][W]
+    // per-wave queue of records that missed their home group (after the cells): hashes,
+    // values (two words for averages), ring positions
+    constexpr int QW = kApplyThreads / 64 * kApplyQ;
+    unsigned char* qbase = reinterpret_cast<unsigned char*>(lcell + 2 * S * W);
+    const int qoff = (threadIdx.x >> 6) * kApplyQ;
+    uint64_t* qh = reinterpret_cast<uint64_t*>(qbase) + qoff;
+    int64_t* qv0 = reinterpret_cast<int64_t*>(qbase + (size_t)QW * 8) + qoff;
+    int64_t* qv1 = reinterpret_cast<int64_t*>(qbase + (size_t)QW * 16) + qoff;  // AV only
+    uint8_t* qps = qbase + (size_t)QW * (AV ? 24 : 16) + qoff;
+    int qn = 0;
     // dirty 128-B lines of the key array (S <= 2048: <= 128 lines)
     __shared__ uint32_t s_kdirty[4];
     // the (up to) two pane positions this flush touches
@@ -1153,6 +1167,25 @@ __global__ void __launch_bounds__(kApplyThreads) GW_APPLY_ATTR k_rgn_apply(Inges
         // The rest (an insert, a key displaced beyond its group, a spill) take the generic
         // probe.  The table never holds an empty slot before a key in the key's probe order,
         // so a key found in its home group is exactly the slot the generic probe would pick.
+        // Records whose key is not in its home group (an insert, a displaced key, a spill) go
+        // to the wave's queue in LDS instead of probing at once: one lane's probe would hold
+        // the whole wave.  64 at a time the wave probes them with every lane busy.
+        auto q_push = [&](bool p, uint64_t hh, int64_t c0, int64_t c1, uint32_t pos) {
+            const uint64_t bal = __ballot(p);
+            if (p) {
+                const int at = qn + __popcll(bal & ((1ull << lane) - 1ull));
+                qh[at] = hh;
+                qv0[at] = c0;
+                if constexpr (AV) qv1[at] = c1;
+                qps[at] = (uint8_t)pos;
+            }
+            qn += __popcll(bal);
+            if (qn >= 64) {
+                const int at = qn - 64 + lane;
+                apply_one(qh[at], qv0[at], AV ? qv1[at] : 1, qps[at]);
+                qn -= 64;
+            }
+        };
         auto apply_step = [&](const Step& c) {
             uint64_t h[kApplyUnroll];
             uint32_t ps[kApplyUnroll];
@@ -1183,21 +1216,23 @@ __global__ void __launch_bounds__(kApplyThreads) GW_APPLY_ATTR k_rgn_apply(Inges
             }
 #pragma unroll
             for (int q = 0; q < kApplyUnroll; ++q) {
-                if (!c.ok[q]) continue;
-                const long long key = (long long)h[q];
-                const int i = ka[q].x == key ? 0 : ka[q].y == key ? 1 : kb[q].x == key ? 2 : kb[q].y == key ? 3 : -1;
-                const int ai = (int)ps[q] == act0 ? 0 : ((int)ps[q] == act1 ? 1 : -1);
-                if (i >= 0 && ai >= 0) {
-                    const int found = g[q] + i;
-                    long long* cl = lcell + (ai * (int)S + found) * (AV ? 2 : 1);
-                    lds_cell_add<AGG>(cl, cl + (AV ? 1 : 0), v0[q], c.v1[q]);
-                    if constexpr (M) {
-                        const uint32_t bit = ((uint32_t)found << (msh + 3)) + ps[q];
-                        atomicOr((uint32_t*)lmask + (bit >> 5), 1u << (bit & 31));
+                bool fast = false;
+                if (c.ok[q]) {
+                    const long long key = (long long)h[q];
+                    const int i = ka[q].x == key ? 0 : ka[q].y == key ? 1 : kb[q].x == key ? 2 : kb[q].y == key ? 3 : -1;
+                    const int ai = (int)ps[q] == act0 ? 0 : ((int)ps[q] == act1 ? 1 : -1);
+                    fast = i >= 0 && ai >= 0;
+                    if (fast) {
+                        const int found = g[q] + i;
+                        long long* cl = lcell + (ai * (int)S + found) * (AV ? 2 : 1);
+                        lds_cell_add<AGG>(cl, cl + (AV ? 1 : 0), v0[q], c.v1[q]);
+                        if constexpr (M) {
+                            const uint32_t bit = ((uint32_t)found << (msh + 3)) + ps[q];
+                            atomicOr((uint32_t*)lmask + (bit >> 5), 1u << (bit & 31));
+                        }
                     }
-                } else {
-                    apply_one(h[q], v0[q], c.v1[q], ps[q]);
                 }
+                q_push(c.ok[q] && !fast, h[q], v0[q], c.v1[q], ps[q]);  // the wave is converged here
             }
         };
         Step sa, sb;
@@ -1212,6 +1247,8 @@ __global__ void __launch_bounds__(kApplyThreads) GW_APPLY_ATTR k_rgn_apply(Inges
             load_step(g, k, sa, live);
             apply_step(sb);
         }
+        if (lane < qn) apply_one(qh[lane], qv0[lane], AV ? qv1[lane] : 1, qps[lane]);  // the rest of the queue
+        qn = 0;
     }
     // Spill pass (only in regions that had a spill): the final LDS key table says which
     // records were not applied: their key is absent (the region was full; no slot ever
@@ -2054,7 +2091,8 @@ hipError_t launch_region_flush(const IngestArgs& a, hipStream_t s) {
     const bool single = a.d2_bits == 0;
     const size_t part_lds = part_lds_bytes(a);
     const int64_t S = pt_S(a.t);
-    const size_t apply_lds = (size_t)(S + pt_mask_words(a.t)) * 8 + (size_t)2 * S * a.t.words * 8;
+    const size_t apply_lds = (size_t)(S + pt_mask_words(a.t)) * 8 + (size_t)2 * S * a.t.words * 8 +
+                             (size_t)(kApplyThreads / 64) * kApplyQ * (a.t.words == 2 ? 25 : 17);  // + miss queues
     const int nb1 = 1 << a.d1_bits;
     if (a.ntiles == 0) return hipSuccess;
 #define L2(A, CM)                                                                                               \

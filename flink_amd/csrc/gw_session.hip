@@ -994,7 +994,7 @@ __device__ __forceinline__ void sp_run(const SegArgs& a, const SessList& l, uint
 // the slow list for k_sp_slow (longer probes, several keys per home slot, the wide table, a
 // list that could outgrow the lane under allowed lateness or the side output).
 constexpr int kSpKeyThreads = 256;
-constexpr int kSpFast = 8;
+constexpr int kSpFast = 4;
 constexpr int kSpProbe = 4;
 template <int AGG>
 __global__ void __launch_bounds__(kSpKeyThreads) k_sp_keys(SegArgs a, const uint32_t* perm, const uint32_t* shd,
@@ -1053,81 +1053,135 @@ __global__ void __launch_bounds__(kSpKeyThreads) k_sp_keys(SegArgs a, const uint
             SP_LOAD_LINE(slot);
             SP_LOAD_OFFS(e);
             SP_LOAD_RECS();
-            const int64_t key = rk[0];
-            bool one = true;  // every record of the run has this key
-            for (uint32_t q = e;;) {
+            // the run's keys: one, or two (home slots shared by two keys of the batch) in a run
+            // of at most kSpFast records; anything else goes to k_sp_slow
+            const int64_t k0 = rk[0];
+            int64_t k1 = k0;
+            bool fit = true;
+            uint32_t L0 = L;
+            if (L <= (uint32_t)kSpFast) {
+                L0 = 1;
 #pragma unroll
-                for (int u = 1; u < kSpFast; ++u) one = one && (q + u >= f || rk[u] == key);
-                q += kSpFast;
-                if (q >= f || !one) break;
-                SP_LOAD_OFFS(q);
-                SP_LOAD_RECS();
-                one = one && rk[0] == key;
-            }
-            if (L > (uint32_t)kSpFast) {
+                for (int u = 1; u < kSpFast; ++u) {
+                    if ((uint32_t)u >= L) continue;
+                    if (rk[u] == k0) { ++L0; continue; }
+                    if (k1 == k0) k1 = rk[u];
+                    else if (rk[u] != k1) fit = false;
+                }
+            } else {
+                for (uint32_t q = e;;) {
+#pragma unroll
+                    for (int u = 1; u < kSpFast; ++u) fit = fit && (q + u >= f || rk[u] == k0);
+                    q += kSpFast;
+                    if (q >= f || !fit) break;
+                    SP_LOAD_OFFS(q);
+                    SP_LOAD_RECS();
+                    fit = fit && rk[0] == k0;
+                }
                 SP_LOAD_OFFS(e);
                 SP_LOAD_RECS();
             }
-            // the key's slot: its home slot's line, or up to kSpProbe - 1 lines further
-            bool found = sentinel;
-            for (int pr_ = 0; pr_ < kSpProbe && !found && one; ++pr_) {
-                if (cur[0] == key) { found = true; break; }
-                if (cur[0] == kEmptyKey) {
-                    const unsigned long long prev = atomicCAS((unsigned long long*)slot_ptr(a.t, slot),
-                                                              (unsigned long long)kEmptyKey, (unsigned long long)key);
-                    if (prev == (unsigned long long)kEmptyKey) {  // a new key: an empty slot has word 1 == 0
-                        found = true;
-                        ins++;
-                        cur[1] = 0;
-                        break;
-                    }
-                    if ((int64_t)prev == key) { found = true; SP_LOAD_LINE(slot); break; }
-                }
-                slot = (slot + 1) & (a.t.cap - 1);
-                SP_LOAD_LINE(slot);
-            }
-            const int64_t w1 = cur[1];
-            const bool fast = found && one && !((uint64_t)w1 & (kBigMeta | kPuntMeta)) &&
-                              (!effects || slot_cnt(w1) + L <= kLaneSess);
-            if (fast) {  // the run replays from registers against the loaded line
-                int64_t* sp = slot_ptr(a.t, slot);
-                int cnt = slot_cnt(w1);
+            const bool two = k1 != k0;
+            const uint32_t L1 = L - L0;
+            // each key's slot: its home slot's line, or up to kSpProbe - 1 lines further
+            // (a free slot is claimed -- harmless if the run then goes to k_sp_slow after all)
+            int64_t slot0 = slot, slot1 = slot, c1w[8];
+#define SP_PROBE(KEY, SL, FOUND)                                                                           \
+    do {                                                                                                   \
+        for (int pr_ = 0; pr_ < kSpProbe && !(FOUND); ++pr_) {                                             \
+            if (cur[0] == (KEY)) { FOUND = true; break; }                                                  \
+            if (cur[0] == kEmptyKey) {                                                                     \
+                const unsigned long long prev_ = atomicCAS((unsigned long long*)slot_ptr(a.t, SL),         \
+                                                           (unsigned long long)kEmptyKey, (unsigned long long)(KEY)); \
+                if (prev_ == (unsigned long long)kEmptyKey) { /* new key: a free slot has word 1 == 0 */   \
+                    FOUND = true;                                                                          \
+                    ins++;                                                                                 \
+                    cur[1] = 0;                                                                            \
+                    break;                                                                                 \
+                }                                                                                          \
+            }                                                                                              \
+            SL = (SL + 1) & (a.t.cap - 1);                                                                 \
+            SP_LOAD_LINE(SL);                                                                              \
+        }                                                                                                  \
+    } while (0)
+            bool f0 = sentinel, f1 = true;
+            if (fit) SP_PROBE(k0, slot0, f0);
+            if (fit && two && f0) {
 #pragma unroll
-                for (int q = 0; q < (8 - 2) / SW; ++q)
-                    if (q < cnt)
-                        sl_put(l, q, Sess{cur[2 + q * SW], cur[3 + q * SW], cur[4 + q * SW],
-                                          SW == 4 ? cur[5 + q * SW] : 0, (int64_t)slot_fired(w1, q)});
-                const unsigned long long l0 = late, m0 = merges;
-                bool ok = true;
-                for (uint32_t q = e; q < f && ok; q += kSpFast) {
-                    if (q != e) {
-                        SP_LOAD_OFFS(q);
+                for (int x = 0; x < 8; ++x) c1w[x] = cur[x];  // key 0's line
+                f1 = false;
+                SP_LOAD_LINE(slot1);
+                SP_PROBE(k1, slot1, f1);
+#pragma unroll
+                for (int x = 0; x < 8; ++x) {  // cur: key 0's line again, c1w: key 1's
+                    const int64_t t = cur[x];
+                    cur[x] = c1w[x];
+                    c1w[x] = t;
+                }
+            }
+#undef SP_PROBE
+            const int64_t w10 = cur[1], w11 = two ? c1w[1] : 0;
+            const bool fast = fit && f0 && f1 && !((uint64_t)(w10 | w11) & (kBigMeta | kPuntMeta)) &&
+                              (!effects || (slot_cnt(w10) + L0 <= kLaneSess && slot_cnt(w11) + L1 <= kLaneSess));
+            if (fast) {  // each key's records replay from registers against its loaded line
+#pragma unroll 1
+                for (int ki = 0; ki < (two ? 2 : 1); ++ki) {
+                    const int64_t key = ki ? k1 : k0;
+                    const int64_t sl = ki ? slot1 : slot0;
+                    if (ki) {
+#pragma unroll
+                        for (int x = 0; x < 8; ++x) cur[x] = c1w[x];
+                    }
+                    const int64_t w1 = cur[1];
+                    int64_t* sp = slot_ptr(a.t, sl);
+                    int cnt = slot_cnt(w1);
+#pragma unroll
+                    for (int q = 0; q < (8 - 2) / SW; ++q)
+                        if (q < cnt)
+                            sl_put(l, q, Sess{cur[2 + q * SW], cur[3 + q * SW], cur[4 + q * SW],
+                                              SW == 4 ? cur[5 + q * SW] : 0, (int64_t)slot_fired(w1, q)});
+                    const unsigned long long l0 = late, m0 = merges;
+                    bool ok = true;
+                    for (uint32_t q = e; q < f && ok; q += kSpFast) {
+                        if (q != e) {
+                            SP_LOAD_OFFS(q);
+                            SP_LOAD_RECS();
+                        }
+                        const int m = (int)min((uint32_t)kSpFast, f - q);
+                        for (int u = 0; u < m && ok; ++u) {
+                            int64_t t = rt[0], v = rv[0], kk = rk[0];  // record u by selects: no scratch
+#pragma unroll
+                            for (int x = 1; x < kSpFast; ++x) {
+                                t = u == x ? rt[x] : t;
+                                v = u == x ? rv[x] : v;
+                                kk = u == x ? rk[x] : kk;
+                            }
+                            if (kk == key)
+                                ok = add_element_tv<AGG>(a, l, cnt, kLaneSess, key, t, v, late, merges, flags, false);
+                        }
+                    }
+                    if (ok) {
+                        sp_store<AGG>(a, l, cnt, sl, sp, w1);
+                    } else {  // outgrew the lane (no effects were written): punt the key's records
+                        late = l0;
+                        merges = m0;
+                        const uint32_t Lk = ki ? L1 : L0;
+                        unsigned long long at = atomicAdd(&a.st->overflow, (unsigned long long)Lk);
+                        for (uint32_t q = e; q < f; ++q) {
+                            const uint32_t o = pr[q];
+                            if (a.p_key[o] != key) continue;
+                            const longlong2 tv = a.p_tv[o];
+                            a.pu_key[at] = key;
+                            a.pu_ts[at] = tv.x;
+                            a.pu_val[at] = tv.y;
+                            ++at;
+                        }
+                        sp[1] = (int64_t)((uint64_t)w1 | kPuntMeta);
+                    }
+                    if (!ki && two) {  // key 1's records: reload the first chunk (the loop moved on)
+                        SP_LOAD_OFFS(e);
                         SP_LOAD_RECS();
                     }
-                    const int m = (int)min((uint32_t)kSpFast, f - q);
-                    for (int u = 0; u < m && ok; ++u) {
-                        int64_t t = rt[0], v = rv[0];  // record u by selects (static indices: no scratch)
-#pragma unroll
-                        for (int x = 1; x < kSpFast; ++x) {
-                            t = u == x ? rt[x] : t;
-                            v = u == x ? rv[x] : v;
-                        }
-                        ok = add_element_tv<AGG>(a, l, cnt, kLaneSess, key, t, v, late, merges, flags, false);
-                    }
-                }
-                if (ok) {
-                    sp_store<AGG>(a, l, cnt, slot, sp, w1);
-                } else {  // outgrew the lane (no effects were written): punt the run
-                    late = l0;
-                    merges = m0;
-                    const unsigned long long at = atomicAdd(&a.st->overflow, (unsigned long long)L);
-                    for (uint32_t q = 0; q < L; ++q) {
-                        const longlong2 tv = a.p_tv[pr[e + q]];
-                        a.pu_key[at + q] = key;
-                        a.pu_ts[at + q] = tv.x;
-                        a.pu_val[at + q] = tv.y;
-                    }
-                    sp[1] = (int64_t)((uint64_t)w1 | kPuntMeta);
                 }
             } else {  // k_sp_slow replays it (a dense launch: no divergence against the fast runs)
                 const uint64_t bal = __ballot(true);
