@@ -186,7 +186,10 @@ struct IngestArgs {
     uint64_t ring_fresh;            // ring positions holding only identities (not in occ)
 };
 
-constexpr int kPartTile = 4096;     // records per P1 tile / P2 round (LDS-sorted)
+#ifndef GW_PART_TILE
+#define GW_PART_TILE 4096
+#endif
+constexpr int kPartTile = GW_PART_TILE;  // records per P1 tile / P2 round (LDS-sorted)
 constexpr int kPartBuckets = 256;   // descriptor row width (<= 8 region bits per pass)
 constexpr int kRgnMaxRegions = 65536;
 constexpr int kMaxGroup = 256;      // P1 tiles per P2 block (G = 7/8 of the pass-1 buckets)

@@ -536,46 +536,34 @@ __global__ void __launch_bounds__(256) k_publish_status(const DevStatus* st, Dev
 #else
 #define GW_APPLY_ATTR
 #endif
-template <int AGG, int FMT, bool GAP>
-__global__ void __launch_bounds__(kPartThreads) GW_P1_ATTR k_rgn_p1(IngestArgs a) {
+// P1 body for one tile: the records' inputs are in registers (item it of thread x is record
+// lo + it * THR + x); lh[] zeroed and s_occ cleared by the caller, with a barrier after.
+// Classifies, ranks by pass-1 bucket (LDS atomics), sorts the tile in LDS (s) and writes it
+// back with its descriptor row.
+template <int AGG, int FMT, bool GAP, int THR, int IT>
+__device__ __forceinline__ void p1_tile(const IngestArgs& a, int64_t g, int64_t lo, int64_t hi, int64_t (&key)[IT],
+                                        const int64_t (&ts)[IT], const int64_t (&val)[IT], const TileLds& s,
+                                        uint32_t* lh, uint32_t* ls, unsigned long long* s_occ,
+                                        unsigned long long& late, unsigned long long& flags,
+                                        unsigned long long& occ_all) {
     constexpr bool C = FMT == kFmtCmp && cmp_agg<AGG>();
     constexpr bool NR = FMT == kFmtNar && cmp_agg<AGG>();
     constexpr bool N4 = NR && AGG == GW_COUNT;  // 4-byte narrow records
     constexpr bool AV = !C && !NR && (AGG == GW_AVG_I64 || AGG == GW_AVG_F64);
     constexpr bool ACC = !(C && AGG == GW_COUNT);  // COUNT records carry no value
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const TileLds s = tile_lds<AV>(smem);
     int32_t* s_v32 = reinterpret_cast<int32_t*>(s.a0);  // C: 32-bit values
     uint32_t* s_r32 = reinterpret_cast<uint32_t*>(s.k);  // N4: the records
-    __shared__ uint32_t lh[kPartBuckets], ls[kPartBuckets];
-    __shared__ unsigned long long s_occ;
-    const int64_t g = blockIdx.x;
-    const int64_t lo = g * kPartTile, hi = min(a.n, lo + (int64_t)kPartTile);
     const int nb = 1 << a.d1_bits;
-    for (int b = threadIdx.x; b < kPartBuckets; b += blockDim.x) lh[b] = 0;
-    if (threadIdx.x == 0) s_occ = 0;
-    __syncthreads();
-    unsigned long long late = 0, flags = 0, occ = 0, wide = 0;
+    unsigned long long occ = 0, wide = 0;
     // Registers per record after classification: the key (compact: the hash word), the
     // value (32 bits for compact records), and bucket << 16 | rank in one word (~0: none).
     using V0 = std::conditional_t<C, int32_t, int64_t>;
-    int64_t key[kPartItems], ts[kPartItems], val[kPartItems];
-    V0 c0[kPartItems];
-    int64_t c1[kPartItems];
-    uint32_t pos[kPartItems], br[kPartItems];
+    V0 c0[IT];
+    int64_t c1[IT];
+    uint32_t pos[IT], br[IT];
 #pragma unroll
-    for (int it = 0; it < kPartItems; ++it) {  // all loads in flight first
-        const int64_t i = lo + it * kPartThreads + threadIdx.x;
-        key[it] = 0; ts[it] = 0; val[it] = 0;
-        if (i < hi) {
-            key[it] = __builtin_nontemporal_load(a.key + i);  // read once: keep it out of the caches
-            ts[it] = __builtin_nontemporal_load(a.ts + i);
-            if (a.val) val[it] = __builtin_nontemporal_load(a.val + i);
-        }
-    }
-#pragma unroll
-    for (int it = 0; it < kPartItems; ++it) {
-        const int64_t i = lo + it * kPartThreads + threadIdx.x;
+    for (int it = 0; it < IT; ++it) {
+        const int64_t i = lo + it * THR + threadIdx.x;
         int bk = -1;
         int64_t v0 = 0, v1 = 0;
         uint32_t ps = 0;
@@ -612,14 +600,15 @@ __global__ void __launch_bounds__(kPartThreads) GW_P1_ATTR k_rgn_p1(IngestArgs a
         pos[it] = ps;
         br[it] = bk >= 0 ? ((uint32_t)bk << 16) | atomicAdd(&lh[bk], 1u) : ~0u;
     }
+    occ_all |= occ;
     occ = wave_ior(occ);
-    if (__lane_id() == 0 && occ) atomicOr(&s_occ, occ);
+    if (__lane_id() == 0 && occ) atomicOr(s_occ, occ);
     __syncthreads();
     scan_buckets(lh, ls, nb);
-    if (threadIdx.x == 0 && s_occ) atomicOr(a.batch_occ, s_occ);
+    if (threadIdx.x == 0 && *s_occ) atomicOr(a.batch_occ, *s_occ);
     __syncthreads();
 #pragma unroll
-    for (int it = 0; it < kPartItems; ++it) {
+    for (int it = 0; it < IT; ++it) {
         if (br[it] == ~0u) continue;
         const uint32_t j = ls[br[it] >> 16] + (br[it] & 0xffffu);
         if constexpr (N4) {
@@ -640,7 +629,7 @@ __global__ void __launch_bounds__(kPartThreads) GW_P1_ATTR k_rgn_p1(IngestArgs a
     const uint32_t cnt = ls[nb - 1] + lh[nb - 1];
     const int64_t tile = a.tile0 + g;
     const int64_t base = tile * kPartTile;
-    for (uint32_t j = threadIdx.x; j < cnt; j += blockDim.x) {
+    for (uint32_t j = threadIdx.x; j < cnt; j += THR) {
         if constexpr (N4) {
             __builtin_nontemporal_store(s_r32[j], reinterpret_cast<uint32_t*>(a.p1_key) + base + j);
             continue;
@@ -655,11 +644,40 @@ __global__ void __launch_bounds__(kPartThreads) GW_P1_ATTR k_rgn_p1(IngestArgs a
             a.p1_pos[base + j] = s.pos[j];
         }
     }
-    for (int b = threadIdx.x; b < nb; b += blockDim.x) a.p1_row[tile * kPartBuckets + b] = desc_pack(ls[b], lh[b]);
+    for (int b = threadIdx.x; b < nb; b += THR) a.p1_row[tile * kPartBuckets + b] = desc_pack(ls[b], lh[b]);
     if constexpr ((C && ACC) || NR) {
         wide = wave_sum(wide);
         if (__lane_id() == 0 && wide) atomicAdd(&a.st->wide_vals, wide);
     }
+}
+
+template <int AGG, int FMT, bool GAP>
+__global__ void __launch_bounds__(kPartThreads) GW_P1_ATTR k_rgn_p1(IngestArgs a) {
+    constexpr bool C = FMT == kFmtCmp && cmp_agg<AGG>();
+    constexpr bool NR = FMT == kFmtNar && cmp_agg<AGG>();
+    constexpr bool AV = !C && !NR && (AGG == GW_AVG_I64 || AGG == GW_AVG_F64);
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const TileLds s = tile_lds<AV>(smem);
+    __shared__ uint32_t lh[kPartBuckets], ls[kPartBuckets];
+    __shared__ unsigned long long s_occ;
+    const int64_t g = blockIdx.x;
+    const int64_t lo = g * kPartTile, hi = min(a.n, lo + (int64_t)kPartTile);
+    for (int b = threadIdx.x; b < kPartBuckets; b += blockDim.x) lh[b] = 0;
+    if (threadIdx.x == 0) s_occ = 0;
+    __syncthreads();
+    unsigned long long late = 0, flags = 0, occ = 0;
+    int64_t key[kPartItems], ts[kPartItems], val[kPartItems];
+#pragma unroll
+    for (int it = 0; it < kPartItems; ++it) {  // all loads in flight first
+        const int64_t i = lo + it * kPartThreads + threadIdx.x;
+        key[it] = 0; ts[it] = 0; val[it] = 0;
+        if (i < hi) {
+            key[it] = __builtin_nontemporal_load(a.key + i);  // read once: keep it out of the caches
+            ts[it] = __builtin_nontemporal_load(a.ts + i);
+            if (a.val) val[it] = __builtin_nontemporal_load(a.val + i);
+        }
+    }
+    p1_tile<AGG, FMT, GAP, kPartThreads, kPartItems>(a, g, lo, hi, key, ts, val, s, lh, ls, &s_occ, late, flags, occ);
     block_commit(a.st, late, 0, flags, occ);
 }
 
@@ -2052,7 +2070,7 @@ static size_t part_lds_bytes(const IngestArgs& a) {
     return (size_t)kPartTile * 8 * (a.t.words == 2 ? 3 : 2) + 2 * kPartTile;
 }
 
-int region_group(int d1_bits) { return std::max(1, std::min(kMaxGroup, 7 * (1 << d1_bits) / 8)); }
+int region_group(int d1_bits) { return std::max(1, std::min(kMaxGroup, 7 * (1 << d1_bits) / 8 * (4096 / kPartTile))); }
 
 // Region path, P1 over one watermark batch: one block per 4096-record tile.
 hipError_t launch_region_p1(const IngestArgs& a, hipStream_t s) {
