@@ -1184,6 +1184,12 @@ __global__ void __launch_bounds__(kSpKeyThreads) k_sp_keys(SegArgs a, const uint
                     }
                 }
             } else {  // k_sp_slow replays it (a dense launch: no divergence against the fast runs)
+                if (a.exp) {  // GW_SP_EXP: why (two shards' spare counters)
+                    if (!fit) atomicAdd(&a.st->sh[0].pad0, 1ull);
+                    else if (!(f0 && f1)) atomicAdd(&a.st->sh[0].pad1, 1ull);
+                    else if ((uint64_t)(w10 | w11) & (kBigMeta | kPuntMeta)) atomicAdd(&a.st->sh[1].pad0, 1ull);
+                    else atomicAdd(&a.st->sh[1].pad1, 1ull);
+                }
                 const uint64_t bal = __ballot(true);
                 unsigned long long at = 0;
                 const int ld = __ffsll((long long)bal) - 1;
@@ -2400,9 +2406,15 @@ static int ingest_region(SessionState* s, int64_t n, const int64_t* key, const i
     if ((rc = session_refresh(s, err))) return rc;
     const int64_t n_punt = (int64_t)s->h_st->overflow;
     s->stats.session_punted += n_punt;
-    if (sp_exp)
-        fprintf(stderr, "[sp_keys] slow home slots %llu of batch %lld, punted %lld\n",
-                (unsigned long long)s->h_st->spills, (long long)n, (long long)n_punt);
+    if (sp_exp) {
+        fprintf(stderr, "[sp_keys] slow home slots %llu of batch %lld (keys %llu, probe %llu, wide %llu, lane %llu), "
+                        "punted %lld\n",
+                (unsigned long long)s->h_st->spills, (long long)n, (unsigned long long)s->h_st->sh[0].pad0,
+                (unsigned long long)s->h_st->sh[0].pad1, (unsigned long long)s->h_st->sh[1].pad0,
+                (unsigned long long)s->h_st->sh[1].pad1, (long long)n_punt);
+        SCHECK(launch_status_set(s->d_st, 0, 0, 6, s->stream));  // ShardCtr pad0
+        SCHECK(launch_status_set(s->d_st, 0, 0, 7, s->stream));  // ShardCtr pad1
+    }
     s->stats.session_slow += (int64_t)s->h_st->spills;
     if ((rc = run_migrate(s, err))) return rc;
     if (!n_punt) return GW_OK;
