@@ -555,6 +555,7 @@ __device__ __forceinline__ void p1_tile(const IngestArgs& a, int64_t g, int64_t 
     uint32_t* s_r32 = reinterpret_cast<uint32_t*>(s.k);  // N4: the records
     const int nb = 1 << a.d1_bits;
     unsigned long long occ = 0, wide = 0;
+    bool special = false;
     // Registers per record after classification: the key (compact: the hash word), the
     // value (32 bits for compact records), and bucket << 16 | rank in one word (~0: none).
     using V0 = std::conditional_t<C, int32_t, int64_t>;
@@ -582,23 +583,51 @@ __device__ __forceinline__ void p1_tile(const IngestArgs& a, int64_t g, int64_t 
         }
         if (st == REC_RING) {
             occ |= 1ull << ps;
-            if (key[it] == kEmptyKey) {  // sentinel slot: rare, straight atomics
-                cell_atomic<AGG>(pt_cell(a.t, a.t.cap, ps), v0, v1);
-                mask_set<AGG>(a.t, a.t.cap, ps);
+            if (key[it] == kEmptyKey) {
+                special = true;  // the sentinel slot: below
             } else {
                 const uint64_t h = slot_hash(key[it]);
                 bk = (int)(pt_key_region(a.t, h) >> a.d2_bits);
                 if constexpr (C) key[it] = (int64_t)cmp_pack(h, ps, a.d1_bits);  // key -> word
                 if constexpr (NR) key[it] = N4 ? (int64_t)nar_pack32(key[it], ps) : (int64_t)nar_pack(key[it], v0, ps);
             }
+        } else if (st != REC_SKIP) {
+            special = true;  // deferred, re-fire or side-output record: below
         }
-        defer_write(a, st == REC_DEFER, key[it], pane, v0, v1);
-        refire_write(a, st == REC_REFIRE, key[it], pane, v0, v1, i);
-        if (a.lo_key) late_write(a, st == REC_LATE, key[it], i);
         c0[it] = (V0)v0;
         c1[it] = v1;
         pos[it] = ps;
         br[it] = bk >= 0 ? ((uint32_t)bk << 16) | atomicAdd(&lh[bk], 1u) : ~0u;
+    }
+    // Rare records (deferred, re-fire, side output, the sentinel key) in a second pass that
+    // only waves holding one run: it re-reads and re-classifies its items (classify is
+    // deterministic; its late / flag counts were taken above) and writes them out, so the
+    // unrolled pass above stays small.
+    if (__any(special)) {
+#pragma unroll 1
+        for (int it = 0; it < IT; ++it) {
+            const int64_t i = lo + it * THR + threadIdx.x;
+            int64_t k = 0, v0 = 0, v1 = 0, pane = 0;
+            uint32_t ps = 0;
+            int st = REC_SKIP;
+            if (i < hi) {
+                unsigned long long dl = 0, df = 0;
+                k = a.key[i];
+                st = classify<AGG, GAP>(a, a.ts[i], a.val ? a.val[i] : 0, ps, pane, v0, v1, dl, df);
+                if (C && ACC && st == REC_RING && (v0 < INT32_MIN || v0 > INT32_MAX)) st = REC_DEFER;
+                if (NR && st == REC_RING &&
+                    ((uint64_t)k >= (uint64_t)(N4 ? kNarCountKeyLimit : kNarKeyLimit) ||
+                     (!N4 && (v0 < -kNarValLimit || v0 >= kNarValLimit))))
+                    st = REC_DEFER;
+                if (st == REC_RING && k == kEmptyKey) {  // sentinel slot: straight atomics
+                    cell_atomic<AGG>(pt_cell(a.t, a.t.cap, ps), v0, v1);
+                    mask_set<AGG>(a.t, a.t.cap, ps);
+                }
+            }
+            defer_write(a, st == REC_DEFER, k, pane, v0, v1);
+            refire_write(a, st == REC_REFIRE, k, pane, v0, v1, i);
+            if (a.lo_key) late_write(a, st == REC_LATE, k, i);
+        }
     }
     occ_all |= occ;
     occ = wave_ior(occ);
