@@ -37,6 +37,8 @@ FLAG_NO_BUFFER = 32
 FLAG_LATE_SIDE_OUTPUT = 64
 FLAG_FIRST_ELEMENT = 128
 FLAG_NO_NARROW = 256
+FLAG_BY_FIELD = 512
+FLAG_BY_LAST = 1024
 
 EXPORTS = [
     "gw_create", "gw_destroy", "gw_last_error", "gw_abi_version", "gw_ingest", "gw_ingest_device",

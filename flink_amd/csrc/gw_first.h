@@ -25,4 +25,16 @@ hipError_t fe_log_regrow(const int64_t* o, int64_t ocap, int64_t* d, int64_t nca
 hipError_t fe_log_gather(const int64_t* log, int64_t cap, const int64_t* seq, int64_t n, int64_t* out, hipStream_t s);
 // Append n payload words at log position pos (a ring of cap words).
 hipError_t fe_log_append(int64_t* log, int64_t cap, int64_t pos, const int64_t* src, int64_t n, hipStream_t s);
+// minBy / maxBy (GW_FLAG_BY_FIELD): scratch bytes fe_by_select needs for n rows.
+size_t fe_by_scratch_bytes(int64_t n);
+// For each of the n rows (key, start, res = the window's MIN / MAX of the field), the sequence of
+// the element it stands for: the first (last) live log record [log_base, log_end) of the row's
+// key and window whose field equals res.  The log holds 4 columns of log_cap words (payload, key,
+// ts, field); records below restored_end are restored elements of the window starting at their
+// ts.  o_seq / o_pay (either may be null) get the sequence and its payload; *d_bad |= 2 when a
+// row has no element in the log.
+hipError_t fe_by_select(int64_t n, const int64_t* key, const int64_t* start, const int64_t* res, const int64_t* log,
+                        int64_t log_cap, int64_t log_base, int64_t log_end, int64_t restored_end, int64_t offset,
+                        int64_t slide, int64_t size, bool last, bool f64, int64_t* o_seq, int64_t* o_pay,
+                        void* scratch, size_t scratch_bytes, int32_t* d_bad, hipStream_t s);
 }  // namespace gw

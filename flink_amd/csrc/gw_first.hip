@@ -189,4 +189,151 @@ hipError_t fe_log_append(int64_t* log, int64_t cap, int64_t pos, const int64_t* 
     return hipGetLastError();
 }
 
+// ---- minBy / maxBy (GW_FLAG_BY_FIELD) ----------------------------------------------------
+// WindowedStream.minBy / maxBy (WindowedStream.java:725-771) reduce with ComparableAggregator's
+// byAggregate branch (ComparableAggregator.java:88-95, Min/MaxByComparator in Comparator.java):
+// the window's state is the ELEMENT whose field is the window's minimum / maximum, the first of
+// equal ones in arrival order (first = true) or the last.  kids[0] folds MIN / MAX of the field
+// (the row's result); at a fire one pass over the live log -- (payload, key, ts, field) of every
+// record whose windows are not all cleaned -- picks the element: each record probes the fired
+// rows of its windows in an open-addressing table of (key, start) and, when its field equals the
+// row's result, offers its sequence (atomicMin for the first, atomicMax for the last).  A record
+// is in a fired window's state exactly when it is in the log with a timestamp in the window: a
+// record of a cleaned window is dropped, and a cleaned window never fires again.  For the first
+// element this also holds for a lateness re-firing's prefix state (the earliest equal record
+// precedes the late record that fired it).  Restored elements (sequences below `restored_end`)
+// stand for their own window only: their timestamp is that window's start.
+
+__device__ __forceinline__ uint64_t by_hash(int64_t key, int64_t start) {
+    uint64_t x = (uint64_t)key * 0x9e3779b97f4a7c15ull ^ ((uint64_t)start + 0x632be59bd9b4e019ull) * 0xbf58476d1ce4e5b9ull;
+    return x ^ (x >> 31);
+}
+
+__device__ __forceinline__ int64_t by_floor_div(int64_t a, int64_t b) {
+    const int64_t q = a / b;
+    return (a % b != 0 && ((a < 0) != (b < 0))) ? q - 1 : q;
+}
+
+// Field equality as Long.compareTo / Double.compare == 0 (NaNs equal, -0.0 != 0.0).
+__device__ __forceinline__ bool by_equal(int64_t a, int64_t b, bool f64) {
+    if (!f64) return a == b;
+    const uint64_t qn = 0x7ff8000000000000ull;
+    const bool na = ((uint64_t)a & 0x7fffffffffffffffull) > 0x7ff0000000000000ull;
+    const bool nb = ((uint64_t)b & 0x7fffffffffffffffull) > 0x7ff0000000000000ull;
+    return (na ? qn : (uint64_t)a) == (nb ? qn : (uint64_t)b);
+}
+
+__global__ void k_by_km_init(int64_t* km) {
+    if (threadIdx.x == 0) { km[0] = INT64_MAX; km[1] = INT64_MIN; }
+}
+
+// Rows into the table (one slot per row, duplicates included); sel[i] = the neutral sequence;
+// km = [min, max] window index over the rows.
+__global__ void k_by_build(int64_t n, const int64_t* key, const int64_t* start, int32_t* table, uint64_t mask,
+                           int64_t* sel, int64_t init, int64_t offset, int64_t slide, int64_t* km) {
+    int64_t lo = INT64_MAX, hi = INT64_MIN;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        sel[i] = init;
+        const int64_t k = by_floor_div(start[i] - offset, slide);
+        lo = min(lo, k);
+        hi = max(hi, k);
+        uint64_t h = by_hash(key[i], start[i]) & mask;
+        while (atomicCAS(&table[h], -1, (int32_t)i) != -1) h = (h + 1) & mask;
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        lo = min(lo, (int64_t)__shfl_xor(lo, o));
+        hi = max(hi, (int64_t)__shfl_xor(hi, o));
+    }
+    if (__lane_id() == 0 && lo <= hi) {
+        atomicMin((long long*)&km[0], (long long)lo);
+        atomicMax((long long*)&km[1], (long long)hi);
+    }
+}
+
+struct ByScanArgs {
+    const int64_t* log;  // 4 columns of cap words: payload, key, ts, field
+    int64_t cap, lo, hi, restored_end;
+    const int32_t* table;
+    uint64_t mask;
+    const int64_t *key, *start, *res;
+    int64_t* sel;
+    const int64_t* km;
+    int64_t offset, slide, size;
+    int last, f64;
+};
+
+__global__ void __launch_bounds__(256) k_by_scan(ByScanArgs a) {
+    const int64_t k_lo = a.km[0], k_hi = a.km[1];
+    for (int64_t q = a.lo + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; q < a.hi;
+         q += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t at = q % a.cap;
+        const int64_t key = a.log[a.cap + at], ts = a.log[2 * a.cap + at], v = a.log[3 * a.cap + at];
+        const int64_t kt = by_floor_div(ts - a.offset, a.slide);
+        int64_t k0 = q < a.restored_end ? kt : by_floor_div(ts - a.offset - a.size, a.slide) + 1;
+        const int64_t k1 = min(kt, k_hi);
+        k0 = max(k0, k_lo);
+        for (int64_t k = k0; k <= k1; ++k) {
+            const int64_t s = a.offset + k * a.slide;
+            uint64_t h = by_hash(key, s) & a.mask;
+            for (int32_t r; (r = a.table[h]) >= 0; h = (h + 1) & a.mask) {
+                if (a.key[r] != key || a.start[r] != s || !by_equal(v, a.res[r], a.f64)) continue;
+                if (a.last) atomicMax((long long*)&a.sel[r], (long long)q);
+                else atomicMin((long long*)&a.sel[r], (long long)q);
+            }
+        }
+    }
+}
+
+// o_pay[i] = the payload of row i's element; bad |= 2 when it is not in the log.
+__global__ void k_by_emit(int64_t n, const int64_t* sel, const int64_t* log, int64_t cap, int64_t base, int64_t end,
+                          int64_t* o_seq, int64_t* o_pay, int32_t* bad) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t q = sel[i];
+        int64_t pay = 0;
+        if (q < base || q >= end) atomicOr(bad, 2);
+        else pay = log[q % cap];
+        if (o_seq) o_seq[i] = q;
+        if (o_pay) o_pay[i] = pay;
+    }
+}
+
+size_t fe_by_scratch_bytes(int64_t n) {
+    uint64_t tcap = 1024;
+    while (tcap < (uint64_t)(2 * n)) tcap <<= 1;
+    return tcap * 4 + (size_t)std::max<int64_t>(n, 1) * 8 + 256;
+}
+
+hipError_t fe_by_select(int64_t n, const int64_t* key, const int64_t* start, const int64_t* res, const int64_t* log,
+                        int64_t log_cap, int64_t log_base, int64_t log_end, int64_t restored_end, int64_t offset,
+                        int64_t slide, int64_t size, bool last, bool f64, int64_t* o_seq, int64_t* o_pay,
+                        void* scratch, size_t scratch_bytes, int32_t* d_bad, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    if (scratch_bytes < fe_by_scratch_bytes(n) || slide <= 0) return hipErrorInvalidValue;
+    uint64_t tcap = 1024;
+    while (tcap < (uint64_t)(2 * n)) tcap <<= 1;
+    uint8_t* p = (uint8_t*)scratch;
+    int64_t* km = (int64_t*)p;
+    int64_t* sel = (int64_t*)(p + 256);
+    int32_t* table = (int32_t*)(p + 256 + (size_t)n * 8);
+    hipError_t e = hipMemsetAsync(table, 0xff, tcap * 4, s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_by_km_init, dim3(1), dim3(64), 0, s, km);
+    hipLaunchKernelGGL(k_by_build, dim3(grid_n(n)), dim3(256), 0, s, n, key, start, table, tcap - 1, sel,
+                       last ? INT64_MIN : INT64_MAX, offset, slide, km);
+    if (log_end > log_base) {
+        ByScanArgs a{};
+        a.log = log; a.cap = log_cap; a.lo = log_base; a.hi = log_end; a.restored_end = restored_end;
+        a.table = table; a.mask = tcap - 1;
+        a.key = key; a.start = start; a.res = res; a.sel = sel; a.km = km;
+        a.offset = offset; a.slide = slide; a.size = size;
+        a.last = last; a.f64 = f64;
+        const int64_t m = log_end - log_base;
+        const unsigned g = (unsigned)std::max<int64_t>(1, std::min<int64_t>((m + 255) / 256, 8192));
+        hipLaunchKernelGGL(k_by_scan, dim3(g), dim3(256), 0, s, a);
+    }
+    hipLaunchKernelGGL(k_by_emit, dim3(grid_n(n)), dim3(256), 0, s, n, sel, log, log_cap, log_base, log_end, o_seq,
+                       o_pay, d_bad);
+    return hipGetLastError();
+}
+
 }  // namespace gw

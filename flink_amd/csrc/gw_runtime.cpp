@@ -154,6 +154,11 @@ struct gw_handle {
     // kids[1] the MIN of each record's arrival sequence; the payload log keeps every record's
     // payload (a ring indexed by sequence) until all windows that could hold it are cleaned.
     bool fe = false;
+    // GW_FLAG_BY_FIELD (minBy / maxBy): kids[0] alone folds MIN / MAX of the field, the log
+    // holds (payload, key, ts, field) per record and each fire picks the element (fe_by_select)
+    bool fe_by = false, fe_by_last = false;
+    int fe_cols = 1;                                    // log columns of fe_log_cap words each
+    int64_t fe_restored_end = 0;                        // sequences below: restored elements
     int64_t fe_seq = 0;                                 // sequence of the next record
     int64_t* fe_log = nullptr;
     int64_t fe_log_cap = 0, fe_log_base = 0;            // live sequences [fe_log_base, fe_seq)
@@ -1999,18 +2004,23 @@ static int make_composite(gw_handle* h, int64_t J) {
     return GW_OK;
 }
 
-// A first-element handle h (its cfg set): kids[0] the aggregate, kids[1] MIN(sequence).
+// A first-element handle h (its cfg set): kids[0] the aggregate, kids[1] MIN(sequence);
+// minBy / maxBy (GW_FLAG_BY_FIELD): kids[0] alone, MIN / MAX of the field.
 static int make_first_element(gw_handle* h) {
     if (h->stream) {  // kernels of its own (sequence, payload log, join) run on kids[0]'s stream
         hipStreamSynchronize(h->stream);
         hipStreamDestroy(h->stream);
         h->stream = nullptr;
     }
+    h->fe_by = (h->cfg.flags & GW_FLAG_BY_FIELD) != 0;
+    h->fe_by_last = (h->cfg.flags & GW_FLAG_BY_LAST) != 0;
+    h->fe_cols = h->fe_by ? 4 : 1;
     gw_config a = h->cfg, b = h->cfg;
-    a.flags &= ~GW_FLAG_FIRST_ELEMENT;
-    b.flags &= ~(GW_FLAG_FIRST_ELEMENT | GW_FLAG_LATE_SIDE_OUTPUT);
+    a.flags &= ~(GW_FLAG_FIRST_ELEMENT | GW_FLAG_BY_FIELD | GW_FLAG_BY_LAST);
+    b.flags &= ~(GW_FLAG_FIRST_ELEMENT | GW_FLAG_BY_FIELD | GW_FLAG_BY_LAST | GW_FLAG_LATE_SIDE_OUTPUT);
     b.agg = GW_MIN_I64;
     for (const gw_config* c : {&a, &b}) {
+        if (c == &b && h->fe_by) break;
         gw_handle* kid = nullptr;
         const int rc = gw_create(c, &kid);
         if (rc) return rc;
@@ -2077,8 +2087,10 @@ int gw_create(const gw_config* cfg, gw_handle** out) {
     int64_t cap = 1024;
     while ((double)cap * 0.7 < (double)hint) cap *= 2;
 
+    if ((cfg->flags & GW_FLAG_BY_LAST) && !(cfg->flags & GW_FLAG_BY_FIELD))
+        return bail(GW_E_INVALID, "GW_FLAG_BY_LAST without GW_FLAG_BY_FIELD");
     if (cfg->assigner == GW_SESSION || cfg->assigner == GW_COUNT_TUMBLING || cfg->assigner == GW_COUNT_SLIDING) {
-        if (cfg->flags & GW_FLAG_FIRST_ELEMENT)
+        if (cfg->flags & (GW_FLAG_FIRST_ELEMENT | GW_FLAG_BY_FIELD))
             return bail(GW_E_UNSUPPORTED, "first-element rows are for tumbling and sliding event-time windows");
         h->session = true;  // the per-key slot path (session merging or count windows)
         rc = session_create(h->sess, *cfg, cap, h->stream, h->d_st, why);
@@ -2087,12 +2099,18 @@ int gw_create(const gw_config* cfg, gw_handle** out) {
         *out = h;
         return GW_OK;
     }
-    if (cfg->flags & GW_FLAG_FIRST_ELEMENT) {
+    if (cfg->flags & (GW_FLAG_FIRST_ELEMENT | GW_FLAG_BY_FIELD)) {
         if (cfg->trigger != GW_EVENT_TIME_TRIGGER)
             return bail(GW_E_UNSUPPORTED, "first-element rows with PurgingTrigger are not supported");
         const int a = cfg->agg;
         if (a == GW_COUNT || a == GW_AVG_I64 || a == GW_AVG_F64)
             return bail(GW_E_INVALID, "first-element rows are for the positional aggregates sum / min / max");
+        if ((cfg->flags & GW_FLAG_BY_FIELD) && !(a == GW_MIN_I64 || a == GW_MAX_I64 || a == GW_MIN_F64 || a == GW_MAX_F64))
+            return bail(GW_E_INVALID, "minBy / maxBy (GW_FLAG_BY_FIELD) take GW_MIN_* / GW_MAX_*");
+        // the last of equal elements of a lateness re-firing's prefix state would need the
+        // re-firing record's sequence per row
+        if ((cfg->flags & GW_FLAG_BY_LAST) && cfg->allowed_lateness > 0)
+            return bail(GW_E_UNSUPPORTED, "minBy / maxBy with first = false under allowed lateness");
         rc = make_first_element(h);
         if (rc) return bail(rc, g_create_error);
         *out = h;
@@ -2252,14 +2270,68 @@ static int fe_reserve_rows(gw_handle* h, int64_t need) {
     return GW_OK;
 }
 
+static int fe_reserve_scratch(gw_handle* h, size_t need) {
+    if (need <= h->fe_scratch_bytes) return GW_OK;
+    if (h->fe_scratch) {
+        hipStreamSynchronize(h->stream);
+        hipFree(h->fe_scratch);
+    }
+    h->fe_scratch = nullptr;
+    h->fe_scratch_bytes = 0;
+    if (hipMalloc(&h->fe_scratch, need) != hipSuccess) return h->fail(GW_E_OOM, "first-element join scratch");
+    h->fe_scratch_bytes = need;
+    return GW_OK;
+}
+
+// minBy / maxBy: per (key, window start, MIN / MAX) the sequence and payload of the window's
+// element (gw_first.hip fe_by_select).  o_seq / o_pay may be null.
+static int by_select(gw_handle* h, int64_t n, const int64_t* key, const int64_t* start, const int64_t* res,
+                     int64_t* o_seq, int64_t* o_pay) {
+    if (n <= 0) return GW_OK;
+    int rc = fe_reserve_scratch(h, fe_by_scratch_bytes(n));
+    if (rc) return rc;
+    const int64_t slide = h->cfg.assigner == GW_TUMBLING ? h->cfg.size : h->cfg.slide;
+    const bool f64 = h->cfg.agg == GW_MIN_F64 || h->cfg.agg == GW_MAX_F64;
+    hipError_t e = hipMemsetAsync(h->fe_bad, 0, 4, h->stream);
+    if (e == hipSuccess)
+        e = fe_by_select(n, key, start, res, h->fe_log, h->fe_log_cap, h->fe_log_base, h->fe_seq, h->fe_restored_end,
+                         h->cfg.offset, slide, h->cfg.size, h->fe_by_last, f64, o_seq, o_pay, h->fe_scratch,
+                         h->fe_scratch_bytes, h->fe_bad, h->stream);
+    int32_t bad = 0;
+    if (e == hipSuccess) e = hipMemcpyAsync(&bad, h->fe_bad, 4, hipMemcpyDeviceToHost, h->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
+    if (e != hipSuccess) return h->fail(GW_E_DEVICE, "minBy / maxBy element: %s", hipGetErrorString(e));
+    if (bad) return h->fail(GW_E_STATE, "minBy / maxBy element: a window's element is not in the log");
+    return GW_OK;
+}
+
 // The rows both operators fired, joined by (key, window start) with the payload of the
 // window's first element, appended to the c_* rows; then the payloads no window can need
-// any more leave the log.
+// any more leave the log.  minBy / maxBy: kids[0]'s rows with their element's payload.
 static int fe_gather(gw_handle* h) {
-    gw_handle *A = h->kids[0], *B = h->kids[1];
+    gw_handle* A = h->kids[0];
     int64_t na = 0, nb = 0;
     int rc = gw_pending_rows(A, &na);
     if (rc) return kid_rc(h, A, rc);
+    if (h->fe_by) {
+        if (na <= 0) return GW_OK;
+        const int64_t *ak, *as, *ae;
+        const void* ar;
+        int64_t x = 0;
+        if ((rc = gw_rows_device(A, &ak, &as, &ae, &ar, &x))) return kid_rc(h, A, rc);
+        if ((rc = fe_reserve_rows(h, h->c_rows + na))) return rc;
+        const int64_t o = h->c_rows;
+        const int64_t* src[4] = {ak, as, ae, (const int64_t*)ar};
+        int64_t* dst[4] = {h->c_key + o, h->c_start + o, h->c_end + o, h->c_res + o};
+        for (int q = 0; q < 4; ++q)
+            if (hipMemcpyAsync(dst[q], src[q], (size_t)na * 8, hipMemcpyDeviceToDevice, h->stream) != hipSuccess)
+                return h->fail(GW_E_DEVICE, "minBy / maxBy rows");
+        if ((rc = by_select(h, na, ak, as, (const int64_t*)ar, nullptr, h->c_pay + o))) return rc;
+        h->c_rows += na;
+        if ((rc = gw_clear_rows(A))) return kid_rc(h, A, rc);
+        return GW_OK;
+    }
+    gw_handle* B = h->kids[1];
     if ((rc = gw_pending_rows(B, &nb))) return kid_rc(h, B, rc);
     if (na != nb) return h->fail(GW_E_STATE, "first-element rows out of step (%lld vs %lld)", (long long)na, (long long)nb);
     if (na > 0) {
@@ -2275,14 +2347,7 @@ static int fe_gather(gw_handle* h) {
                 return h->fail(GW_E_DEVICE, "first-element join: stream ordering");
         }
         if ((rc = fe_reserve_rows(h, h->c_rows + na))) return rc;
-        const size_t need = fe_join_scratch_bytes(na);
-        if (need > h->fe_scratch_bytes) {
-            if (h->fe_scratch) hipFree(h->fe_scratch);
-            h->fe_scratch = nullptr;
-            h->fe_scratch_bytes = 0;
-            if (hipMalloc(&h->fe_scratch, need) != hipSuccess) return h->fail(GW_E_OOM, "first-element join scratch");
-            h->fe_scratch_bytes = need;
-        }
+        if ((rc = fe_reserve_scratch(h, fe_join_scratch_bytes(na)))) return rc;
         const int64_t o = h->c_rows;
         hipError_t e = hipMemsetAsync(h->fe_bad, 0, 4, h->stream);
         if (e == hipSuccess)
@@ -2354,9 +2419,11 @@ static int fe_log_reserve(gw_handle* h, int64_t n) {
     if (need > h->fe_log_cap) {
         const int64_t ncap = std::max<int64_t>(2 * need, 1 << 20);
         int64_t* nl = nullptr;
-        if (hipMalloc((void**)&nl, (size_t)ncap * 8) != hipSuccess) return h->fail(GW_E_OOM, "payload log");
+        if (hipMalloc((void**)&nl, (size_t)ncap * 8 * h->fe_cols) != hipSuccess) return h->fail(GW_E_OOM, "payload log");
         hipError_t e = hipSuccess;
-        if (h->fe_log) e = fe_log_regrow(h->fe_log, h->fe_log_cap, nl, ncap, h->fe_log_base, h->fe_seq, s);
+        for (int c = 0; c < h->fe_cols && h->fe_log && e == hipSuccess; ++c)  // column c at c * cap
+            e = fe_log_regrow(h->fe_log + c * h->fe_log_cap, h->fe_log_cap, nl + c * ncap, ncap, h->fe_log_base,
+                              h->fe_seq, s);
         if (e == hipSuccess) e = hipStreamSynchronize(s);
         if (h->fe_log) hipFree(h->fe_log);
         h->fe_log = nl;
@@ -2389,11 +2456,16 @@ int gw_ingest_payload_device(gw_handle* h, int64_t n, const int64_t* d_key, cons
         if (hipMalloc((void**)&h->fe_seqbuf, (size_t)n * 8) != hipSuccess) return h->fail(GW_E_OOM, "sequence buffer");
         h->fe_seqbuf_cap = n;
     }
-    hipError_t e = fe_iota64(h->fe_seqbuf, n, h->fe_seq, s);
+    hipError_t e = h->fe_by ? hipSuccess : fe_iota64(h->fe_seqbuf, n, h->fe_seq, s);
     if (e == hipSuccess) {
         const int rc = fe_log_reserve(h, n);
         if (rc) return rc;
         e = fe_log_append(h->fe_log, h->fe_log_cap, h->fe_seq, d_payload, n, s);
+        if (h->fe_by) {  // minBy / maxBy: key, ts and field beside the payload
+            const int64_t* col[3] = {d_key, d_ts, (const int64_t*)d_value};
+            for (int c = 0; c < 3 && e == hipSuccess; ++c)
+                e = fe_log_append(h->fe_log + (c + 1) * h->fe_log_cap, h->fe_log_cap, h->fe_seq, col[c], n, s);
+        }
     }
     if ((int64_t)h->fe_batches.size() >= gw_handle::kFeBatches - 1)
         return h->fail(GW_E_STATE, "first-element log: too many batches without a watermark");
@@ -2405,7 +2477,7 @@ int gw_ingest_payload_device(gw_handle* h, int64_t n, const int64_t* d_key, cons
     h->fe_batch_no++;
     int rc = gw_ingest_device(h->kids[0], n, d_key, d_key_hash, d_ts, d_value, (void*)s);
     if (rc) return kid_rc(h, h->kids[0], rc);
-    if ((rc = gw_ingest_device(h->kids[1], n, d_key, d_key_hash, d_ts, h->fe_seqbuf, (void*)s)))
+    if (!h->fe_by && (rc = gw_ingest_device(h->kids[1], n, d_key, d_key_hash, d_ts, h->fe_seqbuf, (void*)s)))
         return kid_rc(h, h->kids[1], rc);
     h->fe_seq += n;
     if (ps != s) {
@@ -3006,10 +3078,16 @@ static int comp_restore(gw_handle* h, const void* buf, int64_t len) {
 // aggregate, payload of the first element) with flags |= kSnapFirstElement, and kids[0]'s
 // timers.  A restore gives the restored first elements new arrival sequences: their payloads
 // go to the log, kids[1] gets (window, key, new sequence) entries.
+// minBy / maxBy handles hold the same entries: the element's payload comes from the log
+// (fe_by_select over the entries' (key, window, MIN / MAX)) instead of kids[1]'s sequence.
 static int fe_snapshot(gw_handle* h, int32_t kg_lo, int32_t kg_hi, void* buf, int64_t cap, int64_t* len) {
-    gw_handle *A = h->kids[0], *B = h->kids[1];
+    gw_handle *A = h->kids[0], *B = h->fe_by ? h->kids[0] : h->kids[1];
     std::vector<uint8_t> ba, bb;
     for (auto pr : {std::make_pair(A, &ba), std::make_pair(B, &bb)}) {
+        if (h->fe_by && pr.second == &bb) {
+            bb = ba;
+            break;
+        }
         int64_t l = 0;
         int rc = gw_snapshot(pr.first, kg_lo, kg_hi, nullptr, 0, &l);
         if (rc) return kid_rc(h, pr.first, rc);
@@ -3025,7 +3103,7 @@ static int fe_snapshot(gw_handle* h, int32_t kg_lo, int32_t kg_hi, void* buf, in
     const int kb = (ha.flags & kSnapKeyHashes) ? 4 : 0;
     const int64_t ea = 24 + kb + A->acc_bytes(), eb = 24 + kb + 8;  // B: MIN_I64 of the sequence
     // pass 1: the sequences of every entry's first element, in entry order
-    std::vector<int64_t> seqs;
+    std::vector<int64_t> seqs, by_key, by_start, by_res;
     struct Sec { const uint8_t *sa, *sb, *ta; int32_t n, t; };
     std::vector<Sec> secs((size_t)nk);
     for (int64_t g = 0; g < nk; ++g) {
@@ -3043,14 +3121,34 @@ static int fe_snapshot(gw_handle* h, int32_t kg_lo, int32_t kg_hi, void* buf, in
             const uint8_t* xa = sc.sa + i * ea;
             const uint8_t* xb = sc.sb + i * eb;
             if (memcmp(xa, xb, 24 + kb) != 0) return h->fail(GW_E_STATE, "first-element snapshot: entries differ");
-            seqs.push_back(gw_handle::rd64(xb + 24 + kb));
+            if (h->fe_by) {  // (start, end, key, [hash], MIN / MAX)
+                by_start.push_back(gw_handle::rd64(xa));
+                by_key.push_back(gw_handle::rd64(xa + 16));
+                by_res.push_back(gw_handle::rd64(xa + 24 + kb));
+            } else {
+                seqs.push_back(gw_handle::rd64(xb + 24 + kb));
+            }
         }
         sc.ta = sc.sa + sc.n * ea + 4;  // past the (empty) merging window set
         sc.t = gw_handle::rd32(sc.ta);
         sc.ta += 4;
         secs[g] = sc;
     }
-    std::vector<int64_t> pays(seqs.size());
+    std::vector<int64_t> pays(h->fe_by ? by_key.size() : seqs.size());
+    if (h->fe_by && !by_key.empty()) {
+        const size_t m = by_key.size();
+        int64_t* d = nullptr;
+        HIPCHECK_H(h, hipMalloc((void**)&d, m * 32));
+        hipError_t e = hipMemcpyAsync(d, by_key.data(), m * 8, hipMemcpyHostToDevice, h->stream);
+        if (e == hipSuccess) e = hipMemcpyAsync(d + m, by_start.data(), m * 8, hipMemcpyHostToDevice, h->stream);
+        if (e == hipSuccess) e = hipMemcpyAsync(d + 2 * m, by_res.data(), m * 8, hipMemcpyHostToDevice, h->stream);
+        int rc = e == hipSuccess ? by_select(h, (int64_t)m, d, d + m, d + 2 * m, nullptr, d + 3 * m)
+                                 : h->fail(GW_E_DEVICE, "minBy / maxBy snapshot: %s", hipGetErrorString(e));
+        if (rc == GW_OK && hipMemcpy(pays.data(), d + 3 * m, m * 8, hipMemcpyDeviceToHost) != hipSuccess)
+            rc = h->fail(GW_E_DEVICE, "minBy / maxBy snapshot");
+        hipFree(d);
+        if (rc) return rc;
+    }
     if (!seqs.empty()) {
         for (int64_t q : seqs)
             if (q < h->fe_log_base || q >= h->fe_seq) return h->fail(GW_E_STATE, "first-element snapshot: payload released");
@@ -3101,10 +3199,11 @@ static int fe_restore(gw_handle* h, const void* buf, int64_t len) {
     memcpy(&hd, buf, sizeof hd);
     if (memcmp(hd.magic, "GWS1", 4) != 0 || hd.version != 4 || !(hd.flags & kSnapFirstElement) || hd.agg != h->cfg.agg)
         return h->fail(GW_E_INVALID, "not a first-element snapshot of this aggregate");
-    gw_handle *A = h->kids[0], *B = h->kids[1];
+    gw_handle *A = h->kids[0], *B = h->fe_by ? nullptr : h->kids[1];
     const int64_t nk = (int64_t)hd.kg_hi - hd.kg_lo + 1, hdr = (int64_t)sizeof hd + (nk + 1) * 8;
     if (nk <= 0 || hd.entries < 0 || len < hdr || hd.entries > len - hdr)
         return h->fail(GW_E_INVALID, "truncated snapshot blob");
+    std::vector<int64_t> by_cols[3];  // minBy / maxBy: the restored elements' key, window start, field
     const int kb = (hd.flags & kSnapKeyHashes) ? 4 : 0;
     const int64_t ea = 24 + kb + A->acc_bytes(), ef = ea + 8;
     const uint8_t* p = (const uint8_t*)buf + hdr;
@@ -3128,6 +3227,11 @@ static int fe_restore(gw_handle* h, const void* buf, int64_t len) {
             gw_handle::be64(pb, seq0 + (int64_t)pays.size());  // the restored first element's new sequence
             pays.push_back(gw_handle::rd64(p + ea));
             max_end = std::max(max_end, gw_handle::rd64(p + 8));
+            if (h->fe_by) {
+                by_cols[0].push_back(gw_handle::rd64(p + 16));
+                by_cols[1].push_back(gw_handle::rd64(p));
+                by_cols[2].push_back(gw_handle::rd64(p + 24 + kb));
+            }
         }
         if (gw_handle::rd32(p) != 0) return h->fail(GW_E_INVALID, "merging window set in a first-element snapshot");
         p += 4;
@@ -3150,17 +3254,21 @@ static int fe_restore(gw_handle* h, const void* buf, int64_t len) {
         int rc = fe_log_reserve(h, m);
         if (rc) return rc;
         int64_t* d = nullptr;
-        HIPCHECK_H(h, hipMalloc((void**)&d, (size_t)m * 8));
+        HIPCHECK_H(h, hipMalloc((void**)&d, (size_t)m * 8 * h->fe_cols));
         hipError_t e = hipMemcpy(d, pays.data(), (size_t)m * 8, hipMemcpyHostToDevice);
-        if (e == hipSuccess) e = fe_log_append(h->fe_log, h->fe_log_cap, h->fe_seq, d, m, h->stream);
+        for (int c = 1; c < h->fe_cols && e == hipSuccess; ++c)
+            e = hipMemcpy(d + c * m, by_cols[c - 1].data(), (size_t)m * 8, hipMemcpyHostToDevice);
+        for (int c = 0; c < h->fe_cols && e == hipSuccess; ++c)
+            e = fe_log_append(h->fe_log + c * h->fe_log_cap, h->fe_log_cap, h->fe_seq, d + c * m, m, h->stream);
         if (e == hipSuccess) e = hipStreamSynchronize(h->stream);
         hipFree(d);
         if (e != hipSuccess) return h->fail(GW_E_DEVICE, "first-element restore: %s", hipGetErrorString(e));
         h->fe_seq += m;
+        if (h->fe_by) h->fe_restored_end = h->fe_seq;  // restored elements stand for their own window
         // released like a batch whose records reach the latest restored window: maxTs + size - 1 = its end - 1
         h->fe_batches.push_back({h->fe_seq, 0, max_end - h->cfg.size, true});
     }
-    for (int w = 0; w < 2; ++w) {
+    for (int w = 0; w < (h->fe_by ? 1 : 2); ++w) {
         std::vector<uint8_t>& pl = w ? pb : pa;
         std::vector<int64_t>& of = w ? ob : oa;
         SnapHdr kh = hd;
@@ -3676,9 +3784,11 @@ int gw_get_stats(const gw_handle* h, gw_stats* out) {
     if (!h || !out) return GW_E_INVALID;
     if (h->fe) {
         gw_get_stats(h->kids[0], out);
-        gw_stats b{};
-        gw_get_stats(h->kids[1], &b);
-        out->table_bytes += b.table_bytes;
+        if (!h->fe_by) {
+            gw_stats b{};
+            gw_get_stats(h->kids[1], &b);
+            out->table_bytes += b.table_bytes;
+        }
         out->rows_fired = h->stats.rows_fired;
         return GW_OK;
     }

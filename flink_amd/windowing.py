@@ -259,6 +259,12 @@ class GpuWindowOperator:
         self._buf_k: List[int] = []
         self._buf_t: List[int] = []
         self._buf_v: List = []
+        # payload handles (FLAG_FIRST_ELEMENT / FLAG_BY_FIELD) on the record-at-a-time surface:
+        # each element is kept on the host and its index travels as the payload
+        self._payload = bool(flags & (N.FLAG_FIRST_ELEMENT | N.FLAG_BY_FIELD))
+        self._by = bool(flags & N.FLAG_BY_FIELD)
+        self._elems: list = []
+        self._buf_p: List[int] = []
         self.output: list = []
 
     # lifecycle -------------------------------------------------------------
@@ -318,6 +324,9 @@ class GpuWindowOperator:
         self._buf_k.append(self._encode_key(self.key_selector(v)))
         self._buf_t.append(int(record.timestamp))
         self._buf_v.append(self.value_selector(v) if self.aggregate != "count" else 0)
+        if self._payload:
+            self._buf_p.append(len(self._elems))
+            self._elems.append(v)
 
     def _flush(self):
         if not self._buf_k:
@@ -330,12 +339,27 @@ class GpuWindowOperator:
             v = np.asarray(self._buf_v, dtype=np.int64)
         self._buf_k, self._buf_t, self._buf_v = [], [], []
         h = None if self._int_keys else np.asarray(self._hash_out, dtype=np.int32)[k]
-        self.process_batch(k, t, v, key_hashes=h)
+        if self._payload:
+            p = np.asarray(self._buf_p, dtype=np.int64)
+            self._buf_p = []
+            self.process_batch_payload(k, t, v, p, key_hashes=h)
+        else:
+            self.process_batch(k, t, v, key_hashes=h)
 
     def process_watermark(self, wm):
         ts = wm.timestamp if isinstance(wm, Watermark) else int(wm)
         self._flush()
         self.advance_watermark(ts)
+        if self._payload:
+            # minBy / maxBy emit the element itself (ComparableAggregator.java:88-95); positional
+            # aggregates the first element beside the result
+            k, s, e, r, pl = self.drain_payload()
+            for i in range(len(k)):
+                el = self._elems[int(pl[i])]
+                val = el if self._by else (self._decode_key(int(k[i])), int(s[i]), int(e[i]), r[i], el)
+                self.output.append(StreamRecord(val, int(e[i]) - 1))
+            self.output.append(Watermark(ts))
+            return
         k, s, e, r = self.drain()
         for i in range(len(k)):
             res = r[i]
@@ -606,10 +630,11 @@ class WindowedStream:
         self._trigger = trig
         return self
 
-    def _op(self, agg, field):
+    def _op(self, agg, field, flags=0):
+        kw = dict(self.keyed.env.op_kwargs)
+        kw["flags"] = kw.get("flags", 0) | flags
         return GpuWindowOperator(self.assigner, agg, self._lateness, self._trigger, self.keyed.key_selector,
-                                 (lambda v: v[field]) if field is not None else (lambda v: 0),
-                                 **self.keyed.env.op_kwargs)
+                                 (lambda v: v[field]) if field is not None else (lambda v: 0), **kw)
 
     # WindowedStream.sum / min / max (:660, :687, :788) on a typed field, aggregate (:310)
     def sum(self, field: int, kind: str = "i64") -> "DataStreamResult":
@@ -620,6 +645,17 @@ class WindowedStream:
 
     def max(self, field: int, kind: str = "i64") -> "DataStreamResult":
         return DataStreamResult(self, self._op(f"max_{kind}", field))
+
+    # WindowedStream.minBy / maxBy (:725-771): the element with the smallest / largest field,
+    # the first of equal ones (first=True) or the last
+    def min_by(self, field: int, first: bool = True, kind: str = "i64") -> "DataStreamResult":
+        return DataStreamResult(self, self._op(f"min_{kind}", field, N.FLAG_BY_FIELD | (0 if first else N.FLAG_BY_LAST)))
+
+    def max_by(self, field: int, first: bool = True, kind: str = "i64") -> "DataStreamResult":
+        return DataStreamResult(self, self._op(f"max_{kind}", field, N.FLAG_BY_FIELD | (0 if first else N.FLAG_BY_LAST)))
+
+    minBy = min_by
+    maxBy = max_by
 
     def aggregate(self, function: str, field: Optional[int] = None) -> "DataStreamResult":
         return DataStreamResult(self, self._op(function, field))

@@ -131,6 +131,15 @@ typedef struct gw_config {
                                         payload of its window's first element in arrival
                                         order (gw_ingest_payload*, gw_drain_payload);
                                         tumbling / sliding windows with EventTimeTrigger    */
+#define GW_FLAG_BY_FIELD       512 /* minBy / maxBy (WindowedStream.minBy(i, first) etc.,
+                                        WindowedStream.java:725-771; ComparableAggregator
+                                        byAggregate, ComparableAggregator.java:88-95): with
+                                        GW_MIN_* / GW_MAX_*, every row carries the payload of
+                                        the window's element whose field is the minimum /
+                                        maximum, the first of equal ones in arrival order
+                                        (implies GW_FLAG_FIRST_ELEMENT's payload ingest/drain) */
+#define GW_FLAG_BY_LAST       1024 /* with GW_FLAG_BY_FIELD: the last of equal ones
+                                        (minBy(i, false)); needs allowed lateness 0         */
 
 typedef struct gw_handle gw_handle;
 

@@ -21,6 +21,11 @@
  *                  tuples: the handle runs with GW_FLAG_FIRST_ELEMENT, each element's payload is
  *                  its arrival sequence, the elements wait in an ElementLog until no window can
  *                  reach them, and each row's payload picks its first element.
+ *   MIN_MAX_BY     WindowedStream.minBy/maxBy(i, first) (WindowedStream.java:725-771): the
+ *                  element itself whose field i is the window's minimum / maximum, the first of
+ *                  equal ones or the last (ComparableAggregator.java:88-95); agg is GW_MIN_* /
+ *                  GW_MAX_*, the handle runs with GW_FLAG_BY_FIELD (+ GW_FLAG_BY_LAST), payloads
+ *                  and the ElementLog as for wide POSITIONAL rows.
  *   AGGREGATE      WindowedStream.aggregate(AggregateFunction): getResult(acc) alone (Long for
  *                  count, Double for avg), PassThroughWindowFunction.
  *   KEYED_WINDOW   Tuple4 (key, window start, window end, result), what a ProcessWindowFunction
@@ -78,7 +83,7 @@ public class GpuWindowOperator<IN, K>
     static { System.loadLibrary("gpuwin_jni"); }
 
     /** What one fired (key, window, result) row becomes (see the class comment). */
-    public enum OutputMode { POSITIONAL, AGGREGATE, KEYED_WINDOW }
+    public enum OutputMode { POSITIONAL, MIN_MAX_BY, AGGREGATE, KEYED_WINDOW }
 
     // gw_assigner / gw_trigger / gw_agg codes of include/gpuwin.h
     private static final int GW_COUNT_TUMBLING = 3, GW_COUNT_SLIDING = 4;
@@ -91,6 +96,7 @@ public class GpuWindowOperator<IN, K>
     private final int batchCapacity;
     private final int inputArity, positionalField;
     private TypeSerializer<IN> inputSerializer;  // Tuple3+ positional: writes the first elements of a snapshot
+    private boolean byFirst = true;              // MIN_MAX_BY: the first of equal elements
 
     private transient long handle;
     private transient ByteBuffer keys, keyHashes, ts, values, oKey, oStart, oEnd, oRes;
@@ -116,7 +122,7 @@ public class GpuWindowOperator<IN, K>
                              int trigger, int agg, KeySelector<IN, K> keySelector,
                              ToLongFunction<IN> longValue, ToDoubleFunction<IN> doubleValue, int batchCapacity,
                              OutputMode mode, int inputArity, int positionalField) {
-        if (mode == OutputMode.POSITIONAL && inputArity > 2
+        if ((mode == OutputMode.POSITIONAL && inputArity > 2 || mode == OutputMode.MIN_MAX_BY)
                 && (assigner > 1 /* tumbling, sliding */ || trigger != 0 /* EventTimeTrigger */)) {
             throw new IllegalArgumentException(
                     "positional sum/min/max on Tuple3+ runs on tumbling / sliding event-time windows with "
@@ -134,6 +140,12 @@ public class GpuWindowOperator<IN, K>
      *  operator writes each window's first element with it when it checkpoints. */
     public GpuWindowOperator<IN, K> withInputSerializer(TypeSerializer<IN> serializer) {
         this.inputSerializer = serializer;
+        return this;
+    }
+
+    /** minBy / maxBy(i, first): false picks the last of equal elements (GW_FLAG_BY_LAST). */
+    public GpuWindowOperator<IN, K> withByFirst(boolean first) {
+        this.byFirst = first;
         return this;
     }
 
@@ -155,7 +167,8 @@ public class GpuWindowOperator<IN, K>
         int maxP = getRuntimeContext().getTaskInfo().getMaxNumberOfParallelSubtasks();
         int device = gpuIndex();
         final int flags = (lateDataTag != null ? 64 /* GW_FLAG_LATE_SIDE_OUTPUT */ : 0)
-                | (wide() ? 128 /* GW_FLAG_FIRST_ELEMENT */ : 0)
+                | (mode == OutputMode.MIN_MAX_BY ? 512 /* GW_FLAG_BY_FIELD */ | (byFirst ? 0 : 1024 /* GW_FLAG_BY_LAST */)
+                        : wide() ? 128 /* GW_FLAG_FIRST_ELEMENT */ : 0)
                 | (parallelism > 1 ? 4 /* GW_FLAG_CHECK_KEY_GROUPS: a foreign key fails the batch */ : 0);
         handle = nativeCreate(assigner, trigger, size, slide, offset, gap, lateness, agg, maxP, parallelism,
                               subtask, device, flags, 1L << 24, batchCapacity);
@@ -323,7 +336,7 @@ public class GpuWindowOperator<IN, K>
         if (++n == batchCapacity) flush();
     }
 
-    private boolean wide() { return mode == OutputMode.POSITIONAL && inputArity > 2; }
+    private boolean wide() { return mode == OutputMode.POSITIONAL && inputArity > 2 || mode == OutputMode.MIN_MAX_BY; }
 
     /** The first element with the aggregated field replaced by the result, in the field's own type. */
     private Object positionalRow(IN first, Object res) {
@@ -366,6 +379,7 @@ public class GpuWindowOperator<IN, K>
                     case POSITIONAL:
                         row = wide() ? positionalRow(elements.get(oPay.getLong(i * 8)), res) : Tuple2.of(key, res);
                         break;
+                    case MIN_MAX_BY: row = elements.get(oPay.getLong(i * 8)); break;
                     case AGGREGATE: row = res; break;
                     default: row = Tuple4.of(key, oStart.getLong(i * 8), end, res);
                 }

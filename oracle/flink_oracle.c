@@ -143,6 +143,10 @@ int wo_validate(const gw_config* c) {
     }
     if (c->allowed_lateness < 0) return GW_E_INVALID;
     if (c->agg < GW_COUNT || c->agg > GW_SUM_I32) return GW_E_INVALID;
+    if ((c->flags & GW_FLAG_BY_FIELD) && (!(c->agg == GW_MIN_I64 || c->agg == GW_MAX_I64 || c->agg == GW_MIN_F64 ||
+                                            c->agg == GW_MAX_F64) ||
+                                          !(c->assigner == GW_TUMBLING || c->assigner == GW_SLIDING)))
+        return GW_E_INVALID;
     if (c->trigger != GW_EVENT_TIME_TRIGGER && c->trigger != GW_PURGING_EVENT_TIME_TRIGGER)
         return GW_E_INVALID;
     return GW_OK;
@@ -290,7 +294,7 @@ static int map_del(map_t* m, const int64_t* k) {
 /* ------------------------------------------------------------------------ */
 /* accumulators (SumFunction / ComparableAggregator / AggregateFunction)      */
 /* ------------------------------------------------------------------------ */
-typedef struct { int64_t i; double d; int64_t c; } acc_t;
+typedef struct { int64_t i; double d; int64_t c; int64_t q; /* minBy/maxBy: the element's arrival number */ } acc_t;
 
 static inline double bits2d(int64_t b) { double d; memcpy(&d, &b, 8); return d; }
 static inline int64_t d2bits(double d) { int64_t b; memcpy(&b, &d, 8); return b; }
@@ -321,6 +325,23 @@ static void reduce_into(acc_t* a, int64_t b, int agg) {
     case GW_MAX_F64: a->d = (java_double_compare(a->d, bits2d(b)) > 0) ? a->d : bits2d(b); break;
     default: break;
     }
+}
+
+/* minBy / maxBy: ComparableAggregator.reduce, byAggregate branch (ComparableAggregator.java:
+ * 88-95) with MinByComparator / MaxByComparator (Comparator.java): c = isExtremal(v1, v2) is 1
+ * when value1's field is strictly smaller (MINBY) / larger (MAXBY), 0 when equal (Long.compareTo
+ * / Double.compareTo), else -1; c == 0 -> first ? value1 : value2; c == 1 -> value1, else value2.
+ * The state element is (field, arrival number q); WindowedStream.minBy/maxBy :725-771. */
+static void by_reduce(acc_t* a, int agg, int first, int64_t v, int64_t q) {
+    int cmp;
+    if (agg == GW_MIN_F64 || agg == GW_MAX_F64) cmp = java_double_compare(a->d, bits2d(v));
+    else cmp = a->i < v ? -1 : (a->i > v ? 1 : 0);
+    int c = (agg == GW_MIN_I64 || agg == GW_MIN_F64) ? (cmp < 0 ? 1 : cmp == 0 ? 0 : -1)
+                                                      : (cmp > 0 ? 1 : cmp == 0 ? 0 : -1);
+    if (c == 1 || (c == 0 && first)) return;
+    if (agg == GW_MIN_F64 || agg == GW_MAX_F64) a->d = bits2d(v);
+    else a->i = v;
+    a->q = q;
 }
 
 /* First element of a window: ReducingState stores the value itself
@@ -394,6 +415,8 @@ struct wo_op {
     int64_t on, ocap, ohead;
     int64_t *lk, *lt, *lv;  /* late side output (GW_FLAG_LATE_SIDE_OUTPUT): the elements themselves */
     int64_t ln, lcap;
+    int64_t cur_seq, nseq;  /* arrival number of the element being processed / of the next one */
+    int64_t* oq;            /* rows: the arrival number of the window's element (minBy / maxBy) */
     map_t cmap;   /* count windows: (key,0,0,0) -> index into cws */
     map_t khash;  /* (key,0,0,0) -> key.hashCode() of keys given a hash (wo_set_key_hashes) */
     struct cw_s* cws;
@@ -444,12 +467,16 @@ static int state_add(wo_op* op, int64_t key, int64_t s, int64_t e, int64_t v) {
     int created = 0;
     ment_t* m = map_upsert(&op->state, k, -1, &created);
     if (!m) return GW_E_OOM;
+    const int by = (op->c.flags & GW_FLAG_BY_FIELD) != 0;
     if (created) {
         int64_t a = acc_alloc(op);
         if (a < 0) return GW_E_OOM;
         m = map_find(&op->state, k);
         m->v = a;
         acc_first(&op->accs[a], op->c.agg, v);
+        op->accs[a].q = op->cur_seq;
+    } else if (by) {
+        by_reduce(&op->accs[m->v], op->c.agg, !(op->c.flags & GW_FLAG_BY_LAST), v, op->cur_seq);
     } else {
         acc_add(&op->accs[m->v], op->c.agg, v);
     }
@@ -573,13 +600,15 @@ static int emit(wo_op* op, int64_t key, int64_t s, int64_t e, const acc_t* a) {
         op->os = (int64_t*)realloc(op->os, 8 * (size_t)nc);
         op->oe = (int64_t*)realloc(op->oe, 8 * (size_t)nc);
         op->orr = (int64_t*)realloc(op->orr, 8 * (size_t)nc);
-        if (!op->ok || !op->os || !op->oe || !op->orr) return GW_E_OOM;
+        op->oq = (int64_t*)realloc(op->oq, 8 * (size_t)nc);
+        if (!op->ok || !op->os || !op->oe || !op->orr || !op->oq) return GW_E_OOM;
         op->ocap = nc;
     }
     op->ok[op->on] = key;
     op->os[op->on] = s;
     op->oe[op->on] = e;
     op->orr[op->on] = acc_result_bits(a, op->c.agg);
+    op->oq[op->on] = a->q;
     op->on++;
     return GW_OK;
 }
@@ -821,6 +850,7 @@ static int count_process_element(wo_op* op, int64_t key, int64_t v) {
 }
 
 int wo_process_element(wo_op* op, int64_t key, int64_t ts, int64_t v) {
+    op->cur_seq = op->nseq++;
     if (op->c.assigner == GW_COUNT_TUMBLING || op->c.assigner == GW_COUNT_SLIDING)
         return count_process_element(op, key, v);
     int64_t ws[64], we[64];
@@ -991,7 +1021,7 @@ void wo_destroy(wo_op* op) {
     free(op->accs);
     free(op->freel);
     free(op->heap);
-    free(op->ok); free(op->os); free(op->oe); free(op->orr);
+    free(op->ok); free(op->os); free(op->oe); free(op->orr); free(op->oq);
     free(op->lk); free(op->lt); free(op->lv);
     free(op);
 }
@@ -1010,6 +1040,10 @@ int64_t wo_drain_late(wo_op* op, int64_t* key, int64_t* ts, int64_t* v, int64_t 
 int64_t wo_output_count(const wo_op* op) { return op->on - op->ohead; }
 
 int64_t wo_drain(wo_op* op, int64_t* key, int64_t* s, int64_t* e, int64_t* r, int64_t cap) {
+    return wo_drain_seq(op, key, s, e, r, NULL, cap);
+}
+
+int64_t wo_drain_seq(wo_op* op, int64_t* key, int64_t* s, int64_t* e, int64_t* r, int64_t* q, int64_t cap) {
     int64_t n = op->on - op->ohead;
     if (n > cap) n = cap;
     for (int64_t i = 0; i < n; i++) {
@@ -1018,6 +1052,7 @@ int64_t wo_drain(wo_op* op, int64_t* key, int64_t* s, int64_t* e, int64_t* r, in
         if (s) s[i] = op->os[j];
         if (e) e[i] = op->oe[j];
         if (r) r[i] = op->orr[j];
+        if (q) q[i] = op->oq[j];
     }
     op->ohead += n;
     if (op->ohead == op->on) op->ohead = op->on = 0;
@@ -1025,6 +1060,7 @@ int64_t wo_drain(wo_op* op, int64_t* key, int64_t* s, int64_t* e, int64_t* r, in
 }
 
 int64_t wo_late_dropped(const wo_op* op) { return op->late; }
+void wo_set_arrival(wo_op* op, int64_t next) { op->nseq = next; }
 int64_t wo_current_watermark(const wo_op* op) { return op->wm; }
 int64_t wo_state_entries(const wo_op* op) { return op->state.n; }
 int64_t wo_timer_count(const wo_op* op) { return op->timers.n; }
@@ -1189,6 +1225,9 @@ int64_t wo_snapshot(wo_op* op, int32_t kg_lo, int32_t kg_hi, uint8_t* buf, int64
             wb_be64(&b, se[a].k1); wb_be64(&b, se[a].k2); wb_be64(&b, se[a].k0);
             if (hashed) wb_be32(&b, key_hash_of(op, se[a].k0));
             wb_acc(&b, op->c.agg, &op->accs[se[a].v]);
+            /* minBy / maxBy: the reduced element is the state (HeapReducingState.java:90-97); the
+             * GPU writes its payload here (flags bit 1), the oracle its arrival number */
+            if (op->c.flags & GW_FLAG_BY_FIELD) wb_be64(&b, op->accs[se[a].v].q);
         }
         wb_be32(&b, (int32_t)(q1 - q));
         for (; q < q1; q++) {
@@ -1221,7 +1260,8 @@ int64_t wo_snapshot(wo_op* op, int32_t kg_lo, int32_t kg_hi, uint8_t* buf, int64
         const uint32_t ver = 4;
         const int64_t slide = op->c.assigner == GW_TUMBLING ? op->c.size : op->c.slide;
         const int32_t i32s[2] = {op->c.agg, op->c.assigner};
-        const int64_t i64s[5] = {op->c.size, slide, op->c.offset, op->c.gap, hashed ? 1 : 0};
+        const int64_t i64s[5] = {op->c.size, slide, op->c.offset, op->c.gap,
+                                 (hashed ? 1 : 0) | ((op->c.flags & GW_FLAG_BY_FIELD) ? 2 : 0)};
         const int32_t mp = op->c.max_parallelism > 0 ? op->c.max_parallelism : 128;
         const int32_t i32b[4] = {mp, kg_lo, kg_hi, 0};
         const int64_t tail[3] = {0, 0, offs[nk]};
@@ -1259,12 +1299,14 @@ int wo_restore(wo_op* op, const uint8_t* buf, int64_t len) {
     const uint8_t* end = p + tail[2];
     const int ab = wo_acc_bytes(op->c.agg);
     const int hb = (i64s[4] & 1) ? 4 : 0;
+    const int qb = (i64s[4] & 2) ? 8 : 0; /* minBy / maxBy: the element's arrival number */
+    if (!qb != !(op->c.flags & GW_FLAG_BY_FIELD)) { op_err(op, "minBy / maxBy snapshot into another operator"); return GW_E_INVALID; }
 #define NEED(x) do { if ((int64_t)(x) > end - p) { op_err(op, "truncated snapshot blob"); return GW_E_INVALID; } } while (0)
     for (int g = 0; g < nk; g++) {
         NEED(4);
         int32_t n = rd_be32(p); p += 4;
         for (int32_t i = 0; i < n; i++) {
-            NEED(24 + hb + ab);
+            NEED(24 + hb + ab + qb);
             int64_t s = rd_be64(p), e = rd_be64(p + 8), key = rd_be64(p + 16);
             if (hb) {
                 const int32_t kh = rd_be32(p + 24);
@@ -1273,7 +1315,8 @@ int wo_restore(wo_op* op, const uint8_t* buf, int64_t len) {
             }
             acc_t a;
             rd_acc(p + 24 + hb, op->c.agg, &a);
-            p += 24 + hb + ab;
+            a.q = qb ? rd_be64(p + 24 + hb + ab) : 0;
+            p += 24 + hb + ab + qb;
             int64_t k[4] = {key, s, e, 0};
             int created = 0;
             ment_t* m = map_upsert(&op->state, k, -1, &created);

@@ -59,7 +59,14 @@ int64_t wo_output_count(const wo_op* op);
 /* Copies and removes up to cap rows. result is 8 bytes per row (int64 or double). */
 int64_t wo_drain(wo_op* op, int64_t* key, int64_t* start, int64_t* end, int64_t* result_bits,
                  int64_t cap);
+/* wo_drain plus q[i]: the arrival number (0-based over every wo_process_element call) of the
+ * element a minBy / maxBy row stands for (GW_FLAG_BY_FIELD; tumbling / sliding windows). */
+int64_t wo_drain_seq(wo_op* op, int64_t* key, int64_t* start, int64_t* end, int64_t* result_bits, int64_t* q,
+                     int64_t cap);
 int64_t wo_late_dropped(const wo_op* op);
+/* The arrival number of the next element (wo_drain_seq's q): a restored operator continues the
+ * numbering of the one that wrote the snapshot. */
+void    wo_set_arrival(wo_op* op, int64_t next);
 /* Late-data side output (config flag GW_FLAG_LATE_SIDE_OUTPUT): the skipped late elements. */
 int64_t wo_late_output_count(const wo_op* op);
 int64_t wo_drain_late(wo_op* op, int64_t* key, int64_t* ts, int64_t* value_bits, int64_t cap);

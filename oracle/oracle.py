@@ -125,6 +125,7 @@ def lib() -> ctypes.CDLL:
             ("wo_process_watermark", ctypes.c_int, [p, i64]),
             ("wo_set_key_hashes", ctypes.c_int, [p, i64, p, p]),
             ("wo_output_count", i64, [p]), ("wo_drain", i64, [p, p, p, p, p, i64]),
+            ("wo_drain_seq", i64, [p, p, p, p, p, p, i64]), ("wo_set_arrival", None, [p, i64]),
             ("wo_late_dropped", i64, [p]), ("wo_late_output_count", i64, [p]),
             ("wo_drain_late", i64, [p, p, p, p, i64]), ("wo_current_watermark", i64, [p]),
             ("wo_state_entries", i64, [p]), ("wo_timer_count", i64, [p]),
@@ -209,6 +210,18 @@ class OracleOperator:
         got = lib().wo_drain(self._h, _p(k), _p(s), _p(e), _p(r), n)
         assert got == n
         return k, s, e, r
+
+    def set_arrival(self, next_seq: int):
+        lib().wo_set_arrival(self._h, next_seq)
+
+    def drain_seq(self):
+        """drain() plus each row's element: its arrival number over every processed record
+        (minBy / maxBy with GW_FLAG_BY_FIELD; ComparableAggregator.java:88-95)."""
+        n = lib().wo_output_count(self._h)
+        k, s, e, r, q = (np.empty(n, np.int64) for _ in range(5))
+        got = lib().wo_drain_seq(self._h, _p(k), _p(s), _p(e), _p(r), _p(q), n)
+        assert got == n
+        return k, s, e, r, q
 
     def snapshot(self, key_group_range=None) -> bytes:
         """Keyed state of key groups [lo, hi] (default all) in the heap backend's per-key-group

@@ -305,4 +305,27 @@ dump("count_windows.json", {"tests": [{
     ],
 }]})
 
+# --------------------------------------------------------------------------------------
+# minBy / maxBy: AggregationFunctionTest.minMaxByTest (flink-runtime/src/test/java/org/apache/
+# flink/streaming/api/AggregationFunctionTest.java:227-345; input getInputByList :491-497).
+# Tuple3(0, i % 3, i) for i in 0..8, keyed by f0, ComparableAggregator(1, MAXBY / MINBY,
+# first) reduced by StreamGroupedReduceOperator: one output per element, the running element.
+# As windows: after element p the row of a window holding elements 0..p stands for expected[p].
+# --------------------------------------------------------------------------------------
+AFT = "flink-runtime/src/test/java/org/apache/flink/streaming/api/AggregationFunctionTest.java"
+dump("minmaxby.json", {
+    "source": AFT + ":227-345",
+    "input": [[0, i % 3, i] for i in range(9)],
+    "by_field": 1,
+    "expected": {
+        "maxBy_first": [[0, 0, 0], [0, 1, 1], [0, 2, 2], [0, 2, 2], [0, 2, 2], [0, 2, 2], [0, 2, 2], [0, 2, 2],
+                        [0, 2, 2]],
+        "maxBy_last": [[0, 0, 0], [0, 1, 1], [0, 2, 2], [0, 2, 2], [0, 2, 2], [0, 2, 5], [0, 2, 5], [0, 2, 5],
+                       [0, 2, 8]],
+        "minBy_first": [[0, 0, 0]] * 9,
+        "minBy_last": [[0, 0, 0], [0, 0, 0], [0, 0, 0], [0, 0, 3], [0, 0, 3], [0, 0, 3], [0, 0, 6], [0, 0, 6],
+                       [0, 0, 6]],
+    },
+})
+
 print("golden vectors written to", HERE)
