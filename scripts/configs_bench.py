@@ -18,6 +18,8 @@ the host cores over a bounded prefix of the same stream.  One JSON line per conf
   q7_first   the same stream as a positional max(2) on Tuple3<auction, bidder, price>: rows
              carry the window's first bid's bidder (GW_FLAG_FIRST_ELEMENT; no CPU baseline,
              the oracle has no first-element rows)
+  q7_maxby   the same stream as maxBy(2) on Tuple3<auction, bidder, price>: rows carry the
+             highest bid itself, the first of equal prices (GW_FLAG_BY_FIELD)
   sessions   event-time sessions, gap 10 s, avg(f64) over 12.5M keys (one GPU's share of
              100M keys on 8 GPUs); keys come in four groups, each active 5 s out of 20 s, so
              sessions close and fire
@@ -42,7 +44,7 @@ def gen(name, nb, steps, dev):
     """Returns (assigner kwargs, agg, keys, ts, vals, watermarks)."""
     n = nb * steps
     idx = torch.arange(n, device=dev, dtype=torch.int64)
-    r = splitmix64(idx, 0x5EED0000 + {"wordcount": 1, "ysb": 2, "q7": 7, "q7_first": 7, "sessions": 5}[name]) & MASK63
+    r = splitmix64(idx, 0x5EED0000 + {"wordcount": 1, "ysb": 2, "q7": 7, "q7_first": 7, "q7_maxby": 7, "sessions": 5}[name]) & MASK63
     if name == "wordcount":
         rng = np.random.default_rng(7)
         vocab = 50_000
@@ -67,7 +69,7 @@ def gen(name, nb, steps, dev):
         campaigns = splitmix64(torch.arange(100, device=dev, dtype=torch.int64), 0xCA11) & MASK63
         ad_campaign = campaigns.repeat_interleave(10)  # ad i belongs to campaign i // 10
         return dict(assigner="tumbling", size=10_000), "count", (ad, etype, ad_campaign), ts, None, wms
-    if name in ("q7", "q7_first"):
+    if name in ("q7", "q7_first", "q7_maxby"):
         keys = r % 10_000_000
         base = idx * 200 // nb
         ts = base - (splitmix64(idx, 78) & MASK63) % 101
@@ -88,18 +90,19 @@ def gen(name, nb, steps, dev):
 
 def run(name, args, dev):
     nb = {"wordcount": 2_000_000, "ysb": 20_000_000, "q7": 10_000_000, "q7_first": 10_000_000,
-          "sessions": 10_000_000}[name]
-    n_timed = args.steps or {"wordcount": 10, "ysb": 60, "q7": 60, "q7_first": 60, "sessions": 100}[name]
+          "q7_maxby": 10_000_000, "sessions": 10_000_000}[name]
+    n_timed = args.steps or {"wordcount": 10, "ysb": 60, "q7": 60, "q7_first": 60, "q7_maxby": 60, "sessions": 100}[name]
     steps = args.warmup + n_timed
     kw, agg, keys, ts, vals, wms = gen(name, nb, steps, dev)
     torch.cuda.synchronize()
     assigner = {"tumbling": lambda: W.TumblingEventTimeWindows.of(kw["size"]),
                 "session": lambda: W.EventTimeSessionWindows.with_gap(kw["gap"]),
                 "count_sliding": lambda: W.CountWindows.of(kw["size"], kw["slide"])}[kw["assigner"]]()
-    cap = {"wordcount": 1 << 16, "ysb": 1024, "q7": 10_000_000, "q7_first": 10_000_000, "sessions": 12_500_000}[name]
-    first = name == "q7_first"
+    cap = {"wordcount": 1 << 16, "ysb": 1024, "q7": 10_000_000, "q7_first": 10_000_000, "q7_maxby": 10_000_000,
+           "sessions": 12_500_000}[name]
+    first = name in ("q7_first", "q7_maxby")
     op = W.GpuWindowOperator(assigner, agg, capacity_hint=cap, max_batch=nb * 2,
-                             flags=N.FLAG_FIRST_ELEMENT if first else 0).open()
+                             flags=(N.FLAG_BY_FIELD if name == "q7_maxby" else N.FLAG_FIRST_ELEMENT) if first else 0).open()
     payload = (splitmix64(torch.arange(keys.numel(), device=dev, dtype=torch.int64), 82) & MASK63) if first else None
     rows = 0
     op_events = 0
@@ -156,7 +159,9 @@ def run(name, args, dev):
     if ysb:
         out["pipeline"] = "filter(event_type == view) + join(ad_id -> campaign_id) on the GPU, then the operator"
     if first:
-        out["note"] = "rows carry the first element's payload (two pane operators + payload log + join)"
+        out["note"] = ("rows carry the highest bid's payload (one MAX pane operator + 4-column log + per-fire probe)"
+                       if name == "q7_maxby" else
+                       "rows carry the first element's payload (two pane operators + payload log + join)")
     if not args.no_cpu_baseline and not first:
         if ysb:  # the oracle times the window operator on the filtered, joined stream
             ad, etype, ad_campaign = keys
