@@ -959,6 +959,9 @@ constexpr int kApplyRuns = 256;  // run descriptors staged in LDS per step (<= b
 constexpr int kApplyGroup = GW_APPLY_GROUP;   // consecutive runs a wave walks as one sequence
 constexpr int kApplyUnroll = GW_APPLY_UNROLL;  // records per lane with their loads in flight together
 constexpr int kApplyQ = 128;                   // per-wave queue of records that missed their home group
+#ifndef GW_APPLY_FAST2
+#define GW_APPLY_FAST2 0
+#endif
 
 template <int AGG, int FMT>
 __global__ void __launch_bounds__(kApplyThreads) GW_APPLY_ATTR k_rgn_apply(IngestArgs a) {
@@ -1261,6 +1264,29 @@ __global__ void __launch_bounds__(kApplyThreads) GW_APPLY_ATTR k_rgn_apply(Inges
                 ka[q] = *reinterpret_cast<const long2*>(&lkeys[g[q]]);
                 kb[q] = *reinterpret_cast<const long2*>(&lkeys[g[q] + 2]);
             }
+#if GW_APPLY_FAST2
+            // a key displaced past its full home group is most often in the next group: read
+            // it too (only where some lane needs it) before falling back to the queue
+#pragma unroll
+            for (int q = 0; q < kApplyUnroll; ++q) {
+                const long long key = (long long)h[q];
+                const bool hit = ka[q].x == key || ka[q].y == key || kb[q].x == key || kb[q].y == key;
+                const bool full = ka[q].x != kEmptyH && ka[q].y != kEmptyH && kb[q].x != kEmptyH && kb[q].y != kEmptyH;
+                const bool nxt = c.ok[q] && !hit && full;
+                if (__any(nxt)) {
+                    if (nxt) {
+                        const int g2 = (g[q] + kProbeGroup) & ((int)S - 1);
+                        const long2 na = *reinterpret_cast<const long2*>(&lkeys[g2]);
+                        const long2 nb = *reinterpret_cast<const long2*>(&lkeys[g2 + 2]);
+                        if (na.x == key || na.y == key || nb.x == key || nb.y == key) {
+                            g[q] = g2;
+                            ka[q] = na;
+                            kb[q] = nb;
+                        }
+                    }
+                }
+            }
+#endif
 #pragma unroll
             for (int q = 0; q < kApplyUnroll; ++q) {
                 bool fast = false;

@@ -32,6 +32,21 @@
 
 #include <rocprim/device/device_radix_sort.hpp>
 
+// The slot sort's rocPRIM configuration: the library's gfx950 default (8 bits per onesweep
+// pass), or GW_SESS_RADIX_BITS bits per pass (fewer passes over the slot bits).
+#ifndef GW_SESS_RADIX_BITS
+#define GW_SESS_RADIX_BITS 0
+#endif
+#if GW_SESS_RADIX_BITS
+using SlotSortConfig = rocprim::radix_sort_config<
+    rocprim::default_config, rocprim::default_config,
+    rocprim::radix_sort_onesweep_config<rocprim::kernel_config<1024, 8>, rocprim::kernel_config<1024, 8>,
+                                        GW_SESS_RADIX_BITS, rocprim::block_radix_rank_algorithm::match>>;
+#else
+using SlotSortConfig = rocprim::default_config;
+#endif
+
+
 namespace gw {
 
 constexpr int kLaneSess = 3;        // sessions a thread replays in LDS
@@ -1976,7 +1991,7 @@ static int ensure_bufs(SessionState* s, int64_t n, std::string& err) {
     if (!s->count_mode) SCHECK(hipMalloc((void**)&s->rec, (size_t)c * 16));
     rocprim::double_buffer<uint32_t> kb(s->slot[0], s->slot[1]), vb(s->perm[0], s->perm[1]);
     size_t bytes = 0;
-    SCHECK(rocprim::radix_sort_pairs(nullptr, bytes, kb, vb, (size_t)c, 0, 32, s->stream));
+    SCHECK(rocprim::radix_sort_pairs<SlotSortConfig>(nullptr, bytes, kb, vb, (size_t)c, 0, 32, s->stream));
     SCHECK(hipMalloc(&s->sort_tmp, bytes));
     s->sort_tmp_bytes = bytes;
     s->buf_cap = c;
@@ -1999,7 +2014,7 @@ static int sort_by_slot(SessionState* s, int64_t n, int64_t cap, const uint32_t*
     s->gshift = s->count_mode ? 0 : std::min(4, std::max(0, bits - sort_bits));
     rocprim::double_buffer<uint32_t> kb(s->slot[0], s->slot[1]), vb(s->perm[0], s->perm[1]);
     size_t bytes = s->sort_tmp_bytes;
-    SCHECK(rocprim::radix_sort_pairs(s->sort_tmp, bytes, kb, vb, (size_t)n, s->gshift, bits, s->stream));
+    SCHECK(rocprim::radix_sort_pairs<SlotSortConfig>(s->sort_tmp, bytes, kb, vb, (size_t)n, s->gshift, bits, s->stream));
     *sk = kb.current();
     *sp = vb.current();
     return GW_OK;
