@@ -37,10 +37,13 @@
 #ifndef GW_SESS_RADIX_BITS
 #define GW_SESS_RADIX_BITS 0
 #endif
+#ifndef GW_SESS_SORT_ITEMS
+#define GW_SESS_SORT_ITEMS 8
+#endif
 #if GW_SESS_RADIX_BITS
 using SlotSortConfig = rocprim::radix_sort_config<
     rocprim::default_config, rocprim::default_config,
-    rocprim::radix_sort_onesweep_config<rocprim::kernel_config<1024, 8>, rocprim::kernel_config<1024, 8>,
+    rocprim::radix_sort_onesweep_config<rocprim::kernel_config<1024, 8>, rocprim::kernel_config<1024, GW_SESS_SORT_ITEMS>,
                                         GW_SESS_RADIX_BITS, rocprim::block_radix_rank_algorithm::match>>;
 #else
 using SlotSortConfig = rocprim::default_config;
