@@ -32,10 +32,12 @@
 
 #include <rocprim/device/device_radix_sort.hpp>
 
-// The slot sort's rocPRIM configuration: the library's gfx950 default (8 bits per onesweep
-// pass), or GW_SESS_RADIX_BITS bits per pass (fewer passes over the slot bits).
+// The slot sort's rocPRIM configuration: 9 bits per onesweep pass, so 12.5M keys' 26 slot
+// bits take 3 passes instead of the library default's 4 at 8 bits (sessions config 7.4 ->
+// 8.5 G events/s; 10 and 11 bits measured slower, profiles/r3/experiments.txt).
+// GW_SESS_RADIX_BITS=0 builds the library default.
 #ifndef GW_SESS_RADIX_BITS
-#define GW_SESS_RADIX_BITS 0
+#define GW_SESS_RADIX_BITS 9
 #endif
 #ifndef GW_SESS_SORT_ITEMS
 #define GW_SESS_SORT_ITEMS 8
