@@ -181,7 +181,10 @@ __device__ __forceinline__ int64_t find_or_insert(const TableView& t, int64_t ke
     uint64_t idx = slot_hash(key) & mask;
     for (int p = 0; p < kMaxProbe; ++p) {
         int64_t* s = slot_ptr(t, (int64_t)idx);
-        int64_t k = *(volatile int64_t*)s;  // a stale kEmptyKey is resolved by the CAS
+        // a plain (cached) load: a key word only ever goes from kEmptyKey to a key, so a stale
+        // read can only be kEmptyKey, which the CAS resolves (a volatile load here is a
+        // system-scope sc0 sc1 load that skips the caches on every probe)
+        const int64_t k = s[0];
         if (k == key) return (int64_t)idx;
         if (k == kEmptyKey) {
             unsigned long long prev = atomicCAS((unsigned long long*)s, (unsigned long long)kEmptyKey,

@@ -67,7 +67,7 @@ __device__ __forceinline__ bool mask_set_bit(uint8_t* m, int64_t j, int shift, u
     const uint64_t bit = ((uint64_t)j << (shift + 3)) + pos;
     uint32_t* w = (uint32_t*)m + (bit >> 5);
     const uint32_t b = 1u << (bit & 31);
-    if (*(volatile uint32_t*)w & b) return false;
+    if (*w & b) return false;  // bits only get set: a stale read is a clear bit, which the OR resolves
     return !(atomicOr(w, b) & b);
 }
 __device__ __forceinline__ uint64_t pt_mask_get(const PaneTable& t, int64_t g) {
@@ -101,7 +101,7 @@ __device__ __forceinline__ int64_t pt_find_or_insert(const PaneTable& t, int64_t
     const int lim = S < kMaxProbe ? (int)S : kMaxProbe;
     for (int p = 0; p < lim; ++p) {
         int64_t* kp = keys + j;
-        const int64_t k = *(volatile int64_t*)kp;
+        const int64_t k = *kp;  // stale only as kEmptyKey (find_or_insert)
         if (k == key) return (r << t.log2S) + j;
         if (k == kEmptyKey) {
             const unsigned long long prev = atomicCAS((unsigned long long*)kp, (unsigned long long)kEmptyKey,

@@ -188,7 +188,7 @@ __device__ __forceinline__ int64_t pt_probe_from(const PaneTable& t, int64_t key
     const int lim = S < kMaxProbe ? (int)S : kMaxProbe;
     for (int p = 0; p < lim; ++p) {
         int64_t* kp = keys + j;
-        if (p) k = *(volatile int64_t*)kp;
+        if (p) k = *kp;
         if (k == key) return (r << t.log2S) + j;
         if (k == kEmptyKey) {
             const unsigned long long prev = atomicCAS((unsigned long long*)kp, (unsigned long long)kEmptyKey,
@@ -229,7 +229,7 @@ __global__ void __launch_bounds__(256) k_ingest(IngestArgs a) {
             reg[u] = pt_key_region(a.t, h);
             home[u] = pt_home(a.t, h);
             k0[u] = (state[u] == REC_RING && key[u] != kEmptyKey)
-                        ? *(volatile int64_t*)(pt_region(a.t, reg[u]) + home[u])
+                        ? *(pt_region(a.t, reg[u]) + home[u])
                         : 0;
         }
 #pragma unroll
