@@ -295,8 +295,10 @@ __device__ __forceinline__ void seg_slot(const SegArgs& a, const SessList& l, in
             const int64_t* x = sp + 2 + q * SW;
             sl_put(l, q, Sess{x[0], x[1], x[2], SW == 4 ? x[3] : 0, (int64_t)slot_fired(w1, q)});
         }
+        // whole-slot groups (gshift 0): every record of [i, j) is the slot's, no slot re-read
         for (int64_t r = i; r < j && ok; ++r)
-            if (a.slot[r] == slot) ok = add_element<AGG>(a, l, cnt, kLaneSess, key, a.perm[r], late, merges, flags, dry);
+            if (a.gshift == 0 || a.slot[r] == slot)
+                ok = add_element<AGG>(a, l, cnt, kLaneSess, key, a.perm[r], late, merges, flags, dry);
         if (!ok || !dry || !effects) break;
         dry = false;
         late = l0;
