@@ -2,7 +2,7 @@
 # Host-side AddressSanitizer run of libgpuwin's CPU-only entry points (no GPU needed; runs here).
 # gw_runtime.cpp is rebuilt with ASan on the host side only (-Xarch_host), linked with the
 # in-tree kernel objects into /tmp/gw_asan/libgpuwin.so, and the CPU tests that reach host
-# parsers (snapshot slicing / key remap on damaged blobs, ABI exports, netbuf host decode)
+# parsers (snapshot slicing / key remap on damaged blobs, ABI exports, reference snapshot keys)
 # run against it through GW_LIB_PATH with the clang ASan runtime preloaded.
 set -eu
 cd "$(dirname "$0")/.."
@@ -17,4 +17,4 @@ OBJS=$(ls flink_amd/_build/*.o | grep -v gw_runtime.cpp.o)
 $ROCM/bin/hipcc --offload-arch=gfx950 -shared -fPIC -shared-libasan -fsanitize=address -o $D/libgpuwin.so \
   $D/gw_runtime.o $OBJS -L$ROCM/lib -lrccl -Wl,-rpath,$ROCM/lib
 GW_LIB_PATH=$D/libgpuwin.so LD_PRELOAD=$ASAN_RT ASAN_OPTIONS=detect_leaks=0:abort_on_error=1 \
-  python -m pytest -q -p no:cacheprovider tests/test_snapshot_fuzz.py tests/test_snapshot_slice.py tests/test_abi.py "$@"
+  python -m pytest -q -p no:cacheprovider tests/test_snapshot_fuzz.py tests/test_snapshot_slice.py tests/test_abi.py tests/test_refsnap_oracle.py "$@"
