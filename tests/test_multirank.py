@@ -1,4 +1,4 @@
-"""World-size-2/4 CPU tests (gloo) of the N>1 path: keyBy exchange by key group
+"""World-size-2/3/4 CPU tests (gloo) of the N>1 path: keyBy exchange by key group
 (KeyByExchange.exchange_partitioned + combine_watermark), one operator per rank owning
 its key groups; the union of the ranks' fired rows must equal a single operator's
 (results independent of parallelism)."""
@@ -26,7 +26,7 @@ def test_numpy_routing_matches_library(oracle_lib):
         assert own[i] == O.wo_operator_index_for_key_group(128, 4, kg)
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 3, 4])  # 3: uneven key-group ranges (128 / 3)
 @pytest.mark.parametrize("cfg", [dict(assigner="sliding", size=1000, slide=250, agg="sum_i64"),
                                  dict(assigner="session", gap=100, agg="count")],
                          ids=["sliding", "session"])
