@@ -85,3 +85,17 @@ def test_create_fails_cleanly_without_gpu():
     op = W.GpuWindowOperator(W.TumblingEventTimeWindows.of(1000), "sum_i64")
     with pytest.raises(N.GpuWinError):
         op.open()
+
+
+def test_missing_library_fails_loudly(tmp_path):
+    """No CPU fallback: with the library absent, the product path raises NativeLibraryError
+    at the first use (a fresh process, so this one's loaded library is not involved)."""
+    import subprocess
+    import sys
+    code = ("from flink_amd import _native as N\n"
+            "from flink_amd import windowing as W\n"
+            "try:\n    N.lib()\nexcept N.NativeLibraryError as e:\n    print('raised', 'no CPU fallback' in str(e))\n")
+    env = dict(os.environ, GW_LIB_PATH=str(tmp_path / "libgpuwin.so"))
+    r = subprocess.run([sys.executable, "-c", code], cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.strip() == "raised True"
