@@ -1686,7 +1686,8 @@ struct gw_handle {
         const size_t first = ov_pending.size();
         std::vector<int64_t> hkeys;  // (key, hash) of a hashed blob's entries
         std::vector<int32_t> hvals;
-#define NEED(x) do { if ((int64_t)(x) > end - p) return fail(GW_E_INVALID, "truncated snapshot blob"); } while (0)
+        // a blob rejected part-way leaves the handle as it was (the entries parsed so far go)
+#define NEED(x) do { if ((int64_t)(x) > end - p) { ov_pending.resize(first); return fail(GW_E_INVALID, "truncated snapshot blob"); } } while (0)
         for (int64_t g = 0; g < nk; ++g) {
             NEED(4);
             const int32_t ns = rd32(p); p += 4;
@@ -1695,9 +1696,11 @@ struct gw_handle {
                 NEED(24 + hb + ab);
                 const int64_t s0 = rd64(p), e0 = rd64(p + 8), key = rd64(p + 16);
                 const i128 k = floor_div((i128)s0 - cfg.offset, (i128)slide());
-                if (win_start(k) != (i128)s0 || (i128)s0 + size() != (i128)e0)
+                if (win_start(k) != (i128)s0 || (i128)s0 + size() != (i128)e0) {
+                    ov_pending.resize(first);
                     return fail(GW_E_INVALID, "snapshot window [%lld, %lld) is not a window of this assigner",
                                 (long long)s0, (long long)e0);
+                }
                 OvEntry e{key, (int64_t)k, 0, 0, 0};
                 if (hb) {
                     hkeys.push_back(key);
@@ -1708,7 +1711,10 @@ struct gw_handle {
                 p += 24 + hb + ab;
             }
             NEED(4);
-            if (rd32(p) != 0) return fail(GW_E_INVALID, "merging window set in a tumbling / sliding snapshot");
+            if (rd32(p) != 0) {
+                ov_pending.resize(first);
+                return fail(GW_E_INVALID, "merging window set in a tumbling / sliding snapshot");
+            }
             p += 4;
             NEED(4);
             const int32_t nt = rd32(p); p += 4;

@@ -243,3 +243,44 @@ def test_region_path_restore_q5_shape(oracle_lib):
     g, glate, _ = resume("gpu", o, kw, blob, keys, ts, vals, batches[6:], old)
     r, rlate, _ = resume("oracle", o, kw, blob, keys, ts, vals, batches[6:], old)
     assert compare(g, r, False) == []
+
+
+def test_rejected_blob_leaves_the_handle_unchanged(oracle_lib):
+    """A blob that fails part-way through (a bad window in its LAST non-empty key group, after
+    the earlier groups parsed) raises GW_E_INVALID and leaves nothing behind: the good blob
+    restored next continues exactly like the oracle restored from it alone (no duplicated
+    windows from the rejected attempt)."""
+    import struct
+    o = oracle_lib
+    kw = dict(assigner="sliding", size=1000, slide=250, agg="sum_i64")
+    keys, ts, vals, batches = stream(21, "sum_i64")
+    cut = 5
+    src = o.OracleOperator(o.make_config(**kw))
+    feed_oracle(src, keys, ts, vals, batches[:cut], [])
+    good = src.snapshot()
+    src.close()
+    kg_lo, kg_hi = struct.unpack_from("<ii", good, 60)
+    nk = kg_hi - kg_lo + 1
+    offs = np.frombuffer(good[96:96 + 8 * (nk + 1)], np.int64)
+    pay0 = 96 + 8 * (nk + 1)
+    last = max(g for g in range(nk) if offs[g + 1] - offs[g] > 40)
+    assert last > 0
+    bad = bytearray(good)
+    bad[pay0 + int(offs[last]) + 4 + 7] ^= 1  # first entry's window start, low byte
+    g = gpu_operator(kw, capacity_hint=4096)
+    with pytest.raises(N.GpuWinError) as ei:
+        g.initialize_state(bytes(bad))
+    assert ei.value.code == -1  # GW_E_INVALID
+    g.initialize_state(good)
+    ora = o.OracleOperator(o.make_config(**kw))
+    ora.restore(good)
+    go, oo = [], []
+    feed_gpu(g, keys, ts, vals, batches[cut:], go)
+    feed_oracle(ora, keys, ts, vals, batches[cut:], oo)
+    g.advance_watermark(W.LONG_MAX)
+    drain(g, go)
+    ora.process_watermark(W.LONG_MAX)
+    oo.append(ora.drain())
+    assert compare(go, oo, False) == []
+    g.close()
+    ora.close()
