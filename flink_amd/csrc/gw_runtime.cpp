@@ -3054,6 +3054,8 @@ static int comp_restore(gw_handle* h, const void* buf, int64_t len) {
         }
     }
     if (p != end) return h->fail(GW_E_INVALID, "snapshot blob has trailing bytes");
+    std::vector<size_t> had(J);  // a class rejecting its part undoes the classes restored before it
+    for (int64_t j = 0; j < J; ++j) had[j] = h->kids[j]->ov_pending.size();
     for (int64_t j = 0; j < J; ++j) {
         offs[j][nk] = (int64_t)pay[j].size();
         SnapHdr kh = hd;
@@ -3066,7 +3068,10 @@ static int comp_restore(gw_handle* h, const void* buf, int64_t len) {
         memcpy(blob.data() + sizeof kh, offs[j].data(), (size_t)(nk + 1) * 8);
         if (!pay[j].empty()) memcpy(blob.data() + sizeof kh + (nk + 1) * 8, pay[j].data(), pay[j].size());
         const int rc = gw_restore(h->kids[j], blob.data(), (int64_t)blob.size());
-        if (rc) return kid_rc(h, h->kids[j], rc);
+        if (rc) {
+            for (int64_t q = 0; q < j; ++q) h->kids[q]->ov_pending.resize(had[q]);
+            return kid_rc(h, h->kids[j], rc);
+        }
     }
     return GW_OK;
 }

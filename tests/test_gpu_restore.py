@@ -245,14 +245,17 @@ def test_region_path_restore_q5_shape(oracle_lib):
     assert compare(g, r, False) == []
 
 
-def test_rejected_blob_leaves_the_handle_unchanged(oracle_lib):
+@pytest.mark.parametrize("kw", [dict(assigner="sliding", size=1000, slide=250, agg="sum_i64"),
+                                dict(assigner="sliding", size=1000, slide=10, agg="sum_i64")],  # 2 window classes
+                         ids=["one-table", "window-classes"])
+def test_rejected_blob_leaves_the_handle_unchanged(oracle_lib, kw):
     """A blob that fails part-way through (a bad window in its LAST non-empty key group, after
     the earlier groups parsed) raises GW_E_INVALID and leaves nothing behind: the good blob
     restored next continues exactly like the oracle restored from it alone (no duplicated
-    windows from the rejected attempt)."""
+    windows from the rejected attempt) -- also when the handle splits its windows into classes
+    and a later class rejects its part after earlier classes restored theirs."""
     import struct
     o = oracle_lib
-    kw = dict(assigner="sliding", size=1000, slide=250, agg="sum_i64")
     keys, ts, vals, batches = stream(21, "sum_i64")
     cut = 5
     src = o.OracleOperator(o.make_config(**kw))
