@@ -52,7 +52,7 @@ def log(msg):
     print(f"[bench] {msg}", file=sys.stderr, flush=True)
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
@@ -65,50 +65,131 @@ def parse():
     ap.add_argument("--wm-interval-ms", type=int, default=200)
     ap.add_argument("--disorder-ms", type=int, default=100)
     ap.add_argument("--exchange", choices=["a2a", "none"], default="a2a",
-                    help="a2a: RCCL all-to-all keyBy exchange; none: each rank generates only its own key groups")
+                    help="a2a: libgpuwin's RCCL keyBy exchange (gw_exchange_*); none: each rank generates "
+                         "records of its own key groups only")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=20.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-host-fed", action="store_true",
                     help="skip the host-fed leg (gw_ingest from host columns: pinned staging + H2D)")
-    ap.add_argument("--host-fed-steps", type=int, default=4)
+    ap.add_argument("--host-fed-steps", type=int, default=6)
     ap.add_argument("--preagg", choices=["auto", "force", "off"], default="auto")
-    ap.add_argument("--producer-stream", choices=["auto", "torch", "handle"], default="auto",
-                    help="stream gw_ingest_device orders after: the exchange output's (torch) stream, or, "
-                         "for columns generated and synchronised before the clock starts, none (handle)")
-    ap.add_argument("--torch-stream", choices=["side", "default"], default="side",
-                    help="stream the step's torch work (exchange) runs on")
     ap.add_argument("--no-kernel-timing", action="store_true",
                     help="no HIP events around the kernels (the roofline fields are then null)")
-    ap.add_argument("--overlap", choices=["on", "off"], default="on",
-                    help="on: double-buffered receive columns, so batch b+1's partition and all-to-all "
-                         "run while the operator still aggregates batch b; off: every step ordered "
-                         "after the previous ingest's reads")
     ap.add_argument("--checksum", action="store_true",
-                    help="drain the fired rows to the host and report an order-independent checksum "
-                         "(key, start, end, result) summed over ranks (a check, not a bench setting)")
-    ap.add_argument("--dist-backend", choices=["nccl", "gloo"], default="nccl",
-                    help="nccl = RCCL over xGMI; gloo = host-staged rehearsal (several ranks may share one GPU)")
-    return ap.parse_args()
+                    help="drain the fired rows of every step to the host and report the oracle's "
+                         "order-independent row checksum (oracle.rows_hash_sum) summed over steps and ranks "
+                         "(a check, not a bench setting)")
+    ap.add_argument("--oracle-check", action="store_true",
+                    help="with --checksum at N=1: also run the CPU oracle over the same stream and report "
+                         "per-watermark agreement (short runs only: the oracle does ~1-2M events/s)")
+    return ap.parse_args(argv)
 
 
-def main():
-    args = parse()
+def make_stream(nb, steps_total, K, E, slide, disorder, agg, dev, rank=0, world=1, key_partitioned=False,
+                maxp=128):
+    """The bench's synthetic Nexmark-Q5 bids in HBM: steps_total watermark batches of nb
+    events.  auction = splitmix64(i) mod K (uniform), ts advancing so each `slide` of event
+    time holds E events with jitter <= disorder, value = splitmix64(i') mod 1e6.  With
+    key_partitioned (N > 1, no exchange) the keys are drawn from this rank's key groups only
+    (KeyGroupRangeAssignment.computeKeyGroupRangeForOperatorIndex), so every rank keeps the
+    same nb, timestamps and watermarks.  Returns (keys, ts, vals or None, wms): the watermark
+    after batch b is BoundedOutOfOrdernessWatermarks' maxTs - bound - 1 over the un-jittered
+    maximum, identical on every rank."""
+    from flink_amd import _native as N
+    n_all = nb * steps_total
+    idx = torch.arange(n_all, device=dev, dtype=torch.int64)
+    seed = 0x5EED0005 + 7919 * rank
+    draw = splitmix64(idx, seed) & MASK63
+    if key_partitioned and world > 1:
+        allk = torch.arange(K, device=dev, dtype=torch.int64)
+        kg = torch.empty(K, dtype=torch.int32, device=dev)
+        owner = torch.empty_like(kg)
+        N.check(N.lib().gw_key_groups_device(K, allk.data_ptr(), None, maxp, world, kg.data_ptr(),
+                                             owner.data_ptr(), None))
+        torch.cuda.synchronize()
+        own = allk[owner == rank]
+        keys = own[draw % own.numel()]
+        del allk, kg, owner, own
+    else:
+        keys = draw % K
+    del draw
+    t0_ms = 1_700_000_000_000
+    jitter = (splitmix64(idx, seed ^ 0x77) & MASK63) % (disorder + 1)
+    ts = t0_ms + (idx * slide) // E - jitter
+    vals = None
+    if agg != "count":
+        v = (splitmix64(idx, seed ^ 0x1234) & MASK63) % 1_000_000
+        vals = v.to(torch.float64).view(torch.int64) if agg.endswith("f64") else v
+    del idx, jitter
+    wms = [t0_ms + (((b + 1) * nb - 1) * slide) // E - disorder - 1 for b in range(steps_total)]
+    torch.cuda.synchronize()
+    return keys, ts, vals, wms
+
+
+def make_operator(W, N, args, K, world=1, rank=0, local=0, nb=None):
+    """The bench's operator: one GpuWindowOperator subtask over this rank's key groups."""
+    flags = {"auto": 0, "force": N.FLAG_FORCE_LDS_PREAGG, "off": N.FLAG_NO_LDS_PREAGG}[args.preagg]
+    return W.GpuWindowOperator(W.SlidingEventTimeWindows.of(args.size_ms, args.slide_ms), args.agg,
+                               capacity_hint=max(K // world, 1024), max_parallelism=128, parallelism=world,
+                               operator_index=rank, device=local, flags=flags, max_batch=nb * 2).open()
+
+
+class Steps:
+    """One step = one watermark batch: (N > 1: gw_exchange_batch = partition + one all-to-all of
+    (count, watermark, columns) + grouped send/receive) -> gw_ingest_device ->
+    gw_advance_watermark (fires every 10th step) -> fired rows consumed.  With `collect` the
+    rows of every watermark are drained to the host and (count, checksum) recorded."""
+
+    def __init__(self, op, N, keys, ts, vals, wms, nb, ex=None, collect=False, ex_stream=None):
+        self.op, self.N, self.ex, self.ex_stream = op, N, ex, ex_stream
+        self.keys, self.ts, self.vals, self.wms, self.nb = keys, ts, vals, wms, nb
+        self.collect = collect
+        self.per_wm = []  # (rows, checksum) per watermark when collecting
+        self.exch_bytes = 0
+
+    def step(self, b, timed=False, b_in=24, rank=0):
+        op, nb = self.op, self.nb
+        lo, hi = b * nb, (b + 1) * nb
+        k, t = self.keys[lo:hi], self.ts[lo:hi]
+        v = self.vals[lo:hi] if self.vals is not None else None
+        if self.ex is not None:
+            # the native exchange on a stream of its own; the ingest orders through the receive
+            # set's hand-off stream, so batch b+1's partition and transfers overlap batch b's
+            # aggregation on the operator's stream
+            n, pk, pt, pv, _, wmin, ist = self.ex.exchange(k, t, v, stream=self.ex_stream, wm=self.wms[b])
+            if timed:
+                self.exch_bytes += (nb - int(self.ex.counts()[0][rank])) * b_in
+            self.N.check(self.N.lib().gw_ingest_device(op.handle, n, pk, None, pt, pv, ist), op.handle)
+            op.advance_watermark(wmin)
+        else:
+            # columns generated and synchronised before the clock: no producer ordering needed
+            self.N.check(self.N.lib().gw_ingest_device(op.handle, nb, k.data_ptr(), None, t.data_ptr(),
+                                                       v.data_ptr() if v is not None else None, op.stream()),
+                         op.handle)
+            op.advance_watermark(self.wms[b])
+        self.consume()
+
+    def consume(self):
+        if self.collect:
+            rows = self.op.drain()
+            self.per_wm.append((len(rows[0]), rows_checksum(rows)))
+        else:
+            self.op.clear_rows()  # DiscardingSink
+
+
+def main(argv=None):
+    args = parse(argv)
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        if world == 1 and args.gpus > 1:
-            raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run (one rank per GPU)")
-    local = local % max(torch.cuda.device_count(), 1)  # rehearsal: ranks may share a GPU
+    if world != args.gpus and world == 1 and args.gpus > 1:
+        raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run (one rank per GPU)")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        if args.dist_backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
-        else:
-            dist.init_process_group("gloo")
+        dist.init_process_group("nccl", device_id=dev)
 
     from flink_amd import _native as N
     from flink_amd import windowing as W
@@ -123,133 +204,26 @@ def main():
     b_in = 16 if agg == "count" else 24
     s_acc = 16 if agg.startswith("avg") else 8
 
-    # ------------------------------------------------------------------ data
     t_gen = time.time()
-    n_all = nb * steps_total
-    idx = torch.arange(n_all, device=dev, dtype=torch.int64)
-    seed = 0x5EED0005 + 7919 * rank
-    keys = (splitmix64(idx, seed) & MASK63) % K
-    if args.exchange == "none" and world > 1:
-        # key-partitioned source: remap every key onto this rank's key groups
-        kg = torch.empty(n_all, dtype=torch.int32, device=dev)
-        owner = torch.empty_like(kg)
-        N.check(N.lib().gw_key_groups_device(n_all, keys.data_ptr(), None, maxp, world, kg.data_ptr(),
-                                             owner.data_ptr(), None))
-        torch.cuda.synchronize()
-        keys = keys[owner == rank]
-        n_all = keys.numel() // steps_total * steps_total
-        keys = keys[:n_all]
-        nb = n_all // steps_total
-        idx = torch.arange(n_all, device=dev, dtype=torch.int64)
-    t0_ms = 1_700_000_000_000
-    jitter = (splitmix64(idx, seed ^ 0x77) & MASK63) % (args.disorder_ms + 1)
-    ts = t0_ms + (idx * slide) // E - jitter
-    vals = None
-    if agg != "count":
-        v = (splitmix64(idx, seed ^ 0x1234) & MASK63) % 1_000_000
-        vals = v.to(torch.float64).view(torch.int64) if agg.endswith("f64") else v
-    del idx, jitter
-    # watermark after step b: BoundedOutOfOrdernessWatermarks (maxTs - bound - 1) over the
-    # un-jittered maximum, identical on every rank
-    wms = [t0_ms + (((b + 1) * nb - 1) * slide) // E - args.disorder_ms - 1 for b in range(steps_total)]
-    torch.cuda.synchronize()
-    log(f"rank {rank}: generated {n_all} events ({n_all * b_in / 1e9:.1f} GB) in {time.time() - t_gen:.1f}s")
+    keys, ts, vals, wms = make_stream(nb, steps_total, K, E, slide, args.disorder_ms, agg, dev, rank, world,
+                                      key_partitioned=args.exchange == "none", maxp=maxp)
+    log(f"rank {rank}: generated {nb * steps_total} events ({nb * steps_total * b_in / 1e9:.1f} GB) "
+        f"in {time.time() - t_gen:.1f}s")
 
-    flags = {"auto": 0, "force": N.FLAG_FORCE_LDS_PREAGG, "off": N.FLAG_NO_LDS_PREAGG}[args.preagg]
-    op = W.GpuWindowOperator(W.SlidingEventTimeWindows.of(size, slide), agg, capacity_hint=max(K // world, 1024),
-                             max_parallelism=maxp, parallelism=world, operator_index=rank, device=local,
-                             flags=flags, max_batch=nb * 2).open()
-    # The step's torch work (exchange partition + all-to-all) runs on a dedicated stream: the
-    # ingest's cross-stream ordering against a non-default stream is cheap, against the
-    # legacy default stream it costs ~25 us per step.
-    side = torch.cuda.Stream(device=dev) if args.torch_stream == "side" else torch.cuda.current_stream(dev)
-    cur = side.cuda_stream
-
+    op = make_operator(W, N, args, K, world, rank, local, nb)
     ex = None
-    native_ex = False
-    if world > 1 and args.exchange == "a2a" and args.dist_backend == "nccl":
-        # the product path: libgpuwin's own RCCL exchange (gw_exchange_*), what a JVM task
-        # drives; torch.distributed only ships its communicator id and times the run
+    if world > 1 and args.exchange == "a2a":
+        # the product path: libgpuwin's own RCCL exchange, what a JVM task drives;
+        # torch.distributed only ships its communicator id and times the run
         from flink_amd.exchange import NativeKeyByExchange
         ex = NativeKeyByExchange(world, rank, max_parallelism=maxp, device=local)
-        native_ex = True
-    elif world > 1:
-        # gloo rehearsal (several ranks may share one GPU): the torch.distributed exchange
-        from flink_amd.exchange import KeyByExchange
-        ex = KeyByExchange(world, rank, max_parallelism=maxp, device=dev)
-
-    exch_bytes = 0
-    rows_sum = 0
-    # Exchanged columns are produced on torch's stream inside each step, so the ingest orders
-    # itself after it (and torch's stream after the read).  Columns generated in HBM before
-    # the clock starts (synchronised above) need no ordering: pass the handle's own stream.
-    exchanged = ex is not None and args.exchange == "a2a"
-    use_torch = args.producer_stream == "torch" or (args.producer_stream == "auto" and exchanged)
-    prod = cur if use_torch else op.stream()
-    # Overlapped exchange: two sets of receive columns used in turn.  The all-to-all of
-    # batch b writes set b%2 once the ingest of batch b-2 has read it (ev_read), and the
-    # ingest orders itself through a hand-off stream that nothing else uses, so the
-    # exchange stream never waits for the ingest of the batch just before it.
-    overlap = exchanged and not native_ex and args.overlap == "on" and args.producer_stream != "handle"
-    if overlap:
-        cap = nb * 2  # received records per step: ~nb for uniform keys (max_batch above)
-        ncols = 3 if vals is not None else 2
-        bufs = [[torch.empty(cap, dtype=torch.int64, device=dev) for _ in range(ncols)] + [None] * (3 - ncols)
-                for _ in range(2)]
-        handoff = torch.cuda.Stream(device=dev)
-        ev_read = [None, None]
-
-    def step(b, timed):
-        if not exchanged:  # nothing of the step runs on a torch stream
-            return step_on_side(b, timed)
-        with torch.cuda.stream(side):
-            return step_on_side(b, timed)
-
-    def step_on_side(b, timed):
-        nonlocal exch_bytes, rows_sum
-        lo, hi = b * nb, (b + 1) * nb
-        k, t, v = keys[lo:hi], ts[lo:hi], (vals[lo:hi] if vals is not None else None)
-        if native_ex:
-            # partition + one all-to-all of (count, watermark, columns) + one host wait +
-            # grouped send/receive, all on `cur`; the ingest orders through the receive set's
-            # hand-off stream, so the next batch's exchange overlaps this batch's aggregation
-            n, pk, pt, pv, _, wmin, ist = ex.exchange(k, t, v, stream=cur, wm=wms[b])
-            if timed:
-                exch_bytes += (nb - int(ex.counts()[0][rank])) * b_in
-            N.check(N.lib().gw_ingest_device(op.handle, n, pk, None, pt, pv, ist), op.handle)
-            op.advance_watermark(wmin)
-            if args.checksum:
-                rows_sum = (rows_sum + rows_checksum(op.drain())) % (1 << 56)
-            op.clear_rows()  # DiscardingSink
-            return None
-        if ex is not None and args.exchange == "a2a":
-            pk, pt, pv, counts = ex.partition(k, t, v, stream=cur)
-            if overlap:
-                s = b % 2
-                (k, t, v), n_recv = ex.exchange_partitioned([pk, pt, pv], counts, out=bufs[s], out_ready=ev_read[s])
-                handoff.wait_event(side.record_event())
-            else:
-                (k, t, v), n_recv = ex.exchange_partitioned([pk, pt, pv], counts)
-            if timed:
-                exch_bytes += (nb - ex.last_send_counts[rank]) * b_in
-        n = k.numel()
-        N.check(N.lib().gw_ingest_device(op.handle, n, k.data_ptr(), None, t.data_ptr(),
-                                         v.data_ptr() if v is not None else None,
-                                         handoff.cuda_stream if overlap else prod), op.handle)
-        if overlap:
-            ev_read[b % 2] = handoff.record_event()  # the ingest's reads of set b%2 are done
-        wm = wms[b]
-        if ex is not None:
-            wm = ex.combine_watermark(wm)  # StatusWatermarkValve: min over inputs
-        op.advance_watermark(wm)
-        if args.checksum:
-            rows_sum = (rows_sum + rows_checksum(op.drain())) % (1 << 56)
-        op.clear_rows()  # DiscardingSink
-        return k, t
+    xs = torch.cuda.Stream(device=dev) if ex is not None else None
+    run = Steps(op, N, keys, ts, vals, wms, nb, ex=ex, collect=args.checksum,
+                ex_stream=xs.cuda_stream if xs is not None else None)
 
     op.enable_kernel_timing(not args.no_kernel_timing)
     for b in range(args.warmup):
-        step(b, False)
+        run.step(b)
     op.flush()  # warmup batches still buffered are applied outside the timed region
     for w in (0, 1, 2):
         op.kernel_time_ms(w)  # reset timers after warmup
@@ -265,7 +239,7 @@ def main():
     cycles = []
     cyc_t, cyc_steps, fires_seen = t0, 0, op.stats()["fires"]
     for b in range(args.warmup, steps_total):
-        step(b, True)
+        run.step(b, True, b_in, rank)
         cyc_steps += 1
         f = op.stats()["fires"]
         if f != fires_seen:
@@ -284,7 +258,7 @@ def main():
     if cyc_steps:
         cycles.append({"steps": cyc_steps, "ms": (time.perf_counter() - cyc_t) * 1e3, "partial": True})
     if dist:
-        e = torch.tensor([elapsed], dtype=torch.float64, device=dev if args.dist_backend == "nccl" else "cpu")
+        e = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
     ingest_ms, ingest_launches = op.kernel_time_ms(0)
@@ -305,23 +279,24 @@ def main():
         dsum += int(torch.unique(comp).numel())
     ingest_bytes_total = events_rank * b_in + 2 * s_acc * dsum
     fire_bytes_total = rows_rank * (32 + s_acc)
-    # The ingest pipeline of one watermark batch: pass 1 (k_part_hist/cols/scatter) per
-    # batch, plus its share of pass 2 + k_rgn_apply, which run once per fire over the
-    # buffered batches.  Device time from HIP events on the operator's stream.
+    # The ingest pipeline of one watermark batch: pass 1 per batch plus its share of the
+    # plan / pass 2 / apply launches, which run once per buffer flush.  Device time from HIP
+    # events on the operator's stream.
     pipe_ms_total = ingest_ms * ingest_launches + apply_ms * apply_launches
     per_launch = ingest_bytes_total / max(ingest_launches, 1)
     pipe_ms = pipe_ms_total / max(ingest_launches, 1)
     achieved = ingest_bytes_total / (pipe_ms_total / 1e3) / 1e9 if pipe_ms_total > 0 else 0.0
     pipeline_gbs = (ingest_bytes_total + fire_bytes_total) / elapsed / 1e9
 
+    checksum = None
     if args.checksum:
-        rows_sum = (rows_sum + rows_checksum(op.drain())) % (1 << 56)
-    tot = torch.tensor([events_rank, rows_rank, rows_sum], dtype=torch.int64,
-                       device=dev if args.dist_backend == "nccl" else "cpu")
+        op.advance_watermark(W.LONG_MAX)  # end of input: everything left fires (outside the clock)
+        run.consume()
+        checksum = wrap64(sum(c for _, c in run.per_wm))
+    tot = torch.tensor([events_rank, rows_rank, checksum or 0], dtype=torch.int64, device=dev)
     if dist:
         dist.all_reduce(tot)
     events_all, rows_all = int(tot[0].item()), int(tot[1].item())
-    rows_sum = int(tot[2].item()) % (1 << 56)
     value = events_all / elapsed
 
     # ------------------------------------------------------------ CPU baseline
@@ -331,6 +306,9 @@ def main():
     host_fed = None
     if rank == 0 and world == 1 and not args.no_host_fed:
         host_fed = host_fed_leg(args, W, keys, ts, vals, wms, nb, agg, size, slide, K, maxp, local)
+    oracle_check = None
+    if rank == 0 and world == 1 and args.checksum and args.oracle_check:
+        oracle_check = oracle_watermarks(args, keys, ts, vals, wms, nb, run.per_wm)
 
     if rank == 0:
         out = {
@@ -356,8 +334,8 @@ def main():
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": "ingest pipeline per watermark batch (region path: pass 1 k_part_* per batch + "
-                          "pass 2 / k_rgn_apply per buffer flush)",
+                "kernel": "ingest pipeline per watermark batch (region path: pass 1 k_rgn_p1 per batch + "
+                          "plan / pass 2 / k_rgn_apply per buffer flush)",
                 "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS, "traffic": traffic_bytes(agg, nb),
                 "bytes_per_launch": per_launch, "avg_launch_ms": pipe_ms, "launches": ingest_launches,
@@ -372,27 +350,57 @@ def main():
             "cpu_baseline": cpu,
         }
         if args.checksum:
-            out["rows_checksum"] = rows_sum
+            out["rows_checksum"] = int(tot[2].item())
+            out["checksum_note"] = ("oracle.rows_hash_sum over every row fired, warmup and the final "
+                                    "MAX_WATERMARK included, summed over ranks (mod 2^64)")
+        if oracle_check is not None:
+            out["oracle_check"] = oracle_check
         if world > 1:
-            out["exchange_gbs_per_gpu"] = exch_bytes / elapsed / 1e9
+            out["exchange_gbs_per_gpu"] = run.exch_bytes / elapsed / 1e9
             out["exchange_path"] = ("gw_exchange_batch (libgpuwin RCCL: partition, one all-to-all of "
                                     "(count, watermark, columns), one host wait, grouped send/recv per batch)"
-                                    if native_ex else "torch.distributed KeyByExchange (gloo rehearsal)")
+                                    if ex is not None else "none (key-partitioned source)")
         print(json.dumps(out), flush=True)
+    if ex is not None:
+        ex.close()
     op.close()
     if dist:
         dist.destroy_process_group()
 
 
+def oracle_watermarks(args, keys, ts, vals, wms, nb, per_wm):
+    """The CPU oracle (oracle/, test infrastructure) over the same stream and watermarks,
+    compared per watermark with the GPU's (row count, checksum); outside every timed region."""
+    from oracle import oracle as O
+    O.build()
+    threads, _ = host_cores()
+    cfg = O.make_config(assigner="sliding", size=args.size_ms, slide=args.slide_ms, agg=args.agg,
+                        max_parallelism=128)
+    nbat = len(wms)
+    rows, cs, sec = O.run_parallel_wm(cfg, threads, np.full(nbat, nb, np.int64), np.array(wms, np.int64),
+                                      keys.cpu().numpy(), ts.cpu().numpy(),
+                                      vals.cpu().numpy() if vals is not None else None)
+    ora = [(int(r), int(c)) for r, c in zip(rows, cs)]
+    bad = [i for i, (g, o) in enumerate(zip(per_wm, ora)) if g != o]
+    return {"watermarks": len(ora), "match": not bad and len(per_wm) == len(ora), "mismatched": bad[:10],
+            "oracle_checksum": wrap64(sum(c for _, c in ora)),
+            "oracle_seconds": sec, "oracle_threads": threads}
+
+
 def rows_checksum(rows) -> int:
-    """Order-independent checksum of fired rows: sum of a 64-bit mix of each (key, start,
-    end, result), mod 2^56 (results compared by their bit pattern)."""
+    """The oracle's order-independent row checksum (oracle.rows_hash_sum: the sum over rows
+    of (key * 0x9e3779b97f4a7c15) ^ (start * 31) ^ (end * 17) ^ result bits, mod 2^64)."""
     k, s, e, r = (np.ascontiguousarray(c).view(np.uint64) for c in rows)
     with np.errstate(over="ignore"):
-        h = k * np.uint64(0x9E3779B97F4A7C15) ^ s * np.uint64(0xBF58476D1CE4E5B9) \
-            ^ e * np.uint64(0x94D049BB133111EB) ^ r * np.uint64(0xD6E8FEB86659FD93)
-        h ^= h >> np.uint64(31)
-    return int((h & np.uint64((1 << 56) - 1)).astype(object).sum() % (1 << 56)) if h.size else 0
+        h = (k * np.uint64(0x9E3779B97F4A7C15)) ^ (s * np.uint64(31)) ^ (e * np.uint64(17)) ^ r
+        tot = h.sum(dtype=np.uint64) if h.size else np.uint64(0)
+    return int(np.array(tot, dtype=np.uint64).view(np.int64))
+
+
+def wrap64(x: int) -> int:
+    """x mod 2^64 as a signed int64."""
+    x &= (1 << 64) - 1
+    return x - (1 << 64) if x >= (1 << 63) else x
 
 
 def traffic_bytes(agg, nb):

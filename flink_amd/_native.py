@@ -17,7 +17,8 @@ ERRORS = {
     -1: "GW_E_INVALID", -2: "GW_E_UNSUPPORTED", -3: "GW_E_DEVICE", -4: "GW_E_OOM",
     -5: "GW_E_OUTPUT_FULL", -6: "GW_E_NO_TIMESTAMP", -7: "GW_E_RANGE", -8: "GW_E_STATE",
 }
-GW_E_OUTPUT_FULL = -5
+GW_E_INVALID, GW_E_UNSUPPORTED, GW_E_DEVICE, GW_E_OOM, GW_E_OUTPUT_FULL = -1, -2, -3, -4, -5
+GW_E_NO_TIMESTAMP, GW_E_RANGE, GW_E_STATE = -6, -7, -8
 
 ASSIGNERS = {"tumbling": 0, "sliding": 1, "session": 2, "count_tumbling": 3, "count_sliding": 4}
 TRIGGERS = {"event_time": 0, "purging_event_time": 1}
@@ -49,7 +50,8 @@ EXPORTS = [
     "gw_key_groups_device", "gw_partition_scratch_bytes", "gw_partition_device",
     "gw_decode_serialized", "gw_ingest_serialized", "gw_ingest_serialized_device",
     "gw_exchange_unique_id", "gw_exchange_create", "gw_exchange_destroy", "gw_exchange_batch",
-    "gw_exchange_min_watermark", "gw_exchange_last_error", "gw_exchange_counts",
+    "gw_exchange_min_watermark", "gw_exchange_last_error", "gw_exchange_counts", "gw_exchange_plan",
+    "gw_window_stagger_offset",
     "gw_ingest_payload", "gw_ingest_payload_device", "gw_drain_payload",
     "gw_snapshot_keys", "gw_snapshot_remap_keys", "gw_snapshot_payloads", "gw_snapshot_remap_payloads",
 ]
@@ -184,6 +186,8 @@ def lib() -> ctypes.CDLL:
         "gw_exchange_batch": (c_int, [p, i64, p, p, p, p, i64, P64, ctypes.POINTER(p), ctypes.POINTER(p),
                                       ctypes.POINTER(p), ctypes.POINTER(p), P64, ctypes.POINTER(p), p]),
         "gw_exchange_counts": (c_int, [p, p, p]),
+        "gw_exchange_plan": (c_int, [i32, p, p, i64, i64, p, p, p, p, P64, P64]),
+        "gw_window_stagger_offset": (c_int, [i32, i64, ctypes.c_double, i64, i64, P64]),
         "gw_exchange_min_watermark": (c_int, [p, i64, P64, p]),
         "gw_exchange_last_error": (ctypes.c_char_p, [p]),
     }
@@ -231,3 +235,19 @@ def snapshot_remap_keys(blob: bytes, mapping: dict) -> bytes:
     dst = np.asarray([mapping[int(k)] for k in src], dtype=np.int64)
     check(lib().gw_snapshot_remap_keys(buf, len(blob), src.ctypes.data, dst.ctypes.data, len(src)))
     return buf.raw[:len(blob)]
+
+
+def exchange_plan(sent_msg, recv_msg, cols_mask: int, wm: int):
+    """gw_exchange_plan (host only): per-peer (send_off, send_cnt, recv_off, recv_cnt), total
+    received, minimum watermark from this rank's sent / received (records, watermark, mask)
+    messages (int64[nranks * 3] each)."""
+    import numpy as np
+    sm = np.ascontiguousarray(sent_msg, dtype=np.int64)
+    rm = np.ascontiguousarray(recv_msg, dtype=np.int64)
+    P = len(sm) // 3
+    out = [np.zeros(P, np.int64) for _ in range(4)]
+    tot, wmin = ctypes.c_int64(), ctypes.c_int64()
+    rc = lib().gw_exchange_plan(P, sm.ctypes.data, rm.ctypes.data, int(cols_mask), int(wm),
+                                *[o.ctypes.data for o in out], ctypes.byref(tot), ctypes.byref(wmin))
+    check(rc)
+    return out, tot.value, wmin.value

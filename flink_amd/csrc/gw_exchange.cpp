@@ -45,6 +45,7 @@ struct gw_exchange {
     int64_t* d_wm = nullptr;
     int64_t* h_wm = nullptr;
     std::vector<int64_t> last_send, last_recv;
+    std::vector<int64_t> plan[4];  // gw_exchange_plan: send offsets, send counts, receive offsets, receive counts
     // per receive set: the hand-off stream the ingest orders on, and its "reads done" event
     hipStream_t handoff[2] = {nullptr, nullptr};
     hipEvent_t ev_recv[2] = {nullptr, nullptr}, ev_free[2] = {nullptr, nullptr};
@@ -110,6 +111,7 @@ int gw_exchange_create(gw_exchange** out, int32_t nranks, int32_t rank, const vo
     }
     ex->last_send.assign(nranks, 0);
     ex->last_recv.assign(nranks, 0);
+    for (auto& v : ex->plan) v.assign(nranks, 0);
     *out = ex;
     return GW_OK;
 }
@@ -133,6 +135,31 @@ void gw_exchange_destroy(gw_exchange* ex) {
 }
 
 const char* gw_exchange_last_error(const gw_exchange* ex) { return ex ? ex->err.c_str() : ""; }
+
+int gw_exchange_plan(int32_t nranks, const int64_t* sent_msg, const int64_t* recv_msg, int64_t cols_mask, int64_t wm,
+                     int64_t* send_off, int64_t* send_cnt, int64_t* recv_off, int64_t* recv_cnt, int64_t* total,
+                     int64_t* wm_min) {
+    constexpr int M = gw_exchange::kMsg;
+    if (nranks < 1 || !sent_msg || !recv_msg || !send_off || !send_cnt || !recv_off || !recv_cnt || !total || !wm_min)
+        return GW_E_INVALID;
+    int64_t so = 0, ro = 0, wmin = wm;
+    bool agree = true;
+    for (int q = 0; q < nranks; ++q) {
+        const int64_t s = sent_msg[M * q], r = recv_msg[M * q];
+        if (s < 0 || r < 0) return GW_E_INVALID;
+        send_off[q] = so;
+        send_cnt[q] = s;
+        recv_off[q] = ro;
+        recv_cnt[q] = r;
+        so += s;
+        ro += r;
+        wmin = std::min(wmin, recv_msg[M * q + 1]);
+        agree &= recv_msg[M * q + 2] == cols_mask;
+    }
+    *total = ro;
+    *wm_min = wmin;
+    return agree ? GW_OK : GW_E_INVALID;
+}
 
 int gw_exchange_batch(gw_exchange* ex, int64_t n, const int64_t* d_key, const int32_t* d_key_hash,
                       const int64_t* d_ts, const int64_t* d_value, int64_t wm, int64_t* n_out,
@@ -179,17 +206,16 @@ int gw_exchange_batch(gw_exchange* ex, int64_t n, const int64_t* d_key, const in
     EX_HIP(hipStreamSynchronize(s));
     const int64_t* sm = ex->h_msg;
     const int64_t* rm = ex->h_msg + M * P;
+    std::vector<int64_t>& so = ex->plan[0];
+    std::vector<int64_t>& sc = ex->plan[1];
+    std::vector<int64_t>& ro = ex->plan[2];
+    std::vector<int64_t>& rc = ex->plan[3];
     int64_t total = 0, wmin = wm;
-    bool cols_agree = true;
-    for (int q = 0; q < P; ++q) {
-        ex->last_send[q] = sm[M * q];
-        ex->last_recv[q] = rm[M * q];
-        total += rm[M * q];
-        wmin = std::min(wmin, rm[M * q + 1]);
-        cols_agree &= rm[M * q + 2] == cols_mask;
-    }
     // every rank sees every rank's mask: all of them fail here together, before any send
-    if (!cols_agree) return ex_fail(ex, GW_E_INVALID, "gw_exchange_batch: ranks pass different columns");
+    if (gw_exchange_plan(P, sm, rm, cols_mask, wm, so.data(), sc.data(), ro.data(), rc.data(), &total, &wmin))
+        return ex_fail(ex, GW_E_INVALID, "gw_exchange_batch: ranks pass different columns");
+    ex->last_send = sc;
+    ex->last_recv = rc;
     // 3. this turn's receive set: free once the ingest two batches ago has read it
     const int u = ex->turn;
     ex->turn ^= 1;
@@ -222,13 +248,9 @@ int gw_exchange_batch(gw_exchange* ex, int64_t n, const int64_t* d_key, const in
     ncclResult_t r = ncclSuccess;
     for (const Col& c : cols) {
         if (!c.src) continue;
-        int64_t so = 0, ro = 0;
         for (int q = 0; q < P && r == ncclSuccess; ++q) {
-            if (sm[M * q]) r = ncclSend((const char*)c.src + so * c.w, (size_t)sm[M * q], c.t, q, ex->comm, s);
-            if (r == ncclSuccess && rm[M * q])
-                r = ncclRecv((char*)c.dst + ro * c.w, (size_t)rm[M * q], c.t, q, ex->comm, s);
-            so += sm[M * q];
-            ro += rm[M * q];
+            if (sc[q]) r = ncclSend((const char*)c.src + so[q] * c.w, (size_t)sc[q], c.t, q, ex->comm, s);
+            if (r == ncclSuccess && rc[q]) r = ncclRecv((char*)c.dst + ro[q] * c.w, (size_t)rc[q], c.t, q, ex->comm, s);
         }
     }
     const ncclResult_t re = ncclGroupEnd();

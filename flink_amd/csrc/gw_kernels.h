@@ -160,6 +160,9 @@ struct IngestArgs {
     int32_t d2_bits;       // 0: single-pass table (apply reads the P1 tiles directly)
     int32_t fmt;           // region record format (gw_pane.hip): 0 wide, 1 compact (hash word +
                            // 32-bit value), 2 narrow (32-bit key + 28-bit value; 4 B for COUNT)
+    int32_t nar2;          // narrow two-pass flushes (k_rgn_apply_nar): P2 groups each round by
+                           // (super-region, ring position); one workgroup per super-region of
+    int32_t sr_bits;       //   2^sr_bits probe regions applies one ring position after another
     int64_t tile0;         // P1: buffer tile of this batch's first tile
     int64_t ntiles;        // flush: buffer tiles in use
     int64_t ngroups;       // flush: P1 tile groups (= P2 blocks per bucket)

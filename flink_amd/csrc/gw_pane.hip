@@ -418,7 +418,7 @@ constexpr uint64_t kCmpSpill = 1ull << 63;
 // does not fit goes to the deferred list (exact); past 1/64 of a window's records the
 // handle drops to compact records at its next window.
 constexpr int kFmtWide = 0, kFmtCmp = 1, kFmtNar = 2;
-constexpr int64_t kNarKeyLimit = 1ll << 32, kNarCountKeyLimit = 1ll << 28, kNarValLimit = 1ll << 27;
+constexpr int64_t kNarKeyLimit = (1ll << 32) - 2, kNarCountKeyLimit = 1ll << 28, kNarValLimit = 1ll << 27;
 __device__ __forceinline__ uint64_t nar_pack(int64_t key, int64_t v, uint32_t pos) {
     return (uint64_t)(uint32_t)key | ((uint64_t)(((uint32_t)(int32_t)v << 4) | pos) << 32);
 }
@@ -834,15 +834,17 @@ __global__ void __launch_bounds__(kPartThreads) k_rgn_p2(IngestArgs a) {
     const TileLds s = tile_lds<AV>(smem);
     int32_t* s_v32 = reinterpret_cast<int32_t*>(s.a0);
     uint32_t* s_r32 = reinterpret_cast<uint32_t*>(s.k);
-    const int lr_sh = 64 - (a.d1_bits + a.d2_bits);  // C: region bits of the hash word
+    // C: region bits of the hash word; narrow two-pass flushes (nar2): super-region bits
+    const int d2r = a.nar2 ? a.d2_bits - a.sr_bits : a.d2_bits;
+    const int lr_sh = 64 - (a.d1_bits + d2r);
     __shared__ uint32_t lh[kPartBuckets], ls[kPartBuckets];
     __shared__ uint32_t r_cnt[kMaxGroup], r_pre[kMaxGroup + 1], wsum[kPartThreads / 64];
     __shared__ int64_t r_src[kMaxGroup];
     const int64_t b1 = blockIdx.x / a.ngroups, j = blockIdx.x - b1 * a.ngroups;
     const int64_t t0 = j * a.p2_group;
     const int nt = (int)min((int64_t)a.p2_group, a.ntiles - t0);
-    const int nb2 = 1 << a.d2_bits;
-    const int64_t m2 = nb2 - 1;
+    const int64_t m2 = ((int64_t)1 << d2r) - 1;
+    const int nb2 = a.nar2 ? (int)(m2 + 1) << 3 : (int)(m2 + 1);  // nar2: (super-region, ring position)
     for (int i = threadIdx.x; i < nt; i += blockDim.x) {
         const uint32_t d = a.p2_desc[b1 * a.ntiles + t0 + i];
         r_cnt[i] = d & 0xffffu;
@@ -886,6 +888,9 @@ __global__ void __launch_bounds__(kPartThreads) k_rgn_p2(IngestArgs a) {
             if constexpr (NR) {  // the key's hash gives its region
                 const int64_t k = N4 ? nar_key32((uint32_t)key[it]) : nar_key((uint64_t)key[it]);
                 bk[it] = (int)((slot_hash(k) >> lr_sh) & (uint64_t)m2);
+                if (a.nar2)
+                    bk[it] = (bk[it] << 3) |
+                             (int)nar_pos(N4 ? (uint32_t)key[it] : (uint32_t)((uint64_t)key[it] >> 32));
             } else {
                 bk[it] = C ? (int)(((uint64_t)key[it] >> lr_sh) & (uint64_t)m2) : (int)(rgn_of(a.t, key[it]) & m2);
             }
@@ -1397,6 +1402,391 @@ __global__ void __launch_bounds__(kApplyThreads) GW_APPLY_ATTR k_rgn_apply(Inges
     spills = wave_sum(spills);
     if (__lane_id() == 0 && spills) atomicAdd(&a.st->spills, spills);
     block_commit(a.st, 0, ins, flags, 0);
+}
+
+// ---------------------------------------------------------------------------
+// Narrow two-pass apply (a.nar2, k_rgn_apply_nar): one workgroup per super-region of
+// F = 2^sr_bits probe regions (F * S slots, consecutive in memory).  P2 wrote each round's
+// records of a super-region grouped by ring position, so the workgroup applies one ring
+// position after another with ONE pane's cells in LDS, while the keys (as 32-bit values:
+// narrow keys are below 2^32 - 2) and the presence mask stay in LDS throughout.  Against
+// k_rgn_apply: 4 + 1 + 8 B of LDS per slot instead of 8 + 1 + 16, so F = 2 regions per
+// workgroup (runs F times longer, F times fewer workgroups and state round trips); a probe
+// group is one 16-B LDS read; no hash pass over the keys on the way in or out; any number of
+// ring positions per flush (no spill for a third one).
+// ---------------------------------------------------------------------------
+constexpr uint32_t kK32Empty = 0xffffffffu;    // a free slot
+constexpr uint32_t kK32Foreign = 0xfffffffeu;  // a slot holding a key no narrow record carries
+constexpr int kNarMaxF = 4;
+constexpr int kNarMaxSlots = kNarMaxF * 2048;
+constexpr int kNarLoadU = 4;  // 16-B state loads per thread in flight together
+
+__device__ __forceinline__ uint32_t k32_of(int64_t k) {
+    return k == kEmptyKey ? kK32Empty : ((uint64_t)k < (uint64_t)kK32Foreign ? (uint32_t)k : kK32Foreign);
+}
+
+template <int AGG>
+__global__ void __launch_bounds__(kApplyThreads) k_rgn_apply_nar(IngestArgs a) {
+    if constexpr (!cmp_agg<AGG>()) {
+        return;
+    } else {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    constexpr bool M = uses_mask<AGG>();
+    constexpr bool N4 = AGG == GW_COUNT;
+    constexpr int W = AGG == GW_AVG_I64 ? 2 : 1;
+    __shared__ uint32_t r_cnt[kApplyRuns], r_src[kApplyRuns];
+    __shared__ uint32_t s_kdirty[kNarMaxSlots / 16 / 32];  // dirty 128-B lines of the int64 key array
+    __shared__ uint32_t s_pos;                              // ring positions holding records
+    const int F = 1 << a.sr_bits;
+    const int S = (int)pt_S(a.t), FS = F * S;
+    const int l2S = a.t.log2S;
+    const int d2v = a.d2_bits - a.sr_bits;
+    const int64_t sr = blockIdx.x;
+    const int64_t bucket = sr >> d2v, col = sr & (((int64_t)1 << d2v) - 1);
+    const int64_t rb = a.rbeg[bucket], re = a.rbeg[bucket + 1];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    uint32_t* lkeys = reinterpret_cast<uint32_t*>(smem);                     // [FS]
+    uint8_t* lmask = reinterpret_cast<uint8_t*>(lkeys + FS);                  // [FS] (M)
+    long long* lcell = reinterpret_cast<long long*>(lmask + (M ? FS : 0));   // [FS][W]
+    uint32_t* qk = reinterpret_cast<uint32_t*>(lcell + (int64_t)FS * W) + wave * kApplyQ;
+    int32_t* qv = reinterpret_cast<int32_t*>(lcell + (int64_t)FS * W) + nw * kApplyQ + wave * kApplyQ;
+    int qn = 0;
+    const uint64_t* rk = reinterpret_cast<const uint64_t*>(a.e_key);
+    const uint32_t* rk32 = reinterpret_cast<const uint32_t*>(a.e_key);
+    const unsigned long long bocc = *(volatile unsigned long long*)a.batch_occ;
+    const int dom_sh = 64 - a.t.log2nreg;  // region = hash >> dom_sh; its low sr_bits: the region in the super-region
+
+    // which ring positions hold records of this super-region (a region without any skips
+    // the state round trip)
+    if (threadIdx.x == 0) s_pos = 0;
+    for (int i = threadIdx.x; i < kNarMaxSlots / 16 / 32; i += blockDim.x) s_kdirty[i] = 0;
+    __syncthreads();
+    {
+        uint32_t any = 0;
+        for (int64_t rnd = rb + threadIdx.x; rnd < re; rnd += blockDim.x)
+            for (unsigned long long pm = bocc & 0xffull; pm; pm &= pm - 1) {
+                const int p = __ffsll((long long)pm) - 1;
+                if (a.r_row[rnd * kPartBuckets + ((col << 3) | p)] & 0xffffu) any |= 1u << p;
+            }
+        any = (uint32_t)wave_ior(any);
+        if (lane == 0 && any) atomicOr(&s_pos, any);
+    }
+    __syncthreads();
+    const uint32_t pmask = s_pos;
+    if (!pmask) return;  // uniform
+
+    // keys (int64 in HBM -> 32-bit in LDS) and presence masks of the F regions
+    {
+        const int nk2 = FS / 2, nm16 = M ? FS / 16 : 0, tot = nk2 + nm16;
+        for (int w0 = threadIdx.x; w0 < tot; w0 += kNarLoadU * blockDim.x) {
+            long2 v[kNarLoadU];
+#pragma unroll
+            for (int u = 0; u < kNarLoadU; ++u) {
+                const int w = w0 + u * blockDim.x;
+                v[u] = long2{0, 0};
+                if (w < nk2) {
+                    const int d = w / (S / 2), j = w - d * (S / 2);
+                    v[u] = reinterpret_cast<const long2*>(pt_region(a.t, sr * F + d))[j];
+                } else if (w < tot) {
+                    const int wm_ = w - nk2, d = wm_ / (S / 16), j = wm_ - d * (S / 16);
+                    v[u] = reinterpret_cast<const long2*>(pt_mask_base(a.t, sr * F + d))[j];
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < kNarLoadU; ++u) {
+                const int w = w0 + u * blockDim.x;
+                if (w < nk2) {
+                    reinterpret_cast<uint2*>(lkeys)[w] = uint2{k32_of(v[u].x), k32_of(v[u].y)};
+                } else if (w < tot) {
+                    reinterpret_cast<long2*>(lmask)[w - nk2] = v[u];
+                }
+            }
+        }
+    }
+    unsigned long long ins = 0, flags = 0, spills = 0;
+
+    // Probe for key k (its hash h) in its region: one 4-key group per step, the first slot
+    // holding k or free decides; a free slot is claimed by CAS (a lost race re-reads the
+    // group).  Returns the slot in the super-region or -1 (the region is full).
+    auto probe_insert = [&](uint32_t k, uint64_t h) -> int {
+        const int d = F > 1 ? (int)((h >> dom_sh) & (uint64_t)(F - 1)) : 0;
+        uint32_t* kd = lkeys + d * S;
+        int g0 = (int)(h & (uint64_t)(S - 1) & ~(uint64_t)(kProbeGroup - 1));
+        for (int p = 0; p < S;) {
+            const uint4 kk = *reinterpret_cast<const uint4*>(kd + g0);
+            const uint32_t hit = (uint32_t)(kk.x == k) | (uint32_t)(kk.y == k) << 1 | (uint32_t)(kk.z == k) << 2 |
+                                 (uint32_t)(kk.w == k) << 3;
+            const uint32_t emp = (uint32_t)(kk.x == kK32Empty) | (uint32_t)(kk.y == kK32Empty) << 1 |
+                                 (uint32_t)(kk.z == kK32Empty) << 2 | (uint32_t)(kk.w == kK32Empty) << 3;
+            const uint32_t m = hit | emp;
+            if (m) {
+                const int i = __ffs((int)m) - 1;
+                const int j = g0 + i;
+                if ((hit >> i) & 1) return d * S + j;
+                const uint32_t prev = atomicCAS(kd + j, kK32Empty, k);
+                if (prev == kK32Empty) {
+                    ins++;
+                    const int line = (d * S + j) >> 4;
+                    atomicOr(&s_kdirty[line >> 5], 1u << (line & 31));
+                    return d * S + j;
+                }
+                if (prev == k) return d * S + j;
+                continue;  // another key took the slot: re-read this group
+            }
+            g0 = (g0 + kProbeGroup) & (S - 1);
+            p += kProbeGroup;
+        }
+        return -1;
+    };
+    auto cell_add = [&](int slot, int64_t v, uint32_t bit) {
+        long long* c = lcell + (int64_t)slot * W;
+        lds_cell_add<AGG>(c, c + (W - 1), v, 1);
+        if constexpr (M) atomicOr(reinterpret_cast<uint32_t*>(lmask) + (slot >> 2), bit << ((slot & 3) * 8));
+    };
+
+    struct Grp {
+        uint32_t pre[kApplyGroup + 1];
+        uint32_t src[kApplyGroup];
+    };
+    struct Step {
+        uint64_t r[kApplyUnroll];
+        bool ok[kApplyUnroll];
+    };
+    const long long id0 = identity0(AGG);
+    const long2 ident = W == 2 ? long2{id0, 0} : long2{id0, id0};
+    for (uint32_t pm = pmask; pm; pm &= pm - 1) {
+        const int p = __ffs((int)pm) - 1;
+        const uint32_t pbit = 1u << p;
+        const int64_t ccol = (col << 3) | p;
+        __syncthreads();  // the previous position's write-back has read the cells
+        {  // this position's pane (an untouched one holds identities)
+            const bool fresh = (a.ring_fresh >> p) & 1;
+            const int per = S * W / 2, tot = FS * W / 2;
+            long2* l2 = reinterpret_cast<long2*>(lcell);
+            for (int w0 = threadIdx.x; w0 < tot; w0 += kNarLoadU * blockDim.x) {
+                long2 v[kNarLoadU];
+#pragma unroll
+                for (int u = 0; u < kNarLoadU; ++u) {
+                    const int w = w0 + u * blockDim.x;
+                    v[u] = ident;
+                    if (w < tot && !fresh) {
+                        const int d = w / per;
+                        v[u] = reinterpret_cast<const long2*>(pt_cell(a.t, (sr * F + d) << l2S, p))[w - d * per];
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < kNarLoadU; ++u) {
+                    const int w = w0 + u * blockDim.x;
+                    if (w < tot) l2[w] = v[u];
+                }
+            }
+        }
+        for (int64_t c0r = rb; c0r < re; c0r += kApplyRuns) {
+            const int nr = (int)min((int64_t)kApplyRuns, re - c0r);
+            __syncthreads();  // the cells are in; the previous block's descriptors consumed
+            for (int i = threadIdx.x; i < nr; i += blockDim.x) {
+                const int64_t rnd = c0r + i;
+                const uint32_t d = a.r_row[rnd * kPartBuckets + ccol];
+                r_cnt[i] = d & 0xffffu;
+                r_src[i] = (uint32_t)(a.r_base[rnd] + (d >> 16));
+            }
+            __syncthreads();
+            auto load_grp = [&](int i0, Grp& g) {
+                g.pre[0] = 0;
+#pragma unroll
+                for (int u = 0; u < kApplyGroup; ++u) {
+                    const int i = i0 + u;
+                    g.pre[u + 1] = g.pre[u] + (i < nr ? r_cnt[i] : 0u);
+                    g.src[u] = i < nr ? r_src[i] : 0u;
+                }
+            };
+            auto load_step = [&](const Grp& g, uint32_t k, Step& st, bool live) {
+                const uint32_t tot = live ? g.pre[kApplyGroup] : 0u;
+#pragma unroll
+                for (int q = 0; q < kApplyUnroll; ++q) {
+                    const uint32_t e = k + q * 64 + lane;
+                    st.ok[q] = e < tot;
+                    uint32_t sb = g.src[0], sp = 0;
+#pragma unroll
+                    for (int w = 1; w < kApplyGroup; ++w) {
+                        if (e >= g.pre[w]) { sb = g.src[w]; sp = g.pre[w]; }
+                    }
+                    const uint32_t x = st.ok[q] ? sb + (e - sp) : 0u;  // unconditional loads
+                    st.r[q] = N4 ? (uint64_t)rk32[x] : rk[x];
+                }
+            };
+            auto advance = [&](int& i0, uint32_t& k, Grp& g) -> bool {
+                k = k == ~0u ? 0u : k + 64 * kApplyUnroll;
+                while (i0 < nr && k >= g.pre[kApplyGroup]) {
+                    i0 += nw * kApplyGroup;
+                    k = 0;
+                    if (i0 < nr) load_grp(i0, g);
+                }
+                return i0 < nr;
+            };
+            // a record whose key is not in its home group waits in the wave's queue; 64 at a
+            // time the wave probes them with every lane busy
+            auto q_push = [&](bool pu, uint32_t kk, int32_t vv) {
+                const uint64_t bal = __ballot(pu);
+                if (pu) {
+                    const int at = qn + __popcll(bal & ((1ull << lane) - 1ull));
+                    qk[at] = kk;
+                    qv[at] = vv;
+                }
+                qn += __popcll(bal);
+                if (qn >= 64) {
+                    const int at = qn - 64 + lane;
+                    const uint32_t k2 = qk[at];
+                    const int s2 = probe_insert(k2, slot_hash((int64_t)k2));
+                    if (s2 >= 0) cell_add(s2, qv[at], pbit);
+                    else { flags |= GW_DF_TABLE_FULL; spills++; }
+                    qn -= 64;
+                }
+            };
+            auto apply_step = [&](const Step& c) {
+                uint32_t kq[kApplyUnroll];
+                int32_t vq[kApplyUnroll];
+                int hq[kApplyUnroll];
+                uint4 ka[kApplyUnroll];
+#pragma unroll
+                for (int q = 0; q < kApplyUnroll; ++q) {
+                    const uint64_t r = c.r[q];
+                    kq[q] = N4 ? (uint32_t)(r >> 4) : (uint32_t)r;
+                    vq[q] = N4 ? 1 : (int32_t)(uint32_t)(r >> 32) >> 4;
+                    const uint64_t h = slot_hash((int64_t)kq[q]);
+                    const int d = F > 1 ? (int)((h >> dom_sh) & (uint64_t)(F - 1)) : 0;
+                    hq[q] = d * S + (int)(h & (uint64_t)(S - 1) & ~(uint64_t)(kProbeGroup - 1));
+                }
+#pragma unroll
+                for (int q = 0; q < kApplyUnroll; ++q) ka[q] = *reinterpret_cast<const uint4*>(lkeys + hq[q]);
+#pragma unroll
+                for (int q = 0; q < kApplyUnroll; ++q) {
+                    const uint32_t k = kq[q];
+                    const int i = ka[q].x == k ? 0 : ka[q].y == k ? 1 : ka[q].z == k ? 2 : ka[q].w == k ? 3 : -1;
+                    const bool fast = c.ok[q] && i >= 0;
+                    if (fast) cell_add(hq[q] + i, vq[q], pbit);
+                    q_push(c.ok[q] && !fast, k, vq[q]);  // the wave is converged here
+                }
+            };
+            int i0 = wave * kApplyGroup;
+            uint32_t k = ~0u;
+            Grp g;
+            if (i0 < nr) load_grp(i0, g);
+            Step sa, sb;
+            bool live = advance(i0, k, g);
+            load_step(g, k, sa, live);
+            while (live) {
+                live = advance(i0, k, g);
+                load_step(g, k, sb, live);
+                apply_step(sa);
+                if (!live) break;
+                live = advance(i0, k, g);
+                load_step(g, k, sa, live);
+                apply_step(sb);
+            }
+            if (lane < qn) {  // the rest of the queue
+                const uint32_t k2 = qk[lane];
+                const int s2 = probe_insert(k2, slot_hash((int64_t)k2));
+                if (s2 >= 0) cell_add(s2, qv[lane], pbit);
+                else { flags |= GW_DF_TABLE_FULL; spills++; }
+            }
+            qn = 0;
+        }
+        __syncthreads();
+        {  // write back this position's pane
+            const int per = S * W / 2, tot = FS * W / 2;
+            const long2* l2 = reinterpret_cast<const long2*>(lcell);
+            for (int w = threadIdx.x; w < tot; w += blockDim.x) {
+                const int d = w / per;
+                reinterpret_cast<long2*>(pt_cell(a.t, (sr * F + d) << l2S, p))[w - d * per] = l2[w];
+            }
+        }
+    }
+    // Spill pass (only after a region filled up): records whose key is absent from the final
+    // key table were not applied; mark them for k_rgn_collect_nar2.
+    if (__syncthreads_or(spills != 0)) {
+        unsigned long long marked = 0;
+        for (uint32_t pm = pmask; pm; pm &= pm - 1) {
+            const int p = __ffs((int)pm) - 1;
+            const int64_t ccol = (col << 3) | p;
+            for (int64_t rnd = rb + wave; rnd < re; rnd += nw) {
+                const uint32_t d = a.r_row[rnd * kPartBuckets + ccol];
+                const int64_t src = a.r_base[rnd] + (d >> 16);
+                for (uint32_t k = lane; k < (d & 0xffffu); k += 64) {
+                    const uint64_t r = N4 ? (uint64_t)rk32[src + k] : rk[src + k];
+                    const uint32_t kk = N4 ? (uint32_t)(r >> 4) : (uint32_t)r;
+                    const uint64_t h = slot_hash((int64_t)kk);
+                    const int dd = F > 1 ? (int)((h >> dom_sh) & (uint64_t)(F - 1)) : 0;
+                    int j = (int)(h & (uint64_t)(S - 1) & ~(uint64_t)(kProbeGroup - 1));
+                    bool present = false;
+                    for (int q = 0; q < S; ++q) {
+                        const uint32_t x = lkeys[dd * S + j];
+                        if (x == kk) { present = true; break; }
+                        if (x == kK32Empty) break;
+                        j = (j + 1) & (S - 1);
+                    }
+                    if (!present) {
+                        if constexpr (N4) const_cast<uint32_t*>(rk32)[src + k] = (uint32_t)r | kNarSpill;
+                        else const_cast<uint64_t*>(rk)[src + k] = r | ((uint64_t)kNarSpill << 32);
+                        marked++;
+                    }
+                }
+            }
+        }
+        spills = marked;
+    }
+    __syncthreads();
+    // write back: the masks whole, the keys of dirty lines (a foreign slot never changes)
+    if constexpr (M) {
+        const int per = S / 16;
+        for (int w = threadIdx.x; w < FS / 16; w += blockDim.x) {
+            const int d = w / per;
+            reinterpret_cast<long2*>(pt_mask_base(a.t, sr * F + d))[w - d * per] = reinterpret_cast<const long2*>(lmask)[w];
+        }
+    }
+    for (int j = threadIdx.x; j < FS; j += blockDim.x) {
+        const int line = j >> 4;
+        if ((s_kdirty[line >> 5] >> (line & 31)) & 1u) {
+            const uint32_t k = lkeys[j];
+            if (k != kK32Foreign) {
+                const int d = j / S;
+                pt_region(a.t, sr * F + d)[j - d * S] = k == kK32Empty ? kEmptyKey : (int64_t)k;
+            }
+        }
+    }
+    spills = wave_sum(spills);
+    if (__lane_id() == 0 && spills) atomicAdd(&a.st->spills, spills);
+    block_commit(a.st, 0, ins, flags, 0);
+    }
+}
+
+// Spilled narrow records of a nar2 flush: one linear pass over the P2 output.
+template <int AGG>
+__global__ void __launch_bounds__(256) k_rgn_collect_nar2(IngestArgs a) {
+    constexpr bool N4 = AGG == GW_COUNT;
+    const int64_t n = a.bk_off[1 << a.d1_bits];
+    int64_t* rk = a.e_key;
+    uint32_t* rk32 = reinterpret_cast<uint32_t*>(rk);
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t base = blockIdx.x * (int64_t)blockDim.x; base < n; base += stride) {
+        const int64_t i = base + threadIdx.x;
+        bool spill = false;
+        int64_t key = 0, pane = 0, c0 = 0;
+        if (i < n) {
+            const uint64_t w = N4 ? (uint64_t)rk32[i] : (uint64_t)rk[i];
+            const uint32_t lo = N4 ? (uint32_t)w : (uint32_t)(w >> 32);
+            if (nar_spilled(lo)) {
+                spill = true;
+                if (N4) rk32[i] = (uint32_t)w & ~kNarSpill;
+                else rk[i] = (int64_t)(w & ~((uint64_t)kNarSpill << 32));
+                key = N4 ? nar_key32((uint32_t)w) : nar_key(w);
+                c0 = N4 ? 1 : nar_val(w);
+                const int64_t rel = ((int64_t)nar_pos(lo) - a.b_pos + a.t.ring) % a.t.ring;
+                pane = a.p_late + (int64_t)a.delta + rel;
+            }
+        }
+        defer_write(a, spill, key, pane, c0, 1);
+    }
 }
 
 // The same for compact records: the spill mark is bit 63 of the word, and the key comes
@@ -2187,6 +2577,25 @@ hipError_t launch_region_flush(const IngestArgs& a, hipStream_t s) {
     } else {                        \
         L2(A, kFmtWide);            \
     }
+    if (a.fmt == kFmtNar && a.nar2) {
+        const int F = 1 << a.sr_bits;
+        const int64_t FS = (int64_t)F * S;
+        const bool M = a.t.has_mask != 0;
+        const size_t lds = (size_t)FS * 4 + (M ? (size_t)FS : 0) + (size_t)FS * a.t.words * 8 +
+                           (size_t)(kApplyThreads / 64) * kApplyQ * 8;
+#define LN(A)                                                                                                   \
+    lds_opt_in((const void*)k_rgn_p2<A, kFmtNar>, part_lds);                                                   \
+    lds_opt_in((const void*)k_rgn_apply_nar<A>, lds);                                                         \
+    hipLaunchKernelGGL(k_rgn_plan1, dim3((unsigned)a.ngroups), dim3(256), 0, s, a);                            \
+    hipLaunchKernelGGL(k_rgn_plan2, dim3((unsigned)nb1), dim3(256), 0, s, a);                                  \
+    hipLaunchKernelGGL(k_rgn_plan3, dim3(1), dim3(256), 0, s, a);                                              \
+    hipLaunchKernelGGL((k_rgn_p2<A, kFmtNar>), dim3((unsigned)(a.ngroups * nb1)), dim3(kPartThreads), part_lds, s, \
+                       a);                                                                                      \
+    hipLaunchKernelGGL(k_rgn_apply_nar<A>, dim3((unsigned)(a.t.nreg >> a.sr_bits)), dim3(kApplyThreads), lds, s, a)
+        GW_AGG_SWITCH(a.t.agg, LN);
+#undef LN
+        return hipGetLastError();
+    }
     GW_AGG_SWITCH(a.t.agg, L);
 #undef L
 #undef L2
@@ -2196,7 +2605,9 @@ hipError_t launch_region_flush(const IngestArgs& a, hipStream_t s) {
 hipError_t launch_region_collect(const IngestArgs& a, hipStream_t s) {
     const int64_t n = a.ntiles * kPartTile;  // upper bound of the buffer's records
 #define L(A)                                                                                         \
-    if (a.fmt == kFmtNar)                                                                            \
+    if (a.fmt == kFmtNar && a.nar2)                                                                  \
+        hipLaunchKernelGGL(k_rgn_collect_nar2<A>, dim3(grid_for(n)), dim3(256), 0, s, a);           \
+    else if (a.fmt == kFmtNar)                                                                       \
         hipLaunchKernelGGL(k_rgn_collect_nar<A>, dim3((unsigned)a.t.nreg), dim3(256), 0, s, a);     \
     else if (a.fmt == kFmtCmp)                                                                       \
         hipLaunchKernelGGL(k_rgn_collect_cmp<A>, dim3((unsigned)a.t.nreg), dim3(256), 0, s, a);     \

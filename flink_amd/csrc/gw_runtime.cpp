@@ -992,6 +992,25 @@ struct gw_handle {
         a.r_base = r_base;
         a.batch_occ = d_tmp + 1;
         a.fmt = buf_fmt;
+        // narrow records of two-pass tables: k_rgn_apply_nar over super-regions of F regions
+        // (GW_NAR_F = 1, 2 or 4, default 2; GW_NAR2=0 keeps k_rgn_apply), while P2's (super-region,
+        // ring position) buckets fit a descriptor row
+        static const int nar_f = [] {
+            const char* e = getenv("GW_NAR_F");
+            const int f = e ? atoi(e) : 2;
+            return f >= 4 ? 2 : f >= 2 ? 1 : 0;
+        }();
+        static const bool nar2_off = [] { const char* e = getenv("GW_NAR2"); return e && atoi(e) == 0; }();
+        a.nar2 = 0;
+        a.sr_bits = 0;
+        if (buf_fmt == 2 && a.d2_bits > 0 && !nar2_off && tv.ring <= 8) {
+            int sr = std::min(nar_f, a.d2_bits);
+            while (a.d2_bits - sr > 5) ++sr;  // (super-region << 3 | position) < kPartBuckets
+            if (sr <= 2) {
+                a.nar2 = 1;
+                a.sr_bits = sr;
+            }
+        }
     }
 
     // Compact region records (gw_pane.hip cmp_pack): integer aggregates whose ring
@@ -1294,6 +1313,35 @@ struct gw_handle {
         hipFree(dh_);
         khm_used += (int64_t)out[2];
         if (out[3]) return fail(GW_E_INVALID, "snapshot: a key with two different key hashes");
+        return GW_OK;
+    }
+
+    // A restored blob's (key, hash) pairs, checked on the host before anything changes: one
+    // hash per key within the blob and the same hash as the map already holds for that key.
+    int khm_check_host(const std::vector<int64_t>& keys, const std::vector<int32_t>& hashes) {
+        if (keys.empty()) return GW_OK;
+        std::vector<std::pair<int64_t, int32_t>> kv(keys.size());
+        for (size_t i = 0; i < keys.size(); ++i) kv[i] = {keys[i], hashes[i]};
+        std::sort(kv.begin(), kv.end());
+        for (size_t i = 1; i < kv.size(); ++i)
+            if (kv[i].first == kv[i - 1].first && kv[i].second != kv[i - 1].second)
+                return fail(GW_E_INVALID, "snapshot: a key with two different key hashes");
+        if (!khm_used) return GW_OK;
+        KhmHost kh;
+        int rc = khm_host(kh);
+        if (rc) return rc;
+        for (const auto& e : kv) {
+            bool known = false;
+            int32_t h0 = 0;
+            if (e.first == kEmptyKey) {
+                known = kh.has_min;
+                h0 = kh.min_hash;
+            } else {
+                auto it = std::lower_bound(kh.kv.begin(), kh.kv.end(), std::make_pair(e.first, INT32_MIN));
+                if (it != kh.kv.end() && it->first == e.first) { known = true; h0 = it->second; }
+            }
+            if (known && h0 != e.second) return fail(GW_E_INVALID, "snapshot: a key with two different key hashes");
+        }
         return GW_OK;
     }
 
@@ -1665,7 +1713,11 @@ struct gw_handle {
 
     // Restore one heap-layout blob (any key-group range; several calls after rescaling).
     // Only before the first record or watermark, as initializeState runs before processing.
-    int restore_heap(const void* buf, int64_t len) {
+    // The blob is parsed and checked whole (windows, counts, key hashes against each other
+    // and against the keys the handle already knows) before anything changes, so a rejected
+    // blob leaves the handle as it was; `dry` stops there (composite handles check every
+    // class's part before restoring any).
+    int restore_heap(const void* buf, int64_t len, bool dry = false) {
         if (!buf || len < (int64_t)sizeof(SnapHeader)) return fail(GW_E_INVALID, "snapshot blob too short");
         SnapHeader hd;
         memcpy(&hd, buf, sizeof hd);
@@ -1683,63 +1735,53 @@ struct gw_handle {
         const uint8_t* end = p + hd.entries;
         const int ab = acc_bytes();
         const int hb = (hd.flags & kSnapKeyHashes) ? 4 : 0;
-        const size_t first = ov_pending.size();
+        std::vector<OvEntry> pend;  // the blob's entries, appended to ov_pending once all is checked
         std::vector<int64_t> hkeys;  // (key, hash) of a hashed blob's entries
         std::vector<int32_t> hvals;
-        // a blob rejected part-way leaves the handle as it was (the entries parsed so far go)
-#define NEED(x) do { if ((int64_t)(x) > end - p) { ov_pending.resize(first); return fail(GW_E_INVALID, "truncated snapshot blob"); } } while (0)
+        auto by_key_k = [](const OvEntry& x, const OvEntry& y) { return x.key != y.key ? x.key < y.key : x.k < y.k; };
+#define NEED(x) do { if ((x) < 0 || (int64_t)(x) > end - p) return fail(GW_E_INVALID, "truncated snapshot blob"); } while (0)
         for (int64_t g = 0; g < nk; ++g) {
             NEED(4);
             const int32_t ns = rd32(p); p += 4;
-            const size_t base = ov_pending.size();
+            NEED((int64_t)ns * (24 + hb + ab));
+            const size_t base = pend.size();
             for (int32_t i = 0; i < ns; ++i) {
-                NEED(24 + hb + ab);
                 const int64_t s0 = rd64(p), e0 = rd64(p + 8), key = rd64(p + 16);
                 const i128 k = floor_div((i128)s0 - cfg.offset, (i128)slide());
-                if (win_start(k) != (i128)s0 || (i128)s0 + size() != (i128)e0) {
-                    ov_pending.resize(first);
+                if (win_start(k) != (i128)s0 || (i128)s0 + size() != (i128)e0)
                     return fail(GW_E_INVALID, "snapshot window [%lld, %lld) is not a window of this assigner",
                                 (long long)s0, (long long)e0);
-                }
                 OvEntry e{key, (int64_t)k, 0, 0, 0};
                 if (hb) {
                     hkeys.push_back(key);
                     hvals.push_back(rd32(p + 24));
                 }
                 acc_from_be(p + 24 + hb, e.a0, e.a1);
-                ov_pending.push_back(e);
+                pend.push_back(e);
                 p += 24 + hb + ab;
             }
             NEED(4);
-            if (rd32(p) != 0) {
-                ov_pending.resize(first);
-                return fail(GW_E_INVALID, "merging window set in a tumbling / sliding snapshot");
-            }
+            if (rd32(p) != 0) return fail(GW_E_INVALID, "merging window set in a tumbling / sliding snapshot");
             p += 4;
             NEED(4);
             const int32_t nt = rd32(p); p += 4;
             NEED((int64_t)nt * 32);
             // an event-time timer at the window's maxTimestamp: the window has not fired
-            std::sort(ov_pending.begin() + base, ov_pending.end(), [](const OvEntry& x, const OvEntry& y) {
-                return x.key != y.key ? x.key < y.key : x.k < y.k;
-            });
+            std::sort(pend.begin() + base, pend.end(), by_key_k);
             for (int32_t i = 0; i < nt; ++i, p += 32) {
                 const int64_t ts = (int64_t)((uint64_t)rd64(p) ^ 0x8000000000000000ull);
                 const int64_t key = rd64(p + 8), s0 = rd64(p + 16), e0 = rd64(p + 24);
                 if (ts != (int64_t)((uint64_t)e0 - 1)) continue;  // cleanup timer: implied by the state
                 const int64_t k = (int64_t)floor_div((i128)s0 - cfg.offset, (i128)slide());
-                auto it = std::lower_bound(ov_pending.begin() + base, ov_pending.end(), OvEntry{key, k, 0, 0, 0},
-                                           [](const OvEntry& x, const OvEntry& y) {
-                                               return x.key != y.key ? x.key < y.key : x.k < y.k;
-                                           });
-                if (it != ov_pending.end() && it->key == key && it->k == k) it->flags |= kOvTimer;
+                auto it = std::lower_bound(pend.begin() + base, pend.end(), OvEntry{key, k, 0, 0, 0}, by_key_k);
+                if (it != pend.end() && it->key == key && it->k == k) it->flags |= kOvTimer;
             }
         }
 #undef NEED
-        if (p != end) {
-            ov_pending.resize(first);
-            return fail(GW_E_INVALID, "snapshot blob has trailing bytes");
-        }
+        if (p != end) return fail(GW_E_INVALID, "snapshot blob has trailing bytes");
+        int rc = khm_check_host(hkeys, hvals);
+        if (rc || dry) return rc;
+        ov_pending.insert(ov_pending.end(), pend.begin(), pend.end());
         return khm_insert_host(hkeys, hvals);
     }
 
@@ -1805,7 +1847,7 @@ struct gw_handle {
         return GW_OK;
     }
 
-    int restore_sessions(const void* buf, int64_t len) {
+    int restore_sessions(const void* buf, int64_t len, bool dry = false) {
         if (!buf || len < (int64_t)sizeof(SnapHeader)) return fail(GW_E_INVALID, "snapshot blob too short");
         SnapHeader hd;
         memcpy(&hd, buf, sizeof hd);
@@ -1836,7 +1878,9 @@ struct gw_handle {
                 hvals.push_back((int32_t)hw);
             }
         }
-        int rc = session_restore(sess, ent.data(), hd.entries, err);
+        int rc = khm_check_host(hkeys, hvals);  // before the table changes
+        if (rc || dry) return rc;
+        rc = session_restore(sess, ent.data(), hd.entries, err);
         if (rc) return fail(rc, "%s", err.c_str());
         return khm_insert_host(hkeys, hvals);
     }
@@ -3000,7 +3044,11 @@ static int comp_snapshot(gw_handle* h, int32_t kg_lo, int32_t kg_hi, void* buf, 
     return GW_OK;
 }
 
-static int comp_restore(gw_handle* h, const void* buf, int64_t len) {
+static int restore_any(gw_handle* h, const void* buf, int64_t len, bool dry);
+
+// Window classes: the blob is cut into one part per class; every part is checked (a dry
+// restore) before any class restores, so a rejected blob leaves every class as it was.
+static int comp_restore(gw_handle* h, const void* buf, int64_t len, bool dry) {
     if (!buf || len < (int64_t)sizeof(SnapHdr)) return h->fail(GW_E_INVALID, "snapshot blob too short");
     SnapHdr hd;
     memcpy(&hd, buf, sizeof hd);
@@ -3054,8 +3102,7 @@ static int comp_restore(gw_handle* h, const void* buf, int64_t len) {
         }
     }
     if (p != end) return h->fail(GW_E_INVALID, "snapshot blob has trailing bytes");
-    std::vector<size_t> had(J);  // a class rejecting its part undoes the classes restored before it
-    for (int64_t j = 0; j < J; ++j) had[j] = h->kids[j]->ov_pending.size();
+    std::vector<std::vector<uint8_t>> blobs(J);
     for (int64_t j = 0; j < J; ++j) {
         offs[j][nk] = (int64_t)pay[j].size();
         SnapHdr kh = hd;
@@ -3063,15 +3110,18 @@ static int comp_restore(gw_handle* h, const void* buf, int64_t len) {
         kh.slide = h->kids[j]->cfg.slide;
         kh.offset = h->kids[j]->cfg.offset;
         kh.entries = (int64_t)pay[j].size();
-        std::vector<uint8_t> blob(sizeof kh + (nk + 1) * 8 + pay[j].size());
+        std::vector<uint8_t>& blob = blobs[j];
+        blob.resize(sizeof kh + (nk + 1) * 8 + pay[j].size());
         memcpy(blob.data(), &kh, sizeof kh);
         memcpy(blob.data() + sizeof kh, offs[j].data(), (size_t)(nk + 1) * 8);
         if (!pay[j].empty()) memcpy(blob.data() + sizeof kh + (nk + 1) * 8, pay[j].data(), pay[j].size());
-        const int rc = gw_restore(h->kids[j], blob.data(), (int64_t)blob.size());
-        if (rc) {
-            for (int64_t q = 0; q < j; ++q) h->kids[q]->ov_pending.resize(had[q]);
-            return kid_rc(h, h->kids[j], rc);
-        }
+        const int rc = restore_any(h->kids[j], blob.data(), (int64_t)blob.size(), true);
+        if (rc) return kid_rc(h, h->kids[j], rc);
+    }
+    if (dry) return GW_OK;
+    for (int64_t j = 0; j < J; ++j) {  // checked above: only a device error can fail here
+        const int rc = restore_any(h->kids[j], blobs[j].data(), (int64_t)blobs[j].size(), false);
+        if (rc) return kid_rc(h, h->kids[j], rc);
     }
     return GW_OK;
 }
@@ -3204,7 +3254,7 @@ static int fe_snapshot(gw_handle* h, int32_t kg_lo, int32_t kg_hi, void* buf, in
     return GW_OK;
 }
 
-static int fe_restore(gw_handle* h, const void* buf, int64_t len) {
+static int fe_restore(gw_handle* h, const void* buf, int64_t len, bool dry) {
     if (!buf || len < (int64_t)sizeof(SnapHdr)) return h->fail(GW_E_INVALID, "snapshot blob too short");
     SnapHdr hd;
     memcpy(&hd, buf, sizeof hd);
@@ -3259,6 +3309,26 @@ static int fe_restore(gw_handle* h, const void* buf, int64_t len) {
     if (p != end) return h->fail(GW_E_INVALID, "snapshot blob has trailing bytes");
     oa[nk] = (int64_t)pa.size();
     ob[nk] = (int64_t)pb.size();
+    // the two operators' blobs, each checked (a dry restore: header, windows, counts, key
+    // hashes, restore before processing) before the log or any operator changes
+    std::vector<uint8_t> blobs[2];
+    for (int w = 0; w < (h->fe_by ? 1 : 2); ++w) {
+        std::vector<uint8_t>& pl = w ? pb : pa;
+        std::vector<int64_t>& of = w ? ob : oa;
+        SnapHdr kh = hd;
+        kh.flags &= ~kSnapFirstElement;
+        kh.agg = w ? GW_MIN_I64 : h->cfg.agg;
+        kh.entries = (int64_t)pl.size();
+        std::vector<uint8_t>& blob = blobs[w];
+        blob.resize(sizeof kh + (size_t)(nk + 1) * 8 + pl.size());
+        memcpy(blob.data(), &kh, sizeof kh);
+        memcpy(blob.data() + sizeof kh, of.data(), (size_t)(nk + 1) * 8);
+        if (!pl.empty()) memcpy(blob.data() + sizeof kh + (nk + 1) * 8, pl.data(), pl.size());
+        gw_handle* kid = w ? B : A;
+        const int rc = restore_any(kid, blob.data(), (int64_t)blob.size(), true);
+        if (rc) return kid_rc(h, kid, rc);
+    }
+    if (dry) return GW_OK;
     // the payloads enter the log as one batch released once every restored window is cleaned
     const int64_t m = (int64_t)pays.size();
     if (m) {
@@ -3279,19 +3349,9 @@ static int fe_restore(gw_handle* h, const void* buf, int64_t len) {
         // released like a batch whose records reach the latest restored window: maxTs + size - 1 = its end - 1
         h->fe_batches.push_back({h->fe_seq, 0, max_end - h->cfg.size, true});
     }
-    for (int w = 0; w < (h->fe_by ? 1 : 2); ++w) {
-        std::vector<uint8_t>& pl = w ? pb : pa;
-        std::vector<int64_t>& of = w ? ob : oa;
-        SnapHdr kh = hd;
-        kh.flags &= ~kSnapFirstElement;
-        kh.agg = w ? GW_MIN_I64 : h->cfg.agg;
-        kh.entries = (int64_t)pl.size();
-        std::vector<uint8_t> blob(sizeof kh + (size_t)(nk + 1) * 8 + pl.size());
-        memcpy(blob.data(), &kh, sizeof kh);
-        memcpy(blob.data() + sizeof kh, of.data(), (size_t)(nk + 1) * 8);
-        if (!pl.empty()) memcpy(blob.data() + sizeof kh + (nk + 1) * 8, pl.data(), pl.size());
+    for (int w = 0; w < (h->fe_by ? 1 : 2); ++w) {  // checked above: only a device error can fail here
         gw_handle* kid = w ? B : A;
-        const int rc = gw_restore(kid, blob.data(), (int64_t)blob.size());
+        const int rc = restore_any(kid, blobs[w].data(), (int64_t)blobs[w].size(), false);
         if (rc) return kid_rc(h, kid, rc);
     }
     return GW_OK;
@@ -3307,14 +3367,18 @@ int gw_snapshot(gw_handle* h, int32_t kg_lo, int32_t kg_hi, void* buf, int64_t c
     return h->snapshot_heap(kg_lo, kg_hi, buf, cap, len);
 }
 
-int gw_restore(gw_handle* h, const void* buf, int64_t len) {
-    if (!h) return GW_E_INVALID;
-    if (h->fe) return fe_restore(h, buf, len);
-    if (!h->kids.empty()) return comp_restore(h, buf, len);
+static int restore_any(gw_handle* h, const void* buf, int64_t len, bool dry) {
+    if (h->fe) return fe_restore(h, buf, len, dry);
+    if (!h->kids.empty()) return comp_restore(h, buf, len, dry);
     if (h->failed) return h->fail(GW_E_STATE, "operator failed earlier: %s", h->err.c_str());
     hipSetDevice(h->cfg.device);
-    if (h->session) return h->restore_sessions(buf, len);
-    return h->restore_heap(buf, len);
+    if (h->session) return h->restore_sessions(buf, len, dry);
+    return h->restore_heap(buf, len, dry);
+}
+
+int gw_restore(gw_handle* h, const void* buf, int64_t len) {
+    if (!h) return GW_E_INVALID;
+    return restore_any(h, buf, len, false);
 }
 
 // The blob layout is gw_handle::SnapHeader (96 bytes: kg_lo at 60, kg_hi at 64, reserved at
@@ -3882,6 +3946,29 @@ int gw_kernel_time_ms(gw_handle* h, int which, double* ms, int64_t* launches) {
     if (launches) *launches = t.launches;
     t.total_ms = 0;
     t.launches = 0;
+    return GW_OK;
+}
+
+// ---------------------------------------------------------------- window stagger
+int gw_window_stagger_offset(int32_t stagger, int64_t processing_time, double random01, int64_t size,
+                             int64_t global_offset, int64_t* offset_out) {
+    if (!offset_out || size <= 0 || global_offset <= -size || global_offset >= size) return GW_E_INVALID;
+    int64_t st = 0;
+    switch (stagger) {
+    case GW_STAGGER_ALIGNED: break;
+    case GW_STAGGER_RANDOM:  // (long) (ThreadLocalRandom.current().nextDouble() * size)
+        if (!(random01 >= 0.0 && random01 < 1.0)) return GW_E_INVALID;
+        st = (int64_t)(random01 * (double)size);
+        break;
+    case GW_STAGGER_NATURAL: {  // currentProcessingTime - getWindowStartWithOffset(currentProcessingTime, 0, size)
+        const int64_t rem = processing_time % size;
+        const int64_t start = processing_time - (rem < 0 ? rem + size : rem);
+        st = std::max<int64_t>(0, processing_time - start);
+        break;
+    }
+    default: return GW_E_INVALID;
+    }
+    *offset_out = (global_offset + st) % size;  // both terms within (-size, size): no overflow
     return GW_OK;
 }
 

@@ -22,6 +22,7 @@ from __future__ import annotations
 
 import ctypes
 import struct
+import time
 from dataclasses import dataclass
 from typing import Any, Callable, Iterable, List, Optional
 
@@ -58,18 +59,37 @@ class WindowAssigner:
         raise NotImplementedError
 
 
-class TumblingEventTimeWindows(WindowAssigner):
-    """TumblingEventTimeWindows.of(size[, offset]) — stagger ALIGNED."""
-    kind = "tumbling"
-
-    def __init__(self, size: int, offset: int = 0):
-        if abs(offset) >= size:  # TumblingEventTimeWindows.java:55-62
-            raise ValueError("TumblingEventTimeWindows parameters must satisfy abs(offset) < size")
-        self.size, self.offset = int(size), int(offset)
+class WindowStagger:
+    """WindowStagger (RS/api/windowing/assigners/WindowStagger.java:27-60): ALIGNED (0), RANDOM
+    (U(0, size)) or NATURAL (the processing time's offset into its window), drawn at the first
+    element; gw_window_stagger_offset computes the resulting window offset."""
+    ALIGNED, RANDOM, NATURAL = 0, 1, 2
 
     @staticmethod
-    def of(size: int, offset: int = 0) -> "TumblingEventTimeWindows":
-        return TumblingEventTimeWindows(size, offset)
+    def window_offset(stagger: int, processing_time: int, size: int, global_offset: int,
+                      random01: Optional[float] = None) -> int:
+        """(global_offset + stagger offset) % size, as TumblingEventTimeWindows.assignWindows
+        uses it (TumblingEventTimeWindows.java:72-79)."""
+        import random
+        r = random.random() if random01 is None else float(random01)
+        out = ctypes.c_int64(0)
+        N.check(N.lib().gw_window_stagger_offset(int(stagger), int(processing_time), r, int(size), int(global_offset),
+                                                 ctypes.byref(out)))
+        return out.value
+
+
+class TumblingEventTimeWindows(WindowAssigner):
+    """TumblingEventTimeWindows.of(size[, offset[, stagger]])."""
+    kind = "tumbling"
+
+    def __init__(self, size: int, offset: int = 0, stagger: int = WindowStagger.ALIGNED):
+        if abs(offset) >= size:  # TumblingEventTimeWindows.java:55-62
+            raise ValueError("TumblingEventTimeWindows parameters must satisfy abs(offset) < size")
+        self.size, self.offset, self.stagger = int(size), int(offset), int(stagger)
+
+    @staticmethod
+    def of(size: int, offset: int = 0, stagger: int = WindowStagger.ALIGNED) -> "TumblingEventTimeWindows":
+        return TumblingEventTimeWindows(size, offset, stagger)
 
     def config(self):
         return dict(assigner="tumbling", size=self.size, slide=self.size, offset=self.offset)
@@ -228,7 +248,8 @@ class GpuWindowOperator:
     def __init__(self, assigner: WindowAssigner, aggregate: str, allowed_lateness: int = 0,
                  trigger=None, key_selector: Callable = None, value_selector: Callable = None,
                  max_parallelism: int = 128, parallelism: int = 1, operator_index: int = 0,
-                 device: int = 0, capacity_hint: int = 0, max_batch: int = 1 << 22, flags: int = 0):
+                 device: int = 0, capacity_hint: int = 0, max_batch: int = 1 << 22, flags: int = 0,
+                 window_function: Optional[Callable] = None, processing_time: Optional[Callable[[], int]] = None):
         if aggregate not in N.AGGS:
             raise ValueError(f"unknown aggregate {aggregate!r}")
         if allowed_lateness < 0:
@@ -266,9 +287,30 @@ class GpuWindowOperator:
         self._elems: list = []
         self._buf_p: List[int] = []
         self.output: list = []
+        # reduce / aggregate(..., ProcessWindowFunction): window_function(key, (start, end), [result],
+        # out) per fired window, out a list the emitted values go to (InternalSingleValueProcess-
+        # WindowFunction: a one-element Iterable of the pre-aggregated result, output stamped
+        # window.maxTimestamp())
+        self.window_function = window_function
+        # processing-time clock in ms (ProcessingTimeService.getCurrentProcessingTime): a staggered
+        # tumbling assigner draws its stagger at the first element
+        self.processing_time = processing_time or (lambda: time.time_ns() // 1_000_000)
+        self._stagger = getattr(assigner, "stagger", WindowStagger.ALIGNED)
+        self._deferred = False        # staggered: the handle is created at the first element
+        self._deferred_wm = LONG_MIN  # watermarks seen before it
+        self._stagger_time = None
 
     # lifecycle -------------------------------------------------------------
     def open(self):
+        if self._stagger != WindowStagger.ALIGNED:
+            # TumblingEventTimeWindows draws its stagger at the first element (:72-79): the
+            # handle, whose windows need the offset, is created then
+            WindowStagger.window_offset(self._stagger, 0, self.cfg.size, self.cfg.offset, 0.0)  # validates
+            self._deferred = True
+            return self
+        return self._create()
+
+    def _create(self):
         h = ctypes.c_void_p()
         rc = N.lib().gw_create(ctypes.byref(self.cfg), ctypes.byref(h))
         if rc == -1:
@@ -276,6 +318,19 @@ class GpuWindowOperator:
         N.check(rc, None)
         self._h = h
         return self
+
+    def _ensure_handle(self):
+        """A staggered operator's first element: draw the stagger at the processing time the
+        first element arrived, create the handle with (offset + stagger) % size, replay the
+        watermark seen so far (no state yet: it fires nothing)."""
+        if not self._deferred:
+            return
+        now = self._stagger_time if self._stagger_time is not None else self.processing_time()
+        self.cfg.offset = WindowStagger.window_offset(self._stagger, now, self.cfg.size, self.cfg.offset)
+        self._deferred = False
+        self._create()
+        if self._deferred_wm != LONG_MIN:
+            self.advance_watermark(self._deferred_wm)
 
     def close(self):
         if self._h:
@@ -320,6 +375,8 @@ class GpuWindowOperator:
 
     # record-at-a-time surface (StreamRecord / Watermark) ----------------------
     def process_element(self, record: StreamRecord):
+        if self._deferred and self._stagger_time is None:
+            self._stagger_time = self.processing_time()  # the stagger is drawn at the first element
         v = record.value
         self._buf_k.append(self._encode_key(self.key_selector(v)))
         self._buf_t.append(int(record.timestamp))
@@ -363,7 +420,13 @@ class GpuWindowOperator:
         k, s, e, r = self.drain()
         for i in range(len(k)):
             res = r[i]
-            self.output.append(StreamRecord((self._decode_key(int(k[i])), int(s[i]), int(e[i]), res), int(e[i]) - 1))
+            key, start, end = self._decode_key(int(k[i])), int(s[i]), int(e[i])
+            if self.window_function is not None:
+                out: list = []
+                self.window_function(key, (start, end), [res], out)
+                self.output.extend(StreamRecord(x, end - 1) for x in out)
+            else:
+                self.output.append(StreamRecord((key, start, end, res), end - 1))
         self.output.append(Watermark(ts))
 
     def end_input(self):
@@ -377,6 +440,7 @@ class GpuWindowOperator:
     # columnar surface ------------------------------------------------------------
     def process_batch(self, keys: np.ndarray, timestamps: np.ndarray, values: Optional[np.ndarray] = None,
                       key_hashes: Optional[np.ndarray] = None):
+        self._ensure_handle()
         keys = np.ascontiguousarray(keys, dtype=np.int64)
         timestamps = np.ascontiguousarray(timestamps, dtype=np.int64)
         if values is not None:
@@ -396,6 +460,7 @@ class GpuWindowOperator:
         """Records with a 64-bit payload each (the Tuple's non-aggregated fields, packed by the
         caller); rows carry the payload of their window's first element in arrival order, as
         SumAggregator / ComparableAggregator keep it (gw_ingest_payload)."""
+        self._ensure_handle()
         keys = np.ascontiguousarray(keys, dtype=np.int64)
         timestamps = np.ascontiguousarray(timestamps, dtype=np.int64)
         values = np.ascontiguousarray(values)
@@ -410,6 +475,7 @@ class GpuWindowOperator:
 
     def process_batch_payload_device(self, keys, timestamps, values, payload, stream=None):
         """Same, with torch device columns produced on `stream` (default: torch's current)."""
+        self._ensure_handle()
         if stream is None:
             import torch
             stream = torch.cuda.current_stream(keys.device).cuda_stream
@@ -436,6 +502,7 @@ class GpuWindowOperator:
         watermarks) on the GPU (gw_ingest_serialized).  Returns (consumed, rows_fired):
         bytes past `consumed` belong to an element spanning into the next buffer and must
         be passed again, prepended to it."""
+        self._ensure_handle()
         consumed, fired = ctypes.c_int64(0), ctypes.c_int64(0)
         buf = ctypes.create_string_buffer(bytes(data), len(data)) if data else None
         N.check(N.lib().gw_ingest_serialized(self._h, buf, len(data), ctypes.byref(layout), ctypes.byref(consumed),
@@ -444,6 +511,7 @@ class GpuWindowOperator:
 
     def process_serialized_device(self, data, layout: "N.GwRecordLayout", stream=None) -> tuple:
         """Same, with the bytes in a device uint8 tensor."""
+        self._ensure_handle()
         if stream is None:
             import torch
             stream = torch.cuda.current_stream(data.device).cuda_stream
@@ -470,6 +538,7 @@ class GpuWindowOperator:
 
     def process_batch_device(self, keys, timestamps, values=None, stream=None):
         """Columns already in HBM (torch tensors or raw device pointers)."""
+        self._ensure_handle()
         def p(x):
             if x is None:
                 return None
@@ -485,12 +554,16 @@ class GpuWindowOperator:
         N.check(rc, self._h)
 
     def process_batch_device_ptr(self, n: int, key_ptr: int, ts_ptr: int, val_ptr: Optional[int], stream=None):
+        self._ensure_handle()
         rc = N.lib().gw_ingest_device(self._h, n, ctypes.c_void_p(key_ptr), None, ctypes.c_void_p(ts_ptr),
                                       ctypes.c_void_p(val_ptr) if val_ptr else None,
                                       ctypes.c_void_p(stream) if stream else None)
         N.check(rc, self._h)
 
     def advance_watermark(self, wm: int) -> int:
+        if self._deferred:  # staggered, no element yet: nothing can fire
+            self._deferred_wm = max(self._deferred_wm, int(wm))
+            return 0
         fired = ctypes.c_int64(0)
         N.check(N.lib().gw_advance_watermark(self._h, int(wm), ctypes.byref(fired)), self._h)
         return fired.value
@@ -498,6 +571,8 @@ class GpuWindowOperator:
     def flush(self):
         """Apply every buffered record to the window state (gw_flush); firing does this
         by itself, a snapshot or a timing boundary calls it explicitly."""
+        if self._deferred:
+            return
         N.check(N.lib().gw_flush(self._h), self._h)
 
     # checkpointing ----------------------------------------------------------------
@@ -505,6 +580,15 @@ class GpuWindowOperator:
         """Keyed window state of the key groups [lo, hi] (default: all), as one blob
         (StreamOperator.snapshotState; restore with initialize_state)."""
         lo, hi = key_group_range if key_group_range is not None else (0, self.cfg.max_parallelism - 1)
+        if self._deferred:  # staggered, no element yet: no window state
+            tmp = GpuWindowOperator(TumblingEventTimeWindows.of(self.cfg.size, self.cfg.offset), self.aggregate,
+                                    self.cfg.allowed_lateness, self.trigger, max_parallelism=self.cfg.max_parallelism,
+                                    device=self.cfg.device, capacity_hint=16, max_batch=16,
+                                    flags=self.cfg.flags).open()
+            try:
+                return tmp.snapshot_state(key_group_range)
+            finally:
+                tmp.close()
         n = ctypes.c_int64(0)
         N.check(N.lib().gw_snapshot(self._h, lo, hi, None, 0, ctypes.byref(n)), self._h)
         buf = ctypes.create_string_buffer(n.value)
@@ -518,6 +602,9 @@ class GpuWindowOperator:
         operator's dictionary first."""
         if isinstance(blobs, (bytes, bytearray)):
             blobs = [blobs]
+        if self._deferred:
+            raise N.GpuWinError(N.GW_E_UNSUPPORTED, "restoring window state into a staggered tumbling operator: "
+                                "the restored windows keep their alignment while a new stagger is drawn")
         for b in blobs:
             b = bytes(b)
             if b[:4] == KEYED_MAGIC:
@@ -541,6 +628,8 @@ class GpuWindowOperator:
         return N.snapshot_remap_keys(blob, {i: self._encode_key(k) for i, k in keys.items()})
 
     def pending_rows(self) -> int:
+        if self._deferred:
+            return 0
         n = ctypes.c_int64(0)
         N.check(N.lib().gw_pending_rows(self._h, ctypes.byref(n)), self._h)
         return n.value
@@ -562,6 +651,8 @@ class GpuWindowOperator:
         return k, s, e, r
 
     def clear_rows(self):
+        if self._deferred:
+            return
         N.check(N.lib().gw_clear_rows(self._h), self._h)
 
     def rows_device(self):
@@ -574,6 +665,8 @@ class GpuWindowOperator:
     def drain_late(self):
         """The late-data side output (flags=FLAG_LATE_SIDE_OUTPUT, WindowedStream.sideOutputLateData):
         the late records since the last call, as (key, timestamp, value bits) numpy columns."""
+        if self._deferred:
+            return tuple(np.empty(0, np.int64) for _ in range(3))
         n = ctypes.c_int64(0)
         N.check(N.lib().gw_pending_late(self._h, ctypes.byref(n)), self._h)
         k, t, v = (np.empty(n.value, np.int64) for _ in range(3))
@@ -585,10 +678,12 @@ class GpuWindowOperator:
 
     @property
     def num_late_records_dropped(self) -> int:
-        return N.lib().gw_late_dropped(self._h)
+        return 0 if self._deferred else N.lib().gw_late_dropped(self._h)
 
     def stats(self) -> dict:
         s = N.GwStats()
+        if self._deferred:
+            return s.as_dict()
         N.check(N.lib().gw_get_stats(self._h, ctypes.byref(s)), self._h)
         return s.as_dict()
 
@@ -605,6 +700,8 @@ class GpuWindowOperator:
         return ms.value, n.value
 
     def synchronize(self):
+        if self._deferred:
+            return
         N.check(N.lib().gw_synchronize(self._h), self._h)
 
 
@@ -630,9 +727,11 @@ class WindowedStream:
         self._trigger = trig
         return self
 
-    def _op(self, agg, field, flags=0):
+    def _op(self, agg, field, flags=0, window_function=None):
         kw = dict(self.keyed.env.op_kwargs)
         kw["flags"] = kw.get("flags", 0) | flags
+        if window_function is not None:
+            kw["window_function"] = window_function
         return GpuWindowOperator(self.assigner, agg, self._lateness, self._trigger, self.keyed.key_selector,
                                  (lambda v: v[field]) if field is not None else (lambda v: 0), **kw)
 
@@ -646,6 +745,16 @@ class WindowedStream:
     def max(self, field: int, kind: str = "i64") -> "DataStreamResult":
         return DataStreamResult(self, self._op(f"max_{kind}", field))
 
+    # reduce / aggregate with a window function (WindowedStream.java:224-276, 342-526): the
+    # pre-aggregated result of each fired window goes through window_function(key, (start, end),
+    # [result], out); `reduce` names the built-in ReduceFunction of the closed set ("sum_i64", ...)
+    def reduce(self, function: str, field: int, window_function: Optional[Callable] = None) -> "DataStreamResult":
+        return DataStreamResult(self, self._op(function, field, window_function=window_function))
+
+    def process(self, function: str, field: Optional[int], window_function: Callable) -> "DataStreamResult":
+        """aggregate(AggregateFunction, ProcessWindowFunction) with the closed-set aggregate."""
+        return DataStreamResult(self, self._op(function, field, window_function=window_function))
+
     # WindowedStream.minBy / maxBy (:725-771): the element with the smallest / largest field,
     # the first of equal ones (first=True) or the last
     def min_by(self, field: int, first: bool = True, kind: str = "i64") -> "DataStreamResult":
@@ -657,8 +766,9 @@ class WindowedStream:
     minBy = min_by
     maxBy = max_by
 
-    def aggregate(self, function: str, field: Optional[int] = None) -> "DataStreamResult":
-        return DataStreamResult(self, self._op(function, field))
+    def aggregate(self, function: str, field: Optional[int] = None,
+                  window_function: Optional[Callable] = None) -> "DataStreamResult":
+        return DataStreamResult(self, self._op(function, field, window_function=window_function))
 
     def count(self) -> "DataStreamResult":
         return DataStreamResult(self, self._op("count", None))

@@ -362,6 +362,20 @@ void* gw_stream(gw_handle* h);
 int  gw_kernel_time_ms(gw_handle* h, int which, double* ms, int64_t* launches);
 int  gw_enable_kernel_timing(gw_handle* h, int enable);
 
+/* ---- window stagger (stateless) ------------------------------------------ */
+/* WindowStagger (RS/api/windowing/assigners/WindowStagger.java:27-60) applied to a tumbling
+ * assigner's global offset as TumblingEventTimeWindows.assignWindows does at the first
+ * element (TumblingEventTimeWindows.java:72-79): *offset_out = (global_offset + stagger) % size
+ * (Java remainder), the offset to create the operator with.  stagger = 0 (ALIGNED),
+ * (long)(random01 * size) (RANDOM: random01 is the caller's ThreadLocalRandom.nextDouble()),
+ * or max(0, processing_time - TimeWindow.getWindowStartWithOffset(processing_time, 0, size))
+ * (NATURAL).  GW_E_INVALID for size <= 0, |global_offset| >= size or random01 outside [0, 1). */
+#define GW_STAGGER_ALIGNED 0
+#define GW_STAGGER_RANDOM  1
+#define GW_STAGGER_NATURAL 2
+int  gw_window_stagger_offset(int32_t stagger, int64_t processing_time, double random01, int64_t size,
+                              int64_t global_offset, int64_t* offset_out);
+
 /* ---- key groups (stateless) ---------------------------------------------- */
 int32_t gw_java_long_hash(int64_t key);             /* Long.hashCode                     */
 int32_t gw_murmur_hash(int32_t code);               /* MathUtils.murmurHash              */
@@ -425,6 +439,17 @@ int  gw_exchange_batch(gw_exchange* ex, int64_t n, const int64_t* d_key, const i
 int  gw_exchange_counts(const gw_exchange* ex, int64_t* send, int64_t* recv);
 int  gw_exchange_min_watermark(gw_exchange* ex, int64_t wm, int64_t* out, void* stream);
 const char* gw_exchange_last_error(const gw_exchange* ex);
+/* The per-peer plan gw_exchange_batch runs after its count all-to-all, as a host function
+ * (no device, no communicator): from the messages this rank sent and received --
+ * msg[3q .. 3q+2] = (records, watermark, column mask) for peer q -- the offsets and counts
+ * of every send and receive (send_off[q]: the first record for q in the rank's
+ * owner-partitioned columns; recv_off[q]: where q's records land in the receive columns,
+ * which hold the peers' records in rank order, as all_to_all_single lays them out), the
+ * total received and the minimum watermark over the ranks (StatusWatermarkValve).
+ * GW_E_INVALID when a peer's column mask differs from this rank's. */
+int  gw_exchange_plan(int32_t nranks, const int64_t* sent_msg, const int64_t* recv_msg, int64_t cols_mask,
+                      int64_t wm, int64_t* send_off, int64_t* send_cnt, int64_t* recv_off, int64_t* recv_cnt,
+                      int64_t* total, int64_t* wm_min);
 
 #ifdef __cplusplus
 }

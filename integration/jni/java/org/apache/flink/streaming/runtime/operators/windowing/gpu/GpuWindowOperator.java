@@ -30,6 +30,25 @@
  *                  count, Double for avg), PassThroughWindowFunction.
  *   KEYED_WINDOW   Tuple4 (key, window start, window end, result), what a ProcessWindowFunction
  *                  emitting (key, window, result) produces.
+ *   WINDOW_FUNCTION the user's window function over the pre-aggregated result:
+ *                  reduce(ReduceFunction, ProcessWindowFunction | WindowFunction) and
+ *                  aggregate(AggregateFunction, ProcessWindowFunction | WindowFunction)
+ *                  (WindowedStream.java:224-276, 342-526).  As InternalSingleValueProcessWindowFunction
+ *                  does, the function gets the key, the window and a one-element Iterable of the
+ *                  GPU's result, and emits through a collector stamped window.maxTimestamp().
+ *                  Per-window / global keyed state of the Context is not available
+ *                  (UnsupportedOperationException).
+ *
+ * Aggregates: the closed set of gw_agg (count, sum, min, max, avg over Long / Double fields).
+ * A job whose AggregateFunction / ReduceFunction is anything else keeps the reference
+ * WindowOperator: it cannot be expressed as a gw_agg, and no GpuWindowOperator is created for it.
+ *
+ * Stagger (TumblingEventTimeWindows.of(size, offset, WindowStagger)): the stagger offset is
+ * drawn at the first element, as TumblingEventTimeWindows.assignWindows does
+ * (TumblingEventTimeWindows.java:72-79), so a staggered operator creates its handle then, with
+ * offset (offset + stagger) % size (gw_window_stagger_offset).  Restoring state into a
+ * staggered operator is refused: the reference would keep the restored windows' alignment
+ * beside a newly drawn one, which one handle cannot hold.
  *
  * Keys (K, as WindowOperator<K, ...> at WindowOperator.java:102): Long keys go to the GPU as
  * they are, and the device computes Long.hashCode.  Any other key type (String, Integer,
@@ -43,6 +62,15 @@
 package org.apache.flink.streaming.runtime.operators.windowing.gpu;
 
 import org.apache.flink.api.common.externalresource.ExternalResourceInfo;
+import org.apache.flink.api.common.functions.DefaultOpenContext;
+import org.apache.flink.api.common.functions.util.FunctionUtils;
+import org.apache.flink.api.common.state.KeyedStateStore;
+import org.apache.flink.streaming.api.functions.windowing.ProcessWindowFunction;
+import org.apache.flink.streaming.api.functions.windowing.WindowFunction;
+import org.apache.flink.streaming.api.operators.TimestampedCollector;
+import org.apache.flink.streaming.api.windowing.assigners.WindowStagger;
+import org.apache.flink.streaming.api.windowing.windows.TimeWindow;
+import org.apache.flink.util.Collector;
 import org.apache.flink.api.java.functions.KeySelector;
 import org.apache.flink.api.java.tuple.Tuple;
 import org.apache.flink.api.java.tuple.Tuple2;
@@ -66,9 +94,11 @@ import java.nio.ByteBuffer;
 import java.nio.ByteOrder;
 import java.util.ArrayDeque;
 import java.util.ArrayList;
+import java.util.Collections;
 import java.util.HashMap;
 import java.util.List;
 import java.util.Map;
+import java.util.concurrent.ThreadLocalRandom;
 
 import org.apache.flink.api.common.typeutils.TypeSerializer;
 import org.apache.flink.core.memory.DataInputViewStreamWrapper;
@@ -83,7 +113,7 @@ public class GpuWindowOperator<IN, K>
     static { System.loadLibrary("gpuwin_jni"); }
 
     /** What one fired (key, window, result) row becomes (see the class comment). */
-    public enum OutputMode { POSITIONAL, MIN_MAX_BY, AGGREGATE, KEYED_WINDOW }
+    public enum OutputMode { POSITIONAL, MIN_MAX_BY, AGGREGATE, KEYED_WINDOW, WINDOW_FUNCTION }
 
     // gw_assigner / gw_trigger / gw_agg codes of include/gpuwin.h
     private static final int GW_COUNT_TUMBLING = 3, GW_COUNT_SLIDING = 4;
@@ -97,6 +127,8 @@ public class GpuWindowOperator<IN, K>
     private final int inputArity, positionalField;
     private TypeSerializer<IN> inputSerializer;  // Tuple3+ positional: writes the first elements of a snapshot
     private boolean byFirst = true;              // MIN_MAX_BY: the first of equal elements
+    private WindowStagger stagger = WindowStagger.ALIGNED;  // tumbling only
+    private ProcessWindowFunction<Object, Object, K, TimeWindow> windowFunction;  // WINDOW_FUNCTION
 
     private transient long handle;
     private transient ByteBuffer keys, keyHashes, ts, values, oKey, oStart, oEnd, oRes;
@@ -115,6 +147,12 @@ public class GpuWindowOperator<IN, K>
     private transient ElementLog<IN> elements;
     private transient ArrayDeque<long[]> batches;
     private transient long batchMaxTs;
+    private transient int createFlags;            // gw_config.flags, decided in open()
+    private transient boolean handleDeferred;     // staggered: the handle comes with the first element
+    private transient long deferredWatermark = Long.MIN_VALUE;
+    private transient TimestampedCollector<Object> collector;
+    private transient WindowContext windowContext;
+    private transient long currentWm = Long.MIN_VALUE;  // the watermark the current firing runs at
 
     /** inputArity: fields of the input Tuple; positionalField: the aggregated field of a
      *  POSITIONAL sum/min/max (the result replaces it in the emitted tuple). */
@@ -149,6 +187,40 @@ public class GpuWindowOperator<IN, K>
         return this;
     }
 
+    /** TumblingEventTimeWindows.of(size, offset, stagger): the stagger offset is drawn at the
+     *  first element (TumblingEventTimeWindows.java:72-79). */
+    public GpuWindowOperator<IN, K> withStagger(WindowStagger stagger) {
+        if (stagger != WindowStagger.ALIGNED && assigner != 0 /* tumbling */) {
+            throw new IllegalArgumentException("WindowStagger applies to TumblingEventTimeWindows only");
+        }
+        this.stagger = stagger;
+        return this;
+    }
+
+    /** reduce / aggregate(..., ProcessWindowFunction): the function sees the key, the window and
+     *  the GPU's pre-aggregated result (OutputMode.WINDOW_FUNCTION). */
+    @SuppressWarnings("unchecked")
+    public GpuWindowOperator<IN, K> withWindowFunction(ProcessWindowFunction<?, ?, K, TimeWindow> fn) {
+        if (mode != OutputMode.WINDOW_FUNCTION) {
+            throw new IllegalArgumentException("a window function needs OutputMode.WINDOW_FUNCTION");
+        }
+        this.windowFunction = (ProcessWindowFunction<Object, Object, K, TimeWindow>) fn;
+        return this;
+    }
+
+    /** reduce / aggregate(..., WindowFunction): the legacy apply() form, wrapped like
+     *  InternalSingleValueWindowFunction wraps it. */
+    @SuppressWarnings("unchecked")
+    public GpuWindowOperator<IN, K> withWindowFunction(WindowFunction<?, ?, K, TimeWindow> fn) {
+        final WindowFunction<Object, Object, K, TimeWindow> wf = (WindowFunction<Object, Object, K, TimeWindow>) fn;
+        return withWindowFunction(new ProcessWindowFunction<Object, Object, K, TimeWindow>() {
+            @Override
+            public void process(K key, Context ctx, Iterable<Object> in, Collector<Object> out) throws Exception {
+                wf.apply(key, ctx.window(), in, out);
+            }
+        });
+    }
+
     /** WindowedStream.sideOutputLateData (WindowOperator.java:440-446, 587-588) for a Tuple2<Long, X>
      *  input: skipped late elements come back as (key, value) with their timestamp. */
     public GpuWindowOperator<IN, K> withLateDataOutput(OutputTag<Tuple2<Object, Object>> tag) {
@@ -162,16 +234,24 @@ public class GpuWindowOperator<IN, K>
     @Override
     public void open() throws Exception {
         super.open();
-        int subtask = getRuntimeContext().getTaskInfo().getIndexOfThisSubtask();
         int parallelism = getRuntimeContext().getTaskInfo().getNumberOfParallelSubtasks();
-        int maxP = getRuntimeContext().getTaskInfo().getMaxNumberOfParallelSubtasks();
-        int device = gpuIndex();
-        final int flags = (lateDataTag != null ? 64 /* GW_FLAG_LATE_SIDE_OUTPUT */ : 0)
+        createFlags = (lateDataTag != null ? 64 /* GW_FLAG_LATE_SIDE_OUTPUT */ : 0)
                 | (mode == OutputMode.MIN_MAX_BY ? 512 /* GW_FLAG_BY_FIELD */ | (byFirst ? 0 : 1024 /* GW_FLAG_BY_LAST */)
                         : wide() ? 128 /* GW_FLAG_FIRST_ELEMENT */ : 0)
                 | (parallelism > 1 ? 4 /* GW_FLAG_CHECK_KEY_GROUPS: a foreign key fails the batch */ : 0);
-        handle = nativeCreate(assigner, trigger, size, slide, offset, gap, lateness, agg, maxP, parallelism,
-                              subtask, device, flags, 1L << 24, batchCapacity);
+        if (mode == OutputMode.WINDOW_FUNCTION) {
+            if (windowFunction == null) throw new IllegalStateException("OutputMode.WINDOW_FUNCTION without withWindowFunction(...)");
+            FunctionUtils.setFunctionRuntimeContext(windowFunction, getRuntimeContext());
+            FunctionUtils.openFunction(windowFunction, DefaultOpenContext.INSTANCE);
+            collector = new TimestampedCollector<>(output);
+            windowContext = new WindowContext();
+        }
+        handleDeferred = stagger != WindowStagger.ALIGNED;
+        if (handleDeferred && restored != null && !restored.isEmpty()) {
+            throw new UnsupportedOperationException("restoring window state into a staggered tumbling operator ("
+                    + stagger + "): the restored windows keep their alignment while a new stagger is drawn");
+        }
+        if (!handleDeferred) createHandle(offset);
         if (lateDataTag != null) { lKey = direct(8); lTs = direct(8); lVal = direct(8); }
         if (wide() && inputSerializer == null && getExecutionConfig() != null
                 && getContainingTask().getConfiguration().isCheckpointingEnabled()) {
@@ -193,7 +273,14 @@ public class GpuWindowOperator<IN, K>
                 if (table != null) {  // the blob's key ids -> this subtask's dictionary ids
                     long[] from = nativeSnapshotKeys(blob);
                     long[] to = new long[from.length];
-                    for (int j = 0; j < from.length; j++) to[j] = dictionary().idOf(table.get(from[j]));
+                    for (int j = 0; j < from.length; j++) {
+                        K key = table.get(from[j]);
+                        if (key == null) {
+                            throw new IllegalStateException("restored window state names key id " + from[j]
+                                    + " that its key table does not hold: corrupt checkpoint");
+                        }
+                        to[j] = dictionary().idOf(key);
+                    }
                     nativeRemapKeys(blob, from, to);
                 }
                 Map<Long, IN> firsts = restoredElements.get(i);
@@ -201,7 +288,14 @@ public class GpuWindowOperator<IN, K>
                     long[] maxEnd = new long[1];
                     long[] from = nativeSnapshotPayloads(blob, maxEnd);
                     long[] to = new long[from.length];
-                    for (int j = 0; j < from.length; j++) to[j] = elements.append(firsts.get(from[j]));
+                    for (int j = 0; j < from.length; j++) {
+                        IN first = firsts.get(from[j]);
+                        if (first == null) {
+                            throw new IllegalStateException("restored window state names element " + from[j]
+                                    + " that the checkpoint does not hold: corrupt checkpoint");
+                        }
+                        to[j] = elements.append(first);
+                    }
                     nativeRemapPayloads(blob, from, to);
                     // kept until the latest restored window is cleaned: maxTs + size - 1 = its end - 1
                     batches.addLast(new long[] {elements.end(), maxEnd[0] - size});
@@ -212,6 +306,25 @@ public class GpuWindowOperator<IN, K>
             restoredKeys = null;
             restoredElements = null;
         }
+    }
+
+    /** The handle, with the windows' offset (the stagger decided by the caller). */
+    private void createHandle(long windowOffset) {
+        int subtask = getRuntimeContext().getTaskInfo().getIndexOfThisSubtask();
+        int parallelism = getRuntimeContext().getTaskInfo().getNumberOfParallelSubtasks();
+        int maxP = getRuntimeContext().getTaskInfo().getMaxNumberOfParallelSubtasks();
+        handle = nativeCreate(assigner, trigger, size, slide, windowOffset, gap, lateness, agg, maxP, parallelism,
+                              subtask, gpuIndex(), createFlags, 1L << 24, batchCapacity);
+    }
+
+    /** A staggered operator's first element: draw the stagger (WindowStagger.getStaggerOffset at
+     *  the current processing time), create the handle, replay the watermark seen so far. */
+    private void createStaggeredHandle() {
+        long now = getProcessingTimeService().getCurrentProcessingTime();
+        int code = stagger == WindowStagger.RANDOM ? 1 : stagger == WindowStagger.NATURAL ? 2 : 0;
+        createHandle(nativeStaggerOffset(code, now, ThreadLocalRandom.current().nextDouble(), size, offset));
+        handleDeferred = false;
+        if (deferredWatermark != Long.MIN_VALUE) nativeAdvanceWatermark(handle, deferredWatermark);  // no state: fires nothing
     }
 
     private KeyDictionary<K> dictionary() {
@@ -245,6 +358,19 @@ public class GpuWindowOperator<IN, K>
     public void snapshotState(StateSnapshotContext context) throws Exception {
         super.snapshotState(context);
         KeyGroupRange range = getKeyedStateBackend().getKeyGroupRange();
+        if (handleDeferred) {  // staggered, no element yet: no window state (an empty blob per key group)
+            KeyedStateCheckpointOutputStream out = context.getRawKeyedOperatorStateOutput();
+            for (int kg : range) {
+                out.startNewKeyGroup(kg);
+                DataOutputStream dos = new DataOutputStream(out);
+                dos.writeInt(0);
+                dos.writeBoolean(false);
+                dos.writeInt(0);
+                dos.writeInt(0);
+                dos.flush();
+            }
+            return;
+        }
         byte[] all = nativeSnapshot(handle, range.getStartKeyGroup(), range.getEndKeyGroup());
         KeyedStateCheckpointOutputStream out = context.getRawKeyedOperatorStateOutput();
         @SuppressWarnings("unchecked")
@@ -288,6 +414,7 @@ public class GpuWindowOperator<IN, K>
             DataInputStream in = new DataInputStream(p.getStream());
             byte[] blob = new byte[in.readInt()];
             in.readFully(blob);
+            if (blob.length == 0) continue;  // written by a staggered operator before its first element
             restored.add(blob);
             boolean keyed = in.readBoolean();
             int nk = in.readInt();
@@ -314,6 +441,7 @@ public class GpuWindowOperator<IN, K>
 
     @Override
     public void processElement(StreamRecord<IN> element) throws Exception {
+        if (handleDeferred) createStaggeredHandle();
         IN v = element.getValue();
         K k = keySelector.getKey(v);
         if (!keyModeKnown) {
@@ -381,6 +509,9 @@ public class GpuWindowOperator<IN, K>
                         break;
                     case MIN_MAX_BY: row = elements.get(oPay.getLong(i * 8)); break;
                     case AGGREGATE: row = res; break;
+                    case WINDOW_FUNCTION:
+                        emitThroughWindowFunction(key, oStart.getLong(i * 8), end, res);
+                        continue;
                     default: row = Tuple4.of(key, oStart.getLong(i * 8), end, res);
                 }
                 // count windows: GlobalWindow.maxTimestamp() = Long.MAX_VALUE
@@ -388,6 +519,48 @@ public class GpuWindowOperator<IN, K>
                 output.collect(new StreamRecord<>(row, tsOut));
             }
             if (got < batchCapacity) break;
+        }
+    }
+
+    /** InternalSingleValueProcessWindowFunction.process: the window function over the one
+     *  pre-aggregated value, output stamped window.maxTimestamp(); with allowed lateness 0 the
+     *  firing also cleans the window up (WindowOperator.clearAllState -> userFunction.clear). */
+    @SuppressWarnings("unchecked")
+    private void emitThroughWindowFunction(Object key, long start, long end, Object res) throws Exception {
+        windowContext.window = new TimeWindow(start, end);
+        collector.setAbsoluteTimestamp(end - 1);
+        windowFunction.process((K) key, windowContext, Collections.singletonList(res), collector);
+        if (lateness == 0) windowFunction.clear(windowContext);
+    }
+
+    /** ProcessWindowFunction.Context of a GPU-fired window. */
+    private final class WindowContext extends ProcessWindowFunction<Object, Object, K, TimeWindow>.Context {
+        TimeWindow window;
+
+        WindowContext() { windowFunction.super(); }
+
+        @Override
+        public TimeWindow window() { return window; }
+
+        @Override
+        public long currentProcessingTime() { return getProcessingTimeService().getCurrentProcessingTime(); }
+
+        @Override
+        public long currentWatermark() { return currentWm; }
+
+        @Override
+        public KeyedStateStore windowState() {
+            throw new UnsupportedOperationException("per-window state in a GPU window function");
+        }
+
+        @Override
+        public KeyedStateStore globalState() {
+            throw new UnsupportedOperationException("keyed global state in a GPU window function");
+        }
+
+        @Override
+        public <X> void output(OutputTag<X> outputTag, X value) {
+            output.collect(outputTag, new StreamRecord<>(value, window.maxTimestamp()));
         }
     }
 
@@ -407,7 +580,13 @@ public class GpuWindowOperator<IN, K>
 
     @Override
     public void processWatermark(Watermark mark) throws Exception {
+        if (handleDeferred) {  // staggered, no element yet: nothing can fire; remember the watermark
+            deferredWatermark = Math.max(deferredWatermark, mark.getTimestamp());
+            super.processWatermark(mark);
+            return;
+        }
         flush();
+        currentWm = mark.getTimestamp();
         nativeAdvanceWatermark(handle, mark.getTimestamp());
         emitRows();
         if (wide()) releaseElements(mark.getTimestamp());
@@ -429,7 +608,11 @@ public class GpuWindowOperator<IN, K>
         }
     }
 
-    /** Non-Long keys <-> dense int64 ids (the GPU keys), with each key's hashCode. */
+    /** Non-Long keys <-> dense int64 ids (the GPU keys), with each key's hashCode.  Ids are never
+     *  released: the dictionary holds every key the subtask has seen (one HashMap entry and one
+     *  list slot per distinct key) for the operator's lifetime, like the reference's heap backend
+     *  holds the key objects of live state, but also for keys whose windows are all cleaned; a job
+     *  with an unbounded key space (session ids) should key by a Long, which needs no dictionary. */
     static final class KeyDictionary<T> {
         private final HashMap<T, Long> ids = new HashMap<>();
         private final ArrayList<T> keys = new ArrayList<>();
@@ -480,6 +663,7 @@ public class GpuWindowOperator<IN, K>
 
     @Override
     public void close() throws Exception {
+        if (windowFunction != null) FunctionUtils.closeFunction(windowFunction);
         if (handle != 0) nativeDestroy(handle);
         handle = 0;
         super.close();
@@ -487,6 +671,8 @@ public class GpuWindowOperator<IN, K>
 
     public long numLateRecordsDropped() { return nativeLateDropped(handle); }
 
+    private static native long nativeStaggerOffset(int stagger, long processingTime, double random01, long size,
+                                                   long globalOffset);
     private static native long nativeCreate(int assigner, int trigger, long size, long slide, long offset, long gap,
                                             long lateness, int agg, int maxParallelism, int parallelism,
                                             int subtask, int device, int flags, long capacityHint, long maxBatch);

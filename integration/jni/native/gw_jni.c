@@ -36,6 +36,16 @@ JNIEXPORT jlong JNICALL CLS(nativeCreate)(JNIEnv* env, jclass c, jint assigner, 
     return (jlong)(intptr_t)h;
 }
 
+/* TumblingEventTimeWindows' stagger at the first element: the offset GpuWindowOperator
+ * creates its handle with (gw_window_stagger_offset). */
+JNIEXPORT jlong JNICALL CLS(nativeStaggerOffset)(JNIEnv* env, jclass c, jint stagger, jlong processingTime,
+                                                 jdouble random01, jlong size, jlong globalOffset) {
+    int64_t off = 0;
+    int rc = gw_window_stagger_offset(stagger, processingTime, random01, size, globalOffset, &off);
+    if (rc) fail(env, 0, rc);
+    return off;
+}
+
 /* keys/ts/values/keyHashes: direct ByteBuffers of n little-endian longs / ints */
 JNIEXPORT void JNICALL CLS(nativeIngest)(JNIEnv* env, jclass c, jlong h, jint n, jobject keys, jobject keyHashes,
                                          jobject ts, jobject values) {

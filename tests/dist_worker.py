@@ -41,6 +41,36 @@ def owners(keys, maxp, p):
     return (kg * p) // maxp
 
 
+def plan_exchange(world, rank, cols, counts, wm):
+    """One batch through gw_exchange_plan: the (count, watermark, column mask) message per peer
+    goes through one all-to-all, the plan gives every send / receive offset, the columns move
+    by point-to-point sends and receives."""
+    from flink_amd import _native as N
+    msg = torch.zeros(world, 3, dtype=torch.int64)
+    msg[:, 0] = counts
+    msg[:, 1] = wm
+    msg[:, 2] = 1
+    rmsg = torch.empty_like(msg)
+    dist.all_to_all_single(rmsg.view(-1), msg.view(-1))
+    (so, sc, ro, rc), total, wmin = N.exchange_plan(msg.view(-1).numpy(), rmsg.view(-1).numpy(), 1, wm)
+    out = []
+    for c in cols:
+        r = torch.empty(total, dtype=c.dtype)
+        reqs = []
+        for q in range(world):
+            if q == rank:
+                r[ro[q]:ro[q] + rc[q]] = c[so[q]:so[q] + sc[q]]
+                continue
+            if sc[q]:
+                reqs.append(dist.isend(c[so[q]:so[q] + sc[q]].contiguous(), q))
+            if rc[q]:
+                reqs.append(dist.irecv(r[ro[q]:ro[q] + rc[q]], q))
+        for x in reqs:
+            x.wait()
+        out.append(r.numpy())
+    return out[0], out[1], out[2], wmin
+
+
 def worker(rank, world, port, cfg_kw, seed, result_q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -65,7 +95,12 @@ def worker(rank, world, port, cfg_kw, seed, result_q):
         counts = torch.from_numpy(np.bincount(own, minlength=world).astype(np.int64))
         cols = [torch.from_numpy(k[order]), torch.from_numpy(t[order]), torch.from_numpy(v[order])]
         (rk, rt, rv), _ = ex.exchange_partitioned(cols, counts)
+        # the native exchange's per-peer plan (gw_exchange_plan), driven over gloo point-to-point
+        # sends / receives as gw_exchange_batch drives ncclSend / ncclRecv: same layout
+        pk, pt, pv, wmin = plan_exchange(world, rank, cols, counts, wm)
+        assert np.array_equal(pk, rk.numpy()) and np.array_equal(pt, rt.numpy()) and np.array_equal(pv, rv.numpy())
         rk, rt, rv = rk.numpy(), rt.numpy(), rv.numpy()
+        assert wmin == ex.combine_watermark(wm)
         bad_owner += int((owners(rk, 128, world) != rank).sum())
         op.process_batch(rk, rt, rv)
         op.process_watermark(ex.combine_watermark(wm))

@@ -91,6 +91,15 @@ asg = [
 ]
 dump("assigners.json", {"source": [SEW + ":39-135", TEW + ":41-97", SES + ":53-66"], "cases": asg})
 
+# TumblingEventTimeWindowsTest.testWindowAssignmentWithStagger (:55-72): NATURAL stagger, size 5000,
+# global offset 0, the first element at processing time 150:
+#   [stagger, size, global offset, processing time, ts, [[start, end]]]
+dump("stagger.json", {"source": TEW + ":55-72", "cases": [
+    ["NATURAL", 5000, 0, 150, 150, [[150, 5150]]],
+    ["NATURAL", 5000, 0, 150, 5099, [[150, 5150]]],
+    ["NATURAL", 5000, 0, 150, 5300, [[5150, 10150]]],
+]})
+
 # --------------------------------------------------------------------------------------
 # TimeWindow.mergeWindows via EventTimeSessionWindows.mergeWindows:
 #   [[input windows], [[merged members...], cover], ...]  (only groups of size > 1)

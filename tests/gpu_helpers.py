@@ -121,3 +121,18 @@ def compare(gpu_out, ora_out, is_double):
                 errs.append(f"watermark #{b}: result differs at row {i}: {int(G[3][i])} vs {int(O[3][i])} "
                             f"(key {int(G[0][i])} window [{int(G[1][i])},{int(G[2][i])}))")
     return errs
+
+
+def corrupt_last_group(blob: bytes) -> bytes:
+    """The blob with the window start of its last non-empty key group's first entry changed
+    (a window of no assigner): the reader rejects it after parsing every earlier group."""
+    import struct
+    kg_lo, kg_hi = struct.unpack_from("<ii", blob, 60)
+    nk = kg_hi - kg_lo + 1
+    offs = np.frombuffer(blob[96:96 + 8 * (nk + 1)], np.int64)
+    pay0 = 96 + 8 * (nk + 1)
+    last = max(g for g in range(nk) if offs[g + 1] - offs[g] > 40)
+    assert last > 0
+    bad = bytearray(blob)
+    bad[pay0 + int(offs[last]) + 4 + 7] ^= 1
+    return bytes(bad)

@@ -9,6 +9,7 @@ typedef int32_t jint;
 typedef int64_t jlong;
 typedef int8_t jbyte;
 typedef uint8_t jboolean;
+typedef double jdouble;
 typedef jint jsize;
 typedef struct _jobject* jobject;
 typedef jobject jclass;

@@ -15,7 +15,7 @@ import pytest
 
 from flink_amd import _native as N
 from flink_amd import windowing as W
-from tests.gpu_helpers import gpu_operator, random_stream, run_oracle
+from tests.gpu_helpers import corrupt_last_group, gpu_operator, random_stream, run_oracle
 
 pytestmark = pytest.mark.gpu
 
@@ -183,3 +183,67 @@ def test_first_element_snapshot_restore(oracle_lib, kw, agg):
         i = np.lexsort((e, s, k))
         g.append((k[i], s[i], e[i], r.view(np.int64)[i], p[i]))
     _check(g, o, agg.endswith("f64"))
+
+
+@pytest.mark.parametrize("kw,agg", [(CONFIGS[4], "sum_i64"), (CONFIGS[3], "min_i64")],
+                         ids=["sliding-lateness-sum", "window-classes-min"])
+def test_first_element_rejected_restores_leave_the_handle_unchanged(oracle_lib, kw, agg):
+    """A first-element blob rejected part-way (GW_E_INVALID) and a restore after the handle took
+    records (GW_E_STATE) leave no trace: no payload in the log, no sequence consumed, no entries in
+    either operator.  The handle then takes the good blob and continues like a handle that never
+    saw the bad one (and, for the refused late restore, like the uninterrupted oracle)."""
+    kw = dict(kw, agg=agg)
+    keys, ts, vals, batches = random_stream(seed=95, n=24000, num_keys=150, n_batches=24, ts_step=3,
+                                            disorder=240, wm_lag=250, agg=agg)
+    payload = np.random.default_rng(96).integers(-(1 << 62), 1 << 62, len(keys)).astype(np.int64)
+    cut = 11
+    a = gpu_operator(kw, flags=N.FLAG_FIRST_ELEMENT)
+    try:
+        for lo, hi, wm in batches[:cut]:
+            a.process_batch_payload(keys[lo:hi], ts[lo:hi], vals[lo:hi], payload[lo:hi])
+            a.advance_watermark(wm)
+            a.drain_payload()
+        blob = a.snapshot_state()
+    finally:
+        a.close()
+
+    def continue_from(op, blobs):
+        for bl in blobs:
+            op.initialize_state(bl)
+        out = []
+        for lo, hi, wm in batches[cut:] + [(len(keys), len(keys), W.LONG_MAX)]:
+            op.process_batch_payload(keys[lo:hi], ts[lo:hi], vals[lo:hi], payload[lo:hi])
+            op.advance_watermark(wm)
+            k, s, e, r, p = op.drain_payload()
+            i = np.lexsort((e, s, k))
+            out.append((k[i], s[i], e[i], r.view(np.int64)[i], p[i]))
+        return out
+
+    b = gpu_operator(kw, flags=N.FLAG_FIRST_ELEMENT)
+    c = gpu_operator(kw, flags=N.FLAG_FIRST_ELEMENT)
+    try:
+        with pytest.raises(N.GpuWinError) as ei:
+            b.initialize_state(corrupt_last_group(blob))
+        assert ei.value.code == N.GW_E_INVALID
+        _check(continue_from(b, [blob]), continue_from(c, [blob]), False)
+    finally:
+        b.close()
+        c.close()
+    # restore after processing started: refused, nothing changes
+    o, _ = _expected(oracle_lib, kw, keys, ts, vals, payload, batches)
+    d = gpu_operator(kw, flags=N.FLAG_FIRST_ELEMENT)
+    outs = []
+    try:
+        for b_, (lo, hi, wm) in enumerate(batches + [(len(keys), len(keys), W.LONG_MAX)]):
+            if b_ == 2:
+                with pytest.raises(N.GpuWinError) as ei:
+                    d.initialize_state(blob)
+                assert ei.value.code == N.GW_E_STATE
+            d.process_batch_payload(keys[lo:hi], ts[lo:hi], vals[lo:hi], payload[lo:hi])
+            d.advance_watermark(wm)
+            k, s, e, r, p = d.drain_payload()
+            i = np.lexsort((e, s, k))
+            outs.append((k[i], s[i], e[i], r.view(np.int64)[i], p[i]))
+    finally:
+        d.close()
+    _check(outs, o, False)

@@ -17,7 +17,7 @@ import pytest
 
 from flink_amd import _native as N
 from flink_amd import windowing as W
-from tests.gpu_helpers import gpu_operator, random_stream
+from tests.gpu_helpers import corrupt_last_group, gpu_operator, random_stream
 from tests.harness import load_golden
 
 pytestmark = pytest.mark.gpu
@@ -220,3 +220,46 @@ def test_datastream_min_by_emits_elements():
         out = stream.key_by(lambda v: v[0]).window(W.TumblingEventTimeWindows.of(10)).min_by(1, first) \
             .execute_and_collect()
         assert {r.value for r in out} == want
+
+
+@pytest.mark.parametrize("kw,agg,first", [(CONFIGS[4], "min_i64", True), (CONFIGS[3], "max_i64", False)],
+                         ids=["sliding-lateness-min-first", "window-classes-max-last"])
+def test_by_field_rejected_restores_leave_the_handle_unchanged(oracle_lib, kw, agg, first):
+    """A minBy / maxBy blob rejected part-way (GW_E_INVALID) and a restore after the handle took
+    records (GW_E_STATE: initializeState runs before processing) change nothing: no element enters
+    the log, no operator keeps restored entries.  The first handle then restores the good blob and
+    continues like the oracle restored from it; the second continues like the uninterrupted
+    oracle."""
+    kw = dict(kw, agg=agg)
+    keys, ts, vals, payload, batches = _stream(93, agg, n=24000, num_keys=150, n_batches=24,
+                                               lateness=kw.get("lateness", 0))
+    cut = 11
+    final = [(len(keys), len(keys), W.LONG_MAX)]
+    a = gpu_operator(kw, flags=_flags(first))
+    try:
+        outs = _run(a, keys, ts, vals, payload, batches[:cut])
+        blob = a.snapshot_state()
+    finally:
+        a.close()
+    b = gpu_operator(kw, flags=_flags(first))
+    try:
+        with pytest.raises(N.GpuWinError) as ei:
+            b.initialize_state(corrupt_last_group(blob))
+        assert ei.value.code == N.GW_E_INVALID
+        b.initialize_state(blob)
+        outs += _run(b, keys, ts, vals, payload, batches[cut:] + final)
+    finally:
+        b.close()
+    o, _ = _expected(oracle_lib, kw, first, keys, ts, vals, payload, batches, cut=cut)
+    _check(outs, o)
+    c = gpu_operator(kw, flags=_flags(first))
+    try:
+        g = _run(c, keys, ts, vals, payload, batches[:2])
+        with pytest.raises(N.GpuWinError) as ei:
+            c.initialize_state(blob)
+        assert ei.value.code == N.GW_E_STATE
+        g += _run(c, keys, ts, vals, payload, batches[2:] + final)
+    finally:
+        c.close()
+    o, _ = _expected(oracle_lib, kw, first, keys, ts, vals, payload, batches)
+    _check(g, o)

@@ -3,7 +3,9 @@ oracle's sequential decoder (bit-exact columns, watermark positions, consumed by
 gw_ingest_serialized* against the oracle operator fed the same decoded channel.
 
 Parity is pinned by the oracle decoder (tests/test_netbuf_oracle.py: two restatements of
-StreamElementSerializer agree); the reference has no serialized-byte fixtures."""
+StreamElementSerializer agree) and by the reference's own serializer bytes
+(tests/golden/serializer/: StreamElementSerializerUpgradeTest's record, LongSerializer's Long),
+decoded here on the device too."""
 import ctypes
 import struct
 
@@ -14,7 +16,7 @@ from flink_amd import _native as N
 from flink_amd import netbuf as NB
 from flink_amd import windowing as W
 from tests.gpu_helpers import compare, gpu_operator, random_stream
-from tests.test_netbuf_oracle import LAYOUTS, random_elements
+from tests.test_netbuf_oracle import LAYOUTS, random_elements, reference_bytes
 
 pytestmark = pytest.mark.gpu
 
@@ -86,6 +88,20 @@ def test_decode_large_stream(oracle_lib):
     assert g[0] == 0 and g[6].records == n and g[6].consumed == len(data)
     assert np.array_equal(g[1], k) and np.array_equal(g[2], t) and np.array_equal(g[3], v)
     assert g[4].tolist() == [500_000, 1_000_000, 1_500_000, 2_000_000] and g[5].tolist() == [1000, 2000, 3000, 4000]
+
+
+def test_decode_reference_serializer_bytes(oracle_lib):
+    """The reference's bytes on the device: the record (1234567890L)@123456 built from
+    StreamElementSerializerUpgradeTest's tag + timestamp and LongSerializer's Long, repeated across
+    several 1-KB chunks with watermarks, decodes bit-exactly like the oracle; the reference's own
+    String record under the Long layout fails the task as a corrupt stream (GW_E_INVALID)."""
+    rec, lng = reference_bytes()
+    element = struct.pack(">i", 17) + rec[:9] + lng
+    data = (element * 100 + NB.watermark(123000)) * 7
+    g = gpu_decode(data, "J", 0, -1)
+    assert g[0] == 0 and g[6].records == 700 and set(g[1].tolist()) == {1234567890} and set(g[2].tolist()) == {123456}
+    assert_same_decode(oracle_lib, data, "J", 0, -1)
+    assert gpu_decode(data + struct.pack(">i", len(rec)) + rec + data, "J", 0, -1)[0] == -1
 
 
 def test_decode_errors():

@@ -108,3 +108,22 @@ def test_no_narrow_flag_keeps_compact(oracle_lib, agg):
     g, o, fmts = run(oracle_lib, kw, keys, ts, vals, batches, 1 << 19, flags=N.FLAG_NO_NARROW)
     assert compare(g, o, False) == []
     assert set(fmts) <= {-1, 1}
+
+
+@pytest.mark.parametrize("agg", ["sum_i64", "count"])
+def test_narrow_two_pass_regions_fill_and_spill(oracle_lib, agg):
+    """A two-pass table (2^19 slots: 256 regions, P2 by (super-region, ring position), the
+    k_rgn_apply_nar flush) that one buffered window overfills with new keys: full regions
+    leave records unapplied, the spill pass marks them, k_rgn_collect_nar2 parks them on the
+    deferred list, the table grows and the merge applies them -- exact against the oracle."""
+    kw = dict(assigner="sliding", size=2000, slide=500, agg=agg)
+    rng = np.random.default_rng(41)
+    n = 1_400_000
+    keys = rng.integers(0, 720_000, n).astype(np.int64)
+    ts = np.arange(n, dtype=np.int64) * 6_000 // n - rng.integers(0, 300, n)
+    vals = rng.integers(-(10 ** 6), 10 ** 6, n).astype(np.int64)
+    cuts = [0, 1_000_000, 1_200_000, n]  # the first batch alone brings ~540K distinct keys
+    batches = [(cuts[b], cuts[b + 1], int(ts[:cuts[b + 1]].max()) - 400) for b in range(3)]
+    g, o, fmts = run(oracle_lib, kw, keys, ts, vals, batches, 1 << 19)
+    assert compare(g, o, False) == []
+    assert fmts[0] == 2

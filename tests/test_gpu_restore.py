@@ -287,3 +287,60 @@ def test_rejected_blob_leaves_the_handle_unchanged(oracle_lib, kw):
     assert compare(go, oo, False) == []
     g.close()
     ora.close()
+
+
+def test_rejected_hashed_blob_leaves_no_key_hashes_behind(oracle_lib):
+    """A blob whose key carries two different Java hashCodes (two window entries of one key)
+    is refused before anything changes -- not its entries, not its (key, hash) pairs in the
+    handle's key-hash map (a stale pair would refuse the good blob or file a key's state under
+    the wrong key group).  The handle that refused it then behaves exactly like a fresh handle
+    restored from the good blob: same rows at every watermark, same snapshot."""
+    import struct
+    kw = dict(CFGS[1], agg="sum_i64")
+    keys, ts, vals, batches = random_stream(seed=31, n=6000, num_keys=60, n_batches=16, ts_step=3,
+                                            disorder=200, wm_lag=250, agg="sum_i64")
+    hashes = ((keys * 7919 + 13) % 1000003).astype(np.int32)
+    cut = 7
+    a = gpu_operator(kw, capacity_hint=4096)
+    for lo, hi, wm in batches[:cut]:
+        a.process_batch(keys[lo:hi], ts[lo:hi], vals[lo:hi], key_hashes=hashes[lo:hi])
+        a.advance_watermark(wm)
+        a.clear_rows()
+    good = a.snapshot_state()
+    a.close()
+    assert struct.unpack_from("<q", good, 48)[0] & 1  # flags: entries carry key hashes
+    kg_lo, kg_hi = struct.unpack_from("<ii", good, 60)
+    nk = kg_hi - kg_lo + 1
+    offs = np.frombuffer(good[96:96 + 8 * (nk + 1)], np.int64)
+    pay0 = 96 + 8 * (nk + 1)
+    eb = 24 + 4 + 8
+    bad = None
+    for g in range(nk):  # a key group holding two entries of one key
+        p = pay0 + int(offs[g])
+        n = struct.unpack_from(">i", good, p)[0]
+        ks = [struct.unpack_from(">q", good, p + 4 + i * eb + 16)[0] for i in range(n)]
+        dup = [i for i in range(1, n) if ks[i] in ks[:i]]
+        if dup:
+            bad = bytearray(good)
+            bad[p + 4 + dup[0] * eb + 24 + 3] ^= 1  # its hash, low byte
+            break
+    assert bad is not None
+    b = gpu_operator(kw, capacity_hint=4096)
+    c = gpu_operator(kw, capacity_hint=4096)
+    try:
+        with pytest.raises(N.GpuWinError) as ei:
+            b.initialize_state(bytes(bad))
+        assert ei.value.code == N.GW_E_INVALID
+        outs = {}
+        for name, op in (("b", b), ("c", c)):
+            op.initialize_state(good)
+            outs[name] = []
+            for lo, hi, wm in batches[cut:] + [(len(keys), len(keys), W.LONG_MAX)]:
+                op.process_batch(keys[lo:hi], ts[lo:hi], vals[lo:hi], key_hashes=hashes[lo:hi])
+                op.advance_watermark(wm)
+                drain(op, outs[name])
+        assert compare(outs["b"], outs["c"], False) == []
+        assert b.snapshot_state() == c.snapshot_state()
+    finally:
+        b.close()
+        c.close()

@@ -1,0 +1,112 @@
+"""Two parts of the WindowedStream surface around the GPU operator (flink_amd.windowing):
+
+* WindowStagger on TumblingEventTimeWindows (TumblingEventTimeWindows.java:72-79,
+  WindowStagger.java:27-60): the stagger is drawn at the first element, so the handle is created
+  then, with offset (offset + stagger) % size.  TumblingEventTimeWindowsTest.
+  testWindowAssignmentWithStagger's vectors (tests/golden/stagger.json) through the operator,
+  RANDOM against the oracle at the drawn offset, watermarks before the first element, and the
+  refused restore into a staggered operator.
+* reduce / aggregate with a window function (WindowedStream.java:224-276, 342-526;
+  InternalSingleValueProcessWindowFunction): the function gets the key, the window and a
+  one-element list holding the GPU's pre-aggregated result; its output is stamped
+  window.maxTimestamp()."""
+import numpy as np
+import pytest
+
+from flink_amd import _native as N
+from flink_amd import windowing as W
+from tests.gpu_helpers import compare, random_stream, run_oracle
+from tests.harness import load_golden
+
+pytestmark = pytest.mark.gpu
+
+
+def test_natural_stagger_vectors():
+    g = load_golden("stagger.json")
+    for _, size, off, ptime, ts, windows in g["cases"]:
+        op = W.GpuWindowOperator(W.TumblingEventTimeWindows.of(size, off, W.WindowStagger.NATURAL), "count",
+                                 processing_time=lambda: ptime).open()
+        try:
+            op.process_watermark(-10_000)  # before the first element: remembered, fires nothing
+            op.process_element(W.StreamRecord((1, 0), ts))
+            op.end_input()
+            rows = [r for r in op.get_output() if isinstance(r, W.StreamRecord)]
+        finally:
+            op.close()
+        assert [(r.value[1], r.value[2]) for r in rows] == [tuple(w) for w in windows]
+        assert [r.timestamp for r in rows] == [windows[0][1] - 1]
+
+
+def test_random_stagger_matches_oracle_at_the_drawn_offset(oracle_lib, monkeypatch):
+    import random
+    monkeypatch.setattr(random, "random", lambda: 0.3141)
+    size = 1000
+    woff = W.WindowStagger.window_offset(W.WindowStagger.RANDOM, 0, size, 100, 0.3141)
+    assert woff == 414
+    keys, ts, vals, batches = random_stream(seed=5, n=8000, num_keys=200, n_batches=8, agg="sum_i64")
+    op = W.GpuWindowOperator(W.TumblingEventTimeWindows.of(size, 100, W.WindowStagger.RANDOM), "sum_i64").open()
+    outs = []
+    try:
+        for lo, hi, wm in batches + [(len(keys), len(keys), W.LONG_MAX)]:
+            if hi > lo:
+                op.process_batch(keys[lo:hi], ts[lo:hi], vals[lo:hi])
+            op.advance_watermark(wm)
+            k, s, e, r = op.drain()
+            outs.append((k, s, e, r))
+    finally:
+        op.close()
+    o, _ = run_oracle(oracle_lib, dict(assigner="tumbling", size=size, slide=size, offset=woff, agg="sum_i64"),
+                      keys, ts, vals, batches)
+    assert compare(outs, o, False) == []
+
+
+def test_staggered_operator_refuses_restored_state():
+    a = W.GpuWindowOperator(W.TumblingEventTimeWindows.of(1000), "count").open()
+    try:
+        a.process_batch(np.arange(10, dtype=np.int64), np.arange(10, dtype=np.int64) * 50)
+        blob = a.snapshot_state()
+    finally:
+        a.close()
+    b = W.GpuWindowOperator(W.TumblingEventTimeWindows.of(1000, 0, W.WindowStagger.NATURAL), "count",
+                            processing_time=lambda: 7).open()
+    try:
+        empty = b.snapshot_state()  # no element yet: no window state
+        assert len(empty) > 0
+        with pytest.raises(N.GpuWinError) as ei:
+            b.initialize_state(blob)
+        assert ei.value.code == N.GW_E_UNSUPPORTED
+    finally:
+        b.close()
+
+
+def test_aggregate_with_process_window_function():
+    """aggregate(count, ProcessWindowFunction): (key, window end, count, 2 * count) per window."""
+    els = [("a", 1), ("b", 2), ("a", 3), ("a", 11), ("b", 12), ("b", 13), ("b", 14)]
+    env = W.StreamExecutionEnvironment()
+    stream = env.from_elements([W.StreamRecord(v, t) for v, t in zip(els, [1, 2, 3, 11, 12, 13, 14])])
+
+    def fn(key, window, elements, out):
+        (c,) = elements  # one pre-aggregated value, as InternalSingleValueProcessWindowFunction passes it
+        out.append((key, window[1], int(c), 2 * int(c)))
+
+    out = stream.key_by(lambda v: v[0]).window(W.TumblingEventTimeWindows.of(10)) \
+        .aggregate("count", None, window_function=fn).execute_and_collect()
+    assert sorted((r.value, r.timestamp) for r in out) == sorted([
+        (("a", 10, 2, 4), 9), (("b", 10, 1, 2), 9), (("a", 20, 1, 2), 19), (("b", 20, 3, 6), 19)])
+
+
+def test_reduce_with_window_function_emits_any_number_of_rows():
+    """reduce(sum, WindowFunction): the function may emit nothing or several records per window."""
+    els = [(1, 5), (1, 7), (2, 1), (2, 1), (3, 100)]
+    env = W.StreamExecutionEnvironment()
+    stream = env.from_elements([W.StreamRecord(v, 10 * i) for i, v in enumerate(els)])
+
+    def fn(key, window, elements, out):
+        s = int(elements[0])
+        for i in range(s % 3):  # 12 -> 0 rows, 2 -> 2 rows, 100 -> 1 row
+            out.append((key, s, i))
+
+    out = stream.key_by(lambda v: v[0]).window(W.TumblingEventTimeWindows.of(1000)) \
+        .reduce("sum_i64", 1, window_function=fn).execute_and_collect()
+    assert sorted(r.value for r in out) == [(2, 2, 0), (2, 2, 1), (3, 100, 0)]
+    assert {r.timestamp for r in out} == {999}

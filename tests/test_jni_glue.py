@@ -324,3 +324,20 @@ def test_payload_table_glue(jni):
     assert exception(jni)[0] == "java/lang/IllegalArgumentException"
     for a in (arr, out, mx, fa, ta, parr):
         jni.fake_bytes_free(a)
+
+
+def test_native_stagger_offset(jni):
+    """GpuWindowOperator's staggered handle: nativeStaggerOffset at the first element's processing
+    time (TumblingEventTimeWindowsTest.testWindowAssignmentWithStagger: NATURAL, size 5000, 150 ->
+    windows from 150); a bad argument is an IllegalArgumentException."""
+    f = getattr(jni, CLS + "nativeStaggerOffset")
+    f.restype = ctypes.c_int64
+    f.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_double, ctypes.c_int64,
+                  ctypes.c_int64]
+    env = jni.fake_env()
+    assert f(env, None, 2, 150, 0.0, 5000, 0) == 150 and exception(jni) is None      # NATURAL
+    assert f(env, None, 1, 0, 0.5, 5000, 4000) == 1500 and exception(jni) is None    # RANDOM
+    assert f(env, None, 0, 999, 0.7, 5000, -100) == -100 and exception(jni) is None  # ALIGNED
+    f(env, None, 1, 0, 1.5, 5000, 0)
+    exc = exception(jni)
+    assert exc is not None and exc[0] == "java/lang/IllegalArgumentException"

@@ -3,10 +3,16 @@
 StreamElementSerializer.deserialize (RS/runtime/streamrecord/StreamElementSerializer.java:
 200-225) over streams written by flink_amd.netbuf (the sender side, :163-197).
 
-Parity pinning: the reference holds no serialized-byte fixtures for this path (its
-StreamElementSerializerTest round-trips objects through a JVM), so the byte format is
-pinned by the two restatements of the published serializer agreeing, and by the round
-trip element -> bytes -> element."""
+Parity pinning: the reference's own serializer bytes (tests/golden/serializer/, copied by
+tests/golden/make_serializer_fixtures.py): StreamElementSerializerUpgradeTest's StreamRecord
+("key", 123456) -- tag 0, big-endian timestamp, String payload -- and LongSerializer's
+1234567890L.  A Tuple1<Long> record is its fields' serializer bytes in order
+(TupleSerializer.serialize :135-144), so the record (1234567890L)@123456 is exactly the
+reference's tag + timestamp followed by the reference's Long bytes: the writer must produce
+them and both decoders must read them back; the reference's own String record must be refused
+under a Long layout (its length does not match), as a corrupt stream.  Beyond that the byte
+format is pinned by the two restatements of the published serializer agreeing, and by the
+round trip element -> bytes -> element."""
 import struct
 
 import numpy as np
@@ -133,3 +139,31 @@ def test_vectorised_serializer_matches_element_serializer():
     fast = NB.serialize_batches("JDI", 0, 1, [(k, t, v)], [123])
     slow = b"".join(NB.record((int(a), float(c), 0), "JDI", int(b)) for a, b, c in zip(k, t, v)) + NB.watermark(123)
     assert fast == slow
+
+
+def reference_bytes():
+    import os
+    d = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "serializer")
+    rec = open(os.path.join(d, "stream-element-serializer.test-data"), "rb").read()
+    lng = open(os.path.join(d, "long-serializer.test-data"), "rb").read()
+    assert rec.hex() == "00000000000001e240046b6579" and lng.hex() == "00000000499602d2"
+    return rec, lng
+
+
+def test_reference_serializer_bytes_pin_the_framing(oracle_lib):
+    """StreamRecord(Tuple1(1234567890L), 123456) is the reference's tag + timestamp bytes and its
+    Long bytes; the writer produces them, the oracle decoder and the Python restatement read them
+    back; the reference's String record (13 bytes) under the Long layout is a corrupt stream."""
+    rec, lng = reference_bytes()
+    element = rec[:9] + lng  # tag 0 + be64 123456, then the Tuple1's only field
+    data = struct.pack(">i", len(element)) + element
+    assert NB.record([1234567890], "J", timestamp=123456) == data
+    rc, k, t, v, wp, wv, res = oracle_lib.decode_stream(data, "J", 0, -1)
+    assert rc == 0 and list(k) == [1234567890] and list(t) == [123456] and res.consumed == len(data)
+    recs, wms, pos = py_decode(data, "J", 0, -1)
+    assert recs == [(1234567890, 123456, 0)] and pos == len(data)
+    # the same record followed by a watermark, then the reference's String record: the decoder
+    # reads the first two and fails the task on the third (length 13 != 1 + 8 + 8)
+    bad = data + NB.watermark(123000) + struct.pack(">i", len(rec)) + rec
+    rc, *_ = oracle_lib.decode_stream(bad, "J", 0, -1)
+    assert rc == -1  # GW_E_INVALID: "Corrupt stream"

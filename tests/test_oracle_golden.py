@@ -188,3 +188,38 @@ def test_parallel_matches_single(oracle_lib):
     r1, c1, _ = o.run_parallel(cfg, 1, blen, wm, keys, ts, vals)
     r4, c4, _ = o.run_parallel(cfg, 4, blen, wm, keys, ts, vals)
     assert r1 == r4 and c1 == c4 and r1 > 0
+
+
+def test_stagger_vectors(oracle_lib):
+    """TumblingEventTimeWindowsTest.testWindowAssignmentWithStagger (tests/golden/stagger.json):
+    the offset gw_window_stagger_offset gives for the first element's processing time, used as
+    the assigner's offset, reproduces the reference's windows."""
+    from flink_amd.windowing import WindowStagger
+    o = oracle_lib
+    for stagger, size, off, ptime, ts, windows in load_golden("stagger.json")["cases"]:
+        woff = WindowStagger.window_offset(getattr(WindowStagger, stagger), ptime, size, off)
+        cfg = o.make_config(assigner="tumbling", size=size, slide=size, offset=woff)
+        s = np.zeros(4, np.int64)
+        e = np.zeros(4, np.int64)
+        P = ctypes.POINTER(ctypes.c_int64)
+        n = o.lib().wo_assign_windows(ctypes.byref(cfg), ts, s.ctypes.data_as(P), e.ctypes.data_as(P), 4)
+        assert sorted(zip(s[:n].tolist(), e[:n].tolist())) == [tuple(w) for w in windows], (stagger, ts)
+
+
+def test_stagger_offsets():
+    """WindowStagger.getStaggerOffset (WindowStagger.java:27-60) + (globalOffset + stagger) % size
+    (TumblingEventTimeWindows.java:72-79, Java remainder)."""
+    from flink_amd.windowing import WindowStagger as S
+    assert S.window_offset(S.ALIGNED, 123, 5000, 100) == 100
+    assert S.window_offset(S.ALIGNED, 123, 5000, -100) == -100
+    assert S.window_offset(S.RANDOM, 0, 5000, 0, 0.5) == 2500          # (long) (0.5 * 5000)
+    assert S.window_offset(S.RANDOM, 0, 5000, 4000, 0.5) == 1500       # (4000 + 2500) % 5000
+    assert S.window_offset(S.RANDOM, 0, 7, 0, 0.99999) == 6
+    assert S.window_offset(S.NATURAL, 150, 5000, 0) == 150
+    assert S.window_offset(S.NATURAL, 12345, 5000, 0) == 2345
+    assert S.window_offset(S.NATURAL, -150, 5000, -100) == 4750        # start of -150's window: -5000
+    assert S.window_offset(S.NATURAL, 5000, 5000, -100) == -100        # stagger 0: Java % keeps the sign
+    from flink_amd import _native as N
+    for bad in ((S.RANDOM, 0, 5000, 0, 1.0), (S.ALIGNED, 0, 0, 0, 0.0), (S.ALIGNED, 0, 100, 100, 0.0), (7, 0, 10, 0, 0.0)):
+        with pytest.raises(N.GpuWinError):
+            S.window_offset(bad[0], bad[1], bad[2], bad[3], bad[4])
