@@ -71,7 +71,8 @@ def parse(argv=None):
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-host-fed", action="store_true",
                     help="skip the host-fed leg (gw_ingest from host columns: pinned staging + H2D)")
-    ap.add_argument("--host-fed-steps", type=int, default=6)
+    ap.add_argument("--host-fed-steps", type=int, default=11,
+                    help="batches of the host-fed leg (the first untimed; 11 includes a 10M-row fire and drain)")
     ap.add_argument("--preagg", choices=["auto", "force", "off"], default="auto")
     ap.add_argument("--no-kernel-timing", action="store_true",
                     help="no HIP events around the kernels (the roofline fields are then null)")
@@ -141,40 +142,54 @@ class Steps:
     rows of every watermark are drained to the host and (count, checksum) recorded."""
 
     def __init__(self, op, N, keys, ts, vals, wms, nb, ex=None, collect=False, ex_stream=None):
+        import ctypes
         self.op, self.N, self.ex, self.ex_stream = op, N, ex, ex_stream
         self.keys, self.ts, self.vals, self.wms, self.nb = keys, ts, vals, wms, nb
         self.collect = collect
         self.per_wm = []  # (rows, checksum) per watermark when collecting
         self.exch_bytes = 0
+        # the host side of a step stays lean (the GPU runs a batch in ~70 us): the library's entry
+        # points and each batch's device column pointers resolved once, before any clock
+        L = N.lib()
+        self._ingest, self._advance, self._clear = L.gw_ingest_device, L.gw_advance_watermark, L.gw_clear_rows
+        self._h, self._stream = op.handle, op.stream()
+        self._fired = ctypes.c_int64(0)
+        self._fired_ref = ctypes.byref(self._fired)
+        es = keys.element_size()
+        self._ptrs = [(keys.data_ptr() + b * nb * es, ts.data_ptr() + b * nb * es,
+                       vals.data_ptr() + b * nb * es if vals is not None else None) for b in range(len(wms))]
 
     def step(self, b, timed=False, b_in=24, rank=0):
-        op, nb = self.op, self.nb
-        lo, hi = b * nb, (b + 1) * nb
-        k, t = self.keys[lo:hi], self.ts[lo:hi]
-        v = self.vals[lo:hi] if self.vals is not None else None
+        """One batch; returns the rows its watermark fired."""
+        op, nb, N = self.op, self.nb, self.N
         if self.ex is not None:
+            lo, hi = b * nb, (b + 1) * nb
+            k, t = self.keys[lo:hi], self.ts[lo:hi]
+            v = self.vals[lo:hi] if self.vals is not None else None
             # the native exchange on a stream of its own; the ingest orders through the receive
             # set's hand-off stream, so batch b+1's partition and transfers overlap batch b's
             # aggregation on the operator's stream
             n, pk, pt, pv, _, wmin, ist = self.ex.exchange(k, t, v, stream=self.ex_stream, wm=self.wms[b])
             if timed:
                 self.exch_bytes += (nb - int(self.ex.counts()[0][rank])) * b_in
-            self.N.check(self.N.lib().gw_ingest_device(op.handle, n, pk, None, pt, pv, ist), op.handle)
-            op.advance_watermark(wmin)
+            N.check(self._ingest(self._h, n, pk, None, pt, pv, ist), self._h)
+            wm = wmin
         else:
             # columns generated and synchronised before the clock: no producer ordering needed
-            self.N.check(self.N.lib().gw_ingest_device(op.handle, nb, k.data_ptr(), None, t.data_ptr(),
-                                                       v.data_ptr() if v is not None else None, op.stream()),
-                         op.handle)
-            op.advance_watermark(self.wms[b])
+            pk, pt, pv = self._ptrs[b]
+            N.check(self._ingest(self._h, nb, pk, None, pt, pv, self._stream), self._h)
+            wm = self.wms[b]
+        N.check(self._advance(self._h, wm, self._fired_ref), self._h)
+        fired = self._fired.value
         self.consume()
+        return fired
 
     def consume(self):
         if self.collect:
             rows = self.op.drain()
             self.per_wm.append((len(rows[0]), rows_checksum(rows)))
         else:
-            self.op.clear_rows()  # DiscardingSink
+            self.N.check(self._clear(self._h), self._h)  # DiscardingSink
 
 
 def main(argv=None):
@@ -237,19 +252,18 @@ def main(argv=None):
     # the device (gw_advance_watermark), so the host clock at the return of such a step
     # closes one cycle of batches + their fire.
     cycles = []
-    cyc_t, cyc_steps, fires_seen = t0, 0, op.stats()["fires"]
+    cyc_t, cyc_steps = t0, 0
     for b in range(args.warmup, steps_total):
-        run.step(b, True, b_in, rank)
+        fired = run.step(b, True, b_in, rank)
         cyc_steps += 1
-        f = op.stats()["fires"]
-        if f != fires_seen:
+        if fired:  # the watermark completed windows: gw_advance_watermark fired them and synchronised
             now = time.perf_counter()
             cycles.append({"steps": cyc_steps, "ms": (now - cyc_t) * 1e3,
                            "events_per_s": cyc_steps * nb / max(now - cyc_t, 1e-9)})
-            cyc_t, cyc_steps, fires_seen = now, 0, f
-        if rank == 0 and time.perf_counter() - last > 30:
-            last = time.perf_counter()
-            log(f"step {b - args.warmup + 1}/{args.steps}")
+            cyc_t, cyc_steps = now, 0
+            if rank == 0 and now - last > 30:
+                last = now
+                log(f"step {b - args.warmup + 1}/{args.steps}")
     op.flush()  # every timed batch is in the window state when the clock stops
     torch.cuda.synchronize()
     if dist:
@@ -419,36 +433,52 @@ def traffic_bytes(agg, nb):
 
 
 def host_fed_leg(args, W, keys, ts, vals, wms, nb, agg, size, slide, K, maxp, local):
-    """The north star's host path: columns in (pageable) host memory -> gw_ingest, which
-    copies them into the handle's pinned staging and then over PCIe into HBM, then the
-    watermark.  A fresh operator over the first --host-fed-steps batches of the same stream;
-    PCIe-inclusive events/s (never the bench's `value`)."""
-    H = max(1, min(args.host_fed_steps, len(wms)))
-    hk = keys[:H * nb].cpu().numpy()
-    ht = ts[:H * nb].cpu().numpy()
-    hv = vals[:H * nb].cpu().numpy() if vals is not None else None
+    """The north star's host path, as the JVM operator drives it (GpuWindowOperator.java): each
+    batch's columns sit in library-owned pinned slots the operator fills in place
+    (gw_stage_columns; filled here from the generated stream before the clock, as the JVM's
+    processElement calls would have), gw_ingest_stage sends them over PCIe on a copy stream
+    (overlapping the previous batch's kernels), gw_advance_watermark fires, and every fired row
+    is drained to host memory (gw_drain) before the next batch, as processWatermark emits them.
+    A fresh operator over the first --host-fed-steps batches of the stream, the first one
+    untimed; PCIe-inclusive events/s (never the bench's `value`)."""
+    H = max(2, min(args.host_fed_steps, len(wms)))
     op = W.GpuWindowOperator(W.SlidingEventTimeWindows.of(size, slide), agg, capacity_hint=K,
                              max_parallelism=maxp, device=local, max_batch=nb).open()
     try:
-        op.process_batch(hk[:nb], ht[:nb], hv[:nb] if hv is not None else None)  # warm: staging allocation
+        op.stage_alloc(H, nb)
+        for b in range(H):
+            k, _, t, v = op.stage_columns(b)
+            lo, hi = b * nb, (b + 1) * nb
+            k[:nb] = keys[lo:hi].cpu().numpy()
+            t[:nb] = ts[lo:hi].cpu().numpy()
+            if vals is not None:
+                v[:nb] = vals[lo:hi].cpu().numpy()
+        with_value = vals is not None
+        op.ingest_stage(0, nb, with_value)  # warm
         op.advance_watermark(wms[0])
-        op.clear_rows()
+        op.drain()
         op.synchronize()
+        rows = 0
+        drain_s = 0.0
         t0 = time.perf_counter()
         for b in range(1, H):
-            lo, hi = b * nb, (b + 1) * nb
-            op.process_batch(hk[lo:hi], ht[lo:hi], hv[lo:hi] if hv is not None else None)
-            op.advance_watermark(wms[b])
-            op.clear_rows()
+            op.ingest_stage(b, nb, with_value)
+            if op.advance_watermark(wms[b]):
+                td = time.perf_counter()
+                rows += len(op.drain()[0])  # processWatermark: the rows reach the host first
+                drain_s += time.perf_counter() - td
         op.flush()
         op.synchronize()
         sec = time.perf_counter() - t0
     finally:
         op.close()
     n = (H - 1) * nb
-    return {"value": n / sec if n else None, "unit": "events/s", "batches": H - 1, "events": n,
-            "bytes_per_event_h2d": 16 if vals is None else 24,
-            "path": "gw_ingest (memcpy into pinned staging + hipMemcpyAsync H2D) + gw_advance_watermark"}
+    bpe = 16 if vals is None else 24
+    return {"value": n / sec, "unit": "events/s", "batches": H - 1, "events": n, "bytes_per_event_h2d": bpe,
+            "h2d_gbs": n * bpe / sec / 1e9, "rows_drained": rows, "drain_seconds": drain_s, "seconds": sec,
+            "path": "library-owned pinned slots filled in place (gw_stage_columns) -> gw_ingest_stage (H2D on a copy "
+                    "stream, two device buffers in turn) -> gw_advance_watermark -> gw_drain of every fired row "
+                    "to host memory"}
 
 
 def host_cores():

@@ -19,6 +19,7 @@ ERRORS = {
 }
 GW_E_INVALID, GW_E_UNSUPPORTED, GW_E_DEVICE, GW_E_OOM, GW_E_OUTPUT_FULL = -1, -2, -3, -4, -5
 GW_E_NO_TIMESTAMP, GW_E_RANGE, GW_E_STATE = -6, -7, -8
+STAGE_VALUE, STAGE_KEY_HASH = 1, 2
 
 ASSIGNERS = {"tumbling": 0, "sliding": 1, "session": 2, "count_tumbling": 3, "count_sliding": 4}
 TRIGGERS = {"event_time": 0, "purging_event_time": 1}
@@ -51,7 +52,7 @@ EXPORTS = [
     "gw_decode_serialized", "gw_ingest_serialized", "gw_ingest_serialized_device",
     "gw_exchange_unique_id", "gw_exchange_create", "gw_exchange_destroy", "gw_exchange_batch",
     "gw_exchange_min_watermark", "gw_exchange_last_error", "gw_exchange_counts", "gw_exchange_plan",
-    "gw_window_stagger_offset",
+    "gw_window_stagger_offset", "gw_stage_alloc", "gw_stage_columns", "gw_ingest_stage",
     "gw_ingest_payload", "gw_ingest_payload_device", "gw_drain_payload",
     "gw_snapshot_keys", "gw_snapshot_remap_keys", "gw_snapshot_payloads", "gw_snapshot_remap_payloads",
 ]
@@ -188,6 +189,9 @@ def lib() -> ctypes.CDLL:
         "gw_exchange_counts": (c_int, [p, p, p]),
         "gw_exchange_plan": (c_int, [i32, p, p, i64, i64, p, p, p, p, P64, P64]),
         "gw_window_stagger_offset": (c_int, [i32, i64, ctypes.c_double, i64, i64, P64]),
+        "gw_stage_alloc": (c_int, [p, i32, i64]),
+        "gw_stage_columns": (c_int, [p, i32, ctypes.POINTER(p), ctypes.POINTER(p), ctypes.POINTER(p), ctypes.POINTER(p)]),
+        "gw_ingest_stage": (c_int, [p, i32, i64, i32]),
         "gw_exchange_min_watermark": (c_int, [p, i64, P64, p]),
         "gw_exchange_last_error": (ctypes.c_char_p, [p]),
     }

@@ -163,6 +163,16 @@ struct IngestArgs {
     int32_t nar2;          // narrow two-pass flushes (k_rgn_apply_nar): P2 groups each round by
                            // (super-region, ring position); one workgroup per super-region of
     int32_t sr_bits;       //   2^sr_bits probe regions applies one ring position after another
+    // nar2 carry (gw_runtime.cpp flush_buffer): a fire's flush applies only the ring positions
+    // the fire needs (apply_mask); the others stay in its P2 output and the next flush applies
+    // them from there (c_*: that output, c_mask: its carried positions)
+    uint64_t apply_mask;
+    uint64_t c_mask;
+    const int64_t* c_rbeg;
+    const uint32_t* c_r_row;
+    const int64_t* c_r_base;
+    int64_t* c_key;
+    int32_t cur_empty;     // no current segments: the carried positions alone
     int64_t tile0;         // P1: buffer tile of this batch's first tile
     int64_t ntiles;        // flush: buffer tiles in use
     int64_t ngroups;       // flush: P1 tile groups (= P2 blocks per bucket)

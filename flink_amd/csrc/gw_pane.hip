@@ -523,6 +523,24 @@ __global__ void __launch_bounds__(256) k_publish_status(const DevStatus* st, Dev
         __hip_atomic_store(&host->pad[kPubSeqWord], seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// The same from one wave at the start of a buffered P1 (workgroup 0, wave 0): the status
+// as the previous launches left it -- stream order has completed them -- plus whatever
+// this launch's other workgroups have already added (every field only grows or gains bits,
+// so an early copy is a superset the host may absorb; gw_runtime.cpp lazy_status counts the
+// launch's records as unaccounted).  Replaces a k_publish_status launch after every P1: no
+// launch, no gap, no extra kernel boundary per batch.
+__device__ __forceinline__ void publish_status_wave(const DevStatus* st, DevStatus* host, unsigned long long seq) {
+    constexpr int kWords = (int)(sizeof(DevStatus) / 8);
+    const unsigned long long* src = reinterpret_cast<const unsigned long long*>(st);
+    unsigned long long* dst = reinterpret_cast<unsigned long long*>(host);
+    const int lane = threadIdx.x & 63;
+    for (int i = lane; i < kWords; i += 64)
+        if (i != kPubSeqWord + (int)(offsetof(DevStatus, pad) / 8))
+            __hip_atomic_store(&dst[i], src[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // one wave: every lane's stores acknowledged
+    if (lane == 0) __hip_atomic_store(&host->pad[kPubSeqWord], seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // P1: one 4096-record tile of the batch -> buffer tile a.tile0 + blockIdx.x.
 // GW_P1_WAVES / GW_APPLY_WAVES: minimum waves per SIMD the register allocation must allow
 // (6 = 3 workgroups of 512 per CU, as many as the LDS allows, at <= 80 VGPRs)
@@ -691,6 +709,7 @@ __global__ void __launch_bounds__(kPartThreads) GW_P1_ATTR k_rgn_p1(IngestArgs a
     __shared__ unsigned long long s_occ;
     const int64_t g = blockIdx.x;
     const int64_t lo = g * kPartTile, hi = min(a.n, lo + (int64_t)kPartTile);
+    if (g == 0 && threadIdx.x < 64 && a.st_host) publish_status_wave(a.st, a.st_host, a.st_seq);
     for (int b = threadIdx.x; b < kPartBuckets; b += blockDim.x) lh[b] = 0;
     if (threadIdx.x == 0) s_occ = 0;
     __syncthreads();
@@ -1443,7 +1462,10 @@ __global__ void __launch_bounds__(kApplyThreads) k_rgn_apply_nar(IngestArgs a) {
     const int d2v = a.d2_bits - a.sr_bits;
     const int64_t sr = blockIdx.x;
     const int64_t bucket = sr >> d2v, col = sr & (((int64_t)1 << d2v) - 1);
-    const int64_t rb = a.rbeg[bucket], re = a.rbeg[bucket + 1];
+    // the runs of this super-region: this flush's rounds (list 0) and the rounds of the
+    // previous flush that carried ring positions (list 1, positions c_mask)
+    const int64_t rb0 = a.cur_empty ? 0 : a.rbeg[bucket], re0 = a.cur_empty ? 0 : a.rbeg[bucket + 1];
+    const int64_t rb1 = a.c_mask ? a.c_rbeg[bucket] : 0, re1 = a.c_mask ? a.c_rbeg[bucket + 1] : 0;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
     uint32_t* lkeys = reinterpret_cast<uint32_t*>(smem);                     // [FS]
     uint8_t* lmask = reinterpret_cast<uint8_t*>(lkeys + FS);                  // [FS] (M)
@@ -1451,10 +1473,21 @@ __global__ void __launch_bounds__(kApplyThreads) k_rgn_apply_nar(IngestArgs a) {
     uint32_t* qk = reinterpret_cast<uint32_t*>(lcell + (int64_t)FS * W) + wave * kApplyQ;
     int32_t* qv = reinterpret_cast<int32_t*>(lcell + (int64_t)FS * W) + nw * kApplyQ + wave * kApplyQ;
     int qn = 0;
-    const uint64_t* rk = reinterpret_cast<const uint64_t*>(a.e_key);
-    const uint32_t* rk32 = reinterpret_cast<const uint32_t*>(a.e_key);
-    const unsigned long long bocc = *(volatile unsigned long long*)a.batch_occ;
+    const unsigned long long cur_pos = a.cur_empty ? 0ull : (*(volatile unsigned long long*)a.batch_occ) & a.apply_mask;
     const int dom_sh = 64 - a.t.log2nreg;  // region = hash >> dom_sh; its low sr_bits: the region in the super-region
+    struct List {
+        const uint32_t* rows;
+        const int64_t* rbase;
+        const uint64_t* rk;
+        const uint32_t* rk32;
+        int64_t rb, re;
+        unsigned long long pos;  // ring positions this list contributes
+    };
+    const List lists[2] = {
+        {a.r_row, a.r_base, reinterpret_cast<const uint64_t*>(a.e_key), reinterpret_cast<const uint32_t*>(a.e_key), rb0,
+         re0, cur_pos & 0xffull},
+        {a.c_r_row, a.c_r_base, reinterpret_cast<const uint64_t*>(a.c_key), reinterpret_cast<const uint32_t*>(a.c_key),
+         rb1, re1, a.c_mask & 0xffull}};
 
     // which ring positions hold records of this super-region (a region without any skips
     // the state round trip)
@@ -1463,11 +1496,14 @@ __global__ void __launch_bounds__(kApplyThreads) k_rgn_apply_nar(IngestArgs a) {
     __syncthreads();
     {
         uint32_t any = 0;
-        for (int64_t rnd = rb + threadIdx.x; rnd < re; rnd += blockDim.x)
-            for (unsigned long long pm = bocc & 0xffull; pm; pm &= pm - 1) {
-                const int p = __ffsll((long long)pm) - 1;
-                if (a.r_row[rnd * kPartBuckets + ((col << 3) | p)] & 0xffffu) any |= 1u << p;
-            }
+        for (int l = 0; l < 2; ++l) {
+            const List& L = lists[l];
+            for (int64_t rnd = L.rb + threadIdx.x; rnd < L.re; rnd += blockDim.x)
+                for (unsigned long long pm = L.pos; pm; pm &= pm - 1) {
+                    const int p = __ffsll((long long)pm) - 1;
+                    if (L.rows[rnd * kPartBuckets + ((col << 3) | p)] & 0xffffu) any |= 1u << p;
+                }
+        }
         any = (uint32_t)wave_ior(any);
         if (lane == 0 && any) atomicOr(&s_pos, any);
     }
@@ -1581,116 +1617,122 @@ __global__ void __launch_bounds__(kApplyThreads) k_rgn_apply_nar(IngestArgs a) {
                 }
             }
         }
-        for (int64_t c0r = rb; c0r < re; c0r += kApplyRuns) {
-            const int nr = (int)min((int64_t)kApplyRuns, re - c0r);
-            __syncthreads();  // the cells are in; the previous block's descriptors consumed
-            for (int i = threadIdx.x; i < nr; i += blockDim.x) {
-                const int64_t rnd = c0r + i;
-                const uint32_t d = a.r_row[rnd * kPartBuckets + ccol];
-                r_cnt[i] = d & 0xffffu;
-                r_src[i] = (uint32_t)(a.r_base[rnd] + (d >> 16));
-            }
-            __syncthreads();
-            auto load_grp = [&](int i0, Grp& g) {
-                g.pre[0] = 0;
-#pragma unroll
-                for (int u = 0; u < kApplyGroup; ++u) {
-                    const int i = i0 + u;
-                    g.pre[u + 1] = g.pre[u] + (i < nr ? r_cnt[i] : 0u);
-                    g.src[u] = i < nr ? r_src[i] : 0u;
+        for (int l = 0; l < 2; ++l) {
+            const List& L = lists[l];
+            if (!((L.pos >> p) & 1)) continue;  // uniform
+            const uint64_t* rk = L.rk;
+            const uint32_t* rk32 = L.rk32;
+            for (int64_t c0r = L.rb; c0r < L.re; c0r += kApplyRuns) {
+                const int nr = (int)min((int64_t)kApplyRuns, L.re - c0r);
+                __syncthreads();  // the cells are in; the previous block's descriptors consumed
+                for (int i = threadIdx.x; i < nr; i += blockDim.x) {
+                    const int64_t rnd = c0r + i;
+                    const uint32_t d = L.rows[rnd * kPartBuckets + ccol];
+                    r_cnt[i] = d & 0xffffu;
+                    r_src[i] = (uint32_t)(L.rbase[rnd] + (d >> 16));
                 }
-            };
-            auto load_step = [&](const Grp& g, uint32_t k, Step& st, bool live) {
-                const uint32_t tot = live ? g.pre[kApplyGroup] : 0u;
+                __syncthreads();
+                auto load_grp = [&](int i0, Grp& g) {
+                    g.pre[0] = 0;
 #pragma unroll
-                for (int q = 0; q < kApplyUnroll; ++q) {
-                    const uint32_t e = k + q * 64 + lane;
-                    st.ok[q] = e < tot;
-                    uint32_t sb = g.src[0], sp = 0;
-#pragma unroll
-                    for (int w = 1; w < kApplyGroup; ++w) {
-                        if (e >= g.pre[w]) { sb = g.src[w]; sp = g.pre[w]; }
+                    for (int u = 0; u < kApplyGroup; ++u) {
+                        const int i = i0 + u;
+                        g.pre[u + 1] = g.pre[u] + (i < nr ? r_cnt[i] : 0u);
+                        g.src[u] = i < nr ? r_src[i] : 0u;
                     }
-                    const uint32_t x = st.ok[q] ? sb + (e - sp) : 0u;  // unconditional loads
-                    st.r[q] = N4 ? (uint64_t)rk32[x] : rk[x];
-                }
-            };
-            auto advance = [&](int& i0, uint32_t& k, Grp& g) -> bool {
-                k = k == ~0u ? 0u : k + 64 * kApplyUnroll;
-                while (i0 < nr && k >= g.pre[kApplyGroup]) {
-                    i0 += nw * kApplyGroup;
-                    k = 0;
-                    if (i0 < nr) load_grp(i0, g);
-                }
-                return i0 < nr;
-            };
-            // a record whose key is not in its home group waits in the wave's queue; 64 at a
-            // time the wave probes them with every lane busy
-            auto q_push = [&](bool pu, uint32_t kk, int32_t vv) {
-                const uint64_t bal = __ballot(pu);
-                if (pu) {
-                    const int at = qn + __popcll(bal & ((1ull << lane) - 1ull));
-                    qk[at] = kk;
-                    qv[at] = vv;
-                }
-                qn += __popcll(bal);
-                if (qn >= 64) {
-                    const int at = qn - 64 + lane;
-                    const uint32_t k2 = qk[at];
-                    const int s2 = probe_insert(k2, slot_hash((int64_t)k2));
-                    if (s2 >= 0) cell_add(s2, qv[at], pbit);
-                    else { flags |= GW_DF_TABLE_FULL; spills++; }
-                    qn -= 64;
-                }
-            };
-            auto apply_step = [&](const Step& c) {
-                uint32_t kq[kApplyUnroll];
-                int32_t vq[kApplyUnroll];
-                int hq[kApplyUnroll];
-                uint4 ka[kApplyUnroll];
+                };
+                auto load_step = [&](const Grp& g, uint32_t k, Step& st, bool live) {
+                    const uint32_t tot = live ? g.pre[kApplyGroup] : 0u;
 #pragma unroll
-                for (int q = 0; q < kApplyUnroll; ++q) {
-                    const uint64_t r = c.r[q];
-                    kq[q] = N4 ? (uint32_t)(r >> 4) : (uint32_t)r;
-                    vq[q] = N4 ? 1 : (int32_t)(uint32_t)(r >> 32) >> 4;
-                    const uint64_t h = slot_hash((int64_t)kq[q]);
-                    const int d = F > 1 ? (int)((h >> dom_sh) & (uint64_t)(F - 1)) : 0;
-                    hq[q] = d * S + (int)(h & (uint64_t)(S - 1) & ~(uint64_t)(kProbeGroup - 1));
-                }
+                    for (int q = 0; q < kApplyUnroll; ++q) {
+                        const uint32_t e = k + q * 64 + lane;
+                        st.ok[q] = e < tot;
+                        uint32_t sb = g.src[0], sp = 0;
 #pragma unroll
-                for (int q = 0; q < kApplyUnroll; ++q) ka[q] = *reinterpret_cast<const uint4*>(lkeys + hq[q]);
+                        for (int w = 1; w < kApplyGroup; ++w) {
+                            if (e >= g.pre[w]) { sb = g.src[w]; sp = g.pre[w]; }
+                        }
+                        const uint32_t x = st.ok[q] ? sb + (e - sp) : 0u;  // unconditional loads
+                        st.r[q] = N4 ? (uint64_t)rk32[x] : rk[x];
+                    }
+                };
+                auto advance = [&](int& i0, uint32_t& k, Grp& g) -> bool {
+                    k = k == ~0u ? 0u : k + 64 * kApplyUnroll;
+                    while (i0 < nr && k >= g.pre[kApplyGroup]) {
+                        i0 += nw * kApplyGroup;
+                        k = 0;
+                        if (i0 < nr) load_grp(i0, g);
+                    }
+                    return i0 < nr;
+                };
+                // a record whose key is not in its home group waits in the wave's queue; 64 at a
+                // time the wave probes them with every lane busy
+                auto q_push = [&](bool pu, uint32_t kk, int32_t vv) {
+                    const uint64_t bal = __ballot(pu);
+                    if (pu) {
+                        const int at = qn + __popcll(bal & ((1ull << lane) - 1ull));
+                        qk[at] = kk;
+                        qv[at] = vv;
+                    }
+                    qn += __popcll(bal);
+                    if (qn >= 64) {
+                        const int at = qn - 64 + lane;
+                        const uint32_t k2 = qk[at];
+                        const int s2 = probe_insert(k2, slot_hash((int64_t)k2));
+                        if (s2 >= 0) cell_add(s2, qv[at], pbit);
+                        else { flags |= GW_DF_TABLE_FULL; spills++; }
+                        qn -= 64;
+                    }
+                };
+                auto apply_step = [&](const Step& c) {
+                    uint32_t kq[kApplyUnroll];
+                    int32_t vq[kApplyUnroll];
+                    int hq[kApplyUnroll];
+                    uint4 ka[kApplyUnroll];
 #pragma unroll
-                for (int q = 0; q < kApplyUnroll; ++q) {
-                    const uint32_t k = kq[q];
-                    const int i = ka[q].x == k ? 0 : ka[q].y == k ? 1 : ka[q].z == k ? 2 : ka[q].w == k ? 3 : -1;
-                    const bool fast = c.ok[q] && i >= 0;
-                    if (fast) cell_add(hq[q] + i, vq[q], pbit);
-                    q_push(c.ok[q] && !fast, k, vq[q]);  // the wave is converged here
-                }
-            };
-            int i0 = wave * kApplyGroup;
-            uint32_t k = ~0u;
-            Grp g;
-            if (i0 < nr) load_grp(i0, g);
-            Step sa, sb;
-            bool live = advance(i0, k, g);
-            load_step(g, k, sa, live);
-            while (live) {
-                live = advance(i0, k, g);
-                load_step(g, k, sb, live);
-                apply_step(sa);
-                if (!live) break;
-                live = advance(i0, k, g);
+                    for (int q = 0; q < kApplyUnroll; ++q) {
+                        const uint64_t r = c.r[q];
+                        kq[q] = N4 ? (uint32_t)(r >> 4) : (uint32_t)r;
+                        vq[q] = N4 ? 1 : (int32_t)(uint32_t)(r >> 32) >> 4;
+                        const uint64_t h = slot_hash((int64_t)kq[q]);
+                        const int d = F > 1 ? (int)((h >> dom_sh) & (uint64_t)(F - 1)) : 0;
+                        hq[q] = d * S + (int)(h & (uint64_t)(S - 1) & ~(uint64_t)(kProbeGroup - 1));
+                    }
+#pragma unroll
+                    for (int q = 0; q < kApplyUnroll; ++q) ka[q] = *reinterpret_cast<const uint4*>(lkeys + hq[q]);
+#pragma unroll
+                    for (int q = 0; q < kApplyUnroll; ++q) {
+                        const uint32_t k = kq[q];
+                        const int i = ka[q].x == k ? 0 : ka[q].y == k ? 1 : ka[q].z == k ? 2 : ka[q].w == k ? 3 : -1;
+                        const bool fast = c.ok[q] && i >= 0;
+                        if (fast) cell_add(hq[q] + i, vq[q], pbit);
+                        q_push(c.ok[q] && !fast, k, vq[q]);  // the wave is converged here
+                    }
+                };
+                int i0 = wave * kApplyGroup;
+                uint32_t k = ~0u;
+                Grp g;
+                if (i0 < nr) load_grp(i0, g);
+                Step sa, sb;
+                bool live = advance(i0, k, g);
                 load_step(g, k, sa, live);
-                apply_step(sb);
+                while (live) {
+                    live = advance(i0, k, g);
+                    load_step(g, k, sb, live);
+                    apply_step(sa);
+                    if (!live) break;
+                    live = advance(i0, k, g);
+                    load_step(g, k, sa, live);
+                    apply_step(sb);
+                }
+                if (lane < qn) {  // the rest of the queue
+                    const uint32_t k2 = qk[lane];
+                    const int s2 = probe_insert(k2, slot_hash((int64_t)k2));
+                    if (s2 >= 0) cell_add(s2, qv[lane], pbit);
+                    else { flags |= GW_DF_TABLE_FULL; spills++; }
+                }
+                qn = 0;
             }
-            if (lane < qn) {  // the rest of the queue
-                const uint32_t k2 = qk[lane];
-                const int s2 = probe_insert(k2, slot_hash((int64_t)k2));
-                if (s2 >= 0) cell_add(s2, qv[lane], pbit);
-                else { flags |= GW_DF_TABLE_FULL; spills++; }
-            }
-            qn = 0;
         }
         __syncthreads();
         {  // write back this position's pane
@@ -1706,29 +1748,32 @@ __global__ void __launch_bounds__(kApplyThreads) k_rgn_apply_nar(IngestArgs a) {
     // key table were not applied; mark them for k_rgn_collect_nar2.
     if (__syncthreads_or(spills != 0)) {
         unsigned long long marked = 0;
-        for (uint32_t pm = pmask; pm; pm &= pm - 1) {
-            const int p = __ffs((int)pm) - 1;
-            const int64_t ccol = (col << 3) | p;
-            for (int64_t rnd = rb + wave; rnd < re; rnd += nw) {
-                const uint32_t d = a.r_row[rnd * kPartBuckets + ccol];
-                const int64_t src = a.r_base[rnd] + (d >> 16);
-                for (uint32_t k = lane; k < (d & 0xffffu); k += 64) {
-                    const uint64_t r = N4 ? (uint64_t)rk32[src + k] : rk[src + k];
-                    const uint32_t kk = N4 ? (uint32_t)(r >> 4) : (uint32_t)r;
-                    const uint64_t h = slot_hash((int64_t)kk);
-                    const int dd = F > 1 ? (int)((h >> dom_sh) & (uint64_t)(F - 1)) : 0;
-                    int j = (int)(h & (uint64_t)(S - 1) & ~(uint64_t)(kProbeGroup - 1));
-                    bool present = false;
-                    for (int q = 0; q < S; ++q) {
-                        const uint32_t x = lkeys[dd * S + j];
-                        if (x == kk) { present = true; break; }
-                        if (x == kK32Empty) break;
-                        j = (j + 1) & (S - 1);
-                    }
-                    if (!present) {
-                        if constexpr (N4) const_cast<uint32_t*>(rk32)[src + k] = (uint32_t)r | kNarSpill;
-                        else const_cast<uint64_t*>(rk)[src + k] = r | ((uint64_t)kNarSpill << 32);
-                        marked++;
+        for (int l = 0; l < 2; ++l) {
+            const List& L = lists[l];
+            for (unsigned long long pm = L.pos & pmask; pm; pm &= pm - 1) {
+                const int p = __ffsll((long long)pm) - 1;
+                const int64_t ccol = (col << 3) | p;
+                for (int64_t rnd = L.rb + wave; rnd < L.re; rnd += nw) {
+                    const uint32_t d = L.rows[rnd * kPartBuckets + ccol];
+                    const int64_t src = L.rbase[rnd] + (d >> 16);
+                    for (uint32_t k = lane; k < (d & 0xffffu); k += 64) {
+                        const uint64_t r = N4 ? (uint64_t)L.rk32[src + k] : L.rk[src + k];
+                        const uint32_t kk = N4 ? (uint32_t)(r >> 4) : (uint32_t)r;
+                        const uint64_t h = slot_hash((int64_t)kk);
+                        const int dd = F > 1 ? (int)((h >> dom_sh) & (uint64_t)(F - 1)) : 0;
+                        int j = (int)(h & (uint64_t)(S - 1) & ~(uint64_t)(kProbeGroup - 1));
+                        bool present = false;
+                        for (int q = 0; q < S; ++q) {
+                            const uint32_t x = lkeys[dd * S + j];
+                            if (x == kk) { present = true; break; }
+                            if (x == kK32Empty) break;
+                            j = (j + 1) & (S - 1);
+                        }
+                        if (!present) {
+                            if constexpr (N4) const_cast<uint32_t*>(L.rk32)[src + k] = (uint32_t)r | kNarSpill;
+                            else const_cast<uint64_t*>(L.rk)[src + k] = r | ((uint64_t)kNarSpill << 32);
+                            marked++;
+                        }
                     }
                 }
             }
@@ -1764,8 +1809,12 @@ __global__ void __launch_bounds__(kApplyThreads) k_rgn_apply_nar(IngestArgs a) {
 template <int AGG>
 __global__ void __launch_bounds__(256) k_rgn_collect_nar2(IngestArgs a) {
     constexpr bool N4 = AGG == GW_COUNT;
-    const int64_t n = a.bk_off[1 << a.d1_bits];
-    int64_t* rk = a.e_key;
+    // this flush's P2 output, then (blockIdx.y == 1) the carried output it applied from
+    const bool carry = blockIdx.y == 1;
+    if (carry ? !a.c_mask : a.cur_empty) return;
+    const int nb1 = 1 << a.d1_bits;
+    const int64_t n = carry ? a.c_rbeg[kPartBuckets + 1 + nb1] : a.bk_off[nb1];
+    int64_t* rk = carry ? a.c_key : a.e_key;
     uint32_t* rk32 = reinterpret_cast<uint32_t*>(rk);
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t base = blockIdx.x * (int64_t)blockDim.x; base < n; base += stride) {
@@ -2557,7 +2606,7 @@ hipError_t launch_region_flush(const IngestArgs& a, hipStream_t s) {
     const size_t apply_lds = (size_t)(S + pt_mask_words(a.t)) * 8 + (size_t)2 * S * a.t.words * 8 +
                              (size_t)(kApplyThreads / 64) * kApplyQ * (a.t.words == 2 ? 25 : 17);  // + miss queues
     const int nb1 = 1 << a.d1_bits;
-    if (a.ntiles == 0) return hipSuccess;
+    if (a.ntiles == 0 && !(a.nar2 && a.c_mask)) return hipSuccess;
 #define L2(A, CM)                                                                                               \
     lds_opt_in((const void*)k_rgn_p2<A, CM>, part_lds);                                                       \
     lds_opt_in((const void*)k_rgn_apply<A, CM>, apply_lds);                                                   \
@@ -2586,11 +2635,13 @@ hipError_t launch_region_flush(const IngestArgs& a, hipStream_t s) {
 #define LN(A)                                                                                                   \
     lds_opt_in((const void*)k_rgn_p2<A, kFmtNar>, part_lds);                                                   \
     lds_opt_in((const void*)k_rgn_apply_nar<A>, lds);                                                         \
-    hipLaunchKernelGGL(k_rgn_plan1, dim3((unsigned)a.ngroups), dim3(256), 0, s, a);                            \
-    hipLaunchKernelGGL(k_rgn_plan2, dim3((unsigned)nb1), dim3(256), 0, s, a);                                  \
-    hipLaunchKernelGGL(k_rgn_plan3, dim3(1), dim3(256), 0, s, a);                                              \
-    hipLaunchKernelGGL((k_rgn_p2<A, kFmtNar>), dim3((unsigned)(a.ngroups * nb1)), dim3(kPartThreads), part_lds, s, \
-                       a);                                                                                      \
+    if (!a.cur_empty) {                                                                                         \
+        hipLaunchKernelGGL(k_rgn_plan1, dim3((unsigned)a.ngroups), dim3(256), 0, s, a);                        \
+        hipLaunchKernelGGL(k_rgn_plan2, dim3((unsigned)nb1), dim3(256), 0, s, a);                              \
+        hipLaunchKernelGGL(k_rgn_plan3, dim3(1), dim3(256), 0, s, a);                                          \
+        hipLaunchKernelGGL((k_rgn_p2<A, kFmtNar>), dim3((unsigned)(a.ngroups * nb1)), dim3(kPartThreads), part_lds, \
+                           s, a);                                                                               \
+    }                                                                                                           \
     hipLaunchKernelGGL(k_rgn_apply_nar<A>, dim3((unsigned)(a.t.nreg >> a.sr_bits)), dim3(kApplyThreads), lds, s, a)
         GW_AGG_SWITCH(a.t.agg, LN);
 #undef LN
@@ -2606,7 +2657,7 @@ hipError_t launch_region_collect(const IngestArgs& a, hipStream_t s) {
     const int64_t n = a.ntiles * kPartTile;  // upper bound of the buffer's records
 #define L(A)                                                                                         \
     if (a.fmt == kFmtNar && a.nar2)                                                                  \
-        hipLaunchKernelGGL(k_rgn_collect_nar2<A>, dim3(grid_for(n)), dim3(256), 0, s, a);           \
+        hipLaunchKernelGGL(k_rgn_collect_nar2<A>, dim3(grid_for(n), 2), dim3(256), 0, s, a);        \
     else if (a.fmt == kFmtNar)                                                                       \
         hipLaunchKernelGGL(k_rgn_collect_nar<A>, dim3((unsigned)a.t.nreg), dim3(256), 0, s, a);     \
     else if (a.fmt == kFmtCmp)                                                                       \

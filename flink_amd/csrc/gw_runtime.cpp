@@ -102,6 +102,33 @@ void par_memcpy(void* dst, const void* src, size_t bytes) {
     for (auto& t : th) t.join();
 }
 
+// Several host copies at once, split evenly over up to 8 threads (the pieces of one drain chunk).
+void par_copy_multi(const std::vector<std::tuple<void*, const void*, size_t>>& parts) {
+    size_t total = 0;
+    for (auto& p : parts) total += std::get<2>(p);
+    const int nt = (int)std::min<size_t>(8, total / ((size_t)1 << 20));
+    if (nt <= 1) {
+        for (auto& p : parts) memcpy(std::get<0>(p), std::get<1>(p), std::get<2>(p));
+        return;
+    }
+    const size_t share = (total + nt - 1) / nt;
+    std::vector<std::thread> th;
+    size_t pi = 0, po = 0;  // next part, offset in it
+    for (int t = 0; t < nt && pi < parts.size(); ++t) {
+        std::vector<std::tuple<char*, const char*, size_t>> mine;
+        size_t left = share;
+        while (left && pi < parts.size()) {
+            const size_t len = std::min(left, std::get<2>(parts[pi]) - po);
+            mine.emplace_back((char*)std::get<0>(parts[pi]) + po, (const char*)std::get<1>(parts[pi]) + po, len);
+            left -= len;
+            po += len;
+            if (po == std::get<2>(parts[pi])) { ++pi; po = 0; }
+        }
+        th.emplace_back([mine] { for (auto& m : mine) memcpy(std::get<0>(m), std::get<1>(m), std::get<2>(m)); });
+    }
+    for (auto& t : th) t.join();
+}
+
 struct KernelTimer {
     std::vector<std::pair<hipEvent_t, hipEvent_t>> pending;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> pool;
@@ -233,6 +260,22 @@ struct gw_handle {
     bool cmp_off = false;           // compact records turned off: too many values beyond 32 bits
     bool nar_off = false;           // narrow records turned off: too many keys / values beyond them
     int64_t buf_limit = (int64_t)1 << 27;  // records (GW_BUFFER_RECORDS)
+    // nar2 carry: a fire's flush applies only the ring positions the fire needs
+    // and leaves the newer ones in its P2 output, which the next flush applies from there.  Two
+    // P2 output sets (key words, round rows, round bases, rbeg | bk_off) used in turn: eset is
+    // the one the next P2 writes; while carry_on, set eset ^ 1 holds carry_mask's positions.
+    int64_t* e2_key = nullptr;
+    uint32_t* r_row2 = nullptr;
+    int64_t* r_base2 = nullptr;
+    int64_t* rbeg2 = nullptr;
+    int64_t e2_cap = 0;             // tiles
+    int eset = 0;
+    bool carry_on = false;
+    uint64_t carry_mask = 0;
+    int64_t* eset_key(int s) const { return s ? e2_key : e_col[0]; }
+    uint32_t* eset_row(int s) const { return s ? r_row2 : r_row; }
+    int64_t* eset_base(int s) const { return s ? r_base2 : r_base; }
+    int64_t* eset_rbeg(int s) const { return s ? rbeg2 : rbeg; }
 
     // allowed lateness > 0 (tumbling / sliding): late records of fired, not yet cleaned
     // windows wait on the re-fire list until the next watermark (process_refire)
@@ -264,15 +307,22 @@ struct gw_handle {
     int64_t def_cap = 0;
     int cur = 0;
 
-    // host-ingest staging
-    // Two pinned slots used in turn: a slot is refilled only after the H2D copy that read it
-    // has completed (ev_stage), so the host fills one slot while the other is in flight.
-    int64_t* h_stage[2] = {nullptr, nullptr};  // pinned: key | ts | val | hash (int32)
-    hipEvent_t ev_stage[2] = {nullptr, nullptr};
-    int stage_slot = 0;
-    int64_t* d_stage = nullptr;  // device: key | ts | val
-    int32_t* d_hash_stage = nullptr;
-    int64_t stage_cap = 0;
+    // Host-ingest staging (gw_ingest, gw_stage_*).  Pinned host slots (key | ts | value columns
+    // of slot_cap records, then the int32 key hashes) that a caller fills in place (a JVM writes
+    // its records straight into them) or gw_ingest copies into; each batch goes over PCIe on a
+    // copy stream into one of two device staging buffers used in turn, so the H2D of batch b+1
+    // runs while batch b is aggregated.  A slot is refilled only after its H2D (ev_slot); a
+    // device buffer is overwritten only after the ingest that read it (ev_dread).
+    std::vector<int64_t*> h_slot;
+    std::vector<hipEvent_t> ev_slot;
+    std::vector<bool> slot_used;
+    int64_t slot_cap = 0;
+    int stage_next = 0;             // gw_ingest's next slot (of the first two)
+    int64_t* d_stage2[2] = {nullptr, nullptr};
+    hipEvent_t ev_dread[2] = {nullptr, nullptr};
+    bool dread_valid[2] = {false, false};
+    int dturn = 0;
+    hipStream_t cstream = nullptr;
 
     // output rows (device SoA), [rows_head, st.rows) pending
     int64_t* o_key = nullptr;
@@ -388,7 +438,9 @@ struct gw_handle {
         hp.lap(3);
         if (async_gen[o] != hgen) return GW_OK;  // the host changed the status since
         memcpy(h_st, h_st_async[o], sizeof(DevStatus));
-        lazy_recs = 0;  // the batches after the absorbed slot are unaccounted for
+        // unaccounted for: the absorbed slot's own batch (its P1 published at its start) and
+        // every batch after it
+        lazy_recs = async_recs[o];
         for (int i = 0; i < kAsync; ++i)
             if (async_pending[i]) lazy_recs += async_recs[i];
         rc = absorb();
@@ -452,6 +504,12 @@ struct gw_handle {
         return GW_OK;
     }
     void free_region() {
+        for (void** p : {(void**)&e2_key, (void**)&r_row2, (void**)&r_base2, (void**)&rbeg2}) {
+            if (*p) hipFree(*p);
+            *p = nullptr;
+        }
+        e2_cap = 0;
+        eset = 0;
         for (auto& p : e_col) { if (p) hipFree(p); p = nullptr; }
         for (auto& p : e_pos) { if (p) hipFree(p); p = nullptr; }
         for (void** p : {(void**)&p1_row, (void**)&p2_desc, (void**)&p2_off, (void**)&p2_roff, (void**)&r_row,
@@ -466,6 +524,10 @@ struct gw_handle {
     int ensure_region(int64_t need, int64_t want) {
         if (!rbeg) HIPCHECK(hipMalloc((void**)&rbeg, (size_t)2 * (kPartBuckets + 1) * 8));  // rbeg | bk_off
         if (need <= buf_cap) return GW_OK;
+        if (carry_on) {  // the carried records live in the buffers about to be re-allocated
+            int rc = flush_buffer();
+            if (rc) return rc;
+        }
         if (nseg) return fail(GW_E_STATE, "internal: region buffer re-allocated with %d segments waiting", nseg);
         const int64_t cap = std::max(need, want);
         const size_t recs = (size_t)cap * kPartTile;
@@ -483,6 +545,21 @@ struct gw_handle {
         HIPCHECK(hipMalloc((void**)&r_row, (size_t)max_rounds(cap) * kPartBuckets * 4));
         HIPCHECK(hipMalloc((void**)&r_base, (size_t)max_rounds(cap) * 8));
         buf_cap = cap;
+        return GW_OK;
+    }
+    // The second P2 output set (nar2 carry), as large as the first.
+    int ensure_eset2() {
+        if (e2_cap == buf_cap && e2_key) return GW_OK;
+        for (void** p : {(void**)&e2_key, (void**)&r_row2, (void**)&r_base2, (void**)&rbeg2}) {
+            if (*p) hipFree(*p);
+            *p = nullptr;
+        }
+        const size_t recs = (size_t)buf_cap * kPartTile;
+        HIPCHECK(hipMalloc((void**)&e2_key, recs * 8));
+        HIPCHECK(hipMalloc((void**)&r_row2, (size_t)max_rounds(buf_cap) * kPartBuckets * 4));
+        HIPCHECK(hipMalloc((void**)&r_base2, (size_t)max_rounds(buf_cap) * 8));
+        HIPCHECK(hipMalloc((void**)&rbeg2, (size_t)2 * (kPartBuckets + 1) * 8));
+        e2_cap = buf_cap;
         return GW_OK;
     }
     int ensure_deferred(int64_t need) {
@@ -532,29 +609,93 @@ struct gw_handle {
         return GW_OK;
     }
     void free_stage() {
-        for (int i = 0; i < 2; ++i) {
-            if (h_stage[i]) hipHostFree(h_stage[i]);
-            if (ev_stage[i]) hipEventDestroy(ev_stage[i]);
-            h_stage[i] = nullptr;
-            ev_stage[i] = nullptr;
+        if (cstream) hipStreamSynchronize(cstream);
+        hipStreamSynchronize(stream);
+        for (size_t i = 0; i < h_slot.size(); ++i) {
+            if (h_slot[i]) hipHostFree(h_slot[i]);
+            if (ev_slot[i]) hipEventDestroy(ev_slot[i]);
         }
-        if (d_stage) hipFree(d_stage);
-        if (d_hash_stage) hipFree(d_hash_stage);
-        d_stage = nullptr;
-        d_hash_stage = nullptr;
-        stage_cap = 0;
+        h_slot.clear();
+        ev_slot.clear();
+        slot_used.clear();
+        for (int t = 0; t < 2; ++t) {
+            if (d_stage2[t]) hipFree(d_stage2[t]);
+            d_stage2[t] = nullptr;
+            dread_valid[t] = false;
+        }
+        slot_cap = 0;
     }
-    int ensure_stage(int64_t n) {
-        if (n <= stage_cap) return GW_OK;
-        HIPCHECK(hipStreamSynchronize(stream));  // no copy still reads the old buffers
+    // `slots` pinned slots of >= n records each (and the two device buffers of that size).
+    int ensure_stage(int64_t n, int slots = 2) {
+        if (n <= slot_cap && (int)h_slot.size() >= slots) return GW_OK;
+        const int64_t cap = std::max(n, slot_cap);
+        const int ns = std::max(slots, (int)h_slot.size());
         free_stage();
-        for (int i = 0; i < 2; ++i) {
-            HIPCHECK(hipHostMalloc((void**)&h_stage[i], (size_t)n * 28, hipHostMallocDefault));
-            HIPCHECK(hipEventCreateWithFlags(&ev_stage[i], hipEventDisableTiming));
+        if (!cstream) HIPCHECK(hipStreamCreateWithFlags(&cstream, hipStreamNonBlocking));
+        for (int t = 0; t < 2; ++t) {
+            if (!ev_dread[t]) HIPCHECK(hipEventCreateWithFlags(&ev_dread[t], hipEventDisableTiming));
+            HIPCHECK(hipMalloc((void**)&d_stage2[t], (size_t)cap * 28));
         }
-        HIPCHECK(hipMalloc((void**)&d_stage, (size_t)n * 24));
-        HIPCHECK(hipMalloc((void**)&d_hash_stage, (size_t)n * 4));
-        stage_cap = n;
+        h_slot.assign(ns, nullptr);
+        ev_slot.assign(ns, nullptr);
+        slot_used.assign(ns, false);
+        for (int i = 0; i < ns; ++i) {
+            HIPCHECK(hipHostMalloc((void**)&h_slot[i], (size_t)cap * 28, hipHostMallocDefault));
+            HIPCHECK(hipEventCreateWithFlags(&ev_slot[i], hipEventDisableTiming));
+        }
+        slot_cap = cap;
+        return GW_OK;
+    }
+    // Fired rows to caller memory (any host memory, e.g. a JVM direct ByteBuffer): large
+    // drains go through two pinned bounce chunks -- the D2H of chunk j+1 runs while chunk j is
+    // copied out by several threads -- instead of one pageable copy per column.
+    int64_t* h_bounce = nullptr;
+    hipEvent_t ev_bounce[2] = {nullptr, nullptr};
+    static constexpr int64_t kBounceRows = (int64_t)1 << 21;  // per chunk and column (16 MB)
+    int drain_to_host(int64_t* const dst[4], const int64_t* const src[4], int64_t c) {
+        static const bool direct = [] { const char* v = getenv("GW_DRAIN_BOUNCE"); return v && atoi(v) == 0; }();
+        if (direct || c < kBounceRows / 4) {
+            hipError_t err = hipSuccess;
+            for (int i = 0; i < 4 && err == hipSuccess; ++i)
+                if (dst[i]) err = hipMemcpyAsync(dst[i], src[i], c * 8, hipMemcpyDeviceToHost, stream);
+            if (err == hipSuccess) err = hipStreamSynchronize(stream);
+            if (err != hipSuccess) return fail(GW_E_DEVICE, "D2H rows: %s", hipGetErrorString(err));
+            return GW_OK;
+        }
+        if (!h_bounce) {
+            HIPCHECK(hipHostMalloc((void**)&h_bounce, (size_t)2 * 4 * kBounceRows * 8, hipHostMallocDefault));
+            for (auto& ev : ev_bounce) HIPCHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        }
+        const int64_t nch = (c + kBounceRows - 1) / kBounceRows;
+        auto issue = [&](int64_t j) -> hipError_t {
+            const int64_t lo = j * kBounceRows, len = std::min(kBounceRows, c - lo);
+            int64_t* b = h_bounce + (j & 1) * 4 * kBounceRows;
+            hipError_t err = hipSuccess;
+            for (int i = 0; i < 4 && err == hipSuccess; ++i)
+                if (dst[i]) err = hipMemcpyAsync(b + i * kBounceRows, src[i] + lo, len * 8, hipMemcpyDeviceToHost, stream);
+            return err == hipSuccess ? hipEventRecord(ev_bounce[j & 1], stream) : err;
+        };
+        hipError_t err = issue(0);
+        for (int64_t j = 0; j < nch && err == hipSuccess; ++j) {
+            if (j + 1 < nch) err = issue(j + 1);
+            if (err == hipSuccess) err = hipEventSynchronize(ev_bounce[j & 1]);
+            if (err != hipSuccess) break;
+            const int64_t lo = j * kBounceRows, len = std::min(kBounceRows, c - lo);
+            const int64_t* b = h_bounce + (j & 1) * 4 * kBounceRows;
+            std::vector<std::tuple<void*, const void*, size_t>> parts;
+            for (int i = 0; i < 4; ++i)
+                if (dst[i]) parts.emplace_back(dst[i] + lo, b + i * kBounceRows, (size_t)len * 8);
+            par_copy_multi(parts);
+        }
+        if (err != hipSuccess) return fail(GW_E_DEVICE, "D2H rows: %s", hipGetErrorString(err));
+        return GW_OK;
+    }
+    // Wait until slot i's last H2D has read it (the caller may write it then).
+    int slot_ready(int i) {
+        if (slot_used[i]) {
+            hipError_t e = hipEventSynchronize(ev_slot[i]);
+            if (e != hipSuccess) return fail(GW_E_DEVICE, "staging: %s", hipGetErrorString(e));
+        }
         return GW_OK;
     }
 
@@ -587,7 +728,7 @@ struct gw_handle {
     }
     // Keep the load factor of the linear-probing table below 0.7.
     int maybe_grow(int64_t incoming) {
-        if (nseg) {  // waiting segments are bucketed for this table's regions: apply them first
+        if (nseg || carry_on) {  // waiting segments are bucketed for this table's regions: apply them first
             if (!(h_st->flags & GW_DF_TABLE_FULL) && (double)h_st->used_slots <= 0.7 * (double)tv.cap) return GW_OK;
             int rc = flush_buffer();  // refreshes the counters (and may grow by itself)
             if (rc) return rc;
@@ -813,6 +954,8 @@ struct gw_handle {
     int rebase(i128 nb) {
         int rc;
         if (nb < B) {
+            // evicted positions may hold panes whose records are still carried: apply them first
+            if (carry_on && (rc = flush_buffer())) return rc;
             uint64_t emask = 0;
             EvictArgs e{};
             for (i128 p = std::max(nb + R, B); p < B + R; ++p) {
@@ -981,15 +1124,16 @@ struct gw_handle {
         a.d1_bits = l2 <= 14 ? std::min(l2, 7) : (l2 + 1) / 2;
         a.d2_bits = l2 - a.d1_bits;
         a.p1_key = e_col[3]; a.p1_a0 = e_col[4]; a.p1_a1 = e_col[5]; a.p1_pos = e_pos[1];
-        a.e_key = e_col[0]; a.e_a0 = e_col[1]; a.e_a1 = e_col[2]; a.e_pos = e_pos[0];
+        a.e_key = eset_key(eset); a.e_a0 = e_col[1]; a.e_a1 = e_col[2]; a.e_pos = e_pos[0];
         a.p1_row = p1_row;
         a.p2_desc = p2_desc;
         a.p2_off = p2_off;
         a.p2_roff = p2_roff;
-        a.rbeg = rbeg;
-        a.bk_off = rbeg + kPartBuckets + 1;
-        a.r_row = r_row;
-        a.r_base = r_base;
+        a.rbeg = eset_rbeg(eset);
+        a.bk_off = a.rbeg + kPartBuckets + 1;
+        a.r_row = eset_row(eset);
+        a.r_base = eset_base(eset);
+        a.apply_mask = ~0ull;
         a.batch_occ = d_tmp + 1;
         a.fmt = buf_fmt;
         // narrow records of two-pass tables: k_rgn_apply_nar over super-regions of F regions
@@ -1042,20 +1186,50 @@ struct gw_handle {
     // P2 + apply over every waiting segment (one fire's worth of batches).  Runs before
     // any fire, rehash, merge or non-region ingest, so the table is exact whenever it is
     // read.
-    int flush_buffer() {
-        if (!nseg) return GW_OK;
+    // apply_mask (a fire, nar2 only): ring positions that must be applied now; the others may
+    // stay in this flush's P2 output until the next flush (carry).  Every other caller applies
+    // everything, carried positions included.
+    int flush_buffer(uint64_t apply_mask = ~0ull) {
+        if (!nseg && !carry_on) return GW_OK;
         int rc;
         IngestArgs a;
         if ((rc = base_args(a, 0, nullptr, nullptr, nullptr))) return rc;
         region_args(a);
+        if (carry_on && !a.nar2) return fail(GW_E_STATE, "internal: carried records without a nar2 flush");
         a.ntiles = buf_tiles;
         a.p2_group = region_group(a.d1_bits);
         a.ngroups = (buf_tiles + a.p2_group - 1) / a.p2_group;
         a.ring_fresh = buf_fresh;
+        a.cur_empty = nseg == 0;
+        if (carry_on) {
+            const int c = eset ^ 1;
+            a.c_mask = carry_mask;
+            a.c_key = eset_key(c);
+            a.c_r_row = eset_row(c);
+            a.c_r_base = eset_base(c);
+            a.c_rbeg = eset_rbeg(c);
+        }
+        // carry only what a fire leaves behind, on the plain path (no lateness, no restored
+        // windows); at most one flush deep
+        uint64_t carry_next = 0;
+        static const bool carry_off = [] { const char* e = getenv("GW_NAR_CARRY"); return e && atoi(e) == 0; }();
+        if (a.nar2 && nseg && apply_mask != ~0ull && cfg.allowed_lateness == 0 && ov_n == 0 && !carry_off) {
+            const uint64_t ring = R >= 64 ? ~0ull : ((1ull << R) - 1);
+            carry_next = ring & ~apply_mask;
+            a.apply_mask = apply_mask;
+            // the next P2 writes the other set; the one carried so far is applied by this flush
+            if (carry_next && (rc = ensure_eset2())) return rc;
+        }
         const int64_t window_recs = buf_recs;
         nseg = 0;  // before any launch: the TABLE_FULL handling below may grow the table
         buf_tiles = 0;
         buf_recs = 0;
+        carry_on = false;
+        if (carry_next) {
+            carry_on = true;
+            carry_mask = carry_next;
+            eset ^= 1;
+        }
         if (timing) {
             auto ev = t_apply.get();
             HIPCHECK(hipEventRecord(ev.first, stream));
@@ -1132,9 +1306,16 @@ struct gw_handle {
             region_args(a);
             a.tile0 = buf_tiles;
             if (nseg == 0) {
+                const int fmt = region_fmt(a.d1_bits);
+                if (carry_on && fmt != buf_fmt) {  // carried records keep their window's format: apply them
+                    if ((rc = flush_buffer())) return rc;
+                    if ((rc = base_args(a, nrec, key, ts, val))) return rc;
+                    region_args(a);
+                    a.tile0 = buf_tiles;
+                }
                 HIPCHECK(hipMemsetAsync(d_tmp + 1, 0, 8, stream));
                 buf_fresh = ~occ;
-                buf_fmt = region_fmt(a.d1_bits);
+                buf_fmt = fmt;
             }
             a.fmt = buf_fmt;
             stats.region_format = buf_fmt;
@@ -1149,7 +1330,6 @@ struct gw_handle {
             } else {
                 HIPCHECK(launch_region_p1(a, stream));
             }
-            if (buffered) HIPCHECK(launch_publish_status(a, stream));
             nseg++;
             buf_tiles += tiles;
             buf_recs += nrec;
@@ -1911,6 +2091,18 @@ struct gw_handle {
                 wm = w;
                 return GW_OK;
             }
+            // buffered records first, then the timers; the flush ends with a status refresh
+            // (and emits no row), so the row count before the firing is read after it: one
+            // host round trip fewer per fire than a refresh before the flush.  Only the ring
+            // positions of panes up to the last one of the last window firing now must be
+            // applied; newer panes may wait for the next flush (nar2 carry).
+            uint64_t need = ~0ull;
+            const i128 plast = kt * m + n - 1;
+            if (plast < B + R - 1) {
+                need = 0;
+                for (i128 P = B; P <= plast; ++P) need |= 1ull << pos_of(P);
+            }
+            if ((rc = flush_buffer(need))) return rc;
             if ((rc = ensure_fresh())) return rc;
             before = (int64_t)h_st->rows;
         }
@@ -2257,6 +2449,13 @@ int gw_destroy(gw_handle* h) {
     if (h->h_nbwm) hipHostFree(h->h_nbwm);
     if (h->h_nbbytes) hipHostFree(h->h_nbbytes);
     if (h->d_nbbytes) hipFree(h->d_nbbytes);
+    h->free_stage();
+    if (h->h_bounce) hipHostFree(h->h_bounce);
+    for (auto ev : h->ev_bounce)
+        if (ev) hipEventDestroy(ev);
+    for (int t = 0; t < 2; ++t)
+        if (h->ev_dread[t]) hipEventDestroy(h->ev_dread[t]);
+    if (h->cstream) hipStreamDestroy(h->cstream);
     if (h->ev_in) hipEventDestroy(h->ev_in);
     if (h->ev_out) hipEventDestroy(h->ev_out);
     if (h->stream && !h->shared_stream) hipStreamDestroy(h->stream);
@@ -2588,6 +2787,8 @@ int gw_drain_payload(gw_handle* h, int64_t* key, int64_t* start, int64_t* end, v
     return h->c_rows - h->c_head > 0 ? GW_E_OUTPUT_FULL : GW_OK;
 }
 
+static int stage_ingest(gw_handle* h, int slot, int64_t n, bool with_hash, bool with_value);
+
 int gw_ingest(gw_handle* h, int64_t n, const int64_t* key, const int32_t* key_hash, const int64_t* ts,
               const void* value) {
     if (!h) return GW_E_INVALID;
@@ -2605,30 +2806,75 @@ int gw_ingest(gw_handle* h, int64_t n, const int64_t* key, const int32_t* key_ha
         const int64_t c = std::min(chunk, n - off);
         int rc = h->ensure_stage(c);
         if (rc) return rc;
-        const int slot = h->stage_slot;
-        h->stage_slot ^= 1;
-        int64_t* hs = h->h_stage[slot];
-        {
-            hipError_t e = hipEventSynchronize(h->ev_stage[slot]);  // the slot's previous H2D is done
-            if (e != hipSuccess) return h->fail(GW_E_DEVICE, "staging: %s", hipGetErrorString(e));
-        }
+        const int slot = h->stage_next;
+        h->stage_next ^= 1;
+        if ((rc = h->slot_ready(slot))) return rc;
+        int64_t* hs = h->h_slot[slot];
+        const int64_t cap = h->slot_cap;
         par_memcpy(hs, key + off, (size_t)c * 8);
-        par_memcpy(hs + c, ts + off, (size_t)c * 8);
-        if (value) par_memcpy(hs + 2 * c, (const int64_t*)value + off, (size_t)c * 8);
-        if (key_hash) memcpy(hs + 3 * c, key_hash + off, (size_t)c * 4);
-        {
-            hipError_t e = hipMemcpyAsync(h->d_stage, hs, (size_t)c * (value ? 24 : 16), hipMemcpyHostToDevice,
-                                          h->stream);
-            if (e == hipSuccess && key_hash)
-                e = hipMemcpyAsync(h->d_hash_stage, hs + 3 * c, (size_t)c * 4, hipMemcpyHostToDevice, h->stream);
-            if (e == hipSuccess) e = hipEventRecord(h->ev_stage[slot], h->stream);
-            if (e != hipSuccess) return h->fail(GW_E_DEVICE, "H2D: %s", hipGetErrorString(e));
-        }
-        if ((rc = h->check_keys(c, h->d_stage, key_hash ? h->d_hash_stage : nullptr))) return rc;
-        rc = ingest_device_impl(h, c, h->d_stage, h->d_stage + c, value ? h->d_stage + 2 * c : nullptr);
-        if (rc) return rc;
+        par_memcpy(hs + cap, ts + off, (size_t)c * 8);
+        if (value) par_memcpy(hs + 2 * cap, (const int64_t*)value + off, (size_t)c * 8);
+        if (key_hash) memcpy(hs + 3 * cap, key_hash + off, (size_t)c * 4);
+        if ((rc = stage_ingest(h, slot, c, key_hash != nullptr, value != nullptr))) return rc;
     }
     return GW_OK;
+}
+
+// One filled pinned slot -> device (copy stream) -> ingest (the handle's stream).
+static int stage_ingest(gw_handle* h, int slot, int64_t n, bool with_hash, bool with_value) {
+    const int t = h->dturn;
+    h->dturn ^= 1;
+    const int64_t cap = h->slot_cap;
+    int64_t* hs = h->h_slot[slot];
+    int64_t* ds = h->d_stage2[t];
+    int32_t* dh = (int32_t*)(ds + 3 * cap);
+    hipError_t e = hipSuccess;
+    if (h->dread_valid[t]) e = hipStreamWaitEvent(h->cstream, h->ev_dread[t], 0);
+    if (e == hipSuccess) e = hipMemcpyAsync(ds, hs, (size_t)n * 8, hipMemcpyHostToDevice, h->cstream);
+    if (e == hipSuccess) e = hipMemcpyAsync(ds + cap, hs + cap, (size_t)n * 8, hipMemcpyHostToDevice, h->cstream);
+    if (e == hipSuccess && with_value)
+        e = hipMemcpyAsync(ds + 2 * cap, hs + 2 * cap, (size_t)n * 8, hipMemcpyHostToDevice, h->cstream);
+    if (e == hipSuccess && with_hash)
+        e = hipMemcpyAsync(dh, hs + 3 * cap, (size_t)n * 4, hipMemcpyHostToDevice, h->cstream);
+    if (e == hipSuccess) e = hipEventRecord(h->ev_slot[slot], h->cstream);
+    if (e == hipSuccess) e = hipStreamWaitEvent(h->stream, h->ev_slot[slot], 0);
+    if (e != hipSuccess) return h->fail(GW_E_DEVICE, "H2D: %s", hipGetErrorString(e));
+    h->slot_used[slot] = true;
+    int rc = h->check_keys(n, ds, with_hash ? dh : nullptr);
+    if (rc == GW_OK) rc = ingest_device_impl(h, n, ds, ds + cap, with_value ? ds + 2 * cap : nullptr);
+    if (hipEventRecord(h->ev_dread[t], h->stream) != hipSuccess) return h->fail(GW_E_DEVICE, "staging event");
+    h->dread_valid[t] = true;
+    return rc;
+}
+
+int gw_stage_alloc(gw_handle* h, int32_t slots, int64_t cap) {
+    if (!h || slots < 1 || slots > 4096 || cap < 1) return GW_E_INVALID;
+    if (!h->kids.empty() || h->fe) return h->fail(GW_E_UNSUPPORTED, "staged ingest on a composite / first-element handle");
+    hipSetDevice(h->cfg.device);
+    return h->ensure_stage(cap, slots);
+}
+
+int gw_stage_columns(gw_handle* h, int32_t slot, int64_t** key, int32_t** key_hash, int64_t** ts, int64_t** value) {
+    if (!h || slot < 0 || slot >= (int)h->h_slot.size()) return GW_E_INVALID;
+    hipSetDevice(h->cfg.device);
+    const int rc = h->slot_ready(slot);
+    if (rc) return rc;
+    int64_t* hs = h->h_slot[slot];
+    if (key) *key = hs;
+    if (ts) *ts = hs + h->slot_cap;
+    if (value) *value = hs + 2 * h->slot_cap;
+    if (key_hash) *key_hash = (int32_t*)(hs + 3 * h->slot_cap);
+    return GW_OK;
+}
+
+int gw_ingest_stage(gw_handle* h, int32_t slot, int64_t n, int32_t cols) {
+    if (!h || slot < 0 || slot >= (int)h->h_slot.size() || n < 0 || n > h->slot_cap) return GW_E_INVALID;
+    if (h->failed) return h->fail(GW_E_STATE, "operator failed earlier: %s", h->err.c_str());
+    const bool with_value = (cols & GW_STAGE_VALUE) != 0, with_hash = (cols & GW_STAGE_KEY_HASH) != 0;
+    if (n > 0 && !with_value && h->cfg.agg != GW_COUNT) return h->fail(GW_E_INVALID, "value column required");
+    hipSetDevice(h->cfg.device);
+    if (n == 0) return GW_OK;
+    return stage_ingest(h, slot, n, with_hash, with_value);
 }
 
 int gw_ingest_device(gw_handle* h, int64_t n, const int64_t* d_key, const int32_t* d_key_hash,
@@ -3670,14 +3916,10 @@ int gw_drain(gw_handle* h, int64_t* key, int64_t* start, int64_t* end, void* res
     rows_view(h, &k, &s, &e, &r, &total);
     const int64_t c = std::min(cap, pending);
     const int64_t o = h->rows_head;
-    hipError_t err = hipSuccess;
     if (c > 0) {
-        if (key) err = hipMemcpyAsync(key, k + o, c * 8, hipMemcpyDeviceToHost, h->stream);
-        if (start && err == hipSuccess) err = hipMemcpyAsync(start, s + o, c * 8, hipMemcpyDeviceToHost, h->stream);
-        if (end && err == hipSuccess) err = hipMemcpyAsync(end, e + o, c * 8, hipMemcpyDeviceToHost, h->stream);
-        if (result && err == hipSuccess) err = hipMemcpyAsync(result, r + o, c * 8, hipMemcpyDeviceToHost, h->stream);
-        if (err == hipSuccess) err = hipStreamSynchronize(h->stream);
-        if (err != hipSuccess) return h->fail(GW_E_DEVICE, "D2H rows: %s", hipGetErrorString(err));
+        int64_t* dst[4] = {key, start, end, (int64_t*)result};
+        const int64_t* src[4] = {k + o, s + o, e + o, r + o};
+        if ((rc = h->drain_to_host(dst, src, c))) return rc;
     }
     *n = c;
     h->rows_head += c;

@@ -88,14 +88,9 @@ struct SegArgs {
     uint32_t* retry;        // wide pass: runs that did not fit K2 (append at st->overflow)
     DevStatus* st;
     int gshift;             // records are grouped by slot >> gshift (the sort skips the low bits)
-    // region-partitioned ingest (k_sp_part / k_sp_group / k_sp_keys)
-    const int64_t* p_key;   // pass-1 output, tile-major, bucket runs inside each tile: keys
+    // bucketed ingest (k_sb_part / k_sb_replay)
+    const int64_t* p_key;   // the bucket records (P2's buffer, or P1's without P2): keys
     const longlong2* p_tv;  //   and (timestamp, value) pairs
-    const uint32_t* col;    // [bucket][tile] run descriptors (start << 16 | count)
-    int64_t ntiles;
-    int lcap, bb;           // log2(table capacity), bucket bits (bucket = home >> (lcap - bb))
-    int exp;                // GW_SP_EXP: measurement variants of k_sp_keys (0: none)
-    uint32_t* slow;         // home slots for k_sp_slow (bucket << 14 | head), append at st->spills
     int64_t* pu_key;        // punted records (arrival order per key), append at st->overflow
     int64_t* pu_ts;
     int64_t* pu_val;
@@ -529,75 +524,171 @@ __global__ void __launch_bounds__(256) k_sess_prep(const int64_t* key, const int
     block_commit(st, 0, ins, flags, 0);
 }
 
-// ---------------------------------------------------------- region-partitioned ingest
-// The default session ingest.  Four launches per batch, no device-wide sort:
-//  * k_sp_part: one workgroup per 4096-record tile hashes every key to its home slot and
-//    writes the tile's records grouped by bucket (the top bb bits of the home slot), one run
-//    per bucket, stable (arrival order inside a run); one descriptor row per tile.
-//  * k_sp_transpose: descriptor rows -> one column per bucket.
-//  * k_sp_group: one workgroup per bucket concatenates the bucket's runs in tile order -- the
-//    bucket's records in arrival order -- and sorts them in LDS by (home slot, arrival) with a
-//    stable radix sort; it writes the order and one head per home slot.
-//  * k_sp_keys: one thread per home slot finds or inserts the key (the probe the sort path's
-//    k_sess_prep makes, here on the line the replay needs anyway) and replays the slot's
-//    records through MergingWindowSet.addWindow semantics (add_element_tv), all of the
-//    batch's records of a key in arrival order.
-// A key that needs the wide table (more in-flight sessions than the lane holds, or already
-// wide) or finds no slot, and every key of a bucket with more than kGrpCap records, is
-// punted: its records go to a punt list in arrival order, which the sort path (k_sess_prep
-// ... k_sess_wide) replays after the launch.
-constexpr int kSessionRegionDefault = 0;  // until it outruns the sort path on the sessions config
-constexpr int kSpTile = 4096;
-constexpr int kSpThreads = 1024;
-constexpr int kSpWaveRecs = kSpTile / (kSpThreads / 64);  // records of one wave (a contiguous chunk)
-constexpr int kSpItems = kSpWaveRecs / 64;
-constexpr int kSpMaxBuckets = 1024;
-constexpr size_t kSpPartLds = (size_t)kSpTile * 3 * 8 + (size_t)(kSpThreads / 64) * kSpMaxBuckets * 2;
+// ---------------------------------------------------------- bucketed session ingest
+// The default session ingest.  Records are grouped by the home slot of
+// their key BEFORE anyone touches the table, so that each key is looked up once per batch
+// (not once per record) and its records are replayed from a bucket that sits in L2:
+//  * P1 k_sb_part<false>: one workgroup per 2048-record tile of the batch partitions the
+//    tile by the coarse digit of the home slot (its top bb1 bits), stably, and writes the
+//    tile back in digit order with one (start, count) descriptor per digit.
+//  * k_sb_cols: descriptor rows -> one column per coarse digit, plus the digit totals.
+//  * P2 k_sb_part<true>: one workgroup per 2048-record chunk of a coarse digit's records
+//    (gathered from P1's runs in tile order, i.e. arrival order) partitions it by the fine
+//    digit (the next bb2 bits), the same way.  Batches of at most 2^6 buckets skip P2.
+//  * P3 k_sb_replay: one workgroup per bucket (coarse, fine) concatenates the bucket's runs
+//    (arrival order), sorts them in LDS by (home slot, arrival) with a stable radix sort,
+//    and replays each home slot's run: one thread finds or inserts the key (sp_key: the
+//    probe the sort path's k_sess_prep makes per record, here once per key) and replays its
+//    records through MergingWindowSet.addWindow semantics (add_element_tv).
+// Long runs stay coalesced: P1's runs are 2048 / 2^bb1 records, P2's 2048 / 2^bb2 (32 at
+// the sessions config's 10M-record batches: 4096 buckets of ~2400 records).  A key that needs
+// the wide table (more in-flight sessions than the lane holds, or already wide) or finds no
+// slot, and every key of a bucket with more than kSbCap records, is punted: its records go to
+// a punt list in arrival order, which the sort path (k_sess_prep ... k_sess_wide) replays.
+constexpr int kSbTile = 2048;
+constexpr int kSbThreads = 512;
+constexpr int kSbItems = kSbTile / kSbThreads;
+constexpr int kSbWaveRecs = kSbTile / (kSbThreads / 64);
+constexpr int kSbMaxDigitBits = 8;
+constexpr int kSbMaxDigits = 1 << kSbMaxDigitBits;
+constexpr int kSbSinglePassBits = 6;      // buckets <= 2^6: P1 partitions by the whole bucket
+constexpr int kSbMeanBits = 11;            // ~2^11 records per bucket
+constexpr int kSbCap = 4096;               // records of a bucket the replay sorts in LDS
+constexpr int kSbPosBits = 12;
+constexpr int kSbMaxHomeBits = 31 - kSbPosBits - 1;  // + the sentinel's code
+constexpr int kSbRThreads = 256;
+constexpr int kSbRItems = kSbCap / kSbRThreads;
+constexpr int kSbRWaveRecs = kSbCap / (kSbRThreads / 64);
+constexpr int kSbBins = 512;
+// P1/P2 LDS: key | ts | value staging, per-(wave, digit) counters, gather map (P2)
+constexpr size_t kSbPartLds = (size_t)kSbTile * 3 * 8 + (size_t)(kSbThreads / 64) * kSbMaxDigits * 2 + kSbTile * 4;
 
-// Pass 1.  Wave w owns the tile's records [w*256, (w+1)*256) (item it of lane l: w*256 +
-// it*64 + l), so arrival order is (wave, item, lane).  Ranks within a bucket are stable:
-// lanes of one bucket find each other with bb ballots, a leader per bucket bumps the wave's
-// private counter, and a block scan over (bucket, wave) turns the counters into offsets.
-__global__ void __launch_bounds__(kSpThreads) k_sp_part(const int64_t* key, const int64_t* ts, const int64_t* val,
-                                                        int64_t n, int64_t cap, int lcap, int bb, int64_t* o_key,
+// Home slot of a key in a table of 2^lcap slots; the sentinel key (the empty marker, which
+// lives in slot cap) goes with the last home slot's bucket.
+__device__ __forceinline__ uint64_t sb_home(int64_t key, int lcap) {
+    const uint64_t m = ((uint64_t)1 << lcap) - 1;
+    return key == kEmptyKey ? m : (slot_hash(key) & m);
+}
+
+// Coarse-bucket geometry shared by P2 and P3: chunk starts of each coarse digit (chunks of
+// kSbTile records) from the digit totals.  cs[0..nc] in LDS; one wave.
+__device__ __forceinline__ void sb_chunk_starts(const uint32_t* ctot, int nc, uint32_t* cs) {
+    if (threadIdx.x < 64) {
+        const int lane = threadIdx.x;
+        uint32_t run = 0;
+        for (int c0 = 0; c0 < nc; c0 += 64) {
+            const int c = c0 + lane;
+            const uint32_t x = c < nc ? (ctot[c] + kSbTile - 1) / kSbTile : 0u;
+            uint32_t incl = x;
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t up = __shfl_up(incl, o);
+                if (lane >= o) incl += up;
+            }
+            if (c < nc) cs[c] = run + incl - x;
+            run += __shfl(incl, 63);
+        }
+        if (lane == 0) cs[nc] = run;
+    }
+    __syncthreads();
+}
+
+// P1 (GATHER false): tile blockIdx.x of the batch (key, ts, val).  P2 (GATHER true): chunk
+// blockIdx.x of the coarse digits' records in P1's buffer (p_key, p_tv; runs col[c][tile],
+// totals ctot).  Either way the workgroup's records, in arrival order, are partitioned by
+// digit = (home >> shift) & (nd - 1), stably: wave w owns records [w*256, (w+1)*256) (item it
+// of lane l: w*256 + it*64 + l), lanes of one digit find each other with ballots, a leader
+// per digit bumps the wave's counter, and a block scan over (digit, wave) turns the counters
+// into offsets.  Out: the records in digit order at blockIdx.x * kSbTile, and one descriptor
+// row (start << 16 | count) per digit.
+template <bool GATHER>
+__global__ void __launch_bounds__(kSbThreads) k_sb_part(const int64_t* key, const int64_t* ts, const int64_t* val,
+                                                        int64_t n, const int64_t* p_key, const longlong2* p_tv,
+                                                        const uint32_t* col, const uint32_t* ctot, int nc,
+                                                        int64_t ntiles, int lcap, int shift, int db, int64_t* o_key,
                                                         longlong2* o_tv, uint32_t* row, DevStatus* st) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     int64_t* s_key = reinterpret_cast<int64_t*>(smem);
-    int64_t* s_ts = s_key + kSpTile;
-    int64_t* s_val = s_ts + kSpTile;
-    uint16_t* wcnt = reinterpret_cast<uint16_t*>(s_val + kSpTile);  // [wave][bucket]
-    __shared__ uint32_t lh[kSpMaxBuckets], ls[kSpMaxBuckets];
-    __shared__ uint32_t wsum[kSpThreads / 64];
-    const int nb = 1 << bb, sh = lcap - bb;
+    int64_t* s_ts = s_key + kSbTile;
+    int64_t* s_val = s_ts + kSbTile;
+    uint16_t* wcnt = reinterpret_cast<uint16_t*>(s_val + kSbTile);  // [wave][digit]
+    uint32_t* gmap = reinterpret_cast<uint32_t*>(wcnt + (kSbThreads / 64) * kSbMaxDigits);
+    __shared__ uint32_t lh[kSbMaxDigits], ls[kSbMaxDigits];
+    __shared__ uint32_t wsum[kSbThreads / 64];
+    __shared__ uint32_t cs[kSbMaxDigits + 1];
+    const int nd = 1 << db;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int64_t tile = blockIdx.x;
-    const int64_t lo = tile * kSpTile, hi = min(n, lo + (int64_t)kSpTile);
-    for (int e = tid; e < (kSpThreads / 64) * nb; e += blockDim.x) wcnt[(e / nb) * kSpMaxBuckets + e % nb] = 0;
-    int64_t k[kSpItems], t[kSpItems], v[kSpItems];
+    const int64_t g = blockIdx.x;
+    int cnt;
+    if constexpr (!GATHER) {
+        const int64_t lo = g * kSbTile;
+        cnt = (int)min((int64_t)kSbTile, n - lo);
+    } else {
+        sb_chunk_starts(ctot, nc, cs);
+        if (g >= cs[nc]) return;  // the grid is an upper bound on the chunks (uniform exit)
+        int c = 0;
+        while (c + 1 < nc && cs[c + 1] <= (uint32_t)g) ++c;
+        const uint32_t j0 = ((uint32_t)g - cs[c]) * kSbTile;
+        cnt = (int)min((uint32_t)kSbTile, ctot[c] - j0);
+        // gather map: position q of this chunk -> its P1 buffer offset.  Tiles in order, a
+        // block of kSbThreads at a time; a thread writes its tile's part of [j0, j0 + cnt).
+        const uint32_t* cc = col + (int64_t)c * ntiles;
+        uint32_t running = 0;
+        for (int64_t t0 = 0; t0 < ntiles && running < j0 + (uint32_t)cnt; t0 += kSbThreads) {
+            const int64_t t = t0 + tid;
+            const uint32_t d = t < ntiles ? cc[t] : 0u;
+            const uint32_t x = d & 0xffffu;
+            uint32_t incl = x;
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t up = __shfl_up(incl, o);
+                if (lane >= o) incl += up;
+            }
+            if (lane == 63) wsum[w] = incl;
+            __syncthreads();
+            uint32_t pre = running + incl - x, tot = 0;
+            for (int q = 0; q < kSbThreads / 64; ++q) {
+                if (q < w) pre += wsum[q];
+                tot += wsum[q];
+            }
+            const uint32_t a0 = max(pre, j0), a1 = min(pre + x, j0 + (uint32_t)cnt);
+            for (uint32_t u = a0; u < a1; ++u) gmap[u - j0] = (uint32_t)(t * kSbTile) + (d >> 16) + (u - pre);
+            running += tot;
+            __syncthreads();  // wsum is rewritten by the next block
+        }
+        __syncthreads();
+    }
+    for (int e = tid; e < (kSbThreads / 64) * nd; e += blockDim.x) wcnt[(e / nd) * kSbMaxDigits + e % nd] = 0;
+    int64_t k[kSbItems], t[kSbItems], v[kSbItems];
 #pragma unroll
-    for (int it = 0; it < kSpItems; ++it) {  // all loads in flight first
-        const int64_t i = lo + w * kSpWaveRecs + it * 64 + lane;
+    for (int it = 0; it < kSbItems; ++it) {  // all loads in flight first
+        const int i = w * kSbWaveRecs + it * 64 + lane;
         k[it] = 0; t[it] = 0; v[it] = 0;
-        if (i < hi) {
-            k[it] = __builtin_nontemporal_load(key + i);
-            t[it] = __builtin_nontemporal_load(ts + i);
-            if (val) v[it] = __builtin_nontemporal_load(val + i);
+        if (i < cnt) {
+            if constexpr (!GATHER) {
+                const int64_t x = g * kSbTile + i;
+                k[it] = __builtin_nontemporal_load(key + x);
+                t[it] = __builtin_nontemporal_load(ts + x);
+                if (val) v[it] = __builtin_nontemporal_load(val + x);
+            } else {
+                const uint32_t o = gmap[i];
+                k[it] = p_key[o];
+                const longlong2 tv = p_tv[o];
+                t[it] = tv.x;
+                v[it] = tv.y;
+            }
         }
     }
     __syncthreads();
     unsigned long long flags = 0;
-    uint16_t* my = wcnt + w * kSpMaxBuckets;
-    uint32_t bk[kSpItems], rk[kSpItems];
+    uint16_t* my = wcnt + w * kSbMaxDigits;
+    uint32_t bk[kSbItems], rk[kSbItems];
 #pragma unroll
-    for (int it = 0; it < kSpItems; ++it) {
-        const int64_t i = lo + w * kSpWaveRecs + it * 64 + lane;
-        const bool ok = i < hi;
-        if (ok && t[it] == INT64_MIN) flags |= GW_DF_NO_TS;
-        const uint32_t b = !ok ? 0u
-                           : k[it] == kEmptyKey ? (uint32_t)(nb - 1)
-                                                : (uint32_t)((slot_hash(k[it]) & (uint64_t)(cap - 1)) >> sh);
+    for (int it = 0; it < kSbItems; ++it) {
+        const int i = w * kSbWaveRecs + it * 64 + lane;
+        const bool ok = i < cnt;
+        if (!GATHER && ok && t[it] == INT64_MIN) flags |= GW_DF_NO_TS;
+        const uint32_t b = ok ? (uint32_t)((sb_home(k[it], lcap) >> shift) & (uint64_t)(nd - 1)) : 0u;
         uint64_t peers = __ballot(ok);
-        for (int q = 0; q < bb; ++q) {
+        for (int q = 0; q < db; ++q) {
             const uint64_t m = __ballot(ok && ((b >> q) & 1u));
             peers &= ((b >> q) & 1u) ? m : ~m;
         }
@@ -612,10 +703,10 @@ __global__ void __launch_bounds__(kSpThreads) k_sp_part(const int64_t* key, cons
         rk[it] = old + (uint32_t)__popcll(peers & ((1ull << lane) - 1ull));
     }
     __syncthreads();
-    {  // bucket totals, exclusive scan over buckets, then per-(wave, bucket) offsets in place
+    {  // digit totals, exclusive scan over digits, then per-(wave, digit) offsets in place
         uint32_t x = 0;
-        if (tid < nb)
-            for (int q = 0; q < kSpThreads / 64; ++q) x += wcnt[q * kSpMaxBuckets + tid];
+        if (tid < nd)
+            for (int q = 0; q < kSbThreads / 64; ++q) x += wcnt[q * kSbMaxDigits + tid];
         uint32_t incl = x;
         for (int o = 1; o < 64; o <<= 1) {
             const uint32_t up = __shfl_up(incl, o);
@@ -625,20 +716,20 @@ __global__ void __launch_bounds__(kSpThreads) k_sp_part(const int64_t* key, cons
         __syncthreads();
         uint32_t off = 0;
         for (int q = 0; q < w; ++q) off += wsum[q];
-        if (tid < nb) {
+        if (tid < nd) {
             ls[tid] = off + incl - x;
             lh[tid] = x;
             uint32_t r = off + incl - x;
-            for (int q = 0; q < kSpThreads / 64; ++q) {
-                const uint32_t c = wcnt[q * kSpMaxBuckets + tid];
-                wcnt[q * kSpMaxBuckets + tid] = (uint16_t)r;
+            for (int q = 0; q < kSbThreads / 64; ++q) {
+                const uint32_t c = wcnt[q * kSbMaxDigits + tid];
+                wcnt[q * kSbMaxDigits + tid] = (uint16_t)r;
                 r += c;
             }
         }
     }
     __syncthreads();
 #pragma unroll
-    for (int it = 0; it < kSpItems; ++it) {
+    for (int it = 0; it < kSbItems; ++it) {
         if (bk[it] == ~0u) continue;
         const uint32_t j = my[bk[it]] + rk[it];
         s_key[j] = k[it];
@@ -646,31 +737,37 @@ __global__ void __launch_bounds__(kSpThreads) k_sp_part(const int64_t* key, cons
         s_val[j] = v[it];
     }
     __syncthreads();
-    const int64_t base = tile * kSpTile;
-    const int cnt = (int)(hi - lo);
-    for (int j = tid; j < cnt; j += blockDim.x) {  // read back by the grouping and the replay
+    const int64_t base = g * kSbTile;
+    for (int j = tid; j < cnt; j += blockDim.x) {
         o_key[base + j] = s_key[j];
         o_tv[base + j] = longlong2{s_ts[j], s_val[j]};
     }
-    for (int b = tid; b < nb; b += blockDim.x) row[tile * nb + b] = (ls[b] << 16) | lh[b];
-    block_commit(st, 0, 0, flags, 0);
+    for (int b = tid; b < nd; b += blockDim.x) row[g * nd + b] = (ls[b] << 16) | lh[b];
+    if (!GATHER) block_commit(st, 0, 0, flags, 0);
 }
 
-// Descriptor rows [tile][bucket] -> columns [bucket][tile] (64 x 64 blocks through LDS).
-__global__ void __launch_bounds__(256) k_sp_transpose(const uint32_t* row, uint32_t* col, int64_t ntiles, int nb) {
+// P1 descriptor rows [tile][digit] -> columns [digit][tile] (64 x 64 blocks through LDS),
+// and the digit totals (one atomic per digit per block; ctot zeroed beforehand).
+__global__ void __launch_bounds__(256) k_sb_cols(const uint32_t* row, uint32_t* col, uint32_t* ctot, int64_t ntiles,
+                                                 int nd) {
     __shared__ uint32_t tt[64][65];
     const int64_t t0 = (int64_t)blockIdx.x * 64;
     const int b0 = blockIdx.y * 64;
     for (int e = threadIdx.x; e < 64 * 64; e += blockDim.x) {
         const int tl = e >> 6, bl = e & 63;
         const int64_t t = t0 + tl;
-        tt[tl][bl] = (t < ntiles && b0 + bl < nb) ? row[t * nb + b0 + bl] : 0u;
+        tt[tl][bl] = (t < ntiles && b0 + bl < nd) ? row[t * nd + b0 + bl] : 0u;
     }
     __syncthreads();
     for (int e = threadIdx.x; e < 64 * 64; e += blockDim.x) {
         const int bl = e >> 6, tl = e & 63;
         const int64_t t = t0 + tl;
-        if (t < ntiles && b0 + bl < nb) col[(int64_t)(b0 + bl) * ntiles + t] = tt[tl][bl];
+        if (t < ntiles && b0 + bl < nd) col[(int64_t)(b0 + bl) * ntiles + t] = tt[tl][bl];
+    }
+    if (threadIdx.x < 64 && b0 + (int)threadIdx.x < nd) {
+        uint32_t s = 0;
+        for (int tl = 0; tl < 64; ++tl) s += tt[tl][threadIdx.x] & 0xffffu;
+        if (s) atomicAdd(ctot + b0 + threadIdx.x, s);
     }
 }
 
@@ -680,35 +777,20 @@ __device__ __forceinline__ constexpr int sess_words() {
     return (AGG == GW_AVG_I64 || AGG == GW_AVG_F64) ? 4 : 3;
 }
 
-// Grouping (k_sp_group): one workgroup per bucket sorts the bucket's records of the batch by
-// (local home slot, arrival) in LDS -- a stable two-pass radix sort over the home bits of
-// 32-bit keys (home << 14 | position) -- and writes the buffer offsets in that order plus
-// one head per home slot.  A bucket holds at most kGrpCap records; the records of a bucket
-// with more (a hot key, a batch far above the table's design size) go to the punt list.
-constexpr int kGrpCap = 16384;
-constexpr int kGrpPosBits = 14;
-constexpr int kGrpThreads = 1024;
-constexpr int kGrpItems = kGrpCap / kGrpThreads;     // per thread per radix pass
-constexpr int kGrpWaveRecs = kGrpCap / (kGrpThreads / 64);
-constexpr int kGrpMaxHomeBits = 31 - kGrpPosBits - 1;  // + the sentinel's code
-constexpr int kGrpBins = 512;
-constexpr size_t kGrpLds = (size_t)kGrpCap * 4 * 2 + (size_t)(kGrpThreads / 64) * kGrpBins * 2;
-
-// One stable LSD radix pass over x[0..n) -> y, digit = (v >> sh) & (2^db - 1), db <= 9.
-// Wave w owns positions [w*kGrpWaveRecs, (w+1)*kGrpWaveRecs) (item it of lane l at
-// w*kGrpWaveRecs + it*64 + l), so (wave, item, lane) is the input order; lanes of one digit
-// find each other with db ballots, and a leader per digit bumps the wave's counter.
-__device__ __forceinline__ void grp_radix_pass(const uint32_t* x, uint32_t* y, int n, int sh, int db,
-                                               uint16_t* wcnt, uint32_t* wsum) {
+// One stable LSD radix pass over x[0..n) -> y in LDS, digit = (v >> sh) & (2^db - 1),
+// db <= 9, kSbRThreads threads.  Wave w owns positions [w*kSbRWaveRecs, ...) (item it of
+// lane l at w*kSbRWaveRecs + it*64 + l), so (wave, item, lane) is the input order.
+__device__ __forceinline__ void sb_radix_pass(const uint32_t* x, uint32_t* y, int n, int sh, int db, uint16_t* wcnt,
+                                              uint32_t* wsum) {
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int nbins = 1 << db;
-    for (int e = tid; e < (kGrpThreads / 64) * kGrpBins; e += blockDim.x) wcnt[e] = 0;
+    for (int e = tid; e < (kSbRThreads / 64) * kSbBins; e += blockDim.x) wcnt[e] = 0;
     __syncthreads();
-    uint16_t* my = wcnt + w * kGrpBins;
-    uint32_t v[kGrpItems], rk[kGrpItems];
+    uint16_t* my = wcnt + w * kSbBins;
+    uint32_t v[kSbRItems], rk[kSbRItems];
 #pragma unroll
-    for (int it = 0; it < kGrpItems; ++it) {
-        const int pos = w * kGrpWaveRecs + it * 64 + lane;
+    for (int it = 0; it < kSbRItems; ++it) {
+        const int pos = w * kSbRWaveRecs + it * 64 + lane;
         const bool ok = pos < n;
         v[it] = ok ? x[pos] : 0u;
         const uint32_t d = (v[it] >> sh) & (uint32_t)(nbins - 1);
@@ -729,171 +811,45 @@ __device__ __forceinline__ void grp_radix_pass(const uint32_t* x, uint32_t* y, i
     }
     __syncthreads();
     {  // digit totals -> exclusive scan over digits -> per-(wave, digit) offsets in place
-        const int per = kGrpBins / kGrpThreads > 0 ? kGrpBins / kGrpThreads : 1;
-        (void)per;
-        uint32_t tot = 0;
-        if (tid < nbins)
-            for (int q = 0; q < kGrpThreads / 64; ++q) tot += wcnt[q * kGrpBins + tid];
-        uint32_t incl = tot;
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t up = __shfl_up(incl, o);
-            if (lane >= o) incl += up;
-        }
-        if (lane == 63) wsum[w] = incl;
-        __syncthreads();
-        uint32_t off = 0;
-        for (int q = 0; q < w; ++q) off += wsum[q];
-        if (tid < nbins) {
-            uint32_t r = off + incl - tot;
-            for (int q = 0; q < kGrpThreads / 64; ++q) {
-                const uint32_t c = wcnt[q * kGrpBins + tid];
-                wcnt[q * kGrpBins + tid] = (uint16_t)r;
-                r += c;
+        for (int d0 = 0; d0 < nbins; d0 += kSbRThreads) {
+            const int d = d0 + tid;
+            uint32_t tot = 0;
+            if (d < nbins)
+                for (int q = 0; q < kSbRThreads / 64; ++q) tot += wcnt[q * kSbBins + d];
+            uint32_t incl = tot;
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t up = __shfl_up(incl, o);
+                if (lane >= o) incl += up;
             }
+            if (lane == 63) wsum[w] = incl;
+            __syncthreads();
+            uint32_t off = d0 ? wsum[kSbRThreads / 64] : 0u, all = off;
+            for (int q = 0; q < kSbRThreads / 64; ++q) {
+                if (q < w) off += wsum[q];
+                all += wsum[q];
+            }
+            if (d < nbins) {
+                uint32_t r = off + incl - tot;
+                for (int q = 0; q < kSbRThreads / 64; ++q) {
+                    const uint32_t c = wcnt[q * kSbBins + d];
+                    wcnt[q * kSbBins + d] = (uint16_t)r;
+                    r += c;
+                }
+            }
+            __syncthreads();
+            if (tid == 0) wsum[kSbRThreads / 64] = all;  // running total for the next digit block
+            __syncthreads();
         }
     }
-    __syncthreads();
 #pragma unroll
-    for (int it = 0; it < kGrpItems; ++it) {
-        const int pos = w * kGrpWaveRecs + it * 64 + lane;
+    for (int it = 0; it < kSbRItems; ++it) {
+        const int pos = w * kSbRWaveRecs + it * 64 + lane;
         if (pos < n) y[my[(v[it] >> sh) & (uint32_t)(nbins - 1)] + rk[it]] = v[it];
     }
     __syncthreads();
 }
 
-// grid: one workgroup per bucket.  Outputs per bucket b (at b * kGrpCap): perm[] the
-// pass-1 buffer offsets of the bucket's records in (home, arrival) order, shd[] heads (sorted
-// index | local home << 14); grp_n[2b] = records, grp_n[2b+1] = heads (both 0 for an
-// oversize bucket, whose records went to the punt list).  gsrc: scratch, offset by position.
-__global__ void __launch_bounds__(kGrpThreads) k_sp_group(SegArgs a, uint32_t* gsrc, uint32_t* perm, uint32_t* shd,
-                                                          uint32_t* grp_n) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    uint32_t* ka = reinterpret_cast<uint32_t*>(smem);
-    uint32_t* kb = ka + kGrpCap;
-    uint16_t* wcnt = reinterpret_cast<uint16_t*>(kb + kGrpCap);
-    __shared__ uint32_t wsum[kGrpThreads / 64];
-    __shared__ uint32_t s_tot, s_nh;
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int64_t b = blockIdx.x;
-    const uint32_t* col = a.col + b * a.ntiles;
-    const int sh = a.lcap - a.bb;
-    const uint64_t hmask = ((uint64_t)1 << sh) - 1;
-    const uint32_t sent = 1u << sh;
-    uint32_t* gs = gsrc + b * kGrpCap;
-    // records of the bucket; an oversize bucket's records all go to the punt list (arrival
-    // order), which the sort path replays: its keys are disjoint from the other buckets'
-    {
-        uint32_t c = 0;
-        for (int64_t t = tid; t < a.ntiles; t += blockDim.x) c += col[t] & 0xffffu;
-        c = (uint32_t)wave_sum(c);
-        if (lane == 0) wsum[w] = c;
-        __syncthreads();
-        if (tid == 0) {
-            uint32_t tot = 0;
-            for (int q = 0; q < kGrpThreads / 64; ++q) tot += wsum[q];
-            s_tot = tot;
-            s_nh = tot > (uint32_t)kGrpCap ? (uint32_t)atomicAdd(&a.st->overflow, (unsigned long long)tot) : 0u;
-        }
-        __syncthreads();
-    }
-    const uint32_t n = s_tot;
-    const bool over = n > (uint32_t)kGrpCap;
-    const uint32_t pbase = s_nh;
-    // the bucket's runs in tile order (arrival order): thread t takes tiles [3t, 3t + 3) of each
-    // chunk of 3 * kGrpThreads tiles, 8 records at a time with their loads issued together
-    uint32_t running = 0;
-    for (int64_t c0 = 0; c0 < a.ntiles; c0 += 3 * kGrpThreads) {
-        uint32_t d[3], sum = 0;
-#pragma unroll
-        for (int q = 0; q < 3; ++q) {
-            const int64_t t = c0 + 3 * tid + q;
-            d[q] = t < a.ntiles ? col[t] : 0u;
-            sum += d[q] & 0xffffu;
-        }
-        uint32_t incl = sum;
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t up = __shfl_up(incl, o);
-            if (lane >= o) incl += up;
-        }
-        if (lane == 63) wsum[w] = incl;
-        __syncthreads();
-        uint32_t pre = running + incl - sum, tot = 0;
-        for (int q = 0; q < kGrpThreads / 64; ++q) {
-            if (q < w) pre += wsum[q];
-            tot += wsum[q];
-        }
-        const uint32_t c0n = d[0] & 0xffffu, c1n = d[1] & 0xffffu;
-        uint32_t s3[3];
-#pragma unroll
-        for (int q = 0; q < 3; ++q) s3[q] = (uint32_t)((c0 + 3 * tid + q) * kSpTile + (d[q] >> 16));
-        for (uint32_t u0 = 0; u0 < sum; u0 += 8) {
-            uint32_t sv[8];
-            int64_t kk[8];
-#pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                const uint32_t uu = u0 + u;
-                sv[u] = uu < c0n ? s3[0] + uu : uu < c0n + c1n ? s3[1] + (uu - c0n) : s3[2] + (uu - c0n - c1n);
-                kk[u] = uu < sum ? a.p_key[sv[u]] : 0;
-            }
-#pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                const uint32_t uu = u0 + u;
-                if (uu >= sum) break;
-                const uint32_t pos = pre + uu;
-                if (over) {
-                    const longlong2 tv = a.p_tv[sv[u]];
-                    a.pu_key[pbase + pos] = kk[u];
-                    a.pu_ts[pbase + pos] = tv.x;
-                    a.pu_val[pbase + pos] = tv.y;
-                } else {
-                    const uint32_t lh = kk[u] == kEmptyKey ? sent : (uint32_t)(slot_hash(kk[u]) & hmask);
-                    ka[pos] = (lh << kGrpPosBits) | pos;
-                    gs[pos] = sv[u];
-                }
-            }
-        }
-        running += tot;
-        __syncthreads();  // wsum is rewritten by the next chunk
-    }
-    if (over) {
-        if (tid == 0) { grp_n[2 * b] = 0; grp_n[2 * b + 1] = 0; }
-        return;
-    }
-    // home bits [kGrpPosBits, kGrpPosBits + sh + 1): two passes
-    const int hb = sh + 1, db0 = (hb + 1) / 2, db1 = hb - db0;
-    grp_radix_pass(ka, kb, (int)n, kGrpPosBits, db0, wcnt, wsum);
-    const uint32_t* fin = kb;
-    if (db1 > 0) {
-        grp_radix_pass(kb, ka, (int)n, kGrpPosBits + db0, db1, wcnt, wsum);
-        fin = ka;
-    }
-    uint32_t* po = perm + b * kGrpCap;
-    uint32_t* ho = shd + b * kGrpCap;
-    uint32_t nh = 0;  // heads in sorted order: ordered compaction per chunk (waves, then lanes)
-    for (uint32_t i0 = 0; i0 < n; i0 += blockDim.x) {
-        const uint32_t i = i0 + tid;
-        bool h = false;
-        uint32_t x = 0;
-        if (i < n) {
-            x = fin[i];
-            po[i] = gs[x & ((1u << kGrpPosBits) - 1u)];
-            h = i == 0 || (fin[i - 1] >> kGrpPosBits) != (x >> kGrpPosBits);
-        }
-        const uint64_t bal = __ballot(h);
-        if (lane == 0) wsum[w] = (uint32_t)__popcll(bal);
-        __syncthreads();
-        uint32_t base = nh, tot = 0;
-        for (int q = 0; q < kGrpThreads / 64; ++q) {
-            if (q < w) base += wsum[q];
-            tot += wsum[q];
-        }
-        if (h) ho[base + __popcll(bal & ((1ull << lane) - 1ull))] = i | ((x >> kGrpPosBits) << kGrpPosBits);
-        nh += tot;
-        __syncthreads();  // wsum is rewritten by the next chunk
-    }
-    if (tid == 0) { grp_n[2 * b] = n; grp_n[2 * b + 1] = nh; }
-}
-
+// sp_store / sp_key / sp_run (the replay of one home slot's run) follow below.
 // The key's list after a replay (cnt sessions in the lane) -> its slot, or to the migration
 // list when it outgrew the slot (the key's later records of the batch then punt until the
 // migration).
@@ -1005,248 +961,167 @@ __device__ __forceinline__ void sp_run(const SegArgs& a, const SessList& l, uint
     }
 }
 
-// Replay: one thread per home slot.  A persistent grid (a multiple of 8 workgroups): the
-// workgroups with blockIdx % 8 == x walk the buckets b == x (mod 8) and deal their chunks of
-// 256 heads round-robin among themselves -- under the round-robin placement of
-// workgroups on the 8 XCDs (speed only, never correctness) a bucket's pass-1 lines are read
-// into one L2 and its records gathered from there.  The thread loads its home slot's line
-// with the offsets of its first kSpFast records, then their keys and (timestamp, value)
-// pairs.  A run of one key that finds its slot within kSpProbe lines of the home slot (or
-// claims a free one there) replays from registers, kSpFast records at a time; the rest go on
-// the slow list for k_sp_slow (longer probes, several keys per home slot, the wide table, a
-// list that could outgrow the lane under allowed lateness or the side output).
-constexpr int kSpKeyThreads = 256;
-constexpr int kSpFast = 4;
-constexpr int kSpProbe = 4;
+// P3: one workgroup per bucket B = (coarse c, fine f).  The bucket's runs are desc[g * nf + f]
+// over the chunks g of coarse digit c ([cs[c], cs[c+1]) from the coarse totals; with P2
+// skipped, nc = 1 and the chunks are P1's tiles).  Concatenated in chunk order they are the
+// bucket's records in arrival order; the workgroup sorts them in LDS by (local home slot,
+// arrival) -- 32-bit keys (home << kSbPosBits | position), a stable radix sort over the home
+// bits -- and one thread per home slot replays the slot's run (sp_run: every key of the run
+// in order of its first record, usually one).  A bucket of more than kSbCap records punts
+// all of them (arrival order) to the sort path: its keys are disjoint from the other buckets'.
 template <int AGG>
-__global__ void __launch_bounds__(kSpKeyThreads) k_sp_keys(SegArgs a, const uint32_t* perm, const uint32_t* shd,
-                                                           const uint32_t* grp_n, int nb) {
-    constexpr int SW = sess_words<AGG>();
-    constexpr uint32_t pm = (1u << kGrpPosBits) - 1u;
-    __shared__ int64_t lane[5 * kLaneSess * kSpKeyThreads];
-    const SessList l{lane + threadIdx.x, kLaneSess * kSpKeyThreads, kSpKeyThreads};
-    const int sh = a.lcap - a.bb;
+__global__ void __launch_bounds__(kSbRThreads) k_sb_replay(SegArgs a, const uint32_t* desc, const uint32_t* ctot,
+                                                           int nc, int64_t nchunks, int bf, int lcap, int sh) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    uint32_t* ka = reinterpret_cast<uint32_t*>(smem);  // sort keys | radix double buffer
+    uint32_t* kb = ka + kSbCap;
+    uint32_t* src = kb + kSbCap;                         // position -> buffer offset, then the order
+    uint32_t* hd = src + kSbCap;                         // run starts (gather), then the heads
+    int64_t* lanes = reinterpret_cast<int64_t*>(smem);  // session lanes (replay; alias ka | kb)
+    uint16_t* wcnt = reinterpret_cast<uint16_t*>(hd);   // radix counters (sort; alias the heads)
+    __shared__ uint32_t wsum[kSbRThreads / 64 + 1];
+    __shared__ uint32_t cs[kSbMaxDigits + 1];
+    __shared__ uint32_t cpre[kSbRThreads + 1];
+    __shared__ uint32_t s_n, s_pb, s_nh;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int nf = 1 << bf;
+    const int64_t B = blockIdx.x;
+    const int c = (int)(B >> bf), f = (int)(B & (nf - 1));
+    int64_t g0 = 0, g1 = nchunks;
+    if (nc > 1) {
+        sb_chunk_starts(ctot, nc, cs);
+        g0 = cs[c];
+        g1 = cs[c + 1];
+    }
+    const uint64_t hmask = ((uint64_t)1 << sh) - 1;
     const uint32_t sent = 1u << sh;
-    const bool effects = a.lateness > 0 || a.lo_key;
-    const int xg = blockIdx.x & 7, per = gridDim.x >> 3, me = blockIdx.x >> 3;
-    unsigned long long late = 0, merges = 0, flags = 0, ins = 0;
-    uint32_t base = 0;  // chunks of this XCD group's earlier buckets: chunk g goes to workgroup g % per
-    for (int64_t b = xg; b < nb; b += 8) {
-        const uint32_t n = grp_n[2 * b], nh = grp_n[2 * b + 1];
-        const uint32_t* pr = perm + b * kGrpCap;
-        const uint32_t* hd = shd + b * kGrpCap;
-        const uint32_t nch = (nh + kSpKeyThreads - 1) / kSpKeyThreads;
-        const uint32_t c0 = (uint32_t)((me - (int)(base % (uint32_t)per) + per) % per);
-        base += nch;
-        for (uint32_t c = c0; c < nch; c += per) {
-            const uint32_t j = c * kSpKeyThreads + threadIdx.x;
-            if (j >= nh) continue;
-            const uint32_t h = hd[j];
-            const uint32_t e = h & pm, lh = h >> kGrpPosBits;
-            const uint32_t f = j + 1 < nh ? (hd[j + 1] & pm) : n;
-            const uint32_t L = f - e;
-            const bool sentinel = lh == sent;
-            int64_t slot = sentinel ? a.t.cap : ((b << sh) | (int64_t)lh);
-            int64_t cur[8], rk[kSpFast], rt[kSpFast], rv[kSpFast];
-            uint32_t ro[kSpFast];
-// (macros, not lambdas: a lambda capturing these arrays by reference would put them in scratch)
-#define SP_LOAD_LINE(sl)                                                                   \
-    do {                                                                                   \
-        const longlong2* p_ = reinterpret_cast<const longlong2*>(slot_ptr(a.t, (sl)));     \
-        _Pragma("unroll") for (int x_ = 0; x_ < 4; ++x_) {                                 \
-            const longlong2 y_ = p_[x_];                                                   \
-            cur[2 * x_] = y_.x;                                                            \
-            cur[2 * x_ + 1] = y_.y;                                                        \
-        }                                                                                  \
-    } while (0)
-#define SP_LOAD_OFFS(c)  /* pass-1 offsets of records [c, c + kSpFast) of the run (clamped) */ \
-    do {                                                                                   \
-        _Pragma("unroll") for (int u_ = 0; u_ < kSpFast; ++u_) ro[u_] = pr[(c) + u_ < f ? (c) + u_ : e]; \
-    } while (0)
-#define SP_LOAD_RECS()                                                                     \
-    do {                                                                                   \
-        _Pragma("unroll") for (int u_ = 0; u_ < kSpFast; ++u_) {                           \
-            rk[u_] = a.p_key[ro[u_]];                                                      \
-            const longlong2 tv_ = a.p_tv[ro[u_]];                                          \
-            rt[u_] = tv_.x;                                                                \
-            rv[u_] = tv_.y;                                                                \
-        }                                                                                  \
-    } while (0)
-            SP_LOAD_LINE(slot);
-            SP_LOAD_OFFS(e);
-            SP_LOAD_RECS();
-            // the run's keys: one, or two (home slots shared by two keys of the batch) in a run
-            // of at most kSpFast records; anything else goes to k_sp_slow
-            const int64_t k0 = rk[0];
-            int64_t k1 = k0;
-            bool fit = true;
-            uint32_t L0 = L;
-            if (L <= (uint32_t)kSpFast) {
-                L0 = 1;
-#pragma unroll
-                for (int u = 1; u < kSpFast; ++u) {
-                    if ((uint32_t)u >= L) continue;
-                    if (rk[u] == k0) { ++L0; continue; }
-                    if (k1 == k0) k1 = rk[u];
-                    else if (rk[u] != k1) fit = false;
-                }
+    // records of the bucket
+    {
+        uint32_t x = 0;
+        for (int64_t g = g0 + tid; g < g1; g += kSbRThreads) x += desc[g * nf + f] & 0xffffu;
+        x = (uint32_t)wave_sum(x);
+        if (lane == 0) wsum[w] = x;
+        __syncthreads();
+        if (tid == 0) {
+            uint32_t tot = 0;
+            for (int q = 0; q < kSbRThreads / 64; ++q) tot += wsum[q];
+            s_n = tot;
+            s_pb = tot > (uint32_t)kSbCap ? (uint32_t)atomicAdd(&a.st->overflow, (unsigned long long)tot) : 0u;
+        }
+        __syncthreads();
+    }
+    const uint32_t n = s_n;
+    const bool over = n > (uint32_t)kSbCap;
+    const uint32_t pbase = s_pb;
+    // the runs in chunk order, kSbRThreads chunks at a time: a scan of their counts, then the
+    // block fills positions [run0, run0 + tot) cooperatively (coalesced within runs)
+    uint32_t run0 = 0;
+    for (int64_t b0 = g0; b0 < g1; b0 += kSbRThreads) {
+        const int64_t g = b0 + tid;
+        const uint32_t d = g < g1 ? desc[g * nf + f] : 0u;
+        const uint32_t x = d & 0xffffu;
+        uint32_t incl = x;
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t up = __shfl_up(incl, o);
+            if (lane >= o) incl += up;
+        }
+        if (lane == 63) wsum[w] = incl;
+        __syncthreads();
+        uint32_t pre = incl - x, tot = 0;
+        for (int q = 0; q < kSbRThreads / 64; ++q) {
+            if (q < w) pre += wsum[q];
+            tot += wsum[q];
+        }
+        cpre[tid] = pre;
+        hd[tid] = (uint32_t)(g * kSbTile) + (d >> 16);  // run starts
+        if (tid == 0) cpre[kSbRThreads] = tot;
+        __syncthreads();
+        for (uint32_t u = tid; u < tot; u += kSbRThreads) {
+            int lo = 0, hi = kSbRThreads - 1;  // last run with cpre <= u
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) >> 1;
+                if (cpre[mid] <= u) lo = mid; else hi = mid - 1;
+            }
+            const uint32_t o = hd[lo] + (u - cpre[lo]);
+            const uint32_t pos = run0 + u;
+            const int64_t kk = a.p_key[o];
+            if (over) {
+                const longlong2 tv = a.p_tv[o];
+                a.pu_key[pbase + pos] = kk;
+                a.pu_ts[pbase + pos] = tv.x;
+                a.pu_val[pbase + pos] = tv.y;
             } else {
-                for (uint32_t q = e;;) {
-#pragma unroll
-                    for (int u = 1; u < kSpFast; ++u) fit = fit && (q + u >= f || rk[u] == k0);
-                    q += kSpFast;
-                    if (q >= f || !fit) break;
-                    SP_LOAD_OFFS(q);
-                    SP_LOAD_RECS();
-                    fit = fit && rk[0] == k0;
-                }
-                SP_LOAD_OFFS(e);
-                SP_LOAD_RECS();
+                const uint32_t lh = kk == kEmptyKey ? sent : (uint32_t)(sb_home(kk, lcap) & hmask);
+                ka[pos] = (lh << kSbPosBits) | pos;
+                src[pos] = o;
             }
-            const bool two = k1 != k0;
-            const uint32_t L1 = L - L0;
-            // each key's slot: its home slot's line, or up to kSpProbe - 1 lines further
-            // (a free slot is claimed -- harmless if the run then goes to k_sp_slow after all)
-            int64_t slot0 = slot, slot1 = slot, c1w[8];
-#define SP_PROBE(KEY, SL, FOUND)                                                                           \
-    do {                                                                                                   \
-        for (int pr_ = 0; pr_ < kSpProbe && !(FOUND); ++pr_) {                                             \
-            if (cur[0] == (KEY)) { FOUND = true; break; }                                                  \
-            if (cur[0] == kEmptyKey) {                                                                     \
-                const unsigned long long prev_ = atomicCAS((unsigned long long*)slot_ptr(a.t, SL),         \
-                                                           (unsigned long long)kEmptyKey, (unsigned long long)(KEY)); \
-                if (prev_ == (unsigned long long)kEmptyKey) { /* new key: a free slot has word 1 == 0 */   \
-                    FOUND = true;                                                                          \
-                    ins++;                                                                                 \
-                    cur[1] = 0;                                                                            \
-                    break;                                                                                 \
-                }                                                                                          \
-            }                                                                                              \
-            SL = (SL + 1) & (a.t.cap - 1);                                                                 \
-            SP_LOAD_LINE(SL);                                                                              \
-        }                                                                                                  \
-    } while (0)
-            bool f0 = sentinel, f1 = true;
-            if (fit) SP_PROBE(k0, slot0, f0);
-            if (fit && two && f0) {
+        }
+        run0 += tot;
+        __syncthreads();  // cpre / the scratch tail are rewritten by the next block
+    }
+    if (over) {
+        block_commit(a.st, 0, 0, 0, 0);
+        return;
+    }
+    // home bits [kSbPosBits, kSbPosBits + sh + 1): passes of <= 9 bits
+    const int hb = sh + 1;
+    const int np = (hb + 8) / 9;
+    const uint32_t* fin = ka;
+    uint32_t* fin_o = kb;
+    for (int p = 0, done = 0; p < np; ++p) {
+        const int db = (hb - done + (np - p) - 1) / (np - p);
+        sb_radix_pass(fin, fin_o, (int)n, kSbPosBits + done, db, wcnt, wsum);
+        done += db;
+        uint32_t* t = const_cast<uint32_t*>(fin);
+        fin = fin_o;
+        fin_o = t;
+    }
+    // fin: the sorted keys; the order (buffer offsets in sorted order) replaces src in place
+    constexpr uint32_t pm = (1u << kSbPosBits) - 1u;
+    {
+        uint32_t o[kSbRItems];
 #pragma unroll
-                for (int x = 0; x < 8; ++x) c1w[x] = cur[x];  // key 0's line
-                f1 = false;
-                SP_LOAD_LINE(slot1);
-                SP_PROBE(k1, slot1, f1);
+        for (int it = 0; it < kSbRItems; ++it) {
+            const uint32_t i = it * kSbRThreads + tid;
+            o[it] = i < n ? src[fin[i] & pm] : 0u;
+        }
+        __syncthreads();
 #pragma unroll
-                for (int x = 0; x < 8; ++x) {  // cur: key 0's line again, c1w: key 1's
-                    const int64_t t = cur[x];
-                    cur[x] = c1w[x];
-                    c1w[x] = t;
-                }
-            }
-#undef SP_PROBE
-            const int64_t w10 = cur[1], w11 = two ? c1w[1] : 0;
-            const bool fast = fit && f0 && f1 && !((uint64_t)(w10 | w11) & (kBigMeta | kPuntMeta)) &&
-                              (!effects || (slot_cnt(w10) + L0 <= kLaneSess && slot_cnt(w11) + L1 <= kLaneSess));
-            if (fast) {  // each key's records replay from registers against its loaded line
-#pragma unroll 1
-                for (int ki = 0; ki < (two ? 2 : 1); ++ki) {
-                    const int64_t key = ki ? k1 : k0;
-                    const int64_t sl = ki ? slot1 : slot0;
-                    if (ki) {
-#pragma unroll
-                        for (int x = 0; x < 8; ++x) cur[x] = c1w[x];
-                    }
-                    const int64_t w1 = cur[1];
-                    int64_t* sp = slot_ptr(a.t, sl);
-                    int cnt = slot_cnt(w1);
-#pragma unroll
-                    for (int q = 0; q < (8 - 2) / SW; ++q)
-                        if (q < cnt)
-                            sl_put(l, q, Sess{cur[2 + q * SW], cur[3 + q * SW], cur[4 + q * SW],
-                                              SW == 4 ? cur[5 + q * SW] : 0, (int64_t)slot_fired(w1, q)});
-                    const unsigned long long l0 = late, m0 = merges;
-                    bool ok = true;
-                    for (uint32_t q = e; q < f && ok; q += kSpFast) {
-                        if (q != e) {
-                            SP_LOAD_OFFS(q);
-                            SP_LOAD_RECS();
-                        }
-                        const int m = (int)min((uint32_t)kSpFast, f - q);
-                        for (int u = 0; u < m && ok; ++u) {
-                            int64_t t = rt[0], v = rv[0], kk = rk[0];  // record u by selects: no scratch
-#pragma unroll
-                            for (int x = 1; x < kSpFast; ++x) {
-                                t = u == x ? rt[x] : t;
-                                v = u == x ? rv[x] : v;
-                                kk = u == x ? rk[x] : kk;
-                            }
-                            if (kk == key)
-                                ok = add_element_tv<AGG>(a, l, cnt, kLaneSess, key, t, v, late, merges, flags, false);
-                        }
-                    }
-                    if (ok) {
-                        sp_store<AGG>(a, l, cnt, sl, sp, w1);
-                    } else {  // outgrew the lane (no effects were written): punt the key's records
-                        late = l0;
-                        merges = m0;
-                        const uint32_t Lk = ki ? L1 : L0;
-                        unsigned long long at = atomicAdd(&a.st->overflow, (unsigned long long)Lk);
-                        for (uint32_t q = e; q < f; ++q) {
-                            const uint32_t o = pr[q];
-                            if (a.p_key[o] != key) continue;
-                            const longlong2 tv = a.p_tv[o];
-                            a.pu_key[at] = key;
-                            a.pu_ts[at] = tv.x;
-                            a.pu_val[at] = tv.y;
-                            ++at;
-                        }
-                        sp[1] = (int64_t)((uint64_t)w1 | kPuntMeta);
-                    }
-                    if (!ki && two) {  // key 1's records: reload the first chunk (the loop moved on)
-                        SP_LOAD_OFFS(e);
-                        SP_LOAD_RECS();
-                    }
-                }
-            } else {  // k_sp_slow replays it (a dense launch: no divergence against the fast runs)
-                if (a.exp) {  // GW_SP_EXP: why (two shards' spare counters)
-                    if (!fit) atomicAdd(&a.st->sh[0].pad0, 1ull);
-                    else if (!(f0 && f1)) atomicAdd(&a.st->sh[0].pad1, 1ull);
-                    else if ((uint64_t)(w10 | w11) & (kBigMeta | kPuntMeta)) atomicAdd(&a.st->sh[1].pad0, 1ull);
-                    else atomicAdd(&a.st->sh[1].pad1, 1ull);
-                }
-                const uint64_t bal = __ballot(true);
-                unsigned long long at = 0;
-                const int ld = __ffsll((long long)bal) - 1;
-                if (__lane_id() == ld) at = atomicAdd(&a.st->spills, (unsigned long long)__popcll(bal));
-                at = __shfl(at, ld);
-                a.slow[at + __popcll(bal & ((1ull << __lane_id()) - 1ull))] = ((uint32_t)b << kGrpPosBits) | j;
-            }
-#undef SP_LOAD_LINE
-#undef SP_LOAD_OFFS
-#undef SP_LOAD_RECS
+        for (int it = 0; it < kSbRItems; ++it) {
+            const uint32_t i = it * kSbRThreads + tid;
+            if (i < n) src[i] = o[it];
         }
     }
-    block_commit(a.st, late, ins, flags, 0, 0, merges);
-}
-
-// The home slots k_sp_keys left (a.slow, st->spills of them) through sp_run.
-template <int AGG>
-__global__ void __launch_bounds__(kSpKeyThreads) k_sp_slow(SegArgs a, const uint32_t* perm, const uint32_t* shd,
-                                                           const uint32_t* grp_n) {
-    constexpr uint32_t pm = (1u << kGrpPosBits) - 1u;
-    __shared__ int64_t lane[5 * kLaneSess * kSpKeyThreads];
-    const SessList l{lane + threadIdx.x, kLaneSess * kSpKeyThreads, kSpKeyThreads};
-    const uint64_t ns = a.st->spills;
+    const uint32_t* pr = src;
+    uint32_t nh = 0;  // heads: sorted index of each home slot's first record
+    for (uint32_t i0 = 0; i0 < n; i0 += kSbRThreads) {
+        const uint32_t i = i0 + tid;
+        const bool h = i < n && (i == 0 || (fin[i - 1] >> kSbPosBits) != (fin[i] >> kSbPosBits));
+        const uint64_t bal = __ballot(h);
+        if (lane == 0) wsum[w] = (uint32_t)__popcll(bal);
+        __syncthreads();
+        uint32_t base = nh, tot = 0;
+        for (int q = 0; q < kSbRThreads / 64; ++q) {
+            if (q < w) base += wsum[q];
+            tot += wsum[q];
+        }
+        if (h) hd[base + __popcll(bal & ((1ull << lane) - 1ull))] = i;
+        nh += tot;
+        __syncthreads();  // wsum is rewritten by the next chunk (and fin by the lanes)
+    }
+    // replay: one thread per home slot's run
+    const SessList l{lanes + tid, kLaneSess * kSbRThreads, kSbRThreads};
     unsigned long long late = 0, merges = 0, flags = 0, ins = 0;
-    for (uint64_t x = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; x < ns; x += (uint64_t)gridDim.x * blockDim.x) {
-        const uint32_t id = a.slow[x];
-        const int64_t b = id >> kGrpPosBits;
-        const uint32_t j = id & pm;
-        const uint32_t n = grp_n[2 * b], nh = grp_n[2 * b + 1];
-        const uint32_t e = shd[b * kGrpCap + j] & pm;
-        const uint32_t f = j + 1 < nh ? (shd[b * kGrpCap + j + 1] & pm) : n;
-        sp_run<AGG>(a, l, e, f, perm + b * kGrpCap, late, merges, flags, ins);
+    for (uint32_t j = tid; j < nh; j += kSbRThreads) {
+        const uint32_t e = hd[j], fe = j + 1 < nh ? hd[j + 1] : n;
+        sp_run<AGG>(a, l, e, fe, pr, late, merges, flags, ins);
     }
     block_commit(a.st, late, ins, flags, 0, 0, merges);
 }
+// P3 LDS: sort keys and radix buffer (then the session lanes), offsets / order, heads
+constexpr size_t kSbReplayLds = (size_t)kSbCap * 4 * 4;
+static_assert((size_t)5 * kLaneSess * kSbRThreads * 8 <= (size_t)kSbCap * 4 * 2, "the lanes alias the sort buffers");
+static_assert((size_t)(kSbRThreads / 64) * kSbBins * 2 <= (size_t)kSbCap * 4, "radix counters alias the heads");
 
 // After a replay with punts: clear the punt marks before the sort path replays the list.
 __global__ void __launch_bounds__(256) k_sp_unpunt(TableView t, const int64_t* pk, int64_t n) {
@@ -1807,14 +1682,12 @@ struct SessionState {
     uint32_t* r1 = nullptr;
     int64_t* mig = nullptr;  // migration lists (main pass -> wide table)
     int64_t* rec = nullptr;  // sessions: (ts, value) per record
-    // region-partitioned ingest (k_sp_*): pass-1 records (SoA), descriptor rows / columns,
-    // punted records
-    int64_t* sp_col3 = nullptr;  // key | ts | value, sp_cap each
-    uint32_t* sp_row = nullptr;  // sp_desc_cap each: rows, then columns
-    int64_t* pu_col3 = nullptr;  // punted key | ts | value, sp_cap each
-    uint32_t* sp_grp = nullptr;  // grouping: offsets by position | offsets in order | heads, counts
-    int64_t sp_cap = 0, sp_desc_cap = 0, sp_grp_cap = 0;
-    int sp_key_grid = 0;
+    // bucketed ingest (k_sb_*): P1 / P2 records (key | ts, value: 24 B each), descriptor
+    // rows / columns / coarse totals, punted records
+    int64_t* sb_rec[2] = {nullptr, nullptr};
+    uint32_t* sb_desc = nullptr;
+    int64_t* pu_col3 = nullptr;  // punted key | ts | value, sb_cap each
+    int64_t sb_cap = 0, sb_desc_cap = 0;
     bool fresh = false;      // h_st matches the device (nothing launched since the last refresh)
     int gshift = 0;          // sessions: the last sort grouped records by slot >> gshift
     uint32_t* due_list = nullptr;  // fire sweep: main-table slots with something due
@@ -1972,7 +1845,7 @@ void session_destroy(SessionState* s) {
     hipFree(s->r0); hipFree(s->r1); hipFree(s->mig); hipFree(s->rec);
     hipFree(s->cnt_plan); hipFree(s->cnt_tmp); hipFree(s->due_list);
     hipFree(s->sort_tmp);
-    hipFree(s->sp_col3); hipFree(s->sp_row); hipFree(s->pu_col3); hipFree(s->sp_grp);
+    hipFree(s->sb_rec[0]); hipFree(s->sb_rec[1]); hipFree(s->sb_desc); hipFree(s->pu_col3);
     hipFree(s->o_key); hipFree(s->o_start); hipFree(s->o_end); hipFree(s->o_res);
     for (auto* p : s->lo_buf) hipFree(p);
     for (int w = 0; w < 2; ++w) for (auto& p : s->ev_pending[w]) s->ev_pool.push_back(p);
@@ -2319,26 +2192,40 @@ static int ingest_sorted(SessionState* s, int64_t n, const int64_t* key, const i
     return GW_OK;
 }
 
-static void sp_opt_in(SessionState* s) {
-    if (!s->sp_key_grid) {  // persistent replay grid: the resident workgroups, a multiple of 8
-        int dev = 0, cus = 0, per = 0;
-        hipGetDevice(&dev);
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-#define L(A) hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void*)k_sp_keys<A>, kSpKeyThreads, 0)
-        GW_AGG_SWITCH(s->cfg.agg, L);
-#undef L
-        s->sp_key_grid = std::max(8, (std::max(cus, 1) * std::max(per, 1)) / 8 * 8);
-    }
+static void sb_opt_in() {
     static bool done = false;
-    if (!done) {
-        hipFuncSetAttribute((const void*)k_sp_part, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kSpPartLds);
-        hipFuncSetAttribute((const void*)k_sp_group, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kGrpLds);
-        done = true;
-    }
+    if (done) return;
+    hipFuncSetAttribute((const void*)k_sb_part<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kSbPartLds);
+    hipFuncSetAttribute((const void*)k_sb_part<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kSbPartLds);
+#define L(A) hipFuncSetAttribute((const void*)k_sb_replay<A>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kSbReplayLds)
+    L(GW_COUNT); L(GW_SUM_I64); L(GW_SUM_I32); L(GW_SUM_F64); L(GW_MIN_I64); L(GW_MIN_F64); L(GW_MAX_I64);
+    L(GW_MAX_F64); L(GW_AVG_I64); L(GW_AVG_F64);
+#undef L
+    done = true;
 }
 
-// Region path (k_sp_part / k_sp_transpose / k_sp_group / k_sp_keys), then migrations, then the sort
-// path over the punted records.
+// Bucket geometry of a batch of n records on a table of 2^lcap slots: bb bucket bits (about
+// 2^kSbMeanBits records per bucket; the sort key holds at most kSbMaxHomeBits home bits per
+// bucket), split into bb1 coarse (P1) and bb2 fine (P2) digit bits.  False: beyond the
+// bucketed path's geometry (the sort path takes the batch).
+static bool sb_geometry(int64_t n, int lcap, int& bb, int& bb1, int& bb2) {
+    bb = 0;
+    while (bb < 2 * kSbMaxDigitBits && (n >> (bb + kSbMeanBits)) > 0) ++bb;
+    bb = std::max(bb, lcap - kSbMaxHomeBits);
+    bb = std::min(bb, lcap);
+    if (bb > 2 * kSbMaxDigitBits) return false;
+    if (bb <= kSbSinglePassBits) {
+        bb1 = bb;
+        bb2 = 0;
+    } else {
+        bb1 = (bb + 1) / 2;
+        bb2 = bb - bb1;
+    }
+    return true;
+}
+
+// Bucketed path (k_sb_part P1 / k_sb_cols / k_sb_part P2 / k_sb_replay), then migrations, then
+// the sort path over the punted records.
 static int ingest_region(SessionState* s, int64_t n, const int64_t* key, const int64_t* ts, const int64_t* val,
                          int64_t wm, std::string& err) {
     int rc;
@@ -2354,90 +2241,78 @@ static int ingest_region(SessionState* s, int64_t n, const int64_t* key, const i
     if ((rc = ensure_bufs(s, n, err))) return rc;  // the migration list
     int lcap = 0;
     while (((int64_t)1 << lcap) < s->tv.cap) ++lcap;
-    int bb = std::min(lcap, 10);
-    if (lcap - bb > kGrpMaxHomeBits) bb = lcap - kGrpMaxHomeBits;  // the sort key's home bits
-    if (bb > 10) return ingest_sorted(s, n, key, ts, val, wm, err);  // beyond 2^26 slots
-    const int nb = 1 << bb;
-    const int64_t ntiles = (n + kSpTile - 1) / kSpTile;
-    const int64_t recs = ntiles * kSpTile;
-    if (recs > s->sp_cap || (int64_t)nb * kGrpCap > s->sp_grp_cap || ntiles * nb > s->sp_desc_cap) {
+    int bb, bb1, bb2;
+    if (!sb_geometry(n, lcap, bb, bb1, bb2)) return ingest_sorted(s, n, key, ts, val, wm, err);
+    const int sh = lcap - bb;
+    const int nd1 = 1 << bb1, nd2 = 1 << bb2;
+    const int64_t ntiles = (n + kSbTile - 1) / kSbTile;
+    const int64_t nch = bb2 ? ntiles + nd1 : 0;  // P2 chunks: an upper bound
+    const int64_t recs = (ntiles + nch) * kSbTile;
+    // descriptors: P1 rows + columns, coarse totals, P2 rows
+    const int64_t dwords = 2 * ntiles * nd1 + nd1 + nch * nd2;
+    if ((ntiles + nd1) * kSbTile > s->sb_cap || dwords > s->sb_desc_cap) {
         SCHECK(hipStreamSynchronize(s->stream));
-        if (recs > s->sp_cap) {
-            hipFree(s->sp_col3); hipFree(s->pu_col3);
-            s->sp_col3 = nullptr; s->pu_col3 = nullptr;
-            const int64_t c = std::max<int64_t>(recs + recs / 4, kSpTile * 16);
-            SCHECK(hipMalloc((void**)&s->sp_col3, (size_t)c * 24));
-            SCHECK(hipMalloc((void**)&s->pu_col3, (size_t)c * 28));  // + the slow-slot list (u32)
-            s->sp_cap = c;
+        if ((ntiles + nd1) * kSbTile > s->sb_cap) {
+            for (auto*& p : s->sb_rec) { hipFree(p); p = nullptr; }
+            hipFree(s->pu_col3);
+            s->pu_col3 = nullptr;
+            const int64_t c = std::max<int64_t>((ntiles + nd1) * kSbTile * 5 / 4, kSbTile * 16);
+            for (auto*& p : s->sb_rec) SCHECK(hipMalloc((void**)&p, (size_t)c * 24));
+            SCHECK(hipMalloc((void**)&s->pu_col3, (size_t)c * 24));
+            s->sb_cap = c;
         }
-        if ((int64_t)nb * kGrpCap > s->sp_grp_cap) {
-            hipFree(s->sp_grp);
-            s->sp_grp = nullptr;
-            const int64_t c = (int64_t)nb * kGrpCap;
-            SCHECK(hipMalloc((void**)&s->sp_grp, (size_t)(3 * c + 2 * nb) * 4));  // offsets by position, order, heads
-            s->sp_grp_cap = c;
-        }
-        if (ntiles * nb > s->sp_desc_cap) {
-            hipFree(s->sp_row);
-            s->sp_row = nullptr;
-            const int64_t c = std::max<int64_t>((ntiles + ntiles / 4 + 16) * nb, 1 << 16);
-            SCHECK(hipMalloc((void**)&s->sp_row, (size_t)c * 2 * 4));
-            s->sp_desc_cap = c;
+        if (dwords > s->sb_desc_cap) {
+            hipFree(s->sb_desc);
+            s->sb_desc = nullptr;
+            const int64_t c = std::max<int64_t>(dwords * 5 / 4, 1 << 16);
+            SCHECK(hipMalloc((void**)&s->sb_desc, (size_t)c * 4));
+            s->sb_desc_cap = c;
         }
     }
-    const int64_t C = s->sp_cap, G = s->sp_grp_cap;
-    int64_t* pk = s->sp_col3;
-    uint32_t* row = s->sp_row;
-    uint32_t* col = s->sp_row + s->sp_desc_cap;
-    uint32_t* gsrc = s->sp_grp;
-    uint32_t* perm = gsrc + G;
-    uint32_t* shd = perm + G;
-    uint32_t* grp_n = shd + G;
-    sp_opt_in(s);
+    (void)recs;
+    const int64_t C = s->sb_cap;
+    int64_t* k1 = s->sb_rec[0];
+    longlong2* tv1 = reinterpret_cast<longlong2*>(k1 + C);
+    int64_t* k2 = s->sb_rec[1];
+    longlong2* tv2 = reinterpret_cast<longlong2*>(k2 + C);
+    uint32_t* row1 = s->sb_desc;
+    uint32_t* col1 = row1 + ntiles * nd1;
+    uint32_t* ctot = col1 + ntiles * nd1;
+    uint32_t* row2 = ctot + nd1;
+    sb_opt_in();
     if ((rc = zero_word_async(s, offsetof(DevStatus, overflow), err))) return rc;
     if ((rc = zero_word_async(s, offsetof(DevStatus, pad[0]), err))) return rc;
     if ((rc = zero_word_async(s, offsetof(DevStatus, pad[1]), err))) return rc;
-    hipLaunchKernelGGL(k_sp_part, dim3((unsigned)ntiles), dim3(kSpThreads), kSpPartLds, s->stream, key, ts, val, n,
-                       s->tv.cap, lcap, bb, pk, reinterpret_cast<longlong2*>(pk + C), row, s->d_st);
-    hipLaunchKernelGGL(k_sp_transpose, dim3((unsigned)((ntiles + 63) / 64), (unsigned)((nb + 63) / 64)), dim3(256), 0,
-                       s->stream, row, col, ntiles, nb);
-    SCHECK(hipGetLastError());
+    hipLaunchKernelGGL(k_sb_part<false>, dim3((unsigned)ntiles), dim3(kSbThreads), kSbPartLds, s->stream, key, ts, val,
+                       n, nullptr, nullptr, nullptr, nullptr, 0, ntiles, lcap, sh + bb2, bb1, k1, tv1, row1, s->d_st);
     SegArgs a{};
     if ((rc = seg_common(s, a, n, wm, err))) return rc;
-    a.p_key = pk;
-    a.p_tv = reinterpret_cast<const longlong2*>(pk + C);
-    a.col = col;
-    a.ntiles = ntiles;
-    a.lcap = lcap;
-    a.bb = bb;
     a.pu_key = s->pu_col3;
     a.pu_ts = s->pu_col3 + C;
     a.pu_val = s->pu_col3 + 2 * C;
-    static const int sp_exp = getenv("GW_SP_EXP") ? atoi(getenv("GW_SP_EXP")) : 0;
-    a.exp = sp_exp;
-    hipLaunchKernelGGL(k_sp_group, dim3((unsigned)nb), dim3(kGrpThreads), kGrpLds, s->stream, a, gsrc, perm, shd, grp_n);
-    a.slow = reinterpret_cast<uint32_t*>(s->pu_col3 + 3 * C);
-    if ((rc = zero_word_async(s, offsetof(DevStatus, spills), err))) return rc;
-#define L(A)                                                                                                   \
-    hipLaunchKernelGGL(k_sp_keys<A>, dim3((unsigned)s->sp_key_grid), dim3(kSpKeyThreads), 0, s->stream, a, perm, shd, \
-                       grp_n, nb);                                                                              \
-    hipLaunchKernelGGL(k_sp_slow<A>, dim3(1024), dim3(kSpKeyThreads), 0, s->stream, a, perm, shd, grp_n)
+    if (bb2) {
+        SCHECK(hipMemsetAsync(ctot, 0, (size_t)nd1 * 4, s->stream));
+        hipLaunchKernelGGL(k_sb_cols, dim3((unsigned)((ntiles + 63) / 64), (unsigned)((nd1 + 63) / 64)), dim3(256), 0,
+                           s->stream, row1, col1, ctot, ntiles, nd1);
+        hipLaunchKernelGGL(k_sb_part<true>, dim3((unsigned)nch), dim3(kSbThreads), kSbPartLds, s->stream, nullptr,
+                           nullptr, nullptr, n, k1, tv1, col1, ctot, nd1, ntiles, lcap, sh, bb2, k2, tv2, row2,
+                           s->d_st);
+        a.p_key = k2;
+        a.p_tv = tv2;
+    } else {
+        a.p_key = k1;
+        a.p_tv = tv1;
+    }
+    SCHECK(hipGetLastError());
+#define L(A)                                                                                                     \
+    hipLaunchKernelGGL(k_sb_replay<A>, dim3((unsigned)(nd1 * nd2)), dim3(kSbRThreads), kSbReplayLds, s->stream, a, \
+                       bb2 ? row2 : row1, ctot, bb2 ? nd1 : 1, bb2 ? nch : ntiles, bb2 ? bb2 : bb1, lcap, sh)
     GW_AGG_SWITCH(s->cfg.agg, L);
 #undef L
     SCHECK(hipGetLastError());
     if ((rc = session_refresh(s, err))) return rc;
     const int64_t n_punt = (int64_t)s->h_st->overflow;
     s->stats.session_punted += n_punt;
-    if (sp_exp) {
-        fprintf(stderr, "[sp_keys] slow home slots %llu of batch %lld (keys %llu, probe %llu, wide %llu, lane %llu), "
-                        "punted %lld\n",
-                (unsigned long long)s->h_st->spills, (long long)n, (unsigned long long)s->h_st->sh[0].pad0,
-                (unsigned long long)s->h_st->sh[0].pad1, (unsigned long long)s->h_st->sh[1].pad0,
-                (unsigned long long)s->h_st->sh[1].pad1, (long long)n_punt);
-        SCHECK(launch_status_set(s->d_st, 0, 0, 6, s->stream));  // ShardCtr pad0
-        SCHECK(launch_status_set(s->d_st, 0, 0, 7, s->stream));  // ShardCtr pad1
-    }
-    s->stats.session_slow += (int64_t)s->h_st->spills;
     if ((rc = run_migrate(s, err))) return rc;
     if (!n_punt) return GW_OK;
     hipLaunchKernelGGL(k_sp_unpunt, dim3(grid_of(n_punt)), dim3(256), 0, s->stream, s->tv, a.pu_key, n_punt);
@@ -2450,7 +2325,7 @@ static int ingest_region(SessionState* s, int64_t n, const int64_t* key, const i
 static bool region_ingest_enabled() {
     const char* p = getenv("GW_SESSION_PATH");
     if (p) return strcmp(p, "sort") != 0;
-    return getenv("GW_SESSION_SORT_BITS") ? false : kSessionRegionDefault != 0;
+    return getenv("GW_SESSION_SORT_BITS") == nullptr;
 }
 
 int session_ingest(SessionState* s, int64_t n, const int64_t* key, const int64_t* ts, const int64_t* val, int64_t wm,

@@ -536,6 +536,29 @@ class GpuWindowOperator:
             raise N.GpuWinError(-1, f"{len(carry)} bytes of an incomplete element at the end of the input")
         return fired
 
+    # staged host ingest (gw_stage_*): pinned library-owned columns filled in place ------------
+    def stage_alloc(self, slots: int, cap: int):
+        """`slots` pinned column slots of `cap` records (gw_stage_alloc)."""
+        self._ensure_handle()
+        N.check(N.lib().gw_stage_alloc(self._h, int(slots), int(cap)), self._h)
+        self._stage_cap = int(cap)
+
+    def stage_columns(self, slot: int):
+        """Slot `slot`'s (key int64, key_hash int32, ts int64, value int64) columns as numpy arrays
+        over the pinned memory, once the slot's previous transfer has read it."""
+        p = [ctypes.c_void_p() for _ in range(4)]
+        N.check(N.lib().gw_stage_columns(self._h, int(slot), *[ctypes.byref(x) for x in p]), self._h)
+        cap = self._stage_cap
+
+        def arr(ptr, ct):
+            return np.ctypeslib.as_array(ctypes.cast(ptr.value, ctypes.POINTER(ct)), shape=(cap,))
+        return arr(p[0], ctypes.c_int64), arr(p[1], ctypes.c_int32), arr(p[2], ctypes.c_int64), arr(p[3], ctypes.c_int64)
+
+    def ingest_stage(self, slot: int, n: int, with_value: bool = True, with_key_hash: bool = False):
+        """The slot's first n records (gw_ingest_stage)."""
+        cols = (N.STAGE_VALUE if with_value else 0) | (N.STAGE_KEY_HASH if with_key_hash else 0)
+        N.check(N.lib().gw_ingest_stage(self._h, int(slot), int(n), cols), self._h)
+
     def process_batch_device(self, keys, timestamps, values=None, stream=None):
         """Columns already in HBM (torch tensors or raw device pointers)."""
         self._ensure_handle()

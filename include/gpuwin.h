@@ -183,6 +183,21 @@ int  gw_abi_version(void);
  * Flink operator sees for the records between two watermarks. */
 int  gw_ingest(gw_handle* h, int64_t n, const int64_t* key, const int32_t* key_hash,
                const int64_t* ts, const void* value);
+/* Library-owned pinned column slots for callers that build a batch in place (the JVM operator
+ * writes each record's fields straight into them as direct ByteBuffers, so no copy precedes the
+ * PCIe transfer).  gw_stage_alloc: `slots` slots of `cap` records.  gw_stage_columns: slot's
+ * key / key_hash / ts / value columns (any pointer may be NULL), once the slot's previous
+ * transfer has read it.  gw_ingest_stage: the slot's first n records, as gw_ingest would take
+ * them (cols: GW_STAGE_VALUE and / or GW_STAGE_KEY_HASH); the transfer runs on a copy stream
+ * into one of two device buffers used in turn, so it overlaps the previous batch's kernels.  The
+ * slot may be refilled after the next gw_stage_columns on it returns.  Not for composite or
+ * first-element handles (GW_E_UNSUPPORTED). */
+#define GW_STAGE_VALUE    1
+#define GW_STAGE_KEY_HASH 2
+int  gw_stage_alloc(gw_handle* h, int32_t slots, int64_t cap);
+int  gw_stage_columns(gw_handle* h, int32_t slot, int64_t** key, int32_t** key_hash, int64_t** ts,
+                      int64_t** value);
+int  gw_ingest_stage(gw_handle* h, int32_t slot, int64_t n, int32_t cols);
 /* Same, with the columns already resident in device memory (d_* are device
  * pointers).  `stream` is the hipStream_t the inputs were produced on (NULL = the
  * default stream).  The handle's stream (gw_stream) reads them after that stream's

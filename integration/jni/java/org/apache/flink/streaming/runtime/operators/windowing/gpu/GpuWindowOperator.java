@@ -153,6 +153,8 @@ public class GpuWindowOperator<IN, K>
     private transient TimestampedCollector<Object> collector;
     private transient WindowContext windowContext;
     private transient long currentWm = Long.MIN_VALUE;  // the watermark the current firing runs at
+    private transient boolean staged;  // the column buffers are the library's pinned slots (gw_stage_*)
+    private transient int slot;        // the slot processElement fills
 
     /** inputArity: fields of the input Tuple; positionalField: the aggregated field of a
      *  POSITIONAL sum/min/max (the result replaces it in the emitted tuple). */
@@ -266,6 +268,7 @@ public class GpuWindowOperator<IN, K>
         }
         keys = direct(8); keyHashes = direct(4); ts = direct(8); values = direct(8);
         oKey = direct(8); oStart = direct(8); oEnd = direct(8); oRes = direct(8);
+        if (!handleDeferred) bindStaging();
         if (restored != null) {  // initializeState runs before open (StreamOperator.java:139)
             for (int i = 0; i < restored.size(); i++) {
                 byte[] blob = restored.get(i);
@@ -308,6 +311,23 @@ public class GpuWindowOperator<IN, K>
         }
     }
 
+    /** Two library-owned pinned slots (gw_stage_alloc) as the operator's column buffers:
+     *  processElement writes each record into the memory the PCIe transfer reads, and the
+     *  transfer of one batch overlaps the GPU work of the previous one.  Composite and
+     *  first-element handles keep their own direct buffers (nativeIngest / nativeIngestPayload). */
+    private void bindStaging() {
+        staged = !wide() && nativeStageAlloc(handle, 2, batchCapacity) == 0;
+        if (staged) bindSlot(0);
+    }
+
+    private void bindSlot(int s) {
+        slot = s;
+        keys = nativeStageColumn(handle, s, 0, batchCapacity).order(ByteOrder.nativeOrder());
+        keyHashes = nativeStageColumn(handle, s, 1, batchCapacity).order(ByteOrder.nativeOrder());
+        ts = nativeStageColumn(handle, s, 2, batchCapacity).order(ByteOrder.nativeOrder());
+        values = nativeStageColumn(handle, s, 3, batchCapacity).order(ByteOrder.nativeOrder());
+    }
+
     /** The handle, with the windows' offset (the stagger decided by the caller). */
     private void createHandle(long windowOffset) {
         int subtask = getRuntimeContext().getTaskInfo().getIndexOfThisSubtask();
@@ -324,6 +344,7 @@ public class GpuWindowOperator<IN, K>
         int code = stagger == WindowStagger.RANDOM ? 1 : stagger == WindowStagger.NATURAL ? 2 : 0;
         createHandle(nativeStaggerOffset(code, now, ThreadLocalRandom.current().nextDouble(), size, offset));
         handleDeferred = false;
+        bindStaging();
         if (deferredWatermark != Long.MIN_VALUE) nativeAdvanceWatermark(handle, deferredWatermark);  // no state: fires nothing
     }
 
@@ -485,6 +506,10 @@ public class GpuWindowOperator<IN, K>
             nativeIngestPayload(handle, n, keys, kh, ts, values, payload);
             batches.addLast(new long[] {elements.end(), batchMaxTs});
             batchMaxTs = Long.MIN_VALUE;
+        } else if (n > 0 && staged) {
+            nativeIngestStage(handle, slot, n, (doubleValue != null || longValue != null ? 1 /* GW_STAGE_VALUE */ : 0)
+                    | (longKeys ? 0 : 2 /* GW_STAGE_KEY_HASH */));
+            bindSlot(slot ^ 1);  // the other slot, once its previous transfer has read it
         } else if (n > 0) {
             nativeIngest(handle, n, keys, kh, ts, values);
         }
@@ -671,6 +696,9 @@ public class GpuWindowOperator<IN, K>
 
     public long numLateRecordsDropped() { return nativeLateDropped(handle); }
 
+    private static native int nativeStageAlloc(long h, int slots, int cap);
+    private static native ByteBuffer nativeStageColumn(long h, int slot, int which, int cap);
+    private static native void nativeIngestStage(long h, int slot, int n, int cols);
     private static native long nativeStaggerOffset(int stagger, long processingTime, double random01, long size,
                                                    long globalOffset);
     private static native long nativeCreate(int assigner, int trigger, long size, long slide, long offset, long gap,

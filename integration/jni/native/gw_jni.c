@@ -56,6 +56,35 @@ JNIEXPORT void JNICALL CLS(nativeIngest)(JNIEnv* env, jclass c, jlong h, jint n,
     fail(env, (gw_handle*)(intptr_t)h, gw_ingest((gw_handle*)(intptr_t)h, n, k, kh, t, v));
 }
 
+/* Staged ingest (gw_stage_*): the operator's column buffers are the library's pinned slots, so
+ * processElement writes each record straight into the memory the PCIe transfer reads.
+ * nativeStageAlloc returns the status without throwing: GW_E_UNSUPPORTED (a composite or
+ * first-element handle) leaves the operator on its own direct buffers and nativeIngest. */
+JNIEXPORT jint JNICALL CLS(nativeStageAlloc)(JNIEnv* env, jclass c, jlong h, jint slots, jint cap) {
+    return gw_stage_alloc((gw_handle*)(intptr_t)h, slots, cap);
+}
+
+/* Column `which` (0 key, 1 key hash, 2 timestamp, 3 value) of a slot as a direct ByteBuffer of
+ * cap entries, once the slot's previous transfer has read it. */
+JNIEXPORT jobject JNICALL CLS(nativeStageColumn)(JNIEnv* env, jclass c, jlong h, jint slot, jint which, jint cap) {
+    gw_handle* g = (gw_handle*)(intptr_t)h;
+    int64_t *k = 0, *t = 0, *v = 0;
+    int32_t* kh = 0;
+    int rc = gw_stage_columns(g, slot, &k, &kh, &t, &v);
+    if (rc) {
+        fail(env, g, rc);
+        return 0;
+    }
+    void* p = which == 0 ? (void*)k : which == 1 ? (void*)kh : which == 2 ? (void*)t : (void*)v;
+    return (*env)->NewDirectByteBuffer(env, p, (jlong)cap * (which == 1 ? 4 : 8));
+}
+
+/* The slot's first n records (cols: GW_STAGE_VALUE | GW_STAGE_KEY_HASH). */
+JNIEXPORT void JNICALL CLS(nativeIngestStage)(JNIEnv* env, jclass c, jlong h, jint slot, jint n, jint cols) {
+    gw_handle* g = (gw_handle*)(intptr_t)h;
+    fail(env, g, gw_ingest_stage(g, slot, n, cols));
+}
+
 /* Network-buffer ingest: `bytes` is a direct ByteBuffer holding one input channel's
  * serialized elements (the payload of its network buffers, in order); `types` the Tuple's
  * field type codes ("JJ" for Tuple2<Long, Long>).  Returns the bytes consumed; the caller

@@ -143,6 +143,9 @@ def run(name, args, dev):
     torch.cuda.synchronize()
     rows = 0
     op_events = 0
+    op.enable_kernel_timing(True)
+    for w in range(3):
+        op.kernel_time_ms(w)  # reset
     t0 = time.perf_counter()
     for b in range(args.warmup, steps):
         step(b)
@@ -150,12 +153,15 @@ def run(name, args, dev):
     op.synchronize()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
+    kt = [op.kernel_time_ms(w) for w in range(3)]  # (avg ms, launches): ingest, fire, flush/apply
     stats = op.stats()
     op.close()
+    roof = roofline(name, kw, agg, keys, ts, nb, args.warmup, steps, op_events, rows, kt, dt)
     out = {"config": name, "window": kw, "aggregate": agg, "events_per_step": nb, "steps": n_timed,
            "value": nb * n_timed / dt, "unit": "events/s", "ms_per_step": dt * 1e3 / n_timed,
            "operator_events_per_s": op_events / dt,
-           "rows_fired": rows, "live_keys": stats.get("live_keys"), "data": "synthetic, generated in HBM"}
+           "rows_fired": rows, "live_keys": stats.get("live_keys"), "data": "synthetic, generated in HBM",
+           "roofline": roof}
     if ysb:
         out["pipeline"] = "filter(event_type == view) + join(ad_id -> campaign_id) on the GPU, then the operator"
     if first:
@@ -174,6 +180,58 @@ def run(name, args, dev):
         else:
             out["cpu_baseline"] = cpu_baseline(kw, agg, keys, ts, vals, wms, nb, args.cpu_seconds)
     return out
+
+
+HBM_PEAK_GBS = 8000.0
+# What bounds each config at the round's code, and the next kernel target.
+BOUND_NOTE = {
+    "sessions": "replay (k_sb_replay: one probe + state line per key of the batch, records gathered from "
+                "the L2-resident bucket) -- the next target",
+    "q7": "region pipeline as in the headline (pass 1 + flush), fire at each 10-s window end",
+    "q7_first": "two pane operators + the payload log and join",
+    "q7_maxby": "MAX pane operator + 4-column log + per-fire probe (k_by_scan)",
+    "ysb": "the torch filter / join ahead of the operator (operator kernels are a small share of the step)",
+    "wordcount": "count-window replay (k_cnt_apply) over a Zipf vocabulary: hot keys serialise",
+}
+
+
+def roofline(name, kw, agg, keys, ts, nb, warm, steps, op_events, rows, kt, dt):
+    """HBM roofline of the operator's own launches over the timed steps: algorithmic bytes
+    (each event's input columns once, each distinct per-batch state entry read
+    and written once, each fired row written once) over their device time (HIP events on the
+    operator's stream: ingest + flush/apply + fire)."""
+    s_acc = 16 if agg.startswith("avg") else 8
+    b_in = 16 if agg == "count" else 24  # key + ts (+ value)
+    dsum = 0
+    if name == "sessions":
+        state = 48  # key, meta, start, end, sum, count: the key's slot line
+        for b in range(warm, steps):
+            dsum += int(torch.unique(keys[b * nb:(b + 1) * nb]).numel())
+    elif name == "wordcount":
+        state = 8 * (2 + kw["size"] // int(np.gcd(kw["size"], kw["slide"])))  # key, meta, the pane ring
+        for b in range(warm, steps):
+            dsum += int(torch.unique(keys[b * nb:(b + 1) * nb]).numel())
+    elif name == "ysb":
+        state = s_acc
+        dsum = None  # <= 100 campaigns x 2 windows per batch: negligible
+    else:
+        state = s_acc
+        size = kw["size"]
+        for b in range(warm, steps):
+            comp = keys[b * nb:(b + 1) * nb] * 4096 + ((ts[b * nb:(b + 1) * nb] // size) % 4096)
+            dsum += int(torch.unique(comp).numel())
+    alg = op_events * b_in + 2 * state * (dsum or 0) + rows * (32 + s_acc)
+    dev_ms = sum(ms * n for ms, n in kt)
+    achieved = alg / (dev_ms / 1e3) / 1e9 if dev_ms > 0 else 0.0
+    return {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+            "algorithmic_bytes": alg, "bytes_per_event": alg / max(op_events, 1),
+            "formula": f"events x {b_in} B + 2 x {state} B x distinct state entries per batch + rows x {32 + s_acc} B",
+            "device_ms_per_step": dev_ms / max(steps - warm, 1),
+            "device_share_of_step": dev_ms / 1e3 / dt if dt > 0 else None,
+            "launch_ms": {"ingest": kt[0], "fire": kt[1], "flush": kt[2]},
+            "distinct_per_batch": (dsum / max(steps - warm, 1)) if dsum is not None else None,
+            "bound_by": BOUND_NOTE.get(name)}
 
 
 def cpu_baseline(kw, agg, keys, ts, vals, wms, nb, seconds):

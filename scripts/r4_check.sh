@@ -7,7 +7,7 @@ export TMPDIR=/tmp
 TAG=${TAG:-chk}
 if [ -n "${TESTS:-}" ]; then
   timeout -k 10 ${TEST_TIMEOUT:-600} python -u -m pytest -x -v --timeout ${PER_TEST:-300} --timeout-method thread \
-      --durations=0 -m gpu $TESTS > gpurun_out/r4/pytest_${TAG}.log 2>&1
+      --durations=0 -m gpu ${K:+-k "$K"} $TESTS > gpurun_out/r4/pytest_${TAG}.log 2>&1
   rc=$?
   tail -25 gpurun_out/r4/pytest_${TAG}.log
   [ $rc -eq 0 ] || exit $rc

@@ -51,9 +51,10 @@ static void f_set_longs(JNIEnv* e, jlongArray a, jsize s, jsize n, const jlong* 
     memcpy(((fake_longs*)a)->data + s, src, (size_t)n * 8);
 }
 
+static jobject f_new_direct(JNIEnv* e, void* a, jlong cap) { (void)e; (void)cap; return (jobject)a; }
 static const struct JNINativeInterface_ g_table = {f_find_class, f_throw_new, f_direct, f_utf, f_rel_utf,
                                                    f_len, f_bytes, f_rel_bytes, f_new_bytes, f_set_region,
-                                                   f_longs, f_rel_longs, f_new_longs, f_set_longs};
+                                                   f_longs, f_rel_longs, f_new_longs, f_set_longs, f_new_direct};
 static JNIEnv g_env = &g_table;
 
 JNIEnv* fake_env(void) { return &g_env; }

@@ -37,5 +37,6 @@ struct JNINativeInterface_ {
     void (*ReleaseLongArrayElements)(JNIEnv* env, jlongArray array, jlong* elems, jint mode);
     jlongArray (*NewLongArray)(JNIEnv* env, jsize len);
     void (*SetLongArrayRegion)(JNIEnv* env, jlongArray array, jsize start, jsize len, const jlong* buf);
+    jobject (*NewDirectByteBuffer)(JNIEnv* env, void* address, jlong capacity);
 };
 #endif

@@ -1,11 +1,13 @@
-"""Region-partitioned session ingest (gw_session.hip k_sp_part / k_sp_group / k_sp_keys), the
-default session path, against the oracle:
+"""Bucketed session ingest (gw_session.hip k_sb_part P1 / k_sb_cols / k_sb_part P2 /
+k_sb_replay), the default session path, against the oracle:
 
 * buckets holding many records of a batch (a small table under large batches: hundreds to
   thousands of records per bucket, so the LDS radix sort, the ordered head list and runs of
-  several records per home slot all work at more than one wave's worth);
+  several records per home slot all work at more than one wave's worth), with and without
+  the second partition pass (P2 runs when a batch needs more than 2^6 buckets);
+* a large table under a small batch (the bucket count set by the sort key's home-bit limit);
 * home slots shared by several keys (more keys than home slots in a bucket);
-* a hot key whose bucket exceeds kGrpCap (16384) records in one batch: the bucket goes to the
+* a hot key whose bucket exceeds kSbCap (4096) records in one batch: the bucket goes to the
   punt list and the sort path replays it (stats()["session_punted"] counts it);
 * keys that need the wide table mid-batch (more sessions than the lane holds), under allowed
   lateness and the late side output too;
@@ -43,8 +45,21 @@ def test_dense_buckets_match_oracle(oracle_lib, agg, gap, lateness):
 
 
 @pytest.mark.parametrize("agg", ["sum_i64", "avg_f64"])
+def test_large_table_small_batches(oracle_lib, agg):
+    """2^25 slots, 120k-record batches: 2^7 buckets (the home bits per bucket are capped), so
+    both partition passes run on a batch the mean-size rule alone would single-pass."""
+    kw = dict(assigner="session", gap=400, agg=agg)
+    keys, ts, vals, batches = random_stream(seed=21, n=480_000, num_keys=90_000, n_batches=4, ts_step=1,
+                                            disorder=300, wm_lag=300, agg=agg)
+    g, glate, st = run_gpu(kw, keys, ts, vals, batches, capacity_hint=20_000_000)
+    o, olate = run_oracle(oracle_lib, kw, keys, ts, vals, batches)
+    assert glate == olate
+    assert compare(g, o, agg == "avg_f64") == []
+
+
+@pytest.mark.parametrize("agg", ["sum_i64", "avg_f64"])
 def test_hot_key_bucket_goes_to_sort_path(oracle_lib, agg):
-    """One key carries 40% of 100k records per batch: its bucket exceeds 16384 records."""
+    """One key carries 40% of 100k records per batch: its bucket exceeds kSbCap records."""
     kw = dict(assigner="session", gap=50, agg=agg)
     keys, ts, vals, batches = random_stream(seed=5, n=300_000, num_keys=20_000, n_batches=3, ts_step=1,
                                             disorder=200, wm_lag=200, agg=agg)

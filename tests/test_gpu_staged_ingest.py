@@ -1,0 +1,83 @@
+"""Staged host ingest (gw_stage_alloc / gw_stage_columns / gw_ingest_stage): the columns a JVM
+operator writes straight into library-owned pinned slots, sent over PCIe on a copy stream into
+two device buffers used in turn.  Against the oracle on the same stream: slots refilled many
+times (each refill waits for the slot's previous transfer), more batches than slots, key hashes
+(String-like keys), COUNT without a value column, and the host path gw_ingest on top of it."""
+import numpy as np
+import pytest
+
+from flink_amd import _native as N
+from flink_amd import windowing as W
+from tests.gpu_helpers import compare, gpu_operator, random_stream, run_oracle
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("agg,slots", [("sum_i64", 2), ("count", 3), ("max_f64", 5)])
+def test_staged_slots_match_oracle(oracle_lib, agg, slots):
+    kw = dict(assigner="sliding", size=2000, slide=500, agg=agg)
+    keys, ts, vals, batches = random_stream(seed=61, n=300_000, num_keys=20_000, n_batches=24, agg=agg)
+    vb = vals.view(np.int64) if vals.dtype == np.float64 else vals
+    cap = max(hi - lo for lo, hi, _ in batches)
+    op = gpu_operator(kw, capacity_hint=1 << 16)
+    outs = []
+    try:
+        op.stage_alloc(slots, cap)
+        for b, (lo, hi, wm) in enumerate(batches):
+            k, _, t, v = op.stage_columns(b % slots)
+            k[:hi - lo] = keys[lo:hi]
+            t[:hi - lo] = ts[lo:hi]
+            if agg != "count":
+                v[:hi - lo] = vb[lo:hi]
+            op.ingest_stage(b % slots, hi - lo, with_value=agg != "count")
+            op.advance_watermark(wm)
+            k_, s_, e_, r_ = op.drain()
+            outs.append((k_, s_, e_, r_.view(np.int64)))
+        op.advance_watermark(W.LONG_MAX)
+        k_, s_, e_, r_ = op.drain()
+        outs.append((k_, s_, e_, r_.view(np.int64)))
+    finally:
+        op.close()
+    o, _ = run_oracle(oracle_lib, kw, keys, ts, vals, batches)
+    assert compare(outs, o, agg.endswith("f64")) == []
+
+
+def test_staged_key_hashes_file_keys_by_their_hash(oracle_lib):
+    """Key ids with a caller-given Java hashCode: a snapshot of the staged handle files each key
+    under its own key group, as gw_ingest with the same hashes does."""
+    kw = dict(assigner="tumbling", size=1000, slide=1000, agg="sum_i64")
+    keys, ts, vals, batches = random_stream(seed=62, n=40_000, num_keys=3_000, n_batches=6, agg="sum_i64")
+    hashes = ((keys * 1_000_003 + 7) % (1 << 31)).astype(np.int32)
+    blobs = []
+    for staged in (True, False):
+        op = gpu_operator(kw, capacity_hint=1 << 14)
+        try:
+            if staged:
+                op.stage_alloc(2, max(hi - lo for lo, hi, _ in batches))
+            for b, (lo, hi, wm) in enumerate(batches):
+                if staged:
+                    k, h, t, v = op.stage_columns(b % 2)
+                    k[:hi - lo], h[:hi - lo], t[:hi - lo], v[:hi - lo] = keys[lo:hi], hashes[lo:hi], ts[lo:hi], vals[lo:hi]
+                    op.ingest_stage(b % 2, hi - lo, with_value=True, with_key_hash=True)
+                else:
+                    op.process_batch(keys[lo:hi], ts[lo:hi], vals[lo:hi], key_hashes=hashes[lo:hi])
+                op.advance_watermark(wm)
+                op.clear_rows()
+            blobs.append(op.snapshot_state())
+        finally:
+            op.close()
+    assert blobs[0] == blobs[1]
+
+
+def test_staged_rejections():
+    op = gpu_operator(dict(assigner="tumbling", size=1000, slide=1000, agg="sum_i64"))
+    try:
+        op.stage_alloc(2, 100)
+        with pytest.raises(N.GpuWinError):
+            op.ingest_stage(2, 10)  # no such slot
+        with pytest.raises(N.GpuWinError):
+            op.ingest_stage(0, 101)  # beyond the slot
+        with pytest.raises(N.GpuWinError):
+            op.ingest_stage(0, 10, with_value=False)  # SUM needs its values
+    finally:
+        op.close()
