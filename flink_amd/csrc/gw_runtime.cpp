@@ -1923,6 +1923,7 @@ struct gw_handle {
         for (int64_t g = 0; g < nk; ++g) {
             NEED(4);
             const int32_t ns = rd32(p); p += 4;
+            if (ns < 0) return fail(GW_E_INVALID, "negative entry count in snapshot key group");
             NEED((int64_t)ns * (24 + hb + ab));
             const size_t base = pend.size();
             for (int32_t i = 0; i < ns; ++i) {
@@ -1945,6 +1946,7 @@ struct gw_handle {
             p += 4;
             NEED(4);
             const int32_t nt = rd32(p); p += 4;
+            if (nt < 0) return fail(GW_E_INVALID, "negative timer count in snapshot key group");
             NEED((int64_t)nt * 32);
             // an event-time timer at the window's maxTimestamp: the window has not fired
             std::sort(pend.begin() + base, pend.end(), by_key_k);

@@ -130,6 +130,19 @@ __device__ __forceinline__ int64_t due_time(int64_t end, bool fired, int64_t lat
 // touches only the slots with something due.
 __device__ __forceinline__ int64_t* due_of(const TableView& t) { return t.base + (t.cap + 1) * (int64_t)t.stride_w; }
 
+// Due summary: per block of kDueBlk slots a lower bound of their due times (after the due
+// array), so the fire sweep reads 8 B per 64 slots and only the blocks that can hold
+// something due.  Writers keep it a lower bound (atomicMin of a new due time); the sweep
+// makes a block's entry exact again after scanning it.  INT64_MIN: scan the block.
+constexpr int kDueBlkBits = 6;
+constexpr int kDueBlk = 1 << kDueBlkBits;
+__host__ __device__ __forceinline__ int64_t due_blocks(int64_t cap) { return (cap + 1 + kDueBlk - 1) >> kDueBlkBits; }
+__device__ __forceinline__ int64_t* dsum_of(const TableView& t) { return due_of(t) + (t.cap + 1); }
+__device__ __forceinline__ void due_set(const TableView& t, int64_t slot, int64_t due) {
+    due_of(t)[slot] = due;
+    if (due != INT64_MAX) atomicMin((long long*)dsum_of(t) + (slot >> kDueBlkBits), (long long)due);
+}
+
 __device__ __forceinline__ int64_t inline_due(const int64_t* sp, int SW, int64_t lateness) {
     const int64_t w1 = sp[1];
     if (slot_big(w1)) return INT64_MAX;
@@ -318,7 +331,7 @@ __device__ __forceinline__ void seg_slot(const SegArgs& a, const SessList& l, in
             due = min(due, due_time(v.e, v.f != 0, a.lateness));
         }
         sp[1] = (int64_t)((fired << 32) | (uint64_t)(uint32_t)cnt);
-        due_of(a.t)[slot] = due;
+        due_set(a.t, slot, due);
     } else {  // more sessions than the slot holds: the finished list moves to the wide table
         const unsigned long long at = atomicAdd(&a.st->pad[0], 1ull);
         int64_t* m = a.mig + at * (2 + kWideWords * kLaneSess);
@@ -869,7 +882,7 @@ __device__ __forceinline__ void sp_store(const SegArgs& a, const SessList& l, in
             due = min(due, due_time(v.e, v.f != 0, a.lateness));
         }
         sp[1] = (int64_t)((fired << 32) | (uint64_t)(uint32_t)cnt);
-        due_of(a.t)[slot] = due;
+        due_set(a.t, slot, due);
     } else {
         const unsigned long long at = atomicAdd(&a.st->pad[0], 1ull);
         int64_t* m = a.mig + at * (2 + kWideWords * kLaneSess);
@@ -1133,20 +1146,25 @@ __global__ void __launch_bounds__(256) k_sp_unpunt(TableView t, const int64_t* p
     }
 }
 
-// Fire sweep, part 1: stream the due array (8 B per slot) and list the slots with
-// something due at `wm` -- a small fraction: the sessions that close at this watermark.
-// Each workgroup scans one contiguous chunk with 16-B loads (4 per lane in flight),
-// collects its hits in LDS and reserves list space with one atomic at the end.
+// Fire sweep, part 1: list the slots with something due at `wm` -- a small fraction: the
+// sessions that close at this watermark.  A wave reads the due summary of 64 blocks (one per
+// lane), then scans each block whose lower bound is <= wm (64 due times, one per lane),
+// lists its due slots and stores the block's exact minimum over the slots it did not list
+// (k_sess_fire lowers it again for the slots it re-arms).  Hits are collected in LDS and
+// list space is reserved with one atomic per workgroup.
 constexpr int kDueBuf = 4096;
 __global__ void __launch_bounds__(256) k_sess_due_scan(TableView t, int64_t wm, uint32_t* list, DevStatus* st) {
     __shared__ uint32_t buf[kDueBuf];
     __shared__ unsigned cnt;
     __shared__ unsigned long long gbase;
-    const int64_t nslots = t.cap + 1;
+    // an ingest's follow-up (punts or migrations) is pending: the host fires again after it
+    if (st->overflow | st->pad[0]) return;
+    const int64_t nslots = t.cap + 1, nblk = due_blocks(t.cap);
     const int64_t* due = due_of(t);
-    constexpr int kStep = 256 * 2 * 4;  // slots per workgroup iteration
-    const int64_t chunk = ((nslots + gridDim.x - 1) / gridDim.x + kStep - 1) / kStep * kStep;
-    const int64_t lo = blockIdx.x * chunk, hi = min(nslots, lo + chunk);
+    int64_t* dsum = dsum_of(t);
+    const int lane = threadIdx.x & 63;
+    const int64_t wave = (blockIdx.x * (int64_t)blockDim.x + threadIdx.x) >> 6;
+    const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
     if (threadIdx.x == 0) cnt = 0;
     __syncthreads();
     auto hit = [&](int64_t i) {
@@ -1157,25 +1175,18 @@ __global__ void __launch_bounds__(256) k_sess_due_scan(TableView t, int64_t wm, 
             list[atomicAdd(&st->n_refire, 1ull)] = (uint32_t)i;
         }
     };
-    for (int64_t b = lo; b < hi; b += kStep) {
-        int64_t d[8];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const int64_t i = b + u * 512 + 2 * threadIdx.x;
-            if (i + 1 < hi) {
-                const longlong2 x = *reinterpret_cast<const longlong2*>(due + i);
-                d[2 * u] = x.x;
-                d[2 * u + 1] = x.y;
-            } else {
-                d[2 * u] = i < hi ? due[i] : INT64_MAX;
-                d[2 * u + 1] = INT64_MAX;
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const int64_t i = b + u * 512 + 2 * threadIdx.x;
-            if (d[2 * u] <= wm && i < hi) hit(i);
-            if (d[2 * u + 1] <= wm && i + 1 < hi) hit(i + 1);
+    for (int64_t b0 = wave * 64; b0 < nblk; b0 += nwaves * 64) {
+        const int64_t bl = b0 + lane;
+        const bool hot = bl < nblk && dsum[bl] <= wm;
+        for (uint64_t m = __ballot(hot); m; m &= m - 1) {  // wave-uniform
+            const int64_t b = b0 + __ffsll((long long)m) - 1;
+            const int64_t i = (b << kDueBlkBits) + lane;
+            const int64_t d = i < nslots ? due[i] : INT64_MAX;
+            const bool h = d <= wm;
+            if (h) hit(i);
+            int64_t mn = h ? INT64_MAX : d;
+            for (int o = 32; o > 0; o >>= 1) mn = min(mn, (int64_t)__shfl_xor(mn, o));
+            if (lane == 0) dsum[b] = mn;
         }
     }
     __syncthreads();
@@ -1250,7 +1261,7 @@ __global__ void __launch_bounds__(256) k_sess_fire(TableView t, const uint32_t* 
                 }
             }
             s[1] = (int64_t)((fired << 32) | (uint64_t)(uint32_t)(cnt - nc));
-            due_of(t)[i] = inline_due(s, SW, lateness);
+            due_set(t, i, inline_due(s, SW, lateness));
         }
     }
     stage_flush(rs, &st->rows, o_key, o_start, o_end, o_res);
@@ -1261,6 +1272,7 @@ template <int AGG>
 __global__ void __launch_bounds__(256) k_sess_fire_wide(TableView w, int64_t wm, int64_t lateness, int purge,
                                                         int64_t* o_key, int64_t* o_start, int64_t* o_end,
                                                         int64_t* o_res, DevStatus* st) {
+    if (st->overflow | st->pad[0]) return;  // as k_sess_due_scan
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i <= w.cap; i += (int64_t)gridDim.x * blockDim.x) {
         if (due_of(w)[i] > wm) continue;
         int64_t* s = slot_ptr(w, i);
@@ -1309,7 +1321,8 @@ __global__ void __launch_bounds__(256) k_sess_rehash(TableView o, TableView n, i
         d[1] = s[1];
         const int nw = words_per_slot < 0 ? (int)s[1] * o.words : words_per_slot;
         for (int w = 0; w < nw; ++w) d[2 + w] = s[2 + w];
-        due_of(n)[j] = due_of(o)[i];
+        if (ins_field < 0) due_of(n)[j] = due_of(o)[i];
+        else due_set(n, j, due_of(o)[i]);
     }
     ins = wave_sum(ins);
     flags = wave_ior(flags);
@@ -1329,6 +1342,9 @@ __global__ void __launch_bounds__(256) k_sess_init(TableView t) {
         s[1] = 0;
         due_of(t)[i] = INT64_MAX;
     }
+    for (int64_t b = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; b < due_blocks(t.cap);
+         b += (int64_t)gridDim.x * blockDim.x)
+        dsum_of(t)[b] = INT64_MAX;
 }
 
 // Restore (gw_restore of a session snapshot): one thread per restored key.  A key with at
@@ -1357,7 +1373,7 @@ __global__ void __launch_bounds__(256) k_sess_restore(TableView t, TableView w, 
                 fired |= (uint64_t)(x[4] != 0) << q;
             }
             sp[1] = (int64_t)((fired << 32) | (uint64_t)cnt);
-            due_of(t)[slot] = inline_due(sp, SW, lateness);
+            due_set(t, slot, inline_due(sp, SW, lateness));
         } else {
             const int64_t g2 = find_or_insert(w, rk[i], inserted);
             if (g2 < 0) { flags |= GW_DF_TABLE_FULL; continue; }
@@ -1689,6 +1705,12 @@ struct SessionState {
     int64_t* pu_col3 = nullptr;  // punted key | ts | value, sb_cap each
     int64_t sb_cap = 0, sb_desc_cap = 0;
     bool fresh = false;      // h_st matches the device (nothing launched since the last refresh)
+    // A bucketed ingest whose host follow-up (punts, migrations) waits for the next sync: the
+    // fire launched right after it checks the device counters and skips itself if the
+    // follow-up has work (k_sess_due_scan), so the common batch costs one host sync, not two.
+    bool sb_pend = false;
+    int64_t sb_wm = 0, sb_new = 0;
+    int64_t* sb_pu[3] = {nullptr, nullptr, nullptr};
     int gshift = 0;          // sessions: the last sort grouped records by slot >> gshift
     uint32_t* due_list = nullptr;  // fire sweep: main-table slots with something due
     int64_t due_list_cap = 0;
@@ -1746,7 +1768,10 @@ static std::pair<hipEvent_t, hipEvent_t> get_ev(SessionState* s) {
     return p;
 }
 
-int session_refresh(SessionState* s, std::string& err) {
+static int sb_finish(SessionState* s, std::string& err);
+
+// Device counters -> host view (one host sync), then a pending ingest's follow-up.
+static int sess_sync(SessionState* s, std::string& err) {
     SCHECK(hipMemcpyAsync(s->h_st, s->d_st, sizeof(DevStatus), hipMemcpyDeviceToHost, s->stream));
     SCHECK(hipStreamSynchronize(s->stream));
     fold_shards(s->h_st);
@@ -1763,6 +1788,12 @@ int session_refresh(SessionState* s, std::string& err) {
     }
     s->fresh = true;
     return GW_OK;
+}
+
+int session_refresh(SessionState* s, std::string& err) {
+    int rc = sess_sync(s, err);
+    if (rc == GW_OK && s->sb_pend) rc = sb_finish(s, err);
+    return rc;
 }
 
 // Entry of a call that launches work: the host view is refreshed unless nothing ran on the
@@ -1795,7 +1826,7 @@ static int alloc_table(SessionState* s, TableView& t, int64_t cap, int ring, int
     t.ring = ring;
     t.words = words;
     t.stride_w = (int)(((2 + ring * words) + 7) / 8 * 8);
-    SCHECK(hipMalloc((void**)&t.base, (size_t)(cap + 1) * (t.stride_w + 1) * 8));  // slots + due times
+    SCHECK(hipMalloc((void**)&t.base, ((size_t)(cap + 1) * (t.stride_w + 1) + (size_t)due_blocks(cap)) * 8));  // slots + due times + due summary
     hipLaunchKernelGGL(k_sess_init, dim3(grid_of(cap + 1)), dim3(256), 0, s->stream, t);
     SCHECK(hipGetLastError());
     return GW_OK;
@@ -2133,6 +2164,7 @@ static int run_migrate(SessionState* s, std::string& err) {
     hipLaunchKernelGGL(k_sess_migrate, dim3(grid_of(n_mig)), dim3(256), 0, s->stream, s->tv, s->wv, s->mig, n_mig,
                        s->cfg.allowed_lateness, s->d_st);
     SCHECK(hipGetLastError());
+    if ((rc = zero_word_async(s, offsetof(DevStatus, pad[0]), err))) return rc;  // (the fire's guard)
     if ((rc = session_refresh(s, err))) return rc;
     if (s->h_st->flags & GW_DF_TABLE_FULL) { err = "session wide table full"; return GW_E_OOM; }
     return GW_OK;
@@ -2310,14 +2342,33 @@ static int ingest_region(SessionState* s, int64_t n, const int64_t* key, const i
     GW_AGG_SWITCH(s->cfg.agg, L);
 #undef L
     SCHECK(hipGetLastError());
-    if ((rc = session_refresh(s, err))) return rc;
+    s->sb_pend = true;
+    s->sb_wm = wm;
+    s->sb_new = n;
+    s->sb_pu[0] = a.pu_key;
+    s->sb_pu[1] = a.pu_ts;
+    s->sb_pu[2] = a.pu_val;
+    s->fresh = false;
+    // without allowed lateness and side output the replay emits nothing, so the follow-up
+    // may wait for the fire's sync (GW_SESSION_SYNC=1: always sync here)
+    static const bool always = getenv("GW_SESSION_SYNC") && atoi(getenv("GW_SESSION_SYNC")) != 0;
+    if (!always && a.lateness == 0 && !a.lo_key) return GW_OK;
+    return session_refresh(s, err);
+}
+
+// The follow-up of a bucketed ingest (h_st fresh): migrations, then the punted records
+// through the sort path.
+static int sb_finish(SessionState* s, std::string& err) {
+    if (!s->sb_pend) return GW_OK;
+    s->sb_pend = false;
+    int rc;
     const int64_t n_punt = (int64_t)s->h_st->overflow;
     s->stats.session_punted += n_punt;
     if ((rc = run_migrate(s, err))) return rc;
     if (!n_punt) return GW_OK;
-    hipLaunchKernelGGL(k_sp_unpunt, dim3(grid_of(n_punt)), dim3(256), 0, s->stream, s->tv, a.pu_key, n_punt);
+    hipLaunchKernelGGL(k_sp_unpunt, dim3(grid_of(n_punt)), dim3(256), 0, s->stream, s->tv, s->sb_pu[0], n_punt);
     SCHECK(hipGetLastError());
-    return ingest_sorted(s, n_punt, a.pu_key, a.pu_ts, a.pu_val, wm, err);
+    return ingest_sorted(s, n_punt, s->sb_pu[0], s->sb_pu[1], s->sb_pu[2], s->sb_wm, err);
 }
 
 // GW_SESSION_PATH=region|sort picks the ingest path (GW_SESSION_SORT_BITS, the sort path's
@@ -2353,42 +2404,57 @@ int session_fire(SessionState* s, int64_t wm, int64_t* fired, std::string& err) 
         return GW_OK;
     }
     int rc;
-    if ((rc = begin_launch(s, err))) return rc;
-    const int64_t before = (int64_t)s->h_st->rows;
-    const int64_t need = before + (int64_t)(s->h_st->used_slots + 1) * s->tv.ring +
-                         (int64_t)(s->h_st->pad[2] + 1) * s->wv.ring;
-    if ((rc = ensure_rows(s, need, err))) return rc;
-    auto ev = s->timing ? get_ev(s) : std::pair<hipEvent_t, hipEvent_t>{};
-    if (s->timing) SCHECK(hipEventRecord(ev.first, s->stream));
-    const unsigned fg = (unsigned)std::min<int64_t>(1024, std::max<int64_t>(1, (s->tv.cap + 1 + 255) / 256));
-    if (s->due_list_cap < s->tv.cap + 1) {
-        hipFree(s->due_list);
-        s->due_list = nullptr;
-        SCHECK(hipMalloc((void**)&s->due_list, (size_t)(s->tv.cap + 1) * 4));
-        s->due_list_cap = s->tv.cap + 1;
-    }
-    if ((rc = zero_word_async(s, offsetof(DevStatus, n_refire), err))) return rc;  // due-list cursor
-    const unsigned sg = (unsigned)std::min<int64_t>(2048, std::max<int64_t>(1, (s->tv.cap + 1) / 2048));
-    hipLaunchKernelGGL(k_sess_due_scan, dim3(sg), dim3(256), 0, s->stream, s->tv, wm, s->due_list, s->d_st);
-    const int purge = (int)(s->cfg.allowed_lateness > 0 && s->cfg.trigger == GW_PURGING_EVENT_TIME_TRIGGER);
+    for (;;) {
+        // spec: an ingest's follow-up is pending (its replay emitted no rows); this fire runs
+        // before the host has looked, and skips itself on the device if there is follow-up work
+        const bool spec = s->sb_pend;
+        if (spec) {
+            s->fresh = false;
+        } else if ((rc = begin_launch(s, err))) {
+            return rc;
+        }
+        const int64_t before = (int64_t)s->h_st->rows;
+        const int64_t keys = (int64_t)s->h_st->used_slots + (spec ? s->sb_new : 0);  // spec: an upper bound
+        const int64_t need = before + (keys + 1) * s->tv.ring + (int64_t)(s->h_st->pad[2] + 1) * s->wv.ring;
+        if ((rc = ensure_rows(s, need, err))) return rc;
+        auto ev = s->timing ? get_ev(s) : std::pair<hipEvent_t, hipEvent_t>{};
+        if (s->timing) SCHECK(hipEventRecord(ev.first, s->stream));
+        const unsigned fg = (unsigned)std::min<int64_t>(1024, std::max<int64_t>(1, (s->tv.cap + 1 + 255) / 256));
+        if (s->due_list_cap < s->tv.cap + 1) {
+            SCHECK(hipStreamSynchronize(s->stream));
+            hipFree(s->due_list);
+            s->due_list = nullptr;
+            SCHECK(hipMalloc((void**)&s->due_list, (size_t)(s->tv.cap + 1) * 4));
+            s->due_list_cap = s->tv.cap + 1;
+        }
+        if ((rc = zero_word_async(s, offsetof(DevStatus, n_refire), err))) return rc;  // due-list cursor
+        const unsigned sg = (unsigned)std::min<int64_t>(2048, std::max<int64_t>(1, (s->tv.cap + 1) / 2048));
+        hipLaunchKernelGGL(k_sess_due_scan, dim3(sg), dim3(256), 0, s->stream, s->tv, wm, s->due_list, s->d_st);
+        const int purge = (int)(s->cfg.allowed_lateness > 0 && s->cfg.trigger == GW_PURGING_EVENT_TIME_TRIGGER);
 #define L(A)                                                                                               \
-    hipLaunchKernelGGL(k_sess_fire<A>, dim3(fg), dim3(256), 0, s->stream, s->tv, s->due_list, wm,            \
-                       s->cfg.allowed_lateness, purge, s->o_key, s->o_start, s->o_end, s->o_res, s->d_st); \
-    if (s->h_st->pad[2])                                                                                    \
-    hipLaunchKernelGGL(k_sess_fire_wide<A>, dim3(grid_of(s->wv.cap + 1)), dim3(256), 0, s->stream, s->wv, wm, \
-                       s->cfg.allowed_lateness, purge, s->o_key, s->o_start, s->o_end, s->o_res, s->d_st)
-    GW_AGG_SWITCH(s->cfg.agg, L);
+        hipLaunchKernelGGL(k_sess_fire<A>, dim3(fg), dim3(256), 0, s->stream, s->tv, s->due_list, wm,        \
+                           s->cfg.allowed_lateness, purge, s->o_key, s->o_start, s->o_end, s->o_res, s->d_st); \
+        if (s->h_st->pad[2])                                                                                \
+        hipLaunchKernelGGL(k_sess_fire_wide<A>, dim3(grid_of(s->wv.cap + 1)), dim3(256), 0, s->stream, s->wv, wm, \
+                           s->cfg.allowed_lateness, purge, s->o_key, s->o_start, s->o_end, s->o_res, s->d_st)
+        GW_AGG_SWITCH(s->cfg.agg, L);
 #undef L
-    SCHECK(hipGetLastError());
-    if (s->timing) {
-        SCHECK(hipEventRecord(ev.second, s->stream));
-        s->ev_pending[1].push_back(ev);
+        SCHECK(hipGetLastError());
+        if (s->timing) {
+            SCHECK(hipEventRecord(ev.second, s->stream));
+            s->ev_pending[1].push_back(ev);
+        }
+        if ((rc = sess_sync(s, err))) return rc;
+        if (spec) {
+            const bool skipped = s->h_st->overflow || s->h_st->pad[0];
+            if ((rc = sb_finish(s, err))) return rc;
+            if (skipped) continue;  // the follow-up has run: fire over the complete state
+        }
+        s->stats.fires++;
+        *fired = (int64_t)s->h_st->rows - before;
+        s->wm = wm;
+        return GW_OK;
     }
-    s->stats.fires++;
-    if ((rc = session_refresh(s, err))) return rc;
-    *fired = (int64_t)s->h_st->rows - before;
-    s->wm = wm;
-    return GW_OK;
 }
 
 void session_rows(SessionState* s, int64_t** k, int64_t** st, int64_t** en, int64_t** r, int64_t* total) {
@@ -2396,7 +2462,8 @@ void session_rows(SessionState* s, int64_t** k, int64_t** st, int64_t** en, int6
     *total = (int64_t)s->h_st->rows;
 }
 
-int session_clear_rows(SessionState* s, std::string& err) { return set_word(s, offsetof(DevStatus, rows), 0, err); }
+// Stream-ordered (no host wait): the host view is updated with it, so a refreshed view stays valid.
+int session_clear_rows(SessionState* s, std::string& err) { return zero_word_async(s, offsetof(DevStatus, rows), err); }
 
 // ---- snapshot / restore of in-flight sessions (gw_snapshot / gw_restore) -------------
 // The heap backend snapshots, per key group, every (key, window) state entry plus the
@@ -2523,6 +2590,7 @@ int session_restore(SessionState* s, const int64_t* ent, int64_t n, std::string&
     if (rc) return rc;
     if (s->h_st->flags & GW_DF_TABLE_FULL) { err = "session state table full"; return GW_E_OOM; }
     if (s->h_st->overflow) {
+        if ((rc = zero_word_async(s, offsetof(DevStatus, overflow), err))) return rc;  // (the fire's guard)
         err = "a restored key already holds sessions in this operator (key group restored twice)";
         return GW_E_UNSUPPORTED;
     }

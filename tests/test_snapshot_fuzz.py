@@ -117,3 +117,25 @@ def test_entry_blob_damage(version, words):
     blob, _, _ = make_blob(version, words, 8, 23, lambda k: (k * 5) % 4, seed=version)
     for m in mutants(blob, version, 400):
         read_all(m, [8, 15, 23])
+
+
+
+@pytest.mark.parametrize("kw", CFGS, ids=lambda c: "-".join(str(v) for v in c.values()))
+@pytest.mark.parametrize("count", [-1, -(2**31)])
+def test_v4_negative_entry_count_rejected(oracle_lib, kw, count):
+    """A key group whose entry count is negative is a damaged blob: the readers that parse the
+    key groups refuse it (GW_E_INVALID) instead of reading it as an empty key group.
+    (gw_snapshot_slice cuts by the offset table without parsing; the restore that reads the
+    slice refuses it the same way -- restore_heap / restore_sessions, GPU handles.)"""
+    blob = oracle_blob(oracle_lib, kw, 13)
+    kg_lo, kg_hi = struct.unpack_from("<ii", blob, 60)
+    nk = kg_hi - kg_lo + 1
+    offs = struct.unpack_from(f"<{nk + 1}q", blob, 96)
+    pay0 = 96 + 8 * (nk + 1)
+    g = next(i for i in range(nk) if offs[i + 1] > offs[i])  # a non-empty key group
+    b = bytearray(blob)
+    struct.pack_into(">i", b, pay0 + offs[g], count)
+    with pytest.raises(N.GpuWinError):
+        N.snapshot_keys(bytes(b))
+    with pytest.raises(N.GpuWinError):
+        N.snapshot_keys(N.snapshot_slice(bytes(b), kg_lo + g))
