@@ -1483,11 +1483,12 @@ __global__ void __launch_bounds__(kApplyThreads) k_rgn_apply_nar(IngestArgs a) {
         int64_t rb, re;
         unsigned long long pos;  // ring positions this list contributes
     };
-    const List lists[2] = {
-        {a.r_row, a.r_base, reinterpret_cast<const uint64_t*>(a.e_key), reinterpret_cast<const uint32_t*>(a.e_key), rb0,
-         re0, cur_pos & 0xffull},
-        {a.c_r_row, a.c_r_base, reinterpret_cast<const uint64_t*>(a.c_key), reinterpret_cast<const uint32_t*>(a.c_key),
-         rb1, re1, a.c_mask & 0xffull}};
+    // two named lists picked by a uniform select (an array indexed by the loop variable would
+    // live in scratch memory)
+    const List list0{a.r_row, a.r_base, reinterpret_cast<const uint64_t*>(a.e_key),
+                     reinterpret_cast<const uint32_t*>(a.e_key), rb0, re0, cur_pos & 0xffull};
+    const List list1{a.c_r_row, a.c_r_base, reinterpret_cast<const uint64_t*>(a.c_key),
+                     reinterpret_cast<const uint32_t*>(a.c_key), rb1, re1, a.c_mask & 0xffull};
 
     // which ring positions hold records of this super-region (a region without any skips
     // the state round trip)
@@ -1497,7 +1498,7 @@ __global__ void __launch_bounds__(kApplyThreads) k_rgn_apply_nar(IngestArgs a) {
     {
         uint32_t any = 0;
         for (int l = 0; l < 2; ++l) {
-            const List& L = lists[l];
+            const List L = l ? list1 : list0;
             for (int64_t rnd = L.rb + threadIdx.x; rnd < L.re; rnd += blockDim.x)
                 for (unsigned long long pm = L.pos; pm; pm &= pm - 1) {
                     const int p = __ffsll((long long)pm) - 1;
@@ -1618,7 +1619,7 @@ __global__ void __launch_bounds__(kApplyThreads) k_rgn_apply_nar(IngestArgs a) {
             }
         }
         for (int l = 0; l < 2; ++l) {
-            const List& L = lists[l];
+            const List L = l ? list1 : list0;
             if (!((L.pos >> p) & 1)) continue;  // uniform
             const uint64_t* rk = L.rk;
             const uint32_t* rk32 = L.rk32;
@@ -1749,7 +1750,7 @@ __global__ void __launch_bounds__(kApplyThreads) k_rgn_apply_nar(IngestArgs a) {
     if (__syncthreads_or(spills != 0)) {
         unsigned long long marked = 0;
         for (int l = 0; l < 2; ++l) {
-            const List& L = lists[l];
+            const List L = l ? list1 : list0;
             for (unsigned long long pm = L.pos & pmask; pm; pm &= pm - 1) {
                 const int p = __ffsll((long long)pm) - 1;
                 const int64_t ccol = (col << 3) | p;

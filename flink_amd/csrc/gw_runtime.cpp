@@ -749,7 +749,7 @@ struct gw_handle {
 
     int merge_deferred() {
         int rc;
-        if (nseg && (rc = flush_buffer())) return rc;  // the merge writes the table directly
+        if ((nseg || carry_on) && (rc = flush_buffer())) return rc;  // the merge writes the table directly
         const int64_t nin = (int64_t)h_st->n_deferred;
         if (nin == 0) return GW_OK;
         for (int attempt = 0; attempt < 8; ++attempt) {
@@ -1285,7 +1285,7 @@ struct gw_handle {
             if (big || (cfg.flags & GW_FLAG_FORCE_REGION)) path = 2;
         }
         if (path == 1) stats.preagg_batches++;
-        if (path != 2 && nseg) {  // the other paths write the table directly: apply first
+        if (path != 2 && (nseg || carry_on)) {  // the other paths write the table directly: apply first
             if ((rc = flush_buffer())) return rc;
             if ((rc = base_args(a, nrec, key, ts, val))) return rc;  // the table may have grown
         }
@@ -1360,7 +1360,7 @@ struct gw_handle {
         }
         // An empty ring with parked records: jump the ring to the data (the buffer holds
         // no in-ring record then; apply it before the ring moves all the same).
-        if (!occ && h_st->n_deferred && nseg && (rc = flush_buffer())) return rc;
+        if (!occ && h_st->n_deferred && (nseg || carry_on) && (rc = flush_buffer())) return rc;
         if (!occ && h_st->n_deferred) {
             i128 dmin;
             if ((rc = deferred_min(dmin))) return rc;
@@ -2108,7 +2108,9 @@ struct gw_handle {
             if ((rc = ensure_fresh())) return rc;
             before = (int64_t)h_st->rows;
         }
-        if ((rc = flush_buffer())) return rc;  // buffered records first, then the timers
+        // buffered records first, then the timers (without lateness only the positions the
+        // firing needs were applied above; the rest stays carried for the next flush)
+        if (cfg.allowed_lateness > 0 && (rc = flush_buffer())) return rc;
         {
             if ((rc = fire_until(kt, ct))) return rc;
             wm = w;

@@ -984,7 +984,8 @@ __device__ __forceinline__ void sp_run(const SegArgs& a, const SessList& l, uint
 // all of them (arrival order) to the sort path: its keys are disjoint from the other buckets'.
 template <int AGG>
 __global__ void __launch_bounds__(kSbRThreads) k_sb_replay(SegArgs a, const uint32_t* desc, const uint32_t* ctot,
-                                                           int nc, int64_t nchunks, int bf, int lcap, int sh) {
+                                                           int nc, int64_t nchunks, int bf, int lcap, int sh,
+                                                           int exp) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     uint32_t* ka = reinterpret_cast<uint32_t*>(smem);  // sort keys | radix double buffer
     uint32_t* kb = ka + kSbCap;
@@ -1072,7 +1073,7 @@ __global__ void __launch_bounds__(kSbRThreads) k_sb_replay(SegArgs a, const uint
         run0 += tot;
         __syncthreads();  // cpre / the scratch tail are rewritten by the next block
     }
-    if (over) {
+    if (over || exp == 2) {  // (exp: GW_SB_EXP timing variants, results invalid: 2 = gather only)
         block_commit(a.st, 0, 0, 0, 0);
         return;
     }
@@ -1121,6 +1122,10 @@ __global__ void __launch_bounds__(kSbRThreads) k_sb_replay(SegArgs a, const uint
         if (h) hd[base + __popcll(bal & ((1ull << lane) - 1ull))] = i;
         nh += tot;
         __syncthreads();  // wsum is rewritten by the next chunk (and fin by the lanes)
+    }
+    if (exp == 1) {  // gather + sort + heads only
+        block_commit(a.st, 0, 0, 0, 0);
+        return;
     }
     // replay: one thread per home slot's run
     const SessList l{lanes + tid, kLaneSess * kSbRThreads, kSbRThreads};
@@ -1182,7 +1187,7 @@ __global__ void __launch_bounds__(256) k_sess_due_scan(TableView t, int64_t wm, 
             const int64_t b = b0 + __ffsll((long long)m) - 1;
             const int64_t i = (b << kDueBlkBits) + lane;
             const int64_t d = i < nslots ? due[i] : INT64_MAX;
-            const bool h = d <= wm;
+            const bool h = i < nslots && d <= wm;  // (wm may be Long.MAX_VALUE: the padding is never due)
             if (h) hit(i);
             int64_t mn = h ? INT64_MAX : d;
             for (int o = 32; o > 0; o >>= 1) mn = min(mn, (int64_t)__shfl_xor(mn, o));
@@ -2312,6 +2317,7 @@ static int ingest_region(SessionState* s, int64_t n, const int64_t* key, const i
     uint32_t* ctot = col1 + ntiles * nd1;
     uint32_t* row2 = ctot + nd1;
     sb_opt_in();
+    static const int sb_exp = getenv("GW_SB_EXP") ? atoi(getenv("GW_SB_EXP")) : 0;
     if ((rc = zero_word_async(s, offsetof(DevStatus, overflow), err))) return rc;
     if ((rc = zero_word_async(s, offsetof(DevStatus, pad[0]), err))) return rc;
     if ((rc = zero_word_async(s, offsetof(DevStatus, pad[1]), err))) return rc;
@@ -2338,7 +2344,7 @@ static int ingest_region(SessionState* s, int64_t n, const int64_t* key, const i
     SCHECK(hipGetLastError());
 #define L(A)                                                                                                     \
     hipLaunchKernelGGL(k_sb_replay<A>, dim3((unsigned)(nd1 * nd2)), dim3(kSbRThreads), kSbReplayLds, s->stream, a, \
-                       bb2 ? row2 : row1, ctot, bb2 ? nd1 : 1, bb2 ? nch : ntiles, bb2 ? bb2 : bb1, lcap, sh)
+                       bb2 ? row2 : row1, ctot, bb2 ? nd1 : 1, bb2 ? nch : ntiles, bb2 ? bb2 : bb1, lcap, sh, sb_exp)
     GW_AGG_SWITCH(s->cfg.agg, L);
 #undef L
     SCHECK(hipGetLastError());
