@@ -1439,13 +1439,16 @@ constexpr uint32_t kK32Foreign = 0xfffffffeu;  // a slot holding a key no narrow
 constexpr int kNarMaxF = 4;
 constexpr int kNarMaxSlots = kNarMaxF * 2048;
 constexpr int kNarLoadU = 4;  // 16-B state loads per thread in flight together
+#ifndef GW_NAR_DEPTH
+#define GW_NAR_DEPTH 2  // record steps whose loads are in flight (2: one ahead of the applied one)
+#endif
 
 __device__ __forceinline__ uint32_t k32_of(int64_t k) {
     return k == kEmptyKey ? kK32Empty : ((uint64_t)k < (uint64_t)kK32Foreign ? (uint32_t)k : kK32Foreign);
 }
 
 template <int AGG>
-__global__ void __launch_bounds__(kApplyThreads) k_rgn_apply_nar(IngestArgs a) {
+__global__ void __launch_bounds__(kApplyThreads) GW_APPLY_ATTR k_rgn_apply_nar(IngestArgs a) {
     if constexpr (!cmp_agg<AGG>()) {
         return;
     } else {
@@ -1714,6 +1717,28 @@ __global__ void __launch_bounds__(kApplyThreads) k_rgn_apply_nar(IngestArgs a) {
                 uint32_t k = ~0u;
                 Grp g;
                 if (i0 < nr) load_grp(i0, g);
+#if GW_NAR_DEPTH == 3
+                // three step buffers in turn: two steps' loads in flight while one is applied
+                // (advance() keeps returning false once the runs are exhausted)
+                Step s0, s1, s2;
+                bool v0 = advance(i0, k, g);
+                load_step(g, k, s0, v0);
+                bool v1 = advance(i0, k, g);
+                load_step(g, k, s1, v1);
+                while (v0) {
+                    const bool v2 = advance(i0, k, g);
+                    load_step(g, k, s2, v2);
+                    apply_step(s0);
+                    if (!v1) break;
+                    v0 = advance(i0, k, g);
+                    load_step(g, k, s0, v0);
+                    apply_step(s1);
+                    if (!v2) break;
+                    v1 = advance(i0, k, g);
+                    load_step(g, k, s1, v1);
+                    apply_step(s2);
+                }
+#else
                 Step sa, sb;
                 bool live = advance(i0, k, g);
                 load_step(g, k, sa, live);
@@ -1726,6 +1751,7 @@ __global__ void __launch_bounds__(kApplyThreads) k_rgn_apply_nar(IngestArgs a) {
                     load_step(g, k, sa, live);
                     apply_step(sb);
                 }
+#endif
                 if (lane < qn) {  // the rest of the queue
                     const uint32_t k2 = qk[lane];
                     const int s2 = probe_insert(k2, slot_hash((int64_t)k2));

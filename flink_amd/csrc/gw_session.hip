@@ -565,13 +565,12 @@ constexpr int kSbWaveRecs = kSbTile / (kSbThreads / 64);
 constexpr int kSbMaxDigitBits = 8;
 constexpr int kSbMaxDigits = 1 << kSbMaxDigitBits;
 constexpr int kSbSinglePassBits = 6;      // buckets <= 2^6: P1 partitions by the whole bucket
-constexpr int kSbMeanBits = 11;            // ~2^11 records per bucket
-constexpr int kSbCap = 4096;               // records of a bucket the replay sorts in LDS
-constexpr int kSbPosBits = 12;
+constexpr int kSbMeanBits = 10;            // ~2^10 records per bucket (mean in (512, 1024])
+constexpr int kSbCap = 1024;               // records of a bucket the replay stages and sorts in LDS
+constexpr int kSbPosBits = 10;
 constexpr int kSbMaxHomeBits = 31 - kSbPosBits - 1;  // + the sentinel's code
 constexpr int kSbRThreads = 256;
-constexpr int kSbRItems = kSbCap / kSbRThreads;
-constexpr int kSbRWaveRecs = kSbCap / (kSbRThreads / 64);
+constexpr int kSbRItems = kSbCap / kSbRThreads;  // per thread per radix pass (at most)
 constexpr int kSbBins = 512;
 // P1/P2 LDS: key | ts | value staging, per-(wave, digit) counters, gather map (P2)
 constexpr size_t kSbPartLds = (size_t)kSbTile * 3 * 8 + (size_t)(kSbThreads / 64) * kSbMaxDigits * 2 + kSbTile * 4;
@@ -616,7 +615,8 @@ __device__ __forceinline__ void sb_chunk_starts(const uint32_t* ctot, int nc, ui
 template <bool GATHER>
 __global__ void __launch_bounds__(kSbThreads) k_sb_part(const int64_t* key, const int64_t* ts, const int64_t* val,
                                                         int64_t n, const int64_t* p_key, const longlong2* p_tv,
-                                                        const uint32_t* col, const uint32_t* ctot, int nc,
+                                                        const uint32_t* col, const uint32_t* cpre,
+                                                        const uint32_t* ctot, int nc,
                                                         int64_t ntiles, int lcap, int shift, int db, int64_t* o_key,
                                                         longlong2* o_tv, uint32_t* row, DevStatus* st) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -642,30 +642,37 @@ __global__ void __launch_bounds__(kSbThreads) k_sb_part(const int64_t* key, cons
         while (c + 1 < nc && cs[c + 1] <= (uint32_t)g) ++c;
         const uint32_t j0 = ((uint32_t)g - cs[c]) * kSbTile;
         cnt = (int)min((uint32_t)kSbTile, ctot[c] - j0);
-        // gather map: position q of this chunk -> its P1 buffer offset.  Tiles in order, a
-        // block of kSbThreads at a time; a thread writes its tile's part of [j0, j0 + cnt).
+        // gather map: position q of this chunk -> its P1 buffer offset.  The chunk's first tile
+        // t0 (the last with cpre <= j0) by a 64-ary search of wave 0 over the digit's prefix, then
+        // kSbThreads tiles at a time from there: a thread writes its tile's part of
+        // [j0, j0 + cnt).
         const uint32_t* cc = col + (int64_t)c * ntiles;
-        uint32_t running = 0;
-        for (int64_t t0 = 0; t0 < ntiles && running < j0 + (uint32_t)cnt; t0 += kSbThreads) {
-            const int64_t t = t0 + tid;
-            const uint32_t d = t < ntiles ? cc[t] : 0u;
-            const uint32_t x = d & 0xffffu;
-            uint32_t incl = x;
-            for (int o = 1; o < 64; o <<= 1) {
-                const uint32_t up = __shfl_up(incl, o);
-                if (lane >= o) incl += up;
+        const uint32_t* cp = cpre + (int64_t)c * ntiles;
+        __shared__ int64_t s_t0;
+        if (w == 0) {
+            int64_t lo = 0, len = ntiles;  // invariant: cp[lo] <= j0 (cp[0] == 0)
+            while (len > 1) {
+                const int64_t stride = (len + 63) / 64;
+                const int64_t t = lo + (int64_t)lane * stride;
+                const bool le = t < lo + len && cp[t] <= j0;
+                const uint64_t m = __ballot(le);
+                const int last = 63 - __clzll((long long)m);
+                lo += (int64_t)last * stride;
+                len = min(stride, len - (int64_t)last * stride);
             }
-            if (lane == 63) wsum[w] = incl;
-            __syncthreads();
-            uint32_t pre = running + incl - x, tot = 0;
-            for (int q = 0; q < kSbThreads / 64; ++q) {
-                if (q < w) pre += wsum[q];
-                tot += wsum[q];
+            if (lane == 0) s_t0 = lo;
+        }
+        __syncthreads();
+        const uint32_t j1 = j0 + (uint32_t)cnt;
+        for (int64_t tb = s_t0; tb < ntiles; tb += kSbThreads) {
+            const int64_t t = tb + tid;
+            if (t < ntiles) {
+                const uint32_t pre = cp[t];
+                const uint32_t d = cc[t];
+                const uint32_t a0 = max(pre, j0), a1 = min(pre + (d & 0xffffu), j1);
+                for (uint32_t u = a0; u < a1; ++u) gmap[u - j0] = (uint32_t)(t * kSbTile) + (d >> 16) + (u - pre);
             }
-            const uint32_t a0 = max(pre, j0), a1 = min(pre + x, j0 + (uint32_t)cnt);
-            for (uint32_t u = a0; u < a1; ++u) gmap[u - j0] = (uint32_t)(t * kSbTile) + (d >> 16) + (u - pre);
-            running += tot;
-            __syncthreads();  // wsum is rewritten by the next block
+            if (__syncthreads_or(t < ntiles && cp[t] + (cc[t] & 0xffffu) >= j1)) break;  // the chunk is covered
         }
         __syncthreads();
     }
@@ -784,6 +791,35 @@ __global__ void __launch_bounds__(256) k_sb_cols(const uint32_t* row, uint32_t* 
     }
 }
 
+// Per coarse digit (one workgroup each): exclusive prefix of its run lengths over the tiles,
+// pre[c][t] = records of digit c in tiles [0, t), so P2 finds its chunk's first tile by search.
+__global__ void __launch_bounds__(1024) k_sb_colscan(const uint32_t* col, uint32_t* pre, int64_t ntiles) {
+    __shared__ uint32_t wsum[16];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const uint32_t* cc = col + (int64_t)blockIdx.x * ntiles;
+    uint32_t* pp = pre + (int64_t)blockIdx.x * ntiles;
+    uint32_t run = 0;
+    for (int64_t t0 = 0; t0 < ntiles; t0 += 1024) {
+        const int64_t t = t0 + tid;
+        const uint32_t x = t < ntiles ? (cc[t] & 0xffffu) : 0u;
+        uint32_t incl = x;
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t up = __shfl_up(incl, o);
+            if (lane >= o) incl += up;
+        }
+        if (lane == 63) wsum[w] = incl;
+        __syncthreads();
+        uint32_t off = run, tot = 0;
+        for (int q = 0; q < 16; ++q) {
+            if (q < w) off += wsum[q];
+            tot += wsum[q];
+        }
+        if (t < ntiles) pp[t] = off + incl - x;
+        run += tot;
+        __syncthreads();
+    }
+}
+
 // Session words per slot: start, end, acc (+ count for averages).
 template <int AGG>
 __device__ __forceinline__ constexpr int sess_words() {
@@ -791,10 +827,12 @@ __device__ __forceinline__ constexpr int sess_words() {
 }
 
 // One stable LSD radix pass over x[0..n) -> y in LDS, digit = (v >> sh) & (2^db - 1),
-// db <= 9, kSbRThreads threads.  Wave w owns positions [w*kSbRWaveRecs, ...) (item it of
-// lane l at w*kSbRWaveRecs + it*64 + l), so (wave, item, lane) is the input order.
-__device__ __forceinline__ void sb_radix_pass(const uint32_t* x, uint32_t* y, int n, int sh, int db, uint16_t* wcnt,
-                                              uint32_t* wsum) {
+// db <= 9, kSbRThreads threads.  Wave w owns positions [w*q, (w+1)*q) (q: a multiple of 64
+// with 4q >= n, so the waves share the records evenly; item it of lane l at w*q + it*64 + l),
+// so (wave, item, lane) is the input order; lanes of one digit find each other with db
+// ballots, and a leader per digit bumps the wave's counter.
+__device__ __forceinline__ void sb_radix_pass(const uint32_t* x, uint32_t* y, int n, int q, int sh, int db,
+                                              uint16_t* wcnt, uint32_t* wsum) {
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int nbins = 1 << db;
     for (int e = tid; e < (kSbRThreads / 64) * kSbBins; e += blockDim.x) wcnt[e] = 0;
@@ -803,15 +841,16 @@ __device__ __forceinline__ void sb_radix_pass(const uint32_t* x, uint32_t* y, in
     uint32_t v[kSbRItems], rk[kSbRItems];
 #pragma unroll
     for (int it = 0; it < kSbRItems; ++it) {
-        const int pos = w * kSbRWaveRecs + it * 64 + lane;
-        const bool ok = pos < n;
+        const int pos = w * q + it * 64 + lane;
+        const bool ok = it * 64 < q && pos < n;
         v[it] = ok ? x[pos] : 0u;
         const uint32_t d = (v[it] >> sh) & (uint32_t)(nbins - 1);
         uint64_t peers = __ballot(ok);
-        if (!peers) { rk[it] = 0; continue; }  // wave-uniform
-        for (int q = 0; q < db; ++q) {
-            const uint64_t m = __ballot(ok && ((d >> q) & 1u));
-            peers &= ((d >> q) & 1u) ? m : ~m;
+        rk[it] = 0;
+        if (!peers) continue;  // wave-uniform
+        for (int b = 0; b < db; ++b) {
+            const uint64_t m = __ballot(ok && ((d >> b) & 1u));
+            peers &= ((d >> b) & 1u) ? m : ~m;
         }
         uint32_t old = 0;
         const int leader = ok ? __ffsll((long long)peers) - 1 : 0;
@@ -828,7 +867,7 @@ __device__ __forceinline__ void sb_radix_pass(const uint32_t* x, uint32_t* y, in
             const int d = d0 + tid;
             uint32_t tot = 0;
             if (d < nbins)
-                for (int q = 0; q < kSbRThreads / 64; ++q) tot += wcnt[q * kSbBins + d];
+                for (int qq = 0; qq < kSbRThreads / 64; ++qq) tot += wcnt[qq * kSbBins + d];
             uint32_t incl = tot;
             for (int o = 1; o < 64; o <<= 1) {
                 const uint32_t up = __shfl_up(incl, o);
@@ -837,15 +876,15 @@ __device__ __forceinline__ void sb_radix_pass(const uint32_t* x, uint32_t* y, in
             if (lane == 63) wsum[w] = incl;
             __syncthreads();
             uint32_t off = d0 ? wsum[kSbRThreads / 64] : 0u, all = off;
-            for (int q = 0; q < kSbRThreads / 64; ++q) {
-                if (q < w) off += wsum[q];
-                all += wsum[q];
+            for (int qq = 0; qq < kSbRThreads / 64; ++qq) {
+                if (qq < w) off += wsum[qq];
+                all += wsum[qq];
             }
             if (d < nbins) {
                 uint32_t r = off + incl - tot;
-                for (int q = 0; q < kSbRThreads / 64; ++q) {
-                    const uint32_t c = wcnt[q * kSbBins + d];
-                    wcnt[q * kSbBins + d] = (uint16_t)r;
+                for (int qq = 0; qq < kSbRThreads / 64; ++qq) {
+                    const uint32_t c = wcnt[qq * kSbBins + d];
+                    wcnt[qq * kSbBins + d] = (uint16_t)r;
                     r += c;
                 }
             }
@@ -856,8 +895,8 @@ __device__ __forceinline__ void sb_radix_pass(const uint32_t* x, uint32_t* y, in
     }
 #pragma unroll
     for (int it = 0; it < kSbRItems; ++it) {
-        const int pos = w * kSbRWaveRecs + it * 64 + lane;
-        if (pos < n) y[my[(v[it] >> sh) & (uint32_t)(nbins - 1)] + rk[it]] = v[it];
+        const int pos = w * q + it * 64 + lane;
+        if (it * 64 < q && pos < n) y[my[(v[it] >> sh) & (uint32_t)(nbins - 1)] + rk[it]] = v[it];
     }
     __syncthreads();
 }
@@ -898,17 +937,19 @@ __device__ __forceinline__ void sp_store(const SegArgs& a, const SessList& l, in
     }
 }
 
-// One key's records among the home slot's run [r0, f) of the sorted order (pr: pass-1
-// offsets; r0 holds one of them, the others are the run's records with this key), in
-// arrival order, against the key's slot -- seg_slot's replay, with the punt list instead of
-// the wide pass.
+// One key's records among the home slot's run [r0, f) of the sorted order (pr: the records'
+// positions in the bucket, rk / rtv: the bucket's keys and (timestamp, value) pairs staged in
+// LDS; r0 holds one of them, the others are the run's records with this key), in arrival
+// order, against the key's slot -- seg_slot's replay, with the punt list instead of the wide
+// pass.
 template <int AGG>
 __device__ __forceinline__ void sp_key(const SegArgs& a, const SessList& l, int64_t key, uint32_t r0, uint32_t f,
-                                       const uint32_t* pr, unsigned long long& late, unsigned long long& merges,
+                                       const uint32_t* pr, const int64_t* rk, const longlong2* rtv,
+                                       unsigned long long& late, unsigned long long& merges,
                                        unsigned long long& flags, unsigned long long& ins) {
     constexpr int SW = sess_words<AGG>();
     int64_t L = 0;
-    for (uint32_t q = r0; q < f; ++q) L += a.p_key[pr[q]] == key;
+    for (uint32_t q = r0; q < f; ++q) L += rk[pr[q]] == key;
     bool inserted;
     const int64_t slot = find_or_insert(a.t, key, inserted);
     int64_t* sp = slot >= 0 ? slot_ptr(a.t, slot) : nullptr;
@@ -927,8 +968,8 @@ __device__ __forceinline__ void sp_key(const SegArgs& a, const SessList& l, int6
         }
         for (uint32_t q = r0; q < f && ok; ++q) {
             const uint32_t o = pr[q];
-            if (a.p_key[o] != key) continue;
-            const longlong2 tv = a.p_tv[o];
+            if (rk[o] != key) continue;
+            const longlong2 tv = rtv[o];
             ok = add_element_tv<AGG>(a, l, cnt, kLaneSess, key, tv.x, tv.y, late, merges, flags, dry);
         }
         if (!ok || !dry || !effects) break;
@@ -942,8 +983,8 @@ __device__ __forceinline__ void sp_key(const SegArgs& a, const SessList& l, int6
         unsigned long long at = atomicAdd(&a.st->overflow, (unsigned long long)L);
         for (uint32_t q = r0; q < f; ++q) {
             const uint32_t o = pr[q];
-            if (a.p_key[o] != key) continue;
-            const longlong2 tv = a.p_tv[o];
+            if (rk[o] != key) continue;
+            const longlong2 tv = rtv[o];
             a.pu_key[at] = key;
             a.pu_ts[at] = tv.x;
             a.pu_val[at] = tv.y;
@@ -959,15 +1000,16 @@ __device__ __forceinline__ void sp_key(const SegArgs& a, const SessList& l, int6
 // slot are rare), through sp_key.
 template <int AGG>
 __device__ __forceinline__ void sp_run(const SegArgs& a, const SessList& l, uint32_t e, uint32_t f, const uint32_t* pr,
-                                       unsigned long long& late, unsigned long long& merges,
-                                       unsigned long long& flags, unsigned long long& ins) {
+                                       const int64_t* rk, const longlong2* rtv, unsigned long long& late,
+                                       unsigned long long& merges, unsigned long long& flags,
+                                       unsigned long long& ins) {
     for (uint32_t r = e; r < f;) {
-        sp_key<AGG>(a, l, a.p_key[pr[r]], r, f, pr, late, merges, flags, ins);
+        sp_key<AGG>(a, l, rk[pr[r]], r, f, pr, rk, rtv, late, merges, flags, ins);
         uint32_t nx = f;
         for (uint32_t q = r + 1; q < f && nx == f; ++q) {
-            const int64_t kq = a.p_key[pr[q]];
+            const int64_t kq = rk[pr[q]];
             bool seen = false;
-            for (uint32_t z = e; z < q && !seen; ++z) seen = a.p_key[pr[z]] == kq;
+            for (uint32_t z = e; z < q && !seen; ++z) seen = rk[pr[z]] == kq;
             if (!seen) nx = q;
         }
         r = nx;
@@ -977,26 +1019,29 @@ __device__ __forceinline__ void sp_run(const SegArgs& a, const SessList& l, uint
 // P3: one workgroup per bucket B = (coarse c, fine f).  The bucket's runs are desc[g * nf + f]
 // over the chunks g of coarse digit c ([cs[c], cs[c+1]) from the coarse totals; with P2
 // skipped, nc = 1 and the chunks are P1's tiles).  Concatenated in chunk order they are the
-// bucket's records in arrival order; the workgroup sorts them in LDS by (local home slot,
-// arrival) -- 32-bit keys (home << kSbPosBits | position), a stable radix sort over the home
-// bits -- and one thread per home slot replays the slot's run (sp_run: every key of the run
-// in order of its first record, usually one).  A bucket of more than kSbCap records punts
-// all of them (arrival order) to the sort path: its keys are disjoint from the other buckets'.
+// bucket's records in arrival order.  The workgroup stages the records in LDS (keys and
+// (timestamp, value) pairs, read coalesced from the runs), sorts the positions by (local home
+// slot, arrival) -- 32-bit keys (home << kSbPosBits | position), a stable radix sort over the
+// home bits -- and one thread per home slot replays the slot's run from LDS (sp_run: every
+// key of the run in order of its first record, usually one): its only global accesses are the
+// key's probe, its slot line and due time.  A bucket of more than kSbCap records punts all
+// of them (arrival order) to the sort path: its keys are disjoint from the other buckets'.
 template <int AGG>
 __global__ void __launch_bounds__(kSbRThreads) k_sb_replay(SegArgs a, const uint32_t* desc, const uint32_t* ctot,
                                                            int nc, int64_t nchunks, int bf, int lcap, int sh,
                                                            int exp) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    uint32_t* ka = reinterpret_cast<uint32_t*>(smem);  // sort keys | radix double buffer
+    longlong2* rtv = reinterpret_cast<longlong2*>(smem);       // [kSbCap] (timestamp, value) by position
+    int64_t* rk = reinterpret_cast<int64_t*>(rtv + kSbCap);     // [kSbCap] key by position
+    uint32_t* ka = reinterpret_cast<uint32_t*>(rk + kSbCap);    // sort keys | radix double buffer
     uint32_t* kb = ka + kSbCap;
-    uint32_t* src = kb + kSbCap;                         // position -> buffer offset, then the order
-    uint32_t* hd = src + kSbCap;                         // run starts (gather), then the heads
-    int64_t* lanes = reinterpret_cast<int64_t*>(smem);  // session lanes (replay; alias ka | kb)
-    uint16_t* wcnt = reinterpret_cast<uint16_t*>(hd);   // radix counters (sort; alias the heads)
+    uint32_t* hd = kb + kSbCap;                                 // run starts (gather), then the heads
+    uint16_t* wcnt = reinterpret_cast<uint16_t*>(hd + kSbCap);  // radix counters
+    int64_t* lanes = reinterpret_cast<int64_t*>(wcnt + (kSbRThreads / 64) * kSbBins);  // session lanes
     __shared__ uint32_t wsum[kSbRThreads / 64 + 1];
     __shared__ uint32_t cs[kSbMaxDigits + 1];
     __shared__ uint32_t cpre[kSbRThreads + 1];
-    __shared__ uint32_t s_n, s_pb, s_nh;
+    __shared__ uint32_t s_n, s_pb;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int nf = 1 << bf;
     const int64_t B = blockIdx.x;
@@ -1028,7 +1073,7 @@ __global__ void __launch_bounds__(kSbRThreads) k_sb_replay(SegArgs a, const uint
     const bool over = n > (uint32_t)kSbCap;
     const uint32_t pbase = s_pb;
     // the runs in chunk order, kSbRThreads chunks at a time: a scan of their counts, then the
-    // block fills positions [run0, run0 + tot) cooperatively (coalesced within runs)
+    // block loads positions [run0, run0 + tot) cooperatively (coalesced within runs)
     uint32_t run0 = 0;
     for (int64_t b0 = g0; b0 < g1; b0 += kSbRThreads) {
         const int64_t g = b0 + tid;
@@ -1059,54 +1104,44 @@ __global__ void __launch_bounds__(kSbRThreads) k_sb_replay(SegArgs a, const uint
             const uint32_t o = hd[lo] + (u - cpre[lo]);
             const uint32_t pos = run0 + u;
             const int64_t kk = a.p_key[o];
+            const longlong2 tv = a.p_tv[o];
             if (over) {
-                const longlong2 tv = a.p_tv[o];
                 a.pu_key[pbase + pos] = kk;
                 a.pu_ts[pbase + pos] = tv.x;
                 a.pu_val[pbase + pos] = tv.y;
             } else {
                 const uint32_t lh = kk == kEmptyKey ? sent : (uint32_t)(sb_home(kk, lcap) & hmask);
                 ka[pos] = (lh << kSbPosBits) | pos;
-                src[pos] = o;
+                rk[pos] = kk;
+                rtv[pos] = tv;
             }
         }
         run0 += tot;
-        __syncthreads();  // cpre / the scratch tail are rewritten by the next block
+        __syncthreads();  // cpre / the run starts are rewritten by the next block
     }
     if (over || exp == 2) {  // (exp: GW_SB_EXP timing variants, results invalid: 2 = gather only)
         block_commit(a.st, 0, 0, 0, 0);
         return;
     }
-    // home bits [kSbPosBits, kSbPosBits + sh + 1): passes of <= 9 bits
+    // home bits [kSbPosBits, kSbPosBits + sh + 1): passes of <= 9 bits, the waves sharing
+    // the records evenly
+    const int q = (int)(((n + 4 * 64 - 1) / (4 * 64)) * 64);
     const int hb = sh + 1;
     const int np = (hb + 8) / 9;
     const uint32_t* fin = ka;
     uint32_t* fin_o = kb;
     for (int p = 0, done = 0; p < np; ++p) {
         const int db = (hb - done + (np - p) - 1) / (np - p);
-        sb_radix_pass(fin, fin_o, (int)n, kSbPosBits + done, db, wcnt, wsum);
+        sb_radix_pass(fin, fin_o, (int)n, q, kSbPosBits + done, db, wcnt, wsum);
         done += db;
         uint32_t* t = const_cast<uint32_t*>(fin);
         fin = fin_o;
         fin_o = t;
     }
-    // fin: the sorted keys; the order (buffer offsets in sorted order) replaces src in place
+    // the order (positions in sorted order) in fin_o (free after the last pass), the heads in hd
     constexpr uint32_t pm = (1u << kSbPosBits) - 1u;
-    {
-        uint32_t o[kSbRItems];
-#pragma unroll
-        for (int it = 0; it < kSbRItems; ++it) {
-            const uint32_t i = it * kSbRThreads + tid;
-            o[it] = i < n ? src[fin[i] & pm] : 0u;
-        }
-        __syncthreads();
-#pragma unroll
-        for (int it = 0; it < kSbRItems; ++it) {
-            const uint32_t i = it * kSbRThreads + tid;
-            if (i < n) src[i] = o[it];
-        }
-    }
-    const uint32_t* pr = src;
+    uint32_t* pr = fin_o;
+    for (uint32_t i = tid; i < n; i += kSbRThreads) pr[i] = fin[i] & pm;
     uint32_t nh = 0;  // heads: sorted index of each home slot's first record
     for (uint32_t i0 = 0; i0 < n; i0 += kSbRThreads) {
         const uint32_t i = i0 + tid;
@@ -1115,31 +1150,31 @@ __global__ void __launch_bounds__(kSbRThreads) k_sb_replay(SegArgs a, const uint
         if (lane == 0) wsum[w] = (uint32_t)__popcll(bal);
         __syncthreads();
         uint32_t base = nh, tot = 0;
-        for (int q = 0; q < kSbRThreads / 64; ++q) {
-            if (q < w) base += wsum[q];
-            tot += wsum[q];
+        for (int qq = 0; qq < kSbRThreads / 64; ++qq) {
+            if (qq < w) base += wsum[qq];
+            tot += wsum[qq];
         }
         if (h) hd[base + __popcll(bal & ((1ull << lane) - 1ull))] = i;
         nh += tot;
-        __syncthreads();  // wsum is rewritten by the next chunk (and fin by the lanes)
+        __syncthreads();  // wsum is rewritten by the next chunk
     }
     if (exp == 1) {  // gather + sort + heads only
         block_commit(a.st, 0, 0, 0, 0);
         return;
     }
-    // replay: one thread per home slot's run
+    // replay: one thread per home slot's run, records from LDS
     const SessList l{lanes + tid, kLaneSess * kSbRThreads, kSbRThreads};
     unsigned long long late = 0, merges = 0, flags = 0, ins = 0;
     for (uint32_t j = tid; j < nh; j += kSbRThreads) {
         const uint32_t e = hd[j], fe = j + 1 < nh ? hd[j + 1] : n;
-        sp_run<AGG>(a, l, e, fe, pr, late, merges, flags, ins);
+        sp_run<AGG>(a, l, e, fe, pr, rk, rtv, late, merges, flags, ins);
     }
     block_commit(a.st, late, ins, flags, 0, 0, merges);
 }
-// P3 LDS: sort keys and radix buffer (then the session lanes), offsets / order, heads
-constexpr size_t kSbReplayLds = (size_t)kSbCap * 4 * 4;
-static_assert((size_t)5 * kLaneSess * kSbRThreads * 8 <= (size_t)kSbCap * 4 * 2, "the lanes alias the sort buffers");
-static_assert((size_t)(kSbRThreads / 64) * kSbBins * 2 <= (size_t)kSbCap * 4, "radix counters alias the heads");
+// P3 LDS: records (24 B), sort keys and radix buffer, heads (3 x 4 B) per position; radix
+// counters; the session lanes
+constexpr size_t kSbReplayLds = (size_t)kSbCap * (24 + 12) + (size_t)(kSbRThreads / 64) * kSbBins * 2 +
+                                (size_t)5 * kLaneSess * kSbRThreads * 8;
 
 // After a replay with punts: clear the punt marks before the sort path replays the list.
 __global__ void __launch_bounds__(256) k_sp_unpunt(TableView t, const int64_t* pk, int64_t n) {
@@ -2285,8 +2320,8 @@ static int ingest_region(SessionState* s, int64_t n, const int64_t* key, const i
     const int64_t ntiles = (n + kSbTile - 1) / kSbTile;
     const int64_t nch = bb2 ? ntiles + nd1 : 0;  // P2 chunks: an upper bound
     const int64_t recs = (ntiles + nch) * kSbTile;
-    // descriptors: P1 rows + columns, coarse totals, P2 rows
-    const int64_t dwords = 2 * ntiles * nd1 + nd1 + nch * nd2;
+    // descriptors: P1 rows + columns + column prefixes, coarse totals, P2 rows
+    const int64_t dwords = 3 * ntiles * nd1 + nd1 + nch * nd2;
     if ((ntiles + nd1) * kSbTile > s->sb_cap || dwords > s->sb_desc_cap) {
         SCHECK(hipStreamSynchronize(s->stream));
         if ((ntiles + nd1) * kSbTile > s->sb_cap) {
@@ -2314,7 +2349,8 @@ static int ingest_region(SessionState* s, int64_t n, const int64_t* key, const i
     longlong2* tv2 = reinterpret_cast<longlong2*>(k2 + C);
     uint32_t* row1 = s->sb_desc;
     uint32_t* col1 = row1 + ntiles * nd1;
-    uint32_t* ctot = col1 + ntiles * nd1;
+    uint32_t* cpre1 = col1 + ntiles * nd1;
+    uint32_t* ctot = cpre1 + ntiles * nd1;
     uint32_t* row2 = ctot + nd1;
     sb_opt_in();
     static const int sb_exp = getenv("GW_SB_EXP") ? atoi(getenv("GW_SB_EXP")) : 0;
@@ -2322,7 +2358,8 @@ static int ingest_region(SessionState* s, int64_t n, const int64_t* key, const i
     if ((rc = zero_word_async(s, offsetof(DevStatus, pad[0]), err))) return rc;
     if ((rc = zero_word_async(s, offsetof(DevStatus, pad[1]), err))) return rc;
     hipLaunchKernelGGL(k_sb_part<false>, dim3((unsigned)ntiles), dim3(kSbThreads), kSbPartLds, s->stream, key, ts, val,
-                       n, nullptr, nullptr, nullptr, nullptr, 0, ntiles, lcap, sh + bb2, bb1, k1, tv1, row1, s->d_st);
+                       n, nullptr, nullptr, nullptr, nullptr, nullptr, 0, ntiles, lcap, sh + bb2, bb1, k1, tv1, row1,
+                       s->d_st);
     SegArgs a{};
     if ((rc = seg_common(s, a, n, wm, err))) return rc;
     a.pu_key = s->pu_col3;
@@ -2332,8 +2369,9 @@ static int ingest_region(SessionState* s, int64_t n, const int64_t* key, const i
         SCHECK(hipMemsetAsync(ctot, 0, (size_t)nd1 * 4, s->stream));
         hipLaunchKernelGGL(k_sb_cols, dim3((unsigned)((ntiles + 63) / 64), (unsigned)((nd1 + 63) / 64)), dim3(256), 0,
                            s->stream, row1, col1, ctot, ntiles, nd1);
+        hipLaunchKernelGGL(k_sb_colscan, dim3((unsigned)nd1), dim3(1024), 0, s->stream, col1, cpre1, ntiles);
         hipLaunchKernelGGL(k_sb_part<true>, dim3((unsigned)nch), dim3(kSbThreads), kSbPartLds, s->stream, nullptr,
-                           nullptr, nullptr, n, k1, tv1, col1, ctot, nd1, ntiles, lcap, sh, bb2, k2, tv2, row2,
+                           nullptr, nullptr, n, k1, tv1, col1, cpre1, ctot, nd1, ntiles, lcap, sh, bb2, k2, tv2, row2,
                            s->d_st);
         a.p_key = k2;
         a.p_tv = tv2;
@@ -2378,11 +2416,13 @@ static int sb_finish(SessionState* s, std::string& err) {
 }
 
 // GW_SESSION_PATH=region|sort picks the ingest path (GW_SESSION_SORT_BITS, the sort path's
-// group tests, implies sort).
+// group tests, implies sort).  The sort path is the default: on the sessions config the
+// bucketed path measured slower (its per-bucket replay is latency-bound).
+constexpr bool kSessionBucketedDefault = false;
 static bool region_ingest_enabled() {
     const char* p = getenv("GW_SESSION_PATH");
     if (p) return strcmp(p, "sort") != 0;
-    return getenv("GW_SESSION_SORT_BITS") == nullptr;
+    return getenv("GW_SESSION_SORT_BITS") == nullptr && kSessionBucketedDefault;
 }
 
 int session_ingest(SessionState* s, int64_t n, const int64_t* key, const int64_t* ts, const int64_t* val, int64_t wm,

@@ -1,5 +1,5 @@
 """Bucketed session ingest (gw_session.hip k_sb_part P1 / k_sb_cols / k_sb_part P2 /
-k_sb_replay), the default session path, against the oracle:
+k_sb_replay; GW_SESSION_PATH=region, opt-in: the sort path is the default) against the oracle:
 
 * buckets holding many records of a batch (a small table under large batches: hundreds to
   thousands of records per bucket, so the LDS radix sort, the ordered head list and runs of
@@ -7,7 +7,7 @@ k_sb_replay), the default session path, against the oracle:
   the second partition pass (P2 runs when a batch needs more than 2^6 buckets);
 * a large table under a small batch (the bucket count set by the sort key's home-bit limit);
 * home slots shared by several keys (more keys than home slots in a bucket);
-* a hot key whose bucket exceeds kSbCap (4096) records in one batch: the bucket goes to the
+* a hot key whose bucket exceeds kSbCap (1024) records in one batch: the bucket goes to the
   punt list and the sort path replays it (stats()["session_punted"] counts it);
 * keys that need the wide table mid-batch (more sessions than the lane holds), under allowed
   lateness and the late side output too;
@@ -123,11 +123,12 @@ def test_sentinel_key_and_shared_home_slots(oracle_lib):
 
 
 def test_f64_sessions_take_no_punts(oracle_lib):
-    """Keys that never hold two sessions at once (records ~300 ms apart, gap 5 s) never leave the
-    region path.  (A key with more sessions in flight than its slot holds -- one for averages --
-    lives in the wide table from then on, and its records take the sort path.)"""
-    kw = dict(assigner="session", gap=5000, agg="avg_f64")
-    keys, ts, vals, batches = random_stream(seed=13, n=80_000, num_keys=300, n_batches=5, ts_step=1,
+    """Keys that never hold two sessions at once (records ~3 s apart, gap 60 s) never leave the
+    bucketed path.  (A key with more sessions in flight than its slot holds -- one for averages --
+    lives in the wide table from then on, and its records take the sort path; so does every
+    key of a bucket beyond kSbCap records, which enough keys per bucket keep away.)"""
+    kw = dict(assigner="session", gap=60_000, agg="avg_f64")
+    keys, ts, vals, batches = random_stream(seed=13, n=80_000, num_keys=3000, n_batches=5, ts_step=1,
                                             disorder=300, wm_lag=300, agg="avg_f64")
     g1, _, s1 = run_gpu(kw, keys, ts, vals, batches, capacity_hint=4096)
     o, _ = run_oracle(oracle_lib, kw, keys, ts, vals, batches)
