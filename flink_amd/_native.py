@@ -52,7 +52,7 @@ EXPORTS = [
     "gw_decode_serialized", "gw_ingest_serialized", "gw_ingest_serialized_device",
     "gw_exchange_unique_id", "gw_exchange_create", "gw_exchange_destroy", "gw_exchange_batch",
     "gw_exchange_min_watermark", "gw_exchange_last_error", "gw_exchange_counts", "gw_exchange_plan",
-    "gw_window_stagger_offset", "gw_stage_alloc", "gw_stage_columns", "gw_ingest_stage",
+    "gw_window_stagger_offset", "gw_stage_alloc", "gw_stage_columns", "gw_ingest_stage", "gw_stage_send",
     "gw_ingest_payload", "gw_ingest_payload_device", "gw_drain_payload",
     "gw_snapshot_keys", "gw_snapshot_remap_keys", "gw_snapshot_payloads", "gw_snapshot_remap_payloads",
 ]
@@ -192,6 +192,7 @@ def lib() -> ctypes.CDLL:
         "gw_stage_alloc": (c_int, [p, i32, i64]),
         "gw_stage_columns": (c_int, [p, i32, ctypes.POINTER(p), ctypes.POINTER(p), ctypes.POINTER(p), ctypes.POINTER(p)]),
         "gw_ingest_stage": (c_int, [p, i32, i64, i32]),
+        "gw_stage_send": (c_int, [p, i32, i64, i32]),
         "gw_exchange_min_watermark": (c_int, [p, i64, P64, p]),
         "gw_exchange_last_error": (ctypes.c_char_p, [p]),
     }

@@ -321,7 +321,13 @@ struct gw_handle {
     int64_t* d_stage2[2] = {nullptr, nullptr};
     hipEvent_t ev_dread[2] = {nullptr, nullptr};
     bool dread_valid[2] = {false, false};
-    int dturn = 0;
+    int dturn = 0;                  // the device buffer the next staged ingest reads
+    int send_turn = 0;              // the device buffer the next H2D fills
+    // a slot already sent ahead (gw_stage_send) into device buffer t, not yet ingested
+    bool pre_valid[2] = {false, false};
+    int pre_slot[2] = {-1, -1};
+    int64_t pre_n[2] = {0, 0};
+    int pre_cols[2] = {0, 0};
     hipStream_t cstream = nullptr;
 
     // output rows (device SoA), [rows_head, st.rows) pending
@@ -622,7 +628,9 @@ struct gw_handle {
             if (d_stage2[t]) hipFree(d_stage2[t]);
             d_stage2[t] = nullptr;
             dread_valid[t] = false;
+            pre_valid[t] = false;
         }
+        dturn = send_turn = 0;
         slot_cap = 0;
     }
     // `slots` pinned slots of >= n records each (and the two device buffers of that size).
@@ -652,9 +660,20 @@ struct gw_handle {
     int64_t* h_bounce = nullptr;
     hipEvent_t ev_bounce[2] = {nullptr, nullptr};
     static constexpr int64_t kBounceRows = (int64_t)1 << 21;  // per chunk and column (16 MB)
+    static bool host_pinned(const void* p) {
+        hipPointerAttribute_t at;
+        if (!p || hipPointerGetAttributes(&at, p) != hipSuccess) {
+            (void)hipGetLastError();  // pageable memory reports an error: clear it
+            return false;
+        }
+        return at.type == hipMemoryTypeHost;
+    }
     int drain_to_host(int64_t* const dst[4], const int64_t* const src[4], int64_t c) {
         static const bool direct = [] { const char* v = getenv("GW_DRAIN_BOUNCE"); return v && atoi(v) == 0; }();
-        if (direct || c < kBounceRows / 4) {
+        bool pinned = true;  // pinned destinations (page-locked: hipHostMalloc / registered) take the D2H directly
+        for (int i = 0; i < 4 && pinned; ++i)
+            if (dst[i]) pinned = host_pinned(dst[i]);
+        if (direct || pinned || c < kBounceRows / 4) {
             hipError_t err = hipSuccess;
             for (int i = 0; i < 4 && err == hipSuccess; ++i)
                 if (dst[i]) err = hipMemcpyAsync(dst[i], src[i], c * 8, hipMemcpyDeviceToHost, stream);
@@ -2824,27 +2843,51 @@ int gw_ingest(gw_handle* h, int64_t n, const int64_t* key, const int32_t* key_ha
     return GW_OK;
 }
 
-// One filled pinned slot -> device (copy stream) -> ingest (the handle's stream).
-static int stage_ingest(gw_handle* h, int slot, int64_t n, bool with_hash, bool with_value) {
-    const int t = h->dturn;
-    h->dturn ^= 1;
+// One filled pinned slot -> the next device staging buffer, on the copy stream (after the
+// ingest that last read that buffer).  cols: GW_STAGE_VALUE | GW_STAGE_KEY_HASH.
+static int stage_send(gw_handle* h, int slot, int64_t n, int cols) {
+    const int t = h->send_turn;
+    if (h->pre_valid[t]) return h->fail(GW_E_STATE, "staging: both device buffers hold batches not yet ingested");
     const int64_t cap = h->slot_cap;
     int64_t* hs = h->h_slot[slot];
     int64_t* ds = h->d_stage2[t];
-    int32_t* dh = (int32_t*)(ds + 3 * cap);
     hipError_t e = hipSuccess;
     if (h->dread_valid[t]) e = hipStreamWaitEvent(h->cstream, h->ev_dread[t], 0);
     if (e == hipSuccess) e = hipMemcpyAsync(ds, hs, (size_t)n * 8, hipMemcpyHostToDevice, h->cstream);
     if (e == hipSuccess) e = hipMemcpyAsync(ds + cap, hs + cap, (size_t)n * 8, hipMemcpyHostToDevice, h->cstream);
-    if (e == hipSuccess && with_value)
+    if (e == hipSuccess && (cols & GW_STAGE_VALUE))
         e = hipMemcpyAsync(ds + 2 * cap, hs + 2 * cap, (size_t)n * 8, hipMemcpyHostToDevice, h->cstream);
-    if (e == hipSuccess && with_hash)
-        e = hipMemcpyAsync(dh, hs + 3 * cap, (size_t)n * 4, hipMemcpyHostToDevice, h->cstream);
+    if (e == hipSuccess && (cols & GW_STAGE_KEY_HASH))
+        e = hipMemcpyAsync(ds + 3 * cap, hs + 3 * cap, (size_t)n * 4, hipMemcpyHostToDevice, h->cstream);
     if (e == hipSuccess) e = hipEventRecord(h->ev_slot[slot], h->cstream);
-    if (e == hipSuccess) e = hipStreamWaitEvent(h->stream, h->ev_slot[slot], 0);
     if (e != hipSuccess) return h->fail(GW_E_DEVICE, "H2D: %s", hipGetErrorString(e));
     h->slot_used[slot] = true;
-    int rc = h->check_keys(n, ds, with_hash ? dh : nullptr);
+    h->pre_valid[t] = true;
+    h->pre_slot[t] = slot;
+    h->pre_n[t] = n;
+    h->pre_cols[t] = cols;
+    h->send_turn ^= 1;
+    return GW_OK;
+}
+
+// A staged batch -> ingest (the handle's stream): the slot sent ahead, or sent now.
+static int stage_ingest(gw_handle* h, int slot, int64_t n, bool with_hash, bool with_value) {
+    const int cols = (with_value ? GW_STAGE_VALUE : 0) | (with_hash ? GW_STAGE_KEY_HASH : 0);
+    const int t = h->dturn;
+    int rc;
+    if (!h->pre_valid[t]) {
+        if ((rc = stage_send(h, slot, n, cols))) return rc;
+    } else if (h->pre_slot[t] != slot || h->pre_n[t] != n || h->pre_cols[t] != cols) {
+        return h->fail(GW_E_STATE, "staging: ingest of slot %d (%lld records) while slot %d (%lld) was sent first",
+                       slot, (long long)n, h->pre_slot[t], (long long)h->pre_n[t]);
+    }
+    h->pre_valid[t] = false;
+    h->dturn ^= 1;
+    const int64_t cap = h->slot_cap;
+    int64_t* ds = h->d_stage2[t];
+    int32_t* dh = (int32_t*)(ds + 3 * cap);
+    if (hipStreamWaitEvent(h->stream, h->ev_slot[slot], 0) != hipSuccess) return h->fail(GW_E_DEVICE, "staging event");
+    rc = h->check_keys(n, ds, with_hash ? dh : nullptr);
     if (rc == GW_OK) rc = ingest_device_impl(h, n, ds, ds + cap, with_value ? ds + 2 * cap : nullptr);
     if (hipEventRecord(h->ev_dread[t], h->stream) != hipSuccess) return h->fail(GW_E_DEVICE, "staging event");
     h->dread_valid[t] = true;
@@ -2869,6 +2912,15 @@ int gw_stage_columns(gw_handle* h, int32_t slot, int64_t** key, int32_t** key_ha
     if (value) *value = hs + 2 * h->slot_cap;
     if (key_hash) *key_hash = (int32_t*)(hs + 3 * h->slot_cap);
     return GW_OK;
+}
+
+int gw_stage_send(gw_handle* h, int32_t slot, int64_t n, int32_t cols) {
+    if (!h || slot < 0 || slot >= (int)h->h_slot.size() || n < 0 || n > h->slot_cap) return GW_E_INVALID;
+    if (h->failed) return h->fail(GW_E_STATE, "operator failed earlier: %s", h->err.c_str());
+    if (n > 0 && !(cols & GW_STAGE_VALUE) && h->cfg.agg != GW_COUNT) return h->fail(GW_E_INVALID, "value column required");
+    hipSetDevice(h->cfg.device);
+    if (n == 0) return GW_OK;
+    return stage_send(h, slot, n, cols & (GW_STAGE_VALUE | GW_STAGE_KEY_HASH));
 }
 
 int gw_ingest_stage(gw_handle* h, int32_t slot, int64_t n, int32_t cols) {

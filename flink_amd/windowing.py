@@ -559,6 +559,12 @@ class GpuWindowOperator:
         cols = (N.STAGE_VALUE if with_value else 0) | (N.STAGE_KEY_HASH if with_key_hash else 0)
         N.check(N.lib().gw_ingest_stage(self._h, int(slot), int(n), cols), self._h)
 
+    def stage_send(self, slot: int, n: int, with_value: bool = True, with_key_hash: bool = False):
+        """Send the slot's first n records over PCIe ahead of their gw_ingest_stage (gw_stage_send):
+        at most one batch ahead; the next ingest_stage must name this slot."""
+        cols = (N.STAGE_VALUE if with_value else 0) | (N.STAGE_KEY_HASH if with_key_hash else 0)
+        N.check(N.lib().gw_stage_send(self._h, int(slot), int(n), cols), self._h)
+
     def process_batch_device(self, keys, timestamps, values=None, stream=None):
         """Columns already in HBM (torch tensors or raw device pointers)."""
         self._ensure_handle()
@@ -657,13 +663,20 @@ class GpuWindowOperator:
         N.check(N.lib().gw_pending_rows(self._h, ctypes.byref(n)), self._h)
         return n.value
 
-    def drain(self):
-        """All pending fired rows as numpy (key, start, end, result) columns."""
+    def drain(self, out=None):
+        """All pending fired rows as numpy (key, start, end, result) columns.  `out`: four int64
+        numpy arrays to fill (e.g. over pinned memory, which the D2H then writes directly);
+        views of their first n entries are returned."""
         n = self.pending_rows()
-        k = np.empty(n, np.int64)
-        s = np.empty(n, np.int64)
-        e = np.empty(n, np.int64)
-        r = np.empty(n, np.int64)
+        if out is not None:
+            if any(len(x) < n for x in out):
+                raise ValueError(f"drain: out arrays hold fewer than the {n} pending rows")
+            k, s, e, r = (x[:n] for x in out)
+        else:
+            k = np.empty(n, np.int64)
+            s = np.empty(n, np.int64)
+            e = np.empty(n, np.int64)
+            r = np.empty(n, np.int64)
         got = ctypes.c_int64(0)
         if n:
             rc = N.lib().gw_drain(self._h, _ptr(k), _ptr(s), _ptr(e), _ptr(r), n, ctypes.byref(got))

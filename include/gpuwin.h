@@ -198,6 +198,11 @@ int  gw_stage_alloc(gw_handle* h, int32_t slots, int64_t cap);
 int  gw_stage_columns(gw_handle* h, int32_t slot, int64_t** key, int32_t** key_hash, int64_t** ts,
                       int64_t** value);
 int  gw_ingest_stage(gw_handle* h, int32_t slot, int64_t n, int32_t cols);
+/* Send a filled slot's first n records over PCIe ahead of its gw_ingest_stage (into the next of
+ * the two device buffers, once the ingest that last read it is done), e.g. batch b+1's while
+ * batch b's rows are drained.  At most one batch ahead: the next gw_ingest_stage must name the
+ * same slot, n and cols (GW_E_STATE otherwise). */
+int  gw_stage_send(gw_handle* h, int32_t slot, int64_t n, int32_t cols);
 /* Same, with the columns already resident in device memory (d_* are device
  * pointers).  `stream` is the hipStream_t the inputs were produced on (NULL = the
  * default stream).  The handle's stream (gw_stream) reads them after that stream's

@@ -85,6 +85,12 @@ JNIEXPORT void JNICALL CLS(nativeIngestStage)(JNIEnv* env, jclass c, jlong h, ji
     fail(env, g, gw_ingest_stage(g, slot, n, cols));
 }
 
+/* A complete slot sent over PCIe ahead of its nativeIngestStage (gw_stage_send). */
+JNIEXPORT void JNICALL CLS(nativeStageSend)(JNIEnv* env, jclass c, jlong h, jint slot, jint n, jint cols) {
+    gw_handle* g = (gw_handle*)(intptr_t)h;
+    fail(env, g, gw_stage_send(g, slot, n, cols));
+}
+
 /* Network-buffer ingest: `bytes` is a direct ByteBuffer holding one input channel's
  * serialized elements (the payload of its network buffers, in order); `types` the Tuple's
  * field type codes ("JJ" for Tuple2<Long, Long>).  Returns the bytes consumed; the caller
