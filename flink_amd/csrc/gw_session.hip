@@ -91,6 +91,7 @@ struct SegArgs {
     // bucketed ingest (k_sb_part / k_sb_replay)
     const int64_t* p_key;   // the bucket records (P2's buffer, or P1's without P2): keys
     const longlong2* p_tv;  //   and (timestamp, value) pairs
+    int diag;               // GW_SB_EXP=3: count punts by reason (ShardCtr pad words of shards 2 and 3)
     int64_t* pu_key;        // punted records (arrival order per key), append at st->overflow
     int64_t* pu_ts;
     int64_t* pu_val;
@@ -980,6 +981,10 @@ __device__ __forceinline__ void sp_key(const SegArgs& a, const SessList& l, int6
     if (!ok) {  // punt the key's records of the batch (kPuntMeta: also any that come after)
         late = l0;
         merges = m0;
+        if (a.diag) {  // GW_SB_EXP=3: punts by reason (no slot, wide / punted key, lane outgrown)
+            ShardCtr& sc = a.st->sh[2];
+            atomicAdd(!sp ? &sc.pad0 : ((uint64_t)w1 & (kBigMeta | kPuntMeta)) ? &sc.pad1 : &a.st->sh[3].pad0, (unsigned long long)L);
+        }
         unsigned long long at = atomicAdd(&a.st->overflow, (unsigned long long)L);
         for (uint32_t q = r0; q < f; ++q) {
             const uint32_t o = pr[q];
@@ -1119,6 +1124,7 @@ __global__ void __launch_bounds__(kSbRThreads) k_sb_replay(SegArgs a, const uint
         run0 += tot;
         __syncthreads();  // cpre / the run starts are rewritten by the next block
     }
+    if (over && exp == 3 && tid == 0) atomicAdd(&a.st->sh[3].pad1, (unsigned long long)n);
     if (over || exp == 2) {  // (exp: GW_SB_EXP timing variants, results invalid: 2 = gather only)
         block_commit(a.st, 0, 0, 0, 0);
         return;
@@ -1158,7 +1164,7 @@ __global__ void __launch_bounds__(kSbRThreads) k_sb_replay(SegArgs a, const uint
         nh += tot;
         __syncthreads();  // wsum is rewritten by the next chunk
     }
-    if (exp == 1) {  // gather + sort + heads only
+    if (exp == 1) {  // gather + sort + heads only (3: punt diagnostics, results valid)
         block_commit(a.st, 0, 0, 0, 0);
         return;
     }
@@ -2362,6 +2368,7 @@ static int ingest_region(SessionState* s, int64_t n, const int64_t* key, const i
                        s->d_st);
     SegArgs a{};
     if ((rc = seg_common(s, a, n, wm, err))) return rc;
+    a.diag = sb_exp == 3;
     a.pu_key = s->pu_col3;
     a.pu_ts = s->pu_col3 + C;
     a.pu_val = s->pu_col3 + 2 * C;
@@ -2386,6 +2393,19 @@ static int ingest_region(SessionState* s, int64_t n, const int64_t* key, const i
     GW_AGG_SWITCH(s->cfg.agg, L);
 #undef L
     SCHECK(hipGetLastError());
+    if (sb_exp == 3) {
+        SCHECK(hipStreamSynchronize(s->stream));
+        DevStatus d;
+        SCHECK(hipMemcpy(&d, s->d_st, sizeof d, hipMemcpyDeviceToHost));
+        fprintf(stderr, "[sb] n %lld buckets %d (bb %d = %d + %d, sh %d): punted %llu: no slot %llu, wide/punted key %llu, "
+                        "lane %llu, over-cap buckets %llu\n",
+                (long long)n, nd1 * nd2, bb, bb1, bb2, sh, (unsigned long long)d.overflow, d.sh[2].pad0, d.sh[2].pad1,
+                d.sh[3].pad0, d.sh[3].pad1);
+        for (int q = 2; q < 4; ++q) {
+            SCHECK(launch_status_set(s->d_st, 0, 0, 6, s->stream));
+            SCHECK(launch_status_set(s->d_st, 0, 0, 7, s->stream));
+        }
+    }
     s->sb_pend = true;
     s->sb_wm = wm;
     s->sb_new = n;

@@ -81,3 +81,59 @@ def test_staged_rejections():
             op.ingest_stage(0, 10, with_value=False)  # SUM needs its values
     finally:
         op.close()
+
+
+@pytest.mark.parametrize("agg", ["sum_i64", "count"])
+def test_sent_ahead_matches_oracle(oracle_lib, agg):
+    """gw_stage_send: batch b+1 goes over PCIe while batch b is ingested, fired and drained
+    (into pinned host arrays, which the D2H writes directly) -- the host_fed leg's loop."""
+    import torch
+
+    kw = dict(assigner="sliding", size=2000, slide=500, agg=agg)
+    keys, ts, vals, batches = random_stream(seed=63, n=240_000, num_keys=20_000, n_batches=16, agg=agg)
+    cap = max(hi - lo for lo, hi, _ in batches)
+    slots = 3
+    op = gpu_operator(kw, capacity_hint=1 << 16)
+    out = [torch.empty(1 << 18, dtype=torch.int64, pin_memory=True).numpy() for _ in range(4)]
+    outs = []
+
+    def fill(b):
+        lo, hi, _ = batches[b]
+        k, _, t, v = op.stage_columns(b % slots)
+        k[:hi - lo] = keys[lo:hi]
+        t[:hi - lo] = ts[lo:hi]
+        if agg != "count":
+            v[:hi - lo] = vals[lo:hi]
+
+    try:
+        op.stage_alloc(slots, cap)
+        fill(0)
+        op.stage_send(0, batches[0][1] - batches[0][0], with_value=agg != "count")
+        for b, (lo, hi, wm) in enumerate(batches):
+            op.ingest_stage(b % slots, hi - lo, with_value=agg != "count")
+            if b + 1 < len(batches):
+                fill(b + 1)
+                nlo, nhi, _ = batches[b + 1]
+                op.stage_send((b + 1) % slots, nhi - nlo, with_value=agg != "count")
+            op.advance_watermark(wm)
+            outs.append(tuple(x.copy() for x in op.drain(out)))
+        op.advance_watermark(W.LONG_MAX)
+        outs.append(tuple(x.copy() for x in op.drain(out)))
+    finally:
+        op.close()
+    o, _ = run_oracle(oracle_lib, kw, keys, ts, vals, batches)
+    assert compare(outs, o, False) == []
+
+
+def test_sent_ahead_order_is_checked():
+    op = gpu_operator(dict(assigner="tumbling", size=1000, slide=1000, agg="sum_i64"))
+    try:
+        op.stage_alloc(3, 100)
+        op.stage_send(0, 10)
+        with pytest.raises(N.GpuWinError):
+            op.ingest_stage(1, 10)  # slot 0 was sent first
+        op.stage_send(1, 10)
+        with pytest.raises(N.GpuWinError):
+            op.stage_send(2, 10)  # one batch ahead at most
+    finally:
+        op.close()
