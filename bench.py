@@ -87,7 +87,7 @@ def parse(argv=None):
 
 
 def make_stream(nb, steps_total, K, E, slide, disorder, agg, dev, rank=0, world=1, key_partitioned=False,
-                maxp=128):
+                maxp=128, t_shift=0):
     """The bench's synthetic Nexmark-Q5 bids in HBM: steps_total watermark batches of nb
     events.  auction = splitmix64(i) mod K (uniform), ts advancing so each `slide` of event
     time holds E events with jitter <= disorder, value = splitmix64(i') mod 1e6.  With
@@ -95,7 +95,8 @@ def make_stream(nb, steps_total, K, E, slide, disorder, agg, dev, rank=0, world=
     (KeyGroupRangeAssignment.computeKeyGroupRangeForOperatorIndex), so every rank keeps the
     same nb, timestamps and watermarks.  Returns (keys, ts, vals or None, wms): the watermark
     after batch b is BoundedOutOfOrdernessWatermarks' maxTs - bound - 1 over the un-jittered
-    maximum, identical on every rank."""
+    maximum, identical on every rank.  t_shift (ms) moves the event-time origin back: the
+    watermark of batch b then completes windows where batch b + t_shift / interval would have."""
     from flink_amd import _native as N
     n_all = nb * steps_total
     idx = torch.arange(n_all, device=dev, dtype=torch.int64)
@@ -114,7 +115,7 @@ def make_stream(nb, steps_total, K, E, slide, disorder, agg, dev, rank=0, world=
     else:
         keys = draw % K
     del draw
-    t0_ms = 1_700_000_000_000
+    t0_ms = 1_700_000_000_000 - t_shift
     jitter = (splitmix64(idx, seed ^ 0x77) & MASK63) % (disorder + 1)
     ts = t0_ms + (idx * slide) // E - jitter
     vals = None
@@ -220,8 +221,13 @@ def main(argv=None):
     s_acc = 16 if agg.startswith("avg") else 8
 
     t_gen = time.time()
+    # The stream's event-time origin is placed so that the last warmup batch's watermark fires:
+    # the clock then starts right after a fire (and its flush), and every fire cycle inside the
+    # timed steps is a whole cycle of slide / interval batches (a cycle cut by the start of the
+    # clock would carry a flush over fewer batches than the steady state).
+    t_shift = (args.warmup - 1) * args.wm_interval_ms if args.warmup >= 1 else 0
     keys, ts, vals, wms = make_stream(nb, steps_total, K, E, slide, args.disorder_ms, agg, dev, rank, world,
-                                      key_partitioned=args.exchange == "none", maxp=maxp)
+                                      key_partitioned=args.exchange == "none", maxp=maxp, t_shift=t_shift)
     log(f"rank {rank}: generated {nb * steps_total} events ({nb * steps_total * b_in / 1e9:.1f} GB) "
         f"in {time.time() - t_gen:.1f}s")
 

@@ -1,0 +1,19 @@
+#!/bin/bash
+# One GPU session of round-4 checks and measurements (steps as in r4_steps.sh: a step ending
+# 0 or 1 lets the next one run; anything else stops here).  BATCH picks the set.
+set -u
+mkdir -p gpurun_out/r4
+case "${BATCH:-a}" in
+a)
+  bash scripts/r4_steps.sh \
+    "GW_SB_EXP=3 GW_SESSION_PATH=region timeout -k 10 200 python -u -m pytest -x -q -s --timeout 150 -m gpu tests/test_gpu_session_region.py -k f64 > gpurun_out/r4/sbdiag.log 2>&1; grep -E 'sb\\]|passed|failed' gpurun_out/r4/sbdiag.log | head -20" \
+    "TESTS=tests/test_gpu_staged_ingest.py TEST_TIMEOUT=300 PER_TEST=200 TAG=stg NOBENCH=1 bash scripts/r4_check.sh" \
+    "VARIANTS='base d3=GW_LIB_PATH=/root/repo/flink_amd/libgpuwin_d3.so d3u2=GW_LIB_PATH=/root/repo/flink_amd/libgpuwin_d3u2.so' RUNS=2 bash scripts/r4_ab.sh" \
+    "GW_HOST_PROFILE=1 timeout -k 10 200 python -u bench.py --no-cpu-baseline --no-host-fed > gpurun_out/r4/bench_hp.json 2> gpurun_out/r4/bench_hp.err && grep 'gw host' gpurun_out/r4/bench_hp.err" \
+    "timeout -k 10 200 python -u bench.py --no-cpu-baseline --no-host-fed --no-kernel-timing > gpurun_out/r4/bench_nkt.json 2> gpurun_out/r4/bench_nkt.err && python3 scripts/json_field.py gpurun_out/r4/bench_nkt.json value" \
+    "timeout -k 10 300 python -u bench.py --no-cpu-baseline > gpurun_out/r4/bench_hf3.json 2> gpurun_out/r4/bench_hf3.err && python3 scripts/json_field.py gpurun_out/r4/bench_hf3.json host_fed" \
+    "CONFIGS='sessions wordcount q7_first q7_maxby' bash scripts/r4_configs.sh"
+  ;;
+*)
+  echo "unknown BATCH"; exit 2 ;;
+esac
