@@ -474,7 +474,17 @@ __device__ __forceinline__ void block_scan2(const uint32_t* cnt, uint32_t* pre, 
     __syncthreads();
 }
 
-// Index i of the run holding record e: pre[i] <= e < pre[i + 1] (pre ascending, n runs).
+// Index i of the run holding record e: pre[i] <= e < pre[i + 1] (pre ascending, n runs,
+// pre[n] = total).  Runs of one bucket over a tile group are of similar length, so a guess
+// proportional to e is usually right or one off: a short walk from it instead of a
+// dependent binary search (7 LDS round trips at 112 runs).
+__device__ __forceinline__ int run_near(const uint32_t* pre, int n, uint32_t e) {
+    const uint32_t tot = pre[n];
+    int i = tot ? (int)min((uint64_t)(n - 1), (uint64_t)e * (uint64_t)n / tot) : 0;
+    while (i > 0 && pre[i] > e) --i;
+    while (i + 1 < n && pre[i + 1] <= e) ++i;
+    return i;
+}
 __device__ __forceinline__ int run_of(const uint32_t* pre, int n, uint32_t e) {
     int l = 0, h = n - 1;
     while (l < h) {
@@ -887,7 +897,7 @@ __global__ void __launch_bounds__(kPartThreads) k_rgn_p2(IngestArgs a) {
             key[it] = 0; c0[it] = 0; c1[it] = 0; pos[it] = 0;
             bk[it] = -1;
             if (e < e1) {
-                const int i = run_of(r_pre, nt, e);
+                const int i = run_near(r_pre, nt, e);
                 const int64_t src = r_src[i] + (e - r_pre[i]);
                 key[it] = N4 ? (int64_t)reinterpret_cast<const uint32_t*>(a.p1_key)[src] : a.p1_key[src];
                 if constexpr (NR) {

@@ -39,8 +39,8 @@ constexpr int64_t kSnapFirstElement = 2; // SnapHeader::flags: v4 entries end wi
 // Host-time profile of the ingest path (GW_HOST_PROFILE=1: printed by gw_destroy).
 struct HostProf {
     bool on = getenv("GW_HOST_PROFILE") != nullptr;
-    double t[8] = {};
-    int64_t n[8] = {};
+    double t[16] = {};
+    int64_t n[16] = {};
     std::chrono::steady_clock::time_point last;
     void mark() { if (on) last = std::chrono::steady_clock::now(); }
     void lap(int i) {
@@ -52,8 +52,10 @@ struct HostProf {
     }
     void dump() {
         if (!on) return;
-        static const char* names[8] = {"prep", "launch", "status-enqueue", "status-wait", "absorb", "api-entry", "-", "-"};
-        for (int i = 0; i < 8; ++i)
+        static const char* names[16] = {"prep", "launch", "status-enqueue", "status-wait", "absorb", "api-entry",
+                                        "ov_finalize", "refresh", "grow", "deferred", "args", "path-flush",
+                                        "region", "fmt", "advance", "-"};
+        for (int i = 0; i < 16; ++i)
             if (n[i]) fprintf(stderr, "[gw host] %-15s %8.2f us x %lld\n", names[i], t[i] / n[i], (long long)n[i]);
     }
 };
@@ -346,6 +348,7 @@ struct gw_handle {
     gw_stats stats{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, -1};
     bool timing = false;
     KernelTimer t_ingest, t_fire, t_apply;
+    int64_t timing_every = 1, timing_ctr = 0;  // region pass 1: time one launch in timing_every
     HostProf hp;
 
     SessionState* sess = nullptr;
@@ -1286,11 +1289,16 @@ struct gw_handle {
     int ingest_pane(int64_t nrec, const int64_t* key, const int64_t* ts, const int64_t* val) {
         int rc;
         if ((rc = ov_finalize())) return rc;
+        hp.lap(6);
         if (dirty && (rc = refresh())) return rc;  // a lagging (lazy) status is fine here
+        hp.lap(7);
         if ((rc = maybe_grow(nrec))) return rc;
+        hp.lap(8);
         if ((rc = ensure_deferred((int64_t)h_st->n_deferred + lazy_recs + nrec))) return rc;
+        hp.lap(9);
         IngestArgs a;
         if ((rc = base_args(a, nrec, key, ts, val))) return rc;
+        hp.lap(10);
         // path: LDS pre-aggregation when the batch repeats few keys many times; region
         // bucketing when the batch is large against the table (its streaming passes cost
         // ~48 B per slot, the direct path ~300 B of scattered traffic per record);
@@ -1308,6 +1316,7 @@ struct gw_handle {
             if ((rc = flush_buffer())) return rc;
             if ((rc = base_args(a, nrec, key, ts, val))) return rc;  // the table may have grown
         }
+        hp.lap(11);
         if (path == 2) {
             region_args(a);
             // Two-pass tables buffer P1 segments across watermarks (P2 + apply once per
@@ -1324,6 +1333,7 @@ struct gw_handle {
             if ((rc = ensure_region(buf_tiles + tiles, want))) return rc;
             region_args(a);
             a.tile0 = buf_tiles;
+            hp.lap(12);
             if (nseg == 0) {
                 const int fmt = region_fmt(a.d1_bits);
                 if (carry_on && fmt != buf_fmt) {  // carried records keep their window's format: apply them
@@ -1339,8 +1349,8 @@ struct gw_handle {
             a.fmt = buf_fmt;
             stats.region_format = buf_fmt;
             if (buffered) arm_status(a);
-            hp.lap(0);
-            if (timing) {
+            hp.lap(13);
+            if (timing && (timing_ctr++ % timing_every) == 0) {  // every timing_every-th batch
                 auto ev = t_ingest.get();
                 HIPCHECK(hipEventRecord(ev.first, stream));
                 HIPCHECK(launch_region_p1(a, stream));
@@ -3257,7 +3267,10 @@ int gw_advance_watermark(gw_handle* h, int64_t wm, int64_t* rows_fired) {
         if (rows_fired) *rows_fired = fired;
         return rc;
     }
-    return h->advance_pane(wm, rows_fired);
+    h->hp.mark();
+    const int rc = h->advance_pane(wm, rows_fired);
+    h->hp.lap(14);
+    return rc;
 }
 
 int gw_flush(gw_handle* h) {
@@ -4216,6 +4229,8 @@ int gw_enable_kernel_timing(gw_handle* h, int enable) {
     if (!h) return GW_E_INVALID;
     for (gw_handle* kid : h->kids) gw_enable_kernel_timing(kid, enable);
     h->timing = enable != 0;
+    h->timing_every = enable > 1 ? enable : 1;
+    h->timing_ctr = 0;
     if (h->sess) session_enable_timing(h->sess, h->timing);
     return GW_OK;
 }

@@ -566,7 +566,7 @@ constexpr int kSbWaveRecs = kSbTile / (kSbThreads / 64);
 constexpr int kSbMaxDigitBits = 8;
 constexpr int kSbMaxDigits = 1 << kSbMaxDigitBits;
 constexpr int kSbSinglePassBits = 6;      // buckets <= 2^6: P1 partitions by the whole bucket
-constexpr int kSbMeanBits = 10;            // ~2^10 records per bucket (mean in (512, 1024])
+constexpr int kSbMeanBits = 9;             // ~2^9 records per bucket (mean in (256, 512]: half the cap)
 constexpr int kSbCap = 1024;               // records of a bucket the replay stages and sorts in LDS
 constexpr int kSbPosBits = 10;
 constexpr int kSbMaxHomeBits = 31 - kSbPosBits - 1;  // + the sentinel's code

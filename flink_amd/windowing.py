@@ -726,8 +726,10 @@ class GpuWindowOperator:
     def stream(self) -> int:
         return N.lib().gw_stream(self._h)
 
-    def enable_kernel_timing(self, on: bool = True):
-        N.check(N.lib().gw_enable_kernel_timing(self._h, 1 if on else 0), self._h)
+    def enable_kernel_timing(self, on=True):
+        """True / 1: time every launch; k > 1: time region pass 1 on every k-th batch only."""
+        k = int(on) if not isinstance(on, bool) else (1 if on else 0)
+        N.check(N.lib().gw_enable_kernel_timing(self._h, k), self._h)
 
     def kernel_time_ms(self, which: int = 0):
         ms = ctypes.c_double(0)

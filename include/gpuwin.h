@@ -380,6 +380,9 @@ void* gw_stream(gw_handle* h);
  * measured with HIP events on the handle's stream.  which: 0 = ingest (per batch;
  * region path: pass 1), 1 = fire, 2 = region pass 2 + apply (per buffer flush). */
 int  gw_kernel_time_ms(gw_handle* h, int which, double* ms, int64_t* launches);
+/* enable: 0 off, 1 every launch, k > 1: the region path's pass 1 (one launch per batch, all
+ * alike) is timed on every k-th batch only (two event records per timed launch cost host
+ * time between batches); `launches` then counts the timed ones. */
 int  gw_enable_kernel_timing(gw_handle* h, int enable);
 
 /* ---- window stagger (stateless) ------------------------------------------ */

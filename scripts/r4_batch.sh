@@ -14,6 +14,13 @@ a)
     "timeout -k 10 300 python -u bench.py --no-cpu-baseline > gpurun_out/r4/bench_hf3.json 2> gpurun_out/r4/bench_hf3.err && python3 scripts/json_field.py gpurun_out/r4/bench_hf3.json host_fed" \
     "CONFIGS='sessions wordcount q7_first q7_maxby' bash scripts/r4_configs.sh"
   ;;
+b)
+  bash scripts/r4_steps.sh \
+    "TESTS='tests/test_gpu_headline.py tests/test_gpu_region_narrow.py tests/test_gpu_session_region.py' TEST_TIMEOUT=500 PER_TEST=400 TAG=b NOBENCH=1 bash scripts/r4_check.sh" \
+    "VARIANTS='base' RUNS=3 bash scripts/r4_ab.sh" \
+    "GW_HOST_PROFILE=1 timeout -k 10 200 python -u bench.py --no-cpu-baseline --no-host-fed > gpurun_out/r4/bench_hp2.json 2> gpurun_out/r4/bench_hp2.err && grep 'gw host' gpurun_out/r4/bench_hp2.err" \
+    "GW_HOST_PROFILE=1 timeout -k 10 200 python -u bench.py --events-per-pane 10000000 --steps 100 --warmup 20 --no-cpu-baseline --no-host-fed > gpurun_out/r4/bench_hp10.json 2> gpurun_out/r4/bench_hp10.err && grep 'gw host' gpurun_out/r4/bench_hp10.err && python3 scripts/json_field.py gpurun_out/r4/bench_hp10.json value"
+  ;;
 *)
   echo "unknown BATCH"; exit 2 ;;
 esac
