@@ -357,6 +357,9 @@ struct gw_handle {
     bool foreign_hash = false;  // a key_hash differed from Long.hashCode(key) (keys are caller ids)
     int ingest_unroll = 2;  // records per thread per iteration of k_ingest (GW_INGEST_UNROLL)
     int64_t region_min_batch = 1 << 16;  // smallest batch for the region path (GW_REGION_MIN_BATCH)
+    // records ingested since the last fire, and over the last fire cycle: the region path
+    // buffers batches until a fire, so its state pass amortises over a whole cycle
+    int64_t recs_since_fire = 0, recs_per_fire = 0;
 
     int fail(int code, const char* fmt, ...) {
         char buf[512];
@@ -676,6 +679,8 @@ struct gw_handle {
         bool pinned = true;  // pinned destinations (page-locked: hipHostMalloc / registered) take the D2H directly
         for (int i = 0; i < 4 && pinned; ++i)
             if (dst[i]) pinned = host_pinned(dst[i]);
+        static const bool dbg = getenv("GW_DRAIN_DEBUG") != nullptr;
+        if (dbg) fprintf(stderr, "[gw drain] %lld rows, %s\n", (long long)c, direct || pinned || c < kBounceRows / 4 ? (pinned ? "direct (pinned)" : "direct") : "bounce");
         if (direct || pinned || c < kBounceRows / 4) {
             hipError_t err = hipSuccess;
             for (int i = 0; i < 4 && err == hipSuccess; ++i)
@@ -1068,6 +1073,7 @@ struct gw_handle {
                 HIPCHECK(launch_fire(f, stream));
             }
             stats.fires++;
+            if (recs_since_fire) recs_per_fire = recs_since_fire, recs_since_fire = 0;
             dirty = true;
             occ &= ~rmask;
             fired_k = k_last + 1;
@@ -1308,7 +1314,11 @@ struct gw_handle {
         if (cfg.flags & GW_FLAG_FORCE_LDS_PREAGG) path = 1;
         else if (!(cfg.flags & GW_FLAG_NO_LDS_PREAGG) && est > 0 && nrec >= 8 * est) path = 1;
         if (path == 0 && tv.nreg <= kRgnMaxRegions && !(cfg.flags & GW_FLAG_NO_REGION)) {
-            const bool big = nrec >= region_min_batch && nrec * 8 >= tv.cap;
+            // large against the table: the batch itself, or (two-pass tables buffer until the
+            // fire) the last fire cycle's records
+            const bool cycle = tv.nreg > (1 << 7) && !(cfg.flags & GW_FLAG_NO_BUFFER) &&  // d2_bits > 0
+                               recs_per_fire * 8 >= tv.cap;
+            const bool big = nrec >= region_min_batch && (nrec * 8 >= tv.cap || cycle);
             if (big || (cfg.flags & GW_FLAG_FORCE_REGION)) path = 2;
         }
         if (path == 1) stats.preagg_batches++;
@@ -1375,6 +1385,7 @@ struct gw_handle {
         stats.events_in += nrec;
         stats.batches++;
         seq_ctr += nrec;
+        recs_since_fire += nrec;
         if (a.lo_key) lo_bound += nrec;
         if (a.q_refire) rf_bound += nrec;
         if (path == 2 && nseg) {  // buffered P1: no host sync (it writes no table cell)

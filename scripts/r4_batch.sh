@@ -21,6 +21,16 @@ b)
     "GW_HOST_PROFILE=1 timeout -k 10 200 python -u bench.py --no-cpu-baseline --no-host-fed > gpurun_out/r4/bench_hp2.json 2> gpurun_out/r4/bench_hp2.err && grep 'gw host' gpurun_out/r4/bench_hp2.err" \
     "GW_HOST_PROFILE=1 timeout -k 10 200 python -u bench.py --events-per-pane 10000000 --steps 100 --warmup 20 --no-cpu-baseline --no-host-fed > gpurun_out/r4/bench_hp10.json 2> gpurun_out/r4/bench_hp10.err && grep 'gw host' gpurun_out/r4/bench_hp10.err && python3 scripts/json_field.py gpurun_out/r4/bench_hp10.json value"
   ;;
+c)
+  bash scripts/r4_steps.sh \
+    "GW_HOST_PROFILE=1 timeout -k 10 200 python -u bench.py --events-per-pane 10000000 --steps 100 --warmup 20 --no-cpu-baseline --no-host-fed > gpurun_out/r4/bench_hp10c.json 2> gpurun_out/r4/bench_hp10c.err && grep 'gw host' gpurun_out/r4/bench_hp10c.err && python3 scripts/json_field.py gpurun_out/r4/bench_hp10c.json value" \
+    "TESTS=tests TEST_TIMEOUT=900 PER_TEST=300 TAG=full NOBENCH=1 bash scripts/r4_check.sh"
+  ;;
+d)
+  bash scripts/r4_steps.sh \
+    "GW_DRAIN_DEBUG=1 timeout -k 10 300 python -u bench.py --no-cpu-baseline > gpurun_out/r4/bench_hf4.json 2> gpurun_out/r4/bench_hf4.err; grep -c drain gpurun_out/r4/bench_hf4.err; grep drain gpurun_out/r4/bench_hf4.err | sed -E 's/[0-9]+ rows/N rows/' | sort | uniq -c; python3 scripts/json_field.py gpurun_out/r4/bench_hf4.json host_fed" \
+    "CONFIGS='q7 ysb' bash scripts/r4_configs.sh"
+  ;;
 *)
   echo "unknown BATCH"; exit 2 ;;
 esac
