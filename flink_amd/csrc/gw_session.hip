@@ -902,7 +902,26 @@ __device__ __forceinline__ void sb_radix_pass(const uint32_t* x, uint32_t* y, in
     __syncthreads();
 }
 
-// sp_store / sp_key / sp_run (the replay of one home slot's run) follow below.
+// sp_store / sp_key / sp_run (the replay of one home slot's run) follow below.  A run's
+// records come through an accessor: staged in LDS by the bucketed replay (LdsRecs), or in
+// HBM in arrival order behind the sorted arrival indices on the keyed sort path (HbmRecs).
+struct LdsRecs {
+    const uint32_t* pr;     // sorted position -> the record's place in the bucket
+    const int64_t* rk;      // keys and (timestamp, value) pairs by place
+    const longlong2* rtv;
+    __device__ __forceinline__ int64_t key(uint32_t q) const { return rk[pr[q]]; }
+    __device__ __forceinline__ longlong2 tv(uint32_t q) const { return rtv[pr[q]]; }
+};
+struct KeyRec { int64_t k, t, v; };  // one record of the batch, as k_sess_kprep copies it
+struct HbmRecs {
+    const uint32_t* perm;   // sorted position -> arrival index
+    const KeyRec* rec;      // the batch's records in arrival order
+    __device__ __forceinline__ int64_t key(uint32_t q) const { return rec[perm[q]].k; }
+    __device__ __forceinline__ longlong2 tv(uint32_t q) const {
+        const KeyRec& r = rec[perm[q]];
+        return longlong2{r.t, r.v};
+    }
+};
 // The key's list after a replay (cnt sessions in the lane) -> its slot, or to the migration
 // list when it outgrew the slot (the key's later records of the batch then punt until the
 // migration).
@@ -943,14 +962,13 @@ __device__ __forceinline__ void sp_store(const SegArgs& a, const SessList& l, in
 // LDS; r0 holds one of them, the others are the run's records with this key), in arrival
 // order, against the key's slot -- seg_slot's replay, with the punt list instead of the wide
 // pass.
-template <int AGG>
+template <int AGG, class RV>
 __device__ __forceinline__ void sp_key(const SegArgs& a, const SessList& l, int64_t key, uint32_t r0, uint32_t f,
-                                       const uint32_t* pr, const int64_t* rk, const longlong2* rtv,
-                                       unsigned long long& late, unsigned long long& merges,
+                                       const RV& rv, unsigned long long& late, unsigned long long& merges,
                                        unsigned long long& flags, unsigned long long& ins) {
     constexpr int SW = sess_words<AGG>();
     int64_t L = 0;
-    for (uint32_t q = r0; q < f; ++q) L += rk[pr[q]] == key;
+    for (uint32_t q = r0; q < f; ++q) L += rv.key(q) == key;
     bool inserted;
     const int64_t slot = find_or_insert(a.t, key, inserted);
     int64_t* sp = slot >= 0 ? slot_ptr(a.t, slot) : nullptr;
@@ -968,9 +986,8 @@ __device__ __forceinline__ void sp_key(const SegArgs& a, const SessList& l, int6
             sl_put(l, q, Sess{x[0], x[1], x[2], SW == 4 ? x[3] : 0, (int64_t)slot_fired(w1, q)});
         }
         for (uint32_t q = r0; q < f && ok; ++q) {
-            const uint32_t o = pr[q];
-            if (rk[o] != key) continue;
-            const longlong2 tv = rtv[o];
+            if (rv.key(q) != key) continue;
+            const longlong2 tv = rv.tv(q);
             ok = add_element_tv<AGG>(a, l, cnt, kLaneSess, key, tv.x, tv.y, late, merges, flags, dry);
         }
         if (!ok || !dry || !effects) break;
@@ -987,9 +1004,8 @@ __device__ __forceinline__ void sp_key(const SegArgs& a, const SessList& l, int6
         }
         unsigned long long at = atomicAdd(&a.st->overflow, (unsigned long long)L);
         for (uint32_t q = r0; q < f; ++q) {
-            const uint32_t o = pr[q];
-            if (rk[o] != key) continue;
-            const longlong2 tv = rtv[o];
+            if (rv.key(q) != key) continue;
+            const longlong2 tv = rv.tv(q);
             a.pu_key[at] = key;
             a.pu_ts[at] = tv.x;
             a.pu_val[at] = tv.y;
@@ -1003,18 +1019,17 @@ __device__ __forceinline__ void sp_key(const SegArgs& a, const SessList& l, int6
 
 // Every key of a home slot's run [e, f), in order of its first record (several keys per home
 // slot are rare), through sp_key.
-template <int AGG>
-__device__ __forceinline__ void sp_run(const SegArgs& a, const SessList& l, uint32_t e, uint32_t f, const uint32_t* pr,
-                                       const int64_t* rk, const longlong2* rtv, unsigned long long& late,
-                                       unsigned long long& merges, unsigned long long& flags,
-                                       unsigned long long& ins) {
+template <int AGG, class RV>
+__device__ __forceinline__ void sp_run(const SegArgs& a, const SessList& l, uint32_t e, uint32_t f, const RV& rv,
+                                       unsigned long long& late, unsigned long long& merges,
+                                       unsigned long long& flags, unsigned long long& ins) {
     for (uint32_t r = e; r < f;) {
-        sp_key<AGG>(a, l, rk[pr[r]], r, f, pr, rk, rtv, late, merges, flags, ins);
+        sp_key<AGG>(a, l, rv.key(r), r, f, rv, late, merges, flags, ins);
         uint32_t nx = f;
         for (uint32_t q = r + 1; q < f && nx == f; ++q) {
-            const int64_t kq = rk[pr[q]];
+            const int64_t kq = rv.key(q);
             bool seen = false;
-            for (uint32_t z = e; z < q && !seen; ++z) seen = rk[pr[z]] == kq;
+            for (uint32_t z = e; z < q && !seen; ++z) seen = rv.key(z) == kq;
             if (!seen) nx = q;
         }
         r = nx;
@@ -1173,7 +1188,7 @@ __global__ void __launch_bounds__(kSbRThreads) k_sb_replay(SegArgs a, const uint
     unsigned long long late = 0, merges = 0, flags = 0, ins = 0;
     for (uint32_t j = tid; j < nh; j += kSbRThreads) {
         const uint32_t e = hd[j], fe = j + 1 < nh ? hd[j + 1] : n;
-        sp_run<AGG>(a, l, e, fe, pr, rk, rtv, late, merges, flags, ins);
+        sp_run<AGG>(a, l, e, fe, LdsRecs{pr, rk, rtv}, late, merges, flags, ins);
     }
     block_commit(a.st, late, ins, flags, 0, 0, merges);
 }
@@ -1190,6 +1205,69 @@ __global__ void __launch_bounds__(256) k_sp_unpunt(TableView t, const int64_t* p
         int64_t* sp = slot_ptr(t, slot);
         if ((uint64_t)sp[1] & kPuntMeta) atomicAnd((unsigned long long*)(sp + 1), ~(unsigned long long)kPuntMeta);
     }
+}
+
+// ---------------------------------------------------------- keyed sort path (the default)
+// The sort path's grouping without its per-record table probe: records are grouped by a
+// 32-bit code of their key's hash whose top bits are the key's home slot (the hash rotated
+// right by lcap), so that the table is probed once per key of the batch, by the thread that
+// replays the key's run, and the runs reach the table in home-slot order.
+//  * k_sess_kprep: per record its code and arrival index, and a copy of the record (key,
+//    timestamp, value) in arrival order -- a pure stream, no table access.
+//  * a stable radix sort of (code, arrival index) over the code's top sbits bits;
+//  * k_sess_kseg: one thread per group of equal sorted codes (a run), replaying every key of
+//    the run in order of its first record (sp_run, as the bucketed replay does from LDS; two
+//    keys share a run only when their codes collide).  Keys that find no slot, live in the
+//    wide table or outgrow the lane are punted with their records, as on the bucketed path.
+__device__ __forceinline__ uint32_t key_code(int64_t key, int lcap) {
+    const uint64_t h = slot_hash(key);
+    return (uint32_t)(((h >> lcap) | (h << (64 - lcap))) >> 32);
+}
+
+__global__ void __launch_bounds__(256) k_sess_kprep(const int64_t* key, const int64_t* ts, const int64_t* val,
+                                                    int64_t n, int lcap, uint32_t* code, uint32_t* perm,
+                                                    KeyRec* rec, DevStatus* st) {
+    unsigned long long flags = 0;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t k = key[i], t = ts[i];
+        if (t == INT64_MIN) flags |= GW_DF_NO_TS;
+        code[i] = key_code(k, lcap);
+        perm[i] = (uint32_t)i;
+        rec[i] = KeyRec{k, t, val ? val[i] : 0};
+    }
+    block_commit(st, 0, 0, flags, 0);
+}
+
+// Each wave takes kSegChunk consecutive sorted records, compacts the run heads among them
+// into LDS with ballots and replays them 64 at a time (a run that starts in the chunk belongs
+// to it, however far it extends).
+template <int AGG>
+__global__ void __launch_bounds__(kSegThreads) k_sess_kseg(SegArgs a, const uint32_t* code, int shift,
+                                                           const KeyRec* rec) {
+    __shared__ int64_t lane[5 * kLaneSess * kSegThreads];
+    __shared__ uint32_t heads[kSegThreads / 64][kSegChunk];
+    const SessList l{lane + threadIdx.x, kLaneSess * kSegThreads, kSegThreads};
+    unsigned long long late = 0, merges = 0, flags = 0, ins = 0;
+    const int w = threadIdx.x >> 6, ln = threadIdx.x & 63;
+    const int64_t base = (blockIdx.x * (int64_t)(kSegThreads / 64) + w) * kSegChunk;
+    int nh = 0;
+    for (int c = 0; c < kSegChunk; c += 64) {
+        const int64_t i = base + c + ln;
+        const bool h = i < a.n && (i == 0 || (code[i] >> shift) != (code[i - 1] >> shift));
+        const uint64_t b = __ballot(h);
+        if (h) heads[w][nh + __popcll(b & ((1ull << ln) - 1ull))] = (uint32_t)(i - base);
+        nh += __popcll(b);
+    }
+    __syncthreads();
+    const HbmRecs rv{a.perm, rec};
+    for (int q = ln; q < nh; q += 64) {
+        const int64_t i = base + heads[w][q];
+        const uint32_t g = code[i] >> shift;
+        int64_t j = i + 1;
+        while (j < a.n && (code[j] >> shift) == g) ++j;
+        sp_run<AGG>(a, l, (uint32_t)i, (uint32_t)j, rv, late, merges, flags, ins);
+    }
+    block_commit(a.st, late, ins, flags, 0, 0, merges);
 }
 
 // Fire sweep, part 1: list the slots with something due at `wm` -- a small fraction: the
@@ -1743,7 +1821,8 @@ struct SessionState {
     uint32_t* r0 = nullptr;  // punted / retried run heads
     uint32_t* r1 = nullptr;
     int64_t* mig = nullptr;  // migration lists (main pass -> wide table)
-    int64_t* rec = nullptr;  // sessions: (ts, value) per record
+    int64_t* rec = nullptr;  // sessions: (ts, value) per record (sort path), KeyRec (keyed sort path)
+    int64_t* ks_pu = nullptr;  // keyed sort path: punted key | ts | value, buf_cap each
     // bucketed ingest (k_sb_*): P1 / P2 records (key | ts, value: 24 B each), descriptor
     // rows / columns / coarse totals, punted records
     int64_t* sb_rec[2] = {nullptr, nullptr};
@@ -1919,7 +1998,7 @@ void session_destroy(SessionState* s) {
     hipFree(s->d_st);
     hipHostFree(s->h_st);
     for (int q = 0; q < 2; ++q) { hipFree(s->slot[q]); hipFree(s->perm[q]); }
-    hipFree(s->r0); hipFree(s->r1); hipFree(s->mig); hipFree(s->rec);
+    hipFree(s->r0); hipFree(s->r1); hipFree(s->mig); hipFree(s->rec); hipFree(s->ks_pu);
     hipFree(s->cnt_plan); hipFree(s->cnt_tmp); hipFree(s->due_list);
     hipFree(s->sort_tmp);
     hipFree(s->sb_rec[0]); hipFree(s->sb_rec[1]); hipFree(s->sb_desc); hipFree(s->pu_col3);
@@ -1935,9 +2014,10 @@ static int ensure_bufs(SessionState* s, int64_t n, std::string& err) {
     const int64_t c = std::max<int64_t>(n + n / 4, 1 << 16);
     SCHECK(hipStreamSynchronize(s->stream));
     for (int q = 0; q < 2; ++q) { hipFree(s->slot[q]); hipFree(s->perm[q]); }
-    hipFree(s->r0); hipFree(s->r1); hipFree(s->mig); hipFree(s->sort_tmp); hipFree(s->rec);
+    hipFree(s->r0); hipFree(s->r1); hipFree(s->mig); hipFree(s->sort_tmp); hipFree(s->rec); hipFree(s->ks_pu);
     s->mig = nullptr;
     s->rec = nullptr;
+    s->ks_pu = nullptr;
     for (int q = 0; q < 2; ++q) {
         SCHECK(hipMalloc((void**)&s->slot[q], c * 4));
         SCHECK(hipMalloc((void**)&s->perm[q], c * 4));
@@ -1945,7 +2025,8 @@ static int ensure_bufs(SessionState* s, int64_t n, std::string& err) {
     SCHECK(hipMalloc((void**)&s->r0, c * 4));
     SCHECK(hipMalloc((void**)&s->r1, c * 4));
     if (!s->count_mode) SCHECK(hipMalloc((void**)&s->mig, (size_t)c * (2 + kWideWords * kLaneSess) * 8));
-    if (!s->count_mode) SCHECK(hipMalloc((void**)&s->rec, (size_t)c * 16));
+    if (!s->count_mode) SCHECK(hipMalloc((void**)&s->rec, (size_t)c * sizeof(KeyRec)));
+    if (!s->count_mode) SCHECK(hipMalloc((void**)&s->ks_pu, (size_t)c * 24));
     rocprim::double_buffer<uint32_t> kb(s->slot[0], s->slot[1]), vb(s->perm[0], s->perm[1]);
     size_t bytes = 0;
     SCHECK(rocprim::radix_sort_pairs<SlotSortConfig>(nullptr, bytes, kb, vb, (size_t)c, 0, 32, s->stream));
@@ -2420,6 +2501,64 @@ static int ingest_region(SessionState* s, int64_t n, const int64_t* key, const i
     return session_refresh(s, err);
 }
 
+// Keyed sort path (k_sess_kprep / sort / k_sess_kseg), then -- at the next sync, as for the
+// bucketed path -- migrations and the punted records through the sort path.
+static int ingest_keyed(SessionState* s, int64_t n, const int64_t* key, const int64_t* ts, const int64_t* val,
+                        int64_t wm, std::string& err) {
+    int rc;
+    // room for n new keys, as group_records keeps it (keys that still find no slot punt)
+    if ((double)(s->h_st->used_slots + n) > 0.7 * (double)s->tv.cap &&
+        ((double)s->h_st->used_slots > 0.7 * (double)s->tv.cap ||
+         (double)(s->h_st->used_slots + n) > 0.95 * (double)s->tv.cap)) {
+        int64_t want = s->tv.cap;
+        while ((double)(s->h_st->used_slots + n) > 0.7 * (double)want) want *= 2;
+        if ((rc = regrow(s, s->tv, want, s->tv.ring, false, err))) return rc;
+    }
+    int lcap = 0;
+    while (((int64_t)1 << lcap) < s->tv.cap) ++lcap;
+    if (lcap < 1 || lcap > 30) return ingest_sorted(s, n, key, ts, val, wm, err);
+    if ((rc = ensure_bufs(s, n, err))) return rc;
+    // code bits sorted: the home slot and two more hash bits, in whole 9-bit radix passes (a
+    // run mixes keys only when their codes collide in these bits)
+    static const int kbits_env = getenv("GW_SESSION_KEY_BITS") ? atoi(getenv("GW_SESSION_KEY_BITS")) : 0;
+    int sbits = kbits_env > 0 ? std::min(32, kbits_env) : std::min(32, (lcap + 2 + 8) / 9 * 9);
+    const int shift = 32 - sbits;
+    if ((rc = zero_word_async(s, offsetof(DevStatus, overflow), err))) return rc;
+    if ((rc = zero_word_async(s, offsetof(DevStatus, pad[0]), err))) return rc;
+    if ((rc = zero_word_async(s, offsetof(DevStatus, pad[1]), err))) return rc;
+    KeyRec* rec = reinterpret_cast<KeyRec*>(s->rec);
+    hipLaunchKernelGGL(k_sess_kprep, dim3(grid_of(n)), dim3(256), 0, s->stream, key, ts, val, n, lcap, s->slot[0],
+                       s->perm[0], rec, s->d_st);
+    SCHECK(hipGetLastError());
+    rocprim::double_buffer<uint32_t> kb(s->slot[0], s->slot[1]), vb(s->perm[0], s->perm[1]);
+    size_t bytes = s->sort_tmp_bytes;
+    SCHECK(rocprim::radix_sort_pairs<SlotSortConfig>(s->sort_tmp, bytes, kb, vb, (size_t)n, shift, 32, s->stream));
+    SegArgs a{};
+    if ((rc = seg_common(s, a, n, wm, err))) return rc;
+    a.slot = kb.current();
+    a.perm = vb.current();
+    const int64_t C = s->buf_cap;
+    a.pu_key = s->ks_pu;
+    a.pu_ts = s->ks_pu + C;
+    a.pu_val = s->ks_pu + 2 * C;
+    const int64_t per_block = (int64_t)kSegChunk * (kSegThreads / 64);
+    const unsigned gs = (unsigned)((n + per_block - 1) / per_block);
+#define L(A) hipLaunchKernelGGL(k_sess_kseg<A>, dim3(gs), dim3(kSegThreads), 0, s->stream, a, a.slot, shift, rec)
+    GW_AGG_SWITCH(s->cfg.agg, L);
+#undef L
+    SCHECK(hipGetLastError());
+    s->sb_pend = true;
+    s->sb_wm = wm;
+    s->sb_new = n;
+    s->sb_pu[0] = a.pu_key;
+    s->sb_pu[1] = a.pu_ts;
+    s->sb_pu[2] = a.pu_val;
+    s->fresh = false;
+    static const bool always = getenv("GW_SESSION_SYNC") && atoi(getenv("GW_SESSION_SYNC")) != 0;
+    if (!always && a.lateness == 0 && !a.lo_key) return GW_OK;
+    return session_refresh(s, err);
+}
+
 // The follow-up of a bucketed ingest (h_st fresh): migrations, then the punted records
 // through the sort path.
 static int sb_finish(SessionState* s, std::string& err) {
@@ -2435,14 +2574,15 @@ static int sb_finish(SessionState* s, std::string& err) {
     return ingest_sorted(s, n_punt, s->sb_pu[0], s->sb_pu[1], s->sb_pu[2], s->sb_wm, err);
 }
 
-// GW_SESSION_PATH=region|sort picks the ingest path (GW_SESSION_SORT_BITS, the sort path's
-// group tests, implies sort).  The sort path is the default: on the sessions config the
-// bucketed path measured slower (its per-bucket replay is latency-bound).
-constexpr bool kSessionBucketedDefault = false;
-static bool region_ingest_enabled() {
+// GW_SESSION_PATH=keyed|region|sort picks the ingest path (GW_SESSION_SORT_BITS, the sort
+// path's group tests, implies sort).  The keyed sort path is the default: on the sessions
+// config the bucketed path measured slower (its per-bucket replay is
+// latency-bound), and the slot sort path probes the table once per record.
+enum { kPathKeyed = 0, kPathRegion = 1, kPathSort = 2 };
+static int session_path() {
     const char* p = getenv("GW_SESSION_PATH");
-    if (p) return strcmp(p, "sort") != 0;
-    return getenv("GW_SESSION_SORT_BITS") == nullptr && kSessionBucketedDefault;
+    if (p) return !strcmp(p, "sort") ? kPathSort : !strcmp(p, "region") ? kPathRegion : kPathKeyed;
+    return getenv("GW_SESSION_SORT_BITS") ? kPathSort : kPathKeyed;
 }
 
 int session_ingest(SessionState* s, int64_t n, const int64_t* key, const int64_t* ts, const int64_t* val, int64_t wm,
@@ -2454,7 +2594,10 @@ int session_ingest(SessionState* s, int64_t n, const int64_t* key, const int64_t
     if ((int64_t)n > (int64_t)0x7fffffffLL) { err = "batch too large"; return GW_E_INVALID; }
     auto ev = s->timing ? get_ev(s) : std::pair<hipEvent_t, hipEvent_t>{};
     if (s->timing) SCHECK(hipEventRecord(ev.first, s->stream));
-    rc = region_ingest_enabled() ? ingest_region(s, n, key, ts, val, wm, err) : ingest_sorted(s, n, key, ts, val, wm, err);
+    static const int path = session_path();
+    rc = path == kPathKeyed    ? ingest_keyed(s, n, key, ts, val, wm, err)
+         : path == kPathRegion ? ingest_region(s, n, key, ts, val, wm, err)
+                               : ingest_sorted(s, n, key, ts, val, wm, err);
     if (rc) return rc;
     if (s->timing) {
         SCHECK(hipEventRecord(ev.second, s->stream));

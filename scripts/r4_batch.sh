@@ -23,8 +23,9 @@ b)
   ;;
 c)
   bash scripts/r4_steps.sh \
-    "GW_HOST_PROFILE=1 timeout -k 10 200 python -u bench.py --events-per-pane 10000000 --steps 100 --warmup 20 --no-cpu-baseline --no-host-fed > gpurun_out/r4/bench_hp10c.json 2> gpurun_out/r4/bench_hp10c.err && grep 'gw host' gpurun_out/r4/bench_hp10c.err && python3 scripts/json_field.py gpurun_out/r4/bench_hp10c.json value" \
-    "TESTS=tests TEST_TIMEOUT=900 PER_TEST=300 TAG=full NOBENCH=1 bash scripts/r4_check.sh"
+    "TESTS=tests TEST_TIMEOUT=800 PER_TEST=300 TAG=full NOBENCH=1 bash scripts/r4_check.sh" \
+    "CONFIGS=sessions NO_E10M=1 bash scripts/r4_configs.sh" \
+    "GW_HOST_PROFILE=1 timeout -k 10 200 python -u bench.py --events-per-pane 10000000 --steps 100 --warmup 20 --no-cpu-baseline --no-host-fed > gpurun_out/r4/bench_hp10c.json 2> gpurun_out/r4/bench_hp10c.err && grep 'gw host' gpurun_out/r4/bench_hp10c.err && python3 scripts/json_field.py gpurun_out/r4/bench_hp10c.json value"
   ;;
 d)
   bash scripts/r4_steps.sh \
