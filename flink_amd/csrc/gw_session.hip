@@ -1238,6 +1238,48 @@ __global__ void __launch_bounds__(256) k_sess_kprep(const int64_t* key, const in
     block_commit(st, 0, 0, flags, 0);
 }
 
+// The common run in one pass over its records (no allowed lateness, no side output: the
+// replay has no effect beyond the key's slot, written at the end): the run is taken to hold
+// one key, so every record is loaded once, the next one in flight while the current one
+// replays.  Returns false, having written nothing, when the run turns out to hold another
+// key, the key finds no slot or is marked wide / punted, or the lane overflows; sp_run then
+// replays the run from the slot as it was.
+template <int AGG>
+__device__ __forceinline__ bool kseg_fast(const SegArgs& a, const SessList& l, uint32_t e, uint32_t f,
+                                          const HbmRecs& rv, unsigned long long& late, unsigned long long& merges,
+                                          unsigned long long& flags, unsigned long long& ins) {
+    constexpr int SW = sess_words<AGG>();
+    KeyRec r = rv.rec[rv.perm[e]];
+    const int64_t key = r.k;
+    bool inserted;
+    const int64_t slot = find_or_insert(a.t, key, inserted);
+    if (slot < 0) return false;
+    ins += inserted;  // (sp_run finds the slot again without inserting)
+    int64_t* sp = slot_ptr(a.t, slot);
+    const int64_t w1 = sp[1];
+    if ((uint64_t)w1 & (kBigMeta | kPuntMeta)) return false;
+    int cnt = slot_cnt(w1);
+    for (int q = 0; q < cnt; ++q) {
+        const int64_t* x = sp + 2 + q * SW;
+        sl_put(l, q, Sess{x[0], x[1], x[2], SW == 4 ? x[3] : 0, (int64_t)slot_fired(w1, q)});
+    }
+    const unsigned long long l0 = late, m0 = merges, f0 = flags;
+    for (uint32_t q = e;;) {
+        KeyRec nx{};
+        if (q + 1 < f) nx = rv.rec[rv.perm[q + 1]];  // in flight during this record's replay
+        if (r.k != key || !add_element_tv<AGG>(a, l, cnt, kLaneSess, key, r.t, r.v, late, merges, flags, true)) {
+            late = l0;
+            merges = m0;
+            flags = f0;
+            return false;
+        }
+        if (++q >= f) break;
+        r = nx;
+    }
+    sp_store<AGG>(a, l, cnt, slot, sp, w1);
+    return true;
+}
+
 // Each wave takes kSegChunk consecutive sorted records, compacts the run heads among them
 // into LDS with ballots and replays them 64 at a time (a run that starts in the chunk belongs
 // to it, however far it extends).
@@ -1260,12 +1302,14 @@ __global__ void __launch_bounds__(kSegThreads) k_sess_kseg(SegArgs a, const uint
     }
     __syncthreads();
     const HbmRecs rv{a.perm, rec};
+    const bool effects = a.lateness > 0 || a.lo_key;
     for (int q = ln; q < nh; q += 64) {
         const int64_t i = base + heads[w][q];
         const uint32_t g = code[i] >> shift;
         int64_t j = i + 1;
         while (j < a.n && (code[j] >> shift) == g) ++j;
-        sp_run<AGG>(a, l, (uint32_t)i, (uint32_t)j, rv, late, merges, flags, ins);
+        if (effects || !kseg_fast<AGG>(a, l, (uint32_t)i, (uint32_t)j, rv, late, merges, flags, ins))
+            sp_run<AGG>(a, l, (uint32_t)i, (uint32_t)j, rv, late, merges, flags, ins);
     }
     block_commit(a.st, late, ins, flags, 0, 0, merges);
 }
@@ -2520,7 +2564,7 @@ static int ingest_keyed(SessionState* s, int64_t n, const int64_t* key, const in
     if ((rc = ensure_bufs(s, n, err))) return rc;
     // code bits sorted: the home slot and two more hash bits, in whole 9-bit radix passes (a
     // run mixes keys only when their codes collide in these bits)
-    static const int kbits_env = getenv("GW_SESSION_KEY_BITS") ? atoi(getenv("GW_SESSION_KEY_BITS")) : 0;
+    const int kbits_env = getenv("GW_SESSION_KEY_BITS") ? atoi(getenv("GW_SESSION_KEY_BITS")) : 0;
     int sbits = kbits_env > 0 ? std::min(32, kbits_env) : std::min(32, (lcap + 2 + 8) / 9 * 9);
     const int shift = 32 - sbits;
     if ((rc = zero_word_async(s, offsetof(DevStatus, overflow), err))) return rc;
@@ -2594,7 +2638,7 @@ int session_ingest(SessionState* s, int64_t n, const int64_t* key, const int64_t
     if ((int64_t)n > (int64_t)0x7fffffffLL) { err = "batch too large"; return GW_E_INVALID; }
     auto ev = s->timing ? get_ev(s) : std::pair<hipEvent_t, hipEvent_t>{};
     if (s->timing) SCHECK(hipEventRecord(ev.first, s->stream));
-    static const int path = session_path();
+    const int path = session_path();  // read per batch: tests switch paths within one process
     rc = path == kPathKeyed    ? ingest_keyed(s, n, key, ts, val, wm, err)
          : path == kPathRegion ? ingest_region(s, n, key, ts, val, wm, err)
                                : ingest_sorted(s, n, key, ts, val, wm, err);

@@ -23,12 +23,15 @@ b)
   ;;
 c)
   bash scripts/r4_steps.sh \
-    "TESTS=tests TEST_TIMEOUT=800 PER_TEST=300 TAG=full NOBENCH=1 bash scripts/r4_check.sh" \
-    "CONFIGS=sessions NO_E10M=1 bash scripts/r4_configs.sh" \
-    "GW_HOST_PROFILE=1 timeout -k 10 200 python -u bench.py --events-per-pane 10000000 --steps 100 --warmup 20 --no-cpu-baseline --no-host-fed > gpurun_out/r4/bench_hp10c.json 2> gpurun_out/r4/bench_hp10c.err && grep 'gw host' gpurun_out/r4/bench_hp10c.err && python3 scripts/json_field.py gpurun_out/r4/bench_hp10c.json value"
+    "GW_SESSION_PATH=sort timeout -k 10 200 python -u -m pytest -x -q --timeout 150 -m gpu tests/test_gpu_multirank.py -k session > gpurun_out/r4/mr_sort.log 2>&1; tail -3 gpurun_out/r4/mr_sort.log" \
+    "timeout -k 10 200 python -u -m pytest -x -q --timeout 150 -m gpu tests/test_gpu_multirank.py -k session > gpurun_out/r4/mr_keyed.log 2>&1; tail -3 gpurun_out/r4/mr_keyed.log" \
+    "TESTS=tests/test_gpu_session_keyed.py TEST_TIMEOUT=400 PER_TEST=150 TAG=keyed NOBENCH=1 bash scripts/r4_check.sh" \
+    "CONFIGS=sessions NO_E10M=1 bash scripts/r4_configs.sh"
   ;;
 d)
   bash scripts/r4_steps.sh \
+    "timeout -k 10 120 python -u scripts/h2d_probe.py && HSA_ENABLE_SDMA=0 timeout -k 10 120 python -u scripts/h2d_probe.py" \
+    "HSA_ENABLE_SDMA=0 timeout -k 10 300 python -u bench.py --no-cpu-baseline > gpurun_out/r4/bench_hf_nosdma.json 2> gpurun_out/r4/bench_hf_nosdma.err; python3 scripts/json_field.py gpurun_out/r4/bench_hf_nosdma.json host_fed" \
     "GW_DRAIN_DEBUG=1 timeout -k 10 300 python -u bench.py --no-cpu-baseline > gpurun_out/r4/bench_hf4.json 2> gpurun_out/r4/bench_hf4.err; grep -c drain gpurun_out/r4/bench_hf4.err; grep drain gpurun_out/r4/bench_hf4.err | sed -E 's/[0-9]+ rows/N rows/' | sort | uniq -c; python3 scripts/json_field.py gpurun_out/r4/bench_hf4.json host_fed" \
     "CONFIGS='q7 ysb' bash scripts/r4_configs.sh"
   ;;
