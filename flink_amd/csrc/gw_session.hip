@@ -1219,19 +1219,19 @@ __global__ void __launch_bounds__(256) k_sp_unpunt(TableView t, const int64_t* p
 //    the run in order of its first record (sp_run, as the bucketed replay does from LDS; two
 //    keys share a run only when their codes collide).  Keys that find no slot, live in the
 //    wide table or outgrow the lane are punted with their records, as on the bucketed path.
-__device__ __forceinline__ uint32_t key_code(int64_t key, int lcap) {
+__device__ __forceinline__ uint32_t key_code(int64_t key, int lcap, int sbits) {
     const uint64_t h = slot_hash(key);
-    return (uint32_t)(((h >> lcap) | (h << (64 - lcap))) >> 32);
+    return (uint32_t)(((h >> lcap) | (h << (64 - lcap))) >> (64 - sbits));
 }
 
 __global__ void __launch_bounds__(256) k_sess_kprep(const int64_t* key, const int64_t* ts, const int64_t* val,
-                                                    int64_t n, int lcap, uint32_t* code, uint32_t* perm,
-                                                    KeyRec* rec, DevStatus* st) {
+                                                    int64_t n, int lcap, int sbits, uint32_t* code,
+                                                    uint32_t* perm, KeyRec* rec, DevStatus* st) {
     unsigned long long flags = 0;
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
         const int64_t k = key[i], t = ts[i];
         if (t == INT64_MIN) flags |= GW_DF_NO_TS;
-        code[i] = key_code(k, lcap);
+        code[i] = key_code(k, lcap, sbits);
         perm[i] = (uint32_t)i;
         rec[i] = KeyRec{k, t, val ? val[i] : 0};
     }
@@ -1302,7 +1302,7 @@ __global__ void __launch_bounds__(kSegThreads) k_sess_kseg(SegArgs a, const uint
     }
     __syncthreads();
     const HbmRecs rv{a.perm, rec};
-    const bool effects = a.lateness > 0 || a.lo_key;
+    const bool effects = a.lateness > 0 || a.lo_key || a.diag;  // diag: GW_KSEG_FAST=0
     for (int q = ln; q < nh; q += 64) {
         const int64_t i = base + heads[w][q];
         const uint32_t g = code[i] >> shift;
@@ -2566,19 +2566,20 @@ static int ingest_keyed(SessionState* s, int64_t n, const int64_t* key, const in
     // run mixes keys only when their codes collide in these bits)
     const int kbits_env = getenv("GW_SESSION_KEY_BITS") ? atoi(getenv("GW_SESSION_KEY_BITS")) : 0;
     int sbits = kbits_env > 0 ? std::min(32, kbits_env) : std::min(32, (lcap + 2 + 8) / 9 * 9);
-    const int shift = 32 - sbits;
+    const int shift = 0;  // the code holds exactly the sorted bits (a sort from bit 0)
     if ((rc = zero_word_async(s, offsetof(DevStatus, overflow), err))) return rc;
     if ((rc = zero_word_async(s, offsetof(DevStatus, pad[0]), err))) return rc;
     if ((rc = zero_word_async(s, offsetof(DevStatus, pad[1]), err))) return rc;
     KeyRec* rec = reinterpret_cast<KeyRec*>(s->rec);
-    hipLaunchKernelGGL(k_sess_kprep, dim3(grid_of(n)), dim3(256), 0, s->stream, key, ts, val, n, lcap, s->slot[0],
-                       s->perm[0], rec, s->d_st);
+    hipLaunchKernelGGL(k_sess_kprep, dim3(grid_of(n)), dim3(256), 0, s->stream, key, ts, val, n, lcap, sbits,
+                       s->slot[0], s->perm[0], rec, s->d_st);
     SCHECK(hipGetLastError());
     rocprim::double_buffer<uint32_t> kb(s->slot[0], s->slot[1]), vb(s->perm[0], s->perm[1]);
     size_t bytes = s->sort_tmp_bytes;
-    SCHECK(rocprim::radix_sort_pairs<SlotSortConfig>(s->sort_tmp, bytes, kb, vb, (size_t)n, shift, 32, s->stream));
+    SCHECK(rocprim::radix_sort_pairs<SlotSortConfig>(s->sort_tmp, bytes, kb, vb, (size_t)n, 0, sbits, s->stream));
     SegArgs a{};
     if ((rc = seg_common(s, a, n, wm, err))) return rc;
+    a.diag = getenv("GW_KSEG_FAST") && atoi(getenv("GW_KSEG_FAST")) == 0;
     a.slot = kb.current();
     a.perm = vb.current();
     const int64_t C = s->buf_cap;
