@@ -331,6 +331,11 @@ struct gw_handle {
     int64_t pre_n[2] = {0, 0};
     int pre_cols[2] = {0, 0};
     hipStream_t cstream = nullptr;
+    // staged H2D split over extra copy streams (GW_STAGE_STREAMS > 1): several DMA queues
+    // in flight, joined back into cstream by events
+    std::vector<hipStream_t> cx;
+    std::vector<hipEvent_t> cx_ev;
+    hipEvent_t ev_fork = nullptr;
 
     // output rows (device SoA), [rows_head, st.rows) pending
     int64_t* o_key = nullptr;
@@ -646,6 +651,19 @@ struct gw_handle {
         const int ns = std::max(slots, (int)h_slot.size());
         free_stage();
         if (!cstream) HIPCHECK(hipStreamCreateWithFlags(&cstream, hipStreamNonBlocking));
+        if (cx.empty()) {
+            const char* e = getenv("GW_STAGE_STREAMS");
+            const int ncx = e ? std::min(8, std::max(1, atoi(e))) : 1;
+            if (ncx > 1) {
+                HIPCHECK(hipEventCreateWithFlags(&ev_fork, hipEventDisableTiming));
+                cx.assign(ncx, nullptr);
+                cx_ev.assign(ncx, nullptr);
+                for (int i = 0; i < ncx; ++i) {
+                    HIPCHECK(hipStreamCreateWithFlags(&cx[i], hipStreamNonBlocking));
+                    HIPCHECK(hipEventCreateWithFlags(&cx_ev[i], hipEventDisableTiming));
+                }
+            }
+        }
         for (int t = 0; t < 2; ++t) {
             if (!ev_dread[t]) HIPCHECK(hipEventCreateWithFlags(&ev_dread[t], hipEventDisableTiming));
             HIPCHECK(hipMalloc((void**)&d_stage2[t], (size_t)cap * 28));
@@ -2500,6 +2518,11 @@ int gw_destroy(gw_handle* h) {
     for (int t = 0; t < 2; ++t)
         if (h->ev_dread[t]) hipEventDestroy(h->ev_dread[t]);
     if (h->cstream) hipStreamDestroy(h->cstream);
+    for (size_t i = 0; i < h->cx.size(); ++i) {
+        hipStreamDestroy(h->cx[i]);
+        hipEventDestroy(h->cx_ev[i]);
+    }
+    if (h->ev_fork) hipEventDestroy(h->ev_fork);
     if (h->ev_in) hipEventDestroy(h->ev_in);
     if (h->ev_out) hipEventDestroy(h->ev_out);
     if (h->stream && !h->shared_stream) hipStreamDestroy(h->stream);
@@ -2874,12 +2897,31 @@ static int stage_send(gw_handle* h, int slot, int64_t n, int cols) {
     int64_t* ds = h->d_stage2[t];
     hipError_t e = hipSuccess;
     if (h->dread_valid[t]) e = hipStreamWaitEvent(h->cstream, h->ev_dread[t], 0);
-    if (e == hipSuccess) e = hipMemcpyAsync(ds, hs, (size_t)n * 8, hipMemcpyHostToDevice, h->cstream);
-    if (e == hipSuccess) e = hipMemcpyAsync(ds + cap, hs + cap, (size_t)n * 8, hipMemcpyHostToDevice, h->cstream);
-    if (e == hipSuccess && (cols & GW_STAGE_VALUE))
-        e = hipMemcpyAsync(ds + 2 * cap, hs + 2 * cap, (size_t)n * 8, hipMemcpyHostToDevice, h->cstream);
-    if (e == hipSuccess && (cols & GW_STAGE_KEY_HASH))
-        e = hipMemcpyAsync(ds + 3 * cap, hs + 3 * cap, (size_t)n * 4, hipMemcpyHostToDevice, h->cstream);
+    // the columns (key, ts, value, key hash), each cut into one piece per copy stream
+    const int ns = h->cx.empty() ? 1 : (int)h->cx.size();
+    if (ns > 1 && e == hipSuccess) {
+        e = hipEventRecord(h->ev_fork, h->cstream);
+        for (int k = 0; k < ns && e == hipSuccess; ++k) e = hipStreamWaitEvent(h->cx[k], h->ev_fork, 0);
+    }
+    const int64_t piece = (n + ns - 1) / ns;
+    for (int c = 0; c < 4 && e == hipSuccess; ++c) {
+        if (c == 2 && !(cols & GW_STAGE_VALUE)) continue;
+        if (c == 3 && !(cols & GW_STAGE_KEY_HASH)) continue;
+        const size_t w = c == 3 ? 4 : 8;
+        char* d = reinterpret_cast<char*>(ds + c * cap);
+        const char* hsrc = reinterpret_cast<const char*>(hs + c * cap);
+        for (int k = 0; k < ns && e == hipSuccess; ++k) {
+            const int64_t lo = k * piece, hi = std::min(n, lo + piece);
+            if (hi > lo)
+                e = hipMemcpyAsync(d + lo * w, hsrc + lo * w, (size_t)(hi - lo) * w, hipMemcpyHostToDevice,
+                                   ns > 1 ? h->cx[k] : h->cstream);
+        }
+    }
+    if (ns > 1)
+        for (int k = 0; k < ns && e == hipSuccess; ++k) {
+            e = hipEventRecord(h->cx_ev[k], h->cx[k]);
+            if (e == hipSuccess) e = hipStreamWaitEvent(h->cstream, h->cx_ev[k], 0);
+        }
     if (e == hipSuccess) e = hipEventRecord(h->ev_slot[slot], h->cstream);
     if (e != hipSuccess) return h->fail(GW_E_DEVICE, "H2D: %s", hipGetErrorString(e));
     h->slot_used[slot] = true;

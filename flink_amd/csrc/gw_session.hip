@@ -141,7 +141,11 @@ __host__ __device__ __forceinline__ int64_t due_blocks(int64_t cap) { return (ca
 __device__ __forceinline__ int64_t* dsum_of(const TableView& t) { return due_of(t) + (t.cap + 1); }
 __device__ __forceinline__ void due_set(const TableView& t, int64_t slot, int64_t due) {
     due_of(t)[slot] = due;
-    if (due != INT64_MAX) atomicMin((long long*)dsum_of(t) + (slot >> kDueBlkBits), (long long)due);
+    if (due == INT64_MAX) return;
+    // only a lower due time changes the bound; within a kernel the bound only falls, so a
+    // plain read that is stale is high, and costs no more than the atomic it then does
+    long long* d = (long long*)dsum_of(t) + (slot >> kDueBlkBits);
+    if ((long long)due < *d) atomicMin(d, (long long)due);
 }
 
 __device__ __forceinline__ int64_t inline_due(const int64_t* sp, int SW, int64_t lateness) {
@@ -1246,15 +1250,13 @@ __global__ void __launch_bounds__(256) k_sess_kprep(const int64_t* key, const in
 // replays the run from the slot as it was.
 template <int AGG>
 __device__ __forceinline__ bool kseg_fast(const SegArgs& a, const SessList& l, uint32_t e, uint32_t f,
-                                          const HbmRecs& rv, unsigned long long& late, unsigned long long& merges,
-                                          unsigned long long& flags, unsigned long long& ins) {
+                                          const HbmRecs& rv, uint32_t rslot, unsigned long long& late,
+                                          unsigned long long& merges, unsigned long long& flags) {
     constexpr int SW = sess_words<AGG>();
+    if (rslot == ~0u) return false;  // k_sess_kprobe found no slot
     KeyRec r = rv.rec[rv.perm[e]];
     const int64_t key = r.k;
-    bool inserted;
-    const int64_t slot = find_or_insert(a.t, key, inserted);
-    if (slot < 0) return false;
-    ins += inserted;  // (sp_run finds the slot again without inserting)
+    const int64_t slot = rslot;
     int64_t* sp = slot_ptr(a.t, slot);
     const int64_t w1 = sp[1];
     if ((uint64_t)w1 & (kBigMeta | kPuntMeta)) return false;
@@ -1278,6 +1280,23 @@ __device__ __forceinline__ bool kseg_fast(const SegArgs& a, const SessList& l, u
     }
     sp_store<AGG>(a, l, cnt, slot, sp, w1);
     return true;
+}
+
+// The key of every run's first record finds or inserts its slot (rslot[run start]; ~0: no
+// slot): one probe per run with as many in flight as the grid holds, where k_sess_kseg's
+// lanes would wait on each probe between replays.
+__global__ void __launch_bounds__(256) k_sess_kprobe(TableView t, const uint32_t* code, const uint32_t* perm,
+                                                     const KeyRec* rec, int64_t n, uint32_t* rslot,
+                                                     DevStatus* st) {
+    unsigned long long ins = 0;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        if (i > 0 && code[i] == code[i - 1]) continue;
+        bool inserted;
+        const int64_t s = find_or_insert(t, rec[perm[i]].k, inserted);
+        ins += inserted;
+        rslot[i] = s < 0 ? ~0u : (uint32_t)s;
+    }
+    block_commit(st, 0, ins, 0, 0);
 }
 
 // Each wave takes kSegChunk consecutive sorted records, compacts the run heads among them
@@ -1308,7 +1327,7 @@ __global__ void __launch_bounds__(kSegThreads) k_sess_kseg(SegArgs a, const uint
         const uint32_t g = code[i] >> shift;
         int64_t j = i + 1;
         while (j < a.n && (code[j] >> shift) == g) ++j;
-        if (effects || !kseg_fast<AGG>(a, l, (uint32_t)i, (uint32_t)j, rv, late, merges, flags, ins))
+        if (effects || !kseg_fast<AGG>(a, l, (uint32_t)i, (uint32_t)j, rv, a.runs[i], late, merges, flags))
             sp_run<AGG>(a, l, (uint32_t)i, (uint32_t)j, rv, late, merges, flags, ins);
     }
     block_commit(a.st, late, ins, flags, 0, 0, merges);
@@ -2582,6 +2601,9 @@ static int ingest_keyed(SessionState* s, int64_t n, const int64_t* key, const in
     a.diag = getenv("GW_KSEG_FAST") && atoi(getenv("GW_KSEG_FAST")) == 0;
     a.slot = kb.current();
     a.perm = vb.current();
+    a.runs = s->r0;  // per run start: the slot k_sess_kprobe found
+    hipLaunchKernelGGL(k_sess_kprobe, dim3(grid_of(n)), dim3(256), 0, s->stream, s->tv, a.slot, a.perm, rec, n, s->r0,
+                       s->d_st);
     const int64_t C = s->buf_cap;
     a.pu_key = s->ks_pu;
     a.pu_ts = s->ks_pu + C;

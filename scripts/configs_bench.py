@@ -185,8 +185,8 @@ def run(name, args, dev):
 HBM_PEAK_GBS = 8000.0
 # What bounds each config at the round's code, and the next kernel target.
 BOUND_NOTE = {
-    "sessions": "replay (k_sb_replay: one probe + state line per key of the batch, records gathered from "
-                "the L2-resident bucket) -- the next target",
+    "sessions": "keyed sort path: k_sess_kseg (one table probe + slot line per key of the batch, one "
+                "24-B record gather per record) -- the next target; then the 3-pass radix sort",
     "q7": "region pipeline as in the headline (pass 1 + flush), fire at each 10-s window end",
     "q7_first": "two pane operators + the payload log and join",
     "q7_maxby": "MAX pane operator + 4-column log + per-fire probe (k_by_scan)",

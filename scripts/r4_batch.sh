@@ -11,7 +11,7 @@ a)
     "VARIANTS='base d3=GW_LIB_PATH=/root/repo/flink_amd/libgpuwin_d3.so d3u2=GW_LIB_PATH=/root/repo/flink_amd/libgpuwin_d3u2.so' RUNS=2 bash scripts/r4_ab.sh" \
     "GW_HOST_PROFILE=1 timeout -k 10 200 python -u bench.py --no-cpu-baseline --no-host-fed > gpurun_out/r4/bench_hp.json 2> gpurun_out/r4/bench_hp.err && grep 'gw host' gpurun_out/r4/bench_hp.err" \
     "timeout -k 10 200 python -u bench.py --no-cpu-baseline --no-host-fed --no-kernel-timing > gpurun_out/r4/bench_nkt.json 2> gpurun_out/r4/bench_nkt.err && python3 scripts/json_field.py gpurun_out/r4/bench_nkt.json value" \
-    "timeout -k 10 300 python -u bench.py --no-cpu-baseline > gpurun_out/r4/bench_hf3.json 2> gpurun_out/r4/bench_hf3.err && python3 scripts/json_field.py gpurun_out/r4/bench_hf3.json host_fed" \
+    "timeout -k 10 300 python -u bench.py --no-cpu-baseline > gpurun_out/r4/bench_hf3.json 2> gpurun_out/r4/bench_hf3.err && python3 scripts/json_field.py gpurun_out/r4/bench_hf3.json host_fed.value; python3 scripts/json_field.py gpurun_out/r4/bench_hf3.json host_fed.h2d_gbs" \
     "CONFIGS='sessions wordcount q7_first q7_maxby' bash scripts/r4_configs.sh"
   ;;
 b)
@@ -23,16 +23,19 @@ b)
   ;;
 c)
   bash scripts/r4_steps.sh \
-    "GW_SESSION_PATH=sort timeout -k 10 200 python -u -m pytest -x -q --timeout 150 -m gpu tests/test_gpu_multirank.py -k session > gpurun_out/r4/mr_sort.log 2>&1; tail -3 gpurun_out/r4/mr_sort.log" \
-    "timeout -k 10 200 python -u -m pytest -x -q --timeout 150 -m gpu tests/test_gpu_multirank.py -k session > gpurun_out/r4/mr_keyed.log 2>&1; tail -3 gpurun_out/r4/mr_keyed.log" \
-    "TESTS=tests/test_gpu_session_keyed.py TEST_TIMEOUT=400 PER_TEST=150 TAG=keyed NOBENCH=1 bash scripts/r4_check.sh" \
+    "TESTS='tests/test_gpu_session_keyed.py tests/test_gpu_multirank.py' K='session or keyed or sentinel or colliding or punts' TEST_TIMEOUT=400 PER_TEST=150 TAG=keyed NOBENCH=1 bash scripts/r4_check.sh" \
     "CONFIGS=sessions NO_E10M=1 bash scripts/r4_configs.sh"
   ;;
 d)
   bash scripts/r4_steps.sh \
     "timeout -k 10 120 python -u scripts/h2d_probe.py && HSA_ENABLE_SDMA=0 timeout -k 10 120 python -u scripts/h2d_probe.py" \
-    "HSA_ENABLE_SDMA=0 timeout -k 10 300 python -u bench.py --no-cpu-baseline > gpurun_out/r4/bench_hf_nosdma.json 2> gpurun_out/r4/bench_hf_nosdma.err; python3 scripts/json_field.py gpurun_out/r4/bench_hf_nosdma.json host_fed" \
-    "GW_DRAIN_DEBUG=1 timeout -k 10 300 python -u bench.py --no-cpu-baseline > gpurun_out/r4/bench_hf4.json 2> gpurun_out/r4/bench_hf4.err; grep -c drain gpurun_out/r4/bench_hf4.err; grep drain gpurun_out/r4/bench_hf4.err | sed -E 's/[0-9]+ rows/N rows/' | sort | uniq -c; python3 scripts/json_field.py gpurun_out/r4/bench_hf4.json host_fed" \
+    "HSA_ENABLE_SDMA=0 timeout -k 10 300 python -u bench.py --no-cpu-baseline > gpurun_out/r4/bench_hf_nosdma.json 2> gpurun_out/r4/bench_hf_nosdma.err; python3 scripts/json_field.py gpurun_out/r4/bench_hf_nosdma.json host_fed.value; python3 scripts/json_field.py gpurun_out/r4/bench_hf_nosdma.json host_fed.h2d_gbs" \
+    "GW_DRAIN_DEBUG=1 GW_STAGE_STREAMS=2 timeout -k 10 300 python -u bench.py --no-cpu-baseline > gpurun_out/r4/bench_hf_s2.json 2> gpurun_out/r4/bench_hf_s2.err; python3 scripts/json_field.py gpurun_out/r4/bench_hf_s2.json host_fed.value; python3 scripts/json_field.py gpurun_out/r4/bench_hf_s2.json host_fed.h2d_gbs; grep drain gpurun_out/r4/bench_hf_s2.err | sed -E 's/[0-9]+ rows/N rows/' | sort | uniq -c" \
+    "GW_STAGE_STREAMS=4 timeout -k 10 300 python -u bench.py --no-cpu-baseline > gpurun_out/r4/bench_hf_s4.json 2> gpurun_out/r4/bench_hf_s4.err; python3 scripts/json_field.py gpurun_out/r4/bench_hf_s4.json host_fed.value; python3 scripts/json_field.py gpurun_out/r4/bench_hf_s4.json host_fed.h2d_gbs" \
+    "timeout -k 10 500 python -u scripts/configs_bench.py --only wordcount,ysb,q7,sessions,q7_first,q7_maxby > gpurun_out/r4/configs_plain.log 2> gpurun_out/r4/configs_plain.err; grep -c '^{' gpurun_out/r4/configs_plain.log"
+  ;;
+e)
+  bash scripts/r4_steps.sh \
     "CONFIGS='q7 ysb' bash scripts/r4_configs.sh"
   ;;
 *)
