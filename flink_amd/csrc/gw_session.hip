@@ -2641,15 +2641,16 @@ static int sb_finish(SessionState* s, std::string& err) {
     return ingest_sorted(s, n_punt, s->sb_pu[0], s->sb_pu[1], s->sb_pu[2], s->sb_wm, err);
 }
 
-// GW_SESSION_PATH=keyed|region|sort picks the ingest path (GW_SESSION_SORT_BITS, the sort
-// path's group tests, implies sort).  The keyed sort path is the default: on the sessions
-// config the bucketed path measured slower (its per-bucket replay is
-// latency-bound), and the slot sort path probes the table once per record.
+// GW_SESSION_PATH=sort|keyed|region picks the ingest path (GW_SESSION_SORT_BITS, the sort
+// path's group tests, implies sort).  The slot sort path is the default: on the sessions
+// config the keyed and bucketed paths measured slower (all three are bound by
+// random line accesses -- probes, record gathers, slot lines -- and the slot sort path makes
+// the fewest per record).
 enum { kPathKeyed = 0, kPathRegion = 1, kPathSort = 2 };
 static int session_path() {
     const char* p = getenv("GW_SESSION_PATH");
-    if (p) return !strcmp(p, "sort") ? kPathSort : !strcmp(p, "region") ? kPathRegion : kPathKeyed;
-    return getenv("GW_SESSION_SORT_BITS") ? kPathSort : kPathKeyed;
+    if (p) return !strcmp(p, "keyed") ? kPathKeyed : !strcmp(p, "region") ? kPathRegion : kPathSort;
+    return kPathSort;
 }
 
 int session_ingest(SessionState* s, int64_t n, const int64_t* key, const int64_t* ts, const int64_t* val, int64_t wm,
