@@ -51,6 +51,30 @@ def main():
         src.copy_(dsrc, non_blocking=True)
 
     out["d2h_gbs"] = nbytes / timed(d2h) / 1e9
+    # the library's own pinned slots: hipHostMalloc with each flag set, copied as three
+    # 80-MB columns with hipMemcpyAsync (what gw_stage_send does)
+    import ctypes
+    hip = ctypes.CDLL("libamdhip64.so")
+    hip.hipHostMalloc.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t, ctypes.c_uint]
+    hip.hipMemcpyAsync.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p]
+    hip.hipHostFree.argtypes = [ctypes.c_void_p]
+    stream = torch.cuda.current_stream().cuda_stream
+    for name, flags in (("default", 0x0), ("noncoherent", 0x80000000), ("coherent", 0x40000000),
+                        ("portable", 0x1)):
+        ptr = ctypes.c_void_p()
+        if hip.hipHostMalloc(ctypes.byref(ptr), nbytes, flags) != 0:
+            out[f"hm_{name}"] = "alloc failed"
+            continue
+        ctypes.memset(ptr, 1, nbytes)
+        col = nbytes // 3
+
+        def three(ptr=ptr, col=col):
+            for c in range(3):
+                hip.hipMemcpyAsync(ctypes.c_void_p(dst.data_ptr() + c * col), ctypes.c_void_p(ptr.value + c * col),
+                                   col, 1, ctypes.c_void_p(stream))
+
+        out[f"hm_{name}_3col_gbs"] = nbytes / timed(three) / 1e9
+        hip.hipHostFree(ptr)
     print(json.dumps(out))
 
 

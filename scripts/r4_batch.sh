@@ -36,6 +36,8 @@ d)
   ;;
 e)
   bash scripts/r4_steps.sh \
+    "timeout -k 10 120 python -u scripts/h2d_probe.py" \
+    "GW_HOST_PROFILE=1 timeout -k 10 300 python -u scripts/configs_bench.py --only q7 --no-cpu-baseline > gpurun_out/r4/q7_hp.log 2> gpurun_out/r4/q7_hp.err; grep 'gw host' gpurun_out/r4/q7_hp.err; python3 scripts/json_field.py gpurun_out/r4/q7_hp.log value" \
     "CONFIGS='q7 ysb' bash scripts/r4_configs.sh"
   ;;
 *)
