@@ -581,7 +581,10 @@ struct gw_handle {
     }
     int ensure_deferred(int64_t need) {
         if (need <= def_cap) return GW_OK;
-        int64_t nc = std::max<int64_t>(need + (need > (1 << 24) ? need / 8 : need / 2), 1 << 16);
+        // 1.5x: a reallocation costs a sync, ~1 ms of hipMalloc and a copy (measured on the Q7
+        // stream, whose few values beyond the narrow record's 28 bits defer and grow the list
+        // over a fire cycle), so the list grows in few steps
+        int64_t nc = std::max<int64_t>(need + need / 2, 1 << 16);
         for (int b = 0; b < 2; ++b) {
             int64_t* nk; int64_t* np; int64_t* n0; int64_t* n1;
             HIPCHECK(hipMalloc((void**)&nk, nc * 8));
@@ -1318,6 +1321,11 @@ struct gw_handle {
         hp.lap(7);
         if ((rc = maybe_grow(nrec))) return rc;
         hp.lap(8);
+        // room for every deferred entry the launches since the last exact status may have
+        // written; when that bound outgrows the list, learn the exact count first (one sync)
+        // rather than growing it by the bound (a reallocation: a sync and a copy) -- the bound
+        // keeps growing while host writes leave the published status slots stale
+        if (lazy_recs > 0 && (int64_t)h_st->n_deferred + lazy_recs + nrec > def_cap && (rc = refresh())) return rc;
         if ((rc = ensure_deferred((int64_t)h_st->n_deferred + lazy_recs + nrec))) return rc;
         hp.lap(9);
         IngestArgs a;

@@ -40,6 +40,17 @@ e)
     "GW_HOST_PROFILE=1 timeout -k 10 300 python -u scripts/configs_bench.py --only q7 --no-cpu-baseline > gpurun_out/r4/q7_hp.log 2> gpurun_out/r4/q7_hp.err; grep 'gw host' gpurun_out/r4/q7_hp.err; python3 scripts/json_field.py gpurun_out/r4/q7_hp.log value" \
     "CONFIGS='q7 ysb' bash scripts/r4_configs.sh"
   ;;
+f)
+  export TMPDIR=/tmp
+  bash scripts/r4_steps.sh \
+    "timeout -k 10 300 rocprofv3 --memory-copy-trace --kernel-trace -d gpurun_out/r4/hf_trace -o run --output-format csv -- python3 -u bench.py --steps 2 --warmup 1 --no-cpu-baseline --host-fed-steps 21 > gpurun_out/r4/hf_trace.json 2> gpurun_out/r4/hf_trace.err; python3 scripts/json_field.py gpurun_out/r4/hf_trace.json host_fed.value; ls gpurun_out/r4/hf_trace; python3 scripts/copy_timeline.py gpurun_out/r4/hf_trace/run_memory_copy_trace.csv | tail -45"
+  ;;
+g)
+  bash scripts/r4_steps.sh \
+    "GW_HOST_PROFILE=1 timeout -k 10 300 python -u scripts/configs_bench.py --only q7 --no-cpu-baseline > gpurun_out/r4/q7_hp2.log 2> gpurun_out/r4/q7_hp2.err; grep 'gw host' gpurun_out/r4/q7_hp2.err; python3 scripts/json_field.py gpurun_out/r4/q7_hp2.log value" \
+    "timeout -k 10 400 python -u bench.py > gpurun_out/r4/bench_final.json 2> gpurun_out/r4/bench_final.err; python3 scripts/json_field.py gpurun_out/r4/bench_final.json value; python3 scripts/json_field.py gpurun_out/r4/bench_final.json roofline.frac; python3 scripts/json_field.py gpurun_out/r4/bench_final.json host_fed.value" \
+    "TAG=r4hl timeout -k 10 700 bash scripts/headline_profile.sh > gpurun_out/r4/hl_profile.log 2>&1; tail -30 gpurun_out/r4/hl_profile.log"
+  ;;
 *)
   echo "unknown BATCH"; exit 2 ;;
 esac
