@@ -11,7 +11,8 @@ b = json.loads(open(bench).read().strip().splitlines()[-1])
 rows = [r for r in csv.DictReader(open(trace)) if "gw::" in r["Kernel_Name"]]
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 name = lambda r: r["Kernel_Name"].split("(")[0].replace("void gw::", "").replace("gw::", "").split("<")[0]
-applies = [i for i, r in enumerate(rows) if name(r) == "k_rgn_apply"]
+APPLY = ("k_rgn_apply", "k_rgn_apply_nar")
+applies = [i for i, r in enumerate(rows) if name(r) in APPLY]
 # bench: warmup, flush (apply #k), timed steps (fires flush), final flush (last apply)
 steps, warm = b["steps"], b["warmup"]
 p1_idx = [i for i, r in enumerate(rows) if name(r) == "k_rgn_p1"]
@@ -22,7 +23,7 @@ dur = {}
 for r in rows[start + 1:end + 1]:
     n = name(r)
     dur.setdefault(n, []).append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6)
-pipe = ["k_rgn_p1", "k_rgn_plan1", "k_rgn_plan2", "k_rgn_plan3", "k_rgn_p2", "k_rgn_apply"]
+pipe = ["k_rgn_p1", "k_rgn_plan1", "k_rgn_plan2", "k_rgn_plan3", "k_rgn_p2", "k_rgn_apply", "k_rgn_apply_nar"]
 tot = sum(sum(dur.get(k, [])) for k in pipe)
 nb = len(dur.get("k_rgn_p1", []))
 print(f"timed batches (k_rgn_p1 dispatches): {nb} (bench steps {steps})")

@@ -2,7 +2,7 @@
 passes (FETCH_SIZE, WRITE_SIZE) over `bench.py --steps S --warmup W` (every batch is
 applied by the end of the run: bench.py flushes before and after the timed steps).
 
-Pipeline kernels: k_rgn_p1 (per batch), k_rgn_plan1/2/3, k_rgn_p2, k_rgn_apply (per
+Pipeline kernels: k_rgn_p1 (per batch), k_rgn_plan1/2/3, k_rgn_p2, k_rgn_apply or k_rgn_apply_nar (per
 flush).  bytes/batch = sum over those dispatches / number of k_rgn_p1 dispatches.
 gfx950 correction (MI355X_MICROARCH.md, HBM): FETCH_SIZE reports half the bytes of wide
 streaming reads -> x2; WRITE_SIZE as is.  Both counters are in KiB.
@@ -15,7 +15,7 @@ import json
 import os
 import sys
 
-PIPE = ("k_rgn_p1", "k_rgn_plan1", "k_rgn_plan2", "k_rgn_plan3", "k_rgn_p2", "k_rgn_apply")
+PIPE = ("k_rgn_p1", "k_rgn_plan1", "k_rgn_plan2", "k_rgn_plan3", "k_rgn_p2", "k_rgn_apply", "k_rgn_apply_nar")
 
 root, agg, nb, out = sys.argv[1], sys.argv[2], int(sys.argv[3]), sys.argv[4]
 tot = {"FETCH_SIZE": {}, "WRITE_SIZE": {}}
