@@ -312,24 +312,25 @@ struct gw_handle {
     // Host-ingest staging (gw_ingest, gw_stage_*).  Pinned host slots (key | ts | value columns
     // of slot_cap records, then the int32 key hashes) that a caller fills in place (a JVM writes
     // its records straight into them) or gw_ingest copies into; each batch goes over PCIe on a
-    // copy stream into one of two device staging buffers used in turn, so the H2D of batch b+1
-    // runs while batch b is aggregated.  A slot is refilled only after its H2D (ev_slot); a
+    // copy stream into one of three device staging buffers used in turn, so the H2D of batches
+    // b+1 and b+2 runs while batch b is aggregated, fired and drained.  A slot is refilled only after its H2D (ev_slot); a
     // device buffer is overwritten only after the ingest that read it (ev_dread).
     std::vector<int64_t*> h_slot;
     std::vector<hipEvent_t> ev_slot;
     std::vector<bool> slot_used;
     int64_t slot_cap = 0;
     int stage_next = 0;             // gw_ingest's next slot (of the first two)
-    int64_t* d_stage2[2] = {nullptr, nullptr};
-    hipEvent_t ev_dread[2] = {nullptr, nullptr};
-    bool dread_valid[2] = {false, false};
+    static constexpr int kStageBufs = 3;  // device buffers: up to two batches sent ahead of the ingest
+    int64_t* d_stage2[kStageBufs] = {};
+    hipEvent_t ev_dread[kStageBufs] = {};
+    bool dread_valid[kStageBufs] = {};
     int dturn = 0;                  // the device buffer the next staged ingest reads
     int send_turn = 0;              // the device buffer the next H2D fills
     // a slot already sent ahead (gw_stage_send) into device buffer t, not yet ingested
-    bool pre_valid[2] = {false, false};
-    int pre_slot[2] = {-1, -1};
-    int64_t pre_n[2] = {0, 0};
-    int pre_cols[2] = {0, 0};
+    bool pre_valid[kStageBufs] = {};
+    int pre_slot[kStageBufs] = {-1, -1, -1};
+    int64_t pre_n[kStageBufs] = {};
+    int pre_cols[kStageBufs] = {};
     hipStream_t cstream = nullptr;
     // staged H2D split over extra copy streams (GW_STAGE_STREAMS > 1): several DMA queues
     // in flight, joined back into cstream by events
@@ -638,7 +639,7 @@ struct gw_handle {
         h_slot.clear();
         ev_slot.clear();
         slot_used.clear();
-        for (int t = 0; t < 2; ++t) {
+        for (int t = 0; t < kStageBufs; ++t) {
             if (d_stage2[t]) hipFree(d_stage2[t]);
             d_stage2[t] = nullptr;
             dread_valid[t] = false;
@@ -667,7 +668,7 @@ struct gw_handle {
                 }
             }
         }
-        for (int t = 0; t < 2; ++t) {
+        for (int t = 0; t < kStageBufs; ++t) {
             if (!ev_dread[t]) HIPCHECK(hipEventCreateWithFlags(&ev_dread[t], hipEventDisableTiming));
             HIPCHECK(hipMalloc((void**)&d_stage2[t], (size_t)cap * 28));
         }
@@ -2523,7 +2524,7 @@ int gw_destroy(gw_handle* h) {
     if (h->h_bounce) hipHostFree(h->h_bounce);
     for (auto ev : h->ev_bounce)
         if (ev) hipEventDestroy(ev);
-    for (int t = 0; t < 2; ++t)
+    for (int t = 0; t < gw_handle::kStageBufs; ++t)
         if (h->ev_dread[t]) hipEventDestroy(h->ev_dread[t]);
     if (h->cstream) hipStreamDestroy(h->cstream);
     for (size_t i = 0; i < h->cx.size(); ++i) {
@@ -2899,7 +2900,7 @@ int gw_ingest(gw_handle* h, int64_t n, const int64_t* key, const int32_t* key_ha
 // ingest that last read that buffer).  cols: GW_STAGE_VALUE | GW_STAGE_KEY_HASH.
 static int stage_send(gw_handle* h, int slot, int64_t n, int cols) {
     const int t = h->send_turn;
-    if (h->pre_valid[t]) return h->fail(GW_E_STATE, "staging: both device buffers hold batches not yet ingested");
+    if (h->pre_valid[t]) return h->fail(GW_E_STATE, "staging: every device buffer holds a batch not yet ingested");
     const int64_t cap = h->slot_cap;
     int64_t* hs = h->h_slot[slot];
     int64_t* ds = h->d_stage2[t];
@@ -2937,7 +2938,7 @@ static int stage_send(gw_handle* h, int slot, int64_t n, int cols) {
     h->pre_slot[t] = slot;
     h->pre_n[t] = n;
     h->pre_cols[t] = cols;
-    h->send_turn ^= 1;
+    h->send_turn = (h->send_turn + 1) % gw_handle::kStageBufs;
     return GW_OK;
 }
 
@@ -2947,13 +2948,15 @@ static int stage_ingest(gw_handle* h, int slot, int64_t n, bool with_hash, bool 
     const int t = h->dturn;
     int rc;
     if (!h->pre_valid[t]) {
+        if (h->send_turn != t)  // a later batch went ahead of this one
+            return h->fail(GW_E_STATE, "staging: ingest of slot %d, which was not sent, after later batches were", slot);
         if ((rc = stage_send(h, slot, n, cols))) return rc;
     } else if (h->pre_slot[t] != slot || h->pre_n[t] != n || h->pre_cols[t] != cols) {
         return h->fail(GW_E_STATE, "staging: ingest of slot %d (%lld records) while slot %d (%lld) was sent first",
                        slot, (long long)n, h->pre_slot[t], (long long)h->pre_n[t]);
     }
     h->pre_valid[t] = false;
-    h->dturn ^= 1;
+    h->dturn = (h->dturn + 1) % gw_handle::kStageBufs;
     const int64_t cap = h->slot_cap;
     int64_t* ds = h->d_stage2[t];
     int32_t* dh = (int32_t*)(ds + 3 * cap);

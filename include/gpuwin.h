@@ -189,7 +189,7 @@ int  gw_ingest(gw_handle* h, int64_t n, const int64_t* key, const int32_t* key_h
  * key / key_hash / ts / value columns (any pointer may be NULL), once the slot's previous
  * transfer has read it.  gw_ingest_stage: the slot's first n records, as gw_ingest would take
  * them (cols: GW_STAGE_VALUE and / or GW_STAGE_KEY_HASH); the transfer runs on a copy stream
- * into one of two device buffers used in turn, so it overlaps the previous batch's kernels.  The
+ * into one of three device buffers used in turn, so it overlaps the previous batches' kernels.  The
  * slot may be refilled after the next gw_stage_columns on it returns.  Not for composite or
  * first-element handles (GW_E_UNSUPPORTED). */
 #define GW_STAGE_VALUE    1
@@ -199,9 +199,9 @@ int  gw_stage_columns(gw_handle* h, int32_t slot, int64_t** key, int32_t** key_h
                       int64_t** value);
 int  gw_ingest_stage(gw_handle* h, int32_t slot, int64_t n, int32_t cols);
 /* Send a filled slot's first n records over PCIe ahead of its gw_ingest_stage (into the next of
- * the two device buffers, once the ingest that last read it is done), e.g. batch b+1's while
- * batch b's rows are drained.  At most one batch ahead: the next gw_ingest_stage must name the
- * same slot, n and cols (GW_E_STATE otherwise). */
+ * the three device buffers, once the ingest that last read it is done), e.g. batches b+1 and b+2
+ * while batch b is fired and its rows drained.  At most two batches ahead; the gw_ingest_stage
+ * calls must name the sent slots, n and cols in the order they were sent (GW_E_STATE otherwise). */
 int  gw_stage_send(gw_handle* h, int32_t slot, int64_t n, int32_t cols);
 /* Same, with the columns already resident in device memory (d_* are device
  * pointers).  `stream` is the hipStream_t the inputs were produced on (NULL = the

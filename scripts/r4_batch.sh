@@ -51,6 +51,11 @@ g)
     "timeout -k 10 400 python -u bench.py > gpurun_out/r4/bench_final.json 2> gpurun_out/r4/bench_final.err; python3 scripts/json_field.py gpurun_out/r4/bench_final.json value; python3 scripts/json_field.py gpurun_out/r4/bench_final.json roofline.frac; python3 scripts/json_field.py gpurun_out/r4/bench_final.json host_fed.value" \
     "TAG=r4hl timeout -k 10 700 bash scripts/headline_profile.sh > gpurun_out/r4/hl_profile.log 2>&1; tail -30 gpurun_out/r4/hl_profile.log"
   ;;
+h)
+  bash scripts/r4_steps.sh \
+    "TESTS=tests/test_gpu_staged_ingest.py TEST_TIMEOUT=300 PER_TEST=150 TAG=stg2 NOBENCH=1 bash scripts/r4_check.sh" \
+    "timeout -k 10 400 python -u bench.py --no-cpu-baseline > gpurun_out/r4/bench_hf5.json 2> gpurun_out/r4/bench_hf5.err; python3 scripts/json_field.py gpurun_out/r4/bench_hf5.json value; python3 scripts/json_field.py gpurun_out/r4/bench_hf5.json host_fed.value; python3 scripts/json_field.py gpurun_out/r4/bench_hf5.json host_fed.h2d_gbs"
+  ;;
 *)
   echo "unknown BATCH"; exit 2 ;;
 esac

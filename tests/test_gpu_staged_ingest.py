@@ -1,6 +1,6 @@
 """Staged host ingest (gw_stage_alloc / gw_stage_columns / gw_ingest_stage): the columns a JVM
 operator writes straight into library-owned pinned slots, sent over PCIe on a copy stream into
-two device buffers used in turn.  Against the oracle on the same stream: slots refilled many
+three device buffers used in turn.  Against the oracle on the same stream: slots refilled many
 times (each refill waits for the slot's previous transfer), more batches than slots, key hashes
 (String-like keys), COUNT without a value column, and the host path gw_ingest on top of it."""
 import numpy as np
@@ -83,16 +83,18 @@ def test_staged_rejections():
         op.close()
 
 
+@pytest.mark.parametrize("ahead", [1, 2])
 @pytest.mark.parametrize("agg", ["sum_i64", "count"])
-def test_sent_ahead_matches_oracle(oracle_lib, agg):
-    """gw_stage_send: batch b+1 goes over PCIe while batch b is ingested, fired and drained
-    (into pinned host arrays, which the D2H writes directly) -- the host_fed leg's loop."""
+def test_sent_ahead_matches_oracle(oracle_lib, agg, ahead):
+    """gw_stage_send: batches b+1 (.. b+ahead) go over PCIe while batch b is ingested, fired
+    and drained (into pinned host arrays, which the D2H writes directly) -- the host_fed leg's
+    loop."""
     import torch
 
     kw = dict(assigner="sliding", size=2000, slide=500, agg=agg)
     keys, ts, vals, batches = random_stream(seed=63, n=240_000, num_keys=20_000, n_batches=16, agg=agg)
     cap = max(hi - lo for lo, hi, _ in batches)
-    slots = 3
+    slots = 4
     op = gpu_operator(kw, capacity_hint=1 << 16)
     out = [torch.empty(1 << 18, dtype=torch.int64, pin_memory=True).numpy() for _ in range(4)]
     outs = []
@@ -107,14 +109,15 @@ def test_sent_ahead_matches_oracle(oracle_lib, agg):
 
     try:
         op.stage_alloc(slots, cap)
-        fill(0)
-        op.stage_send(0, batches[0][1] - batches[0][0], with_value=agg != "count")
+        for b in range(ahead):
+            fill(b)
+            op.stage_send(b, batches[b][1] - batches[b][0], with_value=agg != "count")
         for b, (lo, hi, wm) in enumerate(batches):
             op.ingest_stage(b % slots, hi - lo, with_value=agg != "count")
-            if b + 1 < len(batches):
-                fill(b + 1)
-                nlo, nhi, _ = batches[b + 1]
-                op.stage_send((b + 1) % slots, nhi - nlo, with_value=agg != "count")
+            if b + ahead < len(batches):
+                fill(b + ahead)
+                nlo, nhi, _ = batches[b + ahead]
+                op.stage_send((b + ahead) % slots, nhi - nlo, with_value=agg != "count")
             op.advance_watermark(wm)
             outs.append(tuple(x.copy() for x in op.drain(out)))
         op.advance_watermark(W.LONG_MAX)
@@ -128,12 +131,13 @@ def test_sent_ahead_matches_oracle(oracle_lib, agg):
 def test_sent_ahead_order_is_checked():
     op = gpu_operator(dict(assigner="tumbling", size=1000, slide=1000, agg="sum_i64"))
     try:
-        op.stage_alloc(3, 100)
+        op.stage_alloc(4, 100)
         op.stage_send(0, 10)
         with pytest.raises(N.GpuWinError):
             op.ingest_stage(1, 10)  # slot 0 was sent first
         op.stage_send(1, 10)
+        op.stage_send(2, 10)
         with pytest.raises(N.GpuWinError):
-            op.stage_send(2, 10)  # one batch ahead at most
+            op.stage_send(3, 10)  # two batches ahead at most (three device buffers)
     finally:
         op.close()
