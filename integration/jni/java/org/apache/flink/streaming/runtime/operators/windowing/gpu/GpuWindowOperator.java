@@ -699,7 +699,7 @@ public class GpuWindowOperator<IN, K>
     private static native int nativeStageAlloc(long h, int slots, int cap);
     private static native ByteBuffer nativeStageColumn(long h, int slot, int which, int cap);
     private static native void nativeIngestStage(long h, int slot, int n, int cols);
-    /** gw_stage_send: a complete slot over PCIe ahead of its nativeIngestStage (one batch ahead). */
+    /** gw_stage_send: a complete slot over PCIe ahead of its nativeIngestStage (up to two batches ahead). */
     private static native void nativeStageSend(long h, int slot, int n, int cols);
     private static native long nativeStaggerOffset(int stagger, long processingTime, double random01, long size,
                                                    long globalOffset);
