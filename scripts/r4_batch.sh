@@ -56,6 +56,11 @@ h)
     "TESTS=tests/test_gpu_staged_ingest.py TEST_TIMEOUT=300 PER_TEST=150 TAG=stg2 NOBENCH=1 bash scripts/r4_check.sh" \
     "timeout -k 10 400 python -u bench.py --no-cpu-baseline > gpurun_out/r4/bench_hf5.json 2> gpurun_out/r4/bench_hf5.err; python3 scripts/json_field.py gpurun_out/r4/bench_hf5.json value; python3 scripts/json_field.py gpurun_out/r4/bench_hf5.json host_fed.value; python3 scripts/json_field.py gpurun_out/r4/bench_hf5.json host_fed.h2d_gbs"
   ;;
+full)
+  bash scripts/r4_steps.sh \
+    "TESTS=tests TEST_TIMEOUT=1000 PER_TEST=300 TAG=full2 NOBENCH=1 bash scripts/r4_check.sh" \
+    "timeout -k 10 200 python -u -c 'import __graft_entry__ as g; g.smoke()' > gpurun_out/r4/smoke.log 2>&1; tail -5 gpurun_out/r4/smoke.log"
+  ;;
 *)
   echo "unknown BATCH"; exit 2 ;;
 esac
