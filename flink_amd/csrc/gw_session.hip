@@ -139,6 +139,55 @@ constexpr int kDueBlkBits = 6;
 constexpr int kDueBlk = 1 << kDueBlkBits;
 __host__ __device__ __forceinline__ int64_t due_blocks(int64_t cap) { return (cap + 1 + kDueBlk - 1) >> kDueBlkBits; }
 __device__ __forceinline__ int64_t* dsum_of(const TableView& t) { return due_of(t) + (t.cap + 1); }
+
+// Dense key array beside the slot lines (after the due summary): a probe reads 8 B per slot
+// instead of a 64-B slot line, so the probes of a batch touch cap x 8 B (268 MB at 2^25
+// slots, mostly resident in the memory-side cache) rather than the whole table.  The slot
+// line keeps its key word too (every reader of a slot's key uses it): a claimed slot gets
+// its key in both places, the dense word first (the CAS), then the line.  Within the kernel
+// that claims a slot another thread may find the key in the dense array before the line
+// holds it; no kernel reads a line's key word in the launch that claims it.
+__host__ __device__ __forceinline__ size_t table_words(int64_t cap, int stride_w) {
+    return (size_t)(cap + 1) * (stride_w + 1) + (size_t)due_blocks(cap) + (size_t)(cap + 1);
+}
+__device__ __forceinline__ int64_t* keys_of(const TableView& t) { return dsum_of(t) + due_blocks(t.cap); }
+
+__device__ __forceinline__ int64_t sess_find_or_insert(const TableView& t, int64_t key, bool& inserted) {
+    inserted = false;
+    if (key == kEmptyKey) return t.cap;  // sentinel slot
+    int64_t* keys = keys_of(t);
+    const uint64_t mask = (uint64_t)t.cap - 1;
+    uint64_t idx = slot_hash(key) & mask;
+    for (int p = 0; p < kMaxProbe; ++p) {
+        const int64_t k = keys[idx];  // plain load: a stale read can only be kEmptyKey (the CAS resolves it)
+        if (k == key) return (int64_t)idx;
+        if (k == kEmptyKey) {
+            const unsigned long long prev = atomicCAS((unsigned long long*)(keys + idx), (unsigned long long)kEmptyKey,
+                                                      (unsigned long long)key);
+            if (prev == (unsigned long long)kEmptyKey) {
+                inserted = true;
+                slot_ptr(t, (int64_t)idx)[0] = key;
+                return (int64_t)idx;
+            }
+            if ((int64_t)prev == key) return (int64_t)idx;
+        }
+        idx = (idx + 1) & mask;
+    }
+    return -1;
+}
+__device__ __forceinline__ int64_t sess_find_slot(const TableView& t, int64_t key) {
+    if (key == kEmptyKey) return t.cap;
+    const int64_t* keys = keys_of(t);
+    const uint64_t mask = (uint64_t)t.cap - 1;
+    uint64_t idx = slot_hash(key) & mask;
+    for (int p = 0; p < kMaxProbe; ++p) {
+        const int64_t k = keys[idx];
+        if (k == key) return (int64_t)idx;
+        if (k == kEmptyKey) return -1;
+        idx = (idx + 1) & mask;
+    }
+    return -1;
+}
 __device__ __forceinline__ void due_set(const TableView& t, int64_t slot, int64_t due) {
     due_of(t)[slot] = due;
     if (due == INT64_MAX) return;
@@ -422,7 +471,7 @@ __global__ void __launch_bounds__(kSegThreads) k_sess_segment(SegArgs a) {
 // The key of main-table slot g moves to the wide table: a wide slot with its sessions.
 __device__ __forceinline__ int64_t wide_slot_of(const TableView& w, int64_t key, unsigned long long& flags) {
     bool inserted;
-    const int64_t g2 = find_or_insert(w, key, inserted);
+    const int64_t g2 = sess_find_or_insert(w, key, inserted);
     if (g2 < 0) flags |= GW_DF_TABLE_FULL;
     return g2;
 }
@@ -436,7 +485,7 @@ __global__ void __launch_bounds__(256) k_sess_migrate(TableView t, TableView w, 
         int64_t* sp = slot_ptr(t, m[0]);
         const int64_t key = m[0] == t.cap ? kEmptyKey : sp[0];
         bool inserted;
-        const int64_t g2 = find_or_insert(w, key, inserted);
+        const int64_t g2 = sess_find_or_insert(w, key, inserted);
         if (g2 < 0) { flags |= GW_DF_TABLE_FULL; continue; }
         ins += inserted;
         int64_t* d = slot_ptr(w, g2);
@@ -476,7 +525,7 @@ __global__ void __launch_bounds__(256) k_sess_wide(SegArgs a) {
         int64_t* sp = slot_ptr(a.t, (int64_t)slot);
         const int64_t key = (int64_t)slot == a.t.cap ? kEmptyKey : sp[0];
         bool inserted;
-        const int64_t g2 = find_or_insert(a.w, key, inserted);
+        const int64_t g2 = sess_find_or_insert(a.w, key, inserted);
         if (g2 < 0) {
             flags |= GW_DF_TABLE_FULL;
             const unsigned long long at = atomicAdd(&a.st->overflow, 1ull);
@@ -529,7 +578,7 @@ __global__ void __launch_bounds__(256) k_sess_prep(const int64_t* key, const int
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
         if (ts && ts[i] == INT64_MIN) flags |= GW_DF_NO_TS;
         bool inserted;
-        int64_t s = find_or_insert(t, key[i], inserted);
+        int64_t s = sess_find_or_insert(t, key[i], inserted);
         ins += inserted;
         if (s < 0) { flags |= GW_DF_TABLE_FULL; s = 0; }
         slot[i] = (uint32_t)s;
@@ -974,7 +1023,7 @@ __device__ __forceinline__ void sp_key(const SegArgs& a, const SessList& l, int6
     int64_t L = 0;
     for (uint32_t q = r0; q < f; ++q) L += rv.key(q) == key;
     bool inserted;
-    const int64_t slot = find_or_insert(a.t, key, inserted);
+    const int64_t slot = sess_find_or_insert(a.t, key, inserted);
     int64_t* sp = slot >= 0 ? slot_ptr(a.t, slot) : nullptr;
     if (sp) ins += inserted;
     const int64_t w1 = sp ? sp[1] : 0;
@@ -1204,7 +1253,7 @@ constexpr size_t kSbReplayLds = (size_t)kSbCap * (24 + 12) + (size_t)(kSbRThread
 // After a replay with punts: clear the punt marks before the sort path replays the list.
 __global__ void __launch_bounds__(256) k_sp_unpunt(TableView t, const int64_t* pk, int64_t n) {
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t slot = find_slot(t, pk[i]);
+        const int64_t slot = sess_find_slot(t, pk[i]);
         if (slot < 0) continue;
         int64_t* sp = slot_ptr(t, slot);
         if ((uint64_t)sp[1] & kPuntMeta) atomicAnd((unsigned long long*)(sp + 1), ~(unsigned long long)kPuntMeta);
@@ -1292,7 +1341,7 @@ __global__ void __launch_bounds__(256) k_sess_kprobe(TableView t, const uint32_t
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
         if (i > 0 && code[i] == code[i - 1]) continue;
         bool inserted;
-        const int64_t s = find_or_insert(t, rec[perm[i]].k, inserted);
+        const int64_t s = sess_find_or_insert(t, rec[perm[i]].k, inserted);
         ins += inserted;
         rslot[i] = s < 0 ? ~0u : (uint32_t)s;
     }
@@ -1501,7 +1550,7 @@ __global__ void __launch_bounds__(256) k_sess_rehash(TableView o, TableView n, i
         if (s[1] == 0) continue;
         const int64_t key = i == o.cap ? kEmptyKey : s[0];
         bool inserted;
-        const int64_t j = find_or_insert(n, key, inserted);
+        const int64_t j = sess_find_or_insert(n, key, inserted);
         if (j < 0) { flags |= GW_DF_TABLE_FULL; continue; }
         ins += inserted;
         int64_t* d = slot_ptr(n, j);
@@ -1532,6 +1581,8 @@ __global__ void __launch_bounds__(256) k_sess_init(TableView t) {
     for (int64_t b = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; b < due_blocks(t.cap);
          b += (int64_t)gridDim.x * blockDim.x)
         dsum_of(t)[b] = INT64_MAX;
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i <= t.cap; i += (int64_t)gridDim.x * blockDim.x)
+        keys_of(t)[i] = kEmptyKey;
 }
 
 // Restore (gw_restore of a session snapshot): one thread per restored key.  A key with at
@@ -1543,7 +1594,7 @@ __global__ void __launch_bounds__(256) k_sess_restore(TableView t, TableView w, 
     unsigned long long ins = 0, flags = 0, ins2 = 0;
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
         bool inserted;
-        const int64_t slot = find_or_insert(t, rk[i], inserted);
+        const int64_t slot = sess_find_or_insert(t, rk[i], inserted);
         ins += inserted;
         if (slot < 0) { flags |= GW_DF_TABLE_FULL; continue; }
         int64_t* sp = slot_ptr(t, slot);
@@ -1562,7 +1613,7 @@ __global__ void __launch_bounds__(256) k_sess_restore(TableView t, TableView w, 
             sp[1] = (int64_t)((fired << 32) | (uint64_t)cnt);
             due_set(t, slot, inline_due(sp, SW, lateness));
         } else {
-            const int64_t g2 = find_or_insert(w, rk[i], inserted);
+            const int64_t g2 = sess_find_or_insert(w, rk[i], inserted);
             if (g2 < 0) { flags |= GW_DF_TABLE_FULL; continue; }
             ins2 += inserted;
             int64_t* d = slot_ptr(w, g2);
@@ -1857,7 +1908,7 @@ __global__ void __launch_bounds__(256) k_cnt_restore(TableView t, const int64_t*
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
         const int64_t* e = ent + i * (2 + words);
         bool inserted;
-        const int64_t j = find_or_insert(t, e[0], inserted);
+        const int64_t j = sess_find_or_insert(t, e[0], inserted);
         if (j < 0) { flags |= GW_DF_TABLE_FULL; continue; }
         ins += inserted;
         int64_t* d = slot_ptr(t, j);
@@ -2014,7 +2065,7 @@ static int alloc_table(SessionState* s, TableView& t, int64_t cap, int ring, int
     t.ring = ring;
     t.words = words;
     t.stride_w = (int)(((2 + ring * words) + 7) / 8 * 8);
-    SCHECK(hipMalloc((void**)&t.base, ((size_t)(cap + 1) * (t.stride_w + 1) + (size_t)due_blocks(cap)) * 8));  // slots + due times + due summary
+    SCHECK(hipMalloc((void**)&t.base, table_words(cap, t.stride_w) * 8));  // slots + due times + due summary + keys
     hipLaunchKernelGGL(k_sess_init, dim3(grid_of(cap + 1)), dim3(256), 0, s->stream, t);
     SCHECK(hipGetLastError());
     return GW_OK;

@@ -61,6 +61,13 @@ full)
     "TESTS=tests TEST_TIMEOUT=1000 PER_TEST=300 TAG=full2 NOBENCH=1 bash scripts/r4_check.sh" \
     "timeout -k 10 200 python -u -c 'import __graft_entry__ as g; g.smoke()' > gpurun_out/r4/smoke.log 2>&1; tail -5 gpurun_out/r4/smoke.log"
   ;;
+i)
+  bash scripts/r4_steps.sh \
+    "TESTS=tests K='session or count' TEST_TIMEOUT=700 PER_TEST=300 TAG=sess_mirror NOBENCH=1 bash scripts/r4_check.sh" \
+    "timeout -k 10 300 python -u scripts/configs_bench.py --only sessions > gpurun_out/r4/sess_mirror.log 2> gpurun_out/r4/sess_mirror.err; python3 scripts/json_field.py gpurun_out/r4/sess_mirror.log value; python3 scripts/json_field.py gpurun_out/r4/sess_mirror.log roofline.device_ms_per_step" \
+    "GW_SESSION_PATH=keyed timeout -k 10 300 python -u scripts/configs_bench.py --only sessions --no-cpu-baseline > gpurun_out/r4/sess_mirror_keyed.log 2> gpurun_out/r4/sess_mirror_keyed.err; python3 scripts/json_field.py gpurun_out/r4/sess_mirror_keyed.log value" \
+    "VARIANTS='base p2d=GW_LIB_PATH=/root/repo/flink_amd/libgpuwin_p2d.so' RUNS=2 bash scripts/r4_ab.sh"
+  ;;
 *)
   echo "unknown BATCH"; exit 2 ;;
 esac
