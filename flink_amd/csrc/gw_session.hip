@@ -432,6 +432,20 @@ __device__ __forceinline__ void seg_run(const SegArgs& a, const SessList& l, int
         if ((x >> a.gshift) != grp) break;
         L += x == slot;
     }
+    if ((int64_t)slot == a.t.cap + 1) {  // keys k_sess_prep found no slot for: replayed after a regrow
+        unsigned long long at = atomicAdd(&a.st->spills, (unsigned long long)L);
+        struct alignas(16) TsVal { int64_t ts, v; };
+        for (int64_t r = i; r < j; ++r) {
+            if (a.slot[r] != slot) continue;
+            const uint32_t idx = a.perm[r];
+            const TsVal tv = reinterpret_cast<const TsVal*>(a.rec)[idx];
+            a.pu_key[at] = a.key[idx];
+            a.pu_ts[at] = tv.ts;
+            a.pu_val[at] = tv.v;
+            ++at;
+        }
+        return;
+    }
     seg_slot<AGG>(a, l, i, j, slot, L, late, merges, flags);
 }
 
@@ -580,7 +594,7 @@ __global__ void __launch_bounds__(256) k_sess_prep(const int64_t* key, const int
         bool inserted;
         int64_t s = sess_find_or_insert(t, key[i], inserted);
         ins += inserted;
-        if (s < 0) { flags |= GW_DF_TABLE_FULL; s = 0; }
+        if (s < 0) { flags |= GW_DF_TABLE_FULL; s = t.cap + 1; }  // no slot: sorts last, the segment punts it
         slot[i] = (uint32_t)s;
         perm[i] = (uint32_t)i;
         if (rec) {
@@ -1394,7 +1408,7 @@ __global__ void __launch_bounds__(256) k_sess_due_scan(TableView t, int64_t wm, 
     __shared__ unsigned cnt;
     __shared__ unsigned long long gbase;
     // an ingest's follow-up (punts or migrations) is pending: the host fires again after it
-    if (st->overflow | st->pad[0]) return;
+    if (st->overflow | st->pad[0] | st->spills) return;
     const int64_t nslots = t.cap + 1, nblk = due_blocks(t.cap);
     const int64_t* due = due_of(t);
     int64_t* dsum = dsum_of(t);
@@ -1508,7 +1522,7 @@ template <int AGG>
 __global__ void __launch_bounds__(256) k_sess_fire_wide(TableView w, int64_t wm, int64_t lateness, int purge,
                                                         int64_t* o_key, int64_t* o_start, int64_t* o_end,
                                                         int64_t* o_res, DevStatus* st) {
-    if (st->overflow | st->pad[0]) return;  // as k_sess_due_scan
+    if (st->overflow | st->pad[0] | st->spills) return;  // as k_sess_due_scan
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i <= w.cap; i += (int64_t)gridDim.x * blockDim.x) {
         if (due_of(w)[i] > wm) continue;
         int64_t* s = slot_ptr(w, i);
@@ -1948,6 +1962,8 @@ struct SessionState {
     // fire launched right after it checks the device counters and skips itself if the
     // follow-up has work (k_sess_due_scan), so the common batch costs one host sync, not two.
     bool sb_pend = false;
+    bool sort_pend = false;  // ... and that ingest took the slot sort path: its tail (sort_tail) waits
+    SegArgs sort_a{};
     int64_t sb_wm = 0, sb_new = 0;
     int64_t* sb_pu[3] = {nullptr, nullptr, nullptr};
     int gshift = 0;          // sessions: the last sort grouped records by slot >> gshift
@@ -2269,7 +2285,7 @@ int session_drain_late(SessionState* s, int64_t* key, int64_t* ts, int64_t* val,
 // Slot per record and the stable grouping by slot (both modes).  Grows the main table to
 // keep its load below 0.7 for `n` possible new keys.
 static int group_records(SessionState* s, int64_t n, const int64_t* key, const int64_t* ts, const int64_t* val,
-                         const uint32_t** sk, const uint32_t** sp, std::string& err) {
+                         const uint32_t** sk, const uint32_t** sp, std::string& err, bool defer = false) {
     int rc;
     if ((double)(s->h_st->used_slots + n) > 0.7 * (double)s->tv.cap &&
         ((double)s->h_st->used_slots > 0.7 * (double)s->tv.cap ||
@@ -2282,6 +2298,9 @@ static int group_records(SessionState* s, int64_t n, const int64_t* key, const i
     for (int attempt = 0;; ++attempt) {
         hipLaunchKernelGGL(k_sess_prep, dim3(grid_of(n)), dim3(256), 0, s->stream, key, ts, val, n, s->tv, s->slot[0],
                            s->perm[0], s->count_mode ? nullptr : s->rec, s->d_st);
+        // deferred (sessions): no host wait here; records without a slot sort last and the
+        // segment punts them for a replay after a regrow (sort_tail)
+        if (defer && !s->count_mode) break;
         if ((rc = session_refresh(s, err))) return rc;
         if (!(s->h_st->flags & GW_DF_TABLE_FULL)) break;
         if (attempt > 4) { err = "session state table full"; return GW_E_OOM; }
@@ -2414,11 +2433,19 @@ static int run_migrate(SessionState* s, std::string& err) {
 // Sort path: slot per record (k_sess_prep), stable radix sort by slot, one thread per key run
 // (k_sess_segment), migrations, then the wide pass over punted runs.  Replays the punt list
 // of the region path, and is the whole ingest under GW_SESSION_PATH=sort.
+static int sort_tail(SessionState* s, SegArgs a, int64_t wm, std::string& err);
+
+// defer: return right after the segment launch (no host wait) when the replay emits nothing
+// (no allowed lateness, no side output); the tail -- migrations, the wide pass over punted
+// runs, records without a slot -- runs at the next sync (sb_finish), and the watermark's fire
+// launched before it skips itself on the device while that work is pending.
 static int ingest_sorted(SessionState* s, int64_t n, const int64_t* key, const int64_t* ts, const int64_t* val,
-                         int64_t wm, std::string& err) {
+                         int64_t wm, std::string& err, bool defer = false) {
     int rc;
     SegArgs a{};
-    if ((rc = group_records(s, n, key, ts, val, &a.slot, &a.perm, err))) return rc;
+    static const bool always = getenv("GW_SESSION_SYNC") && atoi(getenv("GW_SESSION_SYNC")) != 0;
+    defer = defer && !always && s->cfg.allowed_lateness == 0 && !(s->cfg.flags & GW_FLAG_LATE_SIDE_OUTPUT);
+    if ((rc = group_records(s, n, key, ts, val, &a.slot, &a.perm, err, defer))) return rc;
     a.rec = s->rec;
     a.gshift = s->gshift;
     a.key = key;
@@ -2428,13 +2455,39 @@ static int ingest_sorted(SessionState* s, int64_t n, const int64_t* key, const i
     // main pass (st->overflow, pad[0], pad[1] were zeroed by k_sess_prep)
     s->h_st->overflow = s->h_st->pad[0] = s->h_st->pad[1] = 0;
     a.punt = s->r0;
+    const int64_t C = s->buf_cap;  // records without a slot (deferred prep): punt columns
+    a.pu_key = s->ks_pu;
+    a.pu_ts = s->ks_pu + C;
+    a.pu_val = s->ks_pu + 2 * C;
     const int64_t per_block = (int64_t)kSegChunk * (kSegThreads / 64);
     const unsigned gs = (unsigned)((n + per_block - 1) / per_block);
 #define L(A) hipLaunchKernelGGL(k_sess_segment<A>, dim3(gs), dim3(kSegThreads), 0, s->stream, a)
     GW_AGG_SWITCH(s->cfg.agg, L);
 #undef L
     SCHECK(hipGetLastError());
+    if (defer) {
+        s->sort_a = a;
+        s->sort_pend = true;
+        s->sb_pend = true;
+        s->sb_wm = wm;
+        s->sb_new = n;
+        s->fresh = false;
+        return GW_OK;
+    }
     if ((rc = session_refresh(s, err))) return rc;
+    return sort_tail(s, a, wm, err);
+}
+
+// The slot sort path after its segment (h_st fresh): migrations, the wide pass over the
+// punted runs, then the records whose keys found no slot (a deferred prep) after a regrow.
+static int sort_tail(SessionState* s, SegArgs a, int64_t wm, std::string& err) {
+    int rc;
+    const int64_t n_fail = (int64_t)s->h_st->spills;
+    if (n_fail > 0) {  // the prep's TABLE_FULL is handled below, not an error of the passes before
+        if ((rc = zero_word_async(s, offsetof(DevStatus, spills), err))) return rc;
+        SCHECK(launch_status_set(s->d_st, 0, 0, 2, s->stream));  // zero sh[].flags
+        s->h_st->flags &= ~GW_DF_TABLE_FULL;
+    }
     int64_t n_punt = (int64_t)s->h_st->overflow;
     if ((rc = run_migrate(s, err))) return rc;
     // wide pass over the punted runs; runs that do not fit K2 retry after widening
@@ -2461,6 +2514,10 @@ static int ingest_sorted(SessionState* s, int64_t n, const int64_t* key, const i
             if ((rc = ensure_wide(s, n_punt, (int64_t)s->h_st->pad[1], err))) return rc;
         }
         std::swap(rin, rout);
+    }
+    if (n_fail > 0) {
+        if ((rc = regrow(s, s->tv, s->tv.cap * 2, s->tv.ring, false, err))) return rc;
+        if ((rc = ingest_sorted(s, n_fail, a.pu_key, a.pu_ts, a.pu_val, wm, err, false))) return rc;
     }
     return GW_OK;
 }
@@ -2682,6 +2739,10 @@ static int ingest_keyed(SessionState* s, int64_t n, const int64_t* key, const in
 static int sb_finish(SessionState* s, std::string& err) {
     if (!s->sb_pend) return GW_OK;
     s->sb_pend = false;
+    if (s->sort_pend) {
+        s->sort_pend = false;
+        return sort_tail(s, s->sort_a, s->sb_wm, err);
+    }
     int rc;
     const int64_t n_punt = (int64_t)s->h_st->overflow;
     s->stats.session_punted += n_punt;
@@ -2716,7 +2777,7 @@ int session_ingest(SessionState* s, int64_t n, const int64_t* key, const int64_t
     const int path = session_path();  // read per batch: tests switch paths within one process
     rc = path == kPathKeyed    ? ingest_keyed(s, n, key, ts, val, wm, err)
          : path == kPathRegion ? ingest_region(s, n, key, ts, val, wm, err)
-                               : ingest_sorted(s, n, key, ts, val, wm, err);
+                               : ingest_sorted(s, n, key, ts, val, wm, err, true);
     if (rc) return rc;
     if (s->timing) {
         SCHECK(hipEventRecord(ev.second, s->stream));
@@ -2774,7 +2835,7 @@ int session_fire(SessionState* s, int64_t wm, int64_t* fired, std::string& err) 
         }
         if ((rc = sess_sync(s, err))) return rc;
         if (spec) {
-            const bool skipped = s->h_st->overflow || s->h_st->pad[0];
+            const bool skipped = s->h_st->overflow || s->h_st->pad[0] || s->h_st->spills;
             if ((rc = sb_finish(s, err))) return rc;
             if (skipped) continue;  // the follow-up has run: fire over the complete state
         }

@@ -68,6 +68,13 @@ i)
     "GW_SESSION_PATH=keyed timeout -k 10 300 python -u scripts/configs_bench.py --only sessions --no-cpu-baseline > gpurun_out/r4/sess_mirror_keyed.log 2> gpurun_out/r4/sess_mirror_keyed.err; python3 scripts/json_field.py gpurun_out/r4/sess_mirror_keyed.log value" \
     "VARIANTS='base p2d=GW_LIB_PATH=/root/repo/flink_amd/libgpuwin_p2d.so' RUNS=2 bash scripts/r4_ab.sh"
   ;;
+j)
+  bash scripts/r4_steps.sh \
+    "TESTS='tests/test_gpu_session_deferred.py' TEST_TIMEOUT=300 PER_TEST=150 TAG=sdefer NOBENCH=1 bash scripts/r4_check.sh" \
+    "TESTS=tests K='session or count or multirank or staged' TEST_TIMEOUT=700 PER_TEST=300 TAG=sess_defer NOBENCH=1 bash scripts/r4_check.sh" \
+    "timeout -k 10 300 python -u scripts/configs_bench.py --only sessions > gpurun_out/r4/sess_defer.log 2> gpurun_out/r4/sess_defer.err; python3 scripts/json_field.py gpurun_out/r4/sess_defer.log value; python3 scripts/json_field.py gpurun_out/r4/sess_defer.log roofline.device_ms_per_step; python3 scripts/json_field.py gpurun_out/r4/sess_defer.log ms_per_step" \
+    "CONFIGS=sessions NO_E10M=1 bash scripts/r4_configs.sh"
+  ;;
 *)
   echo "unknown BATCH"; exit 2 ;;
 esac
