@@ -851,9 +851,6 @@ __global__ void __launch_bounds__(256) k_rgn_plan3(IngestArgs a) {
     }
 }
 
-#ifndef GW_P2_DIRECT
-#define GW_P2_DIRECT 0
-#endif
 // P2: block (b1, j) -> rounds p2_roff[b1, j] ... of bucket b1, records at p2_off[b1, j].
 template <int AGG, int FMT>
 __global__ void __launch_bounds__(kPartThreads) k_rgn_p2(IngestArgs a) {
@@ -940,12 +937,6 @@ __global__ void __launch_bounds__(kPartThreads) k_rgn_p2(IngestArgs a) {
                 s_r32[jj] = (uint32_t)key[it];
                 continue;
             }
-#if GW_P2_DIRECT
-            if constexpr (NR) {  // experiment: scatter straight to the round's output (L2 merges the lines)
-                a.e_key[base + jj] = key[it];
-                continue;
-            }
-#endif
             s.k[jj] = key[it];
             if constexpr (NR) continue;
             if constexpr (C) {
@@ -959,9 +950,6 @@ __global__ void __launch_bounds__(kPartThreads) k_rgn_p2(IngestArgs a) {
         __syncthreads();
         const int64_t rnd = rnd0 + e0 / kPartTile;
         for (uint32_t jj = threadIdx.x; jj < e1 - e0; jj += blockDim.x) {
-#if GW_P2_DIRECT
-            if constexpr (NR && !N4) break;
-#endif
             if constexpr (N4) {
                 __builtin_nontemporal_store(s_r32[jj], reinterpret_cast<uint32_t*>(a.e_key) + base + jj);
                 continue;
