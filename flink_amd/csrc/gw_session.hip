@@ -2510,7 +2510,12 @@ static int sort_tail(SessionState* s, SegArgs a, int64_t wm, std::string& err) {
         if ((rc = session_refresh(s, err))) return rc;
         n_punt = (int64_t)s->h_st->overflow;
         if (n_punt) {
+            // keys that found no wide slot within the probe limit (hash-colliding keys): a
+            // bigger table spreads them, which the load rule alone would not ask for
+            const bool full = (s->h_st->flags & GW_DF_TABLE_FULL) != 0;
             SCHECK(launch_status_set(s->d_st, 0, 0, 2, s->stream));  // zero sh[].flags (TABLE_FULL of the wide table)
+            s->h_st->flags &= ~GW_DF_TABLE_FULL;
+            if (full && (rc = regrow(s, s->wv, s->wv.cap * 2, s->wv.ring, true, err))) return rc;
             if ((rc = ensure_wide(s, n_punt, (int64_t)s->h_st->pad[1], err))) return rc;
         }
         std::swap(rin, rout);

@@ -75,6 +75,11 @@ j)
     "timeout -k 10 300 python -u scripts/configs_bench.py --only sessions > gpurun_out/r4/sess_defer.log 2> gpurun_out/r4/sess_defer.err; python3 scripts/json_field.py gpurun_out/r4/sess_defer.log value; python3 scripts/json_field.py gpurun_out/r4/sess_defer.log roofline.device_ms_per_step; python3 scripts/json_field.py gpurun_out/r4/sess_defer.log ms_per_step" \
     "CONFIGS=sessions NO_E10M=1 bash scripts/r4_configs.sh"
   ;;
+k)
+  bash scripts/r4_steps.sh \
+    "TESTS='tests/test_gpu_session_deferred.py' TEST_TIMEOUT=300 PER_TEST=150 TAG=sdefer2 NOBENCH=1 bash scripts/r4_check.sh" \
+    "TESTS=tests K='session or count or multirank or staged' TEST_TIMEOUT=700 PER_TEST=300 TAG=sess_defer2 NOBENCH=1 bash scripts/r4_check.sh"
+  ;;
 *)
   echo "unknown BATCH"; exit 2 ;;
 esac

@@ -43,11 +43,14 @@ def test_key_for_hash_inverts_the_slot_hash():
         assert x ^ (x >> 32) == h
 
 
+@pytest.mark.parametrize("gap", [5000, 300])
 @pytest.mark.parametrize("sync", [False, True])
-def test_keys_without_a_slot_replay_after_a_regrow(oracle_lib, monkeypatch, sync):
+def test_keys_without_a_slot_replay_after_a_regrow(oracle_lib, monkeypatch, sync, gap):
+    """gap 5000: each hot key holds one session per batch; gap 300: hot keys open many and
+    move to the wide table, where they collide as well (the wide table then grows too)."""
     if sync:
         monkeypatch.setenv("GW_SESSION_SYNC", "1")
-    kw = dict(assigner="session", gap=300, agg="sum_i64")
+    kw = dict(assigner="session", gap=gap, agg="sum_i64")
     keys, ts, vals, batches = random_stream(seed=71, n=40_000, num_keys=5000, n_batches=4, ts_step=1,
                                             disorder=200, wm_lag=200)
     hot = colliding_keys(300)
