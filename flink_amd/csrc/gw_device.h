@@ -136,7 +136,10 @@ inline void fold_shards(DevStatus* h) {
 
 // Fired-row staging in LDS: rows are appended with LDS atomics and flushed to the
 // global output with one device atomic per flush and coalesced stores.
-constexpr int kRowStage = 1024;
+#ifndef GW_ROW_STAGE
+#define GW_ROW_STAGE 1024
+#endif
+constexpr int kRowStage = GW_ROW_STAGE;  // rows a fire workgroup stages in LDS before one output reservation
 struct RowStage {
     long long k[kRowStage], s[kRowStage], e[kRowStage], r[kRowStage];
     unsigned cnt;

@@ -80,6 +80,10 @@ k)
     "TESTS='tests/test_gpu_session_deferred.py' TEST_TIMEOUT=300 PER_TEST=150 TAG=sdefer2 NOBENCH=1 bash scripts/r4_check.sh" \
     "TESTS=tests K='session or count or multirank or staged' TEST_TIMEOUT=700 PER_TEST=300 TAG=sess_defer2 NOBENCH=1 bash scripts/r4_check.sh"
   ;;
+l)
+  bash scripts/r4_steps.sh \
+    "VARIANTS='base rs512=GW_LIB_PATH=/root/repo/flink_amd/libgpuwin_rs512.so rs256=GW_LIB_PATH=/root/repo/flink_amd/libgpuwin_rs256.so' RUNS=2 bash scripts/r4_ab.sh"
+  ;;
 *)
   echo "unknown BATCH"; exit 2 ;;
 esac
