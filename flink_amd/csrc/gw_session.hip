@@ -2421,12 +2421,21 @@ static int run_migrate(SessionState* s, std::string& err) {
     const int64_t n_mig = (int64_t)s->h_st->pad[0];
     if (!n_mig) return GW_OK;
     if ((rc = ensure_wide(s, n_mig, (int64_t)s->h_st->pad[1], err))) return rc;
-    hipLaunchKernelGGL(k_sess_migrate, dim3(grid_of(n_mig)), dim3(256), 0, s->stream, s->tv, s->wv, s->mig, n_mig,
-                       s->cfg.allowed_lateness, s->d_st);
-    SCHECK(hipGetLastError());
+    // A key that finds no wide slot within the probe limit (hash-colliding keys) leaves its
+    // entry; the table doubles and the whole list runs again (an entry already moved finds its
+    // wide slot and is written again with the same contents).
+    for (int attempt = 0;; ++attempt) {
+        hipLaunchKernelGGL(k_sess_migrate, dim3(grid_of(n_mig)), dim3(256), 0, s->stream, s->tv, s->wv, s->mig, n_mig,
+                           s->cfg.allowed_lateness, s->d_st);
+        SCHECK(hipGetLastError());
+        if ((rc = session_refresh(s, err))) return rc;
+        if (!(s->h_st->flags & GW_DF_TABLE_FULL)) break;
+        if (attempt >= 8) { err = "session wide table full"; return GW_E_OOM; }
+        SCHECK(launch_status_set(s->d_st, 0, 0, 2, s->stream));  // zero sh[].flags
+        s->h_st->flags &= ~GW_DF_TABLE_FULL;
+        if ((rc = regrow(s, s->wv, s->wv.cap * 2, s->wv.ring, true, err))) return rc;
+    }
     if ((rc = zero_word_async(s, offsetof(DevStatus, pad[0]), err))) return rc;  // (the fire's guard)
-    if ((rc = session_refresh(s, err))) return rc;
-    if (s->h_st->flags & GW_DF_TABLE_FULL) { err = "session wide table full"; return GW_E_OOM; }
     return GW_OK;
 }
 
