@@ -83,7 +83,7 @@ struct SegArgs {
     TableView w;            // wide table: ring = K2, words = kWideWords
     uint32_t* punt;         // main pass: runs for the wide table (append at st->overflow)
     int64_t* mig;           // main pass: finished lists of more than K1 sessions (append at st->pad[0])
-    const uint32_t* runs;   // wide pass: run heads to replay
+    const uint32_t* runs;   // wide pass: run heads to replay; keyed path: slot per run start (k_sess_kprobe)
     int64_t n_runs;
     uint32_t* retry;        // wide pass: runs that did not fit K2 (append at st->overflow)
     DevStatus* st;
@@ -91,8 +91,10 @@ struct SegArgs {
     // bucketed ingest (k_sb_part / k_sb_replay)
     const int64_t* p_key;   // the bucket records (P2's buffer, or P1's without P2): keys
     const longlong2* p_tv;  //   and (timestamp, value) pairs
-    int diag;               // GW_SB_EXP=3: count punts by reason (ShardCtr pad words of shards 2 and 3)
-    int64_t* pu_key;        // punted records (arrival order per key), append at st->overflow
+    int diag;               // bucketed: GW_SB_EXP=3 counts punts by reason (ShardCtr pad words of shards 2
+                            // and 3); keyed: GW_KSEG_FAST=0 replays every run through sp_run
+    int64_t* pu_key;        // punted records (arrival order per key), append at st->overflow (bucketed,
+                            // keyed) or st->spills (slot sort: keys the prep found no slot for)
     int64_t* pu_ts;
     int64_t* pu_val;
 };
