@@ -2601,7 +2601,13 @@ static size_t part_lds_bytes(const IngestArgs& a) {
     return (size_t)kPartTile * 8 * (a.t.words == 2 ? 3 : 2) + 2 * kPartTile;
 }
 
-int region_group(int d1_bits) { return std::max(1, std::min(kMaxGroup, 7 * (1 << d1_bits) / 8 * (4096 / kPartTile))); }
+int region_group(int d1_bits) {
+    // GW_P2_GROUP: P1 tiles per P2 workgroup (experiments; default 7/8 of the pass-1 buckets,
+    // so a bucket's runs over a group fill about one 4096-record round)
+    static const int env = getenv("GW_P2_GROUP") ? atoi(getenv("GW_P2_GROUP")) : 0;
+    if (env > 0) return std::min(kMaxGroup, env);
+    return std::max(1, std::min(kMaxGroup, 7 * (1 << d1_bits) / 8 * (4096 / kPartTile)));
+}
 
 // Region path, P1 over one watermark batch: one block per 4096-record tile.
 hipError_t launch_region_p1(const IngestArgs& a, hipStream_t s) {
