@@ -205,7 +205,7 @@ struct IngestArgs {
 constexpr int kPartTile = GW_PART_TILE;  // records per P1 tile / P2 round (LDS-sorted)
 constexpr int kPartBuckets = 256;   // descriptor row width (<= 8 region bits per pass)
 constexpr int kRgnMaxRegions = 65536;
-constexpr int kMaxGroup = 256;      // P1 tiles per P2 block (G = 7/8 of the pass-1 buckets)
+constexpr int kMaxGroup = 256;      // P1 tiles per P2 block (G = 7/4 of the pass-1 buckets; LDS keeps 4 blocks per CU)
 
 struct MergeArgs {
     const int64_t* i_key;

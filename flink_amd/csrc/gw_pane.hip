@@ -2602,11 +2602,12 @@ static size_t part_lds_bytes(const IngestArgs& a) {
 }
 
 int region_group(int d1_bits) {
-    // GW_P2_GROUP: P1 tiles per P2 workgroup (experiments; default 7/8 of the pass-1 buckets,
-    // so a bucket's runs over a group fill about one 4096-record round)
+    // P1 tiles per P2 workgroup: 7/4 of the pass-1 buckets, so a bucket's runs over a group
+    // fill about two 4096-record rounds (one round per workgroup: flush 0.668 -> 0.653 ms at
+    // the headline with two, 0.82 ms with half a round; GW_P2_GROUP overrides for experiments)
     static const int env = getenv("GW_P2_GROUP") ? atoi(getenv("GW_P2_GROUP")) : 0;
     if (env > 0) return std::min(kMaxGroup, env);
-    return std::max(1, std::min(kMaxGroup, 7 * (1 << d1_bits) / 8 * (4096 / kPartTile)));
+    return std::max(1, std::min(kMaxGroup, 7 * (1 << d1_bits) / 4 * (4096 / kPartTile)));
 }
 
 // Region path, P1 over one watermark batch: one block per 4096-record tile.
