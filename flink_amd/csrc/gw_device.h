@@ -160,22 +160,6 @@ __device__ __forceinline__ void stage_flush(RowStage& rs, unsigned long long* cu
     __syncthreads();
 }
 
-// The same with the workgroup's output offset known in advance (rs.base, advanced here).
-__device__ __forceinline__ void stage_flush_at(RowStage& rs, int64_t* ok, int64_t* os, int64_t* oe, int64_t* orr) {
-    __syncthreads();
-    const unsigned c = rs.cnt;
-    const unsigned long long b = rs.base;
-    for (unsigned j = threadIdx.x; j < c; j += blockDim.x) {
-        ok[b + j] = rs.k[j]; os[b + j] = rs.s[j]; oe[b + j] = rs.e[j]; orr[b + j] = rs.r[j];
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        rs.cnt = 0;
-        rs.base = b + c;
-    }
-    __syncthreads();
-}
-
 // Exclusive wave scan of per-lane counts + one atomic per wave.
 __device__ __forceinline__ unsigned long long wave_reserve_n(unsigned long long* ctr, unsigned cnt) {
     const int lane = __lane_id();

@@ -256,10 +256,6 @@ struct FireArgs {
     int64_t* o_end;
     int64_t* o_res;
     DevStatus* st;
-    // 1024 + 1 words of the handle: per-workgroup row counts, then their output offsets (fires
-    // of mask-based aggregates without restored windows count first and write rows with no
-    // atomics on the row cursor; nullptr: one atomic per staged 1024 rows)
-    unsigned long long* blk;
 };
 
 // Late records of fired, not yet cleaned windows (allowed lateness > 0), in (key, arrival)

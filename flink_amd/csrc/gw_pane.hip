@@ -2158,61 +2158,13 @@ __global__ void __launch_bounds__(256) k_deferred_min(const int64_t* pane, int64
 // SoA layout makes every key / mask / cell access coalesced.  Rows are staged in LDS
 // and flushed with one device atomic per flush.  Retired pane arrays are overwritten
 // with the identity unconditionally (full-line coalesced stores).
-// Fire, counting pass (mask-based aggregates, no restored windows): the rows each workgroup of
-// the k_fire launch with the same grid will emit -- a slot emits one row per fired window its
-// presence mask touches -- into a.blk[blockIdx.x].  Reads 1 B of mask per slot.  Then
-// k_fire_offsets turns the counts into output offsets after the row cursor and advances it,
-// so k_fire writes its staged rows with no same-address atomics: on Q5's 10M-row fires those
-// serialised ~10K reservations at the memory side (a quarter of the fire).
-template <int AGG>
-__global__ void __launch_bounds__(256) k_fire_count(FireArgs a) {
-    __shared__ unsigned long long part[4];
-    const int64_t nslots = a.t.cap + 1;
-    const int64_t chunk = ((nslots + gridDim.x - 1) / gridDim.x + 255) / 256 * 256;
-    const int64_t c0 = blockIdx.x * chunk, c1 = min(nslots, c0 + chunk);
-    unsigned long long cnt = 0;
-    for (int64_t g = c0 + threadIdx.x; g < c1; g += blockDim.x) {
-        const uint64_t mask = presence<AGG>(a.t, g);
-        for (int w = 0; w < a.nwin; ++w) cnt += (mask & a.wmask[w]) != 0;
-    }
-    cnt = wave_sum(cnt);
-    if (__lane_id() == 0) part[threadIdx.x >> 6] = cnt;
-    __syncthreads();
-    if (threadIdx.x == 0) a.blk[blockIdx.x] = part[0] + part[1] + part[2] + part[3];
-}
-
-__global__ void __launch_bounds__(1024) k_fire_offsets(FireArgs a, int nblk) {
-    __shared__ unsigned long long wsum[16];
-    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-    const unsigned long long x = t < nblk ? a.blk[t] : 0ull;
-    unsigned long long incl = x;
-    for (int o = 1; o < 64; o <<= 1) {
-        const unsigned long long up = __shfl_up(incl, o);
-        if (lane >= o) incl += up;
-    }
-    if (lane == 63) wsum[w] = incl;
-    __syncthreads();
-    unsigned long long pre = 0, tot = 0;
-    for (int q = 0; q < 16; ++q) {
-        if (q < w) pre += wsum[q];
-        tot += wsum[q];
-    }
-    const unsigned long long base = a.st->rows;
-    __syncthreads();  // every thread has read the cursor before it moves
-    if (t < nblk) a.blk[t] = base + pre + incl - x;
-    if (t == 0) a.st->rows = base + tot;
-}
-
 template <int AGG>
 __global__ void __launch_bounds__(256) k_fire(FireArgs a) {
     __shared__ RowStage rs;
     const int64_t nslots = a.t.cap + 1;
     const int64_t id0 = identity0(AGG);
     const int W = a.t.words;
-    if (threadIdx.x == 0) {
-        rs.cnt = 0;
-        if (a.blk) rs.base = a.blk[blockIdx.x];  // offsets from k_fire_offsets: no reservations
-    }
+    if (threadIdx.x == 0) rs.cnt = 0;
     if (blockIdx.x == 0 && threadIdx.x < kShards) atomicAnd(&a.st->sh[threadIdx.x].occ, ~a.rmask);
     __syncthreads();
     const int64_t chunk = ((nslots + gridDim.x - 1) / gridDim.x + 255) / 256 * 256;
@@ -2231,10 +2183,7 @@ __global__ void __launch_bounds__(256) k_fire(FireArgs a) {
         for (int w = 0; w < a.nwin; ++w) {
             const bool flush = rs.cnt + blockDim.x > kRowStage;  // uniform: read before any append
             __syncthreads();
-            if (flush) {
-                if (a.blk) stage_flush_at(rs, a.o_key, a.o_start, a.o_end, a.o_res);
-                else stage_flush(rs, &a.st->rows, a.o_key, a.o_start, a.o_end, a.o_res);
-            }
+            if (flush) stage_flush(rs, &a.st->rows, a.o_key, a.o_start, a.o_end, a.o_res);
             uint64_t m = mask & a.wmask[w];
             bool ov_hit = false;
             int64_t o0 = 0, o1 = 0;
@@ -2285,8 +2234,7 @@ __global__ void __launch_bounds__(256) k_fire(FireArgs a) {
             }
         }
     }
-    if (a.blk) stage_flush_at(rs, a.o_key, a.o_start, a.o_end, a.o_res);
-    else stage_flush(rs, &a.st->rows, a.o_key, a.o_start, a.o_end, a.o_res);
+    stage_flush(rs, &a.st->rows, a.o_key, a.o_start, a.o_end, a.o_res);
 }
 
 // Fire sweep without restored-window overlay, for passes whose windows cover at most
@@ -2818,16 +2766,7 @@ hipError_t launch_fire(const FireArgs& a, hipStream_t s) {
         return hipGetLastError();
     }
     const int fg = (int)std::min<int64_t>(1024, std::max<int64_t>(1, (a.t.cap + 1 + 255) / 256));
-    FireArgs f = a;
-    const bool mask_agg = !(a.t.agg == GW_COUNT || a.t.agg == GW_AVG_I64 || a.t.agg == GW_AVG_F64);
-    if (!(a.blk && a.nwin > 0 && a.ov.head == nullptr && mask_agg)) f.blk = nullptr;
-    if (f.blk) {
-#define L(A) hipLaunchKernelGGL(k_fire_count<A>, dim3(fg), dim3(256), 0, s, f)
-        GW_AGG_SWITCH(a.t.agg, L);
-#undef L
-        hipLaunchKernelGGL(k_fire_offsets, dim3(1), dim3(1024), 0, s, f, fg);
-    }
-#define L(A) hipLaunchKernelGGL(k_fire<A>, dim3(fg), dim3(256), 0, s, f)
+#define L(A) hipLaunchKernelGGL(k_fire<A>, dim3(fg), dim3(256), 0, s, a)
     GW_AGG_SWITCH(a.t.agg, L);
 #undef L
     return hipGetLastError();

@@ -332,7 +332,6 @@ struct gw_handle {
     int64_t pre_n[kStageBufs] = {};
     int pre_cols[kStageBufs] = {};
     hipStream_t cstream = nullptr;
-    unsigned long long* d_fireblk = nullptr;  // k_fire_count / k_fire_offsets scratch (1025 words)
     // staged H2D split over extra copy streams (GW_STAGE_STREAMS > 1): several DMA queues
     // in flight, joined back into cstream by events
     std::vector<hipStream_t> cx;
@@ -1064,8 +1063,6 @@ struct gw_handle {
             f.ov = ov_view();
             f.k0 = (int64_t)k_first;
             f.nwin = nwin;
-            if (!d_fireblk) HIPCHECK(hipMalloc((void**)&d_fireblk, 1025 * sizeof(unsigned long long)));
-            f.blk = d_fireblk;  // per-workgroup row offsets (launch_fire decides whether to count first)
             const i128 start0 = (i128)cfg.offset + k_first * (i128)slide();
             const i128 endl = (i128)cfg.offset + k_last * (i128)slide() + size();
             if (!fits64(start0) || !fits64(endl))
@@ -2530,7 +2527,6 @@ int gw_destroy(gw_handle* h) {
     for (int t = 0; t < gw_handle::kStageBufs; ++t)
         if (h->ev_dread[t]) hipEventDestroy(h->ev_dread[t]);
     if (h->cstream) hipStreamDestroy(h->cstream);
-    if (h->d_fireblk) hipFree(h->d_fireblk);
     for (size_t i = 0; i < h->cx.size(); ++i) {
         hipStreamDestroy(h->cx[i]);
         hipEventDestroy(h->cx_ev[i]);
