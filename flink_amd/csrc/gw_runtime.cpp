@@ -7,6 +7,10 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
+#include <functional>
+#include <map>
+#include <set>
 #include <atomic>
 #include <chrono>
 #include <thread>
@@ -328,6 +332,7 @@ struct gw_handle {
     int send_turn = 0;              // the device buffer the next H2D fills
     // a slot already sent ahead (gw_stage_send) into device buffer t, not yet ingested
     bool pre_valid[kStageBufs] = {};
+    bool slots_out = false;  // gw_stage_columns handed out pointers into the pinned slots
     int pre_slot[kStageBufs] = {-1, -1, -1};
     int64_t pre_n[kStageBufs] = {};
     int pre_cols[kStageBufs] = {};
@@ -651,6 +656,16 @@ struct gw_handle {
     // `slots` pinned slots of >= n records each (and the two device buffers of that size).
     int ensure_stage(int64_t n, int slots = 2) {
         if (n <= slot_cap && (int)h_slot.size() >= slots) return GW_OK;
+        // reallocating frees the slots: not while batches sent ahead wait in the device
+        // buffers, nor once a caller holds pointers into them (JVM direct ByteBuffers)
+        for (int t = 0; t < kStageBufs; ++t)
+            if (pre_valid[t])
+                return fail(GW_E_STATE, "staging: %lld records need larger staging buffers while batches sent "
+                                        "ahead (gw_stage_send) are not ingested yet", (long long)n);
+        if (slots_out)
+            return fail(GW_E_STATE, "staging: %lld records (%d slots) need larger pinned slots than gw_stage_alloc "
+                                    "made (%lld records, %d slots), and gw_stage_columns handed those out",
+                        (long long)n, slots, (long long)slot_cap, (int)h_slot.size());
         const int64_t cap = std::max(n, slot_cap);
         const int ns = std::max(slots, (int)h_slot.size());
         free_stage();
@@ -2034,21 +2049,204 @@ struct gw_handle {
         return khm_insert_host(hkeys, hvals);
     }
 
-    // Session windows: the blob (version 2) holds, per key group, every in-flight session
-    // as a 40-B (key, start, end, a0, a1) entry; no timer state (a session fires when the
-    // watermark passes end - 1, whichever handle holds it).
-    // Session windows (blob version 2): every in-flight session as a (key, start, end,
-    // a0, a1, fired) entry per key group (fired: kept after firing, under allowed lateness) -- the reference's (key, window) state entries plus its
-    // merging window set -- and no timer state (a session fires when the watermark passes
-    // end - 1, whichever handle holds it).  Count windows (version 3): per key, the
+    // Session windows (blob version 4, the heap layout of snapshot_heap): per key group the
+    // "window-contents" entries of the in-flight sessions, the merging window sets and the
+    // event-time timers (snapshot_sessions_heap).  Count windows (version 3): per key, the
     // element count and the ring of count-pane accumulators -- the CountTrigger count and
     // the window contents the evicting operator keeps (EvictingWindowOperator.java:92-135).
-    uint32_t slot_blob_version() const { return cfg.assigner == GW_SESSION ? 2u : 3u; }
+    uint32_t slot_blob_version() const { return cfg.assigner == GW_SESSION ? 4u : 3u; }
+
+    // Session windows in the heap backend's layout (HeapSnapshotStrategy.java:97-154), per key
+    // group and big-endian like snapshot_heap:
+    //   "window-contents": be32 n; n x (state window, key, [be32 key hash,] accumulator): one
+    //       entry per in-flight session holding state (CopyOnWriteStateMapSnapshot.writeState
+    //       :127-149).  The GPU keeps a session's state under the session itself, so its state
+    //       window is the window; a fired session under PurgingTrigger holds no state (its
+    //       contents were purged, WindowOperator.java:482-484) and has no entry;
+    //   "merging-window-set": be32 m; m x (key, [be32 key hash,] be32 c, c x (window, state
+    //       window)): the key's MergingWindowSet mapping (MergingWindowSet.persist :99-106);
+    //   timers: be32 t; t x (flipSignBit(ts), key, window) (TimerSerializer :147-152): the
+    //       trigger's timer at maxTimestamp while the session has not fired
+    //       (EventTimeTrigger.onElement / onMerge) and, under allowed lateness, its cleanup
+    //       timer (registerCleanupTimer :631-643; with lateness 0 the two coincide).
+    // Order: keys ascending, a key's sessions by start, its timers by (window, time).
+    int snapshot_sessions_heap(int32_t kg_lo, int32_t kg_hi, void* buf, int64_t cap, int64_t* len) {
+        int rc;
+        if ((rc = session_refresh(sess, err))) return fail(rc, "%s", err.c_str());
+        KhmHost kh;
+        if ((rc = khm_host(kh))) return rc;
+        const bool hashed = kh.on();
+        std::vector<int64_t> ent;  // (key, start, end, a0, a1, fired) per session
+        std::vector<int32_t> kgs;
+        if ((rc = session_collect(sess, kg_lo, kg_hi, ent, kgs, err,
+                                  hashed ? std::function<int32_t(int64_t)>([&](int64_t k) { return kh.hash(k); })
+                                         : std::function<int32_t(int64_t)>())))
+            return fail(rc, "%s", err.c_str());
+        const int nk = kg_hi - kg_lo + 1;
+        std::vector<std::vector<int64_t>> by_kg(nk);
+        for (size_t i = 0; i < kgs.size(); ++i) by_kg[kgs[i] - kg_lo].push_back((int64_t)i);
+        const bool purging = cfg.trigger == GW_PURGING_EVENT_TIME_TRIGGER;
+        const i128 LMAX = INT64_MAX;
+        std::vector<uint8_t> pay;
+        std::vector<int64_t> offs(nk + 1, 0);
+        for (int g = 0; g < nk; ++g) {
+            offs[g] = (int64_t)pay.size();
+            auto& ix = by_kg[g];
+            std::sort(ix.begin(), ix.end(), [&](int64_t x, int64_t y) {
+                const int64_t* a = &ent[6 * x];
+                const int64_t* b = &ent[6 * y];
+                return a[0] != b[0] ? a[0] < b[0] : a[1] < b[1];
+            });
+            std::vector<uint8_t> st, ms, tm;
+            int32_t nst = 0, nms = 0, ntm = 0;
+            for (size_t a = 0; a < ix.size();) {
+                const int64_t key = ent[6 * ix[a]];
+                size_t b = a;
+                while (b < ix.size() && ent[6 * ix[b]] == key) ++b;
+                be64(ms, key);
+                if (hashed) be32(ms, kh.hash(key));
+                be32(ms, (int32_t)(b - a));
+                nms++;
+                for (size_t q = a; q < b; ++q) {
+                    const int64_t* x = &ent[6 * ix[q]];
+                    const int64_t s0 = x[1], e0 = x[2];
+                    const bool fired = x[5] != 0;
+                    be64(ms, s0); be64(ms, e0); be64(ms, s0); be64(ms, e0);
+                    if (!(purging && fired)) {
+                        be64(st, s0); be64(st, e0); be64(st, key);
+                        if (hashed) be32(st, kh.hash(key));
+                        acc_to_be(st, x[3], x[4]);
+                        nst++;
+                    }
+                    const i128 mx = (i128)e0 - 1;
+                    if (!fired) {
+                        be64(tm, (int64_t)((uint64_t)(int64_t)mx ^ 0x8000000000000000ull));
+                        be64(tm, key); be64(tm, s0); be64(tm, e0);
+                        ntm++;
+                    }
+                    const i128 ct = mx + (i128)cfg.allowed_lateness;
+                    if (cfg.allowed_lateness > 0 && ct < LMAX) {
+                        be64(tm, (int64_t)((uint64_t)(int64_t)ct ^ 0x8000000000000000ull));
+                        be64(tm, key); be64(tm, s0); be64(tm, e0);
+                        ntm++;
+                    }
+                }
+                a = b;
+            }
+            be32(pay, nst);
+            pay.insert(pay.end(), st.begin(), st.end());
+            be32(pay, nms);
+            pay.insert(pay.end(), ms.begin(), ms.end());
+            be32(pay, ntm);
+            pay.insert(pay.end(), tm.begin(), tm.end());
+        }
+        offs[nk] = (int64_t)pay.size();
+        const int64_t need = (int64_t)sizeof(SnapHeader) + (int64_t)(nk + 1) * 8 + (int64_t)pay.size();
+        *len = need;
+        if (!buf) return GW_OK;
+        if (cap < need) return fail(GW_E_OUTPUT_FULL, "snapshot needs %lld bytes", (long long)need);
+        SnapHeader hd{};
+        memcpy(hd.magic, "GWS1", 4);
+        hd.version = 4;
+        hd.agg = cfg.agg; hd.assigner = cfg.assigner;
+        hd.size = cfg.size; hd.slide = cfg.slide; hd.offset = cfg.offset; hd.gap = cfg.gap;
+        hd.flags = hashed ? kSnapKeyHashes : 0;
+        hd.max_parallelism = cfg.max_parallelism; hd.kg_lo = kg_lo; hd.kg_hi = kg_hi;
+        hd.entries = (int64_t)pay.size();
+        char* out = (char*)buf;
+        memcpy(out, &hd, sizeof hd);
+        memcpy(out + sizeof hd, offs.data(), (nk + 1) * 8);
+        if (!pay.empty()) memcpy(out + sizeof hd + (nk + 1) * 8, pay.data(), pay.size());
+        return GW_OK;
+    }
+
+    // Reads a session blob of the heap layout back into (key, start, end, a0, a1, fired)
+    // sessions: each merging-window-set mapping (window -> state window) takes the state of
+    // its state window (any original window, as the reference's MergingWindowSet.addWindow
+    // keeps it, :188-201), or none; a session has fired when its trigger timer at
+    // maxTimestamp is gone.  A session without state that has not fired is a trigger outside
+    // EventTimeTrigger / PurgingTrigger (GW_E_UNSUPPORTED); state no mapping names, or
+    // overlapping sessions of one key, are a corrupt blob.
+    int parse_session_heap(const SnapHeader& hd, const uint8_t* p, const uint8_t* end, std::vector<int64_t>& out,
+                           std::vector<int64_t>& hkeys, std::vector<int32_t>& hvals) {
+        const int64_t nk = (int64_t)hd.kg_hi - hd.kg_lo + 1;
+        const int ab = acc_bytes();
+        const int hb = (hd.flags & kSnapKeyHashes) ? 4 : 0;
+        const int64_t id0 = cfg.agg == GW_AVG_F64 ? INT64_MIN : identity0(cfg.agg);  // a purged session
+        typedef std::tuple<int64_t, int64_t, int64_t> KW;  // (key, start, end)
+#define NEED(x) do { if ((x) < 0 || (int64_t)(x) > end - p) return fail(GW_E_INVALID, "truncated snapshot blob"); } while (0)
+        for (int64_t g = 0; g < nk; ++g) {
+            NEED(4);
+            const int32_t ns = rd32(p); p += 4;
+            if (ns < 0) return fail(GW_E_INVALID, "negative entry count in snapshot key group");
+            NEED((int64_t)ns * (24 + hb + ab));
+            std::map<KW, std::pair<std::pair<int64_t, int64_t>, bool>> state;  // -> (acc, used)
+            for (int32_t i = 0; i < ns; ++i, p += 24 + hb + ab) {
+                const int64_t s0 = rd64(p), e0 = rd64(p + 8), key = rd64(p + 16);
+                int64_t a0, a1;
+                acc_from_be(p + 24 + hb, a0, a1);
+                if (hb) { hkeys.push_back(key); hvals.push_back(rd32(p + 24)); }
+                if (!state.emplace(KW{key, s0, e0}, std::make_pair(std::make_pair(a0, a1), false)).second)
+                    return fail(GW_E_INVALID, "two state entries of one (key, window) in a snapshot key group");
+            }
+            NEED(4);
+            const int32_t nm = rd32(p); p += 4;
+            if (nm < 0) return fail(GW_E_INVALID, "negative merging window set count in snapshot key group");
+            std::vector<std::array<int64_t, 5>> ses;  // (key, start, end, state start, state end)
+            for (int32_t i = 0; i < nm; ++i) {
+                NEED(12 + hb);
+                const int64_t key = rd64(p);
+                if (hb) { hkeys.push_back(key); hvals.push_back(rd32(p + 8)); }
+                const int32_t c = rd32(p + 8 + hb);
+                p += 12 + hb;
+                if (c < 0) return fail(GW_E_INVALID, "negative merging window set size");
+                NEED((int64_t)c * 32);
+                for (int32_t j = 0; j < c; ++j, p += 32)
+                    ses.push_back({key, rd64(p), rd64(p + 8), rd64(p + 16), rd64(p + 24)});
+            }
+            NEED(4);
+            const int32_t nt = rd32(p); p += 4;
+            if (nt < 0) return fail(GW_E_INVALID, "negative timer count in snapshot key group");
+            NEED((int64_t)nt * 32);
+            std::set<KW> armed;  // sessions whose trigger timer (at maxTimestamp) is still set
+            for (int32_t i = 0; i < nt; ++i, p += 32) {
+                const int64_t ts = (int64_t)((uint64_t)rd64(p) ^ 0x8000000000000000ull);
+                const int64_t key = rd64(p + 8), s0 = rd64(p + 16), e0 = rd64(p + 24);
+                if (ts == (int64_t)((uint64_t)e0 - 1)) armed.insert(KW{key, s0, e0});
+            }
+            std::sort(ses.begin(), ses.end());
+            for (size_t i = 0; i < ses.size(); ++i) {
+                const auto& x = ses[i];
+                if (x[2] <= x[1]) return fail(GW_E_INVALID, "empty session window in a snapshot");
+                if (i && ses[i - 1][0] == x[0] && ses[i - 1][2] >= x[1])  // TimeWindow.intersects is inclusive
+                    return fail(GW_E_INVALID, "overlapping sessions of one key in a snapshot");
+                const bool fired = armed.count(KW{x[0], x[1], x[2]}) == 0;
+                auto it = state.find(KW{x[0], x[3], x[4]});
+                int64_t a0 = id0, a1 = 0;
+                if (it != state.end()) {
+                    if (it->second.second) return fail(GW_E_INVALID, "two sessions share one state window");
+                    it->second.second = true;
+                    a0 = it->second.first.first;
+                    a1 = it->second.first.second;
+                } else if (!fired) {
+                    return fail(GW_E_UNSUPPORTED, "a session without state whose timer has not fired "
+                                                  "(a trigger other than EventTimeTrigger / PurgingTrigger)");
+                }
+                out.insert(out.end(), {x[0], x[1], x[2], a0, a1, (int64_t)fired});
+            }
+            for (auto& kv : state)
+                if (!kv.second.second) return fail(GW_E_INVALID, "a state entry outside every merging window set");
+        }
+#undef NEED
+        if (p != end) return fail(GW_E_INVALID, "snapshot blob has trailing bytes");
+        return GW_OK;
+    }
 
     int snapshot_sessions(int32_t kg_lo, int32_t kg_hi, void* buf, int64_t cap, int64_t* len) {
         int rc;
         if (kg_lo < 0 || kg_hi < kg_lo || kg_hi >= cfg.max_parallelism)
             return fail(GW_E_INVALID, "key-group range [%d, %d] outside [0, %d)", kg_lo, kg_hi, cfg.max_parallelism);
+        if (cfg.assigner == GW_SESSION) return snapshot_sessions_heap(kg_lo, kg_hi, buf, cap, len);
         if ((rc = session_refresh(sess, err))) return fail(rc, "%s", err.c_str());
         KhmHost kh;
         if ((rc = khm_host(kh))) return rc;
@@ -2100,8 +2298,26 @@ struct gw_handle {
         if (!buf || len < (int64_t)sizeof(SnapHeader)) return fail(GW_E_INVALID, "snapshot blob too short");
         SnapHeader hd;
         memcpy(&hd, buf, sizeof hd);
-        if (memcmp(hd.magic, "GWS1", 4) != 0 || hd.version < 1 || hd.version > 3)
+        if (memcmp(hd.magic, "GWS1", 4) != 0 || hd.version < 1 || hd.version > kSnapMaxVersion)
             return fail(GW_E_INVALID, "not a gpuwin snapshot");
+        if (cfg.assigner == GW_SESSION) {
+            if (hd.version != 4 || hd.agg != cfg.agg || hd.assigner != cfg.assigner || hd.gap != cfg.gap ||
+                hd.max_parallelism != cfg.max_parallelism || (hd.flags & ~kSnapKeyHashes))
+                return fail(GW_E_INVALID, "snapshot of a different window / aggregate / max parallelism");
+            const int64_t nk = (int64_t)hd.kg_hi - hd.kg_lo + 1;
+            const int64_t pay0 = (int64_t)sizeof hd + (nk + 1) * 8;
+            if (nk <= 0 || hd.entries < 0 || len < pay0 || hd.entries > len - pay0)
+                return fail(GW_E_INVALID, "truncated snapshot blob");
+            const uint8_t* p = (const uint8_t*)buf + pay0;
+            std::vector<int64_t> ent, hkeys;
+            std::vector<int32_t> hvals;
+            int rc = parse_session_heap(hd, p, p + hd.entries, ent, hkeys, hvals);
+            if (rc == GW_OK) rc = khm_check_host(hkeys, hvals);  // before the table changes
+            if (rc || dry) return rc;
+            rc = session_restore(sess, ent.data(), (int64_t)(ent.size() / 6), err);
+            if (rc) return fail(rc, "%s", err.c_str());
+            return khm_insert_host(hkeys, hvals);
+        }
         const bool hashed = (hd.flags & kSnapKeyHashes) != 0;
         const int64_t ew0 = session_entry_words(sess), ew = ew0 + (hashed ? 1 : 0);
         if (hd.version != slot_blob_version() || hd.agg != cfg.agg || hd.assigner != cfg.assigner ||
@@ -2876,6 +3092,9 @@ int gw_ingest(gw_handle* h, int64_t n, const int64_t* key, const int32_t* key_ha
     if (h->failed) return h->fail(GW_E_STATE, "operator failed earlier: %s", h->err.c_str());
     if (n < 0 || (n > 0 && (!key || !ts))) return h->fail(GW_E_INVALID, "null key/ts column");
     if (n > 0 && !value && h->cfg.agg != GW_COUNT) return h->fail(GW_E_INVALID, "value column required");
+    if (h->slots_out && n > 0)  // gw_ingest copies through the same pinned slots the caller now fills
+        return h->fail(GW_E_STATE, "gw_ingest on a handle whose pinned slots were handed out (gw_stage_columns): "
+                                   "ingest them with gw_ingest_stage");
     hipSetDevice(h->cfg.device);
     const int64_t chunk = h->cfg.max_batch;
     for (int64_t off = 0; off < n; off += chunk) {
@@ -2981,6 +3200,7 @@ int gw_stage_columns(gw_handle* h, int32_t slot, int64_t** key, int32_t** key_ha
     const int rc = h->slot_ready(slot);
     if (rc) return rc;
     int64_t* hs = h->h_slot[slot];
+    h->slots_out = true;
     if (key) *key = hs;
     if (ts) *ts = hs + h->slot_cap;
     if (value) *value = hs + 2 * h->slot_cap;
@@ -3838,12 +4058,13 @@ static bool blob_keys(const uint8_t* b, int64_t len, F&& f) {
         const int32_t m = gw_handle::rd32(p);
         p += 4;
         if (m < 0) return false;
-        for (int32_t i = 0; i < m; ++i) {  // merging window sets: (key, be32 c, c x 32 B)
-            if (end - p < 12) return false;
-            const int32_t c = gw_handle::rd32(p + 8);
-            if (c < 0 || (int64_t)c * 32 > end - p - 12) return false;
+        const int64_t mh = 12 + ((hd.flags & kSnapKeyHashes) ? 4 : 0);
+        for (int32_t i = 0; i < m; ++i) {  // merging window sets: (key, [be32 hash,] be32 c, c x 32 B)
+            if (end - p < mh) return false;
+            const int32_t c = gw_handle::rd32(p + mh - 4);
+            if (c < 0 || (int64_t)c * 32 > end - p - mh) return false;
             f(p, true);
-            p += 12 + (int64_t)c * 32;
+            p += mh + (int64_t)c * 32;
         }
         if (end - p < 4) return false;
         const int32_t t = gw_handle::rd32(p);

@@ -561,7 +561,8 @@ class GpuWindowOperator:
 
     def stage_send(self, slot: int, n: int, with_value: bool = True, with_key_hash: bool = False):
         """Send the slot's first n records over PCIe ahead of their gw_ingest_stage (gw_stage_send):
-        at most one batch ahead; the next ingest_stage must name this slot."""
+        up to two batches ahead (three device buffers); ingest_stage calls must follow the send
+        order."""
         cols = (N.STAGE_VALUE if with_value else 0) | (N.STAGE_KEY_HASH if with_key_hash else 0)
         N.check(N.lib().gw_stage_send(self._h, int(slot), int(n), cols), self._h)
 
@@ -632,13 +633,41 @@ class GpuWindowOperator:
         if isinstance(blobs, (bytes, bytearray)):
             blobs = [blobs]
         if self._deferred:
-            raise N.GpuWinError(N.GW_E_UNSUPPORTED, "restoring window state into a staggered tumbling operator: "
-                                "the restored windows keep their alignment while a new stagger is drawn")
+            self._adopt_restored_stagger(blobs)
+        if self._deferred:  # no restored window state: the stagger is drawn at the first element
+            return
         for b in blobs:
             b = bytes(b)
             if b[:4] == KEYED_MAGIC:
                 b = self._rekey(b)
             N.check(N.lib().gw_restore(self._h, b, len(b)), self._h)
+
+    def _adopt_restored_stagger(self, blobs):
+        """A staggered tumbling operator restored from window state keeps the stagger the state
+        was written under: the blobs' window offset (header), which is (offset + stagger) %
+        size of the operator that wrote them.  The reference draws a new stagger after a restore
+        (TumblingEventTimeWindows.java:72-79: staggerOffset starts out null) and keeps the
+        restored windows at their old alignment beside it; one handle holds one alignment, so
+        the old draw is reused -- for RANDOM a valid draw of the same distribution, for NATURAL
+        the first element's processing time of the run that wrote the state.  Blobs without
+        state leave the operator to draw at its first element; blobs of one restore carrying
+        different staggers (subtasks' independent draws merged by a rescale) are refused."""
+        offs = set()
+        for b in blobs:
+            b = bytes(b)
+            if b[:4] == KEYED_MAGIC:
+                b = unpack_keyed_snapshot(b)[0]
+            hdr = struct.unpack_from("<4sIii5q4i3q", b, 0)
+            nk = hdr[11] - hdr[10] + 1
+            if hdr[15] > 12 * nk:  # payload beyond the empty sections (n = m = t = 0) of each key group
+                offs.add(int(hdr[6]))
+        if len(offs) > 1:
+            raise N.GpuWinError(N.GW_E_UNSUPPORTED, "restoring window state of staggered tumbling operators "
+                                f"drawn with different staggers (window offsets {sorted(offs)}) into one")
+        if offs:
+            self.cfg.offset = offs.pop()
+            self._deferred = False
+            self._create()
 
     def snapshot_state_keyed(self, key_group_range=None) -> bytes:
         """snapshot_state plus the real keys behind the dictionary ids its entries name, as

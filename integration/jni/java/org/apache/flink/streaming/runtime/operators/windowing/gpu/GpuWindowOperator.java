@@ -46,9 +46,11 @@
  * Stagger (TumblingEventTimeWindows.of(size, offset, WindowStagger)): the stagger offset is
  * drawn at the first element, as TumblingEventTimeWindows.assignWindows does
  * (TumblingEventTimeWindows.java:72-79), so a staggered operator creates its handle then, with
- * offset (offset + stagger) % size (gw_window_stagger_offset).  Restoring state into a
- * staggered operator is refused: the reference would keep the restored windows' alignment
- * beside a newly drawn one, which one handle cannot hold.
+ * offset (offset + stagger) % size (gw_window_stagger_offset).  A staggered operator restored
+ * from window state reuses the stagger the state was written under (the blob's window offset):
+ * the reference would draw a new one and keep the restored windows' alignment beside it, which
+ * one handle cannot hold; for RANDOM the old draw is a valid draw.  Restored key groups drawn
+ * with different staggers are refused.
  *
  * Keys (K, as WindowOperator<K, ...> at WindowOperator.java:102): Long keys go to the GPU as
  * they are, and the device computes Long.hashCode.  Any other key type (String, Integer,
@@ -250,10 +252,17 @@ public class GpuWindowOperator<IN, K>
         }
         handleDeferred = stagger != WindowStagger.ALIGNED;
         if (handleDeferred && restored != null && !restored.isEmpty()) {
-            throw new UnsupportedOperationException("restoring window state into a staggered tumbling operator ("
-                    + stagger + "): the restored windows keep their alignment while a new stagger is drawn");
+            // Restored window state keeps the stagger it was written under (the blob header's
+            // window offset): the reference draws a new stagger after a restore and keeps the
+            // restored windows at their old alignment beside it (TumblingEventTimeWindows.java:
+            // 53,72-79); one handle holds one alignment, so the old draw is reused.
+            long drawn = restoredWindowOffset(restored);
+            if (drawn != Long.MIN_VALUE) {
+                createHandle(drawn);
+                handleDeferred = false;
+            }
         }
-        if (!handleDeferred) createHandle(offset);
+        if (!handleDeferred && handle == 0) createHandle(offset);
         if (lateDataTag != null) { lKey = direct(8); lTs = direct(8); lVal = direct(8); }
         if (wide() && inputSerializer == null && getExecutionConfig() != null
                 && getContainingTask().getConfiguration().isCheckpointingEnabled()) {
@@ -269,6 +278,7 @@ public class GpuWindowOperator<IN, K>
         keys = direct(8); keyHashes = direct(4); ts = direct(8); values = direct(8);
         oKey = direct(8); oStart = direct(8); oEnd = direct(8); oRes = direct(8);
         if (!handleDeferred) bindStaging();
+        if (restored != null && handleDeferred) restored = null;  // staggered: the blobs hold no window state
         if (restored != null) {  // initializeState runs before open (StreamOperator.java:139)
             for (int i = 0; i < restored.size(); i++) {
                 byte[] blob = restored.get(i);
@@ -326,6 +336,27 @@ public class GpuWindowOperator<IN, K>
         keyHashes = nativeStageColumn(handle, s, 1, batchCapacity).order(ByteOrder.nativeOrder());
         ts = nativeStageColumn(handle, s, 2, batchCapacity).order(ByteOrder.nativeOrder());
         values = nativeStageColumn(handle, s, 3, batchCapacity).order(ByteOrder.nativeOrder());
+    }
+
+    /** The window offset restored state of a staggered operator was written under, or
+     *  Long.MIN_VALUE when no blob holds window state (the stagger is then drawn at the first
+     *  element).  Blob header (include/gpuwin.h gw_snapshot, little-endian): window offset at
+     *  byte 32, key-group range at 60 / 64, payload bytes at 88; a key group without state
+     *  is 12 bytes (no entries, no merging window set, no timers). */
+    static long restoredWindowOffset(List<byte[]> blobs) {
+        long found = Long.MIN_VALUE;
+        for (byte[] b : blobs) {
+            ByteBuffer h = ByteBuffer.wrap(b).order(ByteOrder.LITTLE_ENDIAN);
+            long nk = (long) h.getInt(64) - h.getInt(60) + 1;
+            if (h.getLong(88) <= 12 * nk) continue;
+            long off = h.getLong(32);
+            if (found != Long.MIN_VALUE && found != off) {
+                throw new UnsupportedOperationException("restoring window state of staggered tumbling operators "
+                        + "drawn with different staggers (window offsets " + found + ", " + off + ") into one");
+            }
+            found = off;
+        }
+        return found;
     }
 
     /** The handle, with the windows' offset (the stagger decided by the caller). */

@@ -708,9 +708,18 @@ static int merge_function(wo_op* op, int64_t key, int64_t rs, int64_t re,
     return GW_OK;
 }
 
+/* The MergeFunction of MergingWindowSet.addWindow (MergingWindowSet.java:210-214):
+ * (mergeResult, mergedWindows, stateWindowResult, mergedStateWindows). */
+typedef int (*mws_merge_fn)(void* ctx, int64_t key, int64_t rs, int64_t re, const int64_t* mw, int nmw,
+                            int64_t tss, int64_t tse, const int64_t* msw, int nmsw);
+static int op_merge_fn(void* ctx, int64_t key, int64_t rs, int64_t re, const int64_t* mw, int nmw,
+                       int64_t tss, int64_t tse, const int64_t* msw, int nmsw) {
+    return merge_function((wo_op*)ctx, key, rs, re, mw, nmw, tss, tse, msw, nmsw);
+}
+
 /* MergingWindowSet.addWindow (MergingWindowSet.java:153-224). */
-static int mws_add_window(wo_op* op, int64_t key, mws_t* m, int64_t ns, int64_t ne,
-                          int64_t* rs_out, int64_t* re_out) {
+static int mws_add_window_cb(mws_merge_fn fn, void* ctx, int64_t key, mws_t* m, int64_t ns, int64_t ne,
+                             int64_t* rs_out, int64_t* re_out) {
     int n = m->n + 1;
     int64_t* s = (int64_t*)malloc(sizeof(int64_t) * 6 * (size_t)n);
     int64_t* e = s + n;
@@ -776,7 +785,7 @@ static int mws_add_window(wo_op* op, int64_t key, mws_t* m, int64_t ns, int64_t 
         for (int j = 0; j < nm; j++)
             if (mw[2 * j] == gs[g] && mw[2 * j + 1] == ge[g]) contains_result = 1;
         if (!(contains_result && nm == 1))
-            rc = merge_function(op, key, gs[g], ge[g], mw, nm, tss, tse, msw, nmsw);
+            rc = fn(ctx, key, gs[g], ge[g], mw, nm, tss, tse, msw, nmsw);
     }
     if (rc == GW_OK && (!any_merge || (rs == ns && re == ne && !merged_new)))
         mws_put(m, rs, re, rs, re);
@@ -786,6 +795,79 @@ static int mws_add_window(wo_op* op, int64_t key, mws_t* m, int64_t ns, int64_t 
     *rs_out = rs;
     *re_out = re;
     return rc;
+}
+static int mws_add_window(wo_op* op, int64_t key, mws_t* m, int64_t ns, int64_t ne,
+                          int64_t* rs_out, int64_t* re_out) {
+    return mws_add_window_cb(op_merge_fn, op, key, m, ns, ne, rs_out, re_out);
+}
+
+/* A stand-alone MergingWindowSet of EventTimeSessionWindows (test hook for the reference's
+ * MergingWindowSetTest, SJT/runtime/operators/windowing/MergingWindowSetTest.java:62-495):
+ * addWindow with a recording MergeFunction, getStateWindow, retireWindow, the restore from
+ * a ListState and the persisted list. */
+struct wo_mws {
+    mws_t m;
+    int merged;                   /* the MergeFunction ran during the last add */
+    int64_t target[2], state[2];  /* mergeResult, stateWindowResult */
+    int nsrc, nmsw;
+    int64_t src[2 * 64], msw[2 * 64];
+};
+static int rec_merge_fn(void* ctx, int64_t key, int64_t rs, int64_t re, const int64_t* mw, int nmw,
+                        int64_t tss, int64_t tse, const int64_t* msw, int nmsw) {
+    (void)key;
+    wo_mws* w = (wo_mws*)ctx;
+    if (w->merged) return GW_E_STATE; /* "More than one merge for adding a Window should not occur." */
+    if (nmw > 64 || nmsw > 64) return GW_E_UNSUPPORTED;
+    w->merged = 1;
+    w->target[0] = rs; w->target[1] = re;
+    w->state[0] = tss; w->state[1] = tse;
+    w->nsrc = nmw;
+    memcpy(w->src, mw, sizeof(int64_t) * 2 * (size_t)nmw);
+    w->nmsw = nmsw;
+    memcpy(w->msw, msw, sizeof(int64_t) * 2 * (size_t)nmsw);
+    return GW_OK;
+}
+wo_mws* wo_mws_create(void) { return (wo_mws*)calloc(1, sizeof(wo_mws)); }
+void wo_mws_destroy(wo_mws* w) {
+    if (!w) return;
+    free(w->m.w);
+    free(w);
+}
+/* addWindow(new TimeWindow(s, e), mergeFunction): result window into res[2]; info[] gets
+ * merged, target (2), state window (2), nsrc, nsrc x (s, e), nmsw, nmsw x (s, e). */
+int wo_mws_add(wo_mws* w, int64_t s, int64_t e, int64_t* res, int64_t* info) {
+    w->merged = 0;
+    w->nsrc = w->nmsw = 0;
+    int rc = mws_add_window_cb(rec_merge_fn, w, 0, &w->m, s, e, &res[0], &res[1]);
+    if (rc) return rc;
+    int q = 0;
+    info[q++] = w->merged;
+    info[q++] = w->target[0]; info[q++] = w->target[1];
+    info[q++] = w->state[0]; info[q++] = w->state[1];
+    info[q++] = w->nsrc;
+    for (int i = 0; i < 2 * w->nsrc; i++) info[q++] = w->src[i];
+    info[q++] = w->nmsw;
+    for (int i = 0; i < 2 * w->nmsw; i++) info[q++] = w->msw[i];
+    return GW_OK;
+}
+/* getStateWindow: 1 and the state window in out[2], 0 when the window is not in flight */
+int wo_mws_state_window(const wo_mws* w, int64_t s, int64_t e, int64_t* out) {
+    int i = mws_find(&w->m, s, e);
+    if (i < 0) return 0;
+    out[0] = w->m.w[4 * i + 2];
+    out[1] = w->m.w[4 * i + 3];
+    return 1;
+}
+/* retireWindow: GW_E_STATE ("not in in-flight window set") when absent */
+int wo_mws_retire(wo_mws* w, int64_t s, int64_t e) {
+    return mws_remove(&w->m, s, e, NULL, NULL) ? GW_OK : GW_E_STATE;
+}
+/* the constructor's restore from the ListState: mapping.put(f0, f1) per element */
+void wo_mws_put(wo_mws* w, int64_t s, int64_t e, int64_t ss, int64_t se) { mws_put(&w->m, s, e, ss, se); }
+/* persist(): the mapping as (window, state window) quadruples; returns their number */
+int wo_mws_list(const wo_mws* w, int64_t* out, int cap) {
+    for (int i = 0; i < w->m.n && i < cap; i++) memcpy(out + 4 * i, w->m.w + 4 * i, 4 * sizeof(int64_t));
+    return w->m.n;
 }
 
 /* ------------------------------------------------------------------------ */
@@ -1081,7 +1163,7 @@ const char* wo_last_error(const wo_op* op) { return op ? op->err : "null operato
  *                         (TimeWindow.Serializer :159-169, LongSerializer, and the
  *                         accumulator as LongSerializer / DoubleSerializer / IntSerializer /
  *                         Tuple2(sum, count) for the closed set of aggregates);
- *   "merging-window-set": int32 m; m x (key, int32 c, c x (window, state window)) -- the
+ *   "merging-window-set": int32 m; m x (key, [int32 key hash,] int32 c, c x (window, state window)) -- the
  *                         MergingWindowSet ListState<Tuple2<W, W>> of session windows
  *                         (MergingWindowSet.persist :99-106); 0 for other assigners;
  *   timers:               int32 t; t x (flipSignBit(ts), key, window.start, window.end).
@@ -1241,6 +1323,9 @@ int64_t wo_snapshot(wo_op* op, int32_t kg_lo, int32_t kg_hi, uint8_t* buf, int64
                                           (idx[4 * j] == idx[4 * j - 4] && idx[4 * j + 1] < idx[4 * j - 3])); j--)
                     for (int c = 0; c < 4; c++) { int64_t x = idx[4 * j + c]; idx[4 * j + c] = idx[4 * j - 4 + c]; idx[4 * j - 4 + c] = x; }
             wb_be64(&b, me[q].k0);
+            /* a key whose sessions all fired and purged holds no state entry: the set carries
+             * its hash too, so a restore can file it under its key group */
+            if (hashed) wb_be32(&b, key_hash_of(op, me[q].k0));
             wb_be32(&b, w->n);
             for (int i = 0; i < 4 * w->n; i++) wb_be64(&b, idx[i]);
             free(idx);
@@ -1334,10 +1419,15 @@ int wo_restore(wo_op* op, const uint8_t* buf, int64_t len) {
         NEED(4);
         int32_t nm = rd_be32(p); p += 4;
         for (int32_t i = 0; i < nm; i++) {
-            NEED(12);
+            NEED(12 + hb);
             int64_t key = rd_be64(p);
-            int32_t c = rd_be32(p + 8);
-            p += 12;
+            if (hb) {
+                const int32_t kh = rd_be32(p + 8);
+                const int rc = wo_set_key_hashes(op, 1, &key, &kh);
+                if (rc) return rc;
+            }
+            int32_t c = rd_be32(p + 8 + hb);
+            p += 12 + hb;
             NEED((int64_t)c * 32);
             mws_t* w = mws_get(op, key, 1);
             for (int32_t j = 0; j < c; j++, p += 32)

@@ -84,6 +84,22 @@ int64_t wo_snapshot(wo_op* op, int32_t kg_lo, int32_t kg_hi, uint8_t* buf, int64
 int     wo_restore(wo_op* op, const uint8_t* buf, int64_t len);
 int     wo_acc_bytes(int agg);
 
+/* A stand-alone MergingWindowSet of session windows (MergingWindowSet.java:77-224), the unit
+ * MergingWindowSetTest drives: wo_mws_add = addWindow with a recording MergeFunction (res[2]
+ * = the result window; info = merged?, mergeResult (2), stateWindowResult (2), n sources, the
+ * merged windows (2 each), n state windows, the merged state windows (2 each)).
+ * wo_mws_state_window = getStateWindow (returns 0 for null); wo_mws_retire = retireWindow
+ * (GW_E_STATE when absent); wo_mws_put = the restore from the ListState; wo_mws_list = the
+ * persisted (window, state window) list, returns its length. */
+typedef struct wo_mws wo_mws;
+wo_mws* wo_mws_create(void);
+void    wo_mws_destroy(wo_mws* w);
+int     wo_mws_add(wo_mws* w, int64_t start, int64_t end, int64_t* res, int64_t* info);
+int     wo_mws_state_window(const wo_mws* w, int64_t start, int64_t end, int64_t* out);
+int     wo_mws_retire(wo_mws* w, int64_t start, int64_t end);
+void    wo_mws_put(wo_mws* w, int64_t start, int64_t end, int64_t state_start, int64_t state_end);
+int     wo_mws_list(const wo_mws* w, int64_t* out, int cap);
+
 /* Multi-threaded CPU baseline: `threads` operator instances, each owning the key
  * groups of one subtask (computeKeyGroupRangeForOperatorIndex), like a Flink job
  * at parallelism = threads.  Runs the whole stream: batches of batch_len records,

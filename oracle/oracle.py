@@ -140,6 +140,12 @@ def lib() -> ctypes.CDLL:
                                             p, p, p, p, p, ctypes.POINTER(ctypes.c_double)]),
             ("wo_snapshot", i64, [p, i32, i32, p, i64]), ("wo_restore", ctypes.c_int, [p, p, i64]),
             ("wo_acc_bytes", ctypes.c_int, [ctypes.c_int]),
+            ("wo_mws_create", p, []), ("wo_mws_destroy", None, [p]),
+            ("wo_mws_add", ctypes.c_int, [p, i64, i64, P64, P64]),
+            ("wo_mws_state_window", ctypes.c_int, [p, i64, i64, P64]),
+            ("wo_mws_retire", ctypes.c_int, [p, i64, i64]),
+            ("wo_mws_put", None, [p, i64, i64, i64, i64]),
+            ("wo_mws_list", ctypes.c_int, [p, P64, ctypes.c_int]),
             ("wo_run_parallel_wm", i64, [ctypes.POINTER(GwConfig), ctypes.c_int, i64, p, p, p, p, p, p, p,
                                           ctypes.POINTER(ctypes.c_double)]),
         ]:
@@ -162,6 +168,53 @@ def _p(a: np.ndarray):
 
 class OracleError(RuntimeError):
     pass
+
+
+class MergingWindowSet:
+    """The oracle's MergingWindowSet of session windows (MergingWindowSet.java:77-224), driven the
+    way MergingWindowSetTest drives the reference's (test hook)."""
+
+    def __init__(self, restored=()):
+        self._h = lib().wo_mws_create()
+        for (s, e), (ss, se) in restored:  # the constructor reading its ListState
+            lib().wo_mws_put(self._h, s, e, ss, se)
+
+    def close(self):
+        if self._h:
+            lib().wo_mws_destroy(self._h)
+            self._h = None
+
+    def add_window(self, w):
+        """-> (result window, merge) with merge None when the MergeFunction did not run, else
+        {"target": w, "state_window": w, "sources": [w], "merged_state_windows": [w]}."""
+        res = (ctypes.c_int64 * 2)()
+        info = (ctypes.c_int64 * 600)()
+        rc = lib().wo_mws_add(self._h, w[0], w[1], res, info)
+        if rc:
+            raise OracleError(f"addWindow failed: {rc}")
+        result = (res[0], res[1])
+        if not info[0]:
+            return result, None
+        q = 5
+        ns = info[q]; q += 1
+        src = [(info[q + 2 * i], info[q + 2 * i + 1]) for i in range(ns)]; q += 2 * ns
+        nm = info[q]; q += 1
+        msw = [(info[q + 2 * i], info[q + 2 * i + 1]) for i in range(nm)]
+        return result, {"target": (info[1], info[2]), "state_window": (info[3], info[4]), "sources": src,
+                        "merged_state_windows": msw}
+
+    def state_window(self, w):
+        out = (ctypes.c_int64 * 2)()
+        return (out[0], out[1]) if lib().wo_mws_state_window(self._h, w[0], w[1], out) else None
+
+    def retire(self, w):
+        if lib().wo_mws_retire(self._h, w[0], w[1]):
+            raise OracleError(f"Window {w} is not in in-flight window set.")
+
+    def persisted(self):
+        out = (ctypes.c_int64 * 4096)()
+        n = lib().wo_mws_list(self._h, out, 1024)
+        return sorted(((out[4 * i], out[4 * i + 1]), (out[4 * i + 2], out[4 * i + 3])) for i in range(n))
 
 
 class OracleOperator:

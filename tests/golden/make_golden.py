@@ -114,6 +114,96 @@ dump("merge_windows.json", {"source": SES + ":68-165", "cases": [
 ]})
 
 # --------------------------------------------------------------------------------------
+# MergingWindowSet driven directly, EventTimeSessionWindows.withGap(3 ms)
+# (MergingWindowSetTest.java).  Steps:
+#   ["add", window, result, merge]   merge: null (the MergeFunction did not run) or
+#       {"target": w, "state_window": [allowed w...], "sources": [w...] (as a set),
+#        "merged_state_windows": [[allowed set of w]...] | null (unchecked)}
+#   ["state", window, [allowed state windows] | null (getStateWindow == null)]
+#   ["retire", window]        ["persist", [[window, state window]...] (as a set)]
+# "restore": the ListState the set is constructed from.  Where the reference accepts any of
+# several state windows (the first element of a HashSet, MergingWindowSet.java:190) every
+# allowed answer is listed.
+# --------------------------------------------------------------------------------------
+MWST = ("flink-streaming-java/src/test/java/org/apache/flink/streaming/runtime/operators/"
+        "windowing/MergingWindowSetTest.java")
+W0_4, W3_5, W0_5, W4_6, W0_6 = [0, 4], [3, 5], [0, 5], [4, 6], [0, 6]
+mws_tests = [
+    {"name": "incremental_merging", "source": MWST + ":90-206", "restore": [], "steps": [
+        ["add", W0_4, W0_4, None], ["state", W0_4, [W0_4]],
+        ["add", W0_4, W0_4, None],
+        ["add", W3_5, W0_5, {"target": W0_5, "state_window": [W0_4], "sources": [W0_4],
+                             "merged_state_windows": [[]]}],
+        ["add", W4_6, W0_6, {"target": W0_6, "state_window": [W0_4], "sources": [W0_5],
+                             "merged_state_windows": [[]]}],
+        ["state", W0_6, [W0_4]],
+        ["add", [1, 4], W0_6, None], ["add", W0_4, W0_6, None], ["add", W3_5, W0_6, None],
+        ["add", W4_6, W0_6, None], ["state", W0_6, [W0_4]],
+        ["add", [11, 14], [11, 14], None], ["state", W0_6, [W0_4]], ["state", [11, 14], [[11, 14]]],
+        ["add", [10, 13], [10, 14], {"target": [10, 14], "state_window": [[11, 14]], "sources": [[11, 14]],
+                                     "merged_state_windows": [[]]}],
+        ["add", [12, 15], [10, 15], {"target": [10, 15], "state_window": [[11, 14]], "sources": [[10, 14]],
+                                     "merged_state_windows": [[]]}],
+        ["add", [11, 14], [10, 15], None],
+        ["state", W0_6, [W0_4]], ["state", [10, 15], [[11, 14]]],
+        ["retire", W0_6], ["state", W0_6, None], ["state", [10, 15], [[11, 14]]],
+    ]},
+    {"name": "late_merging", "source": MWST + ":208-303", "restore": [], "steps": [
+        ["add", [0, 3], [0, 3], None], ["state", [0, 3], [[0, 3]]],
+        ["add", [5, 8], [5, 8], None], ["state", [5, 8], [[5, 8]]],
+        ["add", [10, 13], [10, 13], None], ["state", [10, 13], [[10, 13]]],
+        ["add", [8, 10], [5, 13], {"target": [5, 13], "state_window": [[5, 8], [10, 13]],
+                                   "sources": [[5, 8], [10, 13]],
+                                   "merged_state_windows": [[[10, 13]], [[5, 8]]]}],
+        ["state", [0, 3], [[0, 3]]],
+        ["add", [5, 8], [5, 13], None], ["add", [8, 10], [5, 13], None], ["add", [10, 13], [5, 13], None],
+        ["state", [5, 13], [[5, 8], [10, 13]]],
+        ["add", [3, 5], [0, 13], {"target": [0, 13], "state_window": [[0, 3], [5, 8], [10, 13]],
+                                  "sources": [[0, 3], [5, 13]],
+                                  "merged_state_windows": [[[0, 3]], [[5, 8]], [[10, 13]]]}],
+        ["state", [0, 13], [[0, 3], [5, 8], [10, 13]]],
+    ]},
+    {"name": "large_window_covering_single_window", "source": MWST + ":305-332", "restore": [], "steps": [
+        ["add", [1, 2], [1, 2], None], ["state", [1, 2], [[1, 2]]],
+        ["add", [0, 3], [0, 3], {"target": [0, 3], "state_window": [[1, 2]], "sources": [[1, 2]],
+                                 "merged_state_windows": None}],
+        ["state", [0, 3], [[1, 2]]],
+    ]},
+    {"name": "adding_identical_windows", "source": MWST + ":334-360", "restore": [], "steps": [
+        ["add", [1, 2], [1, 2], None], ["state", [1, 2], [[1, 2]]],
+        ["add", [1, 2], [1, 2], None], ["state", [1, 2], [[1, 2]]],
+    ]},
+    {"name": "large_window_covering_multiple_windows", "source": MWST + ":362-419", "restore": [], "steps": [
+        ["add", [1, 3], [1, 3], None], ["state", [1, 3], [[1, 3]]],
+        ["add", [5, 8], [5, 8], None], ["state", [5, 8], [[5, 8]]],
+        ["add", [10, 13], [10, 13], None], ["state", [10, 13], [[10, 13]]],
+        # transcribed as written (:402-415): the alternatives name (0, 3), which the set never
+        # holds (the first window is (1, 3)), so only {(5, 8), (10, 13)} can pass -- the
+        # reference's HashSet order makes (1, 3) the state window here, and so must the oracle
+        ["add", [0, 13], [0, 13], {"target": [0, 13], "state_window": [[1, 3], [5, 8], [10, 13]],
+                                   "sources": [[1, 3], [5, 8], [10, 13]],
+                                   "merged_state_windows": [[[0, 3], [5, 8]], [[0, 3], [10, 13]],
+                                                            [[5, 8], [10, 13]]]}],
+        ["state", [0, 13], [[1, 3], [5, 8], [10, 13]]],
+    ]},
+    {"name": "restore_from_state", "source": MWST + ":421-438",
+     "restore": [[[17, 42], [42, 17]], [[1, 2], [3, 4]]], "steps": [
+        ["state", [17, 42], [[42, 17]]], ["state", [1, 2], [[3, 4]]],
+    ]},
+    {"name": "persist", "source": MWST + ":440-472", "restore": [], "steps": [
+        ["add", [1, 2], [1, 2], None], ["add", [17, 42], [17, 42], None],
+        ["state", [1, 2], [[1, 2]]], ["state", [17, 42], [[17, 42]]],
+        ["persist", [[[1, 2], [1, 2]], [[17, 42], [17, 42]]]],
+    ]},
+    {"name": "persist_only_if_have_updates", "source": MWST + ":474-495",
+     "restore": [[[17, 42], [42, 17]], [[1, 2], [3, 4]]], "steps": [
+        ["state", [17, 42], [[42, 17]]], ["state", [1, 2], [[3, 4]]],
+        ["persist", [[[1, 2], [3, 4]], [[17, 42], [42, 17]]]],
+    ]},
+]
+dump("merging_window_set.json", {"source": MWST, "gap": 3, "tests": mws_tests})
+
+# --------------------------------------------------------------------------------------
 # Operator harness tests (KeyedOneInputStreamOperatorTestHarness, HashMapStateBackend).
 # ops: ["e", key, value, ts] | ["w", wm, [expected rows]]
 # expected row: [key, result, timestamp(=end-1), start|null, end|null]

@@ -10,7 +10,7 @@ ACC_BYTES = {"sum_i32": 4, "avg_i64": 16, "avg_f64": 16}
 
 
 def parse(blob: bytes, agg: str):
-    """-> dict kg -> {"state": [(start, end, key, acc..., [key hash])], "sets": [(key, ((w, sw), ...))],
+    """-> dict kg -> {"state": [(start, end, key, acc..., [key hash])], "sets": [(key, ((w, sw), ...), [key hash])],
     "timers": [(ts, key, start, end)]}; acc as raw big-endian ints (doubles by their bits)."""
     h = HDR.unpack(blob[:96])
     assert h[0] == b"GWS1" and h[1] == 4, h[:2]
@@ -34,11 +34,14 @@ def parse(blob: bytes, agg: str):
             state.append((s, e, k) + acc + kh)
         m, = struct.unpack_from(">i", pay, p); p += 4
         sets = []
-        for _ in range(m):
-            k, c = struct.unpack_from(">qi", pay, p); p += 12
+        for _ in range(m):  # (key, [be32 key hash,] be32 c, c x (window, state window))
+            k, = struct.unpack_from(">q", pay, p); p += 8
+            kh = struct.unpack_from(">i", pay, p) if hb else ()
+            p += hb
+            c, = struct.unpack_from(">i", pay, p); p += 4
             ws = [struct.unpack_from(">qqqq", pay, p + 32 * j) for j in range(c)]
             p += 32 * c
-            sets.append((k, tuple(sorted(ws))))
+            sets.append((k, tuple(sorted(ws))) + kh)
         t, = struct.unpack_from(">i", pay, p); p += 4
         timers = []
         for _ in range(t):
@@ -47,3 +50,20 @@ def parse(blob: bytes, agg: str):
         assert p == offs[g + 1]
         out[kg_lo + g] = {"state": sorted(state), "sets": sorted(sets), "timers": sorted(timers)}
     return out
+
+
+def normalize_sessions(sec):
+    """One key group's session state with every entry filed under its window instead of its
+    state window (the merging window set maps window -> state window, MergingWindowSet.java:
+    116; the reference keeps a merged session's state under one of its original windows,
+    :188-201, the GPU under the session itself): -> (state, sets) with sets as (key, windows)."""
+    ns = {}
+    for x in sec["sets"]:
+        for (s, e, ss, se) in x[1]:
+            ns[(x[0], ss, se)] = (s, e)
+    state = []
+    for x in sec["state"]:
+        s, e = ns[(x[2], x[0], x[1])]
+        state.append((s, e) + x[2:])
+    sets = [(x[0], tuple((w[0], w[1]) for w in x[1])) + x[2:] for x in sec["sets"]]
+    return sorted(state), sorted(sets)

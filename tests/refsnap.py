@@ -19,7 +19,8 @@ then varint chars), namespaces TimeWindow (start, end: TimeWindow.Serializer :15
 """
 import struct
 
-STATE_NAMES = ("window-contents", "_timer_state/processing_window-timers", "_timer_state/event_window-timers")
+STATE_NAMES = ("window-contents", "_timer_state/processing_window-timers", "_timer_state/event_window-timers",
+               "merging-window-set", "count")
 
 
 class Reader:
@@ -115,8 +116,13 @@ def state_ids(backend: bytes):
 
 def parse(data: bytes, value_reader=None):
     """-> {key group: {"state": [(start, end, key, value)], "event": [(ts, key, start, end)],
-    "processing": [...]}}.  value_reader(Reader) decodes one state value (default: the
-    Tuple2<String, Integer> of WindowOperatorMigrationTest's reducing state)."""
+    "processing": [...], "sets": [(key, [((start, end), (state start, state end))])],
+    "count": [(start, end, key, count)]}}.  value_reader(Reader) decodes one state value
+    (default: the Tuple2<String, Integer> of WindowOperatorMigrationTest's reducing state).
+    Session snapshots also hold the MergingWindowSet ListState "merging-window-set"
+    (MergingWindowSet.persist :99-106; namespace VoidNamespace = one byte,
+    VoidNamespaceSerializer.java:62-70; value ListSerializer :118-128 = int n, then n
+    Tuple2<TimeWindow, TimeWindow>) and, under a CountTrigger, its ReducingState<Long> "count"."""
     vr = value_reader or (lambda r: (r.jstring(), r.i32()))
     start, count, offs, be = keyed_state(data)
     ids = state_ids(be)
@@ -127,7 +133,7 @@ def parse(data: bytes, value_reader=None):
         kg = r.i32()
         if kg != start + i:
             raise ValueError(f"key group {kg} at position {i}")
-        sec = {"state": [], "event": [], "processing": []}
+        sec = {"state": [], "event": [], "processing": [], "sets": [], "count": []}
         while r.p < end:
             name = ids[r.i16()]
             n = r.i32()
@@ -136,6 +142,15 @@ def parse(data: bytes, value_reader=None):
                     s, e = r.i64(), r.i64()
                     k = r.jstring()
                     sec["state"].append((s, e, k, vr(r)))
+                elif name == "merging-window-set":
+                    if r.u8() != 0:
+                        raise ValueError("VoidNamespace byte")
+                    k = r.jstring()
+                    sec["sets"].append((k, [((r.i64(), r.i64()), (r.i64(), r.i64())) for _ in range(r.i32())]))
+                elif name == "count":
+                    s, e = r.i64(), r.i64()
+                    k = r.jstring()
+                    sec["count"].append((s, e, k, r.i64()))
                 else:
                     ts = r.i64() ^ -(1 << 63)
                     k = r.jstring()
@@ -147,15 +162,29 @@ def parse(data: bytes, value_reader=None):
     return out
 
 
-def migration_fixtures():
-    """Paths of the committed reduce-event-time fixtures, by Flink version."""
+def migration_fixtures(kind="reduce-event-time"):
+    """Paths of the committed fixtures of one kind ("reduce-event-time",
+    "session-with-stateful-trigger"), by Flink version."""
     import glob
     import os
     here = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "ref_snapshots")
     out = {}
-    for f in sorted(glob.glob(os.path.join(here, "win-op-migration-test-reduce-event-time-flink*-snapshot"))):
+    for f in sorted(glob.glob(os.path.join(here, f"win-op-migration-test-{kind}-flink*-snapshot"))):
         out[f.split("-flink")[1].replace("-snapshot", "")] = f
     return out
+
+
+def list_value(r):
+    """ListState<Tuple2<String, Integer>> contents (ListSerializer: int n + the elements)."""
+    return [(r.jstring(), r.i32()) for _ in range(r.i32())]
+
+
+# WindowOperatorMigrationTest.writeSessionWindowsWithCountTriggerSnapshot (:97-152):
+# EventTimeSessionWindows.withGap(3 s), PurgingTrigger(CountTrigger(4)), the records below
+# (key, value, ts) in arrival order, no watermark, then the snapshot.
+SESSION_MIGRATION_GAP = 3000
+SESSION_MIGRATION_INPUT = [("key2", 1, 0), ("key2", 2, 1000), ("key2", 3, 2500), ("key2", 4, 3500),
+                           ("key1", 1, 10), ("key1", 2, 1000)]
 
 
 # WindowOperatorMigrationTest.java:407-426 (records, in arrival order) and the watermarks after them
@@ -188,5 +217,34 @@ def to_gpuwin_blob(parsed, ids, java_hash, agg_code, assigner_code, size, slide,
         pay += part
     offs.append(len(pay))
     hdr = struct.pack("<4sIii5q4i3q", b"GWS1", 4, agg_code, assigner_code, size, slide, offset, 0, 1,
+                      max_parallelism, lo, hi, 0, 0, 0, len(pay))
+    return hdr + struct.pack(f"<{len(offs)}q", *offs) + pay
+
+
+def to_gpuwin_session_blob(parsed, ids, java_hash, agg_code, assigner_code, gap, max_parallelism=1):
+    """A parsed reference session snapshot as a gw_snapshot version-4 blob with key hashes:
+    "window-contents" entries (state window, key) with the sum of the listed elements' Int
+    field as an IntSerializer accumulator, the merging window sets (window -> state window) and
+    the event-time timers."""
+    kgs = sorted(parsed)
+    lo, hi = kgs[0], kgs[-1]
+    pay, offs = b"", []
+    for kg in range(lo, hi + 1):
+        offs.append(len(pay))
+        sec = parsed.get(kg, {"state": [], "sets": [], "event": []})
+        part = struct.pack(">i", len(sec["state"]))
+        for s, e, k, v in sec["state"]:
+            part += struct.pack(">qqqii", s, e, ids[k], java_hash(k), sum(x[1] for x in v))
+        part += struct.pack(">i", len(sec["sets"]))
+        for k, ws in sec["sets"]:
+            part += struct.pack(">qii", ids[k], java_hash(k), len(ws))
+            for (s, e), (ss, se) in ws:
+                part += struct.pack(">qqqq", s, e, ss, se)
+        part += struct.pack(">i", len(sec["event"]))
+        for ts, k, s, e in sec["event"]:
+            part += struct.pack(">qqqq", ts ^ -(1 << 63), ids[k], s, e)
+        pay += part
+    offs.append(len(pay))
+    hdr = struct.pack("<4sIii5q4i3q", b"GWS1", 4, agg_code, assigner_code, 0, 0, 0, gap, 1,
                       max_parallelism, lo, hi, 0, 0, 0, len(pay))
     return hdr + struct.pack(f"<{len(offs)}q", *offs) + pay

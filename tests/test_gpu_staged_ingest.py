@@ -141,3 +141,32 @@ def test_sent_ahead_order_is_checked():
             op.stage_send(3, 10)  # two batches ahead at most (three device buffers)
     finally:
         op.close()
+
+
+def test_staging_is_not_reallocated_under_the_caller(oracle_lib):
+    """Pinned slots handed out by gw_stage_columns (JVM direct ByteBuffers point into them) and
+    batches sent ahead stay valid: a gw_ingest of the same handle (it copies through those slots,
+    and a larger batch would reallocate them) is refused with GW_E_STATE, and the sent batch
+    still ingests exactly (against the oracle)."""
+    kw = dict(assigner="tumbling", size=1000, slide=1000, agg="sum_i64")
+    keys, ts, vals, batches = random_stream(seed=64, n=300, num_keys=50, n_batches=1, agg="sum_i64")
+    op = gpu_operator(kw)
+    try:
+        op.stage_alloc(2, 100)
+        k, _, t, v = op.stage_columns(0)
+        k[:100], t[:100], v[:100] = keys[:100], ts[:100], vals[:100]
+        op.stage_send(0, 100)
+        with pytest.raises(N.GpuWinError) as ei:
+            op.process_batch(keys[100:300], ts[100:300], vals[100:300])  # 200 records: larger slots
+        assert ei.value.code == N.GW_E_STATE
+        op.ingest_stage(0, 100)
+        with pytest.raises(N.GpuWinError) as ei:
+            op.process_batch(keys[100:150], ts[100:150], vals[100:150])
+        assert ei.value.code == N.GW_E_STATE
+        op.advance_watermark(W.LONG_MAX)
+        k_, s_, e_, r_ = op.drain()
+    finally:
+        op.close()
+    o, _ = run_oracle(oracle_lib, kw, keys[:100], ts[:100], vals[:100], [(0, 100, W.LONG_MIN)])
+    assert compare([(np.empty(0, np.int64),) * 4, (k_, s_, e_, r_)], o, False) == []
+

@@ -4,8 +4,8 @@
   WindowStagger.java:27-60): the stagger is drawn at the first element, so the handle is created
   then, with offset (offset + stagger) % size.  TumblingEventTimeWindowsTest.
   testWindowAssignmentWithStagger's vectors (tests/golden/stagger.json) through the operator,
-  RANDOM against the oracle at the drawn offset, watermarks before the first element, and the
-  refused restore into a staggered operator.
+  RANDOM against the oracle at the drawn offset, watermarks before the first element, and a
+  staggered operator restoring under the stagger its state was written with.
 * reduce / aggregate with a window function (WindowedStream.java:224-276, 342-526;
   InternalSingleValueProcessWindowFunction): the function gets the key, the window and a
   one-element list holding the GPU's pre-aggregated result; its output is stamped
@@ -60,23 +60,67 @@ def test_random_stagger_matches_oracle_at_the_drawn_offset(oracle_lib, monkeypat
     assert compare(outs, o, False) == []
 
 
-def test_staggered_operator_refuses_restored_state():
-    a = W.GpuWindowOperator(W.TumblingEventTimeWindows.of(1000), "count").open()
+@pytest.mark.parametrize("stagger", [W.WindowStagger.RANDOM, W.WindowStagger.NATURAL])
+def test_staggered_operator_restores_under_the_drawn_stagger(oracle_lib, stagger):
+    """A staggered operator that fails over restores its window state and timers
+    (TumblingEventTimeWindows.java:53,72-79 draws a fresh stagger after a restore; one handle
+    holds one alignment, so the stagger the state was written under is reused): the restored
+    run fires exactly what the uninterrupted one does.  A restore without window state still
+    draws at the first element; blobs drawn with different staggers are refused."""
+    size = 1000
+    keys, ts, vals, batches = random_stream(seed=23, n=8000, num_keys=150, n_batches=8, agg="sum_i64")
+
+    def mk(ptime):
+        return W.GpuWindowOperator(W.TumblingEventTimeWindows.of(size, 0, stagger), "sum_i64",
+                                   processing_time=lambda: ptime).open()
+
+    def feed(op, bs, outs):
+        for lo, hi, wm in bs:
+            op.process_batch(keys[lo:hi], ts[lo:hi], vals[lo:hi])
+            op.advance_watermark(wm)
+            k, s, e, r = op.drain()
+            outs.append((k, s, e, r))
+
+    import random
+    rnd = random.random
+    random.random = lambda: 0.25
     try:
-        a.process_batch(np.arange(10, dtype=np.int64), np.arange(10, dtype=np.int64) * 50)
+        full, outs = mk(333), []
+        feed(full, batches, outs)
+        full.advance_watermark(W.LONG_MAX)
+        outs.append(full.drain())
+        full.close()
+        a, got = mk(333), []
+        feed(a, batches[:4], got)
         blob = a.snapshot_state()
-    finally:
         a.close()
-    b = W.GpuWindowOperator(W.TumblingEventTimeWindows.of(1000, 0, W.WindowStagger.NATURAL), "count",
-                            processing_time=lambda: 7).open()
+        random.random = lambda: 0.75  # a fresh draw would differ
+        b = mk(777)
+        b.initialize_state(blob)
+        feed(b, batches[4:], got)
+        b.advance_watermark(W.LONG_MAX)
+        got.append(b.drain())
+        b.close()
+    finally:
+        random.random = rnd
+    assert compare(got, outs, False) == []
+    c = mk(7)  # a blob without window state: the stagger is still drawn at the first element
     try:
-        empty = b.snapshot_state()  # no element yet: no window state
-        assert len(empty) > 0
+        c.initialize_state(c.snapshot_state())
+        assert c._deferred
+    finally:
+        c.close()
+    other = W.GpuWindowOperator(W.TumblingEventTimeWindows.of(size, 400), "sum_i64").open()
+    other.process_batch(keys[:50], ts[:50], vals[:50])
+    oblob = other.snapshot_state()
+    other.close()
+    d = mk(7)
+    try:
         with pytest.raises(N.GpuWinError) as ei:
-            b.initialize_state(blob)
+            d.initialize_state([blob, oblob])
         assert ei.value.code == N.GW_E_UNSUPPORTED
     finally:
-        b.close()
+        d.close()
 
 
 def test_aggregate_with_process_window_function():

@@ -115,6 +115,46 @@ def test_merge_windows(oracle_lib):
         assert sorted(got) == sorted(exp)
 
 
+@pytest.mark.parametrize("test", load_golden("merging_window_set.json")["tests"], ids=lambda t: t["name"])
+def test_merging_window_set_vectors(oracle_lib, test):
+    """MergingWindowSetTest (MergingWindowSet.java:77-224 driven directly): the result window of
+    every addWindow, whether the MergeFunction ran and with which merge result, sources, state
+    window and merged state windows, getStateWindow, retireWindow and the persisted list."""
+    def w(x):
+        return None if x is None else (x[0], x[1])
+
+    m = oracle_lib.MergingWindowSet([(w(a), w(b)) for a, b in test["restore"]])
+    try:
+        for st in test["steps"]:
+            if st[0] == "add":
+                res, merge = m.add_window(w(st[1]))
+                assert res == w(st[2]), st
+                exp = st[3]
+                if exp is None:
+                    assert merge is None, st
+                    continue
+                assert merge is not None, st
+                assert merge["target"] == w(exp["target"]), st
+                assert merge["state_window"] in [w(x) for x in exp["state_window"]], st
+                assert sorted(merge["sources"]) == sorted(w(x) for x in exp["sources"]), st
+                # mergedStateWindows never holds the merge target (:260, :300)
+                assert merge["target"] not in merge["merged_state_windows"]
+                if exp["merged_state_windows"] is not None:
+                    alts = [sorted(w(x) for x in alt) for alt in exp["merged_state_windows"]]
+                    assert sorted(merge["merged_state_windows"]) in alts, st
+            elif st[0] == "state":
+                got = m.state_window(w(st[1]))
+                assert (got is None) if st[2] is None else got in [w(x) for x in st[2]], st
+            elif st[0] == "retire":
+                m.retire(w(st[1]))
+            elif st[0] == "persist":
+                assert m.persisted() == sorted((w(a), w(b)) for a, b in st[1]), st
+        with pytest.raises(oracle_lib.OracleError):  # retireWindow of a window not in flight (:125-131)
+            m.retire((-5, -1))
+    finally:
+        m.close()
+
+
 @pytest.mark.parametrize("test", load_golden("operator_harness.json")["tests"], ids=lambda t: t["name"])
 def test_operator_harness_vectors(oracle_lib, test):
     o = oracle_lib

@@ -99,3 +99,41 @@ def test_key_table_and_remap_on_cpu():
     assert sorted((t, m[k], s, e) for t, k, s, e in p0["timers"]) == p1["timers"]
     with pytest.raises(N.GpuWinError):
         N.snapshot_remap_keys(blob[:-3], {0: 1})
+
+
+# ---------------------------------------------------------------- session windows
+SESSION_FIXTURES = refsnap.migration_fixtures("session-with-stateful-trigger")
+
+
+def test_session_fixtures_pin_the_merging_window_set_layout():
+    """writeSessionWindowsWithCountTriggerSnapshot (WindowOperatorMigrationTest.java:97-152) for
+    16 Flink versions: the heap backend writes the MergingWindowSet as the ListState
+    "merging-window-set" (VoidNamespace, key, list of (window, state window)), and a session
+    keeps its state under the window it started as: key1's [10, 4000) under [10, 3010), key2's
+    [0, 6500) under [0, 3000).  The oracle's MergingWindowSet, fed the same records, holds
+    exactly that mapping and the same event-time timers (maxTimestamp = cleanup time at
+    lateness 0), and files key1's state (1 + 2) under the same state window.  Key2's contents
+    differ by design: the fixture's PurgingTrigger(CountTrigger(4)) purged them on key2's 4th
+    element; the oracle runs EventTimeTrigger (the closed set)."""
+    assert len(SESSION_FIXTURES) == 16, sorted(SESSION_FIXTURES)
+    parsed = {v: refsnap.parse(open(p, "rb").read(), refsnap.list_value) for v, p in SESSION_FIXTURES.items()}
+    ref = parsed["2.2"]
+    assert all(p == ref for p in parsed.values())
+    sec = ref[0]
+    op = O.OracleOperator(O.make_config("session", gap=refsnap.SESSION_MIGRATION_GAP, agg="sum_i32",
+                                        max_parallelism=1))
+    inp = refsnap.SESSION_MIGRATION_INPUT
+    keys = np.array([IDS[k] for k, _, _ in inp], np.int64)
+    op.set_key_hashes(keys, np.array([java_string_hash(k) for k, _, _ in inp], np.int32))
+    op.process_batch(keys, np.array([t for _, _, t in inp], np.int64), np.array([v for _, v, _ in inp], np.int64))
+    got = heapsnap.parse(op.snapshot((0, 0)), "sum_i32")[0]
+    op.close()
+    sets = sorted((KEYS[x[0]], sorted(((a, b), (c, d)) for a, b, c, d in x[1])) for x in got["sets"])
+    assert sets == sorted((k, sorted(ws)) for k, ws in sec["sets"])
+    for x in got["sets"]:  # the set record carries the key's String.hashCode
+        assert x[2] == java_string_hash(KEYS[x[0]])
+    assert sorted((t, KEYS[k], s, e) for t, k, s, e in got["timers"]) == sorted(sec["event"])
+    st = {(KEYS[k], s, e): v for s, e, k, v, *_ in got["state"]}
+    for s, e, k, elems in sec["state"]:
+        assert st[(k, s, e)] == sum(v for _, v in elems)  # key1 under [10, 3010): 1 + 2
+    assert st[("key2", 0, 3000)] == 10  # key2's state window is the fixture's [0, 3000)
