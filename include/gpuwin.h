@@ -236,15 +236,20 @@ int  gw_flush(gw_handle* h);
  *   (no merging window set), be32 t + t event-time timers (flipSignBit(ts), key, start,
  *   end) as TimerSerializer.serialize writes them (:147-152; the window's maxTimestamp
  *   and, under lateness, its cleanup time);
- *   version 2 (session windows): every in-flight session as (key, start, end, a0, a1,
- *   fired) int64 words -- the (key, window) state plus the merging window set
- *   (MergingWindowSet.java:95-104);
+ *   version 4 (session windows): the same three sections -- be32 n + n "window-contents"
+ *   entries (state window, key, [be32 key hash,] state) of the sessions holding state (a
+ *   session fired under PurgingTrigger holds none), be32 m + m "merging-window-set" records
+ *   (key, [be32 key hash,] be32 c, c x (window, state window)) as MergingWindowSet.persist
+ *   writes its ListState (:99-106), be32 t + t timers (maxTimestamp while a session has not
+ *   fired; its cleanup time under allowed lateness).  libgpuwin names each session as its own
+ *   state window; a restore takes any state window the set names (the reference keeps a
+ *   merged session's state under one of its original windows, MergingWindowSet.java:188-201);
  *   version 3 (count windows): per key (key, element count, ring of count-pane
  *   accumulators): the CountTrigger count and the evicting operator's window contents.
  * Keys fed with a key_hash column (String, Integer, ... keys as caller ids) are filed
  * under the key group of that hash (KeyGroupRangeAssignment.java:63-66), and the blob
- * carries each entry's key hash (header flags bit 0: a be32 after the key in version 4,
- * one more int64 word per entry in versions 2 and 3).  A window-class composite writes
+ * carries each entry's key hash (header flags bit 0: a be32 after the key of every
+ * version-4 entry and merging-window-set record, one more int64 word per entry in version 3).  A window-class composite writes
  * its classes' entries merged per key group.  Two calls: buf == NULL returns the size in
  * *len; then a buffer of cap >= *len. */
 int  gw_snapshot(gw_handle* h, int32_t kg_lo, int32_t kg_hi, void* buf, int64_t cap, int64_t* len);
