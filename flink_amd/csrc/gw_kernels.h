@@ -197,21 +197,12 @@ struct IngestArgs {
     DevStatus* st_host;             // buffered P1: pinned host slot k_publish_status copies the status into
     unsigned long long st_seq;      //     and the stamp it writes last
     uint64_t ring_fresh;            // ring positions holding only identities (not in occ)
-    // narrow single-pass flushes (a.nar1; k_rgn_p1n / k_rgn_apply_n1, gw_pane.hip): P1 sorts each
-    // 8192-record tile straight by super-region (2^sr_bits probe regions), one workgroup per
-    // super-region applies its runs from every tile of the flush -- no P2
-    int32_t nar1;
-    int32_t n1_nb;                  // super-regions = P1 buckets (<= kN1MaxBuckets)
-    uint16_t* n1_row;               // [tile][n1_nb + 1] first record of each bucket; [n1_nb]: the tile's count
-    uint8_t* n1_occ;                // [tile] ring positions of the tile's records
 };
 
 #ifndef GW_PART_TILE
 #define GW_PART_TILE 4096
 #endif
 constexpr int kPartTile = GW_PART_TILE;  // records per P1 tile / P2 round (LDS-sorted)
-constexpr int kN1Tile = 8192;            // records per nar1 P1 tile (= 2 kPartTile units of the buffer)
-constexpr int kN1MaxBuckets = 4096;      // nar1 super-regions (P1 buckets) at most
 constexpr int kPartBuckets = 256;   // descriptor row width (<= 8 region bits per pass)
 constexpr int kRgnMaxRegions = 65536;
 constexpr int kMaxGroup = 256;      // P1 tiles per P2 block (G = 7/4 of the pass-1 buckets; LDS keeps 4 blocks per CU)

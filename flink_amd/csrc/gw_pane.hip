@@ -1875,499 +1875,6 @@ __global__ void __launch_bounds__(256) k_rgn_collect_nar2(IngestArgs a) {
     }
 }
 
-// ---------------------------------------------------------------------------
-// Narrow single-pass flushes (a.nar1): P1 sorts each 8192-record tile by super-region --
-// the table's top (log2nreg - sr_bits) hash bits, 2^sr_bits probe regions each -- and the
-// flush is ONE kernel: a workgroup per super-region walks its run of every buffered tile
-// (descriptor rows of 16-bit starts) and applies it in LDS as k_rgn_apply_nar does.  Each
-// record is written once (P1) and read once (apply) between the input and the state, against
-// twice each through P2.  A tile's runs are short (~4 records at 2048
-// super-regions); consecutive super-regions run on one XCD at the same time (the blockIdx
-// mapping below), so they read each descriptor line and each run line through that XCD's L2.
-// ---------------------------------------------------------------------------
-constexpr int kN1Threads = 1024;
-constexpr int kN1Items = kN1Tile / kN1Threads;
-constexpr int kN1ApplyThreads = 1024;
-constexpr int kN1U = 4;  // records per lane whose loads are in flight together
-
-__device__ __forceinline__ int n1_bucket(const IngestArgs& a, uint64_t h) {
-    const int bits = a.t.log2nreg - a.sr_bits;
-    return bits <= 0 ? 0 : (int)(h >> (64 - bits));
-}
-
-// Exclusive block scan of c[0..n) into s[0..n], s[n] = total (n <= 8 * blockDim.x; s may be c:
-// each thread reads its own entries before it writes them).
-__device__ __forceinline__ void block_scan_n(const uint32_t* c, uint32_t* s, int n, uint32_t* wsum) {
-    const int t = threadIdx.x, lane = t & 63, w = t >> 6, nw = blockDim.x >> 6;
-    const int per = (n + blockDim.x - 1) / blockDim.x;  // <= 8
-    uint32_t v[8], sum = 0;
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-        const int i = t * per + q;
-        v[q] = q < per && i < n ? c[i] : 0u;
-        sum += v[q];
-    }
-    uint32_t incl = sum;
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t up = __shfl_up(incl, o);
-        if (lane >= o) incl += up;
-    }
-    if (lane == 63) wsum[w] = incl;
-    __syncthreads();
-    uint32_t off = 0;
-    for (int q = 0; q < w; ++q) off += wsum[q];
-    uint32_t ex = off + incl - sum;
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-        const int i = t * per + q;
-        if (q < per && i < n) s[i] = ex;
-        ex += v[q];
-    }
-    if (t == blockDim.x - 1) {
-        uint32_t tot = 0;
-        for (int q = 0; q < nw; ++q) tot += wsum[q];
-        s[n] = tot;
-    }
-    __syncthreads();
-}
-
-template <int AGG>
-__global__ void __launch_bounds__(kN1Threads) GW_P1_ATTR k_rgn_p1n(IngestArgs a) {
-    if constexpr (!cmp_agg<AGG>()) {
-        return;
-    } else {
-    constexpr bool N4 = AGG == GW_COUNT;
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const int nb = a.n1_nb;
-    uint64_t* s_r64 = reinterpret_cast<uint64_t*>(smem);
-    uint32_t* s_r32 = reinterpret_cast<uint32_t*>(smem);
-    // bucket counts, then (scanned in place) bucket starts, [nb] = the tile's count
-    uint32_t* lh = reinterpret_cast<uint32_t*>(smem + (size_t)kN1Tile * (N4 ? 4 : 8));  // [nb + 1]
-    uint32_t* ls = lh;
-    __shared__ uint32_t wsum[kN1Threads / 64];
-    __shared__ unsigned long long s_occ;
-    const int64_t g = blockIdx.x;
-    const int64_t lo = g * kN1Tile, hi = min(a.n, lo + (int64_t)kN1Tile);
-    if (g == 0 && threadIdx.x < 64 && a.st_host) publish_status_wave(a.st, a.st_host, a.st_seq);
-    for (int b = threadIdx.x; b < nb; b += kN1Threads) lh[b] = 0;
-    if (threadIdx.x == 0) s_occ = 0;
-    int64_t key[kN1Items], ts[kN1Items], val[kN1Items];
-#pragma unroll
-    for (int it = 0; it < kN1Items; ++it) {  // all loads in flight first
-        const int64_t i = lo + it * kN1Threads + threadIdx.x;
-        key[it] = 0; ts[it] = 0; val[it] = 0;
-        if (i < hi) {
-            key[it] = __builtin_nontemporal_load(a.key + i);
-            ts[it] = __builtin_nontemporal_load(a.ts + i);
-            if (a.val) val[it] = __builtin_nontemporal_load(a.val + i);
-        }
-    }
-    __syncthreads();  // lh zeroed
-    unsigned long long late = 0, flags = 0, occ = 0, wide = 0;
-    bool special = false;
-    uint64_t rec[kN1Items];
-    uint32_t br[kN1Items];  // bucket << 14 | rank, ~0: none
-#pragma unroll
-    for (int it = 0; it < kN1Items; ++it) {
-        const int64_t i = lo + it * kN1Threads + threadIdx.x;
-        int64_t v0 = 0, v1 = 0, pane = 0;
-        uint32_t ps = 0;
-        int st = REC_SKIP;
-        if (i < hi) st = classify<AGG, false>(a, ts[it], val[it], ps, pane, v0, v1, late, flags);
-        if (st == REC_RING &&
-            ((uint64_t)key[it] >= (uint64_t)(N4 ? kNarCountKeyLimit : kNarKeyLimit) ||
-             (!N4 && (v0 < -kNarValLimit || v0 >= kNarValLimit)))) {
-            st = REC_DEFER;  // beyond the narrow record (the sentinel key too): the deferred list
-            wide++;
-        }
-        br[it] = ~0u;
-        rec[it] = 0;
-        if (st == REC_RING) {
-            occ |= 1ull << ps;
-            const int bk = n1_bucket(a, slot_hash(key[it]));
-            rec[it] = N4 ? (uint64_t)nar_pack32(key[it], ps) : nar_pack(key[it], v0, ps);
-            br[it] = ((uint32_t)bk << 14) | atomicAdd(&lh[bk], 1u);
-        } else if (st != REC_SKIP) {
-            special = true;
-        }
-    }
-    // deferred / re-fire / side-output records: a second pass in the waves holding one
-    if (__any(special)) {
-#pragma unroll 1
-        for (int it = 0; it < kN1Items; ++it) {
-            const int64_t i = lo + it * kN1Threads + threadIdx.x;
-            int64_t k = 0, v0 = 0, v1 = 0, pane = 0;
-            uint32_t ps = 0;
-            int st = REC_SKIP;
-            if (i < hi) {
-                unsigned long long dl = 0, df = 0;
-                k = a.key[i];
-                st = classify<AGG, false>(a, a.ts[i], a.val ? a.val[i] : 0, ps, pane, v0, v1, dl, df);
-                if (st == REC_RING &&
-                    ((uint64_t)k >= (uint64_t)(N4 ? kNarCountKeyLimit : kNarKeyLimit) ||
-                     (!N4 && (v0 < -kNarValLimit || v0 >= kNarValLimit))))
-                    st = REC_DEFER;
-            }
-            defer_write(a, st == REC_DEFER, k, pane, v0, v1);
-            refire_write(a, st == REC_REFIRE, k, pane, v0, v1, i);
-            if (a.lo_key) late_write(a, st == REC_LATE, k, i);
-        }
-    }
-    {
-        const unsigned long long ow = wave_ior(occ);
-        if (__lane_id() == 0 && ow) atomicOr(&s_occ, ow);
-    }
-    __syncthreads();
-    block_scan_n(lh, ls, nb, wsum);  // ends with a barrier
-    if (threadIdx.x == 0 && s_occ) atomicOr(a.batch_occ, s_occ);
-#pragma unroll
-    for (int it = 0; it < kN1Items; ++it) {
-        if (br[it] == ~0u) continue;
-        const uint32_t j = ls[br[it] >> 14] + (br[it] & 0x3fffu);
-        if constexpr (N4) s_r32[j] = (uint32_t)rec[it];
-        else s_r64[j] = rec[it];
-    }
-    __syncthreads();
-    const uint32_t cnt = ls[nb];
-    const int64_t tile = a.tile0 + g;
-    const int64_t base = tile * kN1Tile;
-    for (uint32_t j = threadIdx.x; j < cnt; j += kN1Threads) {
-        if constexpr (N4) __builtin_nontemporal_store(s_r32[j], reinterpret_cast<uint32_t*>(a.p1_key) + base + j);
-        else __builtin_nontemporal_store(s_r64[j], reinterpret_cast<uint64_t*>(a.p1_key) + base + j);
-    }
-    uint16_t* row = a.n1_row + tile * (int64_t)(nb + 1);
-    for (int b = threadIdx.x; b <= nb; b += kN1Threads) row[b] = (uint16_t)ls[b];
-    if (threadIdx.x == 0) a.n1_occ[tile] = (uint8_t)s_occ;
-    wide = wave_sum(wide);
-    if (__lane_id() == 0 && wide) atomicAdd(&a.st->wide_vals, wide);
-    block_commit(a.st, late, 0, flags, occ);
-    }
-}
-
-// The flush of a nar1 buffer: one workgroup per super-region (F = 2^sr_bits regions of S
-// slots, consecutive in memory); keys (32-bit) and presence masks in LDS throughout, one
-// ring position's pane at a time.  Per position, the waves take 64 tiles at a time: each
-// lane reads its tile's run bounds (two 16-bit starts), a wave scan lays the runs end to end,
-// and every lane finds the run of each of its records by a search over the lanes' offsets
-// (shuffles), loads kN1U records together and applies them (probe of the home group in LDS;
-// misses through the wave's queue).  The next 64 tiles' bounds load while this chunk applies.
-template <int AGG>
-__global__ void __launch_bounds__(kN1ApplyThreads) k_rgn_apply_n1(IngestArgs a) {
-    if constexpr (!cmp_agg<AGG>()) {
-        return;
-    } else {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    constexpr bool M = uses_mask<AGG>();
-    constexpr bool N4 = AGG == GW_COUNT;
-    constexpr int W = AGG == GW_AVG_I64 ? 2 : 1;
-    __shared__ uint32_t s_kdirty[kNarMaxSlots / 16 / 32];
-    const int F = 1 << a.sr_bits;
-    const int S = (int)pt_S(a.t), FS = F * S;
-    const int l2S = a.t.log2S;
-    const int nb = a.n1_nb;
-    // consecutive super-regions on one XCD at a time (workgroups are dealt to the XCDs in turn)
-    const int64_t nsr = gridDim.x;
-    const int64_t sr = (nsr & 7) == 0 ? (int64_t)(blockIdx.x & 7) * (nsr >> 3) + (blockIdx.x >> 3) : blockIdx.x;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
-    uint32_t* lkeys = reinterpret_cast<uint32_t*>(smem);                     // [FS]
-    uint8_t* lmask = reinterpret_cast<uint8_t*>(lkeys + FS);                  // [FS] (M)
-    long long* lcell = reinterpret_cast<long long*>(lmask + (M ? FS : 0));   // [FS][W]
-    uint32_t* qk = reinterpret_cast<uint32_t*>(lcell + (int64_t)FS * W) + wave * kApplyQ;
-    int32_t* qv = reinterpret_cast<int32_t*>(lcell + (int64_t)FS * W) + nw * kApplyQ + wave * kApplyQ;
-    int qn = 0;
-    const unsigned long long pmask = (*(volatile unsigned long long*)a.batch_occ) & a.apply_mask & 0xffull;
-    if (!pmask) return;  // uniform
-    const int dom_sh = 64 - a.t.log2nreg;
-    const int64_t ntiles = a.ntiles;
-    const uint64_t* rk = reinterpret_cast<const uint64_t*>(a.p1_key);
-    const uint32_t* rk32 = reinterpret_cast<const uint32_t*>(a.p1_key);
-    for (int i = threadIdx.x; i < kNarMaxSlots / 16 / 32; i += blockDim.x) s_kdirty[i] = 0;
-    {  // keys (int64 in HBM -> 32-bit in LDS) and presence masks of the F regions
-        const int nk2 = FS / 2, nm16 = M ? FS / 16 : 0, tot = nk2 + nm16;
-        for (int w0 = threadIdx.x; w0 < tot; w0 += kNarLoadU * blockDim.x) {
-            long2 v[kNarLoadU];
-#pragma unroll
-            for (int u = 0; u < kNarLoadU; ++u) {
-                const int w = w0 + u * blockDim.x;
-                v[u] = long2{0, 0};
-                if (w < nk2) {
-                    const int d = w / (S / 2), j = w - d * (S / 2);
-                    v[u] = reinterpret_cast<const long2*>(pt_region(a.t, sr * F + d))[j];
-                } else if (w < tot) {
-                    const int wm_ = w - nk2, d = wm_ / (S / 16), j = wm_ - d * (S / 16);
-                    v[u] = reinterpret_cast<const long2*>(pt_mask_base(a.t, sr * F + d))[j];
-                }
-            }
-#pragma unroll
-            for (int u = 0; u < kNarLoadU; ++u) {
-                const int w = w0 + u * blockDim.x;
-                if (w < nk2) reinterpret_cast<uint2*>(lkeys)[w] = uint2{k32_of(v[u].x), k32_of(v[u].y)};
-                else if (w < tot) reinterpret_cast<long2*>(lmask)[w - nk2] = v[u];
-            }
-        }
-    }
-    unsigned long long ins = 0, flags = 0, spills = 0;
-    auto probe_insert = [&](uint32_t k, uint64_t h) -> int {
-        const int d = F > 1 ? (int)((h >> dom_sh) & (uint64_t)(F - 1)) : 0;
-        uint32_t* kd = lkeys + d * S;
-        int g0 = (int)(h & (uint64_t)(S - 1) & ~(uint64_t)(kProbeGroup - 1));
-        for (int p = 0; p < S;) {
-            const uint4 kk = *reinterpret_cast<const uint4*>(kd + g0);
-            const uint32_t hit = (uint32_t)(kk.x == k) | (uint32_t)(kk.y == k) << 1 | (uint32_t)(kk.z == k) << 2 |
-                                 (uint32_t)(kk.w == k) << 3;
-            const uint32_t emp = (uint32_t)(kk.x == kK32Empty) | (uint32_t)(kk.y == kK32Empty) << 1 |
-                                 (uint32_t)(kk.z == kK32Empty) << 2 | (uint32_t)(kk.w == kK32Empty) << 3;
-            const uint32_t m = hit | emp;
-            if (m) {
-                const int i = __ffs((int)m) - 1;
-                const int j = g0 + i;
-                if ((hit >> i) & 1) return d * S + j;
-                const uint32_t prev = atomicCAS(kd + j, kK32Empty, k);
-                if (prev == kK32Empty) {
-                    ins++;
-                    const int line = (d * S + j) >> 4;
-                    atomicOr(&s_kdirty[line >> 5], 1u << (line & 31));
-                    return d * S + j;
-                }
-                if (prev == k) return d * S + j;
-                continue;
-            }
-            g0 = (g0 + kProbeGroup) & (S - 1);
-            p += kProbeGroup;
-        }
-        return -1;
-    };
-    auto cell_add = [&](int slot, int64_t v, uint32_t bit) {
-        long long* c = lcell + (int64_t)slot * W;
-        lds_cell_add<AGG>(c, c + (W - 1), v, 1);
-        if constexpr (M) atomicOr(reinterpret_cast<uint32_t*>(lmask) + (slot >> 2), bit << ((slot & 3) * 8));
-    };
-    auto q_push = [&](bool pu, uint32_t kk, int32_t vv, uint32_t pbit) {
-        const uint64_t bal = __ballot(pu);
-        if (pu) {
-            const int at = qn + __popcll(bal & ((1ull << lane) - 1ull));
-            qk[at] = kk;
-            qv[at] = vv;
-        }
-        qn += __popcll(bal);
-        if (qn >= 64) {
-            const int at = qn - 64 + lane;
-            const uint32_t k2 = qk[at];
-            const int s2 = probe_insert(k2, slot_hash((int64_t)k2));
-            if (s2 >= 0) cell_add(s2, qv[at], pbit);
-            else { flags |= GW_DF_TABLE_FULL; spills++; }
-            qn -= 64;
-        }
-    };
-    const long long id0 = identity0(AGG);
-    const long2 ident = W == 2 ? long2{id0, 0} : long2{id0, id0};
-    // run bounds of the 64 tiles starting at c (this lane: tile c + lane) holding position p
-    struct Runs {
-        int64_t src;   // first record of the lane's run in the buffer
-        uint32_t cnt;  // its length
-    };
-    auto load_runs = [&](int64_t c, int p) -> Runs {
-        const int64_t t = c + lane;
-        Runs r{0, 0u};
-        if (t < ntiles && ((a.n1_occ[t] >> p) & 1)) {
-            const uint16_t* row = a.n1_row + t * (int64_t)(nb + 1) + sr;
-            const uint32_t s0 = row[0], s1 = row[1];
-            r.src = t * (int64_t)kN1Tile + s0;
-            r.cnt = s1 - s0;
-        }
-        return r;
-    };
-    for (unsigned long long pm = pmask; pm; pm &= pm - 1) {
-        const int p = __ffsll((long long)pm) - 1;
-        const uint32_t pbit = 1u << p;
-        __syncthreads();  // the previous position's write-back has read the cells
-        {  // this position's pane (an untouched one holds identities)
-            const bool fresh = (a.ring_fresh >> p) & 1;
-            const int per = S * W / 2, tot = FS * W / 2;
-            long2* l2 = reinterpret_cast<long2*>(lcell);
-            for (int w0 = threadIdx.x; w0 < tot; w0 += kNarLoadU * blockDim.x) {
-                long2 v[kNarLoadU];
-#pragma unroll
-                for (int u = 0; u < kNarLoadU; ++u) {
-                    const int w = w0 + u * blockDim.x;
-                    v[u] = ident;
-                    if (w < tot && !fresh) {
-                        const int d = w / per;
-                        v[u] = reinterpret_cast<const long2*>(pt_cell(a.t, (sr * F + d) << l2S, p))[w - d * per];
-                    }
-                }
-#pragma unroll
-                for (int u = 0; u < kNarLoadU; ++u) {
-                    const int w = w0 + u * blockDim.x;
-                    if (w < tot) l2[w] = v[u];
-                }
-            }
-        }
-        __syncthreads();
-        int64_t c = (int64_t)wave * 64;
-        Runs cur = load_runs(c, p);
-        while (c < ntiles) {  // uniform per wave
-            const int64_t cn = c + (int64_t)nw * 64;
-            const Runs nxt = load_runs(cn, p);  // in flight while this chunk applies
-            uint32_t incl = cur.cnt;
-            for (int o = 1; o < 64; o <<= 1) {
-                const uint32_t up = __shfl_up(incl, o);
-                if (lane >= o) incl += up;
-            }
-            const uint32_t total = __shfl(incl, 63);
-            const uint32_t excl = incl - cur.cnt;
-            for (uint32_t e0 = 0; e0 < total; e0 += 64 * kN1U) {
-                uint64_t r[kN1U];
-                bool ok[kN1U];
-#pragma unroll
-                for (int q = 0; q < kN1U; ++q) {
-                    const uint32_t e = e0 + q * 64 + lane;
-                    ok[q] = e < total;
-                    int j = 0;  // the last lane whose run starts at or before e
-#pragma unroll
-                    for (int st = 32; st; st >>= 1) {
-                        const uint32_t v = __shfl(excl, j + st);
-                        if (v <= e) j += st;
-                    }
-                    const int64_t src = __shfl(cur.src, j) + (int64_t)(e - __shfl(excl, j));
-                    r[q] = ok[q] ? (N4 ? (uint64_t)rk32[src] : rk[src]) : 0ull;
-                }
-                uint32_t kq[kN1U];
-                int32_t vq[kN1U];
-                int hq[kN1U];
-                uint4 ka[kN1U];
-#pragma unroll
-                for (int q = 0; q < kN1U; ++q) {
-                    const uint32_t low = N4 ? (uint32_t)r[q] : (uint32_t)(r[q] >> 32);
-                    ok[q] = ok[q] && nar_pos(low) == (uint32_t)p;  // a tile's other positions: their own pass
-                    kq[q] = N4 ? (uint32_t)(r[q] >> 4) : (uint32_t)r[q];
-                    vq[q] = N4 ? 1 : (int32_t)low >> 4;
-                    const uint64_t h = slot_hash((int64_t)kq[q]);
-                    const int d = F > 1 ? (int)((h >> dom_sh) & (uint64_t)(F - 1)) : 0;
-                    hq[q] = d * S + (int)(h & (uint64_t)(S - 1) & ~(uint64_t)(kProbeGroup - 1));
-                }
-#pragma unroll
-                for (int q = 0; q < kN1U; ++q) ka[q] = *reinterpret_cast<const uint4*>(lkeys + hq[q]);
-#pragma unroll
-                for (int q = 0; q < kN1U; ++q) {
-                    const uint32_t k = kq[q];
-                    const int i = ka[q].x == k ? 0 : ka[q].y == k ? 1 : ka[q].z == k ? 2 : ka[q].w == k ? 3 : -1;
-                    const bool fast = ok[q] && i >= 0;
-                    if (fast) cell_add(hq[q] + i, vq[q], pbit);
-                    q_push(ok[q] && !fast, k, vq[q], pbit);
-                }
-            }
-            cur = nxt;
-            c = cn;
-        }
-        if (lane < qn) {  // the rest of the queue
-            const uint32_t k2 = qk[lane];
-            const int s2 = probe_insert(k2, slot_hash((int64_t)k2));
-            if (s2 >= 0) cell_add(s2, qv[lane], pbit);
-            else { flags |= GW_DF_TABLE_FULL; spills++; }
-        }
-        qn = 0;
-        __syncthreads();
-        {  // write back this position's pane
-            const int per = S * W / 2, tot = FS * W / 2;
-            const long2* l2 = reinterpret_cast<const long2*>(lcell);
-            for (int w = threadIdx.x; w < tot; w += blockDim.x) {
-                const int d = w / per;
-                reinterpret_cast<long2*>(pt_cell(a.t, (sr * F + d) << l2S, p))[w - d * per] = l2[w];
-            }
-        }
-    }
-    // Spill pass (only after a region filled up): records whose key is absent from the final
-    // key table were not applied; mark them for k_rgn_collect_n1.
-    if (__syncthreads_or(spills != 0)) {
-        unsigned long long marked = 0;
-        for (int64_t t = threadIdx.x >> 6; t < ntiles; t += nw) {
-            if (!(a.n1_occ[t] & pmask)) continue;
-            const uint16_t* row = a.n1_row + t * (int64_t)(nb + 1) + sr;
-            const int64_t src = t * (int64_t)kN1Tile + row[0];
-            const uint32_t cnt = (uint32_t)row[1] - row[0];
-            for (uint32_t k = lane; k < cnt; k += 64) {
-                const uint64_t r = N4 ? (uint64_t)rk32[src + k] : rk[src + k];
-                const uint32_t low = N4 ? (uint32_t)r : (uint32_t)(r >> 32);
-                if (!((pmask >> nar_pos(low)) & 1)) continue;
-                const uint32_t kk = N4 ? (uint32_t)(r >> 4) : (uint32_t)r;
-                const uint64_t h = slot_hash((int64_t)kk);
-                const int dd = F > 1 ? (int)((h >> dom_sh) & (uint64_t)(F - 1)) : 0;
-                int j = (int)(h & (uint64_t)(S - 1) & ~(uint64_t)(kProbeGroup - 1));
-                bool present = false;
-                for (int q = 0; q < S; ++q) {
-                    const uint32_t x = lkeys[dd * S + j];
-                    if (x == kk) { present = true; break; }
-                    if (x == kK32Empty) break;
-                    j = (j + 1) & (S - 1);
-                }
-                if (!present) {
-                    if constexpr (N4) const_cast<uint32_t*>(rk32)[src + k] = (uint32_t)r | kNarSpill;
-                    else const_cast<uint64_t*>(rk)[src + k] = r | ((uint64_t)kNarSpill << 32);
-                    marked++;
-                }
-            }
-        }
-        spills = marked;
-    }
-    __syncthreads();
-    if constexpr (M) {
-        const int per = S / 16;
-        for (int w = threadIdx.x; w < FS / 16; w += blockDim.x) {
-            const int d = w / per;
-            reinterpret_cast<long2*>(pt_mask_base(a.t, sr * F + d))[w - d * per] = reinterpret_cast<const long2*>(lmask)[w];
-        }
-    }
-    for (int j = threadIdx.x; j < FS; j += blockDim.x) {
-        const int line = j >> 4;
-        if ((s_kdirty[line >> 5] >> (line & 31)) & 1u) {
-            const uint32_t k = lkeys[j];
-            if (k != kK32Foreign) {
-                const int d = j / S;
-                pt_region(a.t, sr * F + d)[j - d * S] = k == kK32Empty ? kEmptyKey : (int64_t)k;
-            }
-        }
-    }
-    spills = wave_sum(spills);
-    if (__lane_id() == 0 && spills) atomicAdd(&a.st->spills, spills);
-    block_commit(a.st, 0, ins, flags, 0);
-    }
-}
-
-// Spilled records of a nar1 flush: one pass over the buffered tiles (a tile's count is the
-// last start of its descriptor row).
-template <int AGG>
-__global__ void __launch_bounds__(256) k_rgn_collect_n1(IngestArgs a) {
-    constexpr bool N4 = AGG == GW_COUNT;
-    const int nb = a.n1_nb;
-    int64_t* rk = a.p1_key;
-    uint32_t* rk32 = reinterpret_cast<uint32_t*>(rk);
-    const int64_t n = a.ntiles * (int64_t)kN1Tile;
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t base = blockIdx.x * (int64_t)blockDim.x; base < n; base += stride) {
-        const int64_t i = base + threadIdx.x;
-        bool spill = false;
-        int64_t key = 0, pane = 0, c0 = 0;
-        if (i < n) {
-            const int64_t t = i / kN1Tile;
-            if ((i - t * kN1Tile) < (int64_t)a.n1_row[t * (int64_t)(nb + 1) + nb]) {
-                const uint64_t w = N4 ? (uint64_t)rk32[i] : (uint64_t)rk[i];
-                const uint32_t lo = N4 ? (uint32_t)w : (uint32_t)(w >> 32);
-                if (nar_spilled(lo)) {
-                    spill = true;
-                    if (N4) rk32[i] = (uint32_t)w & ~kNarSpill;
-                    else rk[i] = (int64_t)(w & ~((uint64_t)kNarSpill << 32));
-                    key = N4 ? nar_key32((uint32_t)w) : nar_key(w);
-                    c0 = N4 ? 1 : nar_val(w);
-                    const int64_t rel = ((int64_t)nar_pos(lo) - a.b_pos + a.t.ring) % a.t.ring;
-                    pane = a.p_late + (int64_t)a.delta + rel;
-                }
-            }
-        }
-        defer_write(a, spill, key, pane, c0, 1);
-    }
-}
-
 // The same for compact records: the spill mark is bit 63 of the word, and the key comes
 // back from the hash, whose top bits are the record's bucket -- so one workgroup per
 // region walks the region's runs as the apply does.
@@ -3260,17 +2767,6 @@ int region_group(int d1_bits) {
 
 // Region path, P1 over one watermark batch: one block per 4096-record tile.
 hipError_t launch_region_p1(const IngestArgs& a, hipStream_t s) {
-    if (a.nar1) {  // narrow single-pass: 8192-record tiles bucketed by super-region
-        const int64_t t1 = (a.n + kN1Tile - 1) / kN1Tile;
-        if (t1 == 0) return hipSuccess;
-        const size_t lds = (size_t)kN1Tile * (a.t.agg == GW_COUNT ? 4 : 8) + (size_t)(a.n1_nb + 1) * 4;
-#define L(A)                                                                                          \
-    lds_opt_in((const void*)k_rgn_p1n<A>, lds);                                                      \
-    hipLaunchKernelGGL(k_rgn_p1n<A>, dim3((unsigned)t1), dim3(kN1Threads), lds, s, a)
-        GW_AGG_SWITCH(a.t.agg, L);
-#undef L
-        return hipGetLastError();
-    }
     const int64_t tiles = (a.n + kPartTile - 1) / kPartTile;
     if (tiles == 0) return hipSuccess;
     const size_t part_lds = part_lds_bytes(a);
@@ -3329,19 +2825,6 @@ hipError_t launch_region_flush(const IngestArgs& a, hipStream_t s) {
     } else {                        \
         L2(A, kFmtWide);            \
     }
-    if (a.fmt == kFmtNar && a.nar1) {
-        const int F = 1 << a.sr_bits;
-        const int64_t FS = (int64_t)F * S;
-        const bool M = a.t.has_mask != 0;
-        const size_t lds = (size_t)FS * 4 + (M ? (size_t)FS : 0) + (size_t)FS * a.t.words * 8 +
-                           (size_t)(kN1ApplyThreads / 64) * kApplyQ * 8;
-#define LN(A)                                                                                                   \
-    lds_opt_in((const void*)k_rgn_apply_n1<A>, lds);                                                          \
-    hipLaunchKernelGGL(k_rgn_apply_n1<A>, dim3((unsigned)(a.t.nreg >> a.sr_bits)), dim3(kN1ApplyThreads), lds, s, a)
-        GW_AGG_SWITCH(a.t.agg, LN);
-#undef LN
-        return hipGetLastError();
-    }
     if (a.fmt == kFmtNar && a.nar2) {
         const int F = 1 << a.sr_bits;
         const int64_t FS = (int64_t)F * S;
@@ -3372,9 +2855,7 @@ hipError_t launch_region_flush(const IngestArgs& a, hipStream_t s) {
 hipError_t launch_region_collect(const IngestArgs& a, hipStream_t s) {
     const int64_t n = a.ntiles * kPartTile;  // upper bound of the buffer's records
 #define L(A)                                                                                         \
-    if (a.fmt == kFmtNar && a.nar1)                                                                  \
-        hipLaunchKernelGGL(k_rgn_collect_n1<A>, dim3(grid_for(a.ntiles * (int64_t)kN1Tile)), dim3(256), 0, s, a); \
-    else if (a.fmt == kFmtNar && a.nar2)                                                             \
+    if (a.fmt == kFmtNar && a.nar2)                                                                  \
         hipLaunchKernelGGL(k_rgn_collect_nar2<A>, dim3(grid_for(n), 2), dim3(256), 0, s, a);        \
     else if (a.fmt == kFmtNar)                                                                       \
         hipLaunchKernelGGL(k_rgn_collect_nar<A>, dim3((unsigned)a.t.nreg), dim3(256), 0, s, a);     \

@@ -246,8 +246,6 @@ struct gw_handle {
     int64_t* e_col[6] = {};         // e_key e_a0 e_a1 (P2 output) p1_key p1_a0 p1_a1 (P1 output)
     uint8_t* e_pos[2] = {};         // e_pos p1_pos
     uint32_t* p1_row = nullptr;     // [tile][kPartBuckets]
-    uint16_t* n1_row = nullptr;     // nar1: [tile / 2][kN1MaxBuckets + 1] run starts per super-region
-    uint8_t* n1_occ = nullptr;      // nar1: [tile / 2] ring positions of the tile
     uint32_t* p2_desc = nullptr;    // [bucket][tile]
     int64_t* p2_off = nullptr;      // [blocks + 1], blocks = buckets x groups <= 2 tiles + kPartBuckets
     int64_t* p2_roff = nullptr;
@@ -538,7 +536,7 @@ struct gw_handle {
         for (auto& p : e_col) { if (p) hipFree(p); p = nullptr; }
         for (auto& p : e_pos) { if (p) hipFree(p); p = nullptr; }
         for (void** p : {(void**)&p1_row, (void**)&p2_desc, (void**)&p2_off, (void**)&p2_roff, (void**)&r_row,
-                         (void**)&r_base, (void**)&n1_row, (void**)&n1_occ}) {
+                         (void**)&r_base}) {
             if (*p) hipFree(*p);
             *p = nullptr;
         }
@@ -564,8 +562,6 @@ struct gw_handle {
         }
         for (auto& p : e_pos) HIPCHECK(hipMalloc((void**)&p, recs));
         HIPCHECK(hipMalloc((void**)&p1_row, (size_t)cap * kPartBuckets * 4));
-        HIPCHECK(hipMalloc((void**)&n1_row, (size_t)(cap / 2 + 1) * (kN1MaxBuckets + 1) * 2));
-        HIPCHECK(hipMalloc((void**)&n1_occ, (size_t)(cap / 2 + 1)));
         HIPCHECK(hipMalloc((void**)&p2_desc, (size_t)cap * kPartBuckets * 4));
         HIPCHECK(hipMalloc((void**)&p2_off, (size_t)max_blocks(cap) * 8));
         HIPCHECK(hipMalloc((void**)&p2_roff, (size_t)max_blocks(cap) * 8));
@@ -1205,30 +1201,13 @@ struct gw_handle {
         a.apply_mask = ~0ull;
         a.batch_occ = d_tmp + 1;
         a.fmt = buf_fmt;
-        a.n1_row = n1_row;
-        a.n1_occ = n1_occ;
         nar_mode(a);
     }
 
-    // Narrow records of two-pass tables: the single-pass flush (nar1: P1 buckets by super-region
-    // of F = 4 regions, one apply kernel, GW_NAR1=0 turns it off) while the super-regions fit a
-    // P1 tile's bucket table, else P2 + k_rgn_apply_nar (nar2).  Fixed per flush window: the
-    // format and the table geometry do not change while segments wait.
+    // Narrow records of two-pass tables: P2 groups each round by (super-region, ring position)
+    // and k_rgn_apply_nar applies a super-region one position after another (nar2).  Fixed per
+    // flush window: the format and the table geometry do not change while segments wait.
     void nar_mode(IngestArgs& a) const {
-        static const bool nar1_off = [] { const char* e = getenv("GW_NAR1"); return e && atoi(e) == 0; }();
-        a.nar1 = 0;
-        a.n1_nb = 0;
-        if (buf_fmt == 2 && a.d2_bits > 0 && !nar1_off && tv.ring <= 8 && tv.log2nreg >= 2) {
-            const int sr = 2;  // F = 4: 8192 slots per workgroup (4096 for AVG's two-word cells)
-            const int64_t nb = tv.nreg >> sr;
-            if (nb >= 8 && nb <= kN1MaxBuckets) {
-                a.nar1 = 1;
-                a.nar2 = 0;
-                a.sr_bits = sr;
-                a.n1_nb = (int32_t)nb;
-                return;
-            }
-        }
         // narrow records of two-pass tables: k_rgn_apply_nar over super-regions of F regions
         // (GW_NAR_F = 1, 2 or 4, default 2; GW_NAR2=0 keeps k_rgn_apply), while P2's (super-region,
         // ring position) buckets fit a descriptor row
@@ -1289,7 +1268,7 @@ struct gw_handle {
         if ((rc = base_args(a, 0, nullptr, nullptr, nullptr))) return rc;
         region_args(a);
         if (carry_on && !a.nar2) return fail(GW_E_STATE, "internal: carried records without a nar2 flush");
-        a.ntiles = a.nar1 ? buf_tiles / 2 : buf_tiles;
+        a.ntiles = buf_tiles;
         a.p2_group = region_group(a.d1_bits);
         a.ngroups = (buf_tiles + a.p2_group - 1) / a.p2_group;
         a.ring_fresh = buf_fresh;
@@ -1402,9 +1381,7 @@ struct gw_handle {
             // Two-pass tables buffer P1 segments across watermarks (P2 + apply once per
             // fire); single-pass tables apply every batch.
             const bool buffered = a.d2_bits > 0 && !(cfg.flags & GW_FLAG_NO_BUFFER);
-            // nar1 tiles are 8192 records, two buffer tiles each; the window's mode is known once
-            // its format is, so the buffer is reserved for either
-            const int64_t tiles = 2 * ((nrec + kN1Tile - 1) / kN1Tile);
+            const int64_t tiles = (nrec + kPartTile - 1) / kPartTile;
             if (nseg && buf_tiles + tiles > buf_cap) {
                 if ((rc = flush_buffer())) return rc;
                 if ((rc = base_args(a, nrec, key, ts, val))) return rc;
@@ -1430,7 +1407,6 @@ struct gw_handle {
             }
             a.fmt = buf_fmt;
             nar_mode(a);
-            if (a.nar1) a.tile0 = buf_tiles / 2;
             stats.region_format = buf_fmt;
             if (buffered) arm_status(a);
             hp.lap(13);
@@ -1444,7 +1420,7 @@ struct gw_handle {
                 HIPCHECK(launch_region_p1(a, stream));
             }
             nseg++;
-            buf_tiles += a.nar1 ? tiles : (nrec + kPartTile - 1) / kPartTile;
+            buf_tiles += tiles;
             buf_recs += nrec;
             if (!buffered && (rc = flush_buffer())) return rc;
         } else if (timing) {
