@@ -12,9 +12,9 @@
 // that could hold the record are cleaned).
 #include <algorithm>
 
-#include <rocprim/device/device_radix_sort.hpp>
 
 #include "gw_first.h"
+#include "gw_sort.h"
 
 namespace gw {
 
@@ -28,9 +28,10 @@ __global__ void k_fe_iota32(uint32_t* d, int64_t n) {
         d[i] = (uint32_t)i;
 }
 
-__global__ void k_fe_gather_key(const int64_t* src, const uint32_t* idx, int64_t* dst, int64_t n) {
+// int64 -> its unsigned radix order (sign bit flipped), gathered through idx (or not: idx null)
+__global__ void k_fe_gather_key(const int64_t* src, const uint32_t* idx, uint64_t* dst, int64_t n) {
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-        dst[i] = src[idx[i]];
+        dst[i] = (uint64_t)src[idx ? idx[i] : i] ^ 0x8000000000000000ull;
 }
 
 // The batch's largest timestamp: wave then block reduction, one device atomic per block
@@ -101,38 +102,35 @@ hipError_t fe_log_gather(const int64_t* log, int64_t cap, const int64_t* seq, in
 }
 
 size_t fe_join_scratch_bytes(int64_t n) {
-    size_t bytes = 0;
-    rocprim::double_buffer<int64_t> kb(nullptr, nullptr);
-    rocprim::double_buffer<uint32_t> vb(nullptr, nullptr);
-    rocprim::radix_sort_pairs(nullptr, bytes, kb, vb, (size_t)std::max<int64_t>(n, 1));
+    const size_t bytes = (size_t)sort_scratch_bytes(std::max<int64_t>(n, 1));
     const size_t a = (size_t)std::max<int64_t>(n, 1);
     // sort temp + 2 key buffers (8 B) + 2 index buffers (4 B) per side, two sides
     return ((bytes + 255) / 256 * 256) + 2 * (a * 16 + a * 8) + 1024;
 }
 
-// (key, start) order of one side: indices sorted by start, then stably by key.
+// (key, start) order of one side: indices sorted by start, then stably by key (gw_sort.hip,
+// int64 values in radix order: the sign bit flipped).
 static hipError_t sort_side(int64_t n, const int64_t* key, const int64_t* start, uint32_t*& order, uint8_t*& p,
                             void* tmp, size_t tmp_bytes, hipStream_t s) {
+    (void)tmp_bytes;
     const size_t a = (size_t)n;
-    int64_t* k0 = (int64_t*)p; p += a * 8;
-    int64_t* k1 = (int64_t*)p; p += a * 8;
+    uint64_t* k0 = (uint64_t*)p; p += a * 8;
+    uint64_t* k1 = (uint64_t*)p; p += a * 8;
     uint32_t* v0 = (uint32_t*)p; p += a * 4;
     uint32_t* v1 = (uint32_t*)p; p += a * 4;
     hipLaunchKernelGGL(k_fe_iota32, dim3(grid_n(n)), dim3(256), 0, s, v0, n);
-    hipError_t e = hipMemcpyAsync(k0, start, a * 8, hipMemcpyDeviceToDevice, s);
+    hipLaunchKernelGGL(k_fe_gather_key, dim3(grid_n(n)), dim3(256), 0, s, start, (const uint32_t*)nullptr, k0, n);
+    int alt = 0;
+    hipError_t e = sort_pairs_u64(k0, v0, k1, v1, n, 0, 64, tmp, s, &alt);
     if (e != hipSuccess) return e;
-    rocprim::double_buffer<int64_t> kb(k0, k1);
-    rocprim::double_buffer<uint32_t> vb(v0, v1);
-    size_t bytes = tmp_bytes;
-    if ((e = rocprim::radix_sort_pairs(tmp, bytes, kb, vb, a, 0, 64, s)) != hipSuccess) return e;
+    uint32_t* va = alt ? v1 : v0;
+    uint32_t* vb = alt ? v0 : v1;
     // second pass: the keys of the start-sorted order, sorted stably
-    int64_t* kk = kb.alternate();
-    hipLaunchKernelGGL(k_fe_gather_key, dim3(grid_n(n)), dim3(256), 0, s, key, vb.current(), kk, n);
-    rocprim::double_buffer<int64_t> kb2(kk, kb.current());
-    rocprim::double_buffer<uint32_t> vb2(vb.current(), vb.alternate());
-    bytes = tmp_bytes;
-    if ((e = rocprim::radix_sort_pairs(tmp, bytes, kb2, vb2, a, 0, 64, s)) != hipSuccess) return e;
-    order = vb2.current();
+    uint64_t* kk = alt ? k0 : k1;
+    uint64_t* ko = alt ? k1 : k0;
+    hipLaunchKernelGGL(k_fe_gather_key, dim3(grid_n(n)), dim3(256), 0, s, key, va, kk, n);
+    if ((e = sort_pairs_u64(kk, va, ko, vb, n, 0, 64, tmp, s, &alt)) != hipSuccess) return e;
+    order = alt ? vb : va;
     return hipGetLastError();
 }
 
@@ -142,12 +140,7 @@ hipError_t fe_join(int64_t n, const int64_t* a_key, const int64_t* a_start, cons
                    int64_t* o_end, int64_t* o_res, int64_t* o_pay, void* scratch, size_t scratch_bytes,
                    int32_t* d_bad, hipStream_t s) {
     if (n <= 0) return hipSuccess;
-    size_t tmp_bytes = 0;
-    {
-        rocprim::double_buffer<int64_t> kb(nullptr, nullptr);
-        rocprim::double_buffer<uint32_t> vb(nullptr, nullptr);
-        rocprim::radix_sort_pairs(nullptr, tmp_bytes, kb, vb, (size_t)n);
-    }
+    const size_t tmp_bytes = (size_t)sort_scratch_bytes(n);
     if (scratch_bytes < fe_join_scratch_bytes(n)) return hipErrorInvalidValue;
     uint8_t* p = (uint8_t*)scratch;
     void* tmp = p;

@@ -12,7 +12,7 @@
 //   EventTimeTrigger + onEventTime: a session fires once when end-1 <= watermark.
 //
 // MI355X design: per watermark batch every record finds its key's slot,
-// a stable radix sort by slot (rocPRIM) groups each key's records in ARRIVAL order, and one
+// a stable radix sort by slot (gw_sort.hip) groups each key's records in ARRIVAL order, and one
 // thread per key replays them through MergingWindowSet.addWindow semantics -- the
 // reference's own record-at-a-time order, so late records, immediate firings and merges
 // behave exactly as in the reference, with no separate replay path.  The thread keeps the
@@ -29,28 +29,6 @@
 #include <cstring>
 #include <cstdio>
 #include <vector>
-
-#include <rocprim/device/device_radix_sort.hpp>
-
-// The slot sort's rocPRIM configuration: 9 bits per onesweep pass, so 12.5M keys' 26 slot
-// bits take 3 passes instead of the library default's 4 at 8 bits (sessions config 7.4 ->
-// 8.5 G events/s; 10 and 11 bits measured slower, profiles/r3/experiments.txt).
-// GW_SESS_RADIX_BITS=0 builds the library default.
-#ifndef GW_SESS_RADIX_BITS
-#define GW_SESS_RADIX_BITS 9
-#endif
-#ifndef GW_SESS_SORT_ITEMS
-#define GW_SESS_SORT_ITEMS 8
-#endif
-#if GW_SESS_RADIX_BITS
-using SlotSortConfig = rocprim::radix_sort_config<
-    rocprim::default_config, rocprim::default_config,
-    rocprim::radix_sort_onesweep_config<rocprim::kernel_config<1024, 8>, rocprim::kernel_config<1024, GW_SESS_SORT_ITEMS>,
-                                        GW_SESS_RADIX_BITS, rocprim::block_radix_rank_algorithm::match>>;
-#else
-using SlotSortConfig = rocprim::default_config;
-#endif
-
 
 namespace gw {
 
@@ -2159,9 +2137,7 @@ static int ensure_bufs(SessionState* s, int64_t n, std::string& err) {
     if (!s->count_mode) SCHECK(hipMalloc((void**)&s->mig, (size_t)c * (2 + kWideWords * kLaneSess) * 8));
     if (!s->count_mode) SCHECK(hipMalloc((void**)&s->rec, (size_t)c * sizeof(KeyRec)));
     if (!s->count_mode) SCHECK(hipMalloc((void**)&s->ks_pu, (size_t)c * 24));
-    rocprim::double_buffer<uint32_t> kb(s->slot[0], s->slot[1]), vb(s->perm[0], s->perm[1]);
-    size_t bytes = 0;
-    SCHECK(rocprim::radix_sort_pairs<SlotSortConfig>(nullptr, bytes, kb, vb, (size_t)c, 0, 32, s->stream));
+    const size_t bytes = (size_t)sort_scratch_bytes(c);
     SCHECK(hipMalloc(&s->sort_tmp, bytes));
     s->sort_tmp_bytes = bytes;
     s->buf_cap = c;
@@ -2182,11 +2158,11 @@ static int sort_by_slot(SessionState* s, int64_t n, int64_t cap, const uint32_t*
     int sort_bits = 32;
     if (const char* e = getenv("GW_SESSION_SORT_BITS")) sort_bits = std::max(1, atoi(e));
     s->gshift = s->count_mode ? 0 : std::min(4, std::max(0, bits - sort_bits));
-    rocprim::double_buffer<uint32_t> kb(s->slot[0], s->slot[1]), vb(s->perm[0], s->perm[1]);
-    size_t bytes = s->sort_tmp_bytes;
-    SCHECK(rocprim::radix_sort_pairs<SlotSortConfig>(s->sort_tmp, bytes, kb, vb, (size_t)n, s->gshift, bits, s->stream));
-    *sk = kb.current();
-    *sp = vb.current();
+    int alt = 0;
+    SCHECK(sort_pairs_u32(s->slot[0], s->perm[0], s->slot[1], s->perm[1], n, s->gshift, bits, s->sort_tmp, s->stream,
+                          &alt));
+    *sk = s->slot[alt];
+    *sp = s->perm[alt];
     return GW_OK;
 }
 
@@ -2717,14 +2693,13 @@ static int ingest_keyed(SessionState* s, int64_t n, const int64_t* key, const in
     hipLaunchKernelGGL(k_sess_kprep, dim3(grid_of(n)), dim3(256), 0, s->stream, key, ts, val, n, lcap, sbits,
                        s->slot[0], s->perm[0], rec, s->d_st);
     SCHECK(hipGetLastError());
-    rocprim::double_buffer<uint32_t> kb(s->slot[0], s->slot[1]), vb(s->perm[0], s->perm[1]);
-    size_t bytes = s->sort_tmp_bytes;
-    SCHECK(rocprim::radix_sort_pairs<SlotSortConfig>(s->sort_tmp, bytes, kb, vb, (size_t)n, 0, sbits, s->stream));
+    int alt = 0;
+    SCHECK(sort_pairs_u32(s->slot[0], s->perm[0], s->slot[1], s->perm[1], n, 0, sbits, s->sort_tmp, s->stream, &alt));
     SegArgs a{};
     if ((rc = seg_common(s, a, n, wm, err))) return rc;
     a.diag = getenv("GW_KSEG_FAST") && atoi(getenv("GW_KSEG_FAST")) == 0;
-    a.slot = kb.current();
-    a.perm = vb.current();
+    a.slot = s->slot[alt];
+    a.perm = s->perm[alt];
     a.runs = s->r0;  // per run start: the slot k_sess_kprobe found
     hipLaunchKernelGGL(k_sess_kprobe, dim3(grid_of(n)), dim3(256), 0, s->stream, s->tv, a.slot, a.perm, rec, n, s->r0,
                        s->d_st);
