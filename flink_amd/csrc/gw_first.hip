@@ -23,11 +23,6 @@ __global__ void k_fe_iota64(int64_t* d, int64_t n, int64_t base) {
         d[i] = base + i;
 }
 
-__global__ void k_fe_iota32(uint32_t* d, int64_t n) {
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-        d[i] = (uint32_t)i;
-}
-
 // int64 -> its unsigned radix order (sign bit flipped), gathered through idx (or not: idx null)
 __global__ void k_fe_gather_key(const int64_t* src, const uint32_t* idx, uint64_t* dst, int64_t n) {
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
@@ -118,10 +113,9 @@ static hipError_t sort_side(int64_t n, const int64_t* key, const int64_t* start,
     uint64_t* k1 = (uint64_t*)p; p += a * 8;
     uint32_t* v0 = (uint32_t*)p; p += a * 4;
     uint32_t* v1 = (uint32_t*)p; p += a * 4;
-    hipLaunchKernelGGL(k_fe_iota32, dim3(grid_n(n)), dim3(256), 0, s, v0, n);
     hipLaunchKernelGGL(k_fe_gather_key, dim3(grid_n(n)), dim3(256), 0, s, start, (const uint32_t*)nullptr, k0, n);
     int alt = 0;
-    hipError_t e = sort_pairs_u64(k0, v0, k1, v1, n, 0, 64, tmp, s, &alt);
+    hipError_t e = sort_pairs_u64(k0, v0, k1, v1, n, 0, 64, tmp, s, &alt, /*iota=*/true);
     if (e != hipSuccess) return e;
     uint32_t* va = alt ? v1 : v0;
     uint32_t* vb = alt ? v0 : v1;

@@ -36,7 +36,6 @@ constexpr int kLaneSess = 3;        // sessions a thread replays in LDS
 constexpr int kSegThreads = 128;
 constexpr int kWideWords = 5;       // wide-table session: start, end, a0, a1, fired
 constexpr uint64_t kBigMeta = 1ull << 31;  // main-table slot word 1: the key lives in the wide table
-constexpr uint64_t kPuntMeta = 1ull << 30; // ... the key's later records of this batch go to the punt list
 
 struct SegArgs {
     const uint32_t* slot;   // sorted main-table slot of each record
@@ -61,18 +60,13 @@ struct SegArgs {
     TableView w;            // wide table: ring = K2, words = kWideWords
     uint32_t* punt;         // main pass: runs for the wide table (append at st->overflow)
     int64_t* mig;           // main pass: finished lists of more than K1 sessions (append at st->pad[0])
-    const uint32_t* runs;   // wide pass: run heads to replay; keyed path: slot per run start (k_sess_kprobe)
+    const uint32_t* runs;   // wide pass: run heads to replay
     int64_t n_runs;
     uint32_t* retry;        // wide pass: runs that did not fit K2 (append at st->overflow)
     DevStatus* st;
     int gshift;             // records are grouped by slot >> gshift (the sort skips the low bits)
-    // bucketed ingest (k_sb_part / k_sb_replay)
-    const int64_t* p_key;   // the bucket records (P2's buffer, or P1's without P2): keys
-    const longlong2* p_tv;  //   and (timestamp, value) pairs
-    int diag;               // bucketed: GW_SB_EXP=3 counts punts by reason (ShardCtr pad words of shards 2
-                            // and 3); keyed: GW_KSEG_FAST=0 replays every run through sp_run
-    int64_t* pu_key;        // punted records (arrival order per key), append at st->overflow (bucketed,
-                            // keyed) or st->spills (slot sort: keys the prep found no slot for)
+    int64_t* pu_key;        // records of keys the prep found no slot for (arrival order), append at
+                            // st->spills: replayed after a regrow
     int64_t* pu_ts;
     int64_t* pu_val;
 };
@@ -561,7 +555,7 @@ __global__ void __launch_bounds__(256) k_sess_wide(SegArgs a) {
 }
 
 __global__ void __launch_bounds__(256) k_sess_prep(const int64_t* key, const int64_t* ts, const int64_t* val, int64_t n,
-                                                   TableView t, uint32_t* slot, uint32_t* perm, int64_t* rec,
+                                                   TableView t, uint32_t* slot, int64_t* rec,
                                                    DevStatus* st) {
     unsigned long long ins = 0, flags = 0;
     if (blockIdx.x == 0 && threadIdx.x == 0) {  // the main pass's counters (nothing reads them before it)
@@ -575,805 +569,13 @@ __global__ void __launch_bounds__(256) k_sess_prep(const int64_t* key, const int
         int64_t s = sess_find_or_insert(t, key[i], inserted);
         ins += inserted;
         if (s < 0) { flags |= GW_DF_TABLE_FULL; s = t.cap + 1; }  // no slot: sorts last, the segment punts it
-        slot[i] = (uint32_t)s;
-        perm[i] = (uint32_t)i;
+        slot[i] = (uint32_t)s;  // (the arrival index, perm, is made by the sort's first pass)
         if (rec) {
             rec[2 * i] = ts[i];
             rec[2 * i + 1] = val ? val[i] : 0;
         }
     }
     block_commit(st, 0, ins, flags, 0);
-}
-
-// ---------------------------------------------------------- bucketed session ingest
-// The default session ingest.  Records are grouped by the home slot of
-// their key BEFORE anyone touches the table, so that each key is looked up once per batch
-// (not once per record) and its records are replayed from a bucket that sits in L2:
-//  * P1 k_sb_part<false>: one workgroup per 2048-record tile of the batch partitions the
-//    tile by the coarse digit of the home slot (its top bb1 bits), stably, and writes the
-//    tile back in digit order with one (start, count) descriptor per digit.
-//  * k_sb_cols: descriptor rows -> one column per coarse digit, plus the digit totals.
-//  * P2 k_sb_part<true>: one workgroup per 2048-record chunk of a coarse digit's records
-//    (gathered from P1's runs in tile order, i.e. arrival order) partitions it by the fine
-//    digit (the next bb2 bits), the same way.  Batches of at most 2^6 buckets skip P2.
-//  * P3 k_sb_replay: one workgroup per bucket (coarse, fine) concatenates the bucket's runs
-//    (arrival order), sorts them in LDS by (home slot, arrival) with a stable radix sort,
-//    and replays each home slot's run: one thread finds or inserts the key (sp_key: the
-//    probe the sort path's k_sess_prep makes per record, here once per key) and replays its
-//    records through MergingWindowSet.addWindow semantics (add_element_tv).
-// Long runs stay coalesced: P1's runs are 2048 / 2^bb1 records, P2's 2048 / 2^bb2 (32 at
-// the sessions config's 10M-record batches: 4096 buckets of ~2400 records).  A key that needs
-// the wide table (more in-flight sessions than the lane holds, or already wide) or finds no
-// slot, and every key of a bucket with more than kSbCap records, is punted: its records go to
-// a punt list in arrival order, which the sort path (k_sess_prep ... k_sess_wide) replays.
-constexpr int kSbTile = 2048;
-constexpr int kSbThreads = 512;
-constexpr int kSbItems = kSbTile / kSbThreads;
-constexpr int kSbWaveRecs = kSbTile / (kSbThreads / 64);
-constexpr int kSbMaxDigitBits = 8;
-constexpr int kSbMaxDigits = 1 << kSbMaxDigitBits;
-constexpr int kSbSinglePassBits = 6;      // buckets <= 2^6: P1 partitions by the whole bucket
-constexpr int kSbMeanBits = 9;             // ~2^9 records per bucket (mean in (256, 512]: half the cap)
-constexpr int kSbCap = 1024;               // records of a bucket the replay stages and sorts in LDS
-constexpr int kSbPosBits = 10;
-constexpr int kSbMaxHomeBits = 31 - kSbPosBits - 1;  // + the sentinel's code
-constexpr int kSbRThreads = 256;
-constexpr int kSbRItems = kSbCap / kSbRThreads;  // per thread per radix pass (at most)
-constexpr int kSbBins = 512;
-// P1/P2 LDS: key | ts | value staging, per-(wave, digit) counters, gather map (P2)
-constexpr size_t kSbPartLds = (size_t)kSbTile * 3 * 8 + (size_t)(kSbThreads / 64) * kSbMaxDigits * 2 + kSbTile * 4;
-
-// Home slot of a key in a table of 2^lcap slots; the sentinel key (the empty marker, which
-// lives in slot cap) goes with the last home slot's bucket.
-__device__ __forceinline__ uint64_t sb_home(int64_t key, int lcap) {
-    const uint64_t m = ((uint64_t)1 << lcap) - 1;
-    return key == kEmptyKey ? m : (slot_hash(key) & m);
-}
-
-// Coarse-bucket geometry shared by P2 and P3: chunk starts of each coarse digit (chunks of
-// kSbTile records) from the digit totals.  cs[0..nc] in LDS; one wave.
-__device__ __forceinline__ void sb_chunk_starts(const uint32_t* ctot, int nc, uint32_t* cs) {
-    if (threadIdx.x < 64) {
-        const int lane = threadIdx.x;
-        uint32_t run = 0;
-        for (int c0 = 0; c0 < nc; c0 += 64) {
-            const int c = c0 + lane;
-            const uint32_t x = c < nc ? (ctot[c] + kSbTile - 1) / kSbTile : 0u;
-            uint32_t incl = x;
-            for (int o = 1; o < 64; o <<= 1) {
-                const uint32_t up = __shfl_up(incl, o);
-                if (lane >= o) incl += up;
-            }
-            if (c < nc) cs[c] = run + incl - x;
-            run += __shfl(incl, 63);
-        }
-        if (lane == 0) cs[nc] = run;
-    }
-    __syncthreads();
-}
-
-// P1 (GATHER false): tile blockIdx.x of the batch (key, ts, val).  P2 (GATHER true): chunk
-// blockIdx.x of the coarse digits' records in P1's buffer (p_key, p_tv; runs col[c][tile],
-// totals ctot).  Either way the workgroup's records, in arrival order, are partitioned by
-// digit = (home >> shift) & (nd - 1), stably: wave w owns records [w*256, (w+1)*256) (item it
-// of lane l: w*256 + it*64 + l), lanes of one digit find each other with ballots, a leader
-// per digit bumps the wave's counter, and a block scan over (digit, wave) turns the counters
-// into offsets.  Out: the records in digit order at blockIdx.x * kSbTile, and one descriptor
-// row (start << 16 | count) per digit.
-template <bool GATHER>
-__global__ void __launch_bounds__(kSbThreads) k_sb_part(const int64_t* key, const int64_t* ts, const int64_t* val,
-                                                        int64_t n, const int64_t* p_key, const longlong2* p_tv,
-                                                        const uint32_t* col, const uint32_t* cpre,
-                                                        const uint32_t* ctot, int nc,
-                                                        int64_t ntiles, int lcap, int shift, int db, int64_t* o_key,
-                                                        longlong2* o_tv, uint32_t* row, DevStatus* st) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    int64_t* s_key = reinterpret_cast<int64_t*>(smem);
-    int64_t* s_ts = s_key + kSbTile;
-    int64_t* s_val = s_ts + kSbTile;
-    uint16_t* wcnt = reinterpret_cast<uint16_t*>(s_val + kSbTile);  // [wave][digit]
-    uint32_t* gmap = reinterpret_cast<uint32_t*>(wcnt + (kSbThreads / 64) * kSbMaxDigits);
-    __shared__ uint32_t lh[kSbMaxDigits], ls[kSbMaxDigits];
-    __shared__ uint32_t wsum[kSbThreads / 64];
-    __shared__ uint32_t cs[kSbMaxDigits + 1];
-    const int nd = 1 << db;
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int64_t g = blockIdx.x;
-    int cnt;
-    if constexpr (!GATHER) {
-        const int64_t lo = g * kSbTile;
-        cnt = (int)min((int64_t)kSbTile, n - lo);
-    } else {
-        sb_chunk_starts(ctot, nc, cs);
-        if (g >= cs[nc]) return;  // the grid is an upper bound on the chunks (uniform exit)
-        int c = 0;
-        while (c + 1 < nc && cs[c + 1] <= (uint32_t)g) ++c;
-        const uint32_t j0 = ((uint32_t)g - cs[c]) * kSbTile;
-        cnt = (int)min((uint32_t)kSbTile, ctot[c] - j0);
-        // gather map: position q of this chunk -> its P1 buffer offset.  The chunk's first tile
-        // t0 (the last with cpre <= j0) by a 64-ary search of wave 0 over the digit's prefix, then
-        // kSbThreads tiles at a time from there: a thread writes its tile's part of
-        // [j0, j0 + cnt).
-        const uint32_t* cc = col + (int64_t)c * ntiles;
-        const uint32_t* cp = cpre + (int64_t)c * ntiles;
-        __shared__ int64_t s_t0;
-        if (w == 0) {
-            int64_t lo = 0, len = ntiles;  // invariant: cp[lo] <= j0 (cp[0] == 0)
-            while (len > 1) {
-                const int64_t stride = (len + 63) / 64;
-                const int64_t t = lo + (int64_t)lane * stride;
-                const bool le = t < lo + len && cp[t] <= j0;
-                const uint64_t m = __ballot(le);
-                const int last = 63 - __clzll((long long)m);
-                lo += (int64_t)last * stride;
-                len = min(stride, len - (int64_t)last * stride);
-            }
-            if (lane == 0) s_t0 = lo;
-        }
-        __syncthreads();
-        const uint32_t j1 = j0 + (uint32_t)cnt;
-        for (int64_t tb = s_t0; tb < ntiles; tb += kSbThreads) {
-            const int64_t t = tb + tid;
-            if (t < ntiles) {
-                const uint32_t pre = cp[t];
-                const uint32_t d = cc[t];
-                const uint32_t a0 = max(pre, j0), a1 = min(pre + (d & 0xffffu), j1);
-                for (uint32_t u = a0; u < a1; ++u) gmap[u - j0] = (uint32_t)(t * kSbTile) + (d >> 16) + (u - pre);
-            }
-            if (__syncthreads_or(t < ntiles && cp[t] + (cc[t] & 0xffffu) >= j1)) break;  // the chunk is covered
-        }
-        __syncthreads();
-    }
-    for (int e = tid; e < (kSbThreads / 64) * nd; e += blockDim.x) wcnt[(e / nd) * kSbMaxDigits + e % nd] = 0;
-    int64_t k[kSbItems], t[kSbItems], v[kSbItems];
-#pragma unroll
-    for (int it = 0; it < kSbItems; ++it) {  // all loads in flight first
-        const int i = w * kSbWaveRecs + it * 64 + lane;
-        k[it] = 0; t[it] = 0; v[it] = 0;
-        if (i < cnt) {
-            if constexpr (!GATHER) {
-                const int64_t x = g * kSbTile + i;
-                k[it] = __builtin_nontemporal_load(key + x);
-                t[it] = __builtin_nontemporal_load(ts + x);
-                if (val) v[it] = __builtin_nontemporal_load(val + x);
-            } else {
-                const uint32_t o = gmap[i];
-                k[it] = p_key[o];
-                const longlong2 tv = p_tv[o];
-                t[it] = tv.x;
-                v[it] = tv.y;
-            }
-        }
-    }
-    __syncthreads();
-    unsigned long long flags = 0;
-    uint16_t* my = wcnt + w * kSbMaxDigits;
-    uint32_t bk[kSbItems], rk[kSbItems];
-#pragma unroll
-    for (int it = 0; it < kSbItems; ++it) {
-        const int i = w * kSbWaveRecs + it * 64 + lane;
-        const bool ok = i < cnt;
-        if (!GATHER && ok && t[it] == INT64_MIN) flags |= GW_DF_NO_TS;
-        const uint32_t b = ok ? (uint32_t)((sb_home(k[it], lcap) >> shift) & (uint64_t)(nd - 1)) : 0u;
-        uint64_t peers = __ballot(ok);
-        for (int q = 0; q < db; ++q) {
-            const uint64_t m = __ballot(ok && ((b >> q) & 1u));
-            peers &= ((b >> q) & 1u) ? m : ~m;
-        }
-        uint32_t old = 0;
-        const int leader = ok ? __ffsll((long long)peers) - 1 : 0;
-        if (ok && lane == leader) {
-            old = my[b];
-            my[b] = (uint16_t)(old + __popcll(peers));
-        }
-        old = __shfl(old, leader);
-        bk[it] = ok ? b : ~0u;
-        rk[it] = old + (uint32_t)__popcll(peers & ((1ull << lane) - 1ull));
-    }
-    __syncthreads();
-    {  // digit totals, exclusive scan over digits, then per-(wave, digit) offsets in place
-        uint32_t x = 0;
-        if (tid < nd)
-            for (int q = 0; q < kSbThreads / 64; ++q) x += wcnt[q * kSbMaxDigits + tid];
-        uint32_t incl = x;
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t up = __shfl_up(incl, o);
-            if (lane >= o) incl += up;
-        }
-        if (lane == 63) wsum[w] = incl;
-        __syncthreads();
-        uint32_t off = 0;
-        for (int q = 0; q < w; ++q) off += wsum[q];
-        if (tid < nd) {
-            ls[tid] = off + incl - x;
-            lh[tid] = x;
-            uint32_t r = off + incl - x;
-            for (int q = 0; q < kSbThreads / 64; ++q) {
-                const uint32_t c = wcnt[q * kSbMaxDigits + tid];
-                wcnt[q * kSbMaxDigits + tid] = (uint16_t)r;
-                r += c;
-            }
-        }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int it = 0; it < kSbItems; ++it) {
-        if (bk[it] == ~0u) continue;
-        const uint32_t j = my[bk[it]] + rk[it];
-        s_key[j] = k[it];
-        s_ts[j] = t[it];
-        s_val[j] = v[it];
-    }
-    __syncthreads();
-    const int64_t base = g * kSbTile;
-    for (int j = tid; j < cnt; j += blockDim.x) {
-        o_key[base + j] = s_key[j];
-        o_tv[base + j] = longlong2{s_ts[j], s_val[j]};
-    }
-    for (int b = tid; b < nd; b += blockDim.x) row[g * nd + b] = (ls[b] << 16) | lh[b];
-    if (!GATHER) block_commit(st, 0, 0, flags, 0);
-}
-
-// P1 descriptor rows [tile][digit] -> columns [digit][tile] (64 x 64 blocks through LDS),
-// and the digit totals (one atomic per digit per block; ctot zeroed beforehand).
-__global__ void __launch_bounds__(256) k_sb_cols(const uint32_t* row, uint32_t* col, uint32_t* ctot, int64_t ntiles,
-                                                 int nd) {
-    __shared__ uint32_t tt[64][65];
-    const int64_t t0 = (int64_t)blockIdx.x * 64;
-    const int b0 = blockIdx.y * 64;
-    for (int e = threadIdx.x; e < 64 * 64; e += blockDim.x) {
-        const int tl = e >> 6, bl = e & 63;
-        const int64_t t = t0 + tl;
-        tt[tl][bl] = (t < ntiles && b0 + bl < nd) ? row[t * nd + b0 + bl] : 0u;
-    }
-    __syncthreads();
-    for (int e = threadIdx.x; e < 64 * 64; e += blockDim.x) {
-        const int bl = e >> 6, tl = e & 63;
-        const int64_t t = t0 + tl;
-        if (t < ntiles && b0 + bl < nd) col[(int64_t)(b0 + bl) * ntiles + t] = tt[tl][bl];
-    }
-    if (threadIdx.x < 64 && b0 + (int)threadIdx.x < nd) {
-        uint32_t s = 0;
-        for (int tl = 0; tl < 64; ++tl) s += tt[tl][threadIdx.x] & 0xffffu;
-        if (s) atomicAdd(ctot + b0 + threadIdx.x, s);
-    }
-}
-
-// Per coarse digit (one workgroup each): exclusive prefix of its run lengths over the tiles,
-// pre[c][t] = records of digit c in tiles [0, t), so P2 finds its chunk's first tile by search.
-__global__ void __launch_bounds__(1024) k_sb_colscan(const uint32_t* col, uint32_t* pre, int64_t ntiles) {
-    __shared__ uint32_t wsum[16];
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const uint32_t* cc = col + (int64_t)blockIdx.x * ntiles;
-    uint32_t* pp = pre + (int64_t)blockIdx.x * ntiles;
-    uint32_t run = 0;
-    for (int64_t t0 = 0; t0 < ntiles; t0 += 1024) {
-        const int64_t t = t0 + tid;
-        const uint32_t x = t < ntiles ? (cc[t] & 0xffffu) : 0u;
-        uint32_t incl = x;
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t up = __shfl_up(incl, o);
-            if (lane >= o) incl += up;
-        }
-        if (lane == 63) wsum[w] = incl;
-        __syncthreads();
-        uint32_t off = run, tot = 0;
-        for (int q = 0; q < 16; ++q) {
-            if (q < w) off += wsum[q];
-            tot += wsum[q];
-        }
-        if (t < ntiles) pp[t] = off + incl - x;
-        run += tot;
-        __syncthreads();
-    }
-}
-
-// Session words per slot: start, end, acc (+ count for averages).
-template <int AGG>
-__device__ __forceinline__ constexpr int sess_words() {
-    return (AGG == GW_AVG_I64 || AGG == GW_AVG_F64) ? 4 : 3;
-}
-
-// One stable LSD radix pass over x[0..n) -> y in LDS, digit = (v >> sh) & (2^db - 1),
-// db <= 9, kSbRThreads threads.  Wave w owns positions [w*q, (w+1)*q) (q: a multiple of 64
-// with 4q >= n, so the waves share the records evenly; item it of lane l at w*q + it*64 + l),
-// so (wave, item, lane) is the input order; lanes of one digit find each other with db
-// ballots, and a leader per digit bumps the wave's counter.
-__device__ __forceinline__ void sb_radix_pass(const uint32_t* x, uint32_t* y, int n, int q, int sh, int db,
-                                              uint16_t* wcnt, uint32_t* wsum) {
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int nbins = 1 << db;
-    for (int e = tid; e < (kSbRThreads / 64) * kSbBins; e += blockDim.x) wcnt[e] = 0;
-    __syncthreads();
-    uint16_t* my = wcnt + w * kSbBins;
-    uint32_t v[kSbRItems], rk[kSbRItems];
-#pragma unroll
-    for (int it = 0; it < kSbRItems; ++it) {
-        const int pos = w * q + it * 64 + lane;
-        const bool ok = it * 64 < q && pos < n;
-        v[it] = ok ? x[pos] : 0u;
-        const uint32_t d = (v[it] >> sh) & (uint32_t)(nbins - 1);
-        uint64_t peers = __ballot(ok);
-        rk[it] = 0;
-        if (!peers) continue;  // wave-uniform
-        for (int b = 0; b < db; ++b) {
-            const uint64_t m = __ballot(ok && ((d >> b) & 1u));
-            peers &= ((d >> b) & 1u) ? m : ~m;
-        }
-        uint32_t old = 0;
-        const int leader = ok ? __ffsll((long long)peers) - 1 : 0;
-        if (ok && lane == leader) {
-            old = my[d];
-            my[d] = (uint16_t)(old + __popcll(peers));
-        }
-        old = __shfl(old, leader);
-        rk[it] = old + (uint32_t)__popcll(peers & ((1ull << lane) - 1ull));
-    }
-    __syncthreads();
-    {  // digit totals -> exclusive scan over digits -> per-(wave, digit) offsets in place
-        for (int d0 = 0; d0 < nbins; d0 += kSbRThreads) {
-            const int d = d0 + tid;
-            uint32_t tot = 0;
-            if (d < nbins)
-                for (int qq = 0; qq < kSbRThreads / 64; ++qq) tot += wcnt[qq * kSbBins + d];
-            uint32_t incl = tot;
-            for (int o = 1; o < 64; o <<= 1) {
-                const uint32_t up = __shfl_up(incl, o);
-                if (lane >= o) incl += up;
-            }
-            if (lane == 63) wsum[w] = incl;
-            __syncthreads();
-            uint32_t off = d0 ? wsum[kSbRThreads / 64] : 0u, all = off;
-            for (int qq = 0; qq < kSbRThreads / 64; ++qq) {
-                if (qq < w) off += wsum[qq];
-                all += wsum[qq];
-            }
-            if (d < nbins) {
-                uint32_t r = off + incl - tot;
-                for (int qq = 0; qq < kSbRThreads / 64; ++qq) {
-                    const uint32_t c = wcnt[qq * kSbBins + d];
-                    wcnt[qq * kSbBins + d] = (uint16_t)r;
-                    r += c;
-                }
-            }
-            __syncthreads();
-            if (tid == 0) wsum[kSbRThreads / 64] = all;  // running total for the next digit block
-            __syncthreads();
-        }
-    }
-#pragma unroll
-    for (int it = 0; it < kSbRItems; ++it) {
-        const int pos = w * q + it * 64 + lane;
-        if (it * 64 < q && pos < n) y[my[(v[it] >> sh) & (uint32_t)(nbins - 1)] + rk[it]] = v[it];
-    }
-    __syncthreads();
-}
-
-// sp_store / sp_key / sp_run (the replay of one home slot's run) follow below.  A run's
-// records come through an accessor: staged in LDS by the bucketed replay (LdsRecs), or in
-// HBM in arrival order behind the sorted arrival indices on the keyed sort path (HbmRecs).
-struct LdsRecs {
-    const uint32_t* pr;     // sorted position -> the record's place in the bucket
-    const int64_t* rk;      // keys and (timestamp, value) pairs by place
-    const longlong2* rtv;
-    __device__ __forceinline__ int64_t key(uint32_t q) const { return rk[pr[q]]; }
-    __device__ __forceinline__ longlong2 tv(uint32_t q) const { return rtv[pr[q]]; }
-};
-struct KeyRec { int64_t k, t, v; };  // one record of the batch, as k_sess_kprep copies it
-struct HbmRecs {
-    const uint32_t* perm;   // sorted position -> arrival index
-    const KeyRec* rec;      // the batch's records in arrival order
-    __device__ __forceinline__ int64_t key(uint32_t q) const { return rec[perm[q]].k; }
-    __device__ __forceinline__ longlong2 tv(uint32_t q) const {
-        const KeyRec& r = rec[perm[q]];
-        return longlong2{r.t, r.v};
-    }
-};
-// The key's list after a replay (cnt sessions in the lane) -> its slot, or to the migration
-// list when it outgrew the slot (the key's later records of the batch then punt until the
-// migration).
-template <int AGG>
-__device__ __forceinline__ void sp_store(const SegArgs& a, const SessList& l, int cnt, int64_t slot, int64_t* sp,
-                                         int64_t w1) {
-    constexpr int SW = sess_words<AGG>();
-    if (cnt <= a.t.ring) {
-        uint64_t fired = 0;
-        int64_t due = INT64_MAX;
-        for (int q = 0; q < cnt; ++q) {
-            const Sess v = sl_get(l, q);
-            int64_t* x = sp + 2 + q * SW;
-            x[0] = v.s; x[1] = v.e; x[2] = v.a0;
-            if (SW == 4) x[3] = v.a1;
-            fired |= (uint64_t)(v.f != 0) << q;
-            due = min(due, due_time(v.e, v.f != 0, a.lateness));
-        }
-        sp[1] = (int64_t)((fired << 32) | (uint64_t)(uint32_t)cnt);
-        due_set(a.t, slot, due);
-    } else {
-        const unsigned long long at = atomicAdd(&a.st->pad[0], 1ull);
-        int64_t* m = a.mig + at * (2 + kWideWords * kLaneSess);
-        m[0] = slot;
-        m[1] = cnt;
-        for (int q = 0; q < cnt; ++q) {
-            const Sess v = sl_get(l, q);
-            int64_t* x = m + 2 + q * kWideWords;
-            x[0] = v.s; x[1] = v.e; x[2] = v.a0; x[3] = v.a1; x[4] = v.f;
-        }
-        atomicMax(&a.st->pad[1], (unsigned long long)cnt);
-        sp[1] = (int64_t)((uint64_t)w1 | kPuntMeta);
-    }
-}
-
-// One key's records among the home slot's run [r0, f) of the sorted order (pr: the records'
-// positions in the bucket, rk / rtv: the bucket's keys and (timestamp, value) pairs staged in
-// LDS; r0 holds one of them, the others are the run's records with this key), in arrival
-// order, against the key's slot -- seg_slot's replay, with the punt list instead of the wide
-// pass.
-template <int AGG, class RV>
-__device__ __forceinline__ void sp_key(const SegArgs& a, const SessList& l, int64_t key, uint32_t r0, uint32_t f,
-                                       const RV& rv, unsigned long long& late, unsigned long long& merges,
-                                       unsigned long long& flags, unsigned long long& ins) {
-    constexpr int SW = sess_words<AGG>();
-    int64_t L = 0;
-    for (uint32_t q = r0; q < f; ++q) L += rv.key(q) == key;
-    bool inserted;
-    const int64_t slot = sess_find_or_insert(a.t, key, inserted);
-    int64_t* sp = slot >= 0 ? slot_ptr(a.t, slot) : nullptr;
-    if (sp) ins += inserted;
-    const int64_t w1 = sp ? sp[1] : 0;
-    bool ok = sp && !((uint64_t)w1 & (kBigMeta | kPuntMeta));
-    bool dry = ok && slot_cnt(w1) + L > kLaneSess;  // could outgrow the lane
-    const bool effects = a.lateness > 0 || a.lo_key;
-    const unsigned long long l0 = late, m0 = merges;
-    int cnt = 0;
-    while (ok) {  // at most two replays: dry, then (with effects) the real one
-        cnt = slot_cnt(w1);
-        for (int q = 0; q < cnt; ++q) {
-            const int64_t* x = sp + 2 + q * SW;
-            sl_put(l, q, Sess{x[0], x[1], x[2], SW == 4 ? x[3] : 0, (int64_t)slot_fired(w1, q)});
-        }
-        for (uint32_t q = r0; q < f && ok; ++q) {
-            if (rv.key(q) != key) continue;
-            const longlong2 tv = rv.tv(q);
-            ok = add_element_tv<AGG>(a, l, cnt, kLaneSess, key, tv.x, tv.y, late, merges, flags, dry);
-        }
-        if (!ok || !dry || !effects) break;
-        dry = false;
-        late = l0;
-        merges = m0;
-    }
-    if (!ok) {  // punt the key's records of the batch (kPuntMeta: also any that come after)
-        late = l0;
-        merges = m0;
-        if (a.diag) {  // GW_SB_EXP=3: punts by reason (no slot, wide / punted key, lane outgrown)
-            ShardCtr& sc = a.st->sh[2];
-            atomicAdd(!sp ? &sc.pad0 : ((uint64_t)w1 & (kBigMeta | kPuntMeta)) ? &sc.pad1 : &a.st->sh[3].pad0, (unsigned long long)L);
-        }
-        unsigned long long at = atomicAdd(&a.st->overflow, (unsigned long long)L);
-        for (uint32_t q = r0; q < f; ++q) {
-            if (rv.key(q) != key) continue;
-            const longlong2 tv = rv.tv(q);
-            a.pu_key[at] = key;
-            a.pu_ts[at] = tv.x;
-            a.pu_val[at] = tv.y;
-            ++at;
-        }
-        if (sp) sp[1] = (int64_t)((uint64_t)w1 | kPuntMeta);
-        return;
-    }
-    sp_store<AGG>(a, l, cnt, slot, sp, w1);
-}
-
-// Every key of a home slot's run [e, f), in order of its first record (several keys per home
-// slot are rare), through sp_key.
-template <int AGG, class RV>
-__device__ __forceinline__ void sp_run(const SegArgs& a, const SessList& l, uint32_t e, uint32_t f, const RV& rv,
-                                       unsigned long long& late, unsigned long long& merges,
-                                       unsigned long long& flags, unsigned long long& ins) {
-    for (uint32_t r = e; r < f;) {
-        sp_key<AGG>(a, l, rv.key(r), r, f, rv, late, merges, flags, ins);
-        uint32_t nx = f;
-        for (uint32_t q = r + 1; q < f && nx == f; ++q) {
-            const int64_t kq = rv.key(q);
-            bool seen = false;
-            for (uint32_t z = e; z < q && !seen; ++z) seen = rv.key(z) == kq;
-            if (!seen) nx = q;
-        }
-        r = nx;
-    }
-}
-
-// P3: one workgroup per bucket B = (coarse c, fine f).  The bucket's runs are desc[g * nf + f]
-// over the chunks g of coarse digit c ([cs[c], cs[c+1]) from the coarse totals; with P2
-// skipped, nc = 1 and the chunks are P1's tiles).  Concatenated in chunk order they are the
-// bucket's records in arrival order.  The workgroup stages the records in LDS (keys and
-// (timestamp, value) pairs, read coalesced from the runs), sorts the positions by (local home
-// slot, arrival) -- 32-bit keys (home << kSbPosBits | position), a stable radix sort over the
-// home bits -- and one thread per home slot replays the slot's run from LDS (sp_run: every
-// key of the run in order of its first record, usually one): its only global accesses are the
-// key's probe, its slot line and due time.  A bucket of more than kSbCap records punts all
-// of them (arrival order) to the sort path: its keys are disjoint from the other buckets'.
-template <int AGG>
-__global__ void __launch_bounds__(kSbRThreads) k_sb_replay(SegArgs a, const uint32_t* desc, const uint32_t* ctot,
-                                                           int nc, int64_t nchunks, int bf, int lcap, int sh,
-                                                           int exp) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    longlong2* rtv = reinterpret_cast<longlong2*>(smem);       // [kSbCap] (timestamp, value) by position
-    int64_t* rk = reinterpret_cast<int64_t*>(rtv + kSbCap);     // [kSbCap] key by position
-    uint32_t* ka = reinterpret_cast<uint32_t*>(rk + kSbCap);    // sort keys | radix double buffer
-    uint32_t* kb = ka + kSbCap;
-    uint32_t* hd = kb + kSbCap;                                 // run starts (gather), then the heads
-    uint16_t* wcnt = reinterpret_cast<uint16_t*>(hd + kSbCap);  // radix counters
-    int64_t* lanes = reinterpret_cast<int64_t*>(wcnt + (kSbRThreads / 64) * kSbBins);  // session lanes
-    __shared__ uint32_t wsum[kSbRThreads / 64 + 1];
-    __shared__ uint32_t cs[kSbMaxDigits + 1];
-    __shared__ uint32_t cpre[kSbRThreads + 1];
-    __shared__ uint32_t s_n, s_pb;
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int nf = 1 << bf;
-    const int64_t B = blockIdx.x;
-    const int c = (int)(B >> bf), f = (int)(B & (nf - 1));
-    int64_t g0 = 0, g1 = nchunks;
-    if (nc > 1) {
-        sb_chunk_starts(ctot, nc, cs);
-        g0 = cs[c];
-        g1 = cs[c + 1];
-    }
-    const uint64_t hmask = ((uint64_t)1 << sh) - 1;
-    const uint32_t sent = 1u << sh;
-    // records of the bucket
-    {
-        uint32_t x = 0;
-        for (int64_t g = g0 + tid; g < g1; g += kSbRThreads) x += desc[g * nf + f] & 0xffffu;
-        x = (uint32_t)wave_sum(x);
-        if (lane == 0) wsum[w] = x;
-        __syncthreads();
-        if (tid == 0) {
-            uint32_t tot = 0;
-            for (int q = 0; q < kSbRThreads / 64; ++q) tot += wsum[q];
-            s_n = tot;
-            s_pb = tot > (uint32_t)kSbCap ? (uint32_t)atomicAdd(&a.st->overflow, (unsigned long long)tot) : 0u;
-        }
-        __syncthreads();
-    }
-    const uint32_t n = s_n;
-    const bool over = n > (uint32_t)kSbCap;
-    const uint32_t pbase = s_pb;
-    // the runs in chunk order, kSbRThreads chunks at a time: a scan of their counts, then the
-    // block loads positions [run0, run0 + tot) cooperatively (coalesced within runs)
-    uint32_t run0 = 0;
-    for (int64_t b0 = g0; b0 < g1; b0 += kSbRThreads) {
-        const int64_t g = b0 + tid;
-        const uint32_t d = g < g1 ? desc[g * nf + f] : 0u;
-        const uint32_t x = d & 0xffffu;
-        uint32_t incl = x;
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t up = __shfl_up(incl, o);
-            if (lane >= o) incl += up;
-        }
-        if (lane == 63) wsum[w] = incl;
-        __syncthreads();
-        uint32_t pre = incl - x, tot = 0;
-        for (int q = 0; q < kSbRThreads / 64; ++q) {
-            if (q < w) pre += wsum[q];
-            tot += wsum[q];
-        }
-        cpre[tid] = pre;
-        hd[tid] = (uint32_t)(g * kSbTile) + (d >> 16);  // run starts
-        if (tid == 0) cpre[kSbRThreads] = tot;
-        __syncthreads();
-        for (uint32_t u = tid; u < tot; u += kSbRThreads) {
-            int lo = 0, hi = kSbRThreads - 1;  // last run with cpre <= u
-            while (lo < hi) {
-                const int mid = (lo + hi + 1) >> 1;
-                if (cpre[mid] <= u) lo = mid; else hi = mid - 1;
-            }
-            const uint32_t o = hd[lo] + (u - cpre[lo]);
-            const uint32_t pos = run0 + u;
-            const int64_t kk = a.p_key[o];
-            const longlong2 tv = a.p_tv[o];
-            if (over) {
-                a.pu_key[pbase + pos] = kk;
-                a.pu_ts[pbase + pos] = tv.x;
-                a.pu_val[pbase + pos] = tv.y;
-            } else {
-                const uint32_t lh = kk == kEmptyKey ? sent : (uint32_t)(sb_home(kk, lcap) & hmask);
-                ka[pos] = (lh << kSbPosBits) | pos;
-                rk[pos] = kk;
-                rtv[pos] = tv;
-            }
-        }
-        run0 += tot;
-        __syncthreads();  // cpre / the run starts are rewritten by the next block
-    }
-    if (over && exp == 3 && tid == 0) atomicAdd(&a.st->sh[3].pad1, (unsigned long long)n);
-    if (over || exp == 2) {  // (exp: GW_SB_EXP timing variants, results invalid: 2 = gather only)
-        block_commit(a.st, 0, 0, 0, 0);
-        return;
-    }
-    // home bits [kSbPosBits, kSbPosBits + sh + 1): passes of <= 9 bits, the waves sharing
-    // the records evenly
-    const int q = (int)(((n + 4 * 64 - 1) / (4 * 64)) * 64);
-    const int hb = sh + 1;
-    const int np = (hb + 8) / 9;
-    const uint32_t* fin = ka;
-    uint32_t* fin_o = kb;
-    for (int p = 0, done = 0; p < np; ++p) {
-        const int db = (hb - done + (np - p) - 1) / (np - p);
-        sb_radix_pass(fin, fin_o, (int)n, q, kSbPosBits + done, db, wcnt, wsum);
-        done += db;
-        uint32_t* t = const_cast<uint32_t*>(fin);
-        fin = fin_o;
-        fin_o = t;
-    }
-    // the order (positions in sorted order) in fin_o (free after the last pass), the heads in hd
-    constexpr uint32_t pm = (1u << kSbPosBits) - 1u;
-    uint32_t* pr = fin_o;
-    for (uint32_t i = tid; i < n; i += kSbRThreads) pr[i] = fin[i] & pm;
-    uint32_t nh = 0;  // heads: sorted index of each home slot's first record
-    for (uint32_t i0 = 0; i0 < n; i0 += kSbRThreads) {
-        const uint32_t i = i0 + tid;
-        const bool h = i < n && (i == 0 || (fin[i - 1] >> kSbPosBits) != (fin[i] >> kSbPosBits));
-        const uint64_t bal = __ballot(h);
-        if (lane == 0) wsum[w] = (uint32_t)__popcll(bal);
-        __syncthreads();
-        uint32_t base = nh, tot = 0;
-        for (int qq = 0; qq < kSbRThreads / 64; ++qq) {
-            if (qq < w) base += wsum[qq];
-            tot += wsum[qq];
-        }
-        if (h) hd[base + __popcll(bal & ((1ull << lane) - 1ull))] = i;
-        nh += tot;
-        __syncthreads();  // wsum is rewritten by the next chunk
-    }
-    if (exp == 1) {  // gather + sort + heads only (3: punt diagnostics, results valid)
-        block_commit(a.st, 0, 0, 0, 0);
-        return;
-    }
-    // replay: one thread per home slot's run, records from LDS
-    const SessList l{lanes + tid, kLaneSess * kSbRThreads, kSbRThreads};
-    unsigned long long late = 0, merges = 0, flags = 0, ins = 0;
-    for (uint32_t j = tid; j < nh; j += kSbRThreads) {
-        const uint32_t e = hd[j], fe = j + 1 < nh ? hd[j + 1] : n;
-        sp_run<AGG>(a, l, e, fe, LdsRecs{pr, rk, rtv}, late, merges, flags, ins);
-    }
-    block_commit(a.st, late, ins, flags, 0, 0, merges);
-}
-// P3 LDS: records (24 B), sort keys and radix buffer, heads (3 x 4 B) per position; radix
-// counters; the session lanes
-constexpr size_t kSbReplayLds = (size_t)kSbCap * (24 + 12) + (size_t)(kSbRThreads / 64) * kSbBins * 2 +
-                                (size_t)5 * kLaneSess * kSbRThreads * 8;
-
-// After a replay with punts: clear the punt marks before the sort path replays the list.
-__global__ void __launch_bounds__(256) k_sp_unpunt(TableView t, const int64_t* pk, int64_t n) {
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t slot = sess_find_slot(t, pk[i]);
-        if (slot < 0) continue;
-        int64_t* sp = slot_ptr(t, slot);
-        if ((uint64_t)sp[1] & kPuntMeta) atomicAnd((unsigned long long*)(sp + 1), ~(unsigned long long)kPuntMeta);
-    }
-}
-
-// ---------------------------------------------------------- keyed sort path (the default)
-// The sort path's grouping without its per-record table probe: records are grouped by a
-// 32-bit code of their key's hash whose top bits are the key's home slot (the hash rotated
-// right by lcap), so that the table is probed once per key of the batch, by the thread that
-// replays the key's run, and the runs reach the table in home-slot order.
-//  * k_sess_kprep: per record its code and arrival index, and a copy of the record (key,
-//    timestamp, value) in arrival order -- a pure stream, no table access.
-//  * a stable radix sort of (code, arrival index) over the code's top sbits bits;
-//  * k_sess_kseg: one thread per group of equal sorted codes (a run), replaying every key of
-//    the run in order of its first record (sp_run, as the bucketed replay does from LDS; two
-//    keys share a run only when their codes collide).  Keys that find no slot, live in the
-//    wide table or outgrow the lane are punted with their records, as on the bucketed path.
-__device__ __forceinline__ uint32_t key_code(int64_t key, int lcap, int sbits) {
-    const uint64_t h = slot_hash(key);
-    return (uint32_t)(((h >> lcap) | (h << (64 - lcap))) >> (64 - sbits));
-}
-
-__global__ void __launch_bounds__(256) k_sess_kprep(const int64_t* key, const int64_t* ts, const int64_t* val,
-                                                    int64_t n, int lcap, int sbits, uint32_t* code,
-                                                    uint32_t* perm, KeyRec* rec, DevStatus* st) {
-    unsigned long long flags = 0;
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t k = key[i], t = ts[i];
-        if (t == INT64_MIN) flags |= GW_DF_NO_TS;
-        code[i] = key_code(k, lcap, sbits);
-        perm[i] = (uint32_t)i;
-        rec[i] = KeyRec{k, t, val ? val[i] : 0};
-    }
-    block_commit(st, 0, 0, flags, 0);
-}
-
-// The common run in one pass over its records (no allowed lateness, no side output: the
-// replay has no effect beyond the key's slot, written at the end): the run is taken to hold
-// one key, so every record is loaded once, the next one in flight while the current one
-// replays.  Returns false, having written nothing, when the run turns out to hold another
-// key, the key finds no slot or is marked wide / punted, or the lane overflows; sp_run then
-// replays the run from the slot as it was.
-template <int AGG>
-__device__ __forceinline__ bool kseg_fast(const SegArgs& a, const SessList& l, uint32_t e, uint32_t f,
-                                          const HbmRecs& rv, uint32_t rslot, unsigned long long& late,
-                                          unsigned long long& merges, unsigned long long& flags) {
-    constexpr int SW = sess_words<AGG>();
-    if (rslot == ~0u) return false;  // k_sess_kprobe found no slot
-    KeyRec r = rv.rec[rv.perm[e]];
-    const int64_t key = r.k;
-    const int64_t slot = rslot;
-    int64_t* sp = slot_ptr(a.t, slot);
-    const int64_t w1 = sp[1];
-    if ((uint64_t)w1 & (kBigMeta | kPuntMeta)) return false;
-    int cnt = slot_cnt(w1);
-    for (int q = 0; q < cnt; ++q) {
-        const int64_t* x = sp + 2 + q * SW;
-        sl_put(l, q, Sess{x[0], x[1], x[2], SW == 4 ? x[3] : 0, (int64_t)slot_fired(w1, q)});
-    }
-    const unsigned long long l0 = late, m0 = merges, f0 = flags;
-    for (uint32_t q = e;;) {
-        KeyRec nx{};
-        if (q + 1 < f) nx = rv.rec[rv.perm[q + 1]];  // in flight during this record's replay
-        if (r.k != key || !add_element_tv<AGG>(a, l, cnt, kLaneSess, key, r.t, r.v, late, merges, flags, true)) {
-            late = l0;
-            merges = m0;
-            flags = f0;
-            return false;
-        }
-        if (++q >= f) break;
-        r = nx;
-    }
-    sp_store<AGG>(a, l, cnt, slot, sp, w1);
-    return true;
-}
-
-// The key of every run's first record finds or inserts its slot (rslot[run start]; ~0: no
-// slot): one probe per run with as many in flight as the grid holds, where k_sess_kseg's
-// lanes would wait on each probe between replays.
-__global__ void __launch_bounds__(256) k_sess_kprobe(TableView t, const uint32_t* code, const uint32_t* perm,
-                                                     const KeyRec* rec, int64_t n, uint32_t* rslot,
-                                                     DevStatus* st) {
-    unsigned long long ins = 0;
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-        if (i > 0 && code[i] == code[i - 1]) continue;
-        bool inserted;
-        const int64_t s = sess_find_or_insert(t, rec[perm[i]].k, inserted);
-        ins += inserted;
-        rslot[i] = s < 0 ? ~0u : (uint32_t)s;
-    }
-    block_commit(st, 0, ins, 0, 0);
-}
-
-// Each wave takes kSegChunk consecutive sorted records, compacts the run heads among them
-// into LDS with ballots and replays them 64 at a time (a run that starts in the chunk belongs
-// to it, however far it extends).
-template <int AGG>
-__global__ void __launch_bounds__(kSegThreads) k_sess_kseg(SegArgs a, const uint32_t* code, int shift,
-                                                           const KeyRec* rec) {
-    __shared__ int64_t lane[5 * kLaneSess * kSegThreads];
-    __shared__ uint32_t heads[kSegThreads / 64][kSegChunk];
-    const SessList l{lane + threadIdx.x, kLaneSess * kSegThreads, kSegThreads};
-    unsigned long long late = 0, merges = 0, flags = 0, ins = 0;
-    const int w = threadIdx.x >> 6, ln = threadIdx.x & 63;
-    const int64_t base = (blockIdx.x * (int64_t)(kSegThreads / 64) + w) * kSegChunk;
-    int nh = 0;
-    for (int c = 0; c < kSegChunk; c += 64) {
-        const int64_t i = base + c + ln;
-        const bool h = i < a.n && (i == 0 || (code[i] >> shift) != (code[i - 1] >> shift));
-        const uint64_t b = __ballot(h);
-        if (h) heads[w][nh + __popcll(b & ((1ull << ln) - 1ull))] = (uint32_t)(i - base);
-        nh += __popcll(b);
-    }
-    __syncthreads();
-    const HbmRecs rv{a.perm, rec};
-    const bool effects = a.lateness > 0 || a.lo_key || a.diag;  // diag: GW_KSEG_FAST=0
-    for (int q = ln; q < nh; q += 64) {
-        const int64_t i = base + heads[w][q];
-        const uint32_t g = code[i] >> shift;
-        int64_t j = i + 1;
-        while (j < a.n && (code[j] >> shift) == g) ++j;
-        if (effects || !kseg_fast<AGG>(a, l, (uint32_t)i, (uint32_t)j, rv, a.runs[i], late, merges, flags))
-            sp_run<AGG>(a, l, (uint32_t)i, (uint32_t)j, rv, late, merges, flags, ins);
-    }
-    block_commit(a.st, late, ins, flags, 0, 0, merges);
 }
 
 // Fire sweep, part 1: list the slots with something due at `wm` -- a small fraction: the
@@ -1929,23 +1131,16 @@ struct SessionState {
     uint32_t* r0 = nullptr;  // punted / retried run heads
     uint32_t* r1 = nullptr;
     int64_t* mig = nullptr;  // migration lists (main pass -> wide table)
-    int64_t* rec = nullptr;  // sessions: (ts, value) per record (sort path), KeyRec (keyed sort path)
-    int64_t* ks_pu = nullptr;  // keyed sort path: punted key | ts | value, buf_cap each
-    // bucketed ingest (k_sb_*): P1 / P2 records (key | ts, value: 24 B each), descriptor
-    // rows / columns / coarse totals, punted records
-    int64_t* sb_rec[2] = {nullptr, nullptr};
-    uint32_t* sb_desc = nullptr;
-    int64_t* pu_col3 = nullptr;  // punted key | ts | value, sb_cap each
-    int64_t sb_cap = 0, sb_desc_cap = 0;
+    int64_t* rec = nullptr;  // sessions: (ts, value) per record in arrival order
+    int64_t* pu_rec = nullptr;  // sessions: records of keys the prep found no slot for, key | ts | value
     bool fresh = false;      // h_st matches the device (nothing launched since the last refresh)
-    // A bucketed ingest whose host follow-up (punts, migrations) waits for the next sync: the
-    // fire launched right after it checks the device counters and skips itself if the
-    // follow-up has work (k_sess_due_scan), so the common batch costs one host sync, not two.
+    // An ingest whose host follow-up (sort_tail: migrations, the wide pass, records without a
+    // slot) waits for the next sync: the fire launched right after it checks the device
+    // counters and skips itself if the follow-up has work (k_sess_due_scan), so the common
+    // batch costs one host sync, not two.
     bool sb_pend = false;
-    bool sort_pend = false;  // ... and that ingest took the slot sort path: its tail (sort_tail) waits
     SegArgs sort_a{};
     int64_t sb_wm = 0, sb_new = 0;
-    int64_t* sb_pu[3] = {nullptr, nullptr, nullptr};
     int gshift = 0;          // sessions: the last sort grouped records by slot >> gshift
     uint32_t* due_list = nullptr;  // fire sweep: main-table slots with something due
     int64_t due_list_cap = 0;
@@ -2108,10 +1303,9 @@ void session_destroy(SessionState* s) {
     hipFree(s->d_st);
     hipHostFree(s->h_st);
     for (int q = 0; q < 2; ++q) { hipFree(s->slot[q]); hipFree(s->perm[q]); }
-    hipFree(s->r0); hipFree(s->r1); hipFree(s->mig); hipFree(s->rec); hipFree(s->ks_pu);
+    hipFree(s->r0); hipFree(s->r1); hipFree(s->mig); hipFree(s->rec); hipFree(s->pu_rec);
     hipFree(s->cnt_plan); hipFree(s->cnt_tmp); hipFree(s->due_list);
     hipFree(s->sort_tmp);
-    hipFree(s->sb_rec[0]); hipFree(s->sb_rec[1]); hipFree(s->sb_desc); hipFree(s->pu_col3);
     hipFree(s->o_key); hipFree(s->o_start); hipFree(s->o_end); hipFree(s->o_res);
     for (auto* p : s->lo_buf) hipFree(p);
     for (int w = 0; w < 2; ++w) for (auto& p : s->ev_pending[w]) s->ev_pool.push_back(p);
@@ -2124,10 +1318,10 @@ static int ensure_bufs(SessionState* s, int64_t n, std::string& err) {
     const int64_t c = std::max<int64_t>(n + n / 4, 1 << 16);
     SCHECK(hipStreamSynchronize(s->stream));
     for (int q = 0; q < 2; ++q) { hipFree(s->slot[q]); hipFree(s->perm[q]); }
-    hipFree(s->r0); hipFree(s->r1); hipFree(s->mig); hipFree(s->sort_tmp); hipFree(s->rec); hipFree(s->ks_pu);
+    hipFree(s->r0); hipFree(s->r1); hipFree(s->mig); hipFree(s->sort_tmp); hipFree(s->rec); hipFree(s->pu_rec);
     s->mig = nullptr;
     s->rec = nullptr;
-    s->ks_pu = nullptr;
+    s->pu_rec = nullptr;
     for (int q = 0; q < 2; ++q) {
         SCHECK(hipMalloc((void**)&s->slot[q], c * 4));
         SCHECK(hipMalloc((void**)&s->perm[q], c * 4));
@@ -2135,8 +1329,8 @@ static int ensure_bufs(SessionState* s, int64_t n, std::string& err) {
     SCHECK(hipMalloc((void**)&s->r0, c * 4));
     SCHECK(hipMalloc((void**)&s->r1, c * 4));
     if (!s->count_mode) SCHECK(hipMalloc((void**)&s->mig, (size_t)c * (2 + kWideWords * kLaneSess) * 8));
-    if (!s->count_mode) SCHECK(hipMalloc((void**)&s->rec, (size_t)c * sizeof(KeyRec)));
-    if (!s->count_mode) SCHECK(hipMalloc((void**)&s->ks_pu, (size_t)c * 24));
+    if (!s->count_mode) SCHECK(hipMalloc((void**)&s->rec, (size_t)c * 16));
+    if (!s->count_mode) SCHECK(hipMalloc((void**)&s->pu_rec, (size_t)c * 24));
     const size_t bytes = (size_t)sort_scratch_bytes(c);
     SCHECK(hipMalloc(&s->sort_tmp, bytes));
     s->sort_tmp_bytes = bytes;
@@ -2160,7 +1354,7 @@ static int sort_by_slot(SessionState* s, int64_t n, int64_t cap, const uint32_t*
     s->gshift = s->count_mode ? 0 : std::min(4, std::max(0, bits - sort_bits));
     int alt = 0;
     SCHECK(sort_pairs_u32(s->slot[0], s->perm[0], s->slot[1], s->perm[1], n, s->gshift, bits, s->sort_tmp, s->stream,
-                          &alt));
+                          &alt, /*iota=*/true));
     *sk = s->slot[alt];
     *sp = s->perm[alt];
     return GW_OK;
@@ -2275,7 +1469,7 @@ static int group_records(SessionState* s, int64_t n, const int64_t* key, const i
     if ((rc = ensure_bufs(s, n, err))) return rc;
     for (int attempt = 0;; ++attempt) {
         hipLaunchKernelGGL(k_sess_prep, dim3(grid_of(n)), dim3(256), 0, s->stream, key, ts, val, n, s->tv, s->slot[0],
-                           s->perm[0], s->count_mode ? nullptr : s->rec, s->d_st);
+                           s->count_mode ? nullptr : s->rec, s->d_st);
         // deferred (sessions): no host wait here; records without a slot sort last and the
         // segment punts them for a replay after a regrow (sort_tail)
         if (defer && !s->count_mode) break;
@@ -2417,9 +1611,8 @@ static int run_migrate(SessionState* s, std::string& err) {
     return GW_OK;
 }
 
-// Sort path: slot per record (k_sess_prep), stable radix sort by slot, one thread per key run
-// (k_sess_segment), migrations, then the wide pass over punted runs.  Replays the punt list
-// of the region path, and is the whole ingest under GW_SESSION_PATH=sort.
+// Session ingest: slot per record (k_sess_prep), stable radix sort by slot (gw_sort.hip), one
+// thread per key run (k_sess_segment), migrations, then the wide pass over punted runs.
 static int sort_tail(SessionState* s, SegArgs a, int64_t wm, std::string& err);
 
 // defer: return right after the segment launch (no host wait) when the replay emits nothing
@@ -2443,9 +1636,9 @@ static int ingest_sorted(SessionState* s, int64_t n, const int64_t* key, const i
     s->h_st->overflow = s->h_st->pad[0] = s->h_st->pad[1] = 0;
     a.punt = s->r0;
     const int64_t C = s->buf_cap;  // records without a slot (deferred prep): punt columns
-    a.pu_key = s->ks_pu;
-    a.pu_ts = s->ks_pu + C;
-    a.pu_val = s->ks_pu + 2 * C;
+    a.pu_key = s->pu_rec;
+    a.pu_ts = s->pu_rec + C;
+    a.pu_val = s->pu_rec + 2 * C;
     const int64_t per_block = (int64_t)kSegChunk * (kSegThreads / 64);
     const unsigned gs = (unsigned)((n + per_block - 1) / per_block);
 #define L(A) hipLaunchKernelGGL(k_sess_segment<A>, dim3(gs), dim3(kSegThreads), 0, s->stream, a)
@@ -2454,7 +1647,6 @@ static int ingest_sorted(SessionState* s, int64_t n, const int64_t* key, const i
     SCHECK(hipGetLastError());
     if (defer) {
         s->sort_a = a;
-        s->sort_pend = true;
         s->sb_pend = true;
         s->sb_wm = wm;
         s->sb_new = n;
@@ -2471,6 +1663,7 @@ static int sort_tail(SessionState* s, SegArgs a, int64_t wm, std::string& err) {
     int rc;
     const int64_t n_fail = (int64_t)s->h_st->spills;
     if (n_fail > 0) {  // the prep's TABLE_FULL is handled below, not an error of the passes before
+        s->stats.session_punted += n_fail;
         if ((rc = zero_word_async(s, offsetof(DevStatus, spills), err))) return rc;
         SCHECK(launch_status_set(s->d_st, 0, 0, 2, s->stream));  // zero sh[].flags
         s->h_st->flags &= ~GW_DF_TABLE_FULL;
@@ -2514,246 +1707,12 @@ static int sort_tail(SessionState* s, SegArgs a, int64_t wm, std::string& err) {
     return GW_OK;
 }
 
-static void sb_opt_in() {
-    static bool done = false;
-    if (done) return;
-    hipFuncSetAttribute((const void*)k_sb_part<false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kSbPartLds);
-    hipFuncSetAttribute((const void*)k_sb_part<true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kSbPartLds);
-#define L(A) hipFuncSetAttribute((const void*)k_sb_replay<A>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kSbReplayLds)
-    L(GW_COUNT); L(GW_SUM_I64); L(GW_SUM_I32); L(GW_SUM_F64); L(GW_MIN_I64); L(GW_MIN_F64); L(GW_MAX_I64);
-    L(GW_MAX_F64); L(GW_AVG_I64); L(GW_AVG_F64);
-#undef L
-    done = true;
-}
-
-// Bucket geometry of a batch of n records on a table of 2^lcap slots: bb bucket bits (about
-// 2^kSbMeanBits records per bucket; the sort key holds at most kSbMaxHomeBits home bits per
-// bucket), split into bb1 coarse (P1) and bb2 fine (P2) digit bits.  False: beyond the
-// bucketed path's geometry (the sort path takes the batch).
-static bool sb_geometry(int64_t n, int lcap, int& bb, int& bb1, int& bb2) {
-    bb = 0;
-    while (bb < 2 * kSbMaxDigitBits && (n >> (bb + kSbMeanBits)) > 0) ++bb;
-    bb = std::max(bb, lcap - kSbMaxHomeBits);
-    bb = std::min(bb, lcap);
-    if (bb > 2 * kSbMaxDigitBits) return false;
-    if (bb <= kSbSinglePassBits) {
-        bb1 = bb;
-        bb2 = 0;
-    } else {
-        bb1 = (bb + 1) / 2;
-        bb2 = bb - bb1;
-    }
-    return true;
-}
-
-// Bucketed path (k_sb_part P1 / k_sb_cols / k_sb_part P2 / k_sb_replay), then migrations, then
-// the sort path over the punted records.
-static int ingest_region(SessionState* s, int64_t n, const int64_t* key, const int64_t* ts, const int64_t* val,
-                         int64_t wm, std::string& err) {
-    int rc;
-    // room for n new keys, as group_records keeps it: every key of the batch finds a slot
-    // within the probe limit unless the table is nearly full (the punt list takes those)
-    if ((double)(s->h_st->used_slots + n) > 0.7 * (double)s->tv.cap &&
-        ((double)s->h_st->used_slots > 0.7 * (double)s->tv.cap ||
-         (double)(s->h_st->used_slots + n) > 0.95 * (double)s->tv.cap)) {
-        int64_t want = s->tv.cap;
-        while ((double)(s->h_st->used_slots + n) > 0.7 * (double)want) want *= 2;
-        if ((rc = regrow(s, s->tv, want, s->tv.ring, false, err))) return rc;
-    }
-    if ((rc = ensure_bufs(s, n, err))) return rc;  // the migration list
-    int lcap = 0;
-    while (((int64_t)1 << lcap) < s->tv.cap) ++lcap;
-    int bb, bb1, bb2;
-    if (!sb_geometry(n, lcap, bb, bb1, bb2)) return ingest_sorted(s, n, key, ts, val, wm, err);
-    const int sh = lcap - bb;
-    const int nd1 = 1 << bb1, nd2 = 1 << bb2;
-    const int64_t ntiles = (n + kSbTile - 1) / kSbTile;
-    const int64_t nch = bb2 ? ntiles + nd1 : 0;  // P2 chunks: an upper bound
-    const int64_t recs = (ntiles + nch) * kSbTile;
-    // descriptors: P1 rows + columns + column prefixes, coarse totals, P2 rows
-    const int64_t dwords = 3 * ntiles * nd1 + nd1 + nch * nd2;
-    if ((ntiles + nd1) * kSbTile > s->sb_cap || dwords > s->sb_desc_cap) {
-        SCHECK(hipStreamSynchronize(s->stream));
-        if ((ntiles + nd1) * kSbTile > s->sb_cap) {
-            for (auto*& p : s->sb_rec) { hipFree(p); p = nullptr; }
-            hipFree(s->pu_col3);
-            s->pu_col3 = nullptr;
-            const int64_t c = std::max<int64_t>((ntiles + nd1) * kSbTile * 5 / 4, kSbTile * 16);
-            for (auto*& p : s->sb_rec) SCHECK(hipMalloc((void**)&p, (size_t)c * 24));
-            SCHECK(hipMalloc((void**)&s->pu_col3, (size_t)c * 24));
-            s->sb_cap = c;
-        }
-        if (dwords > s->sb_desc_cap) {
-            hipFree(s->sb_desc);
-            s->sb_desc = nullptr;
-            const int64_t c = std::max<int64_t>(dwords * 5 / 4, 1 << 16);
-            SCHECK(hipMalloc((void**)&s->sb_desc, (size_t)c * 4));
-            s->sb_desc_cap = c;
-        }
-    }
-    (void)recs;
-    const int64_t C = s->sb_cap;
-    int64_t* k1 = s->sb_rec[0];
-    longlong2* tv1 = reinterpret_cast<longlong2*>(k1 + C);
-    int64_t* k2 = s->sb_rec[1];
-    longlong2* tv2 = reinterpret_cast<longlong2*>(k2 + C);
-    uint32_t* row1 = s->sb_desc;
-    uint32_t* col1 = row1 + ntiles * nd1;
-    uint32_t* cpre1 = col1 + ntiles * nd1;
-    uint32_t* ctot = cpre1 + ntiles * nd1;
-    uint32_t* row2 = ctot + nd1;
-    sb_opt_in();
-    static const int sb_exp = getenv("GW_SB_EXP") ? atoi(getenv("GW_SB_EXP")) : 0;
-    if ((rc = zero_word_async(s, offsetof(DevStatus, overflow), err))) return rc;
-    if ((rc = zero_word_async(s, offsetof(DevStatus, pad[0]), err))) return rc;
-    if ((rc = zero_word_async(s, offsetof(DevStatus, pad[1]), err))) return rc;
-    hipLaunchKernelGGL(k_sb_part<false>, dim3((unsigned)ntiles), dim3(kSbThreads), kSbPartLds, s->stream, key, ts, val,
-                       n, nullptr, nullptr, nullptr, nullptr, nullptr, 0, ntiles, lcap, sh + bb2, bb1, k1, tv1, row1,
-                       s->d_st);
-    SegArgs a{};
-    if ((rc = seg_common(s, a, n, wm, err))) return rc;
-    a.diag = sb_exp == 3;
-    a.pu_key = s->pu_col3;
-    a.pu_ts = s->pu_col3 + C;
-    a.pu_val = s->pu_col3 + 2 * C;
-    if (bb2) {
-        SCHECK(hipMemsetAsync(ctot, 0, (size_t)nd1 * 4, s->stream));
-        hipLaunchKernelGGL(k_sb_cols, dim3((unsigned)((ntiles + 63) / 64), (unsigned)((nd1 + 63) / 64)), dim3(256), 0,
-                           s->stream, row1, col1, ctot, ntiles, nd1);
-        hipLaunchKernelGGL(k_sb_colscan, dim3((unsigned)nd1), dim3(1024), 0, s->stream, col1, cpre1, ntiles);
-        hipLaunchKernelGGL(k_sb_part<true>, dim3((unsigned)nch), dim3(kSbThreads), kSbPartLds, s->stream, nullptr,
-                           nullptr, nullptr, n, k1, tv1, col1, cpre1, ctot, nd1, ntiles, lcap, sh, bb2, k2, tv2, row2,
-                           s->d_st);
-        a.p_key = k2;
-        a.p_tv = tv2;
-    } else {
-        a.p_key = k1;
-        a.p_tv = tv1;
-    }
-    SCHECK(hipGetLastError());
-#define L(A)                                                                                                     \
-    hipLaunchKernelGGL(k_sb_replay<A>, dim3((unsigned)(nd1 * nd2)), dim3(kSbRThreads), kSbReplayLds, s->stream, a, \
-                       bb2 ? row2 : row1, ctot, bb2 ? nd1 : 1, bb2 ? nch : ntiles, bb2 ? bb2 : bb1, lcap, sh, sb_exp)
-    GW_AGG_SWITCH(s->cfg.agg, L);
-#undef L
-    SCHECK(hipGetLastError());
-    if (sb_exp == 3) {
-        SCHECK(hipStreamSynchronize(s->stream));
-        DevStatus d;
-        SCHECK(hipMemcpy(&d, s->d_st, sizeof d, hipMemcpyDeviceToHost));
-        fprintf(stderr, "[sb] n %lld buckets %d (bb %d = %d + %d, sh %d): punted %llu: no slot %llu, wide/punted key %llu, "
-                        "lane %llu, over-cap buckets %llu\n",
-                (long long)n, nd1 * nd2, bb, bb1, bb2, sh, (unsigned long long)d.overflow, d.sh[2].pad0, d.sh[2].pad1,
-                d.sh[3].pad0, d.sh[3].pad1);
-        for (int q = 2; q < 4; ++q) {
-            SCHECK(launch_status_set(s->d_st, 0, 0, 6, s->stream));
-            SCHECK(launch_status_set(s->d_st, 0, 0, 7, s->stream));
-        }
-    }
-    s->sb_pend = true;
-    s->sb_wm = wm;
-    s->sb_new = n;
-    s->sb_pu[0] = a.pu_key;
-    s->sb_pu[1] = a.pu_ts;
-    s->sb_pu[2] = a.pu_val;
-    s->fresh = false;
-    // without allowed lateness and side output the replay emits nothing, so the follow-up
-    // may wait for the fire's sync (GW_SESSION_SYNC=1: always sync here)
-    static const bool always = getenv("GW_SESSION_SYNC") && atoi(getenv("GW_SESSION_SYNC")) != 0;
-    if (!always && a.lateness == 0 && !a.lo_key) return GW_OK;
-    return session_refresh(s, err);
-}
-
-// Keyed sort path (k_sess_kprep / sort / k_sess_kseg), then -- at the next sync, as for the
-// bucketed path -- migrations and the punted records through the sort path.
-static int ingest_keyed(SessionState* s, int64_t n, const int64_t* key, const int64_t* ts, const int64_t* val,
-                        int64_t wm, std::string& err) {
-    int rc;
-    // room for n new keys, as group_records keeps it (keys that still find no slot punt)
-    if ((double)(s->h_st->used_slots + n) > 0.7 * (double)s->tv.cap &&
-        ((double)s->h_st->used_slots > 0.7 * (double)s->tv.cap ||
-         (double)(s->h_st->used_slots + n) > 0.95 * (double)s->tv.cap)) {
-        int64_t want = s->tv.cap;
-        while ((double)(s->h_st->used_slots + n) > 0.7 * (double)want) want *= 2;
-        if ((rc = regrow(s, s->tv, want, s->tv.ring, false, err))) return rc;
-    }
-    int lcap = 0;
-    while (((int64_t)1 << lcap) < s->tv.cap) ++lcap;
-    if (lcap < 1 || lcap > 30) return ingest_sorted(s, n, key, ts, val, wm, err);
-    if ((rc = ensure_bufs(s, n, err))) return rc;
-    // code bits sorted: the home slot and two more hash bits, in whole 9-bit radix passes (a
-    // run mixes keys only when their codes collide in these bits)
-    const int kbits_env = getenv("GW_SESSION_KEY_BITS") ? atoi(getenv("GW_SESSION_KEY_BITS")) : 0;
-    int sbits = kbits_env > 0 ? std::min(32, kbits_env) : std::min(32, (lcap + 2 + 8) / 9 * 9);
-    const int shift = 0;  // the code holds exactly the sorted bits (a sort from bit 0)
-    if ((rc = zero_word_async(s, offsetof(DevStatus, overflow), err))) return rc;
-    if ((rc = zero_word_async(s, offsetof(DevStatus, pad[0]), err))) return rc;
-    if ((rc = zero_word_async(s, offsetof(DevStatus, pad[1]), err))) return rc;
-    KeyRec* rec = reinterpret_cast<KeyRec*>(s->rec);
-    hipLaunchKernelGGL(k_sess_kprep, dim3(grid_of(n)), dim3(256), 0, s->stream, key, ts, val, n, lcap, sbits,
-                       s->slot[0], s->perm[0], rec, s->d_st);
-    SCHECK(hipGetLastError());
-    int alt = 0;
-    SCHECK(sort_pairs_u32(s->slot[0], s->perm[0], s->slot[1], s->perm[1], n, 0, sbits, s->sort_tmp, s->stream, &alt));
-    SegArgs a{};
-    if ((rc = seg_common(s, a, n, wm, err))) return rc;
-    a.diag = getenv("GW_KSEG_FAST") && atoi(getenv("GW_KSEG_FAST")) == 0;
-    a.slot = s->slot[alt];
-    a.perm = s->perm[alt];
-    a.runs = s->r0;  // per run start: the slot k_sess_kprobe found
-    hipLaunchKernelGGL(k_sess_kprobe, dim3(grid_of(n)), dim3(256), 0, s->stream, s->tv, a.slot, a.perm, rec, n, s->r0,
-                       s->d_st);
-    const int64_t C = s->buf_cap;
-    a.pu_key = s->ks_pu;
-    a.pu_ts = s->ks_pu + C;
-    a.pu_val = s->ks_pu + 2 * C;
-    const int64_t per_block = (int64_t)kSegChunk * (kSegThreads / 64);
-    const unsigned gs = (unsigned)((n + per_block - 1) / per_block);
-#define L(A) hipLaunchKernelGGL(k_sess_kseg<A>, dim3(gs), dim3(kSegThreads), 0, s->stream, a, a.slot, shift, rec)
-    GW_AGG_SWITCH(s->cfg.agg, L);
-#undef L
-    SCHECK(hipGetLastError());
-    s->sb_pend = true;
-    s->sb_wm = wm;
-    s->sb_new = n;
-    s->sb_pu[0] = a.pu_key;
-    s->sb_pu[1] = a.pu_ts;
-    s->sb_pu[2] = a.pu_val;
-    s->fresh = false;
-    static const bool always = getenv("GW_SESSION_SYNC") && atoi(getenv("GW_SESSION_SYNC")) != 0;
-    if (!always && a.lateness == 0 && !a.lo_key) return GW_OK;
-    return session_refresh(s, err);
-}
-
-// The follow-up of a bucketed ingest (h_st fresh): migrations, then the punted records
-// through the sort path.
+// The deferred tail of the last ingest (h_st fresh): migrations, the wide pass, records
+// without a slot (sort_tail).
 static int sb_finish(SessionState* s, std::string& err) {
     if (!s->sb_pend) return GW_OK;
     s->sb_pend = false;
-    if (s->sort_pend) {
-        s->sort_pend = false;
-        return sort_tail(s, s->sort_a, s->sb_wm, err);
-    }
-    int rc;
-    const int64_t n_punt = (int64_t)s->h_st->overflow;
-    s->stats.session_punted += n_punt;
-    if ((rc = run_migrate(s, err))) return rc;
-    if (!n_punt) return GW_OK;
-    hipLaunchKernelGGL(k_sp_unpunt, dim3(grid_of(n_punt)), dim3(256), 0, s->stream, s->tv, s->sb_pu[0], n_punt);
-    SCHECK(hipGetLastError());
-    return ingest_sorted(s, n_punt, s->sb_pu[0], s->sb_pu[1], s->sb_pu[2], s->sb_wm, err);
-}
-
-// GW_SESSION_PATH=sort|keyed|region picks the ingest path (GW_SESSION_SORT_BITS, the sort
-// path's group tests, implies sort).  The slot sort path is the default: on the sessions
-// config the keyed and bucketed paths measured slower (all three are bound by
-// random line accesses -- probes, record gathers, slot lines -- and the slot sort path makes
-// the fewest per record).
-enum { kPathKeyed = 0, kPathRegion = 1, kPathSort = 2 };
-static int session_path() {
-    const char* p = getenv("GW_SESSION_PATH");
-    if (p) return !strcmp(p, "keyed") ? kPathKeyed : !strcmp(p, "region") ? kPathRegion : kPathSort;
-    return kPathSort;
+    return sort_tail(s, s->sort_a, s->sb_wm, err);
 }
 
 int session_ingest(SessionState* s, int64_t n, const int64_t* key, const int64_t* ts, const int64_t* val, int64_t wm,
@@ -2765,11 +1724,7 @@ int session_ingest(SessionState* s, int64_t n, const int64_t* key, const int64_t
     if ((int64_t)n > (int64_t)0x7fffffffLL) { err = "batch too large"; return GW_E_INVALID; }
     auto ev = s->timing ? get_ev(s) : std::pair<hipEvent_t, hipEvent_t>{};
     if (s->timing) SCHECK(hipEventRecord(ev.first, s->stream));
-    const int path = session_path();  // read per batch: tests switch paths within one process
-    rc = path == kPathKeyed    ? ingest_keyed(s, n, key, ts, val, wm, err)
-         : path == kPathRegion ? ingest_region(s, n, key, ts, val, wm, err)
-                               : ingest_sorted(s, n, key, ts, val, wm, err, true);
-    if (rc) return rc;
+    if ((rc = ingest_sorted(s, n, key, ts, val, wm, err, true))) return rc;
     if (s->timing) {
         SCHECK(hipEventRecord(ev.second, s->stream));
         s->ev_pending[0].push_back(ev);

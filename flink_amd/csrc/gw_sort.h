@@ -4,12 +4,13 @@
 namespace gw {
 // Stable LSD radix sort of (key, uint32 value) pairs by key bits [lo, hi) (gw_sort.hip): digits of
 // <= 9 bits, one launch per digit.  The result is in (k1, v1) if *result_in_alt, else in
-// (k0, v0); v0 / v1 may be null (keys only).  scratch: sort_scratch_bytes(n) bytes.
+// (k0, v0); v0 / v1 may be null (keys only).  iota: v0's contents are not read, the values are the
+// arrival indices 0..n-1.  scratch: sort_scratch_bytes(n) bytes.
 int64_t sort_scratch_bytes(int64_t n);
 hipError_t sort_pairs_u32(uint32_t* k0, uint32_t* v0, uint32_t* k1, uint32_t* v1, int64_t n, int lo, int hi,
-                          void* scratch, hipStream_t s, int* result_in_alt);
+                          void* scratch, hipStream_t s, int* result_in_alt, bool iota = false);
 hipError_t sort_pairs_u64(uint64_t* k0, uint32_t* v0, uint64_t* k1, uint32_t* v1, int64_t n, int lo, int hi,
-                          void* scratch, hipStream_t s, int* result_in_alt);
+                          void* scratch, hipStream_t s, int* result_in_alt, bool iota = false);
 // sort_pairs_u64 over bits [0, bits) (the re-fire list)
 int64_t radix_sort_scratch_bytes(int64_t n);
 hipError_t radix_sort_pairs(uint64_t* k0, uint32_t* v0, uint64_t* k1, uint32_t* v1, int64_t n, int bits,

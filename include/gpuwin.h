@@ -161,10 +161,10 @@ typedef struct gw_stats {
     int64_t region_format;    /* record format of the last region flush window: 0 wide,
                                  1 compact (hash word + 32-bit value), 2 narrow (32-bit
                                  key + 28-bit value; 4 B for COUNT); -1 none yet       */
-    int64_t session_punted;   /* session records the region ingest handed to the sort path
-                                 (keys needing the wide table, or without a free slot)  */
-    int64_t session_slow;     /* session home slots the region ingest replayed on its
-                                 general path (displaced or shared slots, long runs)     */
+    int64_t session_punted;   /* session records whose key found no free slot in the main
+                                 table: replayed after the table grew                    */
+    int64_t session_slow;     /* reserved (0): the removed bucketed session ingest's
+                                 general-path count                                      */
 } gw_stats;
 
 /* ---- lifecycle ------------------------------------------------------------ */

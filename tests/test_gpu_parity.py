@@ -368,6 +368,56 @@ def test_lds_preaggregation_low_cardinality(oracle_lib, agg, flags):
     assert _cmp(g, o, agg) == []
 
 
+@pytest.mark.parametrize("agg", ["count", "sum_i64", "avg_f64", "max_i64"])
+def test_lds_preaggregation_overflowing_key_cache(oracle_lib, agg):
+    """Forced pre-aggregation with 6000 keys (beyond a workgroup's 1024-entry key cache and
+    2048 LDS cells: those records go to the table directly), the sentinel key Long.MIN_VALUE,
+    and a table that starts at 16 slots (keys without a slot defer; the table grows)."""
+    kw = dict(assigner="sliding", size=4000, slide=2000, agg=agg)
+    keys, ts, vals, batches = random_stream(seed=19, n=600_000, num_keys=6000, n_batches=6, ts_step=1, agg=agg)
+    keys[::101] = W.LONG_MIN
+    g, _, stats = run_gpu(kw, keys, ts, vals, batches, flags=N.FLAG_FORCE_LDS_PREAGG, capacity_hint=16)
+    o, _ = run_oracle(oracle_lib, kw, keys, ts, vals, batches)
+    assert stats["preagg_batches"] > 0
+    assert _cmp(g, o, agg) == []
+
+
+def test_lds_preaggregation_ysb_20m():
+    """YSB-shaped, at full batch size: 20M records of 100 campaigns (random 64-bit ids) in
+    10-s tumbling windows, one batch, COUNT; every (campaign, window) count checked exactly
+    against numpy (the pre-aggregation path is taken automatically)."""
+    import torch
+    n = 20_000_000
+    rng = np.random.default_rng(23)
+    campaigns = rng.integers(-(1 << 62), 1 << 62, 100, dtype=np.int64)
+    cidx = rng.integers(0, 100, n)
+    keys = campaigns[cidx]
+    ts = (np.arange(n, dtype=np.int64) // 400) - rng.integers(0, 51, n)
+    op = W.GpuWindowOperator(W.TumblingEventTimeWindows.of(10_000), "count", capacity_hint=1024,
+                             max_batch=n).open()
+    try:
+        dk = torch.from_numpy(keys).cuda()
+        dt = torch.from_numpy(ts).cuda()
+        N.check(N.lib().gw_ingest_device(op.handle, n, dk.data_ptr(), None, dt.data_ptr(), None, op.stream()),
+                op.handle)
+        op.advance_watermark(W.LONG_MAX)
+        k, s, e, r = op.drain()
+        stats = op.stats()
+    finally:
+        op.close()
+    assert stats["preagg_batches"] == 1
+    win = ts // 10_000  # floor: TimeWindow.getWindowStartWithOffset for negative ts too
+    w0 = int(win.min())
+    nw = int(win.max()) - w0 + 1
+    cnt = np.bincount(cidx * nw + (win - w0), minlength=100 * nw)
+    nz = np.nonzero(cnt)[0]
+    exp = sorted(zip(campaigns[nz // nw].tolist(), ((nz % nw + w0) * 10_000).tolist(), cnt[nz].tolist()))
+    got = sorted(zip(k.tolist(), s.tolist(), r.view(np.int64).tolist()))
+    assert len(got) == len(exp)
+    assert got == exp
+    assert np.all(e - s == 10_000)
+
+
 @pytest.mark.parametrize("flags", [N.FLAG_NO_REGION, N.FLAG_FORCE_REGION], ids=["direct", "region"])
 def test_special_keys_and_timestamps(oracle_lib, flags):
     """Long.MIN_VALUE (the table's empty marker) and Long.MAX_VALUE as keys, negative
