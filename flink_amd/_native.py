@@ -55,6 +55,8 @@ EXPORTS = [
     "gw_window_stagger_offset", "gw_stage_alloc", "gw_stage_columns", "gw_ingest_stage", "gw_stage_send",
     "gw_ingest_payload", "gw_ingest_payload_device", "gw_drain_payload",
     "gw_snapshot_keys", "gw_snapshot_remap_keys", "gw_snapshot_payloads", "gw_snapshot_remap_payloads",
+    "gw_pack_geom_init", "gw_pack_records", "gw_unpack_records", "gw_partition_packed_device", "gw_unpack_device",
+    "gw_exchange_enable_packing", "gw_exchange_last_packed", "gw_exchange_plan_packed",
 ]
 EXCHANGE_ID_BYTES = 128
 
@@ -76,6 +78,12 @@ def record_layout(types: str, key_field: int, value_field: int = -1) -> GwRecord
     lay.nfields, lay.key_field, lay.value_field = len(types), key_field, value_field
     lay.types = types.encode()
     return lay
+
+
+class GwPackGeom(ctypes.Structure):
+    """gw_pack_geom: packed exchange records (include/gpuwin.h)."""
+    _fields_ = [("pane", ctypes.c_int64), ("offset", ctypes.c_int64), ("base_pane", ctypes.c_int64),
+                ("enabled", ctypes.c_int32), ("pad", ctypes.c_int32)]
 
 
 class NativeLibraryError(RuntimeError):
@@ -195,6 +203,15 @@ def lib() -> ctypes.CDLL:
         "gw_stage_send": (c_int, [p, i32, i64, i32]),
         "gw_exchange_min_watermark": (c_int, [p, i64, P64, p]),
         "gw_exchange_last_error": (ctypes.c_char_p, [p]),
+        "gw_pack_geom_init": (c_int, [ctypes.POINTER(GwPackGeom), i64, i64, i64, i64]),
+        "gw_pack_records": (c_int, [i64, p, p, p, ctypes.POINTER(GwPackGeom), p, p]),
+        "gw_unpack_records": (c_int, [i64, p, ctypes.POINTER(GwPackGeom), p, p, p]),
+        "gw_partition_packed_device": (c_int, [i64, p, p, p, i32, i32, ctypes.POINTER(GwPackGeom), p, p, p, p, p, p,
+                                               p]),
+        "gw_unpack_device": (c_int, [i64, p, ctypes.POINTER(GwPackGeom), p, p, p, p]),
+        "gw_exchange_enable_packing": (c_int, [p, i64, i64, i64, i32]),
+        "gw_exchange_last_packed": (i64, [p]),
+        "gw_exchange_plan_packed": (c_int, [i32, p, p, p, p, p, p, P64, P64]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -242,17 +259,70 @@ def snapshot_remap_keys(blob: bytes, mapping: dict) -> bytes:
     return buf.raw[:len(blob)]
 
 
+MSG_WORDS = 4  # exchange message per peer: (records, watermark, column mask, packed records)
+
+
 def exchange_plan(sent_msg, recv_msg, cols_mask: int, wm: int):
     """gw_exchange_plan (host only): per-peer (send_off, send_cnt, recv_off, recv_cnt), total
-    received, minimum watermark from this rank's sent / received (records, watermark, mask)
-    messages (int64[nranks * 3] each)."""
+    received, minimum watermark from this rank's sent / received (records, watermark, mask,
+    packed records) messages (int64[nranks * 4] each)."""
     import numpy as np
     sm = np.ascontiguousarray(sent_msg, dtype=np.int64)
     rm = np.ascontiguousarray(recv_msg, dtype=np.int64)
-    P = len(sm) // 3
+    P = len(sm) // MSG_WORDS
     out = [np.zeros(P, np.int64) for _ in range(4)]
     tot, wmin = ctypes.c_int64(), ctypes.c_int64()
     rc = lib().gw_exchange_plan(P, sm.ctypes.data, rm.ctypes.data, int(cols_mask), int(wm),
                                 *[o.ctypes.data for o in out], ctypes.byref(tot), ctypes.byref(wmin))
     check(rc)
     return out, tot.value, wmin.value
+
+
+def exchange_plan_packed(sent_msg, recv_msg):
+    """gw_exchange_plan_packed: per-peer (send_packed, recv_other_off, recv_packed_off,
+    recv_packed), total other, total packed."""
+    import numpy as np
+    sm = np.ascontiguousarray(sent_msg, dtype=np.int64)
+    rm = np.ascontiguousarray(recv_msg, dtype=np.int64)
+    P = len(sm) // MSG_WORDS
+    out = [np.zeros(P, np.int64) for _ in range(4)]
+    to, tp = ctypes.c_int64(), ctypes.c_int64()
+    check(lib().gw_exchange_plan_packed(P, sm.ctypes.data, rm.ctypes.data, *[o.ctypes.data for o in out],
+                                        ctypes.byref(to), ctypes.byref(tp)))
+    return out, to.value, tp.value
+
+
+def pack_geom(size: int, slide: int, offset: int, watermark: int):
+    """gw_pack_geom_init; None when the geometry does not pack (size < slide, no watermark yet)."""
+    g = GwPackGeom()
+    rc = lib().gw_pack_geom_init(ctypes.byref(g), int(size), int(slide), int(offset), int(watermark))
+    if rc == GW_E_UNSUPPORTED:
+        return None
+    check(rc)
+    return g
+
+
+def pack_records(keys, ts, vals, g: GwPackGeom):
+    """gw_pack_records (host): (words uint64[n], fits bool[n])."""
+    import numpy as np
+    keys = np.ascontiguousarray(keys, np.int64)
+    ts = np.ascontiguousarray(ts, np.int64)
+    vals = None if vals is None else np.ascontiguousarray(vals, np.int64)
+    n = keys.size
+    w = np.zeros(n, np.uint64)
+    f = np.zeros(n, np.uint8)
+    check(lib().gw_pack_records(n, keys.ctypes.data, ts.ctypes.data, None if vals is None else vals.ctypes.data,
+                                ctypes.byref(g), w.ctypes.data, f.ctypes.data))
+    return w, f.astype(bool)
+
+
+def unpack_records(words, g: GwPackGeom, with_values: bool = True):
+    """gw_unpack_records (host): (keys, ts, values or None)."""
+    import numpy as np
+    words = np.ascontiguousarray(words, np.uint64)
+    n = words.size
+    k, t = np.zeros(n, np.int64), np.zeros(n, np.int64)
+    v = np.zeros(n, np.int64) if with_values else None
+    check(lib().gw_unpack_records(n, words.ctypes.data, ctypes.byref(g), k.ctypes.data, t.ctypes.data,
+                                  None if v is None else v.ctypes.data))
+    return k, t, v

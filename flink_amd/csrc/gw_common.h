@@ -19,6 +19,41 @@ constexpr int kMaxRing = 64;              // pane ring length limit (64-bit pres
 constexpr int kMaxProbe = 128;            // linear-probe limit before a record is parked
 
 // ---------------------------------------------------------------------------
+// Packed exchange records (include/gpuwin.h gw_pack_geom; gw_keygroups.hip partition,
+// gw_exchange.cpp): one 8-byte word instead of 24 B of key, ts and value,
+//   lo32 = key, hi32 = value << 4 | d   (d = the record's pane - base_pane, 0 <= d < 16)
+// for a record whose key is in [0, 2^32), whose value (when the batch has values) is in
+// [-2^27, 2^27), and whose pane floor((ts - offset) / pane) lies in [base_pane, base_pane + 16).
+// Unpacked, its timestamp is its pane's start: for tumbling / sliding windows with
+// size >= slide and pane = gcd(size, slide) every window decision (assignWindows, isLate,
+// the cleanup time) depends on the pane alone.
+// ---------------------------------------------------------------------------
+using PackGeom = gw_pack_geom;
+constexpr int kPackPanes = 16;
+constexpr int64_t kPackValLimit = 1ll << 27;
+
+GW_HD bool pack_word(const PackGeom& g, int64_t key, int64_t ts, bool has_val, int64_t v, uint64_t& w) {
+    if ((uint64_t)key >> 32) return false;
+    constexpr int64_t kLim = 1ll << 62;  // |ts|, |offset| below it: no overflow below
+    if (ts < -kLim || ts >= kLim || g.offset < -kLim || g.offset >= kLim) return false;
+    const int64_t rel = ts - g.offset;
+    int64_t q = rel / g.pane;
+    if (rel % g.pane < 0) --q;  // floor (TimeWindow.getWindowStartWithOffset)
+    int64_t d;
+    if (__builtin_sub_overflow(q, g.base_pane, &d) || d < 0 || d >= kPackPanes) return false;
+    if (!has_val) v = 0;
+    else if (v < -kPackValLimit || v >= kPackValLimit) return false;
+    w = (uint64_t)(uint32_t)key | ((uint64_t)(((uint32_t)(int32_t)v << 4) | (uint32_t)d) << 32);
+    return true;
+}
+GW_HD void unpack_word(const PackGeom& g, uint64_t w, int64_t& key, int64_t& ts, int64_t& v) {
+    const uint32_t hi = (uint32_t)(w >> 32);
+    key = (int64_t)(uint32_t)w;
+    ts = (g.base_pane + (int64_t)(hi & 15u)) * g.pane + g.offset;
+    v = (int64_t)((int32_t)hi >> 4);
+}
+
+// ---------------------------------------------------------------------------
 // Java hashing (bit-exact with the reference)
 // ---------------------------------------------------------------------------
 GW_HD uint32_t rotl32(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }

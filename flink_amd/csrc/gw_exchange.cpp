@@ -10,7 +10,13 @@
 // per-owner counts go through one RCCL all-to-all, and every column moves as one grouped
 // ncclSend / ncclRecv per peer (xGMI point-to-point links; no host copy of the records).
 // The watermark combine (StatusWatermarkValve.inputWatermark, min over input channels)
-// is an RCCL all-reduce(MIN) of one int64.
+// rides the count all-to-all.
+//
+// Packing (gw_exchange_enable_packing): a record that fits travels as one 8-byte word
+// (gw_common.h pack_word: key, value and its pane relative to the watermark before the batch)
+// instead of 24 B; the partition sorts each destination's records into (packed, other), both
+// go out per peer, and the receiver unpacks the words behind the other records.  The base
+// pane comes from the previous batch's combined watermark, which every rank knows alike.
 #include "gw_kernels.h"
 
 #include <hip/hip_runtime.h>
@@ -32,20 +38,28 @@ struct gw_exchange {
     int64_t* part = nullptr;  // partitioned key | ts | value columns, cap records each
     int32_t* part_hash = nullptr;
     int64_t part_cap = 0;
+    uint64_t* part_packed = nullptr;  // packed words (partition numbering), cap records
     int64_t* recv[2] = {nullptr, nullptr};  // receive sets used in turn: key | ts | value columns
     int32_t* recv_hash[2] = {nullptr, nullptr};
+    uint64_t* recv_packed[2] = {nullptr, nullptr};
     int64_t recv_cap[2] = {0, 0};
     int turn = 0;
-    // One all-to-all message per peer and batch: (records for it, watermark, column mask).
-    // d_msg: [nranks][kMsg] send | [nranks][kMsg] receive; h_msg its pinned copy.
-    static constexpr int kMsg = 3;
-    int64_t* d_counts = nullptr;  // [nranks] partition counts
+    // packing (gw_exchange_enable_packing): window geometry and the last combined watermark
+    bool pack_on = false, pack_values = false;
+    int64_t pack_size = 0, pack_slide = 0, pack_offset = 0;
+    int64_t last_wm = INT64_MIN;
+    int64_t last_packed = 0;
+    // One all-to-all message per peer and batch: (records for it, watermark, column mask,
+    // packed records).  d_msg: [nranks][kMsg] send | [nranks][kMsg] receive; h_msg its pinned copy.
+    static constexpr int kMsg = 4;
+    int64_t* d_counts = nullptr;  // [2 nranks] partition counts (packing: packed, other per peer)
     int64_t* d_msg = nullptr;
     int64_t* h_msg = nullptr;
     int64_t* d_wm = nullptr;
     int64_t* h_wm = nullptr;
     std::vector<int64_t> last_send, last_recv;
     std::vector<int64_t> plan[4];  // gw_exchange_plan: send offsets, send counts, receive offsets, receive counts
+    std::vector<int64_t> pplan[4];  // gw_exchange_plan_packed: send packed, receive other / packed offsets, packed
     // per receive set: the hand-off stream the ingest orders on, and its "reads done" event
     hipStream_t handoff[2] = {nullptr, nullptr};
     hipEvent_t ev_recv[2] = {nullptr, nullptr}, ev_free[2] = {nullptr, nullptr};
@@ -95,12 +109,12 @@ int gw_exchange_create(gw_exchange** out, int32_t nranks, int32_t rank, const vo
     ncclUniqueId u;
     memcpy(&u, id, sizeof(u));
     if (ncclCommInitRank(&ex->comm, nranks, u, rank) != ncclSuccess) return bail(GW_E_DEVICE);
-    const size_t words = (size_t)nranks * (1 + 2 * gw_exchange::kMsg) + 2;
+    const size_t words = (size_t)nranks * (2 + 2 * gw_exchange::kMsg) + 2;
     if (hipMalloc((void**)&ex->d_counts, words * 8) != hipSuccess) return bail(GW_E_OOM);
     if (hipHostMalloc((void**)&ex->h_msg, (size_t)(2 * gw_exchange::kMsg * nranks + 2) * 8, hipHostMallocDefault) !=
         hipSuccess)
         return bail(GW_E_OOM);
-    ex->d_msg = ex->d_counts + nranks;
+    ex->d_msg = ex->d_counts + 2 * nranks;
     ex->d_wm = ex->d_msg + 2 * gw_exchange::kMsg * nranks;
     ex->h_wm = ex->h_msg + 2 * gw_exchange::kMsg * nranks;
     for (int q = 0; q < 2; ++q) {
@@ -112,6 +126,7 @@ int gw_exchange_create(gw_exchange** out, int32_t nranks, int32_t rank, const vo
     ex->last_send.assign(nranks, 0);
     ex->last_recv.assign(nranks, 0);
     for (auto& v : ex->plan) v.assign(nranks, 0);
+    for (auto& v : ex->pplan) v.assign(nranks, 0);
     *out = ex;
     return GW_OK;
 }
@@ -123,7 +138,8 @@ void gw_exchange_destroy(gw_exchange* ex) {
     hipFree(ex->scratch);
     hipFree(ex->part);
     hipFree(ex->part_hash);
-    for (int q = 0; q < 2; ++q) { hipFree(ex->recv[q]); hipFree(ex->recv_hash[q]); }
+    hipFree(ex->part_packed);
+    for (int q = 0; q < 2; ++q) { hipFree(ex->recv[q]); hipFree(ex->recv_hash[q]); hipFree(ex->recv_packed[q]); }
     hipFree(ex->d_counts);
     hipHostFree(ex->h_msg);
     for (int q = 0; q < 2; ++q) {
@@ -146,7 +162,8 @@ int gw_exchange_plan(int32_t nranks, const int64_t* sent_msg, const int64_t* rec
     bool agree = true;
     for (int q = 0; q < nranks; ++q) {
         const int64_t s = sent_msg[M * q], r = recv_msg[M * q];
-        if (s < 0 || r < 0) return GW_E_INVALID;
+        const int64_t sp = sent_msg[M * q + 3], rp = recv_msg[M * q + 3];
+        if (s < 0 || r < 0 || sp < 0 || sp > s || rp < 0 || rp > r) return GW_E_INVALID;
         send_off[q] = so;
         send_cnt[q] = s;
         recv_off[q] = ro;
@@ -161,6 +178,65 @@ int gw_exchange_plan(int32_t nranks, const int64_t* sent_msg, const int64_t* rec
     return agree ? GW_OK : GW_E_INVALID;
 }
 
+int gw_exchange_plan_packed(int32_t nranks, const int64_t* sent_msg, const int64_t* recv_msg, int64_t* send_packed,
+                            int64_t* recv_other_off, int64_t* recv_packed_off, int64_t* recv_packed,
+                            int64_t* total_other, int64_t* total_packed) {
+    constexpr int M = gw_exchange::kMsg;
+    if (nranks < 1 || !sent_msg || !recv_msg || !send_packed || !recv_other_off || !recv_packed_off ||
+        !recv_packed || !total_other || !total_packed)
+        return GW_E_INVALID;
+    int64_t wo = 0, po = 0;
+    for (int q = 0; q < nranks; ++q) {
+        const int64_t s = sent_msg[M * q], r = recv_msg[M * q];
+        const int64_t sp = sent_msg[M * q + 3], rp = recv_msg[M * q + 3];
+        if (s < 0 || r < 0 || sp < 0 || sp > s || rp < 0 || rp > r) return GW_E_INVALID;
+        send_packed[q] = sp;
+        recv_other_off[q] = wo;
+        recv_packed_off[q] = po;
+        recv_packed[q] = rp;
+        wo += r - rp;
+        po += rp;
+    }
+    *total_other = wo;
+    *total_packed = po;
+    return GW_OK;
+}
+
+static int64_t gcd64(int64_t a, int64_t b) {
+    while (b) { const int64_t t = a % b; a = b; b = t; }
+    return a;
+}
+
+int gw_pack_geom_init(gw_pack_geom* g, int64_t size, int64_t slide, int64_t offset, int64_t watermark) {
+    if (!g || size <= 0 || slide <= 0) return GW_E_INVALID;
+    *g = gw_pack_geom{};
+    if (size < slide || watermark == INT64_MIN) return GW_E_UNSUPPORTED;
+    const int64_t pane = gcd64(size, slide);
+    __int128 rel = (__int128)watermark - offset;
+    __int128 q = rel / pane;
+    if (rel % pane < 0) --q;
+    if (q > INT64_MAX || q < INT64_MIN) return GW_E_UNSUPPORTED;
+    g->pane = pane;
+    g->offset = offset;
+    g->base_pane = (int64_t)q;
+    g->enabled = 1;
+    return GW_OK;
+}
+
+int gw_exchange_enable_packing(gw_exchange* ex, int64_t size, int64_t slide, int64_t offset, int32_t with_values) {
+    if (!ex || size <= 0 || slide <= 0) return GW_E_INVALID;
+    if (size < slide) return ex_fail(ex, GW_E_UNSUPPORTED, "packing needs size >= slide");
+    if (ex->nranks > 128) return ex_fail(ex, GW_E_UNSUPPORTED, "packing needs <= 128 ranks");
+    ex->pack_on = true;
+    ex->pack_values = with_values != 0;
+    ex->pack_size = size;
+    ex->pack_slide = slide;
+    ex->pack_offset = offset;
+    return GW_OK;
+}
+
+int64_t gw_exchange_last_packed(const gw_exchange* ex) { return ex ? ex->last_packed : 0; }
+
 int gw_exchange_batch(gw_exchange* ex, int64_t n, const int64_t* d_key, const int32_t* d_key_hash,
                       const int64_t* d_ts, const int64_t* d_value, int64_t wm, int64_t* n_out,
                       const int64_t** d_key_out, const int32_t** d_key_hash_out, const int64_t** d_ts_out,
@@ -169,19 +245,29 @@ int gw_exchange_batch(gw_exchange* ex, int64_t n, const int64_t* d_key, const in
     hipStream_t s = (hipStream_t)stream;
     const int P = ex->nranks;
     constexpr int M = gw_exchange::kMsg;
-    // 1. stable device partition by owner subtask
+    // packing this batch: configured, a previous combined watermark, no key-hash column, and
+    // values only if the caller declared them packable -- the same on every rank (the mask
+    // check below fails every rank otherwise)
+    gw_pack_geom g{};
+    if (ex->pack_on && !d_key_hash && (!d_value || ex->pack_values))
+        (void)gw_pack_geom_init(&g, ex->pack_size, ex->pack_slide, ex->pack_offset, ex->last_wm);
+    const bool packed = g.enabled != 0;
+    // 1. stable device partition by owner (packing: by owner, then packed / not)
     if (n > ex->part_cap) {
         EX_HIP(hipStreamSynchronize(s));
         hipFree(ex->part);
         hipFree(ex->part_hash);
+        hipFree(ex->part_packed);
         ex->part = nullptr;
         ex->part_hash = nullptr;
+        ex->part_packed = nullptr;
         const int64_t c = n + n / 4 + 1024;
         EX_HIP(hipMalloc((void**)&ex->part, (size_t)c * 3 * 8));
         EX_HIP(hipMalloc((void**)&ex->part_hash, (size_t)c * 4));
         ex->part_cap = c;
     }
-    const int64_t need = partition_scratch_bytes(std::max<int64_t>(n, 1), P);
+    if (packed && !ex->part_packed) EX_HIP(hipMalloc((void**)&ex->part_packed, (size_t)ex->part_cap * 8));
+    const int64_t need = partition_scratch_bytes(std::max<int64_t>(n, 1), 2 * P);
     if (need > ex->scratch_bytes) {
         EX_HIP(hipStreamSynchronize(s));
         hipFree(ex->scratch);
@@ -194,13 +280,15 @@ int gw_exchange_batch(gw_exchange* ex, int64_t n, const int64_t* d_key, const in
     int64_t* pv = pt + ex->part_cap;
     if (n > 0) {
         EX_HIP(launch_partition(n, d_key, d_key_hash, d_ts, d_value, ex->max_p, P, pk, pt, d_value ? pv : nullptr,
-                                ex->d_counts, ex->scratch, s, d_key_hash ? ex->part_hash : nullptr));
+                                ex->d_counts, ex->scratch, s, d_key_hash ? ex->part_hash : nullptr,
+                                packed ? &g : nullptr, ex->part_packed));
     } else {
-        EX_HIP(hipMemsetAsync(ex->d_counts, 0, (size_t)P * 8, s));
+        EX_HIP(hipMemsetAsync(ex->d_counts, 0, (size_t)2 * P * 8, s));
     }
-    // 2. one message per peer: (count, watermark, columns); all-to-all, then one host wait
-    const int64_t cols_mask = (d_value ? 1 : 0) | (d_key_hash ? 2 : 0);
-    EX_HIP(launch_exchange_message(ex->d_counts, P, wm, cols_mask, ex->d_msg, s));
+    // 2. one message per peer: (records, watermark, columns, packed records); all-to-all,
+    // then one host wait
+    const int64_t cols_mask = (d_value ? 1 : 0) | (d_key_hash ? 2 : 0) | (packed ? 4 : 0);
+    EX_HIP(launch_exchange_message(ex->d_counts, P, wm, cols_mask, packed ? 1 : 0, ex->d_msg, s));
     EX_NCCL(ncclAllToAll(ex->d_msg, ex->d_msg + M * P, M, ncclInt64, ex->comm, s));
     EX_HIP(hipMemcpyAsync(ex->h_msg, ex->d_msg, (size_t)2 * M * P * 8, hipMemcpyDeviceToHost, s));
     EX_HIP(hipStreamSynchronize(s));
@@ -210,12 +298,20 @@ int gw_exchange_batch(gw_exchange* ex, int64_t n, const int64_t* d_key, const in
     std::vector<int64_t>& sc = ex->plan[1];
     std::vector<int64_t>& ro = ex->plan[2];
     std::vector<int64_t>& rc = ex->plan[3];
-    int64_t total = 0, wmin = wm;
+    std::vector<int64_t>& sp = ex->pplan[0];
+    std::vector<int64_t>& rwo = ex->pplan[1];
+    std::vector<int64_t>& rpo = ex->pplan[2];
+    std::vector<int64_t>& rp = ex->pplan[3];
+    int64_t total = 0, wmin = wm, tw = 0, tp = 0;
     // every rank sees every rank's mask: all of them fail here together, before any send
     if (gw_exchange_plan(P, sm, rm, cols_mask, wm, so.data(), sc.data(), ro.data(), rc.data(), &total, &wmin))
-        return ex_fail(ex, GW_E_INVALID, "gw_exchange_batch: ranks pass different columns");
+        return ex_fail(ex, GW_E_INVALID, "gw_exchange_batch: ranks pass different columns or packing");
+    if (gw_exchange_plan_packed(P, sm, rm, sp.data(), rwo.data(), rpo.data(), rp.data(), &tw, &tp))
+        return ex_fail(ex, GW_E_INVALID, "gw_exchange_batch: bad packed counts");
     ex->last_send = sc;
     ex->last_recv = rc;
+    ex->last_packed = tp;
+    ex->last_wm = wmin;  // the next batch's base pane
     // 3. this turn's receive set: free once the ingest two batches ago has read it
     const int u = ex->turn;
     ex->turn ^= 1;
@@ -227,18 +323,23 @@ int gw_exchange_batch(gw_exchange* ex, int64_t n, const int64_t* d_key, const in
         EX_HIP(hipStreamSynchronize(s));
         hipFree(ex->recv[u]);
         hipFree(ex->recv_hash[u]);
+        hipFree(ex->recv_packed[u]);
         ex->recv[u] = nullptr;
         ex->recv_hash[u] = nullptr;
+        ex->recv_packed[u] = nullptr;
         const int64_t c = total + total / 4 + 1024;
         EX_HIP(hipMalloc((void**)&ex->recv[u], (size_t)c * 3 * 8));
         EX_HIP(hipMalloc((void**)&ex->recv_hash[u], (size_t)c * 4));
         ex->recv_cap[u] = c;
     }
+    if (packed && !ex->recv_packed[u]) EX_HIP(hipMalloc((void**)&ex->recv_packed[u], (size_t)ex->recv_cap[u] * 8));
     int64_t* rk = ex->recv[u];
     int64_t* rt = rk + ex->recv_cap[u];
     int64_t* rv = rt + ex->recv_cap[u];
     int32_t* rh = ex->recv_hash[u];
-    // 4. columns: grouped point-to-point send / receive per peer (the group is always closed)
+    // 4. grouped point-to-point send / receive per peer (the group is always closed): per
+    // peer its packed words, then each column of its other records, which land behind the
+    // other peers' other records in rank order; the unpacked words follow them all
     struct Col { const void* src; void* dst; ncclDataType_t t; size_t w; };
     const Col cols[4] = {{pk, rk, ncclInt64, 8},
                          {pt, rt, ncclInt64, 8},
@@ -246,16 +347,23 @@ int gw_exchange_batch(gw_exchange* ex, int64_t n, const int64_t* d_key, const in
                          {d_key_hash ? ex->part_hash : nullptr, rh, ncclInt32, 4}};
     EX_NCCL(ncclGroupStart());
     ncclResult_t r = ncclSuccess;
+    for (int q = 0; q < P && r == ncclSuccess && packed; ++q) {
+        if (sp[q]) r = ncclSend(ex->part_packed + so[q], (size_t)sp[q], ncclUint64, q, ex->comm, s);
+        if (r == ncclSuccess && rp[q]) r = ncclRecv(ex->recv_packed[u] + rpo[q], (size_t)rp[q], ncclUint64, q, ex->comm, s);
+    }
     for (const Col& c : cols) {
         if (!c.src) continue;
         for (int q = 0; q < P && r == ncclSuccess; ++q) {
-            if (sc[q]) r = ncclSend((const char*)c.src + so[q] * c.w, (size_t)sc[q], c.t, q, ex->comm, s);
-            if (r == ncclSuccess && rc[q]) r = ncclRecv((char*)c.dst + ro[q] * c.w, (size_t)rc[q], c.t, q, ex->comm, s);
+            const int64_t ns = sc[q] - sp[q], nr = rc[q] - rp[q];
+            if (ns) r = ncclSend((const char*)c.src + (so[q] + sp[q]) * c.w, (size_t)ns, c.t, q, ex->comm, s);
+            if (r == ncclSuccess && nr) r = ncclRecv((char*)c.dst + rwo[q] * c.w, (size_t)nr, c.t, q, ex->comm, s);
         }
     }
     const ncclResult_t re = ncclGroupEnd();
     if (r != ncclSuccess) return ex_fail(ex, GW_E_DEVICE, std::string("ncclSend/ncclRecv: ") + ncclGetErrorString(r));
     if (re != ncclSuccess) return ex_fail(ex, GW_E_DEVICE, std::string("ncclGroupEnd: ") + ncclGetErrorString(re));
+    if (packed && tp > 0)
+        EX_HIP(launch_unpack(tp, ex->recv_packed[u], g, rk + tw, rt + tw, d_value ? rv + tw : nullptr, s));
     // 5. hand-off: the ingest of this set orders after the receives on handoff[u] (and makes
     // handoff[u] wait for its reads); the exchange that reuses the set waits for handoff[u]
     EX_HIP(hipEventRecord(ex->ev_recv[u], s));

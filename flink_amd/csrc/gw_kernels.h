@@ -346,10 +346,16 @@ int64_t partition_scratch_bytes(int64_t n, int32_t p);
 // [kg_lo, kg_hi] when check_range (out[1] must start at ~0)
 hipError_t launch_check_keys(int64_t n, const int64_t* key, const int32_t* key_hash, int32_t max_p, int32_t kg_lo,
                              int32_t kg_hi, int check_range, unsigned long long* out, hipStream_t s);
+// Stable partition by owner.  pack (enabled): 2p buckets -- 2q: q's packed words in
+// packed_out, 2q + 1: q's other records in the columns -- at positions of one numbering;
+// counts[2q], counts[2q + 1] their sizes.
 hipError_t launch_partition(int64_t n, const int64_t* key, const int32_t* key_hash, const int64_t* ts,
                             const int64_t* val, int32_t max_p, int32_t p, int64_t* key_out,
                             int64_t* ts_out, int64_t* val_out, int64_t* counts, void* scratch,
-                            hipStream_t s, int32_t* hash_out = nullptr);
+                            hipStream_t s, int32_t* hash_out = nullptr, const PackGeom* pack = nullptr,
+                            uint64_t* packed_out = nullptr);
+hipError_t launch_unpack(int64_t n, const uint64_t* w, const PackGeom& g, int64_t* key, int64_t* ts, int64_t* val,
+                         hipStream_t s);
 
 // Key -> Java hashCode of the keys a handle was fed with a key_hash column (String,
 // Integer, ... keys mapped to int64 ids by the caller).  The heap backend files a key's
@@ -367,9 +373,10 @@ hipError_t launch_khmap_insert(const KeyHashMap& m, int64_t n, const int64_t* ke
                                unsigned long long* out, hipStream_t s);
 // p[0..n) = v
 hipError_t launch_fill64(int64_t* p, int64_t n, int64_t v, hipStream_t s);
-// keyBy exchange message per peer q: msg[3q..3q+2] = (counts[q], wm, cols)
-hipError_t launch_exchange_message(const int64_t* counts, int32_t p, int64_t wm, int64_t cols, int64_t* msg,
-                                   hipStream_t s);
+// keyBy exchange message per peer q: msg[4q..4q+3] = (records, wm, cols, packed records);
+// packed: counts holds 2 buckets per peer (packed, other)
+hipError_t launch_exchange_message(const int64_t* counts, int32_t p, int64_t wm, int64_t cols, int packed,
+                                   int64_t* msg, hipStream_t s);
 // Every entry of `from` into the empty map `to`.
 hipError_t launch_khmap_rehash(const KeyHashMap& from, const KeyHashMap& to, hipStream_t s);
 

@@ -35,19 +35,31 @@ __global__ void __launch_bounds__(256) k_key_groups(int64_t n, const int64_t* ke
     }
 }
 
+// Destination bucket of record i: its owner, or (packing) 2 * owner + (does not fit).
+__device__ __forceinline__ int32_t dest_of(const int64_t* key, const int32_t* key_hash, const int64_t* ts,
+                                           const int64_t* val, int64_t i, int32_t max_p, int32_t p,
+                                           const PackGeom& g, uint64_t& w) {
+    const int32_t o = owner_of(key, key_hash, i, max_p, p);
+    if (!g.enabled) return o;
+    return 2 * o + (pack_word(g, key[i], ts[i], val != nullptr, val ? val[i] : 0, w) ? 0 : 1);
+}
+
 // pass 1: counts[block][dest]
 __global__ void __launch_bounds__(256) k_part_hist(int64_t n, const int64_t* key, const int32_t* key_hash,
-                                                   int32_t max_p, int32_t p, uint32_t* block_counts) {
+                                                   const int64_t* ts, const int64_t* val, int32_t max_p, int32_t p,
+                                                   PackGeom g, uint32_t* block_counts) {
     __shared__ uint32_t h[kPartMaxDest];
-    for (int d = threadIdx.x; d < p; d += blockDim.x) h[d] = 0;
+    const int32_t nd = g.enabled ? 2 * p : p;
+    for (int d = threadIdx.x; d < nd; d += blockDim.x) h[d] = 0;
     __syncthreads();
     const int64_t t0 = (int64_t)blockIdx.x * blockDim.x * kPartItems;
     for (int it = 0; it < kPartItems; ++it) {
         const int64_t i = t0 + (int64_t)it * blockDim.x + threadIdx.x;
-        if (i < n) atomicAdd(&h[owner_of(key, key_hash, i, max_p, p)], 1u);
+        uint64_t w;
+        if (i < n) atomicAdd(&h[dest_of(key, key_hash, ts, val, i, max_p, p, g, w)], 1u);
     }
     __syncthreads();
-    for (int d = threadIdx.x; d < p; d += blockDim.x) block_counts[(int64_t)d * gridDim.x + blockIdx.x] = h[d];
+    for (int d = threadIdx.x; d < nd; d += blockDim.x) block_counts[(int64_t)d * gridDim.x + blockIdx.x] = h[d];
 }
 
 // pass 2: exclusive scan over (dest-major, block-minor); totals per dest.
@@ -77,14 +89,18 @@ __global__ void __launch_bounds__(1024) k_part_scan(uint32_t* block_counts, int6
 }
 
 // pass 3: stable scatter.  Tile order = it-major then thread, i.e. global order.
+// Packing: bucket 2q holds q's packed words (packed_out), bucket 2q + 1 its other records
+// (key_out | ts_out | val_out), at positions of one shared numbering.
 __global__ void __launch_bounds__(256) k_part_scatter(int64_t n, const int64_t* key, const int32_t* key_hash,
                                                       const int64_t* ts, const int64_t* val, int32_t max_p,
-                                                      int32_t p, const int64_t* offsets, int64_t* key_out,
-                                                      int64_t* ts_out, int64_t* val_out, int32_t* hash_out) {
+                                                      int32_t p_owners, PackGeom g, const int64_t* offsets,
+                                                      int64_t* key_out, int64_t* ts_out, int64_t* val_out,
+                                                      int32_t* hash_out, uint64_t* packed_out) {
     __shared__ int64_t cursor[kPartMaxDest];
     __shared__ uint32_t wave_cnt[4][kPartMaxDest];
     const int lane = __lane_id();
     const int wave = threadIdx.x >> 6;
+    const int32_t p = g.enabled ? 2 * p_owners : p_owners;  // buckets
     for (int d = threadIdx.x; d < p; d += blockDim.x) cursor[d] = offsets[(int64_t)d * gridDim.x + blockIdx.x];
     const int64_t t0 = (int64_t)blockIdx.x * blockDim.x * kPartItems;
     for (int it = 0; it < kPartItems; ++it) {
@@ -92,7 +108,8 @@ __global__ void __launch_bounds__(256) k_part_scatter(int64_t n, const int64_t* 
         __syncthreads();
         const int64_t i = t0 + (int64_t)it * blockDim.x + threadIdx.x;
         const bool valid = i < n;
-        const int32_t d = valid ? owner_of(key, key_hash, i, max_p, p) : -1;
+        uint64_t w = 0;
+        const int32_t d = valid ? dest_of(key, key_hash, ts, val, i, max_p, p_owners, g, w) : -1;
         // peers: lanes of this wave with the same destination (8 ballots cover p <= 256)
         unsigned long long peers = __ballot(valid);
         for (int b = 0; b < 8; ++b) {
@@ -105,11 +122,15 @@ __global__ void __launch_bounds__(256) k_part_scatter(int64_t n, const int64_t* 
         __syncthreads();
         if (valid) {
             int64_t pos = cursor[d] + rank_in_wave;
-            for (int w = 0; w < wave; ++w) pos += wave_cnt[w][d];
-            key_out[pos] = key[i];
-            ts_out[pos] = ts[i];
-            if (val) val_out[pos] = val[i];
-            if (hash_out) hash_out[pos] = key_hash[i];
+            for (int q = 0; q < wave; ++q) pos += wave_cnt[q][d];
+            if (g.enabled && !(d & 1)) {
+                packed_out[pos] = w;
+            } else {
+                key_out[pos] = key[i];
+                ts_out[pos] = ts[i];
+                if (val) val_out[pos] = val[i];
+                if (hash_out) hash_out[pos] = key_hash[i];
+            }
         }
         __syncthreads();
         for (int dd = threadIdx.x; dd < p; dd += blockDim.x)
@@ -231,17 +252,19 @@ hipError_t launch_fill64(int64_t* p, int64_t n, int64_t v, hipStream_t s) {
 }
 
 __global__ void __launch_bounds__(256) k_exchange_message(const int64_t* counts, int32_t p, int64_t wm, int64_t cols,
-                                                          int64_t* msg) {
+                                                          int packed, int64_t* msg) {
     for (int q = threadIdx.x; q < p; q += blockDim.x) {
-        msg[3 * q] = counts[q];
-        msg[3 * q + 1] = wm;
-        msg[3 * q + 2] = cols;
+        const int64_t pk = packed ? counts[2 * q] : 0;
+        msg[4 * q] = packed ? pk + counts[2 * q + 1] : counts[q];
+        msg[4 * q + 1] = wm;
+        msg[4 * q + 2] = cols;
+        msg[4 * q + 3] = pk;
     }
 }
 
-hipError_t launch_exchange_message(const int64_t* counts, int32_t p, int64_t wm, int64_t cols, int64_t* msg,
-                                   hipStream_t s) {
-    hipLaunchKernelGGL(k_exchange_message, dim3(1), dim3(256), 0, s, counts, p, wm, cols, msg);
+hipError_t launch_exchange_message(const int64_t* counts, int32_t p, int64_t wm, int64_t cols, int packed,
+                                   int64_t* msg, hipStream_t s) {
+    hipLaunchKernelGGL(k_exchange_message, dim3(1), dim3(256), 0, s, counts, p, wm, cols, packed, msg);
     return hipGetLastError();
 }
 
@@ -283,15 +306,43 @@ int64_t partition_scratch_bytes(int64_t n, int32_t p) {
 
 hipError_t launch_partition(int64_t n, const int64_t* key, const int32_t* key_hash, const int64_t* ts,
                             const int64_t* val, int32_t max_p, int32_t p, int64_t* key_out, int64_t* ts_out,
-                            int64_t* val_out, int64_t* counts, void* scratch, hipStream_t s, int32_t* hash_out) {
-    if (p < 1 || p > kPartMaxDest) return hipErrorInvalidValue;
+                            int64_t* val_out, int64_t* counts, void* scratch, hipStream_t s, int32_t* hash_out,
+                            const PackGeom* pack, uint64_t* packed_out) {
+    PackGeom g{};
+    if (pack && pack->enabled) {
+        if (key_hash || !packed_out || pack->pane <= 0) return hipErrorInvalidValue;
+        g = *pack;
+    }
+    const int32_t nd = g.enabled ? 2 * p : p;
+    if (p < 1 || nd > kPartMaxDest) return hipErrorInvalidValue;
     const int64_t nb = part_blocks(n);
     uint32_t* bc = (uint32_t*)scratch;
-    int64_t* off = (int64_t*)(((uintptr_t)(bc + nb * p) + 15) & ~(uintptr_t)15);
-    hipLaunchKernelGGL(k_part_hist, dim3((unsigned)nb), dim3(256), 0, s, n, key, key_hash, max_p, p, bc);
-    hipLaunchKernelGGL(k_part_scan, dim3(1), dim3(1024), 0, s, bc, nb, p, off, counts);
-    hipLaunchKernelGGL(k_part_scatter, dim3((unsigned)nb), dim3(256), 0, s, n, key, key_hash, ts, val, max_p, p,
-                       off, key_out, ts_out, val_out, key_hash ? hash_out : nullptr);
+    int64_t* off = (int64_t*)(((uintptr_t)(bc + nb * nd) + 15) & ~(uintptr_t)15);
+    hipLaunchKernelGGL(k_part_hist, dim3((unsigned)nb), dim3(256), 0, s, n, key, key_hash, ts, val, max_p, p, g, bc);
+    hipLaunchKernelGGL(k_part_scan, dim3(1), dim3(1024), 0, s, bc, nb, nd, off, counts);
+    hipLaunchKernelGGL(k_part_scatter, dim3((unsigned)nb), dim3(256), 0, s, n, key, key_hash, ts, val, max_p, p, g,
+                       off, key_out, ts_out, val_out, key_hash ? hash_out : nullptr, packed_out);
+    return hipGetLastError();
+}
+
+// Packed words back to (key, ts, value): ts = the start of the word's pane.
+__global__ void __launch_bounds__(256) k_unpack(int64_t n, const uint64_t* w, PackGeom g, int64_t* key, int64_t* ts,
+                                                int64_t* val) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        int64_t k, t, v;
+        unpack_word(g, w[i], k, t, v);
+        key[i] = k;
+        ts[i] = t;
+        if (val) val[i] = v;
+    }
+}
+
+hipError_t launch_unpack(int64_t n, const uint64_t* w, const PackGeom& g, int64_t* key, int64_t* ts, int64_t* val,
+                         hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    int64_t b = (n + 255) / 256;
+    if (b > 4096) b = 4096;
+    hipLaunchKernelGGL(k_unpack, dim3((unsigned)b), dim3(256), 0, s, n, w, g, key, ts, val);
     return hipGetLastError();
 }
 

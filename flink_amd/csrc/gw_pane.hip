@@ -297,7 +297,7 @@ __device__ __forceinline__ void lds_cell_add(long long* a0, long long* a1, int64
 constexpr int kPreKeys = 1024;
 
 template <int AGG>
-__global__ void __launch_bounds__(256) k_ingest_preagg(IngestArgs a) {
+__global__ void __launch_bounds__(256) k_ingest_preagg(IngestArgs a, int exp) {
     constexpr bool AV = AGG == GW_AVG_I64 || AGG == GW_AVG_F64;
     __shared__ long long s_key[kPreKeys];
     __shared__ long long s_g[kPreKeys + 1];  // + the sentinel key's slot (t.cap)
@@ -342,7 +342,7 @@ __global__ void __launch_bounds__(256) k_ingest_preagg(IngestArgs a) {
         for (int it = 0; it < kPreaggItems; ++it) {
             lk[it] = -1;
             if (state[it] != REC_RING) continue;
-            if (key[it] == kEmptyKey) { lk[it] = kPreKeys; continue; }
+            if (key[it] == kEmptyKey || (exp & 1)) { lk[it] = kPreKeys; continue; }
             uint32_t h = (uint32_t)slot_hash(key[it]) & (kPreKeys - 1);
             for (int p = 0; p < 16; ++p) {
                 long long cur = s_key[h];
@@ -387,7 +387,9 @@ __global__ void __launch_bounds__(256) k_ingest_preagg(IngestArgs a) {
                 } else {
                     occ |= 1ull << pos[it];
                     bool done = false;
-                    if (lk[it] >= 0) {
+                    if (exp & 2) {
+                        done = true;
+                    } else if (lk[it] >= 0) {
                         const uint32_t cell = (uint32_t)lk[it] * R + pos[it];
                         uint32_t h = (cell * 0x9E3779B1u) >> (32 - 11);  // kLdsCells = 2^11
                         for (int p = 0; p < 32 && !done; ++p) {
@@ -2789,8 +2791,10 @@ hipError_t launch_ingest(const IngestArgs& a, int path, int unroll, hipStream_t 
             (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
             cus = std::max(cus, 1);
         }
-        const int g = (int)std::max<int64_t>(1, std::min<int64_t>(2 * cus, (a.n + 2047) / 2048));
-#define L(A) hipLaunchKernelGGL(k_ingest_preagg<A>, dim3(g), dim3(256), 0, s, a)
+        static const int bpc = getenv("GW_PREAGG_BPC") ? std::max(1, atoi(getenv("GW_PREAGG_BPC"))) : 2;
+        const int g = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)bpc * cus, (a.n + 2047) / 2048));
+        static const int exp = getenv("GW_PREAGG_EXP") ? atoi(getenv("GW_PREAGG_EXP")) : 0;  // measurement only
+#define L(A) hipLaunchKernelGGL(k_ingest_preagg<A>, dim3(g), dim3(256), 0, s, a, exp)
         GW_AGG_SWITCH(a.t.agg, L);
 #undef L
     } else if (unroll == 4) {

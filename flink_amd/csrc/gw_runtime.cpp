@@ -4601,6 +4601,57 @@ int gw_key_groups_device(int64_t n, const int64_t* d_key, const int32_t* d_key_h
 
 int64_t gw_partition_scratch_bytes(int64_t n, int32_t p) { return partition_scratch_bytes(n, p); }
 
+int gw_pack_records(int64_t n, const int64_t* key, const int64_t* ts, const int64_t* value, const gw_pack_geom* g,
+                    uint64_t* words, uint8_t* fits) {
+    if (n < 0 || !g || !g->enabled || g->pane <= 0 || (n > 0 && (!key || !ts || !words || !fits))) return GW_E_INVALID;
+    for (int64_t i = 0; i < n; ++i) {
+        uint64_t w = 0;
+        fits[i] = pack_word(*g, key[i], ts[i], value != nullptr, value ? value[i] : 0, w) ? 1 : 0;
+        words[i] = fits[i] ? w : 0;
+    }
+    return GW_OK;
+}
+
+int gw_unpack_records(int64_t n, const uint64_t* words, const gw_pack_geom* g, int64_t* key, int64_t* ts,
+                      int64_t* value) {
+    if (n < 0 || !g || !g->enabled || g->pane <= 0 || (n > 0 && (!words || !key || !ts))) return GW_E_INVALID;
+    for (int64_t i = 0; i < n; ++i) {
+        int64_t k, t, v;
+        unpack_word(*g, words[i], k, t, v);
+        key[i] = k;
+        ts[i] = t;
+        if (value) value[i] = v;
+    }
+    return GW_OK;
+}
+
+int gw_partition_packed_device(int64_t n, const int64_t* d_key, const int64_t* d_ts, const int64_t* d_value,
+                               int32_t max_p, int32_t p, const gw_pack_geom* g, uint64_t* d_packed_out,
+                               int64_t* d_key_out, int64_t* d_ts_out, int64_t* d_value_out, int64_t* d_counts,
+                               void* d_scratch, void* stream) {
+    if (n < 0 || max_p <= 0 || p <= 0 || p > max_p || p > 128 || !g || !g->enabled || g->pane <= 0 || !d_counts)
+        return GW_E_INVALID;
+    hipStream_t s = (hipStream_t)stream;
+    if (n == 0) {
+        hipError_t e = hipMemsetAsync(d_counts, 0, (size_t)2 * p * 8, s);
+        return e == hipSuccess ? GW_OK : GW_E_DEVICE;
+    }
+    if (!d_key || !d_ts || !d_packed_out || !d_key_out || !d_ts_out || (d_value && !d_value_out) || !d_scratch)
+        return GW_E_INVALID;
+    hipError_t e = launch_partition(n, d_key, nullptr, d_ts, d_value, max_p, p, d_key_out, d_ts_out, d_value_out,
+                                    d_counts, d_scratch, s, nullptr, g, d_packed_out);
+    if (e != hipSuccess) { g_create_error = hipGetErrorString(e); return GW_E_DEVICE; }
+    return GW_OK;
+}
+
+int gw_unpack_device(int64_t n, const uint64_t* d_words, const gw_pack_geom* g, int64_t* d_key, int64_t* d_ts,
+                     int64_t* d_value, void* stream) {
+    if (n < 0 || !g || !g->enabled || g->pane <= 0 || (n > 0 && (!d_words || !d_key || !d_ts))) return GW_E_INVALID;
+    hipError_t e = launch_unpack(n, d_words, *g, d_key, d_ts, d_value, (hipStream_t)stream);
+    if (e != hipSuccess) { g_create_error = hipGetErrorString(e); return GW_E_DEVICE; }
+    return GW_OK;
+}
+
 int gw_partition_device(int64_t n, const int64_t* d_key, const int32_t* d_key_hash, const int64_t* d_ts,
                         const void* d_value, int32_t max_p, int32_t p, int64_t* d_key_out, int64_t* d_ts_out,
                         void* d_value_out, int64_t* d_counts, void* d_scratch, void* stream) {

@@ -20,6 +20,31 @@ import torch.distributed as dist
 from . import _native as N
 
 
+def owners_np(keys, max_parallelism: int, parallelism: int):
+    """Owner subtask of int64 keys on the host (vectorised KeyGroupRangeAssignment.
+    assignKeyToParallelOperator: Long.hashCode, MathUtils.murmurHash, key group * p / maxP;
+    KeyGroupRangeAssignment.java:63-77,124-127, MathUtils.java:137-155) -- the host partition
+    of KeyByExchange.exchange_packed; the device partition is gw_keygroups.hip."""
+    import numpy as np
+    u = np.ascontiguousarray(keys, np.int64).view(np.uint64)
+    c = (u ^ (u >> np.uint64(32))).astype(np.uint32)
+    with np.errstate(over="ignore"):
+        c = (c * np.uint32(0xcc9e2d51)).astype(np.uint32)
+        c = ((c << np.uint32(15)) | (c >> np.uint32(17))).astype(np.uint32)
+        c = (c * np.uint32(0x1b873593)).astype(np.uint32)
+        c = ((c << np.uint32(13)) | (c >> np.uint32(19))).astype(np.uint32)
+        c = (c * np.uint32(5) + np.uint32(0xe6546b64)).astype(np.uint32)
+        c ^= np.uint32(4)
+        c ^= c >> np.uint32(16)
+        c = (c * np.uint32(0x85ebca6b)).astype(np.uint32)
+        c ^= c >> np.uint32(13)
+        c = (c * np.uint32(0xc2b2ae35)).astype(np.uint32)
+        c ^= c >> np.uint32(16)
+    r = c.view(np.int32).astype(np.int64)
+    r = np.where(r >= 0, r, np.where(r == -(1 << 31), 0, -r))
+    return (r % max_parallelism) * parallelism // max_parallelism
+
+
 class KeyByExchange:
     def __init__(self, parallelism: int, rank: int, max_parallelism: int = 128, group=None,
                  device: Optional[torch.device] = None):
@@ -108,6 +133,96 @@ class KeyByExchange:
         (rk, rt, rv), _ = self.exchange_partitioned([pk, pt, pv], counts)
         return rk, rt, rv
 
+    # ---------------------------------------------------------------- packed exchange
+    def exchange_packed(self, keys: torch.Tensor, ts: torch.Tensor, vals: Optional[torch.Tensor], geom, wm: int):
+        """The packed protocol of gw_exchange_batch (include/gpuwin.h gw_pack_geom) over
+        torch.distributed point-to-point transfers: records that fit travel as 8-byte words,
+        the rest as (key, ts, value).  geom: N.pack_geom(size, slide, offset, watermark before
+        the batch) -- the same on every rank -- or None (nothing packs).  The partition runs on
+        the device for GPU tensors (gw_partition_packed_device), on the host otherwise
+        (gw_pack_records + a stable sort by (owner, does not fit)); the receiver unpacks the
+        words behind the other records, as gw_exchange_batch does.  Returns host numpy
+        (keys, ts, values, packed records received, minimum watermark over the ranks)."""
+        import numpy as np
+        M, P = N.MSG_WORDS, self.p
+        n = keys.numel()
+        has_v = vals is not None
+        ptr = lambda t: t.data_ptr() if t is not None else None
+        if geom is not None and keys.is_cuda:
+            dev = keys.device
+            need = N.lib().gw_partition_scratch_bytes(max(n, 1), 2 * P)
+            if self._scratch is None or self._scratch.numel() < need:
+                self._scratch = torch.empty(need, dtype=torch.uint8, device=dev)
+            words = torch.empty(n, dtype=torch.int64, device=dev)
+            pk, pt = torch.empty_like(keys), torch.empty_like(ts)
+            pv = torch.empty_like(vals) if has_v else None
+            counts = torch.empty(2 * P, dtype=torch.int64, device=dev)
+            N.check(N.lib().gw_partition_packed_device(n, ptr(keys), ptr(ts), ptr(vals), self.maxp, P, geom,
+                                                       ptr(words), ptr(pk), ptr(pt), ptr(pv), ptr(counts),
+                                                       ptr(self._scratch), torch.cuda.current_stream(dev).cuda_stream))
+            torch.cuda.synchronize(dev)
+            words, pk, pt = words.cpu().numpy().view(np.uint64), pk.cpu().numpy(), pt.cpu().numpy()
+            pv = pv.cpu().numpy() if has_v else None
+            c2 = counts.cpu().numpy().reshape(P, 2)
+        else:
+            k, t = keys.cpu().numpy(), ts.cpu().numpy()
+            v = vals.cpu().numpy() if has_v else None
+            own = owners_np(k, self.maxp, P)
+            if geom is not None:
+                w, fits = N.pack_records(k, t, v, geom)
+            else:
+                w, fits = np.zeros(n, np.uint64), np.zeros(n, bool)
+            bucket = 2 * own + (~fits).astype(np.int64)
+            order = np.argsort(bucket, kind="stable")
+            words, pk, pt = w[order], k[order], t[order]
+            pv = v[order] if has_v else None
+            c2 = np.bincount(bucket, minlength=2 * P).reshape(P, 2)
+        mask = (1 if has_v else 0) | (4 if geom is not None else 0)
+        msg = torch.zeros(P, M, dtype=torch.int64)
+        msg[:, 0] = torch.from_numpy(c2.sum(1))
+        msg[:, 1] = int(wm)
+        msg[:, 2] = mask
+        msg[:, 3] = torch.from_numpy(c2[:, 0].copy())
+        rmsg = torch.empty_like(msg)
+        dist.all_to_all_single(rmsg.view(-1), msg.view(-1), group=self.group)
+        sm, rm = msg.view(-1).numpy(), rmsg.view(-1).numpy()
+        (so, sc, ro, rc), total, wmin = N.exchange_plan(sm, rm, mask, int(wm))
+        (sp, rwo, rpo, rp), tw, tp = N.exchange_plan_packed(sm, rm)
+        self.last_send_counts = sc.tolist()
+
+        def move(src, dst, s_off, s_cnt, r_off, r_cnt):
+            reqs = []
+            for q in range(P):
+                if q == self.rank:
+                    dst[r_off[q]:r_off[q] + r_cnt[q]] = src[s_off[q]:s_off[q] + s_cnt[q]]
+                    continue
+                if s_cnt[q]:
+                    reqs.append(dist.isend(torch.from_numpy(np.ascontiguousarray(src[s_off[q]:s_off[q] + s_cnt[q]])),
+                                           q, group=self.group))
+                if r_cnt[q]:
+                    reqs.append(dist.irecv(torch.from_numpy(dst[r_off[q]:r_off[q] + r_cnt[q]]), q, group=self.group))
+            for x in reqs:
+                x.wait()
+
+        rw = np.zeros(tp, np.int64)
+        move(words.view(np.int64), rw, so, sp, rpo, rp)  # words as int64: gloo has no uint64
+        other_s = so + sp
+        other_n_s, other_n_r = sc - sp, rc - rp
+        out = []
+        for col in (pk, pt, pv):
+            if col is None:
+                out.append(None)
+                continue
+            r = np.zeros(total, np.int64)
+            move(col, r, other_s, other_n_s, rwo, other_n_r)
+            out.append(r)
+        if tp:
+            kk, tt, vv = N.unpack_records(rw.view(np.uint64), geom, has_v)
+            out[0][tw:], out[1][tw:] = kk, tt
+            if has_v:
+                out[2][tw:] = vv
+        return out[0], out[1], out[2], tp, wmin
+
     # ---------------------------------------------------------------- watermark
     def combine_watermark(self, wm: int) -> int:
         """Minimum over all ranks (StatusWatermarkValve), on a host (gloo) group."""
@@ -182,6 +297,15 @@ class NativeKeyByExchange:
                                               ctypes.byref(ot), ctypes.byref(ov), ctypes.byref(wm_out),
                                               ctypes.byref(ist), s))
         return n_out.value, ok.value, ot.value, ov.value, oh.value, wm_out.value, ist.value
+
+    def enable_packing(self, size: int, slide: int, offset: int = 0, with_values: bool = True):
+        """gw_exchange_enable_packing: later batches ship the records that fit as 8-byte words."""
+        self._check(N.lib().gw_exchange_enable_packing(self._h, int(size), int(slide), int(offset),
+                                                       1 if with_values else 0))
+
+    def last_packed(self) -> int:
+        """Records this rank received packed in the last batch."""
+        return int(N.lib().gw_exchange_last_packed(self._h))
 
     def counts(self):
         """(send, receive) record counts per peer of the last batch."""

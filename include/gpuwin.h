@@ -425,6 +425,44 @@ int  gw_partition_device(int64_t n, const int64_t* d_key, const int32_t* d_key_h
                          int64_t* d_key_out, int64_t* d_ts_out, void* d_value_out,
                          int64_t* d_counts, void* d_scratch, void* stream);
 
+/* Packed exchange records: one 8-byte word per record instead of 24 B of key, ts and value
+ *   lo32 = key, hi32 = value << 4 | d        (d = pane - base_pane, 0 <= d < 16)
+ * for records whose key is in [0, 2^32), whose value (if the batch has values) is in
+ * [-2^27, 2^27), and whose pane floor((ts - offset) / pane) lies in [base_pane, base_pane + 16);
+ * the others travel as (key, ts, value).  Unpacked, a record's timestamp is its pane's start,
+ * which changes no window decision of a tumbling / sliding assigner with size >= slide and
+ * pane = gcd(size, slide) (assignWindows, isWindowLate and the cleanup time depend on the pane
+ * alone).  Not for sessions, size < slide, the late side output, first-element / minBy
+ * handles or floating values: those need the record's own timestamp or value.
+ * gw_pack_geom_init: pane = gcd(size, slide) and base_pane = the pane of `watermark` (the
+ * operator's watermark before the batch: records of earlier panes travel unpacked);
+ * GW_E_UNSUPPORTED when size < slide or watermark = Long.MIN_VALUE.
+ * gw_pack_records / gw_unpack_records: the same packing on the host (fits[i] = 0: record i
+ * does not pack). */
+typedef struct gw_pack_geom {
+    int64_t pane;
+    int64_t offset;
+    int64_t base_pane;
+    int32_t enabled;
+    int32_t pad;
+} gw_pack_geom;
+int  gw_pack_geom_init(gw_pack_geom* g, int64_t size, int64_t slide, int64_t offset, int64_t watermark);
+int  gw_pack_records(int64_t n, const int64_t* key, const int64_t* ts, const int64_t* value, const gw_pack_geom* g,
+                     uint64_t* words, uint8_t* fits);
+int  gw_unpack_records(int64_t n, const uint64_t* words, const gw_pack_geom* g, int64_t* key, int64_t* ts,
+                       int64_t* value);
+/* Device: stable partition by owner with packing (g->enabled): counts[2q] packed words of
+ * subtask q (in d_packed_out), counts[2q + 1] its other records (in the columns), buckets laid
+ * out q-major (q's packed words, then its other records, then q + 1's ...) at positions of one
+ * numbering into both outputs.  parallelism <= 128.  d_scratch: gw_partition_scratch_bytes(n,
+ * 2 * parallelism).  gw_unpack_device: n words back to columns. */
+int  gw_partition_packed_device(int64_t n, const int64_t* d_key, const int64_t* d_ts, const int64_t* d_value,
+                                int32_t max_parallelism, int32_t parallelism, const gw_pack_geom* g,
+                                uint64_t* d_packed_out, int64_t* d_key_out, int64_t* d_ts_out, int64_t* d_value_out,
+                                int64_t* d_counts, void* d_scratch, void* stream);
+int  gw_unpack_device(int64_t n, const uint64_t* d_words, const gw_pack_geom* g, int64_t* d_key, int64_t* d_ts,
+                      int64_t* d_value, void* stream);
+
 /* ---- keyBy exchange over RCCL (one process per GPU) ------------------------
  * Replaces the network shuffle behind KeyGroupStreamPartitioner.selectChannel
  * (flink-runtime/.../streaming/runtime/partitioner/KeyGroupStreamPartitioner.java:55-64)
@@ -465,19 +503,36 @@ int  gw_exchange_batch(gw_exchange* ex, int64_t n, const int64_t* d_key, const i
                        const int64_t** d_key_out, const int32_t** d_key_hash_out, const int64_t** d_ts_out,
                        const int64_t** d_value_out, int64_t* wm_out, void** ingest_stream, void* stream);
 int  gw_exchange_counts(const gw_exchange* ex, int64_t* send, int64_t* recv);
+/* Packing (gw_pack_geom above) for the following batches of a tumbling / sliding operator
+ * (size >= slide) without the late side output: from the second batch on, the records that
+ * fit travel as 8-byte words (base pane: the previous batch's combined watermark) and arrive
+ * unpacked, behind the records that did not fit; per key the arrival order then differs, so
+ * only for integer aggregates (with_values: the value column is an integer sum / min / max /
+ * count operand).  Every rank must enable it alike (else GW_E_INVALID on every rank at the
+ * next batch).  gw_exchange_last_packed: records this rank received packed in the last batch. */
+int  gw_exchange_enable_packing(gw_exchange* ex, int64_t size, int64_t slide, int64_t offset, int32_t with_values);
+int64_t gw_exchange_last_packed(const gw_exchange* ex);
 int  gw_exchange_min_watermark(gw_exchange* ex, int64_t wm, int64_t* out, void* stream);
 const char* gw_exchange_last_error(const gw_exchange* ex);
 /* The per-peer plan gw_exchange_batch runs after its count all-to-all, as a host function
  * (no device, no communicator): from the messages this rank sent and received --
- * msg[3q .. 3q+2] = (records, watermark, column mask) for peer q -- the offsets and counts
- * of every send and receive (send_off[q]: the first record for q in the rank's
- * owner-partitioned columns; recv_off[q]: where q's records land in the receive columns,
- * which hold the peers' records in rank order, as all_to_all_single lays them out), the
- * total received and the minimum watermark over the ranks (StatusWatermarkValve).
- * GW_E_INVALID when a peer's column mask differs from this rank's. */
+ * msg[4q .. 4q+3] = (records, watermark, column mask, packed records) for peer q -- the
+ * offsets and counts of every send and receive (send_off[q]: the first record for q in the
+ * rank's owner-partitioned numbering; recv_off[q]: where q's records land when nothing is
+ * packed: the receive columns hold the peers' records in rank order, as all_to_all_single
+ * lays them out), the total received and the minimum watermark over the ranks
+ * (StatusWatermarkValve).  GW_E_INVALID when a peer's column mask (value column, key hashes,
+ * packing) differs from this rank's.
+ * gw_exchange_plan_packed: the packed split -- send_packed[q] of q's records are words (at
+ * send_off[q]), the rest follow them; q's unpacked-in-transit records land at
+ * recv_other_off[q] of the receive columns, its words at recv_packed_off[q] of the word
+ * buffer (recv_packed[q] of them), and are unpacked to positions total_other + recv_packed_off[q]. */
 int  gw_exchange_plan(int32_t nranks, const int64_t* sent_msg, const int64_t* recv_msg, int64_t cols_mask,
                       int64_t wm, int64_t* send_off, int64_t* send_cnt, int64_t* recv_off, int64_t* recv_cnt,
                       int64_t* total, int64_t* wm_min);
+int  gw_exchange_plan_packed(int32_t nranks, const int64_t* sent_msg, const int64_t* recv_msg, int64_t* send_packed,
+                             int64_t* recv_other_off, int64_t* recv_packed_off, int64_t* recv_packed,
+                             int64_t* total_other, int64_t* total_packed);
 
 #ifdef __cplusplus
 }

@@ -6,7 +6,7 @@ export TMPDIR=/tmp
 [ -n "${SKIP_SORTB:-}" ] || CFGS="0 2" bash scripts/r5/sortbench.sh
 for v in ${VARS:-default}; do
   tag=${v//=/_}; tag=${tag//,/_}
-  env $(echo $v | tr ',' ' ' | sed 's/default//') timeout -k 10 300 python -u scripts/configs_bench.py --only sessions --steps 40 --no-cpu-baseline > gpurun_out/r5/sab/$tag.jsonl 2> gpurun_out/r5/sab/$tag.err || { tail -20 gpurun_out/r5/sab/$tag.err; exit 4; }
+  env $(echo $v | tr ',' ' ' | sed 's/default//') timeout -k 10 300 python -u scripts/configs_bench.py --only ${ONLY:-sessions} --steps 40 --no-cpu-baseline > gpurun_out/r5/sab/$tag.jsonl 2> gpurun_out/r5/sab/$tag.err || { tail -20 gpurun_out/r5/sab/$tag.err; exit 4; }
   echo "$tag: $(python scripts/r5/jf.py gpurun_out/r5/sab/$tag.jsonl value ms_per_step roofline.launch_ms.ingest)"
 done
 [ -n "${TESTS:-}" ] || exit 0

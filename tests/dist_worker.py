@@ -42,11 +42,11 @@ def owners(keys, maxp, p):
 
 
 def plan_exchange(world, rank, cols, counts, wm):
-    """One batch through gw_exchange_plan: the (count, watermark, column mask) message per peer
+    """One batch through gw_exchange_plan: the (count, watermark, column mask, 0 packed) message per peer
     goes through one all-to-all, the plan gives every send / receive offset, the columns move
     by point-to-point sends and receives."""
     from flink_amd import _native as N
-    msg = torch.zeros(world, 3, dtype=torch.int64)
+    msg = torch.zeros(world, N.MSG_WORDS, dtype=torch.int64)
     msg[:, 0] = counts
     msg[:, 1] = wm
     msg[:, 2] = 1
@@ -112,6 +112,52 @@ def worker(rank, world, port, cfg_kw, seed, result_q):
     mine = list(zip(k.tolist(), s.tolist(), e.tolist(), r.tolist()))
     gathered = [None] * world
     dist.all_gather_object(gathered, (mine, bad_owner, op.late_dropped))
+    if rank == 0:
+        result_q.put(gathered)
+    dist.destroy_process_group()
+
+
+def worker_packed(rank, world, port, cfg_kw, seed, result_q):
+    """The same job through the packed protocol (KeyByExchange.exchange_packed on the host:
+    gw_pack_records, gw_exchange_plan / gw_exchange_plan_packed, point-to-point transfers,
+    gw_unpack_records); the base pane of a batch is the watermark the ranks combined after the
+    previous one."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from flink_amd import _native as N
+    from flink_amd.exchange import KeyByExchange
+    from oracle import oracle as O
+    from tests.gpu_helpers import random_stream
+
+    keys, ts, vals, batches = random_stream(seed=seed, n=24000, num_keys=500, n_batches=12, ts_step=1,
+                                            agg=cfg_kw["agg"])
+    ex = KeyByExchange(world, rank, max_parallelism=128)
+    op = O.OracleOperator(O.make_config(**cfg_kw, parallelism=world, operator_index=rank))
+    size, slide = cfg_kw["size"], cfg_kw.get("slide", cfg_kw["size"])
+    rows, bad_owner, packed, sent = [], 0, 0, 0
+    last = -(1 << 63)
+    for lo, hi, wm in batches:
+        idx = np.arange(lo, hi)
+        idx = idx[idx % world == rank]
+        g = N.pack_geom(size, slide, cfg_kw.get("offset", 0), last)
+        rk, rt, rv, tp, wmin = ex.exchange_packed(torch.from_numpy(keys[idx]), torch.from_numpy(ts[idx]),
+                                                  torch.from_numpy(vals[idx]), g, wm)
+        assert wmin == ex.combine_watermark(wm)
+        last = wmin
+        packed += tp
+        sent += rk.size
+        bad_owner += int((owners(rk, 128, world) != rank).sum())
+        op.process_batch(rk, rt, rv)
+        op.process_watermark(wmin)
+        rows.append(op.drain())
+    op.process_watermark(ex.combine_watermark((1 << 63) - 1))
+    rows.append(op.drain())
+    k = np.concatenate([r[0] for r in rows]); s = np.concatenate([r[1] for r in rows])
+    e = np.concatenate([r[2] for r in rows]); r = np.concatenate([r[3] for r in rows])
+    mine = list(zip(k.tolist(), s.tolist(), e.tolist(), r.tolist()))
+    gathered = [None] * world
+    dist.all_gather_object(gathered, (mine, bad_owner, op.late_dropped, packed, sent))
     if rank == 0:
         result_q.put(gathered)
     dist.destroy_process_group()

@@ -13,11 +13,15 @@ import pytest
 from flink_amd import _native as N
 
 
-def messages(counts, wms, masks):
-    """msg[r] (sent by r) and rmsg[r] (received by r): (records, watermark, mask) per peer."""
+def messages(counts, wms, masks, packed=None):
+    """msg[r] (sent by r) and rmsg[r] (received by r): (records, watermark, mask, packed
+    records) per peer."""
     P = len(wms)
-    sent = [np.array([[counts[r][q], wms[r], masks[r]] for q in range(P)], np.int64).ravel() for r in range(P)]
-    recv = [np.array([[counts[q][r], wms[q], masks[q]] for q in range(P)], np.int64).ravel() for r in range(P)]
+    pk = np.zeros_like(counts) if packed is None else packed
+    sent = [np.array([[counts[r][q], wms[r], masks[r], pk[r][q]] for q in range(P)], np.int64).ravel()
+            for r in range(P)]
+    recv = [np.array([[counts[q][r], wms[q], masks[q], pk[q][r]] for q in range(P)], np.int64).ravel()
+            for r in range(P)]
     return sent, recv
 
 
@@ -66,3 +70,34 @@ def test_negative_counts_are_invalid():
     sent, recv = messages(np.array([[1, -2], [3, 4]]), np.zeros(2, np.int64), [1, 1])
     with pytest.raises(N.GpuWinError):
         N.exchange_plan(sent[0], recv[0], 1, 0)
+
+
+@pytest.mark.parametrize("P", [2, 3, 4, 8])
+def test_packed_plans_agree_across_ranks(P):
+    """gw_exchange_plan_packed: q's packed words go first in its send range, its other records
+    follow; on the receiver the other records of all peers come first (rank order), then the
+    peers' words in rank order -- what r receives from q is what q sent to r."""
+    rng = np.random.default_rng(100 + P)
+    counts = rng.integers(0, 600, (P, P))
+    packed = (counts * rng.random((P, P))).astype(np.int64)
+    packed[rng.random((P, P)) < 0.2] = 0
+    sent, recv = messages(counts, np.zeros(P, np.int64), [5] * P, packed)
+    for r in range(P):
+        (so, sc, _, rc), total, _ = N.exchange_plan(sent[r], recv[r], 5, 0)
+        (sp, rwo, rpo, rp), tw, tp = N.exchange_plan_packed(sent[r], recv[r])
+        assert list(sp) == list(packed[r]) and list(rp) == list(packed[:, r])
+        assert tw + tp == total and tp == packed[:, r].sum()
+        assert list(rwo) == list(np.concatenate([[0], np.cumsum(counts[:, r] - packed[:, r])[:-1]]))
+        assert list(rpo) == list(np.concatenate([[0], np.cumsum(packed[:, r])[:-1]]))
+        for q in range(P):  # the sender's view of the same transfer
+            (_, qsc, _, _), _, _ = N.exchange_plan(sent[q], recv[q], 5, 0)
+            (qsp, _, _, _), _, _ = N.exchange_plan_packed(sent[q], recv[q])
+            assert qsp[r] == rp[q] and qsc[r] - qsp[r] == rc[q] - rp[q]
+
+
+def test_packed_count_above_records_is_invalid():
+    sent, recv = messages(np.array([[4, 4], [4, 4]]), np.zeros(2, np.int64), [5, 5], np.array([[5, 0], [0, 0]]))
+    with pytest.raises(N.GpuWinError):
+        N.exchange_plan(sent[0], recv[0], 5, 0)
+    with pytest.raises(N.GpuWinError):
+        N.exchange_plan_packed(sent[0], recv[0])

@@ -69,3 +69,48 @@ def test_two_ranks_on_the_gpu_equal_single_operator(oracle_lib, cfg, flags):
         if rows:
             ks = np.array([r[0] for r in rows], np.int64)
             assert (owners(ks, 128, world) == rank).all()
+
+
+PACKED_CASES = [
+    (dict(assigner="sliding", size=1000, slide=250, agg="sum_i64"), 0),
+    (dict(assigner="tumbling", size=700, slide=700, agg="max_i64", lateness=300), N.FLAG_FORCE_REGION),
+]
+
+
+@pytest.mark.parametrize("cfg,flags", PACKED_CASES, ids=["sliding_sum", "tumbling_max_region_lateness"])
+def test_two_ranks_packed_exchange_equal_single_operator(oracle_lib, cfg, flags):
+    """The packed protocol (device partition with packing, words + other records over gloo,
+    unpack on the receiver) at world size 2: same rows as one operator, most records packed."""
+    from tests.dist_worker_gpu import worker_packed
+    from tests.gpu_helpers import random_stream
+    world = 2
+    stream_kw = dict(seed=29, n=40000, num_keys=3000, n_batches=10, ts_step=1, disorder=400, wm_lag=300)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = random.randint(20000, 40000)
+    procs = [ctx.Process(target=worker_packed, args=(r, world, port, cfg, stream_kw, flags, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        gathered = q.get(timeout=150)
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+    assert all(p.exitcode == 0 for p in procs)
+    assert all(g[1] == 0 for g in gathered)
+    assert sum(g[4] for g in gathered) == 40000 and sum(g[3] for g in gathered) > 0.7 * 40000
+    o = oracle_lib
+    keys, ts, vals, batches = random_stream(**stream_kw, agg=cfg["agg"])
+    op = o.OracleOperator(o.make_config(**cfg))
+    single = []
+    for lo, hi, wm in batches:
+        op.process_batch(keys[lo:hi], ts[lo:hi], vals[lo:hi])
+        op.process_watermark(wm)
+        single.append(op.drain())
+    op.process_watermark((1 << 63) - 1)
+    single.append(op.drain())
+    ref = sorted(row for r in single for row in zip(*[x.tolist() for x in r]))
+    union = sorted(row for g in gathered for row in g[0])
+    assert sum(g[2] for g in gathered) == op.late_dropped
+    assert len(union) == len(ref) > 0
+    assert union == ref
