@@ -67,6 +67,9 @@ def parse(argv=None):
     ap.add_argument("--exchange", choices=["a2a", "none"], default="a2a",
                     help="a2a: libgpuwin's RCCL keyBy exchange (gw_exchange_*); none: each rank generates "
                          "records of its own key groups only")
+    ap.add_argument("--pack", choices=["auto", "off"], default="auto",
+                    help="auto: the exchange ships records that fit as 8-byte words (gw_exchange_enable_packing; "
+                         "integer aggregates); off: every record as 24 B")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=20.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-host-fed", action="store_true",
@@ -172,8 +175,9 @@ class Steps:
             # set's hand-off stream, so batch b+1's partition and transfers overlap batch b's
             # aggregation on the operator's stream
             n, pk, pt, pv, _, wmin, ist = self.ex.exchange(k, t, v, stream=self.ex_stream, wm=self.wms[b])
-            if timed:
-                self.exch_bytes += (nb - int(self.ex.counts()[0][rank])) * b_in
+            if timed:  # bytes this rank sent to its peers (received packed share as the estimate)
+                f = self.ex.last_packed() / max(n, 1)
+                self.exch_bytes += (nb - int(self.ex.counts()[0][rank])) * (8 * f + b_in * (1 - f))
             N.check(self._ingest(self._h, n, pk, None, pt, pv, ist), self._h)
             wm = wmin
         else:
@@ -239,6 +243,8 @@ def main(argv=None):
         # torch.distributed only ships its communicator id and times the run
         from flink_amd.exchange import NativeKeyByExchange
         ex = NativeKeyByExchange(world, rank, max_parallelism=maxp, device=local)
+        if args.pack == "auto" and not agg.endswith("f64"):
+            ex.enable_packing(size, slide, 0, with_values=agg != "count")
     xs = torch.cuda.Stream(device=dev) if ex is not None else None
     run = Steps(op, N, keys, ts, vals, wms, nb, ex=ex, collect=args.checksum,
                 ex_stream=xs.cuda_stream if xs is not None else None)
@@ -382,7 +388,9 @@ def main(argv=None):
         if world > 1:
             out["exchange_gbs_per_gpu"] = run.exch_bytes / elapsed / 1e9
             out["exchange_path"] = ("gw_exchange_batch (libgpuwin RCCL: partition, one all-to-all of "
-                                    "(count, watermark, columns), one host wait, grouped send/recv per batch)"
+                                    "(count, watermark, columns, packed count), one host wait, grouped send/recv "
+                                    "per batch" + (", 8-B packed words" if args.pack == "auto" and not agg.endswith("f64")
+                                                   else ", 24-B records") + ")"
                                     if ex is not None else "none (key-partitioned source)")
         print(json.dumps(out), flush=True)
     if ex is not None:

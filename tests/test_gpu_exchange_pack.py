@@ -78,7 +78,7 @@ def test_device_partition_matches_host(P, with_values):
                                 dict(assigner="tumbling", size=600, agg="count", lateness=300)],
                          ids=["sliding_sum", "tumbling_count_lateness"])
 def test_packed_native_exchange_fires_like_the_oracle(oracle_lib, kw):
-    keys, ts, vals, batches = random_stream(31, 60000, 2000, 12, ts_step=1, disorder=400, wm_lag=300)
+    keys, ts, vals, batches = random_stream(31, 60000, 2000, 30, ts_step=1, disorder=400, wm_lag=300)
     slide = kw.get("slide", kw["size"])
     ex = NativeKeyByExchange(1, 0)
     ex.enable_packing(kw["size"], slide, 0, with_values=kw["agg"] != "count")
