@@ -322,20 +322,38 @@ __global__ void __launch_bounds__(256) k_ingest_preagg(IngestArgs a, int exp) {
     }
     __syncthreads();
     int par = 0;
+    // the next tile's inputs load while this tile is processed (two workgroups per CU do not
+    // hide a tile's load latency on their own)
+    int64_t nk[kPreaggItems], nt[kPreaggItems], nv[kPreaggItems];
+    auto load_tile = [&](int64_t t0) {
+#pragma unroll
+        for (int it = 0; it < kPreaggItems; ++it) {
+            const int64_t i = t0 + (int64_t)it * blockDim.x + threadIdx.x;
+            const bool ok = i < a.n;
+            nk[it] = ok ? a.key[i] : 0;
+            nt[it] = ok ? a.ts[i] : 0;
+            nv[it] = ok && a.val ? a.val[i] : 0;
+        }
+    };
+    load_tile(blockIdx.x * tile);
     for (int64_t t0 = blockIdx.x * tile; t0 < a.n; t0 += (int64_t)gridDim.x * tile, par ^= 1) {
         int64_t key[kPreaggItems], pane[kPreaggItems], c0[kPreaggItems], c1[kPreaggItems];
+        int64_t tsv[kPreaggItems], vv[kPreaggItems];
         uint32_t pos[kPreaggItems];
         int state[kPreaggItems], lk[kPreaggItems];
 #pragma unroll
         for (int it = 0; it < kPreaggItems; ++it) {
+            key[it] = nk[it];
+            tsv[it] = nt[it];
+            vv[it] = nv[it];
+        }
+        if (t0 + (int64_t)gridDim.x * tile < a.n) load_tile(t0 + (int64_t)gridDim.x * tile);
+#pragma unroll
+        for (int it = 0; it < kPreaggItems; ++it) {
             const int64_t i = t0 + (int64_t)it * blockDim.x + threadIdx.x;
             state[it] = REC_SKIP;
-            key[it] = 0; pane[it] = 0; c0[it] = 0; c1[it] = 0; pos[it] = 0;
-            if (i < a.n) {
-                key[it] = a.key[i];
-                state[it] = classify<AGG>(a, a.ts[i], a.val ? a.val[i] : 0, pos[it], pane[it], c0[it], c1[it], late,
-                                          flags);
-            }
+            pane[it] = 0; c0[it] = 0; c1[it] = 0; pos[it] = 0;
+            if (i < a.n) state[it] = classify<AGG>(a, tsv[it], vv[it], pos[it], pane[it], c0[it], c1[it], late, flags);
         }
         // phase A: each record's key in the cache (claimed by CAS on first sight)
 #pragma unroll
@@ -416,7 +434,7 @@ __global__ void __launch_bounds__(256) k_ingest_preagg(IngestArgs a, int exp) {
     __syncthreads();
     for (int j = threadIdx.x; j < kLdsCells; j += blockDim.x) {  // the workgroup's cells -> table
         const uint32_t cell = s_cell[j];
-        if (cell == ~0u) continue;
+        if (cell == ~0u || (exp & 4)) continue;
         const uint32_t l = cell / R, pos = cell - l * R;
         const int64_t g = s_g[l];
         if (g < 0) continue;  // (records of an unplaced key deferred above; no cell was made)
