@@ -18,7 +18,8 @@ steps, warm = b["steps"], b["warmup"]
 p1_idx = [i for i, r in enumerate(rows) if name(r) == "k_rgn_p1"]
 first_timed_p1 = p1_idx[warm]
 start = max(i for i in applies if i < first_timed_p1)
-end = applies[-1]
+last_timed_p1 = p1_idx[warm + steps - 1]
+end = min(i for i in applies if i > last_timed_p1)  # the final flush (a host-fed leg may follow)
 dur = {}
 for r in rows[start + 1:end + 1]:
     n = name(r)
@@ -27,7 +28,7 @@ pipe = ["k_rgn_p1", "k_rgn_plan1", "k_rgn_plan2", "k_rgn_plan3", "k_rgn_p2", "k_
 tot = sum(sum(dur.get(k, [])) for k in pipe)
 nb = len(dur.get("k_rgn_p1", []))
 print(f"timed batches (k_rgn_p1 dispatches): {nb} (bench steps {steps})")
-for k in pipe + ["k_fire"]:
+for k in pipe + ["k_fire", "k_fire2"]:
     v = dur.get(k, [])
     if v:
         print(f"  {k:14s} dispatches {len(v):3d}  avg {sum(v) / len(v):8.4f} ms  total {sum(v):8.3f} ms")
