@@ -23,10 +23,40 @@ __global__ void k_fe_iota64(int64_t* d, int64_t n, int64_t base) {
         d[i] = base + i;
 }
 
-// int64 -> its unsigned radix order (sign bit flipped), gathered through idx (or not: idx null)
-__global__ void k_fe_gather_key(const int64_t* src, const uint32_t* idx, uint64_t* dst, int64_t n) {
+// int64 -> its unsigned radix order (sign bit flipped) less the column's smallest such value,
+// gathered through idx (or not: idx null)
+__global__ void k_fe_gather_key(const int64_t* src, const uint32_t* idx, uint64_t* dst, int64_t n, uint64_t lo) {
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-        dst[i] = (uint64_t)src[idx ? idx[i] : i] ^ 0x8000000000000000ull;
+        dst[i] = ((uint64_t)src[idx ? idx[i] : i] ^ 0x8000000000000000ull) - lo;
+}
+
+// Smallest and largest radix-order value of four columns (the join's keys and starts):
+// out[2c] = min, out[2c + 1] = max of column c; out preset to (~0, 0).  The sorts then cover
+// only the bits of max - min (keys below 2^24: 3 passes, not 8; one window start: none).
+__global__ void __launch_bounds__(256) k_fe_range(const int64_t* c0, const int64_t* c1, const int64_t* c2,
+                                                  const int64_t* c3, int64_t n, unsigned long long* out) {
+    const int64_t* col[4] = {c0, c1, c2, c3};
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        unsigned long long lo = ~0ull, hi = 0;
+        for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+            const unsigned long long v = (unsigned long long)col[c][i] ^ 0x8000000000000000ull;
+            lo = min(lo, v);
+            hi = max(hi, v);
+        }
+        for (int o = 32; o > 0; o >>= 1) {
+            lo = min(lo, (unsigned long long)__shfl_xor(lo, o));
+            hi = max(hi, (unsigned long long)__shfl_xor(hi, o));
+        }
+        if (__lane_id() == 0) {
+            atomicMin(&out[2 * c], lo);
+            atomicMax(&out[2 * c + 1], hi);
+        }
+    }
+}
+
+__global__ void k_fe_range_init(unsigned long long* out) {
+    if (threadIdx.x < 8) out[threadIdx.x] = (threadIdx.x & 1) ? 0ull : ~0ull;
 }
 
 // The batch's largest timestamp: wave then block reduction, one device atomic per block
@@ -99,31 +129,42 @@ hipError_t fe_log_gather(const int64_t* log, int64_t cap, const int64_t* seq, in
 size_t fe_join_scratch_bytes(int64_t n) {
     const size_t bytes = (size_t)sort_scratch_bytes(std::max<int64_t>(n, 1));
     const size_t a = (size_t)std::max<int64_t>(n, 1);
-    // sort temp + 2 key buffers (8 B) + 2 index buffers (4 B) per side, two sides
-    return ((bytes + 255) / 256 * 256) + 2 * (a * 16 + a * 8) + 1024;
+    // sort temp + 2 key buffers (8 B) + 2 index buffers (4 B) per side, two sides, the ranges
+    return ((bytes + 255) / 256 * 256) + 2 * (a * 16 + a * 8) + 1024 + 64;
+}
+
+static int range_bits(uint64_t lo, uint64_t hi) {
+    if (hi <= lo) return 0;
+    return 64 - __builtin_clzll(hi - lo);
 }
 
 // (key, start) order of one side: indices sorted by start, then stably by key (gw_sort.hip,
-// int64 values in radix order: the sign bit flipped).
-static hipError_t sort_side(int64_t n, const int64_t* key, const int64_t* start, uint32_t*& order, uint8_t*& p,
-                            void* tmp, size_t tmp_bytes, hipStream_t s) {
-    (void)tmp_bytes;
+// int64 values in radix order: the sign bit flipped, less the column's minimum; only the bits of
+// the column's range are sorted).
+static hipError_t sort_side(int64_t n, const int64_t* key, const int64_t* start, const uint64_t* rk,
+                            const uint64_t* rs, uint32_t*& order, uint8_t*& p, void* tmp, hipStream_t s) {
     const size_t a = (size_t)n;
     uint64_t* k0 = (uint64_t*)p; p += a * 8;
     uint64_t* k1 = (uint64_t*)p; p += a * 8;
     uint32_t* v0 = (uint32_t*)p; p += a * 4;
     uint32_t* v1 = (uint32_t*)p; p += a * 4;
-    hipLaunchKernelGGL(k_fe_gather_key, dim3(grid_n(n)), dim3(256), 0, s, start, (const uint32_t*)nullptr, k0, n);
+    const int sbits = range_bits(rs[0], rs[1]), kbits = range_bits(rk[0], rk[1]);
     int alt = 0;
-    hipError_t e = sort_pairs_u64(k0, v0, k1, v1, n, 0, 64, tmp, s, &alt, /*iota=*/true);
-    if (e != hipSuccess) return e;
+    hipError_t e;
+    if (sbits) hipLaunchKernelGGL(k_fe_gather_key, dim3(grid_n(n)), dim3(256), 0, s, start, (const uint32_t*)nullptr, k0, n,
+                                  rs[0]);
+    if ((e = sort_pairs_u64(k0, v0, k1, v1, n, 0, sbits, tmp, s, &alt, /*iota=*/true)) != hipSuccess) return e;
     uint32_t* va = alt ? v1 : v0;
     uint32_t* vb = alt ? v0 : v1;
-    // second pass: the keys of the start-sorted order, sorted stably
+    // second sort: the keys of the start-sorted order, stably
     uint64_t* kk = alt ? k0 : k1;
     uint64_t* ko = alt ? k1 : k0;
-    hipLaunchKernelGGL(k_fe_gather_key, dim3(grid_n(n)), dim3(256), 0, s, key, va, kk, n);
-    if ((e = sort_pairs_u64(kk, va, ko, vb, n, 0, 64, tmp, s, &alt)) != hipSuccess) return e;
+    if (!kbits) {
+        order = va;
+        return hipGetLastError();
+    }
+    hipLaunchKernelGGL(k_fe_gather_key, dim3(grid_n(n)), dim3(256), 0, s, key, va, kk, n, rk[0]);
+    if ((e = sort_pairs_u64(kk, va, ko, vb, n, 0, kbits, tmp, s, &alt)) != hipSuccess) return e;
     order = alt ? vb : va;
     return hipGetLastError();
 }
@@ -139,9 +180,20 @@ hipError_t fe_join(int64_t n, const int64_t* a_key, const int64_t* a_start, cons
     uint8_t* p = (uint8_t*)scratch;
     void* tmp = p;
     p += (tmp_bytes + 255) / 256 * 256;
+    unsigned long long* d_range = (unsigned long long*)(p + 2 * ((size_t)n * 16 + (size_t)n * 8) + 1024);
+    // the columns' ranges (one small device-to-host copy: the sorts' pass counts depend on it)
+    hipLaunchKernelGGL(k_fe_range_init, dim3(1), dim3(64), 0, s, d_range);
+    const unsigned rg = (unsigned)std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 512));
+    hipLaunchKernelGGL(k_fe_range, dim3(rg), dim3(256), 0, s, a_key, a_start, b_key, b_start, n, d_range);
+    uint64_t r[8];
+    hipError_t e = hipMemcpyAsync(r, d_range, sizeof r, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e != hipSuccess) return e;
+    // one range per column over both sides: equal (key, start) pairs map to equal sort keys
+    uint64_t rk[2] = {std::min(r[0], r[4]), std::max(r[1], r[5])}, rs[2] = {std::min(r[2], r[6]), std::max(r[3], r[7])};
     uint32_t *pa = nullptr, *pb = nullptr;
-    hipError_t e = sort_side(n, a_key, a_start, pa, p, tmp, tmp_bytes, s);
-    if (e == hipSuccess) e = sort_side(n, b_key, b_start, pb, p, tmp, tmp_bytes, s);
+    e = sort_side(n, a_key, a_start, rk, rs, pa, p, tmp, s);
+    if (e == hipSuccess) e = sort_side(n, b_key, b_start, rk, rs, pb, p, tmp, s);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_fe_zip, dim3(grid_n(n)), dim3(256), 0, s, n, pa, pb, a_key, a_start, a_end, a_res, b_key,
                        b_start, b_res, log, log_base, log_cap, o_key, o_start, o_end, o_res, o_pay, d_bad);
