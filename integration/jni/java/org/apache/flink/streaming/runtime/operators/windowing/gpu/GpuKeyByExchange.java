@@ -48,6 +48,14 @@ public final class GpuKeyByExchange implements AutoCloseable {
 
     public long minWatermark(long wm, long stream) { return nativeMinWatermark(handle, wm, stream); }
 
+    /** From the next batch on, records whose key fits 32 bits, value 28 bits and pane the 16
+     *  after the watermark's travel as 8-byte words (include/gpuwin.h gw_exchange_enable_packing):
+     *  for a tumbling / sliding operator with size >= slide, no late side output and an integer
+     *  aggregate.  Every subtask must call it alike. */
+    public void enablePacking(long size, long slide, long offset, boolean withValues) {
+        nativeEnablePacking(handle, size, slide, offset, withValues);
+    }
+
     @Override
     public void close() {
         if (handle != 0) nativeDestroy(handle);
@@ -60,4 +68,5 @@ public final class GpuKeyByExchange implements AutoCloseable {
     private static native void nativeBatch(long h, long n, long keyPtr, long hashPtr, long tsPtr, long valuePtr,
                                            long watermark, long stream, ByteBuffer out);
     private static native long nativeMinWatermark(long h, long wm, long stream);
+    private static native void nativeEnablePacking(long h, long size, long slide, long offset, boolean withValues);
 }

@@ -369,6 +369,14 @@ JNIEXPORT void JNICALL XCLS(nativeBatch)(JNIEnv* env, jclass c, jlong x, jlong n
     fail_ex(env, (gw_exchange*)(intptr_t)x, rc);
 }
 
+/* Packed records from the next batch on (gw_exchange_enable_packing): a tumbling / sliding
+ * operator with size >= slide, no late side output, integer aggregate. */
+JNIEXPORT void JNICALL XCLS(nativeEnablePacking)(JNIEnv* env, jclass c, jlong x, jlong size, jlong slide,
+                                                 jlong offset, jboolean withValues) {
+    fail_ex(env, (gw_exchange*)(intptr_t)x,
+            gw_exchange_enable_packing((gw_exchange*)(intptr_t)x, size, slide, offset, withValues ? 1 : 0));
+}
+
 /* StatusWatermarkValve: the minimum of the subtasks' watermarks. */
 JNIEXPORT jlong JNICALL XCLS(nativeMinWatermark)(JNIEnv* env, jclass c, jlong x, jlong wm, jlong stream) {
     int64_t out = wm;
