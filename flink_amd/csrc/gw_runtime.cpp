@@ -1349,13 +1349,17 @@ struct gw_handle {
         // rather than growing it by the bound (a reallocation: a sync and a copy) -- the bound
         // keeps growing while host writes leave the published status slots stale
         if (lazy_recs > 0 && (int64_t)h_st->n_deferred + lazy_recs + nrec > def_cap) {
+            if (hp.on)
+                fprintf(stderr, "[gw host] deferred bound: n_deferred %lld lazy %lld nrec %lld cap %lld\n",
+                        (long long)h_st->n_deferred, (long long)lazy_recs, (long long)nrec, (long long)def_cap);
             if ((rc = refresh())) return rc;
-            // GW_DEF_GROW=k: also grow the list to n_deferred + k batches here (this sync has
-            // happened anyway), so that later batches skip this sync.  Measured (profiles/r5/
-            // defgrow/): k = 4 at 1M-record batches 5.7 G against 9.3 G without (the pipelined
-            // status path then waits on every batch instead), at 10M-record batches 50.5 G
-            // against 49.0 G: not the default.
-            static const int grow = getenv("GW_DEF_GROW") ? atoi(getenv("GW_DEF_GROW")) : 0;
+            // and grow the list to n_deferred + (kAsync + 1) batches (this sync has happened
+            // anyway): the steady state leaves kAsync batches' launches unaccounted, and a list
+            // sized for fewer synced here on every batch.  Measured (profiles/r5/defgrow/): Q5
+            // at 1M-record batches 11.5 G against 10.4 G (after a 15-batch warmup: the one
+            // reallocation, ~1.5 ms, lands in the first region-path batch), at 10M-record
+            // batches 50.5 G against 49.0 G.  GW_DEF_GROW=0: the round-4 policy.
+            static const int grow = getenv("GW_DEF_GROW") ? atoi(getenv("GW_DEF_GROW")) : kAsync + 1;
             if (grow && (rc = ensure_deferred((int64_t)h_st->n_deferred + grow * nrec))) return rc;
         }
         if ((rc = ensure_deferred((int64_t)h_st->n_deferred + lazy_recs + nrec))) return rc;
