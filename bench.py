@@ -67,9 +67,13 @@ def parse(argv=None):
     ap.add_argument("--exchange", choices=["a2a", "none"], default="a2a",
                     help="a2a: libgpuwin's RCCL keyBy exchange (gw_exchange_*); none: each rank generates "
                          "records of its own key groups only")
-    ap.add_argument("--pack", choices=["auto", "off"], default="auto",
+    ap.add_argument("--pack", choices=["auto", "unpack", "off"], default="auto",
                     help="auto: the exchange ships records that fit as 8-byte words (gw_exchange_enable_packing; "
-                         "integer aggregates); off: every record as 24 B")
+                         "integer aggregates) and pass 1 decodes them (gw_ingest_packed_device); unpack: the "
+                         "receiver unpacks them to columns first; off: every record as 24 B")
+    ap.add_argument("--force-exchange", action="store_true",
+                    help="run the RCCL exchange path at N = 1 too (a one-rank communicator: every record comes "
+                         "back to this rank) -- a check of the N > 1 code path on one GPU")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=20.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-host-fed", action="store_true",
@@ -157,6 +161,8 @@ class Steps:
         # points and each batch's device column pointers resolved once, before any clock
         L = N.lib()
         self._ingest, self._advance, self._clear = L.gw_ingest_device, L.gw_advance_watermark, L.gw_clear_rows
+        self._ingest_packed = L.gw_ingest_packed_device
+        self._byref = ctypes.byref
         self._h, self._stream = op.handle, op.stream()
         self._fired = ctypes.c_int64(0)
         self._fired_ref = ctypes.byref(self._fired)
@@ -176,9 +182,13 @@ class Steps:
             # aggregation on the operator's stream
             n, pk, pt, pv, _, wmin, ist = self.ex.exchange(k, t, v, stream=self.ex_stream, wm=self.wms[b])
             if timed:  # bytes this rank sent to its peers (received packed share as the estimate)
-                f = self.ex.last_packed() / max(n, 1)
+                f = self.ex.last_packed() / max(nb, 1)
                 self.exch_bytes += (nb - int(self.ex.counts()[0][rank])) * (8 * f + b_in * (1 - f))
-            N.check(self._ingest(self._h, n, pk, None, pt, pv, ist), self._h)
+            nw, pw, geom = self.ex.last_words()
+            if nw:  # words kept packed: pass 1 decodes them
+                N.check(self._ingest_packed(self._h, n, pk, pt, pv, nw, pw, self._byref(geom), ist), self._h)
+            else:
+                N.check(self._ingest(self._h, n, pk, None, pt, pv, ist), self._h)
             wm = wmin
         else:
             # columns generated and synchronised before the clock: no producer ordering needed
@@ -238,13 +248,14 @@ def main(argv=None):
 
     op = make_operator(W, N, args, K, world, rank, local, nb)
     ex = None
-    if world > 1 and args.exchange == "a2a":
+    if (world > 1 and args.exchange == "a2a") or args.force_exchange:
         # the product path: libgpuwin's own RCCL exchange, what a JVM task drives;
         # torch.distributed only ships its communicator id and times the run
         from flink_amd.exchange import NativeKeyByExchange
         ex = NativeKeyByExchange(world, rank, max_parallelism=maxp, device=local)
-        if args.pack == "auto" and not agg.endswith("f64"):
+        if args.pack != "off" and not agg.endswith("f64"):
             ex.enable_packing(size, slide, 0, with_values=agg != "count")
+            ex.keep_words(args.pack == "auto")
     xs = torch.cuda.Stream(device=dev) if ex is not None else None
     run = Steps(op, N, keys, ts, vals, wms, nb, ex=ex, collect=args.checksum,
                 ex_stream=xs.cuda_stream if xs is not None else None)
@@ -385,11 +396,13 @@ def main(argv=None):
                                     "MAX_WATERMARK included, summed over ranks (mod 2^64)")
         if oracle_check is not None:
             out["oracle_check"] = oracle_check
-        if world > 1:
+        if world > 1 or ex is not None:
+            pk = args.pack != "off" and not agg.endswith("f64")
             out["exchange_gbs_per_gpu"] = run.exch_bytes / elapsed / 1e9
             out["exchange_path"] = ("gw_exchange_batch (libgpuwin RCCL: partition, one all-to-all of "
                                     "(count, watermark, columns, packed count), one host wait, grouped send/recv "
-                                    "per batch" + (", 8-B packed words" if args.pack == "auto" and not agg.endswith("f64")
+                                    "per batch" + ((", 8-B packed words decoded by pass 1" if args.pack == "auto"
+                                                    else ", 8-B packed words unpacked to columns") if pk
                                                    else ", 24-B records") + ")"
                                     if ex is not None else "none (key-partitioned source)")
         print(json.dumps(out), flush=True)

@@ -57,6 +57,7 @@ EXPORTS = [
     "gw_snapshot_keys", "gw_snapshot_remap_keys", "gw_snapshot_payloads", "gw_snapshot_remap_payloads",
     "gw_pack_geom_init", "gw_pack_records", "gw_unpack_records", "gw_partition_packed_device", "gw_unpack_device",
     "gw_exchange_enable_packing", "gw_exchange_last_packed", "gw_exchange_plan_packed",
+    "gw_exchange_set_unpack", "gw_exchange_last_words", "gw_ingest_packed_device",
 ]
 EXCHANGE_ID_BYTES = 128
 
@@ -212,6 +213,9 @@ def lib() -> ctypes.CDLL:
         "gw_exchange_enable_packing": (c_int, [p, i64, i64, i64, i32]),
         "gw_exchange_last_packed": (i64, [p]),
         "gw_exchange_plan_packed": (c_int, [i32, p, p, p, p, p, p, P64, P64]),
+        "gw_exchange_set_unpack": (c_int, [p, i32]),
+        "gw_exchange_last_words": (c_int, [p, P64, ctypes.POINTER(p), ctypes.POINTER(GwPackGeom)]),
+        "gw_ingest_packed_device": (c_int, [p, i64, p, p, p, i64, p, ctypes.POINTER(GwPackGeom), p]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)

@@ -49,6 +49,9 @@ struct gw_exchange {
     int64_t pack_size = 0, pack_slide = 0, pack_offset = 0;
     int64_t last_wm = INT64_MIN;
     int64_t last_packed = 0;
+    bool unpack = true;                    // false: the words stay packed (gw_exchange_last_words)
+    const uint64_t* last_words = nullptr;
+    gw_pack_geom last_geom{};
     // One all-to-all message per peer and batch: (records for it, watermark, column mask,
     // packed records).  d_msg: [nranks][kMsg] send | [nranks][kMsg] receive; h_msg its pinned copy.
     static constexpr int kMsg = 4;
@@ -237,6 +240,20 @@ int gw_exchange_enable_packing(gw_exchange* ex, int64_t size, int64_t slide, int
 
 int64_t gw_exchange_last_packed(const gw_exchange* ex) { return ex ? ex->last_packed : 0; }
 
+int gw_exchange_set_unpack(gw_exchange* ex, int32_t unpack) {
+    if (!ex) return GW_E_INVALID;
+    ex->unpack = unpack != 0;
+    return GW_OK;
+}
+
+int gw_exchange_last_words(const gw_exchange* ex, int64_t* n_words, const uint64_t** d_words, gw_pack_geom* g) {
+    if (!ex || !n_words || !d_words) return GW_E_INVALID;
+    *n_words = ex->last_words ? ex->last_packed : 0;
+    *d_words = ex->last_words;
+    if (g) *g = ex->last_geom;
+    return GW_OK;
+}
+
 int gw_exchange_batch(gw_exchange* ex, int64_t n, const int64_t* d_key, const int32_t* d_key_hash,
                       const int64_t* d_ts, const int64_t* d_value, int64_t wm, int64_t* n_out,
                       const int64_t** d_key_out, const int32_t** d_key_hash_out, const int64_t** d_ts_out,
@@ -362,14 +379,21 @@ int gw_exchange_batch(gw_exchange* ex, int64_t n, const int64_t* d_key, const in
     const ncclResult_t re = ncclGroupEnd();
     if (r != ncclSuccess) return ex_fail(ex, GW_E_DEVICE, std::string("ncclSend/ncclRecv: ") + ncclGetErrorString(r));
     if (re != ncclSuccess) return ex_fail(ex, GW_E_DEVICE, std::string("ncclGroupEnd: ") + ncclGetErrorString(re));
-    if (packed && tp > 0)
-        EX_HIP(launch_unpack(tp, ex->recv_packed[u], g, rk + tw, rt + tw, d_value ? rv + tw : nullptr, s));
+    ex->last_words = nullptr;
+    ex->last_geom = g;
+    if (packed && tp > 0) {
+        if (ex->unpack)
+            EX_HIP(launch_unpack(tp, ex->recv_packed[u], g, rk + tw, rt + tw, d_value ? rv + tw : nullptr, s));
+        else
+            ex->last_words = ex->recv_packed[u];
+    }
+    const int64_t n_cols = (packed && !ex->unpack) ? tw : total;  // records in the columns
     // 5. hand-off: the ingest of this set orders after the receives on handoff[u] (and makes
     // handoff[u] wait for its reads); the exchange that reuses the set waits for handoff[u]
     EX_HIP(hipEventRecord(ex->ev_recv[u], s));
     EX_HIP(hipStreamWaitEvent(ex->handoff[u], ex->ev_recv[u], 0));
     ex->set_used[u] = true;
-    *n_out = total;
+    *n_out = n_cols;
     *d_key_out = rk;
     *d_ts_out = rt;
     if (d_value_out) *d_value_out = d_value ? rv : nullptr;

@@ -119,6 +119,11 @@ struct IngestArgs {
     const int64_t* ts;
     const int64_t* val;
     int64_t n;
+    // packed exchange words (gw_ingest_packed_device): records [pk_from, n) are pk_w[i -
+    // pk_from], decoded by the region P1 itself (unpack_word: key, pane start, value)
+    const uint64_t* pk_w;
+    int64_t pk_from;
+    gw_pack_geom pk_g;
     int64_t t_late;     // first non-late timestamp (start of the first unfired window)
     int64_t p_late;     // its pane index
     uint64_t delta;     // ring base pane B - p_late (>= 0)

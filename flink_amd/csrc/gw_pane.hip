@@ -817,9 +817,17 @@ __global__ void __launch_bounds__(kPartThreads) GW_P1_ATTR k_rgn_p1(IngestArgs a
         const int64_t i = lo + it * kPartThreads + threadIdx.x;
         key[it] = 0; ts[it] = 0; val[it] = 0;
         if (i < hi) {
-            key[it] = __builtin_nontemporal_load(a.key + i);  // read once: keep it out of the caches
-            ts[it] = __builtin_nontemporal_load(a.ts + i);
-            if (a.val) val[it] = __builtin_nontemporal_load(a.val + i);
+            if (a.pk_w && i >= a.pk_from) {  // a packed exchange word: 8 B instead of 24
+                int64_t k, t, v;
+                unpack_word(a.pk_g, __builtin_nontemporal_load(a.pk_w + (i - a.pk_from)), k, t, v);
+                key[it] = k;
+                ts[it] = t;
+                if (a.val) val[it] = v;
+            } else {
+                key[it] = __builtin_nontemporal_load(a.key + i);  // read once: keep it out of the caches
+                ts[it] = __builtin_nontemporal_load(a.ts + i);
+                if (a.val) val[it] = __builtin_nontemporal_load(a.val + i);
+            }
         }
     }
     p1_tile<AGG, FMT, GAP, kPartThreads, kPartItems>(a, g, lo, hi, key, ts, val, s, lh, ls, &s_occ, late, flags, occ);

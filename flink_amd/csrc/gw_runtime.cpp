@@ -361,6 +361,13 @@ struct gw_handle {
     KernelTimer t_ingest, t_fire, t_apply;
     int64_t timing_every = 1, timing_ctr = 0;  // region pass 1: time one launch in timing_every
     HostProf hp;
+    // gw_ingest_packed_device: the batch's records [pk_from, n) are packed exchange words that
+    // the region P1 decodes itself; other paths get them unpacked into pk_stage first
+    const uint64_t* pk_w = nullptr;
+    int64_t pk_from = 0;
+    gw_pack_geom pk_g{};
+    int64_t* pk_stage = nullptr;
+    int64_t pk_stage_cap = 0;
 
     SessionState* sess = nullptr;
     // key checks (gw_ingest* with key_hash, GW_FLAG_CHECK_KEY_GROUPS): device words, see k_check_keys
@@ -1149,6 +1156,7 @@ struct gw_handle {
         if (B < pl) B = pl;
         a = IngestArgs{};
         a.key = key; a.ts = ts; a.val = val; a.n = nrec;
+        a.pk_w = pk_w; a.pk_from = pk_from; a.pk_g = pk_g;
         a.t_late = (int64_t)t_late;
         a.p_late = (int64_t)pl;
         a.delta = (uint64_t)(B - pl);
@@ -1336,6 +1344,34 @@ struct gw_handle {
         return GW_OK;
     }
 
+    // The packed words of the current batch unpacked behind its other records, in pk_stage;
+    // key / ts / val then point there and the batch has no words any more.
+    int pk_materialize(int64_t nrec, const int64_t*& key, const int64_t*& ts, const int64_t*& val) {
+        if (nrec > pk_stage_cap) {
+            HIPCHECK(hipStreamSynchronize(stream));
+            hipFree(pk_stage);
+            pk_stage = nullptr;
+            const int64_t c = std::max<int64_t>(nrec + nrec / 4, 1 << 16);
+            HIPCHECK(hipMalloc((void**)&pk_stage, (size_t)c * 3 * 8));
+            pk_stage_cap = c;
+        }
+        int64_t* k = pk_stage;
+        int64_t* t = k + pk_stage_cap;
+        int64_t* v = val ? t + pk_stage_cap : nullptr;
+        if (pk_from > 0) {
+            HIPCHECK(hipMemcpyAsync(k, key, (size_t)pk_from * 8, hipMemcpyDeviceToDevice, stream));
+            HIPCHECK(hipMemcpyAsync(t, ts, (size_t)pk_from * 8, hipMemcpyDeviceToDevice, stream));
+            if (v) HIPCHECK(hipMemcpyAsync(v, val, (size_t)pk_from * 8, hipMemcpyDeviceToDevice, stream));
+        }
+        HIPCHECK(launch_unpack(nrec - pk_from, pk_w, pk_g, k + pk_from, t + pk_from, v ? v + pk_from : nullptr, stream));
+        key = k;
+        ts = t;
+        val = v;
+        pk_w = nullptr;
+        pk_from = 0;
+        return GW_OK;
+    }
+
     int ingest_pane(int64_t nrec, const int64_t* key, const int64_t* ts, const int64_t* val) {
         int rc;
         if ((rc = ov_finalize())) return rc;
@@ -1384,6 +1420,10 @@ struct gw_handle {
             if (big || (cfg.flags & GW_FLAG_FORCE_REGION)) path = 2;
         }
         if (path == 1) stats.preagg_batches++;
+        if (pk_w && (path != 2 || a.lo_key)) {  // only the region P1 decodes packed words
+            if ((rc = pk_materialize(nrec, key, ts, val))) return rc;
+            if ((rc = base_args(a, nrec, key, ts, val))) return rc;
+        }
         if (path != 2 && (nseg || carry_on)) {  // the other paths write the table directly: apply first
             if ((rc = flush_buffer())) return rc;
             if ((rc = base_args(a, nrec, key, ts, val))) return rc;  // the table may have grown
@@ -2724,6 +2764,7 @@ int gw_destroy(gw_handle* h) {
     }
     h->hp.dump();
     if (h->stream) hipStreamSynchronize(h->stream);
+    if (h->pk_stage) hipFree(h->pk_stage);
     h->khm_free();
     if (h->sess) session_destroy(h->sess);
     h->ov_free();
@@ -3274,12 +3315,62 @@ int gw_ingest_device(gw_handle* h, int64_t n, const int64_t* d_key, const int32_
     }
     if (n == 0) return GW_OK;
     h->hp.lap(5);
-    int rc = h->check_keys(n, d_key, d_key_hash);
+    int rc = h->check_keys(h->pk_w ? h->pk_from : n, d_key, d_key_hash);  // (packed words: routed already)
     if (rc == GW_OK) rc = ingest_device_impl(h, n, d_key, d_ts, (const int64_t*)d_value);
     if (foreign) {
         hipEventRecord(h->ev_out, h->stream);
         hipStreamWaitEvent(ps, h->ev_out, 0);
     }
+    return rc;
+}
+
+int gw_ingest_packed_device(gw_handle* h, int64_t n_other, const int64_t* d_key, const int64_t* d_ts,
+                            const int64_t* d_value, int64_t n_words, const uint64_t* d_words, const gw_pack_geom* g,
+                            void* stream) {
+    if (!h) return GW_E_INVALID;
+    if (n_other < 0 || n_words < 0 || (n_words > 0 && (!d_words || !g || !g->enabled || g->pane <= 0)))
+        return h->fail(GW_E_INVALID, "gw_ingest_packed_device: bad word arguments");
+    if (n_words == 0) return gw_ingest_device(h, n_other, d_key, nullptr, d_ts, d_value, stream);
+    const bool vals = h->cfg.agg != GW_COUNT;
+    if (n_other > 0 && (!d_key || !d_ts || (vals && !d_value))) return h->fail(GW_E_INVALID, "null key/ts/value column");
+    const int64_t n = n_other + n_words;
+    // columns of no records: any non-null pointer (never read below pk_from = 0)
+    const int64_t* dummy = (const int64_t*)d_words;
+    const int64_t* k = n_other ? d_key : dummy;
+    const int64_t* t = n_other ? d_ts : dummy;
+    const int64_t* v = vals ? (n_other ? d_value : dummy) : nullptr;
+    const bool plain = !h->fe && h->kids.empty() && !h->session && n <= kMaxIngest;
+    if (!plain) {  // unpack into the handle's staging columns on the producer stream, then as usual
+        if (n > h->pk_stage_cap) {
+            hipStreamSynchronize((hipStream_t)stream);
+            hipStreamSynchronize(h->stream);
+            hipFree(h->pk_stage);
+            h->pk_stage = nullptr;
+            const int64_t c = std::max<int64_t>(n + n / 4, 1 << 16);
+            if (hipMalloc((void**)&h->pk_stage, (size_t)c * 3 * 8) != hipSuccess)
+                return h->fail(GW_E_OOM, "packed staging: out of device memory");
+            h->pk_stage_cap = c;
+        }
+        int64_t* sk = h->pk_stage;
+        int64_t* st = sk + h->pk_stage_cap;
+        int64_t* sv = vals ? st + h->pk_stage_cap : nullptr;
+        hipStream_t ps = (hipStream_t)stream;
+        if (n_other > 0) {
+            hipMemcpyAsync(sk, d_key, (size_t)n_other * 8, hipMemcpyDeviceToDevice, ps);
+            hipMemcpyAsync(st, d_ts, (size_t)n_other * 8, hipMemcpyDeviceToDevice, ps);
+            if (sv) hipMemcpyAsync(sv, d_value, (size_t)n_other * 8, hipMemcpyDeviceToDevice, ps);
+        }
+        if (launch_unpack(n_words, d_words, *g, sk + n_other, st + n_other, sv ? sv + n_other : nullptr, ps) !=
+            hipSuccess)
+            return h->fail(GW_E_DEVICE, "packed staging: unpack launch failed");
+        return gw_ingest_device(h, n, sk, nullptr, st, sv, stream);
+    }
+    h->pk_w = d_words;
+    h->pk_from = n_other;
+    h->pk_g = *g;
+    const int rc = gw_ingest_device(h, n, k, nullptr, t, v, stream);
+    h->pk_w = nullptr;
+    h->pk_from = 0;
     return rc;
 }
 

@@ -303,6 +303,17 @@ class NativeKeyByExchange:
         self._check(N.lib().gw_exchange_enable_packing(self._h, int(size), int(slide), int(offset),
                                                        1 if with_values else 0))
 
+    def keep_words(self, keep: bool = True):
+        """gw_exchange_set_unpack(!keep): received words stay packed for gw_ingest_packed_device."""
+        self._check(N.lib().gw_exchange_set_unpack(self._h, 0 if keep else 1))
+
+    def last_words(self):
+        """(n_words, device pointer, GwPackGeom) of the last batch's words kept packed."""
+        import ctypes
+        n, w, g = ctypes.c_int64(), ctypes.c_void_p(), N.GwPackGeom()
+        self._check(N.lib().gw_exchange_last_words(self._h, ctypes.byref(n), ctypes.byref(w), ctypes.byref(g)))
+        return n.value, w.value, g
+
     def last_packed(self) -> int:
         """Records this rank received packed in the last batch."""
         return int(N.lib().gw_exchange_last_packed(self._h))

@@ -590,6 +590,16 @@ class GpuWindowOperator:
                                       ctypes.c_void_p(stream) if stream else None)
         N.check(rc, self._h)
 
+    def process_batch_packed_device_ptr(self, n_other: int, key_ptr, ts_ptr, val_ptr, n_words: int, words_ptr,
+                                        geom, stream=None):
+        """gw_ingest_packed_device: n_other column records followed by n_words packed exchange
+        words (NativeKeyByExchange.last_words)."""
+        self._ensure_handle()
+        vp = lambda x: ctypes.c_void_p(x) if x else None
+        rc = N.lib().gw_ingest_packed_device(self._h, n_other, vp(key_ptr), vp(ts_ptr), vp(val_ptr), n_words,
+                                             vp(words_ptr), ctypes.byref(geom), vp(stream))
+        N.check(rc, self._h)
+
     def advance_watermark(self, wm: int) -> int:
         if self._deferred:  # staggered, no element yet: nothing can fire
             self._deferred_wm = max(self._deferred_wm, int(wm))

@@ -462,6 +462,14 @@ int  gw_partition_packed_device(int64_t n, const int64_t* d_key, const int64_t* 
                                 int64_t* d_counts, void* d_scratch, void* stream);
 int  gw_unpack_device(int64_t n, const uint64_t* d_words, const gw_pack_geom* g, int64_t* d_key, int64_t* d_ts,
                       int64_t* d_value, void* stream);
+/* gw_ingest_device for a batch of n_other column records followed by n_words packed words
+ * (gw_exchange_last_words): the words' timestamps are their panes' starts (gw_pack_geom).  A
+ * plain pane operator's region pass 1 decodes the words itself; other paths and handles
+ * (sessions, window classes, first-element, the late side output) get them unpacked first.
+ * Column pointers may be NULL when n_other = 0. */
+int  gw_ingest_packed_device(gw_handle* h, int64_t n_other, const int64_t* d_key, const int64_t* d_ts,
+                             const int64_t* d_value, int64_t n_words, const uint64_t* d_words,
+                             const gw_pack_geom* g, void* stream);
 
 /* ---- keyBy exchange over RCCL (one process per GPU) ------------------------
  * Replaces the network shuffle behind KeyGroupStreamPartitioner.selectChannel
@@ -512,6 +520,13 @@ int  gw_exchange_counts(const gw_exchange* ex, int64_t* send, int64_t* recv);
  * next batch).  gw_exchange_last_packed: records this rank received packed in the last batch. */
 int  gw_exchange_enable_packing(gw_exchange* ex, int64_t size, int64_t slide, int64_t offset, int32_t with_values);
 int64_t gw_exchange_last_packed(const gw_exchange* ex);
+/* gw_exchange_set_unpack(ex, 0): the received words stay packed -- gw_exchange_batch's
+ * *n_out and columns then hold only the records that travelled unpacked, and
+ * gw_exchange_last_words gives the words (device, valid like the columns) and their geometry
+ * for gw_ingest_packed_device, whose region pass 1 decodes them (8 B read per record instead
+ * of an unpack pass writing 24 B that pass 1 reads again). */
+int  gw_exchange_set_unpack(gw_exchange* ex, int32_t unpack);
+int  gw_exchange_last_words(const gw_exchange* ex, int64_t* n_words, const uint64_t** d_words, gw_pack_geom* g);
 int  gw_exchange_min_watermark(gw_exchange* ex, int64_t wm, int64_t* out, void* stream);
 const char* gw_exchange_last_error(const gw_exchange* ex);
 /* The per-peer plan gw_exchange_batch runs after its count all-to-all, as a host function

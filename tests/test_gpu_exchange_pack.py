@@ -118,3 +118,116 @@ def test_packed_native_exchange_fires_like_the_oracle(oracle_lib, kw):
     op.close()
     ora.close()
     ex.close()
+
+
+def _ingest_both(kw, flags, keys, ts, vals, batches, with_values, oracle_lib, classes=False):
+    """Operator A ingests each batch as (column records, packed words) through
+    gw_ingest_packed_device; the oracle gets the original records.  The words are the records
+    that pack against the watermark before the batch (gw_pack_records on the host)."""
+    from gpu_helpers import make_assigner
+    slide = kw.get("slide", kw["size"])
+    op = W.GpuWindowOperator(make_assigner(kw), kw["agg"], kw.get("lateness", 0), capacity_hint=4096,
+                             flags=flags).open()
+    ora = oracle_lib.OracleOperator(oracle_lib.make_config(**kw))
+    g, o, last, packed = [], [], W.LONG_MIN, 0
+    s = torch.cuda.current_stream().cuda_stream
+    for lo, hi, wm in batches:
+        k, t, v = keys[lo:hi], ts[lo:hi], vals[lo:hi]
+        geom = N.pack_geom(kw["size"], slide, kw.get("offset", 0), last)
+        if geom is None:
+            op.process_batch(k, t, v if with_values else None)
+        else:
+            w, fits = N.pack_records(k, t, v if with_values else None, geom)
+            other = ~fits
+            dk = torch.from_numpy(np.ascontiguousarray(k[other])).cuda()
+            dt = torch.from_numpy(np.ascontiguousarray(t[other])).cuda()
+            dv = torch.from_numpy(np.ascontiguousarray(v[other])).cuda() if with_values else None
+            dw = torch.from_numpy(np.ascontiguousarray(w[fits]).view(np.int64)).cuda()
+            torch.cuda.synchronize()
+            op.process_batch_packed_device_ptr(int(other.sum()), dk.data_ptr() if other.any() else None,
+                                               dt.data_ptr() if other.any() else None,
+                                               dv.data_ptr() if (dv is not None and other.any()) else None,
+                                               int(fits.sum()), dw.data_ptr() if fits.any() else None, geom, stream=s)
+            torch.cuda.synchronize()
+            packed += int(fits.sum())
+        op.advance_watermark(wm)
+        last = wm
+        kk, ss, ee, rr = op.drain()
+        g.append((kk, ss, ee, rr.view(np.int64)))
+        ora.process_batch(k, t, v)
+        ora.process_watermark(wm)
+        o.append(ora.drain())
+    op.advance_watermark(W.LONG_MAX)
+    kk, ss, ee, rr = op.drain()
+    g.append((kk, ss, ee, rr.view(np.int64)))
+    ora.process_watermark(W.LONG_MAX)
+    o.append(ora.drain())
+    late = (op.num_late_records_dropped, ora.late_dropped)
+    op.close()
+    ora.close()
+    return g, o, late, packed
+
+
+@pytest.mark.parametrize("kw,flags", [
+    (dict(assigner="sliding", size=1000, slide=250, agg="sum_i64"), N.FLAG_FORCE_REGION),
+    (dict(assigner="sliding", size=1000, slide=250, agg="sum_i64"), N.FLAG_NO_REGION),
+    (dict(assigner="tumbling", size=500, agg="count", lateness=300), N.FLAG_FORCE_REGION),
+    (dict(assigner="tumbling", size=500, agg="max_i64"), N.FLAG_FORCE_LDS_PREAGG),
+    (dict(assigner="sliding", size=1200, slide=400, agg="avg_i64", lateness=400), N.FLAG_FORCE_REGION),
+    (dict(assigner="sliding", size=40_000, slide=500, agg="min_i64"), 0),  # window classes: staged unpack
+], ids=["region_sum", "direct_sum", "region_count_lateness", "preagg_max", "region_avg_lateness", "classes_min"])
+def test_packed_ingest_matches_the_oracle(oracle_lib, kw, flags):
+    """gw_ingest_packed_device: the region P1 decodes the words itself; the direct and
+    pre-aggregation paths and window-class composites unpack them into staging first."""
+    keys, ts, vals, batches = random_stream(43, 120_000, 5000, 24, ts_step=1, disorder=300, wm_lag=300,
+                                            agg=kw["agg"])
+    with_values = kw["agg"] != "count"
+    g, o, late, packed = _ingest_both(kw, flags, keys, ts, vals, batches, with_values, oracle_lib)
+    assert late[0] == late[1]
+    assert packed > 0.5 * keys.size
+    assert compare(g, o, kw["agg"].startswith("avg")) == []
+
+
+@pytest.mark.parametrize("kw", [dict(assigner="sliding", size=1000, slide=250, agg="sum_i64"),
+                                dict(assigner="tumbling", size=600, agg="count")], ids=["sliding_sum", "tumbling_count"])
+def test_exchange_words_into_packed_ingest(oracle_lib, kw):
+    """The native exchange keeping words packed (gw_exchange_set_unpack(0)) feeding
+    gw_ingest_packed_device: what the oracle fires."""
+    keys, ts, vals, batches = random_stream(37, 60000, 2000, 30, ts_step=1, disorder=400, wm_lag=300)
+    slide = kw.get("slide", kw["size"])
+    ex = NativeKeyByExchange(1, 0)
+    ex.enable_packing(kw["size"], slide, 0, with_values=kw["agg"] != "count")
+    ex.keep_words(True)
+    assigner = (W.SlidingEventTimeWindows.of(kw["size"], slide) if kw["assigner"] == "sliding"
+                else W.TumblingEventTimeWindows.of(kw["size"]))
+    op = W.GpuWindowOperator(assigner, kw["agg"], capacity_hint=4096, flags=N.FLAG_FORCE_REGION).open()
+    ora = oracle_lib.OracleOperator(oracle_lib.make_config(**kw))
+    g, o, words = [], [], 0
+    xs = torch.cuda.Stream()
+    for lo, hi, wm in batches:
+        k = torch.from_numpy(keys[lo:hi]).cuda()
+        t = torch.from_numpy(ts[lo:hi]).cuda()
+        v = torch.from_numpy(vals[lo:hi]).cuda() if kw["agg"] != "count" else None
+        torch.cuda.synchronize()
+        n, pk, pt, pv, _, wmin, ist = ex.exchange(k, t, v, stream=xs.cuda_stream, wm=wm)
+        nw, pw, geom = ex.last_words()
+        assert n + nw == hi - lo
+        words += nw
+        op.process_batch_packed_device_ptr(n, pk, pt, pv, nw, pw, geom, stream=ist)
+        op.advance_watermark(wmin)
+        kk, ss, ee, rr = op.drain()
+        g.append((kk, ss, ee, rr.view(np.int64)))
+        ora.process_batch(keys[lo:hi], ts[lo:hi], vals[lo:hi])
+        ora.process_watermark(wm)
+        o.append(ora.drain())
+    op.advance_watermark(W.LONG_MAX)
+    kk, ss, ee, rr = op.drain()
+    g.append((kk, ss, ee, rr.view(np.int64)))
+    ora.process_watermark(W.LONG_MAX)
+    o.append(ora.drain())
+    assert words > 0.8 * keys.size
+    assert op.num_late_records_dropped == ora.late_dropped
+    assert compare(g, o, False) == []
+    op.close()
+    ora.close()
+    ex.close()
