@@ -62,33 +62,51 @@ __global__ void __launch_bounds__(256) k_part_hist(int64_t n, const int64_t* key
     for (int d = threadIdx.x; d < nd; d += blockDim.x) block_counts[(int64_t)d * gridDim.x + blockIdx.x] = h[d];
 }
 
-// pass 2: exclusive scan over (dest-major, block-minor); totals per dest.
+// pass 2: exclusive scan over (dest-major, block-minor); totals per dest.  One block: each
+// thread sums a contiguous run of the counts, a wave-shuffle scan over the threads' sums, each
+// thread writes its run's offsets; a destination's total is the difference of the offsets at
+// its first entry and the next destination's (each found from its thread's prefix plus a walk
+// of at most `per` counts) -- not a serial loop over the blocks per destination (that loop took
+// ~320 us at 10M records: 4883 dependent loads per destination).
 __global__ void __launch_bounds__(1024) k_part_scan(uint32_t* block_counts, int64_t nblk, int32_t p,
                                                     int64_t* offsets, int64_t* counts) {
     __shared__ unsigned long long part[1024];
+    __shared__ unsigned long long wsum[16];
     const int64_t total = nblk * p;
     const int64_t per = (total + blockDim.x - 1) / blockDim.x;
-    const int64_t lo = threadIdx.x * per, hi = min(total, lo + per);
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const int64_t lo = t * per, hi = min(total, lo + per);
     unsigned long long s = 0;
     for (int64_t i = lo; i < hi; ++i) s += block_counts[i];
-    part[threadIdx.x] = s;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        unsigned long long run = 0;
-        for (int i = 0; i < (int)blockDim.x; ++i) { unsigned long long v = part[i]; part[i] = run; run += v; }
+    unsigned long long incl = s;
+    for (int o = 1; o < 64; o <<= 1) {
+        const unsigned long long up = __shfl_up(incl, o);
+        if (lane >= o) incl += up;
     }
+    if (lane == 63) wsum[w] = incl;
     __syncthreads();
-    unsigned long long run = part[threadIdx.x];
-    for (int64_t i = lo; i < hi; ++i) { unsigned long long v = block_counts[i]; offsets[i] = (int64_t)run; run += v; }
+    unsigned long long off = 0;
+    for (int q = 0; q < w; ++q) off += wsum[q];
+    const unsigned long long excl = off + incl - s;
+    part[t] = excl;
+    unsigned long long run = excl;
+    for (int64_t i = lo; i < hi; ++i) { const unsigned long long v = block_counts[i]; offsets[i] = (int64_t)run; run += v; }
     __syncthreads();
-    for (int d = threadIdx.x; d < p; d += blockDim.x) {
-        unsigned long long c = 0;
-        for (int64_t b = 0; b < nblk; ++b) c += block_counts[(int64_t)d * nblk + b];
-        counts[d] = (int64_t)c;
-    }
+    // offset of entry i (i <= total) from the thread prefixes
+    auto offset_at = [&](int64_t i) -> unsigned long long {
+        if (i >= total) {
+            unsigned long long tot = 0;
+            for (int q = 0; q < (int)(blockDim.x >> 6); ++q) tot += wsum[q];
+            return tot;
+        }
+        const int64_t th = i / per;
+        unsigned long long o = part[th];
+        for (int64_t j = th * per; j < i; ++j) o += block_counts[j];
+        return o;
+    };
+    for (int d = t; d < p; d += blockDim.x) counts[d] = (int64_t)(offset_at((int64_t)(d + 1) * nblk) - offset_at((int64_t)d * nblk));
 }
 
-// pass 3: stable scatter.  Tile order = it-major then thread, i.e. global order.
 // Packing: bucket 2q holds q's packed words (packed_out), bucket 2q + 1 its other records
 // (key_out | ts_out | val_out), at positions of one shared numbering.
 __global__ void __launch_bounds__(256) k_part_scatter(int64_t n, const int64_t* key, const int32_t* key_hash,

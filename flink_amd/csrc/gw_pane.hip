@@ -651,6 +651,19 @@ __device__ __forceinline__ void publish_status_wave(const DevStatus* st, DevStat
 #else
 #define GW_APPLY_ATTR
 #endif
+// Record i of a batch (key, timestamp, value): from the columns, or decoded from its packed
+// exchange word (gw_ingest_packed_device: records [pk_from, n)).
+__device__ __forceinline__ void load_record(const IngestArgs& a, int64_t i, int64_t& k, int64_t& t, int64_t& v) {
+    if (a.pk_w && i >= a.pk_from) {
+        unpack_word(a.pk_g, a.pk_w[i - a.pk_from], k, t, v);
+        if (!a.val) v = 0;
+    } else {
+        k = a.key[i];
+        t = a.ts[i];
+        v = a.val ? a.val[i] : 0;
+    }
+}
+
 // P1 body for one tile: the records' inputs are in registers (item it of thread x is record
 // lo + it * THR + x); lh[] zeroed and s_occ cleared by the caller, with a barrier after.
 // Classifies, ranks by pass-1 bucket (LDS atomics), sorts the tile in LDS (s) and writes it
@@ -727,8 +740,9 @@ __device__ __forceinline__ void p1_tile(const IngestArgs& a, int64_t g, int64_t 
             int st = REC_SKIP;
             if (i < hi) {
                 unsigned long long dl = 0, df = 0;
-                k = a.key[i];
-                st = classify<AGG, GAP>(a, a.ts[i], a.val ? a.val[i] : 0, ps, pane, v0, v1, dl, df);
+                int64_t t, v;
+                load_record(a, i, k, t, v);
+                st = classify<AGG, GAP>(a, t, v, ps, pane, v0, v1, dl, df);
                 if (C && ACC && st == REC_RING && (v0 < INT32_MIN || v0 > INT32_MAX)) st = REC_DEFER;
                 if (NR && st == REC_RING &&
                     ((uint64_t)k >= (uint64_t)(N4 ? kNarCountKeyLimit : kNarKeyLimit) ||
