@@ -65,6 +65,7 @@ struct SegArgs {
     uint32_t* retry;        // wide pass: runs that did not fit K2 (append at st->overflow)
     DevStatus* st;
     int gshift;             // records are grouped by slot >> gshift (the sort skips the low bits)
+    int exp;                // measurement only (GW_SEG_EXP): 1 no record gathers, 2 no slot write-back
     int64_t* pu_key;        // records of keys the prep found no slot for (arrival order), append at
                             // st->spills: replayed after a regrow
     int64_t* pu_ts;
@@ -300,7 +301,7 @@ __device__ __forceinline__ bool add_element(const SegArgs& a, const SessList& l,
                                             int64_t idx, unsigned long long& late, unsigned long long& merges,
                                             unsigned long long& flags, bool dry = false) {
     struct alignas(16) TsVal { int64_t ts, v; };
-    const TsVal tv = reinterpret_cast<const TsVal*>(a.rec)[idx];
+    const TsVal tv = (a.exp & 1) ? TsVal{a.wm + 1 + (int64_t)(idx & 7), 1} : reinterpret_cast<const TsVal*>(a.rec)[idx];
     return add_element_tv<AGG>(a, l, cnt, cap, key, tv.ts, tv.v, late, merges, flags, dry);
 }
 
@@ -347,6 +348,7 @@ __device__ __forceinline__ void seg_slot(const SegArgs& a, const SessList& l, in
         a.punt[at] = (uint32_t)i;  // the wide pass replays this slot's records from i to the group's end
         return;
     }
+    if (a.exp & 2) return;
     if (cnt <= a.t.ring) {
         uint64_t fired = 0;
         int64_t due = INT64_MAX;
@@ -1628,6 +1630,8 @@ static int ingest_sorted(SessionState* s, int64_t n, const int64_t* key, const i
     if ((rc = group_records(s, n, key, ts, val, &a.slot, &a.perm, err, defer))) return rc;
     a.rec = s->rec;
     a.gshift = s->gshift;
+    static const int seg_exp = getenv("GW_SEG_EXP") ? atoi(getenv("GW_SEG_EXP")) : 0;
+    a.exp = seg_exp;
     a.key = key;
     a.ts = ts;
     a.val = val;
