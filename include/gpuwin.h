@@ -425,7 +425,10 @@ int  gw_partition_device(int64_t n, const int64_t* d_key, const int32_t* d_key_h
                          int64_t* d_key_out, int64_t* d_ts_out, void* d_value_out,
                          int64_t* d_counts, void* d_scratch, void* stream);
 
-/* Packed exchange records: one 8-byte word per record instead of 24 B of key, ts and value
+/* Packed exchange records -- this path's serialized form of the records RecordWriter.emit
+ * ships to the key group's owner (flink-runtime/.../io/network/api/writer/RecordWriter.java:
+ * 104-110, KeyGroupStreamPartitioner.java:55-64), chosen for xGMI: one 8-byte word per record
+ * instead of 24 B of key, ts and value
  *   lo32 = key, hi32 = value << 4 | d        (d = pane - base_pane, 0 <= d < 16)
  * for records whose key is in [0, 2^32), whose value (if the batch has values) is in
  * [-2^27, 2^27), and whose pane floor((ts - offset) / pane) lies in [base_pane, base_pane + 16);
@@ -463,6 +466,8 @@ int  gw_partition_packed_device(int64_t n, const int64_t* d_key, const int64_t* 
 int  gw_unpack_device(int64_t n, const uint64_t* d_words, const gw_pack_geom* g, int64_t* d_key, int64_t* d_ts,
                       int64_t* d_value, void* stream);
 /* gw_ingest_device for a batch of n_other column records followed by n_words packed words
+ * (the receive side of the packed exchange: what StreamTaskNetworkInput deserializes before
+ * WindowOperator.processElement, WindowOperator.java:293-447, sees record by record)
  * (gw_exchange_last_words): the words' timestamps are their panes' starts (gw_pack_geom).  A
  * plain pane operator's region pass 1 decodes the words itself; other paths and handles
  * (sessions, window classes, first-element, the late side output) get them unpacked first.
