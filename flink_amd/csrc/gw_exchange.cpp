@@ -24,6 +24,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -33,6 +34,7 @@ using namespace gw;
 struct gw_exchange {
     ncclComm_t comm = nullptr;
     int32_t nranks = 0, rank = 0, device = 0, max_p = 128;
+    bool no_regions = false;  // GW_PART_REGIONS=0: the three-pass contiguous partition (A/B)
     void* scratch = nullptr;  // partition scratch
     int64_t scratch_bytes = 0;
     int64_t* part = nullptr;  // partitioned key | ts | value columns, cap records each
@@ -105,6 +107,7 @@ int gw_exchange_create(gw_exchange** out, int32_t nranks, int32_t rank, const vo
     gw_exchange* ex = new gw_exchange();
     ex->nranks = nranks;
     ex->rank = rank;
+    if (const char* e = getenv("GW_PART_REGIONS")) ex->no_regions = atoi(e) == 0;
     ex->device = device;
     ex->max_p = max_parallelism;
     auto bail = [&](int rc) { gw_exchange_destroy(ex); return rc; };
@@ -269,7 +272,11 @@ int gw_exchange_batch(gw_exchange* ex, int64_t n, const int64_t* d_key, const in
     if (ex->pack_on && !d_key_hash && (!d_value || ex->pack_values))
         (void)gw_pack_geom_init(&g, ex->pack_size, ex->pack_slide, ex->pack_offset, ex->last_wm);
     const bool packed = g.enabled != 0;
-    // 1. stable device partition by owner (packing: by owner, then packed / not)
+    // 1. stable device partition by owner (packing: by owner, then packed / not).  Up to
+    // kPartRegionMaxOwners ranks into one region per owner (single pass, buffers P times the
+    // batch: 36 B x P per record of capacity), beyond that the contiguous three-pass layout.
+    const bool regions = P <= kPartRegionMaxOwners && !ex->no_regions;
+    const int64_t R = regions ? P : 1;
     if (n > ex->part_cap) {
         EX_HIP(hipStreamSynchronize(s));
         hipFree(ex->part);
@@ -279,11 +286,11 @@ int gw_exchange_batch(gw_exchange* ex, int64_t n, const int64_t* d_key, const in
         ex->part_hash = nullptr;
         ex->part_packed = nullptr;
         const int64_t c = n + n / 4 + 1024;
-        EX_HIP(hipMalloc((void**)&ex->part, (size_t)c * 3 * 8));
-        EX_HIP(hipMalloc((void**)&ex->part_hash, (size_t)c * 4));
+        EX_HIP(hipMalloc((void**)&ex->part, (size_t)c * R * 3 * 8));
+        EX_HIP(hipMalloc((void**)&ex->part_hash, (size_t)c * R * 4));
         ex->part_cap = c;
     }
-    if (packed && !ex->part_packed) EX_HIP(hipMalloc((void**)&ex->part_packed, (size_t)ex->part_cap * 8));
+    if (packed && !ex->part_packed) EX_HIP(hipMalloc((void**)&ex->part_packed, (size_t)ex->part_cap * R * 8));
     const int64_t need = partition_scratch_bytes(std::max<int64_t>(n, 1), 2 * P);
     if (need > ex->scratch_bytes) {
         EX_HIP(hipStreamSynchronize(s));
@@ -292,10 +299,15 @@ int gw_exchange_batch(gw_exchange* ex, int64_t n, const int64_t* d_key, const in
         EX_HIP(hipMalloc(&ex->scratch, (size_t)need));
         ex->scratch_bytes = need;
     }
+    const int64_t col = ex->part_cap * R;  // one column of the partition buffer
     int64_t* pk = ex->part;
-    int64_t* pt = pk + ex->part_cap;
-    int64_t* pv = pt + ex->part_cap;
-    if (n > 0) {
+    int64_t* pt = pk + col;
+    int64_t* pv = pt + col;
+    if (n > 0 && regions) {
+        EX_HIP(launch_partition_regions(n, d_key, d_key_hash, d_ts, d_value, ex->max_p, P, ex->part_cap, pk, pt,
+                                        d_value ? pv : nullptr, d_key_hash ? ex->part_hash : nullptr,
+                                        packed ? &g : nullptr, ex->part_packed, ex->d_counts, ex->scratch, s));
+    } else if (n > 0) {
         EX_HIP(launch_partition(n, d_key, d_key_hash, d_ts, d_value, ex->max_p, P, pk, pt, d_value ? pv : nullptr,
                                 ex->d_counts, ex->scratch, s, d_key_hash ? ex->part_hash : nullptr,
                                 packed ? &g : nullptr, ex->part_packed));
@@ -362,23 +374,42 @@ int gw_exchange_batch(gw_exchange* ex, int64_t n, const int64_t* d_key, const in
                          {pt, rt, ncclInt64, 8},
                          {d_value ? pv : nullptr, rv, ncclInt64, 8},
                          {d_key_hash ? ex->part_hash : nullptr, rh, ncclInt32, 4}};
+    // The rank's own share does not leave the device: a device-to-device copy on the same
+    // stream (the copy engine path runs at HBM speed; RCCL's send/receive to self ran its
+    // copy on a few channels, ~1 TB/s), queued after the group so it overlaps nothing it must
+    // not.  At P ranks it is 1/P of the records.
+    const int me = ex->rank;
+    // where peer q's packed words / other records start in the partition buffers
+    auto pw_off = [&](int q) -> int64_t { return regions ? q * ex->part_cap : so[q]; };
+    auto pc_off = [&](int q) -> int64_t { return regions ? q * ex->part_cap : so[q] + sp[q]; };
     EX_NCCL(ncclGroupStart());
     ncclResult_t r = ncclSuccess;
     for (int q = 0; q < P && r == ncclSuccess && packed; ++q) {
-        if (sp[q]) r = ncclSend(ex->part_packed + so[q], (size_t)sp[q], ncclUint64, q, ex->comm, s);
+        if (q == me) continue;
+        if (sp[q]) r = ncclSend(ex->part_packed + pw_off(q), (size_t)sp[q], ncclUint64, q, ex->comm, s);
         if (r == ncclSuccess && rp[q]) r = ncclRecv(ex->recv_packed[u] + rpo[q], (size_t)rp[q], ncclUint64, q, ex->comm, s);
     }
     for (const Col& c : cols) {
         if (!c.src) continue;
         for (int q = 0; q < P && r == ncclSuccess; ++q) {
+            if (q == me) continue;
             const int64_t ns = sc[q] - sp[q], nr = rc[q] - rp[q];
-            if (ns) r = ncclSend((const char*)c.src + (so[q] + sp[q]) * c.w, (size_t)ns, c.t, q, ex->comm, s);
+            if (ns) r = ncclSend((const char*)c.src + pc_off(q) * c.w, (size_t)ns, c.t, q, ex->comm, s);
             if (r == ncclSuccess && nr) r = ncclRecv((char*)c.dst + rwo[q] * c.w, (size_t)nr, c.t, q, ex->comm, s);
         }
     }
     const ncclResult_t re = ncclGroupEnd();
     if (r != ncclSuccess) return ex_fail(ex, GW_E_DEVICE, std::string("ncclSend/ncclRecv: ") + ncclGetErrorString(r));
     if (re != ncclSuccess) return ex_fail(ex, GW_E_DEVICE, std::string("ncclGroupEnd: ") + ncclGetErrorString(re));
+    if (packed && sp[me])  // send count = receive count for the rank itself
+        EX_HIP(hipMemcpyAsync(ex->recv_packed[u] + rpo[me], ex->part_packed + pw_off(me), (size_t)sp[me] * 8,
+                              hipMemcpyDeviceToDevice, s));
+    for (const Col& c : cols) {
+        const int64_t ns = sc[me] - sp[me];
+        if (c.src && ns)
+            EX_HIP(hipMemcpyAsync((char*)c.dst + rwo[me] * c.w, (const char*)c.src + pc_off(me) * c.w,
+                                  (size_t)ns * c.w, hipMemcpyDeviceToDevice, s));
+    }
     ex->last_words = nullptr;
     ex->last_geom = g;
     if (packed && tp > 0) {

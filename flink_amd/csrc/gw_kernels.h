@@ -351,6 +351,14 @@ int64_t partition_scratch_bytes(int64_t n, int32_t p);
 // [kg_lo, kg_hi] when check_range (out[1] must start at ~0)
 hipError_t launch_check_keys(int64_t n, const int64_t* key, const int32_t* key_hash, int32_t max_p, int32_t kg_lo,
                              int32_t kg_hi, int check_range, unsigned long long* out, hipStream_t s);
+// Stable single-pass partition into per-owner regions of capacity cap (n <= cap, p <=
+// kPartRegionMaxOwners): owner q's packed words at packed_out + q * cap, its other records at
+// the columns + q * cap; counts as launch_partition's.  scratch: partition_scratch_bytes(n, nd).
+constexpr int32_t kPartRegionMaxOwners = 16;
+hipError_t launch_partition_regions(int64_t n, const int64_t* key, const int32_t* key_hash, const int64_t* ts,
+                                    const int64_t* val, int32_t max_p, int32_t p, int64_t cap, int64_t* key_out,
+                                    int64_t* ts_out, int64_t* val_out, int32_t* hash_out, const PackGeom* pack,
+                                    uint64_t* packed_out, int64_t* counts, void* scratch, hipStream_t s);
 // Stable partition by owner.  pack (enabled): 2p buckets -- 2q: q's packed words in
 // packed_out, 2q + 1: q's other records in the columns -- at positions of one numbering;
 // counts[2q], counts[2q + 1] their sizes.

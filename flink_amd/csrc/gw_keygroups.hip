@@ -10,19 +10,13 @@
 // The partition is a stable counting sort of the record columns by destination
 // subtask (= GPU rank), the send-side half of the RCCL all-to-all that replaces the
 // Netty keyBy shuffle.  Three passes: per-block histogram, one-block scan, stable
-// scatter (wave64 ballot matching for in-wave ranks).
+// scatter (wave64 ballot matching for in-wave ranks, the tile ranked in LDS before any store).
 #include "gw_kernels.h"
 
 namespace gw {
 
 constexpr int kPartMaxDest = 256;
 constexpr int kPartItems = 8;  // records per thread per block tile
-
-__device__ __forceinline__ int32_t owner_of(const int64_t* key, const int32_t* key_hash, int64_t i,
-                                            int32_t max_p, int32_t p) {
-    const int32_t h = key_hash ? key_hash[i] : java_long_hash(key[i]);
-    return operator_for_key_group(max_p, p, key_group_for_hash(h, max_p));
-}
 
 __global__ void __launch_bounds__(256) k_key_groups(int64_t n, const int64_t* key, const int32_t* key_hash,
                                                     int32_t max_p, int32_t p, int32_t* kg, int32_t* owner) {
@@ -35,28 +29,68 @@ __global__ void __launch_bounds__(256) k_key_groups(int64_t n, const int64_t* ke
     }
 }
 
-// Destination bucket of record i: its owner, or (packing) 2 * owner + (does not fit).
-__device__ __forceinline__ int32_t dest_of(const int64_t* key, const int32_t* key_hash, const int64_t* ts,
-                                           const int64_t* val, int64_t i, int32_t max_p, int32_t p,
-                                           const PackGeom& g, uint64_t& w) {
-    const int32_t o = owner_of(key, key_hash, i, max_p, p);
-    if (!g.enabled) return o;
-    return 2 * o + (pack_word(g, key[i], ts[i], val != nullptr, val ? val[i] : 0, w) ? 0 : 1);
+// Bits that tell destinations 0..nd-1 apart: wave peer matching needs only these ballots
+// (one at a single owner with packing, four at eight owners), not eight.
+__host__ __device__ inline int dest_bits(int32_t nd) {
+    int b = 0;
+    while ((1 << b) < nd) ++b;
+    return b;
 }
 
-// pass 1: counts[block][dest]
+// Lanes of this wave with destination d (valid lanes only).
+__device__ __forceinline__ unsigned long long wave_peers(bool valid, int32_t d, int nbits) {
+    unsigned long long peers = __ballot(valid);
+    for (int b = 0; b < nbits; ++b) {
+        const bool bit = (d >> b) & 1;
+        const unsigned long long bb = __ballot(bit);
+        peers &= bit ? bb : ~bb;
+    }
+    return peers;
+}
+
+// Destination bucket of one record from its loaded columns: its owner, or (packing)
+// 2 * owner + (does not fit).
+__device__ __forceinline__ int32_t dest_rec(int64_t k, int32_t kh, bool has_hash, int64_t t, bool has_val, int64_t v,
+                                            int32_t max_p, int32_t p, const PackGeom& g, uint64_t& w) {
+    const int32_t h = has_hash ? kh : java_long_hash(k);
+    const int32_t o = operator_for_key_group(max_p, p, key_group_for_hash(h, max_p));
+    if (!g.enabled) return o;
+    return 2 * o + (pack_word(g, k, t, has_val, has_val ? v : 0, w) ? 0 : 1);
+}
+
+// pass 1: counts[block][dest].  The tile's columns are loaded before any counting (all loads
+// in flight at once), and each wave adds its peers' count once per destination instead of one
+// LDS atomic per record (one owner: every record of a wave hits the same counter).
 __global__ void __launch_bounds__(256) k_part_hist(int64_t n, const int64_t* key, const int32_t* key_hash,
                                                    const int64_t* ts, const int64_t* val, int32_t max_p, int32_t p,
                                                    PackGeom g, uint32_t* block_counts) {
     __shared__ uint32_t h[kPartMaxDest];
     const int32_t nd = g.enabled ? 2 * p : p;
+    const int nbits = dest_bits(nd);
     for (int d = threadIdx.x; d < nd; d += blockDim.x) h[d] = 0;
-    __syncthreads();
-    const int64_t t0 = (int64_t)blockIdx.x * blockDim.x * kPartItems;
+    const int64_t t0 = (int64_t)blockIdx.x * blockDim.x * kPartItems + threadIdx.x;
+    const bool has_hash = key_hash != nullptr, has_val = val != nullptr;
+    int64_t kk[kPartItems], tt[kPartItems], vv[kPartItems];
+    int32_t hh[kPartItems];
+#pragma unroll
     for (int it = 0; it < kPartItems; ++it) {
-        const int64_t i = t0 + (int64_t)it * blockDim.x + threadIdx.x;
+        const int64_t i = t0 + (int64_t)it * blockDim.x;
+        const bool ok = i < n;
+        kk[it] = ok && !has_hash ? key[i] : 0;
+        hh[it] = ok && has_hash ? key_hash[i] : 0;
+        tt[it] = ok && g.enabled ? ts[i] : 0;
+        vv[it] = ok && g.enabled && has_val ? val[i] : 0;
+    }
+    __syncthreads();
+    const int lane = __lane_id();
+#pragma unroll
+    for (int it = 0; it < kPartItems; ++it) {
+        const int64_t i = t0 + (int64_t)it * blockDim.x;
+        const bool ok = i < n;
         uint64_t w;
-        if (i < n) atomicAdd(&h[dest_of(key, key_hash, ts, val, i, max_p, p, g, w)], 1u);
+        const int32_t d = ok ? dest_rec(kk[it], hh[it], has_hash, tt[it], has_val, vv[it], max_p, p, g, w) : 0;
+        const unsigned long long peers = wave_peers(ok, d, nbits);
+        if (ok && __popcll(peers & ((1ull << lane) - 1ull)) == 0) atomicAdd(&h[d], (uint32_t)__popcll(peers));
     }
     __syncthreads();
     for (int d = threadIdx.x; d < nd; d += blockDim.x) block_counts[(int64_t)d * gridDim.x + blockIdx.x] = h[d];
@@ -108,52 +142,181 @@ __global__ void __launch_bounds__(1024) k_part_scan(uint32_t* block_counts, int6
 }
 
 // Packing: bucket 2q holds q's packed words (packed_out), bucket 2q + 1 its other records
-// (key_out | ts_out | val_out), at positions of one shared numbering.
+// (key_out | ts_out | val_out), at positions of one shared numbering.  The whole tile is
+// loaded and ranked before any store: per (item, wave, destination) the wave's peer count goes
+// to LDS, one thread per destination turns the counts into tile-relative offsets in (item,
+// wave) order -- which keeps the partition stable -- and every record is stored at its
+// block offset + that offset + its rank among its wave's peers: two barriers per tile rather
+// than three per item.  Dynamic LDS: kPartItems * 4 * nd counts + nd block offsets.
 __global__ void __launch_bounds__(256) k_part_scatter(int64_t n, const int64_t* key, const int32_t* key_hash,
                                                       const int64_t* ts, const int64_t* val, int32_t max_p,
                                                       int32_t p_owners, PackGeom g, const int64_t* offsets,
                                                       int64_t* key_out, int64_t* ts_out, int64_t* val_out,
                                                       int32_t* hash_out, uint64_t* packed_out) {
-    __shared__ int64_t cursor[kPartMaxDest];
-    __shared__ uint32_t wave_cnt[4][kPartMaxDest];
+    extern __shared__ int64_t part_lds[];
+    const int32_t nd = g.enabled ? 2 * p_owners : p_owners;  // buckets
+    int64_t* base = part_lds;                                 // [nd]
+    uint32_t* cnt = (uint32_t*)(part_lds + nd);               // [kPartItems][4][nd]
     const int lane = __lane_id();
     const int wave = threadIdx.x >> 6;
-    const int32_t p = g.enabled ? 2 * p_owners : p_owners;  // buckets
-    for (int d = threadIdx.x; d < p; d += blockDim.x) cursor[d] = offsets[(int64_t)d * gridDim.x + blockIdx.x];
-    const int64_t t0 = (int64_t)blockIdx.x * blockDim.x * kPartItems;
+    const int nbits = dest_bits(nd);
+    for (int d = threadIdx.x; d < nd; d += blockDim.x) base[d] = offsets[(int64_t)d * gridDim.x + blockIdx.x];
+    for (int e = threadIdx.x; e < kPartItems * 4 * nd; e += blockDim.x) cnt[e] = 0;
+    const int64_t t0 = (int64_t)blockIdx.x * blockDim.x * kPartItems + threadIdx.x;
+    const bool has_hash = key_hash != nullptr, has_val = val != nullptr;
+    int64_t kk[kPartItems], tt[kPartItems], vv[kPartItems];
+    int32_t hh[kPartItems];
+#pragma unroll
     for (int it = 0; it < kPartItems; ++it) {
-        for (int d = threadIdx.x; d < 4 * p; d += blockDim.x) wave_cnt[d / p][d % p] = 0;
-        __syncthreads();
-        const int64_t i = t0 + (int64_t)it * blockDim.x + threadIdx.x;
-        const bool valid = i < n;
-        uint64_t w = 0;
-        const int32_t d = valid ? dest_of(key, key_hash, ts, val, i, max_p, p_owners, g, w) : -1;
-        // peers: lanes of this wave with the same destination (8 ballots cover p <= 256)
-        unsigned long long peers = __ballot(valid);
-        for (int b = 0; b < 8; ++b) {
-            const bool bit = (d >> b) & 1;
-            const unsigned long long bb = __ballot(bit);
-            peers &= bit ? bb : ~bb;
+        const int64_t i = t0 + (int64_t)it * blockDim.x;
+        const bool ok = i < n;
+        kk[it] = ok ? key[i] : 0;
+        tt[it] = ok ? ts[i] : 0;
+        vv[it] = ok && has_val ? val[i] : 0;
+        hh[it] = ok && has_hash ? key_hash[i] : 0;
+    }
+    __syncthreads();  // base / cnt initialised
+    int32_t dd[kPartItems];
+    uint32_t rk[kPartItems];
+    uint64_t ww[kPartItems];
+#pragma unroll
+    for (int it = 0; it < kPartItems; ++it) {
+        const int64_t i = t0 + (int64_t)it * blockDim.x;
+        const bool ok = i < n;
+        ww[it] = 0;
+        dd[it] = ok ? dest_rec(kk[it], hh[it], has_hash, tt[it], has_val, vv[it], max_p, p_owners, g, ww[it]) : -1;
+        const unsigned long long peers = wave_peers(ok, dd[it], nbits);
+        rk[it] = (uint32_t)__popcll(peers & ((1ull << lane) - 1ull));
+        if (ok && rk[it] == 0) cnt[(it * 4 + wave) * nd + dd[it]] = (uint32_t)__popcll(peers);
+    }
+    __syncthreads();
+    for (int d = threadIdx.x; d < nd; d += blockDim.x) {
+        uint32_t run = 0;
+        for (int e = 0; e < kPartItems * 4; ++e) {
+            const uint32_t c = cnt[e * nd + d];
+            cnt[e * nd + d] = run;
+            run += c;
         }
-        const unsigned rank_in_wave = (unsigned)__popcll(peers & ((1ull << lane) - 1ull));
-        if (valid && rank_in_wave == 0) wave_cnt[wave][d] = (uint32_t)__popcll(peers);
-        __syncthreads();
-        if (valid) {
-            int64_t pos = cursor[d] + rank_in_wave;
-            for (int q = 0; q < wave; ++q) pos += wave_cnt[q][d];
-            if (g.enabled && !(d & 1)) {
-                packed_out[pos] = w;
-            } else {
-                key_out[pos] = key[i];
-                ts_out[pos] = ts[i];
-                if (val) val_out[pos] = val[i];
-                if (hash_out) hash_out[pos] = key_hash[i];
-            }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int it = 0; it < kPartItems; ++it) {
+        const int32_t d = dd[it];
+        if (d < 0) continue;
+        const int64_t pos = base[d] + cnt[(it * 4 + wave) * nd + d] + rk[it];
+        if (g.enabled && !(d & 1)) {
+            packed_out[pos] = ww[it];
+        } else {
+            key_out[pos] = kk[it];
+            ts_out[pos] = tt[it];
+            if (has_val) val_out[pos] = vv[it];
+            if (hash_out) hash_out[pos] = hh[it];
         }
-        __syncthreads();
-        for (int dd = threadIdx.x; dd < p; dd += blockDim.x)
-            cursor[dd] += wave_cnt[0][dd] + wave_cnt[1][dd] + wave_cnt[2][dd] + wave_cnt[3][dd];
-        __syncthreads();
+    }
+}
+
+// Single-pass partition into per-destination regions (the exchange's own layout; the
+// contiguous gw_partition_device layout keeps the three passes above).  Destination q's
+// records go to region q of capacity cap: packed words at packed_out + q * cap, other records
+// at key_out / ts_out / val_out / hash_out + q * cap.  With a region per destination a record's
+// position needs only the counts of the same destination in earlier tiles, so the histogram
+// and scan passes go: tiles are taken in order from a counter (tile_ctr), each publishes its
+// per-destination count and looks back over earlier tiles' published counts (decoupled
+// look-back, as the grouping sort's passes do, gw_sort.hip), and the last tile writes the
+// totals.  status: [ntiles][nd] words, zeroed before the launch.  Costs P * cap records of
+// memory per buffer -- the exchange uses it up to kPartRegionMaxOwners owners.
+constexpr uint64_t kPrLocal = 1ull << 62, kPrIncl = 1ull << 63, kPrMask = kPrLocal - 1;
+
+__device__ __forceinline__ uint64_t part_look_back(const uint64_t* status, int64_t t, int nd, int d) {
+    uint64_t excl = 0;
+    for (int64_t q = t - 1; q >= 0; --q) {
+        uint64_t x = __hip_atomic_load(status + q * nd + d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        while (!(x & (kPrLocal | kPrIncl)))
+            x = __hip_atomic_load(status + q * nd + d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        excl += x & kPrMask;
+        if (x & kPrIncl) break;
+    }
+    return excl;
+}
+
+__global__ void __launch_bounds__(256) k_part_regions(int64_t n, const int64_t* key, const int32_t* key_hash,
+                                                      const int64_t* ts, const int64_t* val, int32_t max_p,
+                                                      int32_t p_owners, PackGeom g, int64_t cap, uint64_t* status,
+                                                      uint32_t* tile_ctr, int64_t ntiles, int64_t* key_out,
+                                                      int64_t* ts_out, int64_t* val_out, int32_t* hash_out,
+                                                      uint64_t* packed_out, int64_t* counts) {
+    extern __shared__ int64_t part_lds[];
+    __shared__ int64_t s_tile;
+    const int32_t nd = g.enabled ? 2 * p_owners : p_owners;
+    int64_t* base = part_lds;                    // [nd]
+    uint32_t* cnt = (uint32_t*)(part_lds + nd);  // [kPartItems][4][nd]
+    const int lane = __lane_id();
+    const int wave = threadIdx.x >> 6;
+    const int nbits = dest_bits(nd);
+    if (threadIdx.x == 0) s_tile = (int64_t)atomicAdd(tile_ctr, 1u);
+    for (int e = threadIdx.x; e < kPartItems * 4 * nd; e += blockDim.x) cnt[e] = 0;
+    __syncthreads();
+    const int64_t tile = s_tile;
+    const int64_t t0 = tile * blockDim.x * kPartItems + threadIdx.x;
+    const bool has_hash = key_hash != nullptr, has_val = val != nullptr;
+    int64_t kk[kPartItems], tt[kPartItems], vv[kPartItems];
+    int32_t hh[kPartItems], dd[kPartItems];
+    uint32_t rk[kPartItems];
+    uint64_t ww[kPartItems];
+#pragma unroll
+    for (int it = 0; it < kPartItems; ++it) {
+        const int64_t i = t0 + (int64_t)it * blockDim.x;
+        const bool ok = i < n;
+        kk[it] = ok ? key[i] : 0;
+        tt[it] = ok ? ts[i] : 0;
+        vv[it] = ok && has_val ? val[i] : 0;
+        hh[it] = ok && has_hash ? key_hash[i] : 0;
+    }
+#pragma unroll
+    for (int it = 0; it < kPartItems; ++it) {
+        const int64_t i = t0 + (int64_t)it * blockDim.x;
+        const bool ok = i < n;
+        ww[it] = 0;
+        dd[it] = ok ? dest_rec(kk[it], hh[it], has_hash, tt[it], has_val, vv[it], max_p, p_owners, g, ww[it]) : -1;
+        const unsigned long long peers = wave_peers(ok, dd[it], nbits);
+        rk[it] = (uint32_t)__popcll(peers & ((1ull << lane) - 1ull));
+        if (ok && rk[it] == 0) cnt[(it * 4 + wave) * nd + dd[it]] = (uint32_t)__popcll(peers);
+    }
+    __syncthreads();
+    for (int d = threadIdx.x; d < nd; d += blockDim.x) {
+        uint32_t run = 0;
+        for (int e = 0; e < kPartItems * 4; ++e) {
+            const uint32_t c = cnt[e * nd + d];
+            cnt[e * nd + d] = run;
+            run += c;
+        }
+        uint64_t* st = status + tile * nd + d;
+        uint64_t excl = 0;
+        if (tile == 0) {
+            __hip_atomic_store(st, (uint64_t)run | kPrIncl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            __hip_atomic_store(st, (uint64_t)run | kPrLocal, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            excl = part_look_back(status, tile, nd, d);
+            __hip_atomic_store(st, (excl + run) | kPrIncl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        base[d] = (int64_t)excl;
+        if (tile == ntiles - 1) counts[d] = (int64_t)(excl + run);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int it = 0; it < kPartItems; ++it) {
+        const int32_t d = dd[it];
+        if (d < 0) continue;
+        const int32_t q = g.enabled ? d >> 1 : d;
+        const int64_t pos = q * cap + base[d] + cnt[(it * 4 + wave) * nd + d] + rk[it];
+        if (g.enabled && !(d & 1)) {
+            packed_out[pos] = ww[it];
+        } else {
+            key_out[pos] = kk[it];
+            ts_out[pos] = tt[it];
+            if (has_val) val_out[pos] = vv[it];
+            if (hash_out) hash_out[pos] = hh[it];
+        }
     }
 }
 
@@ -338,8 +501,32 @@ hipError_t launch_partition(int64_t n, const int64_t* key, const int32_t* key_ha
     int64_t* off = (int64_t*)(((uintptr_t)(bc + nb * nd) + 15) & ~(uintptr_t)15);
     hipLaunchKernelGGL(k_part_hist, dim3((unsigned)nb), dim3(256), 0, s, n, key, key_hash, ts, val, max_p, p, g, bc);
     hipLaunchKernelGGL(k_part_scan, dim3(1), dim3(1024), 0, s, bc, nb, nd, off, counts);
-    hipLaunchKernelGGL(k_part_scatter, dim3((unsigned)nb), dim3(256), 0, s, n, key, key_hash, ts, val, max_p, p, g,
+    const size_t lds = (size_t)nd * 8 + (size_t)kPartItems * 4 * nd * 4;
+    hipLaunchKernelGGL(k_part_scatter, dim3((unsigned)nb), dim3(256), lds, s, n, key, key_hash, ts, val, max_p, p, g,
                        off, key_out, ts_out, val_out, key_hash ? hash_out : nullptr, packed_out);
+    return hipGetLastError();
+}
+
+hipError_t launch_partition_regions(int64_t n, const int64_t* key, const int32_t* key_hash, const int64_t* ts,
+                                    const int64_t* val, int32_t max_p, int32_t p, int64_t cap, int64_t* key_out,
+                                    int64_t* ts_out, int64_t* val_out, int32_t* hash_out, const PackGeom* pack,
+                                    uint64_t* packed_out, int64_t* counts, void* scratch, hipStream_t s) {
+    PackGeom g{};
+    if (pack && pack->enabled) {
+        if (key_hash || !packed_out || pack->pane <= 0) return hipErrorInvalidValue;
+        g = *pack;
+    }
+    const int32_t nd = g.enabled ? 2 * p : p;
+    if (p < 1 || p > kPartRegionMaxOwners || n > cap || n < 1) return hipErrorInvalidValue;
+    const int64_t nb = part_blocks(n);
+    uint64_t* status = (uint64_t*)scratch;
+    uint32_t* ctr = (uint32_t*)(status + nb * nd);
+    hipError_t e = hipMemsetAsync(scratch, 0, (size_t)nb * nd * 8 + 8, s);
+    if (e != hipSuccess) return e;
+    const size_t lds = (size_t)nd * 8 + (size_t)kPartItems * 4 * nd * 4;
+    hipLaunchKernelGGL(k_part_regions, dim3((unsigned)nb), dim3(256), lds, s, n, key, key_hash, ts, val, max_p, p,
+                       g, cap, status, ctr, nb, key_out, ts_out, val_out, key_hash ? hash_out : nullptr, packed_out,
+                       counts);
     return hipGetLastError();
 }
 

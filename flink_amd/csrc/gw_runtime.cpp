@@ -4748,6 +4748,29 @@ int gw_partition_packed_device(int64_t n, const int64_t* d_key, const int64_t* d
     return GW_OK;
 }
 
+int gw_partition_regions_device(int64_t n, const int64_t* d_key, const int64_t* d_ts, const int64_t* d_value,
+                                int32_t max_p, int32_t p, const gw_pack_geom* g, int64_t cap, uint64_t* d_packed_out,
+                                int64_t* d_key_out, int64_t* d_ts_out, int64_t* d_value_out, int64_t* d_counts,
+                                void* d_scratch, void* stream) {
+    const bool packed = g && g->enabled;
+    if (n < 0 || max_p <= 0 || p <= 0 || p > max_p || p > kPartRegionMaxOwners || !d_counts || cap < n ||
+        (packed && g->pane <= 0))
+        return GW_E_INVALID;
+    hipStream_t s = (hipStream_t)stream;
+    if (n == 0) {
+        hipError_t e = hipMemsetAsync(d_counts, 0, (size_t)(packed ? 2 : 1) * p * 8, s);
+        return e == hipSuccess ? GW_OK : GW_E_DEVICE;
+    }
+    if (!d_key || !d_ts || (packed && !d_packed_out) || !d_key_out || !d_ts_out || (d_value && !d_value_out) ||
+        !d_scratch)
+        return GW_E_INVALID;
+    hipError_t e = launch_partition_regions(n, d_key, nullptr, d_ts, d_value, max_p, p, cap, d_key_out, d_ts_out,
+                                            d_value_out, nullptr, packed ? g : nullptr, d_packed_out, d_counts,
+                                            d_scratch, s);
+    if (e != hipSuccess) { g_create_error = hipGetErrorString(e); return GW_E_DEVICE; }
+    return GW_OK;
+}
+
 int gw_unpack_device(int64_t n, const uint64_t* d_words, const gw_pack_geom* g, int64_t* d_key, int64_t* d_ts,
                      int64_t* d_value, void* stream) {
     if (n < 0 || !g || !g->enabled || g->pane <= 0 || (n > 0 && (!d_words || !d_key || !d_ts))) return GW_E_INVALID;

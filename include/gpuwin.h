@@ -463,6 +463,16 @@ int  gw_partition_packed_device(int64_t n, const int64_t* d_key, const int64_t* 
                                 int32_t max_parallelism, int32_t parallelism, const gw_pack_geom* g,
                                 uint64_t* d_packed_out, int64_t* d_key_out, int64_t* d_ts_out, int64_t* d_value_out,
                                 int64_t* d_counts, void* d_scratch, void* stream);
+/* The exchange's single-pass partition (ranks <= 16): owner q's records go to region q of
+ * capacity cap >= n -- its packed words (g enabled, else none) at d_packed_out + q * cap, its
+ * other records at d_key_out / d_ts_out / d_value_out + q * cap, both in arrival order; d_counts
+ * as gw_partition_packed_device's ([2p] with g enabled, else [p]).  No histogram pass: a
+ * region per owner lets each tile's positions follow from earlier tiles' counts alone.  g may
+ * be NULL (no packing); scratch: gw_partition_scratch_bytes(n, 2p). */
+int  gw_partition_regions_device(int64_t n, const int64_t* d_key, const int64_t* d_ts, const int64_t* d_value,
+                                 int32_t max_parallelism, int32_t parallelism, const gw_pack_geom* g, int64_t cap,
+                                 uint64_t* d_packed_out, int64_t* d_key_out, int64_t* d_ts_out,
+                                 int64_t* d_value_out, int64_t* d_counts, void* d_scratch, void* stream);
 int  gw_unpack_device(int64_t n, const uint64_t* d_words, const gw_pack_geom* g, int64_t* d_key, int64_t* d_ts,
                       int64_t* d_value, void* stream);
 /* gw_ingest_device for a batch of n_other column records followed by n_words packed words
