@@ -229,14 +229,20 @@ constexpr uint64_t kPrLocal = 1ull << 62, kPrIncl = 1ull << 63, kPrMask = kPrLoc
 
 __device__ __forceinline__ uint64_t part_look_back(const uint64_t* status, int64_t t, int nd, int d) {
     uint64_t excl = 0;
-    for (int64_t q = t - 1; q >= 0; --q) {
-        uint64_t x = __hip_atomic_load(status + q * nd + d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        while (!(x & (kPrLocal | kPrIncl)))
-            x = __hip_atomic_load(status + q * nd + d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        excl += x & kPrMask;
-        if (x & kPrIncl) break;
+    for (int64_t q = t - 1;; q -= 4) {  // four earlier tiles' words per round trip
+        uint64_t x[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            x[j] = q - j >= 0 ? __hip_atomic_load(status + (q - j) * nd + d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                              : kPrIncl;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            while (!(x[j] & (kPrLocal | kPrIncl)))
+                x[j] = __hip_atomic_load(status + (q - j) * nd + d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            excl += x[j] & kPrMask;
+            if (x[j] & kPrIncl) return excl;
+        }
     }
-    return excl;
 }
 
 __global__ void __launch_bounds__(256) k_part_regions(int64_t n, const int64_t* key, const int32_t* key_hash,
