@@ -70,6 +70,31 @@ def test_pack_rule_and_round_trip(size, slide, offset, with_values):
         assert np.array_equal(uv, vals[fits])
 
 
+@pytest.mark.parametrize("pane,offset,wm", [(1 << 40, -(1 << 45) + 3, (1 << 61) - 12345),
+                                             (1 << 58, 17, -(1 << 61)),
+                                             ((1 << 59) + 7, -5, (1 << 61) + 99),  # 16 * pane overflows
+                                             (3, -(1 << 61), -(1 << 61) + 10),
+                                             (999_983, (1 << 61) - 1, -(1 << 61))])
+def test_pack_rule_extreme_geometry(pane, offset, wm):
+    """The pane offset without a 64-bit division (compares against base_pane * pane + k * pane)
+    equals floor division, and the division path where those products overflow."""
+    rng = np.random.default_rng(pane % 1000)
+    g = N.pack_geom(pane, pane, offset, wm)
+    assert g.pane == pane and g.base_pane == (wm - offset) // pane
+    n = 20_000
+    keys = rng.integers(0, 1 << 32, n)
+    start = g.base_pane * pane + offset if abs(g.base_pane) < (1 << 62) // pane else wm
+    span = min(pane, 1 << 40)
+    ts = np.clip(start + rng.integers(-2 * span, 18 * span, n, dtype=np.int64) * max(pane // span, 1)
+                 + rng.integers(-2, 3, n), -LIM - 2, LIM + 2).astype(np.int64)
+    ts[:6] = [start, start - 1, start + 16 * pane - 1 if 16 * pane < LIM else LIM - 1, LIM - 1, -LIM, wm]
+    w, fits = N.pack_records(keys, ts, None, g)
+    ew, efits = np_pack(keys, ts, None, pane, offset, g.base_pane)
+    assert np.array_equal(fits, efits)
+    assert np.array_equal(w[fits], ew[fits])
+    assert 0.1 < fits.mean() < 0.9
+
+
 def test_geometry_that_does_not_pack():
     assert N.pack_geom(100, 300, 0, 5000) is None  # size < slide: gaps between windows
     assert N.pack_geom(100, 100, 0, -(1 << 63)) is None  # no watermark yet
