@@ -34,7 +34,8 @@ using namespace gw;
 struct gw_exchange {
     ncclComm_t comm = nullptr;
     int32_t nranks = 0, rank = 0, device = 0, max_p = 128;
-    bool no_regions = false;  // GW_PART_REGIONS=0: the three-pass contiguous partition (A/B)
+    bool no_regions = false;
+    int part_turn = 0;  // status half of the next region partition  // GW_PART_REGIONS=0: the three-pass contiguous partition (A/B)
     void* scratch = nullptr;  // partition scratch
     int64_t scratch_bytes = 0;
     int64_t* part = nullptr;  // partitioned key | ts | value columns, cap records each
@@ -291,13 +292,18 @@ int gw_exchange_batch(gw_exchange* ex, int64_t n, const int64_t* d_key, const in
         ex->part_cap = c;
     }
     if (packed && !ex->part_packed) EX_HIP(hipMalloc((void**)&ex->part_packed, (size_t)ex->part_cap * R * 8));
-    const int64_t need = partition_scratch_bytes(std::max<int64_t>(n, 1), 2 * P);
+    const int64_t need = regions ? partition_regions_scratch_bytes(ex->part_cap, 2 * P)
+                                 : partition_scratch_bytes(std::max<int64_t>(n, 1), 2 * P);
     if (need > ex->scratch_bytes) {
         EX_HIP(hipStreamSynchronize(s));
         hipFree(ex->scratch);
         ex->scratch = nullptr;
         EX_HIP(hipMalloc(&ex->scratch, (size_t)need));
         ex->scratch_bytes = need;
+        if (regions) {  // both status halves start zeroed; each launch then zeroes the next's
+            EX_HIP(hipMemsetAsync(ex->scratch, 0, (size_t)need, s));
+            ex->part_turn = 0;
+        }
     }
     const int64_t col = ex->part_cap * R;  // one column of the partition buffer
     int64_t* pk = ex->part;
@@ -306,7 +312,9 @@ int gw_exchange_batch(gw_exchange* ex, int64_t n, const int64_t* d_key, const in
     if (n > 0 && regions) {
         EX_HIP(launch_partition_regions(n, d_key, d_key_hash, d_ts, d_value, ex->max_p, P, ex->part_cap, pk, pt,
                                         d_value ? pv : nullptr, d_key_hash ? ex->part_hash : nullptr,
-                                        packed ? &g : nullptr, ex->part_packed, ex->d_counts, ex->scratch, s));
+                                        packed ? &g : nullptr, ex->part_packed, ex->d_counts, ex->scratch, s,
+                                        ex->part_turn, 2 * P));
+        ex->part_turn ^= 1;
     } else if (n > 0) {
         EX_HIP(launch_partition(n, d_key, d_key_hash, d_ts, d_value, ex->max_p, P, pk, pt, d_value ? pv : nullptr,
                                 ex->d_counts, ex->scratch, s, d_key_hash ? ex->part_hash : nullptr,

@@ -358,7 +358,12 @@ constexpr int32_t kPartRegionMaxOwners = 16;
 hipError_t launch_partition_regions(int64_t n, const int64_t* key, const int32_t* key_hash, const int64_t* ts,
                                     const int64_t* val, int32_t max_p, int32_t p, int64_t cap, int64_t* key_out,
                                     int64_t* ts_out, int64_t* val_out, int32_t* hash_out, const PackGeom* pack,
-                                    uint64_t* packed_out, int64_t* counts, void* scratch, hipStream_t s);
+                                    uint64_t* packed_out, int64_t* counts, void* scratch, hipStream_t s,
+                                    int turn = -1, int32_t nd_max = 0);
+// turn >= 0 (a caller launching repeatedly on one stream, alternating turn): scratch of
+// partition_regions_scratch_bytes(cap, nd_max), zeroed once at allocation; each launch zeroes
+// the half the next one uses (no memset per launch).  turn < 0: a memset of this launch's words.
+int64_t partition_regions_scratch_bytes(int64_t cap, int32_t nd);
 // Stable partition by owner.  pack (enabled): 2p buckets -- 2q: q's packed words in
 // packed_out, 2q + 1: q's other records in the columns -- at positions of one numbering;
 // counts[2q], counts[2q + 1] their sizes.

@@ -13,6 +13,8 @@
 // scatter (wave64 ballot matching for in-wave ranks, the tile ranked in LDS before any store).
 #include "gw_kernels.h"
 
+#include <algorithm>
+
 namespace gw {
 
 constexpr int kPartMaxDest = 256;
@@ -250,7 +252,8 @@ __global__ void __launch_bounds__(256) k_part_regions(int64_t n, const int64_t* 
                                                       int32_t p_owners, PackGeom g, int64_t cap, uint64_t* status,
                                                       uint32_t* tile_ctr, int64_t ntiles, int64_t* key_out,
                                                       int64_t* ts_out, int64_t* val_out, int32_t* hash_out,
-                                                      uint64_t* packed_out, int64_t* counts) {
+                                                      uint64_t* packed_out, int64_t* counts, uint64_t* zero_next,
+                                                      int64_t zero_words) {
     extern __shared__ int64_t part_lds[];
     __shared__ int64_t s_tile;
     const int32_t nd = g.enabled ? 2 * p_owners : p_owners;
@@ -261,6 +264,10 @@ __global__ void __launch_bounds__(256) k_part_regions(int64_t n, const int64_t* 
     const int nbits = dest_bits(nd);
     if (threadIdx.x == 0) s_tile = (int64_t)atomicAdd(tile_ctr, 1u);
     for (int e = threadIdx.x; e < kPartItems * 4 * nd; e += blockDim.x) cnt[e] = 0;
+    // the other status half (the previous launch's, done): zeroed here for the next launch
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < zero_words;
+         e += (int64_t)gridDim.x * blockDim.x)
+        zero_next[e] = 0;
     __syncthreads();
     const int64_t tile = s_tile;
     const int64_t t0 = tile * blockDim.x * kPartItems + threadIdx.x;
@@ -513,26 +520,41 @@ hipError_t launch_partition(int64_t n, const int64_t* key, const int32_t* key_ha
     return hipGetLastError();
 }
 
+int64_t partition_regions_scratch_bytes(int64_t cap, int32_t nd) {
+    return 2 * (part_blocks(std::max<int64_t>(cap, 1)) * nd + 8) * 8;
+}
+
 hipError_t launch_partition_regions(int64_t n, const int64_t* key, const int32_t* key_hash, const int64_t* ts,
                                     const int64_t* val, int32_t max_p, int32_t p, int64_t cap, int64_t* key_out,
                                     int64_t* ts_out, int64_t* val_out, int32_t* hash_out, const PackGeom* pack,
-                                    uint64_t* packed_out, int64_t* counts, void* scratch, hipStream_t s) {
+                                    uint64_t* packed_out, int64_t* counts, void* scratch, hipStream_t s, int turn,
+                                    int32_t nd_max) {
     PackGeom g{};
     if (pack && pack->enabled) {
         if (key_hash || !packed_out || pack->pane <= 0) return hipErrorInvalidValue;
         g = *pack;
     }
     const int32_t nd = g.enabled ? 2 * p : p;
-    if (p < 1 || p > kPartRegionMaxOwners || n > cap || n < 1) return hipErrorInvalidValue;
+    if (p < 1 || p > kPartRegionMaxOwners || n > cap || n < 1 || (turn >= 0 && nd > nd_max))
+        return hipErrorInvalidValue;
     const int64_t nb = part_blocks(n);
-    uint64_t* status = (uint64_t*)scratch;
+    uint64_t *status, *zero_next = nullptr;
+    int64_t zero_words = 0;
+    if (turn < 0) {  // stateless: zero this launch's words first
+        status = (uint64_t*)scratch;
+        hipError_t e = hipMemsetAsync(scratch, 0, (size_t)(nb * nd + 1) * 8, s);
+        if (e != hipSuccess) return e;
+    } else {  // two halves sized for cap: this launch's (zeroed by the last) and the next's
+        const int64_t half = part_blocks(cap) * nd_max + 8;
+        status = (uint64_t*)scratch + (turn & 1) * half;
+        zero_next = (uint64_t*)scratch + ((turn + 1) & 1) * half;
+        zero_words = half;
+    }
     uint32_t* ctr = (uint32_t*)(status + nb * nd);
-    hipError_t e = hipMemsetAsync(scratch, 0, (size_t)nb * nd * 8 + 8, s);
-    if (e != hipSuccess) return e;
     const size_t lds = (size_t)nd * 8 + (size_t)kPartItems * 4 * nd * 4;
     hipLaunchKernelGGL(k_part_regions, dim3((unsigned)nb), dim3(256), lds, s, n, key, key_hash, ts, val, max_p, p,
                        g, cap, status, ctr, nb, key_out, ts_out, val_out, key_hash ? hash_out : nullptr, packed_out,
-                       counts);
+                       counts, zero_next, zero_words);
     return hipGetLastError();
 }
 
