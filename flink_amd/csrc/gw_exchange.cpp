@@ -18,6 +18,7 @@
 // go out per peer, and the receiver unpacks the words behind the other records.  The base
 // pane comes from the previous batch's combined watermark, which every rank knows alike.
 #include "gw_kernels.h"
+#include "gw_wait.h"
 
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
@@ -41,6 +42,7 @@ struct gw_exchange {
     int64_t* part = nullptr;  // partitioned key | ts | value columns, cap records each
     int32_t* part_hash = nullptr;
     int64_t part_cap = 0;
+    int64_t part_regions = 0;  // regions the partition buffers were allocated for (1: contiguous)
     uint64_t* part_packed = nullptr;  // packed words (partition numbering), cap records
     int64_t* recv[2] = {nullptr, nullptr};  // receive sets used in turn: key | ts | value columns
     int32_t* recv_hash[2] = {nullptr, nullptr};
@@ -70,6 +72,11 @@ struct gw_exchange {
     hipStream_t handoff[2] = {nullptr, nullptr};
     hipEvent_t ev_recv[2] = {nullptr, nullptr}, ev_free[2] = {nullptr, nullptr};
     bool set_used[2] = {false, false};
+    // fail fast (gw_wait.h): every host wait is bounded; on expiry or an asynchronous RCCL error
+    // the communicator is aborted and every later call fails with GW_E_STATE
+    int64_t timeout_ms = 60000;
+    bool aborted = false;
+    hipStream_t last_stream = nullptr;  // the caller's exchange stream of the last batch
     std::string err;
 };
 
@@ -82,11 +89,51 @@ static int ex_fail(gw_exchange* ex, int rc, const std::string& what) {
         hipError_t e_ = (x);                                                                 \
         if (e_ != hipSuccess) return ex_fail(ex, GW_E_DEVICE, std::string(#x ": ") + hipGetErrorString(e_)); \
     } while (0)
+#define EX_LIVE(ex)                                                                          \
+    do {                                                                                     \
+        if ((ex)->aborted)                                                                   \
+            return ex_fail(ex, GW_E_STATE, "exchange aborted after an earlier failure: " + (ex)->err); \
+    } while (0)
 #define EX_NCCL(x)                                                                           \
     do {                                                                                     \
         ncclResult_t r_ = (x);                                                               \
         if (r_ != ncclSuccess) return ex_fail(ex, GW_E_DEVICE, std::string(#x ": ") + ncclGetErrorString(r_)); \
     } while (0)
+
+static void ex_abort(gw_exchange* ex) {
+    if (ex->aborted) return;
+    ex->aborted = true;
+    if (ex->comm) {
+        (void)ncclCommAbort(ex->comm);  // kernels waiting on a dead peer return; the communicator is gone
+        ex->comm = nullptr;
+    }
+}
+
+// Wait for everything queued on s (a collective and what follows it), bounded: the stream
+// completes, or its error, the communicator's asynchronous error or the deadline aborts the
+// communicator and fails the call (GW_E_STATE; the JVM side throws and fails the task).
+static int ex_wait(gw_exchange* ex, hipStream_t s, const char* what) {
+    EX_LIVE(ex);
+    hipError_t herr = hipSuccess;
+    ncclResult_t aerr = ncclSuccess;
+    const WaitResult w = poll_until_done(
+        [&] {
+            herr = hipStreamQuery(s);
+            return herr == hipSuccess ? 0 : herr == hipErrorNotReady ? 1 : 2;
+        },
+        [&] {
+            if (ncclCommGetAsyncError(ex->comm, &aerr) != ncclSuccess) return 1;
+            return aerr == ncclSuccess || aerr == ncclInProgress ? 0 : 1;
+        },
+        steady_now_ns, relax_backoff, ex->timeout_ms * 1000000);
+    if (w == WaitResult::kDone) return GW_OK;
+    std::string why = std::string(what) + ": ";
+    if (w == WaitResult::kStreamError) why += std::string("stream error: ") + hipGetErrorString(herr);
+    else if (w == WaitResult::kCommError) why += std::string("RCCL asynchronous error: ") + ncclGetErrorString(aerr);
+    else why += "no completion within " + std::to_string(ex->timeout_ms) + " ms (a peer died or diverged)";
+    ex_abort(ex);
+    return ex_fail(ex, GW_E_STATE, why + "; communicator aborted");
+}
 
 extern "C" {
 
@@ -140,7 +187,13 @@ int gw_exchange_create(gw_exchange** out, int32_t nranks, int32_t rank, const vo
 
 void gw_exchange_destroy(gw_exchange* ex) {
     if (!ex) return;
-    hipDeviceSynchronize();
+    // the last batch's collectives may still wait on a peer: bounded, then abort
+    if (!ex->aborted && ex->last_stream && ex_wait(ex, ex->last_stream, "gw_exchange_destroy") != GW_OK) {
+        // aborted: the kernels that waited on the peer have returned
+    }
+    for (int q = 0; q < 2; ++q)
+        if (!ex->aborted && ex->handoff[q]) (void)ex_wait(ex, ex->handoff[q], "gw_exchange_destroy");
+    if (!ex->aborted) (void)hipDeviceSynchronize();
     if (ex->comm) ncclCommDestroy(ex->comm);
     hipFree(ex->scratch);
     hipFree(ex->part);
@@ -158,6 +211,12 @@ void gw_exchange_destroy(gw_exchange* ex) {
 }
 
 const char* gw_exchange_last_error(const gw_exchange* ex) { return ex ? ex->err.c_str() : ""; }
+
+int gw_exchange_set_timeout(gw_exchange* ex, int64_t timeout_ms) {
+    if (!ex || timeout_ms < 0) return GW_E_INVALID;
+    ex->timeout_ms = timeout_ms;
+    return GW_OK;
+}
 
 int gw_exchange_plan(int32_t nranks, const int64_t* sent_msg, const int64_t* recv_msg, int64_t cols_mask, int64_t wm,
                      int64_t* send_off, int64_t* send_cnt, int64_t* recv_off, int64_t* recv_cnt, int64_t* total,
@@ -207,6 +266,22 @@ int gw_exchange_plan_packed(int32_t nranks, const int64_t* sent_msg, const int64
     *total_other = wo;
     *total_packed = po;
     return GW_OK;
+}
+
+typedef __int128 i128;
+// Region-partition buffers above this fall back to the contiguous layout (36 B x P
+// per record of capacity is ~72 GB per rank at 16 ranks and 100M-record batches).
+constexpr int64_t kRegionBudget = (int64_t)16 << 30;
+
+// (pane, offset, base pane) of a packing geometry folded to 32 non-zero bits
+static uint64_t geom_fold(const gw_pack_geom& g) {
+    uint64_t h = 0x9e3779b97f4a7c15ull;
+    for (int64_t v : {g.pane, g.offset, g.base_pane}) {
+        h ^= (uint64_t)v;
+        h *= 0xbf58476d1ce4e5b9ull;
+        h ^= h >> 31;
+    }
+    return (h >> 32) | 1;
 }
 
 static int64_t gcd64(int64_t a, int64_t b) {
@@ -263,7 +338,9 @@ int gw_exchange_batch(gw_exchange* ex, int64_t n, const int64_t* d_key, const in
                       const int64_t** d_key_out, const int32_t** d_key_hash_out, const int64_t** d_ts_out,
                       const int64_t** d_value_out, int64_t* wm_out, void** ingest_stream, void* stream) {
     if (!ex || n < 0 || !n_out || !d_key_out || !d_ts_out || (n > 0 && (!d_key || !d_ts))) return GW_E_INVALID;
+    EX_LIVE(ex);
     hipStream_t s = (hipStream_t)stream;
+    ex->last_stream = s;
     const int P = ex->nranks;
     constexpr int M = gw_exchange::kMsg;
     // packing this batch: configured, a previous combined watermark, no key-hash column, and
@@ -276,26 +353,34 @@ int gw_exchange_batch(gw_exchange* ex, int64_t n, const int64_t* d_key, const in
     // 1. stable device partition by owner (packing: by owner, then packed / not).  Up to
     // kPartRegionMaxOwners ranks into one region per owner (single pass, buffers P times the
     // batch: 36 B x P per record of capacity), beyond that the contiguous three-pass layout.
-    const bool regions = P <= kPartRegionMaxOwners && !ex->no_regions;
+    // The region layout holds P times the batch (24 B of columns + 8 B of words per record and
+    // region, + 4 B with a key-hash column); past kRegionBudget it falls back to the contiguous
+    // three-pass layout, whose buffers hold the batch once.  The choice is local to the rank.
+    const int64_t want_cap = std::max(n + n / 4 + 1024, ex->part_cap);
+    const bool regions = P <= kPartRegionMaxOwners && !ex->no_regions &&
+                         (i128)want_cap * P * (32 + (d_key_hash ? 4 : 0)) <= (i128)kRegionBudget;
     const int64_t R = regions ? P : 1;
-    if (n > ex->part_cap) {
-        EX_HIP(hipStreamSynchronize(s));
+    if (n > ex->part_cap || R != ex->part_regions) {
+        const int rc_w = ex_wait(ex, s, "partition buffer");  // the last batch's sends read them
+        if (rc_w != GW_OK) return rc_w;
         hipFree(ex->part);
         hipFree(ex->part_hash);
         hipFree(ex->part_packed);
         ex->part = nullptr;
         ex->part_hash = nullptr;
         ex->part_packed = nullptr;
-        const int64_t c = n + n / 4 + 1024;
+        const int64_t c = want_cap;
         EX_HIP(hipMalloc((void**)&ex->part, (size_t)c * R * 3 * 8));
-        EX_HIP(hipMalloc((void**)&ex->part_hash, (size_t)c * R * 4));
         ex->part_cap = c;
+        ex->part_regions = R;
     }
+    if (d_key_hash && !ex->part_hash) EX_HIP(hipMalloc((void**)&ex->part_hash, (size_t)ex->part_cap * R * 4));
     if (packed && !ex->part_packed) EX_HIP(hipMalloc((void**)&ex->part_packed, (size_t)ex->part_cap * R * 8));
     const int64_t need = regions ? partition_regions_scratch_bytes(ex->part_cap, 2 * P)
                                  : partition_scratch_bytes(std::max<int64_t>(n, 1), 2 * P);
     if (need > ex->scratch_bytes) {
-        EX_HIP(hipStreamSynchronize(s));
+        const int rc_w = ex_wait(ex, s, "partition scratch");
+        if (rc_w != GW_OK) return rc_w;
         hipFree(ex->scratch);
         ex->scratch = nullptr;
         EX_HIP(hipMalloc(&ex->scratch, (size_t)need));
@@ -324,11 +409,18 @@ int gw_exchange_batch(gw_exchange* ex, int64_t n, const int64_t* d_key, const in
     }
     // 2. one message per peer: (records, watermark, columns, packed records); all-to-all,
     // then one host wait
-    const int64_t cols_mask = (d_value ? 1 : 0) | (d_key_hash ? 2 : 0) | (packed ? 4 : 0);
+    // The column mask also carries the packing geometry (pane, offset, base pane) folded to 32
+    // bits: ranks packing against different windows fail together below instead of decoding
+    // each other's words with the wrong panes.
+    const int64_t cols_mask = (d_value ? 1 : 0) | (d_key_hash ? 2 : 0) | (packed ? 4 : 0) |
+                              (packed ? (int64_t)(geom_fold(g) << 32) : 0);
     EX_HIP(launch_exchange_message(ex->d_counts, P, wm, cols_mask, packed ? 1 : 0, ex->d_msg, s));
     EX_NCCL(ncclAllToAll(ex->d_msg, ex->d_msg + M * P, M, ncclInt64, ex->comm, s));
     EX_HIP(hipMemcpyAsync(ex->h_msg, ex->d_msg, (size_t)2 * M * P * 8, hipMemcpyDeviceToHost, s));
-    EX_HIP(hipStreamSynchronize(s));
+    {
+        const int rc_w = ex_wait(ex, s, "gw_exchange_batch: count all-to-all");
+        if (rc_w != GW_OK) return rc_w;
+    }
     const int64_t* sm = ex->h_msg;
     const int64_t* rm = ex->h_msg + M * P;
     std::vector<int64_t>& so = ex->plan[0];
@@ -342,7 +434,7 @@ int gw_exchange_batch(gw_exchange* ex, int64_t n, const int64_t* d_key, const in
     int64_t total = 0, wmin = wm, tw = 0, tp = 0;
     // every rank sees every rank's mask: all of them fail here together, before any send
     if (gw_exchange_plan(P, sm, rm, cols_mask, wm, so.data(), sc.data(), ro.data(), rc.data(), &total, &wmin))
-        return ex_fail(ex, GW_E_INVALID, "gw_exchange_batch: ranks pass different columns or packing");
+        return ex_fail(ex, GW_E_INVALID, "gw_exchange_batch: ranks pass different columns or packing geometry");
     if (gw_exchange_plan_packed(P, sm, rm, sp.data(), rwo.data(), rpo.data(), rp.data(), &tw, &tp))
         return ex_fail(ex, GW_E_INVALID, "gw_exchange_batch: bad packed counts");
     ex->last_send = sc;
@@ -357,7 +449,10 @@ int gw_exchange_batch(gw_exchange* ex, int64_t n, const int64_t* d_key, const in
         EX_HIP(hipStreamWaitEvent(s, ex->ev_free[u], 0));
     }
     if (total > ex->recv_cap[u]) {
-        EX_HIP(hipStreamSynchronize(s));
+        {
+            const int rc_w = ex_wait(ex, s, "receive buffer");
+            if (rc_w != GW_OK) return rc_w;
+        }
         hipFree(ex->recv[u]);
         hipFree(ex->recv_hash[u]);
         hipFree(ex->recv_packed[u]);
@@ -366,9 +461,9 @@ int gw_exchange_batch(gw_exchange* ex, int64_t n, const int64_t* d_key, const in
         ex->recv_packed[u] = nullptr;
         const int64_t c = total + total / 4 + 1024;
         EX_HIP(hipMalloc((void**)&ex->recv[u], (size_t)c * 3 * 8));
-        EX_HIP(hipMalloc((void**)&ex->recv_hash[u], (size_t)c * 4));
         ex->recv_cap[u] = c;
     }
+    if (d_key_hash && !ex->recv_hash[u]) EX_HIP(hipMalloc((void**)&ex->recv_hash[u], (size_t)ex->recv_cap[u] * 4));
     if (packed && !ex->recv_packed[u]) EX_HIP(hipMalloc((void**)&ex->recv_packed[u], (size_t)ex->recv_cap[u] * 8));
     int64_t* rk = ex->recv[u];
     int64_t* rt = rk + ex->recv_cap[u];
@@ -453,12 +548,17 @@ int gw_exchange_counts(const gw_exchange* ex, int64_t* send, int64_t* recv) {
 
 int gw_exchange_min_watermark(gw_exchange* ex, int64_t wm, int64_t* out, void* stream) {
     if (!ex || !out) return GW_E_INVALID;
+    EX_LIVE(ex);
     hipStream_t s = (hipStream_t)stream;
+    ex->last_stream = s;
     *ex->h_wm = wm;
     EX_HIP(hipMemcpyAsync(ex->d_wm, ex->h_wm, 8, hipMemcpyHostToDevice, s));
     EX_NCCL(ncclAllReduce(ex->d_wm, ex->d_wm, 1, ncclInt64, ncclMin, ex->comm, s));
     EX_HIP(hipMemcpyAsync(ex->h_wm, ex->d_wm, 8, hipMemcpyDeviceToHost, s));
-    EX_HIP(hipStreamSynchronize(s));
+    {
+        const int rc_w = ex_wait(ex, s, "gw_exchange_min_watermark");
+        if (rc_w != GW_OK) return rc_w;
+    }
     *out = *ex->h_wm;
     return GW_OK;
 }

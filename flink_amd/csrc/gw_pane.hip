@@ -296,8 +296,14 @@ __device__ __forceinline__ void lds_cell_add(long long* a0, long long* a1, int64
 // tile (round 4: one flush per 2048-record tile put ~3.3K atomics on each hot cell).
 constexpr int kPreKeys = 1024;
 
+// Experiment builds only (flink_amd.build --define GW_PREAGG_EXP=n --out ...), results
+// discarded: 1 no key cache, 2 no LDS cells, 4 no table adds.  The product library is built with 0.
+#ifndef GW_PREAGG_EXP
+#define GW_PREAGG_EXP 0
+#endif
 template <int AGG>
-__global__ void __launch_bounds__(256) k_ingest_preagg(IngestArgs a, int exp) {
+__global__ void __launch_bounds__(256) k_ingest_preagg(IngestArgs a) {
+    constexpr int exp = GW_PREAGG_EXP;
     constexpr bool AV = AGG == GW_AVG_I64 || AGG == GW_AVG_F64;
     __shared__ long long s_key[kPreKeys];
     __shared__ long long s_g[kPreKeys + 1];  // + the sentinel key's slot (t.cap)
@@ -2346,163 +2352,6 @@ __global__ void __launch_bounds__(256) k_fire(FireArgs a) {
     stage_flush(rs, &a.st->rows, a.o_key, a.o_start, a.o_end, a.o_res);
 }
 
-// Fire sweep without restored-window overlay, for passes whose windows cover at most
-// kFirePos ring positions (every sliding/tumbling fire of a ring of <= 8 panes; Nexmark Q5:
-// 5 of 6).  Each thread takes U slots per step and issues every load of the step at
-// once -- keys, presence masks and the cells of all covered positions, unconditionally
-// and coalesced -- so a wave keeps U * (2 + positions) loads in flight instead of one
-// dependent chain per slot.  Presence picks the cells to fold in registers (mask bit, or
-// the count word for COUNT / AVG; an absent cell is never folded).  Rows are compacted
-// per wave with ballots and staged in LDS as (key, result, window); a block reserves its
-// staged rows in the output with one device atomic per kFireStage rows.  Same rows,
-// same retire as k_fire (row order within a fire is unspecified for both).
-constexpr int kFirePos = 8;
-constexpr int kFireStage = 2048;
-constexpr int kFireThreads = 256;
-template <int AGG, int U>
-__global__ void __launch_bounds__(kFireThreads) k_fire_sweep(FireArgs a) {
-    constexpr bool M = uses_mask<AGG>();
-    constexpr bool AV = AGG == GW_AVG_I64 || AGG == GW_AVG_F64;
-    constexpr int NW = kFireThreads / 64;
-    __shared__ long long s_k[kFireStage], s_r[kFireStage];
-    __shared__ uint8_t s_w[kFireStage];
-    __shared__ unsigned s_wave[NW];
-    __shared__ unsigned s_cnt;
-    __shared__ unsigned long long s_base;
-    const int64_t nslots = a.t.cap + 1;
-    const int64_t id0 = identity0(AGG);
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    if (threadIdx.x == 0) s_cnt = 0;
-    if (blockIdx.x == 0 && threadIdx.x < kShards) atomicAnd(&a.st->sh[threadIdx.x].occ, ~a.rmask);
-    // the ring positions this pass folds (uniform)
-    uint64_t need = 0;
-    for (int w = 0; w < a.nwin; ++w) need |= a.wmask[w];
-    int posl[kFirePos];
-    int np = 0;
-#pragma unroll
-    for (int q = 0; q < kFirePos; ++q) {
-        posl[q] = need ? __ffsll((long long)need) - 1 : 0;
-        if (need) { need &= need - 1; np = q + 1; }
-    }
-    const int64_t S = pt_S(a.t);
-    const int64_t MW = pt_mask_words(a.t);
-    auto flush = [&]() {  // every thread; ends with s_cnt == 0
-        __syncthreads();
-        const unsigned c = s_cnt;
-        if (threadIdx.x == 0 && c) s_base = atomicAdd(&a.st->rows, (unsigned long long)c);
-        __syncthreads();
-        const unsigned long long b = s_base;
-        for (unsigned j = threadIdx.x; j < c; j += kFireThreads) {
-            const int64_t st = a.start0 + (int64_t)s_w[j] * a.slide;
-            a.o_key[b + j] = s_k[j];
-            a.o_start[b + j] = st;
-            a.o_end[b + j] = st + a.size;
-            a.o_res[b + j] = s_r[j];
-        }
-        __syncthreads();
-        if (threadIdx.x == 0) s_cnt = 0;
-        __syncthreads();
-    };
-    __syncthreads();
-    const int64_t tile = (int64_t)kFireThreads * U;
-    for (int64_t base = (int64_t)blockIdx.x * tile; base < nslots; base += (int64_t)gridDim.x * tile) {
-        int64_t key[U], c0[U][kFirePos], c1[U][kFirePos];
-        uint64_t mask[U];
-        bool live[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {  // all loads of the step in flight together
-            const int64_t g0 = base + u * kFireThreads + threadIdx.x;
-            live[u] = g0 < nslots;
-            const int64_t g = live[u] ? g0 : nslots - 1;
-            int64_t* rg = pt_region(a.t, g >> a.t.log2S);
-            const int64_t j = g & (S - 1);
-            key[u] = rg[j];
-            mask[u] = M ? mask_get((const uint8_t*)(rg + S), j, a.t.mask_shift) : 0;
-            const int64_t* cells = rg + S + MW;
-#pragma unroll
-            for (int q = 0; q < kFirePos; ++q) {
-                c0[u][q] = id0;
-                c1[u][q] = 0;
-                if (q < np) {
-                    const int64_t* c = cells + ((int64_t)posl[q] * S + j) * (AV ? 2 : 1);
-                    c0[u][q] = c[0];
-                    if constexpr (AV) c1[u][q] = c[1];
-                }
-            }
-        }
-        for (int w = 0; w < a.nwin; ++w) {
-            const uint64_t wm = a.wmask[w];
-            int64_t res[U];
-            uint64_t bal[U];
-            unsigned tot = 0;
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                int64_t r0 = id0, r1 = 0;
-                bool any = false;
-#pragma unroll
-                for (int q = 0; q < kFirePos; ++q) {
-                    if (q < np && ((wm >> posl[q]) & 1)) {
-                        const bool pres = M ? ((mask[u] >> posl[q]) & 1) != 0 : (AV ? c1[u][q] : c0[u][q]) != 0;
-                        if (pres) {
-                            fold_cell(AGG, r0, r1, c0[u][q], c1[u][q]);
-                            any = true;
-                        }
-                    }
-                }
-                any = any && live[u];
-                res[u] = cell_result(AGG, r0, r1);
-                bal[u] = __ballot(any);
-                tot += (unsigned)__popcll(bal[u]);
-            }
-            if (lane == 0) s_wave[wave] = tot;
-            __syncthreads();
-            unsigned woff = 0, btot = 0;
-#pragma unroll
-            for (int q = 0; q < NW; ++q) {
-                const unsigned v = s_wave[q];
-                woff += q < wave ? v : 0u;
-                btot += v;
-            }
-            if (s_cnt + btot > (unsigned)kFireStage) flush();  // uniform
-            else __syncthreads();  // everyone has read s_wave and s_cnt
-            unsigned o = s_cnt + woff;
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                if ((bal[u] >> lane) & 1) {
-                    const unsigned j = o + (unsigned)__popcll(bal[u] & ((1ull << lane) - 1ull));
-                    s_k[j] = key[u];
-                    s_r[j] = res[u];
-                    s_w[j] = (uint8_t)w;
-                }
-                o += (unsigned)__popcll(bal[u]);
-            }
-            __syncthreads();
-            if (threadIdx.x == 0) s_cnt += btot;
-        }
-        if (a.rmask) {  // clearAllState of the panes no later window covers
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                if (!live[u]) continue;
-                const int64_t g = base + u * kFireThreads + threadIdx.x;
-                int64_t* rg = pt_region(a.t, g >> a.t.log2S);
-                const int64_t j = g & (S - 1);
-                if constexpr (M) {
-                    if (mask[u] & a.rmask) mask_put((uint8_t*)(rg + S), j, a.t.mask_shift, mask[u] & ~a.rmask);
-                }
-                uint64_t m = a.rmask;
-                while (m) {
-                    const int pos = __ffsll((long long)m) - 1;
-                    m &= m - 1;
-                    int64_t* c = rg + S + MW + ((int64_t)pos * S + j) * (AV ? 2 : 1);
-                    c[0] = id0;
-                    if constexpr (AV) c[1] = 0;
-                }
-            }
-        }
-    }
-    flush();
-}
-
 // Fire sweep, round 5 (k_fire2): the latency-hiding form of k_fire for passes without a
 // restored-window overlay whose windows read at most 6 ring positions (Nexmark Q5: 5 of 6;
 // tumbling: 1).  Every lane takes U slots per step and loads each slot's key, presence mask
@@ -2833,8 +2682,7 @@ hipError_t launch_ingest(const IngestArgs& a, int path, int unroll, hipStream_t 
         }
         static const int bpc = getenv("GW_PREAGG_BPC") ? std::max(1, atoi(getenv("GW_PREAGG_BPC"))) : 2;
         const int g = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)bpc * cus, (a.n + 2047) / 2048));
-        static const int exp = getenv("GW_PREAGG_EXP") ? atoi(getenv("GW_PREAGG_EXP")) : 0;  // measurement only
-#define L(A) hipLaunchKernelGGL(k_ingest_preagg<A>, dim3(g), dim3(256), 0, s, a, exp)
+#define L(A) hipLaunchKernelGGL(k_ingest_preagg<A>, dim3(g), dim3(256), 0, s, a)
         GW_AGG_SWITCH(a.t.agg, L);
 #undef L
     } else if (unroll == 4) {
@@ -3018,29 +2866,8 @@ hipError_t launch_deferred_min(const int64_t* pane, int64_t n, DevStatus* st, hi
 hipError_t launch_fire(const FireArgs& a, hipStream_t s) {
     uint64_t need = 0;
     for (int w = 0; w < a.nwin; ++w) need |= a.wmask[w];
-    const bool sweep = a.ov.head == nullptr && __builtin_popcountll(need) <= kFirePos && a.nwin <= 255;
-#ifdef GW_EXP_FIRE_SWEEP
-    if (sweep) {
-#else
-    if (false && sweep) {  // measured slower than k_fire on Q5 (0.37 vs 0.30 ms per fire)
-#endif
-        // 4 slots per thread (2 for the two-word AVG cells); ~4 blocks per CU
-        const bool av = a.t.agg == GW_AVG_I64 || a.t.agg == GW_AVG_F64;
-#ifndef GW_FIRE_U
-#define GW_FIRE_U 4
-#endif
-        const int64_t tile = (int64_t)kFireThreads * (av ? 2 : GW_FIRE_U);
-        const int fg = (int)std::min<int64_t>(1024, std::max<int64_t>(1, (a.t.cap + 1 + tile - 1) / tile));
-#define L(A)                                                                                              \
-    if (av) hipLaunchKernelGGL((k_fire_sweep<A, 2>), dim3(fg), dim3(kFireThreads), 0, s, a);             \
-    else hipLaunchKernelGGL((k_fire_sweep<A, GW_FIRE_U>), dim3(fg), dim3(kFireThreads), 0, s, a)
-        GW_AGG_SWITCH(a.t.agg, L);
-#undef L
-        return hipGetLastError();
-    }
-    static const bool f2_off = [] { const char* e = getenv("GW_FIRE2"); return e && atoi(e) == 0; }();
     const int npos = __builtin_popcountll(need);
-    if (!f2_off && a.ov.head == nullptr && npos >= 1 && npos <= 6 && a.nwin <= 255 &&
+    if (a.ov.head == nullptr && npos >= 1 && npos <= 6 && a.nwin <= 255 &&
         (int64_t)a.nwin * kF2Threads * 2 <= kF2Stage) {
         const bool av = a.t.agg == GW_AVG_I64 || a.t.agg == GW_AVG_F64;
         const int64_t tile = (int64_t)kF2Threads * (av ? 1 : 2);  // U slots per lane

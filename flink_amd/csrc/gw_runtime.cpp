@@ -723,8 +723,9 @@ struct gw_handle {
         bool pinned = true;  // pinned destinations (page-locked: hipHostMalloc / registered) take the D2H directly
         for (int i = 0; i < 4 && pinned; ++i)
             if (dst[i]) pinned = host_pinned(dst[i]);
-        static const bool dbg = getenv("GW_DRAIN_DEBUG") != nullptr;
-        if (dbg) fprintf(stderr, "[gw drain] %lld rows, %s\n", (long long)c, direct || pinned || c < kBounceRows / 4 ? (pinned ? "direct (pinned)" : "direct") : "bounce");
+#ifdef GW_DEBUG_LOG  // experiment builds only
+        fprintf(stderr, "[gw drain] %lld rows, %s\n", (long long)c, direct || pinned || c < kBounceRows / 4 ? (pinned ? "direct (pinned)" : "direct") : "bounce");
+#endif
         if (direct || pinned || c < kBounceRows / 4) {
             hipError_t err = hipSuccess;
             for (int i = 0; i < 4 && err == hipSuccess; ++i)
@@ -910,6 +911,9 @@ struct gw_handle {
         if ((rc = refresh())) return rc;
         const int64_t nrf = (int64_t)h_st->n_refire;
         rf_bound = 0;
+        if (nrf > kSortMaxRecords)  // one watermark's late records beyond the grouping sort
+            return fail(GW_E_UNSUPPORTED, "%lld late records of fired windows between two watermarks (limit %lld)",
+                        (long long)nrf, (long long)kSortMaxRecords);
         if (nrf) {
             const int64_t span = seq_ctr - rf_seq_base;
             const int seq_bits = span < ((int64_t)1 << 32) ? 32 : 64;
@@ -2820,10 +2824,22 @@ int gw_destroy(gw_handle* h) {
 static int ingest_device_impl(gw_handle* h, int64_t n, const int64_t* key, const int64_t* ts,
                               const int64_t* val) {
     if (h->session) {
-        int rc = session_ingest(h->sess, n, key, ts, val, h->wm, h->err);
-        if (rc == GW_OK) { h->stats.events_in += n; h->stats.batches++; }
-        else if (rc == GW_E_DEVICE || rc == GW_E_NO_TIMESTAMP || rc == GW_E_RANGE) h->failed = true;
-        return rc;
+        // the grouping sort takes < 2^30 records (gw_sort.h kSortMaxRecords): larger calls go
+        // in pieces, each at the same watermark -- the reference processes them one by one
+        // anyway, and every piece keeps its records' arrival order
+        for (int64_t off = 0; off < n || (n <= 0 && off == 0); off += kSortMaxRecords) {
+            const int64_t c = std::min<int64_t>(kSortMaxRecords, n - off);
+            int rc = session_ingest(h->sess, c, key + off, ts ? ts + off : nullptr, val ? val + off : nullptr, h->wm,
+                                    h->err);
+            if (rc != GW_OK) {
+                if (rc == GW_E_DEVICE || rc == GW_E_NO_TIMESTAMP || rc == GW_E_RANGE) h->failed = true;
+                return rc;
+            }
+            if (n <= 0) break;
+        }
+        h->stats.events_in += n;
+        h->stats.batches++;
+        return GW_OK;
     }
     // the region buffer indexes records with 32-bit offsets: split very large calls
     for (int64_t off = 0; off < n; off += kMaxIngest) {
@@ -3331,6 +3347,26 @@ int gw_ingest_packed_device(gw_handle* h, int64_t n_other, const int64_t* d_key,
     if (n_other < 0 || n_words < 0 || (n_words > 0 && (!d_words || !g || !g->enabled || g->pane <= 0)))
         return h->fail(GW_E_INVALID, "gw_ingest_packed_device: bad word arguments");
     if (n_words == 0) return gw_ingest_device(h, n_other, d_key, nullptr, d_ts, d_value, stream);
+    {  // a word's timestamp is its pane's start: only handles whose every decision depends on the
+       // pane alone may take it (gpuwin.h gw_pack_geom)
+        const gw_config& c = h->cfg;
+        const bool fp_in = c.agg == GW_SUM_F64 || c.agg == GW_MIN_F64 || c.agg == GW_MAX_F64 || c.agg == GW_AVG_F64;
+        // (window-class composites may: every class window's bounds lie on the pane grid, so a
+        // record and its pane's start fall into the same windows of every class)
+        if (h->session || h->fe || (c.flags & GW_FLAG_LATE_SIDE_OUTPUT) || fp_in ||
+            (c.assigner != GW_TUMBLING && c.assigner != GW_SLIDING))
+            return h->fail(GW_E_UNSUPPORTED,
+                           "gw_ingest_packed_device: packed words need a plain tumbling / sliding handle over an "
+                           "integer aggregate without the late side output (unpack them for this handle)");
+        const int64_t size = c.size, slide = c.assigner == GW_TUMBLING ? c.size : c.slide;
+        const i128 doff = (i128)c.offset - (i128)g->offset;
+        if (size < slide || size % g->pane || slide % g->pane || doff % g->pane)
+            return h->fail(GW_E_UNSUPPORTED,
+                           "gw_ingest_packed_device: the words' pane geometry (pane %lld, offset %lld) does not "
+                           "divide this handle's windows (size %lld, slide %lld, offset %lld)",
+                           (long long)g->pane, (long long)g->offset, (long long)size, (long long)slide,
+                           (long long)c.offset);
+    }
     const bool vals = h->cfg.agg != GW_COUNT;
     if (n_other > 0 && (!d_key || !d_ts || (vals && !d_value))) return h->fail(GW_E_INVALID, "null key/ts/value column");
     const int64_t n = n_other + n_words;
@@ -3409,8 +3445,9 @@ static int nb_layout(const gw_record_layout* lay, int agg, NbLayout& L, std::str
 }
 
 static int nb_status_code(const NbStatus& st, std::string& why) {
-    static const bool dbg = getenv("GW_NB_DEBUG") != nullptr;
-    if (dbg) fprintf(stderr, "gw netbuf: fallback %llu walkback %llu\n", st.fallback, st.walkback);
+#ifdef GW_DEBUG_LOG  // experiment builds only
+    fprintf(stderr, "gw netbuf: fallback %llu walkback %llu\n", st.fallback, st.walkback);
+#endif
     if (st.corrupt) { why = "Corrupt stream: unknown tag or element length (StreamElementSerializer)"; return GW_E_INVALID; }
     if (st.unsupported) { why = "stream element longer than GW_MAX_ELEMENT bytes"; return GW_E_UNSUPPORTED; }
     if (st.full) { why = "decoded records / watermarks exceed the output capacity"; return GW_E_OUTPUT_FULL; }

@@ -32,6 +32,12 @@
 
 namespace gw {
 
+// Experiment builds only (flink_amd.build --define GW_SEG_EXP=n --out ...), results discarded:
+// 1 no record gathers, 2 no slot write-back.  The product library is built with 0.
+#ifndef GW_SEG_EXP
+#define GW_SEG_EXP 0
+#endif
+
 constexpr int kLaneSess = 3;        // sessions a thread replays in LDS
 constexpr int kSegThreads = 128;
 constexpr int kWideWords = 5;       // wide-table session: start, end, a0, a1, fired
@@ -65,7 +71,6 @@ struct SegArgs {
     uint32_t* retry;        // wide pass: runs that did not fit K2 (append at st->overflow)
     DevStatus* st;
     int gshift;             // records are grouped by slot >> gshift (the sort skips the low bits)
-    int exp;                // measurement only (GW_SEG_EXP): 1 no record gathers, 2 no slot write-back
     int64_t* pu_key;        // records of keys the prep found no slot for (arrival order), append at
                             // st->spills: replayed after a regrow
     int64_t* pu_ts;
@@ -301,7 +306,7 @@ __device__ __forceinline__ bool add_element(const SegArgs& a, const SessList& l,
                                             int64_t idx, unsigned long long& late, unsigned long long& merges,
                                             unsigned long long& flags, bool dry = false) {
     struct alignas(16) TsVal { int64_t ts, v; };
-    const TsVal tv = (a.exp & 1) ? TsVal{a.wm + 1 + (int64_t)(idx & 7), 1} : reinterpret_cast<const TsVal*>(a.rec)[idx];
+    const TsVal tv = (GW_SEG_EXP & 1) ? TsVal{a.wm + 1 + (int64_t)(idx & 7), 1} : reinterpret_cast<const TsVal*>(a.rec)[idx];
     return add_element_tv<AGG>(a, l, cnt, cap, key, tv.ts, tv.v, late, merges, flags, dry);
 }
 
@@ -348,7 +353,7 @@ __device__ __forceinline__ void seg_slot(const SegArgs& a, const SessList& l, in
         a.punt[at] = (uint32_t)i;  // the wide pass replays this slot's records from i to the group's end
         return;
     }
-    if (a.exp & 2) return;
+    if (GW_SEG_EXP & 2) return;
     if (cnt <= a.t.ring) {
         uint64_t fired = 0;
         int64_t due = INT64_MAX;
@@ -1547,7 +1552,7 @@ static int count_ingest(SessionState* s, int64_t n, const int64_t* key, const in
     int rc;
     if ((rc = begin_launch(s, err))) return rc;
     if (n <= 0) return GW_OK;
-    if ((int64_t)n > (int64_t)0x7fffffffLL) { err = "batch too large"; return GW_E_INVALID; }
+    if (n > kSortMaxRecords) { err = "batch too large for the grouping sort (split by the caller)"; return GW_E_INVALID; }
     // every element fires at most one window
     if ((rc = ensure_rows(s, (int64_t)s->h_st->rows + n, err))) return rc;
     auto ev = s->timing ? get_ev(s) : std::pair<hipEvent_t, hipEvent_t>{};
@@ -1630,8 +1635,6 @@ static int ingest_sorted(SessionState* s, int64_t n, const int64_t* key, const i
     if ((rc = group_records(s, n, key, ts, val, &a.slot, &a.perm, err, defer))) return rc;
     a.rec = s->rec;
     a.gshift = s->gshift;
-    static const int seg_exp = getenv("GW_SEG_EXP") ? atoi(getenv("GW_SEG_EXP")) : 0;
-    a.exp = seg_exp;
     a.key = key;
     a.ts = ts;
     a.val = val;
@@ -1725,7 +1728,7 @@ int session_ingest(SessionState* s, int64_t n, const int64_t* key, const int64_t
     int rc;
     if ((rc = begin_launch(s, err))) return rc;
     if (n <= 0) return GW_OK;
-    if ((int64_t)n > (int64_t)0x7fffffffLL) { err = "batch too large"; return GW_E_INVALID; }
+    if (n > kSortMaxRecords) { err = "batch too large for the grouping sort (split by the caller)"; return GW_E_INVALID; }
     auto ev = s->timing ? get_ev(s) : std::pair<hipEvent_t, hipEvent_t>{};
     if (s->timing) SCHECK(hipEventRecord(ev.first, s->stream));
     if ((rc = ingest_sorted(s, n, key, ts, val, wm, err, true))) return rc;

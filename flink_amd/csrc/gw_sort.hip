@@ -31,6 +31,11 @@ namespace gw {
 
 constexpr uint32_t kOsLocal = 1u << 30, kOsIncl = 2u << 30, kOsMask = (1u << 30) - 1;
 constexpr int kOsMaxBins = 512;
+// Experiment builds only (flink_amd.build --define GW_SORT_EXP=n --out ...), results discarded:
+// 1 no look-back, 2 no ranking, 4 no write-out.  The product library is built with 0.
+#ifndef GW_SORT_EXP
+#define GW_SORT_EXP 0
+#endif
 
 struct SortPlan {
     int npass;
@@ -124,7 +129,8 @@ __global__ void __launch_bounds__(NT) k_os_pass(const K* __restrict__ kin, const
                                                 K* __restrict__ kout, uint32_t* __restrict__ vout, int64_t n,
                                                 int shift, int width, const uint32_t* __restrict__ gbase,
                                                 uint32_t* status, uint32_t* next_status, int64_t ntiles,
-                                                uint32_t* tile_ctr, int exp) {
+                                                uint32_t* tile_ctr) {
+    constexpr int exp = GW_SORT_EXP;
     constexpr int NW = NT / 64, TILE = NT * NI;
     __shared__ uint32_t cnt[NW][kOsMaxBins];  // per wave: running count of each digit; then its base
     __shared__ uint32_t lstart[kOsMaxBins + 1];  // the tile's exclusive scan over digits
@@ -272,10 +278,6 @@ static OsCfg os_cfg(int key_bytes) {
     if (c >= 0 && c < (int)(sizeof kOsCfgs / sizeof kOsCfgs[0])) return kOsCfgs[c];
     return key_bytes == 8 ? kOsCfgs[4] : kOsCfgs[0];
 }
-static int os_exp() {  // measurement only: 1 no look-back, 2 no ranking, 4 no write-out
-    static const int e = getenv("GW_SORT_EXP") ? atoi(getenv("GW_SORT_EXP")) : 0;
-    return e;
-}
 static int64_t os_tiles(int64_t n, int tile) { return n <= 0 ? 0 : (n + tile - 1) / tile; }
 
 // scratch: ghist[8][512] (+ 64 words), two look-back regions
@@ -301,7 +303,7 @@ static hipError_t os_launch(const K* kin, const uint32_t* vin, K* kout, uint32_t
                             const uint32_t* gbase, uint32_t* status, uint32_t* next_status, int64_t nt,
                             uint32_t* tile_ctr, hipStream_t s) {
     hipLaunchKernelGGL((k_os_pass<K, V, NT, NI>), dim3((unsigned)nt), dim3(NT), 0, s, kin, vin, kout, vout, n, shift,
-                       width, gbase, status, next_status, nt, tile_ctr, os_exp());
+                       width, gbase, status, next_status, nt, tile_ctr);
     return hipGetLastError();
 }
 
@@ -326,6 +328,7 @@ template <typename K>
 static hipError_t sort_pairs_impl(K* k0, uint32_t* v0, K* k1, uint32_t* v1, int64_t n, int lo, int hi, void* scratch,
                                   hipStream_t s, int* result_in_alt, bool iota) {
     *result_in_alt = 0;
+    if (n > kSortMaxRecords) return hipErrorInvalidValue;  // the 30-bit prefix field would spill into the flags
     const OsCfg c = os_cfg((int)sizeof(K));
     const SortPlan p = plan_for(lo, hi, c.maxw);
     if (n <= 1 || p.npass == 0) return iota && n > 0 ? launch_iota(v0, n, s) : hipSuccess;

@@ -265,6 +265,11 @@ class NativeKeyByExchange:
         self._h = h
         self.p, self.rank, self.maxp, self.device = parallelism, rank, max_parallelism, device
 
+    def set_timeout(self, timeout_ms: int):
+        """gw_exchange_set_timeout: the bound of every host wait (0: none).  On expiry or an
+        asynchronous RCCL error the communicator is aborted and the call raises GW_E_STATE."""
+        self._check(N.lib().gw_exchange_set_timeout(self._h, int(timeout_ms)))
+
     def close(self):
         if getattr(self, "_h", None):
             N.lib().gw_exchange_destroy(self._h)

@@ -479,9 +479,12 @@ int  gw_unpack_device(int64_t n, const uint64_t* d_words, const gw_pack_geom* g,
  * (the receive side of the packed exchange: what StreamTaskNetworkInput deserializes before
  * WindowOperator.processElement, WindowOperator.java:293-447, sees record by record)
  * (gw_exchange_last_words): the words' timestamps are their panes' starts (gw_pack_geom).  A
- * plain pane operator's region pass 1 decodes the words itself; other paths and handles
- * (sessions, window classes, first-element, the late side output) get them unpacked first.
- * Column pointers may be NULL when n_other = 0. */
+ * plain pane operator's region pass 1 decodes the words itself; the direct / pre-aggregation
+ * paths and window-class handles get them unpacked first.  GW_E_UNSUPPORTED when n_words > 0
+ * and the handle needs a record's own timestamp or value (sessions, count windows,
+ * first-element / minBy handles, the late side output, floating aggregates) or when g's pane
+ * does not divide the handle's size, slide and offset difference.  Column pointers may be NULL
+ * when n_other = 0. */
 int  gw_ingest_packed_device(gw_handle* h, int64_t n_other, const int64_t* d_key, const int64_t* d_ts,
                              const int64_t* d_value, int64_t n_words, const uint64_t* d_words,
                              const gw_pack_geom* g, void* stream);
@@ -514,13 +517,22 @@ int  gw_ingest_packed_device(gw_handle* h, int64_t n_other, const int64_t* d_key
  * the hand-off stream, so the exchange of the next batch never waits for this batch's
  * ingest, only the reuse of this receive set two batches later does.  All ranks call it
  * for every batch (n may be 0).  gw_exchange_counts: the last batch's per-peer send and
- * receive record counts (nranks each; either may be NULL). */
+ * receive record counts (nranks each; either may be NULL).
+ *
+ * Failure: no host wait of the exchange is unbounded (a failed channel fails the task in the
+ * reference; here a dead or diverging peer would otherwise leave every rank spinning in RCCL).
+ * Each wait polls the stream, ncclCommGetAsyncError and a deadline (gw_exchange_set_timeout,
+ * default 60000 ms; 0: none); on a stream error, an asynchronous RCCL error or expiry the
+ * communicator is aborted (ncclCommAbort) and the call returns GW_E_STATE with the reason in
+ * gw_exchange_last_error.  Every later call on that exchange returns GW_E_STATE; destroy it
+ * and fail the task (the JVM side throws, GpuKeyByExchange.java). */
 #define GW_EXCHANGE_ID_BYTES 128
 typedef struct gw_exchange gw_exchange;
 int  gw_exchange_unique_id(void* id);
 int  gw_exchange_create(gw_exchange** out, int32_t nranks, int32_t rank, const void* id, int32_t device,
                         int32_t max_parallelism);
 void gw_exchange_destroy(gw_exchange* ex);
+int  gw_exchange_set_timeout(gw_exchange* ex, int64_t timeout_ms);
 int  gw_exchange_batch(gw_exchange* ex, int64_t n, const int64_t* d_key, const int32_t* d_key_hash,
                        const int64_t* d_ts, const int64_t* d_value, int64_t wm, int64_t* n_out,
                        const int64_t** d_key_out, const int32_t** d_key_hash_out, const int64_t** d_ts_out,

@@ -48,6 +48,13 @@ public final class GpuKeyByExchange implements AutoCloseable {
 
     public long minWatermark(long wm, long stream) { return nativeMinWatermark(handle, wm, stream); }
 
+    /** Bound of every host wait of the exchange (include/gpuwin.h gw_exchange_set_timeout;
+     *  default 60 s, 0: none).  A dead or diverging peer, an asynchronous RCCL error or a
+     *  stream error aborts the communicator: {@link #batch} / {@link #minWatermark} then throw
+     *  IllegalStateException (the task fails and restarts from its checkpoint, as a failed
+     *  network channel fails it in the reference), and so does every later call. */
+    public void setTimeout(long timeoutMs) { nativeSetTimeout(handle, timeoutMs); }
+
     /** From the next batch on, records whose key fits 32 bits, value 28 bits and pane the 16
      *  after the watermark's travel as 8-byte words (include/gpuwin.h gw_exchange_enable_packing):
      *  for a tumbling / sliding operator with size >= slide, no late side output and an integer
@@ -69,4 +76,5 @@ public final class GpuKeyByExchange implements AutoCloseable {
                                            long watermark, long stream, ByteBuffer out);
     private static native long nativeMinWatermark(long h, long wm, long stream);
     private static native void nativeEnablePacking(long h, long size, long slide, long offset, boolean withValues);
+    private static native void nativeSetTimeout(long h, long timeoutMs);
 }

@@ -322,8 +322,11 @@ JNIEXPORT void JNICALL CLS(nativeRemapPayloads)(JNIEnv* env, jclass c, jbyteArra
 
 static jint fail_ex(JNIEnv* env, gw_exchange* x, int rc) {
     if (rc < 0) {
+        /* GW_E_STATE: the communicator was aborted (a peer died or diverged, an asynchronous
+         * RCCL error, a wait past gw_exchange_set_timeout): the task fails */
         jclass ex = (*env)->FindClass(env, rc == GW_E_INVALID ? "java/lang/IllegalArgumentException"
-                                                             : "java/lang/RuntimeException");
+                                           : rc == GW_E_STATE ? "java/lang/IllegalStateException"
+                                                              : "java/lang/RuntimeException");
         (*env)->ThrowNew(env, ex, x ? gw_exchange_last_error(x) : "gw_exchange: invalid argument or device error");
     }
     return rc;
@@ -375,6 +378,10 @@ JNIEXPORT void JNICALL XCLS(nativeEnablePacking)(JNIEnv* env, jclass c, jlong x,
                                                  jlong offset, jboolean withValues) {
     fail_ex(env, (gw_exchange*)(intptr_t)x,
             gw_exchange_enable_packing((gw_exchange*)(intptr_t)x, size, slide, offset, withValues ? 1 : 0));
+}
+
+JNIEXPORT void JNICALL XCLS(nativeSetTimeout)(JNIEnv* env, jclass c, jlong x, jlong timeoutMs) {
+    fail_ex(env, (gw_exchange*)(intptr_t)x, gw_exchange_set_timeout((gw_exchange*)(intptr_t)x, timeoutMs));
 }
 
 /* StatusWatermarkValve: the minimum of the subtasks' watermarks. */

@@ -99,3 +99,22 @@ def test_missing_library_fails_loudly(tmp_path):
     r = subprocess.run([sys.executable, "-c", code], cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr
     assert r.stdout.strip() == "raised True"
+
+
+def test_grouping_sort_refuses_counts_beyond_its_prefix_field():
+    """gw_sort.hip keeps a tile's per-digit prefix in 30 bits of its look-back word: the sort
+    returns hipErrorInvalidValue for n >= 2^30 before any launch (host-side guard; the session,
+    count-window and re-fire callers split or refuse such batches), instead of spilling the
+    prefix into the flag bits."""
+    L = N.lib()
+    p = ctypes.c_void_p
+    for sym in ("_ZN2gw14sort_pairs_u32EPjS0_S0_S0_liiPvP12ihipStream_tPib",
+                "_ZN2gw14sort_pairs_u64EPmPjS0_S1_liiPvP12ihipStream_tPib"):
+        f = getattr(L, sym)
+        f.restype = ctypes.c_int
+        f.argtypes = [p, p, p, p, ctypes.c_int64, ctypes.c_int, ctypes.c_int, p, p, ctypes.POINTER(ctypes.c_int),
+                      ctypes.c_bool]
+        alt = ctypes.c_int(-1)
+        for n in (1 << 30, (1 << 31) - 1, 1 << 40):
+            assert f(None, None, None, None, n, 0, 26, None, None, ctypes.byref(alt), False) == 1  # hipErrorInvalidValue
+            assert alt.value == 0

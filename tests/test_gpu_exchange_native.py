@@ -29,8 +29,11 @@ def dev_view(ptr, n, typestr="<i8"):
 
 def test_exchange_round_trip_and_watermark():
     ex = NativeKeyByExchange(1, 0)
+    ex.set_timeout(30_000)  # bounded waits (gw_wait.h; the CPU tests cover expiry and errors)
     rng = np.random.default_rng(1)
     for n in (0, 1, 1000, 300_000, 17):
+        if n == 17:
+            ex.set_timeout(0)  # no deadline: only errors end a wait
         k = torch.from_numpy(rng.integers(-(1 << 62), 1 << 62, n).astype(np.int64)).cuda()
         t = torch.from_numpy(rng.integers(0, 1 << 40, n).astype(np.int64)).cuda()
         v = torch.from_numpy(rng.integers(-(1 << 40), 1 << 40, n).astype(np.int64)).cuda()

@@ -278,3 +278,40 @@ def test_exchange_words_into_packed_ingest(oracle_lib, kw):
     op.close()
     ora.close()
     ex.close()
+
+
+@pytest.mark.parametrize("case", ["session", "first_element", "side_output", "float", "pane_mismatch",
+                                  "offset_mismatch", "count_window"])
+def test_packed_ingest_refuses_handles_needing_the_record(case):
+    """A word's timestamp is its pane's start: gw_ingest_packed_device refuses (GW_E_UNSUPPORTED,
+    the handle unchanged) any handle whose decisions need the record's own timestamp or value,
+    and words whose pane grid does not divide the handle's windows."""
+    from gpu_helpers import gpu_operator
+    size, slide, flags, agg = 1000, 250, 0, "sum_i64"
+    geom = N.pack_geom(1000, 250, 0, 10_000)
+    kw = dict(assigner="sliding", size=size, slide=slide, agg=agg)
+    if case == "session":
+        kw = dict(assigner="session", gap=100, agg=agg)
+    elif case == "count_window":
+        kw = dict(assigner="count_tumbling", size=5, agg=agg)
+    elif case == "first_element":
+        flags = N.FLAG_FIRST_ELEMENT
+    elif case == "side_output":
+        flags = N.FLAG_LATE_SIDE_OUTPUT
+    elif case == "float":
+        kw["agg"] = "sum_f64"
+    elif case == "pane_mismatch":
+        geom = N.pack_geom(1000, 400, 0, 10_000)  # pane 200 does not divide slide 250
+    elif case == "offset_mismatch":
+        geom = N.pack_geom(1000, 250, 10, 10_000)
+    op = gpu_operator(kw, flags=flags)
+    w, fits = N.pack_records(np.arange(64, dtype=np.int64), np.full(64, 10_100, np.int64),
+                             np.ones(64, np.int64), geom)
+    assert fits.all()
+    dw = torch.from_numpy(w.view(np.int64)).cuda()
+    torch.cuda.synchronize()
+    with pytest.raises(N.GpuWinError) as e:
+        op.process_batch_packed_device_ptr(0, None, None, None, 64, dw.data_ptr(), geom,
+                                           stream=torch.cuda.current_stream().cuda_stream)
+    assert e.value.code == N.GW_E_UNSUPPORTED
+    op.close()

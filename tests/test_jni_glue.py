@@ -100,6 +100,19 @@ def test_exchange_glue_maps_invalid_arguments(jni):
         assert exc is not None and exc[0] == "java/lang/IllegalArgumentException"
 
 
+def test_exchange_set_timeout_glue(jni):
+    """GpuKeyByExchange.setTimeout: a missing exchange or a negative bound is
+    IllegalArgumentException (an aborted exchange's GW_E_STATE maps to IllegalStateException)."""
+    p = ctypes.c_void_p
+    st = getattr(jni, XCLS + "nativeSetTimeout")
+    st.restype = None
+    st.argtypes = [p, p, ctypes.c_int64, ctypes.c_int64]
+    env = jni.fake_env()
+    st(env, None, 0, 5000)
+    exc = exception(jni)
+    assert exc is not None and exc[0] == "java/lang/IllegalArgumentException"
+
+
 def _payload_fns(jni):
     p, i32, i64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64
     ing = getattr(jni, CLS + "nativeIngestPayload")
