@@ -145,10 +145,12 @@ def make_operator(W, N, args, K, world=1, rank=0, local=0, nb=None):
 
 
 class Steps:
-    """One step = one watermark batch: (N > 1: gw_exchange_batch = partition + one all-to-all of
-    (count, watermark, columns) + grouped send/receive) -> gw_ingest_device ->
-    gw_advance_watermark (fires every 10th step) -> fired rows consumed.  With `collect` the
-    rows of every watermark are drained to the host and (count, checksum) recorded."""
+    """One step = one watermark batch: (N > 1: the keyBy exchange, pipelined one batch ahead --
+    gw_exchange_begin of batch b + 1 (partition + the all-to-all of (count, watermark, columns)),
+    then gw_exchange_finish of batch b (its one host wait + grouped send/receive)) ->
+    gw_ingest_device -> gw_advance_watermark (fires every 10th step) -> fired rows consumed.
+    With `collect` the rows of every watermark are drained to the host and (count, checksum)
+    recorded."""
 
     def __init__(self, op, N, keys, ts, vals, wms, nb, ex=None, collect=False, ex_stream=None):
         import ctypes
@@ -157,6 +159,7 @@ class Steps:
         self.collect = collect
         self.per_wm = []  # (rows, checksum) per watermark when collecting
         self.exch_bytes = 0
+        self.begun = -1  # the last batch whose exchange has begun
         # the host side of a step stays lean (the GPU runs a batch in ~70 us): the library's entry
         # points and each batch's device column pointers resolved once, before any clock
         L = N.lib()
@@ -170,17 +173,27 @@ class Steps:
         self._ptrs = [(keys.data_ptr() + b * nb * es, ts.data_ptr() + b * nb * es,
                        vals.data_ptr() + b * nb * es if vals is not None else None) for b in range(len(wms))]
 
-    def step(self, b, timed=False, b_in=24, rank=0):
-        """One batch; returns the rows its watermark fired."""
+    def _begin(self, b):
+        nb = self.nb
+        lo, hi = b * nb, (b + 1) * nb
+        v = self.vals[lo:hi] if self.vals is not None else None
+        self.ex.begin(self.keys[lo:hi], self.ts[lo:hi], v, stream=self.ex_stream, wm=self.wms[b])
+        self.begun = b
+
+    def step(self, b, timed=False, b_in=24, rank=0, last=None):
+        """One batch; returns the rows its watermark fired.  last: the last batch of this phase
+        (warmup / timed): the exchange begins batches up to it one step ahead."""
         op, nb, N = self.op, self.nb, self.N
         if self.ex is not None:
-            lo, hi = b * nb, (b + 1) * nb
-            k, t = self.keys[lo:hi], self.ts[lo:hi]
-            v = self.vals[lo:hi] if self.vals is not None else None
             # the native exchange on a stream of its own; the ingest orders through the receive
             # set's hand-off stream, so batch b+1's partition and transfers overlap batch b's
-            # aggregation on the operator's stream
-            n, pk, pt, pv, _, wmin, ist = self.ex.exchange(k, t, v, stream=self.ex_stream, wm=self.wms[b])
+            # aggregation on the operator's stream, and batch b+1 is partitioned and its counts
+            # exchanged before the host waits for batch b's
+            if self.begun < b:
+                self._begin(b)
+            if last is not None and b + 1 <= last and self.begun < b + 1:
+                self._begin(b + 1)
+            n, pk, pt, pv, _, wmin, ist = self.ex.finish(self.ex_stream)
             if timed:  # bytes this rank sent to its peers (received packed share as the estimate)
                 f = self.ex.last_packed() / max(nb, 1)
                 self.exch_bytes += (nb - int(self.ex.counts()[0][rank])) * (8 * f + b_in * (1 - f))
@@ -264,7 +277,7 @@ def main(argv=None):
     # cost host time between batches; the fire and flush timers run on every launch
     op.enable_kernel_timing(0 if args.no_kernel_timing else 4)
     for b in range(args.warmup):
-        run.step(b)
+        run.step(b, last=args.warmup - 1)
     op.flush()  # warmup batches still buffered are applied outside the timed region
     for w in (0, 1, 2):
         op.kernel_time_ms(w)  # reset timers after warmup
@@ -280,7 +293,7 @@ def main(argv=None):
     cycles = []
     cyc_t, cyc_steps = t0, 0
     for b in range(args.warmup, steps_total):
-        fired = run.step(b, True, b_in, rank)
+        fired = run.step(b, True, b_in, rank, last=steps_total - 1)
         cyc_steps += 1
         if fired:  # the watermark completed windows: gw_advance_watermark fired them and synchronised
             now = time.perf_counter()
@@ -399,9 +412,9 @@ def main(argv=None):
         if world > 1 or ex is not None:
             pk = args.pack != "off" and not agg.endswith("f64")
             out["exchange_gbs_per_gpu"] = run.exch_bytes / elapsed / 1e9
-            out["exchange_path"] = ("gw_exchange_batch (libgpuwin RCCL: partition, one all-to-all of "
-                                    "(count, watermark, columns, packed count), one host wait, grouped send/recv "
-                                    "per batch" + ((", 8-B packed words decoded by pass 1" if args.pack == "auto"
+            out["exchange_path"] = ("gw_exchange_begin / gw_exchange_finish one batch ahead (libgpuwin RCCL: "
+                                    "partition, one all-to-all of (count, watermark, columns, packed count), one "
+                                    "bounded host wait, grouped send/recv per batch" + ((", 8-B packed words decoded by pass 1" if args.pack == "auto"
                                                     else ", 8-B packed words unpacked to columns") if pk
                                                    else ", 24-B records") + ")"
                                     if ex is not None else "none (key-partitioned source)")

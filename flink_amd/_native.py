@@ -50,7 +50,7 @@ EXPORTS = [
     "gw_key_group_for_hash", "gw_operator_for_key_group", "gw_default_max_parallelism",
     "gw_key_groups_device", "gw_partition_scratch_bytes", "gw_partition_device",
     "gw_decode_serialized", "gw_ingest_serialized", "gw_ingest_serialized_device",
-    "gw_exchange_unique_id", "gw_exchange_create", "gw_exchange_destroy", "gw_exchange_set_timeout", "gw_exchange_batch",
+    "gw_exchange_unique_id", "gw_exchange_create", "gw_exchange_destroy", "gw_exchange_set_timeout", "gw_exchange_batch", "gw_exchange_begin", "gw_exchange_finish",
     "gw_exchange_min_watermark", "gw_exchange_last_error", "gw_exchange_counts", "gw_exchange_plan",
     "gw_window_stagger_offset", "gw_stage_alloc", "gw_stage_columns", "gw_ingest_stage", "gw_stage_send",
     "gw_ingest_payload", "gw_ingest_payload_device", "gw_drain_payload",
@@ -196,6 +196,9 @@ def lib() -> ctypes.CDLL:
         "gw_exchange_set_timeout": (c_int, [p, i64]),
         "gw_exchange_batch": (c_int, [p, i64, p, p, p, p, i64, P64, ctypes.POINTER(p), ctypes.POINTER(p),
                                       ctypes.POINTER(p), ctypes.POINTER(p), P64, ctypes.POINTER(p), p]),
+        "gw_exchange_begin": (c_int, [p, i64, p, p, p, p, i64, p]),
+        "gw_exchange_finish": (c_int, [p, P64, ctypes.POINTER(p), ctypes.POINTER(p), ctypes.POINTER(p),
+                                       ctypes.POINTER(p), P64, ctypes.POINTER(p), p]),
         "gw_exchange_counts": (c_int, [p, p, p]),
         "gw_exchange_plan": (c_int, [i32, p, p, i64, i64, p, p, p, p, P64, P64]),
         "gw_window_stagger_offset": (c_int, [i32, i64, ctypes.c_double, i64, i64, P64]),

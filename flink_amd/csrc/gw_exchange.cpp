@@ -37,13 +37,27 @@ struct gw_exchange {
     int32_t nranks = 0, rank = 0, device = 0, max_p = 128;
     bool no_regions = false;
     int part_turn = 0;  // status half of the next region partition  // GW_PART_REGIONS=0: the three-pass contiguous partition (A/B)
-    void* scratch = nullptr;  // partition scratch
+    void* scratch = nullptr;  // partition scratch (used only inside a partition launch: shared)
     int64_t scratch_bytes = 0;
-    int64_t* part = nullptr;  // partitioned key | ts | value columns, cap records each
-    int32_t* part_hash = nullptr;
-    int64_t part_cap = 0;
-    int64_t part_regions = 0;  // regions the partition buffers were allocated for (1: contiguous)
-    uint64_t* part_packed = nullptr;  // packed words (partition numbering), cap records
+    // Two partition sets, so batch b + 1 can be partitioned and its counts exchanged
+    // (gw_exchange_begin) before batch b's columns are sent (gw_exchange_finish).
+    struct PartSet {
+        int64_t* part = nullptr;  // partitioned key | ts | value columns, cap records each
+        int32_t* part_hash = nullptr;
+        uint64_t* part_packed = nullptr;  // packed words (partition numbering), cap records
+        int64_t part_cap = 0;
+        int64_t part_regions = 0;  // regions the buffers were allocated for (1: contiguous)
+        int64_t* d_counts = nullptr;  // [2 nranks] partition counts (packing: packed, other per peer)
+        int64_t* d_msg = nullptr;     // [nranks][kMsg] send | [nranks][kMsg] receive
+        int64_t* h_msg = nullptr;     // its pinned copy
+        hipEvent_t ev_msg = nullptr;  // after the copy
+        // the begun batch
+        int64_t n = 0, wm = 0, cols_mask = 0;
+        bool regions = false, packed = false, has_value = false, has_hash = false;
+        gw_pack_geom g{};
+        hipStream_t stream = nullptr;
+    } ps[2];
+    int64_t begun = 0, finished = 0;  // batches begun / finished (set of batch i: i & 1)
     int64_t* recv[2] = {nullptr, nullptr};  // receive sets used in turn: key | ts | value columns
     int32_t* recv_hash[2] = {nullptr, nullptr};
     uint64_t* recv_packed[2] = {nullptr, nullptr};
@@ -58,11 +72,8 @@ struct gw_exchange {
     const uint64_t* last_words = nullptr;
     gw_pack_geom last_geom{};
     // One all-to-all message per peer and batch: (records for it, watermark, column mask,
-    // packed records).  d_msg: [nranks][kMsg] send | [nranks][kMsg] receive; h_msg its pinned copy.
+    // packed records), per partition set.
     static constexpr int kMsg = 4;
-    int64_t* d_counts = nullptr;  // [2 nranks] partition counts (packing: packed, other per peer)
-    int64_t* d_msg = nullptr;
-    int64_t* h_msg = nullptr;
     int64_t* d_wm = nullptr;
     int64_t* h_wm = nullptr;
     std::vector<int64_t> last_send, last_recv;
@@ -135,6 +146,30 @@ static int ex_wait(gw_exchange* ex, hipStream_t s, const char* what) {
     return ex_fail(ex, GW_E_STATE, why + "; communicator aborted");
 }
 
+// The same for one event (gw_exchange_finish: the count all-to-all's copy to the host).
+static int ex_wait_event(gw_exchange* ex, hipEvent_t ev, const char* what) {
+    EX_LIVE(ex);
+    hipError_t herr = hipSuccess;
+    ncclResult_t aerr = ncclSuccess;
+    const WaitResult w = poll_until_done(
+        [&] {
+            herr = hipEventQuery(ev);
+            return herr == hipSuccess ? 0 : herr == hipErrorNotReady ? 1 : 2;
+        },
+        [&] {
+            if (ncclCommGetAsyncError(ex->comm, &aerr) != ncclSuccess) return 1;
+            return aerr == ncclSuccess || aerr == ncclInProgress ? 0 : 1;
+        },
+        steady_now_ns, relax_backoff, ex->timeout_ms * 1000000);
+    if (w == WaitResult::kDone) return GW_OK;
+    std::string why = std::string(what) + ": ";
+    if (w == WaitResult::kStreamError) why += std::string("stream error: ") + hipGetErrorString(herr);
+    else if (w == WaitResult::kCommError) why += std::string("RCCL asynchronous error: ") + ncclGetErrorString(aerr);
+    else why += "no completion within " + std::to_string(ex->timeout_ms) + " ms (a peer died or diverged)";
+    ex_abort(ex);
+    return ex_fail(ex, GW_E_STATE, why + "; communicator aborted");
+}
+
 extern "C" {
 
 int gw_exchange_unique_id(void* id) {
@@ -163,14 +198,17 @@ int gw_exchange_create(gw_exchange** out, int32_t nranks, int32_t rank, const vo
     ncclUniqueId u;
     memcpy(&u, id, sizeof(u));
     if (ncclCommInitRank(&ex->comm, nranks, u, rank) != ncclSuccess) return bail(GW_E_DEVICE);
-    const size_t words = (size_t)nranks * (2 + 2 * gw_exchange::kMsg) + 2;
-    if (hipMalloc((void**)&ex->d_counts, words * 8) != hipSuccess) return bail(GW_E_OOM);
-    if (hipHostMalloc((void**)&ex->h_msg, (size_t)(2 * gw_exchange::kMsg * nranks + 2) * 8, hipHostMallocDefault) !=
-        hipSuccess)
-        return bail(GW_E_OOM);
-    ex->d_msg = ex->d_counts + 2 * nranks;
-    ex->d_wm = ex->d_msg + 2 * gw_exchange::kMsg * nranks;
-    ex->h_wm = ex->h_msg + 2 * gw_exchange::kMsg * nranks;
+    const size_t words = (size_t)nranks * (2 + 2 * gw_exchange::kMsg);
+    for (auto& q : ex->ps) {
+        if (hipMalloc((void**)&q.d_counts, words * 8) != hipSuccess) return bail(GW_E_OOM);
+        if (hipHostMalloc((void**)&q.h_msg, (size_t)(2 * gw_exchange::kMsg * nranks) * 8, hipHostMallocDefault) !=
+            hipSuccess)
+            return bail(GW_E_OOM);
+        q.d_msg = q.d_counts + 2 * nranks;
+        if (hipEventCreateWithFlags(&q.ev_msg, hipEventDisableTiming) != hipSuccess) return bail(GW_E_DEVICE);
+    }
+    if (hipMalloc((void**)&ex->d_wm, 8) != hipSuccess) return bail(GW_E_OOM);
+    if (hipHostMalloc((void**)&ex->h_wm, 8, hipHostMallocDefault) != hipSuccess) return bail(GW_E_OOM);
     for (int q = 0; q < 2; ++q) {
         if (hipStreamCreateWithFlags(&ex->handoff[q], hipStreamNonBlocking) != hipSuccess ||
             hipEventCreateWithFlags(&ex->ev_recv[q], hipEventDisableTiming) != hipSuccess ||
@@ -196,12 +234,17 @@ void gw_exchange_destroy(gw_exchange* ex) {
     if (!ex->aborted) (void)hipDeviceSynchronize();
     if (ex->comm) ncclCommDestroy(ex->comm);
     hipFree(ex->scratch);
-    hipFree(ex->part);
-    hipFree(ex->part_hash);
-    hipFree(ex->part_packed);
+    for (auto& q : ex->ps) {
+        hipFree(q.part);
+        hipFree(q.part_hash);
+        hipFree(q.part_packed);
+        hipFree(q.d_counts);
+        hipHostFree(q.h_msg);
+        if (q.ev_msg) hipEventDestroy(q.ev_msg);
+    }
     for (int q = 0; q < 2; ++q) { hipFree(ex->recv[q]); hipFree(ex->recv_hash[q]); hipFree(ex->recv_packed[q]); }
-    hipFree(ex->d_counts);
-    hipHostFree(ex->h_msg);
+    hipFree(ex->d_wm);
+    hipHostFree(ex->h_wm);
     for (int q = 0; q < 2; ++q) {
         if (ex->handoff[q]) hipStreamDestroy(ex->handoff[q]);
         if (ex->ev_recv[q]) hipEventDestroy(ex->ev_recv[q]);
@@ -333,50 +376,49 @@ int gw_exchange_last_words(const gw_exchange* ex, int64_t* n_words, const uint64
     return GW_OK;
 }
 
-int gw_exchange_batch(gw_exchange* ex, int64_t n, const int64_t* d_key, const int32_t* d_key_hash,
-                      const int64_t* d_ts, const int64_t* d_value, int64_t wm, int64_t* n_out,
-                      const int64_t** d_key_out, const int32_t** d_key_hash_out, const int64_t** d_ts_out,
-                      const int64_t** d_value_out, int64_t* wm_out, void** ingest_stream, void* stream) {
-    if (!ex || n < 0 || !n_out || !d_key_out || !d_ts_out || (n > 0 && (!d_key || !d_ts))) return GW_E_INVALID;
+int gw_exchange_begin(gw_exchange* ex, int64_t n, const int64_t* d_key, const int32_t* d_key_hash,
+                      const int64_t* d_ts, const int64_t* d_value, int64_t wm, void* stream) {
+    if (!ex || n < 0 || (n > 0 && (!d_key || !d_ts))) return GW_E_INVALID;
     EX_LIVE(ex);
+    if (ex->begun - ex->finished >= 2)
+        return ex_fail(ex, GW_E_STATE, "gw_exchange_begin: two batches begun and not finished");
     hipStream_t s = (hipStream_t)stream;
     ex->last_stream = s;
+    gw_exchange::PartSet& q = ex->ps[ex->begun & 1];
     const int P = ex->nranks;
     constexpr int M = gw_exchange::kMsg;
-    // packing this batch: configured, a previous combined watermark, no key-hash column, and
-    // values only if the caller declared them packable -- the same on every rank (the mask
-    // check below fails every rank otherwise)
+    // packing this batch: configured, a combined watermark known from a finished batch, no
+    // key-hash column, and values only if the caller declared them packable -- the same on
+    // every rank (the message check in gw_exchange_finish fails every rank otherwise)
     gw_pack_geom g{};
     if (ex->pack_on && !d_key_hash && (!d_value || ex->pack_values))
         (void)gw_pack_geom_init(&g, ex->pack_size, ex->pack_slide, ex->pack_offset, ex->last_wm);
     const bool packed = g.enabled != 0;
     // 1. stable device partition by owner (packing: by owner, then packed / not).  Up to
     // kPartRegionMaxOwners ranks into one region per owner (single pass, buffers P times the
-    // batch: 36 B x P per record of capacity), beyond that the contiguous three-pass layout.
-    // The region layout holds P times the batch (24 B of columns + 8 B of words per record and
-    // region, + 4 B with a key-hash column); past kRegionBudget it falls back to the contiguous
-    // three-pass layout, whose buffers hold the batch once.  The choice is local to the rank.
-    const int64_t want_cap = std::max(n + n / 4 + 1024, ex->part_cap);
+    // batch: 24 B of columns + 8 B of words per record and region, + 4 B with a key-hash
+    // column); past kRegionBudget, or beyond 16 ranks, the contiguous three-pass layout,
+    // whose buffers hold the batch once.  The choice is local to the rank.
+    const int64_t want_cap = std::max(n + n / 4 + 1024, q.part_cap);
     const bool regions = P <= kPartRegionMaxOwners && !ex->no_regions &&
                          (i128)want_cap * P * (32 + (d_key_hash ? 4 : 0)) <= (i128)kRegionBudget;
     const int64_t R = regions ? P : 1;
-    if (n > ex->part_cap || R != ex->part_regions) {
-        const int rc_w = ex_wait(ex, s, "partition buffer");  // the last batch's sends read them
+    if (n > q.part_cap || R != q.part_regions) {
+        const int rc_w = ex_wait(ex, s, "partition buffer");  // this set's last sends read them
         if (rc_w != GW_OK) return rc_w;
-        hipFree(ex->part);
-        hipFree(ex->part_hash);
-        hipFree(ex->part_packed);
-        ex->part = nullptr;
-        ex->part_hash = nullptr;
-        ex->part_packed = nullptr;
-        const int64_t c = want_cap;
-        EX_HIP(hipMalloc((void**)&ex->part, (size_t)c * R * 3 * 8));
-        ex->part_cap = c;
-        ex->part_regions = R;
+        hipFree(q.part);
+        hipFree(q.part_hash);
+        hipFree(q.part_packed);
+        q.part = nullptr;
+        q.part_hash = nullptr;
+        q.part_packed = nullptr;
+        EX_HIP(hipMalloc((void**)&q.part, (size_t)want_cap * R * 3 * 8));
+        q.part_cap = want_cap;
+        q.part_regions = R;
     }
-    if (d_key_hash && !ex->part_hash) EX_HIP(hipMalloc((void**)&ex->part_hash, (size_t)ex->part_cap * R * 4));
-    if (packed && !ex->part_packed) EX_HIP(hipMalloc((void**)&ex->part_packed, (size_t)ex->part_cap * R * 8));
-    const int64_t need = regions ? partition_regions_scratch_bytes(ex->part_cap, 2 * P)
+    if (d_key_hash && !q.part_hash) EX_HIP(hipMalloc((void**)&q.part_hash, (size_t)q.part_cap * R * 4));
+    if (packed && !q.part_packed) EX_HIP(hipMalloc((void**)&q.part_packed, (size_t)q.part_cap * R * 8));
+    const int64_t need = regions ? partition_regions_scratch_bytes(q.part_cap, 2 * P)
                                  : partition_scratch_bytes(std::max<int64_t>(n, 1), 2 * P);
     if (need > ex->scratch_bytes) {
         const int rc_w = ex_wait(ex, s, "partition scratch");
@@ -385,44 +427,70 @@ int gw_exchange_batch(gw_exchange* ex, int64_t n, const int64_t* d_key, const in
         ex->scratch = nullptr;
         EX_HIP(hipMalloc(&ex->scratch, (size_t)need));
         ex->scratch_bytes = need;
-        if (regions) {  // both status halves start zeroed; each launch then zeroes the next's
-            EX_HIP(hipMemsetAsync(ex->scratch, 0, (size_t)need, s));
-            ex->part_turn = 0;
-        }
+        EX_HIP(hipMemsetAsync(ex->scratch, 0, (size_t)need, s));  // both status halves start zeroed
+        ex->part_turn = 0;
     }
-    const int64_t col = ex->part_cap * R;  // one column of the partition buffer
-    int64_t* pk = ex->part;
+    const int64_t col = q.part_cap * R;  // one column of the partition buffer
+    int64_t* pk = q.part;
     int64_t* pt = pk + col;
     int64_t* pv = pt + col;
     if (n > 0 && regions) {
-        EX_HIP(launch_partition_regions(n, d_key, d_key_hash, d_ts, d_value, ex->max_p, P, ex->part_cap, pk, pt,
-                                        d_value ? pv : nullptr, d_key_hash ? ex->part_hash : nullptr,
-                                        packed ? &g : nullptr, ex->part_packed, ex->d_counts, ex->scratch, s,
+        EX_HIP(launch_partition_regions(n, d_key, d_key_hash, d_ts, d_value, ex->max_p, P, q.part_cap, pk, pt,
+                                        d_value ? pv : nullptr, d_key_hash ? q.part_hash : nullptr,
+                                        packed ? &g : nullptr, q.part_packed, q.d_counts, ex->scratch, s,
                                         ex->part_turn, 2 * P));
         ex->part_turn ^= 1;
     } else if (n > 0) {
         EX_HIP(launch_partition(n, d_key, d_key_hash, d_ts, d_value, ex->max_p, P, pk, pt, d_value ? pv : nullptr,
-                                ex->d_counts, ex->scratch, s, d_key_hash ? ex->part_hash : nullptr,
-                                packed ? &g : nullptr, ex->part_packed));
+                                q.d_counts, ex->scratch, s, d_key_hash ? q.part_hash : nullptr,
+                                packed ? &g : nullptr, q.part_packed));
     } else {
-        EX_HIP(hipMemsetAsync(ex->d_counts, 0, (size_t)2 * P * 8, s));
+        EX_HIP(hipMemsetAsync(q.d_counts, 0, (size_t)2 * P * 8, s));
     }
-    // 2. one message per peer: (records, watermark, columns, packed records); all-to-all,
-    // then one host wait
+    // 2. one message per peer: (records, watermark, columns, packed records); the all-to-all
+    // and its copy to the host are queued here, the host reads them in gw_exchange_finish.
     // The column mask also carries the packing geometry (pane, offset, base pane) folded to 32
-    // bits: ranks packing against different windows fail together below instead of decoding
-    // each other's words with the wrong panes.
-    const int64_t cols_mask = (d_value ? 1 : 0) | (d_key_hash ? 2 : 0) | (packed ? 4 : 0) |
-                              (packed ? (int64_t)(geom_fold(g) << 32) : 0);
-    EX_HIP(launch_exchange_message(ex->d_counts, P, wm, cols_mask, packed ? 1 : 0, ex->d_msg, s));
-    EX_NCCL(ncclAllToAll(ex->d_msg, ex->d_msg + M * P, M, ncclInt64, ex->comm, s));
-    EX_HIP(hipMemcpyAsync(ex->h_msg, ex->d_msg, (size_t)2 * M * P * 8, hipMemcpyDeviceToHost, s));
+    // bits: ranks packing against different windows fail together instead of decoding each
+    // other's words with the wrong panes.
+    q.cols_mask = (d_value ? 1 : 0) | (d_key_hash ? 2 : 0) | (packed ? 4 : 0) |
+                  (packed ? (int64_t)(geom_fold(g) << 32) : 0);
+    EX_HIP(launch_exchange_message(q.d_counts, P, wm, q.cols_mask, packed ? 1 : 0, q.d_msg, s));
+    EX_NCCL(ncclAllToAll(q.d_msg, q.d_msg + M * P, M, ncclInt64, ex->comm, s));
+    EX_HIP(hipMemcpyAsync(q.h_msg, q.d_msg, (size_t)2 * M * P * 8, hipMemcpyDeviceToHost, s));
+    EX_HIP(hipEventRecord(q.ev_msg, s));
+    q.n = n;
+    q.wm = wm;
+    q.regions = regions;
+    q.packed = packed;
+    q.g = g;
+    q.has_value = d_value != nullptr;
+    q.has_hash = d_key_hash != nullptr;
+    q.stream = s;
+    ex->begun++;
+    return GW_OK;
+}
+
+int gw_exchange_finish(gw_exchange* ex, int64_t* n_out, const int64_t** d_key_out, const int32_t** d_key_hash_out,
+                       const int64_t** d_ts_out, const int64_t** d_value_out, int64_t* wm_out, void** ingest_stream,
+                       void* stream) {
+    if (!ex || !n_out || !d_key_out || !d_ts_out) return GW_E_INVALID;
+    EX_LIVE(ex);
+    if (ex->finished == ex->begun) return ex_fail(ex, GW_E_STATE, "gw_exchange_finish: no batch begun");
+    hipStream_t s = (hipStream_t)stream;
+    gw_exchange::PartSet& q = ex->ps[ex->finished & 1];
+    if (s != q.stream) return ex_fail(ex, GW_E_INVALID, "gw_exchange_finish: not the stream the batch began on");
+    const int P = ex->nranks;
+    constexpr int M = gw_exchange::kMsg;
+    // the host's one wait per batch: this batch's count all-to-all (the next batch's partition,
+    // begun already, keeps the stream busy meanwhile)
     {
-        const int rc_w = ex_wait(ex, s, "gw_exchange_batch: count all-to-all");
+        const int rc_w = ex_wait_event(ex, q.ev_msg, "gw_exchange_finish: count all-to-all");
         if (rc_w != GW_OK) return rc_w;
     }
-    const int64_t* sm = ex->h_msg;
-    const int64_t* rm = ex->h_msg + M * P;
+    const bool packed = q.packed, regions = q.regions;
+    const gw_pack_geom g = q.g;
+    const int64_t* sm = q.h_msg;
+    const int64_t* rm = q.h_msg + M * P;
     std::vector<int64_t>& so = ex->plan[0];
     std::vector<int64_t>& sc = ex->plan[1];
     std::vector<int64_t>& ro = ex->plan[2];
@@ -431,16 +499,21 @@ int gw_exchange_batch(gw_exchange* ex, int64_t n, const int64_t* d_key, const in
     std::vector<int64_t>& rwo = ex->pplan[1];
     std::vector<int64_t>& rpo = ex->pplan[2];
     std::vector<int64_t>& rp = ex->pplan[3];
-    int64_t total = 0, wmin = wm, tw = 0, tp = 0;
+    int64_t total = 0, wmin = q.wm, tw = 0, tp = 0;
     // every rank sees every rank's mask: all of them fail here together, before any send
-    if (gw_exchange_plan(P, sm, rm, cols_mask, wm, so.data(), sc.data(), ro.data(), rc.data(), &total, &wmin))
+    if (gw_exchange_plan(P, sm, rm, q.cols_mask, q.wm, so.data(), sc.data(), ro.data(), rc.data(), &total, &wmin)) {
+        ex->finished++;
         return ex_fail(ex, GW_E_INVALID, "gw_exchange_batch: ranks pass different columns or packing geometry");
-    if (gw_exchange_plan_packed(P, sm, rm, sp.data(), rwo.data(), rpo.data(), rp.data(), &tw, &tp))
+    }
+    if (gw_exchange_plan_packed(P, sm, rm, sp.data(), rwo.data(), rpo.data(), rp.data(), &tw, &tp)) {
+        ex->finished++;
         return ex_fail(ex, GW_E_INVALID, "gw_exchange_batch: bad packed counts");
+    }
+    ex->finished++;
     ex->last_send = sc;
     ex->last_recv = rc;
     ex->last_packed = tp;
-    ex->last_wm = wmin;  // the next batch's base pane
+    ex->last_wm = wmin;  // the base pane of the batches begun from now on
     // 3. this turn's receive set: free once the ingest two batches ago has read it
     const int u = ex->turn;
     ex->turn ^= 1;
@@ -463,49 +536,53 @@ int gw_exchange_batch(gw_exchange* ex, int64_t n, const int64_t* d_key, const in
         EX_HIP(hipMalloc((void**)&ex->recv[u], (size_t)c * 3 * 8));
         ex->recv_cap[u] = c;
     }
-    if (d_key_hash && !ex->recv_hash[u]) EX_HIP(hipMalloc((void**)&ex->recv_hash[u], (size_t)ex->recv_cap[u] * 4));
+    if (q.has_hash && !ex->recv_hash[u]) EX_HIP(hipMalloc((void**)&ex->recv_hash[u], (size_t)ex->recv_cap[u] * 4));
     if (packed && !ex->recv_packed[u]) EX_HIP(hipMalloc((void**)&ex->recv_packed[u], (size_t)ex->recv_cap[u] * 8));
     int64_t* rk = ex->recv[u];
     int64_t* rt = rk + ex->recv_cap[u];
     int64_t* rv = rt + ex->recv_cap[u];
     int32_t* rh = ex->recv_hash[u];
+    const int64_t col = q.part_cap * q.part_regions;
+    int64_t* pk = q.part;
+    int64_t* pt = pk + col;
+    int64_t* pv = pt + col;
     // 4. grouped point-to-point send / receive per peer (the group is always closed): per
     // peer its packed words, then each column of its other records, which land behind the
     // other peers' other records in rank order; the unpacked words follow them all
     struct Col { const void* src; void* dst; ncclDataType_t t; size_t w; };
     const Col cols[4] = {{pk, rk, ncclInt64, 8},
                          {pt, rt, ncclInt64, 8},
-                         {d_value ? pv : nullptr, rv, ncclInt64, 8},
-                         {d_key_hash ? ex->part_hash : nullptr, rh, ncclInt32, 4}};
+                         {q.has_value ? pv : nullptr, rv, ncclInt64, 8},
+                         {q.has_hash ? q.part_hash : nullptr, rh, ncclInt32, 4}};
     // The rank's own share does not leave the device: a device-to-device copy on the same
     // stream (the copy engine path runs at HBM speed; RCCL's send/receive to self ran its
     // copy on a few channels, ~1 TB/s), queued after the group so it overlaps nothing it must
     // not.  At P ranks it is 1/P of the records.
     const int me = ex->rank;
     // where peer q's packed words / other records start in the partition buffers
-    auto pw_off = [&](int q) -> int64_t { return regions ? q * ex->part_cap : so[q]; };
-    auto pc_off = [&](int q) -> int64_t { return regions ? q * ex->part_cap : so[q] + sp[q]; };
+    auto pw_off = [&](int r) -> int64_t { return regions ? r * q.part_cap : so[r]; };
+    auto pc_off = [&](int r) -> int64_t { return regions ? r * q.part_cap : so[r] + sp[r]; };
     EX_NCCL(ncclGroupStart());
     ncclResult_t r = ncclSuccess;
-    for (int q = 0; q < P && r == ncclSuccess && packed; ++q) {
-        if (q == me) continue;
-        if (sp[q]) r = ncclSend(ex->part_packed + pw_off(q), (size_t)sp[q], ncclUint64, q, ex->comm, s);
-        if (r == ncclSuccess && rp[q]) r = ncclRecv(ex->recv_packed[u] + rpo[q], (size_t)rp[q], ncclUint64, q, ex->comm, s);
+    for (int pe = 0; pe < P && r == ncclSuccess && packed; ++pe) {
+        if (pe == me) continue;
+        if (sp[pe]) r = ncclSend(q.part_packed + pw_off(pe), (size_t)sp[pe], ncclUint64, pe, ex->comm, s);
+        if (r == ncclSuccess && rp[pe]) r = ncclRecv(ex->recv_packed[u] + rpo[pe], (size_t)rp[pe], ncclUint64, pe, ex->comm, s);
     }
     for (const Col& c : cols) {
         if (!c.src) continue;
-        for (int q = 0; q < P && r == ncclSuccess; ++q) {
-            if (q == me) continue;
-            const int64_t ns = sc[q] - sp[q], nr = rc[q] - rp[q];
-            if (ns) r = ncclSend((const char*)c.src + pc_off(q) * c.w, (size_t)ns, c.t, q, ex->comm, s);
-            if (r == ncclSuccess && nr) r = ncclRecv((char*)c.dst + rwo[q] * c.w, (size_t)nr, c.t, q, ex->comm, s);
+        for (int pe = 0; pe < P && r == ncclSuccess; ++pe) {
+            if (pe == me) continue;
+            const int64_t ns = sc[pe] - sp[pe], nr = rc[pe] - rp[pe];
+            if (ns) r = ncclSend((const char*)c.src + pc_off(pe) * c.w, (size_t)ns, c.t, pe, ex->comm, s);
+            if (r == ncclSuccess && nr) r = ncclRecv((char*)c.dst + rwo[pe] * c.w, (size_t)nr, c.t, pe, ex->comm, s);
         }
     }
     const ncclResult_t re = ncclGroupEnd();
     if (r != ncclSuccess) return ex_fail(ex, GW_E_DEVICE, std::string("ncclSend/ncclRecv: ") + ncclGetErrorString(r));
     if (re != ncclSuccess) return ex_fail(ex, GW_E_DEVICE, std::string("ncclGroupEnd: ") + ncclGetErrorString(re));
     if (packed && sp[me])  // send count = receive count for the rank itself
-        EX_HIP(hipMemcpyAsync(ex->recv_packed[u] + rpo[me], ex->part_packed + pw_off(me), (size_t)sp[me] * 8,
+        EX_HIP(hipMemcpyAsync(ex->recv_packed[u] + rpo[me], q.part_packed + pw_off(me), (size_t)sp[me] * 8,
                               hipMemcpyDeviceToDevice, s));
     for (const Col& c : cols) {
         const int64_t ns = sc[me] - sp[me];
@@ -517,7 +594,7 @@ int gw_exchange_batch(gw_exchange* ex, int64_t n, const int64_t* d_key, const in
     ex->last_geom = g;
     if (packed && tp > 0) {
         if (ex->unpack)
-            EX_HIP(launch_unpack(tp, ex->recv_packed[u], g, rk + tw, rt + tw, d_value ? rv + tw : nullptr, s));
+            EX_HIP(launch_unpack(tp, ex->recv_packed[u], g, rk + tw, rt + tw, q.has_value ? rv + tw : nullptr, s));
         else
             ex->last_words = ex->recv_packed[u];
     }
@@ -530,11 +607,24 @@ int gw_exchange_batch(gw_exchange* ex, int64_t n, const int64_t* d_key, const in
     *n_out = n_cols;
     *d_key_out = rk;
     *d_ts_out = rt;
-    if (d_value_out) *d_value_out = d_value ? rv : nullptr;
-    if (d_key_hash_out) *d_key_hash_out = d_key_hash ? rh : nullptr;
+    if (d_value_out) *d_value_out = q.has_value ? rv : nullptr;
+    if (d_key_hash_out) *d_key_hash_out = q.has_hash ? rh : nullptr;
     if (wm_out) *wm_out = wmin;
     if (ingest_stream) *ingest_stream = (void*)ex->handoff[u];
     return GW_OK;
+}
+
+int gw_exchange_batch(gw_exchange* ex, int64_t n, const int64_t* d_key, const int32_t* d_key_hash,
+                      const int64_t* d_ts, const int64_t* d_value, int64_t wm, int64_t* n_out,
+                      const int64_t** d_key_out, const int32_t** d_key_hash_out, const int64_t** d_ts_out,
+                      const int64_t** d_value_out, int64_t* wm_out, void** ingest_stream, void* stream) {
+    if (!ex || n < 0 || !n_out || !d_key_out || !d_ts_out || (n > 0 && (!d_key || !d_ts))) return GW_E_INVALID;
+    if (ex->begun != ex->finished)
+        return ex_fail(ex, GW_E_STATE, "gw_exchange_batch with a batch begun: finish it first");
+    const int rc = gw_exchange_begin(ex, n, d_key, d_key_hash, d_ts, d_value, wm, stream);
+    if (rc != GW_OK) return rc;
+    return gw_exchange_finish(ex, n_out, d_key_out, d_key_hash_out, d_ts_out, d_value_out, wm_out, ingest_stream,
+                              stream);
 }
 
 int gw_exchange_counts(const gw_exchange* ex, int64_t* send, int64_t* recv) {

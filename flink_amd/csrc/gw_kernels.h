@@ -2,8 +2,11 @@
 //
 // Pane state table: `cap` slots in `nreg` regions of S = 2^log2S slots,
 // plus one sentinel region (slot index `cap`) for the key Long.MIN_VALUE, which doubles
-// as the empty marker.  A key's region is the top bits of its hash, its home slot the low
-// bits; linear probing stays inside the region.  Each region is stored SoA:
+// as the empty marker.  The regions form 2^rb1 buckets of `nsub` regions each (nsub need not
+// be a power of two, so the table can sit at load ~0.8 instead of a power of two at <= 0.7):
+// a key's bucket is the top rb1 bits of its hash, its region within the bucket the next 32
+// bits scaled to nsub (multiply-high), its home slot the low bits; linear probing stays
+// inside the region.  Each region is stored SoA:
 //
 //     keys [S]                int64, kEmptyKey while free (set once by CAS)
 //     mask [S]                presence bits per ring cell (SUM/MIN/MAX only), 1/2/4/8
@@ -21,10 +24,11 @@ namespace gw {
 struct PaneTable {
     int64_t* base;
     int64_t cap;           // slots = nreg << log2S (sentinel slot index = cap)
-    int64_t nreg;          // regions (power of two), + 1 sentinel region allocated
+    int64_t nreg;          // regions = nsub << rb1, + 1 sentinel region allocated
     int64_t region_words;  // S + mask words + S * R * W
     int32_t log2S;
-    int32_t log2nreg;
+    int32_t rb1;           // bucket bits: the pass-1 buckets of the region path (0: one region)
+    int32_t nsub;          // regions per bucket (1: single-pass table)
     int32_t ring;          // R
     int32_t words;         // W
     int32_t agg;
@@ -76,9 +80,16 @@ __device__ __forceinline__ uint64_t pt_mask_get(const PaneTable& t, int64_t g) {
 __device__ __forceinline__ void pt_mask_put(const PaneTable& t, int64_t g, uint64_t v) {
     mask_put(pt_mask_base(t, g >> t.log2S), g & (pt_S(t) - 1), t.mask_shift, v);
 }
-// region and home slot of a key hash (independent bit ranges)
+// bucket, region within the bucket, region and home slot of a key hash (independent bit
+// ranges: the top rb1 bits, the 32 below them, the low log2S)
+GW_HD int64_t pt_bucket(const PaneTable& t, uint64_t h) { return t.rb1 == 0 ? 0 : (int64_t)(h >> (64 - t.rb1)); }
+// also valid on a compact region word (its top rb1 bits replaced, gw_pane.hip cmp_pack)
+GW_HD int32_t pt_sub(const PaneTable& t, uint64_t h) {
+    const uint32_t u = (uint32_t)((h << t.rb1) >> 32);
+    return (int32_t)(((uint64_t)u * (uint32_t)t.nsub) >> 32);
+}
 GW_HD int64_t pt_key_region(const PaneTable& t, uint64_t h) {
-    return t.log2nreg == 0 ? 0 : (int64_t)(h >> (64 - t.log2nreg));
+    return t.nsub == 1 ? pt_bucket(t, h) : pt_bucket(t, h) * t.nsub + pt_sub(t, h);
 }
 // The home slot is aligned to a group of kProbeGroup slots: linear probing then starts
 // on a 32-B group boundary, so k_rgn_apply compares a whole group of keys per LDS step
@@ -161,8 +172,8 @@ struct IngestArgs {
     int64_t* d_a1;
     DevStatus* st;
     // region path (k_rgn_p1 / k_rgn_plan* / k_rgn_p2 / k_rgn_apply, gw_pane.hip)
-    int32_t d1_bits;       // region = (pass-1 bucket << d2_bits) | pass-2 bucket
-    int32_t d2_bits;       // 0: single-pass table (apply reads the P1 tiles directly)
+    int32_t d1_bits;       // region = pass-1 bucket * nsub + pass-2 bucket (t.rb1, t.nsub)
+    int32_t two_pass;      // 0: single-pass table, nsub = 1 (apply reads the P1 tiles directly)
     int32_t fmt;           // region record format (gw_pane.hip): 0 wide, 1 compact (hash word +
                            // 32-bit value), 2 narrow (32-bit key + 28-bit value; 4 B for COUNT)
     int32_t nar2;          // narrow two-pass flushes (k_rgn_apply_nar): P2 groups each round by
@@ -255,6 +266,8 @@ struct FireArgs {
     int64_t slide;
     int64_t size;
     uint64_t rmask;     // ring positions retired after this pass
+    int32_t lazy_retire;  // presence-mask aggregates: retiring clears the mask bits only; the
+                          // cells keep stale values behind clear bits (gw_runtime.cpp stale_pos)
     uint64_t wmask[kMaxRing];
     int64_t* o_key;
     int64_t* o_start;
@@ -338,6 +351,9 @@ hipError_t launch_refire_keys(int mode, const int64_t* src, int64_t base, uint64
                               hipStream_t s);
 hipError_t launch_deferred_min(const int64_t* pane, int64_t n, DevStatus* st, hipStream_t s);
 hipError_t launch_fire(const FireArgs& a, hipStream_t s);
+// Cells of ring positions `pmask` whose presence bit is clear -> the identity (the retires a
+// lazy fire left behind, before a kernel that adds into cells with device atomics)
+hipError_t launch_clean_stale(const PaneTable& t, uint64_t pmask, hipStream_t s);
 hipError_t launch_evict(const EvictArgs& a, hipStream_t s);
 hipError_t launch_rehash(const PaneTable& o, const PaneTable& n, DevStatus* st, hipStream_t s);
 hipError_t launch_status_set(DevStatus* st, int word, unsigned long long v, int shard_field, hipStream_t s);

@@ -456,13 +456,14 @@ __global__ void __launch_bounds__(256) k_ingest_preagg(IngestArgs a) {
 // ---------------------------------------------------------------------------
 // region path: tile-local two-level bucketing, then one workgroup per region
 // ---------------------------------------------------------------------------
-// In-ring records are bucketed by table region (the top log2nreg bits of the key hash)
-// without histogram passes:
+// In-ring records are bucketed by table region (gw_kernels.h pt_key_region: bucket = the top
+// rb1 bits of the key hash, region within the bucket = the next bits scaled to nsub) without
+// histogram passes:
 //   P1  (per watermark batch) one block per 4096-record tile classifies its records,
-//       sorts them in LDS by pass-1 bucket (top d1 region bits) and writes the tile
+//       sorts them in LDS by pass-1 bucket (top d1 = rb1 hash bits) and writes the tile
 //       back contiguously, plus one descriptor row: per bucket (start << 16 | count).
 //   P2  (per flush, two-pass tables) block (b1, j) gathers bucket b1's runs from a group
-//       of G P1 tiles, sorts them by the remaining d2 region bits in LDS and writes
+//       of G P1 tiles, sorts them by region within the bucket (pt_sub) in LDS and writes
 //       rounds of <= 4096 records, each with a descriptor row of its own.  Two small
 //       plan kernels place the blocks' outputs (bucket-major) and their rounds.
 //   apply  one workgroup per region gathers its runs (from the P2 rounds of its bucket,
@@ -721,7 +722,7 @@ __device__ __forceinline__ void p1_tile(const IngestArgs& a, int64_t g, int64_t 
                 special = true;  // the sentinel slot: below
             } else {
                 const uint64_t h = slot_hash(key[it]);
-                bk = (int)(pt_key_region(a.t, h) >> a.d2_bits);
+                bk = (int)pt_bucket(a.t, h);
                 if constexpr (C) key[it] = (int64_t)cmp_pack(h, ps, a.d1_bits);  // key -> word
                 if constexpr (NR) key[it] = N4 ? (int64_t)nar_pack32(key[it], ps) : (int64_t)nar_pack(key[it], v0, ps);
             }
@@ -978,17 +979,15 @@ __global__ void __launch_bounds__(kPartThreads) k_rgn_p2(IngestArgs a) {
     const TileLds s = tile_lds<AV>(smem);
     int32_t* s_v32 = reinterpret_cast<int32_t*>(s.a0);
     uint32_t* s_r32 = reinterpret_cast<uint32_t*>(s.k);
-    // C: region bits of the hash word; narrow two-pass flushes (nar2): super-region bits
-    const int d2r = a.nar2 ? a.d2_bits - a.sr_bits : a.d2_bits;
-    const int lr_sh = 64 - (a.d1_bits + d2r);
+    // pass-2 bucket: the region within the pass-1 bucket (pt_sub; C: of the hash word); narrow
+    // two-pass flushes (nar2): (super-region, ring position)
     __shared__ uint32_t lh[kPartBuckets], ls[kPartBuckets];
     __shared__ uint32_t r_cnt[kMaxGroup], r_pre[kMaxGroup + 1], wsum[kPartThreads / 64];
     __shared__ int64_t r_src[kMaxGroup];
     const int64_t b1 = blockIdx.x / a.ngroups, j = blockIdx.x - b1 * a.ngroups;
     const int64_t t0 = j * a.p2_group;
     const int nt = (int)min((int64_t)a.p2_group, a.ntiles - t0);
-    const int64_t m2 = ((int64_t)1 << d2r) - 1;
-    const int nb2 = a.nar2 ? (int)(m2 + 1) << 3 : (int)(m2 + 1);  // nar2: (super-region, ring position)
+    const int nb2 = a.nar2 ? (a.t.nsub >> a.sr_bits) << 3 : a.t.nsub;  // nar2: (super-region, ring position)
     for (int i = threadIdx.x; i < nt; i += blockDim.x) {
         const uint32_t d = a.p2_desc[b1 * a.ntiles + t0 + i];
         r_cnt[i] = d & 0xffffu;
@@ -1031,12 +1030,12 @@ __global__ void __launch_bounds__(kPartThreads) k_rgn_p2(IngestArgs a) {
             if (bk[it] < 0) continue;
             if constexpr (NR) {  // the key's hash gives its region
                 const int64_t k = N4 ? nar_key32((uint32_t)key[it]) : nar_key((uint64_t)key[it]);
-                bk[it] = (int)((slot_hash(k) >> lr_sh) & (uint64_t)m2);
+                bk[it] = pt_sub(a.t, slot_hash(k));
                 if (a.nar2)
-                    bk[it] = (bk[it] << 3) |
+                    bk[it] = ((bk[it] >> a.sr_bits) << 3) |
                              (int)nar_pos(N4 ? (uint32_t)key[it] : (uint32_t)((uint64_t)key[it] >> 32));
             } else {
-                bk[it] = C ? (int)(((uint64_t)key[it] >> lr_sh) & (uint64_t)m2) : (int)(rgn_of(a.t, key[it]) & m2);
+                bk[it] = pt_sub(a.t, C ? (uint64_t)key[it] : slot_hash(key[it]));
             }
             rank[it] = atomicAdd(&lh[bk[it]], 1u);
         }
@@ -1126,8 +1125,8 @@ __global__ void __launch_bounds__(kApplyThreads) GW_APPLY_ATTR k_rgn_apply(Inges
     const int64_t S = pt_S(a.t);
     const int W = a.t.words;
     // this region's runs: rounds [rb, re) of its bucket, column col of their rows
-    const int64_t bucket = r >> a.d2_bits, col = r & (((int64_t)1 << a.d2_bits) - 1);
-    const bool single = a.d2_bits == 0;
+    const int64_t bucket = r / a.t.nsub, col = r - bucket * a.t.nsub;
+    const bool single = !a.two_pass;
     const int64_t rb = single ? 0 : a.rbeg[bucket], re = single ? a.ntiles : a.rbeg[bucket + 1];
     const int64_t ccol = single ? r : col;
     const uint32_t* rows = single ? a.p1_row : a.r_row;
@@ -1204,6 +1203,17 @@ __global__ void __launch_bounds__(kApplyThreads) GW_APPLY_ATTR k_rgn_apply(Inges
     // the barrier also waits for the LDS-DMA
     const int any = __syncthreads_or((int)(d0 & 0xffffu)) || (re - rb > kApplyRuns);
     if (!any) return;
+    if constexpr (M) {  // a clear presence bit: the cell is the identity whatever it holds (a lazy
+                        // fire retire, k_fire2); the loaded pane arrays are read after the run
+                        // loop's first barrier
+        for (int ai = 0; ai < 2; ++ai) {
+            const int act = ai ? act1 : act0;
+            if (!(ai ? ld1 : ld0)) continue;
+            long long* lc = lcell + (int64_t)ai * S;
+            for (int j = threadIdx.x; j < (int)S; j += blockDim.x)
+                if (!((mask_get(lmask, j, msh) >> act) & 1)) lc[j] = id0;
+        }
+    }
     if ((int)threadIdx.x < nr0) {
         r_cnt[threadIdx.x] = d0 & 0xffffu;
         r_src[threadIdx.x] = (uint32_t)(base0 + (d0 >> 16));
@@ -1587,9 +1597,9 @@ __global__ void __launch_bounds__(kApplyThreads) GW_APPLY_ATTR k_rgn_apply_nar(I
     const int F = 1 << a.sr_bits;
     const int S = (int)pt_S(a.t), FS = F * S;
     const int l2S = a.t.log2S;
-    const int d2v = a.d2_bits - a.sr_bits;
+    const int64_t ncol = a.t.nsub >> a.sr_bits;  // super-regions per bucket
     const int64_t sr = blockIdx.x;
-    const int64_t bucket = sr >> d2v, col = sr & (((int64_t)1 << d2v) - 1);
+    const int64_t bucket = sr / ncol, col = sr - bucket * ncol;
     // the runs of this super-region: this flush's rounds (list 0) and the rounds of the
     // previous flush that carried ring positions (list 1, positions c_mask)
     const int64_t rb0 = a.cur_empty ? 0 : a.rbeg[bucket], re0 = a.cur_empty ? 0 : a.rbeg[bucket + 1];
@@ -1602,7 +1612,7 @@ __global__ void __launch_bounds__(kApplyThreads) GW_APPLY_ATTR k_rgn_apply_nar(I
     int32_t* qv = reinterpret_cast<int32_t*>(lcell + (int64_t)FS * W) + nw * kApplyQ + wave * kApplyQ;
     int qn = 0;
     const unsigned long long cur_pos = a.cur_empty ? 0ull : (*(volatile unsigned long long*)a.batch_occ) & a.apply_mask;
-    const int dom_sh = 64 - a.t.log2nreg;  // region = hash >> dom_sh; its low sr_bits: the region in the super-region
+    // the region of hash h within the super-region: the low sr_bits of its region within the bucket (pt_sub)
     struct List {
         const uint32_t* rows;
         const int64_t* rbase;
@@ -1674,7 +1684,7 @@ __global__ void __launch_bounds__(kApplyThreads) GW_APPLY_ATTR k_rgn_apply_nar(I
     // holding k or free decides; a free slot is claimed by CAS (a lost race re-reads the
     // group).  Returns the slot in the super-region or -1 (the region is full).
     auto probe_insert = [&](uint32_t k, uint64_t h) -> int {
-        const int d = F > 1 ? (int)((h >> dom_sh) & (uint64_t)(F - 1)) : 0;
+        const int d = F > 1 ? (int)(pt_sub(a.t, h) & (F - 1)) : 0;
         uint32_t* kd = lkeys + d * S;
         int g0 = (int)(h & (uint64_t)(S - 1) & ~(uint64_t)(kProbeGroup - 1));
         for (int p = 0; p < S;) {
@@ -1742,7 +1752,14 @@ __global__ void __launch_bounds__(kApplyThreads) GW_APPLY_ATTR k_rgn_apply_nar(I
 #pragma unroll
                 for (int u = 0; u < kNarLoadU; ++u) {
                     const int w = w0 + u * blockDim.x;
-                    if (w < tot) l2[w] = v[u];
+                    if (w >= tot) continue;
+                    if constexpr (M) {  // a clear presence bit: the cell is the identity whatever it holds
+                        // (a lazy fire retire, k_fire2); one byte of mask per slot (ring <= 8), slots 2w, 2w + 1
+                        const uint16_t mb = reinterpret_cast<const uint16_t*>(lmask)[w];
+                        if (!((mb >> p) & 1)) v[u].x = id0;
+                        if (!((mb >> (8 + p)) & 1)) v[u].y = id0;
+                    }
+                    l2[w] = v[u];
                 }
             }
         }
@@ -1824,7 +1841,7 @@ __global__ void __launch_bounds__(kApplyThreads) GW_APPLY_ATTR k_rgn_apply_nar(I
                         kq[q] = N4 ? (uint32_t)(r >> 4) : (uint32_t)r;
                         vq[q] = N4 ? 1 : (int32_t)(uint32_t)(r >> 32) >> 4;
                         const uint64_t h = slot_hash((int64_t)kq[q]);
-                        const int d = F > 1 ? (int)((h >> dom_sh) & (uint64_t)(F - 1)) : 0;
+                        const int d = F > 1 ? (int)(pt_sub(a.t, h) & (F - 1)) : 0;
                         hq[q] = d * S + (int)(h & (uint64_t)(S - 1) & ~(uint64_t)(kProbeGroup - 1));
                     }
 #pragma unroll
@@ -1912,7 +1929,7 @@ __global__ void __launch_bounds__(kApplyThreads) GW_APPLY_ATTR k_rgn_apply_nar(I
                         const uint64_t r = N4 ? (uint64_t)L.rk32[src + k] : L.rk[src + k];
                         const uint32_t kk = N4 ? (uint32_t)(r >> 4) : (uint32_t)r;
                         const uint64_t h = slot_hash((int64_t)kk);
-                        const int dd = F > 1 ? (int)((h >> dom_sh) & (uint64_t)(F - 1)) : 0;
+                        const int dd = F > 1 ? (int)(pt_sub(a.t, h) & (F - 1)) : 0;
                         int j = (int)(h & (uint64_t)(S - 1) & ~(uint64_t)(kProbeGroup - 1));
                         bool present = false;
                         for (int q = 0; q < S; ++q) {
@@ -1997,8 +2014,8 @@ template <int AGG>
 __global__ void __launch_bounds__(256) k_rgn_collect_cmp(IngestArgs a) {
     constexpr bool ACC = AGG != GW_COUNT;
     const int64_t r = blockIdx.x;
-    const int64_t bucket = r >> a.d2_bits, col = r & (((int64_t)1 << a.d2_bits) - 1);
-    const bool single = a.d2_bits == 0;
+    const int64_t bucket = r / a.t.nsub, col = r - bucket * a.t.nsub;
+    const bool single = !a.two_pass;
     const int64_t rb = single ? 0 : a.rbeg[bucket], re = single ? a.ntiles : a.rbeg[bucket + 1];
     const int64_t ccol = single ? r : col;
     const uint32_t* rows = single ? a.p1_row : a.r_row;
@@ -2035,8 +2052,8 @@ template <int AGG>
 __global__ void __launch_bounds__(256) k_rgn_collect_nar(IngestArgs a) {
     constexpr bool N4 = AGG == GW_COUNT;
     const int64_t r = blockIdx.x;
-    const int64_t bucket = r >> a.d2_bits, col = r & (((int64_t)1 << a.d2_bits) - 1);
-    const bool single = a.d2_bits == 0;
+    const int64_t bucket = r / a.t.nsub, col = r - bucket * a.t.nsub;
+    const bool single = !a.two_pass;
     const int64_t rb = single ? 0 : a.rbeg[bucket], re = single ? a.ntiles : a.rbeg[bucket + 1];
     const int64_t ccol = single ? r : col;
     const uint32_t* rows = single ? a.p1_row : a.r_row;
@@ -2073,7 +2090,7 @@ __global__ void __launch_bounds__(256) k_rgn_collect_nar(IngestArgs a) {
 // buffer) on the deferred list; the host has made room for st->spills entries.
 template <int AGG>
 __global__ void __launch_bounds__(256) k_rgn_collect(IngestArgs a) {
-    const bool single = a.d2_bits == 0;
+    const bool single = !a.two_pass;
     const int nb = 1 << a.d1_bits;
     const int64_t n = single ? a.ntiles * kPartTile : a.bk_off[nb];
     const int64_t* rk = single ? a.p1_key : a.e_key;
@@ -2338,6 +2355,7 @@ __global__ void __launch_bounds__(256) k_fire(FireArgs a) {
         if (live && a.rmask) {
             if constexpr (uses_mask<AGG>()) {
                 if (mask & a.rmask) pt_mask_put(a.t, g, mask & ~a.rmask);
+                if (a.lazy_retire && g != a.t.cap) continue;  // as k_fire2
             }
             uint64_t m = a.rmask;
             while (m) {
@@ -2480,6 +2498,9 @@ __global__ void __launch_bounds__(kF2Threads) k_fire2(FireArgs a) {
                 if constexpr (M) {
                     if (b.mask[u] & a.rmask) mask_put((uint8_t*)(rg + S), j, ms, b.mask[u] & ~a.rmask);
                 }
+                // presence-mask aggregates (lazy_retire): the clear bits are the retire; the
+                // sentinel slot, which pass 1 adds into with device atomics, is reset for real
+                if (M && a.lazy_retire && g != a.t.cap) continue;
                 for (uint64_t m = a.rmask; m; m &= m - 1) {
                     const int pos = __ffsll((long long)m) - 1;
                     int64_t* c = rg + S + MW + ((int64_t)pos * S + j) * (AV ? 2 : 1);
@@ -2505,6 +2526,21 @@ __global__ void __launch_bounds__(kF2Threads) k_fire2(FireArgs a) {
         }
     }
     flush();
+}
+
+// Lazy retires (FireArgs::lazy_retire) made good: every cell of ring positions `pm` whose
+// presence bit is clear becomes the identity.  Run before a kernel that adds into cells with
+// device atomics (direct / pre-aggregation ingest, deferred merge); the region apply and every
+// reader go by the presence bits and need no cleaning.
+template <int AGG>
+__global__ void __launch_bounds__(256) k_clean_stale(PaneTable t, uint64_t pm) {
+    if constexpr (uses_mask<AGG>()) {
+        const int64_t id0 = identity0(AGG);
+        for (int64_t g = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; g < t.cap; g += (int64_t)gridDim.x * blockDim.x) {
+            const uint64_t m = pt_mask_get(t, g);
+            for (uint64_t q = pm & ~m; q; q &= q - 1) pt_cell(t, g, __ffsll((long long)q) - 1)[0] = id0;
+        }
+    }
 }
 
 // Move the cells of ring positions `emask` to the deferred list (ring re-base down).
@@ -2765,7 +2801,7 @@ hipError_t launch_publish_status(const IngestArgs& a, hipStream_t s) {
 // Region path, per flush over a.ntiles buffer tiles: plan + P2 (two-pass tables), then
 // one workgroup per region applies its runs.
 hipError_t launch_region_flush(const IngestArgs& a, hipStream_t s) {
-    const bool single = a.d2_bits == 0;
+    const bool single = !a.two_pass;
     const size_t part_lds = part_lds_bytes(a);
     const int64_t S = pt_S(a.t);
     const size_t apply_lds = (size_t)(S + pt_mask_words(a.t)) * 8 + (size_t)2 * S * a.t.words * 8 +
@@ -2891,6 +2927,14 @@ hipError_t launch_fire(const FireArgs& a, hipStream_t s) {
     const int fg = (int)std::min<int64_t>(1024, std::max<int64_t>(1, (a.t.cap + 1 + 255) / 256));
 #define L(A) hipLaunchKernelGGL(k_fire<A>, dim3(fg), dim3(256), 0, s, a)
     GW_AGG_SWITCH(a.t.agg, L);
+#undef L
+    return hipGetLastError();
+}
+
+hipError_t launch_clean_stale(const PaneTable& t, uint64_t pmask, hipStream_t s) {
+    if (!t.has_mask || !pmask) return hipSuccess;
+#define L(A) hipLaunchKernelGGL(k_clean_stale<A>, dim3(grid_for(t.cap)), dim3(256), 0, s, t, pmask)
+    GW_AGG_SWITCH(t.agg, L);
 #undef L
     return hipGetLastError();
 }

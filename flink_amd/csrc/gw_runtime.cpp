@@ -253,6 +253,7 @@ struct gw_handle {
     uint32_t* r_row = nullptr;      // [rounds][kPartBuckets], rounds <= tiles + blocks
     int64_t* r_base = nullptr;      // [rounds]
     int64_t buf_cap = 0;            // tiles
+    uint64_t stale_pos = 0;         // ring positions retired lazily, not yet cleaned (lazy_retire)
     static int64_t max_blocks(int64_t tiles) { return 2 * tiles + kPartBuckets + 1; }
     static int64_t max_rounds(int64_t tiles) { return tiles + max_blocks(tiles); }
 
@@ -511,22 +512,54 @@ struct gw_handle {
     int take_occ() { occ = h_st->occ; return GW_OK; }
 
     // ---------------------------------------------------------------- memory
-    // Region-major table: nreg = cap / S regions of S slots (S chosen in alloc_table).
+    // Pane-table load: the table is sized for the expected keys at kTableLoad and grows past
+    // kGrowLoad.  The geometry allows any load (regions per bucket need not be a
+    // power of two); measured on the headline (profiles/r6/): 0.8 -- 12.6M slots for 10M keys,
+    // ~85% of the keys in their home group of 4 slots against 0.93 at 0.6 -- made the apply
+    // and the fire slower, so the default stays at 0.6 (8192 regions for 10M keys).
+#ifndef GW_TABLE_LOAD
+#define GW_TABLE_LOAD 0.6
+#endif
+    static constexpr double kTableLoad = GW_TABLE_LOAD,
+                            kGrowLoad = GW_TABLE_LOAD + 0.1 < 0.88 ? GW_TABLE_LOAD + 0.1 : 0.88;
+    // Region-major table: nreg = nsub << rb1 regions of S slots (table_geometry).
     static size_t pane_table_bytes(const PaneTable& t) { return (size_t)(t.nreg + 1) * (size_t)t.region_words * 8; }
-    int alloc_table(PaneTable& t, int64_t cap) {
-        t = tv;
-        // 2048 slots (1024 for two-word cells): keys + mask + two pane arrays take ~50 KB
-        // of LDS in k_rgn_apply (1024-slot regions measured slower: 0.28 vs 0.21 ms)
+    // At least `want` slots: regions of S = 2048 slots (1024 for two-word cells: keys + mask +
+    // two pane arrays take ~50 KB of LDS in k_rgn_apply; 1024-slot regions measured slower).  Up
+    // to 128 regions: a power of two, single-pass (one pass-1 bucket per region).  Beyond: 2^rb1
+    // = 128 (256 past 8192 regions) pass-1 buckets of nsub regions, nsub any even number (a
+    // multiple of 4 past 64), so the capacity follows the keys in steps of 1/64 instead of 2x.
+    static void table_geometry(PaneTable& t, int64_t want) {
         int64_t S = t.words == 2 ? 1024 : 2048;
-        if (S > cap) S = cap;
+        want = std::max<int64_t>(want, 16);
+        int64_t nreg_want = (want + S - 1) / S;
+        if (nreg_want <= 1) {  // one region of a power of two (>= 16) slots
+            S = 16;
+            while (S < want) S *= 2;
+            nreg_want = 1;
+        }
         int l2s = 0;
         while (((int64_t)1 << l2s) < S) ++l2s;
-        t.cap = cap;
         t.log2S = l2s;
-        t.nreg = cap >> l2s;
-        int l2r = 0;
-        while (((int64_t)1 << l2r) < t.nreg) ++l2r;
-        t.log2nreg = l2r;
+        if (nreg_want <= 128) {
+            int l2r = 0;
+            while (((int64_t)1 << l2r) < nreg_want) ++l2r;
+            t.rb1 = l2r;
+            t.nsub = 1;
+        } else {
+            t.rb1 = nreg_want <= 128 * 64 ? 7 : 8;
+            int64_t nsub = (nreg_want + (1 << t.rb1) - 1) >> t.rb1;
+            const int64_t q = nsub > 64 ? 4 : 2;  // nar2 super-regions of 2 (4) regions
+            nsub = std::min<int64_t>((nsub + q - 1) / q * q, kRgnMaxRegions >> t.rb1);
+            t.nsub = (int32_t)nsub;
+        }
+        t.nreg = (int64_t)t.nsub << t.rb1;
+        t.cap = t.nreg << l2s;
+    }
+    int alloc_table(PaneTable& t, int64_t want) {
+        t = tv;
+        table_geometry(t, want);
+        const int64_t S = pt_S(t);
         t.mask_shift = t.ring <= 8 ? 0 : t.ring <= 16 ? 1 : t.ring <= 32 ? 2 : 3;
         t.region_words = S + pt_mask_words(t) + S * (int64_t)t.ring * t.words;
         HIPCHECK(hipMalloc((void**)&t.base, pane_table_bytes(t)));
@@ -801,18 +834,21 @@ struct gw_handle {
     // Keep the load factor of the linear-probing table below 0.7.
     int maybe_grow(int64_t incoming) {
         if (nseg || carry_on) {  // waiting segments are bucketed for this table's regions: apply them first
-            if (!(h_st->flags & GW_DF_TABLE_FULL) && (double)h_st->used_slots <= 0.7 * (double)tv.cap) return GW_OK;
+            if (!(h_st->flags & GW_DF_TABLE_FULL) && (double)h_st->used_slots <= kGrowLoad * (double)tv.cap) return GW_OK;
             int rc = flush_buffer();  // refreshes the counters (and may grow by itself)
             if (rc) return rc;
         }
         const int64_t used = (int64_t)h_st->used_slots;
         const bool full = (h_st->flags & GW_DF_TABLE_FULL) != 0;
-        if (!full && (double)used <= 0.7 * (double)tv.cap) return GW_OK;
+        if (!full && (double)used <= kGrowLoad * (double)tv.cap) return GW_OK;
         const int64_t live = live_count() + ov_nkeys;
         // parked records that failed to insert are potential new keys
         const int64_t pending = full ? std::max<int64_t>(incoming, (int64_t)h_st->n_deferred) : 0;
-        int64_t want = std::max<int64_t>(tv.cap, 1024);
-        while ((double)(live + pending) > 0.5 * (double)want || (full && want <= tv.cap)) want *= 2;
+        // room for the live keys at the creation load, and at least 1.25x (2x when regions
+        // filled up) the current table
+        const double floor_x = full ? 2.0 : 1.25;
+        const int64_t want = std::max<int64_t>((int64_t)((double)(live + pending) / kTableLoad) + 1,
+                                               (int64_t)(floor_x * (double)std::max<int64_t>(tv.cap, 1024)));
         return rehash(want);
     }
 
@@ -836,6 +872,7 @@ struct gw_handle {
             const int o = cur ^ 1;
             a.d_key = dk[o]; a.d_pane = dp[o]; a.d_a0 = da0[o]; a.d_a1 = da1[o];
             a.st = d_st;
+            if ((rc = clean_stale())) return rc;
             HIPCHECK(launch_merge_deferred(a, stream));
             cur = o;
             if ((rc = refresh())) return rc;
@@ -972,6 +1009,7 @@ struct gw_handle {
             a.t = tv;
             a.d_key = dk[cur]; a.d_pane = dp[cur]; a.d_a0 = da0[cur]; a.d_a1 = da1[cur];
             a.st = d_st;
+            if ((rc = clean_stale())) return rc;
             HIPCHECK(launch_merge_deferred(a, stream));
             if ((rc = set_field(offsetof(DevStatus, n_refire), 0))) return rc;
             dirty = true;
@@ -987,6 +1025,21 @@ struct gw_handle {
     }
 
     // Clear the ring panes below pane `upto` (their windows are fired and cleaned).
+    // Presence-mask aggregates retire a pane by clearing its presence bits only (the cells
+    // keep stale values behind them: 8 B per slot and position less to write per fire); the
+    // positions are remembered and cleaned before a kernel that adds into cells with device
+    // atomics (clean_stale).  The region apply and every reader go by the bits.
+    void lazy_retire(FireArgs& f) {
+        f.lazy_retire = tv.has_mask ? 1 : 0;
+        if (tv.has_mask) stale_pos |= f.rmask;
+    }
+    int clean_stale() {
+        if (!stale_pos) return GW_OK;
+        HIPCHECK(launch_clean_stale(tv, stale_pos, stream));
+        stale_pos = 0;
+        return GW_OK;
+    }
+
     int retire_below(i128 upto) {
         uint64_t rmask = 0;
         for (i128 p = B; p < upto && p < B + R; ++p) rmask |= 1ull << pos_of(p);
@@ -997,6 +1050,7 @@ struct gw_handle {
             f.nwin = 0;
             f.rmask = rmask;
             f.st = d_st;
+            lazy_retire(f);
             HIPCHECK(launch_fire(f, stream));
             occ &= ~rmask;
             dirty = true;
@@ -1111,6 +1165,7 @@ struct gw_handle {
                 return rc;
             f.o_key = o_key; f.o_start = o_start; f.o_end = o_end; f.o_res = o_res;
             f.st = d_st;
+            lazy_retire(f);
             if (timing) {
                 auto ev = t_fire.get();
                 HIPCHECK(hipEventRecord(ev.first, stream));
@@ -1195,11 +1250,9 @@ struct gw_handle {
 
     // Region arrays of the current table geometry.
     void region_args(IngestArgs& a) {
-        int l2 = 0;
-        while (((int64_t)1 << l2) < tv.nreg) ++l2;
-        // <= 7 bits in P1 keeps ~32 records per bucket run of a 4096-record tile
-        a.d1_bits = l2 <= 14 ? std::min(l2, 7) : (l2 + 1) / 2;
-        a.d2_bits = l2 - a.d1_bits;
+        // 128 pass-1 buckets keep ~32 records per bucket run of a 4096-record tile
+        a.d1_bits = tv.rb1;
+        a.two_pass = tv.nsub > 1;
         a.p1_key = e_col[3]; a.p1_a0 = e_col[4]; a.p1_a1 = e_col[5]; a.p1_pos = e_pos[1];
         a.e_key = eset_key(eset); a.e_a0 = e_col[1]; a.e_a1 = e_col[2]; a.e_pos = e_pos[0];
         a.p1_row = p1_row;
@@ -1231,10 +1284,10 @@ struct gw_handle {
         static const bool nar2_off = [] { const char* e = getenv("GW_NAR2"); return e && atoi(e) == 0; }();
         a.nar2 = 0;
         a.sr_bits = 0;
-        if (buf_fmt == 2 && a.d2_bits > 0 && !nar2_off && tv.ring <= 8) {
-            int sr = std::min(nar_f, a.d2_bits);
-            while (a.d2_bits - sr > 5) ++sr;  // (super-region << 3 | position) < kPartBuckets
-            if (sr <= 2) {
+        if (buf_fmt == 2 && a.two_pass && !nar2_off && tv.ring <= 8) {
+            int sr = nar_f;
+            while ((tv.nsub >> sr) > 32) ++sr;  // (super-region << 3 | position) < kPartBuckets
+            if (sr <= 2 && tv.nsub % (1 << sr) == 0) {
                 a.nar2 = 1;
                 a.sr_bits = sr;
             }
@@ -1418,7 +1471,7 @@ struct gw_handle {
         if (path == 0 && tv.nreg <= kRgnMaxRegions && !(cfg.flags & GW_FLAG_NO_REGION)) {
             // large against the table: the batch itself, or (two-pass tables buffer until the
             // fire) the last fire cycle's records
-            const bool cycle = tv.nreg > (1 << 7) && !(cfg.flags & GW_FLAG_NO_BUFFER) &&  // d2_bits > 0
+            const bool cycle = tv.nsub > 1 && !(cfg.flags & GW_FLAG_NO_BUFFER) &&  // two-pass
                                recs_per_fire * 8 >= tv.cap;
             const bool big = nrec >= region_min_batch && (nrec * 8 >= tv.cap || cycle);
             if (big || (cfg.flags & GW_FLAG_FORCE_REGION)) path = 2;
@@ -1437,7 +1490,7 @@ struct gw_handle {
             region_args(a);
             // Two-pass tables buffer P1 segments across watermarks (P2 + apply once per
             // fire); single-pass tables apply every batch.
-            const bool buffered = a.d2_bits > 0 && !(cfg.flags & GW_FLAG_NO_BUFFER);
+            const bool buffered = a.two_pass && !(cfg.flags & GW_FLAG_NO_BUFFER);
             const int64_t tiles = (nrec + kPartTile - 1) / kPartTile;
             if (nseg && buf_tiles + tiles > buf_cap) {
                 if ((rc = flush_buffer())) return rc;
@@ -1480,6 +1533,8 @@ struct gw_handle {
             buf_tiles += tiles;
             buf_recs += nrec;
             if (!buffered && (rc = flush_buffer())) return rc;
+        } else if ((rc = clean_stale())) {
+            return rc;
         } else if (timing) {
             auto ev = t_ingest.get();
             HIPCHECK(hipEventRecord(ev.first, stream));
@@ -2119,7 +2174,131 @@ struct gw_handle {
     // event-time timers (snapshot_sessions_heap).  Count windows (version 3): per key, the
     // element count and the ring of count-pane accumulators -- the CountTrigger count and
     // the window contents the evicting operator keeps (EvictingWindowOperator.java:92-135).
-    uint32_t slot_blob_version() const { return cfg.assigner == GW_SESSION ? 4u : 3u; }
+    uint32_t slot_blob_version() const { return cfg.assigner == GW_COUNT_SLIDING ? 3u : 4u; }
+
+    // countWindow(size) = GlobalWindows + PurgingTrigger(CountTrigger(size)) (KeyedStream.java:
+    // 676-678) in the heap layout (blob version 4, as oracle/flink_oracle.c count_snapshot):
+    // per key group "window-contents" = be32 n; n x (GlobalWindow = one byte 0, key, [be32
+    // hash,] state) -- the fold of the key's elements since its last FIRE_AND_PURGE, i.e. the
+    // current count pane (a tumbling count window is one pane); "count" = be32 n; n x (byte 0,
+    // key, [be32 hash,] be64 c mod size) -- CountTrigger's ReducingState<Long>
+    // (CountTrigger.java:39-40); be32 0 timers (GlobalWindow ends at Long.MAX_VALUE: no cleanup
+    // timer; CountTrigger registers none).  A key whose element count is a multiple of size
+    // was just purged and holds no state.  The sliding form keeps the version-3 layout.
+    int snapshot_count_heap(int32_t kg_lo, int32_t kg_hi, void* buf, int64_t cap, int64_t* len) {
+        int rc;
+        if ((rc = session_refresh(sess, err))) return fail(rc, "%s", err.c_str());
+        KhmHost kh;
+        if ((rc = khm_host(kh))) return rc;
+        const bool hashed = kh.on();
+        std::vector<int64_t> ent;
+        std::vector<int32_t> kgs;
+        if ((rc = session_collect(sess, kg_lo, kg_hi, ent, kgs, err,
+                                  hashed ? std::function<int32_t(int64_t)>([&](int64_t k) { return kh.hash(k); })
+                                         : std::function<int32_t(int64_t)>())))
+            return fail(rc, "%s", err.c_str());
+        const int64_t ew = session_entry_words(sess), W = tv.words;
+        const int64_t ring = (ew - 2) / W;
+        const int nk = kg_hi - kg_lo + 1;
+        std::vector<std::vector<int64_t>> by_kg(nk);
+        for (size_t i = 0; i < kgs.size(); ++i) {
+            const int64_t c = ent[ew * i + 1];
+            if (c % cfg.size != 0) by_kg[kgs[i] - kg_lo].push_back((int64_t)i);
+        }
+        std::vector<uint8_t> pay;
+        std::vector<int64_t> offs(nk + 1, 0);
+        for (int g = 0; g < nk; ++g) {
+            offs[g] = (int64_t)pay.size();
+            auto& ix = by_kg[g];
+            std::sort(ix.begin(), ix.end(), [&](int64_t x, int64_t y) { return ent[ew * x] < ent[ew * y]; });
+            std::vector<uint8_t> cnt;
+            be32(pay, (int32_t)ix.size());
+            be32(cnt, (int32_t)ix.size());
+            for (int64_t i : ix) {
+                const int64_t* e = &ent[ew * i];
+                const int64_t key = e[0], c = e[1];
+                const int64_t* cell = e + 2 + (((c - 1) / cfg.size) % ring) * W;  // the current count pane
+                pay.push_back(0);
+                be64(pay, key);
+                if (hashed) be32(pay, kh.hash(key));
+                acc_to_be(pay, cell[0], W == 2 ? cell[1] : 0);
+                cnt.push_back(0);
+                be64(cnt, key);
+                if (hashed) be32(cnt, kh.hash(key));
+                be64(cnt, c % cfg.size);
+            }
+            pay.insert(pay.end(), cnt.begin(), cnt.end());
+            be32(pay, 0);
+        }
+        offs[nk] = (int64_t)pay.size();
+        const int64_t need = (int64_t)sizeof(SnapHeader) + (int64_t)(nk + 1) * 8 + (int64_t)pay.size();
+        *len = need;
+        if (!buf) return GW_OK;
+        if (cap < need) return fail(GW_E_OUTPUT_FULL, "snapshot needs %lld bytes", (long long)need);
+        SnapHeader hd{};
+        memcpy(hd.magic, "GWS1", 4);
+        hd.version = 4;
+        hd.agg = cfg.agg; hd.assigner = cfg.assigner;
+        hd.size = cfg.size; hd.slide = cfg.slide; hd.offset = cfg.offset; hd.gap = cfg.gap;
+        hd.flags = hashed ? kSnapKeyHashes : 0;
+        hd.max_parallelism = cfg.max_parallelism; hd.kg_lo = kg_lo; hd.kg_hi = kg_hi;
+        hd.entries = (int64_t)pay.size();
+        char* out = (char*)buf;
+        memcpy(out, &hd, sizeof hd);
+        memcpy(out + sizeof hd, offs.data(), (nk + 1) * 8);
+        if (!pay.empty()) memcpy(out + sizeof hd + (nk + 1) * 8, pay.data(), pay.size());
+        return GW_OK;
+    }
+    // ... and back into version-3 entries (key, element count = the trigger's count, the
+    // contents in count pane 0 of the ring, identities elsewhere)
+    int parse_count_heap(const SnapHeader& hd, const uint8_t* p, const uint8_t* end, std::vector<int64_t>& ent,
+                         std::vector<int64_t>& hkeys, std::vector<int32_t>& hvals) {
+        const int64_t nk = (int64_t)hd.kg_hi - hd.kg_lo + 1;
+        const int hb = (hd.flags & kSnapKeyHashes) ? 4 : 0, ab = acc_bytes();
+        const int64_t ew = session_entry_words(sess), W = tv.words;
+#define NEED(x) do { if ((int64_t)(x) > end - p) return fail(GW_E_INVALID, "truncated snapshot blob"); } while (0)
+        for (int64_t g = 0; g < nk; ++g) {
+            NEED(4);
+            const int32_t n = rd32(p);
+            p += 4;
+            if (n < 0) return fail(GW_E_INVALID, "corrupt snapshot blob");
+            NEED((int64_t)n * (9 + hb + ab));
+            const uint8_t* st = p;
+            p += (int64_t)n * (9 + hb + ab);
+            NEED(4);
+            const int32_t m = rd32(p);
+            p += 4;
+            if (m != n) return fail(GW_E_INVALID, "count-window contents without their CountTrigger count");
+            NEED((int64_t)m * (17 + hb));
+            for (int32_t i = 0; i < n; ++i) {
+                const uint8_t* x = st + (int64_t)i * (9 + hb + ab);
+                const uint8_t* c = p + (int64_t)i * (17 + hb);
+                const int64_t key = rd64(x + 1), cnt = rd64(c + 9 + hb);
+                if (x[0] != 0 || c[0] != 0 || rd64(c + 1) != key || cnt <= 0 || cnt >= cfg.size)
+                    return fail(GW_E_INVALID, "corrupt count-window snapshot entry");
+                if (hb) { hkeys.push_back(key); hvals.push_back(rd32(x + 9)); }
+                const size_t at = ent.size();
+                ent.resize(at + (size_t)ew, 0);
+                ent[at] = key;
+                ent[at + 1] = cnt;
+                for (int64_t q = 2; q < ew; q += W) {  // identities, then the contents in pane 0
+                    ent[at + q] = identity0(cfg.agg);
+                    if (W == 2) ent[at + q + 1] = 0;
+                }
+                int64_t a0, a1;
+                acc_from_be(x + 9 + hb, a0, a1);
+                ent[at + 2] = a0;
+                if (W == 2) ent[at + 3] = a1;
+            }
+            p += (int64_t)m * (17 + hb);
+            NEED(4);
+            if (rd32(p) != 0) return fail(GW_E_INVALID, "count windows hold no timers");
+            p += 4;
+        }
+#undef NEED
+        if (p != end) return fail(GW_E_INVALID, "snapshot blob has trailing bytes");
+        return GW_OK;
+    }
 
     // Session windows in the heap backend's layout (HeapSnapshotStrategy.java:97-154), per key
     // group and big-endian like snapshot_heap:
@@ -2312,6 +2491,7 @@ struct gw_handle {
         if (kg_lo < 0 || kg_hi < kg_lo || kg_hi >= cfg.max_parallelism)
             return fail(GW_E_INVALID, "key-group range [%d, %d] outside [0, %d)", kg_lo, kg_hi, cfg.max_parallelism);
         if (cfg.assigner == GW_SESSION) return snapshot_sessions_heap(kg_lo, kg_hi, buf, cap, len);
+        if (cfg.assigner == GW_COUNT_TUMBLING) return snapshot_count_heap(kg_lo, kg_hi, buf, cap, len);
         if ((rc = session_refresh(sess, err))) return fail(rc, "%s", err.c_str());
         KhmHost kh;
         if ((rc = khm_host(kh))) return rc;
@@ -2380,6 +2560,24 @@ struct gw_handle {
             if (rc == GW_OK) rc = khm_check_host(hkeys, hvals);  // before the table changes
             if (rc || dry) return rc;
             rc = session_restore(sess, ent.data(), (int64_t)(ent.size() / 6), err);
+            if (rc) return fail(rc, "%s", err.c_str());
+            return khm_insert_host(hkeys, hvals);
+        }
+        if (cfg.assigner == GW_COUNT_TUMBLING) {
+            if (hd.version != 4 || hd.agg != cfg.agg || hd.assigner != cfg.assigner || hd.size != cfg.size ||
+                hd.max_parallelism != cfg.max_parallelism || (hd.flags & ~kSnapKeyHashes))
+                return fail(GW_E_INVALID, "snapshot of a different window / aggregate / max parallelism");
+            const int64_t nk = (int64_t)hd.kg_hi - hd.kg_lo + 1;
+            const int64_t pay0 = (int64_t)sizeof hd + (nk + 1) * 8;
+            if (nk <= 0 || hd.entries < 0 || len < pay0 || hd.entries > len - pay0)
+                return fail(GW_E_INVALID, "truncated snapshot blob");
+            const uint8_t* p = (const uint8_t*)buf + pay0;
+            std::vector<int64_t> ent, hkeys;
+            std::vector<int32_t> hvals;
+            int rc = parse_count_heap(hd, p, p + hd.entries, ent, hkeys, hvals);
+            if (rc == GW_OK) rc = khm_check_host(hkeys, hvals);
+            if (rc || dry) return rc;
+            rc = session_restore(sess, ent.data(), (int64_t)(ent.size() / session_entry_words(sess)), err);
             if (rc) return fail(rc, "%s", err.c_str());
             return khm_insert_host(hkeys, hvals);
         }
@@ -2739,7 +2937,7 @@ int gw_create(const gw_config* cfg, gw_handle** out) {
     h->div = make_udiv((uint64_t)h->g);
     h->fired_k = h->k_for_wm(INT64_MIN) + 1;
     h->B = h->fired_k * h->m;
-    rc = h->alloc_table(h->tv, cap);
+    rc = h->alloc_table(h->tv, std::max<int64_t>(1024, (int64_t)((double)hint / gw_handle::kTableLoad) + 1));
     if (rc) return bail(rc, h->err);
     h->table_bytes = gw_handle::pane_table_bytes(h->tv);
     rc = h->ensure_deferred(1 << 16);
@@ -4196,8 +4394,24 @@ static bool blob_keys(const uint8_t* b, int64_t len, F&& f) {
     }
     if (hd.entries > len - pay0) return false;
     const uint8_t* end = p + hd.entries;
-    const int64_t eb = 24 + ((hd.flags & kSnapKeyHashes) ? 4 : 0) + ((hd.flags & kSnapFirstElement) ? 8 : 0) +
-                       (hd.agg == GW_SUM_I32 ? 4 : (hd.agg == GW_AVG_I64 || hd.agg == GW_AVG_F64) ? 16 : 8);
+    const int64_t ab = hd.agg == GW_SUM_I32 ? 4 : (hd.agg == GW_AVG_I64 || hd.agg == GW_AVG_F64) ? 16 : 8;
+    if (hd.assigner == GW_COUNT_TUMBLING) {  // (GlobalWindow byte, key, [hash,] state) and (byte, key, [hash,] count)
+        const int64_t hb = (hd.flags & kSnapKeyHashes) ? 4 : 0;
+        for (int64_t g = 0; g < nk; ++g) {
+            for (int sec = 0; sec < 2; ++sec) {
+                const int64_t eb = 9 + hb + (sec ? 8 : ab);
+                if (end - p < 4) return false;
+                const int32_t n = gw_handle::rd32(p);
+                p += 4;
+                if (n < 0 || (int64_t)n * eb > end - p) return false;
+                for (int32_t i = 0; i < n; ++i, p += eb) f(p + 1, true);
+            }
+            if (end - p < 4 || gw_handle::rd32(p) != 0) return false;
+            p += 4;
+        }
+        return p == end;
+    }
+    const int64_t eb = 24 + ((hd.flags & kSnapKeyHashes) ? 4 : 0) + ((hd.flags & kSnapFirstElement) ? 8 : 0) + ab;
     for (int64_t g = 0; g < nk; ++g) {
         if (end - p < 4) return false;
         const int32_t n = gw_handle::rd32(p);

@@ -303,6 +303,25 @@ class NativeKeyByExchange:
                                               ctypes.byref(ist), s))
         return n_out.value, ok.value, ot.value, ov.value, oh.value, wm_out.value, ist.value
 
+    def begin(self, keys: torch.Tensor, ts: torch.Tensor, vals: Optional[torch.Tensor] = None,
+              key_hashes: Optional[torch.Tensor] = None, stream=None, wm: int = -(1 << 63)):
+        """gw_exchange_begin: partition a batch and queue its count all-to-all (no host wait).
+        The input columns must stay untouched until the batch is finished."""
+        s = stream if stream is not None else torch.cuda.current_stream(keys.device).cuda_stream
+        ptr = lambda t: t.data_ptr() if t is not None else None
+        self._check(N.lib().gw_exchange_begin(self._h, keys.numel(), ptr(keys), ptr(key_hashes), ptr(ts), ptr(vals),
+                                              int(wm), s))
+
+    def finish(self, stream):
+        """gw_exchange_finish: the oldest begun batch -> what exchange() returns."""
+        import ctypes
+        n_out, wm_out = ctypes.c_int64(), ctypes.c_int64()
+        ok, oh, ot, ov, ist = (ctypes.c_void_p() for _ in range(5))
+        self._check(N.lib().gw_exchange_finish(self._h, ctypes.byref(n_out), ctypes.byref(ok), ctypes.byref(oh),
+                                               ctypes.byref(ot), ctypes.byref(ov), ctypes.byref(wm_out),
+                                               ctypes.byref(ist), stream))
+        return n_out.value, ok.value, ot.value, ov.value, oh.value, wm_out.value, ist.value
+
     def enable_packing(self, size: int, slide: int, offset: int = 0, with_values: bool = True):
         """gw_exchange_enable_packing: later batches ship the records that fit as 8-byte words."""
         self._check(N.lib().gw_exchange_enable_packing(self._h, int(size), int(slide), int(offset),

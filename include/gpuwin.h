@@ -533,6 +533,20 @@ int  gw_exchange_create(gw_exchange** out, int32_t nranks, int32_t rank, const v
                         int32_t max_parallelism);
 void gw_exchange_destroy(gw_exchange* ex);
 int  gw_exchange_set_timeout(gw_exchange* ex, int64_t timeout_ms);
+/* gw_exchange_batch in two halves, so no host wait sits between batches: gw_exchange_begin
+ * partitions a batch and queues its count all-to-all (no wait); gw_exchange_finish takes the
+ * oldest begun batch, waits for its counts (the batch's one host wait, bounded as above),
+ * queues the sends / receives and returns what gw_exchange_batch returns.  Up to two batches
+ * may be begun and not finished (GW_E_STATE beyond); issue begin(b + 1) before finish(b) and
+ * the partition of b + 1 runs while the host waits for b's counts.  Both halves of a batch
+ * on the same stream.  Packing takes its base pane from the combined watermark of the last
+ * batch finished before the begin (the same on every rank, which begin and finish in the
+ * same order). */
+int  gw_exchange_begin(gw_exchange* ex, int64_t n, const int64_t* d_key, const int32_t* d_key_hash,
+                       const int64_t* d_ts, const int64_t* d_value, int64_t wm, void* stream);
+int  gw_exchange_finish(gw_exchange* ex, int64_t* n_out, const int64_t** d_key_out, const int32_t** d_key_hash_out,
+                        const int64_t** d_ts_out, const int64_t** d_value_out, int64_t* wm_out, void** ingest_stream,
+                        void* stream);
 int  gw_exchange_batch(gw_exchange* ex, int64_t n, const int64_t* d_key, const int32_t* d_key_hash,
                        const int64_t* d_ts, const int64_t* d_value, int64_t wm, int64_t* n_out,
                        const int64_t** d_key_out, const int32_t** d_key_hash_out, const int64_t** d_ts_out,

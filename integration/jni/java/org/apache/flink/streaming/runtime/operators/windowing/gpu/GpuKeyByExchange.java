@@ -46,6 +46,21 @@ public final class GpuKeyByExchange implements AutoCloseable {
         return r;
     }
 
+    /** {@link #batch} in two halves, so the host never waits between batches: begin batch
+     *  b + 1 (partition + the count all-to-all, no wait), then finish batch b (its one bounded
+     *  wait, the sends; returns what {@link #batch} returns).  At most two batches begun and not
+     *  finished; both halves on one stream; every subtask begins and finishes in the same order. */
+    public void begin(long n, long keyPtr, long hashPtr, long tsPtr, long valuePtr, long watermark, long stream) {
+        nativeBegin(handle, n, keyPtr, hashPtr, tsPtr, valuePtr, watermark, stream);
+    }
+
+    public long[] finish(long stream) {
+        nativeFinish(handle, stream, out);
+        long[] r = new long[7];
+        for (int i = 0; i < 7; i++) r[i] = out.getLong(8 * i);
+        return r;
+    }
+
     public long minWatermark(long wm, long stream) { return nativeMinWatermark(handle, wm, stream); }
 
     /** Bound of every host wait of the exchange (include/gpuwin.h gw_exchange_set_timeout;
@@ -77,4 +92,7 @@ public final class GpuKeyByExchange implements AutoCloseable {
     private static native long nativeMinWatermark(long h, long wm, long stream);
     private static native void nativeEnablePacking(long h, long size, long slide, long offset, boolean withValues);
     private static native void nativeSetTimeout(long h, long timeoutMs);
+    private static native void nativeBegin(long h, long n, long keyPtr, long hashPtr, long tsPtr, long valuePtr,
+                                           long watermark, long stream);
+    private static native void nativeFinish(long h, long stream, ByteBuffer out);
 }

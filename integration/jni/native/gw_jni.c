@@ -372,6 +372,32 @@ JNIEXPORT void JNICALL XCLS(nativeBatch)(JNIEnv* env, jclass c, jlong x, jlong n
     fail_ex(env, (gw_exchange*)(intptr_t)x, rc);
 }
 
+/* The same batch in two halves, one batch ahead (gw_exchange_begin / gw_exchange_finish): begin
+ * partitions and queues the count all-to-all without a host wait; finish fills `out` as
+ * nativeBatch does for the oldest begun batch. */
+JNIEXPORT void JNICALL XCLS(nativeBegin)(JNIEnv* env, jclass c, jlong x, jlong n, jlong keyPtr, jlong hashPtr,
+                                         jlong tsPtr, jlong valuePtr, jlong wm, jlong stream) {
+    fail_ex(env, (gw_exchange*)(intptr_t)x,
+            gw_exchange_begin((gw_exchange*)(intptr_t)x, n, (const int64_t*)(intptr_t)keyPtr,
+                              (const int32_t*)(intptr_t)hashPtr, (const int64_t*)(intptr_t)tsPtr,
+                              (const int64_t*)(intptr_t)valuePtr, wm, (void*)(intptr_t)stream));
+}
+
+JNIEXPORT void JNICALL XCLS(nativeFinish)(JNIEnv* env, jclass c, jlong x, jlong stream, jobject out) {
+    int64_t* o = (*env)->GetDirectBufferAddress(env, out);
+    const int64_t *k = 0, *t = 0, *v = 0;
+    const int32_t* kh = 0;
+    void* ist = 0;
+    int rc = gw_exchange_finish((gw_exchange*)(intptr_t)x, &o[0], &k, &kh, &t, &v, &o[5], &ist,
+                                (void*)(intptr_t)stream);
+    o[1] = (int64_t)(intptr_t)k;
+    o[2] = (int64_t)(intptr_t)kh;
+    o[3] = (int64_t)(intptr_t)t;
+    o[4] = (int64_t)(intptr_t)v;
+    o[6] = (int64_t)(intptr_t)ist;
+    fail_ex(env, (gw_exchange*)(intptr_t)x, rc);
+}
+
 /* Packed records from the next batch on (gw_exchange_enable_packing): a tumbling / sliding
  * operator with size >= slide, no late side output, integer aggregate. */
 JNIEXPORT void JNICALL XCLS(nativeEnablePacking)(JNIEnv* env, jclass c, jlong x, jlong size, jlong slide,

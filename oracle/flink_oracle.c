@@ -432,6 +432,10 @@ typedef struct cw_s {
     int64_t total;  /* elements of this key so far (the row's end ordinal)     */
     int64_t n, cap; /* window contents                                         */
     int64_t* v;
+    /* restored tumbling contents (wo_restore): the reduced state of `rest` elements that
+     * precede v[] -- the reference keeps the ReducingState's value, not the elements */
+    int64_t rest;
+    acc_t* acc0;
 } cw_t;
 
 static void op_err(wo_op* op, const char* fmt, ...) {
@@ -924,10 +928,21 @@ static int count_process_element(wo_op* op, int64_t key, int64_t v) {
         w->n -= drop;
     }
     acc_t a;
-    acc_first(&a, op->c.agg, w->v[0]);
-    for (int64_t i = 1; i < w->n; i++) acc_add(&a, op->c.agg, w->v[i]);
-    int rc = emit(op, key, w->total - w->n, w->total, &a);
-    if (!sliding) w->n = 0; /* FIRE_AND_PURGE */
+    int64_t i0 = 0;
+    if (w->acc0) { /* restored contents first (tumbling only) */
+        a = *w->acc0;
+    } else {
+        acc_first(&a, op->c.agg, w->v[0]);
+        i0 = 1;
+    }
+    for (int64_t i = i0; i < w->n; i++) acc_add(&a, op->c.agg, w->v[i]);
+    int rc = emit(op, key, w->total - w->n - w->rest, w->total, &a);
+    if (!sliding) { /* FIRE_AND_PURGE */
+        w->n = 0;
+        w->rest = 0;
+        free(w->acc0);
+        w->acc0 = NULL;
+    }
     return rc;
 }
 
@@ -1096,7 +1111,7 @@ void wo_destroy(wo_op* op) {
     map_free(&op->sets);
     map_free(&op->cmap);
     map_free(&op->khash);
-    for (int64_t i = 0; i < op->ncws; i++) free(op->cws[i].v);
+    for (int64_t i = 0; i < op->ncws; i++) { free(op->cws[i].v); free(op->cws[i].acc0); }
     free(op->cws);
     for (int64_t i = 0; i < op->nsets; i++) free(op->msets[i].w);
     free(op->msets);
@@ -1255,9 +1270,167 @@ int wo_set_key_hashes(wo_op* op, int64_t n, const int64_t* key, const int32_t* h
     return GW_OK;
 }
 
+/* The 96-byte blob header (include/gpuwin.h gw_snapshot, gw_runtime.cpp SnapHeader). */
+static void snap_header(const wo_op* op, int32_t kg_lo, int32_t kg_hi, int hashed, int64_t payload, uint8_t* h) {
+    memset(h, 0, 96);
+    memcpy(h, "GWS1", 4);
+    const uint32_t ver = 4;
+    const int64_t slide = op->c.assigner == GW_TUMBLING ? op->c.size : op->c.slide;
+    const int32_t i32s[2] = {op->c.agg, op->c.assigner};
+    const int64_t i64s[5] = {op->c.size, slide, op->c.offset, op->c.gap,
+                             (hashed ? 1 : 0) | ((op->c.flags & GW_FLAG_BY_FIELD) ? 2 : 0)};
+    const int32_t mp = op->c.max_parallelism > 0 ? op->c.max_parallelism : 128;
+    const int32_t i32b[4] = {mp, kg_lo, kg_hi, 0};
+    const int64_t tail[3] = {0, 0, payload};
+    memcpy(h + 4, &ver, 4);
+    memcpy(h + 8, i32s, 8);
+    memcpy(h + 16, i64s, 40);
+    memcpy(h + 56, i32b, 16);
+    memcpy(h + 72, tail, 24);
+}
+
+/* countWindow(size) = GlobalWindows + PurgingTrigger(CountTrigger(size)) (KeyedStream.java:
+ * 676-678) in the heap layout, per key group:
+ *   "window-contents": int32 n; n x (GlobalWindow, key, [int32 key hash,] state): the reduced
+ *                      contents since the key's last FIRE_AND_PURGE (GlobalWindow.Serializer
+ *                      writes one byte 0, GlobalWindow.java:96-98);
+ *   "count":           int32 m; m x (GlobalWindow, key, [int32 key hash,] long): CountTrigger's
+ *                      ReducingState<Long> "count" (CountTrigger.java:39-40, cleared at each
+ *                      FIRE :52-55);
+ *   timers:            int32 0 -- GlobalWindows is not an event-time assigner and its window
+ *                      ends at Long.MAX_VALUE, so no cleanup timer (WindowOperator.java:631-643)
+ *                      and CountTrigger registers none.
+ * A key right after a FIRE_AND_PURGE holds no state.  Keys ascending within a key group.  The
+ * sliding form (CountEvictor + CountTrigger(slide)) keeps the element list itself and is not
+ * written here. */
+static int64_t count_snapshot(wo_op* op, int32_t kg_lo, int32_t kg_hi, uint8_t* buf, int64_t cap) {
+    if (op->c.assigner != GW_COUNT_TUMBLING) return GW_E_UNSUPPORTED;
+    if (kg_lo < 0 || kg_hi < kg_lo) return GW_E_INVALID;
+    const int nk = kg_hi - kg_lo + 1;
+    const int hashed = op->khash.n > 0;
+    int64_t ne = 0;
+    snap_ent* se = (snap_ent*)malloc(sizeof(snap_ent) * (size_t)(op->ncws + 1));
+    if (!se) return GW_E_OOM;
+    for (int64_t i = 0; i < op->cmap.cap; i++) {
+        const ment_t* m = &op->cmap.e[i];
+        if (m->st != 1 || op->cws[m->v].trig == 0) continue;
+        const int32_t kg = key_group_of(op, m->k[0]);
+        if (kg < kg_lo || kg > kg_hi) continue;
+        se[ne++] = (snap_ent){kg, m->k[0], 0, 0, 0, m->v};
+    }
+    qsort(se, (size_t)ne, sizeof(snap_ent), cmp_snap_ent);
+    const int64_t pay0 = 96 + (int64_t)(nk + 1) * 8;
+    wbuf b = {buf, pay0, cap};
+    int64_t* offs = (int64_t*)calloc((size_t)nk + 1, sizeof(int64_t));
+    const uint8_t global_window = 0;
+    int64_t a = 0;
+    for (int g = 0; g < nk; g++) {
+        const int32_t kg = kg_lo + g;
+        offs[g] = b.n - pay0;
+        int64_t a1 = a;
+        while (a1 < ne && se[a1].kg == kg) a1++;
+        wb_be32(&b, (int32_t)(a1 - a));
+        for (int64_t q = a; q < a1; q++) {
+            const cw_t* w = &op->cws[se[q].v];
+            acc_t acc;
+            int64_t i0 = 0;
+            if (w->acc0) {
+                acc = *w->acc0;
+            } else {
+                acc_first(&acc, op->c.agg, w->v[0]);
+                i0 = 1;
+            }
+            for (int64_t i = i0; i < w->n; i++) acc_add(&acc, op->c.agg, w->v[i]);
+            wb_put(&b, &global_window, 1);
+            wb_be64(&b, se[q].k0);
+            if (hashed) wb_be32(&b, key_hash_of(op, se[q].k0));
+            wb_acc(&b, op->c.agg, &acc);
+        }
+        wb_be32(&b, (int32_t)(a1 - a));
+        for (int64_t q = a; q < a1; q++) {
+            wb_put(&b, &global_window, 1);
+            wb_be64(&b, se[q].k0);
+            if (hashed) wb_be32(&b, key_hash_of(op, se[q].k0));
+            wb_be64(&b, op->cws[se[q].v].trig);
+        }
+        wb_be32(&b, 0);
+        a = a1;
+    }
+    offs[nk] = b.n - pay0;
+    const int64_t total = b.n;
+    if (buf && cap >= total) {
+        snap_header(op, kg_lo, kg_hi, hashed, offs[nk], buf);
+        memcpy(buf + 96, offs, (size_t)(nk + 1) * 8);
+    }
+    free(offs);
+    free(se);
+    return total;
+}
+
+/* The restore side of count_snapshot: every (key, contents) entry pairs with the key's
+ * CountTrigger count (a count without contents, or contents without a count, is a state
+ * this operator never writes: GW_E_INVALID). */
+static int count_restore(wo_op* op, const uint8_t* p, const uint8_t* end, int nk, int hb) {
+    const int ab = wo_acc_bytes(op->c.agg);
+#define NEED(x) do { if ((int64_t)(x) > end - p) { op_err(op, "truncated snapshot blob"); return GW_E_INVALID; } } while (0)
+    for (int g = 0; g < nk; g++) {
+        NEED(4);
+        const int32_t n = rd_be32(p); p += 4;
+        if (n < 0) { op_err(op, "corrupt snapshot blob"); return GW_E_INVALID; }
+        NEED((int64_t)n * (9 + hb + ab));
+        const uint8_t* st = p;
+        p += (int64_t)n * (9 + hb + ab);
+        NEED(4);
+        const int32_t m = rd_be32(p); p += 4;
+        if (m != n) { op_err(op, "count-window contents without their CountTrigger count"); return GW_E_INVALID; }
+        NEED((int64_t)m * (17 + hb));
+        for (int32_t i = 0; i < n; i++) {
+            const uint8_t* x = st + (int64_t)i * (9 + hb + ab);
+            const uint8_t* c = p + (int64_t)i * (17 + hb);
+            int64_t key = rd_be64(x + 1);
+            const int64_t cnt = rd_be64(c + 9 + hb);
+            if (x[0] != 0 || c[0] != 0 || rd_be64(c + 1) != key || cnt <= 0 || cnt >= op->c.size) {
+                op_err(op, "corrupt count-window snapshot entry");
+                return GW_E_INVALID;
+            }
+            if (hb) {
+                const int32_t kh = rd_be32(x + 9);
+                const int rc = wo_set_key_hashes(op, 1, &key, &kh);
+                if (rc) return rc;
+            }
+            const int64_t k[4] = {key, 0, 0, 0};
+            int created = 0;
+            ment_t* me = map_upsert(&op->cmap, k, op->ncws, &created);
+            if (!me) return GW_E_OOM;
+            if (!created) { op_err(op, "a restored key already holds count-window state"); return GW_E_INVALID; }
+            if (op->ncws == op->cap_cws) {
+                int64_t nc = op->cap_cws ? op->cap_cws * 2 : 1024;
+                cw_t* nw = (cw_t*)realloc(op->cws, sizeof(cw_t) * (size_t)nc);
+                if (!nw) return GW_E_OOM;
+                op->cws = nw;
+                op->cap_cws = nc;
+            }
+            cw_t* w = &op->cws[op->ncws++];
+            memset(w, 0, sizeof(*w));
+            w->acc0 = (acc_t*)malloc(sizeof(acc_t));
+            if (!w->acc0) return GW_E_OOM;
+            rd_acc(x + 9 + hb, op->c.agg, w->acc0);
+            w->trig = w->total = w->rest = cnt;
+        }
+        p += (int64_t)m * (17 + hb);
+        NEED(4);
+        if (rd_be32(p) != 0) { op_err(op, "count windows hold no timers"); return GW_E_INVALID; }
+        p += 4;
+    }
+#undef NEED
+    if (p != end) { op_err(op, "snapshot blob has trailing bytes"); return GW_E_INVALID; }
+    return GW_OK;
+}
+
 /* Returns the blob size; writes it when buf holds >= that many bytes. Negative on error. */
 int64_t wo_snapshot(wo_op* op, int32_t kg_lo, int32_t kg_hi, uint8_t* buf, int64_t cap) {
-    if (op->c.assigner == GW_COUNT_TUMBLING || op->c.assigner == GW_COUNT_SLIDING) return GW_E_UNSUPPORTED;
+    if (op->c.assigner == GW_COUNT_TUMBLING || op->c.assigner == GW_COUNT_SLIDING)
+        return count_snapshot(op, kg_lo, kg_hi, buf, cap);
     if (kg_lo < 0 || kg_hi < kg_lo) return GW_E_INVALID;
     const int nk = kg_hi - kg_lo + 1;
     const int hashed = op->khash.n > 0; /* header flags bit 0: entries carry the key hash */
@@ -1339,23 +1512,7 @@ int64_t wo_snapshot(wo_op* op, int32_t kg_lo, int32_t kg_hi, uint8_t* buf, int64
     offs[nk] = b.n - pay0;
     const int64_t total = b.n;
     if (buf && cap >= total) {
-        uint8_t h[96];
-        memset(h, 0, sizeof h);
-        memcpy(h, "GWS1", 4);
-        const uint32_t ver = 4;
-        const int64_t slide = op->c.assigner == GW_TUMBLING ? op->c.size : op->c.slide;
-        const int32_t i32s[2] = {op->c.agg, op->c.assigner};
-        const int64_t i64s[5] = {op->c.size, slide, op->c.offset, op->c.gap,
-                                 (hashed ? 1 : 0) | ((op->c.flags & GW_FLAG_BY_FIELD) ? 2 : 0)};
-        const int32_t mp = op->c.max_parallelism > 0 ? op->c.max_parallelism : 128;
-        const int32_t i32b[4] = {mp, kg_lo, kg_hi, 0};
-        const int64_t tail[3] = {0, 0, offs[nk]};
-        memcpy(h + 4, &ver, 4);
-        memcpy(h + 8, i32s, 8);
-        memcpy(h + 16, i64s, 40);
-        memcpy(h + 56, i32b, 16);
-        memcpy(h + 72, tail, 24);
-        memcpy(buf, h, 96);
+        snap_header(op, kg_lo, kg_hi, hashed, offs[nk], buf);
         memcpy(buf + offs_at, offs, (size_t)(nk + 1) * 8);
     }
     free(offs); free(se); free(te); free(me);
@@ -1385,6 +1542,8 @@ int wo_restore(wo_op* op, const uint8_t* buf, int64_t len) {
     const int ab = wo_acc_bytes(op->c.agg);
     const int hb = (i64s[4] & 1) ? 4 : 0;
     const int qb = (i64s[4] & 2) ? 8 : 0; /* minBy / maxBy: the element's arrival number */
+    if (op->c.assigner == GW_COUNT_TUMBLING) return count_restore(op, p, end, nk, hb);
+    if (op->c.assigner == GW_COUNT_SLIDING) { op_err(op, "sliding count windows keep no heap-layout snapshot"); return GW_E_UNSUPPORTED; }
     if (!qb != !(op->c.flags & GW_FLAG_BY_FIELD)) { op_err(op, "minBy / maxBy snapshot into another operator"); return GW_E_INVALID; }
 #define NEED(x) do { if ((int64_t)(x) > end - p) { op_err(op, "truncated snapshot blob"); return GW_E_INVALID; } } while (0)
     for (int g = 0; g < nk; g++) {

@@ -74,3 +74,51 @@ def test_headline_bench_cadence_every_watermark(oracle_lib):
     assert not bad, f"(rows, checksum) differ from the oracle at watermarks {bad[:5]}"
     # bench.py --checksum's figure is the sum of these per-watermark checksums
     assert bench.wrap64(sum(c for _, c in per_wm)) == bench.wrap64(sum(c for _, c in ora))
+
+
+@pytest.mark.timeout(600)
+def test_q5_small_batch_cadence_every_watermark(oracle_lib):
+    """SURVEY §8(d)'s other sweep point: E = 10M events per 2-s pane, so 1M-record watermark
+    batches (bench.py --events-per-pane 10000000), the same sliding 10 s / 2 s sum over 10M
+    keys: 25 batches from a cold handle, i.e. two fires of ~10M windows each behind region
+    flushes of 1M-record segments, the deferred list grown on the way (the handle starts with
+    none) -- every watermark's rows (count and checksum) equal the oracle's."""
+    import torch
+
+    import bench
+    from flink_amd import _native as N
+    from flink_amd import windowing as W
+
+    steps = 25
+    args = bench.parse(["--steps", str(steps), "--warmup", "0", "--checksum", "--events-per-pane", "10000000"])
+    E = args.events_per_pane
+    nb = E * args.wm_interval_ms // args.slide_ms
+    assert nb == 1_000_000 and args.keys == 10_000_000
+    keys, ts, vals, wms = bench.make_stream(nb, steps, args.keys, E, args.slide_ms, args.disorder_ms, args.agg,
+                                            torch.device("cuda", 0))
+    op = bench.make_operator(W, N, args, args.keys, nb=nb)
+    try:
+        run = bench.Steps(op, N, keys, ts, vals, wms, nb, collect=True)
+        for b in range(steps):
+            run.step(b)
+        op.flush()
+        op.advance_watermark(W.LONG_MAX)
+        run.consume()
+        st = op.stats()
+    finally:
+        op.close()
+    assert st["region_format"] == 2, st  # the region path with narrow records, as the bench runs it
+    assert st["late_dropped"] == 0
+    per_wm = run.per_wm
+    assert len(per_wm) == steps + 1
+    assert sum(1 for r, _ in per_wm if r > 0.5 * nb) >= 2  # at least two full fires
+
+    keys_np, ts_np, vals_np = keys.cpu().numpy(), ts.cpu().numpy(), vals.cpu().numpy()
+    del keys, ts, vals
+    cfg = oracle_lib.make_config(assigner="sliding", size=args.size_ms, slide=args.slide_ms, agg=args.agg,
+                                 max_parallelism=128)
+    rows, cs, _ = oracle_lib.run_parallel_wm(cfg, THREADS, np.full(steps, nb, np.int64), np.array(wms, np.int64),
+                                             keys_np, ts_np, vals_np)
+    ora = [(int(r), int(c)) for r, c in zip(rows, cs)]
+    bad = [(i, per_wm[i], ora[i]) for i in range(len(ora)) if per_wm[i] != ora[i]]
+    assert not bad, f"(rows, checksum) differ from the oracle at watermarks {bad[:5]}"

@@ -47,10 +47,32 @@ def stream():
 
 def rows_of(op):
     k, s, e, r = op.drain()
-    return list(zip(k.tolist(), s.tolist(), e.tolist(), r.view(np.int64).tolist()))
+    return np.stack([k, s, e, r.view(np.int64)], axis=1)
 
 
-def run_scenario():
+def ora_rows(ora):
+    return np.stack(ora.drain()[:4], axis=1).astype(np.int64)
+
+
+def sort_rows(parts):
+    a = np.concatenate(parts) if parts else np.zeros((0, 4), np.int64)
+    return a[np.lexsort(a.T[::-1])]
+
+
+class _NoOracle:
+    """Stands in for the oracle in the carry-off child: its rows are compared by digest with
+    the parent's, which checked them against the oracle."""
+
+    def __getattr__(self, name):
+        return lambda *a, **k: None
+
+    def drain(self):
+        return [np.zeros(0, np.int64)] * 4
+
+    late_dropped = 0
+
+
+def run_scenario(with_oracle=True):
     """-> (rows of the uninterrupted run, rows of each restored continuation, the oracle's
     rows for both, late counts, formats seen)."""
     from oracle import oracle as O
@@ -58,7 +80,8 @@ def run_scenario():
     mk = lambda: W.GpuWindowOperator(W.SlidingEventTimeWindows.of(2000, 500), "sum_i64", capacity_hint=300_000,
                                      flags=N.FLAG_FORCE_REGION).open()
     op = mk()
-    ora = O.OracleOperator(O.make_config(**KW))
+    new_ora = (lambda: O.OracleOperator(O.make_config(**KW))) if with_oracle else _NoOracle
+    ora = new_ora()
     g, o, fmts, snaps = [], [], [], {}
     for b, (lo, hi, wm) in enumerate(batches):
         op.process_batch(keys[lo:hi], ts[lo:hi], vals[lo:hi])
@@ -66,15 +89,14 @@ def run_scenario():
         fmts.append(op.stats()["region_format"])
         op.advance_watermark(wm)
         ora.process_watermark(wm)
-        g += rows_of(op)
-        o += list(zip(*[x.tolist() for x in ora.drain()]))
+        g.append(rows_of(op))
+        o.append(ora_rows(ora))
         if b in SNAP_AT:
             snaps[b] = (op.snapshot_state(), ora.snapshot())
-        print(f"batch {b}: {len(g)} rows", flush=True)
     op.advance_watermark(W.LONG_MAX)
     ora.process_watermark(W.LONG_MAX)
-    g += rows_of(op)
-    o += list(zip(*[x.tolist() for x in ora.drain()]))
+    g.append(rows_of(op))
+    o.append(ora_rows(ora))
     late = (op.num_late_records_dropped, ora.late_dropped)
     st = op.stats()
     op.close()
@@ -83,7 +105,7 @@ def run_scenario():
     for b, (blob, oblob) in snaps.items():
         op2 = mk()
         op2.initialize_state(blob)
-        ora2 = O.OracleOperator(O.make_config(**KW))
+        ora2 = new_ora()
         ora2.restore(oblob)
         g2, o2 = [], []
         for lo, hi, wm in batches[b + 1:]:
@@ -91,33 +113,35 @@ def run_scenario():
             ora2.process_batch(keys[lo:hi], ts[lo:hi], vals[lo:hi])
             op2.advance_watermark(wm)
             ora2.process_watermark(wm)
-            g2 += rows_of(op2)
-            o2 += list(zip(*[x.tolist() for x in ora2.drain()]))
+            g2.append(rows_of(op2))
+            o2.append(ora_rows(ora2))
         op2.advance_watermark(W.LONG_MAX)
         ora2.process_watermark(W.LONG_MAX)
-        g2 += rows_of(op2)
-        o2 += list(zip(*[x.tolist() for x in ora2.drain()]))
-        cont.append((sorted(g2), sorted(o2), op2.num_late_records_dropped, ora2.late_dropped))
-        print(f"restored at {b}: {len(g2)} rows", flush=True)
+        g2.append(rows_of(op2))
+        o2.append(ora_rows(ora2))
+        cont.append((sort_rows(g2), sort_rows(o2), op2.num_late_records_dropped, ora2.late_dropped))
         op2.close()
         ora2.close()
-    return sorted(g), sorted(o), late, fmts, st, cont
+    return sort_rows(g), sort_rows(o), late, fmts, st, cont
 
 
 def digest(rows):
-    a = np.array(rows, np.int64).reshape(-1, 4) if rows else np.zeros((0, 4), np.int64)
+    a = np.asarray(rows, np.int64).reshape(-1, 4)
     return [int(a.shape[0]), int((a * np.array([3, 5, 7, 11], np.int64)).sum())]
 
 
-def check(res):
+def check(res, with_oracle=True):
     g, o, late, fmts, st, cont = res
-    assert late[0] == late[1]
-    assert g == o and len(g) > 0
+    if with_oracle:
+        assert late[0] == late[1]
+        assert np.array_equal(g, o) and len(g) > 0
     assert 2 in fmts  # narrow records
     assert st["rehashes"] > 0  # the table grew under the stream
     for g2, o2, l2, lo2 in cont:
+        if not with_oracle:
+            continue
         assert l2 == lo2
-        assert g2 == o2 and len(g2) > 0
+        assert np.array_equal(g2, o2) and len(g2) > 0
     return {"rows": digest(g), "cont": [digest(c[0]) for c in cont]}
 
 
@@ -125,7 +149,7 @@ def test_carry_snapshot_growth_and_early_rebase(oracle_lib):
     mine = check(run_scenario())
     env = dict(os.environ, GW_NAR_CARRY="0")
     code = ("import json, sys; sys.path.insert(0, %r); sys.path.insert(0, %r); "
-            "import test_gpu_nar_carry as t; print('RESULT', json.dumps(t.check(t.run_scenario())))"
+            "import test_gpu_nar_carry as t; print('RESULT', json.dumps(t.check(t.run_scenario(False), False)))"
             % (ROOT, os.path.join(ROOT, "tests")))
     p = subprocess.run([sys.executable, "-c", code], env=env, cwd=ROOT, stdout=subprocess.PIPE, stderr=None,
                        text=True, timeout=300)

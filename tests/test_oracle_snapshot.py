@@ -96,3 +96,53 @@ def test_restore_resets_the_watermark(oracle_lib, kw):
         for k, s, e, r in r_rest:
             m = (ok == k) & (ot >= s) & (ot < e)
             assert m.any()
+
+
+@pytest.mark.parametrize("agg", ["count", "sum_i64", "max_f64", "avg_i64"])
+def test_oracle_count_window_heap_layout(oracle_lib, agg):
+    """countWindow(size) (PurgingTrigger(CountTrigger)) in the heap layout: per key group the
+    reduced contents under the GlobalWindow and CountTrigger's "count" (CountTrigger.java:39-40),
+    no timers; a key right after its FIRE_AND_PURGE holds none.  A restored operator fires
+    every window at the same element as the uninterrupted one with the same result: the count
+    carries the trigger, the reduced state the contents (ordinals restart at the count)."""
+    import struct
+    O = oracle_lib
+    size = 6
+    kw = dict(assigner="count_tumbling", size=size, slide=size, agg=agg)
+    keys, _, vals, _ = random_stream(71, 30_000, 400, 1, agg=agg)
+    vb = vals.view(np.int64) if vals.dtype == np.float64 else vals
+    zeros = np.zeros(keys.size, np.int64)
+    cut = 13_001
+    a = O.OracleOperator(O.make_config(**kw))
+    a.process_batch(keys[:cut], zeros[:cut], vb[:cut])
+    a.drain()
+    blob = a.snapshot()
+    # layout: per key group n x (0, key, acc) then n x (0, key, be64 count) then 0 timers
+    nk = 128
+    offs = struct.unpack_from(f"<{nk + 1}q", blob, 96)
+    pay0 = 96 + 8 * (nk + 1)
+    acc = 16 if agg.startswith("avg") else 8
+    counts = {}
+    for g in range(nk):
+        p = pay0 + offs[g]
+        n = struct.unpack_from(">i", blob, p)[0]
+        p += 4 + n * (9 + acc)
+        assert struct.unpack_from(">i", blob, p)[0] == n
+        p += 4
+        for i in range(n):
+            assert blob[p] == 0
+            k, c = struct.unpack_from(">qq", blob, p + 1)
+            counts[k] = c
+            p += 17
+        assert struct.unpack_from(">i", blob, p)[0] == 0 and p + 4 == pay0 + offs[g + 1]
+    seen = np.bincount(np.unique(keys[:cut], return_inverse=True)[1])
+    expect = {int(k): int(c) % size for k, c in zip(np.unique(keys[:cut]), seen) if c % size}
+    assert counts == expect
+    b = O.OracleOperator(O.make_config(**kw))
+    b.restore(blob)
+    a.process_batch(keys[cut:], zeros[cut:], vb[cut:])
+    b.process_batch(keys[cut:], zeros[cut:], vb[cut:])
+    ka, sa, ea, ra = a.drain()
+    kb, sb, eb, rb = b.drain()
+    assert np.array_equal(ka, kb) and np.array_equal(ra, rb) and np.array_equal(ea - sa, eb - sb) and len(ka) > 1000
+    assert np.all(eb - sb == size)

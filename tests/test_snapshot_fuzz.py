@@ -24,6 +24,7 @@ CFGS = [
     dict(assigner="tumbling", size=1000, slide=1000, agg="sum_i64"),
     dict(assigner="sliding", size=900, slide=300, agg="min_f64", lateness=700),
     dict(assigner="session", gap=150, agg="sum_i32", lateness=400),
+    dict(assigner="count_tumbling", size=7, slide=7, agg="avg_f64"),
 ]
 # header byte offsets (HDR = "<4sIii5q4i3q"): max_parallelism 56, kg_lo 60, kg_hi 64, reserved
 # (entry words) 68, entries 88; the (kg_hi - kg_lo + 2) key-group offsets follow at 96
