@@ -152,12 +152,14 @@ class Steps:
     With `collect` the rows of every watermark are drained to the host and (count, checksum)
     recorded."""
 
-    def __init__(self, op, N, keys, ts, vals, wms, nb, ex=None, collect=False, ex_stream=None):
+    def __init__(self, op, N, keys, ts, vals, wms, nb, ex=None, collect=False, ex_stream=None, keep_rows=False):
         import ctypes
         self.op, self.N, self.ex, self.ex_stream = op, N, ex, ex_stream
         self.keys, self.ts, self.vals, self.wms, self.nb = keys, ts, vals, wms, nb
         self.collect = collect
         self.per_wm = []  # (rows, checksum) per watermark when collecting
+        self.keep_rows = keep_rows  # collect: also keep every watermark's rows (tests' row diff)
+        self.rows = []
         self.exch_bytes = 0
         self.begun = -1  # the last batch whose exchange has begun
         # the host side of a step stays lean (the GPU runs a batch in ~70 us): the library's entry
@@ -217,6 +219,8 @@ class Steps:
         if self.collect:
             rows = self.op.drain()
             self.per_wm.append((len(rows[0]), rows_checksum(rows)))
+            if self.keep_rows:
+                self.rows.append(rows)
         else:
             self.N.check(self._clear(self._h), self._h)  # DiscardingSink
 

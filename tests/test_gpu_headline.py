@@ -13,8 +13,9 @@ warmup 0 and 12 steps:
 
 Every watermark's fired rows are drained and compared with the oracle's
 (wo_run_parallel_wm over the same columns and watermarks): row count and the
-order-independent row checksum oracle.rows_hash_sum, bit-exact.  The bench's --checksum
-reports the same checksum summed over the watermarks.
+order-independent row checksum oracle.rows_hash_sum, bit-exact, then row by row
+(wo_run_parallel_rows: every (key, start, end, result) of every watermark, sorted on both
+sides).  The bench's --checksum reports the same checksum summed over the watermarks.
 
 Reference: WindowOperator.processElement / onEventTime (RS/runtime/operators/windowing/
 WindowOperator.java:293-494); parity rule SURVEY.md §8c.
@@ -47,7 +48,7 @@ def test_headline_bench_cadence_every_watermark(oracle_lib):
     op = bench.make_operator(W, N, args, args.keys, nb=nb)
     try:
         op.enable_kernel_timing(True)
-        run = bench.Steps(op, N, keys, ts, vals, wms, nb, collect=True)
+        run = bench.Steps(op, N, keys, ts, vals, wms, nb, collect=True, keep_rows=True)
         for b in range(steps):
             run.step(b)
         op.flush()
@@ -74,6 +75,18 @@ def test_headline_bench_cadence_every_watermark(oracle_lib):
     assert not bad, f"(rows, checksum) differ from the oracle at watermarks {bad[:5]}"
     # bench.py --checksum's figure is the sum of these per-watermark checksums
     assert bench.wrap64(sum(c for _, c in per_wm)) == bench.wrap64(sum(c for _, c in ora))
+    # and row by row: the oracle's rows of every watermark (run_parallel_rows) against the GPU's
+    ok, os_, oe, orr, ow, _ = oracle_lib.run_parallel_rows(cfg, THREADS, np.full(steps, nb, np.int64),
+                                                           np.array(wms, np.int64), keys_np, ts_np, vals_np,
+                                                           int(sum(r for r, _ in ora)) + 16)
+    del keys_np, ts_np, vals_np
+    for i, (gk, gs, ge, gr) in enumerate(run.rows):
+        sel = ow == i
+        o = np.stack([ok[sel], os_[sel], oe[sel], orr[sel]], axis=1)
+        g = np.stack([gk, gs, ge, gr.view(np.int64)], axis=1)
+        o = o[np.lexsort(o.T[::-1])]
+        g = g[np.lexsort(g.T[::-1])]
+        assert np.array_equal(g, o), f"watermark {i}: rows differ from the oracle's"
 
 
 @pytest.mark.timeout(600)
