@@ -816,11 +816,8 @@ __device__ __forceinline__ void p1_tile(const IngestArgs& a, int64_t g, int64_t 
     }
 }
 
-// THR threads per 4096-record tile: kPartThreads (512) for large batches; 1024 for small ones,
-// whose few tiles leave the CUs short of waves (1M records: 244 workgroups on 256 CUs).
-template <int AGG, int FMT, bool GAP, int THR>
-__global__ void __launch_bounds__(THR) GW_P1_ATTR k_rgn_p1(IngestArgs a) {
-    constexpr int IT = kPartTile / THR;
+template <int AGG, int FMT, bool GAP>
+__global__ void __launch_bounds__(kPartThreads) GW_P1_ATTR k_rgn_p1(IngestArgs a) {
     constexpr bool C = FMT == kFmtCmp && cmp_agg<AGG>();
     constexpr bool NR = FMT == kFmtNar && cmp_agg<AGG>();
     constexpr bool AV = !C && !NR && (AGG == GW_AVG_I64 || AGG == GW_AVG_F64);
@@ -835,10 +832,10 @@ __global__ void __launch_bounds__(THR) GW_P1_ATTR k_rgn_p1(IngestArgs a) {
     if (threadIdx.x == 0) s_occ = 0;
     __syncthreads();
     unsigned long long late = 0, flags = 0, occ = 0;
-    int64_t key[IT], ts[IT], val[IT];
+    int64_t key[kPartItems], ts[kPartItems], val[kPartItems];
 #pragma unroll
-    for (int it = 0; it < IT; ++it) {  // all loads in flight first
-        const int64_t i = lo + it * THR + threadIdx.x;
+    for (int it = 0; it < kPartItems; ++it) {  // all loads in flight first
+        const int64_t i = lo + it * kPartThreads + threadIdx.x;
         key[it] = 0; ts[it] = 0; val[it] = 0;
         if (i < hi) {
             if (a.pk_w && i >= a.pk_from) {  // a packed exchange word: 8 B instead of 24
@@ -854,7 +851,7 @@ __global__ void __launch_bounds__(THR) GW_P1_ATTR k_rgn_p1(IngestArgs a) {
             }
         }
     }
-    p1_tile<AGG, FMT, GAP, THR, IT>(a, g, lo, hi, key, ts, val, s, lh, ls, &s_occ, late, flags, occ);
+    p1_tile<AGG, FMT, GAP, kPartThreads, kPartItems>(a, g, lo, hi, key, ts, val, s, lh, ls, &s_occ, late, flags, occ);
     block_commit(a.st, late, 0, flags, occ);
 }
 
@@ -2710,20 +2707,15 @@ hipError_t launch_table_init(const PaneTable& t, hipStream_t s) {
     return hipGetLastError();
 }
 
-static int num_cus() {
-    static int cus = 0;
-    if (!cus) {
-        int dev = 0;
-        (void)hipGetDevice(&dev);
-        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        cus = std::max(cus, 1);
-    }
-    return cus;
-}
-
 hipError_t launch_ingest(const IngestArgs& a, int path, int unroll, hipStream_t s) {
     if (path == 1) {
-        const int cus = num_cus();
+        static int cus = 0;
+        if (!cus) {
+            int dev = 0;
+            (void)hipGetDevice(&dev);
+            (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+            cus = std::max(cus, 1);
+        }
         static const int bpc = getenv("GW_PREAGG_BPC") ? std::max(1, atoi(getenv("GW_PREAGG_BPC"))) : 2;
         const int g = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)bpc * cus, (a.n + 2047) / 2048));
 #define L(A) hipLaunchKernelGGL(k_ingest_preagg<A>, dim3(g), dim3(256), 0, s, a)
@@ -2782,17 +2774,9 @@ hipError_t launch_region_p1(const IngestArgs& a, hipStream_t s) {
     const size_t part_lds = part_lds_bytes(a);
     // beyond the 64 KB default: opt in (gfx950 has 160 KB of LDS per CU)
     // the gap test (size < slide) only in a variant of its own: it costs the hot pass ~3%
-    // small batches: 1024 threads per tile (more waves per CU while the grid is under-filled)
-    const bool wide_wg = tiles < 2 * (int64_t)num_cus();
 #define P1L(A, F, G)                                                                                            \
-    if (wide_wg) {                                                                                              \
-        lds_opt_in((const void*)k_rgn_p1<A, F, G, 1024>, part_lds);                                            \
-        hipLaunchKernelGGL((k_rgn_p1<A, F, G, 1024>), dim3((unsigned)tiles), dim3(1024), part_lds, s, a);      \
-    } else {                                                                                                    \
-        lds_opt_in((const void*)k_rgn_p1<A, F, G, kPartThreads>, part_lds);                                    \
-        hipLaunchKernelGGL((k_rgn_p1<A, F, G, kPartThreads>), dim3((unsigned)tiles), dim3(kPartThreads), part_lds, \
-                           s, a);                                                                               \
-    }
+    lds_opt_in((const void*)k_rgn_p1<A, F, G>, part_lds);                                                      \
+    hipLaunchKernelGGL((k_rgn_p1<A, F, G>), dim3((unsigned)tiles), dim3(kPartThreads), part_lds, s, a)
 #define L(A)                                  \
     if (a.gap_size) {                         \
         P1L(A, kFmtWide, true);               \

@@ -12,10 +12,9 @@ warmup 0 and 12 steps:
 * batch 11, the closing gw_flush the bench runs before its clock stops, then MAX_WATERMARK.
 
 Every watermark's fired rows are drained and compared with the oracle's
-(wo_run_parallel_wm over the same columns and watermarks): row count and the
-order-independent row checksum oracle.rows_hash_sum, bit-exact, then row by row
-(wo_run_parallel_rows: every (key, start, end, result) of every watermark, sorted on both
-sides).  The bench's --checksum reports the same checksum summed over the watermarks.
+(wo_run_parallel_rows over the same columns and watermarks): row count and the
+order-independent row checksum of oracle.rows_hash_sum, bit-exact, then row by row (every
+(key, start, end, result) of every watermark, sorted on both sides).  The bench's --checksum reports the same checksum summed over the watermarks.
 
 Reference: WindowOperator.processElement / onEventTime (RS/runtime/operators/windowing/
 WindowOperator.java:293-494); parity rule SURVEY.md §8c.
@@ -68,18 +67,21 @@ def test_headline_bench_cadence_every_watermark(oracle_lib):
     del keys, ts, vals
     cfg = oracle_lib.make_config(assigner="sliding", size=args.size_ms, slide=args.slide_ms, agg=args.agg,
                                  max_parallelism=128)
-    rows, cs, _ = oracle_lib.run_parallel_wm(cfg, THREADS, np.full(steps, nb, np.int64), np.array(wms, np.int64),
-                                             keys_np, ts_np, vals_np)
-    ora = [(int(r), int(c)) for r, c in zip(rows, cs)]
+    # the oracle's rows of every watermark (run_parallel_rows; its per-watermark count and
+    # order-independent checksum as rows_hash_sum computes them)
+    ok, os_, oe, orr, ow, _ = oracle_lib.run_parallel_rows(cfg, THREADS, np.full(steps, nb, np.int64),
+                                                           np.array(wms, np.int64), keys_np, ts_np, vals_np,
+                                                           int(sum(r for r, _ in per_wm)) + (1 << 20))
+    del keys_np, ts_np, vals_np
+    ora = []
+    for i in range(steps + 1):
+        sel = ow == i
+        ora.append((int(sel.sum()), bench.rows_checksum((ok[sel], os_[sel], oe[sel], orr[sel]))))
     bad = [(i, per_wm[i], ora[i]) for i in range(len(ora)) if per_wm[i] != ora[i]]
     assert not bad, f"(rows, checksum) differ from the oracle at watermarks {bad[:5]}"
     # bench.py --checksum's figure is the sum of these per-watermark checksums
     assert bench.wrap64(sum(c for _, c in per_wm)) == bench.wrap64(sum(c for _, c in ora))
-    # and row by row: the oracle's rows of every watermark (run_parallel_rows) against the GPU's
-    ok, os_, oe, orr, ow, _ = oracle_lib.run_parallel_rows(cfg, THREADS, np.full(steps, nb, np.int64),
-                                                           np.array(wms, np.int64), keys_np, ts_np, vals_np,
-                                                           int(sum(r for r, _ in ora)) + 16)
-    del keys_np, ts_np, vals_np
+    # and row by row
     for i, (gk, gs, ge, gr) in enumerate(run.rows):
         sel = ow == i
         o = np.stack([ok[sel], os_[sel], oe[sel], orr[sel]], axis=1)
