@@ -71,6 +71,9 @@ def parse(argv=None):
                     help="auto: the exchange ships records that fit as 8-byte words (gw_exchange_enable_packing; "
                          "integer aggregates) and pass 1 decodes them (gw_ingest_packed_device); unpack: the "
                          "receiver unpacks them to columns first; off: every record as 24 B")
+    ap.add_argument("--exchange-stream", choices=["own", "operator"], default="own",
+                    help="own: the exchange (partition, all-to-all, sends) on a stream of its own, overlapping "
+                         "the operator's kernels; operator: on the operator's stream, serialised with them")
     ap.add_argument("--force-exchange", action="store_true",
                     help="run the RCCL exchange path at N = 1 too (a one-rank communicator: every record comes "
                          "back to this rank) -- a check of the N > 1 code path on one GPU")
@@ -273,9 +276,9 @@ def main(argv=None):
         if args.pack != "off" and not agg.endswith("f64"):
             ex.enable_packing(size, slide, 0, with_values=agg != "count")
             ex.keep_words(args.pack == "auto")
-    xs = torch.cuda.Stream(device=dev) if ex is not None else None
+    xs = torch.cuda.Stream(device=dev) if ex is not None and args.exchange_stream == "own" else None
     run = Steps(op, N, keys, ts, vals, wms, nb, ex=ex, collect=args.checksum,
-                ex_stream=xs.cuda_stream if xs is not None else None)
+                ex_stream=xs.cuda_stream if xs is not None else (op.stream() if ex is not None else None))
 
     # pass 1 timed on every 4th batch (all batches are alike): two event records per timed launch
     # cost host time between batches; the fire and flush timers run on every launch

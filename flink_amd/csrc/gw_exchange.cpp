@@ -58,10 +58,16 @@ struct gw_exchange {
         hipStream_t stream = nullptr;
     } ps[2];
     int64_t begun = 0, finished = 0;  // batches begun / finished (set of batch i: i & 1)
-    int64_t* recv[2] = {nullptr, nullptr};  // receive sets used in turn: key | ts | value columns
-    int32_t* recv_hash[2] = {nullptr, nullptr};
-    uint64_t* recv_packed[2] = {nullptr, nullptr};
-    int64_t recv_cap[2] = {0, 0};
+    // Receive sets used in turn (key | ts | value columns, key hashes, packed words).  Three, so
+    // batch b's receives wait only for the ingest of batch b - 3 to have read its set: with two,
+    // the exchange stream waited on the operator's pass 1 of batch b - 2, which itself runs
+    // beside the exchange's partition of a later batch (measured: ~50 us per batch of the
+    // exchange stream idling on that cross-stream event, profiles/r6/exchange/).
+    static constexpr int kSets = 3;
+    int64_t* recv[kSets] = {};
+    int32_t* recv_hash[kSets] = {};
+    uint64_t* recv_packed[kSets] = {};
+    int64_t recv_cap[kSets] = {};
     int turn = 0;
     // packing (gw_exchange_enable_packing): window geometry and the last combined watermark
     bool pack_on = false, pack_values = false;
@@ -80,9 +86,9 @@ struct gw_exchange {
     std::vector<int64_t> plan[4];  // gw_exchange_plan: send offsets, send counts, receive offsets, receive counts
     std::vector<int64_t> pplan[4];  // gw_exchange_plan_packed: send packed, receive other / packed offsets, packed
     // per receive set: the hand-off stream the ingest orders on, and its "reads done" event
-    hipStream_t handoff[2] = {nullptr, nullptr};
-    hipEvent_t ev_recv[2] = {nullptr, nullptr}, ev_free[2] = {nullptr, nullptr};
-    bool set_used[2] = {false, false};
+    hipStream_t handoff[kSets] = {};
+    hipEvent_t ev_recv[kSets] = {}, ev_free[kSets] = {};
+    bool set_used[kSets] = {};
     // fail fast (gw_wait.h): every host wait is bounded; on expiry or an asynchronous RCCL error
     // the communicator is aborted and every later call fails with GW_E_STATE
     int64_t timeout_ms = 60000;
@@ -209,7 +215,7 @@ int gw_exchange_create(gw_exchange** out, int32_t nranks, int32_t rank, const vo
     }
     if (hipMalloc((void**)&ex->d_wm, 8) != hipSuccess) return bail(GW_E_OOM);
     if (hipHostMalloc((void**)&ex->h_wm, 8, hipHostMallocDefault) != hipSuccess) return bail(GW_E_OOM);
-    for (int q = 0; q < 2; ++q) {
+    for (int q = 0; q < gw_exchange::kSets; ++q) {
         if (hipStreamCreateWithFlags(&ex->handoff[q], hipStreamNonBlocking) != hipSuccess ||
             hipEventCreateWithFlags(&ex->ev_recv[q], hipEventDisableTiming) != hipSuccess ||
             hipEventCreateWithFlags(&ex->ev_free[q], hipEventDisableTiming) != hipSuccess)
@@ -229,7 +235,7 @@ void gw_exchange_destroy(gw_exchange* ex) {
     if (!ex->aborted && ex->last_stream && ex_wait(ex, ex->last_stream, "gw_exchange_destroy") != GW_OK) {
         // aborted: the kernels that waited on the peer have returned
     }
-    for (int q = 0; q < 2; ++q)
+    for (int q = 0; q < gw_exchange::kSets; ++q)
         if (!ex->aborted && ex->handoff[q]) (void)ex_wait(ex, ex->handoff[q], "gw_exchange_destroy");
     if (!ex->aborted) (void)hipDeviceSynchronize();
     if (ex->comm) ncclCommDestroy(ex->comm);
@@ -242,10 +248,10 @@ void gw_exchange_destroy(gw_exchange* ex) {
         hipHostFree(q.h_msg);
         if (q.ev_msg) hipEventDestroy(q.ev_msg);
     }
-    for (int q = 0; q < 2; ++q) { hipFree(ex->recv[q]); hipFree(ex->recv_hash[q]); hipFree(ex->recv_packed[q]); }
+    for (int q = 0; q < gw_exchange::kSets; ++q) { hipFree(ex->recv[q]); hipFree(ex->recv_hash[q]); hipFree(ex->recv_packed[q]); }
     hipFree(ex->d_wm);
     hipHostFree(ex->h_wm);
-    for (int q = 0; q < 2; ++q) {
+    for (int q = 0; q < gw_exchange::kSets; ++q) {
         if (ex->handoff[q]) hipStreamDestroy(ex->handoff[q]);
         if (ex->ev_recv[q]) hipEventDestroy(ex->ev_recv[q]);
         if (ex->ev_free[q]) hipEventDestroy(ex->ev_free[q]);
@@ -514,9 +520,9 @@ int gw_exchange_finish(gw_exchange* ex, int64_t* n_out, const int64_t** d_key_ou
     ex->last_recv = rc;
     ex->last_packed = tp;
     ex->last_wm = wmin;  // the base pane of the batches begun from now on
-    // 3. this turn's receive set: free once the ingest two batches ago has read it
+    // 3. this turn's receive set: free once the ingest three batches ago has read it
     const int u = ex->turn;
-    ex->turn ^= 1;
+    ex->turn = (ex->turn + 1) % gw_exchange::kSets;
     if (ex->set_used[u]) {  // everything queued on its hand-off stream so far: the ingest's reads
         EX_HIP(hipEventRecord(ex->ev_free[u], ex->handoff[u]));
         EX_HIP(hipStreamWaitEvent(s, ex->ev_free[u], 0));

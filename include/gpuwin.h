@@ -510,12 +510,12 @@ int  gw_ingest_packed_device(gw_handle* h, int64_t n_other, const int64_t* d_key
  * that every rank sends the same columns (GW_E_INVALID otherwise, on every rank), then
  * enqueues one grouped ncclSend/ncclRecv per column and peer on `stream`.  Out: the *n_out
  * records this rank owns in receive columns owned by the exchange (*d_*_out; NULL for an
- * absent column), valid until the next-but-one call (two receive sets used in turn);
+ * absent column), valid until the next-but-two call (three receive sets used in turn);
  * *wm_out = the minimum of the ranks' watermarks (StatusWatermarkValve); *ingest_stream = a
  * hand-off stream of this receive set, ordered after the receives: pass it as the producer
  * stream of gw_ingest_device, whose "producer waits for my reads" ordering then lands on
  * the hand-off stream, so the exchange of the next batch never waits for this batch's
- * ingest, only the reuse of this receive set two batches later does.  All ranks call it
+ * ingest, only the reuse of this receive set three batches later does.  All ranks call it
  * for every batch (n may be 0).  gw_exchange_counts: the last batch's per-peer send and
  * receive record counts (nranks each; either may be NULL).
  *
