@@ -46,6 +46,8 @@ struct DevStatus {
     unsigned long long n_refire;    // lateness > 0: re-fire list cursor (late records of fired windows)
     unsigned long long n_late_out;  // late side output cursor (GW_FLAG_LATE_SIDE_OUTPUT)
     unsigned long long wide_vals;   // compact region records: values beyond 32 bits sent to the deferred list
+    unsigned long long fire_skip;   // k_fire_guard: 1 = the fire enqueued behind it does nothing
+    unsigned long long fire_rows0;  // k_fire_guard: the output cursor before that fire
     unsigned long long pad[4];      // pad[kPubSeqWord]: stamp of a published host copy (never set on the device)
     ShardCtr sh[kShards];
 };

@@ -268,6 +268,7 @@ struct FireArgs {
     uint64_t rmask;     // ring positions retired after this pass
     int32_t lazy_retire;  // presence-mask aggregates: retiring clears the mask bits only; the
                           // cells keep stale values behind clear bits (gw_runtime.cpp stale_pos)
+    int32_t guarded;      // launched behind k_fire_guard: do nothing when st->fire_skip is set
     uint64_t wmask[kMaxRing];
     int64_t* o_key;
     int64_t* o_start;
@@ -351,6 +352,18 @@ hipError_t launch_refire_keys(int mode, const int64_t* src, int64_t base, uint64
                               hipStream_t s);
 hipError_t launch_deferred_min(const int64_t* pane, int64_t n, DevStatus* st, hipStream_t s);
 hipError_t launch_fire(const FireArgs& a, hipStream_t s);
+// The checks that let a fire be enqueued right behind a flush, without the host reading the
+// status in between (gw_runtime.cpp fast_fire): st->fire_skip = 1 -- the guarded fire does
+// nothing and the host takes the exact path -- when the flush left spilled or wide records or
+// a full table, when the deferred list does not hold expect_ndef entries, when a record error
+// was flagged, or when the fire's rows could exceed the row buffer (the host's own
+// ensure_output test, on the device counters); st->fire_rows0 = the output cursor.
+struct FireGuard {
+    unsigned long long expect_ndef;
+    int64_t o_cap;
+    int64_t nwin;
+};
+hipError_t launch_fire_guard(DevStatus* st, const FireGuard& g, hipStream_t s);
 // Cells of ring positions `pmask` whose presence bit is clear -> the identity (the retires a
 // lazy fire left behind, before a kernel that adds into cells with device atomics)
 hipError_t launch_clean_stale(const PaneTable& t, uint64_t pmask, hipStream_t s);

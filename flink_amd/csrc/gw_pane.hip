@@ -2292,6 +2292,7 @@ __global__ void __launch_bounds__(256) k_deferred_min(const int64_t* pane, int64
 // with the identity unconditionally (full-line coalesced stores).
 template <int AGG>
 __global__ void __launch_bounds__(256) k_fire(FireArgs a) {
+    if (a.guarded && *(volatile unsigned long long*)&a.st->fire_skip) return;  // uniform: set before this launch
     __shared__ RowStage rs;
     const int64_t nslots = a.t.cap + 1;
     const int64_t id0 = identity0(AGG);
@@ -2383,6 +2384,7 @@ constexpr int kF2Threads = 256;
 constexpr int kF2Stage = 2048;
 template <int AGG, int NP, int U>
 __global__ void __launch_bounds__(kF2Threads) k_fire2(FireArgs a) {
+    if (a.guarded && *(volatile unsigned long long*)&a.st->fire_skip) return;  // uniform: set before this launch
     constexpr bool M = uses_mask<AGG>();
     constexpr bool AV = AGG == GW_AVG_I64 || AGG == GW_AVG_F64;
     __shared__ long long s_k[kF2Stage], s_r[kF2Stage];
@@ -2540,6 +2542,28 @@ __global__ void __launch_bounds__(256) k_clean_stale(PaneTable t, uint64_t pm) {
             const uint64_t m = pt_mask_get(t, g);
             for (uint64_t q = pm & ~m; q; q &= q - 1) pt_cell(t, g, __ffsll((long long)q) - 1)[0] = id0;
         }
+    }
+}
+
+// One wave: the guard of a fire enqueued right behind a flush (gw_kernels.h FireGuard), over
+// the status as the launches before it left it.
+__global__ void __launch_bounds__(64) k_fire_guard(DevStatus* st, FireGuard g) {
+    const int lane = threadIdx.x;
+    unsigned long long flags = 0, used = 0;
+    for (int i = lane; i < kShards; i += 64) {
+        flags |= st->sh[i].flags;
+        used += st->sh[i].ins;
+    }
+    flags = wave_ior(flags);
+    used = wave_sum(used);
+    if (lane == 0) {
+        const unsigned long long rows = st->rows;
+        const bool skip = st->spills != 0 || st->wide_vals != 0 ||
+                          (flags & (GW_DF_TABLE_FULL | GW_DF_NO_TS | GW_DF_RANGE)) != 0 ||
+                          st->n_deferred != g.expect_ndef ||
+                          (int64_t)rows + g.nwin * ((int64_t)used + 1) > g.o_cap;
+        st->fire_skip = skip ? 1ull : 0ull;
+        st->fire_rows0 = rows;
     }
 }
 
@@ -2928,6 +2952,11 @@ hipError_t launch_fire(const FireArgs& a, hipStream_t s) {
 #define L(A) hipLaunchKernelGGL(k_fire<A>, dim3(fg), dim3(256), 0, s, a)
     GW_AGG_SWITCH(a.t.agg, L);
 #undef L
+    return hipGetLastError();
+}
+
+hipError_t launch_fire_guard(DevStatus* st, const FireGuard& g, hipStream_t s) {
+    hipLaunchKernelGGL(k_fire_guard, dim3(1), dim3(64), 0, s, st, g);
     return hipGetLastError();
 }
 

@@ -159,6 +159,12 @@ struct KernelTimer {
         }
         pending.clear();
     }
+    void drop_last() {  // the last resolved launch did no work (a skipped guarded fire)
+        if (launches > 0) {
+            launches--;
+            total_ms -= last_ms;
+        }
+    }
     void destroy() {
         for (auto& p : pending) pool.push_back(p);
         for (auto& p : pool) { hipEventDestroy(p.first); hipEventDestroy(p.second); }
@@ -1112,6 +1118,54 @@ struct gw_handle {
     }
     static int popcount(uint64_t x) { return __builtin_popcountll(x); }
 
+    // The fire of windows [k_first, k_last], retiring the ring positions of panes [B, keep).
+    int fire_args(i128 k_first, i128 k_last, i128 keep, FireArgs& f, i128& keep_out) {
+        const int nwin = (int)(k_last - k_first + 1);
+        f.t = tv;
+        f.ov = ov_view();
+        f.k0 = (int64_t)k_first;
+        f.nwin = nwin;
+        const i128 start0 = (i128)cfg.offset + k_first * (i128)slide();
+        const i128 endl = (i128)cfg.offset + k_last * (i128)slide() + size();
+        if (!fits64(start0) || !fits64(endl)) return fail(GW_E_RANGE, "window bounds overflow int64");
+        f.start0 = (int64_t)start0;
+        f.slide = slide();
+        f.size = size();
+        for (int w = 0; w < nwin; ++w) {
+            uint64_t wm_ = 0;
+            const i128 p0 = (k_first + w) * m;
+            for (int j = 0; j < n; ++j) wm_ |= 1ull << pos_of(p0 + j);
+            f.wmask[w] = wm_;
+        }
+        uint64_t rmask = 0;
+        for (i128 p = B; p < keep && p < B + R; ++p) rmask |= 1ull << pos_of(p);
+        f.rmask = rmask;
+        f.st = d_st;
+        keep_out = keep;
+        return GW_OK;
+    }
+    int fire_launch(const FireArgs& f) {
+        if (timing) {
+            auto ev = t_fire.get();
+            HIPCHECK(hipEventRecord(ev.first, stream));
+            HIPCHECK(launch_fire(f, stream));
+            HIPCHECK(hipEventRecord(ev.second, stream));
+            t_fire.pending.push_back(ev);
+        } else {
+            HIPCHECK(launch_fire(f, stream));
+        }
+        return GW_OK;
+    }
+    // Host bookkeeping of a fire that ran.
+    void fired(const FireArgs& f, i128 k_last, i128 keep) {
+        stats.fires++;
+        if (recs_since_fire) recs_per_fire = recs_since_fire, recs_since_fire = 0;
+        dirty = true;
+        occ &= ~f.rmask;
+        fired_k = k_last + 1;
+        if (B < keep) B = keep;
+    }
+
     // Fire every window k <= k_target (end-1 <= wm).
     int fire_until(i128 k_target, i128 c_target) {
         int rc;
@@ -1137,50 +1191,18 @@ struct gw_handle {
             }
             i128 k_last = floor_div(B + R - n, m);
             if (k_last > k_target) k_last = k_target;
-            const int nwin = (int)(k_last - k_first + 1);
-            FireArgs f{};
-            f.t = tv;
-            f.ov = ov_view();
-            f.k0 = (int64_t)k_first;
-            f.nwin = nwin;
-            const i128 start0 = (i128)cfg.offset + k_first * (i128)slide();
-            const i128 endl = (i128)cfg.offset + k_last * (i128)slide() + size();
-            if (!fits64(start0) || !fits64(endl))
-                return fail(GW_E_RANGE, "window bounds overflow int64");
-            f.start0 = (int64_t)start0;
-            f.slide = slide();
-            f.size = size();
-            for (int w = 0; w < nwin; ++w) {
-                uint64_t wm_ = 0;
-                const i128 p0 = (k_first + w) * m;
-                for (int j = 0; j < n; ++j) wm_ |= 1ull << pos_of(p0 + j);
-                f.wmask[w] = wm_;
-            }
             if (k_last < k_first) return fail(GW_E_STATE, "pane ring too short for the retained panes");
-            uint64_t rmask = 0;
-            const i128 keep = lat ? std::min(k_last + 1, c_target) * m : (k_last + 1) * m;
-            for (i128 p = B; p < keep && p < B + R; ++p) rmask |= 1ull << pos_of(p);
-            f.rmask = rmask;
-            if ((rc = ensure_output((int64_t)h_st->rows + (int64_t)nwin * ((int64_t)h_st->used_slots + 1))))
+            FireArgs f{};
+            i128 keep;
+            if ((rc = fire_args(k_first, k_last, lat ? std::min(k_last + 1, c_target) * m : (k_last + 1) * m, f,
+                                keep)))
+                return rc;
+            if ((rc = ensure_output((int64_t)h_st->rows + (int64_t)f.nwin * ((int64_t)h_st->used_slots + 1))))
                 return rc;
             f.o_key = o_key; f.o_start = o_start; f.o_end = o_end; f.o_res = o_res;
-            f.st = d_st;
             lazy_retire(f);
-            if (timing) {
-                auto ev = t_fire.get();
-                HIPCHECK(hipEventRecord(ev.first, stream));
-                HIPCHECK(launch_fire(f, stream));
-                HIPCHECK(hipEventRecord(ev.second, stream));
-                t_fire.pending.push_back(ev);
-            } else {
-                HIPCHECK(launch_fire(f, stream));
-            }
-            stats.fires++;
-            if (recs_since_fire) recs_per_fire = recs_since_fire, recs_since_fire = 0;
-            dirty = true;
-            occ &= ~rmask;
-            fired_k = k_last + 1;
-            if (B < keep) B = keep;
+            if ((rc = fire_launch(f))) return rc;
+            fired(f, k_last, keep);
             if ((rc = refresh())) return rc;
         }
         if (lat) return retire_below(c_target * m);
@@ -1326,10 +1348,25 @@ struct gw_handle {
     // apply_mask (a fire, nar2 only): ring positions that must be applied now; the others may
     // stay in this flush's P2 output until the next flush (carry).  Every other caller applies
     // everything, carried positions included.
+    // A flush is its launches (flush_launch: false when there is nothing to apply) and what the
+    // host does once the status after them is exact (flush_post, after a refresh).
+    struct PendingFlush {
+        IngestArgs a;
+        int64_t window_recs = 0;
+    };
     int flush_buffer(uint64_t apply_mask = ~0ull) {
+        PendingFlush pf;
+        bool launched = false;
+        int rc;
+        if ((rc = flush_launch(apply_mask, pf, launched)) || !launched) return rc;
+        if ((rc = refresh())) return rc;
+        return flush_post(pf);
+    }
+    int flush_launch(uint64_t apply_mask, PendingFlush& pf, bool& launched) {
+        launched = false;
         if (!nseg && !carry_on) return GW_OK;
         int rc;
-        IngestArgs a;
+        IngestArgs& a = pf.a;
         if ((rc = base_args(a, 0, nullptr, nullptr, nullptr))) return rc;
         region_args(a);
         if (carry_on && !a.nar2) return fail(GW_E_STATE, "internal: carried records without a nar2 flush");
@@ -1378,9 +1415,15 @@ struct gw_handle {
         }
         stats.applies++;
         dirty = true;
-        if ((rc = refresh())) return rc;
+        launched = true;
+        pf.window_recs = window_recs;
+        return GW_OK;
+    }
+    int flush_post(PendingFlush& pf) {
+        int rc;
+        IngestArgs& a = pf.a;
         if (h_st->wide_vals) {  // records beyond the window's format went the deferred way: keep it rare
-            if (h_st->wide_vals * 64 > (unsigned long long)window_recs) {
+            if (h_st->wide_vals * 64 > (unsigned long long)pf.window_recs) {
                 if (a.fmt == 2) nar_off = true;
                 else cmp_off = true;
             }
@@ -2613,6 +2656,65 @@ struct gw_handle {
         return khm_insert_host(hkeys, hvals);
     }
 
+#ifndef GW_FAST_FIRE
+#define GW_FAST_FIRE 1  // 0: every fire after a flush waits for the flush's status first
+#endif
+    int64_t fast_fires = 0;  // fires enqueued behind their flush (gw_kernel_time_ms which = 3)
+    // The common fire -- no lateness, no restored windows, nothing deferred, one pass of
+    // windows starting at fired_k -- enqueued right behind the flush that precedes it, with
+    // k_fire_guard between them: ONE host round trip per watermark instead of two (the flush's
+    // status refresh and the fire's).  Everything the fire needs is decided on the host
+    // without the flush's counters: k_first = fired_k holds whenever the lowest pane the host
+    // knows of in the ring gives no later start (the device's ring holds at least those
+    // panes), no ring position is evicted (k_first * m >= B), and the ring reaches k_target.
+    // What the host would have read -- spills, wide records, a full table, a deferred entry,
+    // the row buffer's room -- the guard reads on the device; when any of them would have
+    // changed the host's course the fire does nothing (fire_skip), the flush is finished the
+    // exact way (flush_post) and advance_pane goes on as before.  done: the fire ran.
+    // Measured (profiles/r6/fastfire/): the flush->fire gap of the headline's fire cycle.
+    int fast_fire(i128 kt, uint64_t need, bool& done) {
+        done = false;
+        int rc;
+        const bool eligible = GW_FAST_FIRE && ov_n == 0 && !rf_bound && occ != 0 && h_st->n_deferred == 0;
+        const i128 k_first = fired_k;
+        if (eligible) {
+            const i128 kl = floor_div(ring_min() - n, m) + 1;
+            if (kl > k_first || k_first * m < B || floor_div(k_first * m + R - n, m) < kt) return flush_buffer(need);
+        } else {
+            return flush_buffer(need);
+        }
+        PendingFlush pf;
+        bool launched = false;
+        if ((rc = flush_launch(need, pf, launched))) return rc;
+        const i128 B0 = B;
+        const uint64_t stale0 = stale_pos;
+        B = k_first * m;  // rebase(k_first * m) without an eviction
+        FireArgs f{};
+        i128 keep;
+        if ((rc = fire_args(k_first, kt, (kt + 1) * m, f, keep))) return rc;
+        f.o_key = o_key; f.o_start = o_start; f.o_end = o_end; f.o_res = o_res;
+        f.guarded = 1;
+        lazy_retire(f);
+        FireGuard g{0, o_cap, (int64_t)f.nwin};
+        HIPCHECK(launch_fire_guard(d_st, g, stream));
+        if ((rc = fire_launch(f))) return rc;
+        dirty = true;
+        if ((rc = refresh())) return rc;
+        if (!h_st->fire_skip) {
+            fired(f, kt, keep);
+            dirty = false;  // the refresh above followed the fire
+            occ = h_st->occ;
+            fast_fires++;
+            done = true;
+            return GW_OK;
+        }
+        // the fire did nothing: undo the host's side of it and take the exact path
+        B = B0;
+        stale_pos = stale0;
+        if (timing) t_fire.drop_last();
+        return launched ? flush_post(pf) : GW_OK;
+    }
+
     int advance_pane(int64_t w, int64_t* rows_out) {
         int rc;
         if (rows_out) *rows_out = 0;
@@ -2650,7 +2752,15 @@ struct gw_handle {
                 need = 0;
                 for (i128 P = B; P <= plast; ++P) need |= 1ull << pos_of(P);
             }
-            if ((rc = flush_buffer(need))) return rc;
+            bool done = false;
+            if ((rc = fast_fire(kt, need, done))) return rc;
+            if (done) {
+                wm = w;
+                const int64_t fired_rows = (int64_t)h_st->rows - (int64_t)h_st->fire_rows0;
+                stats.rows_fired += fired_rows;
+                if (rows_out) *rows_out = fired_rows;
+                return GW_OK;
+            }
             if ((rc = ensure_fresh())) return rc;
             before = (int64_t)h_st->rows;
         }
@@ -4901,6 +5011,11 @@ int gw_kernel_time_ms(gw_handle* h, int which, double* ms, int64_t* launches) {
     }
     hipStreamSynchronize(h->stream);
     if (h->sess) return session_kernel_time(h->sess, which, ms, launches);
+    if (which == 3) {
+        if (ms) *ms = 0.0;
+        if (launches) *launches = h->fast_fires;
+        return GW_OK;
+    }
     KernelTimer& t = which == 0 ? h->t_ingest : which == 1 ? h->t_fire : h->t_apply;
     t.resolve();
     if (ms) *ms = t.launches ? t.total_ms / (double)t.launches : 0.0;

@@ -383,7 +383,9 @@ int  gw_synchronize(gw_handle* h);
 void* gw_stream(gw_handle* h);
 /* Average device duration (ms) per launch of each kernel family since the last call,
  * measured with HIP events on the handle's stream.  which: 0 = ingest (per batch;
- * region path: pass 1), 1 = fire, 2 = region pass 2 + apply (per buffer flush). */
+ * region path: pass 1), 1 = fire, 2 = region pass 2 + apply (per buffer flush).
+ * which = 3: *launches = the fires enqueued right behind their flush, without a host
+ * round trip between them (gw_advance_watermark's common case), *ms = 0. */
 int  gw_kernel_time_ms(gw_handle* h, int which, double* ms, int64_t* launches);
 /* enable: 0 off, 1 every launch, k > 1: the region path's pass 1 (one launch per batch, all
  * alike) is timed on every k-th batch only (two event records per timed launch cost host

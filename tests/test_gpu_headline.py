@@ -54,10 +54,12 @@ def test_headline_bench_cadence_every_watermark(oracle_lib):
         op.advance_watermark(W.LONG_MAX)
         run.consume()
         st = op.stats()
+        fast = op.kernel_time_ms(3)[1]
     finally:
         op.close()
     assert st["region_format"] == 2, st  # narrow region records: the headline's path
     assert st["applies"] == 3, st  # batch 0, ONE flush of batches 1..10, batch 11
+    assert fast >= 1  # batch 10's fire was enqueued right behind its flush (gw_runtime.cpp fast_fire)
     assert st["late_dropped"] == 0
     per_wm = run.per_wm
     assert len(per_wm) == steps + 1
