@@ -338,10 +338,13 @@ hipError_t launch_overlay_attach(const PaneTable& t, const Overlay& ov, int32_t*
 // path: 0 direct atomics, 1 LDS pre-aggregation (the region path has its own launchers)
 hipError_t launch_ingest(const IngestArgs& a, int path, int unroll, hipStream_t s);
 // region path: P1 over one batch (a.n records -> buffer tiles from a.tile0) ...
-hipError_t launch_region_p1(const IngestArgs& a, hipStream_t s);
+// e0 / e1 (timing, may be null): events stamped with the first kernel's start and the last
+// kernel's end of the launch (hipExtLaunchKernelGGL), so a timed launch measures its kernels
+// without the marker packets of hipEventRecord around them.
+hipError_t launch_region_p1(const IngestArgs& a, hipStream_t s, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);
 hipError_t launch_publish_status(const IngestArgs& a, hipStream_t s);
 // ... and, per flush, plan + P2 (two-pass tables) + apply over a.ntiles buffer tiles
-hipError_t launch_region_flush(const IngestArgs& a, hipStream_t s);
+hipError_t launch_region_flush(const IngestArgs& a, hipStream_t s, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);
 // ... and after a flush that filled regions: its spilled records -> the deferred list
 hipError_t launch_region_collect(const IngestArgs& a, hipStream_t s);
 int region_group(int d1_bits);  // G: P1 tiles per P2 block
@@ -351,7 +354,7 @@ hipError_t launch_refire(const RefireArgs& a, hipStream_t s);
 hipError_t launch_refire_keys(int mode, const int64_t* src, int64_t base, uint64_t* k, uint32_t* v, int64_t n,
                               hipStream_t s);
 hipError_t launch_deferred_min(const int64_t* pane, int64_t n, DevStatus* st, hipStream_t s);
-hipError_t launch_fire(const FireArgs& a, hipStream_t s);
+hipError_t launch_fire(const FireArgs& a, hipStream_t s, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr);
 // The checks that let a fire be enqueued right behind a flush, without the host reading the
 // status in between (gw_runtime.cpp fast_fire): st->fire_skip = 1 -- the guarded fire does
 // nothing and the host takes the exact path -- when the flush left spilled or wide records or

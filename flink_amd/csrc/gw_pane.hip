@@ -31,6 +31,7 @@
 //           atomics on the state; every HBM access is a contiguous stream.
 //   direct  (small batches)  k_ingest: one device-scope atomic per record.
 //   preagg  (few keys)       k_ingest_preagg: LDS combine per (slot, pane), then atomics.
+#include <hip/hip_ext.h>
 #include <type_traits>
 #include "gw_kernels.h"
 
@@ -2764,6 +2765,22 @@ hipError_t launch_ingest(const IngestArgs& a, int path, int unroll, hipStream_t 
     return hipGetLastError();
 }
 
+// A launch that stamps timing events with its own start / end when given them (e0 / e1 of
+// launch_region_p1 / launch_region_flush / launch_fire), a plain launch otherwise.
+#define GW_TLAUNCH(K, G, B, L, S, E0, E1, ...)                                \
+    do {                                                                      \
+        if ((E0) || (E1)) hipExtLaunchKernelGGL(K, G, B, L, S, E0, E1, 0, __VA_ARGS__); \
+        else hipLaunchKernelGGL(K, G, B, L, S, __VA_ARGS__);                   \
+    } while (0)
+
+// A timed launch with no kernel to run: both events at this point of the stream (so they are
+// valid and measure ~0).
+static hipError_t record_empty(hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
+    if (e0) { const hipError_t e = hipEventRecord(e0, s); if (e != hipSuccess) return e; }
+    if (e1) { const hipError_t e = hipEventRecord(e1, s); if (e != hipSuccess) return e; }
+    return hipSuccess;
+}
+
 // Opt a kernel in to more than 64 KB of dynamic LDS (gfx950 has 160 KB per CU) once per
 // size, not per launch: the attribute call costs host time on every ingest otherwise.
 static void lds_opt_in(const void* f, size_t bytes) {
@@ -2792,15 +2809,15 @@ int region_group(int d1_bits) {
 }
 
 // Region path, P1 over one watermark batch: one block per 4096-record tile.
-hipError_t launch_region_p1(const IngestArgs& a, hipStream_t s) {
+hipError_t launch_region_p1(const IngestArgs& a, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
     const int64_t tiles = (a.n + kPartTile - 1) / kPartTile;
-    if (tiles == 0) return hipSuccess;
+    if (tiles == 0) return record_empty(s, e0, e1);
     const size_t part_lds = part_lds_bytes(a);
     // beyond the 64 KB default: opt in (gfx950 has 160 KB of LDS per CU)
     // the gap test (size < slide) only in a variant of its own: it costs the hot pass ~3%
 #define P1L(A, F, G)                                                                                            \
     lds_opt_in((const void*)k_rgn_p1<A, F, G>, part_lds);                                                      \
-    hipLaunchKernelGGL((k_rgn_p1<A, F, G>), dim3((unsigned)tiles), dim3(kPartThreads), part_lds, s, a)
+    GW_TLAUNCH((k_rgn_p1<A, F, G>), dim3((unsigned)tiles), dim3(kPartThreads), part_lds, s, e0, e1, a)
 #define L(A)                                  \
     if (a.gap_size) {                         \
         P1L(A, kFmtWide, true);               \
@@ -2824,25 +2841,26 @@ hipError_t launch_publish_status(const IngestArgs& a, hipStream_t s) {
 
 // Region path, per flush over a.ntiles buffer tiles: plan + P2 (two-pass tables), then
 // one workgroup per region applies its runs.
-hipError_t launch_region_flush(const IngestArgs& a, hipStream_t s) {
+hipError_t launch_region_flush(const IngestArgs& a, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
     const bool single = !a.two_pass;
     const size_t part_lds = part_lds_bytes(a);
     const int64_t S = pt_S(a.t);
     const size_t apply_lds = (size_t)(S + pt_mask_words(a.t)) * 8 + (size_t)2 * S * a.t.words * 8 +
                              (size_t)(kApplyThreads / 64) * kApplyQ * (a.t.words == 2 ? 25 : 17);  // + miss queues
     const int nb1 = 1 << a.d1_bits;
-    if (a.ntiles == 0 && !(a.nar2 && a.c_mask)) return hipSuccess;
+    if (a.ntiles == 0 && !(a.nar2 && a.c_mask)) return record_empty(s, e0, e1);
 #define L2(A, CM)                                                                                               \
     lds_opt_in((const void*)k_rgn_p2<A, CM>, part_lds);                                                       \
     lds_opt_in((const void*)k_rgn_apply<A, CM>, apply_lds);                                                   \
     if (!single) {                                                                                              \
-        hipLaunchKernelGGL(k_rgn_plan1, dim3((unsigned)a.ngroups), dim3(256), 0, s, a);                        \
+        GW_TLAUNCH(k_rgn_plan1, dim3((unsigned)a.ngroups), dim3(256), 0, s, e0, nullptr, a);                   \
         hipLaunchKernelGGL(k_rgn_plan2, dim3((unsigned)nb1), dim3(256), 0, s, a);                              \
         hipLaunchKernelGGL(k_rgn_plan3, dim3(1), dim3(256), 0, s, a);                                          \
         hipLaunchKernelGGL((k_rgn_p2<A, CM>), dim3((unsigned)(a.ngroups * nb1)), dim3(kPartThreads), part_lds, s, \
                            a);                                                                                  \
     }                                                                                                           \
-    hipLaunchKernelGGL((k_rgn_apply<A, CM>), dim3((unsigned)a.t.nreg), dim3(kApplyThreads), apply_lds, s, a)
+    GW_TLAUNCH((k_rgn_apply<A, CM>), dim3((unsigned)a.t.nreg), dim3(kApplyThreads), apply_lds, s,               \
+               single ? e0 : nullptr, e1, a)
 #define L(A)                        \
     if (a.fmt == kFmtNar) {         \
         L2(A, kFmtNar);             \
@@ -2861,13 +2879,14 @@ hipError_t launch_region_flush(const IngestArgs& a, hipStream_t s) {
     lds_opt_in((const void*)k_rgn_p2<A, kFmtNar>, part_lds);                                                   \
     lds_opt_in((const void*)k_rgn_apply_nar<A>, lds);                                                         \
     if (!a.cur_empty) {                                                                                         \
-        hipLaunchKernelGGL(k_rgn_plan1, dim3((unsigned)a.ngroups), dim3(256), 0, s, a);                        \
+        GW_TLAUNCH(k_rgn_plan1, dim3((unsigned)a.ngroups), dim3(256), 0, s, e0, nullptr, a);                   \
         hipLaunchKernelGGL(k_rgn_plan2, dim3((unsigned)nb1), dim3(256), 0, s, a);                              \
         hipLaunchKernelGGL(k_rgn_plan3, dim3(1), dim3(256), 0, s, a);                                          \
         hipLaunchKernelGGL((k_rgn_p2<A, kFmtNar>), dim3((unsigned)(a.ngroups * nb1)), dim3(kPartThreads), part_lds, \
                            s, a);                                                                               \
     }                                                                                                           \
-    hipLaunchKernelGGL(k_rgn_apply_nar<A>, dim3((unsigned)(a.t.nreg >> a.sr_bits)), dim3(kApplyThreads), lds, s, a)
+    GW_TLAUNCH(k_rgn_apply_nar<A>, dim3((unsigned)(a.t.nreg >> a.sr_bits)), dim3(kApplyThreads), lds, s,        \
+               a.cur_empty ? e0 : nullptr, e1, a)
         GW_AGG_SWITCH(a.t.agg, LN);
 #undef LN
         return hipGetLastError();
@@ -2923,7 +2942,7 @@ hipError_t launch_deferred_min(const int64_t* pane, int64_t n, DevStatus* st, hi
     return hipGetLastError();
 }
 
-hipError_t launch_fire(const FireArgs& a, hipStream_t s) {
+hipError_t launch_fire(const FireArgs& a, hipStream_t s, hipEvent_t e0, hipEvent_t e1) {
     uint64_t need = 0;
     for (int w = 0; w < a.nwin; ++w) need |= a.wmask[w];
     const int npos = __builtin_popcountll(need);
@@ -2933,7 +2952,7 @@ hipError_t launch_fire(const FireArgs& a, hipStream_t s) {
         const int64_t tile = (int64_t)kF2Threads * (av ? 1 : 2);  // U slots per lane
         const int fg = (int)std::min<int64_t>(1024, std::max<int64_t>(1, (a.t.cap + 1 + tile - 1) / tile));
 #define F2(A, NPV) \
-    hipLaunchKernelGGL((k_fire2<A, NPV, (A == GW_AVG_I64 || A == GW_AVG_F64) ? 1 : 2>), dim3(fg), dim3(kF2Threads), 0, s, a)
+    GW_TLAUNCH((k_fire2<A, NPV, (A == GW_AVG_I64 || A == GW_AVG_F64) ? 1 : 2>), dim3(fg), dim3(kF2Threads), 0, s, e0, e1, a)
 #define L(A)                      \
     switch (npos) {               \
     case 1: F2(A, 1); break;      \
@@ -2949,7 +2968,7 @@ hipError_t launch_fire(const FireArgs& a, hipStream_t s) {
         return hipGetLastError();
     }
     const int fg = (int)std::min<int64_t>(1024, std::max<int64_t>(1, (a.t.cap + 1 + 255) / 256));
-#define L(A) hipLaunchKernelGGL(k_fire<A>, dim3(fg), dim3(256), 0, s, a)
+#define L(A) GW_TLAUNCH(k_fire<A>, dim3(fg), dim3(256), 0, s, e0, e1, a)
     GW_AGG_SWITCH(a.t.agg, L);
 #undef L
     return hipGetLastError();

@@ -419,6 +419,7 @@ struct gw_handle {
     int64_t async_recs[kAsync] = {};    // records of the batch each copy follows
     uint64_t hgen = 0;        // host writes to the status (a snapshot older than one is stale)
     int async_slot = 0;
+    bool occ_zeroed = false;  // batch_occ (d_tmp[1]) zeroed behind the last flush, no pass 1 since
     bool lazy = false;        // launches since the last exact status: region P1 only
     int64_t lazy_recs = 0;    // records of those launches (bound on their deferred entries)
 
@@ -441,10 +442,22 @@ struct gw_handle {
         a.st_seq = async_seq[s] = ++pub_ctr;
     }
     // Wait until slot o carries its launch's stamp (the P1 has finished publishing).
+    // The tag is polled in host memory; the stream is queried only after the wait has lasted
+    // 1 ms, then every 1 ms (a failed or finished stream whose P1 never published): each
+    // hipStreamQuery on a busy stream put a ~5-us gap between the queued P1 launches
+    // (profiles/r6/gaps/).
     int wait_published(int o) {
         volatile uint64_t* tag = (volatile uint64_t*)&h_st_async[o]->pad[kPubSeqWord];
+        auto next_query = std::chrono::steady_clock::time_point::min();
         for (int64_t spin = 0; *tag != async_seq[o]; ++spin) {
             if ((spin & 255) == 255) {
+                const auto now = std::chrono::steady_clock::now();
+                if (next_query == std::chrono::steady_clock::time_point::min()) {
+                    next_query = now + std::chrono::milliseconds(1);
+                    continue;
+                }
+                if (now < next_query) { std::this_thread::yield(); continue; }
+                next_query = now + std::chrono::milliseconds(1);
                 const hipError_t q = hipStreamQuery(stream);
                 if (q == hipSuccess && *tag != async_seq[o])
                     return fail(GW_E_DEVICE, "status slot not published by the finished pass 1");
@@ -1147,9 +1160,7 @@ struct gw_handle {
     int fire_launch(const FireArgs& f) {
         if (timing) {
             auto ev = t_fire.get();
-            HIPCHECK(hipEventRecord(ev.first, stream));
-            HIPCHECK(launch_fire(f, stream));
-            HIPCHECK(hipEventRecord(ev.second, stream));
+            HIPCHECK(launch_fire(f, stream, ev.first, ev.second));
             t_fire.pending.push_back(ev);
         } else {
             HIPCHECK(launch_fire(f, stream));
@@ -1406,13 +1417,15 @@ struct gw_handle {
         }
         if (timing) {
             auto ev = t_apply.get();
-            HIPCHECK(hipEventRecord(ev.first, stream));
-            HIPCHECK(launch_region_flush(a, stream));
-            HIPCHECK(hipEventRecord(ev.second, stream));
+            HIPCHECK(launch_region_flush(a, stream, ev.first, ev.second));
             t_apply.pending.push_back(ev);
         } else {
             HIPCHECK(launch_region_flush(a, stream));
         }
+        // the next window's pass-1 occupancy word, zeroed while the device is still busy (behind
+        // the apply that read it) instead of on the host's critical path at its first pass 1
+        HIPCHECK(hipMemsetAsync(d_tmp + 1, 0, 8, stream));
+        occ_zeroed = true;
         stats.applies++;
         dirty = true;
         launched = true;
@@ -1554,7 +1567,8 @@ struct gw_handle {
                     region_args(a);
                     a.tile0 = buf_tiles;
                 }
-                HIPCHECK(hipMemsetAsync(d_tmp + 1, 0, 8, stream));
+                if (!occ_zeroed) HIPCHECK(hipMemsetAsync(d_tmp + 1, 0, 8, stream));
+                occ_zeroed = false;
                 buf_fresh = ~occ;
                 buf_fmt = fmt;
             }
@@ -1565,9 +1579,7 @@ struct gw_handle {
             hp.lap(13);
             if (timing && (timing_ctr++ % timing_every) == 0) {  // every timing_every-th batch
                 auto ev = t_ingest.get();
-                HIPCHECK(hipEventRecord(ev.first, stream));
-                HIPCHECK(launch_region_p1(a, stream));
-                HIPCHECK(hipEventRecord(ev.second, stream));
+                HIPCHECK(launch_region_p1(a, stream, ev.first, ev.second));
                 t_ingest.pending.push_back(ev);
             } else {
                 HIPCHECK(launch_region_p1(a, stream));

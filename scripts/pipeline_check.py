@@ -19,7 +19,11 @@ p1_idx = [i for i, r in enumerate(rows) if name(r) == "k_rgn_p1"]
 first_timed_p1 = p1_idx[warm]
 start = max(i for i in applies if i < first_timed_p1)
 last_timed_p1 = p1_idx[warm + steps - 1]
-end = min(i for i in applies if i > last_timed_p1)  # the final flush (a host-fed leg may follow)
+# the fire's flush after the last timed batch, and bench's closing gw_flush right behind it (the
+# ring positions the last fire left carried): every apply before the next pass 1 (a host-fed
+# leg may follow)
+nxt = min([i for i in p1_idx if i > last_timed_p1] + [len(rows)])
+end = max(i for i in applies if last_timed_p1 < i < nxt)
 dur = {}
 for r in rows[start + 1:end + 1]:
     n = name(r)
