@@ -365,6 +365,7 @@ struct FireGuard {
     unsigned long long expect_ndef;
     int64_t o_cap;
     int64_t nwin;
+    int64_t reset_rows;  // first zero the row cursor (a gw_clear_rows the host deferred to here)
 };
 hipError_t launch_fire_guard(DevStatus* st, const FireGuard& g, hipStream_t s);
 // Cells of ring positions `pmask` whose presence bit is clear -> the identity (the retires a

@@ -2558,7 +2558,8 @@ __global__ void __launch_bounds__(64) k_fire_guard(DevStatus* st, FireGuard g) {
     flags = wave_ior(flags);
     used = wave_sum(used);
     if (lane == 0) {
-        const unsigned long long rows = st->rows;
+        if (g.reset_rows) st->rows = 0;
+        const unsigned long long rows = g.reset_rows ? 0ull : st->rows;
         const bool skip = st->spills != 0 || st->wide_vals != 0 ||
                           (flags & (GW_DF_TABLE_FULL | GW_DF_NO_TS | GW_DF_RANGE)) != 0 ||
                           st->n_deferred != g.expect_ndef ||

@@ -419,6 +419,10 @@ struct gw_handle {
     int64_t async_recs[kAsync] = {};    // records of the batch each copy follows
     uint64_t hgen = 0;        // host writes to the status (a snapshot older than one is stale)
     int async_slot = 0;
+    // gw_clear_rows on the host only: the device's row cursor is zeroed by the next launch that
+    // emits rows (the fast fire's guard, or a status write before any other fire); until then
+    // every status the host reads has its row count taken as 0
+    bool rows_reset_pending = false;
     bool occ_zeroed = false;  // batch_occ (d_tmp[1]) zeroed behind the last flush, no pass 1 since
     bool lazy = false;        // launches since the last exact status: region P1 only
     int64_t lazy_recs = 0;    // records of those launches (bound on their deferred entries)
@@ -499,6 +503,7 @@ struct gw_handle {
     }
     int absorb() {
         fold_shards(h_st);
+        if (rows_reset_pending) h_st->rows = 0;
         if (h_st->flags & GW_DF_NO_TS)
             return fail(GW_E_NO_TIMESTAMP,
                         "Record has Long.MIN_VALUE timestamp (= no timestamp marker). Did you forget to "
@@ -529,6 +534,12 @@ struct gw_handle {
         return GW_OK;
     }
     int take_occ() { occ = h_st->occ; return GW_OK; }
+    // The deferred gw_clear_rows, before a launch that moves the row cursor.
+    int rows_reset_now() {
+        if (!rows_reset_pending) return GW_OK;
+        rows_reset_pending = false;
+        return set_field(offsetof(DevStatus, rows), 0);
+    }
 
     // ---------------------------------------------------------------- memory
     // Pane-table load: the table is sized for the expected keys at kTableLoad and grows past
@@ -1017,6 +1028,7 @@ struct gw_handle {
             r.size = size();
             r.o_key = o_key; r.o_start = o_start; r.o_end = o_end; r.o_res = o_res;
             r.st = d_st;
+            if ((rc = rows_reset_now())) return rc;
             HIPCHECK(launch_refire(r, stream));
             // the records join their panes (windows that fire later fold them)
             if ((rc = ensure_deferred((int64_t)h_st->n_deferred + nrf))) return rc;
@@ -1158,6 +1170,8 @@ struct gw_handle {
         return GW_OK;
     }
     int fire_launch(const FireArgs& f) {
+        int rc;
+        if ((rc = rows_reset_now())) return rc;
         if (timing) {
             auto ev = t_fire.get();
             HIPCHECK(launch_fire(f, stream, ev.first, ev.second));
@@ -2707,7 +2721,8 @@ struct gw_handle {
         f.o_key = o_key; f.o_start = o_start; f.o_end = o_end; f.o_res = o_res;
         f.guarded = 1;
         lazy_retire(f);
-        FireGuard g{0, o_cap, (int64_t)f.nwin};
+        FireGuard g{0, o_cap, (int64_t)f.nwin, rows_reset_pending ? 1 : 0};
+        rows_reset_pending = false;  // the guard zeroes the cursor
         HIPCHECK(launch_fire_guard(d_st, g, stream));
         if ((rc = fire_launch(f))) return rc;
         dirty = true;
@@ -4855,7 +4870,9 @@ int gw_clear_rows(gw_handle* h) {
     h->rows_head = 0;
     if (h->session) return session_clear_rows(h->sess, h->err);
     if (h->h_st->rows == 0) return GW_OK;  // rows only grow in a fire, which refreshes h_st
-    return h->set_field(offsetof(DevStatus, rows), 0);
+    h->h_st->rows = 0;  // the device cursor: by the next launch that emits rows (rows_reset_now)
+    h->rows_reset_pending = true;
+    return GW_OK;
 }
 
 int gw_pending_late(gw_handle* h, int64_t* n) {
