@@ -74,6 +74,11 @@ def parse(argv=None):
     ap.add_argument("--exchange-stream", choices=["own", "operator"], default="own",
                     help="own: the exchange (partition, all-to-all, sends) on a stream of its own, overlapping "
                          "the operator's kernels; operator: on the operator's stream, serialised with them")
+    ap.add_argument("--exchange-ahead", type=int, choices=[1, 2], default=1,
+                    help="batches the exchange finishes ahead of the ingest: 1 finishes batch b right before "
+                         "its ingest (and begins b+1); 2 finishes b+1 (and begins b+2) before batch b is "
+                         "ingested and its watermark fires, so the exchange stream has work queued while the "
+                         "fire's flush holds the operator's stream; measured the same as 1 (profiles/r6/exchange/driver/)")
     ap.add_argument("--force-exchange", action="store_true",
                     help="run the RCCL exchange path at N = 1 too (a one-rank communicator: every record comes "
                          "back to this rank) -- a check of the N > 1 code path on one GPU")
@@ -155,7 +160,8 @@ class Steps:
     With `collect` the rows of every watermark are drained to the host and (count, checksum)
     recorded."""
 
-    def __init__(self, op, N, keys, ts, vals, wms, nb, ex=None, collect=False, ex_stream=None, keep_rows=False):
+    def __init__(self, op, N, keys, ts, vals, wms, nb, ex=None, collect=False, ex_stream=None, keep_rows=False,
+                 ahead=1):
         import ctypes
         self.op, self.N, self.ex, self.ex_stream = op, N, ex, ex_stream
         self.keys, self.ts, self.vals, self.wms, self.nb = keys, ts, vals, wms, nb
@@ -165,6 +171,9 @@ class Steps:
         self.rows = []
         self.exch_bytes = 0
         self.begun = -1  # the last batch whose exchange has begun
+        self.finished = -1  # ... and finished (its receive columns in self.ready until ingested)
+        self.ready = {}
+        self.ahead = ahead
         # the host side of a step stays lean (the GPU runs a batch in ~70 us): the library's entry
         # points and each batch's device column pointers resolved once, before any clock
         L = N.lib()
@@ -185,24 +194,38 @@ class Steps:
         self.ex.begin(self.keys[lo:hi], self.ts[lo:hi], v, stream=self.ex_stream, wm=self.wms[b])
         self.begun = b
 
+    def _finish(self, timed, b_in, rank):
+        """gw_exchange_finish of the oldest begun batch; its receive columns (and words) wait
+        in self.ready until the batch is ingested."""
+        n, pk, pt, pv, _, wmin, ist = self.ex.finish(self.ex_stream)
+        if timed:  # bytes this rank sent to its peers (received packed share as the estimate)
+            f = self.ex.last_packed() / max(self.nb, 1)
+            self.exch_bytes += (self.nb - int(self.ex.counts()[0][rank])) * (8 * f + b_in * (1 - f))
+        self.finished += 1
+        self.ready[self.finished] = (n, pk, pt, pv, wmin, ist, self.ex.last_words())
+
     def step(self, b, timed=False, b_in=24, rank=0, last=None):
         """One batch; returns the rows its watermark fired.  last: the last batch of this phase
-        (warmup / timed): the exchange begins batches up to it one step ahead."""
+        (warmup / timed): the exchange begins and finishes batches up to it ahead of the ingest."""
         op, nb, N = self.op, self.nb, self.N
         if self.ex is not None:
             # the native exchange on a stream of its own; the ingest orders through the receive
-            # set's hand-off stream, so batch b+1's partition and transfers overlap batch b's
-            # aggregation on the operator's stream, and batch b+1 is partitioned and its counts
-            # exchanged before the host waits for batch b's
-            if self.begun < b:
-                self._begin(b)
-            if last is not None and b + 1 <= last and self.begun < b + 1:
-                self._begin(b + 1)
-            n, pk, pt, pv, _, wmin, ist = self.ex.finish(self.ex_stream)
-            if timed:  # bytes this rank sent to its peers (received packed share as the estimate)
-                f = self.ex.last_packed() / max(nb, 1)
-                self.exch_bytes += (nb - int(self.ex.counts()[0][rank])) * (8 * f + b_in * (1 - f))
-            nw, pw, geom = self.ex.last_words()
+            # set's hand-off stream, so later batches' partitions and transfers overlap batch b's
+            # aggregation on the operator's stream.  Batches up to b + ahead - 1 are finished
+            # (their transfers queued) and the one after is begun (partitioned, its counts
+            # exchanged) before batch b is ingested: with ahead = 2 the exchange stream holds the
+            # next batches' work while a firing watermark's flush and fire hold the operator.
+            hi = b + self.ahead - 1
+            if last is not None:
+                hi = max(b, min(hi, last))
+            bh = hi + 1 if (last is not None and hi + 1 <= last) else hi
+            while self.finished < hi:  # (the exchange holds at most two begun, unfinished batches)
+                while self.begun < min(self.finished + 2, bh):
+                    self._begin(self.begun + 1)
+                self._finish(timed, b_in, rank)
+            while self.begun < bh and self.begun - self.finished < 2:
+                self._begin(self.begun + 1)
+            n, pk, pt, pv, wmin, ist, (nw, pw, geom) = self.ready.pop(b)
             if nw:  # words kept packed: pass 1 decodes them
                 N.check(self._ingest_packed(self._h, n, pk, pt, pv, nw, pw, self._byref(geom), ist), self._h)
             else:
@@ -278,7 +301,8 @@ def main(argv=None):
             ex.keep_words(args.pack == "auto")
     xs = torch.cuda.Stream(device=dev) if ex is not None and args.exchange_stream == "own" else None
     run = Steps(op, N, keys, ts, vals, wms, nb, ex=ex, collect=args.checksum,
-                ex_stream=xs.cuda_stream if xs is not None else (op.stream() if ex is not None else None))
+                ex_stream=xs.cuda_stream if xs is not None else (op.stream() if ex is not None else None),
+                ahead=args.exchange_ahead)
 
     # pass 1 timed on every 4th batch (all batches are alike): two event records per timed launch
     # cost host time between batches; the fire and flush timers run on every launch
@@ -419,7 +443,8 @@ def main(argv=None):
         if world > 1 or ex is not None:
             pk = args.pack != "off" and not agg.endswith("f64")
             out["exchange_gbs_per_gpu"] = run.exch_bytes / elapsed / 1e9
-            out["exchange_path"] = ("gw_exchange_begin / gw_exchange_finish one batch ahead (libgpuwin RCCL: "
+            drv = f"{args.exchange_ahead} batch(es) finished ahead of the ingest"
+            out["exchange_path"] = (f"gw_exchange_begin / gw_exchange_finish {drv} (libgpuwin RCCL: "
                                     "partition, one all-to-all of (count, watermark, columns, packed count), one "
                                     "bounded host wait, grouped send/recv per batch" + ((", 8-B packed words decoded by pass 1" if args.pack == "auto"
                                                     else ", 8-B packed words unpacked to columns") if pk

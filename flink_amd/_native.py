@@ -60,6 +60,7 @@ EXPORTS = [
     "gw_exchange_set_unpack", "gw_exchange_last_words", "gw_ingest_packed_device",
 ]
 EXCHANGE_ID_BYTES = 128
+EXCHANGE_RECV_SETS = 3  # gpuwin.h GW_EXCHANGE_RECV_SETS
 
 
 class GwRecordLayout(ctypes.Structure):

@@ -62,8 +62,11 @@ struct gw_exchange {
     // batch b's receives wait only for the ingest of batch b - 3 to have read its set: with two,
     // the exchange stream waited on the operator's pass 1 of batch b - 2, which itself runs
     // beside the exchange's partition of a later batch (measured: ~50 us per batch of the
-    // exchange stream idling on that cross-stream event, profiles/r6/exchange/).
-    static constexpr int kSets = 3;
+    // exchange stream idling on that cross-stream event, profiles/r6/exchange/).  Finishing
+    // batches further ahead of the ingest (bench.py --exchange-ahead 2, or from a host thread of
+    // its own with four sets) measured no faster: the partition then runs beside the flush and
+    // both slow down (profiles/r6/exchange/driver/).
+    static constexpr int kSets = GW_EXCHANGE_RECV_SETS;
     int64_t* recv[kSets] = {};
     int32_t* recv_hash[kSets] = {};
     uint64_t* recv_packed[kSets] = {};
@@ -386,6 +389,7 @@ int gw_exchange_begin(gw_exchange* ex, int64_t n, const int64_t* d_key, const in
                       const int64_t* d_ts, const int64_t* d_value, int64_t wm, void* stream) {
     if (!ex || n < 0 || (n > 0 && (!d_key || !d_ts))) return GW_E_INVALID;
     EX_LIVE(ex);
+    EX_HIP(hipSetDevice(ex->device));  // the calling thread's device (a driver may run the exchange on a thread of its own)
     if (ex->begun - ex->finished >= 2)
         return ex_fail(ex, GW_E_STATE, "gw_exchange_begin: two batches begun and not finished");
     hipStream_t s = (hipStream_t)stream;
@@ -481,6 +485,7 @@ int gw_exchange_finish(gw_exchange* ex, int64_t* n_out, const int64_t** d_key_ou
                        void* stream) {
     if (!ex || !n_out || !d_key_out || !d_ts_out) return GW_E_INVALID;
     EX_LIVE(ex);
+    EX_HIP(hipSetDevice(ex->device));
     if (ex->finished == ex->begun) return ex_fail(ex, GW_E_STATE, "gw_exchange_finish: no batch begun");
     hipStream_t s = (hipStream_t)stream;
     gw_exchange::PartSet& q = ex->ps[ex->finished & 1];

@@ -2806,7 +2806,7 @@ int region_group(int d1_bits) {
     // the headline with two, 0.82 ms with half a round; GW_P2_GROUP overrides for experiments)
     static const int env = getenv("GW_P2_GROUP") ? atoi(getenv("GW_P2_GROUP")) : 0;
     if (env > 0) return std::min(kMaxGroup, env);
-    return std::max(1, std::min(kMaxGroup, 7 * (1 << d1_bits) / 4 * (4096 / kPartTile)));
+    return std::max(1, std::min(kMaxGroup, 7 * (1 << d1_bits) * 4096 / (4 * kPartTile)));
 }
 
 // Region path, P1 over one watermark batch: one block per 4096-record tile.

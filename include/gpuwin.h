@@ -512,12 +512,15 @@ int  gw_ingest_packed_device(gw_handle* h, int64_t n_other, const int64_t* d_key
  * that every rank sends the same columns (GW_E_INVALID otherwise, on every rank), then
  * enqueues one grouped ncclSend/ncclRecv per column and peer on `stream`.  Out: the *n_out
  * records this rank owns in receive columns owned by the exchange (*d_*_out; NULL for an
- * absent column), valid until the next-but-two call (three receive sets used in turn);
+ * absent column), valid until GW_EXCHANGE_RECV_SETS batches later (receive sets used in turn);
  * *wm_out = the minimum of the ranks' watermarks (StatusWatermarkValve); *ingest_stream = a
  * hand-off stream of this receive set, ordered after the receives: pass it as the producer
  * stream of gw_ingest_device, whose "producer waits for my reads" ordering then lands on
  * the hand-off stream, so the exchange of the next batch never waits for this batch's
- * ingest, only the reuse of this receive set three batches later does.  All ranks call it
+ * ingest, only the reuse of this receive set GW_EXCHANGE_RECV_SETS batches later does; that
+ * ordering is taken when the later batch is finished, so a driver that finishes batches ahead of
+ * the ingest (e.g. from a thread of its own) finishes batch b only once the ingest of batch
+ * b - GW_EXCHANGE_RECV_SETS has been issued.  All ranks call it
  * for every batch (n may be 0).  gw_exchange_counts: the last batch's per-peer send and
  * receive record counts (nranks each; either may be NULL).
  *
@@ -529,6 +532,7 @@ int  gw_ingest_packed_device(gw_handle* h, int64_t n_other, const int64_t* d_key
  * gw_exchange_last_error.  Every later call on that exchange returns GW_E_STATE; destroy it
  * and fail the task (the JVM side throws, GpuKeyByExchange.java). */
 #define GW_EXCHANGE_ID_BYTES 128
+#define GW_EXCHANGE_RECV_SETS 3
 typedef struct gw_exchange gw_exchange;
 int  gw_exchange_unique_id(void* id);
 int  gw_exchange_create(gw_exchange** out, int32_t nranks, int32_t rank, const void* id, int32_t device,
@@ -541,7 +545,8 @@ int  gw_exchange_set_timeout(gw_exchange* ex, int64_t timeout_ms);
  * queues the sends / receives and returns what gw_exchange_batch returns.  Up to two batches
  * may be begun and not finished (GW_E_STATE beyond); issue begin(b + 1) before finish(b) and
  * the partition of b + 1 runs while the host waits for b's counts.  Both halves of a batch
- * on the same stream.  Packing takes its base pane from the combined watermark of the last
+ * on the same stream.  Each call selects the exchange's device for the calling thread, so the
+ * exchange may run on a host thread of its own (one thread per exchange at a time).  Packing takes its base pane from the combined watermark of the last
  * batch finished before the begin (the same on every rank, which begin and finish in the
  * same order). */
 int  gw_exchange_begin(gw_exchange* ex, int64_t n, const int64_t* d_key, const int32_t* d_key_hash,
