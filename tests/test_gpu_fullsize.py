@@ -129,7 +129,10 @@ Q7 = dict(assigner="tumbling", size=10_000, slide=10_000)
 
 
 @pytest.mark.timeout(600)
-@pytest.mark.parametrize("agg,full_oracle", [("sum_i64", True), ("count", True)])
+# sum_i64 at this size runs in tests/test_gpu_headline.py (the bench's own cadence, every row of
+# every watermark against the oracle); count here covers the 4-byte narrow records at 2M-record
+# batches (the suite stays under ~600 s of the driver's 900-s step)
+@pytest.mark.parametrize("agg,full_oracle", [("count", True)])
 def test_q5_10m_keys_100m_events(oracle_lib, agg, full_oracle):
     """Nexmark Q5 at its BASELINE size: 10M keys, 100M events (20M per 2-s pane, 50
     watermark batches, 5 windows fire during the stream, the rest at MAX_WATERMARK)."""
