@@ -5,9 +5,9 @@
 # host-fed legs included) and the cross-check of its HIP-event pipeline time against the trace.
 set -u
 export TMPDIR=/tmp
-O=gpurun_out/r6/final
+O=gpurun_out/r6/${FINAL:-final}
 mkdir -p $O profiles/r6
-TAG=r6/final bash scripts/headline_profile.sh > $O/headline_profile.log 2>&1 || { tail -20 $O/headline_profile.log; exit 4; }
+TAG=r6/${FINAL:-final} bash scripts/headline_profile.sh > $O/headline_profile.log 2>&1 || { tail -20 $O/headline_profile.log; exit 4; }
 tail -12 $O/headline_profile.log
 cp $O/traffic.json profiles/r6/traffic.json
 timeout -k 10 600 python -u bench.py > $O/bench.json 2> $O/bench.err || { tail -20 $O/bench.err; exit 5; }
