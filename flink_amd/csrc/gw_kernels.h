@@ -213,6 +213,7 @@ struct IngestArgs {
     DevStatus* st_host;             // buffered P1: pinned host slot k_publish_status copies the status into
     unsigned long long st_seq;      //     and the stamp it writes last
     uint64_t ring_fresh;            // ring positions holding only identities (not in occ)
+    int32_t stale;                  // lazily retired cells may hold stale values behind clear presence bits
 };
 
 #ifndef GW_PART_TILE

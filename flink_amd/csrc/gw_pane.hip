@@ -1207,7 +1207,7 @@ __global__ void __launch_bounds__(kApplyThreads) GW_APPLY_ATTR k_rgn_apply(Inges
     if constexpr (M) {  // a clear presence bit: the cell is the identity whatever it holds (a lazy
                         // fire retire, k_fire2); the loaded pane arrays are read after the run
                         // loop's first barrier
-        for (int ai = 0; ai < 2; ++ai) {
+        for (int ai = 0; ai < 2 && a.stale; ++ai) {
             const int act = ai ? act1 : act0;
             if (!(ai ? ld1 : ld0)) continue;
             long long* lc = lcell + (int64_t)ai * S;
@@ -1583,7 +1583,9 @@ __device__ __forceinline__ uint32_t k32_of(int64_t k) {
     return k == kEmptyKey ? kK32Empty : ((uint64_t)k < (uint64_t)kK32Foreign ? (uint32_t)k : kK32Foreign);
 }
 
-template <int AGG>
+// STALE: cells behind clear presence bits may hold stale values (lazy fire retires, FireArgs::
+// lazy_retire) and are staged as the identity; without it the staging is a plain copy.
+template <int AGG, bool STALE>
 __global__ void __launch_bounds__(kApplyThreads) GW_APPLY_ATTR k_rgn_apply_nar(IngestArgs a) {
     if constexpr (!cmp_agg<AGG>()) {
         return;
@@ -1741,24 +1743,30 @@ __global__ void __launch_bounds__(kApplyThreads) GW_APPLY_ATTR k_rgn_apply_nar(I
             long2* l2 = reinterpret_cast<long2*>(lcell);
             for (int w0 = threadIdx.x; w0 < tot; w0 += kNarLoadU * blockDim.x) {
                 long2 v[kNarLoadU];
+                uint32_t mb[kNarLoadU];
 #pragma unroll
                 for (int u = 0; u < kNarLoadU; ++u) {
                     const int w = w0 + u * blockDim.x;
                     v[u] = ident;
+                    mb[u] = ~0u;
                     if (w < tot && !fresh) {
                         const int d = w / per;
                         v[u] = reinterpret_cast<const long2*>(pt_cell(a.t, (sr * F + d) << l2S, p))[w - d * per];
+                        // a clear presence bit: the cell is the identity whatever it holds (a lazy fire
+                        // retire, k_fire2); one byte of mask per slot (ring <= 8), slots 2w, 2w + 1.  The
+                        // mask's LDS reads are issued here, beside the cells' loads: read where they are
+                        // used, each was a dependent LDS round trip per pair (Q7's apply 335 -> 540 us
+                        // per flush, profiles/r6/q7/)
+                        if constexpr (M && STALE) mb[u] = reinterpret_cast<const uint16_t*>(lmask)[w];
                     }
                 }
 #pragma unroll
                 for (int u = 0; u < kNarLoadU; ++u) {
                     const int w = w0 + u * blockDim.x;
                     if (w >= tot) continue;
-                    if constexpr (M) {  // a clear presence bit: the cell is the identity whatever it holds
-                        // (a lazy fire retire, k_fire2); one byte of mask per slot (ring <= 8), slots 2w, 2w + 1
-                        const uint16_t mb = reinterpret_cast<const uint16_t*>(lmask)[w];
-                        if (!((mb >> p) & 1)) v[u].x = id0;
-                        if (!((mb >> (8 + p)) & 1)) v[u].y = id0;
+                    if constexpr (M && STALE) {
+                        if (!((mb[u] >> p) & 1)) v[u].x = id0;
+                        if (!((mb[u] >> (8 + p)) & 1)) v[u].y = id0;
                     }
                     l2[w] = v[u];
                 }
@@ -2878,7 +2886,8 @@ hipError_t launch_region_flush(const IngestArgs& a, hipStream_t s, hipEvent_t e0
                            (size_t)(kApplyThreads / 64) * kApplyQ * 8;
 #define LN(A)                                                                                                   \
     lds_opt_in((const void*)k_rgn_p2<A, kFmtNar>, part_lds);                                                   \
-    lds_opt_in((const void*)k_rgn_apply_nar<A>, lds);                                                         \
+    lds_opt_in((const void*)k_rgn_apply_nar<A, true>, lds);                                                   \
+    lds_opt_in((const void*)k_rgn_apply_nar<A, false>, lds);                                                  \
     if (!a.cur_empty) {                                                                                         \
         GW_TLAUNCH(k_rgn_plan1, dim3((unsigned)a.ngroups), dim3(256), 0, s, e0, nullptr, a);                   \
         hipLaunchKernelGGL(k_rgn_plan2, dim3((unsigned)nb1), dim3(256), 0, s, a);                              \
@@ -2886,8 +2895,12 @@ hipError_t launch_region_flush(const IngestArgs& a, hipStream_t s, hipEvent_t e0
         hipLaunchKernelGGL((k_rgn_p2<A, kFmtNar>), dim3((unsigned)(a.ngroups * nb1)), dim3(kPartThreads), part_lds, \
                            s, a);                                                                               \
     }                                                                                                           \
-    GW_TLAUNCH(k_rgn_apply_nar<A>, dim3((unsigned)(a.t.nreg >> a.sr_bits)), dim3(kApplyThreads), lds, s,        \
-               a.cur_empty ? e0 : nullptr, e1, a)
+    if (a.stale)                                                                                                \
+        GW_TLAUNCH((k_rgn_apply_nar<A, true>), dim3((unsigned)(a.t.nreg >> a.sr_bits)), dim3(kApplyThreads), lds, \
+                   s, a.cur_empty ? e0 : nullptr, e1, a);                                                       \
+    else                                                                                                        \
+        GW_TLAUNCH((k_rgn_apply_nar<A, false>), dim3((unsigned)(a.t.nreg >> a.sr_bits)), dim3(kApplyThreads),     \
+                   lds, s, a.cur_empty ? e0 : nullptr, e1, a)
         GW_AGG_SWITCH(a.t.agg, LN);
 #undef LN
         return hipGetLastError();

@@ -1060,9 +1060,14 @@ struct gw_handle {
     // keep stale values behind them: 8 B per slot and position less to write per fire); the
     // positions are remembered and cleaned before a kernel that adds into cells with device
     // atomics (clean_stale).  The region apply and every reader go by the bits.
+    // Lazy retires for the sums only: MIN / MAX retire eagerly (the fire writes the identity).
+    // The apply's substitution of the identity for clear presence bits (k_rgn_apply_nar<AGG,
+    // true>) cost Q7's tumbling max 335 -> 540 us per flush for ~25 us of fire per window; the
+    // headline's sum pays ~1% of its apply for ~10% of its fire (profiles/r6/q7/).
     void lazy_retire(FireArgs& f) {
-        f.lazy_retire = tv.has_mask ? 1 : 0;
-        if (tv.has_mask) stale_pos |= f.rmask;
+        const bool lazy = tv.has_mask && (cfg.agg == GW_SUM_I64 || cfg.agg == GW_SUM_I32 || cfg.agg == GW_SUM_F64);
+        f.lazy_retire = lazy ? 1 : 0;
+        if (lazy) stale_pos |= f.rmask;
     }
     int clean_stale() {
         if (!stale_pos) return GW_OK;
@@ -1305,6 +1310,7 @@ struct gw_handle {
         a.p1_row = p1_row;
         a.p2_desc = p2_desc;
         a.p2_off = p2_off;
+        a.stale = stale_pos != 0;
         a.p2_roff = p2_roff;
         a.rbeg = eset_rbeg(eset);
         a.bk_off = a.rbeg + kPartBuckets + 1;
