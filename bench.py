@@ -74,8 +74,6 @@ def parse(argv=None):
     ap.add_argument("--exchange-stream", choices=["own", "operator"], default="own",
                     help="own: the exchange (partition, all-to-all, sends) on a stream of its own, overlapping "
                          "the operator's kernels; operator: on the operator's stream, serialised with them")
-    ap.add_argument("--exchange-priority", type=int, choices=[-1, 0], default=0,
-                    help="HIP priority of the exchange's own stream (-1 high, 0 default)")
     ap.add_argument("--exchange-ahead", type=int, choices=[1, 2], default=1,
                     help="batches the exchange finishes ahead of the ingest: 1 finishes batch b right before "
                          "its ingest (and begins b+1); 2 finishes b+1 (and begins b+2) before batch b is "
@@ -301,8 +299,7 @@ def main(argv=None):
         if args.pack != "off" and not agg.endswith("f64"):
             ex.enable_packing(size, slide, 0, with_values=agg != "count")
             ex.keep_words(args.pack == "auto")
-    xs = (torch.cuda.Stream(device=dev, priority=args.exchange_priority)
-          if ex is not None and args.exchange_stream == "own" else None)
+    xs = torch.cuda.Stream(device=dev) if ex is not None and args.exchange_stream == "own" else None
     run = Steps(op, N, keys, ts, vals, wms, nb, ex=ex, collect=args.checksum,
                 ex_stream=xs.cuda_stream if xs is not None else (op.stream() if ex is not None else None),
                 ahead=args.exchange_ahead)
