@@ -36,6 +36,9 @@ struct gw_exchange {
     ncclComm_t comm = nullptr;
     int32_t nranks = 0, rank = 0, device = 0, max_p = 128;
     bool no_regions = false;
+    // packed batches: region places by atomics, not in arrival order (k_part_regions unstable;
+    // GW_PART_STABLE=1 keeps the look-back for every batch)
+    bool stable_order = false;
     int part_turn = 0;  // status half of the next region partition  // GW_PART_REGIONS=0: the three-pass contiguous partition (A/B)
     void* scratch = nullptr;  // partition scratch (used only inside a partition launch: shared)
     int64_t scratch_bytes = 0;
@@ -200,6 +203,7 @@ int gw_exchange_create(gw_exchange** out, int32_t nranks, int32_t rank, const vo
     ex->nranks = nranks;
     ex->rank = rank;
     if (const char* e = getenv("GW_PART_REGIONS")) ex->no_regions = atoi(e) == 0;
+    if (const char* e = getenv("GW_PART_STABLE")) ex->stable_order = atoi(e) != 0;
     ex->device = device;
     ex->max_p = max_parallelism;
     auto bail = [&](int rc) { gw_exchange_destroy(ex); return rc; };
@@ -210,6 +214,8 @@ int gw_exchange_create(gw_exchange** out, int32_t nranks, int32_t rank, const vo
     const size_t words = (size_t)nranks * (2 + 2 * gw_exchange::kMsg);
     for (auto& q : ex->ps) {
         if (hipMalloc((void**)&q.d_counts, words * 8) != hipSuccess) return bail(GW_E_OOM);
+        // the unstable region partition adds into the counts (k_exchange_message zeroes them after)
+        if (hipMemset(q.d_counts, 0, words * 8) != hipSuccess) return bail(GW_E_DEVICE);
         if (hipHostMalloc((void**)&q.h_msg, (size_t)(2 * gw_exchange::kMsg * nranks) * 8, hipHostMallocDefault) !=
             hipSuccess)
             return bail(GW_E_OOM);
@@ -448,7 +454,7 @@ int gw_exchange_begin(gw_exchange* ex, int64_t n, const int64_t* d_key, const in
         EX_HIP(launch_partition_regions(n, d_key, d_key_hash, d_ts, d_value, ex->max_p, P, q.part_cap, pk, pt,
                                         d_value ? pv : nullptr, d_key_hash ? q.part_hash : nullptr,
                                         packed ? &g : nullptr, q.part_packed, q.d_counts, ex->scratch, s,
-                                        ex->part_turn, 2 * P));
+                                        ex->part_turn, 2 * P, packed && !ex->stable_order ? 1 : 0));
         ex->part_turn ^= 1;
     } else if (n > 0) {
         EX_HIP(launch_partition(n, d_key, d_key_hash, d_ts, d_value, ex->max_p, P, pk, pt, d_value ? pv : nullptr,

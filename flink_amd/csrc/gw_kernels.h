@@ -393,7 +393,7 @@ hipError_t launch_partition_regions(int64_t n, const int64_t* key, const int32_t
                                     const int64_t* val, int32_t max_p, int32_t p, int64_t cap, int64_t* key_out,
                                     int64_t* ts_out, int64_t* val_out, int32_t* hash_out, const PackGeom* pack,
                                     uint64_t* packed_out, int64_t* counts, void* scratch, hipStream_t s,
-                                    int turn = -1, int32_t nd_max = 0);
+                                    int turn = -1, int32_t nd_max = 0, int unstable = 0);
 // turn >= 0 (a caller launching repeatedly on one stream, alternating turn): scratch of
 // partition_regions_scratch_bytes(cap, nd_max), zeroed once at allocation; each launch zeroes
 // the half the next one uses (no memset per launch).  turn < 0: a memset of this launch's words.
@@ -427,7 +427,8 @@ hipError_t launch_khmap_insert(const KeyHashMap& m, int64_t n, const int64_t* ke
 hipError_t launch_fill64(int64_t* p, int64_t n, int64_t v, hipStream_t s);
 // keyBy exchange message per peer q: msg[4q..4q+3] = (records, wm, cols, packed records);
 // packed: counts holds 2 buckets per peer (packed, other)
-hipError_t launch_exchange_message(const int64_t* counts, int32_t p, int64_t wm, int64_t cols, int packed,
+// (zeroes the counts it read: the unstable region partition adds into them)
+hipError_t launch_exchange_message(int64_t* counts, int32_t p, int64_t wm, int64_t cols, int packed,
                                    int64_t* msg, hipStream_t s);
 // Every entry of `from` into the empty map `to`.
 hipError_t launch_khmap_rehash(const KeyHashMap& from, const KeyHashMap& to, hipStream_t s);

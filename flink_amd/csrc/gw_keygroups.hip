@@ -227,6 +227,14 @@ __global__ void __launch_bounds__(256) k_part_scatter(int64_t n, const int64_t* 
 // look-back, as the grouping sort's passes do, gw_sort.hip), and the last tile writes the
 // totals.  status: [ntiles][nd] words, zeroed before the launch.  Costs P * cap records of
 // memory per buffer -- the exchange uses it up to kPartRegionMaxOwners owners.
+// unstable: no look-back -- each tile takes its place in a region with one device atomic on
+// that region's total in counts[] (zeroed before the launch), so tiles land in the order they
+// get there and a region's records are not in arrival order.  The exchange uses it only for
+// packed batches, whose handles (integer sums, counts, min, max) do not see per-key arrival
+// order (the packed words already arrive behind the other records); the look-back walked
+// hundreds of earlier tiles while a whole grid of tiles published at once (round 6: 130 us per
+// 10M records alone, profiles/r6/exchange/unstable/).
+
 constexpr uint64_t kPrLocal = 1ull << 62, kPrIncl = 1ull << 63, kPrMask = kPrLocal - 1;
 
 __device__ __forceinline__ uint64_t part_look_back(const uint64_t* status, int64_t t, int nd, int d) {
@@ -253,7 +261,7 @@ __global__ void __launch_bounds__(256) k_part_regions(int64_t n, const int64_t* 
                                                       uint32_t* tile_ctr, int64_t ntiles, int64_t* key_out,
                                                       int64_t* ts_out, int64_t* val_out, int32_t* hash_out,
                                                       uint64_t* packed_out, int64_t* counts, uint64_t* zero_next,
-                                                      int64_t zero_words) {
+                                                      int64_t zero_words, int unstable) {
     extern __shared__ int64_t part_lds[];
     __shared__ int64_t s_tile;
     const int32_t nd = g.enabled ? 2 * p_owners : p_owners;
@@ -302,6 +310,12 @@ __global__ void __launch_bounds__(256) k_part_regions(int64_t n, const int64_t* 
             const uint32_t c = cnt[e * nd + d];
             cnt[e * nd + d] = run;
             run += c;
+        }
+        if (unstable) {  // a tile's place in each region by one device atomic on the region's total
+            base[d] = run ? (int64_t)atomicAdd(reinterpret_cast<unsigned long long*>(counts) + d,
+                                               (unsigned long long)run)
+                          : 0;
+            continue;
         }
         uint64_t* st = status + tile * nd + d;
         uint64_t excl = 0;
@@ -445,7 +459,9 @@ hipError_t launch_fill64(int64_t* p, int64_t n, int64_t v, hipStream_t s) {
     return hipGetLastError();
 }
 
-__global__ void __launch_bounds__(256) k_exchange_message(const int64_t* counts, int32_t p, int64_t wm, int64_t cols,
+// counts are zeroed once read: the unstable region partition of the next batch on this set
+// adds into them (each thread zeroes only the entries it read).
+__global__ void __launch_bounds__(256) k_exchange_message(int64_t* counts, int32_t p, int64_t wm, int64_t cols,
                                                           int packed, int64_t* msg) {
     for (int q = threadIdx.x; q < p; q += blockDim.x) {
         const int64_t pk = packed ? counts[2 * q] : 0;
@@ -453,10 +469,16 @@ __global__ void __launch_bounds__(256) k_exchange_message(const int64_t* counts,
         msg[4 * q + 1] = wm;
         msg[4 * q + 2] = cols;
         msg[4 * q + 3] = pk;
+        if (packed) {
+            counts[2 * q] = 0;
+            counts[2 * q + 1] = 0;
+        } else {
+            counts[q] = 0;
+        }
     }
 }
 
-hipError_t launch_exchange_message(const int64_t* counts, int32_t p, int64_t wm, int64_t cols, int packed,
+hipError_t launch_exchange_message(int64_t* counts, int32_t p, int64_t wm, int64_t cols, int packed,
                                    int64_t* msg, hipStream_t s) {
     hipLaunchKernelGGL(k_exchange_message, dim3(1), dim3(256), 0, s, counts, p, wm, cols, packed, msg);
     return hipGetLastError();
@@ -528,7 +550,7 @@ hipError_t launch_partition_regions(int64_t n, const int64_t* key, const int32_t
                                     const int64_t* val, int32_t max_p, int32_t p, int64_t cap, int64_t* key_out,
                                     int64_t* ts_out, int64_t* val_out, int32_t* hash_out, const PackGeom* pack,
                                     uint64_t* packed_out, int64_t* counts, void* scratch, hipStream_t s, int turn,
-                                    int32_t nd_max) {
+                                    int32_t nd_max, int unstable) {
     PackGeom g{};
     if (pack && pack->enabled) {
         if (key_hash || !packed_out || pack->pane <= 0) return hipErrorInvalidValue;
@@ -554,7 +576,7 @@ hipError_t launch_partition_regions(int64_t n, const int64_t* key, const int32_t
     const size_t lds = (size_t)nd * 8 + (size_t)kPartItems * 4 * nd * 4;
     hipLaunchKernelGGL(k_part_regions, dim3((unsigned)nb), dim3(256), lds, s, n, key, key_hash, ts, val, max_p, p,
                        g, cap, status, ctr, nb, key_out, ts_out, val_out, key_hash ? hash_out : nullptr, packed_out,
-                       counts, zero_next, zero_words);
+                       counts, zero_next, zero_words, unstable);
     return hipGetLastError();
 }
 
