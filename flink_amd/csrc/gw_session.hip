@@ -1241,10 +1241,12 @@ static int begin_launch(SessionState* s, std::string& err) {
     return rc;
 }
 
-// Zero a device status word without a host round trip (host view updated alike).
+// Zero a device status word without a host round trip (host view updated alike): one
+// one-wave kernel (k_status_set, ~1 us) rather than a runtime fill (~5 us and more host time:
+// ~14 per 10M-record sessions step, profiles/r6/configs/kernel_stats_sessions.csv).
 static int zero_word_async(SessionState* s, size_t off, std::string& err) {
     *reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(s->h_st) + off) = 0;
-    SCHECK(hipMemsetAsync(reinterpret_cast<char*>(s->d_st) + off, 0, 8, s->stream));
+    SCHECK(launch_status_set(s->d_st, (int)(off / 8), 0ull, -1, s->stream));
     return GW_OK;
 }
 
