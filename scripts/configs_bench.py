@@ -114,11 +114,12 @@ def run(name, args, dev):
     def step(b):
         nonlocal rows, op_events
         lo, hi = b * nb, (b + 1) * nb
-        if ysb:  # filter(view) -> project -> join(ad -> campaign), on a torch stream
+        if ysb:  # filter(view) -> project -> join(ad -> campaign), on a torch stream: the view
+            # events' indices once (one stream compaction and its host sync), then the gathers
             with torch.cuda.stream(side):
-                view = etype[lo:hi] == 0
-                k = ad_campaign[ad[lo:hi][view]]
-                t = ts[lo:hi][view]
+                idx = torch.nonzero(etype[lo:hi] == 0).squeeze(1)
+                k = ad_campaign[ad[lo:hi][idx]]
+                t = ts[lo:hi][idx]
             n = k.numel()
             side.synchronize()
             N.check(N.lib().gw_ingest_device(op.handle, n, k.data_ptr(), None, t.data_ptr(), None, op.stream()),
