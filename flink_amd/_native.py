@@ -56,6 +56,7 @@ EXPORTS = [
     "gw_ingest_payload", "gw_ingest_payload_device", "gw_drain_payload",
     "gw_snapshot_keys", "gw_snapshot_remap_keys", "gw_snapshot_payloads", "gw_snapshot_remap_payloads",
     "gw_pack_geom_init", "gw_pack_records", "gw_unpack_records", "gw_partition_packed_device", "gw_partition_regions_device", "gw_unpack_device",
+    "gw_select_lookup_device",
     "gw_exchange_enable_packing", "gw_exchange_last_packed", "gw_exchange_plan_packed",
     "gw_exchange_set_unpack", "gw_exchange_last_words", "gw_ingest_packed_device",
 ]
@@ -217,6 +218,7 @@ def lib() -> ctypes.CDLL:
         "gw_partition_regions_device": (c_int, [i64, p, p, p, i32, i32, ctypes.POINTER(GwPackGeom), i64, p, p, p,
                                                 p, p, p, p]),
         "gw_unpack_device": (c_int, [i64, p, ctypes.POINTER(GwPackGeom), p, p, p, p]),
+        "gw_select_lookup_device": (c_int, [i64, p, i64, p, p, i64, p, p, p, ctypes.POINTER(ctypes.c_int64), p]),
         "gw_exchange_enable_packing": (c_int, [p, i64, i64, i64, i32]),
         "gw_exchange_last_packed": (i64, [p]),
         "gw_exchange_plan_packed": (c_int, [i32, p, p, p, p, p, p, P64, P64]),

@@ -17,7 +17,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "libgpuwin.so")
 OBJDIR = os.path.join(HERE, "_build")
-SOURCES = ["gw_pane.hip", "gw_keygroups.hip", "gw_sort.hip", "gw_session.hip", "gw_netbuf.hip", "gw_first.hip", "gw_runtime.cpp",
+SOURCES = ["gw_pane.hip", "gw_keygroups.hip", "gw_sort.hip", "gw_session.hip", "gw_netbuf.hip", "gw_first.hip", "gw_select.hip", "gw_runtime.cpp",
            "gw_exchange.cpp"]
 ROCM_LIB = os.environ.get("ROCM_PATH", "/opt/rocm") + "/lib"
 ARCH = os.environ.get("GW_OFFLOAD_ARCH", "gfx950")

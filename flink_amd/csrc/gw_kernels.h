@@ -406,6 +406,11 @@ hipError_t launch_partition(int64_t n, const int64_t* key, const int32_t* key_ha
                             int64_t* ts_out, int64_t* val_out, int64_t* counts, void* scratch,
                             hipStream_t s, int32_t* hash_out = nullptr, const PackGeom* pack = nullptr,
                             uint64_t* packed_out = nullptr);
+// gw_select.hip: stable select (sel == want) + dictionary lookup (gw_select_lookup_device)
+hipError_t launch_select_lookup(int64_t n, const int64_t* sel, int64_t want, const int64_t* idx, const int64_t* dict,
+                                int64_t dict_n, const int64_t* ts, int64_t* key_out, int64_t* ts_out, void* scratch,
+                                hipStream_t s);
+size_t select_lookup_scratch_bytes(int64_t n);
 hipError_t launch_unpack(int64_t n, const uint64_t* w, const PackGeom& g, int64_t* key, int64_t* ts, int64_t* val,
                          hipStream_t s);
 

@@ -22,6 +22,7 @@
 #include <string>
 #include <tuple>
 #include <vector>
+#include <mutex>
 
 #include "gw_first.h"
 #include "gw_kernels.h"
@@ -5169,6 +5170,44 @@ int gw_partition_regions_device(int64_t n, const int64_t* d_key, const int64_t* 
                                             d_value_out, nullptr, packed ? g : nullptr, d_packed_out, d_counts,
                                             d_scratch, s);
     if (e != hipSuccess) { g_create_error = hipGetErrorString(e); return GW_E_DEVICE; }
+    return GW_OK;
+}
+
+int gw_select_lookup_device(int64_t n, const int64_t* d_sel, int64_t sel_value, const int64_t* d_idx,
+                            const int64_t* d_dict, int64_t dict_n, const int64_t* d_ts, int64_t* d_key_out,
+                            int64_t* d_ts_out, int64_t* n_out, void* stream) {
+    if (!n_out || n < 0 || dict_n < 0 || (n > 0 && (!d_sel || !d_idx || !d_ts || !d_key_out || !d_ts_out)) ||
+        (dict_n > 0 && !d_dict))
+        return GW_E_INVALID;
+    *n_out = 0;
+    if (n == 0) return GW_OK;
+    // scratch per device, grown as needed (every call waits for its launches before returning,
+    // so a later call may free it)
+    static std::mutex mu;
+    static void* scr[64] = {};
+    static size_t cap[64] = {};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return GW_E_DEVICE;
+    const size_t need = select_lookup_scratch_bytes(n);
+    std::lock_guard<std::mutex> lock(mu);
+    if (need > cap[dev]) {
+        if (scr[dev]) hipFree(scr[dev]);
+        scr[dev] = nullptr;
+        cap[dev] = 0;
+        if (hipMalloc(&scr[dev], need) != hipSuccess) { g_create_error = "gw_select_lookup_device: scratch"; return GW_E_OOM; }
+        cap[dev] = need;
+    }
+    hipStream_t s = (hipStream_t)stream;
+    hipError_t e = launch_select_lookup(n, d_sel, sel_value, d_idx, d_dict, dict_n, d_ts, d_key_out, d_ts_out, scr[dev], s);
+    // the total and the range flag sit behind the tile offsets (gw_select.hip)
+    const int64_t ntiles = (n + 4095) / 4096;
+    const char* tail = (const char*)scr[dev] + ((ntiles * 4 + 15) / 16) * 16 + (size_t)ntiles * 8;
+    int64_t hv[2] = {0, 0};
+    if (e == hipSuccess) e = hipMemcpyAsync(hv, tail, 16, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e != hipSuccess) { g_create_error = hipGetErrorString(e); return GW_E_DEVICE; }
+    if ((int32_t)hv[1]) { g_create_error = "gw_select_lookup_device: index outside the dictionary"; return GW_E_RANGE; }
+    *n_out = hv[0];
     return GW_OK;
 }
 

@@ -235,6 +235,18 @@ def _ptr(a: Optional[np.ndarray]):
     return None if a is None else ctypes.c_void_p(a.ctypes.data)
 
 
+def select_lookup_device(sel, sel_value: int, idx, dictionary, ts, key_out, ts_out, stream) -> int:
+    """gw_select_lookup_device over device tensors (int64): the records with sel == sel_value,
+    in arrival order, as (dictionary[idx], ts) into key_out / ts_out; returns their number.  The
+    filter + projection + static-table join a job chains ahead of keyBy (YSB's view filter
+    and ad -> campaign join), fused on the device."""
+    n_out = ctypes.c_int64(0)
+    N.check(N.lib().gw_select_lookup_device(sel.numel(), sel.data_ptr(), int(sel_value), idx.data_ptr(),
+                                             dictionary.data_ptr(), dictionary.numel(), ts.data_ptr(),
+                                             key_out.data_ptr(), ts_out.data_ptr(), ctypes.byref(n_out), stream))
+    return int(n_out.value)
+
+
 # ------------------------------------------------------------------------ operator
 class GpuWindowOperator:
     """Keyed event-time window operator on one MI355X (one Flink subtask).

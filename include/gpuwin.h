@@ -477,6 +477,15 @@ int  gw_partition_regions_device(int64_t n, const int64_t* d_key, const int64_t*
                                  int64_t* d_value_out, int64_t* d_counts, void* d_scratch, void* stream);
 int  gw_unpack_device(int64_t n, const uint64_t* d_words, const gw_pack_geom* g, int64_t* d_key, int64_t* d_ts,
                       int64_t* d_value, void* stream);
+/* The stages a job chains ahead of keyBy on simple records, fused on the device (no Flink-core
+ * interface: the Yahoo Streaming Benchmark's FilterFunction(event_type == view) + projection +
+ * join against a static ad -> campaign table, AdvertisingTopologyNative): of the n records
+ * whose d_sel[i] == sel_value, in arrival order, d_key_out[j] = d_dict[d_idx[i]] and
+ * d_ts_out[j] = d_ts[i]; *n_out = their number (the call waits for it on `stream`).  An index
+ * outside [0, dict_n) is GW_E_RANGE.  Outputs hold n records at most. */
+int  gw_select_lookup_device(int64_t n, const int64_t* d_sel, int64_t sel_value, const int64_t* d_idx,
+                             const int64_t* d_dict, int64_t dict_n, const int64_t* d_ts, int64_t* d_key_out,
+                             int64_t* d_ts_out, int64_t* n_out, void* stream);
 /* gw_ingest_device for a batch of n_other column records followed by n_words packed words
  * (the receive side of the packed exchange: what StreamTaskNetworkInput deserializes before
  * WindowOperator.processElement, WindowOperator.java:293-447, sees record by record)

@@ -110,12 +110,22 @@ def run(name, args, dev):
     if ysb:
         ad, etype, ad_campaign = keys
         side = torch.cuda.Stream(device=dev)
+        ysb_k = torch.empty(nb, dtype=torch.int64, device=dev)  # the selected batch (device select)
+        ysb_t = torch.empty(nb, dtype=torch.int64, device=dev)
 
     def step(b):
         nonlocal rows, op_events
         lo, hi = b * nb, (b + 1) * nb
-        if ysb:  # filter(view) -> project -> join(ad -> campaign), on a torch stream: the view
-            # events' indices once (one stream compaction and its host sync), then the gathers
+        if ysb and args.ysb_select == "device":
+            # filter(view) -> project -> join(ad -> campaign) fused on the device, on the
+            # operator's stream (gw_select_lookup_device: one read of the columns, the view
+            # events written in arrival order; the call returns their number)
+            n = W.select_lookup_device(etype[lo:hi], 0, ad[lo:hi], ad_campaign, ts[lo:hi], ysb_k, ysb_t, op.stream())
+            N.check(N.lib().gw_ingest_device(op.handle, n, ysb_k.data_ptr(), None, ysb_t.data_ptr(), None,
+                                             op.stream()), op.handle)
+            op_events += n
+        elif ysb:  # the same with torch on a stream of its own: the view events' indices once (one
+            # stream compaction and its host sync), then the gathers
             with torch.cuda.stream(side):
                 idx = torch.nonzero(etype[lo:hi] == 0).squeeze(1)
                 k = ad_campaign[ad[lo:hi][idx]]
@@ -166,7 +176,8 @@ def run(name, args, dev):
            "rows_fired": rows, "live_keys": stats.get("live_keys"), "data": "synthetic, generated in HBM",
            "roofline": roof}
     if ysb:
-        out["pipeline"] = "filter(event_type == view) + join(ad_id -> campaign_id) on the GPU, then the operator"
+        out["pipeline"] = ("filter(event_type == view) + join(ad_id -> campaign_id) on the GPU ("
+                           + ("gw_select_lookup_device" if args.ysb_select == "device" else "torch") + "), then the operator")
     if first:
         out["note"] = ("rows carry the highest bid's payload (one MAX pane operator + 4-column log + per-fire probe)"
                        if name == "q7_maxby" else
@@ -196,7 +207,7 @@ BOUND_NOTE = {
     "q7": "region pipeline as in the headline (pass 1 + flush), fire at each 10-s window end",
     "q7_first": "two pane operators + the payload log and join",
     "q7_maxby": "MAX pane operator + 4-column log + per-fire probe (k_by_scan)",
-    "ysb": "the torch filter / join ahead of the operator (operator kernels are a small share of the step)",
+    "ysb": "the filter / join ahead of the operator (gw_select_lookup_device) and the operator's few-key pre-aggregation (k_ingest_preagg)",
     "wordcount": "count-window replay (k_cnt_apply) over a Zipf vocabulary: hot keys serialise",
 }
 
@@ -290,6 +301,8 @@ def cpu_baseline(kw, agg, keys, ts, vals, wms, blen, seconds, few_keys=False):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--only", default="wordcount,ysb,q7,sessions")
+    ap.add_argument("--ysb-select", choices=["device", "torch"], default="device",
+                    help="YSB's filter + ad -> campaign join: gw_select_lookup_device, or torch ops on a side stream")
     ap.add_argument("--steps", type=int, default=0,
                     help="timed steps (0: per config, long enough that windows / sessions fire: "
                          "wordcount 10, ysb and q7 60 (12 s of event time), sessions 100 (20 s))")
