@@ -33,8 +33,10 @@ size_t fe_by_scratch_bytes(int64_t n);
 // ts, field); records below restored_end are restored elements of the window starting at their
 // ts.  o_seq / o_pay (either may be null) get the sequence and its payload; *d_bad |= 2 when a
 // row has no element in the log.
+// is_max: res is the window's MAX (maxBy), else its MIN (minBy): lets the scan skip records
+// that cannot equal any row of their bucket.
 hipError_t fe_by_select(int64_t n, const int64_t* key, const int64_t* start, const int64_t* res, const int64_t* log,
                         int64_t log_cap, int64_t log_base, int64_t log_end, int64_t restored_end, int64_t offset,
-                        int64_t slide, int64_t size, bool last, bool f64, int64_t* o_seq, int64_t* o_pay,
+                        int64_t slide, int64_t size, bool last, bool f64, bool is_max, int64_t* o_seq, int64_t* o_pay,
                         void* scratch, size_t scratch_bytes, int32_t* d_bad, hipStream_t s);
 }  // namespace gw

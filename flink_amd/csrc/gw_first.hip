@@ -262,21 +262,48 @@ __device__ __forceinline__ bool by_equal(int64_t a, int64_t b, bool f64) {
     return (na ? qn : (uint64_t)a) == (nb ? qn : (uint64_t)b);
 }
 
-__global__ void k_by_km_init(int64_t* km) {
-    if (threadIdx.x == 0) { km[0] = INT64_MAX; km[1] = INT64_MIN; }
+__global__ void k_by_km_init(int64_t* km, int64_t* bound, int64_t nbk, int64_t init) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) { km[0] = INT64_MAX; km[1] = INT64_MIN; }
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < nbk; i += (int64_t)gridDim.x * blockDim.x)
+        bound[i] = init;
+}
+
+// A field as an int64 in Double.compare / Long.compareTo order, equal exactly when by_equal says
+// so (NaNs one value, -0.0 below 0.0).
+__device__ __forceinline__ int64_t by_ord(int64_t v, bool f64) {
+    if (!f64) return v;
+    if (((uint64_t)v & 0x7fffffffffffffffull) > 0x7ff0000000000000ull) v = 0x7ff8000000000000ll;
+    return v >= 0 ? v : v ^ 0x7fffffffffffffffll;
+}
+
+// floor((a) / b) for b > 0 by a double estimate corrected by one step each way (exact while
+// |a| < 2^52; the integer division beyond): the scan runs it twice per log record.
+__device__ __forceinline__ int64_t by_fdiv(int64_t a, int64_t b) {
+    if (a > (1ll << 52) || a < -(1ll << 52)) return by_floor_div(a, b);
+    int64_t q = (int64_t)floor((double)a / (double)b);
+    if (q * b > a) --q;
+    else if ((q + 1) * b <= a) ++q;
+    return q;
 }
 
 // Rows into the table (one slot per row, duplicates included); sel[i] = the neutral sequence;
-// km = [min, max] window index over the rows.
-__global__ void k_by_build(int64_t n, const int64_t* key, const int64_t* start, int32_t* table, uint64_t mask,
-                           int64_t* sel, int64_t init, int64_t offset, int64_t slide, int64_t* km) {
+// km = [min, max] window index over the rows; bound[bucket] = the least (is_max) / greatest
+// field order of the rows in the bucket (the top bits of the row's hash): a log record whose
+// field lies beyond its bucket's bound equals no row there and skips the probe.
+__global__ void k_by_build(int64_t n, const int64_t* key, const int64_t* start, const int64_t* res, int32_t* table,
+                           uint64_t mask, int64_t* sel, int64_t init, int64_t offset, int64_t slide, int64_t* km,
+                           int64_t* bound, int bk_shift, int is_max, int f64) {
     int64_t lo = INT64_MAX, hi = INT64_MIN;
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
         sel[i] = init;
         const int64_t k = by_floor_div(start[i] - offset, slide);
         lo = min(lo, k);
         hi = max(hi, k);
-        uint64_t h = by_hash(key[i], start[i]) & mask;
+        const uint64_t hh = by_hash(key[i], start[i]);
+        const int64_t o = by_ord(res[i], f64 != 0);
+        if (is_max) atomicMin((long long*)&bound[hh >> bk_shift], (long long)o);
+        else atomicMax((long long*)&bound[hh >> bk_shift], (long long)o);
+        uint64_t h = hh & mask;
         while (atomicCAS(&table[h], -1, (int32_t)i) != -1) h = (h + 1) & mask;
     }
     for (int o = 32; o > 0; o >>= 1) {
@@ -297,23 +324,33 @@ struct ByScanArgs {
     const int64_t *key, *start, *res;
     int64_t* sel;
     const int64_t* km;
+    const int64_t* bound;
+    int bk_shift, is_max;
     int64_t offset, slide, size;
     int last, f64;
 };
 
 __global__ void __launch_bounds__(256) k_by_scan(ByScanArgs a) {
     const int64_t k_lo = a.km[0], k_hi = a.km[1];
-    for (int64_t q = a.lo + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; q < a.hi;
-         q += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t at = q % a.cap;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    int64_t q = a.lo + blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    int64_t at = q % a.cap;  // the ring position, advanced with q (no division per record)
+    const int64_t step = stride % a.cap;
+    for (; q < a.hi; q += stride) {
         const int64_t key = a.log[a.cap + at], ts = a.log[2 * a.cap + at], v = a.log[3 * a.cap + at];
-        const int64_t kt = by_floor_div(ts - a.offset, a.slide);
-        int64_t k0 = q < a.restored_end ? kt : by_floor_div(ts - a.offset - a.size, a.slide) + 1;
+        at += step;
+        if (at >= a.cap) at -= a.cap;
+        const int64_t vo = by_ord(v, a.f64 != 0);
+        const int64_t kt = by_fdiv(ts - a.offset, a.slide);
+        int64_t k0 = q < a.restored_end ? kt : by_fdiv(ts - a.offset - a.size, a.slide) + 1;
         const int64_t k1 = min(kt, k_hi);
         k0 = max(k0, k_lo);
         for (int64_t k = k0; k <= k1; ++k) {
             const int64_t s = a.offset + k * a.slide;
-            uint64_t h = by_hash(key, s) & a.mask;
+            const uint64_t hh = by_hash(key, s);
+            const int64_t bd = a.bound[hh >> a.bk_shift];
+            if (a.is_max ? vo < bd : vo > bd) continue;  // below every row's MAX in the bucket (above every MIN)
+            uint64_t h = hh & a.mask;
             for (int32_t r; (r = a.table[h]) >= 0; h = (h + 1) & a.mask) {
                 if (a.key[r] != key || a.start[r] != s || !by_equal(v, a.res[r], a.f64)) continue;
                 if (a.last) atomicMax((long long*)&a.sel[r], (long long)q);
@@ -336,16 +373,23 @@ __global__ void k_by_emit(int64_t n, const int64_t* sel, const int64_t* log, int
     }
 }
 
+// Buckets of the scan's filter: ~16 rows each (a power of two, the top bits of the row hash).
+static int by_bucket_bits(int64_t n) {
+    int b = 6;
+    while (b < 30 && ((int64_t)1 << b) * 16 < n) ++b;
+    return b;
+}
+
 size_t fe_by_scratch_bytes(int64_t n) {
     uint64_t tcap = 1024;
     while (tcap < (uint64_t)(2 * n)) tcap <<= 1;
-    return tcap * 4 + (size_t)std::max<int64_t>(n, 1) * 8 + 256;
+    return tcap * 4 + (size_t)std::max<int64_t>(n, 1) * 8 + 256 + ((size_t)8 << by_bucket_bits(n));
 }
 
 hipError_t fe_by_select(int64_t n, const int64_t* key, const int64_t* start, const int64_t* res, const int64_t* log,
                         int64_t log_cap, int64_t log_base, int64_t log_end, int64_t restored_end, int64_t offset,
-                        int64_t slide, int64_t size, bool last, bool f64, int64_t* o_seq, int64_t* o_pay,
-                        void* scratch, size_t scratch_bytes, int32_t* d_bad, hipStream_t s) {
+                        int64_t slide, int64_t size, bool last, bool f64, bool is_max, int64_t* o_seq,
+                        int64_t* o_pay, void* scratch, size_t scratch_bytes, int32_t* d_bad, hipStream_t s) {
     if (n <= 0) return hipSuccess;
     if (scratch_bytes < fe_by_scratch_bytes(n) || slide <= 0) return hipErrorInvalidValue;
     uint64_t tcap = 1024;
@@ -354,15 +398,21 @@ hipError_t fe_by_select(int64_t n, const int64_t* key, const int64_t* start, con
     int64_t* km = (int64_t*)p;
     int64_t* sel = (int64_t*)(p + 256);
     int32_t* table = (int32_t*)(p + 256 + (size_t)n * 8);
+    const int bbits = by_bucket_bits(n);
+    const int64_t nbk = (int64_t)1 << bbits;
+    int64_t* bound = (int64_t*)(p + 256 + (size_t)n * 8 + tcap * 4);
     hipError_t e = hipMemsetAsync(table, 0xff, tcap * 4, s);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_by_km_init, dim3(1), dim3(64), 0, s, km);
-    hipLaunchKernelGGL(k_by_build, dim3(grid_n(n)), dim3(256), 0, s, n, key, start, table, tcap - 1, sel,
-                       last ? INT64_MIN : INT64_MAX, offset, slide, km);
+    hipLaunchKernelGGL(k_by_km_init, dim3(grid_n(nbk)), dim3(256), 0, s, km, bound, nbk,
+                       is_max ? INT64_MAX : INT64_MIN);
+    hipLaunchKernelGGL(k_by_build, dim3(grid_n(n)), dim3(256), 0, s, n, key, start, res, table, tcap - 1, sel,
+                       last ? INT64_MIN : INT64_MAX, offset, slide, km, bound, 64 - bbits, is_max ? 1 : 0,
+                       f64 ? 1 : 0);
     if (log_end > log_base) {
         ByScanArgs a{};
         a.log = log; a.cap = log_cap; a.lo = log_base; a.hi = log_end; a.restored_end = restored_end;
         a.table = table; a.mask = tcap - 1;
+        a.bound = bound; a.bk_shift = 64 - bbits; a.is_max = is_max ? 1 : 0;
         a.key = key; a.start = start; a.res = res; a.sel = sel; a.km = km;
         a.offset = offset; a.slide = slide; a.size = size;
         a.last = last; a.f64 = f64;

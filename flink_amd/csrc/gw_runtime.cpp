@@ -3261,7 +3261,8 @@ static int by_select(gw_handle* h, int64_t n, const int64_t* key, const int64_t*
     hipError_t e = hipMemsetAsync(h->fe_bad, 0, 4, h->stream);
     if (e == hipSuccess)
         e = fe_by_select(n, key, start, res, h->fe_log, h->fe_log_cap, h->fe_log_base, h->fe_seq, h->fe_restored_end,
-                         h->cfg.offset, slide, h->cfg.size, h->fe_by_last, f64, o_seq, o_pay, h->fe_scratch,
+                         h->cfg.offset, slide, h->cfg.size, h->fe_by_last, f64,
+                         h->cfg.agg == GW_MAX_I64 || h->cfg.agg == GW_MAX_F64, o_seq, o_pay, h->fe_scratch,
                          h->fe_scratch_bytes, h->fe_bad, h->stream);
     int32_t bad = 0;
     if (e == hipSuccess) e = hipMemcpyAsync(&bad, h->fe_bad, 4, hipMemcpyDeviceToHost, h->stream);
