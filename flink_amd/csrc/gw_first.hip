@@ -109,12 +109,6 @@ __global__ void k_fe_gather_log(const int64_t* log, int64_t cap, const int64_t* 
         out[i] = log[seq[i] % cap];
 }
 
-// Copy the live log [base, end) from a ring of ocap words into a ring of ncap words.
-__global__ void k_fe_recopy(const int64_t* o, int64_t ocap, int64_t* d, int64_t ncap, int64_t base, int64_t end) {
-    for (int64_t q = base + blockIdx.x * (int64_t)blockDim.x + threadIdx.x; q < end; q += (int64_t)gridDim.x * blockDim.x)
-        d[q % ncap] = o[q % ocap];
-}
-
 static unsigned grid_n(int64_t n) {
     int64_t g = (n + 255) / 256;
     return (unsigned)std::max<int64_t>(1, std::min<int64_t>(g, 4096));
@@ -215,9 +209,17 @@ hipError_t fe_max_ts(const int64_t* ts, int64_t n, int64_t* out, hipStream_t s) 
 
 hipError_t fe_log_regrow(const int64_t* o, int64_t ocap, int64_t* d, int64_t ncap, int64_t base, int64_t end,
                          hipStream_t s) {
-    if (end <= base) return hipSuccess;
-    hipLaunchKernelGGL(k_fe_recopy, dim3(grid_n(end - base)), dim3(256), 0, s, o, ocap, d, ncap, base, end);
-    return hipGetLastError();
+    // the live range as the few runs that are contiguous in both rings (device-to-device copies;
+    // the element-wise k_fe_recopy did two 64-bit modulos per word: ~440 us per column of a
+    // growing maxBy log, profiles/r6/maxby/)
+    for (int64_t q = base; q < end;) {
+        const int64_t oa = q % ocap, na = q % ncap;
+        const int64_t len = std::min(end - q, std::min(ocap - oa, ncap - na));
+        const hipError_t e = hipMemcpyAsync(d + na, o + oa, (size_t)len * 8, hipMemcpyDeviceToDevice, s);
+        if (e != hipSuccess) return e;
+        q += len;
+    }
+    return hipSuccess;
 }
 
 hipError_t fe_log_append(int64_t* log, int64_t cap, int64_t pos, const int64_t* src, int64_t n, hipStream_t s) {
