@@ -573,9 +573,11 @@ __device__ __forceinline__ void block_scan2(const uint32_t* cnt, uint32_t* pre, 
 // pre[n] = total).  Runs of one bucket over a tile group are of similar length, so a guess
 // proportional to e is usually right or one off: a short walk from it instead of a
 // dependent binary search (7 LDS round trips at 112 runs).
+// (The guess in single precision: the walk corrects any rounding, and a 64-bit integer
+// division per record was ~100 VALU instructions.)
 __device__ __forceinline__ int run_near(const uint32_t* pre, int n, uint32_t e) {
     const uint32_t tot = pre[n];
-    int i = tot ? (int)min((uint64_t)(n - 1), (uint64_t)e * (uint64_t)n / tot) : 0;
+    int i = tot ? min(n - 1, (int)((float)e * ((float)n / (float)tot))) : 0;
     while (i > 0 && pre[i] > e) --i;
     while (i + 1 < n && pre[i + 1] <= e) ++i;
     return i;
