@@ -1665,10 +1665,10 @@ __global__ void __launch_bounds__(kApplyThreads) GW_APPLY_ATTR k_rgn_apply_nar(I
                 const int w = w0 + u * blockDim.x;
                 v[u] = long2{0, 0};
                 if (w < nk2) {
-                    const int d = w / (S / 2), j = w - d * (S / 2);
+                    const int d = w >> (l2S - 1), j = w & (S / 2 - 1);
                     v[u] = reinterpret_cast<const long2*>(pt_region(a.t, sr * F + d))[j];
                 } else if (w < tot) {
-                    const int wm_ = w - nk2, d = wm_ / (S / 16), j = wm_ - d * (S / 16);
+                    const int wm_ = w - nk2, d = wm_ >> (l2S - 4), j = wm_ & (S / 16 - 1);
                     v[u] = reinterpret_cast<const long2*>(pt_mask_base(a.t, sr * F + d))[j];
                 }
             }
@@ -1741,7 +1741,7 @@ __global__ void __launch_bounds__(kApplyThreads) GW_APPLY_ATTR k_rgn_apply_nar(I
         __syncthreads();  // the previous position's write-back has read the cells
         {  // this position's pane (an untouched one holds identities)
             const bool fresh = (a.ring_fresh >> p) & 1;
-            const int per = S * W / 2, tot = FS * W / 2;
+            const int per = S * W / 2, lper = l2S - 1 + (W == 2), tot = FS * W / 2;
             long2* l2 = reinterpret_cast<long2*>(lcell);
             for (int w0 = threadIdx.x; w0 < tot; w0 += kNarLoadU * blockDim.x) {
                 long2 v[kNarLoadU];
@@ -1752,7 +1752,7 @@ __global__ void __launch_bounds__(kApplyThreads) GW_APPLY_ATTR k_rgn_apply_nar(I
                     v[u] = ident;
                     mb[u] = ~0u;
                     if (w < tot && !fresh) {
-                        const int d = w / per;
+                        const int d = w >> lper;
                         v[u] = reinterpret_cast<const long2*>(pt_cell(a.t, (sr * F + d) << l2S, p))[w - d * per];
                         // a clear presence bit: the cell is the identity whatever it holds (a lazy fire
                         // retire, k_fire2); one byte of mask per slot (ring <= 8), slots 2w, 2w + 1.  The
@@ -1916,10 +1916,10 @@ __global__ void __launch_bounds__(kApplyThreads) GW_APPLY_ATTR k_rgn_apply_nar(I
         }
         __syncthreads();
         {  // write back this position's pane
-            const int per = S * W / 2, tot = FS * W / 2;
+            const int per = S * W / 2, lper = l2S - 1 + (W == 2), tot = FS * W / 2;
             const long2* l2 = reinterpret_cast<const long2*>(lcell);
             for (int w = threadIdx.x; w < tot; w += blockDim.x) {
-                const int d = w / per;
+                const int d = w >> lper;
                 reinterpret_cast<long2*>(pt_cell(a.t, (sr * F + d) << l2S, p))[w - d * per] = l2[w];
             }
         }
@@ -1963,9 +1963,9 @@ __global__ void __launch_bounds__(kApplyThreads) GW_APPLY_ATTR k_rgn_apply_nar(I
     __syncthreads();
     // write back: the masks whole, the keys of dirty lines (a foreign slot never changes)
     if constexpr (M) {
-        const int per = S / 16;
+        const int per = S / 16, lper = l2S - 4;
         for (int w = threadIdx.x; w < FS / 16; w += blockDim.x) {
-            const int d = w / per;
+            const int d = w >> lper;
             reinterpret_cast<long2*>(pt_mask_base(a.t, sr * F + d))[w - d * per] = reinterpret_cast<const long2*>(lmask)[w];
         }
     }
@@ -1974,7 +1974,7 @@ __global__ void __launch_bounds__(kApplyThreads) GW_APPLY_ATTR k_rgn_apply_nar(I
         if ((s_kdirty[line >> 5] >> (line & 31)) & 1u) {
             const uint32_t k = lkeys[j];
             if (k != kK32Foreign) {
-                const int d = j / S;
+                const int d = j >> l2S;
                 pt_region(a.t, sr * F + d)[j - d * S] = k == kK32Empty ? kEmptyKey : (int64_t)k;
             }
         }
