@@ -25,6 +25,7 @@ the host cores over a bounded prefix of the same stream.  One JSON line per conf
              sessions close and fire
 """
 import argparse
+import gc
 import json
 import os
 import sys
@@ -313,6 +314,9 @@ def main():
     dev = torch.device("cuda", 0)
     for name in args.only.split(","):
         print(json.dumps(run(name, args, dev)), flush=True)
+        # the previous config's stream (tens of GB) back to the device before the next one
+        gc.collect()
+        torch.cuda.empty_cache()
 
 
 if __name__ == "__main__":
