@@ -573,11 +573,10 @@ __device__ __forceinline__ void block_scan2(const uint32_t* cnt, uint32_t* pre, 
 // pre[n] = total).  Runs of one bucket over a tile group are of similar length, so a guess
 // proportional to e is usually right or one off: a short walk from it instead of a
 // dependent binary search (7 LDS round trips at 112 runs).
-// (The guess in single precision: the walk corrects any rounding, and a 64-bit integer
-// division per record was ~100 VALU instructions.)
-__device__ __forceinline__ int run_near(const uint32_t* pre, int n, uint32_t e) {
-    const uint32_t tot = pre[n];
-    int i = tot ? min(n - 1, (int)((float)e * ((float)n / (float)tot))) : 0;
+// (The guess in single precision from the block's runs per record: the walk corrects any
+// rounding, and a 64-bit integer division per record was ~100 VALU instructions.)
+__device__ __forceinline__ int run_near(const uint32_t* pre, int n, uint32_t e, float runs_per_record) {
+    int i = min(n - 1, (int)((float)e * runs_per_record));
     while (i > 0 && pre[i] > e) --i;
     while (i + 1 < n && pre[i + 1] <= e) ++i;
     return i;
@@ -999,6 +998,7 @@ __global__ void __launch_bounds__(kPartThreads) k_rgn_p2(IngestArgs a) {
     __syncthreads();
     block_scan2(r_cnt, r_pre, nt, wsum);
     const uint32_t total = r_pre[nt];
+    const float rpr = total ? (float)nt / (float)total : 0.f;  // run_near's guess (uniform)
     const int64_t k = b1 * a.ngroups + j;
     const int64_t out0 = a.bk_off[b1] + a.p2_off[k], rnd0 = a.rbeg[b1] + a.p2_roff[k];
     for (uint32_t e0 = 0; e0 < total; e0 += kPartTile) {
@@ -1014,7 +1014,7 @@ __global__ void __launch_bounds__(kPartThreads) k_rgn_p2(IngestArgs a) {
             key[it] = 0; c0[it] = 0; c1[it] = 0; pos[it] = 0;
             bk[it] = -1;
             if (e < e1) {
-                const int i = run_near(r_pre, nt, e);
+                const int i = run_near(r_pre, nt, e, rpr);
                 const int64_t src = r_src[i] + (e - r_pre[i]);
                 key[it] = N4 ? (int64_t)reinterpret_cast<const uint32_t*>(a.p1_key)[src] : a.p1_key[src];
                 if constexpr (NR) {
